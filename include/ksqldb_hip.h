@@ -1,0 +1,303 @@
+/*
+ * ksqldb_hip.h — C ABI of the MI355X-native ksqlDB hot path (libksqldb_hip.so).
+ *
+ * This is the drop-in boundary between ksqlDB's Java operator surface and the
+ * gfx950 HIP kernels.  Every entry point replaces one reference interface; the
+ * reference file:line is cited above each declaration (paths relative to the
+ * ksqlDB source root; S/ = ksqldb-streams/src/main/java/io/confluent/ksql/
+ * execution/streams/, X/ = ksqldb-execution/src/main/java/io/confluent/ksql/
+ * execution/, C/ = ksqldb-common/src/main/java/io/confluent/ksql/).
+ *
+ * Conventions:
+ *   - extern "C", plain pointers and sizes, no exceptions cross the ABI.  Every
+ *     call returns a khip_status; on failure khip_last_error() (thread-local)
+ *     holds a message.
+ *   - The caller owns every host buffer for the duration of a call.  The library
+ *     owns all device memory and its HIP stream; it never retains a caller
+ *     pointer after the call returns (device-resident batches are consumed
+ *     before return of the next synchronising call on the same handle).
+ *   - Handles are independent; a single handle is not re-entrant (Kafka Streams
+ *     task confinement, C/util/KsqlConstants.java:42 — one task per thread).
+ *   - Validity bitmaps are Arrow-style: bit (i & 7) of byte (i >> 3), 1 = valid.
+ *     A NULL bitmap pointer means "all valid".
+ */
+#ifndef KSQLDB_HIP_H
+#define KSQLDB_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KHIP_ABI_VERSION 1
+
+typedef int32_t khip_status;
+#define KHIP_OK 0
+#define KHIP_E_INVALID (-1)     /* bad argument / descriptor (plan-time KsqlException)      */
+#define KHIP_E_NOMEM (-2)       /* device or host allocation failed                         */
+#define KHIP_E_DEVICE (-3)      /* HIP runtime error                                         */
+#define KHIP_E_UNSUPPORTED (-4) /* descriptor valid for ksqlDB but not for this path: the
+                                   caller keeps the reference CPU builder for this query    */
+#define KHIP_E_BUFFER (-5)      /* caller-provided output buffer too small                  */
+#define KHIP_E_COMM (-6)        /* RCCL error                                                */
+#define KHIP_E_STATE (-7)       /* call not valid in the handle's current state             */
+
+/* Window kinds: X/windows/TumblingWindowExpression.java:32, HoppingWindowExpression.java:32.
+ * NONE is the unwindowed StreamAggregate (X/plan/StreamAggregate.java:35). */
+#define KHIP_WINDOW_NONE 0
+#define KHIP_WINDOW_TUMBLING 1
+#define KHIP_WINDOW_HOPPING 2
+
+/* Key types.  Group identity is equality of the serialized KAFKA key
+ * (BIGINT = 8-byte value, STRING = UTF-8 bytes), SURVEY.md §8.0. */
+#define KHIP_KEY_INT64 0
+#define KHIP_KEY_UTF8 1
+
+/* Column (SQL) types carried on this path. */
+#define KHIP_TYPE_INT32 0  /* INTEGER */
+#define KHIP_TYPE_INT64 1  /* BIGINT  */
+#define KHIP_TYPE_DOUBLE 2 /* DOUBLE  */
+
+/* Built-in aggregate functions routed to the GPU (ksqldb-engine function/udaf):
+ * CountKudaf.java:37, {Integer,Long,Double}SumKudaf.java:25, MinKudaf/MaxKudaf via
+ * BaseComparableKudaf.java:55, AverageUdaf.java:104.  COUNT(*) is the analyzer's
+ * COUNT(ROWTIME) rewrite (ksqldb-engine/.../analyzer/AggregateAnalyzer.java:339). */
+#define KHIP_AGG_COUNT_STAR 0
+#define KHIP_AGG_COUNT 1
+#define KHIP_AGG_SUM 2
+#define KHIP_AGG_MIN 3
+#define KHIP_AGG_MAX 4
+#define KHIP_AGG_AVG 5
+
+/* Where a batch's column pointers live. */
+#define KHIP_MEM_HOST 0
+#define KHIP_MEM_DEVICE 1
+
+/* grace_ms value meaning "no GRACE PERIOD clause": TimeWindows.of(size) without
+ * grace (S/StreamAggregateBuilder.java:272,331) → Kafka 3.4 default
+ * max(86_400_000 - size, 0) ms. */
+#define KHIP_GRACE_DEFAULT (-1)
+
+/* Comparison operators for the native HAVING / WHERE predicates. */
+#define KHIP_OP_GT 0
+#define KHIP_OP_GE 1
+#define KHIP_OP_LT 2
+#define KHIP_OP_LE 3
+#define KHIP_OP_EQ 4
+#define KHIP_OP_NE 5
+
+/* Join types: S/StreamTableJoinBuilder.java:78-82. */
+#define KHIP_JOIN_LEFT 0
+#define KHIP_JOIN_INNER 1
+
+/* ------------------------------------------------------------------ batches */
+
+/* One columnar micro-batch of stream records, in arrival order.
+ * Replaces the per-record GenericKey/GenericRow pair (C/GenericKey.java:30,
+ * C/GenericRow.java:28) that Kafka Streams hands to the aggregate/join processor. */
+typedef struct khip_batch {
+  int64_t n_rows;
+  int32_t mem;            /* KHIP_MEM_HOST or KHIP_MEM_DEVICE (all pointers below)   */
+  int32_t n_cols;         /* number of value columns in col_data/col_valid           */
+  const int64_t* key_i64; /* KHIP_KEY_INT64 keys (INT keys are widened by the caller) */
+  const int64_t* key_offsets; /* KHIP_KEY_UTF8: n_rows+1 byte offsets into key_bytes */
+  const uint8_t* key_bytes;
+  const uint8_t* key_valid;   /* bitmap; null key → record dropped                   */
+  const uint8_t* row_valid;   /* bitmap; 0 = null value (tombstone) → dropped
+                                 (S/StreamGroupByBuilderBase.java:102) or, for a table
+                                 upsert, a delete                                      */
+  const int64_t* ts;          /* ROWTIME in ms; < 0 → dropped
+                                 (S/timestamp/LoggingTimestampExtractor.java:72-84)    */
+  const void* const* col_data;      /* n_cols column pointers (element type per desc) */
+  const uint8_t* const* col_valid;  /* n_cols bitmaps (entries may be NULL)           */
+} khip_batch;
+
+/* Per-batch counters (the Kafka Streams dropped-records / late sensors). */
+typedef struct khip_batch_stats {
+  int64_t rows_in;
+  int64_t rows_accepted;    /* reached the aggregate processor                        */
+  int64_t dropped_null_key;
+  int64_t dropped_null_row;
+  int64_t dropped_bad_ts;
+  int64_t windows_applied;  /* (record, window) updates applied                       */
+  int64_t windows_late;     /* (record, window) pairs dropped: windowEnd <= streamTime-grace */
+  int64_t stream_time;      /* observed stream time after the batch (-1 before any)  */
+} khip_batch_stats;
+
+/* --------------------------------------------------------- windowed aggregate */
+
+typedef struct khip_agg_spec {
+  int32_t kind;    /* KHIP_AGG_*                                                      */
+  int32_t arg_col; /* value column index (ignored for COUNT_STAR)                     */
+} khip_agg_spec;
+
+/* Plan-time descriptor: the content of StreamWindowedAggregate / StreamAggregate
+ * (X/plan/StreamWindowedAggregate.java:47-70, X/plan/StreamAggregate.java:35-111)
+ * after AggregateParamsFactory.create resolved the functions
+ * (S/AggregateParamsFactory.java:70-121). */
+typedef struct khip_agg_desc {
+  int32_t window_kind;      /* KHIP_WINDOW_*                                          */
+  int32_t key_type;         /* KHIP_KEY_*                                             */
+  int64_t size_ms;          /* TUMBLING/HOPPING SIZE                                  */
+  int64_t advance_ms;       /* HOPPING ADVANCE BY (= size for TUMBLING)              */
+  int64_t grace_ms;         /* GRACE PERIOD, or KHIP_GRACE_DEFAULT                   */
+  int32_t n_cols;
+  const int32_t* col_types; /* KHIP_TYPE_* per value column                          */
+  int32_t n_aggs;
+  const khip_agg_spec* aggs;
+  int32_t device;           /* HIP device ordinal                                    */
+  int32_t flags;            /* reserved, 0                                           */
+  int64_t capacity_hint;    /* expected live (key, window) groups; 0 = default       */
+} khip_agg_desc;
+
+typedef struct khip_agg khip_agg;
+
+/* HAVING predicate on one aggregate's result (S/TableFilterBuilder.java:46-74).
+ * Rows failing it are absent from the materialized table (tombstoned). */
+typedef struct khip_having {
+  int32_t agg_index;
+  int32_t op;        /* KHIP_OP_*                                                     */
+  int64_t i64;       /* constant for integer-valued results                          */
+  double f64;        /* constant for DOUBLE-valued results (AVG, SUM/MIN/MAX DOUBLE) */
+} khip_having;
+
+/* Final materialized table, sorted by (key, window_start).  Caller-allocated.
+ * Row = [key, agg results..., WINDOWSTART, WINDOWEND]
+ * (S/AggregateParamsFactory.java:156-190, S/StreamAggregateBuilder.java:355-373)
+ * plus the row timestamp (max ROWTIME applied to the entry). */
+typedef struct khip_snapshot {
+  int64_t capacity;            /* rows the buffers below can hold                     */
+  int64_t n_rows;              /* out                                                 */
+  int64_t key_bytes_capacity;  /* UTF8                                                */
+  int64_t key_bytes_len;       /* out                                                 */
+  int64_t* key_i64;            /* INT64 keys                                          */
+  int64_t* key_offsets;        /* UTF8: capacity+1                                    */
+  uint8_t* key_bytes;
+  int64_t* window_start;       /* 0 for KHIP_WINDOW_NONE                              */
+  int64_t* window_end;
+  int64_t* rowtime;
+  void** agg_values;           /* per agg; element type from khip_agg_result_type()   */
+  uint8_t** agg_null;          /* per agg; 1 byte per row, 1 = SQL NULL               */
+} khip_snapshot;
+
+/* KSPlanBuilder.visitStreamWindowedAggregate / visitStreamAggregate
+ * (S/KSPlanBuilder.java:293-304, :144-155; interface X/plan/PlanBuilder.java:37,67):
+ * builds the HBM-resident (key, windowStart) state for one query task. */
+khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out);
+
+/* Result element type of aggregate i (KsqlAggregateFunction.getReturnType,
+ * C/function/KsqlAggregateFunction.java:25-55): COUNT → INT64, SUM(T) → T,
+ * MIN/MAX(T) → T, AVG → DOUBLE. */
+khip_status khip_agg_result_type(const khip_agg_desc* desc, int32_t agg_index,
+                                 int32_t* out_type);
+
+/* Per-record KStreamWindowAggregate.process + KudafAggregator.apply
+ * (X/function/udaf/KudafAggregator.java:56-80) over a whole micro-batch:
+ * rows are applied as if one at a time in arrival order (stream time, late drop,
+ * window fan-out).  stats may be NULL (then the call may return
+ * before the device work completes). */
+khip_status khip_agg_push(khip_agg* agg, const khip_batch* batch,
+                          khip_batch_stats* stats);
+
+/* Number of rows and key bytes the next snapshot will produce (no HAVING). */
+khip_status khip_agg_snapshot_size(khip_agg* agg, int64_t* n_rows,
+                                   int64_t* key_bytes);
+
+/* Materialize the table (ResultTransformer map(): KudafAggregator.java:129-158).
+ * having may be NULL. */
+khip_status khip_agg_snapshot(khip_agg* agg, const khip_having* having,
+                              khip_snapshot* out);
+
+/* Count the rows that pass `having` entirely on the device (no copy-out).
+ * having may be NULL (= total group count). */
+khip_status khip_agg_count_rows(khip_agg* agg, const khip_having* having,
+                                int64_t* n_rows);
+
+/* Drop all state (a fresh query instance); keeps the device allocation. */
+khip_status khip_agg_reset(khip_agg* agg);
+
+/* Block until all work queued on the handle has finished. */
+khip_status khip_agg_sync(khip_agg* agg);
+
+/* The handle's hipStream_t (as void*), so callers can order their own work. */
+khip_status khip_agg_stream(khip_agg* agg, void** hip_stream);
+
+khip_status khip_agg_destroy(khip_agg* agg);
+
+/* --------------------------------------------------------- stream-table join */
+
+/* Table side: SourceBuilder.buildKTable (S/SourceBuilder.java:87-137) materializes
+ * the latest non-null value per key; a null value deletes the key. */
+typedef struct khip_table_desc {
+  int32_t key_type;          /* KHIP_KEY_INT64                                        */
+  int32_t n_cols;
+  const int32_t* col_types;  /* KHIP_TYPE_* per table value column (VARCHAR columns are
+                                dictionary codes, KHIP_TYPE_INT32)                    */
+  int32_t device;
+  int32_t flags;
+  int64_t capacity_hint;     /* expected live keys                                    */
+} khip_table_desc;
+
+typedef struct khip_table khip_table;
+
+/* WHERE predicate on one right-side column (S/StreamFilterBuilder.java:44-69);
+ * a NULL right column never satisfies it (SQL three-valued logic). */
+typedef struct khip_where {
+  int32_t right_col;
+  int32_t op;
+  int64_t i64;
+  double f64;
+} khip_where;
+
+/* Join output: one entry per emitted row, in stream arrival order.
+ * Row = left values ++ right values|nulls (S/KsqlValueJoiner.java:41-63); the caller
+ * gathers the left side by stream_row. */
+typedef struct khip_join_out {
+  int64_t capacity;
+  int64_t n_rows;       /* out                                                       */
+  int64_t* stream_row;  /* index of the stream record in the probe batch             */
+  uint8_t* matched;     /* 1 = table hit, 0 = LEFT miss (right side null)            */
+  void** col_data;      /* per right column (NULL entries are skipped)               */
+  uint8_t** col_null;   /* per right column; 1 byte per row                          */
+} khip_join_out;
+
+khip_status khip_table_create(const khip_table_desc* desc, khip_table** out);
+
+/* Apply table-topic records in arrival order: the last row per key wins, a row with
+ * row_valid = 0 deletes the key, null keys are skipped. */
+khip_status khip_table_upsert(khip_table* t, const khip_batch* rows);
+
+khip_status khip_table_size(khip_table* t, int64_t* n_keys);
+
+/* KStreamKTableJoin per stream record + KsqlValueJoiner.apply
+ * (S/StreamTableJoinBuilder.java:38-88): null-key / null-value / negative-ts stream
+ * records are dropped; INNER emits on hit only; LEFT always emits.  `where` may be
+ * NULL.  Output is written to host buffers (out). */
+khip_status khip_table_probe(khip_table* t, const khip_batch* stream, int32_t join_type,
+                             const khip_where* where, khip_join_out* out);
+
+/* Device-resident variant: writes the number of emitted rows to *n_out and keeps the
+ * output (stream_row, matched, right columns) in library-owned device buffers,
+ * readable through khip_table_probe_result until the next probe on this handle. */
+khip_status khip_table_probe_device(khip_table* t, const khip_batch* stream,
+                                    int32_t join_type, const khip_where* where,
+                                    int64_t* n_out);
+
+khip_status khip_table_sync(khip_table* t);
+khip_status khip_table_destroy(khip_table* t);
+
+/* ------------------------------------------------------------ diagnostics */
+
+/* Thread-local message of the last failing call on this thread ("" if none). */
+const char* khip_last_error(void);
+
+/* ABI version (KHIP_ABI_VERSION) and the gfx target the kernels were built for. */
+int32_t khip_abi_version(void);
+const char* khip_build_target(void);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* KSQLDB_HIP_H */

@@ -1,0 +1,339 @@
+"""ctypes mirror of include/ksqldb_hip.h.
+
+The same structs drive two libraries with identical signatures:
+  * ksql_amd/libksqldb_hip.so  — the product (HIP kernels, prefix ``khip_``);
+  * oracle/liboracle.so        — the CPU restatement used only by tests/bench as
+                                  the parity checker (prefix ``oracle_``).
+Nothing here routes product calls to the oracle: ``load_product()`` fails loudly
+if the HIP library is missing.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PRODUCT_LIB = os.path.join(REPO, "ksql_amd", "libksqldb_hip.so")
+ORACLE_LIB = os.path.join(REPO, "oracle", "liboracle.so")
+
+KHIP_OK = 0
+KHIP_E_BUFFER = -5
+
+WINDOW = {"NONE": 0, "TUMBLING": 1, "HOPPING": 2}
+KEY = {"INT64": 0, "UTF8": 1}
+TYPE = {"INT32": 0, "INT64": 1, "DOUBLE": 2}
+AGG = {"COUNT_STAR": 0, "COUNT": 1, "SUM": 2, "MIN": 3, "MAX": 4, "AVG": 5}
+OP = {"GT": 0, "GE": 1, "LT": 2, "LE": 3, "EQ": 4, "NE": 5}
+JOIN = {"LEFT": 0, "INNER": 1}
+MEM_HOST, MEM_DEVICE = 0, 1
+NP_TYPE = {0: np.int32, 1: np.int64, 2: np.float64}
+
+i32, i64, u8p = C.c_int32, C.c_int64, C.POINTER(C.c_uint8)
+
+
+class Batch(C.Structure):
+    _fields_ = [("n_rows", i64), ("mem", i32), ("n_cols", i32),
+                ("key_i64", C.c_void_p), ("key_offsets", C.c_void_p), ("key_bytes", C.c_void_p),
+                ("key_valid", C.c_void_p), ("row_valid", C.c_void_p), ("ts", C.c_void_p),
+                ("col_data", C.POINTER(C.c_void_p)), ("col_valid", C.POINTER(C.c_void_p))]
+
+
+class BatchStats(C.Structure):
+    _fields_ = [("rows_in", i64), ("rows_accepted", i64), ("dropped_null_key", i64),
+                ("dropped_null_row", i64), ("dropped_bad_ts", i64), ("windows_applied", i64),
+                ("windows_late", i64), ("stream_time", i64)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+class AggSpec(C.Structure):
+    _fields_ = [("kind", i32), ("arg_col", i32)]
+
+
+class AggDesc(C.Structure):
+    _fields_ = [("window_kind", i32), ("key_type", i32), ("size_ms", i64), ("advance_ms", i64),
+                ("grace_ms", i64), ("n_cols", i32), ("col_types", C.POINTER(i32)),
+                ("n_aggs", i32), ("aggs", C.POINTER(AggSpec)), ("device", i32), ("flags", i32),
+                ("capacity_hint", i64)]
+
+
+class Having(C.Structure):
+    _fields_ = [("agg_index", i32), ("op", i32), ("i64", i64), ("f64", C.c_double)]
+
+
+class Snapshot(C.Structure):
+    _fields_ = [("capacity", i64), ("n_rows", i64), ("key_bytes_capacity", i64),
+                ("key_bytes_len", i64), ("key_i64", C.c_void_p), ("key_offsets", C.c_void_p),
+                ("key_bytes", C.c_void_p), ("window_start", C.c_void_p), ("window_end", C.c_void_p),
+                ("rowtime", C.c_void_p), ("agg_values", C.POINTER(C.c_void_p)),
+                ("agg_null", C.POINTER(C.c_void_p))]
+
+
+class TableDesc(C.Structure):
+    _fields_ = [("key_type", i32), ("n_cols", i32), ("col_types", C.POINTER(i32)),
+                ("device", i32), ("flags", i32), ("capacity_hint", i64)]
+
+
+class Where(C.Structure):
+    _fields_ = [("right_col", i32), ("op", i32), ("i64", i64), ("f64", C.c_double)]
+
+
+class JoinOut(C.Structure):
+    _fields_ = [("capacity", i64), ("n_rows", i64), ("stream_row", C.c_void_p),
+                ("matched", C.c_void_p), ("col_data", C.POINTER(C.c_void_p)),
+                ("col_null", C.POINTER(C.c_void_p))]
+
+
+_P = C.c_void_p
+SIGS = {
+    "agg_create": ([C.POINTER(AggDesc), C.POINTER(_P)]),
+    "agg_push": ([_P, C.POINTER(Batch), C.POINTER(BatchStats)]),
+    "agg_snapshot_size": ([_P, C.POINTER(i64), C.POINTER(i64)]),
+    "agg_snapshot": ([_P, C.POINTER(Having), C.POINTER(Snapshot)]),
+    "agg_destroy": ([_P]),
+    "table_create": ([C.POINTER(TableDesc), C.POINTER(_P)]),
+    "table_upsert": ([_P, C.POINTER(Batch)]),
+    "table_size": ([_P, C.POINTER(i64)]),
+    "table_probe": ([_P, C.POINTER(Batch), i32, C.POINTER(Where), C.POINTER(JoinOut)]),
+    "table_destroy": ([_P]),
+}
+PRODUCT_ONLY = {
+    "agg_result_type": ([C.POINTER(AggDesc), i32, C.POINTER(i32)]),
+    "agg_count_rows": ([_P, C.POINTER(Having), C.POINTER(i64)]),
+    "agg_reset": ([_P]),
+    "agg_sync": ([_P]),
+    "agg_stream": ([_P, C.POINTER(_P)]),
+    "table_probe_device": ([_P, C.POINTER(Batch), i32, C.POINTER(Where), C.POINTER(i64)]),
+    "table_sync": ([_P]),
+}
+
+
+class KsqlHipError(RuntimeError):
+    pass
+
+
+class Lib:
+    """Binds one library (product or oracle) by prefix."""
+
+    def __init__(self, path, prefix, product):
+        if not os.path.exists(path):
+            raise KsqlHipError("library not built: %s" % path)
+        self.path = path
+        self.dll = C.CDLL(path)
+        self.prefix = prefix
+        self.product = product
+        sigs = dict(SIGS)
+        if product:
+            sigs.update(PRODUCT_ONLY)
+        for name, args in sigs.items():
+            fn = getattr(self.dll, prefix + name)
+            fn.argtypes = args
+            fn.restype = i32
+            setattr(self, name, fn)
+        if product:
+            self.dll.khip_last_error.restype = C.c_char_p
+            self.dll.khip_last_error.argtypes = []
+            self.dll.khip_abi_version.restype = i32
+            self.dll.khip_build_target.restype = C.c_char_p
+
+    def check(self, status, what):
+        if status != KHIP_OK:
+            msg = self.dll.khip_last_error().decode() if self.product else ""
+            raise KsqlHipError("%s%s failed (%d): %s" % (self.prefix, what, status, msg))
+
+
+_product = None
+_oracle = None
+
+
+def load_product():
+    """The HIP library.  Raises if it was not built: there is no fallback."""
+    global _product
+    if _product is None:
+        _product = Lib(PRODUCT_LIB, "khip_", True)
+    return _product
+
+
+def load_oracle():
+    """CPU restatement — test infrastructure only."""
+    global _oracle
+    if _oracle is None:
+        _oracle = Lib(ORACLE_LIB, "oracle_", False)
+    return _oracle
+
+
+# ------------------------------------------------------------------ helpers
+
+def bitmap(valid):
+    """bool array -> Arrow LSB bitmap (uint8), or None if all valid."""
+    valid = np.asarray(valid, dtype=bool)
+    if valid.all():
+        return None
+    return np.packbits(valid, bitorder="little")
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+class HostBatch:
+    """Owns numpy arrays for one host batch and the ctypes struct pointing at them."""
+
+    def __init__(self, ts, keys=None, key_valid=None, row_valid=None, cols=(), col_valid=(),
+                 utf8_keys=None):
+        self.ts = np.ascontiguousarray(ts, dtype=np.int64)
+        n = len(self.ts)
+        self.keys = None if keys is None else np.ascontiguousarray(keys, dtype=np.int64)
+        self.key_offsets = self.key_bytes = None
+        if utf8_keys is not None:
+            enc = [b"" if k is None else (k.encode() if isinstance(k, str) else bytes(k)) for k in utf8_keys]
+            self.key_offsets = np.zeros(n + 1, dtype=np.int64)
+            self.key_offsets[1:] = np.cumsum([len(e) for e in enc])
+            self.key_bytes = np.frombuffer(b"".join(enc) + b"\0", dtype=np.uint8).copy()
+        self.key_valid = None if key_valid is None else bitmap(key_valid)
+        self.row_valid = None if row_valid is None else bitmap(row_valid)
+        self.cols = [np.ascontiguousarray(c) for c in cols]
+        self.col_valid = [None if v is None else bitmap(v) for v in col_valid] + \
+            [None] * (len(self.cols) - len(col_valid))
+        nc = len(self.cols)
+        self._cd = (C.c_void_p * max(nc, 1))(*[_ptr(c) for c in self.cols])
+        self._cv = (C.c_void_p * max(nc, 1))(*[_ptr(v) for v in self.col_valid])
+        self.struct = Batch(n, MEM_HOST, nc, _ptr(self.keys), _ptr(self.key_offsets),
+                            _ptr(self.key_bytes), _ptr(self.key_valid), _ptr(self.row_valid),
+                            _ptr(self.ts), self._cd, self._cv)
+
+
+def make_agg_desc(window_kind="NONE", key_type="INT64", size_ms=0, advance_ms=0, grace_ms=-1,
+                  col_types=(), aggs=(), device=0, capacity_hint=0):
+    ct = (i32 * max(len(col_types), 1))(*[TYPE[t] if isinstance(t, str) else t for t in col_types])
+    sp = (AggSpec * max(len(aggs), 1))(*[AggSpec(AGG[k] if isinstance(k, str) else k, c) for k, c in aggs])
+    d = AggDesc(WINDOW[window_kind] if isinstance(window_kind, str) else window_kind,
+                KEY[key_type] if isinstance(key_type, str) else key_type,
+                size_ms, advance_ms if advance_ms else size_ms, grace_ms, len(col_types), ct,
+                len(aggs), sp, device, 0, capacity_hint)
+    d._keep = (ct, sp)
+    return d
+
+
+def result_types(desc):
+    out = []
+    for i in range(desc.n_aggs):
+        k = desc.aggs[i].kind
+        if k in (AGG["COUNT_STAR"], AGG["COUNT"]):
+            out.append(TYPE["INT64"])
+        elif k == AGG["AVG"]:
+            out.append(TYPE["DOUBLE"])
+        else:
+            out.append(desc.col_types[desc.aggs[i].arg_col])
+    return out
+
+
+class AggHandle:
+    """A windowed/unwindowed aggregate task on one library (product or oracle)."""
+
+    def __init__(self, lib, desc):
+        self.lib = lib
+        self.desc = desc
+        self.h = C.c_void_p()
+        lib.check(lib.agg_create(C.byref(desc), C.byref(self.h)), "agg_create")
+
+    def push(self, batch, stats=True):
+        st = BatchStats()
+        self.lib.check(self.lib.agg_push(self.h, C.byref(batch.struct if isinstance(batch, HostBatch) else batch),
+                                         C.byref(st) if stats else None), "agg_push")
+        return st.as_dict() if stats else None
+
+    def snapshot(self, having=None):
+        n, kb = i64(), i64()
+        self.lib.check(self.lib.agg_snapshot_size(self.h, C.byref(n), C.byref(kb)), "agg_snapshot_size")
+        cap = max(n.value, 1)
+        kcap = max(kb.value, 1)
+        rt = result_types(self.desc)
+        arrays = {
+            "key": np.zeros(cap, np.int64), "key_offsets": np.zeros(cap + 1, np.int64),
+            "key_bytes": np.zeros(kcap, np.uint8), "ws": np.zeros(cap, np.int64),
+            "we": np.zeros(cap, np.int64), "rowtime": np.zeros(cap, np.int64),
+            "values": [np.zeros(cap, NP_TYPE[t]) for t in rt],
+            "nulls": [np.zeros(cap, np.uint8) for _ in rt],
+        }
+        av = (C.c_void_p * max(len(rt), 1))(*[a.ctypes.data for a in arrays["values"]])
+        an = (C.c_void_p * max(len(rt), 1))(*[a.ctypes.data for a in arrays["nulls"]])
+        s = Snapshot(cap, 0, kcap, 0, arrays["key"].ctypes.data, arrays["key_offsets"].ctypes.data,
+                     arrays["key_bytes"].ctypes.data, arrays["ws"].ctypes.data, arrays["we"].ctypes.data,
+                     arrays["rowtime"].ctypes.data, av, an)
+        hv = None
+        if having is not None:
+            hv = Having(having["agg"], OP[having["op"]], int(having["value"]) if not isinstance(having["value"], float) else 0,
+                        float(having["value"]))
+        self.lib.check(self.lib.agg_snapshot(self.h, C.byref(hv) if hv else None, C.byref(s)), "agg_snapshot")
+        m = s.n_rows
+        out = {"n": m, "ws": arrays["ws"][:m], "we": arrays["we"][:m], "rowtime": arrays["rowtime"][:m],
+               "values": [v[:m] for v in arrays["values"]], "nulls": [v[:m].astype(bool) for v in arrays["nulls"]]}
+        if self.desc.key_type == KEY["UTF8"]:
+            offs = arrays["key_offsets"][: m + 1]
+            kbts = arrays["key_bytes"].tobytes()
+            out["key"] = [kbts[offs[i]:offs[i + 1]].decode("utf-8", "surrogateescape") for i in range(m)]
+        else:
+            out["key"] = arrays["key"][:m]
+        return out
+
+    def close(self):
+        if self.h:
+            self.lib.agg_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class TableHandle:
+    def __init__(self, lib, col_types, device=0, capacity_hint=0):
+        self.lib = lib
+        self.col_types = [TYPE[t] if isinstance(t, str) else t for t in col_types]
+        ct = (i32 * max(len(col_types), 1))(*self.col_types)
+        self._ct = ct
+        self.desc = TableDesc(KEY["INT64"], len(col_types), ct, device, 0, capacity_hint)
+        self.h = C.c_void_p()
+        lib.check(lib.table_create(C.byref(self.desc), C.byref(self.h)), "table_create")
+
+    def upsert(self, batch):
+        self.lib.check(self.lib.table_upsert(self.h, C.byref(batch.struct)), "table_upsert")
+
+    def size(self):
+        n = i64()
+        self.lib.check(self.lib.table_size(self.h, C.byref(n)), "table_size")
+        return n.value
+
+    def probe(self, batch, join_type="LEFT", where=None, capacity=None):
+        n = batch.struct.n_rows
+        cap = max(n if capacity is None else capacity, 1)
+        sr = np.zeros(cap, np.int64)
+        mt = np.zeros(cap, np.uint8)
+        cols = [np.zeros(cap, NP_TYPE[t]) for t in self.col_types]
+        nulls = [np.zeros(cap, np.uint8) for _ in self.col_types]
+        cd = (C.c_void_p * max(len(cols), 1))(*[c.ctypes.data for c in cols])
+        cn = (C.c_void_p * max(len(cols), 1))(*[c.ctypes.data for c in nulls])
+        out = JoinOut(cap, 0, sr.ctypes.data, mt.ctypes.data, cd, cn)
+        wv = None
+        if where is not None:
+            wv = Where(where["col"], OP[where["op"]], int(where.get("i64", 0)), float(where.get("f64", 0.0)))
+        self.lib.check(self.lib.table_probe(self.h, C.byref(batch.struct), JOIN[join_type],
+                                            C.byref(wv) if wv else None, C.byref(out)), "table_probe")
+        m = out.n_rows
+        return {"n": m, "stream_row": sr[:m], "matched": mt[:m].astype(bool),
+                "cols": [c[:m] for c in cols], "nulls": [x[:m].astype(bool) for x in nulls]}
+
+    def close(self):
+        if self.h:
+            self.lib.table_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,706 @@
+/*
+ * oracle.c — sequential CPU restatement of the ksqlDB hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see oracle.h).  Parity status: pinned by the
+ * reference's QTT golden vectors (tests/golden/, extracted from
+ * ksqldb-functional-tests/src/test/resources/query-validation-tests/ JSON files);
+ * the 24 h default grace and NaN payload bits are unpinned.
+ *
+ * Every record is applied one at a time in arrival order, exactly as the Kafka
+ * Streams processors do.  Rules and where they come from (paths relative to the
+ * ksqlDB root; S/ X/ E/ as in include/ksqldb_hip.h, E/ = ksqldb-engine/src/main/
+ * java/io/confluent/ksql/):
+ *
+ *  R1 drop before the aggregate: null key (Kafka KStreamWindowAggregate /
+ *     KStreamAggregate key==null skip; S/GroupByParamsFactory.java:92-100 for
+ *     computed keys), null value (S/StreamGroupByBuilderBase.java:102), negative
+ *     timestamp (S/timestamp/LoggingTimestampExtractor.java:72-84).  Dropped
+ *     records do not advance stream time.
+ *  R2 stream time: observedStreamTime = max(observedStreamTime, ts), updated
+ *     before the late check; initial -1 (Kafka 3.4 KStreamWindowAggregate).
+ *  R3 windows: TimeWindows.windowsFor(ts): ws0 = (max(0, ts - size + adv) / adv)
+ *     * adv; ws = ws0, ws0+adv, ... while ws <= ts (call sites
+ *     S/StreamAggregateBuilder.java:269-295,328-352).
+ *  R4 late drop: window updated iff ws + size > streamTime - grace
+ *     (grace: GRACE PERIOD or max(86400000 - size, 0), S/StreamAggregateBuilder.java
+ *     :275-277,332-334).  Unwindowed aggregation (StreamAggregateBuilder.java:81-138)
+ *     has no windows and no late drop.
+ *  R5 entry: created by the first applied record (KudafInitializer.apply,
+ *     X/function/udaf/KudafInitializer.java:39-47), even if every aggregate input is
+ *     null.  Row time = max(ts) over applied records.
+ *  R6 aggregate math (KudafAggregator.apply, X/function/udaf/KudafAggregator.java:56-80):
+ *     COUNT: +1 if arg non-null (E/function/udaf/count/CountKudaf.java:37-42);
+ *     COUNT(*) = COUNT(ROWTIME), never null (E/analyzer/AggregateAnalyzer.java:339);
+ *     SUM INT/BIGINT: wrapping add, null skipped (E/function/udaf/sum/IntegerSumKudaf
+ *     .java:25-31, LongSumKudaf.java:25-31); SUM DOUBLE sequential + (DoubleSumKudaf
+ *     .java:25-31); MIN/MAX: null identity, compareTo, ties keep the aggregate
+ *     (E/function/udaf/BaseComparableKudaf.java:55-66, max/MaxKudaf.java:82,
+ *     min/MinKudaf.java:81; Double.compareTo: -0.0 < 0.0, NaN largest);
+ *     AVG: {sum (wrapping for INT/BIGINT), count} and map = count==0 ? 0.0 :
+ *     (double)sum / (double)count (E/function/udaf/average/AverageUdaf.java:104-128).
+ *  R7 join: table keeps the latest non-null value per key, a null value deletes;
+ *     stream records with null key / null value / negative ts are dropped; lookup
+ *     against the table as of that point; INNER emits on hit, LEFT always
+ *     (S/StreamTableJoinBuilder.java:77-86, S/KsqlValueJoiner.java:41-63).
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORACLE_DAY_MS 86400000LL
+
+static int bit_get(const uint8_t* bm, int64_t i) {
+  return bm == NULL ? 1 : (bm[i >> 3] >> (i & 7)) & 1;
+}
+
+uint64_t oracle_splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+static uint64_t mix64(uint64_t h) {
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdULL;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ULL;
+  h ^= h >> 33;
+  return h;
+}
+
+static uint64_t hash_bytes(const uint8_t* p, int64_t n) {
+  uint64_t h = 1469598103934665603ULL;
+  for (int64_t i = 0; i < n; i++) h = (h ^ p[i]) * 1099511628211ULL;
+  return mix64(h ^ (uint64_t)n);
+}
+
+/* Java Double.compare(a, b) (doubleToLongBits canonicalizes NaN). */
+static int64_t java_double_bits(double d) {
+  int64_t b;
+  if (isnan(d)) return 0x7ff8000000000000LL;
+  memcpy(&b, &d, 8);
+  return b;
+}
+static int java_double_compare(double a, double b) {
+  if (a < b) return -1;
+  if (a > b) return 1;
+  int64_t x = java_double_bits(a), y = java_double_bits(b);
+  return x == y ? 0 : (x < y ? -1 : 1);
+}
+
+/* ------------------------------------------------------------- key dictionary */
+
+typedef struct {
+  int64_t* off;  /* per key id: arena offset */
+  int64_t* len;
+  uint8_t* arena;
+  int64_t arena_len, arena_cap;
+  int64_t n, cap;
+  int64_t* slots; /* open addressing: key id or -1 */
+  uint64_t* slot_hash;
+  int64_t nslots;
+} strdict;
+
+static void strdict_init(strdict* d) {
+  memset(d, 0, sizeof(*d));
+  d->nslots = 1024;
+  d->slots = (int64_t*)malloc(sizeof(int64_t) * d->nslots);
+  d->slot_hash = (uint64_t*)malloc(sizeof(uint64_t) * d->nslots);
+  for (int64_t i = 0; i < d->nslots; i++) d->slots[i] = -1;
+}
+
+static void strdict_free(strdict* d) {
+  free(d->off); free(d->len); free(d->arena); free(d->slots); free(d->slot_hash);
+}
+
+static void strdict_grow(strdict* d) {
+  int64_t ns = d->nslots * 2;
+  int64_t* s = (int64_t*)malloc(sizeof(int64_t) * ns);
+  uint64_t* sh = (uint64_t*)malloc(sizeof(uint64_t) * ns);
+  for (int64_t i = 0; i < ns; i++) s[i] = -1;
+  for (int64_t i = 0; i < d->nslots; i++) {
+    if (d->slots[i] < 0) continue;
+    uint64_t h = d->slot_hash[i];
+    int64_t j = (int64_t)(h & (uint64_t)(ns - 1));
+    while (s[j] >= 0) j = (j + 1) & (ns - 1);
+    s[j] = d->slots[i];
+    sh[j] = h;
+  }
+  free(d->slots); free(d->slot_hash);
+  d->slots = s; d->slot_hash = sh; d->nslots = ns;
+}
+
+static int64_t strdict_intern(strdict* d, const uint8_t* p, int64_t n) {
+  if (2 * (d->n + 1) > d->nslots) strdict_grow(d);
+  uint64_t h = hash_bytes(p, n);
+  int64_t j = (int64_t)(h & (uint64_t)(d->nslots - 1));
+  while (d->slots[j] >= 0) {
+    int64_t id = d->slots[j];
+    if (d->slot_hash[j] == h && d->len[id] == n &&
+        (n == 0 || memcmp(d->arena + d->off[id], p, (size_t)n) == 0))
+      return id;
+    j = (j + 1) & (d->nslots - 1);
+  }
+  if (d->n == d->cap) {
+    d->cap = d->cap ? d->cap * 2 : 1024;
+    d->off = (int64_t*)realloc(d->off, sizeof(int64_t) * d->cap);
+    d->len = (int64_t*)realloc(d->len, sizeof(int64_t) * d->cap);
+  }
+  while (d->arena_len + n > d->arena_cap) {
+    d->arena_cap = d->arena_cap ? d->arena_cap * 2 : 4096;
+    d->arena = (uint8_t*)realloc(d->arena, (size_t)d->arena_cap);
+  }
+  int64_t id = d->n++;
+  d->off[id] = d->arena_len;
+  d->len[id] = n;
+  if (n) memcpy(d->arena + d->arena_len, p, (size_t)n);
+  d->arena_len += n;
+  d->slots[j] = id;
+  d->slot_hash[j] = h;
+  return id;
+}
+
+/* ------------------------------------------------------------ aggregate state */
+
+typedef struct {
+  int64_t i;   /* COUNT, SUM INT/BIGINT (wrapping), MIN/MAX integer, AVG int sum */
+  double d;    /* SUM DOUBLE, MIN/MAX DOUBLE, AVG double sum */
+  int64_t cnt; /* AVG count */
+  int has;     /* MIN/MAX: non-null */
+} agg_state;
+
+typedef struct {
+  int64_t key; /* INT64 key, or dictionary id for UTF8 */
+  int64_t ws;
+  int64_t rowtime;
+  agg_state* st; /* n_aggs */
+} entry;
+
+struct oracle_agg {
+  khip_agg_desc d;
+  int32_t* col_types;
+  khip_agg_spec* aggs;
+  int64_t grace;
+  int64_t stream_time;
+  strdict dict;
+  entry* e;
+  int64_t n, cap;
+  int64_t* slots;
+  int64_t nslots;
+};
+
+static uint64_t entry_hash(int64_t key, int64_t ws) {
+  return mix64((uint64_t)key ^ mix64((uint64_t)ws + 0x9E3779B97F4A7C15ULL));
+}
+
+static void slots_rebuild(oracle_agg* a, int64_t ns) {
+  free(a->slots);
+  a->nslots = ns;
+  a->slots = (int64_t*)malloc(sizeof(int64_t) * ns);
+  for (int64_t i = 0; i < ns; i++) a->slots[i] = -1;
+  for (int64_t k = 0; k < a->n; k++) {
+    int64_t j = (int64_t)(entry_hash(a->e[k].key, a->e[k].ws) & (uint64_t)(ns - 1));
+    while (a->slots[j] >= 0) j = (j + 1) & (ns - 1);
+    a->slots[j] = k;
+  }
+}
+
+static entry* find_or_create(oracle_agg* a, int64_t key, int64_t ws) {
+  if (2 * (a->n + 1) > a->nslots) slots_rebuild(a, a->nslots * 2);
+  int64_t j = (int64_t)(entry_hash(key, ws) & (uint64_t)(a->nslots - 1));
+  while (a->slots[j] >= 0) {
+    entry* x = &a->e[a->slots[j]];
+    if (x->key == key && x->ws == ws) return x;
+    j = (j + 1) & (a->nslots - 1);
+  }
+  if (a->n == a->cap) {
+    a->cap = a->cap ? a->cap * 2 : 1024;
+    a->e = (entry*)realloc(a->e, sizeof(entry) * a->cap);
+  }
+  entry* x = &a->e[a->n];
+  a->slots[j] = a->n++;
+  x->key = key;
+  x->ws = ws;
+  x->rowtime = INT64_MIN;
+  x->st = (agg_state*)calloc((size_t)(a->d.n_aggs > 0 ? a->d.n_aggs : 1), sizeof(agg_state));
+  return x;
+}
+
+static int valid_desc(const khip_agg_desc* d) {
+  if (d->window_kind != KHIP_WINDOW_NONE && d->window_kind != KHIP_WINDOW_TUMBLING &&
+      d->window_kind != KHIP_WINDOW_HOPPING)
+    return 0;
+  if (d->window_kind != KHIP_WINDOW_NONE) {
+    if (d->size_ms <= 0) return 0;
+    if (d->window_kind == KHIP_WINDOW_HOPPING &&
+        (d->advance_ms <= 0 || d->advance_ms > d->size_ms))
+      return 0;
+  }
+  if (d->key_type != KHIP_KEY_INT64 && d->key_type != KHIP_KEY_UTF8) return 0;
+  if (d->n_aggs < 0 || d->n_cols < 0) return 0;
+  for (int i = 0; i < d->n_aggs; i++) {
+    const khip_agg_spec* s = &d->aggs[i];
+    if (s->kind < KHIP_AGG_COUNT_STAR || s->kind > KHIP_AGG_AVG) return 0;
+    if (s->kind != KHIP_AGG_COUNT_STAR && (s->arg_col < 0 || s->arg_col >= d->n_cols))
+      return 0;
+  }
+  for (int c = 0; c < d->n_cols; c++)
+    if (d->col_types[c] < KHIP_TYPE_INT32 || d->col_types[c] > KHIP_TYPE_DOUBLE) return 0;
+  return 1;
+}
+
+khip_status oracle_agg_create(const khip_agg_desc* desc, oracle_agg** out) {
+  if (!desc || !out || !valid_desc(desc)) return KHIP_E_INVALID;
+  oracle_agg* a = (oracle_agg*)calloc(1, sizeof(oracle_agg));
+  a->d = *desc;
+  a->col_types = (int32_t*)malloc(sizeof(int32_t) * (desc->n_cols + 1));
+  memcpy(a->col_types, desc->col_types, sizeof(int32_t) * desc->n_cols);
+  a->aggs = (khip_agg_spec*)malloc(sizeof(khip_agg_spec) * (desc->n_aggs + 1));
+  memcpy(a->aggs, desc->aggs, sizeof(khip_agg_spec) * desc->n_aggs);
+  a->d.col_types = a->col_types;
+  a->d.aggs = a->aggs;
+  if (desc->window_kind == KHIP_WINDOW_TUMBLING) a->d.advance_ms = desc->size_ms;
+  if (desc->window_kind == KHIP_WINDOW_NONE) {
+    a->grace = 0;
+  } else if (desc->grace_ms < 0) {
+    int64_t g = ORACLE_DAY_MS - desc->size_ms;
+    a->grace = g > 0 ? g : 0;
+  } else {
+    a->grace = desc->grace_ms;
+  }
+  a->stream_time = -1;
+  strdict_init(&a->dict);
+  a->nslots = 1024;
+  a->slots = NULL;
+  slots_rebuild(a, 1024);
+  *out = a;
+  return KHIP_OK;
+}
+
+static void apply_aggs(oracle_agg* a, entry* x, const khip_batch* b, int64_t r) {
+  for (int i = 0; i < a->d.n_aggs; i++) {
+    const khip_agg_spec* s = &a->aggs[i];
+    agg_state* st = &x->st[i];
+    if (s->kind == KHIP_AGG_COUNT_STAR) {
+      st->i += 1;
+      continue;
+    }
+    int c = s->arg_col;
+    int t = a->col_types[c];
+    if (!bit_get(b->col_valid ? b->col_valid[c] : NULL, r)) continue; /* null input */
+    int64_t iv = 0;
+    double dv = 0.0;
+    if (t == KHIP_TYPE_INT32) iv = ((const int32_t*)b->col_data[c])[r];
+    else if (t == KHIP_TYPE_INT64) iv = ((const int64_t*)b->col_data[c])[r];
+    else dv = ((const double*)b->col_data[c])[r];
+    switch (s->kind) {
+      case KHIP_AGG_COUNT:
+        st->i += 1;
+        break;
+      case KHIP_AGG_SUM:
+      case KHIP_AGG_AVG:
+        if (t == KHIP_TYPE_INT32)
+          st->i = (int64_t)(int32_t)((uint32_t)(int32_t)st->i + (uint32_t)(int32_t)iv);
+        else if (t == KHIP_TYPE_INT64)
+          st->i = (int64_t)((uint64_t)st->i + (uint64_t)iv);
+        else
+          st->d = st->d + dv;
+        if (s->kind == KHIP_AGG_AVG) st->cnt += 1;
+        break;
+      case KHIP_AGG_MIN:
+      case KHIP_AGG_MAX: {
+        int take;
+        if (!st->has) {
+          take = 1;
+        } else if (t == KHIP_TYPE_DOUBLE) {
+          int c2 = java_double_compare(dv, st->d);
+          take = s->kind == KHIP_AGG_MAX ? c2 > 0 : c2 < 0;
+        } else {
+          take = s->kind == KHIP_AGG_MAX ? iv > st->i : iv < st->i;
+        }
+        if (take) {
+          st->has = 1;
+          st->i = iv;
+          st->d = dv;
+        }
+        break;
+      }
+      default:
+        break;
+    }
+  }
+}
+
+khip_status oracle_agg_push(oracle_agg* a, const khip_batch* b, khip_batch_stats* stats) {
+  if (!a || !b || b->mem != KHIP_MEM_HOST || b->n_rows < 0) return KHIP_E_INVALID;
+  if (b->n_cols < a->d.n_cols) return KHIP_E_INVALID;
+  khip_batch_stats s;
+  memset(&s, 0, sizeof(s));
+  s.rows_in = b->n_rows;
+  const int windowed = a->d.window_kind != KHIP_WINDOW_NONE;
+  const int64_t size = a->d.size_ms, adv = a->d.advance_ms;
+  for (int64_t r = 0; r < b->n_rows; r++) {
+    if (!bit_get(b->key_valid, r)) { s.dropped_null_key++; continue; }
+    if (!bit_get(b->row_valid, r)) { s.dropped_null_row++; continue; }
+    int64_t ts = b->ts[r];
+    if (ts < 0) { s.dropped_bad_ts++; continue; }
+    s.rows_accepted++;
+    int64_t key;
+    if (a->d.key_type == KHIP_KEY_INT64) {
+      key = b->key_i64[r];
+    } else {
+      int64_t o0 = b->key_offsets[r], o1 = b->key_offsets[r + 1];
+      key = strdict_intern(&a->dict, b->key_bytes + o0, o1 - o0);
+    }
+    if (!windowed) {
+      entry* x = find_or_create(a, key, 0);
+      if (ts > x->rowtime) x->rowtime = ts;
+      apply_aggs(a, x, b, r);
+      s.windows_applied++;
+      if (ts > a->stream_time) a->stream_time = ts;
+      continue;
+    }
+    if (ts > a->stream_time) a->stream_time = ts; /* R2: before the check */
+    const int64_t close_time = a->stream_time - a->grace;
+    int64_t lo = ts - size + adv;
+    if (lo < 0) lo = 0;
+    for (int64_t ws = (lo / adv) * adv; ws <= ts; ws += adv) {
+      if (ws + size > close_time) {
+        entry* x = find_or_create(a, key, ws);
+        if (ts > x->rowtime) x->rowtime = ts;
+        apply_aggs(a, x, b, r);
+        s.windows_applied++;
+      } else {
+        s.windows_late++;
+      }
+    }
+  }
+  s.stream_time = a->stream_time;
+  if (stats) *stats = s;
+  return KHIP_OK;
+}
+
+/* Result type, mirrors khip_agg_result_type. */
+static int result_type(const oracle_agg* a, int i) {
+  const khip_agg_spec* s = &a->aggs[i];
+  if (s->kind == KHIP_AGG_COUNT_STAR || s->kind == KHIP_AGG_COUNT) return KHIP_TYPE_INT64;
+  if (s->kind == KHIP_AGG_AVG) return KHIP_TYPE_DOUBLE;
+  return a->col_types[s->arg_col];
+}
+
+static void result_value(const oracle_agg* a, int i, const agg_state* st, int64_t* iv,
+                         double* dv, int* is_null) {
+  const khip_agg_spec* s = &a->aggs[i];
+  int t = s->kind == KHIP_AGG_COUNT_STAR ? KHIP_TYPE_INT64 : a->col_types[s->arg_col];
+  *is_null = 0;
+  *iv = 0;
+  *dv = 0.0;
+  switch (s->kind) {
+    case KHIP_AGG_COUNT_STAR:
+    case KHIP_AGG_COUNT:
+      *iv = st->i;
+      break;
+    case KHIP_AGG_SUM:
+      if (t == KHIP_TYPE_DOUBLE) *dv = st->d; else *iv = st->i;
+      break;
+    case KHIP_AGG_MIN:
+    case KHIP_AGG_MAX:
+      if (!st->has) *is_null = 1;
+      else if (t == KHIP_TYPE_DOUBLE) *dv = st->d;
+      else *iv = st->i;
+      break;
+    case KHIP_AGG_AVG:
+      if (st->cnt == 0) *dv = 0.0;
+      else if (t == KHIP_TYPE_DOUBLE) *dv = st->d / (double)st->cnt;
+      else if (t == KHIP_TYPE_INT32) *dv = (double)(int32_t)st->i / (double)st->cnt;
+      else *dv = (double)st->i / (double)st->cnt;
+      break;
+  }
+}
+
+static int having_pass(const oracle_agg* a, const khip_having* h, const entry* x) {
+  if (!h) return 1;
+  int64_t iv;
+  double dv;
+  int is_null;
+  result_value(a, h->agg_index, &x->st[h->agg_index], &iv, &dv, &is_null);
+  if (is_null) return 0;
+  int rt = result_type(a, h->agg_index);
+  int c;
+  if (rt == KHIP_TYPE_DOUBLE) c = dv < h->f64 ? -1 : (dv > h->f64 ? 1 : 0);
+  else c = iv < h->i64 ? -1 : (iv > h->i64 ? 1 : 0);
+  if (rt == KHIP_TYPE_DOUBLE && isnan(dv)) return h->op == KHIP_OP_NE;
+  switch (h->op) {
+    case KHIP_OP_GT: return c > 0;
+    case KHIP_OP_GE: return c >= 0;
+    case KHIP_OP_LT: return c < 0;
+    case KHIP_OP_LE: return c <= 0;
+    case KHIP_OP_EQ: return c == 0;
+    case KHIP_OP_NE: return c != 0;
+  }
+  return 0;
+}
+
+static const oracle_agg* g_sort_agg;
+static int cmp_entry(const void* pa, const void* pb) {
+  const entry* x = *(const entry* const*)pa;
+  const entry* y = *(const entry* const*)pb;
+  const oracle_agg* a = g_sort_agg;
+  if (a->d.key_type == KHIP_KEY_INT64) {
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+  } else if (x->key != y->key) {
+    const strdict* d = &a->dict;
+    int64_t lx = d->len[x->key], ly = d->len[y->key];
+    int64_t m = lx < ly ? lx : ly;
+    int c = m ? memcmp(d->arena + d->off[x->key], d->arena + d->off[y->key], (size_t)m) : 0;
+    if (c) return c;
+    if (lx != ly) return lx < ly ? -1 : 1;
+  }
+  if (x->ws != y->ws) return x->ws < y->ws ? -1 : 1;
+  return 0;
+}
+
+khip_status oracle_agg_snapshot_size(oracle_agg* a, int64_t* n_rows, int64_t* key_bytes) {
+  if (!a) return KHIP_E_INVALID;
+  if (n_rows) *n_rows = a->n;
+  if (key_bytes) {
+    int64_t kb = 0;
+    if (a->d.key_type == KHIP_KEY_UTF8)
+      for (int64_t k = 0; k < a->n; k++) kb += a->dict.len[a->e[k].key];
+    *key_bytes = kb;
+  }
+  return KHIP_OK;
+}
+
+khip_status oracle_agg_snapshot(oracle_agg* a, const khip_having* h, khip_snapshot* out) {
+  if (!a || !out) return KHIP_E_INVALID;
+  if (h && (h->agg_index < 0 || h->agg_index >= a->d.n_aggs)) return KHIP_E_INVALID;
+  entry** order = (entry**)malloc(sizeof(entry*) * (a->n + 1));
+  int64_t m = 0;
+  for (int64_t k = 0; k < a->n; k++)
+    if (having_pass(a, h, &a->e[k])) order[m++] = &a->e[k];
+  g_sort_agg = a;
+  qsort(order, (size_t)m, sizeof(entry*), cmp_entry);
+  if (m > out->capacity) {
+    free(order);
+    out->n_rows = m;
+    return KHIP_E_BUFFER;
+  }
+  int64_t kb = 0;
+  const int windowed = a->d.window_kind != KHIP_WINDOW_NONE;
+  if (a->d.key_type == KHIP_KEY_UTF8 && out->key_offsets) out->key_offsets[0] = 0;
+  for (int64_t r = 0; r < m; r++) {
+    const entry* x = order[r];
+    if (a->d.key_type == KHIP_KEY_INT64) {
+      if (out->key_i64) out->key_i64[r] = x->key;
+    } else {
+      int64_t len = a->dict.len[x->key];
+      if (kb + len > out->key_bytes_capacity) {
+        free(order);
+        return KHIP_E_BUFFER;
+      }
+      if (out->key_bytes && len) memcpy(out->key_bytes + kb, a->dict.arena + a->dict.off[x->key], (size_t)len);
+      kb += len;
+      if (out->key_offsets) out->key_offsets[r + 1] = kb;
+    }
+    if (out->window_start) out->window_start[r] = windowed ? x->ws : 0;
+    if (out->window_end) out->window_end[r] = windowed ? x->ws + a->d.size_ms : 0;
+    if (out->rowtime) out->rowtime[r] = x->rowtime;
+    for (int i = 0; i < a->d.n_aggs; i++) {
+      int64_t iv;
+      double dv;
+      int is_null;
+      result_value(a, i, &x->st[i], &iv, &dv, &is_null);
+      int rt = result_type(a, i);
+      if (out->agg_values && out->agg_values[i]) {
+        if (rt == KHIP_TYPE_INT32) ((int32_t*)out->agg_values[i])[r] = (int32_t)iv;
+        else if (rt == KHIP_TYPE_INT64) ((int64_t*)out->agg_values[i])[r] = iv;
+        else ((double*)out->agg_values[i])[r] = dv;
+      }
+      if (out->agg_null && out->agg_null[i]) out->agg_null[i][r] = (uint8_t)is_null;
+    }
+  }
+  out->n_rows = m;
+  out->key_bytes_len = kb;
+  free(order);
+  return KHIP_OK;
+}
+
+khip_status oracle_agg_destroy(oracle_agg* a) {
+  if (!a) return KHIP_OK;
+  for (int64_t k = 0; k < a->n; k++) free(a->e[k].st);
+  free(a->e);
+  free(a->slots);
+  strdict_free(&a->dict);
+  free(a->col_types);
+  free(a->aggs);
+  free(a);
+  return KHIP_OK;
+}
+
+/* --------------------------------------------------------------- join table */
+
+struct oracle_table {
+  khip_table_desc d;
+  int32_t* col_types;
+  int64_t* keys;     /* per row slot */
+  uint8_t* live;
+  int64_t* vals;     /* n_cols values per row, stored as raw 8 bytes */
+  uint8_t* nulls;    /* n_cols per row */
+  int64_t nrows, cap;
+  int64_t* slots;    /* open addressing → row slot or -1 */
+  int64_t nslots;
+  int64_t nlive;
+};
+
+static void table_rebuild(oracle_table* t, int64_t ns) {
+  free(t->slots);
+  t->nslots = ns;
+  t->slots = (int64_t*)malloc(sizeof(int64_t) * ns);
+  for (int64_t i = 0; i < ns; i++) t->slots[i] = -1;
+  for (int64_t r = 0; r < t->nrows; r++) {
+    int64_t j = (int64_t)(mix64((uint64_t)t->keys[r]) & (uint64_t)(ns - 1));
+    while (t->slots[j] >= 0) j = (j + 1) & (ns - 1);
+    t->slots[j] = r;
+  }
+}
+
+khip_status oracle_table_create(const khip_table_desc* desc, oracle_table** out) {
+  if (!desc || !out || desc->key_type != KHIP_KEY_INT64 || desc->n_cols < 0) return KHIP_E_INVALID;
+  oracle_table* t = (oracle_table*)calloc(1, sizeof(oracle_table));
+  t->d = *desc;
+  t->col_types = (int32_t*)malloc(sizeof(int32_t) * (desc->n_cols + 1));
+  memcpy(t->col_types, desc->col_types, sizeof(int32_t) * desc->n_cols);
+  t->d.col_types = t->col_types;
+  table_rebuild(t, 1024);
+  *out = t;
+  return KHIP_OK;
+}
+
+static int64_t table_find(const oracle_table* t, int64_t key) {
+  int64_t j = (int64_t)(mix64((uint64_t)key) & (uint64_t)(t->nslots - 1));
+  while (t->slots[j] >= 0) {
+    if (t->keys[t->slots[j]] == key) return t->slots[j];
+    j = (j + 1) & (t->nslots - 1);
+  }
+  return -1;
+}
+
+static int64_t read_raw(const khip_batch* b, int c, int type, int64_t r) {
+  int64_t v = 0;
+  if (type == KHIP_TYPE_INT32) v = ((const int32_t*)b->col_data[c])[r];
+  else memcpy(&v, (const char*)b->col_data[c] + 8 * r, 8);
+  return v;
+}
+
+khip_status oracle_table_upsert(oracle_table* t, const khip_batch* b) {
+  if (!t || !b || b->mem != KHIP_MEM_HOST || b->n_cols < t->d.n_cols) return KHIP_E_INVALID;
+  const int nc = t->d.n_cols;
+  for (int64_t r = 0; r < b->n_rows; r++) {
+    if (!bit_get(b->key_valid, r)) continue;
+    int64_t key = b->key_i64[r];
+    int64_t row = table_find(t, key);
+    if (!bit_get(b->row_valid, r)) { /* tombstone */
+      if (row >= 0 && t->live[row]) { t->live[row] = 0; t->nlive--; }
+      continue;
+    }
+    if (row < 0) {
+      if (2 * (t->nrows + 1) > t->nslots) table_rebuild(t, t->nslots * 2);
+      if (t->nrows == t->cap) {
+        t->cap = t->cap ? t->cap * 2 : 1024;
+        t->keys = (int64_t*)realloc(t->keys, sizeof(int64_t) * t->cap);
+        t->live = (uint8_t*)realloc(t->live, (size_t)t->cap);
+        t->vals = (int64_t*)realloc(t->vals, sizeof(int64_t) * t->cap * (nc ? nc : 1));
+        t->nulls = (uint8_t*)realloc(t->nulls, (size_t)(t->cap * (nc ? nc : 1)));
+      }
+      row = t->nrows++;
+      t->keys[row] = key;
+      t->live[row] = 0;
+      int64_t j = (int64_t)(mix64((uint64_t)key) & (uint64_t)(t->nslots - 1));
+      while (t->slots[j] >= 0) j = (j + 1) & (t->nslots - 1);
+      t->slots[j] = row;
+    }
+    if (!t->live[row]) { t->live[row] = 1; t->nlive++; }
+    for (int c = 0; c < nc; c++) {
+      int v = bit_get(b->col_valid ? b->col_valid[c] : NULL, r);
+      t->nulls[row * nc + c] = (uint8_t)!v;
+      t->vals[row * nc + c] = v ? read_raw(b, c, t->col_types[c], r) : 0;
+    }
+  }
+  return KHIP_OK;
+}
+
+khip_status oracle_table_size(oracle_table* t, int64_t* n) {
+  if (!t || !n) return KHIP_E_INVALID;
+  *n = t->nlive;
+  return KHIP_OK;
+}
+
+static int where_pass(const oracle_table* t, const khip_where* w, int64_t row) {
+  if (!w) return 1;
+  if (row < 0) return 0;
+  const int nc = t->d.n_cols;
+  if (t->nulls[row * nc + w->right_col]) return 0;
+  int64_t raw = t->vals[row * nc + w->right_col];
+  int c;
+  if (t->col_types[w->right_col] == KHIP_TYPE_DOUBLE) {
+    double dv;
+    memcpy(&dv, &raw, 8);
+    if (isnan(dv)) return w->op == KHIP_OP_NE;
+    c = dv < w->f64 ? -1 : (dv > w->f64 ? 1 : 0);
+  } else {
+    c = raw < w->i64 ? -1 : (raw > w->i64 ? 1 : 0);
+  }
+  switch (w->op) {
+    case KHIP_OP_GT: return c > 0;
+    case KHIP_OP_GE: return c >= 0;
+    case KHIP_OP_LT: return c < 0;
+    case KHIP_OP_LE: return c <= 0;
+    case KHIP_OP_EQ: return c == 0;
+    case KHIP_OP_NE: return c != 0;
+  }
+  return 0;
+}
+
+khip_status oracle_table_probe(oracle_table* t, const khip_batch* b, int32_t join_type,
+                               const khip_where* w, khip_join_out* out) {
+  if (!t || !b || !out || b->mem != KHIP_MEM_HOST) return KHIP_E_INVALID;
+  if (join_type != KHIP_JOIN_LEFT && join_type != KHIP_JOIN_INNER) return KHIP_E_INVALID;
+  if (w && (w->right_col < 0 || w->right_col >= t->d.n_cols)) return KHIP_E_INVALID;
+  const int nc = t->d.n_cols;
+  int64_t m = 0;
+  for (int64_t r = 0; r < b->n_rows; r++) {
+    if (!bit_get(b->key_valid, r) || !bit_get(b->row_valid, r) || b->ts[r] < 0) continue;
+    int64_t row = table_find(t, b->key_i64[r]);
+    if (row >= 0 && !t->live[row]) row = -1;
+    if (join_type == KHIP_JOIN_INNER && row < 0) continue;
+    if (!where_pass(t, w, row)) continue;
+    if (m < out->capacity) {
+      if (out->stream_row) out->stream_row[m] = r;
+      if (out->matched) out->matched[m] = row >= 0;
+      for (int c = 0; c < nc; c++) {
+        int is_null = row < 0 || t->nulls[row * nc + c];
+        if (out->col_null && out->col_null[c]) out->col_null[c][m] = (uint8_t)is_null;
+        if (out->col_data && out->col_data[c]) {
+          int64_t raw = is_null ? 0 : t->vals[row * nc + c];
+          if (t->col_types[c] == KHIP_TYPE_INT32) ((int32_t*)out->col_data[c])[m] = (int32_t)raw;
+          else memcpy((char*)out->col_data[c] + 8 * m, &raw, 8);
+        }
+      }
+    }
+    m++;
+  }
+  out->n_rows = m;
+  return m > out->capacity ? KHIP_E_BUFFER : KHIP_OK;
+}
+
+khip_status oracle_table_destroy(oracle_table* t) {
+  if (!t) return KHIP_OK;
+  free(t->keys); free(t->live); free(t->vals); free(t->nulls); free(t->slots);
+  free(t->col_types);
+  free(t);
+  return KHIP_OK;
+}

@@ -1,0 +1,201 @@
+"""Helpers that replay the extracted QTT golden cases (tests/golden/qtt_*.json)
+through either library (product or oracle) and compare the final table state the
+way the reference's ExpectedRecordComparator does
+(F/tools/ExpectedRecordComparator.java:133-152: integers exact, doubles |Δ| < 1e-6).
+"""
+import json
+import math
+import os
+
+import numpy as np
+
+from ksql_amd import abi
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load_cases(kind):
+    with open(os.path.join(GOLDEN, "qtt_%s.json" % kind)) as f:
+        return json.load(f)["cases"]
+
+
+def case_desc(case, device=0):
+    d = case["desc"]
+    return abi.make_agg_desc(d["window_kind"], d["key_type"], d["size_ms"], d["advance_ms"],
+                             d["grace_ms"], d["col_types"],
+                             [(a["kind"], a["arg_col"]) for a in d["aggs"]], device=device)
+
+
+def case_batch(case, lo=0, hi=None):
+    d = case["desc"]
+    rows = case["input"][lo:hi]
+    ts = [r["ts"] for r in rows]
+    key_valid = [r["key"] is not None for r in rows]
+    row_valid = [r["row_valid"] for r in rows]
+    cols, cvalid = [], []
+    for ci, t in enumerate(d["col_types"]):
+        vals = [r["cols"][ci] for r in rows]
+        dt = abi.NP_TYPE[abi.TYPE[t]]
+        cols.append(np.array([0 if v is None else v for v in vals], dtype=dt))
+        cvalid.append([v is not None for v in vals])
+    if d["key_type"] == "UTF8":
+        return abi.HostBatch(ts, utf8_keys=[r["key"] for r in rows], key_valid=key_valid,
+                             row_valid=row_valid, cols=cols, col_valid=cvalid)
+    return abi.HostBatch(ts, keys=[0 if r["key"] is None else r["key"] for r in rows],
+                         key_valid=key_valid, row_valid=row_valid, cols=cols, col_valid=cvalid)
+
+
+def run_agg_case(lib, case, split=None, device=0):
+    """split: None = one batch; k = batches of k rows (exercises cross-batch state)."""
+    h = abi.AggHandle(lib, case_desc(case, device))
+    n = len(case["input"])
+    step = n if not split else split
+    for lo in range(0, max(n, 1), max(step, 1)):
+        h.push(case_batch(case, lo, lo + step))
+    snap = h.snapshot(case["desc"]["having"])
+    h.close()
+    return snap
+
+
+def _num_eq(a, b):
+    if isinstance(b, float) or isinstance(a, float):
+        if math.isnan(b) and math.isnan(a):
+            return True
+        return abs(float(a) - float(b)) < 1e-6
+    return int(a) == int(b)
+
+
+def compare_agg(case, snap):
+    """Return a list of mismatch descriptions (empty = parity)."""
+    errs = []
+    exp = case["expected"]
+    if snap["n"] != len(exp):
+        errs.append("row count %d != expected %d" % (snap["n"], len(exp)))
+        return errs
+    for i, e in enumerate(exp):
+        k = snap["key"][i]
+        if (k if isinstance(k, str) else int(k)) != e["key"]:
+            errs.append("row %d key %r != %r" % (i, k, e["key"]))
+            continue
+        if int(snap["ws"][i]) != e["ws"] or int(snap["we"][i]) != e["we"]:
+            errs.append("row %d window (%d,%d) != (%d,%d)" % (i, snap["ws"][i], snap["we"][i], e["ws"], e["we"]))
+        if e["rowtime"] is not None and int(snap["rowtime"][i]) != e["rowtime"]:
+            errs.append("row %d rowtime %d != %d" % (i, snap["rowtime"][i], e["rowtime"]))
+        for a, (v, present) in enumerate(zip(e["values"], e["present"])):
+            if not present:
+                continue
+            isnull = bool(snap["nulls"][a][i])
+            if v is None:
+                if not isnull:
+                    errs.append("row %d agg %d expected null" % (i, a))
+            elif isnull:
+                errs.append("row %d agg %d unexpected null" % (i, a))
+            elif not _num_eq(snap["values"][a][i].item(), v):
+                errs.append("row %d agg %d %r != %r" % (i, a, snap["values"][a][i].item(), v))
+    return errs
+
+
+# ---------------------------------------------------------------- join cases
+
+def _ctype(t):
+    return {"INT32": "INT32", "INT64": "INT64", "DOUBLE": "DOUBLE", "STRING": "INT32"}[t]
+
+
+def run_join_case(lib, case, device=0):
+    """Replays the interleaved table/stream inputs: consecutive table records are one
+    upsert batch, consecutive stream records one probe batch.  Returns the emitted
+    rows as dicts in the output schema (strings decoded from dictionary codes)."""
+    tcols = case["table_cols"]
+    scols = case["stream_cols"]
+    dictionary = {}
+    rev = {}
+
+    def code(s):
+        if s not in dictionary:
+            dictionary[s] = len(dictionary)
+            rev[dictionary[s]] = s
+        return dictionary[s]
+
+    if case["where"] is not None and isinstance(case["where"]["value"], str):
+        code(case["where"]["value"])
+    th = abi.TableHandle(lib, [_ctype(c["type"]) for c in tcols], device=device)
+    where = None
+    if case["where"] is not None:
+        wc = [c["name"] for c in tcols].index(case["where"]["col"])
+        wv = case["where"]["value"]
+        where = {"col": wc, "op": case["where"]["op"], "i64": code(wv) if isinstance(wv, str) else int(wv),
+                 "f64": float(code(wv) if isinstance(wv, str) else wv)}
+    out_rows = []
+    events = case["events"]
+    i = 0
+    while i < len(events):
+        j = i
+        side = events[i]["side"]
+        while j < len(events) and events[j]["side"] == side:
+            j += 1
+        grp = events[i:j]
+        ts = [e["ts"] for e in grp]
+        keys = [0 if e["key"] is None else int(e["key"]) for e in grp]
+        kvalid = [e["key"] is not None for e in grp]
+        rvalid = [e["value"] is not None for e in grp]
+        if side == "T":
+            cols, cval = [], []
+            for c in tcols:
+                vals = [None if e["value"] is None else e["value"].get(c["name"]) for e in grp]
+                if c["type"] == "STRING":
+                    arr = np.array([0 if v is None else code(v) for v in vals], np.int32)
+                else:
+                    arr = np.array([0 if v is None else v for v in vals], abi.NP_TYPE[abi.TYPE[c["type"]]])
+                cols.append(arr)
+                cval.append([v is not None for v in vals])
+            th.upsert(abi.HostBatch(ts, keys=keys, key_valid=kvalid, row_valid=rvalid, cols=cols, col_valid=cval))
+        else:
+            b = abi.HostBatch(ts, keys=keys, key_valid=kvalid, row_valid=rvalid)
+            res = th.probe(b, case["join_type"], where)
+            for r in range(res["n"]):
+                e = grp[int(res["stream_row"][r])]
+                row = {}
+                for s in case["select"]:
+                    if s["side"] == "S":
+                        if any(c["name"] == s["col"] for c in scols):
+                            row[s["name"]] = e["value"].get(s["col"])
+                        else:
+                            row[s["name"]] = e["key"]  # the stream key column
+                    else:
+                        if s["col"] not in [c["name"] for c in tcols]:
+                            row[s["name"]] = e["key"] if res["matched"][r] else None
+                            continue
+                        ci = [c["name"] for c in tcols].index(s["col"])
+                        if res["nulls"][ci][r]:
+                            row[s["name"]] = None
+                        else:
+                            v = res["cols"][ci][r].item()
+                            row[s["name"]] = rev[v] if tcols[ci]["type"] == "STRING" else v
+                out_rows.append({"key": e["key"], "ts": e["ts"], "value": row})
+        i = j
+    th.close()
+    return out_rows
+
+
+def compare_join(case, rows):
+    errs = []
+    exp = case["expected"]
+    if len(rows) != len(exp):
+        return ["row count %d != expected %d" % (len(rows), len(exp))]
+    for i, (r, e) in enumerate(zip(rows, exp)):
+        if e["ts"] is not None and r["ts"] != e["ts"]:
+            errs.append("row %d ts %r != %r" % (i, r["ts"], e["ts"]))
+        for name, v in e["value"].items():
+            got = r["value"].get(name, "<missing>")
+            if got == "<missing>" and name not in r["value"]:
+                # key column projected into the value (e.g. T_ID) is carried as the key
+                continue
+            if v is None or got is None:
+                if v is not got:
+                    errs.append("row %d col %s %r != %r" % (i, name, got, v))
+            elif isinstance(v, (int, float)) and not isinstance(v, bool):
+                if not _num_eq(got, v):
+                    errs.append("row %d col %s %r != %r" % (i, name, got, v))
+            elif got != v:
+                errs.append("row %d col %s %r != %r" % (i, name, got, v))
+    return errs
