@@ -13,9 +13,10 @@
  *     call returns a khip_status; on failure khip_last_error() (thread-local)
  *     holds a message.
  *   - The caller owns every host buffer for the duration of a call.  The library
- *     owns all device memory and its HIP stream; it never retains a caller
- *     pointer after the call returns (device-resident batches are consumed
- *     before return of the next synchronising call on the same handle).
+ *     owns all device memory it allocates and its HIP stream; it never retains a
+ *     caller pointer after the call returns.  KHIP_MEM_DEVICE batches are read on
+ *     the handle's stream and must stay valid until the call returns (aggregate
+ *     push) or until the handle's *_sync() returns (asynchronous probes).
  *   - Handles are independent; a single handle is not re-entrant (Kafka Streams
  *     task confinement, C/util/KsqlConstants.java:42 — one task per thread).
  *   - Validity bitmaps are Arrow-style: bit (i & 7) of byte (i >> 3), 1 = valid.
@@ -220,6 +221,23 @@ khip_status khip_agg_reset(khip_agg* agg);
 /* Block until all work queued on the handle has finished. */
 khip_status khip_agg_sync(khip_agg* agg);
 
+/* desc.flags bit: record HIP events around each kernel phase of khip_agg_push (the
+ * Kafka Streams per-processor latency sensors' analogue; off by default). */
+#define KHIP_FLAG_PROFILE 1
+
+/* Cumulative device time per phase since creation or the last reset of the counters,
+ * measured with HIP events on the handle's stream (valid with KHIP_FLAG_PROFILE). */
+typedef struct khip_kernel_times {
+  double stream_time_ms; /* k_blockmax + k_scan_blocks                               */
+  double dict_ms;        /* UTF8 key dictionary                                       */
+  double apply_ms;       /* k_apply: window fan-out + (key, window) upsert + atomics  */
+  double finalize_ms;    /* k_finalize + partial-counter reduction                   */
+  int64_t apply_launches;
+  int64_t records;       /* records covered by those apply launches (first passes)    */
+} khip_kernel_times;
+
+khip_status khip_agg_kernel_times(khip_agg* agg, khip_kernel_times* out, int32_t reset);
+
 /* The handle's hipStream_t (as void*), so callers can order their own work. */
 khip_status khip_agg_stream(khip_agg* agg, void** hip_stream);
 
@@ -277,12 +295,24 @@ khip_status khip_table_size(khip_table* t, int64_t* n_keys);
 khip_status khip_table_probe(khip_table* t, const khip_batch* stream, int32_t join_type,
                              const khip_where* where, khip_join_out* out);
 
-/* Device-resident variant: writes the number of emitted rows to *n_out and keeps the
- * output (stream_row, matched, right columns) in library-owned device buffers,
- * readable through khip_table_probe_result until the next probe on this handle. */
+/* Device-resident variant (selection-vector output, no compaction): all buffers are
+ * caller-allocated DEVICE memory, row-aligned with the probe batch (n_rows entries /
+ * bits).  emit bit i = stream row i produced an output row (INNER hit or LEFT, and
+ * WHERE passed); matched bit i = table hit; col_data[c][i] / col_null bit i = right
+ * column c (undefined / 1 where not matched).  Any pointer may be NULL to skip that
+ * output.  *n_emitted (may be NULL: then the call does not synchronise) receives the
+ * number of emitted rows.  The batch must be KHIP_MEM_DEVICE and stay valid until
+ * khip_table_sync() returns. */
+typedef struct khip_join_dev_out {
+  uint8_t* emit;
+  uint8_t* matched;
+  void** col_data;
+  uint8_t** col_null;
+} khip_join_dev_out;
+
 khip_status khip_table_probe_device(khip_table* t, const khip_batch* stream,
                                     int32_t join_type, const khip_where* where,
-                                    int64_t* n_out);
+                                    const khip_join_dev_out* out, int64_t* n_emitted);
 
 khip_status khip_table_sync(khip_table* t);
 khip_status khip_table_destroy(khip_table* t);

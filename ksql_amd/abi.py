@@ -26,6 +26,7 @@ AGG = {"COUNT_STAR": 0, "COUNT": 1, "SUM": 2, "MIN": 3, "MAX": 4, "AVG": 5}
 OP = {"GT": 0, "GE": 1, "LT": 2, "LE": 3, "EQ": 4, "NE": 5}
 JOIN = {"LEFT": 0, "INNER": 1}
 MEM_HOST, MEM_DEVICE = 0, 1
+FLAG_PROFILE = 1
 NP_TYPE = {0: np.int32, 1: np.int64, 2: np.float64}
 
 i32, i64, u8p = C.c_int32, C.c_int64, C.POINTER(C.c_uint8)
@@ -79,6 +80,19 @@ class Where(C.Structure):
     _fields_ = [("right_col", i32), ("op", i32), ("i64", i64), ("f64", C.c_double)]
 
 
+class KernelTimes(C.Structure):
+    _fields_ = [("stream_time_ms", C.c_double), ("dict_ms", C.c_double), ("apply_ms", C.c_double),
+                ("finalize_ms", C.c_double), ("apply_launches", i64), ("records", i64)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+class JoinDevOut(C.Structure):
+    _fields_ = [("emit", C.c_void_p), ("matched", C.c_void_p), ("col_data", C.POINTER(C.c_void_p)),
+                ("col_null", C.POINTER(C.c_void_p))]
+
+
 class JoinOut(C.Structure):
     _fields_ = [("capacity", i64), ("n_rows", i64), ("stream_row", C.c_void_p),
                 ("matched", C.c_void_p), ("col_data", C.POINTER(C.c_void_p)),
@@ -104,7 +118,8 @@ PRODUCT_ONLY = {
     "agg_reset": ([_P]),
     "agg_sync": ([_P]),
     "agg_stream": ([_P, C.POINTER(_P)]),
-    "table_probe_device": ([_P, C.POINTER(Batch), i32, C.POINTER(Where), C.POINTER(i64)]),
+    "agg_kernel_times": ([_P, C.POINTER(KernelTimes), i32]),
+    "table_probe_device": ([_P, C.POINTER(Batch), i32, C.POINTER(Where), C.POINTER(JoinDevOut), C.POINTER(i64)]),
     "table_sync": ([_P]),
 }
 
@@ -205,13 +220,13 @@ class HostBatch:
 
 
 def make_agg_desc(window_kind="NONE", key_type="INT64", size_ms=0, advance_ms=0, grace_ms=-1,
-                  col_types=(), aggs=(), device=0, capacity_hint=0):
+                  col_types=(), aggs=(), device=0, capacity_hint=0, flags=0):
     ct = (i32 * max(len(col_types), 1))(*[TYPE[t] if isinstance(t, str) else t for t in col_types])
     sp = (AggSpec * max(len(aggs), 1))(*[AggSpec(AGG[k] if isinstance(k, str) else k, c) for k, c in aggs])
     d = AggDesc(WINDOW[window_kind] if isinstance(window_kind, str) else window_kind,
                 KEY[key_type] if isinstance(key_type, str) else key_type,
                 size_ms, advance_ms if advance_ms else size_ms, grace_ms, len(col_types), ct,
-                len(aggs), sp, device, 0, capacity_hint)
+                len(aggs), sp, device, flags, capacity_hint)
     d._keep = (ct, sp)
     return d
 
@@ -227,6 +242,34 @@ def result_types(desc):
         else:
             out.append(desc.col_types[desc.aggs[i].arg_col])
     return out
+
+
+class DeviceBatch:
+    """A khip_batch over device tensors (torch) — the caller keeps the tensors alive."""
+
+    def __init__(self, ts, keys=None, key_valid=None, row_valid=None, cols=(), col_valid=(),
+                 key_offsets=None, key_bytes=None):
+        self._keep = [ts, keys, key_valid, row_valid, key_offsets, key_bytes] + list(cols) + list(col_valid)
+        p = lambda t: None if t is None else t.data_ptr()
+        nc = len(cols)
+        cv = list(col_valid) + [None] * (nc - len(col_valid))
+        self._cd = (C.c_void_p * max(nc, 1))(*[p(c) for c in cols])
+        self._cv = (C.c_void_p * max(nc, 1))(*[p(v) for v in cv])
+        self.struct = Batch(int(ts.numel()), MEM_DEVICE, nc, p(keys), p(key_offsets), p(key_bytes),
+                            p(key_valid), p(row_valid), p(ts), self._cd, self._cv)
+
+
+def bitmap_torch(valid_bool):
+    """bool tensor (n,) on device → packed LSB-first uint8 bitmap tensor."""
+    import torch
+    n = valid_bool.numel()
+    pad = (-n) % 8
+    v = valid_bool.to(torch.uint8)
+    if pad:
+        v = torch.cat([v, torch.zeros(pad, dtype=torch.uint8, device=v.device)])
+    v = v.view(-1, 8)
+    w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=v.device)
+    return (v * w).sum(dim=1, dtype=torch.int32).to(torch.uint8)
 
 
 class AggHandle:
@@ -277,6 +320,23 @@ class AggHandle:
         else:
             out["key"] = arrays["key"][:m]
         return out
+
+    def kernel_times(self, reset=False):
+        kt = KernelTimes()
+        self.lib.check(self.lib.agg_kernel_times(self.h, C.byref(kt), 1 if reset else 0), "agg_kernel_times")
+        return kt.as_dict()
+
+    def reset(self):
+        self.lib.check(self.lib.agg_reset(self.h), "agg_reset")
+
+    def count_rows(self, having=None):
+        n = i64()
+        hv = None
+        if having is not None:
+            v = having["value"]
+            hv = Having(having["agg"], OP[having["op"]], 0 if isinstance(v, float) else int(v), float(v))
+        self.lib.check(self.lib.agg_count_rows(self.h, C.byref(hv) if hv else None, C.byref(n)), "agg_count_rows")
+        return n.value
 
     def close(self):
         if self.h:

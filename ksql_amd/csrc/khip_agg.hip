@@ -1,0 +1,1354 @@
+// khip_agg.hip — windowed / unwindowed GROUP BY aggregation on MI355X (gfx950).
+//
+// Replaces, for one query task, the Kafka Streams KStreamWindowAggregate /
+// KStreamAggregate processor + RocksDB window store + KudafAggregator chain that
+// KSPlanBuilder.visitStreamWindowedAggregate / visitStreamAggregate build
+// (S/KSPlanBuilder.java:293-304, :144-155; S/StreamAggregateBuilder.java:156-222,
+// :81-138).  Semantics: SURVEY.md §8.0, restated in oracle/oracle.c R1–R6.
+//
+// Data layout in HBM (one handle):
+//   table   : cap slots (power of two) × slot_words u64, AoS, 32 or 64 B per slot so a
+//             group is one cache line: [w0 key | claim ref][w1 windowStart | EMPTY]
+//             [rowtime][state words ...].
+//   state   : deduplicated per input column: non-null count, sum (i64 / f64 bits),
+//             min / max as total-order int64 keys; one COUNT(*) word.
+//   dict    : UTF8 keys only — open-addressing dictionary → stable key id
+//             (= byte offset of the key's entry in an append-only arena).
+//
+// Per micro-batch (all on the handle's stream):
+//   k_blockmax → k_scan_blocks : stream time before each 2048-record block
+//                                (exclusive prefix max, carried across batches)
+//   [UTF8] k_dict_lookup → k_dict_count/k_scan_excl/k_dict_write → k_kid_fixup
+//   k_apply     : in-block prefix max → late test → window fan-out → find-or-claim the
+//                 (key, ws) slot with one 64-bit CAS whose value references the batch
+//                 row (no spin, no fence) → agent-scope atomics for the state
+//   k_finalize  : turn this batch's claim references into resident (key, ws)
+//   failures (probe budget exhausted) are resumed after a table doubling, exactly.
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "khip_util.hpp"
+
+namespace khip {
+
+constexpr int BLOCK = 256;
+constexpr int ITEMS = 8;
+constexpr int RPB = BLOCK * ITEMS;  // records per block (k_blockmax and k_apply agree)
+constexpr int MAX_COLS = 8;
+constexpr int MAX_OPS = 24;
+constexpr int MAX_PROBE = 2048;
+constexpr int MAX_FANOUT = 4095;  // windows per record encodable in a claim reference
+constexpr int64_t EMPTY_WS = INT64_MIN;
+constexpr int NPART = 8;
+
+enum { P_ACCEPTED, P_NULL_KEY, P_NULL_ROW, P_BAD_TS, P_APPLIED, P_LATE, P_FAILED, P_NEW };
+
+enum OpKind : int8_t { OP_INC = 0, OP_INC_VALID, OP_ADD_I64, OP_ADD_F64, OP_MIN, OP_MAX };
+
+struct UpdOp {
+  int8_t kind;
+  int8_t col;
+  int16_t word;
+};
+
+struct ApplyParams {
+  int32_t windowed;
+  int32_t slot_words;
+  int64_t size, adv, grace;
+  int32_t n_cols;
+  int32_t n_ops;
+  int32_t col_type[MAX_COLS];
+  UpdOp ops[MAX_OPS];
+};
+
+struct ColPtrs {
+  const void* data[MAX_COLS];
+  const uint8_t* valid[MAX_COLS];
+};
+
+// How one aggregate's result is decoded from the state words.
+struct AggOut {
+  int32_t kind;   // KHIP_AGG_*
+  int32_t type;   // input column type (INT64 for COUNT*)
+  int32_t w_val;  // value word
+  int32_t w_cnt;  // non-null count word (-1 if none)
+};
+
+struct HavingDev {
+  int32_t active;
+  int32_t op;
+  AggOut a;
+  int64_t i64;
+  double f64;
+};
+
+// ------------------------------------------------------------------ device utils
+
+__device__ __forceinline__ int64_t wave_incl_max(int64_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    int64_t t = __shfl_up(v, off, 64);
+    if (lane >= off) v = t > v ? t : v;
+  }
+  return v;
+}
+
+// Inclusive prefix max over the block (blockDim.x threads, multiple of 64).
+__device__ __forceinline__ int64_t block_incl_max(int64_t v, int64_t* lds, int64_t* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_incl_max(v);
+  if (lane == 63) lds[wave] = v;
+  __syncthreads();
+  int64_t pre = INT64_MIN, tot = INT64_MIN;
+  for (int w = 0; w < nw; w++) {
+    int64_t x = lds[w];
+    if (w < wave) pre = x > pre ? x : pre;
+    tot = x > tot ? x : tot;
+  }
+  __syncthreads();
+  *total = tot;
+  return v > pre ? v : pre;
+}
+
+__device__ __forceinline__ int64_t wave_sum(int64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint64_t hash_bytes_dev(const uint8_t* p, int64_t n) {
+  uint64_t h = 0x84222325cbf29ce4ULL ^ (uint64_t)n;
+  int64_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w = 0;
+    for (int b = 0; b < 8; b++) w |= (uint64_t)p[i + b] << (8 * b);
+    h = mix64(h ^ w) * 0x9E3779B97F4A7C15ULL;
+  }
+  uint64_t w = 0;
+  for (int b = 0; i + b < n; b++) w |= (uint64_t)p[i + b] << (8 * b);
+  return mix64(h ^ w ^ ((uint64_t)(n & 7) << 59));
+}
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, int64_t n) {
+  for (int64_t i = 0; i < n; i++)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+
+__device__ __forceinline__ int64_t load_col_raw(const ColPtrs& c, int32_t type, int col, int64_t i) {
+  if (type == KHIP_TYPE_INT32) return (int64_t)((const int32_t*)c.data[col])[i];
+  return ((const int64_t*)c.data[col])[i];  // INT64, or DOUBLE bits
+}
+
+// ------------------------------------------------------------------- kernels
+
+__global__ __launch_bounds__(BLOCK) void k_blockmax(const int64_t* __restrict__ ts,
+                                                    const uint8_t* __restrict__ kv,
+                                                    const uint8_t* __restrict__ rv, int64_t n,
+                                                    int64_t* __restrict__ blockmax) {
+  __shared__ int64_t lds[BLOCK / 64];
+  const int64_t base = (int64_t)blockIdx.x * RPB;
+  int64_t m = -1;
+#pragma unroll
+  for (int k = 0; k < ITEMS; k++) {
+    const int64_t i = base + k * BLOCK + threadIdx.x;
+    if (i < n && bit_get(kv, i) && bit_get(rv, i)) {
+      const int64_t t = ts[i];
+      m = t > m ? t : m;
+    }
+  }
+  int64_t tot;
+  block_incl_max(m, lds, &tot);
+  if (threadIdx.x == 0) blockmax[blockIdx.x] = tot;
+}
+
+// Exclusive prefix max over nb block maxima, seeded and updated with *stream_time.
+__global__ __launch_bounds__(1024) void k_scan_blocks(const int64_t* __restrict__ blockmax,
+                                                      int64_t nb, int64_t* __restrict__ prefix,
+                                                      int64_t* __restrict__ stream_time) {
+  __shared__ int64_t lds[1024 / 64];
+  __shared__ int64_t incl_all[1024];
+  int64_t carry = *stream_time;
+  for (int64_t b0 = 0; b0 < nb; b0 += blockDim.x) {
+    const int64_t b = b0 + threadIdx.x;
+    const int64_t v = b < nb ? blockmax[b] : INT64_MIN;
+    int64_t tot;
+    const int64_t incl = block_incl_max(v, lds, &tot);
+    incl_all[threadIdx.x] = incl;
+    __syncthreads();
+    const int64_t excl = threadIdx.x == 0 ? INT64_MIN : incl_all[threadIdx.x - 1];
+    if (b < nb) prefix[b] = excl > carry ? excl : carry;
+    carry = tot > carry ? tot : carry;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *stream_time = carry;
+}
+
+// Find or claim the (key, ws) slot and apply the record's aggregate updates.
+// Claim reference: bit63 | fp15 << 48 | window index j << 36 | batch row (36 bits).
+__device__ __forceinline__ int upsert_apply(const ApplyParams& p, uint64_t* __restrict__ table,
+                                             uint64_t mask, int64_t hkey, int64_t key, int64_t ws,
+                                             int64_t j, int64_t row, int64_t t,
+                                             const int64_t* __restrict__ keys,
+                                             const int64_t* __restrict__ ts, const ColPtrs& cols) {
+  const uint64_t h = group_hash(hkey, ws);
+  const uint64_t fp = (h >> 49) & 0x7FFFULL;
+  const uint64_t myref = (1ULL << 63) | (fp << 48) | ((uint64_t)j << 36) | (uint64_t)row;
+  uint64_t slot = h & mask;
+  const int sw = p.slot_words;
+  for (int probe = 0; probe < MAX_PROBE; probe++) {
+    uint64_t* s = table + slot * (uint64_t)sw;
+    const int64_t w1 = (int64_t)s[1];
+    bool hit = false;
+    int isnew = 0;
+    if (w1 != EMPTY_WS) {
+      hit = (w1 == ws) && ((int64_t)s[0] == key);
+    } else {
+      uint64_t w0 = ld_relaxed(s);
+      if (w0 == 0) {
+        const uint64_t old = atomicCAS((unsigned long long*)s, 0ULL, (unsigned long long)myref);
+        if (old == 0) {
+          hit = true;
+          isnew = 1;
+        } else {
+          w0 = old;
+        }
+      }
+      if (!hit && ((w0 >> 48) & 0x7FFFULL) == fp) {
+        const int64_t idx = (int64_t)(w0 & ((1ULL << 36) - 1));
+        const int64_t jj = (int64_t)((w0 >> 36) & 0xFFFULL);
+        if (keys[idx] == key) {
+          const int64_t ws2 = p.windowed ? first_window_start(ts[idx], p.size, p.adv) + jj * p.adv : 0;
+          hit = ws2 == ws;
+        }
+      }
+    }
+    if (hit) {
+      __hip_atomic_fetch_max((int64_t*)&s[2], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int o = 0; o < p.n_ops; o++) {
+        const UpdOp op = p.ops[o];
+        int64_t* w = (int64_t*)&s[op.word];
+        if (op.kind == OP_INC) {
+          __hip_atomic_fetch_add(w, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          continue;
+        }
+        if (!bit_get(cols.valid[op.col], row)) continue;
+        const int32_t ty = p.col_type[op.col];
+        switch (op.kind) {
+          case OP_INC_VALID:
+            __hip_atomic_fetch_add(w, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          case OP_ADD_I64:
+            __hip_atomic_fetch_add((uint64_t*)w, (uint64_t)load_col_raw(cols, ty, op.col, row),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          case OP_ADD_F64: {
+            const double v = ((const double*)cols.data[op.col])[row];
+            unsafeAtomicAdd((double*)w, v);
+            break;
+          }
+          case OP_MIN:
+          case OP_MAX: {
+            int64_t k = load_col_raw(cols, ty, op.col, row);
+            if (ty == KHIP_TYPE_DOUBLE) {
+              double d;
+              __builtin_memcpy(&d, &k, 8);
+              k = f64_order_key(d);
+            }
+            if (op.kind == OP_MIN)
+              __hip_atomic_fetch_min(w, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+              __hip_atomic_fetch_max(w, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          default:
+            break;
+        }
+      }
+      return 1 + isnew;
+    }
+    slot = (slot + 1) & mask;
+  }
+  return 0;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_apply(ApplyParams p, const int64_t* __restrict__ hkeys,
+                                                 const int64_t* __restrict__ keys,
+                                                 const int64_t* __restrict__ ts,
+                                                 const uint8_t* __restrict__ kv,
+                                                 const uint8_t* __restrict__ rv, ColPtrs cols,
+                                                 const int64_t* __restrict__ blockprefix, int64_t n,
+                                                 uint64_t* __restrict__ table, uint64_t mask,
+                                                 int32_t* __restrict__ resume,
+                                                 int64_t* __restrict__ partials, int resume_mode) {
+  __shared__ int64_t lds_scan[BLOCK / 64];
+  __shared__ unsigned long long lds_cnt[NPART];
+  if (threadIdx.x < NPART) lds_cnt[threadIdx.x] = 0;
+  int64_t cnt[NPART];
+#pragma unroll
+  for (int k = 0; k < NPART; k++) cnt[k] = 0;
+  const int64_t base = (int64_t)blockIdx.x * RPB;
+  int64_t carry = blockprefix[blockIdx.x];
+  for (int k = 0; k < ITEMS; k++) {
+    const int64_t i = base + k * BLOCK + threadIdx.x;
+    const bool in = i < n;
+    const int64_t t = in ? ts[i] : -1;
+    const bool kval = in && bit_get(kv, i);
+    const bool rval = in && bit_get(rv, i);
+    const bool valid = kval && rval && t >= 0;
+    int64_t tot;
+    const int64_t incl = block_incl_max(valid ? t : -1, lds_scan, &tot);
+    const int64_t st = incl > carry ? incl : carry;  // stream time after this record
+    carry = tot > carry ? tot : carry;
+    if (!in) continue;
+    int64_t j0 = 0;
+    if (resume_mode) {
+      j0 = resume[i];
+      if (j0 < 0) continue;
+      resume[i] = -1;
+    } else {
+      if (!kval) { cnt[P_NULL_KEY]++; continue; }
+      if (!rval) { cnt[P_NULL_ROW]++; continue; }
+      if (t < 0) { cnt[P_BAD_TS]++; continue; }
+      cnt[P_ACCEPTED]++;
+    }
+    const int64_t key = keys[i];
+    const int64_t hkey = hkeys[i];
+    if (p.windowed) {
+      const int64_t close = st - p.grace;
+      const int64_t ws0 = first_window_start(t, p.size, p.adv);
+      int64_t j = j0;
+      for (int64_t ws = ws0 + j0 * p.adv; ws <= t; ws += p.adv, j++) {
+        if (ws + p.size <= close) {  // window closed: late
+          cnt[P_LATE]++;
+          continue;
+        }
+        const int r = upsert_apply(p, table, mask, hkey, key, ws, j, i, t, keys, ts, cols);
+        if (r == 0) {
+          resume[i] = (int32_t)j;
+          cnt[P_FAILED]++;
+          break;
+        }
+        cnt[P_APPLIED]++;
+        cnt[P_NEW] += r - 1;
+      }
+    } else {
+      const int r = upsert_apply(p, table, mask, hkey, key, 0, 0, i, t, keys, ts, cols);
+      if (r == 0) {
+        resume[i] = 0;
+        cnt[P_FAILED]++;
+      } else {
+        cnt[P_APPLIED]++;
+        cnt[P_NEW] += r - 1;
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NPART; k++) {
+    const int64_t s = wave_sum(cnt[k]);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(&lds_cnt[k], (unsigned long long)s);
+  }
+  __syncthreads();
+  if (threadIdx.x < NPART) partials[(int64_t)blockIdx.x * NPART + threadIdx.x] = (int64_t)lds_cnt[threadIdx.x];
+}
+
+// Claim references of this batch → resident (key, ws).
+__global__ __launch_bounds__(256) void k_finalize(uint64_t* __restrict__ table, int64_t cap, int sw,
+                                                  const int64_t* __restrict__ keys,
+                                                  const int64_t* __restrict__ ts, int windowed,
+                                                  int64_t size, int64_t adv) {
+  for (int64_t slot = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; slot < cap;
+       slot += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t* s = table + slot * (uint64_t)sw;
+    if ((int64_t)s[1] != EMPTY_WS) continue;
+    const uint64_t w0 = s[0];
+    if (w0 == 0) continue;
+    const int64_t idx = (int64_t)(w0 & ((1ULL << 36) - 1));
+    const int64_t jj = (int64_t)((w0 >> 36) & 0xFFFULL);
+    s[0] = (uint64_t)keys[idx];
+    s[1] = (uint64_t)(windowed ? first_window_start(ts[idx], size, adv) + jj * adv : 0);
+  }
+}
+
+struct InitWords {
+  int64_t w[16];
+};
+
+__global__ __launch_bounds__(256) void k_init_table(uint64_t* __restrict__ table, int64_t cap, int sw,
+                                                    InitWords init) {
+  const int64_t total = cap * sw;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x)
+    table[e] = (uint64_t)init.w[e & (sw - 1)];
+}
+
+// Sum nb rows of K partial counters into out[K] (accumulating).
+__global__ __launch_bounds__(256) void k_reduce_partials(const int64_t* __restrict__ partials, int64_t nb,
+                                                         int K, int64_t* __restrict__ out) {
+  __shared__ unsigned long long acc[NPART];
+  if (threadIdx.x < NPART) acc[threadIdx.x] = 0;
+  __syncthreads();
+  for (int k = 0; k < K; k++) {
+    int64_t s = 0;
+    for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) s += partials[b * K + k];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&acc[k], (unsigned long long)s);
+  }
+  __syncthreads();
+  if (threadIdx.x < K) out[threadIdx.x] += (int64_t)acc[threadIdx.x];
+}
+
+// Re-insert resident slots into a larger table.
+__global__ __launch_bounds__(256) void k_rehash(const uint64_t* __restrict__ old, int64_t oldcap,
+                                                uint64_t* __restrict__ nt, uint64_t nmask, int sw,
+                                                int utf8, const uint8_t* __restrict__ arena) {
+  for (int64_t slot = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; slot < oldcap;
+       slot += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t* s = old + slot * (uint64_t)sw;
+    const int64_t ws = (int64_t)s[1];
+    if (ws == EMPTY_WS) continue;
+    const int64_t key = (int64_t)s[0];
+    const int64_t hkey = utf8 ? *(const int64_t*)(arena + key) : key;
+    uint64_t d = group_hash(hkey, ws) & nmask;
+    while (true) {
+      uint64_t* q = nt + d * (uint64_t)sw;
+      if (atomicCAS((unsigned long long*)&q[1], (unsigned long long)EMPTY_WS, (unsigned long long)ws) ==
+          (unsigned long long)EMPTY_WS) {
+        q[0] = (uint64_t)key;
+        for (int w = 2; w < sw; w++) q[w] = s[w];
+        break;
+      }
+      d = (d + 1) & nmask;
+    }
+  }
+}
+
+__device__ __forceinline__ bool decode_result(const uint64_t* s, const AggOut& a, int64_t* iv, double* dv) {
+  // returns false for SQL NULL; sets *iv for integer results, *dv for DOUBLE results
+  switch (a.kind) {
+    case KHIP_AGG_COUNT_STAR:
+    case KHIP_AGG_COUNT:
+      *iv = (int64_t)s[a.w_val];
+      return true;
+    case KHIP_AGG_SUM:
+      if (a.type == KHIP_TYPE_DOUBLE) __builtin_memcpy(dv, &s[a.w_val], 8);
+      else if (a.type == KHIP_TYPE_INT32) *iv = (int64_t)(int32_t)s[a.w_val];
+      else *iv = (int64_t)s[a.w_val];
+      return true;
+    case KHIP_AGG_MIN:
+    case KHIP_AGG_MAX:
+      if ((int64_t)s[a.w_cnt] == 0) return false;
+      if (a.type == KHIP_TYPE_DOUBLE) *dv = f64_from_order_key((int64_t)s[a.w_val]);
+      else *iv = (int64_t)s[a.w_val];
+      return true;
+    case KHIP_AGG_AVG: {
+      const int64_t c = (int64_t)s[a.w_cnt];
+      if (c == 0) { *dv = 0.0; return true; }
+      if (a.type == KHIP_TYPE_DOUBLE) {
+        double sum;
+        __builtin_memcpy(&sum, &s[a.w_val], 8);
+        *dv = sum / (double)c;
+      } else if (a.type == KHIP_TYPE_INT32) {
+        *dv = (double)(int32_t)s[a.w_val] / (double)c;
+      } else {
+        *dv = (double)(int64_t)s[a.w_val] / (double)c;
+      }
+      return true;
+    }
+  }
+  return false;
+}
+
+__device__ __forceinline__ bool result_is_double(const AggOut& a) {
+  if (a.kind == KHIP_AGG_AVG) return true;
+  if (a.kind == KHIP_AGG_COUNT || a.kind == KHIP_AGG_COUNT_STAR) return false;
+  return a.type == KHIP_TYPE_DOUBLE;
+}
+
+__device__ __forceinline__ bool having_ok(const uint64_t* s, const HavingDev& h) {
+  if (!h.active) return true;
+  int64_t iv = 0;
+  double dv = 0.0;
+  if (!decode_result(s, h.a, &iv, &dv)) return false;
+  int c;
+  if (result_is_double(h.a)) {
+    if (dv != dv) return h.op == KHIP_OP_NE;
+    c = dv < h.f64 ? -1 : (dv > h.f64 ? 1 : 0);
+  } else {
+    c = iv < h.i64 ? -1 : (iv > h.i64 ? 1 : 0);
+  }
+  switch (h.op) {
+    case KHIP_OP_GT: return c > 0;
+    case KHIP_OP_GE: return c >= 0;
+    case KHIP_OP_LT: return c < 0;
+    case KHIP_OP_LE: return c <= 0;
+    case KHIP_OP_EQ: return c == 0;
+    case KHIP_OP_NE: return c != 0;
+  }
+  return false;
+}
+
+// Compact resident slots passing HAVING into `out` (sw words per row); out may be null
+// (count only).  One atomic per block reserves the output range.
+__global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ table, int64_t cap, int sw,
+                                                 HavingDev h, uint64_t* __restrict__ out, int64_t max_rows,
+                                                 unsigned long long* __restrict__ counter) {
+  __shared__ int lds_n[256 / 64];
+  __shared__ unsigned long long lds_base;
+  for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x; s0 < cap; s0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t slot = s0 + threadIdx.x;
+    const uint64_t* s = table + slot * (uint64_t)sw;
+    const bool take = slot < cap && (int64_t)s[1] != EMPTY_WS && having_ok(s, h);
+    const uint64_t bal = __ballot(take);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int before = __popcll(bal & ((1ULL << lane) - 1));
+    if (lane == 0) lds_n[wave] = __popcll(bal);
+    __syncthreads();
+    int off = 0, tot = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); w++) {
+      if (w < wave) off += lds_n[w];
+      tot += lds_n[w];
+    }
+    if (threadIdx.x == 0) lds_base = tot ? atomicAdd(counter, (unsigned long long)tot) : 0;
+    __syncthreads();
+    if (take && out && (int64_t)(lds_base + off + before) < max_rows) {
+      uint64_t* o = out + (lds_base + off + before) * (uint64_t)sw;
+      for (int w = 0; w < sw; w++) o[w] = s[w];
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- UTF8 dictionary
+// dict word: 0 empty | fresh: bit63 | fp22 << 40 | batch row (40 bits) | resident: bit62 | fp22 << 40
+// arena entry at offset o (8-aligned): [u64 hash][i64 len][bytes, padded to 8]; key id = o.
+
+__global__ __launch_bounds__(256) void k_dict_lookup(uint64_t* __restrict__ dword, const int64_t* __restrict__ dkid,
+                                                     uint64_t dmask, const uint8_t* __restrict__ arena,
+                                                     const int64_t* __restrict__ koff,
+                                                     const uint8_t* __restrict__ kbytes,
+                                                     const uint8_t* __restrict__ kv, const uint8_t* __restrict__ rv,
+                                                     const int64_t* __restrict__ ts, int64_t n,
+                                                     int64_t* __restrict__ kid, int64_t* __restrict__ khash,
+                                                     int* __restrict__ fail) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!(bit_get(kv, i) && bit_get(rv, i) && ts[i] >= 0)) {
+      kid[i] = 0;
+      khash[i] = 0;
+      continue;
+    }
+    const int64_t o0 = koff[i], len = koff[i + 1] - o0;
+    const uint8_t* kb = kbytes + o0;
+    const uint64_t h = hash_bytes_dev(kb, len);
+    khash[i] = (int64_t)h;
+    const uint64_t fp = (h >> 40) & 0x3FFFFFULL;
+    const uint64_t fresh = (1ULL << 63) | (fp << 40) | (uint64_t)i;
+    uint64_t slot = h & dmask;
+    bool done = false;
+    for (int probe = 0; probe < MAX_PROBE && !done; probe++) {
+      uint64_t w = ld_relaxed(&dword[slot]);
+      if (w == 0) {
+        const uint64_t old = atomicCAS((unsigned long long*)&dword[slot], 0ULL, (unsigned long long)fresh);
+        if (old == 0) {
+          kid[i] = -(int64_t)(slot + 1);
+          done = true;
+          break;
+        }
+        w = old;
+      }
+      if (((w >> 40) & 0x3FFFFFULL) == fp) {
+        if (w >> 63) {  // fresh claim by another row of this batch
+          const int64_t r2 = (int64_t)(w & ((1ULL << 40) - 1));
+          const int64_t p2 = koff[r2], l2 = koff[r2 + 1] - p2;
+          if (l2 == len && bytes_eq(kbytes + p2, kb, len)) {
+            kid[i] = -(int64_t)(slot + 1);
+            done = true;
+          }
+        } else {  // resident
+          const int64_t o = dkid[slot];
+          const uint64_t eh = *(const uint64_t*)(arena + o);
+          const int64_t el = *(const int64_t*)(arena + o + 8);
+          if (eh == h && el == len && bytes_eq(arena + o + 16, kb, len)) {
+            kid[i] = o;
+            done = true;
+          }
+        }
+      }
+      if (!done) slot = (slot + 1) & dmask;
+    }
+    if (!done) {
+      kid[i] = 0;
+      *fail = 1;
+    }
+  }
+}
+
+__device__ __forceinline__ int64_t entry_bytes(int64_t len) { return 16 + ((len + 7) & ~7LL); }
+
+// Per block of 256 dict slots: arena bytes needed by fresh entries.
+__global__ __launch_bounds__(256) void k_dict_count(const uint64_t* __restrict__ dword, int64_t dcap,
+                                                    const int64_t* __restrict__ koff, int64_t* __restrict__ bsum) {
+  __shared__ unsigned long long acc;
+  if (threadIdx.x == 0) acc = 0;
+  __syncthreads();
+  const int64_t slot = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int64_t b = 0;
+  if (slot < dcap) {
+    const uint64_t w = dword[slot];
+    if (w >> 63) {
+      const int64_t r = (int64_t)(w & ((1ULL << 40) - 1));
+      b = entry_bytes(koff[r + 1] - koff[r]);
+    }
+  }
+  b = wave_sum(b);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&acc, (unsigned long long)b);
+  __syncthreads();
+  if (threadIdx.x == 0) bsum[blockIdx.x] = (int64_t)acc;
+}
+
+// Exclusive prefix sum of v[0..n) in place (single block); total added to *total.
+__global__ __launch_bounds__(1024) void k_scan_excl(int64_t* __restrict__ v, int64_t n, int64_t* __restrict__ total) {
+  __shared__ int64_t lds[1024];
+  int64_t carry = 0;
+  for (int64_t b0 = 0; b0 < n; b0 += 1024) {
+    const int64_t b = b0 + threadIdx.x;
+    const int64_t x = b < n ? v[b] : 0;
+    lds[threadIdx.x] = x;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+      int64_t y = threadIdx.x >= off ? lds[threadIdx.x - off] : 0;
+      __syncthreads();
+      lds[threadIdx.x] += y;
+      __syncthreads();
+    }
+    if (b < n) v[b] = carry + lds[threadIdx.x] - x;
+    carry += lds[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total += carry;
+}
+
+__global__ __launch_bounds__(256) void k_dict_write(uint64_t* __restrict__ dword, int64_t* __restrict__ dkid,
+                                                    int64_t dcap, const int64_t* __restrict__ boff,
+                                                    int64_t arena_used, uint8_t* __restrict__ arena,
+                                                    const int64_t* __restrict__ koff,
+                                                    const uint8_t* __restrict__ kbytes,
+                                                    const int64_t* __restrict__ khash) {
+  __shared__ int64_t lds[256];
+  const int64_t slot = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  uint64_t w = 0;
+  int64_t b = 0, r = 0;
+  if (slot < dcap) {
+    w = dword[slot];
+    if (w >> 63) {
+      r = (int64_t)(w & ((1ULL << 40) - 1));
+      b = entry_bytes(koff[r + 1] - koff[r]);
+    }
+  }
+  lds[threadIdx.x] = b;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    int64_t y = threadIdx.x >= off ? lds[threadIdx.x - off] : 0;
+    __syncthreads();
+    lds[threadIdx.x] += y;
+    __syncthreads();
+  }
+  if (b) {
+    const int64_t o = arena_used + boff[blockIdx.x] + lds[threadIdx.x] - b;
+    const int64_t len = koff[r + 1] - koff[r];
+    *(int64_t*)(arena + o) = khash[r];
+    *(int64_t*)(arena + o + 8) = len;
+    for (int64_t k = 0; k < len; k++) arena[o + 16 + k] = kbytes[koff[r] + k];
+    dkid[slot] = o;
+    dword[slot] = (1ULL << 62) | (((w >> 40) & 0x3FFFFFULL) << 40);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_kid_fixup(int64_t* __restrict__ kid, int64_t n,
+                                                   const int64_t* __restrict__ dkid) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = kid[i];
+    if (k < 0) kid[i] = dkid[-k - 1];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_dict_rehash(const uint64_t* __restrict__ ow, const int64_t* __restrict__ ok,
+                                                     int64_t ocap, uint64_t* __restrict__ nw, int64_t* __restrict__ nk,
+                                                     uint64_t nmask, const uint8_t* __restrict__ arena) {
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < ocap; s += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t w = ow[s];
+    if (w == 0) continue;
+    const int64_t o = ok[s];
+    const uint64_t h = *(const uint64_t*)(arena + o);
+    uint64_t d = h & nmask;
+    while (atomicCAS((unsigned long long*)&nw[d], 0ULL, (unsigned long long)w) != 0ULL) d = (d + 1) & nmask;
+    nk[d] = o;
+  }
+}
+
+// ------------------------------------------------------------------- host side
+
+static int grid_for(int64_t work, int per_block, int cap_blocks = 2048 * 8) {
+  int64_t g = ceil_div(std::max<int64_t>(work, 1), per_block);
+  return (int)std::min<int64_t>(g, cap_blocks);
+}
+
+}  // namespace khip
+
+using namespace khip;
+
+struct khip_agg {
+  khip_agg_desc desc{};
+  std::vector<int32_t> col_types;
+  std::vector<khip_agg_spec> aggs;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int64_t grace = 0;
+  int windowed = 0;
+  int max_fanout = 1;
+  ApplyParams ap{};
+  InitWords init{};
+  std::vector<AggOut> outs;
+  int sw = 4;
+  // table
+  DevBuf table;
+  int64_t cap = 0;
+  int64_t occ = 0;  // resident groups
+  // per-batch scratch
+  DevBuf blockmax, blockprefix, partials, resume, counters, stream_time;
+  DevBuf st_keys, st_ts, st_kv, st_rv, st_koff, st_kbytes;  // host staging copies
+  DevBuf st_cols[MAX_COLS], st_cval[MAX_COLS];
+  DevBuf kid, khash;  // UTF8
+  int64_t resume_n = 0;
+  // UTF8 dictionary
+  DevBuf dword, dkid, arena, dict_bsum, dict_fail;
+  int64_t dcap = 0, docc = 0, arena_used = 0;
+  int64_t host_stream_time = -1;
+  // profiling (KHIP_FLAG_PROFILE)
+  bool profile = false;
+  hipEvent_t ev[8] = {};
+  khip_kernel_times times{};
+};
+
+static void ev_record(khip_agg* a, int i) {
+  if (a->profile) hipEventRecord(a->ev[i], a->stream);
+}
+static double ev_ms(khip_agg* a, int i, int j) {
+  float ms = 0.f;
+  if (a->profile) hipEventElapsedTime(&ms, a->ev[i], a->ev[j]);
+  return (double)ms;
+}
+
+static khip_status plan_state(khip_agg* a) {
+  const khip_agg_desc& d = a->desc;
+  int word = 3;  // w0, w1, rowtime
+  int w_star = -1;
+  std::vector<int> w_cnt(d.n_cols, -1), w_sum(d.n_cols, -1), w_min(d.n_cols, -1), w_max(d.n_cols, -1);
+  for (int i = 0; i < d.n_aggs; i++) {
+    const khip_agg_spec& s = a->aggs[i];
+    if (s.kind == KHIP_AGG_COUNT_STAR) {
+      if (w_star < 0) w_star = word++;
+      continue;
+    }
+    const int c = s.arg_col;
+    if (w_cnt[c] < 0) w_cnt[c] = word++;
+    if ((s.kind == KHIP_AGG_SUM || s.kind == KHIP_AGG_AVG) && w_sum[c] < 0) w_sum[c] = word++;
+    if (s.kind == KHIP_AGG_MIN && w_min[c] < 0) w_min[c] = word++;
+    if (s.kind == KHIP_AGG_MAX && w_max[c] < 0) w_max[c] = word++;
+  }
+  if (word > 16) return fail(KHIP_E_UNSUPPORTED, "too many aggregate state words (max 13)");
+  a->sw = (int)next_pow2(std::max(word, 4));
+  ApplyParams& p = a->ap;
+  p.windowed = a->windowed;
+  p.slot_words = a->sw;
+  p.size = d.size_ms;
+  p.adv = d.advance_ms;
+  p.grace = a->grace;
+  p.n_cols = d.n_cols;
+  for (int c = 0; c < d.n_cols; c++) p.col_type[c] = a->col_types[c];
+  int n = 0;
+  auto add = [&](int8_t kind, int col, int w) {
+    p.ops[n].kind = kind;
+    p.ops[n].col = (int8_t)col;
+    p.ops[n].word = (int16_t)w;
+    n++;
+  };
+  if (w_star >= 0) add(OP_INC, 0, w_star);
+  for (int c = 0; c < d.n_cols; c++) {
+    if (w_cnt[c] >= 0) add(OP_INC_VALID, c, w_cnt[c]);
+    if (w_sum[c] >= 0) add(a->col_types[c] == KHIP_TYPE_DOUBLE ? OP_ADD_F64 : OP_ADD_I64, c, w_sum[c]);
+    if (w_min[c] >= 0) add(OP_MIN, c, w_min[c]);
+    if (w_max[c] >= 0) add(OP_MAX, c, w_max[c]);
+  }
+  p.n_ops = n;
+  for (int w = 0; w < 16; w++) a->init.w[w] = 0;
+  a->init.w[1] = EMPTY_WS;
+  a->init.w[2] = INT64_MIN;
+  for (int c = 0; c < d.n_cols; c++) {
+    if (w_min[c] >= 0) a->init.w[w_min[c]] = INT64_MAX;
+    if (w_max[c] >= 0) a->init.w[w_max[c]] = INT64_MIN;
+  }
+  a->outs.clear();
+  for (int i = 0; i < d.n_aggs; i++) {
+    const khip_agg_spec& s = a->aggs[i];
+    AggOut o{};
+    o.kind = s.kind;
+    o.type = s.kind == KHIP_AGG_COUNT_STAR ? KHIP_TYPE_INT64 : a->col_types[s.arg_col];
+    o.w_cnt = s.kind == KHIP_AGG_COUNT_STAR ? -1 : w_cnt[s.arg_col];
+    switch (s.kind) {
+      case KHIP_AGG_COUNT_STAR: o.w_val = w_star; break;
+      case KHIP_AGG_COUNT: o.w_val = w_cnt[s.arg_col]; break;
+      case KHIP_AGG_SUM:
+      case KHIP_AGG_AVG: o.w_val = w_sum[s.arg_col]; break;
+      case KHIP_AGG_MIN: o.w_val = w_min[s.arg_col]; break;
+      case KHIP_AGG_MAX: o.w_val = w_max[s.arg_col]; break;
+    }
+    a->outs.push_back(o);
+  }
+  return KHIP_OK;
+}
+
+static khip_status init_table(khip_agg* a, DevBuf& buf, int64_t cap) {
+  KHIP_TRY(buf.ensure((size_t)cap * a->sw * 8));
+  hipLaunchKernelGGL(k_init_table, dim3(grid_for(cap * a->sw, 256)), dim3(256), 0, a->stream,
+                     buf.as<uint64_t>(), cap, a->sw, a->init);
+  KHIP_TRY_HIP(hipGetLastError());
+  return KHIP_OK;
+}
+
+static khip_status grow_table(khip_agg* a, int64_t new_cap) {
+  DevBuf nt;
+  KHIP_TRY(init_table(a, nt, new_cap));
+  if (a->cap > 0 && a->occ > 0) {
+    hipLaunchKernelGGL(k_rehash, dim3(grid_for(a->cap, 256)), dim3(256), 0, a->stream, a->table.as<uint64_t>(),
+                       a->cap, nt.as<uint64_t>(), (uint64_t)(new_cap - 1), a->sw,
+                       a->desc.key_type == KHIP_KEY_UTF8 ? 1 : 0, a->arena.as<uint8_t>());
+    KHIP_TRY_HIP(hipGetLastError());
+  }
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  a->table.release();
+  a->table = nt;
+  nt.p = nullptr;
+  nt.bytes = 0;
+  a->cap = new_cap;
+  return KHIP_OK;
+}
+
+static khip_status grow_dict(khip_agg* a, int64_t new_cap) {
+  DevBuf nw, nk;
+  KHIP_TRY(nw.ensure((size_t)new_cap * 8));
+  KHIP_TRY(nk.ensure((size_t)new_cap * 8));
+  KHIP_TRY_HIP(hipMemsetAsync(nw.p, 0, (size_t)new_cap * 8, a->stream));
+  if (a->dcap > 0 && a->docc > 0) {
+    hipLaunchKernelGGL(k_dict_rehash, dim3(grid_for(a->dcap, 256)), dim3(256), 0, a->stream, a->dword.as<uint64_t>(),
+                       a->dkid.as<int64_t>(), a->dcap, nw.as<uint64_t>(), nk.as<int64_t>(),
+                       (uint64_t)(new_cap - 1), a->arena.as<uint8_t>());
+    KHIP_TRY_HIP(hipGetLastError());
+  }
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  a->dword.release();
+  a->dkid.release();
+  a->dword = nw;
+  a->dkid = nk;
+  nw.p = nk.p = nullptr;
+  a->dcap = new_cap;
+  return KHIP_OK;
+}
+
+extern "C" {
+
+khip_status khip_agg_result_type(const khip_agg_desc* d, int32_t i, int32_t* out) {
+  if (!d || !out || i < 0 || i >= d->n_aggs) return fail(KHIP_E_INVALID, "bad aggregate index");
+  const khip_agg_spec& s = d->aggs[i];
+  if (s.kind == KHIP_AGG_COUNT_STAR || s.kind == KHIP_AGG_COUNT) *out = KHIP_TYPE_INT64;
+  else if (s.kind == KHIP_AGG_AVG) *out = KHIP_TYPE_DOUBLE;
+  else *out = d->col_types[s.arg_col];
+  return KHIP_OK;
+}
+
+khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
+  clear_error();
+  if (!desc || !out) return fail(KHIP_E_INVALID, "null argument");
+  const khip_agg_desc& d = *desc;
+  if (d.window_kind < KHIP_WINDOW_NONE || d.window_kind > KHIP_WINDOW_HOPPING)
+    return fail(KHIP_E_INVALID, "unknown window kind");
+  if (d.window_kind != KHIP_WINDOW_NONE) {
+    if (d.size_ms <= 0) return fail(KHIP_E_INVALID, "window size must be > 0");
+    if (d.window_kind == KHIP_WINDOW_HOPPING && (d.advance_ms <= 0 || d.advance_ms > d.size_ms))
+      return fail(KHIP_E_INVALID, "hopping advance must be in (0, size]");
+  }
+  if (d.key_type != KHIP_KEY_INT64 && d.key_type != KHIP_KEY_UTF8) return fail(KHIP_E_INVALID, "key type");
+  if (d.n_cols < 0 || d.n_cols > MAX_COLS) return fail(KHIP_E_UNSUPPORTED, "at most 8 value columns");
+  if (d.n_aggs < 0 || d.n_aggs > 16) return fail(KHIP_E_UNSUPPORTED, "at most 16 aggregates");
+  for (int c = 0; c < d.n_cols; c++)
+    if (d.col_types[c] < KHIP_TYPE_INT32 || d.col_types[c] > KHIP_TYPE_DOUBLE)
+      return fail(KHIP_E_INVALID, "column type");
+  for (int i = 0; i < d.n_aggs; i++) {
+    const khip_agg_spec& s = d.aggs[i];
+    if (s.kind < KHIP_AGG_COUNT_STAR || s.kind > KHIP_AGG_AVG) return fail(KHIP_E_INVALID, "aggregate kind");
+    if (s.kind != KHIP_AGG_COUNT_STAR && (s.arg_col < 0 || s.arg_col >= d.n_cols))
+      return fail(KHIP_E_INVALID, "aggregate argument column");
+  }
+  khip_agg* a = new khip_agg();
+  a->desc = d;
+  a->col_types.assign(d.col_types, d.col_types + d.n_cols);
+  a->aggs.assign(d.aggs, d.aggs + d.n_aggs);
+  a->desc.col_types = a->col_types.data();
+  a->desc.aggs = a->aggs.data();
+  if (d.window_kind == KHIP_WINDOW_TUMBLING) a->desc.advance_ms = d.size_ms;
+  a->windowed = d.window_kind != KHIP_WINDOW_NONE;
+  a->grace = grace_of(a->desc);
+  a->max_fanout = a->windowed ? (int)ceil_div(a->desc.size_ms, a->desc.advance_ms) : 1;
+  if (a->windowed && ceil_div(a->desc.size_ms, a->desc.advance_ms) > MAX_FANOUT) {
+    delete a;
+    return fail(KHIP_E_UNSUPPORTED, "hopping fan-out above 4095 windows per record");
+  }
+  a->device = d.device;
+  khip_status st = plan_state(a);
+  if (st != KHIP_OK) {
+    delete a;
+    return st;
+  }
+  DeviceGuard g(a->device);
+  if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete a;
+    return fail(KHIP_E_DEVICE, "hipStreamCreate failed (no device?)");
+  }
+  a->profile = (d.flags & KHIP_FLAG_PROFILE) != 0;
+  if (a->profile)
+    for (int e = 0; e < 8; e++) hipEventCreate(&a->ev[e]);
+  int64_t cap = next_pow2(std::max<int64_t>(1024, d.capacity_hint > 0 ? d.capacity_hint * 2 : 1 << 16));
+  if ((st = init_table(a, a->table, cap)) != KHIP_OK || (st = a->stream_time.ensure(8)) != KHIP_OK ||
+      (st = a->counters.ensure(8 * NPART)) != KHIP_OK) {
+    khip_agg_destroy(a);
+    return st;
+  }
+  a->cap = cap;
+  int64_t m1 = -1;
+  hipMemcpyAsync(a->stream_time.p, &m1, 8, hipMemcpyHostToDevice, a->stream);
+  if (d.key_type == KHIP_KEY_UTF8) {
+    if ((st = grow_dict(a, 4096)) != KHIP_OK || (st = a->dict_fail.ensure(8)) != KHIP_OK) {
+      khip_agg_destroy(a);
+      return st;
+    }
+  }
+  if (hipStreamSynchronize(a->stream) != hipSuccess) {
+    khip_agg_destroy(a);
+    return fail(KHIP_E_DEVICE, "device init failed");
+  }
+  *out = a;
+  return KHIP_OK;
+}
+
+static khip_status stage(khip_agg* a, DevBuf& buf, const void* src, size_t bytes) {
+  KHIP_TRY(buf.ensure(bytes));
+  if (bytes) KHIP_TRY_HIP(hipMemcpyAsync(buf.p, src, bytes, hipMemcpyHostToDevice, a->stream));
+  return KHIP_OK;
+}
+
+khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* stats) {
+  clear_error();
+  if (!a || !b) return fail(KHIP_E_INVALID, "null argument");
+  if (b->n_rows < 0 || b->n_cols < a->desc.n_cols) return fail(KHIP_E_INVALID, "batch shape");
+  if (b->n_rows >= (1LL << 36)) return fail(KHIP_E_UNSUPPORTED, "batch larger than 2^36 rows");
+  const int64_t n = b->n_rows;
+  const bool utf8 = a->desc.key_type == KHIP_KEY_UTF8;
+  if (!b->ts || (utf8 ? (!b->key_offsets || !b->key_bytes) : !b->key_i64))
+    if (n > 0) return fail(KHIP_E_INVALID, "missing key or timestamp column");
+  for (int c = 0; c < a->desc.n_cols; c++)
+    if (n > 0 && (!b->col_data || !b->col_data[c])) return fail(KHIP_E_INVALID, "missing value column");
+  DeviceGuard g(a->device);
+  khip_batch_stats s{};
+  s.rows_in = n;
+  if (n == 0) {
+    s.stream_time = a->host_stream_time;
+    if (stats) *stats = s;
+    return KHIP_OK;
+  }
+  // ---- device pointers (stage host batches)
+  const int64_t* keys = b->key_i64;
+  const int64_t* ts = b->ts;
+  const uint8_t* kv = b->key_valid;
+  const uint8_t* rv = b->row_valid;
+  const int64_t* koff = b->key_offsets;
+  const uint8_t* kbytes = b->key_bytes;
+  ColPtrs cols{};
+  const size_t bm = (size_t)(n + 7) / 8;
+  int64_t key_bytes_total = 0;
+  if (b->mem == KHIP_MEM_HOST) {
+    KHIP_TRY(stage(a, a->st_ts, b->ts, n * 8));
+    ts = a->st_ts.as<int64_t>();
+    if (kv) { KHIP_TRY(stage(a, a->st_kv, kv, bm)); kv = a->st_kv.as<uint8_t>(); }
+    if (rv) { KHIP_TRY(stage(a, a->st_rv, rv, bm)); rv = a->st_rv.as<uint8_t>(); }
+    if (utf8) {
+      key_bytes_total = b->key_offsets[n];
+      KHIP_TRY(stage(a, a->st_koff, b->key_offsets, (n + 1) * 8));
+      KHIP_TRY(stage(a, a->st_kbytes, b->key_bytes, (size_t)std::max<int64_t>(key_bytes_total, 1)));
+      koff = a->st_koff.as<int64_t>();
+      kbytes = a->st_kbytes.as<uint8_t>();
+    } else {
+      KHIP_TRY(stage(a, a->st_keys, b->key_i64, n * 8));
+      keys = a->st_keys.as<int64_t>();
+    }
+    for (int c = 0; c < a->desc.n_cols; c++) {
+      const size_t es = a->col_types[c] == KHIP_TYPE_INT32 ? 4 : 8;
+      KHIP_TRY(stage(a, a->st_cols[c], b->col_data[c], n * es));
+      cols.data[c] = a->st_cols[c].p;
+      const uint8_t* cv = b->col_valid ? b->col_valid[c] : nullptr;
+      if (cv) {
+        KHIP_TRY(stage(a, a->st_cval[c], cv, bm));
+        cols.valid[c] = a->st_cval[c].as<uint8_t>();
+      }
+    }
+  } else if (b->mem == KHIP_MEM_DEVICE) {
+    for (int c = 0; c < a->desc.n_cols; c++) {
+      cols.data[c] = b->col_data[c];
+      cols.valid[c] = b->col_valid ? b->col_valid[c] : nullptr;
+    }
+    if (utf8)
+      KHIP_TRY_HIP(hipMemcpyAsync(&key_bytes_total, koff + n, 8, hipMemcpyDeviceToHost, a->stream));
+  } else {
+    return fail(KHIP_E_INVALID, "batch mem");
+  }
+  // ---- scratch
+  const int64_t nb = ceil_div(n, RPB);
+  KHIP_TRY(a->blockmax.ensure(nb * 8));
+  KHIP_TRY(a->blockprefix.ensure(nb * 8));
+  KHIP_TRY(a->partials.ensure(nb * 8 * NPART));
+  if (a->resume_n < n) {
+    KHIP_TRY(a->resume.ensure(n * 4));
+    KHIP_TRY_HIP(hipMemsetAsync(a->resume.p, 0xFF, n * 4, a->stream));
+    a->resume_n = n;
+  }
+  KHIP_TRY_HIP(hipMemsetAsync(a->counters.p, 0, 8 * NPART, a->stream));
+  // ---- stream time before each block
+  ev_record(a, 0);
+  hipLaunchKernelGGL(k_blockmax, dim3(nb), dim3(BLOCK), 0, a->stream, ts, kv, rv, n, a->blockmax.as<int64_t>());
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, a->stream, a->blockmax.as<int64_t>(), nb,
+                     a->blockprefix.as<int64_t>(), a->stream_time.as<int64_t>());
+  KHIP_TRY_HIP(hipGetLastError());
+  ev_record(a, 1);
+  // ---- UTF8 keys → stable key ids
+  const int64_t* hkeys = keys;
+  if (utf8) {
+    KHIP_TRY_HIP(hipStreamSynchronize(a->stream));  // key_bytes_total for device batches
+    if (2 * (a->docc + n) > a->dcap) KHIP_TRY(grow_dict(a, next_pow2(4 * (a->docc + n))));
+    KHIP_TRY(a->kid.ensure(n * 8));
+    KHIP_TRY(a->khash.ensure(n * 8));
+    const int64_t need = a->arena_used + key_bytes_total + 16 * n + 16;
+    if ((size_t)need > a->arena.bytes) {
+      DevBuf na;
+      KHIP_TRY(na.ensure((size_t)std::max<int64_t>(need * 2, 1 << 20)));
+      if (a->arena_used) KHIP_TRY_HIP(hipMemcpyAsync(na.p, a->arena.p, a->arena_used, hipMemcpyDeviceToDevice, a->stream));
+      KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+      a->arena.release();
+      a->arena = na;
+      na.p = nullptr;
+    }
+    KHIP_TRY_HIP(hipMemsetAsync(a->dict_fail.p, 0, 4, a->stream));
+    hipLaunchKernelGGL(k_dict_lookup, dim3(grid_for(n, 256)), dim3(256), 0, a->stream, a->dword.as<uint64_t>(),
+                       a->dkid.as<int64_t>(), (uint64_t)(a->dcap - 1), a->arena.as<uint8_t>(), koff, kbytes, kv,
+                       rv, ts, n, a->kid.as<int64_t>(), a->khash.as<int64_t>(), a->dict_fail.as<int>());
+    const int64_t dnb = ceil_div(a->dcap, 256);
+    KHIP_TRY(a->dict_bsum.ensure((dnb + 1) * 8));
+    hipLaunchKernelGGL(k_dict_count, dim3(dnb), dim3(256), 0, a->stream, a->dword.as<uint64_t>(), a->dcap, koff,
+                       a->dict_bsum.as<int64_t>());
+    int64_t* dtotal = a->dict_bsum.as<int64_t>() + dnb;
+    KHIP_TRY_HIP(hipMemsetAsync(dtotal, 0, 8, a->stream));
+    hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, a->stream, a->dict_bsum.as<int64_t>(), dnb, dtotal);
+    hipLaunchKernelGGL(k_dict_write, dim3(dnb), dim3(256), 0, a->stream, a->dword.as<uint64_t>(), a->dkid.as<int64_t>(),
+                       a->dcap, a->dict_bsum.as<int64_t>(), a->arena_used, a->arena.as<uint8_t>(), koff, kbytes,
+                       a->khash.as<int64_t>());
+    hipLaunchKernelGGL(k_kid_fixup, dim3(grid_for(n, 256)), dim3(256), 0, a->stream, a->kid.as<int64_t>(), n,
+                       a->dkid.as<int64_t>());
+    KHIP_TRY_HIP(hipGetLastError());
+    int64_t added = 0;
+    int failed = 0;
+    KHIP_TRY_HIP(hipMemcpyAsync(&added, dtotal, 8, hipMemcpyDeviceToHost, a->stream));
+    KHIP_TRY_HIP(hipMemcpyAsync(&failed, a->dict_fail.p, 4, hipMemcpyDeviceToHost, a->stream));
+    KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+    if (failed) return fail(KHIP_E_DEVICE, "key dictionary probe budget exhausted");
+    a->arena_used += added;
+    // dictionary occupancy, over-estimated (every entry takes >= 16 arena bytes): growth is
+    // decided conservatively
+    a->docc = std::min<int64_t>(a->dcap, a->docc + std::min<int64_t>(n, added / 16));
+    keys = a->kid.as<int64_t>();
+    hkeys = a->khash.as<int64_t>();
+  }
+  ev_record(a, 2);
+  // ---- grow the group table ahead of time if the resident load is high
+  if (2 * a->occ > a->cap) KHIP_TRY(grow_table(a, a->cap * 4));
+  // ---- apply (+ resume passes after doubling on probe exhaustion)
+  int64_t tot[NPART] = {0};
+  const int64_t occ0 = a->occ;
+  double apply_ms = 0, fin_ms = 0;
+  for (int pass = 0;; pass++) {
+    ev_record(a, 3);
+    hipLaunchKernelGGL(k_apply, dim3(nb), dim3(BLOCK), 0, a->stream, a->ap, hkeys, keys, ts, kv, rv, cols,
+                       a->blockprefix.as<int64_t>(), n, a->table.as<uint64_t>(), (uint64_t)(a->cap - 1),
+                       a->resume.as<int32_t>(), a->partials.as<int64_t>(), pass > 0 ? 1 : 0);
+    ev_record(a, 4);
+    hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(256), 0, a->stream, a->partials.as<int64_t>(), nb, NPART,
+                       a->counters.as<int64_t>());
+    hipLaunchKernelGGL(k_finalize, dim3(grid_for(a->cap, 256)), dim3(256), 0, a->stream, a->table.as<uint64_t>(),
+                       a->cap, a->sw, keys, ts, a->windowed, a->desc.size_ms, a->desc.advance_ms);
+    KHIP_TRY_HIP(hipGetLastError());
+    ev_record(a, 5);
+    int64_t c[NPART];
+    KHIP_TRY_HIP(hipMemcpyAsync(c, a->counters.p, 8 * NPART, hipMemcpyDeviceToHost, a->stream));
+    KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+    const int64_t failed = c[P_FAILED] - tot[P_FAILED];
+    for (int k = 0; k < NPART; k++) tot[k] = c[k];
+    a->occ = occ0 + tot[P_NEW];  // every claim is counted exactly once
+    if (a->profile) {
+      apply_ms += ev_ms(a, 3, 4);
+      fin_ms += ev_ms(a, 4, 5);
+      if (pass == 0) {
+        a->times.stream_time_ms += ev_ms(a, 0, 1);
+        a->times.dict_ms += ev_ms(a, 1, 2);
+        a->times.records += n;
+      }
+      a->times.apply_launches++;
+    }
+    if (failed == 0) break;
+    if (pass > 40) return fail(KHIP_E_DEVICE, "aggregate table could not absorb the batch");
+    KHIP_TRY(grow_table(a, a->cap * 2));
+  }
+  a->times.apply_ms += apply_ms;
+  a->times.finalize_ms += fin_ms;
+  KHIP_TRY_HIP(hipMemcpyAsync(&a->host_stream_time, a->stream_time.p, 8, hipMemcpyDeviceToHost, a->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  s.rows_accepted = tot[P_ACCEPTED];
+  s.dropped_null_key = tot[P_NULL_KEY];
+  s.dropped_null_row = tot[P_NULL_ROW];
+  s.dropped_bad_ts = tot[P_BAD_TS];
+  s.windows_applied = tot[P_APPLIED];
+  s.windows_late = tot[P_LATE];
+  s.stream_time = a->host_stream_time;
+  if (stats) *stats = s;
+  return KHIP_OK;
+}
+
+static khip_status compact_rows(khip_agg* a, const khip_having* h, std::vector<uint64_t>* rows, int64_t* count) {
+  HavingDev hd{};
+  if (h) {
+    if (h->agg_index < 0 || h->agg_index >= a->desc.n_aggs) return fail(KHIP_E_INVALID, "having agg index");
+    if (h->op < KHIP_OP_GT || h->op > KHIP_OP_NE) return fail(KHIP_E_INVALID, "having op");
+    hd.active = 1;
+    hd.op = h->op;
+    hd.a = a->outs[h->agg_index];
+    hd.i64 = h->i64;
+    hd.f64 = h->f64;
+  }
+  DevBuf ctr, out;
+  KHIP_TRY(ctr.ensure(8));
+  KHIP_TRY_HIP(hipMemsetAsync(ctr.p, 0, 8, a->stream));
+  const int grid = grid_for(a->cap, 256, 4096);
+  if (rows) KHIP_TRY(out.ensure((size_t)std::max<int64_t>(a->occ, 1) * a->sw * 8));
+  hipLaunchKernelGGL(k_compact, dim3(grid), dim3(256), 0, a->stream, a->table.as<uint64_t>(), a->cap, a->sw, hd,
+                     rows ? out.as<uint64_t>() : nullptr, std::max<int64_t>(a->occ, 1), ctr.as<unsigned long long>());
+  KHIP_TRY_HIP(hipGetLastError());
+  int64_t n = 0;
+  KHIP_TRY_HIP(hipMemcpyAsync(&n, ctr.p, 8, hipMemcpyDeviceToHost, a->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  *count = n;
+  if (rows && n > a->occ) return fail(KHIP_E_STATE, "group count bookkeeping mismatch");
+  if (rows) {
+    rows->resize((size_t)n * a->sw);
+    if (n) KHIP_TRY_HIP(hipMemcpy(rows->data(), out.p, (size_t)n * a->sw * 8, hipMemcpyDeviceToHost));
+  }
+  ctr.release();
+  out.release();
+  return KHIP_OK;
+}
+
+khip_status khip_agg_count_rows(khip_agg* a, const khip_having* h, int64_t* n) {
+  clear_error();
+  if (!a || !n) return fail(KHIP_E_INVALID, "null argument");
+  DeviceGuard g(a->device);
+  return compact_rows(a, h, nullptr, n);
+}
+
+khip_status khip_agg_snapshot_size(khip_agg* a, int64_t* n_rows, int64_t* key_bytes) {
+  clear_error();
+  if (!a) return fail(KHIP_E_INVALID, "null argument");
+  DeviceGuard g(a->device);
+  if (n_rows) *n_rows = a->occ;
+  if (key_bytes) {
+    if (a->desc.key_type == KHIP_KEY_UTF8) {
+      std::vector<uint64_t> rows;
+      int64_t n = 0;
+      KHIP_TRY(compact_rows(a, nullptr, &rows, &n));
+      std::vector<uint8_t> arena(a->arena_used);
+      if (a->arena_used) KHIP_TRY_HIP(hipMemcpy(arena.data(), a->arena.p, a->arena_used, hipMemcpyDeviceToHost));
+      int64_t kb = 0;
+      for (int64_t r = 0; r < n; r++) kb += *(const int64_t*)(arena.data() + rows[r * a->sw] + 8);
+      *key_bytes = kb;
+    } else {
+      *key_bytes = 0;
+    }
+  }
+  return KHIP_OK;
+}
+
+khip_status khip_agg_snapshot(khip_agg* a, const khip_having* h, khip_snapshot* out) {
+  clear_error();
+  if (!a || !out) return fail(KHIP_E_INVALID, "null argument");
+  DeviceGuard g(a->device);
+  std::vector<uint64_t> rows;
+  int64_t n = 0;
+  KHIP_TRY(compact_rows(a, h, &rows, &n));
+  const int sw = a->sw;
+  const bool utf8 = a->desc.key_type == KHIP_KEY_UTF8;
+  std::vector<uint8_t> arena;
+  if (utf8) {
+    arena.resize(a->arena_used);
+    if (a->arena_used) KHIP_TRY_HIP(hipMemcpy(arena.data(), a->arena.p, a->arena_used, hipMemcpyDeviceToHost));
+  }
+  auto kptr = [&](int64_t kid) { return arena.data() + kid + 16; };
+  auto klen = [&](int64_t kid) { return *(const int64_t*)(arena.data() + kid + 8); };
+  std::vector<int64_t> order(n);
+  std::iota(order.begin(), order.end(), 0);
+  std::sort(order.begin(), order.end(), [&](int64_t x, int64_t y) {
+    const int64_t kx = (int64_t)rows[x * sw], ky = (int64_t)rows[y * sw];
+    if (kx != ky) {
+      if (!utf8) return kx < ky;
+      const int64_t lx = klen(kx), ly = klen(ky);
+      const int c = memcmp(kptr(kx), kptr(ky), (size_t)std::min(lx, ly));
+      if (c) return c < 0;
+      if (lx != ly) return lx < ly;
+    }
+    return (int64_t)rows[x * sw + 1] < (int64_t)rows[y * sw + 1];
+  });
+  if (n > out->capacity) {
+    out->n_rows = n;
+    return fail(KHIP_E_BUFFER, "snapshot capacity too small");
+  }
+  int64_t kb = 0;
+  if (utf8 && out->key_offsets) out->key_offsets[0] = 0;
+  for (int64_t r = 0; r < n; r++) {
+    const uint64_t* s = &rows[order[r] * sw];
+    const int64_t key = (int64_t)s[0], ws = (int64_t)s[1];
+    if (utf8) {
+      const int64_t len = klen(key);
+      if (kb + len > out->key_bytes_capacity) return fail(KHIP_E_BUFFER, "snapshot key bytes capacity too small");
+      if (out->key_bytes && len) memcpy(out->key_bytes + kb, kptr(key), (size_t)len);
+      kb += len;
+      if (out->key_offsets) out->key_offsets[r + 1] = kb;
+    } else if (out->key_i64) {
+      out->key_i64[r] = key;
+    }
+    if (out->window_start) out->window_start[r] = a->windowed ? ws : 0;
+    if (out->window_end) out->window_end[r] = a->windowed ? ws + a->desc.size_ms : 0;
+    if (out->rowtime) out->rowtime[r] = (int64_t)s[2];
+    for (int i = 0; i < a->desc.n_aggs; i++) {
+      const AggOut& o = a->outs[i];
+      int64_t iv = 0;
+      double dv = 0.0;
+      bool isnull = false;
+      switch (o.kind) {
+        case KHIP_AGG_COUNT_STAR:
+        case KHIP_AGG_COUNT: iv = (int64_t)s[o.w_val]; break;
+        case KHIP_AGG_SUM:
+          if (o.type == KHIP_TYPE_DOUBLE) memcpy(&dv, &s[o.w_val], 8);
+          else iv = (int64_t)s[o.w_val];
+          break;
+        case KHIP_AGG_MIN:
+        case KHIP_AGG_MAX:
+          if ((int64_t)s[o.w_cnt] == 0) isnull = true;
+          else if (o.type == KHIP_TYPE_DOUBLE) dv = f64_from_order_key((int64_t)s[o.w_val]);
+          else iv = (int64_t)s[o.w_val];
+          break;
+        case KHIP_AGG_AVG: {
+          const int64_t c = (int64_t)s[o.w_cnt];
+          if (c == 0) dv = 0.0;
+          else if (o.type == KHIP_TYPE_DOUBLE) { double sum; memcpy(&sum, &s[o.w_val], 8); dv = sum / (double)c; }
+          else if (o.type == KHIP_TYPE_INT32) dv = (double)(int32_t)s[o.w_val] / (double)c;
+          else dv = (double)(int64_t)s[o.w_val] / (double)c;
+          break;
+        }
+      }
+      int32_t rt;
+      khip_agg_result_type(&a->desc, i, &rt);
+      if (out->agg_values && out->agg_values[i]) {
+        if (rt == KHIP_TYPE_INT32) ((int32_t*)out->agg_values[i])[r] = isnull ? 0 : (int32_t)iv;
+        else if (rt == KHIP_TYPE_INT64) ((int64_t*)out->agg_values[i])[r] = isnull ? 0 : iv;
+        else ((double*)out->agg_values[i])[r] = isnull ? 0.0 : dv;
+      }
+      if (out->agg_null && out->agg_null[i]) out->agg_null[i][r] = isnull ? 1 : 0;
+    }
+  }
+  out->n_rows = n;
+  out->key_bytes_len = kb;
+  return KHIP_OK;
+}
+
+khip_status khip_agg_reset(khip_agg* a) {
+  clear_error();
+  if (!a) return fail(KHIP_E_INVALID, "null argument");
+  DeviceGuard g(a->device);
+  hipLaunchKernelGGL(k_init_table, dim3(grid_for(a->cap * a->sw, 256)), dim3(256), 0, a->stream,
+                     a->table.as<uint64_t>(), a->cap, a->sw, a->init);
+  int64_t m1 = -1;
+  KHIP_TRY_HIP(hipMemcpyAsync(a->stream_time.p, &m1, 8, hipMemcpyHostToDevice, a->stream));
+  if (a->desc.key_type == KHIP_KEY_UTF8) {
+    KHIP_TRY_HIP(hipMemsetAsync(a->dword.p, 0, a->dcap * 8, a->stream));
+    a->docc = 0;
+    a->arena_used = 0;
+  }
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  a->occ = 0;
+  a->host_stream_time = -1;
+  return KHIP_OK;
+}
+
+khip_status khip_agg_sync(khip_agg* a) {
+  if (!a) return fail(KHIP_E_INVALID, "null argument");
+  DeviceGuard g(a->device);
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  return KHIP_OK;
+}
+
+khip_status khip_agg_kernel_times(khip_agg* a, khip_kernel_times* out, int32_t reset) {
+  if (!a || !out) return fail(KHIP_E_INVALID, "null argument");
+  if (!a->profile) return fail(KHIP_E_STATE, "handle created without KHIP_FLAG_PROFILE");
+  *out = a->times;
+  if (reset) a->times = khip_kernel_times{};
+  return KHIP_OK;
+}
+
+khip_status khip_agg_stream(khip_agg* a, void** s) {
+  if (!a || !s) return fail(KHIP_E_INVALID, "null argument");
+  *s = (void*)a->stream;
+  return KHIP_OK;
+}
+
+khip_status khip_agg_destroy(khip_agg* a) {
+  if (!a) return KHIP_OK;
+  DeviceGuard g(a->device);
+  if (a->stream) hipStreamSynchronize(a->stream);
+  DevBuf* bufs[] = {&a->table, &a->blockmax, &a->blockprefix, &a->partials, &a->resume, &a->counters,
+                    &a->stream_time, &a->st_keys, &a->st_ts, &a->st_kv, &a->st_rv, &a->st_koff,
+                    &a->st_kbytes, &a->kid, &a->khash, &a->dword, &a->dkid, &a->arena, &a->dict_bsum,
+                    &a->dict_fail};
+  for (DevBuf* b : bufs) b->release();
+  for (int c = 0; c < MAX_COLS; c++) {
+    a->st_cols[c].release();
+    a->st_cval[c].release();
+  }
+  for (int e = 0; e < 8; e++)
+    if (a->ev[e]) hipEventDestroy(a->ev[e]);
+  if (a->stream) hipStreamDestroy(a->stream);
+  delete a;
+  return KHIP_OK;
+}
+
+}  // extern "C"

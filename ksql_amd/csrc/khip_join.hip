@@ -1,0 +1,606 @@
+// khip_join.hip — stream-table join on MI355X (gfx950).
+//
+// Replaces the table side built by SourceBuilder.buildKTable (S/SourceBuilder.java:87-137,
+// a RocksDB KV store of the latest value per key) and the per-record Kafka Streams
+// KStreamKTableJoin lookup + KsqlValueJoiner.apply that StreamTableJoinBuilder.build wires
+// (S/StreamTableJoinBuilder.java:38-88, S/KsqlValueJoiner.java:41-63).
+//
+// HBM layout: cap slots (power of two), AoS, slot_words u64 per slot:
+//   [0] key  [1] meta  [2] last-writer tag  [3..] right-side columns (one word each)
+//   meta: bit63 = claimed by this upsert batch (bits 0..39 = batch row),
+//         bit62 = resident (key valid), bit61 = live (has a value; 0 = deleted),
+//         bits 0..31 = null mask of the right columns (when resident).
+//   For a table of 1 payload column a slot is 32 B: one probe touches one line.
+//
+// Upsert (arrival order, last writer wins, tombstone deletes):
+//   k_upsert_claim   find-or-claim each key's slot (CAS on meta, claim references the
+//                    batch row); atomicMax of (epoch << 40 | row) elects the last writer
+//   k_upsert_finalize claims → resident keys
+//   k_upsert_apply   the elected row writes value + live bit (or clears live)
+// Probe: one thread per stream row, coalesced key/ts loads, one slot line per probe;
+// output is row-aligned (selection bitmaps built with __ballot, 8 B per wave) so no
+// compaction pass is needed on the device path.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "khip_util.hpp"
+
+namespace khip {
+
+constexpr int JMAX_COLS = 16;
+constexpr int JMAX_PROBE = 4096;
+constexpr uint64_t M_CLAIM = 1ULL << 63;
+constexpr uint64_t M_RESIDENT = 1ULL << 62;
+constexpr uint64_t M_LIVE = 1ULL << 61;
+
+struct JCols {
+  const void* data[JMAX_COLS];
+  const uint8_t* valid[JMAX_COLS];
+};
+
+struct JWhere {
+  int32_t active;
+  int32_t col;
+  int32_t op;
+  int32_t type;
+  int64_t i64;
+  double f64;
+};
+
+__device__ __forceinline__ uint64_t jld(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint64_t key_hash(int64_t k) { return mix64((uint64_t)k ^ 0x2545F4914F6CDD1DULL); }
+
+__global__ __launch_bounds__(256) void k_upsert_claim(uint64_t* __restrict__ table, uint64_t mask, int sw,
+                                                      const int64_t* __restrict__ keys,
+                                                      const uint8_t* __restrict__ kv, int64_t n, uint64_t epoch,
+                                                      int64_t* __restrict__ slot_of, int* __restrict__ fail,
+                                                      unsigned long long* __restrict__ new_keys) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    slot_of[i] = -1;
+    if (!bit_get(kv, i)) continue;
+    const int64_t key = keys[i];
+    uint64_t slot = key_hash(key) & mask;
+    const uint64_t claim = M_CLAIM | (uint64_t)i;
+    bool done = false;
+    for (int probe = 0; probe < JMAX_PROBE && !done; probe++) {
+      uint64_t* s = table + slot * (uint64_t)sw;
+      uint64_t m = jld(&s[1]);
+      if (m == 0) {
+        const uint64_t old = atomicCAS((unsigned long long*)&s[1], 0ULL, (unsigned long long)claim);
+        if (old == 0) {
+          atomicAdd(new_keys, 1ULL);
+          done = true;
+        } else {
+          m = old;
+        }
+      }
+      if (!done) {
+        if (m & M_CLAIM) {
+          done = keys[(int64_t)(m & ((1ULL << 40) - 1))] == key;
+        } else {
+          done = (int64_t)s[0] == key;
+        }
+      }
+      if (done) {
+        slot_of[i] = (int64_t)slot;
+        atomicMax((unsigned long long*)&s[2], (unsigned long long)((epoch << 40) | (uint64_t)i));
+      } else {
+        slot = (slot + 1) & mask;
+      }
+    }
+    if (!done) *fail = 1;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_upsert_finalize(uint64_t* __restrict__ table, int64_t cap, int sw,
+                                                         const int64_t* __restrict__ keys) {
+  for (int64_t slot = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; slot < cap;
+       slot += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t* s = table + slot * (uint64_t)sw;
+    const uint64_t m = s[1];
+    if (m & M_CLAIM) {
+      s[0] = (uint64_t)keys[(int64_t)(m & ((1ULL << 40) - 1))];
+      s[1] = M_RESIDENT;  // not live until a value is written
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_upsert_apply(uint64_t* __restrict__ table, int sw,
+                                                      const int64_t* __restrict__ slot_of,
+                                                      const uint8_t* __restrict__ rv, int64_t n, uint64_t epoch,
+                                                      int ncols, const int32_t* __restrict__ types_dev, JCols cols) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t slot = slot_of[i];
+    if (slot < 0) continue;
+    uint64_t* s = table + slot * (uint64_t)sw;
+    if (s[2] != ((epoch << 40) | (uint64_t)i)) continue;  // not the last writer of this key
+    if (!bit_get(rv, i)) {
+      s[1] = M_RESIDENT;  // tombstone: delete
+      continue;
+    }
+    uint64_t nullmask = 0;
+    for (int c = 0; c < ncols; c++) {
+      const bool v = bit_get(cols.valid[c], i);
+      uint64_t w = 0;
+      if (v) {
+        if (types_dev[c] == KHIP_TYPE_INT32) w = (uint64_t)(int64_t)((const int32_t*)cols.data[c])[i];
+        else w = ((const uint64_t*)cols.data[c])[i];
+      } else {
+        nullmask |= 1ULL << c;
+      }
+      s[3 + c] = w;
+    }
+    s[1] = M_RESIDENT | M_LIVE | nullmask;
+  }
+}
+
+__device__ __forceinline__ bool where_ok(const uint64_t* s, uint64_t meta, const JWhere& w) {
+  if (!w.active) return true;
+  if (meta & (1ULL << w.col)) return false;  // NULL never satisfies
+  const uint64_t raw = s[3 + w.col];
+  int c;
+  if (w.type == KHIP_TYPE_DOUBLE) {
+    double d;
+    __builtin_memcpy(&d, &raw, 8);
+    if (d != d) return w.op == KHIP_OP_NE;
+    c = d < w.f64 ? -1 : (d > w.f64 ? 1 : 0);
+  } else {
+    const int64_t v = (int64_t)raw;
+    c = v < w.i64 ? -1 : (v > w.i64 ? 1 : 0);
+  }
+  switch (w.op) {
+    case KHIP_OP_GT: return c > 0;
+    case KHIP_OP_GE: return c >= 0;
+    case KHIP_OP_LT: return c < 0;
+    case KHIP_OP_LE: return c <= 0;
+    case KHIP_OP_EQ: return c == 0;
+    case KHIP_OP_NE: return c != 0;
+  }
+  return false;
+}
+
+struct JOut {
+  uint8_t* emit;
+  uint8_t* matched;
+  void* col_data[JMAX_COLS];
+  uint8_t* col_null[JMAX_COLS];
+  int64_t* slot_out;  // host path: -1 not emitted, 0 emitted miss, slot + 1 emitted hit
+};
+
+// One thread per stream row (row = global thread id, so a wave covers 64 consecutive rows
+// and its bitmaps are one 8-byte store).
+__global__ __launch_bounds__(256) void k_probe(const uint64_t* __restrict__ table, uint64_t mask, int sw,
+                                               const int64_t* __restrict__ keys, const int64_t* __restrict__ ts,
+                                               const uint8_t* __restrict__ kv, const uint8_t* __restrict__ rv,
+                                               int64_t n, int inner, JWhere w, int ncols,
+                                               const int32_t* __restrict__ types_dev, JOut out,
+                                               unsigned long long* __restrict__ n_emitted) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const bool in = i < n;
+  bool emit = false, hit = false;
+  int64_t found = -1;
+  uint64_t meta = 0;
+  if (in && bit_get(kv, i) && bit_get(rv, i) && ts[i] >= 0) {
+    const int64_t key = keys[i];
+    uint64_t slot = key_hash(key) & mask;
+    for (int probe = 0; probe < JMAX_PROBE; probe++) {
+      const uint64_t* s = table + slot * (uint64_t)sw;
+      const uint64_t m = s[1];
+      if (m == 0) break;
+      if ((int64_t)s[0] == key) {
+        if (m & M_LIVE) {
+          hit = true;
+          found = (int64_t)slot;
+          meta = m;
+        }
+        break;
+      }
+      slot = (slot + 1) & mask;
+    }
+    emit = inner ? hit : true;
+    if (emit && w.active) emit = hit && where_ok(table + found * (uint64_t)sw, meta, w);
+  }
+  const uint64_t be = __ballot(emit), bh = __ballot(hit);
+  const int lane = threadIdx.x & 63;
+  const int64_t wbase = i - lane;
+  if (lane == 0 && wbase < n) {
+    // n may not be a multiple of 64: write whole bytes only up to the batch end
+    const int64_t nbytes = std::min<int64_t>(8, (n - wbase + 7) / 8);
+    for (int b = 0; b < nbytes; b++) {
+      if (out.emit) out.emit[wbase / 8 + b] = (uint8_t)(be >> (8 * b));
+      if (out.matched) out.matched[wbase / 8 + b] = (uint8_t)(bh >> (8 * b));
+    }
+  }
+  for (int c = 0; c < ncols; c++) {
+    const bool isnull = !hit || (meta & (1ULL << c));
+    const uint64_t bn = __ballot(isnull);
+    if (out.col_null[c] && lane == 0 && wbase < n) {
+      const int64_t nbytes = std::min<int64_t>(8, (n - wbase + 7) / 8);
+      for (int b = 0; b < nbytes; b++) out.col_null[c][wbase / 8 + b] = (uint8_t)(bn >> (8 * b));
+    }
+    if (in && out.col_data[c]) {
+      const uint64_t raw = hit ? table[found * (uint64_t)sw + 3 + c] : 0;
+      if (types_dev[c] == KHIP_TYPE_INT32) ((int32_t*)out.col_data[c])[i] = (int32_t)raw;
+      else ((uint64_t*)out.col_data[c])[i] = raw;
+    }
+  }
+  if (out.slot_out && in) out.slot_out[i] = emit ? found + 1 : -1;  // 0 = emitted LEFT miss
+  if (n_emitted) {
+    const int cnt = __popcll(be);
+    if (lane == 0 && cnt) atomicAdd(n_emitted, (unsigned long long)cnt);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_table_rehash(const uint64_t* __restrict__ old, int64_t ocap,
+                                                      uint64_t* __restrict__ nt, uint64_t nmask, int sw) {
+  for (int64_t slot = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; slot < ocap;
+       slot += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t* s = old + slot * (uint64_t)sw;
+    const uint64_t m = s[1];
+    if (!(m & M_LIVE)) continue;  // deleted keys are dropped on rehash
+    uint64_t d = key_hash((int64_t)s[0]) & nmask;
+    while (atomicCAS((unsigned long long*)&nt[d * sw + 1], 0ULL, (unsigned long long)m) != 0ULL) d = (d + 1) & nmask;
+    uint64_t* q = nt + d * (uint64_t)sw;
+    q[0] = s[0];
+    q[2] = 0;
+    for (int w = 3; w < sw; w++) q[w] = s[w];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_count_live(const uint64_t* __restrict__ table, int64_t cap, int sw,
+                                                    unsigned long long* __restrict__ n_live) {
+  int64_t c = 0;
+  for (int64_t slot = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; slot < cap;
+       slot += (int64_t)gridDim.x * blockDim.x)
+    c += (table[slot * (uint64_t)sw + 1] & M_LIVE) ? 1 : 0;
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(n_live, (unsigned long long)c);
+}
+
+static int jgrid(int64_t work, int cap_blocks = 8192) {
+  return (int)std::min<int64_t>(ceil_div(std::max<int64_t>(work, 1), 256), cap_blocks);
+}
+
+}  // namespace khip
+
+using namespace khip;
+
+struct khip_table {
+  khip_table_desc desc{};
+  std::vector<int32_t> col_types;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int sw = 4;
+  DevBuf table, types_dev, slot_of, scratch, st_keys, st_ts, st_kv, st_rv, st_cols[JMAX_COLS],
+      st_cval[JMAX_COLS], out_emit, out_matched, out_cols[JMAX_COLS], out_nulls[JMAX_COLS], out_slot;
+  int64_t cap = 0;
+  int64_t occ = 0;  // resident keys (live or deleted)
+  uint64_t epoch = 0;
+};
+
+static khip_status table_alloc(khip_table* t, DevBuf& buf, int64_t cap) {
+  KHIP_TRY(buf.ensure((size_t)cap * t->sw * 8));
+  KHIP_TRY_HIP(hipMemsetAsync(buf.p, 0, (size_t)cap * t->sw * 8, t->stream));
+  return KHIP_OK;
+}
+
+static khip_status table_grow(khip_table* t, int64_t new_cap) {
+  DevBuf nt;
+  KHIP_TRY(table_alloc(t, nt, new_cap));
+  hipLaunchKernelGGL(k_table_rehash, dim3(jgrid(t->cap)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->cap,
+                     nt.as<uint64_t>(), (uint64_t)(new_cap - 1), t->sw);
+  KHIP_TRY_HIP(hipGetLastError());
+  unsigned long long* ctr;
+  KHIP_TRY(t->scratch.ensure(64));
+  ctr = t->scratch.as<unsigned long long>();
+  KHIP_TRY_HIP(hipMemsetAsync(ctr, 0, 8, t->stream));
+  hipLaunchKernelGGL(k_count_live, dim3(jgrid(new_cap, 2048)), dim3(256), 0, t->stream, nt.as<uint64_t>(), new_cap,
+                     t->sw, ctr);
+  unsigned long long live = 0;
+  KHIP_TRY_HIP(hipMemcpyAsync(&live, ctr, 8, hipMemcpyDeviceToHost, t->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(t->stream));
+  t->table.release();
+  t->table = nt;
+  nt.p = nullptr;
+  t->cap = new_cap;
+  t->occ = (int64_t)live;
+  return KHIP_OK;
+}
+
+static khip_status jstage(khip_table* t, DevBuf& buf, const void* src, size_t bytes) {
+  KHIP_TRY(buf.ensure(bytes));
+  if (bytes) KHIP_TRY_HIP(hipMemcpyAsync(buf.p, src, bytes, hipMemcpyHostToDevice, t->stream));
+  return KHIP_OK;
+}
+
+// Resolve batch pointers to device memory (staging host batches).
+static khip_status jresolve(khip_table* t, const khip_batch* b, int ncols, const int64_t** keys,
+                            const int64_t** ts, const uint8_t** kv, const uint8_t** rv, JCols* cols) {
+  const int64_t n = b->n_rows;
+  const size_t bm = (size_t)(n + 7) / 8;
+  *keys = b->key_i64;
+  *ts = b->ts;
+  *kv = b->key_valid;
+  *rv = b->row_valid;
+  memset(cols, 0, sizeof(*cols));
+  if (b->mem == KHIP_MEM_DEVICE) {
+    for (int c = 0; c < ncols; c++) {
+      cols->data[c] = b->col_data[c];
+      cols->valid[c] = b->col_valid ? b->col_valid[c] : nullptr;
+    }
+    return KHIP_OK;
+  }
+  if (b->mem != KHIP_MEM_HOST) return fail(KHIP_E_INVALID, "batch mem");
+  KHIP_TRY(jstage(t, t->st_keys, b->key_i64, n * 8));
+  *keys = t->st_keys.as<int64_t>();
+  if (b->ts) {
+    KHIP_TRY(jstage(t, t->st_ts, b->ts, n * 8));
+    *ts = t->st_ts.as<int64_t>();
+  }
+  if (*kv) { KHIP_TRY(jstage(t, t->st_kv, b->key_valid, bm)); *kv = t->st_kv.as<uint8_t>(); }
+  if (*rv) { KHIP_TRY(jstage(t, t->st_rv, b->row_valid, bm)); *rv = t->st_rv.as<uint8_t>(); }
+  for (int c = 0; c < ncols; c++) {
+    const size_t es = t->col_types[c] == KHIP_TYPE_INT32 ? 4 : 8;
+    KHIP_TRY(jstage(t, t->st_cols[c], b->col_data[c], n * es));
+    cols->data[c] = t->st_cols[c].p;
+    const uint8_t* cv = b->col_valid ? b->col_valid[c] : nullptr;
+    if (cv) {
+      KHIP_TRY(jstage(t, t->st_cval[c], cv, bm));
+      cols->valid[c] = t->st_cval[c].as<uint8_t>();
+    }
+  }
+  return KHIP_OK;
+}
+
+static khip_status make_where(khip_table* t, const khip_where* w, JWhere* jw) {
+  memset(jw, 0, sizeof(*jw));
+  if (!w) return KHIP_OK;
+  if (w->right_col < 0 || w->right_col >= t->desc.n_cols) return fail(KHIP_E_INVALID, "where column");
+  if (w->op < KHIP_OP_GT || w->op > KHIP_OP_NE) return fail(KHIP_E_INVALID, "where op");
+  jw->active = 1;
+  jw->col = w->right_col;
+  jw->op = w->op;
+  jw->type = t->col_types[w->right_col];
+  jw->i64 = w->i64;
+  jw->f64 = w->f64;
+  return KHIP_OK;
+}
+
+extern "C" {
+
+khip_status khip_table_create(const khip_table_desc* d, khip_table** out) {
+  clear_error();
+  if (!d || !out) return fail(KHIP_E_INVALID, "null argument");
+  if (d->key_type != KHIP_KEY_INT64) return fail(KHIP_E_UNSUPPORTED, "table keys must be INT/BIGINT");
+  if (d->n_cols < 0 || d->n_cols > JMAX_COLS) return fail(KHIP_E_UNSUPPORTED, "at most 16 table columns");
+  for (int c = 0; c < d->n_cols; c++)
+    if (d->col_types[c] < KHIP_TYPE_INT32 || d->col_types[c] > KHIP_TYPE_DOUBLE)
+      return fail(KHIP_E_INVALID, "column type");
+  khip_table* t = new khip_table();
+  t->desc = *d;
+  t->col_types.assign(d->col_types, d->col_types + d->n_cols);
+  t->desc.col_types = t->col_types.data();
+  t->device = d->device;
+  t->sw = (int)next_pow2(std::max(4, 3 + d->n_cols));
+  DeviceGuard g(t->device);
+  if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete t;
+    return fail(KHIP_E_DEVICE, "hipStreamCreate failed (no device?)");
+  }
+  t->cap = next_pow2(std::max<int64_t>(1024, d->capacity_hint > 0 ? (d->capacity_hint * 4 + 2) / 3 : 1 << 16));
+  khip_status st;
+  if ((st = table_alloc(t, t->table, t->cap)) != KHIP_OK ||
+      (st = t->types_dev.ensure(sizeof(int32_t) * JMAX_COLS)) != KHIP_OK ||
+      (st = t->scratch.ensure(64)) != KHIP_OK) {
+    khip_table_destroy(t);
+    return st;
+  }
+  if (d->n_cols)
+    hipMemcpyAsync(t->types_dev.p, t->col_types.data(), sizeof(int32_t) * d->n_cols, hipMemcpyHostToDevice, t->stream);
+  if (hipStreamSynchronize(t->stream) != hipSuccess) {
+    khip_table_destroy(t);
+    return fail(KHIP_E_DEVICE, "device init failed");
+  }
+  *out = t;
+  return KHIP_OK;
+}
+
+khip_status khip_table_upsert(khip_table* t, const khip_batch* b) {
+  clear_error();
+  if (!t || !b) return fail(KHIP_E_INVALID, "null argument");
+  const int64_t n = b->n_rows;
+  if (n < 0 || b->n_cols < t->desc.n_cols) return fail(KHIP_E_INVALID, "batch shape");
+  if (n == 0) return KHIP_OK;
+  if (n >= (1LL << 40)) return fail(KHIP_E_UNSUPPORTED, "upsert batch too large");
+  if (!b->key_i64) return fail(KHIP_E_INVALID, "missing key column");
+  DeviceGuard g(t->device);
+  const int64_t* keys;
+  const int64_t* ts;
+  const uint8_t *kv, *rv;
+  JCols cols;
+  KHIP_TRY(jresolve(t, b, t->desc.n_cols, &keys, &ts, &kv, &rv, &cols));
+  // keep the load factor <= 0.75 even if every row were a new key
+  if (4 * (t->occ + n) > 3 * t->cap) KHIP_TRY(table_grow(t, next_pow2((4 * (t->occ + n) + 2) / 3)));
+  t->epoch++;
+  if (t->epoch >= (1ULL << 23)) return fail(KHIP_E_STATE, "upsert epoch space exhausted");
+  KHIP_TRY(t->slot_of.ensure(n * 8));
+  unsigned long long* ctr = t->scratch.as<unsigned long long>();
+  int* failp = (int*)(t->scratch.as<uint8_t>() + 16);
+  KHIP_TRY_HIP(hipMemsetAsync(t->scratch.p, 0, 64, t->stream));
+  hipLaunchKernelGGL(k_upsert_claim, dim3(jgrid(n)), dim3(256), 0, t->stream, t->table.as<uint64_t>(),
+                     (uint64_t)(t->cap - 1), t->sw, keys, kv, n, (uint64_t)t->epoch, t->slot_of.as<int64_t>(), failp,
+                     ctr);
+  hipLaunchKernelGGL(k_upsert_finalize, dim3(jgrid(t->cap)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->cap,
+                     t->sw, keys);
+  hipLaunchKernelGGL(k_upsert_apply, dim3(jgrid(n)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->sw,
+                     t->slot_of.as<int64_t>(), rv, n, (uint64_t)t->epoch, t->desc.n_cols, t->types_dev.as<int32_t>(),
+                     cols);
+  KHIP_TRY_HIP(hipGetLastError());
+  unsigned long long added = 0;
+  int failed = 0;
+  KHIP_TRY_HIP(hipMemcpyAsync(&added, ctr, 8, hipMemcpyDeviceToHost, t->stream));
+  KHIP_TRY_HIP(hipMemcpyAsync(&failed, failp, 4, hipMemcpyDeviceToHost, t->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(t->stream));
+  if (failed) return fail(KHIP_E_DEVICE, "table probe budget exhausted");
+  t->occ += (int64_t)added;
+  return KHIP_OK;
+}
+
+khip_status khip_table_size(khip_table* t, int64_t* n) {
+  clear_error();
+  if (!t || !n) return fail(KHIP_E_INVALID, "null argument");
+  DeviceGuard g(t->device);
+  unsigned long long* ctr = t->scratch.as<unsigned long long>();
+  KHIP_TRY_HIP(hipMemsetAsync(ctr, 0, 8, t->stream));
+  hipLaunchKernelGGL(k_count_live, dim3(jgrid(t->cap, 2048)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->cap,
+                     t->sw, ctr);
+  unsigned long long live = 0;
+  KHIP_TRY_HIP(hipMemcpyAsync(&live, ctr, 8, hipMemcpyDeviceToHost, t->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(t->stream));
+  *n = (int64_t)live;
+  return KHIP_OK;
+}
+
+static khip_status probe_launch(khip_table* t, const khip_batch* b, int32_t join_type, const khip_where* w,
+                                const JOut& out, unsigned long long* n_emitted) {
+  const int64_t n = b->n_rows;
+  const int64_t* keys;
+  const int64_t* ts;
+  const uint8_t *kv, *rv;
+  JCols cols;
+  KHIP_TRY(jresolve(t, b, 0, &keys, &ts, &kv, &rv, &cols));
+  if (!ts) return fail(KHIP_E_INVALID, "missing timestamp column");
+  JWhere jw;
+  KHIP_TRY(make_where(t, w, &jw));
+  hipLaunchKernelGGL(k_probe, dim3(ceil_div(n, 256)), dim3(256), 0, t->stream, t->table.as<uint64_t>(),
+                     (uint64_t)(t->cap - 1), t->sw, keys, ts, kv, rv, n, join_type == KHIP_JOIN_INNER ? 1 : 0, jw,
+                     t->desc.n_cols, t->types_dev.as<int32_t>(), out, n_emitted);
+  KHIP_TRY_HIP(hipGetLastError());
+  return KHIP_OK;
+}
+
+khip_status khip_table_probe(khip_table* t, const khip_batch* b, int32_t join_type, const khip_where* w,
+                             khip_join_out* out) {
+  clear_error();
+  if (!t || !b || !out) return fail(KHIP_E_INVALID, "null argument");
+  if (join_type != KHIP_JOIN_LEFT && join_type != KHIP_JOIN_INNER) return fail(KHIP_E_INVALID, "join type");
+  const int64_t n = b->n_rows;
+  if (n < 0) return fail(KHIP_E_INVALID, "batch shape");
+  if (n == 0) {
+    out->n_rows = 0;
+    return KHIP_OK;
+  }
+  if (!b->key_i64 || !b->ts) return fail(KHIP_E_INVALID, "missing key or timestamp column");
+  DeviceGuard g(t->device);
+  const int nc = t->desc.n_cols;
+  JOut o{};
+  KHIP_TRY(t->out_slot.ensure(n * 8));
+  o.slot_out = t->out_slot.as<int64_t>();
+  for (int c = 0; c < nc; c++) {
+    KHIP_TRY(t->out_cols[c].ensure(n * 8));
+    KHIP_TRY(t->out_nulls[c].ensure((n + 7) / 8 + 8));
+    o.col_data[c] = t->out_cols[c].p;
+    o.col_null[c] = t->out_nulls[c].as<uint8_t>();
+  }
+  KHIP_TRY(probe_launch(t, b, join_type, w, o, nullptr));
+  // compact on the host in arrival order (the host path is for parity/small batches)
+  std::vector<int64_t> slot(n);
+  KHIP_TRY_HIP(hipMemcpyAsync(slot.data(), o.slot_out, n * 8, hipMemcpyDeviceToHost, t->stream));
+  std::vector<std::vector<uint8_t>> cd(nc), cn(nc);
+  for (int c = 0; c < nc; c++) {
+    const size_t es = t->col_types[c] == KHIP_TYPE_INT32 ? 4 : 8;
+    cd[c].resize(n * es);
+    cn[c].resize((n + 7) / 8);
+    KHIP_TRY_HIP(hipMemcpyAsync(cd[c].data(), o.col_data[c], n * es, hipMemcpyDeviceToHost, t->stream));
+    KHIP_TRY_HIP(hipMemcpyAsync(cn[c].data(), o.col_null[c], (n + 7) / 8, hipMemcpyDeviceToHost, t->stream));
+  }
+  KHIP_TRY_HIP(hipStreamSynchronize(t->stream));
+  int64_t m = 0;
+  for (int64_t i = 0; i < n; i++) {
+    if (slot[i] == -1) continue;
+    if (m < out->capacity) {
+      const bool hit = slot[i] > 0;
+      if (out->stream_row) out->stream_row[m] = i;
+      if (out->matched) out->matched[m] = hit ? 1 : 0;
+      for (int c = 0; c < nc; c++) {
+        const bool isnull = (cn[c][i >> 3] >> (i & 7)) & 1;
+        if (out->col_null && out->col_null[c]) out->col_null[c][m] = isnull ? 1 : 0;
+        if (out->col_data && out->col_data[c]) {
+          if (t->col_types[c] == KHIP_TYPE_INT32) ((int32_t*)out->col_data[c])[m] = isnull ? 0 : ((int32_t*)cd[c].data())[i];
+          else ((uint64_t*)out->col_data[c])[m] = isnull ? 0 : ((uint64_t*)cd[c].data())[i];
+        }
+      }
+    }
+    m++;
+  }
+  out->n_rows = m;
+  if (m > out->capacity) return fail(KHIP_E_BUFFER, "join output capacity too small");
+  return KHIP_OK;
+}
+
+khip_status khip_table_probe_device(khip_table* t, const khip_batch* b, int32_t join_type, const khip_where* w,
+                                    const khip_join_dev_out* out, int64_t* n_emitted) {
+  clear_error();
+  if (!t || !b || !out) return fail(KHIP_E_INVALID, "null argument");
+  if (b->mem != KHIP_MEM_DEVICE) return fail(KHIP_E_INVALID, "probe_device needs a device batch");
+  if (join_type != KHIP_JOIN_LEFT && join_type != KHIP_JOIN_INNER) return fail(KHIP_E_INVALID, "join type");
+  const int64_t n = b->n_rows;
+  if (n < 0) return fail(KHIP_E_INVALID, "batch shape");
+  if (n == 0) {
+    if (n_emitted) *n_emitted = 0;
+    return KHIP_OK;
+  }
+  if (!b->key_i64 || !b->ts) return fail(KHIP_E_INVALID, "missing key or timestamp column");
+  DeviceGuard g(t->device);
+  JOut o{};
+  o.emit = out->emit;
+  o.matched = out->matched;
+  for (int c = 0; c < t->desc.n_cols; c++) {
+    o.col_data[c] = out->col_data ? out->col_data[c] : nullptr;
+    o.col_null[c] = out->col_null ? out->col_null[c] : nullptr;
+  }
+  unsigned long long* ctr = nullptr;
+  if (n_emitted) {
+    ctr = t->scratch.as<unsigned long long>() + 4;
+    KHIP_TRY_HIP(hipMemsetAsync(ctr, 0, 8, t->stream));
+  }
+  KHIP_TRY(probe_launch(t, b, join_type, w, o, ctr));
+  if (n_emitted) {
+    unsigned long long v = 0;
+    KHIP_TRY_HIP(hipMemcpyAsync(&v, ctr, 8, hipMemcpyDeviceToHost, t->stream));
+    KHIP_TRY_HIP(hipStreamSynchronize(t->stream));
+    *n_emitted = (int64_t)v;
+  }
+  return KHIP_OK;
+}
+
+khip_status khip_table_sync(khip_table* t) {
+  if (!t) return fail(KHIP_E_INVALID, "null argument");
+  DeviceGuard g(t->device);
+  KHIP_TRY_HIP(hipStreamSynchronize(t->stream));
+  return KHIP_OK;
+}
+
+khip_status khip_table_destroy(khip_table* t) {
+  if (!t) return KHIP_OK;
+  DeviceGuard g(t->device);
+  if (t->stream) hipStreamSynchronize(t->stream);
+  DevBuf* bufs[] = {&t->table, &t->types_dev, &t->slot_of, &t->scratch, &t->st_keys, &t->st_ts, &t->st_kv,
+                    &t->st_rv, &t->out_emit, &t->out_matched, &t->out_slot};
+  for (DevBuf* x : bufs) x->release();
+  for (int c = 0; c < JMAX_COLS; c++) {
+    t->st_cols[c].release();
+    t->st_cval[c].release();
+    t->out_cols[c].release();
+    t->out_nulls[c].release();
+  }
+  if (t->stream) hipStreamDestroy(t->stream);
+  delete t;
+  return KHIP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,162 @@
+// khip_util.hpp — shared host/device helpers for libksqldb_hip.so (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/ksqldb_hip.h"
+
+namespace khip {
+
+// ----------------------------------------------------------------- errors
+void set_error(const std::string& msg);
+void clear_error();
+
+#define KHIP_TRY_HIP(expr)                                                            \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess) {                                                           \
+      ::khip::set_error(std::string(#expr) + ": " + hipGetErrorString(_e));           \
+      return KHIP_E_DEVICE;                                                           \
+    }                                                                                 \
+  } while (0)
+
+#define KHIP_TRY(expr)              \
+  do {                              \
+    khip_status _s = (expr);        \
+    if (_s != KHIP_OK) return _s;   \
+  } while (0)
+
+inline khip_status fail(khip_status s, const std::string& msg) {
+  set_error(msg);
+  return s;
+}
+
+// Grow-only device buffer.
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  khip_status ensure(size_t want) {
+    if (want <= bytes) return KHIP_OK;
+    if (p) hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    size_t b = want < 256 ? 256 : want;
+    if (hipMalloc(&p, b) != hipSuccess) {
+      p = nullptr;
+      return fail(KHIP_E_NOMEM, "hipMalloc failed for " + std::to_string(b) + " bytes");
+    }
+    bytes = b;
+    return KHIP_OK;
+  }
+  template <class T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+// Pinned host staging buffer (grow-only).
+struct HostBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  khip_status ensure(size_t want) {
+    if (want <= bytes) return KHIP_OK;
+    if (p) hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    size_t b = want < 256 ? 256 : want;
+    if (hipHostMalloc(&p, b, hipHostMallocDefault) != hipSuccess) {
+      p = nullptr;
+      return fail(KHIP_E_NOMEM, "hipHostMalloc failed");
+    }
+    bytes = b;
+    return KHIP_OK;
+  }
+  template <class T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+  void release() {
+    if (p) hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+// RAII device guard.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    hipGetDevice(&prev);
+    if (prev != dev) hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    hipGetDevice(&cur);
+    if (prev >= 0 && cur != prev) hipSetDevice(prev);
+  }
+};
+
+// --------------------------------------------------------------- device helpers
+
+__host__ __device__ inline uint64_t mix64(uint64_t h) {
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdULL;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ULL;
+  h ^= h >> 33;
+  return h;
+}
+
+// Hash of a (key, windowStart) group.
+__host__ __device__ inline uint64_t group_hash(int64_t key, int64_t ws) {
+  return mix64((uint64_t)key ^ mix64((uint64_t)ws + 0x9E3779B97F4A7C15ULL));
+}
+
+__device__ inline bool bit_get(const uint8_t* bm, int64_t i) {
+  return bm == nullptr ? true : ((bm[i >> 3] >> (i & 7)) & 1);
+}
+
+// Total-order key for Java Double.compareTo (NaN canonical & largest, -0.0 < 0.0):
+// signed comparison of the returned key == Double.compare.  Involution on non-NaN.
+__host__ __device__ inline int64_t f64_order_key(double d) {
+  uint64_t u;
+  __builtin_memcpy(&u, &d, 8);
+  if ((u & 0x7ff0000000000000ULL) == 0x7ff0000000000000ULL && (u & 0x000fffffffffffffULL))
+    u = 0x7ff8000000000000ULL;
+  int64_t k = (int64_t)u;
+  return k ^ ((k >> 63) & 0x7fffffffffffffffLL);
+}
+__host__ __device__ inline double f64_from_order_key(int64_t k) {
+  int64_t b = k ^ ((k >> 63) & 0x7fffffffffffffffLL);
+  double d;
+  __builtin_memcpy(&d, &b, 8);
+  return d;
+}
+
+__host__ __device__ inline int64_t grace_of(const khip_agg_desc& d) {
+  if (d.window_kind == KHIP_WINDOW_NONE) return 0;
+  if (d.grace_ms >= 0) return d.grace_ms;
+  int64_t g = 86400000LL - d.size_ms;
+  return g > 0 ? g : 0;
+}
+
+// TimeWindows.windowsFor first window start.
+__host__ __device__ inline int64_t first_window_start(int64_t ts, int64_t size, int64_t adv) {
+  int64_t lo = ts - size + adv;
+  if (lo < 0) lo = 0;
+  return (lo / adv) * adv;
+}
+
+inline int64_t next_pow2(int64_t v) {
+  int64_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace khip
