@@ -283,7 +283,7 @@ class AggHandle:
 
     def push(self, batch, stats=True):
         st = BatchStats()
-        self.lib.check(self.lib.agg_push(self.h, C.byref(batch.struct if isinstance(batch, HostBatch) else batch),
+        self.lib.check(self.lib.agg_push(self.h, C.byref(batch.struct if hasattr(batch, "struct") else batch),
                                          C.byref(st) if stats else None), "agg_push")
         return st.as_dict() if stats else None
 

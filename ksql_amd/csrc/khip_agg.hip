@@ -37,7 +37,7 @@ constexpr int BLOCK = 256;
 constexpr int ITEMS = 8;
 constexpr int RPB = BLOCK * ITEMS;  // records per block (k_blockmax and k_apply agree)
 constexpr int MAX_COLS = 8;
-constexpr int MAX_OPS = 24;
+constexpr int MAX_OPS = 40;
 constexpr int MAX_PROBE = 2048;
 constexpr int MAX_FANOUT = 4095;  // windows per record encodable in a claim reference
 constexpr int64_t EMPTY_WS = INT64_MIN;
@@ -379,7 +379,7 @@ __global__ __launch_bounds__(256) void k_finalize(uint64_t* __restrict__ table, 
 }
 
 struct InitWords {
-  int64_t w[16];
+  int64_t w[32];
 };
 
 __global__ __launch_bounds__(256) void k_init_table(uint64_t* __restrict__ table, int64_t cap, int sw,
@@ -764,7 +764,7 @@ static khip_status plan_state(khip_agg* a) {
     if (s.kind == KHIP_AGG_MIN && w_min[c] < 0) w_min[c] = word++;
     if (s.kind == KHIP_AGG_MAX && w_max[c] < 0) w_max[c] = word++;
   }
-  if (word > 16) return fail(KHIP_E_UNSUPPORTED, "too many aggregate state words (max 13)");
+  if (word > 32) return fail(KHIP_E_UNSUPPORTED, "too many aggregate state words (max 29)");
   a->sw = (int)next_pow2(std::max(word, 4));
   ApplyParams& p = a->ap;
   p.windowed = a->windowed;
@@ -789,7 +789,7 @@ static khip_status plan_state(khip_agg* a) {
     if (w_max[c] >= 0) add(OP_MAX, c, w_max[c]);
   }
   p.n_ops = n;
-  for (int w = 0; w < 16; w++) a->init.w[w] = 0;
+  for (int w = 0; w < 32; w++) a->init.w[w] = 0;
   a->init.w[1] = EMPTY_WS;
   a->init.w[2] = INT64_MIN;
   for (int c = 0; c < d.n_cols; c++) {

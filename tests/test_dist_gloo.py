@@ -1,0 +1,96 @@
+"""Multi-process (world_size 2, gloo, CPU) coverage of the N>1 path.
+
+bench.py shards the key space across ranks (rank r owns keys k with k % N == r, the
+Kafka key-partitioning analogue) and runs one independent task per rank with its own
+stream time; the final table is the disjoint union of the shards and the throughput is
+all records / max-over-ranks time.  Here each rank runs the CPU oracle on its shard
+(the GPU path is covered by the -m gpu parity tests), and rank 0 checks that the union
+equals one task over all records (no late drops at this disorder),
+and that the max-over-ranks reduction the bench uses is what it claims.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from ksql_amd import abi, synth
+
+WORLD = 2
+N = 30_000
+KEYS = 700
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _shard_snapshot(rank, world):
+    card, ts = synth.possible_fraud(0, N, N, rank=rank, world=world, keys=KEYS)
+    h = abi.AggHandle(abi.load_oracle(), abi.make_agg_desc(window_kind="TUMBLING", size_ms=5000,
+                                                           key_type="INT64", aggs=[("COUNT_STAR", -1)]))
+    h.push(abi.HostBatch(ts, keys=card))
+    s = h.snapshot()
+    h.close()
+    return card, ts, s
+
+
+def _worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        card, ts, s = _shard_snapshot(rank, WORLD)
+        shard = {"key": s["key"], "ws": s["ws"], "cnt": s["values"][0], "rt": s["rowtime"],
+                 "card": card, "ts": ts}
+        gathered = [None] * WORLD
+        dist.all_gather_object(gathered, shard)
+        # the bench's timing reduction: MAX over ranks
+        t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if rank == 0:
+            q.put((gathered, float(t.item())))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_key_sharded_union_equals_single_task():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    gathered, tmax = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert tmax == float(WORLD)
+    # shards own disjoint keys
+    k0, k1 = set(gathered[0]["key"].tolist()), set(gathered[1]["key"].tolist())
+    assert not (k0 & k1)
+    # union of shard tables == one task over every record (arrival order: shard 0 then 1)
+    card = np.concatenate([g["card"] for g in gathered])
+    ts = np.concatenate([g["ts"] for g in gathered])
+    h = abi.AggHandle(abi.load_oracle(), abi.make_agg_desc(window_kind="TUMBLING", size_ms=5000,
+                                                           key_type="INT64", aggs=[("COUNT_STAR", -1)]))
+    h.push(abi.HostBatch(ts, keys=card))
+    ref = h.snapshot()
+    h.close()
+    key = np.concatenate([g["key"] for g in gathered])
+    ws = np.concatenate([g["ws"] for g in gathered])
+    cnt = np.concatenate([g["cnt"] for g in gathered])
+    rt = np.concatenate([g["rt"] for g in gathered])
+    order = np.lexsort((ws, key))
+    assert np.array_equal(key[order], ref["key"])
+    assert np.array_equal(ws[order], ref["ws"])
+    assert np.array_equal(cnt[order], ref["values"][0])
+    assert np.array_equal(rt[order], ref["rowtime"])
+    assert cnt.sum() == WORLD * N
