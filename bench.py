@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--engine", choices=["part", "atomic"], default="part")
     return ap.parse_args()
 
 
@@ -106,7 +107,8 @@ def main():
     torch.cuda.synchronize()
     batch = abi.DeviceBatch(ts, keys=card)
     desc = abi.make_agg_desc(window_kind="TUMBLING", size_ms=5000, key_type="INT64", aggs=[("COUNT_STAR", -1)],
-                             device=local, capacity_hint=int(min(3 * args.keys, 2 * n)), flags=abi.FLAG_PROFILE)
+                             device=local, capacity_hint=int(min(3 * args.keys, 2 * n)),
+                             flags=abi.FLAG_PROFILE | (abi.FLAG_ENGINE_ATOMIC if args.engine == "atomic" else 0))
     h = abi.AggHandle(lib, desc)
     having = {"agg": 0, "op": "GT", "value": 3}
 
@@ -116,7 +118,7 @@ def main():
         rows = h.count_rows(having)
         return st, rows
 
-    for _ in range(args.warmup):
+    for _ in range(max(args.warmup, 1)):
         st, rows = step()
     assert st["rows_accepted"] == n and st["windows_applied"] == n, st
     h.kernel_times(reset=True)
@@ -176,8 +178,9 @@ def main():
             "roofline": {"bound": "hbm", "kernel": "k_apply", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_record": BYTES_PER_RECORD_C2, "apply_ms_per_launch": apply_ms,
+                         "engine": args.engine,
                          "phase_ms_per_step": {k: kt[k] / max(args.steps, 1) for k in
-                                               ("stream_time_ms", "apply_ms", "finalize_ms")}},
+                                               ("stream_time_ms", "partition_ms", "apply_ms", "finalize_ms")}},
             "pcie_inclusive_records_per_s": pcie,
         }
         if world == 1 and not args.no_cpu_baseline:

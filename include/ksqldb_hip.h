@@ -224,14 +224,18 @@ khip_status khip_agg_sync(khip_agg* agg);
 /* desc.flags bit: record HIP events around each kernel phase of khip_agg_push (the
  * Kafka Streams per-processor latency sensors' analogue; off by default). */
 #define KHIP_FLAG_PROFILE 1
+/* desc.flags bit: use the global-atomic engine (one HBM hash table updated with
+ * agent-scope atomics) instead of the default partitioned LDS engine. */
+#define KHIP_FLAG_ENGINE_ATOMIC 2
 
 /* Cumulative device time per phase since creation or the last reset of the counters,
  * measured with HIP events on the handle's stream (valid with KHIP_FLAG_PROFILE). */
 typedef struct khip_kernel_times {
-  double stream_time_ms; /* k_blockmax + k_scan_blocks                               */
+  double stream_time_ms; /* stream-time maxima/scans (+ partition histogram, offsets)  */
   double dict_ms;        /* UTF8 key dictionary                                       */
-  double apply_ms;       /* k_apply: window fan-out + (key, window) upsert + atomics  */
-  double finalize_ms;    /* k_finalize + partial-counter reduction                   */
+  double partition_ms;   /* partitioned engine: k_part_scatter                        */
+  double apply_ms;       /* k_part_agg (LDS aggregation) or k_apply (global atomics)  */
+  double finalize_ms;    /* atomic engine: k_finalize + counter reduction             */
   int64_t apply_launches;
   int64_t records;       /* records covered by those apply launches (first passes)    */
 } khip_kernel_times;

@@ -27,6 +27,7 @@ OP = {"GT": 0, "GE": 1, "LT": 2, "LE": 3, "EQ": 4, "NE": 5}
 JOIN = {"LEFT": 0, "INNER": 1}
 MEM_HOST, MEM_DEVICE = 0, 1
 FLAG_PROFILE = 1
+FLAG_ENGINE_ATOMIC = 2
 NP_TYPE = {0: np.int32, 1: np.int64, 2: np.float64}
 
 i32, i64, u8p = C.c_int32, C.c_int64, C.POINTER(C.c_uint8)
@@ -81,7 +82,8 @@ class Where(C.Structure):
 
 
 class KernelTimes(C.Structure):
-    _fields_ = [("stream_time_ms", C.c_double), ("dict_ms", C.c_double), ("apply_ms", C.c_double),
+    _fields_ = [("stream_time_ms", C.c_double), ("dict_ms", C.c_double), ("partition_ms", C.c_double),
+                ("apply_ms", C.c_double),
                 ("finalize_ms", C.c_double), ("apply_launches", i64), ("records", i64)]
 
     def as_dict(self):

@@ -31,121 +31,9 @@
 
 #include "khip_util.hpp"
 
+#include "khip_agg_internal.hpp"
+
 namespace khip {
-
-constexpr int BLOCK = 256;
-constexpr int ITEMS = 8;
-constexpr int RPB = BLOCK * ITEMS;  // records per block (k_blockmax and k_apply agree)
-constexpr int MAX_COLS = 8;
-constexpr int MAX_OPS = 40;
-constexpr int MAX_PROBE = 2048;
-constexpr int MAX_FANOUT = 4095;  // windows per record encodable in a claim reference
-constexpr int64_t EMPTY_WS = INT64_MIN;
-constexpr int NPART = 8;
-
-enum { P_ACCEPTED, P_NULL_KEY, P_NULL_ROW, P_BAD_TS, P_APPLIED, P_LATE, P_FAILED, P_NEW };
-
-enum OpKind : int8_t { OP_INC = 0, OP_INC_VALID, OP_ADD_I64, OP_ADD_F64, OP_MIN, OP_MAX };
-
-struct UpdOp {
-  int8_t kind;
-  int8_t col;
-  int16_t word;
-};
-
-struct ApplyParams {
-  int32_t windowed;
-  int32_t slot_words;
-  int64_t size, adv, grace;
-  int32_t n_cols;
-  int32_t n_ops;
-  int32_t col_type[MAX_COLS];
-  UpdOp ops[MAX_OPS];
-};
-
-struct ColPtrs {
-  const void* data[MAX_COLS];
-  const uint8_t* valid[MAX_COLS];
-};
-
-// How one aggregate's result is decoded from the state words.
-struct AggOut {
-  int32_t kind;   // KHIP_AGG_*
-  int32_t type;   // input column type (INT64 for COUNT*)
-  int32_t w_val;  // value word
-  int32_t w_cnt;  // non-null count word (-1 if none)
-};
-
-struct HavingDev {
-  int32_t active;
-  int32_t op;
-  AggOut a;
-  int64_t i64;
-  double f64;
-};
-
-// ------------------------------------------------------------------ device utils
-
-__device__ __forceinline__ int64_t wave_incl_max(int64_t v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    int64_t t = __shfl_up(v, off, 64);
-    if (lane >= off) v = t > v ? t : v;
-  }
-  return v;
-}
-
-// Inclusive prefix max over the block (blockDim.x threads, multiple of 64).
-__device__ __forceinline__ int64_t block_incl_max(int64_t v, int64_t* lds, int64_t* total) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  v = wave_incl_max(v);
-  if (lane == 63) lds[wave] = v;
-  __syncthreads();
-  int64_t pre = INT64_MIN, tot = INT64_MIN;
-  for (int w = 0; w < nw; w++) {
-    int64_t x = lds[w];
-    if (w < wave) pre = x > pre ? x : pre;
-    tot = x > tot ? x : tot;
-  }
-  __syncthreads();
-  *total = tot;
-  return v > pre ? v : pre;
-}
-
-__device__ __forceinline__ int64_t wave_sum(int64_t v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-
-__device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ uint64_t hash_bytes_dev(const uint8_t* p, int64_t n) {
-  uint64_t h = 0x84222325cbf29ce4ULL ^ (uint64_t)n;
-  int64_t i = 0;
-  for (; i + 8 <= n; i += 8) {
-    uint64_t w = 0;
-    for (int b = 0; b < 8; b++) w |= (uint64_t)p[i + b] << (8 * b);
-    h = mix64(h ^ w) * 0x9E3779B97F4A7C15ULL;
-  }
-  uint64_t w = 0;
-  for (int b = 0; i + b < n; b++) w |= (uint64_t)p[i + b] << (8 * b);
-  return mix64(h ^ w ^ ((uint64_t)(n & 7) << 59));
-}
-
-__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, int64_t n) {
-  for (int64_t i = 0; i < n; i++)
-    if (a[i] != b[i]) return false;
-  return true;
-}
-
-__device__ __forceinline__ int64_t load_col_raw(const ColPtrs& c, int32_t type, int col, int64_t i) {
-  if (type == KHIP_TYPE_INT32) return (int64_t)((const int32_t*)c.data[col])[i];
-  return ((const int64_t*)c.data[col])[i];  // INT64, or DOUBLE bits
-}
 
 // ------------------------------------------------------------------- kernels
 
@@ -378,10 +266,6 @@ __global__ __launch_bounds__(256) void k_finalize(uint64_t* __restrict__ table, 
   }
 }
 
-struct InitWords {
-  int64_t w[32];
-};
-
 __global__ __launch_bounds__(256) void k_init_table(uint64_t* __restrict__ table, int64_t cap, int sw,
                                                     InitWords init) {
   const int64_t total = cap * sw;
@@ -429,71 +313,6 @@ __global__ __launch_bounds__(256) void k_rehash(const uint64_t* __restrict__ old
       d = (d + 1) & nmask;
     }
   }
-}
-
-__device__ __forceinline__ bool decode_result(const uint64_t* s, const AggOut& a, int64_t* iv, double* dv) {
-  // returns false for SQL NULL; sets *iv for integer results, *dv for DOUBLE results
-  switch (a.kind) {
-    case KHIP_AGG_COUNT_STAR:
-    case KHIP_AGG_COUNT:
-      *iv = (int64_t)s[a.w_val];
-      return true;
-    case KHIP_AGG_SUM:
-      if (a.type == KHIP_TYPE_DOUBLE) __builtin_memcpy(dv, &s[a.w_val], 8);
-      else if (a.type == KHIP_TYPE_INT32) *iv = (int64_t)(int32_t)s[a.w_val];
-      else *iv = (int64_t)s[a.w_val];
-      return true;
-    case KHIP_AGG_MIN:
-    case KHIP_AGG_MAX:
-      if ((int64_t)s[a.w_cnt] == 0) return false;
-      if (a.type == KHIP_TYPE_DOUBLE) *dv = f64_from_order_key((int64_t)s[a.w_val]);
-      else *iv = (int64_t)s[a.w_val];
-      return true;
-    case KHIP_AGG_AVG: {
-      const int64_t c = (int64_t)s[a.w_cnt];
-      if (c == 0) { *dv = 0.0; return true; }
-      if (a.type == KHIP_TYPE_DOUBLE) {
-        double sum;
-        __builtin_memcpy(&sum, &s[a.w_val], 8);
-        *dv = sum / (double)c;
-      } else if (a.type == KHIP_TYPE_INT32) {
-        *dv = (double)(int32_t)s[a.w_val] / (double)c;
-      } else {
-        *dv = (double)(int64_t)s[a.w_val] / (double)c;
-      }
-      return true;
-    }
-  }
-  return false;
-}
-
-__device__ __forceinline__ bool result_is_double(const AggOut& a) {
-  if (a.kind == KHIP_AGG_AVG) return true;
-  if (a.kind == KHIP_AGG_COUNT || a.kind == KHIP_AGG_COUNT_STAR) return false;
-  return a.type == KHIP_TYPE_DOUBLE;
-}
-
-__device__ __forceinline__ bool having_ok(const uint64_t* s, const HavingDev& h) {
-  if (!h.active) return true;
-  int64_t iv = 0;
-  double dv = 0.0;
-  if (!decode_result(s, h.a, &iv, &dv)) return false;
-  int c;
-  if (result_is_double(h.a)) {
-    if (dv != dv) return h.op == KHIP_OP_NE;
-    c = dv < h.f64 ? -1 : (dv > h.f64 ? 1 : 0);
-  } else {
-    c = iv < h.i64 ? -1 : (iv > h.i64 ? 1 : 0);
-  }
-  switch (h.op) {
-    case KHIP_OP_GT: return c > 0;
-    case KHIP_OP_GE: return c >= 0;
-    case KHIP_OP_LT: return c < 0;
-    case KHIP_OP_LE: return c <= 0;
-    case KHIP_OP_EQ: return c == 0;
-    case KHIP_OP_NE: return c != 0;
-  }
-  return false;
 }
 
 // Compact resident slots passing HAVING into `out` (sw words per row); out may be null
@@ -705,48 +524,6 @@ static int grid_for(int64_t work, int per_block, int cap_blocks = 2048 * 8) {
 
 using namespace khip;
 
-struct khip_agg {
-  khip_agg_desc desc{};
-  std::vector<int32_t> col_types;
-  std::vector<khip_agg_spec> aggs;
-  int device = 0;
-  hipStream_t stream = nullptr;
-  int64_t grace = 0;
-  int windowed = 0;
-  int max_fanout = 1;
-  ApplyParams ap{};
-  InitWords init{};
-  std::vector<AggOut> outs;
-  int sw = 4;
-  // table
-  DevBuf table;
-  int64_t cap = 0;
-  int64_t occ = 0;  // resident groups
-  // per-batch scratch
-  DevBuf blockmax, blockprefix, partials, resume, counters, stream_time;
-  DevBuf st_keys, st_ts, st_kv, st_rv, st_koff, st_kbytes;  // host staging copies
-  DevBuf st_cols[MAX_COLS], st_cval[MAX_COLS];
-  DevBuf kid, khash;  // UTF8
-  int64_t resume_n = 0;
-  // UTF8 dictionary
-  DevBuf dword, dkid, arena, dict_bsum, dict_fail;
-  int64_t dcap = 0, docc = 0, arena_used = 0;
-  int64_t host_stream_time = -1;
-  // profiling (KHIP_FLAG_PROFILE)
-  bool profile = false;
-  hipEvent_t ev[8] = {};
-  khip_kernel_times times{};
-};
-
-static void ev_record(khip_agg* a, int i) {
-  if (a->profile) hipEventRecord(a->ev[i], a->stream);
-}
-static double ev_ms(khip_agg* a, int i, int j) {
-  float ms = 0.f;
-  if (a->profile) hipEventElapsedTime(&ms, a->ev[i], a->ev[j]);
-  return (double)ms;
-}
-
 static khip_status plan_state(khip_agg* a) {
   const khip_agg_desc& d = a->desc;
   int word = 3;  // w0, w1, rowtime
@@ -923,11 +700,14 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
     return fail(KHIP_E_DEVICE, "hipStreamCreate failed (no device?)");
   }
   a->profile = (d.flags & KHIP_FLAG_PROFILE) != 0;
+  a->engine = (d.flags & KHIP_FLAG_ENGINE_ATOMIC) ? 1 : 0;
   if (a->profile)
     for (int e = 0; e < 8; e++) hipEventCreate(&a->ev[e]);
-  int64_t cap = next_pow2(std::max<int64_t>(1024, d.capacity_hint > 0 ? d.capacity_hint * 2 : 1 << 16));
+  int64_t cap = a->engine == 1 ? next_pow2(std::max<int64_t>(1024, d.capacity_hint > 0 ? d.capacity_hint * 2 : 1 << 16))
+                                : 1024;
   if ((st = init_table(a, a->table, cap)) != KHIP_OK || (st = a->stream_time.ensure(8)) != KHIP_OK ||
-      (st = a->counters.ensure(8 * NPART)) != KHIP_OK) {
+      (st = a->counters.ensure(8 * NPART)) != KHIP_OK ||
+      (a->engine == 0 && (st = part_init(a, d.capacity_hint > 0 ? d.capacity_hint : (1 << 20))) != KHIP_OK)) {
     khip_agg_destroy(a);
     return st;
   }
@@ -1018,28 +798,11 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   } else {
     return fail(KHIP_E_INVALID, "batch mem");
   }
-  // ---- scratch
-  const int64_t nb = ceil_div(n, RPB);
-  KHIP_TRY(a->blockmax.ensure(nb * 8));
-  KHIP_TRY(a->blockprefix.ensure(nb * 8));
-  KHIP_TRY(a->partials.ensure(nb * 8 * NPART));
-  if (a->resume_n < n) {
-    KHIP_TRY(a->resume.ensure(n * 4));
-    KHIP_TRY_HIP(hipMemsetAsync(a->resume.p, 0xFF, n * 4, a->stream));
-    a->resume_n = n;
-  }
-  KHIP_TRY_HIP(hipMemsetAsync(a->counters.p, 0, 8 * NPART, a->stream));
-  // ---- stream time before each block
-  ev_record(a, 0);
-  hipLaunchKernelGGL(k_blockmax, dim3(nb), dim3(BLOCK), 0, a->stream, ts, kv, rv, n, a->blockmax.as<int64_t>());
-  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, a->stream, a->blockmax.as<int64_t>(), nb,
-                     a->blockprefix.as<int64_t>(), a->stream_time.as<int64_t>());
-  KHIP_TRY_HIP(hipGetLastError());
-  ev_record(a, 1);
   // ---- UTF8 keys → stable key ids
   const int64_t* hkeys = keys;
   if (utf8) {
     KHIP_TRY_HIP(hipStreamSynchronize(a->stream));  // key_bytes_total for device batches
+    ev_record(a, 1);
     if (2 * (a->docc + n) > a->dcap) KHIP_TRY(grow_dict(a, next_pow2(4 * (a->docc + n))));
     KHIP_TRY(a->kid.ensure(n * 8));
     KHIP_TRY(a->khash.ensure(n * 8));
@@ -1082,12 +845,53 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
     a->docc = std::min<int64_t>(a->dcap, a->docc + std::min<int64_t>(n, added / 16));
     keys = a->kid.as<int64_t>();
     hkeys = a->khash.as<int64_t>();
+    ev_record(a, 2);
   }
+  int64_t tot[NPART] = {0};
+  if (a->engine == 0) {
+    // ---- partitioned engine, in slices of < 2^31 records (multiple of 8: bitmaps stay byte aligned)
+    const int64_t slice = 1LL << 31;
+    for (int64_t off = 0; off < n; off += slice) {
+      const int64_t m = std::min(slice, n - off);
+      ColPtrs cs = cols;
+      for (int c = 0; c < a->desc.n_cols; c++) {
+        cs.data[c] = (const char*)cols.data[c] + off * (a->col_types[c] == KHIP_TYPE_INT32 ? 4 : 8);
+        if (cs.valid[c]) cs.valid[c] += off / 8;
+      }
+      KHIP_TRY(part_push(a, m, keys + off, ts + off, kv ? kv + off / 8 : nullptr, rv ? rv + off / 8 : nullptr, cs,
+                         tot));
+    }
+    a->occ += tot[P_NEW];
+    if (a->profile) {  // events of the last slice
+      a->times.stream_time_ms += ev_ms(a, 3, 4);
+      a->times.partition_ms += ev_ms(a, 4, 5);
+      a->times.apply_ms += ev_ms(a, 5, 6);
+      if (utf8) a->times.dict_ms += ev_ms(a, 1, 2);
+      a->times.records += n;
+      a->times.apply_launches++;
+    }
+  } else {
+  // ---- scratch
+  const int64_t nb = ceil_div(n, RPB);
+  KHIP_TRY(a->blockmax.ensure(nb * 8));
+  KHIP_TRY(a->blockprefix.ensure(nb * 8));
+  KHIP_TRY(a->partials.ensure(nb * 8 * NPART));
+  if (a->resume_n < n) {
+    KHIP_TRY(a->resume.ensure(n * 4));
+    KHIP_TRY_HIP(hipMemsetAsync(a->resume.p, 0xFF, n * 4, a->stream));
+    a->resume_n = n;
+  }
+  KHIP_TRY_HIP(hipMemsetAsync(a->counters.p, 0, 8 * NPART, a->stream));
+  // ---- stream time before each block (atomic engine)
+  ev_record(a, 0);
+  hipLaunchKernelGGL(k_blockmax, dim3(nb), dim3(BLOCK), 0, a->stream, ts, kv, rv, n, a->blockmax.as<int64_t>());
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, a->stream, a->blockmax.as<int64_t>(), nb,
+                     a->blockprefix.as<int64_t>(), a->stream_time.as<int64_t>());
+  KHIP_TRY_HIP(hipGetLastError());
   ev_record(a, 2);
   // ---- grow the group table ahead of time if the resident load is high
   if (2 * a->occ > a->cap) KHIP_TRY(grow_table(a, a->cap * 4));
   // ---- apply (+ resume passes after doubling on probe exhaustion)
-  int64_t tot[NPART] = {0};
   const int64_t occ0 = a->occ;
   double apply_ms = 0, fin_ms = 0;
   for (int pass = 0;; pass++) {
@@ -1112,8 +916,8 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
       apply_ms += ev_ms(a, 3, 4);
       fin_ms += ev_ms(a, 4, 5);
       if (pass == 0) {
-        a->times.stream_time_ms += ev_ms(a, 0, 1);
-        a->times.dict_ms += ev_ms(a, 1, 2);
+        a->times.stream_time_ms += ev_ms(a, 0, 3);
+        if (utf8) a->times.dict_ms += ev_ms(a, 1, 2);
         a->times.records += n;
       }
       a->times.apply_launches++;
@@ -1124,6 +928,7 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   }
   a->times.apply_ms += apply_ms;
   a->times.finalize_ms += fin_ms;
+  }
   KHIP_TRY_HIP(hipMemcpyAsync(&a->host_stream_time, a->stream_time.p, 8, hipMemcpyDeviceToHost, a->stream));
   KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
   s.rows_accepted = tot[P_ACCEPTED];
@@ -1147,6 +952,11 @@ static khip_status compact_rows(khip_agg* a, const khip_having* h, std::vector<u
     hd.a = a->outs[h->agg_index];
     hd.i64 = h->i64;
     hd.f64 = h->f64;
+  }
+  if (a->engine == 0) {
+    KHIP_TRY(part_compact(a, hd, rows, count));
+    if (rows && *count > a->occ) return fail(KHIP_E_STATE, "group count bookkeeping mismatch");
+    return KHIP_OK;
   }
   DevBuf ctr, out;
   KHIP_TRY(ctr.ensure(8));
@@ -1299,6 +1109,7 @@ khip_status khip_agg_reset(khip_agg* a) {
                      a->table.as<uint64_t>(), a->cap, a->sw, a->init);
   int64_t m1 = -1;
   KHIP_TRY_HIP(hipMemcpyAsync(a->stream_time.p, &m1, 8, hipMemcpyHostToDevice, a->stream));
+  if (a->engine == 0) KHIP_TRY(part_reset(a));
   if (a->desc.key_type == KHIP_KEY_UTF8) {
     KHIP_TRY_HIP(hipMemsetAsync(a->dword.p, 0, a->dcap * 8, a->stream));
     a->docc = 0;
@@ -1344,6 +1155,7 @@ khip_status khip_agg_destroy(khip_agg* a) {
     a->st_cols[c].release();
     a->st_cval[c].release();
   }
+  part_release(a);
   for (int e = 0; e < 8; e++)
     if (a->ev[e]) hipEventDestroy(a->ev[e]);
   if (a->stream) hipStreamDestroy(a->stream);

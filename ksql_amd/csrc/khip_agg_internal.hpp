@@ -1,0 +1,275 @@
+// khip_agg_internal.hpp — shared declarations of the aggregate engines.
+#pragma once
+
+#include <vector>
+
+#include "khip_util.hpp"
+
+namespace khip {
+
+constexpr int BLOCK = 256;
+constexpr int ITEMS = 8;
+constexpr int RPB = BLOCK * ITEMS;  // records per block (k_blockmax and k_apply agree)
+constexpr int MAX_COLS = 8;
+constexpr int MAX_OPS = 40;
+constexpr int MAX_PROBE = 2048;
+constexpr int MAX_FANOUT = 4095;  // windows per record encodable in a claim reference
+constexpr int64_t EMPTY_WS = INT64_MIN;
+constexpr int NPART = 8;
+
+enum { P_ACCEPTED, P_NULL_KEY, P_NULL_ROW, P_BAD_TS, P_APPLIED, P_LATE, P_FAILED, P_NEW };
+
+enum OpKind : int8_t { OP_INC = 0, OP_INC_VALID, OP_ADD_I64, OP_ADD_F64, OP_MIN, OP_MAX };
+
+struct UpdOp {
+  int8_t kind;
+  int8_t col;
+  int16_t word;
+};
+
+struct ApplyParams {
+  int32_t windowed;
+  int32_t slot_words;
+  int64_t size, adv, grace;
+  int32_t n_cols;
+  int32_t n_ops;
+  int32_t col_type[MAX_COLS];
+  UpdOp ops[MAX_OPS];
+};
+
+struct ColPtrs {
+  const void* data[MAX_COLS];
+  const uint8_t* valid[MAX_COLS];
+};
+
+// How one aggregate's result is decoded from the state words.
+struct AggOut {
+  int32_t kind;   // KHIP_AGG_*
+  int32_t type;   // input column type (INT64 for COUNT*)
+  int32_t w_val;  // value word
+  int32_t w_cnt;  // non-null count word (-1 if none)
+};
+
+struct HavingDev {
+  int32_t active;
+  int32_t op;
+  AggOut a;
+  int64_t i64;
+  double f64;
+};
+
+// ------------------------------------------------------------------ device utils
+
+__device__ __forceinline__ int64_t wave_incl_max(int64_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    int64_t t = __shfl_up(v, off, 64);
+    if (lane >= off) v = t > v ? t : v;
+  }
+  return v;
+}
+
+// Inclusive prefix max over the block (blockDim.x threads, multiple of 64).
+__device__ __forceinline__ int64_t block_incl_max(int64_t v, int64_t* lds, int64_t* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_incl_max(v);
+  if (lane == 63) lds[wave] = v;
+  __syncthreads();
+  int64_t pre = INT64_MIN, tot = INT64_MIN;
+  for (int w = 0; w < nw; w++) {
+    int64_t x = lds[w];
+    if (w < wave) pre = x > pre ? x : pre;
+    tot = x > tot ? x : tot;
+  }
+  __syncthreads();
+  *total = tot;
+  return v > pre ? v : pre;
+}
+
+__device__ __forceinline__ int64_t wave_sum(int64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint64_t hash_bytes_dev(const uint8_t* p, int64_t n) {
+  uint64_t h = 0x84222325cbf29ce4ULL ^ (uint64_t)n;
+  int64_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w = 0;
+    for (int b = 0; b < 8; b++) w |= (uint64_t)p[i + b] << (8 * b);
+    h = mix64(h ^ w) * 0x9E3779B97F4A7C15ULL;
+  }
+  uint64_t w = 0;
+  for (int b = 0; i + b < n; b++) w |= (uint64_t)p[i + b] << (8 * b);
+  return mix64(h ^ w ^ ((uint64_t)(n & 7) << 59));
+}
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, int64_t n) {
+  for (int64_t i = 0; i < n; i++)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+
+__device__ __forceinline__ int64_t load_col_raw(const ColPtrs& c, int32_t type, int col, int64_t i) {
+  if (type == KHIP_TYPE_INT32) return (int64_t)((const int32_t*)c.data[col])[i];
+  return ((const int64_t*)c.data[col])[i];  // INT64, or DOUBLE bits
+}
+
+__device__ __forceinline__ bool decode_result(const uint64_t* s, const AggOut& a, int64_t* iv, double* dv) {
+  // returns false for SQL NULL; sets *iv for integer results, *dv for DOUBLE results
+  switch (a.kind) {
+    case KHIP_AGG_COUNT_STAR:
+    case KHIP_AGG_COUNT:
+      *iv = (int64_t)s[a.w_val];
+      return true;
+    case KHIP_AGG_SUM:
+      if (a.type == KHIP_TYPE_DOUBLE) __builtin_memcpy(dv, &s[a.w_val], 8);
+      else if (a.type == KHIP_TYPE_INT32) *iv = (int64_t)(int32_t)s[a.w_val];
+      else *iv = (int64_t)s[a.w_val];
+      return true;
+    case KHIP_AGG_MIN:
+    case KHIP_AGG_MAX:
+      if ((int64_t)s[a.w_cnt] == 0) return false;
+      if (a.type == KHIP_TYPE_DOUBLE) *dv = f64_from_order_key((int64_t)s[a.w_val]);
+      else *iv = (int64_t)s[a.w_val];
+      return true;
+    case KHIP_AGG_AVG: {
+      const int64_t c = (int64_t)s[a.w_cnt];
+      if (c == 0) { *dv = 0.0; return true; }
+      if (a.type == KHIP_TYPE_DOUBLE) {
+        double sum;
+        __builtin_memcpy(&sum, &s[a.w_val], 8);
+        *dv = sum / (double)c;
+      } else if (a.type == KHIP_TYPE_INT32) {
+        *dv = (double)(int32_t)s[a.w_val] / (double)c;
+      } else {
+        *dv = (double)(int64_t)s[a.w_val] / (double)c;
+      }
+      return true;
+    }
+  }
+  return false;
+}
+
+__device__ __forceinline__ bool result_is_double(const AggOut& a) {
+  if (a.kind == KHIP_AGG_AVG) return true;
+  if (a.kind == KHIP_AGG_COUNT || a.kind == KHIP_AGG_COUNT_STAR) return false;
+  return a.type == KHIP_TYPE_DOUBLE;
+}
+
+__device__ __forceinline__ bool having_ok(const uint64_t* s, const HavingDev& h) {
+  if (!h.active) return true;
+  int64_t iv = 0;
+  double dv = 0.0;
+  if (!decode_result(s, h.a, &iv, &dv)) return false;
+  int c;
+  if (result_is_double(h.a)) {
+    if (dv != dv) return h.op == KHIP_OP_NE;
+    c = dv < h.f64 ? -1 : (dv > h.f64 ? 1 : 0);
+  } else {
+    c = iv < h.i64 ? -1 : (iv > h.i64 ? 1 : 0);
+  }
+  switch (h.op) {
+    case KHIP_OP_GT: return c > 0;
+    case KHIP_OP_GE: return c >= 0;
+    case KHIP_OP_LT: return c < 0;
+    case KHIP_OP_LE: return c <= 0;
+    case KHIP_OP_EQ: return c == 0;
+    case KHIP_OP_NE: return c != 0;
+  }
+  return false;
+}
+
+
+// kernels shared by both engines (defined in khip_agg.hip)
+__global__ void k_scan_blocks(const int64_t* __restrict__ blockmax, int64_t nb, int64_t* __restrict__ prefix,
+                              int64_t* __restrict__ stream_time);
+__global__ void k_scan_excl(int64_t* __restrict__ v, int64_t n, int64_t* __restrict__ total);
+
+struct InitWords {
+  int64_t w[32];
+};
+
+// Partitioned engine state (khip_agg_part.hip).
+struct PartState {
+  int64_t P = 0;          // partitions (power of two), partition = top bits of mix64(key)
+  int log2P = 0;
+  int64_t cmax = 0;       // region capacity (rows) per partition and buffer
+  int H = 0;              // LDS hash entries per workgroup
+  int H_eff = 0;          // max groups placed in LDS before the partition is retried
+  int nwords = 3;         // u64 words per group actually used (key, ws, rowtime, state)
+  int lds_bytes = 0;
+  DevBuf pbase, R, ctr, counts;
+  DevBuf buf[2];          // region storage: P x cmax rows x sw words, double buffered
+  DevBuf sel, cnt, newcnt, fail;  // per partition: buffer select, rows, rows being written, flags
+  DevBuf hist, tilemax, tileprefix, tpart, scan_tmp;
+  DevBuf skey, sts, smeta, scol[MAX_COLS];
+  DevBuf work;            // retry work items
+  int64_t scat_cap = 0;
+};
+
+}  // namespace khip
+
+using namespace khip;
+
+struct khip_agg {
+  khip_agg_desc desc{};
+  std::vector<int32_t> col_types;
+  std::vector<khip_agg_spec> aggs;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int64_t grace = 0;
+  int windowed = 0;
+  int max_fanout = 1;
+  ApplyParams ap{};
+  InitWords init{};
+  std::vector<AggOut> outs;
+  int sw = 4;
+  // table
+  DevBuf table;
+  int64_t cap = 0;
+  int64_t occ = 0;  // resident groups
+  // per-batch scratch
+  DevBuf blockmax, blockprefix, partials, resume, counters, stream_time;
+  DevBuf st_keys, st_ts, st_kv, st_rv, st_koff, st_kbytes;  // host staging copies
+  DevBuf st_cols[MAX_COLS], st_cval[MAX_COLS];
+  DevBuf kid, khash;  // UTF8
+  int64_t resume_n = 0;
+  // UTF8 dictionary
+  DevBuf dword, dkid, arena, dict_bsum, dict_fail;
+  int64_t dcap = 0, docc = 0, arena_used = 0;
+  int64_t host_stream_time = -1;
+  // profiling (KHIP_FLAG_PROFILE)
+  bool profile = false;
+  hipEvent_t ev[8] = {};  // 0-4 atomic engine phases, 5-7 partitioned engine
+  khip_kernel_times times{};
+  int engine = 0;  // 0 partitioned (LDS-owned groups), 1 global-atomic
+  khip::PartState part;
+};
+
+inline void ev_record(khip_agg* a, int i) {
+  if (a->profile) (void)hipEventRecord(a->ev[i], a->stream);
+}
+inline double ev_ms(khip_agg* a, int i, int j) {
+  float ms = 0.f;
+  if (a->profile) (void)hipEventElapsedTime(&ms, a->ev[i], a->ev[j]);
+  return (double)ms;
+}
+inline void ev_record_part(khip_agg* a, int i) { ev_record(a, 3 + i); }
+
+namespace khip {
+khip_status part_init(khip_agg* a, int64_t hint);
+void part_release(khip_agg* a);
+khip_status part_reset(khip_agg* a);
+khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
+                      const uint8_t* rv, const ColPtrs& cols, int64_t* tot);
+khip_status part_compact(khip_agg* a, const HavingDev& h, std::vector<uint64_t>* rows, int64_t* count);
+}  // namespace khip
+
+

@@ -1,0 +1,813 @@
+// khip_agg_part.hip — partitioned (LDS-owned) windowed aggregation engine, the default.
+//
+// Why: the global-atomic engine (k_apply) pays one random HBM line plus 2+ memory-side
+// 64-bit atomics per (record, window); scattered atomics run ~17x below the HBM rate
+// (MI355X_MICROARCH.md, Global float atomics).  Here every (key, window) group is owned
+// by exactly one workgroup, so all updates are LDS atomics and HBM only sees coalesced
+// streams:
+//
+//   k_part_hist      tile of 64K records (XCD-swizzled tile index): validity, stream-time
+//                    tile max, LDS histogram over P key partitions → hist[t][p] (u32)
+//   k_scan_blocks    exclusive prefix max of tile maxima (stream time before each tile)
+//   k_part_colsum / k_part_colbase / k_scan_excl / k_part_colprefix
+//                    column prefix sums → each (tile, partition) chunk's output offset
+//   k_part_scatter   in-tile stream time (block scan), late test, first applied window,
+//                    record → its partition's contiguous range (LDS cursors), SoA
+//   k_part_agg       one workgroup per partition: load the partition's resident groups
+//                    (compact rows) into an LDS hash table, apply its records (window
+//                    fan-out, LDS atomics), write the compacted rows to the other buffer
+//   k_part_commit    flip the partition's buffer, publish its row count
+// A partition whose groups overflow the LDS table (or its region) writes nothing and is
+// retried with 2x sub-passes (groups split by hash bits) / a grown region — exact, since
+// its previous rows are untouched in the other buffer.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "khip_agg_internal.hpp"
+
+namespace khip {
+
+constexpr int PT_THREADS = 1024;
+constexpr int PT_ITEMS = 64;
+constexpr int64_t PT_TILE = (int64_t)PT_THREADS * PT_ITEMS;  // 65536 records per tile
+constexpr int AG_THREADS = 1024;
+constexpr int CH_BITS = 16;  // records per LDS claim-reference chunk
+constexpr int64_t CH = 1LL << CH_BITS;
+constexpr uint32_t L_FRESH = 0x80000000u;
+constexpr uint32_t L_RES = 0xFFFFFFFFu;
+constexpr int MAX_P_LOG2 = 14;  // LDS histogram: 16384 x u32 = 64 KB
+constexpr int TC_MAX = 64;      // tile chunks for the column prefix
+
+enum { T_ACCEPTED, T_NULL_KEY, T_NULL_ROW, T_BAD_TS, T_APPLIED, T_LATE, T_NPART };
+
+struct ColTypes {
+  int32_t t[MAX_COLS];
+};
+
+struct PartAggParams {
+  int32_t windowed;
+  int32_t nwords;  // 3 + state words actually used
+  int32_t sw;      // row stride (u64 words) in regions
+  int32_t H;
+  int32_t H_eff;
+  int32_t has_meta;
+  int64_t size, adv;
+  int64_t cmax;
+  int32_t n_cols;
+  int32_t n_ops;
+  int32_t col_type[MAX_COLS];
+  UpdOp ops[MAX_OPS];
+  InitWords init;
+};
+
+__device__ __forceinline__ uint32_t part_of(int64_t key, int log2P) {
+  return log2P == 0 ? 0u : (uint32_t)(mix64((uint64_t)key ^ 0x6A09E667F3BCC908ULL) >> (64 - log2P));
+}
+
+__device__ __forceinline__ int64_t tile_of(int64_t b, int64_t nT) {
+  // blocks b, b+8, b+16 ... share an XCD (round-robin dispatch): give each XCD a contiguous
+  // run of tiles so consecutive tiles' writes to one partition combine in that XCD's L2
+  const int64_t per = nT / 8, rem = nT % 8, x = b % 8, k = b / 8;
+  return x * per + (x < rem ? x : rem) + k;
+}
+
+__global__ __launch_bounds__(PT_THREADS) void k_part_hist(const int64_t* __restrict__ keys,
+                                                          const int64_t* __restrict__ ts,
+                                                          const uint8_t* __restrict__ kv,
+                                                          const uint8_t* __restrict__ rv, int64_t n, int log2P,
+                                                          int64_t nT, uint32_t* __restrict__ hist,
+                                                          int64_t* __restrict__ tilemax, int64_t* __restrict__ tpart) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t* lh = (uint32_t*)smem;
+  __shared__ int64_t lmax[PT_THREADS / 64];
+  __shared__ unsigned long long lc[4];
+  const int P = 1 << log2P;
+  const int64_t t = tile_of(blockIdx.x, nT);
+  for (int p = threadIdx.x; p < P; p += PT_THREADS) lh[p] = 0;
+  if (threadIdx.x < 4) lc[threadIdx.x] = 0;
+  __syncthreads();
+  int64_t m = -1, c_acc = 0, c_nk = 0, c_nr = 0, c_bt = 0;
+  const int64_t base = t * PT_TILE;
+  for (int r = 0; r < PT_ITEMS; r++) {
+    const int64_t i = base + (int64_t)r * PT_THREADS + threadIdx.x;
+    if (i >= n) break;
+    if (!bit_get(kv, i)) { c_nk++; continue; }
+    if (!bit_get(rv, i)) { c_nr++; continue; }
+    const int64_t x = ts[i];
+    if (x < 0) { c_bt++; continue; }
+    c_acc++;
+    m = x > m ? x : m;
+    atomicAdd(&lh[part_of(keys[i], log2P)], 1u);
+  }
+  int64_t tot;
+  block_incl_max(m, lmax, &tot);
+  c_acc = wave_sum(c_acc); c_nk = wave_sum(c_nk); c_nr = wave_sum(c_nr); c_bt = wave_sum(c_bt);
+  if ((threadIdx.x & 63) == 0) {
+    if (c_acc) atomicAdd(&lc[0], (unsigned long long)c_acc);
+    if (c_nk) atomicAdd(&lc[1], (unsigned long long)c_nk);
+    if (c_nr) atomicAdd(&lc[2], (unsigned long long)c_nr);
+    if (c_bt) atomicAdd(&lc[3], (unsigned long long)c_bt);
+  }
+  __syncthreads();
+  uint32_t* hrow = hist + t * (int64_t)P;
+  for (int p = threadIdx.x; p < P; p += PT_THREADS) hrow[p] = lh[p];
+  if (threadIdx.x == 0) {
+    tilemax[t] = tot;
+    int64_t* tp = tpart + t * T_NPART;
+    tp[T_ACCEPTED] = (int64_t)lc[0];
+    tp[T_NULL_KEY] = (int64_t)lc[1];
+    tp[T_NULL_ROW] = (int64_t)lc[2];
+    tp[T_BAD_TS] = (int64_t)lc[3];
+  }
+}
+
+// csum[c][p] = sum over the tiles of chunk c of hist[t][p]
+__global__ __launch_bounds__(256) void k_part_colsum(const uint32_t* __restrict__ hist, int64_t nT, int P, int TC,
+                                                     int64_t* __restrict__ csum) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  const int c = blockIdx.y;
+  if (p >= P) return;
+  const int64_t t0 = nT * c / TC, t1 = nT * (c + 1) / TC;
+  int64_t s = 0;
+  for (int64_t t = t0; t < t1; t++) s += hist[t * P + p];
+  csum[(int64_t)c * P + p] = s;
+}
+
+// in place: csum[c][p] → exclusive prefix over c; R[p] = column total
+__global__ __launch_bounds__(256) void k_part_colbase(int64_t* __restrict__ csum, int P, int TC,
+                                                      int64_t* __restrict__ R) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  int64_t acc = 0;
+  for (int c = 0; c < TC; c++) {
+    const int64_t v = csum[(int64_t)c * P + p];
+    csum[(int64_t)c * P + p] = acc;
+    acc += v;
+  }
+  R[p] = acc;
+}
+
+// hist[t][p] → absolute output offset of (tile t, partition p)
+__global__ __launch_bounds__(256) void k_part_colprefix(uint32_t* __restrict__ hist, int64_t nT, int P, int TC,
+                                                        const int64_t* __restrict__ csum,
+                                                        const int64_t* __restrict__ pbase) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  const int c = blockIdx.y;
+  if (p >= P) return;
+  const int64_t t0 = nT * c / TC, t1 = nT * (c + 1) / TC;
+  int64_t acc = pbase[p] + csum[(int64_t)c * P + p];
+  for (int64_t t = t0; t < t1; t++) {
+    const uint32_t v = hist[t * P + p];
+    hist[t * P + p] = (uint32_t)acc;
+    acc += v;
+  }
+}
+
+__global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
+    const int64_t* __restrict__ keys, const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
+    const uint8_t* __restrict__ rv, ColPtrs cols, int n_cols, ColTypes ctypes, int64_t n, int log2P, int64_t nT,
+    const uint32_t* __restrict__ offs, const int64_t* __restrict__ tileprefix, int windowed, int64_t size,
+    int64_t adv, int64_t grace, int has_meta, int64_t* __restrict__ skey, int64_t* __restrict__ sts,
+    uint32_t* __restrict__ smeta, ColPtrs scols, int64_t* __restrict__ tpart) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t* cur = (uint32_t*)smem;
+  __shared__ int64_t lmax[PT_THREADS / 64];
+  __shared__ unsigned long long lc[2];
+  const int P = 1 << log2P;
+  const int64_t t = tile_of(blockIdx.x, nT);
+  for (int p = threadIdx.x; p < P; p += PT_THREADS) cur[p] = offs[t * P + p];
+  if (threadIdx.x < 2) lc[threadIdx.x] = 0;
+  __syncthreads();
+  int64_t carry = tileprefix[t];
+  int64_t c_app = 0, c_late = 0;
+  const int64_t base = t * PT_TILE;
+  for (int r = 0; r < PT_ITEMS; r++) {
+    if (base + (int64_t)r * PT_THREADS >= n) break;  // uniform across the block
+    const int64_t i = base + (int64_t)r * PT_THREADS + threadIdx.x;
+    const bool in = i < n;
+    const int64_t x = in ? ts[i] : -1;
+    const bool valid = in && bit_get(kv, i) && bit_get(rv, i) && x >= 0;
+    int64_t tot;
+    const int64_t incl = block_incl_max(valid ? x : -1, lmax, &tot);
+    const int64_t st = incl > carry ? incl : carry;
+    carry = tot > carry ? tot : carry;
+    if (!valid) continue;
+    int64_t jlo = 0, nwin = 1;
+    if (windowed) {
+      const int64_t ws0 = first_window_start(x, size, adv);
+      nwin = (x - ws0) / adv + 1;
+      // applied iff ws + size > st - grace  ⇔  ws >= st - grace - size + 1
+      const int64_t wmin = st - grace - size + 1;
+      if (wmin > ws0) jlo = (wmin - ws0 + adv - 1) / adv;
+      if (jlo > nwin) jlo = nwin;
+    }
+    c_late += jlo;
+    c_app += nwin - jlo;
+    const int64_t key = keys[i];
+    const uint32_t pos = atomicAdd(&cur[part_of(key, log2P)], 1u);
+    skey[pos] = key;
+    sts[pos] = nwin > jlo ? x : -1;
+    if (has_meta) {
+      uint32_t vm = 0;
+      for (int c = 0; c < n_cols; c++) vm |= (bit_get(cols.valid[c], i) ? 1u : 0u) << c;
+      smeta[pos] = (uint32_t)jlo | (vm << 16);
+    }
+    for (int c = 0; c < n_cols; c++)  // raw 8-byte value (INT32 sign-extended, DOUBLE bits)
+      ((int64_t*)scols.data[c])[pos] = load_col_raw(cols, ctypes.t[c], c, i);
+  }
+  c_app = wave_sum(c_app);
+  c_late = wave_sum(c_late);
+  if ((threadIdx.x & 63) == 0) {
+    if (c_app) atomicAdd(&lc[0], (unsigned long long)c_app);
+    if (c_late) atomicAdd(&lc[1], (unsigned long long)c_late);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    tpart[t * T_NPART + T_APPLIED] = (int64_t)lc[0];
+    tpart[t * T_NPART + T_LATE] = (int64_t)lc[1];
+  }
+}
+
+
+// ------------------------------------------------------------------ k_part_agg
+// Work item: blockIdx.x = partition (work == nullptr), or work[blockIdx.x] =
+// p | sub_bits << 16 | sub << 20  (retry with 2^sub_bits sub-passes, sub_bits <= 12).
+// LDS: lref u32[H] | words i64[nwords][H]  (word 0 key, 1 ws, 2 rowtime, 3.. state)
+
+__device__ __forceinline__ bool part_sub_ok(uint64_t h, int sbits, int sub) {
+  return sbits == 0 || (int)((h >> 40) & ((1u << sbits) - 1)) == sub;
+}
+
+__device__ __forceinline__ void lds_apply(const PartAggParams& q, int64_t* lw, int H, int e, int64_t t,
+                                          uint32_t vmask, const ColPtrs& scols, int64_t gi) {
+  atomicMax((long long*)&lw[2 * H + e], (long long)t);
+  for (int o = 0; o < q.n_ops; o++) {
+    const UpdOp op = q.ops[o];
+    int64_t* w = &lw[op.word * H + e];
+    if (op.kind == OP_INC) {
+      atomicAdd((unsigned long long*)w, 1ULL);
+      continue;
+    }
+    if (!((vmask >> op.col) & 1u)) continue;
+    const int64_t raw = ((const int64_t*)scols.data[op.col])[gi];
+    switch (op.kind) {
+      case OP_INC_VALID: atomicAdd((unsigned long long*)w, 1ULL); break;
+      case OP_ADD_I64: atomicAdd((unsigned long long*)w, (unsigned long long)raw); break;
+      case OP_ADD_F64: {
+        double d;
+        __builtin_memcpy(&d, &raw, 8);
+        atomicAdd((double*)w, d);
+        break;
+      }
+      case OP_MIN:
+      case OP_MAX: {
+        int64_t k = raw;
+        if (q.col_type[op.col] == KHIP_TYPE_DOUBLE) {
+          double d;
+          __builtin_memcpy(&d, &raw, 8);
+          k = f64_order_key(d);
+        }
+        if (op.kind == OP_MIN) atomicMin((long long*)w, (long long)k);
+        else atomicMax((long long*)w, (long long)k);
+        break;
+      }
+      default: break;
+    }
+  }
+}
+
+__global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const uint32_t* __restrict__ work,
+                                                         const int64_t* __restrict__ pbase,
+                                                         const int64_t* __restrict__ skey,
+                                                         const int64_t* __restrict__ sts,
+                                                         const uint32_t* __restrict__ smeta, ColPtrs scols,
+                                                         uint64_t* __restrict__ buf0, uint64_t* __restrict__ buf1,
+                                                         const uint8_t* __restrict__ sel,
+                                                         const int64_t* __restrict__ cnt,
+                                                         unsigned long long* __restrict__ newcnt,
+                                                         uint8_t* __restrict__ fail) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = q.H;
+  uint32_t* lref = (uint32_t*)smem;
+  int64_t* lw = (int64_t*)(smem + (((size_t)H * 4 + 15) & ~(size_t)15));
+  __shared__ int lused, lovf;
+  __shared__ int lcnt[AG_THREADS / 64];
+  __shared__ unsigned long long lbase;
+  uint32_t p;
+  int sbits = 0, sub = 0;
+  if (work) {
+    const uint32_t w = work[blockIdx.x];
+    p = w & 0xFFFFu;
+    sbits = (w >> 16) & 0xF;
+    sub = (int)(w >> 20);
+  } else {
+    p = blockIdx.x;
+  }
+  const int64_t rbase = pbase[p], rn = pbase[p + 1] - rbase;
+  if (rn == 0 && !work) return;  // untouched partition: nothing to rewrite
+  for (int e = threadIdx.x; e < H; e += AG_THREADS) {
+    lref[e] = 0;
+    for (int w = 0; w < q.nwords; w++) lw[w * H + e] = q.init.w[w];
+  }
+  if (threadIdx.x == 0) {
+    lused = 0;
+    lovf = 0;
+  }
+  __syncthreads();
+  // 1. resident rows of this partition (distinct groups: insert without comparing)
+  const uint64_t* src = (sel[p] ? buf1 : buf0) + (uint64_t)p * q.cmax * q.sw;
+  const int64_t nrow = cnt[p];
+  for (int64_t r = threadIdx.x; r < nrow; r += AG_THREADS) {
+    const uint64_t* row = src + r * q.sw;
+    const int64_t key = (int64_t)row[0], ws = (int64_t)row[1];
+    const uint64_t h = group_hash(key, ws);
+    if (!part_sub_ok(h, sbits, sub)) continue;
+    if (atomicAdd(&lused, 1) >= q.H_eff) {
+      lovf = 1;
+      break;
+    }
+    int e = (int)(h & (uint64_t)(H - 1));
+    while (atomicCAS(&lref[e], 0u, L_RES) != 0u) e = (e + 1) & (H - 1);
+    for (int w = 0; w < q.nwords; w++) lw[w * H + e] = (int64_t)row[w];
+  }
+  __syncthreads();
+  // 2. this batch's records, in chunks of CH (claim references are chunk-relative)
+  for (int64_t c0 = 0; c0 < rn; c0 += CH) {
+    const int64_t c1 = c0 + CH < rn ? c0 + CH : rn;
+    for (int64_t li = c0 + threadIdx.x; li < c1; li += AG_THREADS) {
+      if (*(volatile int*)&lovf) break;
+      const int64_t gi = rbase + li;
+      const int64_t t = sts[gi];
+      if (t < 0) continue;  // every window late
+      const int64_t key = skey[gi];
+      const uint32_t meta = q.has_meta ? smeta[gi] : 0u;
+      const int64_t jlo = meta & 0xFFFFu;
+      const uint32_t vmask = meta >> 16;
+      const int64_t ws_first = q.windowed ? first_window_start(t, q.size, q.adv) : 0;
+      int64_t j = jlo;
+      for (int64_t ws = ws_first + jlo * q.adv; ws <= (q.windowed ? t : 0); ws += (q.windowed ? q.adv : 1), j++) {
+        const uint64_t h = group_hash(key, ws);
+        if (!part_sub_ok(h, sbits, sub)) continue;
+        const uint32_t ref = L_FRESH | ((uint32_t)j << CH_BITS) | (uint32_t)(li - c0);
+        int e = (int)(h & (uint64_t)(H - 1));
+        bool done = false;
+        for (int probe = 0; probe < H; probe++) {
+          uint32_t v = *(volatile uint32_t*)&lref[e];
+          bool hit = false;
+          if (v == L_RES) {
+            hit = lw[e] == key && lw[H + e] == ws;
+          } else {
+            if (v == 0u) {
+              const uint32_t old = atomicCAS(&lref[e], 0u, ref);
+              if (old == 0u) {
+                if (atomicAdd(&lused, 1) >= q.H_eff) lovf = 1;
+                lw[e] = key;
+                lw[H + e] = ws;
+                hit = true;
+              } else {
+                v = old;
+              }
+            }
+            if (!hit && v != L_RES && (v & L_FRESH)) {
+              const int64_t g2 = rbase + c0 + (int64_t)(v & (uint32_t)(CH - 1));
+              const int64_t j2 = (v >> CH_BITS) & 0x7FFFu;
+              if (skey[g2] == key) {
+                const int64_t ws2 = q.windowed ? first_window_start(sts[g2], q.size, q.adv) + j2 * q.adv : 0;
+                hit = ws2 == ws;
+              }
+            } else if (!hit && v == L_RES) {
+              hit = lw[e] == key && lw[H + e] == ws;
+            }
+          }
+          if (hit) {
+            lds_apply(q, lw, H, e, t, vmask, scols, gi);
+            done = true;
+            break;
+          }
+          e = (e + 1) & (H - 1);
+        }
+        if (!done) lovf = 1;
+        if (!q.windowed) break;
+      }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < H; e += AG_THREADS)
+      if (lref[e] != 0u && lref[e] != L_RES) lref[e] = L_RES;
+    __syncthreads();
+  }
+  if (lovf) {
+    if (threadIdx.x == 0) fail[p] |= 1;
+    return;
+  }
+  // 3. compacted rows → the other buffer (contiguous entry range per thread keeps order)
+  const int per = (H + AG_THREADS - 1) / AG_THREADS;
+  const int e0 = threadIdx.x * per, e1 = e0 + per < H ? e0 + per : H;
+  int mine = 0;
+  for (int e = e0; e < e1; e++) mine += lref[e] != 0u;
+  // block exclusive scan of `mine`
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int incl = mine;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) lcnt[wave] = incl;
+  __syncthreads();
+  int before = 0, total = 0;
+  for (int w = 0; w < AG_THREADS / 64; w++) {
+    if (w < wave) before += lcnt[w];
+    total += lcnt[w];
+  }
+  if (threadIdx.x == 0) lbase = total ? atomicAdd(&newcnt[p], (unsigned long long)total) : 0ULL;
+  __syncthreads();
+  if ((int64_t)(lbase + total) > q.cmax) {
+    if (threadIdx.x == 0) fail[p] |= 2;
+    return;
+  }
+  uint64_t* dst =
+      (sel[p] ? buf0 : buf1) + (uint64_t)p * q.cmax * q.sw + (lbase + (uint64_t)(before + incl - mine)) * q.sw;
+  for (int e = e0; e < e1; e++) {
+    if (lref[e] == 0u) continue;
+    for (int w = 0; w < q.sw; w++) dst[w] = w < q.nwords ? (uint64_t)lw[w * H + e] : 0ULL;
+    dst += q.sw;
+  }
+}
+
+// Publish the partitions processed in this pass (all touched ones, or the retry list).
+__global__ __launch_bounds__(256) void k_part_commit(int P, const int64_t* __restrict__ pbase,
+                                                     const uint32_t* __restrict__ plist, int nlist,
+                                                     uint8_t* __restrict__ sel, int64_t* __restrict__ cnt,
+                                                     unsigned long long* __restrict__ newcnt,
+                                                     const uint8_t* __restrict__ fail,
+                                                     unsigned long long* __restrict__ out /* [new groups, failed] */) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  int64_t added = 0, failed = 0;
+  if (plist ? k < nlist : k < P) {
+    const uint32_t p = plist ? plist[k] : (uint32_t)k;
+    if (plist || pbase[p + 1] > pbase[p]) {
+      if (fail[p] == 0) {
+        added = (int64_t)newcnt[p] - cnt[p];
+        cnt[p] = (int64_t)newcnt[p];
+        sel[p] ^= 1;
+      } else {
+        failed = 1;
+      }
+      newcnt[p] = 0;
+    }
+  }
+  added = wave_sum(added);
+  failed = wave_sum(failed);
+  if ((threadIdx.x & 63) == 0) {
+    if (added) atomicAdd(&out[0], (unsigned long long)added);
+    if (failed) atomicAdd(&out[1], (unsigned long long)failed);
+  }
+}
+
+// Copy every partition's rows into new region buffers with a larger capacity.
+__global__ __launch_bounds__(256) void k_part_regrow(const uint64_t* __restrict__ b0, const uint64_t* __restrict__ b1,
+                                                     const uint8_t* __restrict__ sel, const int64_t* __restrict__ cnt,
+                                                     int64_t ocmax, uint64_t* __restrict__ nb0, int64_t ncmax, int sw) {
+  const int64_t p = blockIdx.x;
+  const uint64_t* src = (sel[p] ? b1 : b0) + (uint64_t)p * ocmax * sw;
+  uint64_t* dst = nb0 + (uint64_t)p * ncmax * sw;
+  const int64_t words = cnt[p] * sw;
+  for (int64_t w = threadIdx.x; w < words; w += 256) dst[w] = src[w];
+}
+
+// Double the partition count: rows of partition p move to 2p / 2p+1 (next hash bit).
+__global__ __launch_bounds__(256) void k_part_split(const uint64_t* __restrict__ b0, const uint64_t* __restrict__ b1,
+                                                    const uint8_t* __restrict__ sel, const int64_t* __restrict__ cnt,
+                                                    int64_t cmax, int sw, int new_log2P, uint64_t* __restrict__ nb,
+                                                    int64_t* __restrict__ ncnt) {
+  __shared__ unsigned int lc[2];
+  const int64_t p = blockIdx.x;
+  if (threadIdx.x < 2) lc[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t* src = (sel[p] ? b1 : b0) + (uint64_t)p * cmax * sw;
+  for (int64_t r = threadIdx.x; r < cnt[p]; r += 256) {
+    const uint64_t* row = src + r * sw;
+    const uint32_t child = part_of((int64_t)row[0], new_log2P);  // == 2p or 2p+1
+    const unsigned k = atomicAdd(&lc[child & 1], 1u);
+    uint64_t* dst = nb + ((uint64_t)child * cmax + k) * sw;
+    for (int w = 0; w < sw; w++) dst[w] = row[w];
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) ncnt[2 * p + threadIdx.x] = lc[threadIdx.x];
+}
+
+// Per partition: rows passing HAVING (count) — or write them at offs[p].
+__global__ __launch_bounds__(256) void k_part_rows(const uint64_t* __restrict__ b0, const uint64_t* __restrict__ b1,
+                                                   const uint8_t* __restrict__ sel, const int64_t* __restrict__ cnt,
+                                                   int64_t cmax, int sw, HavingDev h, int64_t* __restrict__ counts,
+                                                   const int64_t* __restrict__ offs, uint64_t* __restrict__ out) {
+  __shared__ int lcnt[4];
+  __shared__ int64_t lbase;
+  const int64_t p = blockIdx.x;
+  const uint64_t* src = (sel[p] ? b1 : b0) + (uint64_t)p * cmax * sw;
+  const int64_t n = cnt[p];
+  if (threadIdx.x == 0) lbase = out ? offs[p] : 0;
+  int64_t total = 0;
+  for (int64_t r0 = 0; r0 < n; r0 += 256) {
+    const int64_t r = r0 + threadIdx.x;
+    const bool take = r < n && having_ok(src + r * sw, h);
+    const uint64_t bal = __ballot(take);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) lcnt[wave] = __popcll(bal);
+    __syncthreads();
+    int before = __popcll(bal & ((1ULL << lane) - 1)), tot = 0;
+    for (int w = 0; w < 4; w++) {
+      if (w < wave) before += lcnt[w];
+      tot += lcnt[w];
+    }
+    if (take && out) {
+      uint64_t* o = out + (lbase + total + before) * (uint64_t)sw;
+      for (int w = 0; w < sw; w++) o[w] = src[r * sw + w];
+    }
+    total += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && counts) counts[p] = total;
+}
+
+// ------------------------------------------------------------------ host side
+
+static int part_ceil_log2(int64_t v) {
+  int l = 0;
+  while ((1LL << l) < v) l++;
+  return l;
+}
+
+khip_status part_init(khip_agg* a, int64_t hint) {
+  PartState& s = a->part;
+  const int nwords = 3 + (int)(a->ap.n_ops > 0 ? 0 : 0);
+  (void)nwords;
+  // words used = highest word index + 1 (rows are padded to a->sw)
+  int used = 3;
+  for (int o = 0; o < a->ap.n_ops; o++) used = std::max(used, a->ap.ops[o].word + 1);
+  s.nwords = used;
+  const int entry = 4 + 8 * used;
+  // LDS table: the largest power of two within ~150 KB
+  int H = 512;
+  while ((int64_t)(H * 2) * entry + 16 <= 150 * 1024 && H < 8192) H *= 2;
+  s.H = H;
+  s.H_eff = H * 3 / 4;
+  s.lds_bytes = (int)((((size_t)H * 4 + 15) & ~(size_t)15) + (size_t)H * 8 * used);
+  // partitions: ~H/4 groups each at the hinted size (room for 3x growth before retries)
+  const int64_t groups = std::max<int64_t>(hint, 1024);
+  s.log2P = std::min(MAX_P_LOG2, std::max(0, part_ceil_log2(groups * 4 / H)));
+  s.P = 1LL << s.log2P;
+  s.cmax = next_pow2(std::max<int64_t>(64, 2 * groups / s.P + 64));
+  KHIP_TRY(s.sel.ensure(s.P));
+  KHIP_TRY(s.fail.ensure(s.P));
+  KHIP_TRY(s.cnt.ensure(s.P * 8));
+  KHIP_TRY(s.newcnt.ensure(s.P * 8));
+  KHIP_TRY(s.pbase.ensure((s.P + 1) * 8));
+  KHIP_TRY(s.R.ensure((s.P + 1) * 8));
+  KHIP_TRY(s.ctr.ensure(64));
+  for (int b = 0; b < 2; b++) KHIP_TRY(s.buf[b].ensure((size_t)s.P * s.cmax * a->sw * 8));
+  KHIP_TRY_HIP(hipMemsetAsync(s.sel.p, 0, s.P, a->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(s.fail.p, 0, s.P, a->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(s.cnt.p, 0, s.P * 8, a->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(s.newcnt.p, 0, s.P * 8, a->stream));
+  return KHIP_OK;
+}
+
+void part_release(khip_agg* a) {
+  PartState& s = a->part;
+  DevBuf* bufs[] = {&s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist, &s.tilemax,
+                    &s.tileprefix, &s.tpart, &s.scan_tmp, &s.skey, &s.sts, &s.smeta, &s.work,
+                    &s.pbase, &s.R, &s.ctr, &s.counts};
+  for (DevBuf* b : bufs) b->release();
+  for (int c = 0; c < MAX_COLS; c++) s.scol[c].release();
+}
+
+khip_status part_reset(khip_agg* a) {
+  PartState& s = a->part;
+  KHIP_TRY_HIP(hipMemsetAsync(s.cnt.p, 0, s.P * 8, a->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(s.newcnt.p, 0, s.P * 8, a->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(s.fail.p, 0, s.P, a->stream));
+  return KHIP_OK;
+}
+
+static PartAggParams part_params(khip_agg* a) {
+  PartState& s = a->part;
+  PartAggParams q{};
+  q.windowed = a->windowed;
+  q.nwords = s.nwords;
+  q.sw = a->sw;
+  q.H = s.H;
+  q.H_eff = s.H_eff;
+  q.has_meta = (a->desc.window_kind == KHIP_WINDOW_HOPPING || a->desc.n_cols > 0) ? 1 : 0;
+  q.size = a->desc.size_ms;
+  q.adv = a->windowed ? a->desc.advance_ms : 1;
+  q.cmax = s.cmax;
+  q.n_cols = a->desc.n_cols;
+  q.n_ops = a->ap.n_ops;
+  for (int c = 0; c < MAX_COLS; c++) q.col_type[c] = a->ap.col_type[c];
+  for (int o = 0; o < a->ap.n_ops; o++) q.ops[o] = a->ap.ops[o];
+  q.init = a->init;
+  return q;
+}
+
+static khip_status part_regrow(khip_agg* a, int64_t ncmax) {
+  PartState& s = a->part;
+  DevBuf nb[2];
+  for (int b = 0; b < 2; b++) KHIP_TRY(nb[b].ensure((size_t)s.P * ncmax * a->sw * 8));
+  hipLaunchKernelGGL(k_part_regrow, dim3(s.P), dim3(256), 0, a->stream, s.buf[0].as<uint64_t>(),
+                     s.buf[1].as<uint64_t>(), s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.cmax, nb[0].as<uint64_t>(),
+                     ncmax, a->sw);
+  KHIP_TRY_HIP(hipGetLastError());
+  KHIP_TRY_HIP(hipMemsetAsync(s.sel.p, 0, s.P, a->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  for (int b = 0; b < 2; b++) {
+    s.buf[b].release();
+    s.buf[b] = nb[b];
+    nb[b].p = nullptr;
+  }
+  s.cmax = ncmax;
+  return KHIP_OK;
+}
+
+static khip_status part_split(khip_agg* a) {
+  PartState& s = a->part;
+  const int64_t P2 = s.P * 2;
+  DevBuf nb[2], ncnt, nsel, nnew, nfail;
+  for (int b = 0; b < 2; b++) KHIP_TRY(nb[b].ensure((size_t)P2 * s.cmax * a->sw * 8));
+  KHIP_TRY(ncnt.ensure(P2 * 8));
+  KHIP_TRY(nsel.ensure(P2));
+  KHIP_TRY(nnew.ensure(P2 * 8));
+  KHIP_TRY(nfail.ensure(P2));
+  hipLaunchKernelGGL(k_part_split, dim3(s.P), dim3(256), 0, a->stream, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
+                     s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.cmax, a->sw, s.log2P + 1, nb[0].as<uint64_t>(),
+                     ncnt.as<int64_t>());
+  KHIP_TRY_HIP(hipGetLastError());
+  KHIP_TRY_HIP(hipMemsetAsync(nsel.p, 0, P2, a->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(nnew.p, 0, P2 * 8, a->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(nfail.p, 0, P2, a->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  DevBuf* olds[] = {&s.buf[0], &s.buf[1], &s.cnt, &s.sel, &s.newcnt, &s.fail};
+  DevBuf* news[] = {&nb[0], &nb[1], &ncnt, &nsel, &nnew, &nfail};
+  for (int k = 0; k < 6; k++) {
+    olds[k]->release();
+    *olds[k] = *news[k];
+    news[k]->p = nullptr;
+  }
+  s.P = P2;
+  s.log2P += 1;
+  KHIP_TRY(s.pbase.ensure((s.P + 1) * 8));
+  KHIP_TRY(s.R.ensure((s.P + 1) * 8));
+  return KHIP_OK;
+}
+
+// One push slice (n < 2^31).  tot[] receives the P_* counters.
+khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
+                      const uint8_t* rv, const ColPtrs& cols, int64_t* tot) {
+  PartState& s = a->part;
+  // keep the resident groups per partition well inside the LDS table (split = exact re-layout)
+  while (s.log2P < MAX_P_LOG2 && a->occ > s.P * (int64_t)s.H_eff / 2) KHIP_TRY(part_split(a));
+  const int P = (int)s.P;
+  const int64_t nT = ceil_div(n, PT_TILE);
+  const int TC = (int)std::min<int64_t>(nT, TC_MAX);
+  KHIP_TRY(s.hist.ensure((size_t)nT * P * 4));
+  KHIP_TRY(s.tilemax.ensure(nT * 8));
+  KHIP_TRY(s.tileprefix.ensure(nT * 8));
+  KHIP_TRY(s.tpart.ensure(nT * 8 * T_NPART));
+  KHIP_TRY(s.scan_tmp.ensure((size_t)TC * P * 8));
+  if (s.scat_cap < n) {
+    KHIP_TRY(s.skey.ensure(n * 8));
+    KHIP_TRY(s.sts.ensure(n * 8));
+    if (a->desc.window_kind == KHIP_WINDOW_HOPPING || a->desc.n_cols > 0) KHIP_TRY(s.smeta.ensure(n * 4));
+    for (int c = 0; c < a->desc.n_cols; c++) KHIP_TRY(s.scol[c].ensure(n * 8));
+    s.scat_cap = n;
+  }
+  ColTypes ct{};
+  for (int c = 0; c < MAX_COLS; c++) ct.t[c] = a->ap.col_type[c];
+  ColPtrs sc{};
+  for (int c = 0; c < a->desc.n_cols; c++) sc.data[c] = s.scol[c].p;
+  const size_t hist_lds = (size_t)P * 4;
+  // 1. histogram + tile stream-time maxima
+  ev_record_part(a, 0);
+  hipLaunchKernelGGL(k_part_hist, dim3(nT), dim3(PT_THREADS), hist_lds, a->stream, keys, ts, kv, rv, n, s.log2P, nT,
+                     s.hist.as<uint32_t>(), s.tilemax.as<int64_t>(), s.tpart.as<int64_t>());
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, a->stream, s.tilemax.as<int64_t>(), nT,
+                     s.tileprefix.as<int64_t>(), a->stream_time.as<int64_t>());
+  // 2. offsets
+  hipLaunchKernelGGL(k_part_colsum, dim3(ceil_div(P, 256), TC), dim3(256), 0, a->stream, s.hist.as<uint32_t>(), nT, P,
+                     TC, s.scan_tmp.as<int64_t>());
+  hipLaunchKernelGGL(k_part_colbase, dim3(ceil_div(P, 256)), dim3(256), 0, a->stream, s.scan_tmp.as<int64_t>(), P, TC,
+                     s.R.as<int64_t>());
+  KHIP_TRY_HIP(hipMemcpyAsync(s.pbase.p, s.R.p, P * 8, hipMemcpyDeviceToDevice, a->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(s.pbase.as<int64_t>() + P, 0, 8, a->stream));
+  hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, a->stream, s.pbase.as<int64_t>(), (int64_t)P,
+                     s.pbase.as<int64_t>() + P);
+  hipLaunchKernelGGL(k_part_colprefix, dim3(ceil_div(P, 256), TC), dim3(256), 0, a->stream, s.hist.as<uint32_t>(), nT,
+                     P, TC, s.scan_tmp.as<int64_t>(), s.pbase.as<int64_t>());
+  ev_record_part(a, 1);
+  // 3. scatter
+  const int has_meta = (a->desc.window_kind == KHIP_WINDOW_HOPPING || a->desc.n_cols > 0) ? 1 : 0;
+  hipLaunchKernelGGL(k_part_scatter, dim3(nT), dim3(PT_THREADS), hist_lds, a->stream, keys, ts, kv, rv, cols,
+                     a->desc.n_cols, ct, n, s.log2P, nT, s.hist.as<uint32_t>(), s.tileprefix.as<int64_t>(), a->windowed,
+                     a->desc.size_ms, a->windowed ? a->desc.advance_ms : 1, a->grace, has_meta, s.skey.as<int64_t>(),
+                     s.sts.as<int64_t>(), has_meta ? s.smeta.as<uint32_t>() : nullptr, sc, s.tpart.as<int64_t>());
+  KHIP_TRY_HIP(hipGetLastError());
+  ev_record_part(a, 2);
+  // 4. aggregate partitions (+ retries)
+  const PartAggParams q0 = part_params(a);
+  int64_t added_total = 0;
+  std::vector<uint8_t> host_fail;
+  std::vector<int> sbits(P, 0);
+  std::vector<uint32_t> plist, work;
+  for (int pass = 0;; pass++) {
+    PartAggParams q = q0;
+    q.cmax = s.cmax;
+    KHIP_TRY_HIP(hipMemsetAsync(s.ctr.p, 0, 16, a->stream));
+    const uint32_t* wk = pass == 0 ? nullptr : s.work.as<uint32_t>();
+    const int64_t nwork = pass == 0 ? P : (int64_t)work.size();
+    hipFuncSetAttribute((const void*)k_part_agg, hipFuncAttributeMaxDynamicSharedMemorySize, s.lds_bytes);
+    hipLaunchKernelGGL(k_part_agg, dim3(nwork), dim3(AG_THREADS), s.lds_bytes, a->stream, q, wk,
+                       s.pbase.as<int64_t>(), s.skey.as<int64_t>(), s.sts.as<int64_t>(),
+                       has_meta ? s.smeta.as<uint32_t>() : nullptr, sc, s.buf[0].as<uint64_t>(),
+                       s.buf[1].as<uint64_t>(), s.sel.as<uint8_t>(), s.cnt.as<int64_t>(),
+                       s.newcnt.as<unsigned long long>(), s.fail.as<uint8_t>());
+    const int nl = pass == 0 ? P : (int)plist.size();
+    hipLaunchKernelGGL(k_part_commit, dim3(ceil_div(std::max(nl, 1), 256)), dim3(256), 0, a->stream, P,
+                       s.pbase.as<int64_t>(), pass == 0 ? nullptr : s.work.as<uint32_t>() + work.size(), nl,
+                       s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
+                       s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>());
+    KHIP_TRY_HIP(hipGetLastError());
+    if (pass == 0) ev_record_part(a, 3);
+    unsigned long long c2[2];
+    KHIP_TRY_HIP(hipMemcpyAsync(c2, s.ctr.p, 16, hipMemcpyDeviceToHost, a->stream));
+    KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+    added_total += (int64_t)c2[0];
+    if (c2[1] == 0) break;
+    if (pass > 24) return fail(KHIP_E_DEVICE, "partitioned aggregation could not place the batch");
+    // retry the failed partitions: LDS overflow → twice the sub-passes; region overflow → grow
+    host_fail.resize(P);
+    KHIP_TRY_HIP(hipMemcpy(host_fail.data(), s.fail.p, P, hipMemcpyDeviceToHost));
+    KHIP_TRY_HIP(hipMemsetAsync(s.fail.p, 0, P, a->stream));
+    bool grow = false;
+    plist.clear();
+    work.clear();
+    for (int p = 0; p < P; p++) {
+      if (!host_fail[p]) continue;
+      if (host_fail[p] & 1) sbits[p] = sbits[p] + 1;
+      if (host_fail[p] & 2) grow = true;
+      plist.push_back((uint32_t)p);
+      if (sbits[p] > 12) return fail(KHIP_E_DEVICE, "partition needs more than 4096 sub-passes (extreme key skew)");
+      for (int k = 0; k < (1 << sbits[p]); k++) work.push_back((uint32_t)p | ((uint32_t)sbits[p] << 16) | ((uint32_t)k << 20));
+    }
+    if (grow) KHIP_TRY(part_regrow(a, s.cmax * 2));
+    std::vector<uint32_t> both(work);
+    both.insert(both.end(), plist.begin(), plist.end());
+    KHIP_TRY(s.work.ensure(both.size() * 4));
+    KHIP_TRY_HIP(hipMemcpyAsync(s.work.p, both.data(), both.size() * 4, hipMemcpyHostToDevice, a->stream));
+  }
+  // 5. counters
+  std::vector<int64_t> tp((size_t)nT * T_NPART);
+  KHIP_TRY_HIP(hipMemcpy(tp.data(), s.tpart.p, tp.size() * 8, hipMemcpyDeviceToHost));
+  int64_t c[T_NPART] = {0};
+  for (int64_t t = 0; t < nT; t++)
+    for (int k = 0; k < T_NPART; k++) c[k] += tp[t * T_NPART + k];
+  tot[P_ACCEPTED] += c[T_ACCEPTED];
+  tot[P_NULL_KEY] += c[T_NULL_KEY];
+  tot[P_NULL_ROW] += c[T_NULL_ROW];
+  tot[P_BAD_TS] += c[T_BAD_TS];
+  tot[P_APPLIED] += c[T_APPLIED];
+  tot[P_LATE] += c[T_LATE];
+  tot[P_NEW] += added_total;
+  return KHIP_OK;
+}
+
+// Rows passing `h` (all partitions) → rows (sw words each), or just the count.
+khip_status part_compact(khip_agg* a, const HavingDev& h, std::vector<uint64_t>* rows, int64_t* count) {
+  PartState& s = a->part;
+  const int P = (int)s.P;
+  KHIP_TRY(s.counts.ensure((P + 1) * 8));
+  hipLaunchKernelGGL(k_part_rows, dim3(P), dim3(256), 0, a->stream, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
+                     s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.cmax, a->sw, h, s.counts.as<int64_t>(), nullptr,
+                     nullptr);
+  KHIP_TRY_HIP(hipMemsetAsync(s.counts.as<int64_t>() + P, 0, 8, a->stream));
+  hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, a->stream, s.counts.as<int64_t>(), (int64_t)P,
+                     s.counts.as<int64_t>() + P);
+  KHIP_TRY_HIP(hipGetLastError());
+  int64_t n = 0;
+  KHIP_TRY_HIP(hipMemcpyAsync(&n, s.counts.as<int64_t>() + P, 8, hipMemcpyDeviceToHost, a->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  *count = n;
+  if (!rows) return KHIP_OK;
+  DevBuf out;
+  KHIP_TRY(out.ensure((size_t)std::max<int64_t>(n, 1) * a->sw * 8));
+  hipLaunchKernelGGL(k_part_rows, dim3(P), dim3(256), 0, a->stream, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
+                     s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.cmax, a->sw, h, nullptr, s.counts.as<int64_t>(),
+                     out.as<uint64_t>());
+  KHIP_TRY_HIP(hipGetLastError());
+  rows->resize((size_t)n * a->sw);
+  if (n) KHIP_TRY_HIP(hipMemcpyAsync(rows->data(), out.p, (size_t)n * a->sw * 8, hipMemcpyDeviceToHost, a->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  out.release();
+  return KHIP_OK;
+}
+
+}  // namespace khip

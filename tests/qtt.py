@@ -19,11 +19,11 @@ def load_cases(kind):
         return json.load(f)["cases"]
 
 
-def case_desc(case, device=0):
+def case_desc(case, device=0, flags=0):
     d = case["desc"]
     return abi.make_agg_desc(d["window_kind"], d["key_type"], d["size_ms"], d["advance_ms"],
                              d["grace_ms"], d["col_types"],
-                             [(a["kind"], a["arg_col"]) for a in d["aggs"]], device=device)
+                             [(a["kind"], a["arg_col"]) for a in d["aggs"]], device=device, flags=flags)
 
 
 def case_batch(case, lo=0, hi=None):
@@ -45,9 +45,9 @@ def case_batch(case, lo=0, hi=None):
                          key_valid=key_valid, row_valid=row_valid, cols=cols, col_valid=cvalid)
 
 
-def run_agg_case(lib, case, split=None, device=0):
+def run_agg_case(lib, case, split=None, device=0, flags=0):
     """split: None = one batch; k = batches of k rows (exercises cross-batch state)."""
-    h = abi.AggHandle(lib, case_desc(case, device))
+    h = abi.AggHandle(lib, case_desc(case, device, flags))
     n = len(case["input"])
     step = n if not split else split
     for lo in range(0, max(n, 1), max(step, 1)):

@@ -32,10 +32,18 @@ def orc():
     return abi.load_oracle()
 
 
+ENGINES = {"part": 0, "atomic": abi.FLAG_ENGINE_ATOMIC}
+
+
+@pytest.fixture(params=list(ENGINES), scope="module")
+def engine(request):
+    return ENGINES[request.param]
+
+
 @pytest.mark.parametrize("split", [None, 1, 3])
 @pytest.mark.parametrize("case", AGG_CASES, ids=["%s %s" % (c["source"], c["name"]) for c in AGG_CASES])
-def test_qtt_aggregate_golden(prod, case, split):
-    snap = qtt.run_agg_case(prod, case, split)
+def test_qtt_aggregate_golden(prod, case, split, engine):
+    snap = qtt.run_agg_case(prod, case, split, flags=engine)
     assert qtt.compare_agg(case, snap) == []
 
 
@@ -111,10 +119,10 @@ WINDOWS = [
 ]
 
 
-def _run_both(prod, orc, desc_kw, batches, having=None):
+def _run_both(prod, orc, desc_kw, batches, having=None, engine=0):
     out = []
     for lib in (prod, orc):
-        desc = abi.make_agg_desc(**desc_kw)
+        desc = abi.make_agg_desc(**dict(desc_kw, flags=engine if lib is prod else 0))
         h = abi.AggHandle(lib, desc)
         stats = [h.push(b) for b in batches]
         out.append((h.snapshot(having), stats, desc))
@@ -125,31 +133,31 @@ def _run_both(prod, orc, desc_kw, batches, having=None):
 @pytest.mark.parametrize("key_type", ["INT64", "UTF8"])
 @pytest.mark.parametrize("win", range(len(WINDOWS)))
 @pytest.mark.parametrize("nbatches", [1, 4])
-def test_random_vs_oracle(prod, orc, key_type, win, nbatches):
+def test_random_vs_oracle(prod, orc, key_type, win, nbatches, engine):
     rng = np.random.default_rng(1000 * win + nbatches + (7 if key_type == "UTF8" else 0))
     batches = [_random_batch(rng, 4000, key_type, 300, 200_000, 40_000, t0=b * 150_000, neg_ts=0.01)
                for b in range(nbatches)]
     kw = dict(WINDOWS[win], key_type=key_type, col_types=["INT32", "INT64", "DOUBLE", "DOUBLE"], aggs=ALL_AGGS)
-    (g, gs, desc), (o, os_, _) = _run_both(prod, orc, kw, batches)
+    (g, gs, desc), (o, os_, _) = _run_both(prod, orc, kw, batches, engine=engine)
     assert gs == os_
     assert_snap_equal(g, o, desc, ABS_SUM)
 
 
 @pytest.mark.parametrize("having", [{"agg": 0, "op": "GT", "value": 3}, {"agg": 4, "op": "LE", "value": 10.5},
                                     {"agg": 5, "op": "NE", "value": 0}])
-def test_having_vs_oracle(prod, orc, having):
+def test_having_vs_oracle(prod, orc, having, engine):
     rng = np.random.default_rng(5)
     batches = [_random_batch(rng, 20000, "INT64", 2000, 100_000, 5_000)]
     kw = dict(WINDOWS[1], key_type="INT64", col_types=["INT32", "INT64", "DOUBLE", "DOUBLE"], aggs=ALL_AGGS)
-    (g, _, desc), (o, _, _) = _run_both(prod, orc, kw, batches, having)
+    (g, _, desc), (o, _, _) = _run_both(prod, orc, kw, batches, having, engine=engine)
     assert_snap_equal(g, o, desc, ABS_SUM)
-    h = abi.AggHandle(prod, abi.make_agg_desc(**kw))
+    h = abi.AggHandle(prod, abi.make_agg_desc(**dict(kw, flags=engine)))
     h.push(batches[0])
     assert h.count_rows(having) == o["n"]
     h.close()
 
 
-def test_empty_and_all_null_batches(prod, orc):
+def test_empty_and_all_null_batches(prod, orc, engine):
     kw = dict(WINDOWS[3], key_type="INT64", col_types=["INT32", "INT64", "DOUBLE", "DOUBLE"], aggs=ALL_AGGS)
     empty = abi.HostBatch(np.zeros(0, np.int64), keys=np.zeros(0, np.int64),
                           cols=[np.zeros(0, np.int32), np.zeros(0, np.int64), np.zeros(0), np.zeros(0)])
@@ -159,33 +167,33 @@ def test_empty_and_all_null_batches(prod, orc):
     nullvals = abi.HostBatch(np.arange(n), keys=np.arange(n) % 10,
                              cols=[np.zeros(n, np.int32), np.zeros(n, np.int64), np.zeros(n), np.zeros(n)],
                              col_valid=[np.zeros(n, bool)] * 4)
-    (g, gs, desc), (o, os_, _) = _run_both(prod, orc, kw, [empty, allnull, nullvals, empty])
+    (g, gs, desc), (o, os_, _) = _run_both(prod, orc, kw, [empty, allnull, nullvals, empty], engine=engine)
     assert gs == os_
     assert gs[1]["dropped_null_key"] == n
     assert_snap_equal(g, o, desc, ABS_SUM)
     assert g["n"] > 0 and g["nulls"][5].all()  # MIN over only-null inputs is NULL (entry exists)
 
 
-def test_hot_key_contention(prod, orc):
+def test_hot_key_contention(prod, orc, engine):
     n = 200_000
     rng = np.random.default_rng(3)
     b = abi.HostBatch(np.arange(n) // 10, keys=np.zeros(n, np.int64),
                       cols=[rng.integers(-100, 100, n).astype(np.int32), rng.integers(-2**40, 2**40, n),
                             rng.random(n), rng.random(n)])
     kw = dict(WINDOWS[3], key_type="INT64", col_types=["INT32", "INT64", "DOUBLE", "DOUBLE"], aggs=ALL_AGGS)
-    (g, gs, desc), (o, os_, _) = _run_both(prod, orc, kw, [b])
+    (g, gs, desc), (o, os_, _) = _run_both(prod, orc, kw, [b], engine=engine)
     assert gs == os_
     assert_snap_equal(g, o, desc, ABS_SUM)
 
 
-def test_table_growth_and_resume(prod, orc):
+def test_table_growth_and_resume(prod, orc, engine):
     # capacity hint far too small: forces resume passes after probe exhaustion + rehash
     rng = np.random.default_rng(11)
     batches = [_random_batch(rng, 60000, "INT64", 50_000, 1_000_000, 10, null_frac=0.0, t0=i * 1_000_000)
                for i in range(3)]
     kw = dict(WINDOWS[3], key_type="INT64", col_types=["INT32", "INT64", "DOUBLE", "DOUBLE"], aggs=ALL_AGGS,
               capacity_hint=16)
-    (g, gs, desc), (o, os_, _) = _run_both(prod, orc, kw, batches)
+    (g, gs, desc), (o, os_, _) = _run_both(prod, orc, kw, batches, engine=engine)
     assert gs == os_
     assert_snap_equal(g, o, desc, ABS_SUM)
 
