@@ -208,8 +208,8 @@ struct PartState {
   DevBuf pbase, R, ctr, counts;
   DevBuf buf[2];          // region storage: P x cmax rows x sw words, double buffered
   DevBuf sel, cnt, newcnt, fail;  // per partition: buffer select, rows, rows being written, flags
-  DevBuf hist, tilemax, tileprefix, tpart, scan_tmp;
-  DevBuf skey, sts, smeta, scol[MAX_COLS];
+  DevBuf hist, tilemax, tilemin, tileprefix, tpart, scan_tmp;
+  DevBuf skey, sts, smeta, scol[MAX_COLS];  // skey: AoS (key, ts) 16-byte records
   DevBuf work;            // retry work items
   int64_t scat_cap = 0;
 };

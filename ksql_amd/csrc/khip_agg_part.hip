@@ -24,18 +24,17 @@
 #include <cstring>
 #include <vector>
 
+#include <cstdlib>
+
 #include "khip_agg_internal.hpp"
 
 namespace khip {
 
 constexpr int PT_THREADS = 1024;
-constexpr int PT_ITEMS = 64;
-constexpr int64_t PT_TILE = (int64_t)PT_THREADS * PT_ITEMS;  // 65536 records per tile
+constexpr int PT_ITEMS = 64;  // default records per thread per tile (KHIP_TILE_ITEMS overrides)
 constexpr int AG_THREADS = 1024;
-constexpr int CH_BITS = 16;  // records per LDS claim-reference chunk
-constexpr int64_t CH = 1LL << CH_BITS;
-constexpr uint32_t L_FRESH = 0x80000000u;
-constexpr uint32_t L_RES = 0xFFFFFFFFu;
+constexpr uint32_t L_CLAIM = 1u;
+constexpr uint32_t L_READY = 2u;
 constexpr int MAX_P_LOG2 = 14;  // LDS histogram: 16384 x u32 = 64 KB
 constexpr int TC_MAX = 64;      // tile chunks for the column prefix
 
@@ -75,33 +74,50 @@ __device__ __forceinline__ int64_t tile_of(int64_t b, int64_t nT) {
 __global__ __launch_bounds__(PT_THREADS) void k_part_hist(const int64_t* __restrict__ keys,
                                                           const int64_t* __restrict__ ts,
                                                           const uint8_t* __restrict__ kv,
-                                                          const uint8_t* __restrict__ rv, int64_t n, int log2P,
-                                                          int64_t nT, uint32_t* __restrict__ hist,
-                                                          int64_t* __restrict__ tilemax, int64_t* __restrict__ tpart) {
+                                                          const uint8_t* __restrict__ rv, int64_t n, int64_t tile,
+                                                          int log2P, int pad, int64_t nT, uint32_t* __restrict__ hist,
+                                                          int64_t* __restrict__ tilemax, int64_t* __restrict__ tilemin,
+                                                          int64_t* __restrict__ tpart) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint32_t* lh = (uint32_t*)smem;
   __shared__ int64_t lmax[PT_THREADS / 64];
+  __shared__ int64_t lmin[PT_THREADS / 64];
   __shared__ unsigned long long lc[4];
   const int P = 1 << log2P;
   const int64_t t = tile_of(blockIdx.x, nT);
   for (int p = threadIdx.x; p < P; p += PT_THREADS) lh[p] = 0;
   if (threadIdx.x < 4) lc[threadIdx.x] = 0;
   __syncthreads();
-  int64_t m = -1, c_acc = 0, c_nk = 0, c_nr = 0, c_bt = 0;
-  const int64_t base = t * PT_TILE;
-  for (int r = 0; r < PT_ITEMS; r++) {
-    const int64_t i = base + (int64_t)r * PT_THREADS + threadIdx.x;
-    if (i >= n) break;
-    if (!bit_get(kv, i)) { c_nk++; continue; }
-    if (!bit_get(rv, i)) { c_nr++; continue; }
-    const int64_t x = ts[i];
-    if (x < 0) { c_bt++; continue; }
-    c_acc++;
-    m = x > m ? x : m;
-    atomicAdd(&lh[part_of(keys[i], log2P)], 1u);
+  int64_t m = -1, mn = INT64_MAX, c_acc = 0, c_nk = 0, c_nr = 0, c_bt = 0;
+  const int64_t base = t * tile;
+  const int64_t end = base + tile < n ? base + tile : n;
+  for (int64_t i0 = base + threadIdx.x; i0 < end; i0 += 4 * PT_THREADS) {
+    int64_t x[4], k[4];
+    bool ok[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {  // issue the loads of 4 records before using any
+      const int64_t i = i0 + u * PT_THREADS;
+      ok[u] = i < end;
+      x[u] = ok[u] ? ts[i] : 0;
+      k[u] = ok[u] ? keys[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int64_t i = i0 + u * PT_THREADS;
+      if (!ok[u]) continue;
+      if (!bit_get(kv, i)) { c_nk++; continue; }
+      if (!bit_get(rv, i)) { c_nr++; continue; }
+      if (x[u] < 0) { c_bt++; continue; }
+      c_acc++;
+      m = x[u] > m ? x[u] : m;
+      mn = x[u] < mn ? x[u] : mn;
+      atomicAdd(&lh[part_of(k[u], log2P)], 1u);
+    }
   }
   int64_t tot;
   block_incl_max(m, lmax, &tot);
+  int64_t totmin;
+  block_incl_max(-mn, lmin, &totmin);  // min via max of negation (mn >= 0 or INT64_MAX)
   c_acc = wave_sum(c_acc); c_nk = wave_sum(c_nk); c_nr = wave_sum(c_nr); c_bt = wave_sum(c_bt);
   if ((threadIdx.x & 63) == 0) {
     if (c_acc) atomicAdd(&lc[0], (unsigned long long)c_acc);
@@ -111,9 +127,11 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_hist(const int64_t* __restr
   }
   __syncthreads();
   uint32_t* hrow = hist + t * (int64_t)P;
-  for (int p = threadIdx.x; p < P; p += PT_THREADS) hrow[p] = lh[p];
+  // pad: each (tile, partition) run rounded up to whole 64-byte segments (4 records)
+  for (int p = threadIdx.x; p < P; p += PT_THREADS) hrow[p] = pad ? (lh[p] + 3u) & ~3u : lh[p];
   if (threadIdx.x == 0) {
     tilemax[t] = tot;
+    tilemin[t] = -totmin;
     int64_t* tp = tpart + t * T_NPART;
     tp[T_ACCEPTED] = (int64_t)lc[0];
     tp[T_NULL_KEY] = (int64_t)lc[1];
@@ -164,12 +182,32 @@ __global__ __launch_bounds__(256) void k_part_colprefix(uint32_t* __restrict__ h
   }
 }
 
+__device__ __forceinline__ void scatter_one(int64_t key, int64_t x, int64_t jlo, int64_t i, int log2P, uint32_t* cur,
+                                            longlong2* __restrict__ srec, int has_meta, uint32_t* __restrict__ smeta,
+                                            const ColPtrs& cols, int n_cols, const ColTypes& ctypes,
+                                            const ColPtrs& scols, bool applied) {
+  const uint32_t pos = atomicAdd(&cur[part_of(key, log2P)], 1u);
+  longlong2 rec;
+  rec.x = key;
+  rec.y = applied ? x : -1;
+  srec[pos] = rec;  // one 16-byte store per record
+  if (has_meta) {
+    uint32_t vm = 0;
+    for (int c = 0; c < n_cols; c++) vm |= (bit_get(cols.valid[c], i) ? 1u : 0u) << c;
+    smeta[pos] = (uint32_t)jlo | (vm << 16);
+  }
+  for (int c = 0; c < n_cols; c++)  // raw 8-byte value (INT32 sign-extended, DOUBLE bits)
+    ((int64_t*)scols.data[c])[pos] = load_col_raw(cols, ctypes.t[c], c, i);
+}
+
+template <int U>
 __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
     const int64_t* __restrict__ keys, const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
-    const uint8_t* __restrict__ rv, ColPtrs cols, int n_cols, ColTypes ctypes, int64_t n, int log2P, int64_t nT,
-    const uint32_t* __restrict__ offs, const int64_t* __restrict__ tileprefix, int windowed, int64_t size,
-    int64_t adv, int64_t grace, int has_meta, int64_t* __restrict__ skey, int64_t* __restrict__ sts,
-    uint32_t* __restrict__ smeta, ColPtrs scols, int64_t* __restrict__ tpart) {
+    const uint8_t* __restrict__ rv, ColPtrs cols, int n_cols, ColTypes ctypes, int64_t n, int64_t tile, int log2P,
+    int pad, int64_t nT, const uint32_t* __restrict__ offs, const int64_t* __restrict__ pbase,
+    const int64_t* __restrict__ tileprefix, const int64_t* __restrict__ tilemax,
+    const int64_t* __restrict__ tilemin, int windowed, int64_t size, int64_t adv, int64_t grace, int has_meta,
+    longlong2* __restrict__ srec, uint32_t* __restrict__ smeta, ColPtrs scols, int64_t* __restrict__ tpart) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint32_t* cur = (uint32_t*)smem;
   __shared__ int64_t lmax[PT_THREADS / 64];
@@ -181,40 +219,60 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
   __syncthreads();
   int64_t carry = tileprefix[t];
   int64_t c_app = 0, c_late = 0;
-  const int64_t base = t * PT_TILE;
-  for (int r = 0; r < PT_ITEMS; r++) {
-    if (base + (int64_t)r * PT_THREADS >= n) break;  // uniform across the block
-    const int64_t i = base + (int64_t)r * PT_THREADS + threadIdx.x;
-    const bool in = i < n;
-    const int64_t x = in ? ts[i] : -1;
-    const bool valid = in && bit_get(kv, i) && bit_get(rv, i) && x >= 0;
-    int64_t tot;
-    const int64_t incl = block_incl_max(valid ? x : -1, lmax, &tot);
-    const int64_t st = incl > carry ? incl : carry;
-    carry = tot > carry ? tot : carry;
-    if (!valid) continue;
-    int64_t jlo = 0, nwin = 1;
-    if (windowed) {
-      const int64_t ws0 = first_window_start(x, size, adv);
-      nwin = (x - ws0) / adv + 1;
-      // applied iff ws + size > st - grace  ⇔  ws >= st - grace - size + 1
-      const int64_t wmin = st - grace - size + 1;
-      if (wmin > ws0) jlo = (wmin - ws0 + adv - 1) / adv;
-      if (jlo > nwin) jlo = nwin;
+  const int64_t base = t * tile;
+  const int64_t end = base + tile < n ? base + tile : n;
+  // Fast path: no record of this tile can be late when even its earliest first window
+  // outlives the largest stream time the tile can reach (max(prefix, tile max)).
+  const int64_t smax = carry > tilemax[t] ? carry : tilemax[t];
+  const int64_t tmin = tilemin[t];
+  const bool fast = !windowed || tmin == INT64_MAX || first_window_start(tmin, size, adv) + size > smax - grace;
+  if (fast) {
+    // U records per thread per step: the loads of a step are issued together, and since
+    // vmcnt retires loads and stores in issue order, fewer steps = fewer waits behind the
+    // previous step's scattered stores
+    for (int64_t i0 = base + threadIdx.x; i0 < end; i0 += U * PT_THREADS) {
+      int64_t x[U], k[U];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int64_t i = i0 + u * PT_THREADS;
+        ok[u] = i < end;
+        x[u] = ok[u] ? ts[i] : -1;
+        k[u] = ok[u] ? keys[i] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int64_t i = i0 + u * PT_THREADS;
+        if (!ok[u] || x[u] < 0 || !bit_get(kv, i) || !bit_get(rv, i)) continue;
+        const int64_t nwin = windowed ? (x[u] - first_window_start(x[u], size, adv)) / adv + 1 : 1;
+        c_app += nwin;
+        scatter_one(k[u], x[u], 0, i, log2P, cur, srec, has_meta, smeta, cols, n_cols, ctypes, scols, true);
+      }
     }
-    c_late += jlo;
-    c_app += nwin - jlo;
-    const int64_t key = keys[i];
-    const uint32_t pos = atomicAdd(&cur[part_of(key, log2P)], 1u);
-    skey[pos] = key;
-    sts[pos] = nwin > jlo ? x : -1;
-    if (has_meta) {
-      uint32_t vm = 0;
-      for (int c = 0; c < n_cols; c++) vm |= (bit_get(cols.valid[c], i) ? 1u : 0u) << c;
-      smeta[pos] = (uint32_t)jlo | (vm << 16);
+  } else {
+    for (int64_t r = 0; base + r * PT_THREADS < end; r++) {  // uniform across the block
+      const int64_t i = base + (int64_t)r * PT_THREADS + threadIdx.x;
+      const bool in = i < end;
+      const int64_t x = in ? ts[i] : -1;
+      const bool valid = in && bit_get(kv, i) && bit_get(rv, i) && x >= 0;
+      int64_t tot;
+      const int64_t incl = block_incl_max(valid ? x : -1, lmax, &tot);
+      const int64_t st = incl > carry ? incl : carry;
+      carry = tot > carry ? tot : carry;
+      if (!valid) continue;
+      int64_t jlo = 0, nwin = 1;
+      if (windowed) {
+        const int64_t ws0 = first_window_start(x, size, adv);
+        nwin = (x - ws0) / adv + 1;
+        // applied iff ws + size > st - grace  ⇔  ws >= st - grace - size + 1
+        const int64_t wmin = st - grace - size + 1;
+        if (wmin > ws0) jlo = (wmin - ws0 + adv - 1) / adv;
+        if (jlo > nwin) jlo = nwin;
+      }
+      c_late += jlo;
+      c_app += nwin - jlo;
+      scatter_one(keys[i], x, jlo, i, log2P, cur, srec, has_meta, smeta, cols, n_cols, ctypes, scols, nwin > jlo);
     }
-    for (int c = 0; c < n_cols; c++)  // raw 8-byte value (INT32 sign-extended, DOUBLE bits)
-      ((int64_t*)scols.data[c])[pos] = load_col_raw(cols, ctypes.t[c], c, i);
   }
   c_app = wave_sum(c_app);
   c_late = wave_sum(c_late);
@@ -223,12 +281,17 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
     if (c_late) atomicAdd(&lc[1], (unsigned long long)c_late);
   }
   __syncthreads();
+  if (pad) {  // fill each run's tail up to the next run's start with skipped records (ts = -1)
+    for (int p = threadIdx.x; p < P; p += PT_THREADS) {
+      const int64_t stop = t + 1 < nT ? (int64_t)offs[(t + 1) * P + p] : pbase[p + 1];
+      for (int64_t q = cur[p]; q < stop; q++) srec[q] = make_longlong2(0, -1);
+    }
+  }
   if (threadIdx.x == 0) {
     tpart[t * T_NPART + T_APPLIED] = (int64_t)lc[0];
     tpart[t * T_NPART + T_LATE] = (int64_t)lc[1];
   }
 }
-
 
 // ------------------------------------------------------------------ k_part_agg
 // Work item: blockIdx.x = partition (work == nullptr), or work[blockIdx.x] =
@@ -239,25 +302,31 @@ __device__ __forceinline__ bool part_sub_ok(uint64_t h, int sbits, int sub) {
   return sbits == 0 || (int)((h >> 40) & ((1u << sbits) - 1)) == sub;
 }
 
-__device__ __forceinline__ void lds_apply(const PartAggParams& q, int64_t* lw, int H, int e, int64_t t,
+#define KLDS __attribute__((address_space(3)))
+typedef KLDS uint32_t lds_u32;
+typedef KLDS int64_t lds_i64;
+typedef KLDS double lds_f64;
+#define WG_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP
+
+__device__ __forceinline__ void lds_apply(const PartAggParams& q, lds_i64* lw, int H, int e, int64_t t,
                                           uint32_t vmask, const ColPtrs& scols, int64_t gi) {
-  atomicMax((long long*)&lw[2 * H + e], (long long)t);
+  __hip_atomic_fetch_max(&lw[2 * H + e], t, WG_RLX);
   for (int o = 0; o < q.n_ops; o++) {
     const UpdOp op = q.ops[o];
-    int64_t* w = &lw[op.word * H + e];
+    lds_i64* w = &lw[op.word * H + e];
     if (op.kind == OP_INC) {
-      atomicAdd((unsigned long long*)w, 1ULL);
+      __hip_atomic_fetch_add(w, (int64_t)1, WG_RLX);
       continue;
     }
     if (!((vmask >> op.col) & 1u)) continue;
     const int64_t raw = ((const int64_t*)scols.data[op.col])[gi];
     switch (op.kind) {
-      case OP_INC_VALID: atomicAdd((unsigned long long*)w, 1ULL); break;
-      case OP_ADD_I64: atomicAdd((unsigned long long*)w, (unsigned long long)raw); break;
+      case OP_INC_VALID: __hip_atomic_fetch_add(w, (int64_t)1, WG_RLX); break;
+      case OP_ADD_I64: __hip_atomic_fetch_add((KLDS uint64_t*)w, (uint64_t)raw, WG_RLX); break;
       case OP_ADD_F64: {
         double d;
         __builtin_memcpy(&d, &raw, 8);
-        atomicAdd((double*)w, d);
+        __hip_atomic_fetch_add((lds_f64*)w, d, WG_RLX);
         break;
       }
       case OP_MIN:
@@ -268,8 +337,8 @@ __device__ __forceinline__ void lds_apply(const PartAggParams& q, int64_t* lw, i
           __builtin_memcpy(&d, &raw, 8);
           k = f64_order_key(d);
         }
-        if (op.kind == OP_MIN) atomicMin((long long*)w, (long long)k);
-        else atomicMax((long long*)w, (long long)k);
+        if (op.kind == OP_MIN) __hip_atomic_fetch_min(w, k, WG_RLX);
+        else __hip_atomic_fetch_max(w, k, WG_RLX);
         break;
       }
       default: break;
@@ -279,18 +348,20 @@ __device__ __forceinline__ void lds_apply(const PartAggParams& q, int64_t* lw, i
 
 __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const uint32_t* __restrict__ work,
                                                          const int64_t* __restrict__ pbase,
-                                                         const int64_t* __restrict__ skey,
-                                                         const int64_t* __restrict__ sts,
+                                                         const longlong2* __restrict__ srec,
                                                          const uint32_t* __restrict__ smeta, ColPtrs scols,
                                                          uint64_t* __restrict__ buf0, uint64_t* __restrict__ buf1,
                                                          const uint8_t* __restrict__ sel,
                                                          const int64_t* __restrict__ cnt,
                                                          unsigned long long* __restrict__ newcnt,
-                                                         uint8_t* __restrict__ fail) {
+                                                         uint8_t* __restrict__ fail,
+                                                         unsigned long long* __restrict__ need) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = q.H;
-  uint32_t* lref = (uint32_t*)smem;
-  int64_t* lw = (int64_t*)(smem + (((size_t)H * 4 + 15) & ~(size_t)15));
+  lds_u32* lref = (lds_u32*)smem;
+  lds_i64* lw = (lds_i64*)(smem + (((size_t)H * 4 + 15) & ~(size_t)15));
+  volatile lds_u32* vlref = lref;
+  volatile lds_i64* vlw = lw;
   __shared__ int lused, lovf;
   __shared__ int lcnt[AG_THREADS / 64];
   __shared__ unsigned long long lbase;
@@ -306,6 +377,17 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
   }
   const int64_t rbase = pbase[p], rn = pbase[p + 1] - rbase;
   if (rn == 0 && !work) return;  // untouched partition: nothing to rewrite
+  // the first AU records of every thread are loaded before the LDS table is initialised,
+  // so the HBM latency overlaps the init instead of following it
+  constexpr int AU = 8;
+  longlong2 rec[AU];
+  uint32_t meta[AU];
+#pragma unroll
+  for (int u = 0; u < AU; u++) {
+    const int64_t li = threadIdx.x + (int64_t)u * AG_THREADS;
+    rec[u] = li < rn ? srec[rbase + li] : make_longlong2(0, -1);
+    meta[u] = (q.has_meta && li < rn) ? smeta[rbase + li] : 0u;
+  }
   for (int e = threadIdx.x; e < H; e += AG_THREADS) {
     lref[e] = 0;
     for (int w = 0; w < q.nwords; w++) lw[w * H + e] = q.init.w[w];
@@ -328,59 +410,67 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
       break;
     }
     int e = (int)(h & (uint64_t)(H - 1));
-    while (atomicCAS(&lref[e], 0u, L_RES) != 0u) e = (e + 1) & (H - 1);
+    for (;;) {
+      uint32_t expect = 0u;
+      if (__hip_atomic_compare_exchange_strong(&lref[e], &expect, L_READY, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+      e = (e + 1) & (H - 1);
+    }
     for (int w = 0; w < q.nwords; w++) lw[w * H + e] = (int64_t)row[w];
   }
   __syncthreads();
-  // 2. this batch's records, in chunks of CH (claim references are chunk-relative)
-  for (int64_t c0 = 0; c0 < rn; c0 += CH) {
-    const int64_t c1 = c0 + CH < rn ? c0 + CH : rn;
-    for (int64_t li = c0 + threadIdx.x; li < c1; li += AG_THREADS) {
-      if (*(volatile int*)&lovf) break;
-      const int64_t gi = rbase + li;
-      const int64_t t = sts[gi];
-      if (t < 0) continue;  // every window late
-      const int64_t key = skey[gi];
-      const uint32_t meta = q.has_meta ? smeta[gi] : 0u;
-      const int64_t jlo = meta & 0xFFFFu;
-      const uint32_t vmask = meta >> 16;
+  // 2. this batch's records.  Entry states: 0 empty → L_CLAIM (CAS winner writes key/ws)
+  //    → L_READY (workgroup-scope release); a loser waits for READY (the winner is another
+  //    wave, or an earlier instruction of its own wave), then compares key/ws in LDS.
+  for (int64_t l0 = threadIdx.x; l0 < rn; l0 += AU * AG_THREADS) {
+    if (*(volatile KLDS int*)&lovf) break;
+    if (l0 != threadIdx.x) {
+#pragma unroll
+      for (int u = 0; u < AU; u++) {  // AU records in flight per thread
+        const int64_t li = l0 + u * AG_THREADS;
+        rec[u] = li < rn ? srec[rbase + li] : make_longlong2(0, -1);
+        meta[u] = (q.has_meta && li < rn) ? smeta[rbase + li] : 0u;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < AU; u++) {  // unrolled: rec[]/meta[] stay in registers (no scratch)
+      const int64_t t = rec[u].y;
+      if (t < 0) continue;  // every window late (or past the end)
+      const int64_t key = rec[u].x;
+      const int64_t gi = rbase + l0 + u * AG_THREADS;
+      const int64_t jlo = meta[u] & 0xFFFFu;
+      const uint32_t vmask = meta[u] >> 16;
       const int64_t ws_first = q.windowed ? first_window_start(t, q.size, q.adv) : 0;
-      int64_t j = jlo;
-      for (int64_t ws = ws_first + jlo * q.adv; ws <= (q.windowed ? t : 0); ws += (q.windowed ? q.adv : 1), j++) {
+      for (int64_t ws = ws_first + jlo * q.adv; ws <= (q.windowed ? t : 0); ws += (q.windowed ? q.adv : 1)) {
         const uint64_t h = group_hash(key, ws);
         if (!part_sub_ok(h, sbits, sub)) continue;
-        const uint32_t ref = L_FRESH | ((uint32_t)j << CH_BITS) | (uint32_t)(li - c0);
         int e = (int)(h & (uint64_t)(H - 1));
         bool done = false;
         for (int probe = 0; probe < H; probe++) {
-          uint32_t v = *(volatile uint32_t*)&lref[e];
-          bool hit = false;
-          if (v == L_RES) {
-            hit = lw[e] == key && lw[H + e] == ws;
-          } else {
-            if (v == 0u) {
-              const uint32_t old = atomicCAS(&lref[e], 0u, ref);
-              if (old == 0u) {
-                if (atomicAdd(&lused, 1) >= q.H_eff) lovf = 1;
-                lw[e] = key;
-                lw[H + e] = ws;
-                hit = true;
-              } else {
-                v = old;
-              }
+          uint32_t v = vlref[e];
+          if (v == 0u) {
+            uint32_t old = 0u;
+            __hip_atomic_compare_exchange_strong(&lref[e], &old, L_CLAIM, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (old == 0u) {
+              if (atomicAdd(&lused, 1) >= q.H_eff) lovf = 1;
+              vlw[e] = key;
+              vlw[H + e] = ws;
+              // LDS serves one wave's requests in issue order: once READY is visible, so are
+              // key/ws.  Only the compiler must not reorder (no vmcnt/cache instruction needed).
+              __atomic_signal_fence(__ATOMIC_SEQ_CST);
+              vlref[e] = L_READY;
+              lds_apply(q, lw, H, e, t, vmask, scols, gi);
+              done = true;
+              break;
             }
-            if (!hit && v != L_RES && (v & L_FRESH)) {
-              const int64_t g2 = rbase + c0 + (int64_t)(v & (uint32_t)(CH - 1));
-              const int64_t j2 = (v >> CH_BITS) & 0x7FFFu;
-              if (skey[g2] == key) {
-                const int64_t ws2 = q.windowed ? first_window_start(sts[g2], q.size, q.adv) + j2 * q.adv : 0;
-                hit = ws2 == ws;
-              }
-            } else if (!hit && v == L_RES) {
-              hit = lw[e] == key && lw[H + e] == ws;
-            }
+            v = old;
           }
-          if (hit) {
+          for (int spin = 0; v == L_CLAIM; spin++) {  // bounded: the claimer is two stores away
+            __builtin_amdgcn_s_sleep(1);
+            v = vlref[e];
+            if (spin > (1 << 20)) { lovf = 1; break; }
+          }
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+          if (vlw[e] == key && vlw[H + e] == ws) {
             lds_apply(q, lw, H, e, t, vmask, scols, gi);
             done = true;
             break;
@@ -391,11 +481,8 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
         if (!q.windowed) break;
       }
     }
-    __syncthreads();
-    for (int e = threadIdx.x; e < H; e += AG_THREADS)
-      if (lref[e] != 0u && lref[e] != L_RES) lref[e] = L_RES;
-    __syncthreads();
   }
+  __syncthreads();
   if (lovf) {
     if (threadIdx.x == 0) fail[p] |= 1;
     return;
@@ -422,7 +509,10 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
   if (threadIdx.x == 0) lbase = total ? atomicAdd(&newcnt[p], (unsigned long long)total) : 0ULL;
   __syncthreads();
   if ((int64_t)(lbase + total) > q.cmax) {
-    if (threadIdx.x == 0) fail[p] |= 2;
+    if (threadIdx.x == 0) {
+      fail[p] |= 2;
+      atomicMax(need, (unsigned long long)(lbase + total));  // rows this partition needs (lower bound)
+    }
     return;
   }
   uint64_t* dst =
@@ -476,10 +566,11 @@ __global__ __launch_bounds__(256) void k_part_regrow(const uint64_t* __restrict_
 }
 
 // Double the partition count: rows of partition p move to 2p / 2p+1 (next hash bit).
+// nb == nullptr: count only (ncnt = child row counts, used to size the new regions).
 __global__ __launch_bounds__(256) void k_part_split(const uint64_t* __restrict__ b0, const uint64_t* __restrict__ b1,
                                                     const uint8_t* __restrict__ sel, const int64_t* __restrict__ cnt,
                                                     int64_t cmax, int sw, int new_log2P, uint64_t* __restrict__ nb,
-                                                    int64_t* __restrict__ ncnt) {
+                                                    int64_t ncmax, int64_t* __restrict__ ncnt) {
   __shared__ unsigned int lc[2];
   const int64_t p = blockIdx.x;
   if (threadIdx.x < 2) lc[threadIdx.x] = 0;
@@ -489,7 +580,8 @@ __global__ __launch_bounds__(256) void k_part_split(const uint64_t* __restrict__
     const uint64_t* row = src + r * sw;
     const uint32_t child = part_of((int64_t)row[0], new_log2P);  // == 2p or 2p+1
     const unsigned k = atomicAdd(&lc[child & 1], 1u);
-    uint64_t* dst = nb + ((uint64_t)child * cmax + k) * sw;
+    if (!nb) continue;
+    uint64_t* dst = nb + ((uint64_t)child * ncmax + k) * sw;
     for (int w = 0; w < sw; w++) dst[w] = row[w];
   }
   __syncthreads();
@@ -547,15 +639,19 @@ khip_status part_init(khip_agg* a, int64_t hint) {
   for (int o = 0; o < a->ap.n_ops; o++) used = std::max(used, a->ap.ops[o].word + 1);
   s.nwords = used;
   const int entry = 4 + 8 * used;
-  // LDS table: the largest power of two within ~150 KB
-  int H = 512;
-  while ((int64_t)(H * 2) * entry + 16 <= 150 * 1024 && H < 8192) H *= 2;
+  // LDS table: the largest power of two within the budget (default 80 KB: two workgroups
+  // per CU overlap one's load/write-back phases with the other's LDS work)
+  const char* kb = getenv("KHIP_LDS_KB");
+  const int64_t budget = (kb ? atoi(kb) : 150) * 1024;
+  int H = 256;
+  while ((int64_t)(H * 2) * entry + 16 <= budget && H < 16384) H *= 2;
   s.H = H;
   s.H_eff = H * 3 / 4;
   s.lds_bytes = (int)((((size_t)H * 4 + 15) & ~(size_t)15) + (size_t)H * 8 * used);
-  // partitions: ~H/4 groups each at the hinted size (room for 3x growth before retries)
+  // partitions: at most ~H_eff/2 groups each at the hinted size
   const int64_t groups = std::max<int64_t>(hint, 1024);
-  s.log2P = std::min(MAX_P_LOG2, std::max(0, part_ceil_log2(groups * 4 / H)));
+  s.log2P = std::min(MAX_P_LOG2, std::max(0, part_ceil_log2(groups * 2 / s.H_eff)));
+  if (const char* e = getenv("KHIP_PART_LOG2")) s.log2P = std::min(MAX_P_LOG2, atoi(e));
   s.P = 1LL << s.log2P;
   s.cmax = next_pow2(std::max<int64_t>(64, 2 * groups / s.P + 64));
   KHIP_TRY(s.sel.ensure(s.P));
@@ -575,7 +671,7 @@ khip_status part_init(khip_agg* a, int64_t hint) {
 
 void part_release(khip_agg* a) {
   PartState& s = a->part;
-  DevBuf* bufs[] = {&s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist, &s.tilemax,
+  DevBuf* bufs[] = {&s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist, &s.tilemax, &s.tilemin,
                     &s.tileprefix, &s.tpart, &s.scan_tmp, &s.skey, &s.sts, &s.smeta, &s.work,
                     &s.pbase, &s.R, &s.ctr, &s.counts};
   for (DevBuf* b : bufs) b->release();
@@ -633,13 +729,23 @@ static khip_status part_split(khip_agg* a) {
   PartState& s = a->part;
   const int64_t P2 = s.P * 2;
   DevBuf nb[2], ncnt, nsel, nnew, nfail;
-  for (int b = 0; b < 2; b++) KHIP_TRY(nb[b].ensure((size_t)P2 * s.cmax * a->sw * 8));
   KHIP_TRY(ncnt.ensure(P2 * 8));
+  // 1. child row counts → region capacity for the new layout
+  hipLaunchKernelGGL(k_part_split, dim3(s.P), dim3(256), 0, a->stream, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
+                     s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.cmax, a->sw, s.log2P + 1, nullptr, (int64_t)0,
+                     ncnt.as<int64_t>());
+  std::vector<int64_t> hc(P2);
+  KHIP_TRY_HIP(hipMemcpyAsync(hc.data(), ncnt.p, P2 * 8, hipMemcpyDeviceToHost, a->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  const int64_t mx = *std::max_element(hc.begin(), hc.end());
+  const int64_t ncmax = next_pow2(std::max<int64_t>(64, mx * 3 / 2 + 64));
+  // 2. move the rows
+  for (int b = 0; b < 2; b++) KHIP_TRY(nb[b].ensure((size_t)P2 * ncmax * a->sw * 8));
   KHIP_TRY(nsel.ensure(P2));
   KHIP_TRY(nnew.ensure(P2 * 8));
   KHIP_TRY(nfail.ensure(P2));
   hipLaunchKernelGGL(k_part_split, dim3(s.P), dim3(256), 0, a->stream, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
-                     s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.cmax, a->sw, s.log2P + 1, nb[0].as<uint64_t>(),
+                     s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.cmax, a->sw, s.log2P + 1, nb[0].as<uint64_t>(), ncmax,
                      ncnt.as<int64_t>());
   KHIP_TRY_HIP(hipGetLastError());
   KHIP_TRY_HIP(hipMemsetAsync(nsel.p, 0, P2, a->stream));
@@ -655,6 +761,7 @@ static khip_status part_split(khip_agg* a) {
   }
   s.P = P2;
   s.log2P += 1;
+  s.cmax = ncmax;
   KHIP_TRY(s.pbase.ensure((s.P + 1) * 8));
   KHIP_TRY(s.R.ensure((s.P + 1) * 8));
   return KHIP_OK;
@@ -667,19 +774,25 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   // keep the resident groups per partition well inside the LDS table (split = exact re-layout)
   while (s.log2P < MAX_P_LOG2 && a->occ > s.P * (int64_t)s.H_eff / 2) KHIP_TRY(part_split(a));
   const int P = (int)s.P;
-  const int64_t nT = ceil_div(n, PT_TILE);
+  const char* ti = getenv("KHIP_TILE_ITEMS");
+  const int64_t tile = (int64_t)PT_THREADS * (ti ? atoi(ti) : PT_ITEMS);
+  const char* pe = getenv("KHIP_PAD");
+  const int pad = pe ? atoi(pe) : 0;
+  const int64_t nT = ceil_div(n, tile);
   const int TC = (int)std::min<int64_t>(nT, TC_MAX);
   KHIP_TRY(s.hist.ensure((size_t)nT * P * 4));
   KHIP_TRY(s.tilemax.ensure(nT * 8));
+  KHIP_TRY(s.tilemin.ensure(nT * 8));
   KHIP_TRY(s.tileprefix.ensure(nT * 8));
   KHIP_TRY(s.tpart.ensure(nT * 8 * T_NPART));
   KHIP_TRY(s.scan_tmp.ensure((size_t)TC * P * 8));
-  if (s.scat_cap < n) {
-    KHIP_TRY(s.skey.ensure(n * 8));
-    KHIP_TRY(s.sts.ensure(n * 8));
+  const int64_t ncap = pad ? n + 3 * (int64_t)P * nT : n;  // padded runs
+  if (s.scat_cap < ncap) {
+    const int64_t n = ncap;
+    KHIP_TRY(s.skey.ensure(n * 16));  // AoS (key, ts) records
     if (a->desc.window_kind == KHIP_WINDOW_HOPPING || a->desc.n_cols > 0) KHIP_TRY(s.smeta.ensure(n * 4));
     for (int c = 0; c < a->desc.n_cols; c++) KHIP_TRY(s.scol[c].ensure(n * 8));
-    s.scat_cap = n;
+    s.scat_cap = ncap;
   }
   ColTypes ct{};
   for (int c = 0; c < MAX_COLS; c++) ct.t[c] = a->ap.col_type[c];
@@ -688,8 +801,9 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   const size_t hist_lds = (size_t)P * 4;
   // 1. histogram + tile stream-time maxima
   ev_record_part(a, 0);
-  hipLaunchKernelGGL(k_part_hist, dim3(nT), dim3(PT_THREADS), hist_lds, a->stream, keys, ts, kv, rv, n, s.log2P, nT,
-                     s.hist.as<uint32_t>(), s.tilemax.as<int64_t>(), s.tpart.as<int64_t>());
+  hipLaunchKernelGGL(k_part_hist, dim3(nT), dim3(PT_THREADS), hist_lds, a->stream, keys, ts, kv, rv, n, tile, s.log2P,
+                     pad, nT,
+                     s.hist.as<uint32_t>(), s.tilemax.as<int64_t>(), s.tilemin.as<int64_t>(), s.tpart.as<int64_t>());
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, a->stream, s.tilemax.as<int64_t>(), nT,
                      s.tileprefix.as<int64_t>(), a->stream_time.as<int64_t>());
   // 2. offsets
@@ -706,10 +820,15 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   ev_record_part(a, 1);
   // 3. scatter
   const int has_meta = (a->desc.window_kind == KHIP_WINDOW_HOPPING || a->desc.n_cols > 0) ? 1 : 0;
-  hipLaunchKernelGGL(k_part_scatter, dim3(nT), dim3(PT_THREADS), hist_lds, a->stream, keys, ts, kv, rv, cols,
-                     a->desc.n_cols, ct, n, s.log2P, nT, s.hist.as<uint32_t>(), s.tileprefix.as<int64_t>(), a->windowed,
-                     a->desc.size_ms, a->windowed ? a->desc.advance_ms : 1, a->grace, has_meta, s.skey.as<int64_t>(),
-                     s.sts.as<int64_t>(), has_meta ? s.smeta.as<uint32_t>() : nullptr, sc, s.tpart.as<int64_t>());
+  const char* su = getenv("KHIP_SCATTER_U");
+  const int U = su ? atoi(su) : 16;
+  auto scat = U >= 16 ? k_part_scatter<16> : (U >= 8 ? k_part_scatter<8> : k_part_scatter<4>);
+  hipLaunchKernelGGL(scat, dim3(nT), dim3(PT_THREADS), hist_lds, a->stream, keys, ts, kv, rv, cols,
+                     a->desc.n_cols, ct, n, tile, s.log2P, pad, nT, s.hist.as<uint32_t>(), s.pbase.as<int64_t>(),
+                     s.tileprefix.as<int64_t>(),
+                     s.tilemax.as<int64_t>(), s.tilemin.as<int64_t>(), a->windowed, a->desc.size_ms,
+                     a->windowed ? a->desc.advance_ms : 1, a->grace, has_meta, s.skey.as<longlong2>(),
+                     has_meta ? s.smeta.as<uint32_t>() : nullptr, sc, s.tpart.as<int64_t>());
   KHIP_TRY_HIP(hipGetLastError());
   ev_record_part(a, 2);
   // 4. aggregate partitions (+ retries)
@@ -721,15 +840,16 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   for (int pass = 0;; pass++) {
     PartAggParams q = q0;
     q.cmax = s.cmax;
-    KHIP_TRY_HIP(hipMemsetAsync(s.ctr.p, 0, 16, a->stream));
+    KHIP_TRY_HIP(hipMemsetAsync(s.ctr.p, 0, 24, a->stream));
     const uint32_t* wk = pass == 0 ? nullptr : s.work.as<uint32_t>();
     const int64_t nwork = pass == 0 ? P : (int64_t)work.size();
     hipFuncSetAttribute((const void*)k_part_agg, hipFuncAttributeMaxDynamicSharedMemorySize, s.lds_bytes);
     hipLaunchKernelGGL(k_part_agg, dim3(nwork), dim3(AG_THREADS), s.lds_bytes, a->stream, q, wk,
-                       s.pbase.as<int64_t>(), s.skey.as<int64_t>(), s.sts.as<int64_t>(),
+                       s.pbase.as<int64_t>(), s.skey.as<longlong2>(),
                        has_meta ? s.smeta.as<uint32_t>() : nullptr, sc, s.buf[0].as<uint64_t>(),
                        s.buf[1].as<uint64_t>(), s.sel.as<uint8_t>(), s.cnt.as<int64_t>(),
-                       s.newcnt.as<unsigned long long>(), s.fail.as<uint8_t>());
+                       s.newcnt.as<unsigned long long>(), s.fail.as<uint8_t>(),
+                       s.ctr.as<unsigned long long>() + 2);
     const int nl = pass == 0 ? P : (int)plist.size();
     hipLaunchKernelGGL(k_part_commit, dim3(ceil_div(std::max(nl, 1), 256)), dim3(256), 0, a->stream, P,
                        s.pbase.as<int64_t>(), pass == 0 ? nullptr : s.work.as<uint32_t>() + work.size(), nl,
@@ -737,8 +857,8 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                        s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>());
     KHIP_TRY_HIP(hipGetLastError());
     if (pass == 0) ev_record_part(a, 3);
-    unsigned long long c2[2];
-    KHIP_TRY_HIP(hipMemcpyAsync(c2, s.ctr.p, 16, hipMemcpyDeviceToHost, a->stream));
+    unsigned long long c2[3];
+    KHIP_TRY_HIP(hipMemcpyAsync(c2, s.ctr.p, 24, hipMemcpyDeviceToHost, a->stream));
     KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
     added_total += (int64_t)c2[0];
     if (c2[1] == 0) break;
@@ -758,7 +878,9 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
       if (sbits[p] > 12) return fail(KHIP_E_DEVICE, "partition needs more than 4096 sub-passes (extreme key skew)");
       for (int k = 0; k < (1 << sbits[p]); k++) work.push_back((uint32_t)p | ((uint32_t)sbits[p] << 16) | ((uint32_t)k << 20));
     }
-    if (grow) KHIP_TRY(part_regrow(a, s.cmax * 2));
+    // grow straight to what the largest overflowing partition needed (sub-passes of one
+    // partition append to the same region, so its full row count is at least `need`)
+    if (grow) KHIP_TRY(part_regrow(a, next_pow2(std::max<int64_t>(s.cmax * 2, (int64_t)c2[2] * 5 / 4 + 64))));
     std::vector<uint32_t> both(work);
     both.insert(both.end(), plist.begin(), plist.end());
     KHIP_TRY(s.work.ensure(both.size() * 4));
