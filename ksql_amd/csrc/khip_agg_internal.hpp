@@ -191,6 +191,8 @@ __device__ __forceinline__ bool having_ok(const uint64_t* s, const HavingDev& h)
 __global__ void k_scan_blocks(const int64_t* __restrict__ blockmax, int64_t nb, int64_t* __restrict__ prefix,
                               int64_t* __restrict__ stream_time);
 __global__ void k_scan_excl(int64_t* __restrict__ v, int64_t n, int64_t* __restrict__ total);
+__global__ void k_compact(const uint64_t* __restrict__ table, int64_t cap, int sw, HavingDev h,
+                          uint64_t* __restrict__ out, int64_t max_rows, unsigned long long* __restrict__ counter);
 
 struct InitWords {
   int64_t w[32];
@@ -212,6 +214,10 @@ struct PartState {
   DevBuf skey, sts, smeta, scol[MAX_COLS];  // skey: AoS (key, ts) 16-byte records
   DevBuf work;            // retry work items
   int64_t scat_cap = 0;
+  // closed windows (ws + size <= streamTime - grace): never updated again, moved out of the
+  // partition regions into an append-only store so the live table stays LDS-sized
+  DevBuf closed, closed_ctr;
+  int64_t closed_cap = 0, closed_n = 0;
 };
 
 }  // namespace khip

@@ -355,7 +355,9 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
                                                          const int64_t* __restrict__ cnt,
                                                          unsigned long long* __restrict__ newcnt,
                                                          uint8_t* __restrict__ fail,
-                                                         unsigned long long* __restrict__ need) {
+                                                         unsigned long long* __restrict__ need, int64_t close0,
+                                                         uint64_t* __restrict__ closed,
+                                                         unsigned long long* __restrict__ closed_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = q.H;
   lds_u32* lref = (lds_u32*)smem;
@@ -397,12 +399,48 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
     lovf = 0;
   }
   __syncthreads();
-  // 1. resident rows of this partition (distinct groups: insert without comparing)
+  // 1. resident rows of this partition (distinct groups: insert without comparing).  Rows of
+  //    windows already closed before this push (ws + size <= close0) go to the closed store.
   const uint64_t* src = (sel[p] ? buf1 : buf0) + (uint64_t)p * q.cmax * q.sw;
   const int64_t nrow = cnt[p];
+  const bool evict = q.windowed && close0 != INT64_MIN;
+  // the first pass moves the closed rows; a retried partition already moved them (its region
+  // still holds them until it succeeds), so retries only skip them
+  if (evict && !work) {
+    int ne = 0;
+    for (int64_t r = threadIdx.x; r < nrow; r += AG_THREADS) {
+      const uint64_t* row = src + r * q.sw;
+      ne += ((int64_t)row[1] + q.size <= close0) && part_sub_ok(group_hash((int64_t)row[0], (int64_t)row[1]), sbits, sub);
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int incl = ne;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += y;
+    }
+    if (lane == 63) lcnt[wave] = incl;
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int w = 0; w < AG_THREADS / 64; w++) {
+      if (w < wave) before += lcnt[w];
+      total += lcnt[w];
+    }
+    if (threadIdx.x == 0) lbase = total ? atomicAdd(closed_n, (unsigned long long)total) : 0ULL;
+    __syncthreads();
+    uint64_t* dst = closed + (lbase + (uint64_t)(before + incl - ne)) * q.sw;
+    for (int64_t r = threadIdx.x; r < nrow; r += AG_THREADS) {
+      const uint64_t* row = src + r * q.sw;
+      if (!((int64_t)row[1] + q.size <= close0) || !part_sub_ok(group_hash((int64_t)row[0], (int64_t)row[1]), sbits, sub))
+        continue;
+      for (int w = 0; w < q.sw; w++) dst[w] = row[w];
+      dst += q.sw;
+    }
+    __syncthreads();
+  }
   for (int64_t r = threadIdx.x; r < nrow; r += AG_THREADS) {
     const uint64_t* row = src + r * q.sw;
     const int64_t key = (int64_t)row[0], ws = (int64_t)row[1];
+    if (evict && ws + q.size <= close0) continue;
     const uint64_t h = group_hash(key, ws);
     if (!part_sub_ok(h, sbits, sub)) continue;
     if (atomicAdd(&lused, 1) >= q.H_eff) {
@@ -671,7 +709,8 @@ khip_status part_init(khip_agg* a, int64_t hint) {
 
 void part_release(khip_agg* a) {
   PartState& s = a->part;
-  DevBuf* bufs[] = {&s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist, &s.tilemax, &s.tilemin,
+  DevBuf* bufs[] = {&s.closed, &s.closed_ctr, &s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist,
+                    &s.tilemax, &s.tilemin,
                     &s.tileprefix, &s.tpart, &s.scan_tmp, &s.skey, &s.sts, &s.smeta, &s.work,
                     &s.pbase, &s.R, &s.ctr, &s.counts};
   for (DevBuf* b : bufs) b->release();
@@ -680,6 +719,7 @@ void part_release(khip_agg* a) {
 
 khip_status part_reset(khip_agg* a) {
   PartState& s = a->part;
+  s.closed_n = 0;
   KHIP_TRY_HIP(hipMemsetAsync(s.cnt.p, 0, s.P * 8, a->stream));
   KHIP_TRY_HIP(hipMemsetAsync(s.newcnt.p, 0, s.P * 8, a->stream));
   KHIP_TRY_HIP(hipMemsetAsync(s.fail.p, 0, s.P, a->stream));
@@ -833,6 +873,24 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   ev_record_part(a, 2);
   // 4. aggregate partitions (+ retries)
   const PartAggParams q0 = part_params(a);
+  const int64_t close0 = (a->windowed && a->host_stream_time >= 0) ? a->host_stream_time - a->grace : INT64_MIN;
+  if (a->windowed) {  // worst case every live row closes in this push
+    const int64_t live = a->occ - s.closed_n;
+    if (s.closed_cap < s.closed_n + live) {
+      const int64_t ncap = next_pow2(std::max<int64_t>(1024, s.closed_n + live));
+      DevBuf nc;
+      KHIP_TRY(nc.ensure((size_t)ncap * a->sw * 8));
+      if (s.closed_n)
+        KHIP_TRY_HIP(hipMemcpyAsync(nc.p, s.closed.p, (size_t)s.closed_n * a->sw * 8, hipMemcpyDeviceToDevice, a->stream));
+      KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+      s.closed.release();
+      s.closed = nc;
+      nc.p = nullptr;
+      s.closed_cap = ncap;
+    }
+    KHIP_TRY(s.closed_ctr.ensure(8));
+    KHIP_TRY_HIP(hipMemcpyAsync(s.closed_ctr.p, &s.closed_n, 8, hipMemcpyHostToDevice, a->stream));
+  }
   int64_t added_total = 0;
   std::vector<uint8_t> host_fail;
   std::vector<int> sbits(P, 0);
@@ -849,7 +907,8 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                        has_meta ? s.smeta.as<uint32_t>() : nullptr, sc, s.buf[0].as<uint64_t>(),
                        s.buf[1].as<uint64_t>(), s.sel.as<uint8_t>(), s.cnt.as<int64_t>(),
                        s.newcnt.as<unsigned long long>(), s.fail.as<uint8_t>(),
-                       s.ctr.as<unsigned long long>() + 2);
+                       s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
+                       s.closed_ctr.as<unsigned long long>());
     const int nl = pass == 0 ? P : (int)plist.size();
     hipLaunchKernelGGL(k_part_commit, dim3(ceil_div(std::max(nl, 1), 256)), dim3(256), 0, a->stream, P,
                        s.pbase.as<int64_t>(), pass == 0 ? nullptr : s.work.as<uint32_t>() + work.size(), nl,
@@ -887,6 +946,12 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     KHIP_TRY_HIP(hipMemcpyAsync(s.work.p, both.data(), both.size() * 4, hipMemcpyHostToDevice, a->stream));
   }
   // 5. counters
+  if (a->windowed) {
+    int64_t cn = 0;
+    KHIP_TRY_HIP(hipMemcpy(&cn, s.closed_ctr.p, 8, hipMemcpyDeviceToHost));
+    added_total += cn - s.closed_n;  // evicted rows left the live regions but are still groups
+    s.closed_n = cn;
+  }
   std::vector<int64_t> tp((size_t)nT * T_NPART);
   KHIP_TRY_HIP(hipMemcpy(tp.data(), s.tpart.p, tp.size() * 8, hipMemcpyDeviceToHost));
   int64_t c[T_NPART] = {0};
@@ -914,13 +979,31 @@ khip_status part_compact(khip_agg* a, const HavingDev& h, std::vector<uint64_t>*
   hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, a->stream, s.counts.as<int64_t>(), (int64_t)P,
                      s.counts.as<int64_t>() + P);
   KHIP_TRY_HIP(hipGetLastError());
-  int64_t n = 0;
-  KHIP_TRY_HIP(hipMemcpyAsync(&n, s.counts.as<int64_t>() + P, 8, hipMemcpyDeviceToHost, a->stream));
+  int64_t nl = 0;
+  KHIP_TRY_HIP(hipMemcpyAsync(&nl, s.counts.as<int64_t>() + P, 8, hipMemcpyDeviceToHost, a->stream));
+  // closed rows (flat store) passing h
+  DevBuf cctr;
+  KHIP_TRY(cctr.ensure(8));
+  KHIP_TRY_HIP(hipMemsetAsync(cctr.p, 0, 8, a->stream));
+  if (s.closed_n) {
+    hipLaunchKernelGGL(k_compact, dim3((int)std::min<int64_t>(ceil_div(s.closed_n, 256), 4096)), dim3(256), 0, a->stream,
+                       s.closed.as<uint64_t>(), s.closed_n, a->sw, h, (uint64_t*)nullptr, (int64_t)0,
+                       cctr.as<unsigned long long>());
+  }
+  int64_t nc = 0;
+  KHIP_TRY_HIP(hipMemcpyAsync(&nc, cctr.p, 8, hipMemcpyDeviceToHost, a->stream));
   KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  const int64_t n = nl + nc;
   *count = n;
   if (!rows) return KHIP_OK;
   DevBuf out;
   KHIP_TRY(out.ensure((size_t)std::max<int64_t>(n, 1) * a->sw * 8));
+  if (nc) {
+    KHIP_TRY_HIP(hipMemsetAsync(cctr.p, 0, 8, a->stream));
+    hipLaunchKernelGGL(k_compact, dim3((int)std::min<int64_t>(ceil_div(s.closed_n, 256), 4096)), dim3(256), 0, a->stream,
+                       s.closed.as<uint64_t>(), s.closed_n, a->sw, h, out.as<uint64_t>() + (size_t)nl * a->sw, nc,
+                       cctr.as<unsigned long long>());
+  }
   hipLaunchKernelGGL(k_part_rows, dim3(P), dim3(256), 0, a->stream, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
                      s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.cmax, a->sw, h, nullptr, s.counts.as<int64_t>(),
                      out.as<uint64_t>());
