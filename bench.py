@@ -17,8 +17,9 @@ k with k % N == r (key-hash sharding = Kafka partitioning) and processes its own
 records with its own stream time (one Kafka task per partition): no data-path
 collective.  value = all records / max-over-ranks time.
 
-Output: one JSON line (rank 0) with `roofline` for the dominant kernel (k_apply, timed
-with HIP events on the library's own stream) and `cpu_baseline` (the C oracle, a
+Output: one JSON line (rank 0) with `roofline` for the hot path (the device time of every
+kernel of one push, HIP events on the library's own stream; per-kernel breakdown with each
+kernel's own streamed bytes) and `cpu_baseline` (the C oracle, a
 single-threaded restatement of the reference semantics — the JVM reference cannot run
 on this image — timed on a bounded prefix of the same workload).
 """
@@ -76,11 +77,13 @@ def cpu_baseline(n_total, keys, target_s):
             "sample": "first %d of the %d possible_fraud records (C oracle, 1 thread, %.1f s)" % (m, n_total, dt)}
 
 
-def load_traffic(path, n):
+def load_traffic(path, n, engine):
+    """HBM bytes per push from the committed PMC summary (tools/pmc_traffic.py), if it was
+    measured on this workload size and engine."""
     try:
         with open(path) as f:
             t = json.load(f)
-        rec = t.get("possible_fraud", {}).get("k_apply")
+        rec = t.get("possible_fraud", {}).get("push" if engine == "part" else "k_apply")
         if rec and rec.get("records") == n:
             return rec["hbm_bytes_per_launch"]
     except (OSError, ValueError):
@@ -140,6 +143,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kt = h.kernel_times()
+    groups = int(h.count_rows(None))
 
     # PCIe-inclusive rate (host-resident input, one step) for DESIGN.md — not `value`
     pcie = None
@@ -155,9 +159,18 @@ def main():
     if rank == 0:
         ms_step = elapsed * 1000.0 / args.steps
         value = world * n * args.steps / elapsed
-        apply_ms = kt["apply_ms"] / max(kt["apply_launches"], 1)
-        achieved = BYTES_PER_RECORD_C2 * n / (apply_ms / 1000.0) / 1e9
-        traffic = load_traffic(args.traffic_json, n)
+        launches = max(kt["apply_launches"], 1)
+        phase = {k: kt[k] / launches for k in ("stream_time_ms", "partition_ms", "apply_ms", "finalize_ms")}
+        push_ms = sum(phase.values())  # device time of every kernel of one push (HIP events)
+        achieved = BYTES_PER_RECORD_C2 * n / (push_ms / 1000.0) / 1e9
+        traffic = load_traffic(args.traffic_json, n, args.engine)
+        # each kernel's own algorithmic streams (bytes / record) for the breakdown
+        own = ({"stream_time_ms": 16, "partition_ms": 32, "apply_ms": 16 + 32.0 * groups / n, "finalize_ms": 0}
+               if args.engine == "part" else
+               {"stream_time_ms": 8, "partition_ms": 0, "apply_ms": 80, "finalize_ms": 0})
+        per_kernel = {k: {"ms": phase[k], "bytes_per_record": own[k],
+                          "GB/s": own[k] * n / (phase[k] / 1000.0) / 1e9 if phase[k] > 0 else None}
+                      for k in phase if phase[k] > 0}
         out = {
             "metric": "records/sec, windowed GROUP BY (COUNT(*) TUMBLING 5 s GROUP BY card_number HAVING > 3)",
             "value": value,
@@ -173,14 +186,15 @@ def main():
             "data": "synthetic (splitmix64, ksql_amd/synth.py), device-resident columnar batch",
             "config": {"workload": "possible_fraud", "records_per_gpu": n, "keys_per_gpu": args.keys,
                        "window": "TUMBLING 5s, grace default", "having": "COUNT(*) > 3",
-                       "groups_per_gpu": int(h.count_rows(None)), "having_rows_per_gpu": int(rows),
+                       "groups_per_gpu": groups, "having_rows_per_gpu": int(rows),
                        "parallelism": "key-hash shards x%d" % world},
-            "roofline": {"bound": "hbm", "kernel": "k_apply", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "algorithmic_bytes_per_record": BYTES_PER_RECORD_C2, "apply_ms_per_launch": apply_ms,
-                         "engine": args.engine,
-                         "phase_ms_per_step": {k: kt[k] / max(args.steps, 1) for k in
-                                               ("stream_time_ms", "partition_ms", "apply_ms", "finalize_ms")}},
+            "roofline": {"bound": "hbm",
+                         "kernel": ("khip_agg_push = k_part_hist + scans + k_part_scatter + k_part_agg + commit"
+                                    if args.engine == "part" else "khip_agg_push (k_apply dominant)"),
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes_per_record": BYTES_PER_RECORD_C2, "push_ms": push_ms,
+                         "engine": args.engine, "per_kernel": per_kernel},
             "pcie_inclusive_records_per_s": pcie,
         }
         if world == 1 and not args.no_cpu_baseline:

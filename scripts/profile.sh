@@ -16,3 +16,6 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $OUT/fetch.log 2>&1 || { tail -20 $OUT/fetch.log; exit 6; }
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $OUT/write.log 2>&1 || { tail -20 $OUT/write.log; exit 7; }
 find $OUT -name '*.csv' | head -20
+python3 tools/rocprof_summary.py stats $OUT/trace/run_kernel_stats.csv > $OUT/kernel_stats.md
+python3 tools/pmc_traffic.py $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv 100000000 $OUT/traffic.json
+cat $OUT/kernel_stats.md | head -14
