@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     ap.add_argument("--engine", choices=["part", "atomic"], default="part")
+    ap.add_argument("--config", choices=["possible_fraud", "repartition_sum"], default="possible_fraud",
+                    help="possible_fraud = BASELINE configs[1] (the headline); repartition_sum = configs[4]")
     return ap.parse_args()
 
 
@@ -104,6 +106,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     lib = abi.load_product()
+    if args.config == "repartition_sum":
+        return bench_repartition(args, lib, rank, world, local)
 
     n = args.records
     card, ts = synth.possible_fraud(0, n, n, xp="torch", device="cuda", rank=rank, world=world, keys=args.keys)
@@ -203,6 +207,118 @@ def main():
             out["cpu_baseline"] = None
         print(json.dumps(out))
     h.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+BYTES_PER_RECORD_C5 = 136  # read 24 + pack 24 + recv 24 + 2 x 32 (slot)
+
+
+def bench_repartition(args, lib, rank, world, local):
+    """C5: GROUP BY region_id (a value column) forces the repartition.  One step per rank:
+    khip_shuffle_pack (Kafka partitioner) → RCCL count exchange + all-to-all over xGMI (N>1)
+    → khip_shuffle_unpack → SUM(amount) TUMBLING 1 MINUTE push → row count.  Weak scaling:
+    every rank owns one source partition of `records` records (1e9 node-wide at N=8 with the
+    default 125M)."""
+    import torch
+    import torch.distributed as dist
+    from ksql_amd import abi, synth
+    from ksql_amd.repartition import Repartition
+
+    n = args.records if args.records != 100_000_000 else 125_000_000
+    eid, ts, region, amount = synth.repartition_sum(0, n, n, xp="torch", device="cuda", rank=rank, world=world)
+    torch.cuda.synchronize()
+    src = abi.DeviceBatch(ts, cols=[region, amount])
+    comm = None
+    if world > 1:
+        obj = [abi.comm_unique_id(lib) if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm = abi.Comm(lib, world, rank, obj[0], local)
+    rp = Repartition(lib, 0, ["INT64", "INT64"], rank=rank, world=world, comm=comm, device=local)
+    desc = abi.make_agg_desc(window_kind="TUMBLING", size_ms=60_000, key_type="INT64", col_types=["INT64", "INT64"],
+                             aggs=[("SUM", 1)], device=local, capacity_hint=60 * 1_000_000 // max(world, 1),
+                             flags=abi.FLAG_PROFILE)
+    h = abi.AggHandle(lib, desc)
+    phases = {"pack": 0.0, "exchange_unpack": 0.0, "aggregate": 0.0}
+
+    def step(timed=False):
+        t0 = time.perf_counter()
+        send, counts = rp.shuffle.pack(src)
+        t1 = time.perf_counter()
+        if world > 1:
+            recv, rc = comm.alltoall(send, counts, rp.shuffle.row_words)
+        else:
+            recv, rc = send, counts
+        m = int(sum(rc))
+        key, kts, cols, valid = rp.shuffle.unpack(recv, m)
+        t2 = time.perf_counter()
+        h.reset()
+        st = h.push(abi.DeviceBatch(kts, keys=key, cols=cols, col_valid=valid))
+        rows = h.count_rows(None)
+        t3 = time.perf_counter()
+        if timed:
+            phases["pack"] += t1 - t0
+            phases["exchange_unpack"] += t2 - t1
+            phases["aggregate"] += t3 - t2
+        return st, rows, m
+
+    for _ in range(max(args.warmup, 1)):
+        st, rows, m = step()
+    assert st["rows_accepted"] == m, st
+    h.kernel_times(reset=True)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    recv_total = 0
+    for _ in range(args.steps):
+        st, rows, m = step(timed=True)
+        recv_total += m
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kt = h.kernel_times()
+    if rank == 0:
+        ms_step = elapsed * 1000.0 / args.steps
+        per = {k: v * 1000.0 / args.steps for k, v in phases.items()}
+        achieved = BYTES_PER_RECORD_C5 * n / (ms_step / 1000.0) / 1e9
+        launches = max(kt["apply_launches"], 1)
+        push_ms = sum(kt[k] for k in ("stream_time_ms", "partition_ms", "apply_ms", "finalize_ms")) / launches
+        out = {
+            "metric": "records/sec, non-key GROUP BY with repartition (SUM(amount) TUMBLING 1 MINUTE GROUP BY region_id)",
+            "value": world * n * args.steps / elapsed,
+            "unit": "records/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (splitmix64, ksql_amd/synth.py repartition_sum), device-resident columnar batch",
+            "config": {"workload": "repartition_sum", "records_per_gpu": n, "regions": 1_000_000,
+                       "window": "TUMBLING 1 MINUTE", "parallelism": "repartition all-to-all x%d" % world,
+                       "rows_received_rank0": m, "groups_rank0": int(rows)},
+            "roofline": {"bound": "hbm", "kernel": "whole step: pack + all-to-all + unpack + khip_agg_push",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": None, "algorithmic_bytes_per_record": BYTES_PER_RECORD_C5,
+                         "phase_ms": per, "push_device_ms": push_ms},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(out))
+    h.close()
+    rp.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -17,6 +17,10 @@
  *     caller pointer after the call returns.  KHIP_MEM_DEVICE batches are read on
  *     the handle's stream and must stay valid until the call returns (aggregate
  *     push) or until the handle's *_sync() returns (asynchronous probes).
+ *     The handle's stream is a BLOCKING HIP stream: its work is ordered after work
+ *     the caller queued on the legacy default stream (torch's default stream), so
+ *     a device batch produced there needs no extra synchronisation.  A producer on
+ *     any other stream must be synchronised (or waited on) before the call.
  *   - Handles are independent; a single handle is not re-entrant (Kafka Streams
  *     task confinement, C/util/KsqlConstants.java:42 — one task per thread).
  *   - Validity bitmaps are Arrow-style: bit (i & 7) of byte (i >> 3), 1 = valid.
@@ -320,6 +324,73 @@ khip_status khip_table_probe_device(khip_table* t, const khip_batch* stream,
 
 khip_status khip_table_sync(khip_table* t);
 khip_status khip_table_destroy(khip_table* t);
+
+/* ------------------------------------------------ repartition (non-key GROUP BY) */
+
+/* The repartition topic that StreamGroupByBuilderBase.build inserts for a non-key GROUP BY or
+ * PARTITION BY (S/StreamGroupByBuilderBase.java:101-103, S/StreamSelectKeyBuilder.java:73-74):
+ * every record is re-keyed by a value column and routed to the partition Kafka's default
+ * partitioner gives it: toPositive(murmur2(KAFKA-format key bytes)) % n_parts, the key bytes
+ * being big-endian 4 (INT) / 8 (BIGINT) bytes (ksqldb-serde/.../kafka/KafkaSerdeFactory.java:42-43;
+ * kafka-clients Utils.murmur2).  Null-value records and records whose new key is null are dropped
+ * (S/GroupByParamsFactory.java:92-100).  Packed row (u64 words, 2 + n_cols of them):
+ *   [new key][ts][value columns except key_col (raw, INT32 sign-extended)...]
+ *   [validity bits: column c = bit c; the key column's bit is always set]
+ * Order is stable: a destination receives each source's rows in arrival order. */
+typedef struct khip_shuffle_desc {
+  int32_t n_parts;          /* destinations (tasks / GPUs)                                */
+  int32_t key_col;          /* value column that becomes the new key (INT32/INT64)        */
+  int32_t n_cols;           /* value columns carried (all of the batch's columns)         */
+  const int32_t* col_types;
+  int32_t device;
+  int32_t flags;
+} khip_shuffle_desc;
+
+typedef struct khip_shuffle khip_shuffle;
+
+khip_status khip_shuffle_create(const khip_shuffle_desc* desc, khip_shuffle** out);
+
+/* Words per packed row (2 + n_cols). */
+int32_t khip_shuffle_row_words(const khip_shuffle* s);
+
+/* Partition a DEVICE batch into the caller's device buffer `send` (capacity rows x row
+ * words), grouped by destination; counts[n_parts] (host) receives the rows per destination
+ * (destination d's rows start at the sum of counts[0..d)). */
+khip_status khip_shuffle_pack(khip_shuffle* s, const khip_batch* in, uint64_t* send,
+                              int64_t capacity, int64_t* counts);
+
+/* Packed rows (device) → columnar device arrays owned by the caller: key[n], ts[n],
+ * col_data[c][n] (8-byte raw for every column type except INT32 = 4 bytes) and
+ * col_valid[c] bitmaps ((n+7)/8 bytes; may be NULL).  The result is a khip_batch whose
+ * records are the received rows in (source, arrival) order. */
+khip_status khip_shuffle_unpack(khip_shuffle* s, const uint64_t* rows, int64_t n, int64_t* key,
+                                int64_t* ts, void* const* col_data, uint8_t* const* col_valid);
+
+khip_status khip_shuffle_sync(khip_shuffle* s);
+khip_status khip_shuffle_destroy(khip_shuffle* s);
+
+/* RCCL communicator, one rank per GPU (one process per GPU).  The 128-byte unique id is
+ * created on rank 0 and distributed by the caller (the Kafka/ksqlDB control plane, or
+ * torch.distributed in bench.py). */
+typedef struct khip_comm khip_comm;
+#define KHIP_COMM_ID_BYTES 128
+khip_status khip_comm_unique_id(uint8_t id[KHIP_COMM_ID_BYTES]);
+khip_status khip_comm_init(int32_t nranks, int32_t rank, const uint8_t id[KHIP_COMM_ID_BYTES],
+                           int32_t device, khip_comm** out);
+
+/* Collective, step 1: exchange the per-peer row counts (send_counts[nranks] host →
+ * recv_counts[nranks] host), so every rank can size its receive buffer. */
+khip_status khip_comm_exchange_counts(khip_comm* c, const int64_t* send_counts, int64_t* recv_counts);
+
+/* Collective, step 2: all-to-all of packed rows over xGMI (grouped ncclSend/ncclRecv, one pair
+ * per peer, no ring): send rows grouped by destination with send_counts[nranks]; recv_counts
+ * are the ones step 1 returned and recv must hold their sum; the received rows are laid out by
+ * source rank.  A capacity error here is a caller bug that leaves the peers blocked, so size
+ * recv from step 1. */
+khip_status khip_comm_alltoall(khip_comm* c, const uint64_t* send, const int64_t* send_counts,
+                               uint64_t* recv, int64_t recv_capacity, const int64_t* recv_counts,
+                               int32_t row_words);
+khip_status khip_comm_destroy(khip_comm* c);
 
 /* ------------------------------------------------------------ diagnostics */
 

@@ -101,6 +101,13 @@ class JoinOut(C.Structure):
                 ("col_null", C.POINTER(C.c_void_p))]
 
 
+class ShuffleDesc(C.Structure):
+    _fields_ = [("n_parts", i32), ("key_col", i32), ("n_cols", i32), ("col_types", C.POINTER(i32)),
+                ("device", i32), ("flags", i32)]
+
+
+COMM_ID_BYTES = 128
+
 _P = C.c_void_p
 SIGS = {
     "agg_create": ([C.POINTER(AggDesc), C.POINTER(_P)]),
@@ -123,6 +130,16 @@ PRODUCT_ONLY = {
     "agg_kernel_times": ([_P, C.POINTER(KernelTimes), i32]),
     "table_probe_device": ([_P, C.POINTER(Batch), i32, C.POINTER(Where), C.POINTER(JoinDevOut), C.POINTER(i64)]),
     "table_sync": ([_P]),
+    "shuffle_create": ([C.POINTER(ShuffleDesc), C.POINTER(_P)]),
+    "shuffle_pack": ([_P, C.POINTER(Batch), _P, i64, C.POINTER(i64)]),
+    "shuffle_unpack": ([_P, _P, i64, _P, _P, C.POINTER(_P), C.POINTER(_P)]),
+    "shuffle_sync": ([_P]),
+    "shuffle_destroy": ([_P]),
+    "comm_unique_id": ([C.POINTER(C.c_uint8)]),
+    "comm_init": ([i32, i32, C.POINTER(C.c_uint8), i32, C.POINTER(_P)]),
+    "comm_exchange_counts": ([_P, C.POINTER(i64), C.POINTER(i64)]),
+    "comm_alltoall": ([_P, _P, C.POINTER(i64), _P, i64, C.POINTER(i64), i32]),
+    "comm_destroy": ([_P]),
 }
 
 
@@ -153,6 +170,13 @@ class Lib:
             self.dll.khip_last_error.argtypes = []
             self.dll.khip_abi_version.restype = i32
             self.dll.khip_build_target.restype = C.c_char_p
+            self.dll.khip_shuffle_row_words.restype = i32
+            self.dll.khip_shuffle_row_words.argtypes = [_P]
+        else:
+            self.dll.oracle_kafka_partition.argtypes = [_P, i64, i32, i32, _P]
+            self.dll.oracle_kafka_partition.restype = None
+            self.dll.oracle_murmur2.argtypes = [C.c_char_p, i32]
+            self.dll.oracle_murmur2.restype = i32
 
     def check(self, status, what):
         if status != KHIP_OK:
@@ -392,6 +416,103 @@ class TableHandle:
     def close(self):
         if self.h:
             self.lib.table_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ShuffleHandle:
+    """Repartition of a device batch by a value column (khip_shuffle_*), the device side of
+    the repartition topic StreamGroupByBuilderBase inserts for a non-key GROUP BY."""
+
+    def __init__(self, lib, n_parts, key_col, col_types, device=0):
+        self.lib = lib
+        self.col_types = [TYPE[t] if isinstance(t, str) else t for t in col_types]
+        self._ct = (i32 * len(self.col_types))(*self.col_types)
+        self.desc = ShuffleDesc(n_parts, key_col, len(self.col_types), self._ct, device, 0)
+        self.n_parts = n_parts
+        self.device = device
+        self.h = C.c_void_p()
+        lib.check(lib.shuffle_create(C.byref(self.desc), C.byref(self.h)), "shuffle_create")
+        self.row_words = lib.dll.khip_shuffle_row_words(self.h)
+
+    def pack(self, batch, send=None):
+        """Returns (send rows tensor [rows, row_words] uint64-as-int64, counts list)."""
+        import torch
+        counts = (i64 * self.n_parts)()
+        cap = 0 if send is None else send.shape[0]
+        st = self.lib.shuffle_pack(self.h, C.byref(batch.struct), None if send is None else send.data_ptr(),
+                                   cap, counts)
+        if st == KHIP_E_BUFFER:
+            send = torch.empty((max(sum(counts), 1), self.row_words), dtype=torch.int64,
+                               device=torch.device("cuda", self.device))
+            st = self.lib.shuffle_pack(self.h, C.byref(batch.struct), send.data_ptr(), send.shape[0], counts)
+        self.lib.check(st, "shuffle_pack")
+        return send, list(counts)
+
+    def unpack(self, rows, n):
+        """Packed rows → (key, ts, cols, col_valid bitmaps) device tensors."""
+        import torch
+        dev = torch.device("cuda", self.device)
+        key = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        ts = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        tdt = {0: torch.int32, 1: torch.int64, 2: torch.float64}
+        cols = [torch.empty(max(n, 1), dtype=tdt[t], device=dev) for t in self.col_types]
+        valid = [torch.empty(max((n + 7) // 8, 1), dtype=torch.uint8, device=dev) for _ in self.col_types]
+        cd = (C.c_void_p * len(cols))(*[c.data_ptr() for c in cols])
+        cv = (C.c_void_p * len(cols))(*[v.data_ptr() for v in valid])
+        self.lib.check(self.lib.shuffle_unpack(self.h, None if rows is None else rows.data_ptr(), n,
+                                               key.data_ptr(), ts.data_ptr(), cd, cv), "shuffle_unpack")
+        return key[:n], ts[:n], [c[:n] for c in cols], [v[:(n + 7) // 8] for v in valid]
+
+    def close(self):
+        if self.h:
+            self.lib.shuffle_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def comm_unique_id(lib):
+    buf = (C.c_uint8 * COMM_ID_BYTES)()
+    lib.check(lib.comm_unique_id(buf), "comm_unique_id")
+    return bytes(buf)
+
+
+class Comm:
+    """RCCL communicator owned by the library (one rank per GPU)."""
+
+    def __init__(self, lib, nranks, rank, uid, device):
+        self.lib = lib
+        self.nranks = nranks
+        self.device = device
+        self.h = C.c_void_p()
+        idb = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        lib.check(lib.comm_init(nranks, rank, idb, device, C.byref(self.h)), "comm_init")
+
+    def alltoall(self, send, send_counts, row_words):
+        """Two collective steps: exchange counts, then the rows.  Returns (recv, recv_counts)."""
+        import torch
+        sc = (i64 * self.nranks)(*send_counts)
+        rc = (i64 * self.nranks)()
+        self.lib.check(self.lib.comm_exchange_counts(self.h, sc, rc), "comm_exchange_counts")
+        recv = torch.empty((max(sum(rc), 1), row_words), dtype=torch.int64, device=torch.device("cuda", self.device))
+        sp = None if send is None else send.data_ptr()
+        self.lib.check(self.lib.comm_alltoall(self.h, sp, sc, recv.data_ptr(), recv.shape[0], rc, row_words),
+                       "comm_alltoall")
+        return recv, list(rc)
+
+    def close(self):
+        if self.h:
+            self.lib.comm_destroy(self.h)
             self.h = C.c_void_p()
 
     def __del__(self):

@@ -695,7 +695,7 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
     return st;
   }
   DeviceGuard g(a->device);
-  if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&a->stream, hipStreamDefault) != hipSuccess) {
     delete a;
     return fail(KHIP_E_DEVICE, "hipStreamCreate failed (no device?)");
   }

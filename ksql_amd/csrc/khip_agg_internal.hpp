@@ -211,7 +211,13 @@ struct PartState {
   DevBuf buf[2];          // region storage: P x cmax rows x sw words, double buffered
   DevBuf sel, cnt, newcnt, fail;  // per partition: buffer select, rows, rows being written, flags
   DevBuf hist, tilemax, tilemin, tileprefix, tpart, scan_tmp;
-  DevBuf skey, sts, smeta, scol[MAX_COLS];  // skey: AoS (key, ts) 16-byte records
+  // scattered records, AoS, rw u64 words each: key, ts (-1 = no window applied),
+  // [meta = jlo | validity << 16, if meta_word = 2], [the referenced value columns], pad to even
+  DevBuf srec;
+  int rw = 2, meta_word = -1;
+  uint32_t vcols = 0;
+  int8_t col_word[MAX_COLS] = {-1, -1, -1, -1, -1, -1, -1, -1};
+  std::vector<uint8_t> psbits;  // learned sub-pass bits per partition (pass 0 starts there)
   DevBuf work;            // retry work items
   int64_t scat_cap = 0;
   // closed windows (ws + size <= streamTime - grace): never updated again, moved out of the

@@ -44,13 +44,22 @@ struct ColTypes {
   int32_t t[MAX_COLS];
 };
 
+struct RecLayout {
+  int32_t rw, meta_word;
+  uint32_t vcols;  // columns whose validity bit goes into meta
+  int8_t col_word[MAX_COLS];
+  int8_t word_col[2 + 1 + MAX_COLS + 1];  // word → column (-1: key/ts/meta/pad)
+};
+
 struct PartAggParams {
   int32_t windowed;
   int32_t nwords;  // 3 + state words actually used
   int32_t sw;      // row stride (u64 words) in regions
   int32_t H;
   int32_t H_eff;
-  int32_t has_meta;
+  int32_t rw;         // scattered record stride (u64 words)
+  int32_t meta_word;  // 2 or -1
+  int8_t col_word[MAX_COLS];
   int64_t size, adv;
   int64_t cmax;
   int32_t n_cols;
@@ -183,21 +192,25 @@ __global__ __launch_bounds__(256) void k_part_colprefix(uint32_t* __restrict__ h
 }
 
 __device__ __forceinline__ void scatter_one(int64_t key, int64_t x, int64_t jlo, int64_t i, int log2P, uint32_t* cur,
-                                            longlong2* __restrict__ srec, int has_meta, uint32_t* __restrict__ smeta,
-                                            const ColPtrs& cols, int n_cols, const ColTypes& ctypes,
-                                            const ColPtrs& scols, bool applied) {
+                                            uint64_t* __restrict__ srec, const RecLayout& L, const ColPtrs& cols,
+                                            int n_cols, const ColTypes& ctypes, bool applied) {
   const uint32_t pos = atomicAdd(&cur[part_of(key, log2P)], 1u);
-  longlong2 rec;
-  rec.x = key;
-  rec.y = applied ? x : -1;
-  srec[pos] = rec;  // one 16-byte store per record
-  if (has_meta) {
+  uint64_t* r = srec + (uint64_t)pos * L.rw;
+  *(longlong2*)r = make_longlong2(key, applied ? x : -1);  // one 16-byte store
+  if (L.rw > 2) {  // then the rest of the record, 16 bytes at a time, contiguous
     uint32_t vm = 0;
-    for (int c = 0; c < n_cols; c++) vm |= (bit_get(cols.valid[c], i) ? 1u : 0u) << c;
-    smeta[pos] = (uint32_t)jlo | (vm << 16);
+    for (int c = 0; c < n_cols; c++)
+      if ((L.vcols >> c) & 1u) vm |= (bit_get(cols.valid[c], i) ? 1u : 0u) << c;
+    for (int w = 2; w < L.rw; w += 2) {
+      int64_t v[2];
+      for (int k = 0; k < 2; k++) {
+        const int col = L.word_col[w + k];
+        v[k] = (w + k) == L.meta_word ? (int64_t)((uint32_t)jlo | (vm << 16))
+                                      : (col >= 0 ? load_col_raw(cols, ctypes.t[col], col, i) : 0);
+      }
+      *(longlong2*)(r + w) = make_longlong2(v[0], v[1]);
+    }
   }
-  for (int c = 0; c < n_cols; c++)  // raw 8-byte value (INT32 sign-extended, DOUBLE bits)
-    ((int64_t*)scols.data[c])[pos] = load_col_raw(cols, ctypes.t[c], c, i);
 }
 
 template <int U>
@@ -206,8 +219,8 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
     const uint8_t* __restrict__ rv, ColPtrs cols, int n_cols, ColTypes ctypes, int64_t n, int64_t tile, int log2P,
     int pad, int64_t nT, const uint32_t* __restrict__ offs, const int64_t* __restrict__ pbase,
     const int64_t* __restrict__ tileprefix, const int64_t* __restrict__ tilemax,
-    const int64_t* __restrict__ tilemin, int windowed, int64_t size, int64_t adv, int64_t grace, int has_meta,
-    longlong2* __restrict__ srec, uint32_t* __restrict__ smeta, ColPtrs scols, int64_t* __restrict__ tpart) {
+    const int64_t* __restrict__ tilemin, int windowed, int64_t size, int64_t adv, int64_t grace, RecLayout L,
+    uint64_t* __restrict__ srec, int64_t* __restrict__ tpart) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint32_t* cur = (uint32_t*)smem;
   __shared__ int64_t lmax[PT_THREADS / 64];
@@ -246,7 +259,7 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
         if (!ok[u] || x[u] < 0 || !bit_get(kv, i) || !bit_get(rv, i)) continue;
         const int64_t nwin = windowed ? (x[u] - first_window_start(x[u], size, adv)) / adv + 1 : 1;
         c_app += nwin;
-        scatter_one(k[u], x[u], 0, i, log2P, cur, srec, has_meta, smeta, cols, n_cols, ctypes, scols, true);
+        scatter_one(k[u], x[u], 0, i, log2P, cur, srec, L, cols, n_cols, ctypes, true);
       }
     }
   } else {
@@ -271,7 +284,7 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
       }
       c_late += jlo;
       c_app += nwin - jlo;
-      scatter_one(keys[i], x, jlo, i, log2P, cur, srec, has_meta, smeta, cols, n_cols, ctypes, scols, nwin > jlo);
+      scatter_one(keys[i], x, jlo, i, log2P, cur, srec, L, cols, n_cols, ctypes, nwin > jlo);
     }
   }
   c_app = wave_sum(c_app);
@@ -284,7 +297,7 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
   if (pad) {  // fill each run's tail up to the next run's start with skipped records (ts = -1)
     for (int p = threadIdx.x; p < P; p += PT_THREADS) {
       const int64_t stop = t + 1 < nT ? (int64_t)offs[(t + 1) * P + p] : pbase[p + 1];
-      for (int64_t q = cur[p]; q < stop; q++) srec[q] = make_longlong2(0, -1);
+      for (int64_t q = cur[p]; q < stop; q++) *(longlong2*)(srec + (uint64_t)q * L.rw) = make_longlong2(0, -1);
     }
   }
   if (threadIdx.x == 0) {
@@ -309,7 +322,7 @@ typedef KLDS double lds_f64;
 #define WG_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP
 
 __device__ __forceinline__ void lds_apply(const PartAggParams& q, lds_i64* lw, int H, int e, int64_t t,
-                                          uint32_t vmask, const ColPtrs& scols, int64_t gi) {
+                                          uint32_t vmask, const uint64_t* __restrict__ srec, int64_t gi, int64_t w3) {
   __hip_atomic_fetch_max(&lw[2 * H + e], t, WG_RLX);
   for (int o = 0; o < q.n_ops; o++) {
     const UpdOp op = q.ops[o];
@@ -319,7 +332,8 @@ __device__ __forceinline__ void lds_apply(const PartAggParams& q, lds_i64* lw, i
       continue;
     }
     if (!((vmask >> op.col) & 1u)) continue;
-    const int64_t raw = ((const int64_t*)scols.data[op.col])[gi];
+    const int cw = q.col_word[op.col];  // word 3 came with the record's second 16 bytes
+    const int64_t raw = cw == 3 ? w3 : (int64_t)srec[(uint64_t)gi * q.rw + cw];
     switch (op.kind) {
       case OP_INC_VALID: __hip_atomic_fetch_add(w, (int64_t)1, WG_RLX); break;
       case OP_ADD_I64: __hip_atomic_fetch_add((KLDS uint64_t*)w, (uint64_t)raw, WG_RLX); break;
@@ -348,8 +362,7 @@ __device__ __forceinline__ void lds_apply(const PartAggParams& q, lds_i64* lw, i
 
 __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const uint32_t* __restrict__ work,
                                                          const int64_t* __restrict__ pbase,
-                                                         const longlong2* __restrict__ srec,
-                                                         const uint32_t* __restrict__ smeta, ColPtrs scols,
+                                                         const uint64_t* __restrict__ srec, int first,
                                                          uint64_t* __restrict__ buf0, uint64_t* __restrict__ buf1,
                                                          const uint8_t* __restrict__ sel,
                                                          const int64_t* __restrict__ cnt,
@@ -378,17 +391,18 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
     p = blockIdx.x;
   }
   const int64_t rbase = pbase[p], rn = pbase[p + 1] - rbase;
-  if (rn == 0 && !work) return;  // untouched partition: nothing to rewrite
+  if (rn == 0 && first) return;  // untouched partition: nothing to rewrite
   // the first AU records of every thread are loaded before the LDS table is initialised,
   // so the HBM latency overlaps the init instead of following it
   constexpr int AU = 8;
-  longlong2 rec[AU];
-  uint32_t meta[AU];
+  const bool wide = q.rw > 2;
+  longlong2 rec[AU], ext[AU];
 #pragma unroll
   for (int u = 0; u < AU; u++) {
     const int64_t li = threadIdx.x + (int64_t)u * AG_THREADS;
-    rec[u] = li < rn ? srec[rbase + li] : make_longlong2(0, -1);
-    meta[u] = (q.has_meta && li < rn) ? smeta[rbase + li] : 0u;
+    const longlong2* r = (const longlong2*)(srec + (uint64_t)(rbase + li) * q.rw);
+    rec[u] = li < rn ? r[0] : make_longlong2(0, -1);
+    ext[u] = (wide && li < rn) ? r[1] : make_longlong2(0, 0);
   }
   for (int e = threadIdx.x; e < H; e += AG_THREADS) {
     lref[e] = 0;
@@ -406,7 +420,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
   const bool evict = q.windowed && close0 != INT64_MIN;
   // the first pass moves the closed rows; a retried partition already moved them (its region
   // still holds them until it succeeds), so retries only skip them
-  if (evict && !work) {
+  if (evict && first) {
     int ne = 0;
     for (int64_t r = threadIdx.x; r < nrow; r += AG_THREADS) {
       const uint64_t* row = src + r * q.sw;
@@ -465,18 +479,22 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
 #pragma unroll
       for (int u = 0; u < AU; u++) {  // AU records in flight per thread
         const int64_t li = l0 + u * AG_THREADS;
-        rec[u] = li < rn ? srec[rbase + li] : make_longlong2(0, -1);
-        meta[u] = (q.has_meta && li < rn) ? smeta[rbase + li] : 0u;
+        const longlong2* r = (const longlong2*)(srec + (uint64_t)(rbase + li) * q.rw);
+        rec[u] = li < rn ? r[0] : make_longlong2(0, -1);
+        ext[u] = (wide && li < rn) ? r[1] : make_longlong2(0, 0);
       }
     }
 #pragma unroll
-    for (int u = 0; u < AU; u++) {  // unrolled: rec[]/meta[] stay in registers (no scratch)
+    for (int u = 0; u < AU; u++) {  // unrolled: rec[]/ext[] stay in registers (no scratch)
       const int64_t t = rec[u].y;
       if (t < 0) continue;  // every window late (or past the end)
+      if (*(volatile KLDS int*)&lovf) continue;  // the partition will be retried: stop early
       const int64_t key = rec[u].x;
       const int64_t gi = rbase + l0 + u * AG_THREADS;
-      const int64_t jlo = meta[u] & 0xFFFFu;
-      const uint32_t vmask = meta[u] >> 16;
+      const uint32_t meta = q.meta_word == 2 ? (uint32_t)ext[u].x : 0u;
+      const int64_t jlo = meta & 0xFFFFu;
+      const uint32_t vmask = meta >> 16;
+      const int64_t w3 = ext[u].y;
       const int64_t ws_first = q.windowed ? first_window_start(t, q.size, q.adv) : 0;
       for (int64_t ws = ws_first + jlo * q.adv; ws <= (q.windowed ? t : 0); ws += (q.windowed ? q.adv : 1)) {
         const uint64_t h = group_hash(key, ws);
@@ -484,6 +502,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
         int e = (int)(h & (uint64_t)(H - 1));
         bool done = false;
         for (int probe = 0; probe < H; probe++) {
+          if ((probe & 31) == 31 && *(volatile KLDS int*)&lovf) break;  // table overfull
           uint32_t v = vlref[e];
           if (v == 0u) {
             uint32_t old = 0u;
@@ -496,7 +515,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
               // key/ws.  Only the compiler must not reorder (no vmcnt/cache instruction needed).
               __atomic_signal_fence(__ATOMIC_SEQ_CST);
               vlref[e] = L_READY;
-              lds_apply(q, lw, H, e, t, vmask, scols, gi);
+              lds_apply(q, lw, H, e, t, vmask, srec, gi, w3);
               done = true;
               break;
             }
@@ -509,7 +528,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
           }
           __atomic_signal_fence(__ATOMIC_SEQ_CST);
           if (vlw[e] == key && vlw[H + e] == ws) {
-            lds_apply(q, lw, H, e, t, vmask, scols, gi);
+            lds_apply(q, lw, H, e, t, vmask, srec, gi, w3);
             done = true;
             break;
           }
@@ -692,6 +711,24 @@ khip_status part_init(khip_agg* a, int64_t hint) {
   if (const char* e = getenv("KHIP_PART_LOG2")) s.log2P = std::min(MAX_P_LOG2, atoi(e));
   s.P = 1LL << s.log2P;
   s.cmax = next_pow2(std::max<int64_t>(64, 2 * groups / s.P + 64));
+  // more hinted groups per partition than one LDS table holds (P is capped by the LDS
+  // histogram): start every partition with enough sub-passes instead of failing pass 0
+  int s0 = 0;
+  while (s0 < 12 && groups / s.P > ((int64_t)s.H_eff * 7 / 10) << s0) s0++;
+  s.psbits.assign(s.P, (uint8_t)s0);
+  // scattered record layout: key, ts, [meta], the value columns the update ops read
+  bool colref[MAX_COLS] = {false};  // value read (SUM/MIN/MAX); COUNT(col) needs only validity
+  s.vcols = 0;
+  for (int o = 0; o < a->ap.n_ops; o++) {
+    if (a->ap.ops[o].kind == OP_INC) continue;
+    s.vcols |= 1u << a->ap.ops[o].col;
+    if (a->ap.ops[o].kind != OP_INC_VALID) colref[a->ap.ops[o].col] = true;
+  }
+  const bool meta = a->desc.window_kind == KHIP_WINDOW_HOPPING || s.vcols != 0;
+  s.meta_word = meta ? 2 : -1;
+  int w = meta ? 3 : 2;
+  for (int c = 0; c < MAX_COLS; c++) s.col_word[c] = (c < a->desc.n_cols && colref[c]) ? (int8_t)w++ : (int8_t)-1;
+  s.rw = (w + 1) & ~1;
   KHIP_TRY(s.sel.ensure(s.P));
   KHIP_TRY(s.fail.ensure(s.P));
   KHIP_TRY(s.cnt.ensure(s.P * 8));
@@ -711,10 +748,9 @@ void part_release(khip_agg* a) {
   PartState& s = a->part;
   DevBuf* bufs[] = {&s.closed, &s.closed_ctr, &s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist,
                     &s.tilemax, &s.tilemin,
-                    &s.tileprefix, &s.tpart, &s.scan_tmp, &s.skey, &s.sts, &s.smeta, &s.work,
+                    &s.tileprefix, &s.tpart, &s.scan_tmp, &s.srec, &s.work,
                     &s.pbase, &s.R, &s.ctr, &s.counts};
   for (DevBuf* b : bufs) b->release();
-  for (int c = 0; c < MAX_COLS; c++) s.scol[c].release();
 }
 
 khip_status part_reset(khip_agg* a) {
@@ -734,7 +770,9 @@ static PartAggParams part_params(khip_agg* a) {
   q.sw = a->sw;
   q.H = s.H;
   q.H_eff = s.H_eff;
-  q.has_meta = (a->desc.window_kind == KHIP_WINDOW_HOPPING || a->desc.n_cols > 0) ? 1 : 0;
+  q.rw = s.rw;
+  q.meta_word = s.meta_word;
+  for (int c = 0; c < MAX_COLS; c++) q.col_word[c] = s.col_word[c];
   q.size = a->desc.size_ms;
   q.adv = a->windowed ? a->desc.advance_ms : 1;
   q.cmax = s.cmax;
@@ -799,6 +837,10 @@ static khip_status part_split(khip_agg* a) {
     *olds[k] = *news[k];
     news[k]->p = nullptr;
   }
+  // a child holds about half of its parent's groups: one sub-pass bit fewer
+  std::vector<uint8_t> nps(P2);
+  for (int64_t c = 0; c < P2; c++) nps[c] = s.psbits[c >> 1] ? (uint8_t)(s.psbits[c >> 1] - 1) : 0;
+  s.psbits.swap(nps);
   s.P = P2;
   s.log2P += 1;
   s.cmax = ncmax;
@@ -829,15 +871,20 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   const int64_t ncap = pad ? n + 3 * (int64_t)P * nT : n;  // padded runs
   if (s.scat_cap < ncap) {
     const int64_t n = ncap;
-    KHIP_TRY(s.skey.ensure(n * 16));  // AoS (key, ts) records
-    if (a->desc.window_kind == KHIP_WINDOW_HOPPING || a->desc.n_cols > 0) KHIP_TRY(s.smeta.ensure(n * 4));
-    for (int c = 0; c < a->desc.n_cols; c++) KHIP_TRY(s.scol[c].ensure(n * 8));
+    KHIP_TRY(s.srec.ensure((size_t)n * s.rw * 8));  // AoS records
     s.scat_cap = ncap;
   }
   ColTypes ct{};
   for (int c = 0; c < MAX_COLS; c++) ct.t[c] = a->ap.col_type[c];
-  ColPtrs sc{};
-  for (int c = 0; c < a->desc.n_cols; c++) sc.data[c] = s.scol[c].p;
+  RecLayout L{};
+  L.rw = s.rw;
+  L.meta_word = s.meta_word;
+  L.vcols = s.vcols;
+  for (int w = 0; w < (int)sizeof(L.word_col); w++) L.word_col[w] = -1;
+  for (int c = 0; c < MAX_COLS; c++) {
+    L.col_word[c] = s.col_word[c];
+    if (s.col_word[c] >= 0) L.word_col[s.col_word[c]] = (int8_t)c;
+  }
   const size_t hist_lds = (size_t)P * 4;
   // 1. histogram + tile stream-time maxima
   ev_record_part(a, 0);
@@ -859,7 +906,6 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                      P, TC, s.scan_tmp.as<int64_t>(), s.pbase.as<int64_t>());
   ev_record_part(a, 1);
   // 3. scatter
-  const int has_meta = (a->desc.window_kind == KHIP_WINDOW_HOPPING || a->desc.n_cols > 0) ? 1 : 0;
   const char* su = getenv("KHIP_SCATTER_U");
   const int U = su ? atoi(su) : 16;
   auto scat = U >= 16 ? k_part_scatter<16> : (U >= 8 ? k_part_scatter<8> : k_part_scatter<4>);
@@ -867,8 +913,8 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                      a->desc.n_cols, ct, n, tile, s.log2P, pad, nT, s.hist.as<uint32_t>(), s.pbase.as<int64_t>(),
                      s.tileprefix.as<int64_t>(),
                      s.tilemax.as<int64_t>(), s.tilemin.as<int64_t>(), a->windowed, a->desc.size_ms,
-                     a->windowed ? a->desc.advance_ms : 1, a->grace, has_meta, s.skey.as<longlong2>(),
-                     has_meta ? s.smeta.as<uint32_t>() : nullptr, sc, s.tpart.as<int64_t>());
+                     a->windowed ? a->desc.advance_ms : 1, a->grace, L, s.srec.as<uint64_t>(),
+                     s.tpart.as<int64_t>());
   KHIP_TRY_HIP(hipGetLastError());
   ev_record_part(a, 2);
   // 4. aggregate partitions (+ retries)
@@ -893,18 +939,26 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   }
   int64_t added_total = 0;
   std::vector<uint8_t> host_fail;
-  std::vector<int> sbits(P, 0);
+  std::vector<int> sbits(s.psbits.begin(), s.psbits.end());
   std::vector<uint32_t> plist, work;
+  // pass 0: one work item per partition, or its learned 2^sbits sub-passes
+  bool subs0 = false;
+  for (int p = 0; p < P && !subs0; p++) subs0 = sbits[p] > 0;
+  if (subs0) {
+    for (int p = 0; p < P; p++)
+      for (int k = 0; k < (1 << sbits[p]); k++) work.push_back((uint32_t)p | ((uint32_t)sbits[p] << 16) | ((uint32_t)k << 20));
+    KHIP_TRY(s.work.ensure(work.size() * 4));
+    KHIP_TRY_HIP(hipMemcpyAsync(s.work.p, work.data(), work.size() * 4, hipMemcpyHostToDevice, a->stream));
+  }
   for (int pass = 0;; pass++) {
     PartAggParams q = q0;
     q.cmax = s.cmax;
     KHIP_TRY_HIP(hipMemsetAsync(s.ctr.p, 0, 24, a->stream));
-    const uint32_t* wk = pass == 0 ? nullptr : s.work.as<uint32_t>();
-    const int64_t nwork = pass == 0 ? P : (int64_t)work.size();
+    const uint32_t* wk = (pass == 0 && !subs0) ? nullptr : s.work.as<uint32_t>();
+    const int64_t nwork = (pass == 0 && !subs0) ? P : (int64_t)work.size();
     hipFuncSetAttribute((const void*)k_part_agg, hipFuncAttributeMaxDynamicSharedMemorySize, s.lds_bytes);
     hipLaunchKernelGGL(k_part_agg, dim3(nwork), dim3(AG_THREADS), s.lds_bytes, a->stream, q, wk,
-                       s.pbase.as<int64_t>(), s.skey.as<longlong2>(),
-                       has_meta ? s.smeta.as<uint32_t>() : nullptr, sc, s.buf[0].as<uint64_t>(),
+                       s.pbase.as<int64_t>(), s.srec.as<uint64_t>(), pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(),
                        s.buf[1].as<uint64_t>(), s.sel.as<uint8_t>(), s.cnt.as<int64_t>(),
                        s.newcnt.as<unsigned long long>(), s.fail.as<uint8_t>(),
                        s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
@@ -945,6 +999,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     KHIP_TRY(s.work.ensure(both.size() * 4));
     KHIP_TRY_HIP(hipMemcpyAsync(s.work.p, both.data(), both.size() * 4, hipMemcpyHostToDevice, a->stream));
   }
+  for (int p = 0; p < P; p++) s.psbits[p] = (uint8_t)std::max<int>(s.psbits[p], sbits[p]);
   // 5. counters
   if (a->windowed) {
     int64_t cn = 0;

@@ -387,7 +387,7 @@ khip_status khip_table_create(const khip_table_desc* d, khip_table** out) {
   t->device = d->device;
   t->sw = (int)next_pow2(std::max(4, 3 + d->n_cols));
   DeviceGuard g(t->device);
-  if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&t->stream, hipStreamDefault) != hipSuccess) {
     delete t;
     return fail(KHIP_E_DEVICE, "hipStreamCreate failed (no device?)");
   }

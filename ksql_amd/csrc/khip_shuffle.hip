@@ -1,0 +1,422 @@
+// khip_shuffle.hip — repartition for non-key GROUP BY / PARTITION BY, and the RCCL exchange.
+//
+// Replaces the repartition topic round-trip of StreamGroupByBuilderBase.build
+// (S/StreamGroupByBuilderBase.java:101-103: filter(v != null).groupBy(mapper) → sink
+// "<ctx>-repartition" → source) and StreamSelectKeyBuilder (S/StreamSelectKeyBuilder.java:73-74):
+//   k_shuf_hist      per 4096-record tile: drop null value / null new key / negative ts
+//                    (S/GroupByParamsFactory.java:92-100), count rows per destination
+//   (column prefix)  reuses the partitioned engine's k_part_colsum/colbase/colprefix
+//   k_shuf_pack      STABLE scatter of packed rows to their destination's contiguous run
+//                    (wave ballots per destination + cross-wave LDS prefix keep arrival order)
+//   khip_comm_alltoall  grouped ncclSend/ncclRecv, one pair per peer over xGMI (every MI355X
+//                    pair has a direct link, so this is per-link bound, not a ring)
+//   k_shuf_unpack    packed rows → columnar batch (bitmaps built with __ballot)
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "khip_agg_internal.hpp"
+
+namespace khip {
+
+// partitioned-engine column prefix kernels (khip_agg_part.hip)
+__global__ void k_part_colsum(const uint32_t* __restrict__ hist, int64_t nT, int P, int TC, int64_t* __restrict__ csum);
+__global__ void k_part_colbase(int64_t* __restrict__ csum, int P, int TC, int64_t* __restrict__ R);
+__global__ void k_part_colprefix(uint32_t* __restrict__ hist, int64_t nT, int P, int TC,
+                                 const int64_t* __restrict__ csum, const int64_t* __restrict__ pbase);
+
+constexpr int SH_THREADS = 256;
+constexpr int SH_ITEMS = 16;
+constexpr int64_t SH_TILE = (int64_t)SH_THREADS * SH_ITEMS;
+constexpr int SH_MAX_PARTS = 256;
+constexpr int SH_MAX_COLS = 8;
+
+struct ShCols {
+  int32_t key_bytes;
+  const void* data[SH_MAX_COLS];
+  const uint8_t* valid[SH_MAX_COLS];
+  int32_t type[SH_MAX_COLS];
+};
+
+// Kafka's default partitioner over the KAFKA-format key (big-endian 4 / 8 bytes,
+// ksqldb-serde/.../kafka/KafkaSerdeFactory.java:42-43): toPositive(murmur2(bytes)) % n_parts,
+// so a record lands on the same partition the reference's repartition topic would give it.
+__device__ __forceinline__ uint32_t murmur2_word(uint32_t h, uint32_t k) {
+  const uint32_t m = 0x5bd1e995u;
+  k *= m;
+  k ^= k >> 24;
+  k *= m;
+  return (h * m) ^ k;
+}
+
+__device__ __forceinline__ uint32_t shuffle_dest(int64_t key, int key_bytes, int n_parts) {
+  const uint32_t m = 0x5bd1e995u;
+  const uint64_t v = (uint64_t)key;
+  uint32_t h = 0x9747b28cu ^ (uint32_t)key_bytes;
+  // the little-endian load of big-endian bytes is a byte swap of each 32-bit half
+  if (key_bytes == 8) {
+    h = murmur2_word(h, __builtin_bswap32((uint32_t)(v >> 32)));
+    h = murmur2_word(h, __builtin_bswap32((uint32_t)v));
+  } else {
+    h = murmur2_word(h, __builtin_bswap32((uint32_t)v));
+  }
+  h ^= h >> 13;
+  h *= m;
+  h ^= h >> 15;
+  return (h & 0x7fffffffu) % (uint32_t)n_parts;
+}
+
+__device__ __forceinline__ int64_t sh_raw(const ShCols& c, int col, int64_t i) {
+  if (c.type[col] == KHIP_TYPE_INT32) return (int64_t)((const int32_t*)c.data[col])[i];
+  return ((const int64_t*)c.data[col])[i];
+}
+
+__device__ __forceinline__ bool sh_valid(const ShCols& c, int key_col, const uint8_t* rv, const int64_t* ts,
+                                         int64_t i) {
+  return bit_get(rv, i) && bit_get(c.valid[key_col], i) && ts[i] >= 0;
+}
+
+__global__ __launch_bounds__(SH_THREADS) void k_shuf_hist(ShCols c, int key_col, const uint8_t* __restrict__ rv,
+                                                          const int64_t* __restrict__ ts, int64_t n, int n_parts,
+                                                          uint32_t* __restrict__ hist) {
+  __shared__ uint32_t lh[SH_MAX_PARTS];
+  for (int d = threadIdx.x; d < n_parts; d += SH_THREADS) lh[d] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * SH_TILE;
+  for (int r = 0; r < SH_ITEMS; r++) {
+    const int64_t i = base + (int64_t)r * SH_THREADS + threadIdx.x;
+    if (i < n && sh_valid(c, key_col, rv, ts, i)) atomicAdd(&lh[shuffle_dest(sh_raw(c, key_col, i), c.key_bytes, n_parts)], 1u);
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < n_parts; d += SH_THREADS) hist[(int64_t)blockIdx.x * n_parts + d] = lh[d];
+}
+
+__global__ __launch_bounds__(SH_THREADS) void k_shuf_pack(ShCols c, int n_cols, int key_col,
+                                                          const uint8_t* __restrict__ rv, const int64_t* __restrict__ ts,
+                                                          int64_t n, int n_parts, const uint32_t* __restrict__ offs,
+                                                          uint64_t* __restrict__ out, int row_words) {
+  __shared__ uint32_t cur[SH_MAX_PARTS];
+  __shared__ uint32_t wcnt[SH_THREADS / 64][SH_MAX_PARTS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int d = threadIdx.x; d < n_parts; d += SH_THREADS) cur[d] = offs[(int64_t)blockIdx.x * n_parts + d];
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * SH_TILE;
+  const uint64_t lt = (1ULL << lane) - 1;
+  for (int r = 0; r < SH_ITEMS; r++) {
+    const int64_t i = base + (int64_t)r * SH_THREADS + threadIdx.x;
+    const bool v = i < n && sh_valid(c, key_col, rv, ts, i);
+    const int64_t key = v ? sh_raw(c, key_col, i) : 0;
+    const int d = v ? (int)shuffle_dest(key, c.key_bytes, n_parts) : -1;
+    // rank among earlier lanes of this wave with the same destination; wave totals → LDS.
+    // One ballot per destination PRESENT in the wave (peeled by leader lane), not per n_parts.
+    for (int dd = lane; dd < n_parts; dd += 64) wcnt[wave][dd] = 0;
+    int rank = 0;
+    uint64_t pending = __ballot(v);
+    while (pending) {
+      const int dl = __shfl(d, __ffsll((unsigned long long)pending) - 1);
+      const uint64_t m = __ballot(d == dl);
+      if (d == dl) rank = __popcll(m & lt);
+      if (lane == 0) wcnt[wave][dl] = (uint32_t)__popcll(m);
+      pending &= ~m;
+    }
+    __syncthreads();
+    if (v) {
+      uint32_t pos = cur[d] + rank;
+      for (int w = 0; w < wave; w++) pos += wcnt[w][d];
+      uint64_t* o = out + (uint64_t)pos * row_words;
+      o[0] = (uint64_t)key;
+      o[1] = (uint64_t)ts[i];
+      // the key column travels as word 0 only (its validity is implied)
+      uint64_t vm = 1ULL << key_col;
+      int w = 2;
+      for (int cc = 0; cc < n_cols; cc++) {
+        if (cc == key_col) continue;
+        const bool cv = bit_get(c.valid[cc], i);
+        o[w++] = cv ? (uint64_t)sh_raw(c, cc, i) : 0ULL;
+        vm |= (cv ? 1ULL : 0ULL) << cc;
+      }
+      o[w] = vm;
+    }
+    __syncthreads();
+    for (int dd = threadIdx.x; dd < n_parts; dd += SH_THREADS) {
+      uint32_t s = 0;
+      for (int w = 0; w < SH_THREADS / 64; w++) s += wcnt[w][dd];
+      cur[dd] += s;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_shuf_unpack(const uint64_t* __restrict__ rows, int64_t n, int n_cols,
+                                                     int key_col, int row_words, ShCols types, int64_t* __restrict__ key,
+                                                     int64_t* __restrict__ ts, void* const* __restrict__ col_data,
+                                                     uint8_t* const* __restrict__ col_valid) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const bool in = i < n;
+  const uint64_t* r = rows + (in ? i : 0) * (uint64_t)row_words;
+  const uint64_t vm = in ? r[row_words - 1] : 0;
+  if (in) {
+    key[i] = (int64_t)r[0];
+    ts[i] = (int64_t)r[1];
+  }
+  const int lane = threadIdx.x & 63;
+  const int64_t wbase = i - lane;
+  for (int c = 0, w = 2; c < n_cols; c++) {
+    const uint64_t word = c == key_col ? (in ? r[0] : 0) : (in ? r[w++] : 0);
+    if (in && col_data[c]) {
+      if (types.type[c] == KHIP_TYPE_INT32) ((int32_t*)col_data[c])[i] = (int32_t)word;
+      else ((uint64_t*)col_data[c])[i] = word;
+    }
+    const uint64_t b = __ballot(in && ((vm >> c) & 1));
+    if (col_valid && col_valid[c] && lane == 0 && wbase < n) {
+      const int64_t nbytes = std::min<int64_t>(8, (n - wbase + 7) / 8);
+      for (int k = 0; k < nbytes; k++) col_valid[c][wbase / 8 + k] = (uint8_t)(b >> (8 * k));
+    }
+  }
+}
+
+}  // namespace khip
+
+using namespace khip;
+
+struct khip_shuffle {
+  khip_shuffle_desc desc{};
+  std::vector<int32_t> types;
+  hipStream_t stream = nullptr;
+  DevBuf hist, csum, pbase, R, ptrs;
+};
+
+struct khip_comm {
+  ncclComm_t comm = nullptr;
+  int nranks = 0, rank = 0, device = 0;
+  hipStream_t stream = nullptr;
+  DevBuf cnt;
+};
+
+extern "C" {
+
+khip_status khip_shuffle_create(const khip_shuffle_desc* d, khip_shuffle** out) {
+  clear_error();
+  if (!d || !out) return fail(KHIP_E_INVALID, "null argument");
+  if (d->n_parts < 1 || d->n_parts > SH_MAX_PARTS) return fail(KHIP_E_UNSUPPORTED, "1..256 destinations");
+  if (d->n_cols < 1 || d->n_cols > SH_MAX_COLS) return fail(KHIP_E_UNSUPPORTED, "1..8 value columns");
+  if (d->key_col < 0 || d->key_col >= d->n_cols) return fail(KHIP_E_INVALID, "key column");
+  for (int c = 0; c < d->n_cols; c++)
+    if (d->col_types[c] < KHIP_TYPE_INT32 || d->col_types[c] > KHIP_TYPE_DOUBLE) return fail(KHIP_E_INVALID, "column type");
+  if (d->col_types[d->key_col] == KHIP_TYPE_DOUBLE) return fail(KHIP_E_UNSUPPORTED, "DOUBLE group key");
+  khip_shuffle* s = new khip_shuffle();
+  s->desc = *d;
+  s->types.assign(d->col_types, d->col_types + d->n_cols);
+  s->desc.col_types = s->types.data();
+  DeviceGuard g(d->device);
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamDefault) != hipSuccess) {
+    delete s;
+    return fail(KHIP_E_DEVICE, "hipStreamCreate failed (no device?)");
+  }
+  *out = s;
+  return KHIP_OK;
+}
+
+int32_t khip_shuffle_row_words(const khip_shuffle* s) { return s ? 2 + s->desc.n_cols : 0; }
+
+khip_status khip_shuffle_pack(khip_shuffle* s, const khip_batch* b, uint64_t* send, int64_t capacity, int64_t* counts) {
+  clear_error();
+  if (!s || !b || !counts) return fail(KHIP_E_INVALID, "null argument");
+  if (b->mem != KHIP_MEM_DEVICE) return fail(KHIP_E_INVALID, "pack needs a device batch");
+  const int64_t n = b->n_rows;
+  const int N = s->desc.n_parts;
+  if (n == 0) {
+    for (int d = 0; d < N; d++) counts[d] = 0;
+    return KHIP_OK;
+  }
+  if (b->n_cols < s->desc.n_cols || !b->ts || !b->col_data) return fail(KHIP_E_INVALID, "batch shape");
+  if (n >= (1LL << 31)) return fail(KHIP_E_UNSUPPORTED, "pack batch larger than 2^31 rows");
+  DeviceGuard g(s->desc.device);
+  ShCols c{};
+  for (int k = 0; k < s->desc.n_cols; k++) {
+    c.data[k] = b->col_data[k];
+    c.valid[k] = b->col_valid ? b->col_valid[k] : nullptr;
+    c.type[k] = s->types[k];
+  }
+  c.key_bytes = s->types[s->desc.key_col] == KHIP_TYPE_INT32 ? 4 : 8;
+  const int64_t nT = ceil_div(n, SH_TILE);
+  const int TC = (int)std::min<int64_t>(nT, 64);
+  KHIP_TRY(s->hist.ensure((size_t)nT * N * 4));
+  KHIP_TRY(s->csum.ensure((size_t)TC * N * 8));
+  KHIP_TRY(s->pbase.ensure((N + 1) * 8));
+  KHIP_TRY(s->R.ensure((N + 1) * 8));
+  hipLaunchKernelGGL(k_shuf_hist, dim3(nT), dim3(SH_THREADS), 0, s->stream, c, s->desc.key_col, b->row_valid, b->ts, n,
+                     N, s->hist.as<uint32_t>());
+  hipLaunchKernelGGL(k_part_colsum, dim3(ceil_div(N, 256), TC), dim3(256), 0, s->stream, s->hist.as<uint32_t>(), nT, N,
+                     TC, s->csum.as<int64_t>());
+  hipLaunchKernelGGL(k_part_colbase, dim3(ceil_div(N, 256)), dim3(256), 0, s->stream, s->csum.as<int64_t>(), N, TC,
+                     s->R.as<int64_t>());
+  KHIP_TRY_HIP(hipMemcpyAsync(s->pbase.p, s->R.p, N * 8, hipMemcpyDeviceToDevice, s->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(s->pbase.as<int64_t>() + N, 0, 8, s->stream));
+  hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s->stream, s->pbase.as<int64_t>(), (int64_t)N,
+                     s->pbase.as<int64_t>() + N);
+  hipLaunchKernelGGL(k_part_colprefix, dim3(ceil_div(N, 256), TC), dim3(256), 0, s->stream, s->hist.as<uint32_t>(), nT,
+                     N, TC, s->csum.as<int64_t>(), s->pbase.as<int64_t>());
+  KHIP_TRY_HIP(hipGetLastError());
+  std::vector<int64_t> R(N);
+  KHIP_TRY_HIP(hipMemcpyAsync(R.data(), s->R.p, N * 8, hipMemcpyDeviceToHost, s->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(s->stream));
+  int64_t tot = 0;
+  for (int d = 0; d < N; d++) tot += R[d];
+  for (int d = 0; d < N; d++) counts[d] = R[d];
+  if (tot > capacity || !send) return fail(KHIP_E_BUFFER, "send buffer too small");
+  hipLaunchKernelGGL(k_shuf_pack, dim3(nT), dim3(SH_THREADS), 0, s->stream, c, s->desc.n_cols, s->desc.key_col,
+                     b->row_valid, b->ts, n, N, s->hist.as<uint32_t>(), send, 2 + s->desc.n_cols);
+  KHIP_TRY_HIP(hipGetLastError());
+  KHIP_TRY_HIP(hipStreamSynchronize(s->stream));
+  return KHIP_OK;
+}
+
+khip_status khip_shuffle_unpack(khip_shuffle* s, const uint64_t* rows, int64_t n, int64_t* key, int64_t* ts,
+                                void* const* col_data, uint8_t* const* col_valid) {
+  clear_error();
+  if (!s || (n > 0 && (!rows || !key || !ts))) return fail(KHIP_E_INVALID, "null argument");
+  if (n == 0) return KHIP_OK;
+  DeviceGuard g(s->desc.device);
+  const int nc = s->desc.n_cols;
+  ShCols t{};
+  for (int k = 0; k < nc; k++) t.type[k] = s->types[k];
+  // column pointer arrays must be readable by the kernel: stage them in device memory
+  std::vector<uint64_t> host(2 * SH_MAX_COLS, 0);
+  for (int k = 0; k < nc; k++) {
+    host[k] = (uint64_t)(col_data ? col_data[k] : nullptr);
+    host[SH_MAX_COLS + k] = (uint64_t)(col_valid ? col_valid[k] : nullptr);
+  }
+  KHIP_TRY(s->ptrs.ensure(host.size() * 8));
+  KHIP_TRY_HIP(hipMemcpyAsync(s->ptrs.p, host.data(), host.size() * 8, hipMemcpyHostToDevice, s->stream));
+  hipLaunchKernelGGL(k_shuf_unpack, dim3(ceil_div(n, 256)), dim3(256), 0, s->stream, rows, n, nc, s->desc.key_col, 2 + nc, t, key, ts,
+                     (void* const*)s->ptrs.p, (uint8_t* const*)(s->ptrs.as<uint64_t>() + SH_MAX_COLS));
+  KHIP_TRY_HIP(hipGetLastError());
+  KHIP_TRY_HIP(hipStreamSynchronize(s->stream));
+  return KHIP_OK;
+}
+
+khip_status khip_shuffle_sync(khip_shuffle* s) {
+  if (!s) return fail(KHIP_E_INVALID, "null argument");
+  DeviceGuard g(s->desc.device);
+  KHIP_TRY_HIP(hipStreamSynchronize(s->stream));
+  return KHIP_OK;
+}
+
+khip_status khip_shuffle_destroy(khip_shuffle* s) {
+  if (!s) return KHIP_OK;
+  DeviceGuard g(s->desc.device);
+  hipStreamSynchronize(s->stream);
+  s->hist.release();
+  s->csum.release();
+  s->pbase.release();
+  s->R.release();
+  s->ptrs.release();
+  hipStreamDestroy(s->stream);
+  delete s;
+  return KHIP_OK;
+}
+
+// ------------------------------------------------------------------------ RCCL
+
+#define KHIP_TRY_NCCL(expr)                                                       \
+  do {                                                                            \
+    ncclResult_t _r = (expr);                                                     \
+    if (_r != ncclSuccess) {                                                      \
+      ::khip::set_error(std::string(#expr) + ": " + ncclGetErrorString(_r));      \
+      return KHIP_E_COMM;                                                         \
+    }                                                                             \
+  } while (0)
+
+khip_status khip_comm_unique_id(uint8_t id[KHIP_COMM_ID_BYTES]) {
+  clear_error();
+  if (!id) return fail(KHIP_E_INVALID, "null argument");
+  ncclUniqueId u;
+  KHIP_TRY_NCCL(ncclGetUniqueId(&u));
+  memcpy(id, u.internal, KHIP_COMM_ID_BYTES);
+  return KHIP_OK;
+}
+
+khip_status khip_comm_init(int32_t nranks, int32_t rank, const uint8_t id[KHIP_COMM_ID_BYTES], int32_t device,
+                           khip_comm** out) {
+  clear_error();
+  if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks) return fail(KHIP_E_INVALID, "bad communicator arguments");
+  DeviceGuard g(device);
+  khip_comm* c = new khip_comm();
+  c->nranks = nranks;
+  c->rank = rank;
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamDefault) != hipSuccess) {
+    delete c;
+    return fail(KHIP_E_DEVICE, "hipStreamCreate failed");
+  }
+  ncclUniqueId u;
+  memcpy(u.internal, id, KHIP_COMM_ID_BYTES);
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+  if (r != ncclSuccess) {
+    hipStreamDestroy(c->stream);
+    delete c;
+    return fail(KHIP_E_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
+  *out = c;
+  return KHIP_OK;
+}
+
+khip_status khip_comm_exchange_counts(khip_comm* c, const int64_t* send_counts, int64_t* recv_counts) {
+  clear_error();
+  if (!c || !send_counts || !recv_counts) return fail(KHIP_E_INVALID, "null argument");
+  DeviceGuard g(c->device);
+  const int N = c->nranks;
+  KHIP_TRY(c->cnt.ensure(2 * N * 8));
+  int64_t* dsend = c->cnt.as<int64_t>();
+  int64_t* drecv = dsend + N;
+  KHIP_TRY_HIP(hipMemcpyAsync(dsend, send_counts, N * 8, hipMemcpyHostToDevice, c->stream));
+  KHIP_TRY_NCCL(ncclGroupStart());
+  for (int p = 0; p < N; p++) {
+    KHIP_TRY_NCCL(ncclSend(dsend + p, 1, ncclInt64, p, c->comm, c->stream));
+    KHIP_TRY_NCCL(ncclRecv(drecv + p, 1, ncclInt64, p, c->comm, c->stream));
+  }
+  KHIP_TRY_NCCL(ncclGroupEnd());
+  KHIP_TRY_HIP(hipMemcpyAsync(recv_counts, drecv, N * 8, hipMemcpyDeviceToHost, c->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(c->stream));
+  return KHIP_OK;
+}
+
+khip_status khip_comm_alltoall(khip_comm* c, const uint64_t* send, const int64_t* send_counts, uint64_t* recv,
+                               int64_t recv_capacity, const int64_t* recv_counts, int32_t row_words) {
+  clear_error();
+  if (!c || !send_counts || !recv_counts || row_words < 1) return fail(KHIP_E_INVALID, "null argument");
+  DeviceGuard g(c->device);
+  const int N = c->nranks;
+  int64_t tot = 0;
+  for (int p = 0; p < N; p++) tot += recv_counts[p];
+  if (tot > recv_capacity) return fail(KHIP_E_BUFFER, "receive buffer smaller than the exchanged counts");
+  int64_t so = 0, ro = 0;
+  KHIP_TRY_NCCL(ncclGroupStart());
+  for (int p = 0; p < N; p++) {
+    if (send_counts[p])
+      KHIP_TRY_NCCL(ncclSend(send + so * row_words, (size_t)send_counts[p] * row_words, ncclUint64, p, c->comm, c->stream));
+    if (recv_counts[p])
+      KHIP_TRY_NCCL(ncclRecv(recv + ro * row_words, (size_t)recv_counts[p] * row_words, ncclUint64, p, c->comm, c->stream));
+    so += send_counts[p];
+    ro += recv_counts[p];
+  }
+  KHIP_TRY_NCCL(ncclGroupEnd());
+  KHIP_TRY_HIP(hipStreamSynchronize(c->stream));
+  return KHIP_OK;
+}
+
+khip_status khip_comm_destroy(khip_comm* c) {
+  if (!c) return KHIP_OK;
+  DeviceGuard g(c->device);
+  hipStreamSynchronize(c->stream);
+  if (c->comm) ncclCommDestroy(c->comm);
+  c->cnt.release();
+  hipStreamDestroy(c->stream);
+  delete c;
+  return KHIP_OK;
+}
+
+}  // extern "C"

@@ -15,6 +15,10 @@ agree bit for bit.  All randomness is splitmix64 of (stream seed << 40) + index.
   C4 clickstream      users: user_id 1..1e8, level ~ U{Gold, Silver, Platinum} (codes 0..2);
                       clicks: 1e9, userid ~ U[1, 1.1e8], ts = i; LEFT JOIN ... WHERE
                       level = 'Platinum'
+  C5 repartition_sum  1e9 records keyed by a random event id (source partition = event id % N),
+                      region_id BIGINT ~ U[0, 1e6), amount BIGINT ~ U[-1e6, 1e6],
+                      ts = i * 3.6e6 // n + U[0, 1000), GROUP BY region_id (non-key: repartition)
+                      SUM(amount) TUMBLING 1 MINUTE
 Weak scaling: rank r of N owns the keys k with k % N == r (key-hash sharding, the
 Kafka-partition analogue); its records are generated from its own seed.
 """
@@ -118,6 +122,8 @@ CONFIGS = {
                            size_ms=60_000, advance_ms=10_000, grace_ms=60_000, null_pct=1),
     "clickstream_join": dict(users=100_000_000, n=1_000_000_000, seed_users=4, seed_clicks=5,
                              miss_factor=1.1),
+    "repartition_sum": dict(n=1_000_000_000, regions=1_000_000, seed=6, span_ms=3_600_000, disorder_ms=1_000,
+                            size_ms=60_000),
 }
 
 
@@ -172,3 +178,16 @@ def clicks(lo, hi, users, xp="numpy", device=None, seed_clicks=5, miss_factor=1.
     uid = be.u53(_stream(be, seed_clicks, lo, hi, device)) % span + 1
     ts = be.idx(lo, hi, device)
     return uid, ts
+
+
+def repartition_sum(lo, hi, n, xp="numpy", device=None, rank=0, world=1, regions=1_000_000, seed=6,
+                    span_ms=3_600_000, disorder_ms=1_000):
+    """C5 source partition `rank`: (event_id key, ts, region_id BIGINT, amount BIGINT)."""
+    be = backend(xp)
+    s = seed + 1000 * rank
+    eid = (be.u53(_stream(be, s, lo, hi, device, 0, 4)) >> 8) * world + rank
+    i = be.idx(lo, hi, device)
+    ts = (i * span_ms) // n + be.u53(_stream(be, s, lo, hi, device, 1, 4)) % disorder_ms
+    region = be.u53(_stream(be, s, lo, hi, device, 2, 4)) % regions
+    amount = be.u53(_stream(be, s, lo, hi, device, 3, 4)) % 2_000_001 - 1_000_000
+    return eid, ts, region, amount

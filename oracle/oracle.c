@@ -62,6 +62,43 @@ uint64_t oracle_splitmix64(uint64_t x) {
   return z ^ (z >> 31);
 }
 
+int32_t oracle_murmur2(const uint8_t* data, int32_t len) {
+  const uint32_t m = 0x5bd1e995u;
+  uint32_t h = 0x9747b28cu ^ (uint32_t)len;
+  int32_t i;
+  for (i = 0; i + 4 <= len; i += 4) {
+    uint32_t k = (uint32_t)data[i] | ((uint32_t)data[i + 1] << 8) | ((uint32_t)data[i + 2] << 16) |
+                 ((uint32_t)data[i + 3] << 24);
+    k *= m;
+    k ^= k >> 24;
+    k *= m;
+    h *= m;
+    h ^= k;
+  }
+  switch (len & 3) {
+    case 3: h ^= (uint32_t)data[(len & ~3) + 2] << 16; /* fall through */
+    case 2: h ^= (uint32_t)data[(len & ~3) + 1] << 8;  /* fall through */
+    case 1:
+      h ^= (uint32_t)data[len & ~3];
+      h *= m;
+  }
+  h ^= h >> 13;
+  h *= m;
+  h ^= h >> 15;
+  return (int32_t)h;
+}
+
+void oracle_kafka_partition(const int64_t* keys, int64_t n, int32_t key_bytes, int32_t n_parts, int32_t* out) {
+  int64_t i;
+  for (i = 0; i < n; i++) {
+    uint8_t b[8];
+    uint64_t v = (uint64_t)keys[i];
+    int32_t j;
+    for (j = 0; j < key_bytes; j++) b[j] = (uint8_t)(v >> (8 * (key_bytes - 1 - j)));
+    out[i] = (int32_t)(((uint32_t)oracle_murmur2(b, key_bytes) & 0x7fffffffu) % (uint32_t)n_parts);
+  }
+}
+
 static uint64_t mix64(uint64_t h) {
   h ^= h >> 33;
   h *= 0xff51afd7ed558ccdULL;

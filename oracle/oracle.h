@@ -45,6 +45,16 @@ khip_status oracle_table_destroy(oracle_table* t);
  * inputs on the host for the oracle. */
 uint64_t oracle_splitmix64(uint64_t x);
 
+/* R8 repartition routing: the partition Kafka's default partitioner gives a record whose key
+ * is serialized in the KAFKA format (Serdes.Integer / Serdes.Long = big-endian 4 / 8 bytes,
+ * ksqldb-serde/.../kafka/KafkaSerdeFactory.java:42-43):
+ *   toPositive(murmur2(key bytes)) % n_parts          (kafka-clients 7.4.0-ccs, Apache Kafka 3.4:
+ *   Utils.murmur2 / Utils.toPositive, BuiltInPartitioner.partitionForKey — third-party, absent
+ *   from the reference tree; restated from the published algorithm). */
+int32_t oracle_murmur2(const uint8_t* data, int32_t len);
+void oracle_kafka_partition(const int64_t* keys, int64_t n, int32_t key_bytes, int32_t n_parts,
+                            int32_t* out);
+
 #ifdef __cplusplus
 }
 #endif
