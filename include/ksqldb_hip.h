@@ -231,6 +231,9 @@ khip_status khip_agg_sync(khip_agg* agg);
 /* desc.flags bit: use the global-atomic engine (one HBM hash table updated with
  * agent-scope atomics) instead of the default partitioned LDS engine. */
 #define KHIP_FLAG_ENGINE_ATOMIC 2
+/* desc.flags bit (diagnostic): partitioned engine always uses the claim/ready slot protocol
+ * instead of the packed-identity CAS it picks when a push's window range fits. */
+#define KHIP_FLAG_PART_CLAIM 4
 
 /* Cumulative device time per phase since creation or the last reset of the counters,
  * measured with HIP events on the handle's stream (valid with KHIP_FLAG_PROFILE). */

@@ -28,6 +28,7 @@ JOIN = {"LEFT": 0, "INNER": 1}
 MEM_HOST, MEM_DEVICE = 0, 1
 FLAG_PROFILE = 1
 FLAG_ENGINE_ATOMIC = 2
+FLAG_PART_CLAIM = 4
 NP_TYPE = {0: np.int32, 1: np.int64, 2: np.float64}
 
 i32, i64, u8p = C.c_int32, C.c_int64, C.POINTER(C.c_uint8)

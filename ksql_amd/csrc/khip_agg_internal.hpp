@@ -194,6 +194,12 @@ __global__ void k_scan_excl(int64_t* __restrict__ v, int64_t n, int64_t* __restr
 __global__ void k_compact(const uint64_t* __restrict__ table, int64_t cap, int sw, HavingDev h,
                           uint64_t* __restrict__ out, int64_t max_rows, unsigned long long* __restrict__ counter);
 
+// partitioned-engine column prefix kernels (khip_agg_part.hip; also used by khip_shuffle.hip)
+__global__ void k_part_colsum(const uint32_t* __restrict__ hist, int64_t nT, int P, int TC, int64_t* __restrict__ csum);
+__global__ void k_part_colbase(int64_t* __restrict__ csum, int P, int TC, int64_t* __restrict__ R);
+__global__ void k_part_colprefix(uint32_t* __restrict__ hist, int64_t nT, int P, int TC,
+                                 const int64_t* __restrict__ csum, const int64_t* __restrict__ pbase, int pstride);
+
 struct InitWords {
   int64_t w[32];
 };
@@ -224,6 +230,12 @@ struct PartState {
   // partition regions into an append-only store so the live table stays LDS-sized
   DevBuf closed, closed_ctr;
   int64_t closed_cap = 0, closed_n = 0;
+  // identity-CAS mode: wr = [window-index base, enabled] of the current push; res = window-
+  // index range of the resident rows (conservative); res_fresh = no resident rows yet
+  DevBuf wr, res;
+  bool res_fresh = true;
+  // two-level scatter: pass-A records, per-tile bucket histogram / offsets, bucket scans
+  DevBuf srecA, hcoarse, scan_tmpB, RB;
 };
 
 }  // namespace khip

@@ -61,6 +61,9 @@ struct PartAggParams {
   int32_t meta_word;  // 2 or -1
   int8_t col_word[MAX_COLS];
   int64_t size, adv;
+  FastDiv fd;  // division by adv
+  int32_t dbg_mode;  // KHIP_AGG_MODE (timing experiments only; results wrong when != 0)
+  int32_t log2P;
   int64_t cmax;
   int32_t n_cols;
   int32_t n_ops;
@@ -69,8 +72,45 @@ struct PartAggParams {
   InitWords init;
 };
 
+// Key hash: its top log2P bits pick the partition; inside a partition the LDS slot and the
+// sub-pass of a (key, windowStart) group mix its low bits with ws (cheap 32-bit math).
+__device__ __forceinline__ uint64_t key_hash(int64_t key) { return mix64((uint64_t)key ^ 0x6A09E667F3BCC908ULL); }
+
+// inverse of key_hash (mix64 is a bijection): key = unmix64(hk) ^ C
+__device__ __forceinline__ int64_t key_of_hash(uint64_t h) {
+  h ^= h >> 33;
+  h *= 0x9cb4b2f8129337dbULL;  // inverse of 0xc4ceb9fe1a85ec53 mod 2^64
+  h ^= h >> 33;
+  h *= 0x4f74430c22a54005ULL;  // inverse of 0xff51afd7ed558ccd mod 2^64
+  h ^= h >> 33;
+  return (int64_t)(h ^ 0x6A09E667F3BCC908ULL);
+}
+
+// Packed group identity (identity-CAS mode): inside partition p the top log2P bits of the
+// key hash are p, so (hk << log2P) keeps the key exactly; the low log2P bits hold the
+// window index relative to wbase (< 2^log2P - 1, so an identity is never EMPTY_ID).
+constexpr uint64_t EMPTY_ID = ~0ULL;
+__device__ __forceinline__ uint64_t ident_of(uint64_t hk, int64_t widx_rel, int log2P) {
+  return (hk << log2P) | (uint64_t)widx_rel;
+}
+
 __device__ __forceinline__ uint32_t part_of(int64_t key, int log2P) {
-  return log2P == 0 ? 0u : (uint32_t)(mix64((uint64_t)key ^ 0x6A09E667F3BCC908ULL) >> (64 - log2P));
+  return log2P == 0 ? 0u : (uint32_t)(key_hash(key) >> (64 - log2P));
+}
+
+__device__ __forceinline__ uint32_t slot_of(uint64_t hk, int64_t ws, int H) {
+  return ((uint32_t)hk + (uint32_t)ws * 0x9E3779B1u) & (uint32_t)(H - 1);
+}
+
+// 30-bit fingerprint kept with the slot state (low 2 bits): most probes of another group end
+// on the state word alone
+__device__ __forceinline__ uint32_t fp_of(uint64_t hk, int64_t ws) {
+  return ((uint32_t)(hk >> 32) ^ ((uint32_t)ws * 0xC2B2AE35u)) & ~3u;
+}
+
+// sub-pass of a group: 12 bits from hash bits 16..47 (below every partition bit, above the slot bits)
+__device__ __forceinline__ bool sub_ok(uint64_t hk, int64_t ws, int sbits, int sub) {
+  return sbits == 0 || (int)((((uint32_t)(hk >> 16) + (uint32_t)ws * 0x85EBCA77u) >> 20) & ((1u << sbits) - 1)) == sub;
 }
 
 __device__ __forceinline__ int64_t tile_of(int64_t b, int64_t nT) {
@@ -86,7 +126,8 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_hist(const int64_t* __restr
                                                           const uint8_t* __restrict__ rv, int64_t n, int64_t tile,
                                                           int log2P, int pad, int64_t nT, uint32_t* __restrict__ hist,
                                                           int64_t* __restrict__ tilemax, int64_t* __restrict__ tilemin,
-                                                          int64_t* __restrict__ tpart) {
+                                                          int64_t* __restrict__ tpart, int fbits,
+                                                          uint32_t* __restrict__ hcoarse) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint32_t* lh = (uint32_t*)smem;
   __shared__ int64_t lmax[PT_THREADS / 64];
@@ -138,6 +179,14 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_hist(const int64_t* __restr
   uint32_t* hrow = hist + t * (int64_t)P;
   // pad: each (tile, partition) run rounded up to whole 64-byte segments (4 records)
   for (int p = threadIdx.x; p < P; p += PT_THREADS) hrow[p] = pad ? (lh[p] + 3u) & ~3u : lh[p];
+  if (hcoarse) {  // two-level scatter: bucket b = partitions [b << fbits, (b + 1) << fbits)
+    const int B = P >> fbits;
+    for (int b = threadIdx.x; b < B; b += PT_THREADS) {
+      uint32_t c = 0;
+      for (int f = 0; f < (1 << fbits); f++) c += lh[(b << fbits) + ((f + b) & ((1 << fbits) - 1))];
+      hcoarse[t * (int64_t)B + b] = c;
+    }
+  }
   if (threadIdx.x == 0) {
     tilemax[t] = tot;
     tilemin[t] = -totmin;
@@ -178,12 +227,12 @@ __global__ __launch_bounds__(256) void k_part_colbase(int64_t* __restrict__ csum
 // hist[t][p] → absolute output offset of (tile t, partition p)
 __global__ __launch_bounds__(256) void k_part_colprefix(uint32_t* __restrict__ hist, int64_t nT, int P, int TC,
                                                         const int64_t* __restrict__ csum,
-                                                        const int64_t* __restrict__ pbase) {
+                                                        const int64_t* __restrict__ pbase, int pstride) {
   const int p = blockIdx.x * 256 + threadIdx.x;
   const int c = blockIdx.y;
   if (p >= P) return;
   const int64_t t0 = nT * c / TC, t1 = nT * (c + 1) / TC;
-  int64_t acc = pbase[p] + csum[(int64_t)c * P + p];
+  int64_t acc = pbase[(int64_t)p * pstride] + csum[(int64_t)c * P + p];
   for (int64_t t = t0; t < t1; t++) {
     const uint32_t v = hist[t * P + p];
     hist[t * P + p] = (uint32_t)acc;
@@ -219,8 +268,8 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
     const uint8_t* __restrict__ rv, ColPtrs cols, int n_cols, ColTypes ctypes, int64_t n, int64_t tile, int log2P,
     int pad, int64_t nT, const uint32_t* __restrict__ offs, const int64_t* __restrict__ pbase,
     const int64_t* __restrict__ tileprefix, const int64_t* __restrict__ tilemax,
-    const int64_t* __restrict__ tilemin, int windowed, int64_t size, int64_t adv, int64_t grace, RecLayout L,
-    uint64_t* __restrict__ srec, int64_t* __restrict__ tpart) {
+    const int64_t* __restrict__ tilemin, int windowed, int64_t size, int64_t adv, FastDiv fd, int64_t grace,
+    RecLayout L, uint64_t* __restrict__ srec, int64_t* __restrict__ tpart) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint32_t* cur = (uint32_t*)smem;
   __shared__ int64_t lmax[PT_THREADS / 64];
@@ -257,7 +306,11 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
       for (int u = 0; u < U; u++) {
         const int64_t i = i0 + u * PT_THREADS;
         if (!ok[u] || x[u] < 0 || !bit_get(kv, i) || !bit_get(rv, i)) continue;
-        const int64_t nwin = windowed ? (x[u] - first_window_start(x[u], size, adv)) / adv + 1 : 1;
+        // windows [ws0, floor(x/adv)*adv] step adv, ws0 = floor(max(0, x-size+adv)/adv)*adv
+        const int64_t lo = x[u] - size + adv;
+        const int64_t nwin =
+            windowed ? (int64_t)fast_udiv((uint64_t)x[u], fd) - (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), fd) + 1
+                     : 1;
         c_app += nwin;
         scatter_one(k[u], x[u], 0, i, log2P, cur, srec, L, cols, n_cols, ctypes, true);
       }
@@ -275,8 +328,8 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
       if (!valid) continue;
       int64_t jlo = 0, nwin = 1;
       if (windowed) {
-        const int64_t ws0 = first_window_start(x, size, adv);
-        nwin = (x - ws0) / adv + 1;
+        const int64_t ws0 = first_window_start_fd(x, size, adv, fd);
+        nwin = (int64_t)fast_udiv((uint64_t)(x - ws0), fd) + 1;
         // applied iff ws + size > st - grace  ⇔  ws >= st - grace - size + 1
         const int64_t wmin = st - grace - size + 1;
         if (wmin > ws0) jlo = (wmin - ws0 + adv - 1) / adv;
@@ -306,14 +359,53 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
   }
 }
 
+// Two-level scatter, pass B: block (bucket b, tile group g) moves the records that pass A
+// (k_part_scatter over the B = P >> fbits buckets) put in bucket b for tiles [t0, t1) — one
+// contiguous range, since pass A lays each bucket out tile-major — to their partitions' final
+// runs (cursors = the fine offsets of tile t0).  Every partition's run per group is G tiles
+// long, so the stores combine into whole lines where pass A alone would leave ~64-byte runs.
+template <int RW>
+__global__ __launch_bounds__(PT_THREADS) void k_part_refine(const uint64_t* __restrict__ srcA,
+                                                            const uint32_t* __restrict__ offA,
+                                                            const uint32_t* __restrict__ offs,
+                                                            const int64_t* __restrict__ pbase, int64_t nT, int G,
+                                                            int log2P, int fbits, uint64_t* __restrict__ srec) {
+  __shared__ uint32_t cur[1 << 12];
+  const int F = 1 << fbits, P = 1 << log2P, B = P >> fbits;
+  const int64_t ng = (nT + G - 1) / G;
+  const int b = (int)(blockIdx.x / ng);
+  const int64_t g = blockIdx.x % ng;
+  const int64_t t0 = g * G, t1 = t0 + G < nT ? t0 + G : nT;
+  for (int f = threadIdx.x; f < F; f += PT_THREADS) cur[f] = offs[t0 * P + ((int64_t)b << fbits) + f];
+  __syncthreads();
+  const int64_t lo = offA[t0 * B + b];
+  const int64_t hi = t1 < nT ? (int64_t)offA[t1 * B + b] : pbase[(int64_t)(b + 1) << fbits];
+  constexpr int U = 8;
+  for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += U * PT_THREADS) {
+    longlong2 r[U][RW / 2];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t i = i0 + (int64_t)u * PT_THREADS;
+#pragma unroll
+      for (int k = 0; k < RW / 2; k++)
+        r[u][k] = i < hi ? ((const longlong2*)(srcA + (uint64_t)i * RW))[k] : make_longlong2(0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t i = i0 + (int64_t)u * PT_THREADS;
+      if (i >= hi) continue;
+      const uint32_t f = part_of(r[u][0].x, log2P) & (uint32_t)(F - 1);
+      const uint32_t pos = atomicAdd(&cur[f], 1u);
+#pragma unroll
+      for (int k = 0; k < RW / 2; k++) ((longlong2*)(srec + (uint64_t)pos * RW))[k] = r[u][k];
+    }
+  }
+}
+
 // ------------------------------------------------------------------ k_part_agg
 // Work item: blockIdx.x = partition (work == nullptr), or work[blockIdx.x] =
 // p | sub_bits << 16 | sub << 20  (retry with 2^sub_bits sub-passes, sub_bits <= 12).
 // LDS: lref u32[H] | words i64[nwords][H]  (word 0 key, 1 ws, 2 rowtime, 3.. state)
-
-__device__ __forceinline__ bool part_sub_ok(uint64_t h, int sbits, int sub) {
-  return sbits == 0 || (int)((h >> 40) & ((1u << sbits) - 1)) == sub;
-}
 
 #define KLDS __attribute__((address_space(3)))
 typedef KLDS uint32_t lds_u32;
@@ -370,14 +462,18 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
                                                          uint8_t* __restrict__ fail,
                                                          unsigned long long* __restrict__ need, int64_t close0,
                                                          uint64_t* __restrict__ closed,
-                                                         unsigned long long* __restrict__ closed_n) {
+                                                         unsigned long long* __restrict__ closed_n,
+                                                         const int64_t* __restrict__ wr,
+                                                         unsigned long long* __restrict__ dbg) {
+#define AGG_T(k) do { if (dbg && threadIdx.x == 0) dbg[blockIdx.x * 6 + (k)] = wall_clock64(); } while (0)
+  AGG_T(0);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = q.H;
   lds_u32* lref = (lds_u32*)smem;
   lds_i64* lw = (lds_i64*)(smem + (((size_t)H * 4 + 15) & ~(size_t)15));
   volatile lds_u32* vlref = lref;
   volatile lds_i64* vlw = lw;
-  __shared__ int lused, lovf;
+  __shared__ int lovf;
   __shared__ int lcnt[AG_THREADS / 64];
   __shared__ unsigned long long lbase;
   uint32_t p;
@@ -404,15 +500,26 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
     rec[u] = li < rn ? r[0] : make_longlong2(0, -1);
     ext[u] = (wide && li < rn) ? r[1] : make_longlong2(0, 0);
   }
-  for (int e = threadIdx.x; e < H; e += AG_THREADS) {
-    lref[e] = 0;
-    for (int w = 0; w < q.nwords; w++) lw[w * H + e] = q.init.w[w];
+  // identity-CAS mode (the window range of this push fits the packed identity, wr[1]):
+  // plane 0 holds the 64-bit identities, every state word starts initialised, and a group
+  // is found or created by ONE 64-bit CAS — no claim/ready protocol, no spinning.
+  // Otherwise only the slot states are initialised and a claimer writes its entry's words.
+  const bool idm = wr[1] != 0;
+  const int64_t wbase = wr[0];
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+  if (idm) {
+    for (int i = threadIdx.x; i < H / 2; i += AG_THREADS) ((KLDS i64x2*)lw)[i] = i64x2{-1LL, -1LL};
+    for (int w = 2; w < q.nwords; w++) {
+      const int64_t v = q.init.w[w];
+      for (int i = threadIdx.x; i < H / 2; i += AG_THREADS) ((KLDS i64x2*)(lw + w * H))[i] = i64x2{v, v};
+    }
+  } else {
+    for (int i = threadIdx.x; i < H / 4; i += AG_THREADS) ((KLDS u32x4*)lref)[i] = u32x4{0u, 0u, 0u, 0u};
   }
-  if (threadIdx.x == 0) {
-    lused = 0;
-    lovf = 0;
-  }
+  if (threadIdx.x == 0) lovf = 0;
   __syncthreads();
+  AGG_T(1);
   // 1. resident rows of this partition (distinct groups: insert without comparing).  Rows of
   //    windows already closed before this push (ws + size <= close0) go to the closed store.
   const uint64_t* src = (sel[p] ? buf1 : buf0) + (uint64_t)p * q.cmax * q.sw;
@@ -424,7 +531,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
     int ne = 0;
     for (int64_t r = threadIdx.x; r < nrow; r += AG_THREADS) {
       const uint64_t* row = src + r * q.sw;
-      ne += ((int64_t)row[1] + q.size <= close0) && part_sub_ok(group_hash((int64_t)row[0], (int64_t)row[1]), sbits, sub);
+      ne += ((int64_t)row[1] + q.size <= close0) && sub_ok(key_hash((int64_t)row[0]), (int64_t)row[1], sbits, sub);
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int incl = ne;
@@ -444,7 +551,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
     uint64_t* dst = closed + (lbase + (uint64_t)(before + incl - ne)) * q.sw;
     for (int64_t r = threadIdx.x; r < nrow; r += AG_THREADS) {
       const uint64_t* row = src + r * q.sw;
-      if (!((int64_t)row[1] + q.size <= close0) || !part_sub_ok(group_hash((int64_t)row[0], (int64_t)row[1]), sbits, sub))
+      if (!((int64_t)row[1] + q.size <= close0) || !sub_ok(key_hash((int64_t)row[0]), (int64_t)row[1], sbits, sub))
         continue;
       for (int w = 0; w < q.sw; w++) dst[w] = row[w];
       dst += q.sw;
@@ -455,24 +562,49 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
     const uint64_t* row = src + r * q.sw;
     const int64_t key = (int64_t)row[0], ws = (int64_t)row[1];
     if (evict && ws + q.size <= close0) continue;
-    const uint64_t h = group_hash(key, ws);
-    if (!part_sub_ok(h, sbits, sub)) continue;
-    if (atomicAdd(&lused, 1) >= q.H_eff) {
+    const uint64_t hk = key_hash(key);
+    if (!sub_ok(hk, ws, sbits, sub)) continue;
+    uint32_t e = slot_of(hk, ws, H);
+    int probe = 0;
+    if (idm) {
+      const uint64_t id = ident_of(hk, (int64_t)fast_udiv((uint64_t)ws, q.fd) - wbase, q.log2P);
+      for (; probe < H; probe++) {
+        uint64_t expect = EMPTY_ID;
+        if (__hip_atomic_compare_exchange_strong((KLDS uint64_t*)&lw[e], &expect, id, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+          break;
+        e = (e + 1) & (uint32_t)(H - 1);
+      }
+      if (probe == H) {
+        lovf = 1;
+        break;
+      }
+      for (int w = 2; w < q.nwords; w++) lw[w * H + e] = (int64_t)row[w];
+      continue;
+    }
+    for (; probe < H; probe++) {
+      uint32_t expect = 0u;
+      if (__hip_atomic_compare_exchange_strong(&lref[e], &expect, fp_of(hk, ws) | L_READY, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP))
+        break;
+      e = (e + 1) & (uint32_t)(H - 1);
+    }
+    if (probe == H) {  // more resident groups than LDS slots: retry with sub-passes
       lovf = 1;
       break;
     }
-    int e = (int)(h & (uint64_t)(H - 1));
-    for (;;) {
-      uint32_t expect = 0u;
-      if (__hip_atomic_compare_exchange_strong(&lref[e], &expect, L_READY, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-      e = (e + 1) & (H - 1);
-    }
     for (int w = 0; w < q.nwords; w++) lw[w * H + e] = (int64_t)row[w];
   }
+  if (dbg) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
   __syncthreads();
-  // 2. this batch's records.  Entry states: 0 empty → L_CLAIM (CAS winner writes key/ws)
-  //    → L_READY (workgroup-scope release); a loser waits for READY (the winner is another
-  //    wave, or an earlier instruction of its own wave), then compares key/ws in LDS.
+  AGG_T(2);
+  // 2. this batch's records.  Slot states: 0 empty → L_CLAIM (the CAS winner writes key, ws
+  //    and the initial words) → L_READY; a loser waits for READY (the winner is another wave,
+  //    or an earlier instruction of its own wave), then compares key/ws in LDS.  A probe
+  //    sequence that wraps the whole table marks the partition for a retry with sub-passes.
   for (int64_t l0 = threadIdx.x; l0 < rn; l0 += AU * AG_THREADS) {
     if (*(volatile KLDS int*)&lovf) break;
     if (l0 != threadIdx.x) {
@@ -488,58 +620,97 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
     for (int u = 0; u < AU; u++) {  // unrolled: rec[]/ext[] stay in registers (no scratch)
       const int64_t t = rec[u].y;
       if (t < 0) continue;  // every window late (or past the end)
-      if (*(volatile KLDS int*)&lovf) continue;  // the partition will be retried: stop early
       const int64_t key = rec[u].x;
+      const uint64_t hk = key_hash(key);
       const int64_t gi = rbase + l0 + u * AG_THREADS;
       const uint32_t meta = q.meta_word == 2 ? (uint32_t)ext[u].x : 0u;
       const int64_t jlo = meta & 0xFFFFu;
       const uint32_t vmask = meta >> 16;
       const int64_t w3 = ext[u].y;
-      const int64_t ws_first = q.windowed ? first_window_start(t, q.size, q.adv) : 0;
-      for (int64_t ws = ws_first + jlo * q.adv; ws <= (q.windowed ? t : 0); ws += (q.windowed ? q.adv : 1)) {
-        const uint64_t h = group_hash(key, ws);
-        if (!part_sub_ok(h, sbits, sub)) continue;
-        int e = (int)(h & (uint64_t)(H - 1));
-        bool done = false;
-        for (int probe = 0; probe < H; probe++) {
-          if ((probe & 31) == 31 && *(volatile KLDS int*)&lovf) break;  // table overfull
+      int64_t ws = 0, wlast = 0, widx = 0;
+      if (q.windowed) {
+        int64_t lo = t - q.size + q.adv;
+        widx = (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), q.fd) + jlo;
+        ws = widx * q.adv;
+        wlast = t;
+      }
+      for (; ws <= wlast; ws += q.adv, widx++) {
+        if (!sub_ok(hk, ws, sbits, sub)) continue;
+        uint32_t e = slot_of(hk, ws, H);
+        if (idm) {
+          const uint64_t id = ident_of(hk, widx - wbase, q.log2P);
+          bool got = false;
+          for (int probe = 0; probe < H; probe++) {
+            uint64_t old = EMPTY_ID;
+            __hip_atomic_compare_exchange_strong((KLDS uint64_t*)&lw[e], &old, id, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (old == EMPTY_ID || old == id) {
+              got = true;
+              break;
+            }
+            e = (e + 1) & (uint32_t)(H - 1);
+          }
+          if (!got) {
+            lovf = 1;
+            break;
+          }
+          if (!(q.dbg_mode & 1)) lds_apply(q, lw, H, (int)e, t, vmask, srec, gi, w3);
+          continue;
+        }
+        const uint32_t fp = fp_of(hk, ws);
+        bool found = q.dbg_mode & 2;
+        for (int probe = 0; probe < H && !(q.dbg_mode & 2); probe++) {
+          // state, key and ws in one round trip (issue order = LDS service order: a READY
+          // state read before the key/ws reads guarantees they see the claimer's words)
           uint32_t v = vlref[e];
+          int64_t k0 = vlw[e], w0 = vlw[H + e];
           if (v == 0u) {
             uint32_t old = 0u;
-            __hip_atomic_compare_exchange_strong(&lref[e], &old, L_CLAIM, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_compare_exchange_strong(&lref[e], &old, fp | L_CLAIM, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
             if (old == 0u) {
-              if (atomicAdd(&lused, 1) >= q.H_eff) lovf = 1;
               vlw[e] = key;
               vlw[H + e] = ws;
+              for (int w = 2; w < q.nwords; w++) vlw[w * H + e] = q.init.w[w];
               // LDS serves one wave's requests in issue order: once READY is visible, so are
-              // key/ws.  Only the compiler must not reorder (no vmcnt/cache instruction needed).
+              // the entry's words.  Only the compiler must not reorder.
               __atomic_signal_fence(__ATOMIC_SEQ_CST);
-              vlref[e] = L_READY;
-              lds_apply(q, lw, H, e, t, vmask, srec, gi, w3);
-              done = true;
+              vlref[e] = fp | L_READY;
+              found = true;
               break;
             }
             v = old;
+            k0 = vlw[e];
+            w0 = vlw[H + e];
           }
-          for (int spin = 0; v == L_CLAIM; spin++) {  // bounded: the claimer is two stores away
-            __builtin_amdgcn_s_sleep(1);
-            v = vlref[e];
-            if (spin > (1 << 20)) { lovf = 1; break; }
+          if ((v & ~3u) == fp) {  // same fingerprint: maybe this group
+            if ((v & 3u) == L_CLAIM) {  // the claimer is a few stores away
+              for (int spin = 0; (v & 3u) == L_CLAIM && spin <= (1 << 20); spin++) {
+                __builtin_amdgcn_s_sleep(1);
+                v = vlref[e];
+              }
+              if ((v & 3u) == L_CLAIM) break;  // never expected: fail the partition rather than hang
+              __atomic_signal_fence(__ATOMIC_SEQ_CST);
+              k0 = vlw[e];  // read after READY was seen
+              w0 = vlw[H + e];
+            }
+            if (k0 == key && w0 == ws) {
+              found = true;
+              break;
+            }
           }
-          __atomic_signal_fence(__ATOMIC_SEQ_CST);
-          if (vlw[e] == key && vlw[H + e] == ws) {
-            lds_apply(q, lw, H, e, t, vmask, srec, gi, w3);
-            done = true;
-            break;
-          }
-          e = (e + 1) & (H - 1);
+          e = (e + 1) & (uint32_t)(H - 1);
         }
-        if (!done) lovf = 1;
-        if (!q.windowed) break;
+        if (!found) {
+          lovf = 1;
+          break;
+        }
+        if (!(q.dbg_mode & 1)) lds_apply(q, lw, H, (int)e, t, vmask, srec, gi, w3);
       }
     }
   }
   __syncthreads();
+  AGG_T(3);
   if (lovf) {
     if (threadIdx.x == 0) fail[p] |= 1;
     return;
@@ -548,7 +719,11 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
   const int per = (H + AG_THREADS - 1) / AG_THREADS;
   const int e0 = threadIdx.x * per, e1 = e0 + per < H ? e0 + per : H;
   int mine = 0;
-  for (int e = e0; e < e1; e++) mine += lref[e] != 0u;
+  if (idm) {
+    for (int e = e0; e < e1; e++) mine += (uint64_t)lw[e] != EMPTY_ID;
+  } else {
+    for (int e = e0; e < e1; e++) mine += lref[e] != 0u;
+  }
   // block exclusive scan of `mine`
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int incl = mine;
@@ -575,10 +750,90 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
   uint64_t* dst =
       (sel[p] ? buf0 : buf1) + (uint64_t)p * q.cmax * q.sw + (lbase + (uint64_t)(before + incl - mine)) * q.sw;
   for (int e = e0; e < e1; e++) {
-    if (lref[e] == 0u) continue;
-    for (int w = 0; w < q.sw; w++) dst[w] = w < q.nwords ? (uint64_t)lw[w * H + e] : 0ULL;
+    if (idm) {
+      const uint64_t id = (uint64_t)lw[e];
+      if (id == EMPTY_ID) continue;
+      const uint64_t hk = ((uint64_t)p << (64 - q.log2P)) | (id >> q.log2P);
+      dst[0] = (uint64_t)key_of_hash(hk);
+      dst[1] = (uint64_t)(((int64_t)(id & ((1ULL << q.log2P) - 1)) + wbase) * (q.windowed ? q.adv : 0));
+      for (int w = 2; w < q.sw; w++) dst[w] = w < q.nwords ? (uint64_t)lw[w * H + e] : 0ULL;
+    } else {
+      if (lref[e] == 0u) continue;
+      for (int w = 0; w < q.sw; w++) dst[w] = w < q.nwords ? (uint64_t)lw[w * H + e] : 0ULL;
+    }
     dst += q.sw;
   }
+  AGG_T(4);
+  if (dbg) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    AGG_T(5);
+  }
+#undef AGG_T
+}
+
+// Window-index range of this push for the packed identity: the batch's windows plus the
+// live resident ones (res = conservative [min, max] window index of resident rows; rows of
+// windows closed before this push are evicted before they are encoded).  wr = [wbase, ok].
+__global__ __launch_bounds__(1024) void k_part_wrange(const int64_t* __restrict__ tilemin,
+                                                      const int64_t* __restrict__ tilemax, int64_t nT, int windowed,
+                                                      int64_t size, int64_t adv, FastDiv fd, int64_t close0,
+                                                      int log2P, int fresh, int allow, int64_t* __restrict__ res,
+                                                      int64_t* __restrict__ wr) {
+  __shared__ int64_t smin[16], smax[16];
+  int64_t mn = INT64_MAX, mx = -1;
+  for (int64_t t = threadIdx.x; t < nT; t += 1024) {
+    mn = tilemin[t] < mn ? tilemin[t] : mn;
+    mx = tilemax[t] > mx ? tilemax[t] : mx;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const int64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    smin[threadIdx.x >> 6] = mn;
+    smax[threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x) return;
+  for (int w = 0; w < 16; w++) {
+    mn = smin[w] < mn ? smin[w] : mn;
+    mx = smax[w] > mx ? smax[w] : mx;
+  }
+  int64_t lo = INT64_MAX, hi = INT64_MIN;
+  if (mx >= 0) {  // some accepted record
+    if (windowed) {
+      const int64_t l = mn - size + adv;
+      lo = (int64_t)fast_udiv((uint64_t)(l > 0 ? l : 0), fd);
+      hi = (int64_t)fast_udiv((uint64_t)mx, fd);
+    } else {
+      lo = hi = 0;
+    }
+  }
+  if (!fresh) {
+    int64_t rlo = res[0];
+    const int64_t rhi = res[1];
+    if (windowed && close0 != INT64_MIN && rlo != INT64_MAX) {  // live: ws > close0 - size
+      const int64_t c = close0 - size;
+      const int64_t lb = c >= 0 ? (int64_t)fast_udiv((uint64_t)c, fd) + 1 : 0;
+      rlo = rlo > lb ? rlo : lb;
+    }
+    lo = rlo < lo ? rlo : lo;
+    hi = rhi > hi ? rhi : hi;
+  }
+  const bool fits = allow && log2P >= 1 && log2P < 63;
+  if (lo > hi) {  // nothing live, nothing new
+    wr[0] = 0;
+    wr[1] = fits;
+    res[0] = INT64_MAX;
+    res[1] = INT64_MIN;
+    return;
+  }
+  wr[0] = lo;
+  wr[1] = fits && hi - lo < ((int64_t)1 << log2P) - 1;
+  res[0] = lo;
+  res[1] = hi;
 }
 
 // Publish the partitions processed in this pass (all touched ones, or the retry list).
@@ -707,7 +962,8 @@ khip_status part_init(khip_agg* a, int64_t hint) {
   s.lds_bytes = (int)((((size_t)H * 4 + 15) & ~(size_t)15) + (size_t)H * 8 * used);
   // partitions: at most ~H_eff/2 groups each at the hinted size
   const int64_t groups = std::max<int64_t>(hint, 1024);
-  s.log2P = std::min(MAX_P_LOG2, std::max(0, part_ceil_log2(groups * 2 / s.H_eff)));
+  // at least 64 partitions: the packed identity then holds window ranges of up to 63
+  s.log2P = std::min(MAX_P_LOG2, std::max(6, part_ceil_log2(groups * 2 / s.H_eff)));
   if (const char* e = getenv("KHIP_PART_LOG2")) s.log2P = std::min(MAX_P_LOG2, atoi(e));
   s.P = 1LL << s.log2P;
   s.cmax = next_pow2(std::max<int64_t>(64, 2 * groups / s.P + 64));
@@ -746,7 +1002,7 @@ khip_status part_init(khip_agg* a, int64_t hint) {
 
 void part_release(khip_agg* a) {
   PartState& s = a->part;
-  DevBuf* bufs[] = {&s.closed, &s.closed_ctr, &s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist,
+  DevBuf* bufs[] = {&s.srecA, &s.hcoarse, &s.scan_tmpB, &s.RB, &s.wr, &s.res, &s.closed, &s.closed_ctr, &s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist,
                     &s.tilemax, &s.tilemin,
                     &s.tileprefix, &s.tpart, &s.scan_tmp, &s.srec, &s.work,
                     &s.pbase, &s.R, &s.ctr, &s.counts};
@@ -756,6 +1012,7 @@ void part_release(khip_agg* a) {
 khip_status part_reset(khip_agg* a) {
   PartState& s = a->part;
   s.closed_n = 0;
+  s.res_fresh = true;
   KHIP_TRY_HIP(hipMemsetAsync(s.cnt.p, 0, s.P * 8, a->stream));
   KHIP_TRY_HIP(hipMemsetAsync(s.newcnt.p, 0, s.P * 8, a->stream));
   KHIP_TRY_HIP(hipMemsetAsync(s.fail.p, 0, s.P, a->stream));
@@ -775,6 +1032,9 @@ static PartAggParams part_params(khip_agg* a) {
   for (int c = 0; c < MAX_COLS; c++) q.col_word[c] = s.col_word[c];
   q.size = a->desc.size_ms;
   q.adv = a->windowed ? a->desc.advance_ms : 1;
+  q.fd = make_fastdiv((uint64_t)q.adv);
+  q.dbg_mode = getenv("KHIP_AGG_MODE") ? atoi(getenv("KHIP_AGG_MODE")) : 0;
+  q.log2P = s.log2P;
   q.cmax = s.cmax;
   q.n_cols = a->desc.n_cols;
   q.n_ops = a->ap.n_ops;
@@ -849,6 +1109,25 @@ static khip_status part_split(khip_agg* a) {
   return KHIP_OK;
 }
 
+static void agg_probe_report(DevBuf& b, int nb) {
+  std::vector<unsigned long long> t((size_t)nb * 6 + 8);
+  if (hipMemcpy(t.data(), b.p, t.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+  unsigned long long lo = ~0ULL, hi = 0;
+  double ph[5] = {0, 0, 0, 0, 0};
+  int m = 0;
+  for (int i = 0; i < nb; i++) {
+    const unsigned long long* r = &t[(size_t)i * 6];
+    if (!r[0] || !r[5]) continue;
+    m++;
+    lo = std::min(lo, r[0]);
+    hi = std::max(hi, r[5]);
+    for (int k = 0; k < 5; k++) ph[k] += (double)(r[k + 1] - r[k]);
+  }
+  if (!m) return;
+  fprintf(stderr, "[agg probe] %d/%d wgs, span %.1f us, avg per wg (us): init %.2f resident %.2f records %.2f write %.2f drain %.2f\n",
+          m, nb, (hi - lo) / 100.0, ph[0] / m / 100, ph[1] / m / 100, ph[2] / m / 100, ph[3] / m / 100, ph[4] / m / 100);
+}
+
 // One push slice (n < 2^31).  tot[] receives the P_* counters.
 khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
                       const uint8_t* rv, const ColPtrs& cols, int64_t* tot) {
@@ -869,10 +1148,22 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   KHIP_TRY(s.tpart.ensure(nT * 8 * T_NPART));
   KHIP_TRY(s.scan_tmp.ensure((size_t)TC * P * 8));
   const int64_t ncap = pad ? n + 3 * (int64_t)P * nT : n;  // padded runs
+  // two-level scatter (pass A: B = P >> fbits buckets; pass B: partitions inside a bucket)
+  // once single-level runs get short (P large against the tile)
+  const char* s2 = getenv("KHIP_SCATTER2");
+  const bool lvl2 = !pad && s.log2P >= 11 && (s2 ? atoi(s2) != 0 : true);
+  const int fbits = lvl2 ? s.log2P - s.log2P / 2 : 0;
+  const int B = P >> fbits;
   if (s.scat_cap < ncap) {
     const int64_t n = ncap;
     KHIP_TRY(s.srec.ensure((size_t)n * s.rw * 8));  // AoS records
     s.scat_cap = ncap;
+  }
+  if (lvl2) {
+    KHIP_TRY(s.srecA.ensure((size_t)n * s.rw * 8));
+    KHIP_TRY(s.hcoarse.ensure((size_t)nT * B * 4));
+    KHIP_TRY(s.scan_tmpB.ensure((size_t)TC * B * 8));
+    KHIP_TRY(s.RB.ensure((size_t)(B + 1) * 8));
   }
   ColTypes ct{};
   for (int c = 0; c < MAX_COLS; c++) ct.t[c] = a->ap.col_type[c];
@@ -890,7 +1181,8 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   ev_record_part(a, 0);
   hipLaunchKernelGGL(k_part_hist, dim3(nT), dim3(PT_THREADS), hist_lds, a->stream, keys, ts, kv, rv, n, tile, s.log2P,
                      pad, nT,
-                     s.hist.as<uint32_t>(), s.tilemax.as<int64_t>(), s.tilemin.as<int64_t>(), s.tpart.as<int64_t>());
+                     s.hist.as<uint32_t>(), s.tilemax.as<int64_t>(), s.tilemin.as<int64_t>(), s.tpart.as<int64_t>(),
+                     fbits, lvl2 ? s.hcoarse.as<uint32_t>() : (uint32_t*)nullptr);
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, a->stream, s.tilemax.as<int64_t>(), nT,
                      s.tileprefix.as<int64_t>(), a->stream_time.as<int64_t>());
   // 2. offsets
@@ -903,23 +1195,58 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, a->stream, s.pbase.as<int64_t>(), (int64_t)P,
                      s.pbase.as<int64_t>() + P);
   hipLaunchKernelGGL(k_part_colprefix, dim3(ceil_div(P, 256), TC), dim3(256), 0, a->stream, s.hist.as<uint32_t>(), nT,
-                     P, TC, s.scan_tmp.as<int64_t>(), s.pbase.as<int64_t>());
+                     P, TC, s.scan_tmp.as<int64_t>(), s.pbase.as<int64_t>(), 1);
+  if (lvl2) {  // bucket b's region = its partitions' regions [pbase[b << fbits], pbase[(b + 1) << fbits])
+    hipLaunchKernelGGL(k_part_colsum, dim3(ceil_div(B, 256), TC), dim3(256), 0, a->stream, s.hcoarse.as<uint32_t>(), nT,
+                       B, TC, s.scan_tmpB.as<int64_t>());
+    hipLaunchKernelGGL(k_part_colbase, dim3(ceil_div(B, 256)), dim3(256), 0, a->stream, s.scan_tmpB.as<int64_t>(), B, TC,
+                       s.RB.as<int64_t>());
+    hipLaunchKernelGGL(k_part_colprefix, dim3(ceil_div(B, 256), TC), dim3(256), 0, a->stream, s.hcoarse.as<uint32_t>(),
+                       nT, B, TC, s.scan_tmpB.as<int64_t>(), s.pbase.as<int64_t>(), 1 << fbits);
+  }
   ev_record_part(a, 1);
   // 3. scatter
   const char* su = getenv("KHIP_SCATTER_U");
   const int U = su ? atoi(su) : 16;
   auto scat = U >= 16 ? k_part_scatter<16> : (U >= 8 ? k_part_scatter<8> : k_part_scatter<4>);
-  hipLaunchKernelGGL(scat, dim3(nT), dim3(PT_THREADS), hist_lds, a->stream, keys, ts, kv, rv, cols,
-                     a->desc.n_cols, ct, n, tile, s.log2P, pad, nT, s.hist.as<uint32_t>(), s.pbase.as<int64_t>(),
+  hipLaunchKernelGGL(scat, dim3(nT), dim3(PT_THREADS), lvl2 ? (size_t)B * 4 : hist_lds, a->stream, keys, ts, kv, rv,
+                     cols, a->desc.n_cols, ct, n, tile, s.log2P - fbits, pad, nT,
+                     lvl2 ? s.hcoarse.as<uint32_t>() : s.hist.as<uint32_t>(), s.pbase.as<int64_t>(),
                      s.tileprefix.as<int64_t>(),
                      s.tilemax.as<int64_t>(), s.tilemin.as<int64_t>(), a->windowed, a->desc.size_ms,
-                     a->windowed ? a->desc.advance_ms : 1, a->grace, L, s.srec.as<uint64_t>(),
+                     a->windowed ? a->desc.advance_ms : 1, make_fastdiv(a->windowed ? a->desc.advance_ms : 1),
+                     a->grace, L, lvl2 ? s.srecA.as<uint64_t>() : s.srec.as<uint64_t>(),
                      s.tpart.as<int64_t>());
   KHIP_TRY_HIP(hipGetLastError());
+  if (lvl2) {
+    const char* ge = getenv("KHIP_REFINE_RECS");
+    const int64_t per_blk = ge ? atoll(ge) : 32768;
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(nT, per_blk * B / tile));
+    const int64_t ng = ceil_div(nT, G);
+    void (*ref)(const uint64_t*, const uint32_t*, const uint32_t*, const int64_t*, int64_t, int, int, int, uint64_t*);
+    switch (s.rw) {
+      case 2: ref = k_part_refine<2>; break;
+      case 4: ref = k_part_refine<4>; break;
+      case 6: ref = k_part_refine<6>; break;
+      case 8: ref = k_part_refine<8>; break;
+      case 10: ref = k_part_refine<10>; break;
+      default: ref = k_part_refine<12>; break;
+    }
+    hipLaunchKernelGGL(ref, dim3((unsigned)(B * ng)), dim3(PT_THREADS), 0, a->stream, s.srecA.as<uint64_t>(),
+                       s.hcoarse.as<uint32_t>(), s.hist.as<uint32_t>(), s.pbase.as<int64_t>(), nT, G, s.log2P, fbits,
+                       s.srec.as<uint64_t>());
+    KHIP_TRY_HIP(hipGetLastError());
+  }
   ev_record_part(a, 2);
   // 4. aggregate partitions (+ retries)
   const PartAggParams q0 = part_params(a);
   const int64_t close0 = (a->windowed && a->host_stream_time >= 0) ? a->host_stream_time - a->grace : INT64_MIN;
+  KHIP_TRY(s.wr.ensure(16));
+  KHIP_TRY(s.res.ensure(16));
+  hipLaunchKernelGGL(k_part_wrange, dim3(1), dim3(1024), 0, a->stream, s.tilemin.as<int64_t>(), s.tilemax.as<int64_t>(),
+                     nT, a->windowed, a->desc.size_ms, q0.adv, q0.fd, close0, s.log2P, s.res_fresh ? 1 : 0,
+                     (a->desc.flags & KHIP_FLAG_PART_CLAIM) ? 0 : 1, s.res.as<int64_t>(), s.wr.as<int64_t>());
+  s.res_fresh = false;
   if (a->windowed) {  // worst case every live row closes in this push
     const int64_t live = a->occ - s.closed_n;
     if (s.closed_cap < s.closed_n + live) {
@@ -950,8 +1277,18 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     KHIP_TRY(s.work.ensure(work.size() * 4));
     KHIP_TRY_HIP(hipMemcpyAsync(s.work.p, work.data(), work.size() * 4, hipMemcpyHostToDevice, a->stream));
   }
+  // KHIP_AGG_PROBE=1: per-workgroup phase timestamps of pass 0 (wall clock, 100 MHz) → stderr
+  static const bool probe = getenv("KHIP_AGG_PROBE") != nullptr;
+  DevBuf dbgbuf;
+  unsigned long long* dbg = nullptr;
   for (int pass = 0;; pass++) {
     PartAggParams q = q0;
+    dbg = nullptr;
+    if (probe && pass == 0) {
+      KHIP_TRY(dbgbuf.ensure((size_t)std::max<int64_t>(P, (int64_t)work.size()) * 6 * 8 + 64));
+      KHIP_TRY_HIP(hipMemsetAsync(dbgbuf.p, 0, dbgbuf.bytes, a->stream));
+      dbg = dbgbuf.as<unsigned long long>();
+    }
     q.cmax = s.cmax;
     KHIP_TRY_HIP(hipMemsetAsync(s.ctr.p, 0, 24, a->stream));
     const uint32_t* wk = (pass == 0 && !subs0) ? nullptr : s.work.as<uint32_t>();
@@ -962,7 +1299,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                        s.buf[1].as<uint64_t>(), s.sel.as<uint8_t>(), s.cnt.as<int64_t>(),
                        s.newcnt.as<unsigned long long>(), s.fail.as<uint8_t>(),
                        s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
-                       s.closed_ctr.as<unsigned long long>());
+                       s.closed_ctr.as<unsigned long long>(), s.wr.as<int64_t>(), dbg);
     const int nl = pass == 0 ? P : (int)plist.size();
     hipLaunchKernelGGL(k_part_commit, dim3(ceil_div(std::max(nl, 1), 256)), dim3(256), 0, a->stream, P,
                        s.pbase.as<int64_t>(), pass == 0 ? nullptr : s.work.as<uint32_t>() + work.size(), nl,
@@ -974,6 +1311,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     KHIP_TRY_HIP(hipMemcpyAsync(c2, s.ctr.p, 24, hipMemcpyDeviceToHost, a->stream));
     KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
     added_total += (int64_t)c2[0];
+    if (dbg) agg_probe_report(dbgbuf, (int)((pass == 0 && !subs0) ? P : (int64_t)work.size()));
     if (c2[1] == 0) break;
     if (pass > 24) return fail(KHIP_E_DEVICE, "partitioned aggregation could not place the batch");
     // retry the failed partitions: LDS overflow → twice the sub-passes; region overflow → grow

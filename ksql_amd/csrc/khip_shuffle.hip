@@ -21,11 +21,6 @@
 
 namespace khip {
 
-// partitioned-engine column prefix kernels (khip_agg_part.hip)
-__global__ void k_part_colsum(const uint32_t* __restrict__ hist, int64_t nT, int P, int TC, int64_t* __restrict__ csum);
-__global__ void k_part_colbase(int64_t* __restrict__ csum, int P, int TC, int64_t* __restrict__ R);
-__global__ void k_part_colprefix(uint32_t* __restrict__ hist, int64_t nT, int P, int TC,
-                                 const int64_t* __restrict__ csum, const int64_t* __restrict__ pbase);
 
 constexpr int SH_THREADS = 256;
 constexpr int SH_ITEMS = 16;
@@ -258,7 +253,7 @@ khip_status khip_shuffle_pack(khip_shuffle* s, const khip_batch* b, uint64_t* se
   hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s->stream, s->pbase.as<int64_t>(), (int64_t)N,
                      s->pbase.as<int64_t>() + N);
   hipLaunchKernelGGL(k_part_colprefix, dim3(ceil_div(N, 256), TC), dim3(256), 0, s->stream, s->hist.as<uint32_t>(), nT,
-                     N, TC, s->csum.as<int64_t>(), s->pbase.as<int64_t>());
+                     N, TC, s->csum.as<int64_t>(), s->pbase.as<int64_t>(), 1);
   KHIP_TRY_HIP(hipGetLastError());
   std::vector<int64_t> R(N);
   KHIP_TRY_HIP(hipMemcpyAsync(R.data(), s->R.p, N * 8, hipMemcpyDeviceToHost, s->stream));

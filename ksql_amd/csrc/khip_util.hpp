@@ -151,6 +151,43 @@ __host__ __device__ inline int64_t first_window_start(int64_t ts, int64_t size, 
   return (lo / adv) * adv;
 }
 
+// Unsigned 64-bit division by a launch-constant divisor without the ~50-instruction
+// software divide: Granlund & Montgomery, "Division by Invariant Integers using
+// Multiplication" (1994), Fig. 4.1.  l = ceil(log2 d), m = floor(2^64 (2^l - d) / d) + 1,
+// q = (t + ((n - t) >> min(l,1))) >> max(l-1,0), t = mulhi(m, n).  Exact for all n, d >= 1.
+struct FastDiv {
+  uint64_t m;
+  uint32_t sh1, sh2;
+};
+
+inline FastDiv make_fastdiv(uint64_t d) {
+  uint32_t l = 0;
+  while (l < 64 && (1ULL << l) < d) l++;
+  const unsigned __int128 two_l = (unsigned __int128)1 << l;
+  const unsigned __int128 num = ((unsigned __int128)1 << 64) * (two_l - d);
+  FastDiv f;
+  f.m = (uint64_t)(num / d) + 1;
+  f.sh1 = l < 1 ? l : 1;
+  f.sh2 = l > 1 ? l - 1 : 0;
+  return f;
+}
+
+__host__ __device__ inline uint64_t fast_udiv(uint64_t n, const FastDiv& f) {
+#ifdef __HIP_DEVICE_COMPILE__
+  const uint64_t t = __umul64hi(f.m, n);
+#else
+  const uint64_t t = (uint64_t)(((unsigned __int128)f.m * n) >> 64);
+#endif
+  return (t + ((n - t) >> f.sh1)) >> f.sh2;
+}
+
+// first_window_start with the division by `adv` done through `fd` (= make_fastdiv(adv)).
+__host__ __device__ inline int64_t first_window_start_fd(int64_t ts, int64_t size, int64_t adv, const FastDiv& fd) {
+  int64_t lo = ts - size + adv;
+  if (lo < 0) lo = 0;
+  return (int64_t)fast_udiv((uint64_t)lo, fd) * adv;
+}
+
 inline int64_t next_pow2(int64_t v) {
   int64_t p = 1;
   while (p < v) p <<= 1;

@@ -32,7 +32,7 @@ def orc():
     return abi.load_oracle()
 
 
-ENGINES = {"part": 0, "atomic": abi.FLAG_ENGINE_ATOMIC}
+ENGINES = {"part": 0, "part_claim": abi.FLAG_PART_CLAIM, "atomic": abi.FLAG_ENGINE_ATOMIC}
 
 
 @pytest.fixture(params=list(ENGINES), scope="module")
@@ -193,6 +193,19 @@ def test_table_growth_and_resume(prod, orc, engine):
                for i in range(3)]
     kw = dict(WINDOWS[3], key_type="INT64", col_types=["INT32", "INT64", "DOUBLE", "DOUBLE"], aggs=ALL_AGGS,
               capacity_hint=16)
+    (g, gs, desc), (o, os_, _) = _run_both(prod, orc, kw, batches, engine=engine)
+    assert gs == os_
+    assert_snap_equal(g, o, desc, ABS_SUM)
+
+
+@pytest.mark.parametrize("win", [0, 1, 3])
+def test_many_partitions_vs_oracle(prod, orc, win, engine):
+    # a large capacity hint gives 2^14 partitions: two-level scatter (buckets → partitions)
+    # and, while the window range fits, the packed-identity CAS; 3 pushes with eviction
+    rng = np.random.default_rng(77 + win)
+    batches = [_random_batch(rng, 150_000, "INT64", 40_000, 300_000, 20_000, t0=b * 200_000) for b in range(3)]
+    kw = dict(WINDOWS[win], key_type="INT64", col_types=["INT32", "INT64", "DOUBLE", "DOUBLE"], aggs=ALL_AGGS,
+              capacity_hint=30_000_000)
     (g, gs, desc), (o, os_, _) = _run_both(prod, orc, kw, batches, engine=engine)
     assert gs == os_
     assert_snap_equal(g, o, desc, ABS_SUM)
