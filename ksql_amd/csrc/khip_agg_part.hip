@@ -262,14 +262,14 @@ __device__ __forceinline__ void scatter_one(int64_t key, int64_t x, int64_t jlo,
   }
 }
 
-template <int U>
+template <int U, bool NARROW>
 __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
     const int64_t* __restrict__ keys, const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
     const uint8_t* __restrict__ rv, ColPtrs cols, int n_cols, ColTypes ctypes, int64_t n, int64_t tile, int log2P,
     int pad, int64_t nT, const uint32_t* __restrict__ offs, const int64_t* __restrict__ pbase,
     const int64_t* __restrict__ tileprefix, const int64_t* __restrict__ tilemax,
     const int64_t* __restrict__ tilemin, int windowed, int64_t size, int64_t adv, FastDiv fd, int64_t grace,
-    RecLayout L, uint64_t* __restrict__ srec, int64_t* __restrict__ tpart) {
+    RecLayout L, uint64_t* __restrict__ srec, int64_t dummy, int64_t* __restrict__ tpart) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint32_t* cur = (uint32_t*)smem;
   __shared__ int64_t lmax[PT_THREADS / 64];
@@ -288,7 +288,52 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
   const int64_t smax = carry > tilemax[t] ? carry : tilemax[t];
   const int64_t tmin = tilemin[t];
   const bool fast = !windowed || tmin == INT64_MAX || first_window_start(tmin, size, adv) + size > smax - grace;
-  if (fast) {
+  if (fast && NARROW) {
+    // 16-byte (key, ts) records: straight-line steps (no branch around a load or store, so
+    // every wait is counted), next step's loads issued before this step's cursors/stores;
+    // rejected or out-of-range lanes store to the dummy record
+    int64_t x[U], k[U], nxx[U], nxk[U];
+    auto load_step = [&](int64_t i0, int64_t (&dx)[U], int64_t (&dk)[U]) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        int64_t i = i0 + (int64_t)u * PT_THREADS;
+        i = i < end ? i : end - 1;
+        dx[u] = ts[i];
+        dk[u] = keys[i];
+      }
+    };
+    int64_t i0 = base + threadIdx.x;
+    if (i0 < end) load_step(i0, x, k);
+    for (; i0 < end; i0 += U * PT_THREADS) {
+      const int64_t in = i0 + U * PT_THREADS;
+      if (in < end) load_step(in, nxx, nxk);
+      uint32_t pos[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int64_t i = i0 + (int64_t)u * PT_THREADS;
+        const bool ok = i < end && x[u] >= 0 && bit_get(kv, i) && bit_get(rv, i);
+        if (windowed) {
+          const int64_t lo = x[u] - size + adv;
+          c_app += ok ? (int64_t)fast_udiv((uint64_t)x[u], fd) - (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), fd) + 1
+                      : 0;
+        } else {
+          c_app += ok ? 1 : 0;
+        }
+        pos[u] = atomicAdd(&cur[part_of(k[u], log2P)], ok ? 1u : 0u);
+        if (!ok) pos[u] = 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t dst = pos[u] == 0xFFFFFFFFu ? (uint64_t)dummy : (uint64_t)pos[u];
+        *(longlong2*)(srec + dst * 2) = make_longlong2(k[u], x[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        x[u] = nxx[u];
+        k[u] = nxk[u];
+      }
+    }
+  } else if (fast) {
     // U records per thread per step: the loads of a step are issued together, and since
     // vmcnt retires loads and stores in issue order, fewer steps = fewer waits behind the
     // previous step's scattered stores
@@ -369,7 +414,8 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_refine(const uint64_t* __re
                                                             const uint32_t* __restrict__ offA,
                                                             const uint32_t* __restrict__ offs,
                                                             const int64_t* __restrict__ pbase, int64_t nT, int G,
-                                                            int log2P, int fbits, uint64_t* __restrict__ srec) {
+                                                            int log2P, int fbits, int64_t dummy,
+                                                            uint64_t* __restrict__ srec, int mode) {
   __shared__ uint32_t cur[1 << 12];
   const int F = 1 << fbits, P = 1 << log2P, B = P >> fbits;
   const int64_t ng = (nT + G - 1) / G;
@@ -380,25 +426,46 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_refine(const uint64_t* __re
   __syncthreads();
   const int64_t lo = offA[t0 * B + b];
   const int64_t hi = t1 < nT ? (int64_t)offA[t1 * B + b] : pbase[(int64_t)(b + 1) << fbits];
-  constexpr int U = 8;
-  for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += U * PT_THREADS) {
-    longlong2 r[U][RW / 2];
+  if (hi <= lo) return;
+  // Straight-line steps (no branch around a load, so the waits stay counted): U records
+  // per thread; the next step's loads are issued before this step's LDS cursors and
+  // stores; out-of-range lanes load a clamped index and store to the dummy record.
+  constexpr int U = RW <= 2 ? 8 : (RW <= 4 ? 4 : (RW <= 8 ? 2 : 1));  // ~64 VGPRs of records in flight
+  constexpr int H2 = RW / 2;
+  longlong2 r[U][H2], nx[U][H2];
+  auto load_step = [&](int64_t i0, longlong2 (&d)[U][H2]) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int64_t i = i0 + (int64_t)u * PT_THREADS;
+      int64_t i = i0 + (int64_t)u * PT_THREADS;
+      i = i < hi ? i : hi - 1;
 #pragma unroll
-      for (int k = 0; k < RW / 2; k++)
-        r[u][k] = i < hi ? ((const longlong2*)(srcA + (uint64_t)i * RW))[k] : make_longlong2(0, 0);
+      for (int k = 0; k < H2; k++) d[u][k] = ((const longlong2*)(srcA + (uint64_t)i * RW))[k];
     }
+  };
+  int64_t i0 = lo + threadIdx.x;
+  load_step(i0, r);
+  for (; i0 < hi; i0 += U * PT_THREADS) {
+    const int64_t in = i0 + U * PT_THREADS;
+    if (in < hi) load_step(in, nx);
+    uint32_t pos[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int64_t i = i0 + (int64_t)u * PT_THREADS;
-      if (i >= hi) continue;
+      const bool ok = i0 + (int64_t)u * PT_THREADS < hi;
       const uint32_t f = part_of(r[u][0].x, log2P) & (uint32_t)(F - 1);
-      const uint32_t pos = atomicAdd(&cur[f], 1u);
-#pragma unroll
-      for (int k = 0; k < RW / 2; k++) ((longlong2*)(srec + (uint64_t)pos * RW))[k] = r[u][k];
+      pos[u] = atomicAdd(&cur[f], ok ? 1u : 0u);
+      if (!ok) pos[u] = 0xFFFFFFFFu;
     }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      uint64_t dst = pos[u] == 0xFFFFFFFFu ? (uint64_t)dummy : (uint64_t)pos[u];
+      if (mode == 1) dst = pos[u] == 0xFFFFFFFFu ? (uint64_t)dummy : (uint64_t)(i0 + (int64_t)u * PT_THREADS);
+#pragma unroll
+      for (int k = 0; k < H2; k++) ((longlong2*)(srec + dst * RW))[k] = r[u][k];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int k = 0; k < H2; k++) r[u][k] = nx[u][k];
   }
 }
 
@@ -1156,11 +1223,11 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   const int B = P >> fbits;
   if (s.scat_cap < ncap) {
     const int64_t n = ncap;
-    KHIP_TRY(s.srec.ensure((size_t)n * s.rw * 8));  // AoS records
+    KHIP_TRY(s.srec.ensure((size_t)(n + 1) * s.rw * 8));  // AoS records (+1: dummy store target)
     s.scat_cap = ncap;
   }
   if (lvl2) {
-    KHIP_TRY(s.srecA.ensure((size_t)n * s.rw * 8));
+    KHIP_TRY(s.srecA.ensure((size_t)(n + 1) * s.rw * 8));
     KHIP_TRY(s.hcoarse.ensure((size_t)nT * B * 4));
     KHIP_TRY(s.scan_tmpB.ensure((size_t)TC * B * 8));
     KHIP_TRY(s.RB.ensure((size_t)(B + 1) * 8));
@@ -1207,23 +1274,26 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   ev_record_part(a, 1);
   // 3. scatter
   const char* su = getenv("KHIP_SCATTER_U");
-  const int U = su ? atoi(su) : 16;
-  auto scat = U >= 16 ? k_part_scatter<16> : (U >= 8 ? k_part_scatter<8> : k_part_scatter<4>);
+  const bool narrow = s.rw == 2;
+  const int U = su ? atoi(su) : (narrow ? 8 : 16);
+  auto scat = narrow ? (U >= 16 ? k_part_scatter<16, true> : (U >= 8 ? k_part_scatter<8, true> : k_part_scatter<4, true>))
+                     : (U >= 16 ? k_part_scatter<16, false> : (U >= 8 ? k_part_scatter<8, false> : k_part_scatter<4, false>));
   hipLaunchKernelGGL(scat, dim3(nT), dim3(PT_THREADS), lvl2 ? (size_t)B * 4 : hist_lds, a->stream, keys, ts, kv, rv,
                      cols, a->desc.n_cols, ct, n, tile, s.log2P - fbits, pad, nT,
                      lvl2 ? s.hcoarse.as<uint32_t>() : s.hist.as<uint32_t>(), s.pbase.as<int64_t>(),
                      s.tileprefix.as<int64_t>(),
                      s.tilemax.as<int64_t>(), s.tilemin.as<int64_t>(), a->windowed, a->desc.size_ms,
                      a->windowed ? a->desc.advance_ms : 1, make_fastdiv(a->windowed ? a->desc.advance_ms : 1),
-                     a->grace, L, lvl2 ? s.srecA.as<uint64_t>() : s.srec.as<uint64_t>(),
+                     a->grace, L, lvl2 ? s.srecA.as<uint64_t>() : s.srec.as<uint64_t>(), ncap,
                      s.tpart.as<int64_t>());
   KHIP_TRY_HIP(hipGetLastError());
   if (lvl2) {
     const char* ge = getenv("KHIP_REFINE_RECS");
-    const int64_t per_blk = ge ? atoll(ge) : 32768;
+    const int64_t per_blk = ge ? atoll(ge) : 8192;  // measured: 8K records per block (1 KB runs) beat 32K
     const int G = (int)std::max<int64_t>(1, std::min<int64_t>(nT, per_blk * B / tile));
     const int64_t ng = ceil_div(nT, G);
-    void (*ref)(const uint64_t*, const uint32_t*, const uint32_t*, const int64_t*, int64_t, int, int, int, uint64_t*);
+    void (*ref)(const uint64_t*, const uint32_t*, const uint32_t*, const int64_t*, int64_t, int, int, int, int64_t,
+                uint64_t*, int);
     switch (s.rw) {
       case 2: ref = k_part_refine<2>; break;
       case 4: ref = k_part_refine<4>; break;
@@ -1234,7 +1304,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     }
     hipLaunchKernelGGL(ref, dim3((unsigned)(B * ng)), dim3(PT_THREADS), 0, a->stream, s.srecA.as<uint64_t>(),
                        s.hcoarse.as<uint32_t>(), s.hist.as<uint32_t>(), s.pbase.as<int64_t>(), nT, G, s.log2P, fbits,
-                       s.srec.as<uint64_t>());
+                       ncap, s.srec.as<uint64_t>(), getenv("KHIP_REFINE_MODE") ? atoi(getenv("KHIP_REFINE_MODE")) : 0);
     KHIP_TRY_HIP(hipGetLastError());
   }
   ev_record_part(a, 2);

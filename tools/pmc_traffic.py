@@ -16,7 +16,7 @@ import sys
 from collections import defaultdict
 
 PUSH = ["k_part_hist", "k_part_colsum", "k_part_colbase", "k_part_colprefix", "k_scan_blocks", "k_scan_excl",
-        "k_part_scatter", "k_part_agg", "k_part_commit"]
+        "k_part_scatter", "k_part_refine", "k_part_wrange", "k_part_agg", "k_part_commit"]
 
 
 def load(path, counter):
