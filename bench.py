@@ -49,8 +49,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     ap.add_argument("--engine", choices=["part", "atomic"], default="part")
-    ap.add_argument("--config", choices=["possible_fraud", "repartition_sum"], default="possible_fraud",
-                    help="possible_fraud = BASELINE configs[1] (the headline); repartition_sum = configs[4]")
+    ap.add_argument("--config", choices=["possible_fraud", "hopping_double", "clickstream_join", "repartition_sum"],
+                    default="possible_fraud",
+                    help="possible_fraud = BASELINE configs[1] (the headline); hopping_double = configs[2]; "
+                         "clickstream_join = configs[3]; repartition_sum = configs[4]")
+    ap.add_argument("--slice", type=int, default=1 << 27, help="hopping_double: records per micro-batch push")
+    ap.add_argument("--users", type=int, default=100_000_000, help="clickstream_join: table rows")
     return ap.parse_args()
 
 
@@ -108,6 +112,10 @@ def main():
     lib = abi.load_product()
     if args.config == "repartition_sum":
         return bench_repartition(args, lib, rank, world, local)
+    if args.config == "hopping_double":
+        return bench_hopping_double(args, lib, rank, world, local)
+    if args.config == "clickstream_join":
+        return bench_join(args, lib, rank, world, local)
 
     n = args.records
     card, ts = synth.possible_fraud(0, n, n, xp="torch", device="cuda", rank=rank, world=world, keys=args.keys)
@@ -209,6 +217,217 @@ def main():
     h.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def stream_copy_gbs(nbytes=1 << 31):
+    """Achievable HBM rate on this box: one device-to-device copy of `nbytes` (read + write
+    bytes / time), the practical ceiling next to the 8 TB/s spec peak."""
+    import torch
+    a = torch.empty(nbytes // 8, dtype=torch.int64, device="cuda")
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 5
+    del a, b
+    return 2.0 * nbytes / (ms / 1000.0) / 1e9
+
+
+def barrier_sync(world):
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(elapsed, world):
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def finish(world):
+    import torch.distributed as dist
+    if world > 1:
+        dist.destroy_process_group()
+
+
+BYTES_PER_RECORD_C3 = 24.125 + 6 * 2 * 56  # SURVEY.md §8(d): W_in + F x 2 x S_slot = 696.1
+
+
+def bench_hopping_double(args, lib, rank, world, local):
+    """C3: HOPPING (SIZE 1 MINUTE, ADVANCE BY 10 SECONDS, GRACE PERIOD 1 MINUTE) SUM/AVG/MIN/MAX
+    of a DOUBLE with 1 % nulls, 1e9 records (1 h of event time) per GPU, key BIGINT in [0, 1e5).
+    One step = a fresh query instance: reset, the 1e9 device-resident records pushed as
+    event-time micro-batches of `--slice` records (closed windows leave the live table between
+    pushes), and the materialized row count."""
+    import torch
+    from ksql_amd import abi, synth
+    n = args.records if args.records != 100_000_000 else 1_000_000_000
+    S = max(8, args.slice // 8 * 8)
+    cfg = synth.CONFIGS["hopping_double"]
+    key, ts, val, valid = synth.hopping_double(0, n, n, xp="torch", device="cuda", rank=rank, world=world)
+    vb = abi.bitmap_torch(valid)
+    del valid
+    torch.cuda.synchronize()
+    batches = [abi.DeviceBatch(ts[lo:min(lo + S, n)], keys=key[lo:min(lo + S, n)], cols=[val[lo:min(lo + S, n)]],
+                               col_valid=[vb[lo // 8:(min(lo + S, n) + 7) // 8]]) for lo in range(0, n, S)]
+    keys_here = cfg["keys"] // world
+    span_push = cfg["span_ms"] * S / n
+    live = int(keys_here * (span_push + cfg["size_ms"] + cfg["grace_ms"] + cfg["disorder_ms"]) / cfg["advance_ms"])
+    desc = abi.make_agg_desc(window_kind="HOPPING", size_ms=cfg["size_ms"], advance_ms=cfg["advance_ms"],
+                             grace_ms=cfg["grace_ms"], key_type="INT64", col_types=["DOUBLE"],
+                             aggs=[("SUM", 0), ("AVG", 0), ("MIN", 0), ("MAX", 0)], device=local,
+                             capacity_hint=live, flags=abi.FLAG_PROFILE)
+    h = abi.AggHandle(lib, desc)
+
+    def step():
+        h.reset()
+        tot = {"rows_accepted": 0, "windows_applied": 0, "windows_late": 0}
+        for b in batches:
+            st = h.push(b)
+            for k in tot:
+                tot[k] += st[k]
+        return tot, h.count_rows(None)
+
+    for _ in range(max(args.warmup, 1)):
+        st, groups = step()
+    h.kernel_times(reset=True)
+    barrier_sync(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st, groups = step()
+    barrier_sync(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    kt = h.kernel_times()
+    if rank == 0:
+        ms_step = elapsed * 1000.0 / args.steps
+        phase = {k: kt[k] / args.steps for k in ("stream_time_ms", "partition_ms", "apply_ms", "finalize_ms")}
+        push_ms = sum(phase.values())  # device time of every kernel of the step's pushes (HIP events)
+        achieved = BYTES_PER_RECORD_C3 * n / (push_ms / 1000.0) / 1e9
+        out = {
+            "metric": "records/sec, windowed GROUP BY (SUM/AVG/MIN/MAX(value DOUBLE) HOPPING 60 s / 10 s GROUP BY key)",
+            "value": world * n * args.steps / elapsed, "unit": "records/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (splitmix64, ksql_amd/synth.py hopping_double), device-resident columnar batch",
+            "config": {"workload": "hopping_double", "records_per_gpu": n, "keys_per_gpu": keys_here,
+                       "window": "HOPPING 60s/10s GRACE 60s (F=6)", "micro_batch": S, "pushes": len(batches),
+                       "windows_applied": st["windows_applied"], "windows_late": st["windows_late"],
+                       "groups_per_gpu": int(groups), "parallelism": "key-hash shards x%d" % world},
+            "roofline": {"bound": "hbm", "kernel": "khip_agg_push (all kernels of every micro-batch push)",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": None, "algorithmic_bytes_per_record": BYTES_PER_RECORD_C3, "push_ms": push_ms,
+                         "phase_ms_per_step": phase, "stream_copy_GBps": stream_copy_gbs()},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_hopping(n, args.cpu_seconds)
+        print(json.dumps(out))
+    h.close()
+    finish(world)
+
+
+def cpu_baseline_hopping(n_total, target_s):
+    from ksql_amd import abi, synth
+    orc = abi.load_oracle()
+    cfg = synth.CONFIGS["hopping_double"]
+
+    def run(m):
+        key, ts, val, valid = synth.hopping_double(0, m, n_total)
+        b = abi.HostBatch(ts, keys=key, cols=[val], col_valid=[valid])
+        h = abi.AggHandle(orc, abi.make_agg_desc(window_kind="HOPPING", size_ms=cfg["size_ms"],
+                                                 advance_ms=cfg["advance_ms"], grace_ms=cfg["grace_ms"],
+                                                 key_type="INT64", col_types=["DOUBLE"],
+                                                 aggs=[("SUM", 0), ("AVG", 0), ("MIN", 0), ("MAX", 0)]))
+        t0 = time.perf_counter()
+        h.push(b, stats=False)
+        dt = time.perf_counter() - t0
+        h.close()
+        return dt
+
+    m = 500_000
+    dt = run(m)
+    m2 = int(min(max(m * target_s / max(dt, 1e-3), m), 40_000_000))
+    if m2 > m:
+        m, dt = m2, run(m2)
+    return {"value": m / dt, "unit": "records/s", "cores": 1, "kind": "port",
+            "sample": "first %d of the %d hopping_double records (C oracle, 1 thread, %.1f s)" % (m, n_total, dt)}
+
+
+BYTES_PER_PROBE_C4 = 31  # SURVEY.md §8(d): W_in 16 + table slot 8 + 0.30 x output 24
+
+
+def bench_join(args, lib, rank, world, local):
+    """C4: clickstream LEFT JOIN users WHERE level = 'Platinum'.  The 1e8-row users table is
+    replicated in every GPU's HBM (built once, timed separately); each GPU probes its own
+    1e9 clicks (weak scaling, no exchange).  One step = khip_table_probe_device over all
+    clicks: row-aligned emit/matched bitmaps + the right column, then the emitted count."""
+    import torch
+    from ksql_amd import abi, synth
+    n = args.records if args.records != 100_000_000 else 1_000_000_000
+    U = args.users
+    uid, level = synth.users_table(0, U, xp="torch", device="cuda")
+    level = level.to(torch.int32)
+    t = abi.TableHandle(lib, ["INT32"], device=local, capacity_hint=U)
+    tb = abi.DeviceBatch(torch.zeros(U, dtype=torch.int64, device="cuda"), keys=uid, cols=[level])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    t.upsert(tb)
+    t.sync()
+    build_s = time.perf_counter() - t0
+    del tb, uid, level
+    cu, cts = synth.clicks(0, n, U, xp="torch", device="cuda", seed_clicks=5 + 1000 * rank)
+    batch = abi.DeviceBatch(cts, keys=cu)
+    nb = (n + 7) // 8 + 8
+    emit = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    matched = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    col = torch.empty(n, dtype=torch.int32, device="cuda")
+    null = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    where = {"col": 0, "op": "EQ", "i64": synth.LEVELS.index("Platinum")}
+    torch.cuda.synchronize()
+
+    def step():
+        return t.probe_device(batch, "LEFT", where, emit, matched, [col], [null])
+
+    for _ in range(max(args.warmup, 1)):
+        rows = step()
+    barrier_sync(world)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rows = step()
+    barrier_sync(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    if rank == 0:
+        ms_step = elapsed * 1000.0 / args.steps
+        achieved = BYTES_PER_PROBE_C4 * n / (ms_step / 1000.0) / 1e9
+        out = {
+            "metric": "stream records/sec, stream-table LEFT JOIN (clickstream x users WHERE level = 'Platinum')",
+            "value": world * n * args.steps / elapsed, "unit": "records/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic (splitmix64, ksql_amd/synth.py users_table/clicks), device-resident columnar batch",
+            "config": {"workload": "clickstream_join", "table_rows": U, "clicks_per_gpu": n,
+                       "table_build_s": build_s, "table_build_rows_per_s": U / build_s,
+                       "emitted_rows_per_gpu": int(rows), "parallelism": "replicated table x%d" % world},
+            "roofline": {"bound": "hbm", "kernel": "k_probe (khip_table_probe_device)", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "algorithmic_bytes_per_record": BYTES_PER_PROBE_C4, "stream_copy_GBps": stream_copy_gbs()},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(out))
+    t.close()
+    finish(world)
 
 
 BYTES_PER_RECORD_C5 = 136  # SURVEY.md §8(d): read 24 + pack 24 + recv 24 + 2 x 32 (slot)

@@ -414,6 +414,27 @@ class TableHandle:
         return {"n": m, "stream_row": sr[:m], "matched": mt[:m].astype(bool),
                 "cols": [c[:m] for c in cols], "nulls": [x[:m].astype(bool) for x in nulls]}
 
+    def probe_device(self, batch, join_type="LEFT", where=None, emit=None, matched=None, cols=None, nulls=None,
+                     count=True):
+        """khip_table_probe_device: row-aligned device outputs (torch tensors, caller-owned);
+        returns the emitted-row count (synchronising) or None (count=False, asynchronous)."""
+        p = lambda t: None if t is None else t.data_ptr()
+        nc = len(self.col_types)
+        cd = (C.c_void_p * max(nc, 1))(*[p(c) for c in (cols or [None] * nc)])
+        cn = (C.c_void_p * max(nc, 1))(*[p(c) for c in (nulls or [None] * nc)])
+        out = JoinDevOut(p(emit), p(matched), cd, cn)
+        wv = None
+        if where is not None:
+            wv = Where(where["col"], OP[where["op"]], int(where.get("i64", 0)), float(where.get("f64", 0.0)))
+        n = i64()
+        self.lib.check(self.lib.table_probe_device(self.h, C.byref(batch.struct), JOIN[join_type],
+                                                   C.byref(wv) if wv else None, C.byref(out),
+                                                   C.byref(n) if count else None), "table_probe_device")
+        return n.value if count else None
+
+    def sync(self):
+        self.lib.check(self.lib.table_sync(self.h), "table_sync")
+
     def close(self):
         if self.h:
             self.lib.table_destroy(self.h)
