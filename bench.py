@@ -364,6 +364,25 @@ def cpu_baseline_hopping(n_total, target_s):
             "sample": "first %d of the %d hopping_double records (C oracle, 1 thread, %.1f s)" % (m, n_total, dt)}
 
 
+def random_gather_rows_per_s(table_bytes, rows=100_000_000):
+    """Practical ceiling of a hash probe into a table far larger than the caches: torch's
+    gather of `rows` uniformly random 32-byte rows from a `table_bytes` table (one random
+    line per row, the access pattern of a probe), in rows/s."""
+    import torch
+    tab = torch.empty(max(table_bytes // 32, 1), 4, dtype=torch.int64, device="cuda")
+    idx = torch.randint(0, tab.shape[0], (rows,), device="cuda")
+    out = tab[idx]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(3):
+        out = tab[idx]
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 3
+    del tab, idx, out
+    return rows / (ms / 1000.0)
+
+
 BYTES_PER_PROBE_C4 = 31  # SURVEY.md §8(d): W_in 16 + table slot 8 + 0.30 x output 24
 
 
@@ -385,6 +404,8 @@ def bench_join(args, lib, rank, world, local):
     t.upsert(tb)
     t.sync()
     build_s = time.perf_counter() - t0
+    # khip_table_create: cap = next_pow2(4/3 x hint) slots of 32 bytes (one INT32 column)
+    table_bytes = (1 << max(10, ((U * 4 + 2) // 3 - 1).bit_length())) * 32
     del tb, uid, level
     cu, cts = synth.clicks(0, n, U, xp="torch", device="cuda", seed_clicks=5 + 1000 * rank)
     batch = abi.DeviceBatch(cts, keys=cu)
@@ -422,7 +443,9 @@ def bench_join(args, lib, rank, world, local):
                        "emitted_rows_per_gpu": int(rows), "parallelism": "replicated table x%d" % world},
             "roofline": {"bound": "hbm", "kernel": "k_probe (khip_table_probe_device)", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "algorithmic_bytes_per_record": BYTES_PER_PROBE_C4, "stream_copy_GBps": stream_copy_gbs()},
+                         "algorithmic_bytes_per_record": BYTES_PER_PROBE_C4, "stream_copy_GBps": stream_copy_gbs(),
+                         "table_bytes": table_bytes,
+                         "random_gather_rows_per_s": random_gather_rows_per_s(table_bytes)},
             "cpu_baseline": None,
         }
         print(json.dumps(out))

@@ -21,6 +21,7 @@
 // output is row-aligned (selection bitmaps built with __ballot, 8 B per wave) so no
 // compaction pass is needed on the device path.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -171,68 +172,131 @@ struct JOut {
   int64_t* slot_out;  // host path: -1 not emitted, 0 emitted miss, slot + 1 emitted hit
 };
 
-// One thread per stream row (row = global thread id, so a wave covers 64 consecutive rows
-// and its bitmaps are one 8-byte store).
+__device__ __forceinline__ bool where_ok_raw(uint64_t raw, uint64_t meta, const JWhere& w) {
+  if (!w.active) return true;
+  if (meta & (1ULL << w.col)) return false;  // NULL never satisfies
+  int c;
+  if (w.type == KHIP_TYPE_DOUBLE) {
+    double d;
+    __builtin_memcpy(&d, &raw, 8);
+    if (d != d) return w.op == KHIP_OP_NE;
+    c = d < w.f64 ? -1 : (d > w.f64 ? 1 : 0);
+  } else {
+    const int64_t v = (int64_t)raw;
+    c = v < w.i64 ? -1 : (v > w.i64 ? 1 : 0);
+  }
+  switch (w.op) {
+    case KHIP_OP_GT: return c > 0;
+    case KHIP_OP_GE: return c >= 0;
+    case KHIP_OP_LT: return c < 0;
+    case KHIP_OP_LE: return c <= 0;
+    case KHIP_OP_EQ: return c == 0;
+    case KHIP_OP_NE: return c != 0;
+  }
+  return false;
+}
+
+// PR stream rows per thread (row = block base + r * 256 + thread, so for every r a wave
+// covers 64 consecutive rows and its bitmaps are one 8-byte store).  The home slot of all
+// PR rows (32 bytes: key, meta, tag, first column — one line) is loaded before any is
+// examined, so a wave keeps 4 x PR independent HBM reads in flight: the table is far larger
+// than the caches and every probe is a random line, so the kernel is latency/MLP-bound.
+template <int PR>
 __global__ __launch_bounds__(256) void k_probe(const uint64_t* __restrict__ table, uint64_t mask, int sw,
                                                const int64_t* __restrict__ keys, const int64_t* __restrict__ ts,
                                                const uint8_t* __restrict__ kv, const uint8_t* __restrict__ rv,
                                                int64_t n, int inner, JWhere w, int ncols,
                                                const int32_t* __restrict__ types_dev, JOut out,
                                                unsigned long long* __restrict__ n_emitted) {
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const bool in = i < n;
-  bool emit = false, hit = false;
-  int64_t found = -1;
-  uint64_t meta = 0;
-  if (in && bit_get(kv, i) && bit_get(rv, i) && ts[i] >= 0) {
-    const int64_t key = keys[i];
-    uint64_t slot = key_hash(key) & mask;
-    for (int probe = 0; probe < JMAX_PROBE; probe++) {
-      const uint64_t* s = table + slot * (uint64_t)sw;
-      const uint64_t m = s[1];
-      if (m == 0) break;
-      if ((int64_t)s[0] == key) {
-        if (m & M_LIVE) {
-          hit = true;
-          found = (int64_t)slot;
-          meta = m;
-        }
-        break;
-      }
-      slot = (slot + 1) & mask;
-    }
-    emit = inner ? hit : true;
-    if (emit && w.active) emit = hit && where_ok(table + found * (uint64_t)sw, meta, w);
-  }
-  const uint64_t be = __ballot(emit), bh = __ballot(hit);
+  const int64_t base = (int64_t)blockIdx.x * 256 * PR;
   const int lane = threadIdx.x & 63;
-  const int64_t wbase = i - lane;
-  if (lane == 0 && wbase < n) {
-    // n may not be a multiple of 64: write whole bytes only up to the batch end
-    const int64_t nbytes = std::min<int64_t>(8, (n - wbase + 7) / 8);
-    for (int b = 0; b < nbytes; b++) {
-      if (out.emit) out.emit[wbase / 8 + b] = (uint8_t)(be >> (8 * b));
-      if (out.matched) out.matched[wbase / 8 + b] = (uint8_t)(bh >> (8 * b));
-    }
+  int64_t key[PR];
+  bool act[PR];
+  uint64_t slot[PR];
+  longlong2 h0[PR], h1[PR];
+#pragma unroll
+  for (int r = 0; r < PR; r++) {
+    const int64_t i = base + r * 256 + threadIdx.x;
+    const int64_t ic = i < n ? i : n - 1;
+    key[r] = keys[ic];
+    act[r] = i < n && ts[ic] >= 0 && bit_get(kv, ic) && bit_get(rv, ic);
   }
-  for (int c = 0; c < ncols; c++) {
-    const bool isnull = !hit || (meta & (1ULL << c));
-    const uint64_t bn = __ballot(isnull);
-    if (out.col_null[c] && lane == 0 && wbase < n) {
+#pragma unroll
+  for (int r = 0; r < PR; r++) {
+    slot[r] = key_hash(key[r]) & mask;
+    const longlong2* sp = (const longlong2*)(table + slot[r] * (uint64_t)sw);
+    h0[r] = sp[0];
+    h1[r] = sp[1];
+  }
+  int cnt = 0;
+#pragma unroll
+  for (int r = 0; r < PR; r++) {
+    const int64_t i = base + r * 256 + threadIdx.x;
+    bool hit = false, emit = false;
+    int64_t found = -1;
+    uint64_t meta = 0, v0 = 0;
+    if (act[r]) {
+      uint64_t m = (uint64_t)h0[r].y;
+      int64_t k0 = h0[r].x;
+      uint64_t c0 = (uint64_t)h1[r].y, sl = slot[r];
+      // linear probing past the home slot (a minority of rows)
+      for (int probe = 0; probe < JMAX_PROBE; probe++) {
+        if (m == 0) break;
+        if (k0 == key[r]) {
+          if (m & M_LIVE) {
+            hit = true;
+            found = (int64_t)sl;
+            meta = m;
+            v0 = c0;
+          }
+          break;
+        }
+        sl = (sl + 1) & mask;
+        const uint64_t* s = table + sl * (uint64_t)sw;
+        k0 = (int64_t)s[0];
+        m = s[1];
+        c0 = s[3];
+      }
+      emit = inner ? hit : true;
+      if (emit && w.active)
+        emit = hit && where_ok_raw(w.col == 0 ? v0 : table[found * (uint64_t)sw + 3 + w.col], meta, w);
+    }
+    const uint64_t be = __ballot(emit), bh = __ballot(hit);
+    const int64_t wbase = i - lane;
+    if (lane == 0 && wbase < n) {
+      // n may not be a multiple of 64: write whole bytes only up to the batch end
       const int64_t nbytes = std::min<int64_t>(8, (n - wbase + 7) / 8);
-      for (int b = 0; b < nbytes; b++) out.col_null[c][wbase / 8 + b] = (uint8_t)(bn >> (8 * b));
+      if (nbytes == 8 && !(((uintptr_t)out.emit | (uintptr_t)out.matched) & 7)) {
+        if (out.emit) *(uint64_t*)(out.emit + wbase / 8) = be;
+        if (out.matched) *(uint64_t*)(out.matched + wbase / 8) = bh;
+      } else {
+        for (int b = 0; b < nbytes; b++) {
+          if (out.emit) out.emit[wbase / 8 + b] = (uint8_t)(be >> (8 * b));
+          if (out.matched) out.matched[wbase / 8 + b] = (uint8_t)(bh >> (8 * b));
+        }
+      }
     }
-    if (in && out.col_data[c]) {
-      const uint64_t raw = hit ? table[found * (uint64_t)sw + 3 + c] : 0;
-      if (types_dev[c] == KHIP_TYPE_INT32) ((int32_t*)out.col_data[c])[i] = (int32_t)raw;
-      else ((uint64_t*)out.col_data[c])[i] = raw;
+    for (int c = 0; c < ncols; c++) {
+      const bool isnull = !hit || (meta & (1ULL << c));
+      const uint64_t bn = __ballot(isnull);
+      if (out.col_null[c] && lane == 0 && wbase < n) {
+        const int64_t nbytes = std::min<int64_t>(8, (n - wbase + 7) / 8);
+        if (nbytes == 8 && !((uintptr_t)out.col_null[c] & 7)) {
+          *(uint64_t*)(out.col_null[c] + wbase / 8) = bn;
+        } else {
+          for (int b = 0; b < nbytes; b++) out.col_null[c][wbase / 8 + b] = (uint8_t)(bn >> (8 * b));
+        }
+      }
+      if (i < n && out.col_data[c]) {
+        const uint64_t raw = hit ? (c == 0 ? v0 : table[found * (uint64_t)sw + 3 + c]) : 0;
+        if (types_dev[c] == KHIP_TYPE_INT32) ((int32_t*)out.col_data[c])[i] = (int32_t)raw;
+        else ((uint64_t*)out.col_data[c])[i] = raw;
+      }
     }
+    if (out.slot_out && i < n) out.slot_out[i] = emit ? found + 1 : -1;  // 0 = emitted LEFT miss
+    cnt += lane == 0 ? __popcll(be) : 0;
   }
-  if (out.slot_out && in) out.slot_out[i] = emit ? found + 1 : -1;  // 0 = emitted LEFT miss
-  if (n_emitted) {
-    const int cnt = __popcll(be);
-    if (lane == 0 && cnt) atomicAdd(n_emitted, (unsigned long long)cnt);
-  }
+  if (n_emitted && lane == 0 && cnt) atomicAdd(n_emitted, (unsigned long long)cnt);
 }
 
 __global__ __launch_bounds__(256) void k_table_rehash(const uint64_t* __restrict__ old, int64_t ocap,
@@ -476,7 +540,10 @@ static khip_status probe_launch(khip_table* t, const khip_batch* b, int32_t join
   if (!ts) return fail(KHIP_E_INVALID, "missing timestamp column");
   JWhere jw;
   KHIP_TRY(make_where(t, w, &jw));
-  hipLaunchKernelGGL(k_probe, dim3(ceil_div(n, 256)), dim3(256), 0, t->stream, t->table.as<uint64_t>(),
+  static const int pr_env = getenv("KHIP_PROBE_PR") ? atoi(getenv("KHIP_PROBE_PR")) : 4;  // measured: 4 > 8 > 16 > 1
+  const int PR = pr_env >= 16 ? 16 : (pr_env >= 8 ? 8 : (pr_env >= 4 ? 4 : 1));
+  auto kern = PR == 16 ? k_probe<16> : (PR == 8 ? k_probe<8> : (PR == 4 ? k_probe<4> : k_probe<1>));
+  hipLaunchKernelGGL(kern, dim3(ceil_div(n, 256 * PR)), dim3(256), 0, t->stream, t->table.as<uint64_t>(),
                      (uint64_t)(t->cap - 1), t->sw, keys, ts, kv, rv, n, join_type == KHIP_JOIN_INNER ? 1 : 0, jw,
                      t->desc.n_cols, t->types_dev.as<int32_t>(), out, n_emitted);
   KHIP_TRY_HIP(hipGetLastError());
