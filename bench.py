@@ -364,6 +364,66 @@ def cpu_baseline_hopping(n_total, target_s):
             "sample": "first %d of the %d hopping_double records (C oracle, 1 thread, %.1f s)" % (m, n_total, dt)}
 
 
+def cpu_baseline_join(users, target_s):
+    """Oracle stream-table LEFT JOIN (oracle_table_probe, 1 thread).  Bounded sample: a users
+    table of min(users, 1e7) rows built first (untimed), then clicks drawn over the same
+    1.1x id span probed against it (timed), WHERE level = 'Platinum'."""
+    from ksql_amd import abi, synth
+    orc = abi.load_oracle()
+    U = min(users, 10_000_000)
+    uid, level = synth.users_table(0, U)
+    t = abi.TableHandle(orc, ["INT32"], capacity_hint=U)
+    t.upsert(abi.HostBatch(np.zeros(U, np.int64), keys=uid, cols=[level.astype(np.int32)]))
+    where = {"col": 0, "op": "EQ", "i64": synth.LEVELS.index("Platinum")}
+
+    def run(m):
+        cu, cts = synth.clicks(0, m, U, seed_clicks=5)
+        b = abi.HostBatch(cts, keys=cu)
+        t0 = time.perf_counter()
+        t.probe(b, "LEFT", where)
+        return time.perf_counter() - t0
+
+    m = 1_000_000
+    dt = run(m)
+    m2 = int(min(max(m * target_s / max(dt, 1e-3), m), 50_000_000))
+    if m2 > m:
+        m, dt = m2, run(m2)
+    t.close()
+    return {"value": m / dt, "unit": "records/s", "cores": 1, "kind": "port",
+            "sample": "%d clicks probed against a %d-row users table (C oracle, 1 thread, %.1f s)" % (m, U, dt)}
+
+
+def cpu_baseline_repartition(n_total, target_s):
+    """Oracle C5 step on a prefix of rank 0's source partition (1 thread): Kafka partitioner of
+    the new key (oracle_kafka_partition, 8 destinations) + SUM(amount) TUMBLING 1 MINUTE
+    GROUP BY region_id (oracle_agg_push)."""
+    from ksql_amd import abi, synth
+    orc = abi.load_oracle()
+
+    def run(m):
+        _eid, ts, region, amount = synth.repartition_sum(0, m, n_total)
+        region = np.ascontiguousarray(region, np.int64)
+        dest = np.empty(m, np.int32)
+        h = abi.AggHandle(orc, abi.make_agg_desc(window_kind="TUMBLING", size_ms=60_000, key_type="INT64",
+                                                 col_types=["INT64"], aggs=[("SUM", 0)]))
+        b = abi.HostBatch(ts, keys=region, cols=[amount])
+        t0 = time.perf_counter()
+        orc.dll.oracle_kafka_partition(region.ctypes.data, m, 8, 8, dest.ctypes.data)
+        h.push(b, stats=False)
+        dt = time.perf_counter() - t0
+        h.close()
+        return dt
+
+    m = 1_000_000
+    dt = run(m)
+    m2 = int(min(max(m * target_s / max(dt, 1e-3), m), 60_000_000))
+    if m2 > m:
+        m, dt = m2, run(m2)
+    return {"value": m / dt, "unit": "records/s", "cores": 1, "kind": "port",
+            "sample": "first %d of rank 0's %d repartition_sum records: partitioner + aggregate "
+                      "(C oracle, 1 thread, %.1f s)" % (m, n_total, dt)}
+
+
 def random_gather_rows_per_s(table_bytes, rows=100_000_000):
     """Practical ceiling of a hash probe into a table far larger than the caches: torch's
     gather of `rows` uniformly random 32-byte rows from a `table_bytes` table (one random
@@ -448,6 +508,8 @@ def bench_join(args, lib, rank, world, local):
                          "random_gather_rows_per_s": random_gather_rows_per_s(table_bytes)},
             "cpu_baseline": None,
         }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_join(U, args.cpu_seconds)
         print(json.dumps(out))
     t.close()
     finish(world)
@@ -556,6 +618,8 @@ def bench_repartition(args, lib, rank, world, local):
                          "phase_ms": per, "push_device_ms": push_ms},
             "cpu_baseline": None,
         }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_repartition(n, args.cpu_seconds)
         print(json.dumps(out))
     h.close()
     rp.close()
