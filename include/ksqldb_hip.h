@@ -214,6 +214,24 @@ khip_status khip_agg_snapshot_size(khip_agg* agg, int64_t* n_rows,
 khip_status khip_agg_snapshot(khip_agg* agg, const khip_having* having,
                               khip_snapshot* out);
 
+/* Pull query against the materialized table (KsMaterializedWindowTable.get(key, partition,
+ * windowStartBounds, windowEndBounds), S/materialization/ks/KsMaterializedWindowTable.java:70-120,
+ * and the all-keys scan get(partition, ...) :122-165; unwindowed KsMaterializedTable.get).
+ * Bounds are closed ranges in epoch ms (an open Guava Range end becomes lo+1 / hi-1; unbounded =
+ * INT64_MIN / INT64_MAX); they are ignored for KHIP_WINDOW_NONE tables. */
+typedef struct khip_pull {
+  int64_t n_keys;        /* 0 = every key (scan); else keys[] (INT64 key tables only)          */
+  const int64_t* keys;   /* host memory, any order, duplicates allowed                         */
+  int64_t ws_lo, ws_hi;  /* WINDOWSTART bounds, inclusive                                      */
+  int64_t we_lo, we_hi;  /* WINDOWEND bounds, inclusive                                        */
+} khip_pull;
+
+/* Rows matching `q` (and `having`, may be NULL: HAVING-tombstoned rows are absent from the
+ * table) in snapshot layout, sorted by (key, window start).  The filter runs on the device
+ * over the HBM-resident state; only matching rows cross PCIe. */
+khip_status khip_agg_get(khip_agg* agg, const khip_pull* q, const khip_having* having,
+                         khip_snapshot* out);
+
 /* Count the rows that pass `having` entirely on the device (no copy-out).
  * having may be NULL (= total group count). */
 khip_status khip_agg_count_rows(khip_agg* agg, const khip_having* having,

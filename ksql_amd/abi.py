@@ -73,6 +73,11 @@ class Snapshot(C.Structure):
                 ("agg_null", C.POINTER(C.c_void_p))]
 
 
+class Pull(C.Structure):
+    _fields_ = [("n_keys", i64), ("keys", C.c_void_p), ("ws_lo", i64), ("ws_hi", i64),
+                ("we_lo", i64), ("we_hi", i64)]
+
+
 class TableDesc(C.Structure):
     _fields_ = [("key_type", i32), ("n_cols", i32), ("col_types", C.POINTER(i32)),
                 ("device", i32), ("flags", i32), ("capacity_hint", i64)]
@@ -125,6 +130,7 @@ SIGS = {
 PRODUCT_ONLY = {
     "agg_result_type": ([C.POINTER(AggDesc), i32, C.POINTER(i32)]),
     "agg_count_rows": ([_P, C.POINTER(Having), C.POINTER(i64)]),
+    "agg_get": ([_P, C.POINTER(Pull), C.POINTER(Having), C.POINTER(Snapshot)]),
     "agg_reset": ([_P]),
     "agg_sync": ([_P]),
     "agg_stream": ([_P, C.POINTER(_P)]),
@@ -315,6 +321,23 @@ class AggHandle:
         return st.as_dict() if stats else None
 
     def snapshot(self, having=None):
+        return self._materialize(having, lambda hv, s: self.lib.check(
+            self.lib.agg_snapshot(self.h, hv, s), "agg_snapshot"))
+
+    def get(self, keys=None, ws=(None, None), we=(None, None), having=None):
+        """Pull query (khip_agg_get): rows of `keys` (None = every key) whose WINDOWSTART and
+        WINDOWEND lie in the closed bounds (None = unbounded), sorted by (key, ws)."""
+        lo, hi = -(1 << 63), (1 << 63) - 1
+        ka = None if keys is None else np.ascontiguousarray(keys, np.int64)
+        q = Pull(0 if ka is None else len(ka), None if ka is None or len(ka) == 0 else ka.ctypes.data,
+                 lo if ws[0] is None else ws[0], hi if ws[1] is None else ws[1],
+                 lo if we[0] is None else we[0], hi if we[1] is None else we[1])
+        if ka is not None and len(ka) == 0:
+            return self._materialize(None, lambda hv, s: None, empty=True)
+        return self._materialize(having, lambda hv, s: self.lib.check(
+            self.lib.agg_get(self.h, C.byref(q), hv, s), "agg_get"))
+
+    def _materialize(self, having, call, empty=False):
         n, kb = i64(), i64()
         self.lib.check(self.lib.agg_snapshot_size(self.h, C.byref(n), C.byref(kb)), "agg_snapshot_size")
         cap = max(n.value, 1)
@@ -336,7 +359,8 @@ class AggHandle:
         if having is not None:
             hv = Having(having["agg"], OP[having["op"]], int(having["value"]) if not isinstance(having["value"], float) else 0,
                         float(having["value"]))
-        self.lib.check(self.lib.agg_snapshot(self.h, C.byref(hv) if hv else None, C.byref(s)), "agg_snapshot")
+        if not empty:
+            call(C.byref(hv) if hv else None, C.byref(s))
         m = s.n_rows
         out = {"n": m, "ws": arrays["ws"][:m], "we": arrays["we"][:m], "rowtime": arrays["rowtime"][:m],
                "values": [v[:m] for v in arrays["values"]], "nulls": [v[:m].astype(bool) for v in arrays["nulls"]]}

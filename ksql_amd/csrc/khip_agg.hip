@@ -942,8 +942,10 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   return KHIP_OK;
 }
 
-static khip_status compact_rows(khip_agg* a, const khip_having* h, std::vector<uint64_t>* rows, int64_t* count) {
+static khip_status compact_rows(khip_agg* a, const khip_having* h, std::vector<uint64_t>* rows, int64_t* count,
+                                const HavingDev* pull = nullptr) {
   HavingDev hd{};
+  if (pull) hd = *pull;
   if (h) {
     if (h->agg_index < 0 || h->agg_index >= a->desc.n_aggs) return fail(KHIP_E_INVALID, "having agg index");
     if (h->op < KHIP_OP_GT || h->op > KHIP_OP_NE) return fail(KHIP_E_INVALID, "having op");
@@ -1009,13 +1011,9 @@ khip_status khip_agg_snapshot_size(khip_agg* a, int64_t* n_rows, int64_t* key_by
   return KHIP_OK;
 }
 
-khip_status khip_agg_snapshot(khip_agg* a, const khip_having* h, khip_snapshot* out) {
-  clear_error();
-  if (!a || !out) return fail(KHIP_E_INVALID, "null argument");
-  DeviceGuard g(a->device);
-  std::vector<uint64_t> rows;
-  int64_t n = 0;
-  KHIP_TRY(compact_rows(a, h, &rows, &n));
+// Sort compacted rows by (key, window start) and write them to the caller's snapshot buffers
+// (ResultTransformer map() + WindowBoundsPopulator).
+static khip_status emit_snapshot(khip_agg* a, const std::vector<uint64_t>& rows, int64_t n, khip_snapshot* out) {
   const int sw = a->sw;
   const bool utf8 = a->desc.key_type == KHIP_KEY_UTF8;
   std::vector<uint8_t> arena;
@@ -1099,6 +1097,48 @@ khip_status khip_agg_snapshot(khip_agg* a, const khip_having* h, khip_snapshot* 
   out->n_rows = n;
   out->key_bytes_len = kb;
   return KHIP_OK;
+}
+
+khip_status khip_agg_snapshot(khip_agg* a, const khip_having* h, khip_snapshot* out) {
+  clear_error();
+  if (!a || !out) return fail(KHIP_E_INVALID, "null argument");
+  DeviceGuard g(a->device);
+  std::vector<uint64_t> rows;
+  int64_t n = 0;
+  KHIP_TRY(compact_rows(a, h, &rows, &n));
+  return emit_snapshot(a, rows, n, out);
+}
+
+khip_status khip_agg_get(khip_agg* a, const khip_pull* q, const khip_having* h, khip_snapshot* out) {
+  clear_error();
+  if (!a || !q || !out) return fail(KHIP_E_INVALID, "null argument");
+  if (q->n_keys < 0 || (q->n_keys > 0 && !q->keys)) return fail(KHIP_E_INVALID, "pull keys");
+  if (q->n_keys > 0 && a->desc.key_type != KHIP_KEY_INT64)
+    return fail(KHIP_E_UNSUPPORTED, "pull query by key needs an INT64 key table");
+  DeviceGuard g(a->device);
+  HavingDev pd{};
+  pd.pull = 1;
+  pd.pull_windowed = a->windowed;
+  pd.ws_lo = q->ws_lo;
+  pd.ws_hi = q->ws_hi;
+  pd.we_lo = q->we_lo;
+  pd.we_hi = q->we_hi;
+  pd.size_ms = a->desc.size_ms;
+  DevBuf dkeys;
+  std::vector<int64_t> k;  // outlives the copy: compact_rows synchronises the stream
+  if (q->n_keys > 0) {
+    k.assign(q->keys, q->keys + q->n_keys);
+    std::sort(k.begin(), k.end());
+    k.erase(std::unique(k.begin(), k.end()), k.end());
+    KHIP_TRY(dkeys.ensure(k.size() * 8));
+    KHIP_TRY_HIP(hipMemcpyAsync(dkeys.p, k.data(), k.size() * 8, hipMemcpyHostToDevice, a->stream));
+    pd.keys = dkeys.as<int64_t>();
+    pd.n_keys = (int64_t)k.size();
+  }
+  std::vector<uint64_t> rows;
+  int64_t n = 0;
+  KHIP_TRY(compact_rows(a, h, &rows, &n, &pd));
+  return emit_snapshot(a, rows, n, out);
 }
 
 khip_status khip_agg_reset(khip_agg* a) {

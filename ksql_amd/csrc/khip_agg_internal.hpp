@@ -56,7 +56,33 @@ struct HavingDev {
   AggOut a;
   int64_t i64;
   double f64;
+  // pull-query filter (khip_agg_get; KsMaterializedWindowTable.get): key in the sorted unique
+  // `keys` (when n_keys > 0) and WINDOWSTART / WINDOWEND inside closed bounds (windowed tables)
+  int32_t pull;
+  int32_t pull_windowed;
+  const int64_t* keys;
+  int64_t n_keys;
+  int64_t ws_lo, ws_hi, we_lo, we_hi, size_ms;
 };
+
+__device__ __forceinline__ bool pull_ok(const uint64_t* s, const HavingDev& h) {
+  if (!h.pull) return true;
+  if (h.n_keys > 0) {
+    const int64_t k = (int64_t)s[0];
+    int64_t lo = 0, hi = h.n_keys;  // lower_bound
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (h.keys[mid] < k) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo >= h.n_keys || h.keys[lo] != k) return false;
+  }
+  if (h.pull_windowed) {
+    const int64_t ws = (int64_t)s[1], we = ws + h.size_ms;
+    if (ws < h.ws_lo || ws > h.ws_hi || we < h.we_lo || we > h.we_hi) return false;
+  }
+  return true;
+}
 
 // ------------------------------------------------------------------ device utils
 
@@ -164,6 +190,7 @@ __device__ __forceinline__ bool result_is_double(const AggOut& a) {
 }
 
 __device__ __forceinline__ bool having_ok(const uint64_t* s, const HavingDev& h) {
+  if (!pull_ok(s, h)) return false;
   if (!h.active) return true;
   int64_t iv = 0;
   double dv = 0.0;
