@@ -168,6 +168,20 @@ def main():
         h.count_rows(having)
         pcie = n / (time.perf_counter() - t1)
 
+    # pull-query latency on the materialized table (khip_agg_get), not `value`
+    pull = None
+    if rank == 0:
+        qk = card[: 1 << 12].cpu().numpy()
+        pull = {}
+        for nk in (1, 100, 4096):
+            h.get(qk[:nk])  # warm
+            t1 = time.perf_counter()
+            reps = 5
+            for _ in range(reps):
+                r = h.get(qk[:nk])
+            pull["keys_%d_ms" % nk] = (time.perf_counter() - t1) * 1000.0 / reps
+            pull["keys_%d_rows" % nk] = int(r["n"])
+
     if rank == 0:
         ms_step = elapsed * 1000.0 / args.steps
         value = world * n * args.steps / elapsed
@@ -208,6 +222,7 @@ def main():
                          "algorithmic_bytes_per_record": BYTES_PER_RECORD_C2, "push_ms": push_ms,
                          "engine": args.engine, "per_kernel": per_kernel},
             "pcie_inclusive_records_per_s": pcie,
+            "pull_query": pull,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(n, args.keys, args.cpu_seconds)

@@ -321,8 +321,7 @@ class AggHandle:
         return st.as_dict() if stats else None
 
     def snapshot(self, having=None):
-        return self._materialize(having, lambda hv, s: self.lib.check(
-            self.lib.agg_snapshot(self.h, hv, s), "agg_snapshot"))
+        return self._materialize(having, lambda hv, s: self.lib.agg_snapshot(self.h, hv, s), "agg_snapshot")
 
     def get(self, keys=None, ws=(None, None), we=(None, None), having=None):
         """Pull query (khip_agg_get): rows of `keys` (None = every key) whose WINDOWSTART and
@@ -333,15 +332,27 @@ class AggHandle:
                  lo if ws[0] is None else ws[0], hi if ws[1] is None else ws[1],
                  lo if we[0] is None else we[0], hi if we[1] is None else we[1])
         if ka is not None and len(ka) == 0:
-            return self._materialize(None, lambda hv, s: None, empty=True)
-        return self._materialize(having, lambda hv, s: self.lib.check(
-            self.lib.agg_get(self.h, C.byref(q), hv, s), "agg_get"))
+            return self._materialize(None, None, "agg_get", cap=1)
+        # point lookups: start from a small output buffer, grow to the row count on KHIP_E_BUFFER
+        return self._materialize(having, lambda hv, s: self.lib.agg_get(self.h, C.byref(q), hv, s), "agg_get",
+                                 cap=4096 if self.desc.key_type == KEY["INT64"] else None)
 
-    def _materialize(self, having, call, empty=False):
-        n, kb = i64(), i64()
-        self.lib.check(self.lib.agg_snapshot_size(self.h, C.byref(n), C.byref(kb)), "agg_snapshot_size")
-        cap = max(n.value, 1)
-        kcap = max(kb.value, 1)
+    def _materialize(self, having, call, what, cap=None):
+        if cap is None:
+            n, kb = i64(), i64()
+            self.lib.check(self.lib.agg_snapshot_size(self.h, C.byref(n), C.byref(kb)), "agg_snapshot_size")
+            cap, kcap = max(n.value, 1), max(kb.value, 1)
+        else:
+            kcap = 1
+        while True:
+            out, st, n_needed = self._materialize_into(having, call, cap, kcap)
+            if st == KHIP_E_BUFFER and n_needed > cap:
+                cap = n_needed
+                continue
+            self.lib.check(st, what)
+            return out
+
+    def _materialize_into(self, having, call, cap, kcap):
         rt = result_types(self.desc)
         arrays = {
             "key": np.zeros(cap, np.int64), "key_offsets": np.zeros(cap + 1, np.int64),
@@ -359,8 +370,9 @@ class AggHandle:
         if having is not None:
             hv = Having(having["agg"], OP[having["op"]], int(having["value"]) if not isinstance(having["value"], float) else 0,
                         float(having["value"]))
-        if not empty:
-            call(C.byref(hv) if hv else None, C.byref(s))
+        st = KHIP_OK if call is None else call(C.byref(hv) if hv else None, C.byref(s))
+        if st != KHIP_OK:
+            return None, st, s.n_rows
         m = s.n_rows
         out = {"n": m, "ws": arrays["ws"][:m], "we": arrays["we"][:m], "rowtime": arrays["rowtime"][:m],
                "values": [v[:m] for v in arrays["values"]], "nulls": [v[:m].astype(bool) for v in arrays["nulls"]]}
@@ -370,7 +382,7 @@ class AggHandle:
             out["key"] = [kbts[offs[i]:offs[i + 1]].decode("utf-8", "surrogateescape") for i in range(m)]
         else:
             out["key"] = arrays["key"][:m]
-        return out
+        return out, KHIP_OK, m
 
     def kernel_times(self, reset=False):
         kt = KernelTimes()

@@ -63,6 +63,7 @@ struct HavingDev {
   const int64_t* keys;
   int64_t n_keys;
   int64_t ws_lo, ws_hi, we_lo, we_hi, size_ms;
+  int32_t log2P;  // partitioned engine: partitions = 2^log2P (partition-directed lookups)
 };
 
 __device__ __forceinline__ bool pull_ok(const uint64_t* s, const HavingDev& h) {

@@ -974,7 +974,19 @@ __global__ __launch_bounds__(256) void k_part_rows(const uint64_t* __restrict__ 
                                                    const int64_t* __restrict__ offs, uint64_t* __restrict__ out) {
   __shared__ int lcnt[4];
   __shared__ int64_t lbase;
+  __shared__ int lhit;
   const int64_t p = blockIdx.x;
+  if (h.pull && h.n_keys > 0 && h.n_keys <= (int64_t)blockDim.x) {
+    // point lookup: only the partitions owning one of the query keys are read
+    if (threadIdx.x == 0) lhit = 0;
+    __syncthreads();
+    if (threadIdx.x < h.n_keys && part_of(h.keys[threadIdx.x], h.log2P) == (uint32_t)p) lhit = 1;
+    __syncthreads();
+    if (!lhit) {
+      if (threadIdx.x == 0 && counts) counts[p] = 0;
+      return;
+    }
+  }
   const uint64_t* src = (sel[p] ? b1 : b0) + (uint64_t)p * cmax * sw;
   const int64_t n = cnt[p];
   if (threadIdx.x == 0) lbase = out ? offs[p] : 0;
@@ -1431,8 +1443,10 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
 }
 
 // Rows passing `h` (all partitions) → rows (sw words each), or just the count.
-khip_status part_compact(khip_agg* a, const HavingDev& h, std::vector<uint64_t>* rows, int64_t* count) {
+khip_status part_compact(khip_agg* a, const HavingDev& h_in, std::vector<uint64_t>* rows, int64_t* count) {
   PartState& s = a->part;
+  HavingDev h = h_in;
+  h.log2P = s.log2P;
   const int P = (int)s.P;
   KHIP_TRY(s.counts.ensure((P + 1) * 8));
   hipLaunchKernelGGL(k_part_rows, dim3(P), dim3(256), 0, a->stream, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),

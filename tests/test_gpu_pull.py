@@ -145,3 +145,22 @@ def test_pull_null_arguments_rejected(prod):
     assert prod.agg_get(h.h, C.byref(q), None, C.byref(s)) == -1
     assert prod.agg_get(h.h, None, None, C.byref(s)) == -1
     h.close()
+
+
+def test_pull_point_lookup_many_partitions(prod, orc):
+    """Partition-directed point lookups (≤ 256 keys read only their partitions) on a table large
+    enough for many partitions, vs the oracle snapshot; plus a > 256-key lookup (scan path)."""
+    rng = np.random.default_rng(11)
+    n = 3_000_000
+    keys = rng.integers(0, 1_500_000, n)
+    ts = np.sort(rng.integers(0, 20_000, n))
+    b = abi.HostBatch(ts, keys=keys)
+    kw = dict(window_kind="TUMBLING", size_ms=5000, key_type="INT64", aggs=[("COUNT_STAR", -1)])
+    (g, desc), (o, _) = _tables(prod, orc, kw, [b], 0)
+    full = o.snapshot()
+    uk = np.unique(full["key"])
+    for q in [uk[:1], rng.choice(uk, 100), np.concatenate([rng.choice(uk, 200), [-1, 10**9]]), rng.choice(uk, 5000)]:
+        for ws in [(None, None), (5000, 10_000)]:
+            assert_snap_equal(g.get(q, ws), _filter(full, q, ws, (None, None), True), desc)
+    g.close()
+    o.close()
