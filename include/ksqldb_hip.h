@@ -218,12 +218,15 @@ khip_status khip_agg_snapshot(khip_agg* agg, const khip_having* having,
  * windowStartBounds, windowEndBounds), S/materialization/ks/KsMaterializedWindowTable.java:70-120,
  * and the all-keys scan get(partition, ...) :122-165; unwindowed KsMaterializedTable.get).
  * Bounds are closed ranges in epoch ms (an open Guava Range end becomes lo+1 / hi-1; unbounded =
- * INT64_MIN / INT64_MAX); they are ignored for KHIP_WINDOW_NONE tables. */
+ * INT64_MIN / INT64_MAX); they are ignored for KHIP_WINDOW_NONE tables.  UTF8 keys are mapped
+ * to their dictionary ids by a read-only device probe; keys never pushed match no row. */
 typedef struct khip_pull {
-  int64_t n_keys;        /* 0 = every key (scan); else keys[] (INT64 key tables only)          */
-  const int64_t* keys;   /* host memory, any order, duplicates allowed                         */
+  int64_t n_keys;        /* 0 = every key (scan); else the n_keys keys below                   */
+  const int64_t* keys;   /* INT64 key tables: host memory, any order, duplicates allowed       */
   int64_t ws_lo, ws_hi;  /* WINDOWSTART bounds, inclusive                                      */
   int64_t we_lo, we_hi;  /* WINDOWEND bounds, inclusive                                        */
+  const int64_t* key_offsets;  /* UTF8 key tables: n_keys+1 offsets (from 0) into key_bytes    */
+  const uint8_t* key_bytes;    /* serialized KAFKA STRING keys (byte equality, like the push)  */
 } khip_pull;
 
 /* Rows matching `q` (and `having`, may be NULL: HAVING-tombstoned rows are absent from the

@@ -75,7 +75,7 @@ class Snapshot(C.Structure):
 
 class Pull(C.Structure):
     _fields_ = [("n_keys", i64), ("keys", C.c_void_p), ("ws_lo", i64), ("ws_hi", i64),
-                ("we_lo", i64), ("we_hi", i64)]
+                ("we_lo", i64), ("we_hi", i64), ("key_offsets", C.c_void_p), ("key_bytes", C.c_void_p)]
 
 
 class TableDesc(C.Structure):
@@ -327,10 +327,19 @@ class AggHandle:
         """Pull query (khip_agg_get): rows of `keys` (None = every key) whose WINDOWSTART and
         WINDOWEND lie in the closed bounds (None = unbounded), sorted by (key, ws)."""
         lo, hi = -(1 << 63), (1 << 63) - 1
-        ka = None if keys is None else np.ascontiguousarray(keys, np.int64)
+        koff = kbytes = None
+        if keys is not None and self.desc.key_type == KEY["UTF8"]:
+            enc = [k.encode("utf-8", "surrogateescape") if isinstance(k, str) else bytes(k) for k in keys]
+            koff = np.zeros(len(enc) + 1, np.int64)
+            koff[1:] = np.cumsum([len(e) for e in enc]) if enc else []
+            kbytes = np.frombuffer(b"".join(enc) or b"\0", np.uint8).copy()
+            ka = np.zeros(len(enc), np.int64)
+        else:
+            ka = None if keys is None else np.ascontiguousarray(keys, np.int64)
         q = Pull(0 if ka is None else len(ka), None if ka is None or len(ka) == 0 else ka.ctypes.data,
                  lo if ws[0] is None else ws[0], hi if ws[1] is None else ws[1],
-                 lo if we[0] is None else we[0], hi if we[1] is None else we[1])
+                 lo if we[0] is None else we[0], hi if we[1] is None else we[1],
+                 None if koff is None else koff.ctypes.data, None if kbytes is None else kbytes.ctypes.data)
         if ka is not None and len(ka) == 0:
             return self._materialize(None, None, "agg_get", cap=1)
         # point lookups: start from a small output buffer, grow to the row count on KHIP_E_BUFFER

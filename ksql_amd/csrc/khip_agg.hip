@@ -410,6 +410,36 @@ __global__ __launch_bounds__(256) void k_dict_lookup(uint64_t* __restrict__ dwor
   }
 }
 
+// Read-only dictionary probe (pull queries): key bytes → resident key id (arena offset), or -1
+// when the key was never seen.  Every dictionary word is resident between pushes.
+__global__ __launch_bounds__(256) void k_dict_find(const uint64_t* __restrict__ dword, const int64_t* __restrict__ dkid,
+                                                   uint64_t dmask, const uint8_t* __restrict__ arena,
+                                                   const int64_t* __restrict__ koff, const uint8_t* __restrict__ kbytes,
+                                                   int64_t n, int64_t* __restrict__ kid) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t o0 = koff[i], len = koff[i + 1] - o0;
+    const uint8_t* kb = kbytes + o0;
+    const uint64_t h = hash_bytes_dev(kb, len);
+    const uint64_t fp = (h >> 40) & 0x3FFFFFULL;
+    uint64_t slot = h & dmask;
+    int64_t found = -1;
+    for (int probe = 0; probe <= (int)dmask && probe < (1 << 20); probe++) {
+      const uint64_t w = dword[slot];
+      if (w == 0) break;
+      if (((w >> 40) & 0x3FFFFFULL) == fp) {
+        const int64_t o = dkid[slot];
+        if (*(const uint64_t*)(arena + o) == h && *(const int64_t*)(arena + o + 8) == len &&
+            bytes_eq(arena + o + 16, kb, len)) {
+          found = o;
+          break;
+        }
+      }
+      slot = (slot + 1) & dmask;
+    }
+    kid[i] = found;
+  }
+}
+
 __device__ __forceinline__ int64_t entry_bytes(int64_t len) { return 16 + ((len + 7) & ~7LL); }
 
 // Per block of 256 dict slots: arena bytes needed by fresh entries.
@@ -1112,9 +1142,11 @@ khip_status khip_agg_snapshot(khip_agg* a, const khip_having* h, khip_snapshot* 
 khip_status khip_agg_get(khip_agg* a, const khip_pull* q, const khip_having* h, khip_snapshot* out) {
   clear_error();
   if (!a || !q || !out) return fail(KHIP_E_INVALID, "null argument");
-  if (q->n_keys < 0 || (q->n_keys > 0 && !q->keys)) return fail(KHIP_E_INVALID, "pull keys");
-  if (q->n_keys > 0 && a->desc.key_type != KHIP_KEY_INT64)
-    return fail(KHIP_E_UNSUPPORTED, "pull query by key needs an INT64 key table");
+  if (q->n_keys < 0 || (q->n_keys > 0 && a->desc.key_type == KHIP_KEY_INT64 && !q->keys))
+    return fail(KHIP_E_INVALID, "pull keys");
+  const bool utf8 = a->desc.key_type == KHIP_KEY_UTF8;
+  if (q->n_keys > 0 && utf8 && (!q->key_offsets || !q->key_bytes || q->key_offsets[0] != 0))
+    return fail(KHIP_E_INVALID, "pull UTF8 keys need key_offsets (from 0) and key_bytes");
   DeviceGuard g(a->device);
   HavingDev pd{};
   pd.pull = 1;
@@ -1126,7 +1158,32 @@ khip_status khip_agg_get(khip_agg* a, const khip_pull* q, const khip_having* h, 
   pd.size_ms = a->desc.size_ms;
   DevBuf dkeys;
   std::vector<int64_t> k;  // outlives the copy: compact_rows synchronises the stream
-  if (q->n_keys > 0) {
+  if (q->n_keys > 0 && utf8) {
+    // key bytes → dictionary ids on the device (read-only probe); unseen keys match nothing
+    const int64_t nk = q->n_keys, nb = q->key_offsets[nk];
+    k.assign((size_t)nk, -1);
+    if (a->docc > 0 && a->dcap > 0) {
+      DevBuf doff, dbytes, dkid;
+      KHIP_TRY(doff.ensure((size_t)(nk + 1) * 8));
+      KHIP_TRY(dbytes.ensure((size_t)std::max<int64_t>(nb, 1)));
+      KHIP_TRY(dkid.ensure((size_t)nk * 8));
+      KHIP_TRY_HIP(hipMemcpyAsync(doff.p, q->key_offsets, (size_t)(nk + 1) * 8, hipMemcpyHostToDevice, a->stream));
+      if (nb) KHIP_TRY_HIP(hipMemcpyAsync(dbytes.p, q->key_bytes, (size_t)nb, hipMemcpyHostToDevice, a->stream));
+      hipLaunchKernelGGL(k_dict_find, dim3(grid_for(nk, 256, 4096)), dim3(256), 0, a->stream, a->dword.as<uint64_t>(),
+                         a->dkid.as<int64_t>(), (uint64_t)(a->dcap - 1), a->arena.as<uint8_t>(), doff.as<int64_t>(),
+                         dbytes.as<uint8_t>(), nk, dkid.as<int64_t>());
+      KHIP_TRY_HIP(hipGetLastError());
+      KHIP_TRY_HIP(hipMemcpyAsync(k.data(), dkid.p, (size_t)nk * 8, hipMemcpyDeviceToHost, a->stream));
+      KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+    }
+    std::sort(k.begin(), k.end());
+    k.erase(std::unique(k.begin(), k.end()), k.end());
+    if (k.size() > 1 && k[0] == -1) k.erase(k.begin());  // -1 (unseen) never matches a row
+    KHIP_TRY(dkeys.ensure(k.size() * 8));
+    KHIP_TRY_HIP(hipMemcpyAsync(dkeys.p, k.data(), k.size() * 8, hipMemcpyHostToDevice, a->stream));
+    pd.keys = dkeys.as<int64_t>();
+    pd.n_keys = (int64_t)k.size();
+  } else if (q->n_keys > 0) {
     k.assign(q->keys, q->keys + q->n_keys);
     std::sort(k.begin(), k.end());
     k.erase(std::unique(k.begin(), k.end()), k.end());

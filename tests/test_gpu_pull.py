@@ -38,7 +38,10 @@ def engine(request):
 
 def _filter(o, keys, ws, we, windowed):
     m = np.ones(o["n"], bool)
-    if keys is not None:
+    if keys is not None and isinstance(o["key"], list):
+        ks = set(keys)
+        m &= np.array([k in ks for k in o["key"]], bool)
+    elif keys is not None:
         m &= np.isin(o["key"], np.asarray(keys, np.int64))
     if windowed:
         lo, hi = ws
@@ -121,19 +124,25 @@ def test_pull_sees_closed_windows(prod, orc):
     o.close()
 
 
-def test_pull_utf8_scan_and_key_lookup_unsupported(prod, orc):
-    """`SELECT * FROM hourly_metrics WHERE WINDOWSTART = …` over a VARCHAR-keyed table (README.md:45):
-    bounds-only scans work on UTF-8 keys; by-key lookups on them report KHIP_E_UNSUPPORTED (the
-    caller keeps the reference's store)."""
+def test_pull_utf8_keys(prod, orc, engine):
+    """`SELECT * FROM hourly_metrics WHERE url = … AND WINDOWSTART = …` over a VARCHAR-keyed table
+    (README.md:45-46): key bytes are mapped to dictionary ids by a read-only device probe; keys
+    never pushed (and the empty string) match nothing; bounds-only scans work too."""
     rng = np.random.default_rng(4)
-    batches = [_random_batch(rng, 5000, "UTF8", 200, 100_000, 5_000)]
+    batches = [_random_batch(rng, 5000, "UTF8", 200, 100_000, 5_000) for _ in range(2)]
     kw = dict(WINDOWS[1], key_type="UTF8", col_types=COLS, aggs=ALL_AGGS)
-    (g, desc), (o, _) = _tables(prod, orc, kw, batches, 0)
+    (g, desc), (o, _) = _tables(prod, orc, kw, batches, engine)
     full = o.snapshot()
-    got = g.get(None, (50_000, 50_000))
-    assert_snap_equal(got, _filter(full, None, (50_000, 50_000), (None, None), True), desc, ABS_SUM)
-    with pytest.raises(abi.KsqlHipError, match=r"\(-4\)"):
-        g.get([1, 2])
+    uk = sorted(set(full["key"]))
+    queries = [
+        (None, (50_000, 50_000)),
+        (uk[:1], (None, None)),
+        ([uk[i] for i in rng.choice(len(uk), 30)], (20_000, 80_000)),
+        ([uk[3], "never-pushed", "", "éè-7", uk[3]], (None, None)),
+        (["never-pushed"], (None, None)),
+    ]
+    for keys, ws in queries:
+        assert_snap_equal(g.get(keys, ws), _filter(full, keys, ws, (None, None), True), desc, ABS_SUM)
     g.close()
     o.close()
 
