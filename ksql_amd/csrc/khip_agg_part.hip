@@ -35,7 +35,9 @@ constexpr int PT_ITEMS = 64;  // default records per thread per tile (KHIP_TILE_
 constexpr int AG_THREADS = 1024;
 constexpr uint32_t L_CLAIM = 1u;
 constexpr uint32_t L_READY = 2u;
-constexpr int MAX_P_LOG2 = 14;  // LDS histogram: 16384 x u32 = 64 KB
+constexpr int MAX_P_LOG2 = 15;    // LDS histogram: 32768 x u32 = 128 KB (of 160 KB)
+constexpr int SPLIT_P_LOG2 = 14;  // growth by splitting stops here (more partitions cost the
+                                  // scatter more than they save the LDS aggregate)
 constexpr int TC_MAX = 64;      // tile chunks for the column prefix
 
 enum { T_ACCEPTED, T_NULL_KEY, T_NULL_ROW, T_BAD_TS, T_APPLIED, T_LATE, T_NPART };
@@ -1042,7 +1044,10 @@ khip_status part_init(khip_agg* a, int64_t hint) {
   // partitions: at most ~H_eff/2 groups each at the hinted size
   const int64_t groups = std::max<int64_t>(hint, 1024);
   // at least 64 partitions: the packed identity then holds window ranges of up to 63
-  s.log2P = std::min(MAX_P_LOG2, std::max(6, part_ceil_log2(groups * 2 / s.H_eff)));
+  s.log2P = std::min(SPLIT_P_LOG2, std::max(6, part_ceil_log2(groups * 2 / s.H_eff)));
+  // hinted groups would need sub-passes at 2^14 partitions (each re-reads the partition's
+  // records): one more partition bit instead (measured: C5 push 12.1 → 9.8 ms)
+  if (s.log2P == SPLIT_P_LOG2 && groups >> SPLIT_P_LOG2 > (int64_t)s.H_eff * 7 / 10) s.log2P = MAX_P_LOG2;
   if (const char* e = getenv("KHIP_PART_LOG2")) s.log2P = std::min(MAX_P_LOG2, atoi(e));
   s.P = 1LL << s.log2P;
   s.cmax = next_pow2(std::max<int64_t>(64, 2 * groups / s.P + 64));
@@ -1212,7 +1217,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                       const uint8_t* rv, const ColPtrs& cols, int64_t* tot) {
   PartState& s = a->part;
   // keep the resident groups per partition well inside the LDS table (split = exact re-layout)
-  while (s.log2P < MAX_P_LOG2 && a->occ > s.P * (int64_t)s.H_eff / 2) KHIP_TRY(part_split(a));
+  while (s.log2P < SPLIT_P_LOG2 && a->occ > s.P * (int64_t)s.H_eff / 2) KHIP_TRY(part_split(a));
   const int P = (int)s.P;
   const char* ti = getenv("KHIP_TILE_ITEMS");
   const int64_t tile = (int64_t)PT_THREADS * (ti ? atoi(ti) : PT_ITEMS);
@@ -1256,6 +1261,8 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     if (s.col_word[c] >= 0) L.word_col[s.col_word[c]] = (int8_t)c;
   }
   const size_t hist_lds = (size_t)P * 4;
+  if (hist_lds > 64 * 1024)
+    hipFuncSetAttribute((const void*)k_part_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hist_lds);
   // 1. histogram + tile stream-time maxima
   ev_record_part(a, 0);
   hipLaunchKernelGGL(k_part_hist, dim3(nT), dim3(PT_THREADS), hist_lds, a->stream, keys, ts, kv, rv, n, tile, s.log2P,
@@ -1290,6 +1297,8 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   const int U = su ? atoi(su) : (narrow ? 8 : 16);
   auto scat = narrow ? (U >= 16 ? k_part_scatter<16, true> : (U >= 8 ? k_part_scatter<8, true> : k_part_scatter<4, true>))
                      : (U >= 16 ? k_part_scatter<16, false> : (U >= 8 ? k_part_scatter<8, false> : k_part_scatter<4, false>));
+  if (!lvl2 && hist_lds > 64 * 1024)
+    hipFuncSetAttribute((const void*)scat, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hist_lds);
   hipLaunchKernelGGL(scat, dim3(nT), dim3(PT_THREADS), lvl2 ? (size_t)B * 4 : hist_lds, a->stream, keys, ts, kv, rv,
                      cols, a->desc.n_cols, ct, n, tile, s.log2P - fbits, pad, nT,
                      lvl2 ? s.hcoarse.as<uint32_t>() : s.hist.as<uint32_t>(), s.pbase.as<int64_t>(),

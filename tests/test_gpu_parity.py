@@ -211,6 +211,19 @@ def test_many_partitions_vs_oracle(prod, orc, win, engine):
     assert_snap_equal(g, o, desc, ABS_SUM)
 
 
+@pytest.mark.parametrize("win", [1, 3])
+def test_max_partitions_vs_oracle(prod, orc, win):
+    # a hint past 2^14 x 0.7 LDS tables of groups gives 2^15 partitions (128 KB LDS histogram)
+    rng = np.random.default_rng(91 + win)
+    batches = [_random_batch(rng, 200_000, "INT64", 60_000, 300_000, 20_000, t0=b * 200_000) for b in range(2)]
+    kw = dict(WINDOWS[win], key_type="INT64", col_types=["INT32", "INT64", "DOUBLE", "DOUBLE"],
+              aggs=[("COUNT_STAR", -1), ("SUM", 1), ("MAX", 0)],
+              capacity_hint=60_000_000)
+    (g, gs, desc), (o, os_, _) = _run_both(prod, orc, kw, batches)
+    assert gs == os_
+    assert_snap_equal(g, o, desc)
+
+
 def test_special_doubles(prod, orc):
     vals = np.array([0.0, -0.0, np.nan, np.inf, -np.inf, 1e-310, -1e-310, 5.0, np.nan, -0.0])
     n = len(vals)
