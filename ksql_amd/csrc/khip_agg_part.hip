@@ -1217,7 +1217,8 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                       const uint8_t* rv, const ColPtrs& cols, int64_t* tot) {
   PartState& s = a->part;
   // keep the resident groups per partition well inside the LDS table (split = exact re-layout)
-  while (s.log2P < SPLIT_P_LOG2 && a->occ > s.P * (int64_t)s.H_eff / 2) KHIP_TRY(part_split(a));
+  // live groups only: closed (evicted) windows live in the flat store, not in the LDS tables
+  while (s.log2P < SPLIT_P_LOG2 && a->occ - s.closed_n > s.P * (int64_t)s.H_eff / 2) KHIP_TRY(part_split(a));
   const int P = (int)s.P;
   const char* ti = getenv("KHIP_TILE_ITEMS");
   const int64_t tile = (int64_t)PT_THREADS * (ti ? atoi(ti) : PT_ITEMS);
