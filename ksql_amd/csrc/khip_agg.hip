@@ -1192,6 +1192,7 @@ khip_status khip_agg_get(khip_agg* a, const khip_pull* q, const khip_having* h, 
     pd.keys = dkeys.as<int64_t>();
     pd.n_keys = (int64_t)k.size();
   }
+  if (pd.n_keys > 0) pd.host_keys = k.data();
   std::vector<uint64_t> rows;
   int64_t n = 0;
   KHIP_TRY(compact_rows(a, h, &rows, &n, &pd));

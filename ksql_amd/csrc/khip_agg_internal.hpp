@@ -64,6 +64,10 @@ struct HavingDev {
   int64_t n_keys;
   int64_t ws_lo, ws_hi, we_lo, we_hi, size_ms;
   int32_t log2P;  // partitioned engine: partitions = 2^log2P (partition-directed lookups)
+  const int64_t* host_keys;  // host copy of `keys` (host side only)
+  // partitioned engine, > 256 keys: keys grouped by partition (sorted within each), offsets P+1
+  const int64_t* pkeys;
+  const int64_t* pkoff;
 };
 
 __device__ __forceinline__ bool pull_ok(const uint64_t* s, const HavingDev& h) {

@@ -978,7 +978,17 @@ __global__ __launch_bounds__(256) void k_part_rows(const uint64_t* __restrict__ 
   __shared__ int64_t lbase;
   __shared__ int lhit;
   const int64_t p = blockIdx.x;
-  if (h.pull && h.n_keys > 0 && h.n_keys <= (int64_t)blockDim.x) {
+  HavingDev hp = h;  // this partition's view of the query keys
+  if (h.pkoff) {
+    // point lookup, many keys: the keys of this partition only (grouped on the host)
+    const int64_t k0 = h.pkoff[p], k1 = h.pkoff[p + 1];
+    if (k0 == k1) {
+      if (threadIdx.x == 0 && counts) counts[p] = 0;
+      return;
+    }
+    hp.keys = h.pkeys + k0;
+    hp.n_keys = k1 - k0;
+  } else if (h.pull && h.n_keys > 0 && h.n_keys <= (int64_t)blockDim.x) {
     // point lookup: only the partitions owning one of the query keys are read
     if (threadIdx.x == 0) lhit = 0;
     __syncthreads();
@@ -995,7 +1005,7 @@ __global__ __launch_bounds__(256) void k_part_rows(const uint64_t* __restrict__ 
   int64_t total = 0;
   for (int64_t r0 = 0; r0 < n; r0 += 256) {
     const int64_t r = r0 + threadIdx.x;
-    const bool take = r < n && having_ok(src + r * sw, h);
+    const bool take = r < n && having_ok(src + r * sw, hp);
     const uint64_t bal = __ballot(take);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) lcnt[wave] = __popcll(bal);
@@ -1457,6 +1467,34 @@ khip_status part_compact(khip_agg* a, const HavingDev& h_in, std::vector<uint64_
   PartState& s = a->part;
   HavingDev h = h_in;
   h.log2P = s.log2P;
+  // more query keys than one block checks at once: group them by partition on the host so
+  // every k_part_rows block reads only its own keys (and partitions without keys exit)
+  DevBuf pk, pko;
+  std::vector<int64_t> hpk, hpko;
+  if (h.pull && h.n_keys > 256 && h.host_keys) {
+    const int64_t nk = h.n_keys;
+    const int P = (int)s.P;
+    std::vector<std::pair<uint32_t, int64_t>> kp((size_t)nk);
+    for (int64_t i = 0; i < nk; i++) {
+      const int64_t key = h.host_keys[i];
+      const uint64_t hk = mix64((uint64_t)key ^ 0x6A09E667F3BCC908ULL);  // key_hash
+      kp[(size_t)i] = {s.log2P == 0 ? 0u : (uint32_t)(hk >> (64 - s.log2P)), key};
+    }
+    std::sort(kp.begin(), kp.end());
+    hpk.resize((size_t)nk);
+    hpko.assign((size_t)P + 1, 0);
+    for (int64_t i = 0; i < nk; i++) {
+      hpk[(size_t)i] = kp[(size_t)i].second;
+      hpko[kp[(size_t)i].first + 1]++;
+    }
+    for (int q = 0; q < P; q++) hpko[q + 1] += hpko[q];
+    KHIP_TRY(pk.ensure((size_t)nk * 8));
+    KHIP_TRY(pko.ensure((size_t)(P + 1) * 8));
+    KHIP_TRY_HIP(hipMemcpyAsync(pk.p, hpk.data(), (size_t)nk * 8, hipMemcpyHostToDevice, a->stream));
+    KHIP_TRY_HIP(hipMemcpyAsync(pko.p, hpko.data(), (size_t)(P + 1) * 8, hipMemcpyHostToDevice, a->stream));
+    h.pkeys = pk.as<int64_t>();
+    h.pkoff = pko.as<int64_t>();
+  }
   const int P = (int)s.P;
   KHIP_TRY(s.counts.ensure((P + 1) * 8));
   hipLaunchKernelGGL(k_part_rows, dim3(P), dim3(256), 0, a->stream, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
