@@ -13,7 +13,7 @@ for cfg in possible_fraud hopping_double clickstream_join repartition_sum; do
   grep '^{' gpurun_out/legs/$cfg.log > gpurun_out/legs/$cfg.jsonl
   cut -c1-600 gpurun_out/legs/$cfg.jsonl
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/legs/prof_c5 -o c5 -- \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/legs/prof_c5 -o c5 --output-format csv -- \
   python3 bench.py --config repartition_sum --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/legs/prof_c5.log 2>&1 \
   || { tail -30 gpurun_out/legs/prof_c5.log; exit 2; }
 find gpurun_out/legs/prof_c5 -name '*kernel_stats.csv' | head -3
