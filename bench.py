@@ -1,32 +1,51 @@
 #!/usr/bin/env python3
 """Headline benchmark: windowed GROUP BY records/sec on MI355X (BASELINE.json metric).
 
-Workload (N=1): BASELINE.json configs[1], "possible_fraud":
+Workload (default, N=1): BASELINE.json configs[1], "possible_fraud":
     CREATE TABLE possible_fraud AS SELECT card_number, COUNT(*) FROM ...
     WINDOW TUMBLING (SIZE 5 SECONDS) GROUP BY card_number HAVING COUNT(*) > 3;
-  100M records, 10M distinct card numbers (BIGINT form), 10 s of event time with
-  <= 500 ms disorder (ksql_amd/synth.py).  One step = a fresh query instance over the
-  whole workload: reset the HBM table, push the 100M device-resident records through
-  the C ABI (stream time, late drop, window assignment, (key, window) upsert), and
-  materialize the HAVING result count on the device.  Inputs are generated in HBM
-  before the timed region; the PCIe-inclusive rate is reported separately
-  (DESIGN.md).
+  100M records, 10M distinct card numbers (BIGINT form; --utf8: 16-byte VARCHAR card numbers
+  through the device key dictionary), 10 s of event time with <= 500 ms disorder
+  (ksql_amd/synth.py).  One step = a fresh query instance over the whole workload: reset the
+  HBM table, push the 100M device-resident records through the C ABI (stream time, late drop,
+  window assignment, (key, window) upsert), and count the HAVING rows on the device.  Inputs
+  are generated in HBM before the timed region; the PCIe-inclusive rate is reported
+  separately (never `value`).
 
-Multi-GPU (torchrun): weak scaling, one process per GPU.  Rank r owns the card numbers
-k with k % N == r (key-hash sharding = Kafka partitioning) and processes its own 100M
-records with its own stream time (one Kafka task per partition): no data-path
-collective.  value = all records / max-over-ranks time.
+Other legs (--config), one JSON line each, same contract:
+  hourly_metrics   configs[0]: 1M page views, VARCHAR url keys, COUNT(*) TUMBLING 1 HOUR
+  hopping_double   configs[2]: 1e9 records, HOPPING 60 s / 10 s SUM/AVG/MIN/MAX(DOUBLE)
+  clickstream_join configs[3]: 1e8-row users table in HBM, 1e9 clicks, LEFT JOIN + WHERE
+  repartition_sum  configs[4]: GROUP BY a value column → pack → RCCL all-to-all → aggregate
 
-Output: one JSON line (rank 0) with `roofline` for the hot path (the device time of every
-kernel of one push, HIP events on the library's own stream; per-kernel breakdown with each
-kernel's own streamed bytes) and `cpu_baseline` (the C oracle, a
-single-threaded restatement of the reference semantics — the JVM reference cannot run
-on this image — timed on a bounded prefix of the same workload).
+Multi-GPU: `--gpus N` (N > 1) without torchrun's environment relaunches this script under
+`torch.distributed.run` (one process per GPU, 127.0.0.1 rendezvous) before anything touches
+the GPU.  Weak scaling: rank r owns the keys k with k % N == r (key-hash sharding = Kafka
+partitioning) and processes its own records with its own stream time (one Kafka task per
+partition): no data-path collective, except the repartition leg's all-to-all.  Every rank
+runs barrier + synchronize around exactly --steps timed steps; value = all ranks' records /
+max-over-ranks time.
+
+Output: one JSON line (rank 0) with `roofline` and `cpu_baseline`:
+  roofline.achieved / frac   algorithmic bytes per step ÷ the wall time of one
+                             step (ms_per_step, barrier-to-barrier) — the conservative figure;
+  roofline.push              the same bytes ÷ the device time of the push's kernels alone (HIP
+                             events on the library's stream), with a per-kernel breakdown;
+  roofline.traffic           HBM bytes per step from the committed rocprofv3 PMC summary
+                             (profiles/traffic.json, FETCH_SIZE x 2 + WRITE_SIZE, gfx950
+                             correction) when it was measured on this exact configuration;
+  cpu_baseline               the oracle (oracle/oracle.c, a C restatement of the reference
+                             semantics — the JVM reference cannot run on this image) timed on a
+                             bounded sample of the same workload, single-threaded and with P
+                             threads over P key-hash shards, with the host's CPU model.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
@@ -35,7 +54,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
-BYTES_PER_RECORD_C2 = 80  # W_in 16 + F(1) * 2 * S_slot(32)
+CPU_LABEL = "CPU restatement of the reference semantics (oracle/oracle.c), not the JVM reference"
 
 
 def parse():
@@ -43,213 +62,91 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--records", type=int, default=100_000_000)
-    ap.add_argument("--keys", type=int, default=10_000_000)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU baseline sample time")
+    ap.add_argument("--config", choices=["possible_fraud", "hourly_metrics", "hopping_double", "clickstream_join",
+                                         "repartition_sum"], default="possible_fraud",
+                    help="possible_fraud = BASELINE configs[1] (the headline); hourly_metrics = configs[0]; "
+                         "hopping_double = configs[2]; clickstream_join = configs[3]; repartition_sum = configs[4]")
+    ap.add_argument("--records", type=int, default=None, help="records per GPU (default: the config's)")
+    ap.add_argument("--keys", type=int, default=10_000_000, help="possible_fraud: card numbers per GPU")
+    ap.add_argument("--utf8", action="store_true", help="possible_fraud: VARCHAR card numbers (16 bytes)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target CPU baseline sample time per run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     ap.add_argument("--engine", choices=["part", "atomic"], default="part")
-    ap.add_argument("--config", choices=["possible_fraud", "hopping_double", "clickstream_join", "repartition_sum"],
-                    default="possible_fraud",
-                    help="possible_fraud = BASELINE configs[1] (the headline); hopping_double = configs[2]; "
-                         "clickstream_join = configs[3]; repartition_sum = configs[4]")
     ap.add_argument("--slice", type=int, default=1 << 27, help="hopping_double: records per micro-batch push")
     ap.add_argument("--users", type=int, default=100_000_000, help="clickstream_join: table rows")
+    ap.add_argument("--no-extras", action="store_true", help="skip the PCIe-inclusive and pull-query side numbers")
     return ap.parse_args()
 
 
-def cpu_baseline(n_total, keys, target_s):
-    """Oracle (single-threaded C restatement) on a prefix of the same workload."""
-    from ksql_amd import abi, synth
-    orc = abi.load_oracle()
+# ------------------------------------------------------------------ multi-GPU launch
 
-    def run(m):
-        card, ts = synth.possible_fraud(0, m, n_total, keys=keys)
-        b = abi.HostBatch(ts, keys=card)
-        h = abi.AggHandle(orc, abi.make_agg_desc(window_kind="TUMBLING", size_ms=5000, key_type="INT64",
-                                                 aggs=[("COUNT_STAR", -1)]))
-        t0 = time.perf_counter()
-        h.push(b, stats=False)
-        dt = time.perf_counter() - t0
-        h.close()
-        return dt
-
-    m = 1_000_000
-    dt = run(m)
-    m2 = int(min(max(m * target_s / max(dt, 1e-3), m), 60_000_000))
-    if m2 > m:
-        m, dt = m2, run(m2)
-    return {"value": m / dt, "unit": "records/s", "cores": 1, "kind": "port",
-            "sample": "first %d of the %d possible_fraud records (C oracle, 1 thread, %.1f s)" % (m, n_total, dt)}
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
 
-def load_traffic(path, n, engine):
-    """HBM bytes per push from the committed PMC summary (tools/pmc_traffic.py), if it was
-    measured on this workload size and engine."""
+def relaunch(args):
+    """--gpus N without torchrun's environment: run this script under torch.distributed.run as
+    a child (one rank per GPU) and exit with its code.  Nothing here has touched the GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ------------------------------------------------------------------ helpers
+
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "model": model}
+
+
+def cpu_threads():
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def sized_run(run, m0, target_s, m_max):
+    """run(m) -> seconds; grow the sample so it takes about target_s (bounded by m_max)."""
+    dt = run(m0)
+    m = int(min(max(m0 * target_s / max(dt, 1e-3), m0), m_max))
+    if m > m0:
+        dt = run(m)
+        return m, dt
+    return m0, dt
+
+
+def cpu_baseline_block(single, par, P, unit, sample):
+    return {"value": par[0] / par[1], "unit": unit, "cores": P, "kind": "port", "sample": sample % (par[0], P),
+            "single_thread": {"value": single[0] / single[1], "cores": 1, "records": single[0],
+                              "seconds": single[1]},
+            "parallel_seconds": par[1], "cpu": cpu_info(), "label": CPU_LABEL}
+
+
+def load_traffic(path, config, n, variant=""):
+    """HBM bytes per step from the committed PMC summary (tools/pmc_traffic.py), if it was
+    measured on this configuration and size."""
     try:
         with open(path) as f:
             t = json.load(f)
-        rec = t.get("possible_fraud", {}).get("push" if engine == "part" else "k_apply")
+        rec = t.get(config + variant)
         if rec and rec.get("records") == n:
-            return rec["hbm_bytes_per_launch"]
+            return rec["hbm_bytes_per_step"]
     except (OSError, ValueError):
         pass
     return None
-
-
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
-    from ksql_amd import abi, synth
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    lib = abi.load_product()
-    if args.config == "repartition_sum":
-        return bench_repartition(args, lib, rank, world, local)
-    if args.config == "hopping_double":
-        return bench_hopping_double(args, lib, rank, world, local)
-    if args.config == "clickstream_join":
-        return bench_join(args, lib, rank, world, local)
-
-    n = args.records
-    card, ts = synth.possible_fraud(0, n, n, xp="torch", device="cuda", rank=rank, world=world, keys=args.keys)
-    torch.cuda.synchronize()
-    batch = abi.DeviceBatch(ts, keys=card)
-    desc = abi.make_agg_desc(window_kind="TUMBLING", size_ms=5000, key_type="INT64", aggs=[("COUNT_STAR", -1)],
-                             device=local, capacity_hint=int(min(3 * args.keys, 2 * n)),
-                             flags=abi.FLAG_PROFILE | (abi.FLAG_ENGINE_ATOMIC if args.engine == "atomic" else 0))
-    h = abi.AggHandle(lib, desc)
-    having = {"agg": 0, "op": "GT", "value": 3}
-
-    def step():
-        h.reset()
-        st = h.push(batch)
-        rows = h.count_rows(having)
-        return st, rows
-
-    for _ in range(max(args.warmup, 1)):
-        st, rows = step()
-    assert st["rows_accepted"] == n and st["windows_applied"] == n, st
-    h.kernel_times(reset=True)
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        st, rows = step()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    kt = h.kernel_times()
-    groups = int(h.count_rows(None))
-
-    # PCIe-inclusive rate (host-resident input, one step) for DESIGN.md — not `value`
-    pcie = None
-    if rank == 0 and n <= 100_000_000:
-        hb = abi.HostBatch(ts.cpu().numpy(), keys=card.cpu().numpy())
-        h.reset()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        h.push(hb)
-        h.count_rows(having)
-        pcie = n / (time.perf_counter() - t1)
-
-    # pull-query latency on the materialized table (khip_agg_get, SURVEY §8(f)-3), not `value`
-    pull = None
-    if rank == 0:
-        qk = card[: 1 << 12].cpu().numpy()
-        pull = {}
-        for nk in (1, 100, 4096):
-            h.get(qk[:nk])  # warm
-            t1 = time.perf_counter()
-            reps = 5
-            for _ in range(reps):
-                r = h.get(qk[:nk])
-            pull["keys_%d_ms" % nk] = (time.perf_counter() - t1) * 1000.0 / reps
-            pull["keys_%d_rows" % nk] = int(r["n"])
-
-    if rank == 0:
-        ms_step = elapsed * 1000.0 / args.steps
-        value = world * n * args.steps / elapsed
-        launches = max(kt["apply_launches"], 1)
-        phase = {k: kt[k] / launches for k in ("stream_time_ms", "partition_ms", "apply_ms", "finalize_ms")}
-        push_ms = sum(phase.values())  # device time of every kernel of one push (HIP events)
-        achieved = BYTES_PER_RECORD_C2 * n / (push_ms / 1000.0) / 1e9
-        traffic = load_traffic(args.traffic_json, n, args.engine)
-        # each kernel's own algorithmic streams (bytes / record) for the breakdown
-        own = ({"stream_time_ms": 16, "partition_ms": 32, "apply_ms": 16 + 32.0 * groups / n, "finalize_ms": 0}
-               if args.engine == "part" else
-               {"stream_time_ms": 8, "partition_ms": 0, "apply_ms": 80, "finalize_ms": 0})
-        per_kernel = {k: {"ms": phase[k], "bytes_per_record": own[k],
-                          "GB/s": own[k] * n / (phase[k] / 1000.0) / 1e9 if phase[k] > 0 else None}
-                      for k in phase if phase[k] > 0}
-        out = {
-            "metric": "records/sec, windowed GROUP BY (COUNT(*) TUMBLING 5 s GROUP BY card_number HAVING > 3)",
-            "value": value,
-            "unit": "records/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "int64",
-            "data": "synthetic (splitmix64, ksql_amd/synth.py), device-resident columnar batch",
-            "config": {"workload": "possible_fraud", "records_per_gpu": n, "keys_per_gpu": args.keys,
-                       "window": "TUMBLING 5s, grace default", "having": "COUNT(*) > 3",
-                       "groups_per_gpu": groups, "having_rows_per_gpu": int(rows),
-                       "parallelism": "key-hash shards x%d" % world},
-            "roofline": {"bound": "hbm",
-                         "kernel": ("khip_agg_push = k_part_hist + scans + k_part_scatter + k_part_agg + commit"
-                                    if args.engine == "part" else "khip_agg_push (k_apply dominant)"),
-                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "algorithmic_bytes_per_record": BYTES_PER_RECORD_C2, "push_ms": push_ms,
-                         "engine": args.engine, "per_kernel": per_kernel},
-            "pcie_inclusive_records_per_s": pcie,
-            "pull_query": pull,
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(n, args.keys, args.cpu_seconds)
-        else:
-            out["cpu_baseline"] = None
-        print(json.dumps(out))
-    h.close()
-    if world > 1:
-        dist.destroy_process_group()
-
-
-def stream_copy_gbs(nbytes=1 << 31):
-    """Achievable HBM rate on this box: one device-to-device copy of `nbytes` (read + write
-    bytes / time), the practical ceiling next to the 8 TB/s spec peak."""
-    import torch
-    a = torch.empty(nbytes // 8, dtype=torch.int64, device="cuda")
-    b = torch.empty_like(a)
-    b.copy_(a)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(5):
-        b.copy_(a)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / 5
-    del a, b
-    return 2.0 * nbytes / (ms / 1000.0) / 1e9
 
 
 def barrier_sync(world):
@@ -270,24 +167,302 @@ def max_over_ranks(elapsed, world):
     return elapsed
 
 
-def finish(world):
+def timed_loop(step, steps, world):
+    barrier_sync(world)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = step()
+    barrier_sync(world)
+    return r, max_over_ranks(time.perf_counter() - t0, world)
+
+
+def roofline(bytes_per_step, ms_step, push_ms=None, per_kernel=None, traffic=None, bytes_per_record=None,
+             kernel="", extra=None):
+    achieved = bytes_per_step / (ms_step / 1000.0) / 1e9
+    r = {"bound": "hbm", "kernel": kernel, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "algorithmic_bytes_per_record": bytes_per_record,
+         "basis": "algorithmic bytes per step / ms_per_step (wall, barrier to barrier)"}
+    if push_ms:
+        pa = bytes_per_step / (push_ms / 1000.0) / 1e9
+        r["push"] = {"ms": push_ms, "achieved": pa, "frac": pa / HBM_PEAK_GBS,
+                     "basis": "the same bytes / device time of the push kernels (HIP events, library stream)"}
+        if per_kernel:
+            r["push"]["per_kernel"] = per_kernel
+    if traffic:
+        r["traffic_over_algorithmic"] = traffic / bytes_per_step
+    if extra:
+        r.update(extra)
+    return r
+
+
+def line(metric, value, world, args, ms_step, dtype, data, config, roof, cpu, **kw):
+    out = {"metric": metric, "value": value, "unit": "records/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": dtype, "data": data, "config": config, "roofline": roof,
+           "cpu_baseline": cpu}
+    out.update(kw)
+    print(json.dumps(out), flush=True)
+
+
+def push_phases(kt, launches):
+    launches = max(launches, 1)
+    return {k: kt[k] / launches for k in ("stream_time_ms", "dict_ms", "partition_ms", "apply_ms", "finalize_ms")}
+
+
+def stream_copy_gbs(nbytes=1 << 31):
+    """Achievable HBM rate on this box: one device-to-device copy (read + write bytes / time)."""
+    import torch
+    a = torch.empty(nbytes // 8, dtype=torch.int64, device="cuda")
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 5
+    del a, b
+    return 2.0 * nbytes / (ms / 1000.0) / 1e9
+
+
+# ------------------------------------------------------------------ main
+
+def main():
+    args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None:
+        return relaunch(args)
+    import torch
     import torch.distributed as dist
+    from ksql_amd import abi
+
+    world = int(world_env or "1")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    lib = abi.load_product()
+    legs = {"possible_fraud": bench_possible_fraud, "hourly_metrics": bench_hourly_metrics,
+            "hopping_double": bench_hopping_double, "clickstream_join": bench_join,
+            "repartition_sum": bench_repartition}
+    legs[args.config](args, lib, rank, world, local)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
+
+# ------------------------------------------------------------------ C2 possible_fraud
+
+BYTES_PER_RECORD_C2 = 80  # SURVEY.md §8(d): W_in 16 + F(1) x 2 x S_slot(32)
+BYTES_PER_RECORD_C2_UTF8 = 16 + 8 + 8 + 64  # key bytes 16 + offset 8 + ts 8 + 2 x S_slot(32)
+
+
+def bench_possible_fraud(args, lib, rank, world, local):
+    import torch
+    from ksql_amd import abi, synth
+    n = args.records or 100_000_000
+    card, ts = synth.possible_fraud(0, n, n, xp="torch", device="cuda", rank=rank, world=world, keys=args.keys)
+    if args.utf8:
+        offs, kbytes = synth.card_utf8(card, xp="torch")
+        batch = abi.DeviceBatch(ts, key_offsets=offs, key_bytes=kbytes)
+    else:
+        batch = abi.DeviceBatch(ts, keys=card)
+    torch.cuda.synchronize()
+    desc = abi.make_agg_desc(window_kind="TUMBLING", size_ms=5000, key_type="UTF8" if args.utf8 else "INT64",
+                             aggs=[("COUNT_STAR", -1)], device=local, capacity_hint=int(min(3 * args.keys, 2 * n)),
+                             flags=abi.FLAG_PROFILE | (abi.FLAG_ENGINE_ATOMIC if args.engine == "atomic" else 0))
+    h = abi.AggHandle(lib, desc)
+    having = {"agg": 0, "op": "GT", "value": 3}
+
+    def step():
+        h.reset()
+        st = h.push(batch)
+        return st, h.count_rows(having)
+
+    for _ in range(max(args.warmup, 1)):
+        st, rows = step()
+    assert st["rows_accepted"] == n and st["windows_applied"] == n, st
+    h.kernel_times(reset=True)
+    (st, rows), elapsed = timed_loop(step, args.steps, world)
+    kt = h.kernel_times()
+    groups = int(h.count_rows(None))
+
+    pcie = pull = None
+    if rank == 0 and not args.no_extras and not args.utf8 and n <= 100_000_000:
+        # PCIe-inclusive rate (host-resident input, one step) for DESIGN.md — never `value`
+        hb = abi.HostBatch(ts.cpu().numpy(), keys=card.cpu().numpy())
+        h.reset()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        h.push(hb)
+        h.count_rows(having)
+        pcie = n / (time.perf_counter() - t1)
+        del hb
+        # pull-query latency on the materialized table (khip_agg_get, SURVEY §8(f)-3)
+        qk = card[: 1 << 12].cpu().numpy()
+        pull = {}
+        for nk in (1, 100, 4096):
+            h.get(qk[:nk])
+            t1 = time.perf_counter()
+            for _ in range(5):
+                r = h.get(qk[:nk])
+            pull["keys_%d_ms" % nk] = (time.perf_counter() - t1) * 1000.0 / 5
+            pull["keys_%d_rows" % nk] = int(r["n"])
+    h.close()
+    if rank != 0:
+        return
+    ms_step = elapsed * 1000.0 / args.steps
+    phase = push_phases(kt, kt["apply_launches"])
+    push_ms = sum(phase.values())
+    bpr = BYTES_PER_RECORD_C2_UTF8 if args.utf8 else BYTES_PER_RECORD_C2
+    own = {"stream_time_ms": 16, "dict_ms": 32, "partition_ms": 32, "apply_ms": 16 + 32.0 * groups / n,
+           "finalize_ms": 0}
+    per_kernel = {k: {"ms": phase[k], "bytes_per_record": own[k],
+                      "GB/s": own[k] * n / (phase[k] / 1000.0) / 1e9} for k in phase if phase[k] > 0}
+    variant = "_utf8" if args.utf8 else ""
+    traffic = load_traffic(args.traffic_json, "possible_fraud" + ("_atomic" if args.engine == "atomic" else ""), n,
+                           variant)
+    roof = roofline(bpr * n, ms_step, push_ms, per_kernel, traffic, bpr,
+                    kernel="khip_agg_push (k_part_hist + scans + k_part_scatter + k_part_agg + commit) + HAVING count")
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_agg(
+            lambda m: synth.possible_fraud(0, m, n, keys=args.keys), args.utf8,
+            dict(window_kind="TUMBLING", size_ms=5000, aggs=[("COUNT_STAR", -1)]),
+            args.cpu_seconds, 40_000_000, "first %%d of the %d possible_fraud records, %%d key-hash shards" % n)
+    line("records/sec, windowed GROUP BY (COUNT(*) TUMBLING 5 s GROUP BY card_number HAVING > 3)",
+         world * n * args.steps / elapsed, world, args, ms_step, "int64",
+         "synthetic (splitmix64, ksql_amd/synth.py), device-resident columnar batch",
+         {"workload": "possible_fraud", "key": "VARCHAR(16) card_number" if args.utf8 else "BIGINT card_number",
+          "records_per_gpu": n, "keys_per_gpu": args.keys, "window": "TUMBLING 5s, grace default",
+          "having": "COUNT(*) > 3", "groups_per_gpu": groups, "having_rows_per_gpu": int(rows),
+          "parallelism": "key-hash shards x%d" % world},
+         roof, cpu, pcie_inclusive_records_per_s=pcie, pull_query=pull)
+
+
+def cpu_baseline_agg(gen, utf8, kw, target_s, m_max, sample):
+    """Oracle on a prefix of the workload: 1 thread (sequential oracle_agg_push) and P threads
+    (oracle_agg_push_sharded over P key-hash shards).  Each run is a fresh task."""
+    from ksql_amd import abi, synth
+    orc = abi.load_oracle()
+    P = cpu_threads()
+
+    def batch(m):
+        out = gen(m)
+        key, ts = out[0], out[1]
+        cols = list(out[2:3]) if len(out) > 2 else []
+        cval = list(out[3:4]) if len(out) > 3 else []
+        if utf8:
+            offs, kb = synth.card_utf8(key)
+            return abi.HostBatch(ts, key_offsets=offs, key_bytes=kb, cols=cols, col_valid=cval)
+        return abi.HostBatch(ts, keys=key, cols=cols, col_valid=cval)
+
+    def run(m, shards):
+        b = batch(m)
+        desc = abi.make_agg_desc(key_type="UTF8" if utf8 else "INT64", **kw)
+        h = abi.AggHandle(orc, desc) if shards == 1 else abi.ShardedOracleAgg(orc, desc, shards)
+        t0 = time.perf_counter()
+        h.push(b, stats=False)
+        dt = time.perf_counter() - t0
+        h.close()
+        return dt
+
+    single = sized_run(lambda m: run(m, 1), 500_000, target_s, m_max)
+    par = sized_run(lambda m: run(m, P), 1_000_000, target_s, m_max)
+    return cpu_baseline_block(single, par, P, "records/s", sample)
+
+
+# ------------------------------------------------------------------ C1 hourly_metrics
+
+def bench_hourly_metrics(args, lib, rank, world, local):
+    """configs[0]: COUNT(*) TUMBLING 1 HOUR GROUP BY url over 1M page views (VARCHAR url keys through
+    the device dictionary).  One step = reset + push + row count.  The reference's own
+    CPU-runnable case; at 1M records one step is a handful of small launches."""
+    import torch
+    from ksql_amd import abi, synth
+    n = args.records or synth.CONFIGS["hourly_metrics"]["n"]
+    offs, kb, ts = synth.hourly_metrics_utf8(0, n, n)
+    dev = lambda a: torch.from_numpy(a).to("cuda")
+    batch = abi.DeviceBatch(dev(ts), key_offsets=dev(offs), key_bytes=dev(kb))
+    torch.cuda.synchronize()
+    kw = dict(window_kind="TUMBLING", size_ms=3_600_000, key_type="UTF8", aggs=[("COUNT_STAR", -1)])
+    h = abi.AggHandle(lib, abi.make_agg_desc(**kw, device=local, capacity_hint=40_000, flags=abi.FLAG_PROFILE))
+
+    def step():
+        h.reset()
+        st = h.push(batch)
+        return st, h.count_rows(None)
+
+    for _ in range(max(args.warmup, 1)):
+        st, groups = step()
+    assert st["rows_accepted"] == n, st
+    h.kernel_times(reset=True)
+    (st, groups), elapsed = timed_loop(step, args.steps, world)
+    kt = h.kernel_times()
+    h.close()
+    if rank != 0:
+        return
+    ms_step = elapsed * 1000.0 / args.steps
+    bpr = float(kb.size) / n + 8 + 8 + 2 * 32  # key bytes + offset + ts + 2 x S_slot(32)
+    phase = push_phases(kt, kt["apply_launches"])
+    roof = roofline(bpr * n, ms_step, sum(phase.values()), None, None, bpr,
+                    kernel="khip_agg_push (UTF8 dictionary + partitioned aggregate) + row count",
+                    extra={"note": "1M records: launch/latency-bound, not HBM-bound"})
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_hourly(n, args.cpu_seconds)
+    line("records/sec, windowed GROUP BY (COUNT(*) TUMBLING 1 HOUR GROUP BY url)",
+         world * n * args.steps / elapsed, world, args, ms_step, "int64",
+         "synthetic (splitmix64, ksql_amd/synth.py hourly_metrics), device-resident columnar batch",
+         {"workload": "hourly_metrics", "key": "VARCHAR url", "records_per_gpu": n, "urls": 10_000,
+          "window": "TUMBLING 1 HOUR", "groups_per_gpu": int(groups), "parallelism": "key-hash shards x%d" % world},
+         roof, cpu)
+
+
+def cpu_baseline_hourly(n, target_s):
+    from ksql_amd import abi, synth
+    orc = abi.load_oracle()
+    P = cpu_threads()
+    kw = dict(window_kind="TUMBLING", size_ms=3_600_000, key_type="UTF8", aggs=[("COUNT_STAR", -1)])
+    offs, kb, ts = synth.hourly_metrics_utf8(0, n, n)
+    b = abi.HostBatch(ts, key_offsets=offs, key_bytes=kb)
+
+    def run(shards, reps):
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            h = abi.AggHandle(orc, abi.make_agg_desc(**kw)) if shards == 1 else \
+                abi.ShardedOracleAgg(orc, abi.make_agg_desc(**kw), shards)
+            h.push(b, stats=False)
+            h.close()
+        return time.perf_counter() - t0
+
+    out = []
+    for shards in (1, P):
+        dt = run(shards, 1)
+        reps = max(1, int(target_s / max(dt, 1e-3)))
+        out.append((n * reps, run(shards, reps)))
+    return cpu_baseline_block(out[0], out[1], P, "records/s",
+                              "%%d records (the 1M-record hourly_metrics run, repeated), %%d key-hash shards")
+
+
+# ------------------------------------------------------------------ C3 hopping_double
 
 BYTES_PER_RECORD_C3 = 24.125 + 6 * 2 * 56  # SURVEY.md §8(d): W_in + F x 2 x S_slot = 696.1
 
 
 def bench_hopping_double(args, lib, rank, world, local):
-    """C3: HOPPING (SIZE 1 MINUTE, ADVANCE BY 10 SECONDS, GRACE PERIOD 1 MINUTE) SUM/AVG/MIN/MAX
-    of a DOUBLE with 1 % nulls, 1e9 records (1 h of event time) per GPU, key BIGINT in [0, 1e5).
-    One step = a fresh query instance: reset, the 1e9 device-resident records pushed as
-    event-time micro-batches of `--slice` records (closed windows leave the live table between
-    pushes), and the materialized row count."""
+    """configs[2]: HOPPING (SIZE 1 MINUTE, ADVANCE BY 10 SECONDS, GRACE PERIOD 1 MINUTE)
+    SUM/AVG/MIN/MAX of a DOUBLE with 1 % nulls, 1e9 records (1 h of event time) per GPU, key
+    BIGINT in [0, 1e5).  One step = a fresh query instance: reset, the device-resident records
+    pushed as event-time micro-batches of --slice records (closed windows leave the live table
+    between pushes), and the materialized row count."""
     import torch
     from ksql_amd import abi, synth
-    n = args.records if args.records != 100_000_000 else 1_000_000_000
+    n = args.records or 1_000_000_000
     S = max(8, args.slice // 8 * 8)
     cfg = synth.CONFIGS["hopping_double"]
     key, ts, val, valid = synth.hopping_double(0, n, n, xp="torch", device="cuda", rank=rank, world=world)
@@ -299,11 +474,9 @@ def bench_hopping_double(args, lib, rank, world, local):
     keys_here = cfg["keys"] // world
     span_push = cfg["span_ms"] * S / n
     live = int(keys_here * (span_push + cfg["size_ms"] + cfg["grace_ms"] + cfg["disorder_ms"]) / cfg["advance_ms"])
-    desc = abi.make_agg_desc(window_kind="HOPPING", size_ms=cfg["size_ms"], advance_ms=cfg["advance_ms"],
-                             grace_ms=cfg["grace_ms"], key_type="INT64", col_types=["DOUBLE"],
-                             aggs=[("SUM", 0), ("AVG", 0), ("MIN", 0), ("MAX", 0)], device=local,
-                             capacity_hint=live, flags=abi.FLAG_PROFILE)
-    h = abi.AggHandle(lib, desc)
+    kw = dict(window_kind="HOPPING", size_ms=cfg["size_ms"], advance_ms=cfg["advance_ms"], grace_ms=cfg["grace_ms"],
+              key_type="INT64", col_types=["DOUBLE"], aggs=[("SUM", 0), ("AVG", 0), ("MIN", 0), ("MAX", 0)])
+    h = abi.AggHandle(lib, abi.make_agg_desc(**kw, device=local, capacity_hint=live, flags=abi.FLAG_PROFILE))
 
     def step():
         h.reset()
@@ -317,132 +490,50 @@ def bench_hopping_double(args, lib, rank, world, local):
     for _ in range(max(args.warmup, 1)):
         st, groups = step()
     h.kernel_times(reset=True)
-    barrier_sync(world)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        st, groups = step()
-    barrier_sync(world)
-    elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    (st, groups), elapsed = timed_loop(step, args.steps, world)
     kt = h.kernel_times()
-    if rank == 0:
-        ms_step = elapsed * 1000.0 / args.steps
-        phase = {k: kt[k] / args.steps for k in ("stream_time_ms", "partition_ms", "apply_ms", "finalize_ms")}
-        push_ms = sum(phase.values())  # device time of every kernel of the step's pushes (HIP events)
-        achieved = BYTES_PER_RECORD_C3 * n / (push_ms / 1000.0) / 1e9
-        out = {
-            "metric": "records/sec, windowed GROUP BY (SUM/AVG/MIN/MAX(value DOUBLE) HOPPING 60 s / 10 s GROUP BY key)",
-            "value": world * n * args.steps / elapsed, "unit": "records/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (splitmix64, ksql_amd/synth.py hopping_double), device-resident columnar batch",
-            "config": {"workload": "hopping_double", "records_per_gpu": n, "keys_per_gpu": keys_here,
-                       "window": "HOPPING 60s/10s GRACE 60s (F=6)", "micro_batch": S, "pushes": len(batches),
-                       "windows_applied": st["windows_applied"], "windows_late": st["windows_late"],
-                       "groups_per_gpu": int(groups), "parallelism": "key-hash shards x%d" % world},
-            "roofline": {"bound": "hbm", "kernel": "khip_agg_push (all kernels of every micro-batch push)",
-                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None, "algorithmic_bytes_per_record": BYTES_PER_RECORD_C3, "push_ms": push_ms,
-                         "phase_ms_per_step": phase, "stream_copy_GBps": stream_copy_gbs()},
-            "cpu_baseline": None,
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline_hopping(n, args.cpu_seconds)
-        print(json.dumps(out))
     h.close()
-    finish(world)
+    if rank != 0:
+        return
+    ms_step = elapsed * 1000.0 / args.steps
+    phase = {k: kt[k] / args.steps for k in ("stream_time_ms", "partition_ms", "apply_ms", "finalize_ms")}
+    # what the kernels actually stream per record (LDS fan-out: one record in, F window
+    # updates in LDS): hist 16 + scatter 24 read / 32 write + agg 32 + resident rows in and out
+    moved = 16 + 24 + 32 + 32 + 2 * 64.0 * groups / n
+    roof = roofline(BYTES_PER_RECORD_C3 * n, ms_step, sum(phase.values()), None,
+                    load_traffic(args.traffic_json, "hopping_double", n), BYTES_PER_RECORD_C3,
+                    kernel="khip_agg_push (all kernels of every micro-batch push) + row count",
+                    extra={"algorithmic_equivalent": True,
+                           "note": "SURVEY §8(d)'s 696 B/record assumes one HBM slot RMW per (record, window); "
+                                   "the engine fans the 6 windows out in LDS, so frac here is an "
+                                   "algorithmic-equivalent rate, not HBM bandwidth: see streamed_* and traffic",
+                           "streamed_bytes_per_record": moved,
+                           "streamed_frac": moved * n / (ms_step / 1000.0) / 1e9 / HBM_PEAK_GBS,
+                           "phase_ms_per_step": phase, "stream_copy_GBps": stream_copy_gbs()})
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_agg(lambda m: synth.hopping_double(0, m, n), False,
+                               {k: v for k, v in kw.items() if k != "key_type"},
+                               args.cpu_seconds, 20_000_000,
+                               "first %%d of the %d hopping_double records, %%d key-hash shards" % n)
+    line("records/sec, windowed GROUP BY (SUM/AVG/MIN/MAX(value DOUBLE) HOPPING 60 s / 10 s GROUP BY key)",
+         world * n * args.steps / elapsed, world, args, ms_step, "f64",
+         "synthetic (splitmix64, ksql_amd/synth.py hopping_double), device-resident columnar batch",
+         {"workload": "hopping_double", "records_per_gpu": n, "keys_per_gpu": keys_here,
+          "window": "HOPPING 60s/10s GRACE 60s (F=6)", "micro_batch": S, "pushes": len(batches),
+          "windows_applied": st["windows_applied"], "windows_late": st["windows_late"],
+          "groups_per_gpu": int(groups), "parallelism": "key-hash shards x%d" % world},
+         roof, cpu)
 
 
-def cpu_baseline_hopping(n_total, target_s):
-    from ksql_amd import abi, synth
-    orc = abi.load_oracle()
-    cfg = synth.CONFIGS["hopping_double"]
+# ------------------------------------------------------------------ C4 clickstream_join
 
-    def run(m):
-        key, ts, val, valid = synth.hopping_double(0, m, n_total)
-        b = abi.HostBatch(ts, keys=key, cols=[val], col_valid=[valid])
-        h = abi.AggHandle(orc, abi.make_agg_desc(window_kind="HOPPING", size_ms=cfg["size_ms"],
-                                                 advance_ms=cfg["advance_ms"], grace_ms=cfg["grace_ms"],
-                                                 key_type="INT64", col_types=["DOUBLE"],
-                                                 aggs=[("SUM", 0), ("AVG", 0), ("MIN", 0), ("MAX", 0)]))
-        t0 = time.perf_counter()
-        h.push(b, stats=False)
-        dt = time.perf_counter() - t0
-        h.close()
-        return dt
-
-    m = 500_000
-    dt = run(m)
-    m2 = int(min(max(m * target_s / max(dt, 1e-3), m), 40_000_000))
-    if m2 > m:
-        m, dt = m2, run(m2)
-    return {"value": m / dt, "unit": "records/s", "cores": 1, "kind": "port",
-            "sample": "first %d of the %d hopping_double records (C oracle, 1 thread, %.1f s)" % (m, n_total, dt)}
-
-
-def cpu_baseline_join(users, target_s):
-    """Oracle stream-table LEFT JOIN (oracle_table_probe, 1 thread).  Bounded sample: a users
-    table of min(users, 1e7) rows built first (untimed), then clicks drawn over the same
-    1.1x id span probed against it (timed), WHERE level = 'Platinum'."""
-    from ksql_amd import abi, synth
-    orc = abi.load_oracle()
-    U = min(users, 10_000_000)
-    uid, level = synth.users_table(0, U)
-    t = abi.TableHandle(orc, ["INT32"], capacity_hint=U)
-    t.upsert(abi.HostBatch(np.zeros(U, np.int64), keys=uid, cols=[level.astype(np.int32)]))
-    where = {"col": 0, "op": "EQ", "i64": synth.LEVELS.index("Platinum")}
-
-    def run(m):
-        cu, cts = synth.clicks(0, m, U, seed_clicks=5)
-        b = abi.HostBatch(cts, keys=cu)
-        t0 = time.perf_counter()
-        t.probe(b, "LEFT", where)
-        return time.perf_counter() - t0
-
-    m = 1_000_000
-    dt = run(m)
-    m2 = int(min(max(m * target_s / max(dt, 1e-3), m), 50_000_000))
-    if m2 > m:
-        m, dt = m2, run(m2)
-    t.close()
-    return {"value": m / dt, "unit": "records/s", "cores": 1, "kind": "port",
-            "sample": "%d clicks probed against a %d-row users table (C oracle, 1 thread, %.1f s)" % (m, U, dt)}
-
-
-def cpu_baseline_repartition(n_total, target_s):
-    """Oracle C5 step on a prefix of rank 0's source partition (1 thread): Kafka partitioner of
-    the new key (oracle_kafka_partition, 8 destinations) + SUM(amount) TUMBLING 1 MINUTE
-    GROUP BY region_id (oracle_agg_push)."""
-    from ksql_amd import abi, synth
-    orc = abi.load_oracle()
-
-    def run(m):
-        _eid, ts, region, amount = synth.repartition_sum(0, m, n_total)
-        region = np.ascontiguousarray(region, np.int64)
-        dest = np.empty(m, np.int32)
-        h = abi.AggHandle(orc, abi.make_agg_desc(window_kind="TUMBLING", size_ms=60_000, key_type="INT64",
-                                                 col_types=["INT64"], aggs=[("SUM", 0)]))
-        b = abi.HostBatch(ts, keys=region, cols=[amount])
-        t0 = time.perf_counter()
-        orc.dll.oracle_kafka_partition(region.ctypes.data, m, 8, 8, dest.ctypes.data)
-        h.push(b, stats=False)
-        dt = time.perf_counter() - t0
-        h.close()
-        return dt
-
-    m = 1_000_000
-    dt = run(m)
-    m2 = int(min(max(m * target_s / max(dt, 1e-3), m), 60_000_000))
-    if m2 > m:
-        m, dt = m2, run(m2)
-    return {"value": m / dt, "unit": "records/s", "cores": 1, "kind": "port",
-            "sample": "first %d of rank 0's %d repartition_sum records: partitioner + aggregate "
-                      "(C oracle, 1 thread, %.1f s)" % (m, n_total, dt)}
+BYTES_PER_PROBE_C4 = 31  # SURVEY.md §8(d): W_in 16 + table slot 8 + 0.30 x output 24
 
 
 def random_gather_rows_per_s(table_bytes, rows=100_000_000):
-    """Practical ceiling of a hash probe into a table far larger than the caches: torch's
-    gather of `rows` uniformly random 32-byte rows from a `table_bytes` table (one random
-    line per row, the access pattern of a probe), in rows/s."""
+    """Practical ceiling of a hash probe into a table far larger than the caches: torch's gather
+    of `rows` uniformly random 32-byte rows from a `table_bytes` table, in rows/s."""
     import torch
     tab = torch.empty(max(table_bytes // 32, 1), 4, dtype=torch.int64, device="cuda")
     idx = torch.randint(0, tab.shape[0], (rows,), device="cuda")
@@ -458,17 +549,14 @@ def random_gather_rows_per_s(table_bytes, rows=100_000_000):
     return rows / (ms / 1000.0)
 
 
-BYTES_PER_PROBE_C4 = 31  # SURVEY.md §8(d): W_in 16 + table slot 8 + 0.30 x output 24
-
-
 def bench_join(args, lib, rank, world, local):
-    """C4: clickstream LEFT JOIN users WHERE level = 'Platinum'.  The 1e8-row users table is
-    replicated in every GPU's HBM (built once, timed separately); each GPU probes its own
-    1e9 clicks (weak scaling, no exchange).  One step = khip_table_probe_device over all
-    clicks: row-aligned emit/matched bitmaps + the right column, then the emitted count."""
+    """configs[3]: clickstream LEFT JOIN users WHERE level = 'Platinum'.  The 1e8-row users table
+    is replicated in every GPU's HBM (built once, timed separately); each GPU probes its own 1e9
+    clicks (weak scaling, no exchange).  One step = khip_table_probe_device over all clicks:
+    row-aligned emit/matched bitmaps + the right column, then the emitted count."""
     import torch
     from ksql_amd import abi, synth
-    n = args.records if args.records != 100_000_000 else 1_000_000_000
+    n = args.records or 1_000_000_000
     U = args.users
     uid, level = synth.users_table(0, U, xp="torch", device="cuda")
     level = level.to(torch.int32)
@@ -479,8 +567,6 @@ def bench_join(args, lib, rank, world, local):
     t.upsert(tb)
     t.sync()
     build_s = time.perf_counter() - t0
-    # khip_table_create: cap = next_pow2(4/3 x hint) slots of 32 bytes (one INT32 column)
-    table_bytes = (1 << max(10, ((U * 4 + 2) // 3 - 1).bit_length())) * 32
     del tb, uid, level
     cu, cts = synth.clicks(0, n, U, xp="torch", device="cuda", seed_clicks=5 + 1000 * rank)
     batch = abi.DeviceBatch(cts, keys=cu)
@@ -497,54 +583,77 @@ def bench_join(args, lib, rank, world, local):
 
     for _ in range(max(args.warmup, 1)):
         rows = step()
-    barrier_sync(world)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        rows = step()
-    barrier_sync(world)
-    elapsed = max_over_ranks(time.perf_counter() - t0, world)
-    if rank == 0:
-        ms_step = elapsed * 1000.0 / args.steps
-        achieved = BYTES_PER_PROBE_C4 * n / (ms_step / 1000.0) / 1e9
-        out = {
-            "metric": "stream records/sec, stream-table LEFT JOIN (clickstream x users WHERE level = 'Platinum')",
-            "value": world * n * args.steps / elapsed, "unit": "records/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "int64",
-            "data": "synthetic (splitmix64, ksql_amd/synth.py users_table/clicks), device-resident columnar batch",
-            "config": {"workload": "clickstream_join", "table_rows": U, "clicks_per_gpu": n,
-                       "table_build_s": build_s, "table_build_rows_per_s": U / build_s,
-                       "emitted_rows_per_gpu": int(rows), "parallelism": "replicated table x%d" % world},
-            "roofline": {"bound": "hbm", "kernel": "k_probe (khip_table_probe_device)", "achieved": achieved,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "algorithmic_bytes_per_record": BYTES_PER_PROBE_C4, "stream_copy_GBps": stream_copy_gbs(),
-                         "table_bytes": table_bytes,
-                         "random_gather_rows_per_s": random_gather_rows_per_s(table_bytes)},
-            "cpu_baseline": None,
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline_join(U, args.cpu_seconds)
-        print(json.dumps(out))
+    rows, elapsed = timed_loop(step, args.steps, world)
+    # khip_table_create: cap = next_pow2(4/3 x hint) slots of 32 bytes (one INT32 column)
+    info = {"table_bytes": (1 << max(10, ((U * 4 + 2) // 3 - 1).bit_length())) * 32}
     t.close()
-    finish(world)
+    if rank != 0:
+        return
+    ms_step = elapsed * 1000.0 / args.steps
+    roof = roofline(BYTES_PER_PROBE_C4 * n, ms_step, None, None, load_traffic(args.traffic_json, "clickstream_join", n),
+                    BYTES_PER_PROBE_C4, kernel="khip_table_probe_device (probe kernels) + emitted count",
+                    extra={"stream_copy_GBps": stream_copy_gbs(), "table": info,
+                           "random_gather_rows_per_s": random_gather_rows_per_s(info["table_bytes"])})
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_join(U, args.cpu_seconds)
+    line("stream records/sec, stream-table LEFT JOIN (clickstream x users WHERE level = 'Platinum')",
+         world * n * args.steps / elapsed, world, args, ms_step, "int64",
+         "synthetic (splitmix64, ksql_amd/synth.py users_table/clicks), device-resident columnar batch",
+         {"workload": "clickstream_join", "table_rows": U, "clicks_per_gpu": n, "table_build_s": build_s,
+          "table_build_rows_per_s": U / build_s, "emitted_rows_per_gpu": int(rows),
+          "parallelism": "replicated table x%d" % world},
+         roof, cpu)
 
+
+def cpu_baseline_join(users, target_s):
+    """Oracle stream-table LEFT JOIN WHERE level = 'Platinum': a users table of min(users, 1e7)
+    rows built first (untimed), then clicks over the same 1.1x id span probed against it —
+    1 thread, and P threads over P chunks of the stream (the table is read-only)."""
+    from ksql_amd import abi, synth
+    orc = abi.load_oracle()
+    P = cpu_threads()
+    U = min(users, 10_000_000)
+    uid, level = synth.users_table(0, U)
+    t = abi.TableHandle(orc, ["INT32"], capacity_hint=U)
+    t.upsert(abi.HostBatch(np.zeros(U, np.int64), keys=uid, cols=[level.astype(np.int32)]))
+    where = {"col": 0, "op": "EQ", "i64": synth.LEVELS.index("Platinum")}
+
+    def run(m, threads):
+        cu, cts = synth.clicks(0, m, U, seed_clicks=5)
+        bounds = np.linspace(0, m, threads + 1).astype(np.int64)
+        bs = [abi.HostBatch(cts[bounds[k]:bounds[k + 1]], keys=cu[bounds[k]:bounds[k + 1]]) for k in range(threads)]
+        th = [threading.Thread(target=t.probe, args=(bs[k], "LEFT", where)) for k in range(threads)]
+        t0 = time.perf_counter()
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        return time.perf_counter() - t0
+
+    single = sized_run(lambda m: run(m, 1), 1_000_000, target_s, 50_000_000)
+    par = sized_run(lambda m: run(m, P), 2_000_000, target_s, 100_000_000)
+    t.close()
+    return cpu_baseline_block(single, par, P, "records/s",
+                              "%%d clicks probed against a %d-row users table, %%d threads" % U)
+
+
+# ------------------------------------------------------------------ C5 repartition_sum
 
 BYTES_PER_RECORD_C5 = 136  # SURVEY.md §8(d): read 24 + pack 24 + recv 24 + 2 x 32 (slot)
 
 
 def bench_repartition(args, lib, rank, world, local):
-    """C5: GROUP BY region_id (a value column) forces the repartition.  One step per rank:
-    khip_shuffle_pack (Kafka partitioner) → RCCL count exchange + all-to-all over xGMI (N>1)
-    → khip_shuffle_unpack → SUM(amount) TUMBLING 1 MINUTE push → row count.  Weak scaling:
-    every rank owns one source partition of `records` records (1e9 node-wide at N=8 with the
-    default 125M)."""
+    """configs[4]: GROUP BY region_id (a value column) forces the repartition.  One step per rank:
+    khip_shuffle_pack (Kafka partitioner) → RCCL count exchange + all-to-all over xGMI (N > 1) →
+    khip_shuffle_unpack → SUM(amount) TUMBLING 1 MINUTE push → row count.  Weak scaling: every
+    rank owns one source partition of --records records (1e9 node-wide at N = 8 with 125M)."""
     import torch
     import torch.distributed as dist
     from ksql_amd import abi, synth
     from ksql_amd.repartition import Repartition
 
-    n = args.records if args.records != 100_000_000 else 125_000_000
+    n = args.records or 125_000_000
     eid, ts, region, amount = synth.repartition_sum(0, n, n, xp="torch", device="cuda", rank=rank, world=world)
     torch.cuda.synchronize()
     src = abi.DeviceBatch(ts, cols=[region, amount])
@@ -559,8 +668,9 @@ def bench_repartition(args, lib, rank, world, local):
                              flags=abi.FLAG_PROFILE)
     h = abi.AggHandle(lib, desc)
     phases = {"pack": 0.0, "exchange_unpack": 0.0, "aggregate": 0.0}
+    state = {"timed": False, "m": 0}
 
-    def step(timed=False):
+    def step():
         t0 = time.perf_counter()
         send, counts = rp.shuffle.pack(src)
         t1 = time.perf_counter()
@@ -575,74 +685,83 @@ def bench_repartition(args, lib, rank, world, local):
         st = h.push(abi.DeviceBatch(kts, keys=key, cols=cols, col_valid=valid))
         rows = h.count_rows(None)
         t3 = time.perf_counter()
-        if timed:
+        if state["timed"]:
             phases["pack"] += t1 - t0
             phases["exchange_unpack"] += t2 - t1
             phases["aggregate"] += t3 - t2
+        state["m"] = m
         return st, rows, m
 
     for _ in range(max(args.warmup, 1)):
         st, rows, m = step()
     assert st["rows_accepted"] == m, st
     h.kernel_times(reset=True)
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    barrier()
-    t0 = time.perf_counter()
-    recv_total = 0
-    for _ in range(args.steps):
-        st, rows, m = step(timed=True)
-        recv_total += m
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    state["timed"] = True
+    (st, rows, m), elapsed = timed_loop(step, args.steps, world)
     kt = h.kernel_times()
-    if rank == 0:
-        ms_step = elapsed * 1000.0 / args.steps
-        per = {k: v * 1000.0 / args.steps for k, v in phases.items()}
-        achieved = BYTES_PER_RECORD_C5 * n / (ms_step / 1000.0) / 1e9
-        launches = max(kt["apply_launches"], 1)
-        push_ms = sum(kt[k] for k in ("stream_time_ms", "partition_ms", "apply_ms", "finalize_ms")) / launches
-        out = {
-            "metric": "records/sec, non-key GROUP BY with repartition (SUM(amount) TUMBLING 1 MINUTE GROUP BY region_id)",
-            "value": world * n * args.steps / elapsed,
-            "unit": "records/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "int64",
-            "data": "synthetic (splitmix64, ksql_amd/synth.py repartition_sum), device-resident columnar batch",
-            "config": {"workload": "repartition_sum", "records_per_gpu": n, "regions": 1_000_000,
-                       "window": "TUMBLING 1 MINUTE", "parallelism": "repartition all-to-all x%d" % world,
-                       "rows_received_rank0": m, "groups_rank0": int(rows)},
-            "roofline": {"bound": "hbm", "kernel": "whole step: pack + all-to-all + unpack + khip_agg_push",
-                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None, "algorithmic_bytes_per_record": BYTES_PER_RECORD_C5,
-                         "phase_ms": per, "push_device_ms": push_ms},
-            "cpu_baseline": None,
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline_repartition(n, args.cpu_seconds)
-        print(json.dumps(out))
     h.close()
     rp.close()
     if comm is not None:
         comm.close()
-    if world > 1:
-        dist.destroy_process_group()
+    if rank != 0:
+        return
+    ms_step = elapsed * 1000.0 / args.steps
+    per = {k: v * 1000.0 / args.steps for k, v in phases.items()}
+    push_ms = sum(push_phases(kt, kt["apply_launches"]).values())
+    roof = roofline(BYTES_PER_RECORD_C5 * n, ms_step, None, None, load_traffic(args.traffic_json, "repartition_sum", n),
+                    BYTES_PER_RECORD_C5, kernel="whole step: pack + all-to-all + unpack + khip_agg_push + row count",
+                    extra={"phase_ms": per, "push_device_ms": push_ms})
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_repartition(n, args.cpu_seconds)
+    line("records/sec, non-key GROUP BY with repartition (SUM(amount) TUMBLING 1 MINUTE GROUP BY region_id)",
+         world * n * args.steps / elapsed, world, args, ms_step, "int64",
+         "synthetic (splitmix64, ksql_amd/synth.py repartition_sum), device-resident columnar batch",
+         {"workload": "repartition_sum", "records_per_gpu": n, "regions": 1_000_000, "window": "TUMBLING 1 MINUTE",
+          "parallelism": "repartition all-to-all x%d" % world, "rows_received_rank0": m, "groups_rank0": int(rows)},
+         roof, cpu)
+
+
+def cpu_baseline_repartition(n_total, target_s):
+    """Oracle C5 step on a prefix of rank 0's source partition: Kafka partitioner of the new key
+    (oracle_kafka_partition, 8 destinations) + SUM(amount) TUMBLING 1 MINUTE GROUP BY region_id —
+    1 thread, and P threads (partitioner over P chunks, aggregate over P key-hash shards)."""
+    from ksql_amd import abi, synth
+    orc = abi.load_oracle()
+    P = cpu_threads()
+    kw = dict(window_kind="TUMBLING", size_ms=60_000, key_type="INT64", col_types=["INT64", "INT64"],
+              aggs=[("SUM", 1)])
+
+    def run(m, threads):
+        _eid, ts, region, amount = synth.repartition_sum(0, m, n_total)
+        region = np.ascontiguousarray(region, np.int64)
+        dest = np.empty(m, np.int32)
+        b = abi.HostBatch(ts, keys=region, cols=[region, amount])
+        h = abi.AggHandle(orc, abi.make_agg_desc(**kw)) if threads == 1 else \
+            abi.ShardedOracleAgg(orc, abi.make_agg_desc(**kw), threads)
+        bounds = np.linspace(0, m, threads + 1).astype(np.int64)
+
+        def part(k):
+            lo, hi = int(bounds[k]), int(bounds[k + 1])
+            orc.dll.oracle_kafka_partition(region.ctypes.data + 8 * lo, hi - lo, 8, 8, dest.ctypes.data + 4 * lo)
+
+        t0 = time.perf_counter()
+        th = [threading.Thread(target=part, args=(k,)) for k in range(threads)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        h.push(b, stats=False)
+        dt = time.perf_counter() - t0
+        h.close()
+        return dt
+
+    single = sized_run(lambda m: run(m, 1), 1_000_000, target_s, 40_000_000)
+    par = sized_run(lambda m: run(m, P), 2_000_000, target_s, 80_000_000)
+    return cpu_baseline_block(single, par, P, "records/s",
+                              "first %%d of rank 0's %d repartition_sum records: partitioner + aggregate, %%d threads"
+                              % n_total)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -13,7 +13,10 @@ import os
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PRODUCT_LIB = os.path.join(REPO, "ksql_amd", "libksqldb_hip.so")
+# KSQL_AMD_LIB_VARIANT=tune loads the tuning build (same HIP kernels, KHIP_* knobs read from the
+# environment; ksql_amd/Makefile TUNING=1) for GPU parameter sweeps.  Both are the HIP library.
+PRODUCT_LIB = os.path.join(REPO, "ksql_amd", "libksqldb_hip_tune.so" if os.environ.get("KSQL_AMD_LIB_VARIANT") == "tune"
+                           else "libksqldb_hip.so")
 ORACLE_LIB = os.path.join(REPO, "oracle", "liboracle.so")
 
 KHIP_OK = 0
@@ -184,6 +187,12 @@ class Lib:
             self.dll.oracle_kafka_partition.restype = None
             self.dll.oracle_murmur2.argtypes = [C.c_char_p, i32]
             self.dll.oracle_murmur2.restype = i32
+            self.dll.oracle_agg_push_sharded.argtypes = [C.POINTER(_P), i32, C.POINTER(Batch), C.POINTER(BatchStats)]
+            self.dll.oracle_agg_push_sharded.restype = i32
+            self.dll.oracle_agg_snapshot_size_sharded.argtypes = [C.POINTER(_P), i32, C.POINTER(i64), C.POINTER(i64)]
+            self.dll.oracle_agg_snapshot_size_sharded.restype = i32
+            self.dll.oracle_agg_snapshot_sharded.argtypes = [C.POINTER(_P), i32, C.POINTER(Having), C.POINTER(Snapshot)]
+            self.dll.oracle_agg_snapshot_sharded.restype = i32
 
     def check(self, status, what):
         if status != KHIP_OK:
@@ -229,11 +238,14 @@ class HostBatch:
     """Owns numpy arrays for one host batch and the ctypes struct pointing at them."""
 
     def __init__(self, ts, keys=None, key_valid=None, row_valid=None, cols=(), col_valid=(),
-                 utf8_keys=None):
+                 utf8_keys=None, key_offsets=None, key_bytes=None):
+        """utf8_keys: a list of str/bytes (None → b""), or the columnar form key_offsets
+        (int64, n+1) + key_bytes (uint8)."""
         self.ts = np.ascontiguousarray(ts, dtype=np.int64)
         n = len(self.ts)
         self.keys = None if keys is None else np.ascontiguousarray(keys, dtype=np.int64)
-        self.key_offsets = self.key_bytes = None
+        self.key_offsets = None if key_offsets is None else np.ascontiguousarray(key_offsets, dtype=np.int64)
+        self.key_bytes = None if key_bytes is None else np.ascontiguousarray(key_bytes, dtype=np.uint8)
         if utf8_keys is not None:
             enc = [b"" if k is None else (k.encode() if isinstance(k, str) else bytes(k)) for k in utf8_keys]
             self.key_offsets = np.zeros(n + 1, dtype=np.int64)
@@ -320,8 +332,11 @@ class AggHandle:
                                          C.byref(st) if stats else None), "agg_push")
         return st.as_dict() if stats else None
 
-    def snapshot(self, having=None):
-        return self._materialize(having, lambda hv, s: self.lib.agg_snapshot(self.h, hv, s), "agg_snapshot")
+    def snapshot(self, having=None, raw_keys=False):
+        """raw_keys: UTF8 keys as the columnar (key_offsets, key_bytes) arrays instead of a list of
+        str (for tables of tens of millions of rows)."""
+        return self._materialize(having, lambda hv, s: self.lib.agg_snapshot(self.h, hv, s), "agg_snapshot",
+                                 raw_keys=raw_keys)
 
     def get(self, keys=None, ws=(None, None), we=(None, None), having=None):
         """Pull query (khip_agg_get): rows of `keys` (None = every key) whose WINDOWSTART and
@@ -346,7 +361,7 @@ class AggHandle:
         return self._materialize(having, lambda hv, s: self.lib.agg_get(self.h, C.byref(q), hv, s), "agg_get",
                                  cap=4096 if self.desc.key_type == KEY["INT64"] else None)
 
-    def _materialize(self, having, call, what, cap=None):
+    def _materialize(self, having, call, what, cap=None, raw_keys=False):
         if cap is None:
             n, kb = i64(), i64()
             self.lib.check(self.lib.agg_snapshot_size(self.h, C.byref(n), C.byref(kb)), "agg_snapshot_size")
@@ -354,14 +369,14 @@ class AggHandle:
         else:
             kcap = 1
         while True:
-            out, st, n_needed = self._materialize_into(having, call, cap, kcap)
+            out, st, n_needed = self._materialize_into(having, call, cap, kcap, raw_keys)
             if st == KHIP_E_BUFFER and n_needed > cap:
                 cap = n_needed
                 continue
             self.lib.check(st, what)
             return out
 
-    def _materialize_into(self, having, call, cap, kcap):
+    def _materialize_into(self, having, call, cap, kcap, raw_keys=False):
         rt = result_types(self.desc)
         arrays = {
             "key": np.zeros(cap, np.int64), "key_offsets": np.zeros(cap + 1, np.int64),
@@ -385,7 +400,10 @@ class AggHandle:
         m = s.n_rows
         out = {"n": m, "ws": arrays["ws"][:m], "we": arrays["we"][:m], "rowtime": arrays["rowtime"][:m],
                "values": [v[:m] for v in arrays["values"]], "nulls": [v[:m].astype(bool) for v in arrays["nulls"]]}
-        if self.desc.key_type == KEY["UTF8"]:
+        if self.desc.key_type == KEY["UTF8"] and raw_keys:
+            out["key_offsets"] = arrays["key_offsets"][: m + 1]
+            out["key_bytes"] = arrays["key_bytes"][: int(arrays["key_offsets"][m]) if m else 0]
+        elif self.desc.key_type == KEY["UTF8"]:
             offs = arrays["key_offsets"][: m + 1]
             kbts = arrays["key_bytes"].tobytes()
             out["key"] = [kbts[offs[i]:offs[i + 1]].decode("utf-8", "surrogateescape") for i in range(m)]
@@ -420,6 +438,57 @@ class AggHandle:
             self.close()
         except Exception:
             pass
+
+
+class ShardedOracleAgg(AggHandle):
+    """The oracle's key-sharded P-thread restatement (oracle_agg_push_sharded): one task's
+    windowed aggregate over P key-hash shards, one thread each — results identical to the
+    sequential oracle.  Test infrastructure / CPU baseline only."""
+
+    def __init__(self, orc, desc, shards):
+        assert not orc.product
+        self.lib = orc
+        self.desc = desc
+        self.P = int(shards)
+        self._hs = (C.c_void_p * self.P)()
+        for p in range(self.P):
+            h = C.c_void_p()
+            orc.check(orc.agg_create(C.byref(desc), C.byref(h)), "agg_create")
+            self._hs[p] = h
+        self.h = self._hs[0]
+        d = orc.dll
+        self._push = d.oracle_agg_push_sharded
+        self._size = d.oracle_agg_snapshot_size_sharded
+        self._snap = d.oracle_agg_snapshot_sharded
+
+    def push(self, batch, stats=True):
+        st = BatchStats()
+        self.lib.check(self._push(self._hs, self.P, C.byref(batch.struct), C.byref(st) if stats else None),
+                       "agg_push_sharded")
+        return st.as_dict() if stats else None
+
+    def snapshot(self, having=None, raw_keys=False):
+        return self._materialize(having, lambda hv, s: self._snap(self._hs, self.P, hv, s), "agg_snapshot_sharded",
+                                 raw_keys=raw_keys)
+
+    def _materialize(self, having, call, what, cap=None, raw_keys=False):
+        if cap is None:
+            n, kb = i64(), i64()
+            self.lib.check(self._size(self._hs, self.P, C.byref(n), C.byref(kb)), "agg_snapshot_size_sharded")
+            cap, kcap = max(n.value, 1), max(kb.value, 1)
+        else:
+            kcap = 1
+        out, st, _ = self._materialize_into(having, call, cap, kcap, raw_keys)
+        self.lib.check(st, what)
+        return out
+
+    def close(self):
+        if getattr(self, "_hs", None) is not None:
+            for p in range(self.P):
+                if self._hs[p]:
+                    self.lib.agg_destroy(self._hs[p])
+            self._hs = None
+            self.h = C.c_void_p()
 
 
 class TableHandle:

@@ -1044,8 +1044,7 @@ khip_status part_init(khip_agg* a, int64_t hint) {
   const int entry = 4 + 8 * used;
   // LDS table: the largest power of two within the budget (default 80 KB: two workgroups
   // per CU overlap one's load/write-back phases with the other's LDS work)
-  const char* kb = getenv("KHIP_LDS_KB");
-  const int64_t budget = (kb ? atoi(kb) : 150) * 1024;
+  const int64_t budget = knob("KHIP_LDS_KB", 150) * 1024;
   int H = 256;
   while ((int64_t)(H * 2) * entry + 16 <= budget && H < 16384) H *= 2;
   s.H = H;
@@ -1058,7 +1057,7 @@ khip_status part_init(khip_agg* a, int64_t hint) {
   // hinted groups would need sub-passes at 2^14 partitions (each re-reads the partition's
   // records): one more partition bit instead (measured: C5 push 12.1 → 9.8 ms)
   if (s.log2P == SPLIT_P_LOG2 && groups >> SPLIT_P_LOG2 > (int64_t)s.H_eff * 7 / 10) s.log2P = MAX_P_LOG2;
-  if (const char* e = getenv("KHIP_PART_LOG2")) s.log2P = std::min(MAX_P_LOG2, atoi(e));
+  s.log2P = (int)std::min<int64_t>(MAX_P_LOG2, knob("KHIP_PART_LOG2", s.log2P));
   s.P = 1LL << s.log2P;
   s.cmax = next_pow2(std::max<int64_t>(64, 2 * groups / s.P + 64));
   // more hinted groups per partition than one LDS table holds (P is capped by the LDS
@@ -1127,7 +1126,7 @@ static PartAggParams part_params(khip_agg* a) {
   q.size = a->desc.size_ms;
   q.adv = a->windowed ? a->desc.advance_ms : 1;
   q.fd = make_fastdiv((uint64_t)q.adv);
-  q.dbg_mode = getenv("KHIP_AGG_MODE") ? atoi(getenv("KHIP_AGG_MODE")) : 0;
+  q.dbg_mode = (int32_t)knob("KHIP_AGG_MODE", 0);
   q.log2P = s.log2P;
   q.cmax = s.cmax;
   q.n_cols = a->desc.n_cols;
@@ -1230,10 +1229,8 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   // live groups only: closed (evicted) windows live in the flat store, not in the LDS tables
   while (s.log2P < SPLIT_P_LOG2 && a->occ - s.closed_n > s.P * (int64_t)s.H_eff / 2) KHIP_TRY(part_split(a));
   const int P = (int)s.P;
-  const char* ti = getenv("KHIP_TILE_ITEMS");
-  const int64_t tile = (int64_t)PT_THREADS * (ti ? atoi(ti) : PT_ITEMS);
-  const char* pe = getenv("KHIP_PAD");
-  const int pad = pe ? atoi(pe) : 0;
+  const int64_t tile = (int64_t)PT_THREADS * knob("KHIP_TILE_ITEMS", PT_ITEMS);
+  const int pad = (int)knob("KHIP_PAD", 0);
   const int64_t nT = ceil_div(n, tile);
   const int TC = (int)std::min<int64_t>(nT, TC_MAX);
   KHIP_TRY(s.hist.ensure((size_t)nT * P * 4));
@@ -1245,8 +1242,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   const int64_t ncap = pad ? n + 3 * (int64_t)P * nT : n;  // padded runs
   // two-level scatter (pass A: B = P >> fbits buckets; pass B: partitions inside a bucket)
   // once single-level runs get short (P large against the tile)
-  const char* s2 = getenv("KHIP_SCATTER2");
-  const bool lvl2 = !pad && s.log2P >= 11 && (s2 ? atoi(s2) != 0 : true);
+  const bool lvl2 = !pad && s.log2P >= 11 && knob("KHIP_SCATTER2", 1) != 0;
   const int fbits = lvl2 ? s.log2P - s.log2P / 2 : 0;
   const int B = P >> fbits;
   if (s.scat_cap < ncap) {
@@ -1303,9 +1299,8 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   }
   ev_record_part(a, 1);
   // 3. scatter
-  const char* su = getenv("KHIP_SCATTER_U");
-  const bool narrow = s.rw == 2;
-  const int U = su ? atoi(su) : (narrow ? 8 : 16);
+    const bool narrow = s.rw == 2;
+  const int U = (int)knob("KHIP_SCATTER_U", narrow ? 8 : 16);
   auto scat = narrow ? (U >= 16 ? k_part_scatter<16, true> : (U >= 8 ? k_part_scatter<8, true> : k_part_scatter<4, true>))
                      : (U >= 16 ? k_part_scatter<16, false> : (U >= 8 ? k_part_scatter<8, false> : k_part_scatter<4, false>));
   if (!lvl2 && hist_lds > 64 * 1024)
@@ -1320,8 +1315,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                      s.tpart.as<int64_t>());
   KHIP_TRY_HIP(hipGetLastError());
   if (lvl2) {
-    const char* ge = getenv("KHIP_REFINE_RECS");
-    const int64_t per_blk = ge ? atoll(ge) : 8192;  // measured: 8K records per block (1 KB runs) beat 32K
+    const int64_t per_blk = knob("KHIP_REFINE_RECS", 8192);  // measured: 8K records per block (1 KB runs) beat 32K
     const int G = (int)std::max<int64_t>(1, std::min<int64_t>(nT, per_blk * B / tile));
     const int64_t ng = ceil_div(nT, G);
     void (*ref)(const uint64_t*, const uint32_t*, const uint32_t*, const int64_t*, int64_t, int, int, int, int64_t,
@@ -1336,7 +1330,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     }
     hipLaunchKernelGGL(ref, dim3((unsigned)(B * ng)), dim3(PT_THREADS), 0, a->stream, s.srecA.as<uint64_t>(),
                        s.hcoarse.as<uint32_t>(), s.hist.as<uint32_t>(), s.pbase.as<int64_t>(), nT, G, s.log2P, fbits,
-                       ncap, s.srec.as<uint64_t>(), getenv("KHIP_REFINE_MODE") ? atoi(getenv("KHIP_REFINE_MODE")) : 0);
+                       ncap, s.srec.as<uint64_t>(), (int)knob("KHIP_REFINE_MODE", 0));
     KHIP_TRY_HIP(hipGetLastError());
   }
   ev_record_part(a, 2);
@@ -1380,7 +1374,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     KHIP_TRY_HIP(hipMemcpyAsync(s.work.p, work.data(), work.size() * 4, hipMemcpyHostToDevice, a->stream));
   }
   // KHIP_AGG_PROBE=1: per-workgroup phase timestamps of pass 0 (wall clock, 100 MHz) → stderr
-  static const bool probe = getenv("KHIP_AGG_PROBE") != nullptr;
+  const bool probe = knob("KHIP_AGG_PROBE", 0) != 0;
   DevBuf dbgbuf;
   unsigned long long* dbg = nullptr;
   for (int pass = 0;; pass++) {

@@ -14,9 +14,11 @@
 //
 // Upsert (arrival order, last writer wins, tombstone deletes):
 //   k_upsert_claim   find-or-claim each key's slot (CAS on meta, claim references the
-//                    batch row); atomicMax of (epoch << 40 | row) elects the last writer
-//   k_upsert_finalize claims → resident keys
-//   k_upsert_apply   the elected row writes value + live bit (or clears live)
+//                    batch row, new slots appended to a claimed list); atomicMax of
+//                    (row + 1) into the tag word elects the last writer of the batch
+//   k_upsert_finalize claimed slots only → resident keys
+//   k_upsert_apply   the elected row writes value + live bit (or clears live) and zeroes
+//                    the tag, so tags never carry over between batches
 // Probe: one thread per stream row, coalesced key/ts loads, one slot line per probe;
 // output is row-aligned (selection bitmaps built with __ballot, 8 B per wave) so no
 // compaction pass is needed on the device path.
@@ -57,9 +59,10 @@ __device__ __forceinline__ uint64_t key_hash(int64_t k) { return mix64((uint64_t
 
 __global__ __launch_bounds__(256) void k_upsert_claim(uint64_t* __restrict__ table, uint64_t mask, int sw,
                                                       const int64_t* __restrict__ keys,
-                                                      const uint8_t* __restrict__ kv, int64_t n, uint64_t epoch,
+                                                      const uint8_t* __restrict__ kv, int64_t n,
                                                       int64_t* __restrict__ slot_of, int* __restrict__ fail,
-                                                      unsigned long long* __restrict__ new_keys) {
+                                                      unsigned long long* __restrict__ new_keys,
+                                                      int64_t* __restrict__ claimed) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     slot_of[i] = -1;
     if (!bit_get(kv, i)) continue;
@@ -73,7 +76,7 @@ __global__ __launch_bounds__(256) void k_upsert_claim(uint64_t* __restrict__ tab
       if (m == 0) {
         const uint64_t old = atomicCAS((unsigned long long*)&s[1], 0ULL, (unsigned long long)claim);
         if (old == 0) {
-          atomicAdd(new_keys, 1ULL);
+          claimed[atomicAdd(new_keys, 1ULL)] = (int64_t)slot;
           done = true;
         } else {
           m = old;
@@ -88,7 +91,7 @@ __global__ __launch_bounds__(256) void k_upsert_claim(uint64_t* __restrict__ tab
       }
       if (done) {
         slot_of[i] = (int64_t)slot;
-        atomicMax((unsigned long long*)&s[2], (unsigned long long)((epoch << 40) | (uint64_t)i));
+        atomicMax((unsigned long long*)&s[2], (unsigned long long)(i + 1));
       } else {
         slot = (slot + 1) & mask;
       }
@@ -97,11 +100,13 @@ __global__ __launch_bounds__(256) void k_upsert_claim(uint64_t* __restrict__ tab
   }
 }
 
-__global__ __launch_bounds__(256) void k_upsert_finalize(uint64_t* __restrict__ table, int64_t cap, int sw,
-                                                         const int64_t* __restrict__ keys) {
-  for (int64_t slot = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; slot < cap;
-       slot += (int64_t)gridDim.x * blockDim.x) {
-    uint64_t* s = table + slot * (uint64_t)sw;
+__global__ __launch_bounds__(256) void k_upsert_finalize(uint64_t* __restrict__ table, int sw,
+                                                         const int64_t* __restrict__ keys,
+                                                         const int64_t* __restrict__ claimed,
+                                                         const unsigned long long* __restrict__ n_claimed) {
+  const int64_t nc = (int64_t)*n_claimed;
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < nc; k += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t* s = table + (uint64_t)claimed[k] * (uint64_t)sw;
     const uint64_t m = s[1];
     if (m & M_CLAIM) {
       s[0] = (uint64_t)keys[(int64_t)(m & ((1ULL << 40) - 1))];
@@ -112,13 +117,13 @@ __global__ __launch_bounds__(256) void k_upsert_finalize(uint64_t* __restrict__ 
 
 __global__ __launch_bounds__(256) void k_upsert_apply(uint64_t* __restrict__ table, int sw,
                                                       const int64_t* __restrict__ slot_of,
-                                                      const uint8_t* __restrict__ rv, int64_t n, uint64_t epoch,
-                                                      int ncols, const int32_t* __restrict__ types_dev, JCols cols) {
+                                                      const uint8_t* __restrict__ rv, int64_t n, int ncols, const int32_t* __restrict__ types_dev, JCols cols) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t slot = slot_of[i];
     if (slot < 0) continue;
     uint64_t* s = table + slot * (uint64_t)sw;
-    if (s[2] != ((epoch << 40) | (uint64_t)i)) continue;  // not the last writer of this key
+    if (s[2] != (uint64_t)(i + 1)) continue;  // not the last writer of this key
+    s[2] = 0;  // only the winner matches: clearing cannot change another row's decision
     if (!bit_get(rv, i)) {
       s[1] = M_RESIDENT;  // tombstone: delete
       continue;
@@ -343,7 +348,7 @@ struct khip_table {
       st_cval[JMAX_COLS], out_emit, out_matched, out_cols[JMAX_COLS], out_nulls[JMAX_COLS], out_slot;
   int64_t cap = 0;
   int64_t occ = 0;  // resident keys (live or deleted)
-  uint64_t epoch = 0;
+  DevBuf claimed;    // slots claimed by the current upsert batch
 };
 
 static khip_status table_alloc(khip_table* t, DevBuf& buf, int64_t cap) {
@@ -489,20 +494,18 @@ khip_status khip_table_upsert(khip_table* t, const khip_batch* b) {
   KHIP_TRY(jresolve(t, b, t->desc.n_cols, &keys, &ts, &kv, &rv, &cols));
   // keep the load factor <= 0.75 even if every row were a new key
   if (4 * (t->occ + n) > 3 * t->cap) KHIP_TRY(table_grow(t, next_pow2((4 * (t->occ + n) + 2) / 3)));
-  t->epoch++;
-  if (t->epoch >= (1ULL << 23)) return fail(KHIP_E_STATE, "upsert epoch space exhausted");
   KHIP_TRY(t->slot_of.ensure(n * 8));
+  KHIP_TRY(t->claimed.ensure(n * 8));
   unsigned long long* ctr = t->scratch.as<unsigned long long>();
   int* failp = (int*)(t->scratch.as<uint8_t>() + 16);
   KHIP_TRY_HIP(hipMemsetAsync(t->scratch.p, 0, 64, t->stream));
   hipLaunchKernelGGL(k_upsert_claim, dim3(jgrid(n)), dim3(256), 0, t->stream, t->table.as<uint64_t>(),
-                     (uint64_t)(t->cap - 1), t->sw, keys, kv, n, (uint64_t)t->epoch, t->slot_of.as<int64_t>(), failp,
-                     ctr);
-  hipLaunchKernelGGL(k_upsert_finalize, dim3(jgrid(t->cap)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->cap,
-                     t->sw, keys);
+                     (uint64_t)(t->cap - 1), t->sw, keys, kv, n, t->slot_of.as<int64_t>(), failp, ctr,
+                     t->claimed.as<int64_t>());
+  hipLaunchKernelGGL(k_upsert_finalize, dim3(jgrid(n)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->sw, keys,
+                     t->claimed.as<int64_t>(), (const unsigned long long*)ctr);
   hipLaunchKernelGGL(k_upsert_apply, dim3(jgrid(n)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->sw,
-                     t->slot_of.as<int64_t>(), rv, n, (uint64_t)t->epoch, t->desc.n_cols, t->types_dev.as<int32_t>(),
-                     cols);
+                     t->slot_of.as<int64_t>(), rv, n, t->desc.n_cols, t->types_dev.as<int32_t>(), cols);
   KHIP_TRY_HIP(hipGetLastError());
   unsigned long long added = 0;
   int failed = 0;
@@ -540,7 +543,7 @@ static khip_status probe_launch(khip_table* t, const khip_batch* b, int32_t join
   if (!ts) return fail(KHIP_E_INVALID, "missing timestamp column");
   JWhere jw;
   KHIP_TRY(make_where(t, w, &jw));
-  static const int pr_env = getenv("KHIP_PROBE_PR") ? atoi(getenv("KHIP_PROBE_PR")) : 4;  // measured: 4 > 8 > 16 > 1
+  const int pr_env = (int)knob("KHIP_PROBE_PR", 4);  // measured: 4 > 8 > 16 > 1
   const int PR = pr_env >= 16 ? 16 : (pr_env >= 8 ? 8 : (pr_env >= 4 ? 4 : 1));
   auto kern = PR == 16 ? k_probe<16> : (PR == 8 ? k_probe<8> : (PR == 4 ? k_probe<4> : k_probe<1>));
   hipLaunchKernelGGL(kern, dim3(ceil_div(n, 256 * PR)), dim3(256), 0, t->stream, t->table.as<uint64_t>(),
@@ -656,7 +659,7 @@ khip_status khip_table_destroy(khip_table* t) {
   if (!t) return KHIP_OK;
   DeviceGuard g(t->device);
   if (t->stream) hipStreamSynchronize(t->stream);
-  DevBuf* bufs[] = {&t->table, &t->types_dev, &t->slot_of, &t->scratch, &t->st_keys, &t->st_ts, &t->st_kv,
+  DevBuf* bufs[] = {&t->table, &t->types_dev, &t->slot_of, &t->claimed, &t->scratch, &t->st_keys, &t->st_ts, &t->st_kv,
                     &t->st_rv, &t->out_emit, &t->out_matched, &t->out_slot};
   for (DevBuf* x : bufs) x->release();
   for (int c = 0; c < JMAX_COLS; c++) {

@@ -359,6 +359,25 @@ khip_status khip_comm_init(int32_t nranks, int32_t rank, const uint8_t id[KHIP_C
   return KHIP_OK;
 }
 
+// Inside ncclGroupStart/End: remember the first failure but keep going, so the group is always
+// closed (an open group on one rank leaves its peers blocked in their own ncclGroupEnd).
+struct GroupErr {
+  ncclResult_t r = ncclSuccess;
+  const char* what = nullptr;
+  void note(ncclResult_t x, const char* w) {
+    if (x != ncclSuccess && r == ncclSuccess) {
+      r = x;
+      what = w;
+    }
+  }
+  khip_status finish(ncclResult_t end) {
+    note(end, "ncclGroupEnd");
+    if (r == ncclSuccess) return KHIP_OK;
+    ::khip::set_error(std::string(what) + ": " + ncclGetErrorString(r));
+    return KHIP_E_COMM;
+  }
+};
+
 khip_status khip_comm_exchange_counts(khip_comm* c, const int64_t* send_counts, int64_t* recv_counts) {
   clear_error();
   if (!c || !send_counts || !recv_counts) return fail(KHIP_E_INVALID, "null argument");
@@ -369,11 +388,12 @@ khip_status khip_comm_exchange_counts(khip_comm* c, const int64_t* send_counts, 
   int64_t* drecv = dsend + N;
   KHIP_TRY_HIP(hipMemcpyAsync(dsend, send_counts, N * 8, hipMemcpyHostToDevice, c->stream));
   KHIP_TRY_NCCL(ncclGroupStart());
+  GroupErr ge;
   for (int p = 0; p < N; p++) {
-    KHIP_TRY_NCCL(ncclSend(dsend + p, 1, ncclInt64, p, c->comm, c->stream));
-    KHIP_TRY_NCCL(ncclRecv(drecv + p, 1, ncclInt64, p, c->comm, c->stream));
+    ge.note(ncclSend(dsend + p, 1, ncclInt64, p, c->comm, c->stream), "ncclSend");
+    ge.note(ncclRecv(drecv + p, 1, ncclInt64, p, c->comm, c->stream), "ncclRecv");
   }
-  KHIP_TRY_NCCL(ncclGroupEnd());
+  KHIP_TRY(ge.finish(ncclGroupEnd()));
   KHIP_TRY_HIP(hipMemcpyAsync(recv_counts, drecv, N * 8, hipMemcpyDeviceToHost, c->stream));
   KHIP_TRY_HIP(hipStreamSynchronize(c->stream));
   return KHIP_OK;
@@ -390,15 +410,18 @@ khip_status khip_comm_alltoall(khip_comm* c, const uint64_t* send, const int64_t
   if (tot > recv_capacity) return fail(KHIP_E_BUFFER, "receive buffer smaller than the exchanged counts");
   int64_t so = 0, ro = 0;
   KHIP_TRY_NCCL(ncclGroupStart());
+  GroupErr ge;
   for (int p = 0; p < N; p++) {
     if (send_counts[p])
-      KHIP_TRY_NCCL(ncclSend(send + so * row_words, (size_t)send_counts[p] * row_words, ncclUint64, p, c->comm, c->stream));
+      ge.note(ncclSend(send + so * row_words, (size_t)send_counts[p] * row_words, ncclUint64, p, c->comm, c->stream),
+              "ncclSend");
     if (recv_counts[p])
-      KHIP_TRY_NCCL(ncclRecv(recv + ro * row_words, (size_t)recv_counts[p] * row_words, ncclUint64, p, c->comm, c->stream));
+      ge.note(ncclRecv(recv + ro * row_words, (size_t)recv_counts[p] * row_words, ncclUint64, p, c->comm, c->stream),
+              "ncclRecv");
     so += send_counts[p];
     ro += recv_counts[p];
   }
-  KHIP_TRY_NCCL(ncclGroupEnd());
+  KHIP_TRY(ge.finish(ncclGroupEnd()));
   KHIP_TRY_HIP(hipStreamSynchronize(c->stream));
   return KHIP_OK;
 }

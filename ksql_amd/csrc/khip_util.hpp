@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <string>
 
@@ -32,6 +33,20 @@ void clear_error();
 inline khip_status fail(khip_status s, const std::string& msg) {
   set_error(msg);
   return s;
+}
+
+// Tuning knobs (tile sizes, unroll factors, LDS budget...).  Only the tuning build
+// (make TUNING=1 → libksqldb_hip_tune.so) reads them from the environment, for GPU sweeps;
+// the release library always uses the measured defaults, so a stray variable cannot change
+// what it computes or how fast.
+inline int64_t knob(const char* name, int64_t dflt) {
+#ifdef KHIP_TUNING
+  const char* e = getenv(name);
+  return e ? atoll(e) : dflt;
+#else
+  (void)name;
+  return dflt;
+#endif
 }
 
 // Grow-only device buffer.

@@ -141,6 +141,9 @@ def possible_fraud(lo, hi, n, xp="numpy", device=None, rank=0, world=1, keys=10_
     return card, ts
 
 
+URL_PREFIX = b"http://ex.com/p/"
+
+
 def hourly_metrics(lo, hi, n=1_000_000, keys=10_000, seed=1):
     """C1 (host only): (url strings, ts)."""
     be = _Np()
@@ -148,6 +151,44 @@ def hourly_metrics(lo, hi, n=1_000_000, keys=10_000, seed=1):
     ts = np.arange(lo, hi, dtype=np.int64) * 10
     urls = ["http://ex.com/p/%d" % k for k in kid.tolist()]
     return urls, ts
+
+
+def hourly_metrics_utf8(lo, hi, n=1_000_000, keys=10_000, seed=1):
+    """C1 as a columnar UTF-8 key column: (key_offsets int64[m+1], key_bytes uint8, ts), the
+    same urls as hourly_metrics(), built without Python strings."""
+    be = _Np()
+    kid = be.u53(_stream(be, seed, lo, hi, None)) % keys
+    ts = np.arange(lo, hi, dtype=np.int64) * 10
+    nd = np.ones(len(kid), np.int64)
+    for p in (10, 100, 1000, 10_000, 100_000):
+        nd += (kid >= p)
+    lens = len(URL_PREFIX) + nd
+    offs = np.zeros(len(kid) + 1, np.int64)
+    offs[1:] = np.cumsum(lens)
+    out = np.empty(int(offs[-1]), np.uint8)
+    pre = np.frombuffer(URL_PREFIX, np.uint8)
+    for j in range(len(pre)):
+        out[offs[:-1] + j] = pre[j]
+    for j in range(int(nd.max()) if len(nd) else 0):  # digit j from the left
+        has = nd > j
+        d = (kid[has] // (10 ** (nd[has] - 1 - j))) % 10
+        out[offs[:-1][has] + len(pre) + j] = (d + 48).astype(np.uint8)
+    return offs, out, ts
+
+
+def card_utf8(card, xp="numpy"):
+    """16-digit card numbers (int64 4000000000000000 + id) → UTF-8 key column
+    (key_offsets [n+1], key_bytes [16 n]): the VARCHAR card_number of possible_fraud."""
+    if xp == "numpy" or xp is np:
+        p10 = 10 ** np.arange(15, -1, -1, dtype=np.int64)
+        digits = ((card[:, None] // p10[None, :]) % 10 + 48).astype(np.uint8).reshape(-1)
+        offs = np.arange(len(card) + 1, dtype=np.int64) * 16
+        return offs, digits
+    import torch
+    p10 = torch.tensor([10 ** k for k in range(15, -1, -1)], dtype=torch.int64, device=card.device)
+    digits = ((card[:, None] // p10[None, :]) % 10 + 48).to(torch.uint8).reshape(-1)
+    offs = torch.arange(card.numel() + 1, dtype=torch.int64, device=card.device) * 16
+    return offs, digits
 
 
 def hopping_double(lo, hi, n, xp="numpy", device=None, rank=0, world=1, keys=100_000, seed=3,

@@ -43,9 +43,11 @@
  *     against the table as of that point; INNER emits on hit, LEFT always
  *     (S/StreamTableJoinBuilder.java:77-86, S/KsqlValueJoiner.java:41-63).
  */
+#define _GNU_SOURCE
 #include "oracle.h"
 
 #include <math.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -481,23 +483,24 @@ static int having_pass(const oracle_agg* a, const khip_having* h, const entry* x
   return 0;
 }
 
-static const oracle_agg* g_sort_agg;
-static int cmp_entry(const void* pa, const void* pb) {
-  const entry* x = *(const entry* const*)pa;
-  const entry* y = *(const entry* const*)pb;
-  const oracle_agg* a = g_sort_agg;
-  if (a->d.key_type == KHIP_KEY_INT64) {
+/* Order of the snapshot: (key bytes, ws).  x and y may come from different shards
+ * (oracle_agg_snapshot_sharded), each with its own key dictionary. */
+static int cmp_entry2(const oracle_agg* ax, const entry* x, const oracle_agg* ay, const entry* y) {
+  if (ax->d.key_type == KHIP_KEY_INT64) {
     if (x->key != y->key) return x->key < y->key ? -1 : 1;
-  } else if (x->key != y->key) {
-    const strdict* d = &a->dict;
-    int64_t lx = d->len[x->key], ly = d->len[y->key];
+  } else if (ax != ay || x->key != y->key) {
+    int64_t lx = ax->dict.len[x->key], ly = ay->dict.len[y->key];
     int64_t m = lx < ly ? lx : ly;
-    int c = m ? memcmp(d->arena + d->off[x->key], d->arena + d->off[y->key], (size_t)m) : 0;
+    int c = m ? memcmp(ax->dict.arena + ax->dict.off[x->key], ay->dict.arena + ay->dict.off[y->key], (size_t)m) : 0;
     if (c) return c;
     if (lx != ly) return lx < ly ? -1 : 1;
   }
   if (x->ws != y->ws) return x->ws < y->ws ? -1 : 1;
   return 0;
+}
+static int cmp_entry(const void* pa, const void* pb, void* ctx) {
+  const oracle_agg* a = (const oracle_agg*)ctx;
+  return cmp_entry2(a, *(const entry* const*)pa, a, *(const entry* const*)pb);
 }
 
 khip_status oracle_agg_snapshot_size(oracle_agg* a, int64_t* n_rows, int64_t* key_bytes) {
@@ -512,33 +515,28 @@ khip_status oracle_agg_snapshot_size(oracle_agg* a, int64_t* n_rows, int64_t* ke
   return KHIP_OK;
 }
 
-khip_status oracle_agg_snapshot(oracle_agg* a, const khip_having* h, khip_snapshot* out) {
-  if (!a || !out) return KHIP_E_INVALID;
-  if (h && (h->agg_index < 0 || h->agg_index >= a->d.n_aggs)) return KHIP_E_INVALID;
-  entry** order = (entry**)malloc(sizeof(entry*) * (a->n + 1));
-  int64_t m = 0;
-  for (int64_t k = 0; k < a->n; k++)
-    if (having_pass(a, h, &a->e[k])) order[m++] = &a->e[k];
-  g_sort_agg = a;
-  qsort(order, (size_t)m, sizeof(entry*), cmp_entry);
+typedef struct {
+  const oracle_agg* a; /* owner (shard) of the entry: its dictionary holds the key bytes */
+  const entry* x;
+} owned_entry;
+
+/* Rows [0, m) of the snapshot (ResultTransformer map + WindowBoundsPopulator). */
+static khip_status write_rows(const owned_entry* rows, int64_t m, khip_snapshot* out) {
   if (m > out->capacity) {
-    free(order);
     out->n_rows = m;
     return KHIP_E_BUFFER;
   }
   int64_t kb = 0;
-  const int windowed = a->d.window_kind != KHIP_WINDOW_NONE;
-  if (a->d.key_type == KHIP_KEY_UTF8 && out->key_offsets) out->key_offsets[0] = 0;
+  if (m > 0 && rows[0].a->d.key_type == KHIP_KEY_UTF8 && out->key_offsets) out->key_offsets[0] = 0;
   for (int64_t r = 0; r < m; r++) {
-    const entry* x = order[r];
+    const oracle_agg* a = rows[r].a;
+    const entry* x = rows[r].x;
+    const int windowed = a->d.window_kind != KHIP_WINDOW_NONE;
     if (a->d.key_type == KHIP_KEY_INT64) {
       if (out->key_i64) out->key_i64[r] = x->key;
     } else {
       int64_t len = a->dict.len[x->key];
-      if (kb + len > out->key_bytes_capacity) {
-        free(order);
-        return KHIP_E_BUFFER;
-      }
+      if (kb + len > out->key_bytes_capacity) return KHIP_E_BUFFER;
       if (out->key_bytes && len) memcpy(out->key_bytes + kb, a->dict.arena + a->dict.off[x->key], (size_t)len);
       kb += len;
       if (out->key_offsets) out->key_offsets[r + 1] = kb;
@@ -562,8 +560,26 @@ khip_status oracle_agg_snapshot(oracle_agg* a, const khip_having* h, khip_snapsh
   }
   out->n_rows = m;
   out->key_bytes_len = kb;
-  free(order);
   return KHIP_OK;
+}
+
+khip_status oracle_agg_snapshot(oracle_agg* a, const khip_having* h, khip_snapshot* out) {
+  if (!a || !out) return KHIP_E_INVALID;
+  if (h && (h->agg_index < 0 || h->agg_index >= a->d.n_aggs)) return KHIP_E_INVALID;
+  entry** order = (entry**)malloc(sizeof(entry*) * (a->n + 1));
+  int64_t m = 0;
+  for (int64_t k = 0; k < a->n; k++)
+    if (having_pass(a, h, &a->e[k])) order[m++] = &a->e[k];
+  qsort_r(order, (size_t)m, sizeof(entry*), cmp_entry, a);
+  owned_entry* rows = (owned_entry*)malloc(sizeof(owned_entry) * (m + 1));
+  for (int64_t r = 0; r < m; r++) {
+    rows[r].a = a;
+    rows[r].x = order[r];
+  }
+  free(order);
+  khip_status st = write_rows(rows, m, out);
+  free(rows);
+  return st;
 }
 
 khip_status oracle_agg_destroy(oracle_agg* a) {
@@ -576,6 +592,212 @@ khip_status oracle_agg_destroy(oracle_agg* a) {
   free(a->aggs);
   free(a);
   return KHIP_OK;
+}
+
+/* ------------------------------------------------- P-thread (key-sharded) restatement
+ *
+ * The same rules R1-R6 over P shards of the key space, one thread per shard: the multi-core
+ * CPU baseline ("P threads over P key-hash partitions") and a faster checker
+ * for full-size parity tests.  Results equal oracle_agg_push over the whole batch: a group
+ * lives in exactly one shard, and the only cross-record state that is not per group — the
+ * task's stream time (R2) — is computed first, sequentially, as the stream time after each
+ * record, then every shard applies its own records in arrival order against it. */
+
+static uint32_t shard_of(const oracle_agg* a, const khip_batch* b, int64_t r, int32_t P) {
+  uint64_t h;
+  if (a->d.key_type == KHIP_KEY_INT64) {
+    h = mix64((uint64_t)b->key_i64[r]);
+  } else {
+    const int64_t o0 = b->key_offsets[r], o1 = b->key_offsets[r + 1];
+    h = hash_bytes(b->key_bytes + o0, o1 - o0);
+  }
+  return (uint32_t)((h >> 32) % (uint64_t)P);
+}
+
+typedef struct {
+  oracle_agg* a;
+  const khip_batch* b;
+  const int64_t* idx; /* this shard's records, in arrival order */
+  int64_t n;
+  const int64_t* st_after; /* stream time after each record (R2), by batch row */
+  int64_t applied, late;
+} shard_job;
+
+static void* shard_run(void* arg) {
+  shard_job* j = (shard_job*)arg;
+  oracle_agg* a = j->a;
+  const khip_batch* b = j->b;
+  const int windowed = a->d.window_kind != KHIP_WINDOW_NONE;
+  const int64_t size = a->d.size_ms, adv = a->d.advance_ms;
+  for (int64_t k = 0; k < j->n; k++) {
+    const int64_t r = j->idx[k];
+    const int64_t ts = b->ts[r];
+    int64_t key;
+    if (a->d.key_type == KHIP_KEY_INT64) {
+      key = b->key_i64[r];
+    } else {
+      const int64_t o0 = b->key_offsets[r], o1 = b->key_offsets[r + 1];
+      key = strdict_intern(&a->dict, b->key_bytes + o0, o1 - o0);
+    }
+    if (!windowed) {
+      entry* x = find_or_create(a, key, 0);
+      if (ts > x->rowtime) x->rowtime = ts;
+      apply_aggs(a, x, b, r);
+      j->applied++;
+      continue;
+    }
+    const int64_t close_time = j->st_after[r] - a->grace;
+    int64_t lo = ts - size + adv;
+    if (lo < 0) lo = 0;
+    for (int64_t ws = (lo / adv) * adv; ws <= ts; ws += adv) {
+      if (ws + size > close_time) {
+        entry* x = find_or_create(a, key, ws);
+        if (ts > x->rowtime) x->rowtime = ts;
+        apply_aggs(a, x, b, r);
+        j->applied++;
+      } else {
+        j->late++;
+      }
+    }
+  }
+  return NULL;
+}
+
+khip_status oracle_agg_push_sharded(oracle_agg** shards, int32_t P, const khip_batch* b, khip_batch_stats* stats) {
+  if (!shards || P < 1 || !b || b->mem != KHIP_MEM_HOST || b->n_rows < 0) return KHIP_E_INVALID;
+  oracle_agg* a0 = shards[0];
+  if (b->n_cols < a0->d.n_cols) return KHIP_E_INVALID;
+  const int64_t n = b->n_rows;
+  khip_batch_stats s;
+  memset(&s, 0, sizeof(s));
+  s.rows_in = n;
+  int64_t* st_after = (int64_t*)malloc(sizeof(int64_t) * (n + 1));
+  uint32_t* sh = (uint32_t*)malloc(sizeof(uint32_t) * (n + 1));
+  int64_t* cnt = (int64_t*)calloc((size_t)P + 1, sizeof(int64_t));
+  int64_t st = a0->stream_time;
+  for (int64_t r = 0; r < n; r++) { /* R1 drops and R2 stream time, sequential */
+    sh[r] = UINT32_MAX;
+    if (!bit_get(b->key_valid, r)) { s.dropped_null_key++; continue; }
+    if (!bit_get(b->row_valid, r)) { s.dropped_null_row++; continue; }
+    if (b->ts[r] < 0) { s.dropped_bad_ts++; continue; }
+    s.rows_accepted++;
+    if (b->ts[r] > st) st = b->ts[r];
+    st_after[r] = st;
+    sh[r] = shard_of(a0, b, r, P);
+    cnt[sh[r] + 1]++;
+  }
+  for (int32_t p = 0; p < P; p++) cnt[p + 1] += cnt[p];
+  int64_t* idx = (int64_t*)malloc(sizeof(int64_t) * (n + 1));
+  int64_t* fill = (int64_t*)malloc(sizeof(int64_t) * ((size_t)P + 1));
+  memcpy(fill, cnt, sizeof(int64_t) * (size_t)P);
+  for (int64_t r = 0; r < n; r++)
+    if (sh[r] != UINT32_MAX) idx[fill[sh[r]]++] = r;
+  shard_job* jobs = (shard_job*)calloc((size_t)P, sizeof(shard_job));
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)P);
+  for (int32_t p = 0; p < P; p++) {
+    jobs[p].a = shards[p];
+    jobs[p].b = b;
+    jobs[p].idx = idx + cnt[p];
+    jobs[p].n = cnt[p + 1] - cnt[p];
+    jobs[p].st_after = st_after;
+    pthread_create(&th[p], NULL, shard_run, &jobs[p]);
+  }
+  for (int32_t p = 0; p < P; p++) {
+    pthread_join(th[p], NULL);
+    s.windows_applied += jobs[p].applied;
+    s.windows_late += jobs[p].late;
+    shards[p]->stream_time = st;
+  }
+  s.stream_time = st;
+  if (stats) *stats = s;
+  free(jobs); free(th); free(fill); free(idx); free(cnt); free(sh); free(st_after);
+  return KHIP_OK;
+}
+
+khip_status oracle_agg_snapshot_size_sharded(oracle_agg** shards, int32_t P, int64_t* n_rows, int64_t* key_bytes) {
+  int64_t n = 0, kb = 0;
+  for (int32_t p = 0; p < P; p++) {
+    int64_t a = 0, k = 0;
+    oracle_agg_snapshot_size(shards[p], &a, &k);
+    n += a;
+    kb += k;
+  }
+  if (n_rows) *n_rows = n;
+  if (key_bytes) *key_bytes = kb;
+  return KHIP_OK;
+}
+
+typedef struct {
+  oracle_agg* a;
+  const khip_having* h;
+  entry** order;
+  int64_t m;
+} sort_job;
+
+static void* sort_run(void* arg) {
+  sort_job* j = (sort_job*)arg;
+  oracle_agg* a = j->a;
+  j->order = (entry**)malloc(sizeof(entry*) * (a->n + 1));
+  j->m = 0;
+  for (int64_t k = 0; k < a->n; k++)
+    if (having_pass(a, j->h, &a->e[k])) j->order[j->m++] = &a->e[k];
+  qsort_r(j->order, (size_t)j->m, sizeof(entry*), cmp_entry, a);
+  return NULL;
+}
+
+/* Snapshot of the union of the shards: each shard sorted on its own thread, then a P-way
+ * merge (binary heap of shard cursors) into (key, ws) order. */
+khip_status oracle_agg_snapshot_sharded(oracle_agg** shards, int32_t P, const khip_having* h, khip_snapshot* out) {
+  if (!shards || P < 1 || !out) return KHIP_E_INVALID;
+  if (h && (h->agg_index < 0 || h->agg_index >= shards[0]->d.n_aggs)) return KHIP_E_INVALID;
+  sort_job* jobs = (sort_job*)calloc((size_t)P, sizeof(sort_job));
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)P);
+  for (int32_t p = 0; p < P; p++) {
+    jobs[p].a = shards[p];
+    jobs[p].h = h;
+    pthread_create(&th[p], NULL, sort_run, &jobs[p]);
+  }
+  int64_t m = 0;
+  for (int32_t p = 0; p < P; p++) {
+    pthread_join(th[p], NULL);
+    m += jobs[p].m;
+  }
+  owned_entry* rows = (owned_entry*)malloc(sizeof(owned_entry) * (m + 1));
+  int64_t* cur = (int64_t*)calloc((size_t)P, sizeof(int64_t));
+  int32_t* heap = (int32_t*)malloc(sizeof(int32_t) * (size_t)P);
+  int32_t hn = 0;
+#define HEAD(p) (jobs[p].order[cur[p]])
+#define LESS(p, q) (cmp_entry2(jobs[p].a, HEAD(p), jobs[q].a, HEAD(q)) < 0)
+  for (int32_t p = 0; p < P; p++) {
+    if (jobs[p].m == 0) continue;
+    int32_t i = hn++;
+    heap[i] = p;
+    while (i > 0 && LESS(heap[i], heap[(i - 1) / 2])) {
+      int32_t t = heap[i]; heap[i] = heap[(i - 1) / 2]; heap[(i - 1) / 2] = t;
+      i = (i - 1) / 2;
+    }
+  }
+  for (int64_t r = 0; r < m; r++) {
+    const int32_t p = heap[0];
+    rows[r].a = jobs[p].a;
+    rows[r].x = HEAD(p);
+    if (++cur[p] == jobs[p].m) heap[0] = heap[--hn];
+    int32_t i = 0;
+    for (;;) {
+      int32_t l = 2 * i + 1, rr = l + 1, k = i;
+      if (l < hn && LESS(heap[l], heap[k])) k = l;
+      if (rr < hn && LESS(heap[rr], heap[k])) k = rr;
+      if (k == i) break;
+      int32_t t = heap[i]; heap[i] = heap[k]; heap[k] = t;
+      i = k;
+    }
+  }
+#undef LESS
+#undef HEAD
+  khip_status st = write_rows(rows, m, out);
+  for (int32_t p = 0; p < P; p++) free(jobs[p].order);
+  free(rows); free(cur); free(heap); free(jobs); free(th);
+  return st;
 }
 
 /* --------------------------------------------------------------- join table */

@@ -32,6 +32,15 @@ khip_status oracle_agg_snapshot(oracle_agg* agg, const khip_having* having,
                                 khip_snapshot* out);
 khip_status oracle_agg_destroy(oracle_agg* agg);
 
+/* Key-sharded P-thread restatement (same results as oracle_agg_push over the batch): shards[]
+ * are P handles created with the same descriptor and only ever pushed together. */
+khip_status oracle_agg_push_sharded(oracle_agg** shards, int32_t P, const khip_batch* batch,
+                                    khip_batch_stats* stats);
+khip_status oracle_agg_snapshot_size_sharded(oracle_agg** shards, int32_t P, int64_t* n_rows,
+                                             int64_t* key_bytes);
+khip_status oracle_agg_snapshot_sharded(oracle_agg** shards, int32_t P, const khip_having* having,
+                                        khip_snapshot* out);
+
 khip_status oracle_table_create(const khip_table_desc* desc, oracle_table** out);
 khip_status oracle_table_upsert(oracle_table* t, const khip_batch* rows);
 khip_status oracle_table_size(oracle_table* t, int64_t* n_keys);

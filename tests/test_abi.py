@@ -38,9 +38,13 @@ def test_version_and_target():
 
 
 def test_library_is_gfx950_code_object():
+    """Every offload bundle in the library targets gfx950 (one code object per HIP source),
+    and no other GPU target (another gfx, or a CUDA sm_) is embedded."""
     data = open(abi.PRODUCT_LIB, "rb").read()
-    assert b"gfx950" in data
-    assert b"sm_" not in data[:0]  # no CUDA target
+    targets = re.findall(rb"hipv4-amdgcn-amd-amdhsa--(gfx[0-9a-f]+)", data)
+    assert len(targets) >= 4, targets  # agg, agg_part, join, shuffle
+    assert set(targets) == {b"gfx950"}
+    assert re.search(rb"nvptx|sm_[0-9]{2}\b", data) is None
 
 
 @pytest.mark.parametrize("bad", [

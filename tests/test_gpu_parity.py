@@ -59,7 +59,13 @@ def _nan_eq(a, b):
     return (a == b) | (np.isnan(a) & np.isnan(b)) if a.dtype.kind == "f" else (a == b)
 
 
-def assert_snap_equal(g, o, desc, abs_sum_agg=None):
+def assert_snap_equal(g, o, desc, abs_sum_agg=None, count_agg=None):
+    """Integer results, keys, windows, row times, null flags and DOUBLE MIN/MAX bit-exact.
+    DOUBLE-input SUM/AVG within DOUBLE_RTOL (north star 1e-12) relative to the magnitude the
+    summation error is bounded by: for SUM max(|sum|, sum|x|), for AVG max(|avg|, sum|x| / n)
+    — sum|x| from the abs_sum_agg column (SUM over |x|), n from count_agg (COUNT(x)).  Without
+    them (non-negative inputs) the bound is the plain relative error.  AVG of an integer
+    column is an exact int sum divided once, so it is compared bit-exact."""
     assert g["n"] == o["n"], (g["n"], o["n"])
     if isinstance(g["key"], list):
         assert g["key"] == o["key"]
@@ -73,11 +79,16 @@ def assert_snap_equal(g, o, desc, abs_sum_agg=None):
         assert np.array_equal(g["nulls"][a], o["nulls"][a]), "nulls of agg %d" % a
         kind = desc.aggs[a].kind
         gv, ov = g["values"][a], o["values"][a]
-        dbl_sum = rts[a] == abi.TYPE["DOUBLE"] and kind in (abi.AGG["SUM"], abi.AGG["AVG"])
+        in_dbl = kind != abi.AGG["COUNT_STAR"] and desc.col_types[desc.aggs[a].arg_col] == abi.TYPE["DOUBLE"]
+        dbl_sum = in_dbl and kind in (abi.AGG["SUM"], abi.AGG["AVG"])
         if dbl_sum:
             scale = np.abs(ov)
             if abs_sum_agg is not None:
-                scale = np.maximum(scale, np.abs(o["values"][abs_sum_agg]))
+                bound = np.abs(o["values"][abs_sum_agg])
+                if kind == abi.AGG["AVG"]:
+                    assert count_agg is not None, "AVG bound needs the non-null count"
+                    bound = bound / np.maximum(o["values"][count_agg], 1)
+                scale = np.maximum(scale, bound)
             err = np.abs(gv - ov)
             ok = (err <= DOUBLE_RTOL * scale + 1e-300) | (np.isnan(gv) & np.isnan(ov))
             assert ok.all(), "agg %d max rel err %g" % (a, np.max(err / np.maximum(scale, 1e-300)))
@@ -107,8 +118,10 @@ def _random_batch(rng, n, key_type, nkeys, span, disorder, null_frac=0.05, t0=0,
 
 
 ALL_AGGS = [("COUNT_STAR", -1), ("COUNT", 0), ("SUM", 0), ("SUM", 1), ("SUM", 2), ("MIN", 0), ("MAX", 0),
-            ("MIN", 1), ("MAX", 1), ("MIN", 2), ("MAX", 2), ("AVG", 0), ("AVG", 1), ("AVG", 2), ("SUM", 3)]
-ABS_SUM = len(ALL_AGGS) - 1
+            ("MIN", 1), ("MAX", 1), ("MIN", 2), ("MAX", 2), ("AVG", 0), ("AVG", 1), ("AVG", 2), ("COUNT", 2),
+            ("SUM", 3)]
+ABS_SUM = len(ALL_AGGS) - 1  # SUM(|x|) of the DOUBLE column: the summation error bound
+CNT_DBL = len(ALL_AGGS) - 2  # COUNT(x) of the DOUBLE column: AVG's divisor
 
 WINDOWS = [
     dict(window_kind="NONE"),
@@ -140,7 +153,7 @@ def test_random_vs_oracle(prod, orc, key_type, win, nbatches, engine):
     kw = dict(WINDOWS[win], key_type=key_type, col_types=["INT32", "INT64", "DOUBLE", "DOUBLE"], aggs=ALL_AGGS)
     (g, gs, desc), (o, os_, _) = _run_both(prod, orc, kw, batches, engine=engine)
     assert gs == os_
-    assert_snap_equal(g, o, desc, ABS_SUM)
+    assert_snap_equal(g, o, desc, ABS_SUM, CNT_DBL)
 
 
 @pytest.mark.parametrize("having", [{"agg": 0, "op": "GT", "value": 3}, {"agg": 4, "op": "LE", "value": 10.5},
@@ -150,7 +163,7 @@ def test_having_vs_oracle(prod, orc, having, engine):
     batches = [_random_batch(rng, 20000, "INT64", 2000, 100_000, 5_000)]
     kw = dict(WINDOWS[1], key_type="INT64", col_types=["INT32", "INT64", "DOUBLE", "DOUBLE"], aggs=ALL_AGGS)
     (g, _, desc), (o, _, _) = _run_both(prod, orc, kw, batches, having, engine=engine)
-    assert_snap_equal(g, o, desc, ABS_SUM)
+    assert_snap_equal(g, o, desc, ABS_SUM, CNT_DBL)
     h = abi.AggHandle(prod, abi.make_agg_desc(**dict(kw, flags=engine)))
     h.push(batches[0])
     assert h.count_rows(having) == o["n"]
@@ -170,7 +183,7 @@ def test_empty_and_all_null_batches(prod, orc, engine):
     (g, gs, desc), (o, os_, _) = _run_both(prod, orc, kw, [empty, allnull, nullvals, empty], engine=engine)
     assert gs == os_
     assert gs[1]["dropped_null_key"] == n
-    assert_snap_equal(g, o, desc, ABS_SUM)
+    assert_snap_equal(g, o, desc, ABS_SUM, CNT_DBL)
     assert g["n"] > 0 and g["nulls"][5].all()  # MIN over only-null inputs is NULL (entry exists)
 
 
@@ -183,7 +196,7 @@ def test_hot_key_contention(prod, orc, engine):
     kw = dict(WINDOWS[3], key_type="INT64", col_types=["INT32", "INT64", "DOUBLE", "DOUBLE"], aggs=ALL_AGGS)
     (g, gs, desc), (o, os_, _) = _run_both(prod, orc, kw, [b], engine=engine)
     assert gs == os_
-    assert_snap_equal(g, o, desc, ABS_SUM)
+    assert_snap_equal(g, o, desc, ABS_SUM, CNT_DBL)
 
 
 def test_table_growth_and_resume(prod, orc, engine):
@@ -195,7 +208,7 @@ def test_table_growth_and_resume(prod, orc, engine):
               capacity_hint=16)
     (g, gs, desc), (o, os_, _) = _run_both(prod, orc, kw, batches, engine=engine)
     assert gs == os_
-    assert_snap_equal(g, o, desc, ABS_SUM)
+    assert_snap_equal(g, o, desc, ABS_SUM, CNT_DBL)
 
 
 @pytest.mark.parametrize("win", [0, 1, 3])
@@ -208,7 +221,7 @@ def test_many_partitions_vs_oracle(prod, orc, win, engine):
               capacity_hint=30_000_000)
     (g, gs, desc), (o, os_, _) = _run_both(prod, orc, kw, batches, engine=engine)
     assert gs == os_
-    assert_snap_equal(g, o, desc, ABS_SUM)
+    assert_snap_equal(g, o, desc, ABS_SUM, CNT_DBL)
 
 
 @pytest.mark.parametrize("win", [1, 3])

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 from ksql_amd import abi
-from test_gpu_parity import ALL_AGGS, ABS_SUM, ENGINES, WINDOWS, _random_batch, assert_snap_equal
+from test_gpu_parity import ALL_AGGS, ABS_SUM, CNT_DBL, ENGINES, WINDOWS, _random_batch, assert_snap_equal
 
 pytestmark = pytest.mark.gpu
 
@@ -89,7 +89,7 @@ def test_pull_by_keys_and_bounds(prod, orc, win, engine):
     for keys, ws, we in queries:
         got = g.get(keys, ws, we)
         exp = _filter(full, keys, ws, we, windowed)
-        assert_snap_equal(got, exp, desc, ABS_SUM)
+        assert_snap_equal(got, exp, desc, ABS_SUM, CNT_DBL)
     assert g.get([], (None, None), (None, None))["n"] == 0
     g.close()
     o.close()
@@ -104,7 +104,7 @@ def test_pull_with_having(prod, orc, engine):
     exp_all = o.snapshot(having)
     keys = np.unique(exp_all["key"])[:50]
     got = g.get(keys, (0, 50_000), (None, None), having=having)
-    assert_snap_equal(got, _filter(exp_all, keys, (0, 50_000), (None, None), True), desc, ABS_SUM)
+    assert_snap_equal(got, _filter(exp_all, keys, (0, 50_000), (None, None), True), desc, ABS_SUM, CNT_DBL)
     g.close()
     o.close()
 
@@ -119,7 +119,7 @@ def test_pull_sees_closed_windows(prod, orc):
     full = o.snapshot()
     keys = np.unique(full["key"])[:40]
     for ws in [(0, 99_999), (400_000, 800_000), (None, None)]:
-        assert_snap_equal(g.get(keys, ws), _filter(full, keys, ws, (None, None), True), desc, ABS_SUM)
+        assert_snap_equal(g.get(keys, ws), _filter(full, keys, ws, (None, None), True), desc, ABS_SUM, CNT_DBL)
     g.close()
     o.close()
 
@@ -142,7 +142,7 @@ def test_pull_utf8_keys(prod, orc, engine):
         (["never-pushed"], (None, None)),
     ]
     for keys, ws in queries:
-        assert_snap_equal(g.get(keys, ws), _filter(full, keys, ws, (None, None), True), desc, ABS_SUM)
+        assert_snap_equal(g.get(keys, ws), _filter(full, keys, ws, (None, None), True), desc, ABS_SUM, CNT_DBL)
     g.close()
     o.close()
 
