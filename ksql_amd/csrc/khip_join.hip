@@ -282,7 +282,8 @@ __global__ __launch_bounds__(256) void k_probe(const uint64_t* __restrict__ tabl
       }
     }
     for (int c = 0; c < ncols; c++) {
-      const bool isnull = !hit || (meta & (1ULL << c));
+      // rows past the batch end keep a 0 bit (the bitmap's last byte is partial when n % 8 != 0)
+      const bool isnull = i < n && (!hit || (meta & (1ULL << c)));
       const uint64_t bn = __ballot(isnull);
       if (out.col_null[c] && lane == 0 && wbase < n) {
         const int64_t nbytes = std::min<int64_t>(8, (n - wbase + 7) / 8);
