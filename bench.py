@@ -289,7 +289,7 @@ def bench_possible_fraud(args, lib, rank, world, local):
     h.kernel_times(reset=True)
     (st, rows), elapsed = timed_loop(step, args.steps, world)
     kt = h.kernel_times()
-    groups = int(h.count_rows(None))
+    groups = int(h.snapshot_size())  # host bookkeeping: no device work after the timed loop
 
     pcie = pull = None
     if rank == 0 and not args.no_extras and not args.utf8 and n <= 100_000_000:
@@ -446,7 +446,7 @@ def cpu_baseline_hourly(n, target_s):
         reps = max(1, int(target_s / max(dt, 1e-3)))
         out.append((n * reps, run(shards, reps)))
     return cpu_baseline_block(out[0], out[1], P, "records/s",
-                              "%%d records (the 1M-record hourly_metrics run, repeated), %%d key-hash shards")
+                              "%d records (the 1M-record hourly_metrics run, repeated), %d key-hash shards")
 
 
 # ------------------------------------------------------------------ C3 hopping_double

@@ -419,6 +419,12 @@ class AggHandle:
     def reset(self):
         self.lib.check(self.lib.agg_reset(self.h), "agg_reset")
 
+    def snapshot_size(self):
+        """Rows of the materialized table (khip_agg_snapshot_size, no key-byte count: no device work)."""
+        n = i64()
+        self.lib.check(self.lib.agg_snapshot_size(self.h, C.byref(n), None), "agg_snapshot_size")
+        return n.value
+
     def count_rows(self, having=None):
         n = i64()
         hv = None

@@ -1,13 +1,19 @@
 #!/usr/bin/env python3
-"""HBM traffic per push from rocprofv3 FETCH_SIZE / WRITE_SIZE passes (separate runs).
+"""HBM traffic per bench step from rocprofv3 FETCH_SIZE / WRITE_SIZE passes (separate runs).
 
-FETCH_SIZE/WRITE_SIZE are in KB.  On gfx950 FETCH_SIZE reports 1/2 of the bytes of wide
-coalesced streaming reads (MI355X_MICROARCH.md, HBM); we calibrate on k_part_hist, whose
-reads are exactly 16 B x records (key + ts), and apply that factor to every kernel's reads.
-WRITE_SIZE is taken as reported.
+The profiled command is `bench.py --config <leg> --steps S --warmup W --no-cpu-baseline
+--no-extras`: every library dispatch of the run belongs to one of the S + W identical steps
+(the generators and the copy-rate probe are torch kernels and are excluded by name), so
+bytes per step = sum over the library's dispatches / (S + W).
+
+Units and the gfx950 correction (MI355X_MICROARCH.md, HBM / rocprofv3): FETCH_SIZE and
+WRITE_SIZE are in KB; FETCH_SIZE reports 1/2 of the bytes of a wide coalesced streaming read,
+so reads are doubled; WRITE_SIZE is taken as reported.  Where the run contains k_part_hist,
+whose reads are exactly 16 B x records (key + ts), the measured factor is reported beside the
+guide's 2.0 as a check of the correction on this access pattern.
 
 usage: pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv> <records>
-                      <out json> [config]
+                      <steps incl. warmup> <out json> <config key>
 """
 import csv
 import json
@@ -15,8 +21,19 @@ import re
 import sys
 from collections import defaultdict
 
-PUSH = ["k_part_hist", "k_part_colsum", "k_part_colbase", "k_part_colprefix", "k_scan_blocks", "k_scan_excl",
-        "k_part_scatter", "k_part_refine", "k_part_wrange", "k_part_agg", "k_part_commit"]
+
+def kname(raw):
+    name = re.sub(r"\(.*", "", raw).replace("khip::", "").replace("void ", "")
+    return re.sub(r"<.*", "", name).strip()
+
+
+# library kernels that run outside the timed step of a leg (the join's table build)
+OUTSIDE_STEP = ("k_upsert_claim", "k_upsert_finalize", "k_upsert_apply", "k_table_rehash", "k_count_live")
+
+
+def library_kernel(name):
+    # the library's kernels (torch's are at::native::...), minus the setup ones
+    return name.startswith("k_") and name not in OUTSIDE_STEP
 
 
 def load(path, counter):
@@ -24,9 +41,9 @@ def load(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        name = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("khip::", "").replace("void ", "")
-        name = re.sub(r"<.*", "", name).strip()
-        per[name].append(float(r["Counter_Value"]) * 1024.0)
+        name = kname(r["Kernel_Name"])
+        if library_kernel(name):
+            per[name].append(float(r["Counter_Value"]) * 1024.0)
     return per
 
 
@@ -34,32 +51,30 @@ def main():
     fetch = load(sys.argv[1], "FETCH_SIZE")
     write = load(sys.argv[2], "WRITE_SIZE")
     n = int(sys.argv[3])
-    cfg = sys.argv[5] if len(sys.argv) > 5 else "possible_fraud"
-    hist = fetch.get("k_part_hist")
-    factor = (16.0 * n) / (sum(hist) / len(hist)) if hist else 2.0
+    steps = int(sys.argv[4])
+    out_path, cfg = sys.argv[5], sys.argv[6]
     per_kernel = {}
     total = 0.0
-    for k in PUSH:
-        if k not in fetch and k not in write:
-            continue
-        f = fetch.get(k, [0.0])
-        w = write.get(k, [0.0])
-        calls_per_push = 1 if k not in ("k_scan_excl",) else 1
-        rd = factor * sum(f) / len(f)
-        wr = sum(w) / len(w)
-        per_kernel[k] = {"read_bytes": rd, "write_bytes": wr}
-        total += (rd + wr) * calls_per_push
-    out = {cfg: {"push": {"records": n, "hbm_bytes_per_launch": total, "fetch_calibration_factor": factor,
-                          "per_kernel": per_kernel,
-                          "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
-                                    "FETCH scaled by the k_part_hist calibration (16 B/record)"}}}
+    for k in sorted(set(fetch) | set(write)):
+        rd = 2.0 * sum(fetch.get(k, [])) / steps
+        wr = sum(write.get(k, [])) / steps
+        per_kernel[k] = {"read_bytes_per_step": rd, "write_bytes_per_step": wr,
+                         "dispatches_per_step": len(fetch.get(k, write.get(k, []))) / steps}
+        total += rd + wr
+    rec = {"records": n, "hbm_bytes_per_step": total, "hbm_bytes_per_record": total / n,
+           "fetch_correction": 2.0, "per_kernel": per_kernel,
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over the same bench "
+                     "command; library kernels only; FETCH_SIZE x 2 (gfx950 wide-stream correction)"}
+    hist = fetch.get("k_part_hist")
+    if hist:
+        rec["k_part_hist_fetch_factor_measured"] = (16.0 * n * len(hist) / steps) / sum(hist)
     try:
-        prev = json.load(open(sys.argv[4]))
+        prev = json.load(open(out_path))
     except (OSError, ValueError):
         prev = {}
-    prev.update(out)
-    json.dump(prev, open(sys.argv[4], "w"), indent=1)
-    print(json.dumps(out, indent=1))
+    prev[cfg] = rec
+    json.dump(prev, open(out_path, "w"), indent=1)
+    print(json.dumps({cfg: {k: v for k, v in rec.items() if k != "per_kernel"}}, indent=1))
 
 
 if __name__ == "__main__":
