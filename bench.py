@@ -272,11 +272,12 @@ def bench_possible_fraud(args, lib, rank, world, local):
     else:
         batch = abi.DeviceBatch(ts, keys=card)
     torch.cuda.synchronize()
+    having = {"agg": 0, "op": "GT", "value": 3}  # the query's HAVING: part of the plan (TableFilter)
     desc = abi.make_agg_desc(window_kind="TUMBLING", size_ms=5000, key_type="UTF8" if args.utf8 else "INT64",
                              aggs=[("COUNT_STAR", -1)], device=local, capacity_hint=int(min(3 * args.keys, 2 * n)),
-                             flags=abi.FLAG_PROFILE | (abi.FLAG_ENGINE_ATOMIC if args.engine == "atomic" else 0))
+                             flags=abi.FLAG_PROFILE | (abi.FLAG_ENGINE_ATOMIC if args.engine == "atomic" else 0),
+                             having=having)
     h = abi.AggHandle(lib, desc)
-    having = {"agg": 0, "op": "GT", "value": 3}
 
     def step():
         h.reset()

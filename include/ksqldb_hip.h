@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KHIP_ABI_VERSION 1
+#define KHIP_ABI_VERSION 2
 
 typedef int32_t khip_status;
 #define KHIP_OK 0
@@ -132,6 +132,25 @@ typedef struct khip_batch_stats {
 
 /* --------------------------------------------------------- windowed aggregate */
 
+/* Window store retention (WINDOW ... RETENTION, X/windows/KsqlWindowExpression.java:26-54, passed to
+ * the store by S/StreamAggregateBuilder.java:293,322,350 → X/runtime/MaterializedFactory.java:47).
+ * Without the clause Kafka Streams keeps windows for size + grace. */
+#define KHIP_RETENTION_DEFAULT (-1)
+
+/* Output refinement (S/StreamAggregateBuilder.java:282-285): EMIT CHANGES emits every update,
+ * EMIT FINAL (EmitStrategy.onWindowClose) emits a window once, when it closes. */
+#define KHIP_EMIT_CHANGES 0
+#define KHIP_EMIT_FINAL 1
+
+/* HAVING predicate on one aggregate's result (S/TableFilterBuilder.java:46-74).
+ * Rows failing it are absent from the materialized table (tombstoned). */
+typedef struct khip_having {
+  int32_t agg_index;
+  int32_t op;        /* KHIP_OP_*                                                     */
+  int64_t i64;       /* constant for integer-valued results                          */
+  double f64;        /* constant for DOUBLE-valued results (AVG, SUM/MIN/MAX DOUBLE) */
+} khip_having;
+
 typedef struct khip_agg_spec {
   int32_t kind;    /* KHIP_AGG_*                                                      */
   int32_t arg_col; /* value column index (ignored for COUNT_STAR)                     */
@@ -152,20 +171,19 @@ typedef struct khip_agg_desc {
   int32_t n_aggs;
   const khip_agg_spec* aggs;
   int32_t device;           /* HIP device ordinal                                    */
-  int32_t flags;            /* reserved, 0                                           */
+  int32_t flags;            /* KHIP_FLAG_* below, 0 by default                        */
   int64_t capacity_hint;    /* expected live (key, window) groups; 0 = default       */
+  /* ABI 2 */
+  int64_t retention_ms;     /* window retention, or KHIP_RETENTION_DEFAULT; must be >= size +
+                               grace (Kafka Streams rejects a shorter one)               */
+  int32_t emit;             /* KHIP_EMIT_CHANGES or KHIP_EMIT_FINAL                      */
+  int32_t has_having;       /* 1: `having` is the query's HAVING (the TableFilter step after
+                               the aggregate); the library then keeps its row count and
+                               changelog tombstones up to date as records arrive          */
+  khip_having having;
 } khip_agg_desc;
 
 typedef struct khip_agg khip_agg;
-
-/* HAVING predicate on one aggregate's result (S/TableFilterBuilder.java:46-74).
- * Rows failing it are absent from the materialized table (tombstoned). */
-typedef struct khip_having {
-  int32_t agg_index;
-  int32_t op;        /* KHIP_OP_*                                                     */
-  int64_t i64;       /* constant for integer-valued results                          */
-  double f64;        /* constant for DOUBLE-valued results (AVG, SUM/MIN/MAX DOUBLE) */
-} khip_having;
 
 /* Final materialized table, sorted by (key, window_start).  Caller-allocated.
  * Row = [key, agg results..., WINDOWSTART, WINDOWEND]

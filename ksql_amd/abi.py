@@ -19,6 +19,7 @@ PRODUCT_LIB = os.path.join(REPO, "ksql_amd", "libksqldb_hip_tune.so" if os.envir
                            else "libksqldb_hip.so")
 ORACLE_LIB = os.path.join(REPO, "oracle", "liboracle.so")
 
+ABI_VERSION = 2  # include/ksqldb_hip.h KHIP_ABI_VERSION the structs below mirror
 KHIP_OK = 0
 KHIP_E_BUFFER = -5
 
@@ -32,6 +33,8 @@ MEM_HOST, MEM_DEVICE = 0, 1
 FLAG_PROFILE = 1
 FLAG_ENGINE_ATOMIC = 2
 FLAG_PART_CLAIM = 4
+RETENTION_DEFAULT = -1
+EMIT = {"CHANGES": 0, "FINAL": 1}
 NP_TYPE = {0: np.int32, 1: np.int64, 2: np.float64}
 
 i32, i64, u8p = C.c_int32, C.c_int64, C.POINTER(C.c_uint8)
@@ -57,15 +60,17 @@ class AggSpec(C.Structure):
     _fields_ = [("kind", i32), ("arg_col", i32)]
 
 
+class Having(C.Structure):
+    _fields_ = [("agg_index", i32), ("op", i32), ("i64", i64), ("f64", C.c_double)]
+
+
 class AggDesc(C.Structure):
     _fields_ = [("window_kind", i32), ("key_type", i32), ("size_ms", i64), ("advance_ms", i64),
                 ("grace_ms", i64), ("n_cols", i32), ("col_types", C.POINTER(i32)),
                 ("n_aggs", i32), ("aggs", C.POINTER(AggSpec)), ("device", i32), ("flags", i32),
-                ("capacity_hint", i64)]
-
-
-class Having(C.Structure):
-    _fields_ = [("agg_index", i32), ("op", i32), ("i64", i64), ("f64", C.c_double)]
+                ("capacity_hint", i64),
+                # ABI 2
+                ("retention_ms", i64), ("emit", i32), ("has_having", i32), ("having", Having)]
 
 
 class Snapshot(C.Structure):
@@ -264,14 +269,24 @@ class HostBatch:
                             _ptr(self.ts), self._cd, self._cv)
 
 
+def having_struct(having):
+    """{"agg": i, "op": "GT", "value": v} → Having (integer constant for int values, both set)."""
+    v = having["value"]
+    return Having(having["agg"], OP[having["op"]], 0 if isinstance(v, float) else int(v), float(v))
+
+
 def make_agg_desc(window_kind="NONE", key_type="INT64", size_ms=0, advance_ms=0, grace_ms=-1,
-                  col_types=(), aggs=(), device=0, capacity_hint=0, flags=0):
+                  col_types=(), aggs=(), device=0, capacity_hint=0, flags=0, retention_ms=RETENTION_DEFAULT,
+                  emit="CHANGES", having=None):
+    """having: the query's HAVING ({"agg", "op", "value"}), maintained by the library (ABI 2)."""
     ct = (i32 * max(len(col_types), 1))(*[TYPE[t] if isinstance(t, str) else t for t in col_types])
     sp = (AggSpec * max(len(aggs), 1))(*[AggSpec(AGG[k] if isinstance(k, str) else k, c) for k, c in aggs])
     d = AggDesc(WINDOW[window_kind] if isinstance(window_kind, str) else window_kind,
                 KEY[key_type] if isinstance(key_type, str) else key_type,
                 size_ms, advance_ms if advance_ms else size_ms, grace_ms, len(col_types), ct,
-                len(aggs), sp, device, flags, capacity_hint)
+                len(aggs), sp, device, flags, capacity_hint, retention_ms,
+                EMIT[emit] if isinstance(emit, str) else emit, 0 if having is None else 1,
+                Having() if having is None else having_struct(having))
     d._keep = (ct, sp)
     return d
 

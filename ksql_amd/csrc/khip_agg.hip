@@ -704,6 +704,19 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
     if (s.kind != KHIP_AGG_COUNT_STAR && (s.arg_col < 0 || s.arg_col >= d.n_cols))
       return fail(KHIP_E_INVALID, "aggregate argument column");
   }
+  if (d.emit != KHIP_EMIT_CHANGES && d.emit != KHIP_EMIT_FINAL) return fail(KHIP_E_INVALID, "emit strategy");
+  if (d.emit == KHIP_EMIT_FINAL && d.window_kind == KHIP_WINDOW_NONE)
+    return fail(KHIP_E_INVALID, "EMIT FINAL needs a windowed aggregation");
+  if (d.window_kind != KHIP_WINDOW_NONE && d.retention_ms != KHIP_RETENTION_DEFAULT) {
+    // TimeWindowedKStreamImpl: retention < size + grace is an IllegalArgumentException
+    const int64_t g = grace_of(d);
+    if (d.retention_ms < 0 || d.retention_ms < d.size_ms + g)
+      return fail(KHIP_E_INVALID, "retention must be at least window size + grace");
+  }
+  if (d.has_having) {
+    if (d.having.agg_index < 0 || d.having.agg_index >= d.n_aggs) return fail(KHIP_E_INVALID, "having agg index");
+    if (d.having.op < KHIP_OP_GT || d.having.op > KHIP_OP_NE) return fail(KHIP_E_INVALID, "having op");
+  }
   khip_agg* a = new khip_agg();
   a->desc = d;
   a->col_types.assign(d.col_types, d.col_types + d.n_cols);
@@ -723,6 +736,13 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
   if (st != KHIP_OK) {
     delete a;
     return st;
+  }
+  if (d.has_having) {
+    a->having.active = 1;
+    a->having.op = d.having.op;
+    a->having.a = a->outs[d.having.agg_index];
+    a->having.i64 = d.having.i64;
+    a->having.f64 = d.having.f64;
   }
   DeviceGuard g(a->device);
   if (hipStreamCreateWithFlags(&a->stream, hipStreamDefault) != hipSuccess) {
@@ -959,8 +979,10 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   a->times.apply_ms += apply_ms;
   a->times.finalize_ms += fin_ms;
   }
-  KHIP_TRY_HIP(hipMemcpyAsync(&a->host_stream_time, a->stream_time.p, 8, hipMemcpyDeviceToHost, a->stream));
-  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  if (a->engine != 0) {  // the partitioned engine brought it back with its end-of-push counters
+    KHIP_TRY_HIP(hipMemcpyAsync(&a->host_stream_time, a->stream_time.p, 8, hipMemcpyDeviceToHost, a->stream));
+    KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  }
   s.rows_accepted = tot[P_ACCEPTED];
   s.dropped_null_key = tot[P_NULL_KEY];
   s.dropped_null_row = tot[P_NULL_ROW];
@@ -1016,6 +1038,12 @@ khip_status khip_agg_count_rows(khip_agg* a, const khip_having* h, int64_t* n) {
   clear_error();
   if (!a || !n) return fail(KHIP_E_INVALID, "null argument");
   DeviceGuard g(a->device);
+  // the query's own HAVING: counts maintained by the aggregate kernel, no table scan
+  if (h && a->engine == 0 && a->desc.has_having && h->agg_index == a->desc.having.agg_index &&
+      h->op == a->desc.having.op && h->i64 == a->desc.having.i64 &&
+      (h->f64 == a->desc.having.f64 || (h->f64 != h->f64 && a->desc.having.f64 != a->desc.having.f64)) &&
+      part_having_count(a, n))
+    return KHIP_OK;
   return compact_rows(a, h, nullptr, n);
 }
 

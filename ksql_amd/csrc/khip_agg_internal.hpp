@@ -152,35 +152,36 @@ __device__ __forceinline__ int64_t load_col_raw(const ColPtrs& c, int32_t type, 
   return ((const int64_t*)c.data[col])[i];  // INT64, or DOUBLE bits
 }
 
-__device__ __forceinline__ bool decode_result(const uint64_t* s, const AggOut& a, int64_t* iv, double* dv) {
-  // returns false for SQL NULL; sets *iv for integer results, *dv for DOUBLE results
+// One aggregate's result from its value word and non-null count word.  Returns false for
+// SQL NULL; sets *iv for integer results, *dv for DOUBLE results.
+__device__ __forceinline__ bool decode_words(uint64_t val, uint64_t cntw, const AggOut& a, int64_t* iv, double* dv) {
   switch (a.kind) {
     case KHIP_AGG_COUNT_STAR:
     case KHIP_AGG_COUNT:
-      *iv = (int64_t)s[a.w_val];
+      *iv = (int64_t)val;
       return true;
     case KHIP_AGG_SUM:
-      if (a.type == KHIP_TYPE_DOUBLE) __builtin_memcpy(dv, &s[a.w_val], 8);
-      else if (a.type == KHIP_TYPE_INT32) *iv = (int64_t)(int32_t)s[a.w_val];
-      else *iv = (int64_t)s[a.w_val];
+      if (a.type == KHIP_TYPE_DOUBLE) __builtin_memcpy(dv, &val, 8);
+      else if (a.type == KHIP_TYPE_INT32) *iv = (int64_t)(int32_t)val;
+      else *iv = (int64_t)val;
       return true;
     case KHIP_AGG_MIN:
     case KHIP_AGG_MAX:
-      if ((int64_t)s[a.w_cnt] == 0) return false;
-      if (a.type == KHIP_TYPE_DOUBLE) *dv = f64_from_order_key((int64_t)s[a.w_val]);
-      else *iv = (int64_t)s[a.w_val];
+      if ((int64_t)cntw == 0) return false;
+      if (a.type == KHIP_TYPE_DOUBLE) *dv = f64_from_order_key((int64_t)val);
+      else *iv = (int64_t)val;
       return true;
     case KHIP_AGG_AVG: {
-      const int64_t c = (int64_t)s[a.w_cnt];
+      const int64_t c = (int64_t)cntw;
       if (c == 0) { *dv = 0.0; return true; }
       if (a.type == KHIP_TYPE_DOUBLE) {
         double sum;
-        __builtin_memcpy(&sum, &s[a.w_val], 8);
+        __builtin_memcpy(&sum, &val, 8);
         *dv = sum / (double)c;
       } else if (a.type == KHIP_TYPE_INT32) {
-        *dv = (double)(int32_t)s[a.w_val] / (double)c;
+        *dv = (double)(int32_t)val / (double)c;
       } else {
-        *dv = (double)(int64_t)s[a.w_val] / (double)c;
+        *dv = (double)(int64_t)val / (double)c;
       }
       return true;
     }
@@ -188,10 +189,38 @@ __device__ __forceinline__ bool decode_result(const uint64_t* s, const AggOut& a
   return false;
 }
 
+__device__ __forceinline__ bool decode_result(const uint64_t* s, const AggOut& a, int64_t* iv, double* dv) {
+  return decode_words(s[a.w_val], a.w_cnt >= 0 ? s[a.w_cnt] : 0, a, iv, dv);
+}
+
 __device__ __forceinline__ bool result_is_double(const AggOut& a) {
   if (a.kind == KHIP_AGG_AVG) return true;
   if (a.kind == KHIP_AGG_COUNT || a.kind == KHIP_AGG_COUNT_STAR) return false;
   return a.type == KHIP_TYPE_DOUBLE;
+}
+
+// HAVING on an aggregate's value / count words (no pull filter)
+__device__ __forceinline__ bool having_ok_words(uint64_t val, uint64_t cntw, const HavingDev& h) {
+  if (!h.active) return true;
+  int64_t iv = 0;
+  double dv = 0.0;
+  if (!decode_words(val, cntw, h.a, &iv, &dv)) return false;
+  int c;
+  if (result_is_double(h.a)) {
+    if (dv != dv) return h.op == KHIP_OP_NE;
+    c = dv < h.f64 ? -1 : (dv > h.f64 ? 1 : 0);
+  } else {
+    c = iv < h.i64 ? -1 : (iv > h.i64 ? 1 : 0);
+  }
+  switch (h.op) {
+    case KHIP_OP_GT: return c > 0;
+    case KHIP_OP_GE: return c >= 0;
+    case KHIP_OP_LT: return c < 0;
+    case KHIP_OP_LE: return c <= 0;
+    case KHIP_OP_EQ: return c == 0;
+    case KHIP_OP_NE: return c != 0;
+  }
+  return false;
 }
 
 __device__ __forceinline__ bool having_ok(const uint64_t* s, const HavingDev& h) {
@@ -268,6 +297,17 @@ struct PartState {
   bool res_fresh = true;
   // two-level scatter: pass-A records, per-tile bucket histogram / offsets, bucket scans
   DevBuf srecA, hcoarse, scan_tmpB, RB;
+  // k_part_merge (delta-only LDS): entries, LDS bytes, plane layout (khip_agg_part.hip)
+  int mH = 0, m_lds = 0, rt_off = 0;
+  int32_t plane_off[MAX_OPS] = {};
+  int8_t plane_w64[MAX_OPS] = {};
+  int8_t word_op[32] = {};
+  // the query's HAVING maintained on the device: rows passing it per partition (hcnt; hnew =
+  // being written this push) and in the closed store (hclosed).  hvalid = false once a push
+  // took a path that does not maintain them (fallback kernel, split) until the next reset.
+  DevBuf hcnt, hnew, hclosed;
+  bool hvalid = true;
+  HostBuf pinfo;  // pinned: push info (window range, event-time span) and end-of-push stats
 };
 
 }  // namespace khip
@@ -306,6 +346,7 @@ struct khip_agg {
   hipEvent_t ev[8] = {};  // 0-4 atomic engine phases, 5-7 partitioned engine
   khip_kernel_times times{};
   int engine = 0;  // 0 partitioned (LDS-owned groups), 1 global-atomic
+  khip::HavingDev having{};  // the query's HAVING (desc.has_having), maintained by the merge kernel
   khip::PartState part;
 };
 
@@ -326,6 +367,7 @@ khip_status part_reset(khip_agg* a);
 khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
                       const uint8_t* rv, const ColPtrs& cols, int64_t* tot);
 khip_status part_compact(khip_agg* a, const HavingDev& h, std::vector<uint64_t>* rows, int64_t* count);
+bool part_having_count(khip_agg* a, int64_t* n);
 }  // namespace khip
 
 

@@ -841,6 +841,397 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
 #undef AGG_T
 }
 
+// ------------------------------------------------------------------ k_part_merge
+// The default aggregate kernel when the push's windows fit the packed identity (wr[1]) and
+// its event-time span fits 31 bits.  One work item = one partition (or one of its sub-passes).
+// Unlike k_part_agg, LDS holds only the groups THIS PUSH touches, as deltas in compact planes:
+//   id u64[H] | rowtime u32[H] (ts - tbase + 1, 0 = none; bit 31 = matched by a resident row)
+//   | one plane per update op: u64 (SUM, MIN, MAX) then u32 (COUNT, non-null count)
+// and the partition's resident rows are merged on the way out (old row ⊕ delta → new buffer),
+// so the LDS footprint does not grow with the resident state (C2 COUNT(*): 16 B per group →
+// 4096 groups in 64 KB, two workgroups per CU).  Phases:
+//   0. pass 0 only: resident rows of windows closed before this push → closed store
+//   1. records (prefetched before the LDS init): window fan-out, find-or-claim the packed
+//      identity with one 64-bit LDS CAS, LDS atomics on the delta planes
+//   2. resident rows: probe their identity, mark the matched delta entries
+//   3. count (resident live rows + unmatched deltas) per wave, block scan, reserve the
+//      partition's region range with one atomic, check capacity
+//   4. write merged resident rows, then new rows, wave-compacted (ballot ranks) so each store
+//      instruction covers consecutive rows; count the rows passing the query's HAVING
+// A partition whose deltas overflow H writes nothing and is retried with 2x sub-passes (it
+// has already moved its closed rows in pass 0; retries skip them).
+constexpr int MG_THREADS = 512;
+constexpr int MG_AU = 8;
+constexpr uint32_t RT_MATCHED = 0x80000000u;
+
+struct MergeParams {
+  int32_t windowed;
+  int32_t sw;      // row words in the regions
+  int32_t nwords;  // words used (3 + state words)
+  int32_t H;       // LDS delta entries (multiple of 64)
+  int32_t rw;      // scattered record words
+  int32_t meta_word;
+  int32_t log2P;
+  int32_t n_ops;
+  int64_t size, adv;
+  FastDiv fd;
+  int64_t cmax;
+  int64_t tbase;  // rowtime planes hold ts - tbase + 1 (push span < 2^31 - 1)
+  int8_t col_word[MAX_COLS];
+  int32_t col_type[MAX_COLS];
+  UpdOp ops[MAX_OPS];
+  int32_t plane_off[MAX_OPS];  // byte offset of op o's delta plane
+  int8_t plane_w64[MAX_OPS];   // 1: u64 plane, 0: u32 plane
+  int32_t rt_off;              // byte offset of the rowtime plane
+  int32_t lds_bytes;
+  int8_t word_op[32];  // row word → update op (-1: key / ws / rowtime / padding)
+  InitWords init;
+  HavingDev having;  // the query's HAVING (active = 0: none): rows passing it are counted
+};
+
+__device__ __forceinline__ uint32_t mg_slot(uint64_t id, int H) {
+  const uint32_t h = ((uint32_t)id * 0x9E3779B1u) ^ (uint32_t)(id >> 32) * 0x85EBCA77u;
+  return (uint32_t)(((uint64_t)h * (uint32_t)H) >> 32);
+}
+
+// barrier without the vmcnt(0) that __syncthreads() implies: LDS writes are waited for, the
+// wave's outstanding global loads (the record prefetch) stay in flight
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <class T>
+__device__ __forceinline__ KLDS T* mg_plane(char* smem, int32_t off) {
+  return (KLDS T*)((KLDS char*)smem + off);
+}
+
+// Word w (>= 3) of the merged row: resident row `old` (nullptr: a new group) ⊕ delta entry e.
+__device__ __forceinline__ uint64_t mg_word(const MergeParams& q, char* smem, int w, const uint64_t* old, int e) {
+  const int op_of_w = q.word_op[w];
+  if (op_of_w < 0) return old ? old[w] : (uint64_t)q.init.w[w];
+  const UpdOp op = q.ops[op_of_w];
+  uint64_t d;
+  if (q.plane_w64[op_of_w]) d = (uint64_t)mg_plane<int64_t>(smem, q.plane_off[op_of_w])[e];
+  else d = (uint64_t)mg_plane<uint32_t>(smem, q.plane_off[op_of_w])[e];
+  if (!old) return d;
+  const uint64_t o = old[w];
+  switch (op.kind) {
+    case OP_INC:
+    case OP_INC_VALID:
+    case OP_ADD_I64: return o + d;
+    case OP_ADD_F64: {
+      double a, b;
+      __builtin_memcpy(&a, &o, 8);
+      __builtin_memcpy(&b, &d, 8);
+      a += b;
+      uint64_t r;
+      __builtin_memcpy(&r, &a, 8);
+      return r;
+    }
+    case OP_MIN: return (int64_t)d < (int64_t)o ? d : o;
+    case OP_MAX: return (int64_t)d > (int64_t)o ? d : o;
+  }
+  return o;
+}
+
+// Resident row → its delta entry: -2 = not in this work item (closed, or another sub-pass),
+// -1 = live but untouched by this push, else the entry index.
+__device__ __forceinline__ int mg_find(const MergeParams& q, const KLDS uint64_t* ids, const uint64_t* row, bool evict,
+                                       int64_t close0, int sbits, int sub, int64_t wbase, int H) {
+  const int64_t key = (int64_t)row[0], ws = (int64_t)row[1];
+  if (evict && ws + q.size <= close0) return -2;
+  const uint64_t hk = key_hash(key);
+  if (!sub_ok(hk, ws, sbits, sub)) return -2;
+  const int64_t widx = q.windowed ? (int64_t)fast_udiv((uint64_t)ws, q.fd) : 0;
+  const uint64_t id = ident_of(hk, widx - wbase, q.log2P);
+  uint32_t e = mg_slot(id, H);
+  for (int probe = 0; probe < H; probe++) {
+    const uint64_t v = ids[e];
+    if (v == id) return (int)e;
+    if (v == EMPTY_ID) return -1;
+    e = e + 1 == (uint32_t)H ? 0u : e + 1;
+  }
+  return -1;
+}
+
+__global__ __launch_bounds__(MG_THREADS) void k_part_merge(
+    MergeParams q, const uint32_t* __restrict__ work, const int64_t* __restrict__ pbase,
+    const uint64_t* __restrict__ srec, int first, uint64_t* __restrict__ buf0, uint64_t* __restrict__ buf1,
+    const uint8_t* __restrict__ sel, const int64_t* __restrict__ cnt, unsigned long long* __restrict__ newcnt,
+    uint8_t* __restrict__ fail, unsigned long long* __restrict__ need, int64_t close0, uint64_t* __restrict__ closed,
+    unsigned long long* __restrict__ closed_n, const int64_t* __restrict__ wr,
+    unsigned long long* __restrict__ hnew, unsigned long long* __restrict__ hclosed) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int lovf;
+  __shared__ int wsum[MG_THREADS / 64];
+  __shared__ unsigned long long lbase;
+  const int H = q.H;
+  KLDS uint64_t* ids = mg_plane<uint64_t>(smem, 0);
+  KLDS uint32_t* rt = mg_plane<uint32_t>(smem, q.rt_off);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int NW = MG_THREADS / 64;
+  uint32_t p;
+  int sbits = 0, sub = 0;
+  if (work) {
+    const uint32_t w = work[blockIdx.x];
+    p = w & 0xFFFFu;
+    sbits = (w >> 16) & 0xF;
+    sub = (int)(w >> 20);
+  } else {
+    p = blockIdx.x;
+  }
+  const int64_t rbase = pbase[p], rn = pbase[p + 1] - rbase;
+  if (rn == 0 && first) return;  // untouched partition: nothing to rewrite
+  const int64_t wbase = wr[0];
+  const bool wide = q.rw > 2;
+  // records of the first chunk in flight before anything else
+  longlong2 rec[MG_AU], ext[MG_AU];
+#pragma unroll
+  for (int u = 0; u < MG_AU; u++) {
+    const int64_t li = threadIdx.x + (int64_t)u * MG_THREADS;
+    const longlong2* r = (const longlong2*)(srec + (uint64_t)(rbase + li) * q.rw);
+    rec[u] = li < rn ? r[0] : make_longlong2(0, -1);
+    ext[u] = (wide && li < rn) ? r[1] : make_longlong2(0, 0);
+  }
+  const uint64_t* src = (sel[p] ? buf1 : buf0) + (uint64_t)p * q.cmax * q.sw;
+  const int64_t nrow = cnt[p];
+  const bool evict = q.windowed && close0 != INT64_MIN;
+  // 0. closed resident rows → closed store (pass 0 only; retries skip them)
+  if (evict && first) {
+    int ne = 0, nh = 0;
+    for (int64_t r = threadIdx.x; r < nrow; r += MG_THREADS) {
+      const uint64_t* row = src + r * q.sw;
+      ne += ((int64_t)row[1] + q.size <= close0) && sub_ok(key_hash((int64_t)row[0]), (int64_t)row[1], sbits, sub);
+    }
+    int incl = ne;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int w = 0; w < NW; w++) {
+      if (w < wave) before += wsum[w];
+      total += wsum[w];
+    }
+    if (threadIdx.x == 0) lbase = total ? atomicAdd(closed_n, (unsigned long long)total) : 0ULL;
+    __syncthreads();
+    uint64_t* dst = closed + (lbase + (uint64_t)(before + incl - ne)) * q.sw;
+    for (int64_t r = threadIdx.x; r < nrow; r += MG_THREADS) {
+      const uint64_t* row = src + r * q.sw;
+      if (!((int64_t)row[1] + q.size <= close0) || !sub_ok(key_hash((int64_t)row[0]), (int64_t)row[1], sbits, sub))
+        continue;
+      for (int w = 0; w < q.sw; w++) dst[w] = row[w];
+      dst += q.sw;
+      nh += having_ok(row, q.having) ? 1 : 0;
+    }
+    if (q.having.active) {
+      nh = (int)wave_sum(nh);
+      if (lane == 0 && nh) atomicAdd(hclosed, (unsigned long long)nh);
+    }
+    __syncthreads();
+  }
+  // LDS init (the prefetched records are still in flight)
+  for (int i = threadIdx.x; i < H; i += MG_THREADS) {
+    ids[i] = EMPTY_ID;
+    rt[i] = 0u;
+  }
+  for (int o = 0; o < q.n_ops; o++) {
+    const UpdOp op = q.ops[o];
+    if (q.plane_w64[o]) {
+      const int64_t v = op.kind == OP_MIN ? INT64_MAX : (op.kind == OP_MAX ? INT64_MIN : 0);
+      KLDS int64_t* pl = mg_plane<int64_t>(smem, q.plane_off[o]);
+      for (int i = threadIdx.x; i < H; i += MG_THREADS) pl[i] = v;
+    } else {
+      KLDS uint32_t* pl = mg_plane<uint32_t>(smem, q.plane_off[o]);
+      for (int i = threadIdx.x; i < H; i += MG_THREADS) pl[i] = 0u;
+    }
+  }
+  if (threadIdx.x == 0) lovf = 0;
+  lds_barrier();
+  // 1. this push's records
+  for (int64_t l0 = threadIdx.x; l0 < rn; l0 += MG_AU * MG_THREADS) {
+    if (*(volatile KLDS int*)&lovf) break;
+    if (l0 != threadIdx.x) {
+#pragma unroll
+      for (int u = 0; u < MG_AU; u++) {
+        const int64_t li = l0 + u * MG_THREADS;
+        const longlong2* r = (const longlong2*)(srec + (uint64_t)(rbase + li) * q.rw);
+        rec[u] = li < rn ? r[0] : make_longlong2(0, -1);
+        ext[u] = (wide && li < rn) ? r[1] : make_longlong2(0, 0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < MG_AU; u++) {
+      const int64_t t = rec[u].y;
+      if (t < 0) continue;  // every window late (or past the end)
+      const uint64_t hk = key_hash(rec[u].x);
+      const int64_t gi = rbase + l0 + u * MG_THREADS;
+      const uint32_t meta = q.meta_word == 2 ? (uint32_t)ext[u].x : 0u;
+      const int64_t jlo = meta & 0xFFFFu;
+      const uint32_t vmask = meta >> 16;
+      const int64_t w3 = ext[u].y;
+      const uint32_t trel = (uint32_t)(t - q.tbase + 1);
+      int64_t widx = 0, wlast = 0;
+      if (q.windowed) {
+        const int64_t lo = t - q.size + q.adv;
+        widx = (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), q.fd) + jlo;
+        wlast = (int64_t)fast_udiv((uint64_t)t, q.fd);
+      }
+      for (; widx <= wlast; widx++) {
+        if (!sub_ok(hk, widx * q.adv, sbits, sub)) continue;
+        const uint64_t id = ident_of(hk, widx - wbase, q.log2P);
+        uint32_t e = mg_slot(id, H);
+        bool got = false;
+        for (int probe = 0; probe < H; probe++) {
+          uint64_t old = EMPTY_ID;
+          __hip_atomic_compare_exchange_strong(&ids[e], &old, id, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (old == EMPTY_ID || old == id) {
+            got = true;
+            break;
+          }
+          e = e + 1 == (uint32_t)H ? 0u : e + 1;
+        }
+        if (!got) {
+          lovf = 1;
+          break;
+        }
+        __hip_atomic_fetch_max(&rt[e], trel, WG_RLX);
+        for (int o = 0; o < q.n_ops; o++) {
+          const UpdOp op = q.ops[o];
+          if (op.kind == OP_INC) {
+            __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, q.plane_off[o])[e], 1u, WG_RLX);
+            continue;
+          }
+          if (!((vmask >> op.col) & 1u)) continue;
+          if (op.kind == OP_INC_VALID) {
+            __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, q.plane_off[o])[e], 1u, WG_RLX);
+            continue;
+          }
+          const int cw = q.col_word[op.col];
+          const int64_t raw = cw == 3 ? w3 : (int64_t)srec[(uint64_t)gi * q.rw + cw];
+          KLDS int64_t* pl = mg_plane<int64_t>(smem, q.plane_off[o]);
+          switch (op.kind) {
+            case OP_ADD_I64: __hip_atomic_fetch_add((KLDS uint64_t*)&pl[e], (uint64_t)raw, WG_RLX); break;
+            case OP_ADD_F64: {
+              double d;
+              __builtin_memcpy(&d, &raw, 8);
+              __hip_atomic_fetch_add((KLDS double*)&pl[e], d, WG_RLX);
+              break;
+            }
+            case OP_MIN:
+            case OP_MAX: {
+              int64_t k = raw;
+              if (q.col_type[op.col] == KHIP_TYPE_DOUBLE) {
+                double d;
+                __builtin_memcpy(&d, &raw, 8);
+                k = f64_order_key(d);
+              }
+              if (op.kind == OP_MIN) __hip_atomic_fetch_min(&pl[e], k, WG_RLX);
+              else __hip_atomic_fetch_max(&pl[e], k, WG_RLX);
+              break;
+            }
+            default: break;
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (lovf) {
+    if (threadIdx.x == 0) fail[p] |= 1;
+    return;
+  }
+  // 2. resident rows: mark the delta entries they absorb; count live rows
+  int n_mine = 0;
+  for (int64_t r0 = 0; r0 < nrow; r0 += MG_THREADS) {
+    const int64_t r = r0 + threadIdx.x;
+    if (r >= nrow) break;
+    const int e = mg_find(q, ids, src + r * q.sw, evict, close0, sbits, sub, wbase, H);
+    if (e >= 0) rt[e] |= RT_MATCHED;  // one resident row per identity: a plain store
+    n_mine += e != -2 ? 1 : 0;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < H; i += MG_THREADS) n_mine += (ids[i] != EMPTY_ID && !(rt[i] & RT_MATCHED)) ? 1 : 0;
+  // 3. per-wave row counts → the partition's region range (one atomic per work item)
+  const int wave_rows = (int)wave_sum(n_mine);
+  if (lane == 0) wsum[wave] = wave_rows;
+  __syncthreads();
+  int wave_before = 0, total = 0;
+  for (int w = 0; w < NW; w++) {
+    if (w < wave) wave_before += wsum[w];
+    total += wsum[w];
+  }
+  if (threadIdx.x == 0) lbase = total ? atomicAdd(&newcnt[p], (unsigned long long)total) : 0ULL;
+  __syncthreads();
+  if ((int64_t)(lbase + total) > q.cmax) {
+    if (threadIdx.x == 0) {
+      fail[p] |= 2;
+      atomicMax(need, (unsigned long long)(lbase + total));
+    }
+    return;
+  }
+  // 4. write: lanes take ranks from ballots so consecutive lanes store consecutive rows; each
+  //    wave owns a contiguous output range
+  uint64_t* dst0 = (sel[p] ? buf0 : buf1) + (uint64_t)p * q.cmax * q.sw;
+  uint64_t cur = lbase + (uint64_t)wave_before;
+  const uint64_t lt = (1ULL << lane) - 1;
+  const int hv = q.having.a.w_val, hc = q.having.a.w_cnt;
+  int nh = 0;
+  for (int64_t r0 = 0; r0 < nrow; r0 += MG_THREADS) {
+    const int64_t r = r0 + threadIdx.x;
+    const uint64_t* row = src + (r < nrow ? r : 0) * q.sw;
+    const int e = r < nrow ? mg_find(q, ids, row, evict, close0, sbits, sub, wbase, H) : -2;
+    const bool live = e != -2;
+    const uint64_t b = __ballot(live);
+    if (live) {
+      uint64_t* dst = dst0 + (cur + __popcll(b & lt)) * q.sw;
+      uint64_t w2 = row[2];
+      if (e >= 0) {
+        const uint32_t rr = rt[e] & ~RT_MATCHED;
+        const int64_t t = rr ? q.tbase + (int64_t)rr - 1 : INT64_MIN;
+        w2 = t > (int64_t)w2 ? (uint64_t)t : w2;
+      }
+      *(longlong2*)dst = make_longlong2((int64_t)row[0], (int64_t)row[1]);
+      for (int w = 2; w < q.sw; w += 2) {
+        const uint64_t a = w == 2 ? w2 : (e >= 0 ? mg_word(q, smem, w, row, e) : row[w]);
+        const uint64_t c = e >= 0 ? mg_word(q, smem, w + 1, row, e) : row[w + 1];
+        *(longlong2*)(dst + w) = make_longlong2((int64_t)a, (int64_t)c);
+      }
+      if (q.having.active)
+        nh += having_ok_words(e >= 0 ? mg_word(q, smem, hv, row, e) : row[hv],
+                              hc < 0 ? 0 : (e >= 0 ? mg_word(q, smem, hc, row, e) : row[hc]), q.having);
+    }
+    cur += __popcll(b);
+  }
+  for (int i0 = wave * 64; i0 < H; i0 += MG_THREADS) {  // delta entries, 64 per wave step
+    const int e = i0 + lane;
+    const uint64_t id = e < H ? ids[e] : EMPTY_ID;
+    const bool isnew = id != EMPTY_ID && !(rt[e] & RT_MATCHED);
+    const uint64_t b = __ballot(isnew);
+    if (isnew) {
+      uint64_t* dst = dst0 + (cur + __popcll(b & lt)) * q.sw;
+      const uint64_t hk = ((uint64_t)p << (64 - q.log2P)) | (id >> q.log2P);
+      const int64_t ws = (((int64_t)(id & ((1ULL << q.log2P) - 1))) + wbase) * (q.windowed ? q.adv : 0);
+      *(longlong2*)dst = make_longlong2(key_of_hash(hk), ws);
+      for (int w = 2; w < q.sw; w += 2) {
+        const uint64_t a = w == 2 ? (uint64_t)(q.tbase + (int64_t)rt[e] - 1) : mg_word(q, smem, w, nullptr, e);
+        *(longlong2*)(dst + w) = make_longlong2((int64_t)a, (int64_t)mg_word(q, smem, w + 1, nullptr, e));
+      }
+      if (q.having.active)
+        nh += having_ok_words(mg_word(q, smem, hv, nullptr, e), hc < 0 ? 0 : mg_word(q, smem, hc, nullptr, e),
+                              q.having);
+    }
+    cur += __popcll(b);
+  }
+  if (q.having.active) {
+    nh = (int)wave_sum(nh);
+    if (lane == 0 && nh) atomicAdd(&hnew[p], (unsigned long long)nh);
+  }
+}
+
 // Window-index range of this push for the packed identity: the batch's windows plus the
 // live resident ones (res = conservative [min, max] window index of resident rows; rows of
 // windows closed before this push are evicted before they are encoded).  wr = [wbase, ok].
@@ -848,7 +1239,7 @@ __global__ __launch_bounds__(1024) void k_part_wrange(const int64_t* __restrict_
                                                       const int64_t* __restrict__ tilemax, int64_t nT, int windowed,
                                                       int64_t size, int64_t adv, FastDiv fd, int64_t close0,
                                                       int log2P, int fresh, int allow, int64_t* __restrict__ res,
-                                                      int64_t* __restrict__ wr) {
+                                                      int64_t* __restrict__ wr /* [wbase, ok, tmin, tmax] */) {
   __shared__ int64_t smin[16], smax[16];
   int64_t mn = INT64_MAX, mx = -1;
   for (int64_t t = threadIdx.x; t < nT; t += 1024) {
@@ -870,6 +1261,8 @@ __global__ __launch_bounds__(1024) void k_part_wrange(const int64_t* __restrict_
     mn = smin[w] < mn ? smin[w] : mn;
     mx = smax[w] > mx ? smax[w] : mx;
   }
+  wr[2] = mn;  // event-time span of the accepted records (INT64_MAX / -1: none)
+  wr[3] = mx;
   int64_t lo = INT64_MAX, hi = INT64_MIN;
   if (mx >= 0) {  // some accepted record
     if (windowed) {
@@ -911,7 +1304,9 @@ __global__ __launch_bounds__(256) void k_part_commit(int P, const int64_t* __res
                                                      uint8_t* __restrict__ sel, int64_t* __restrict__ cnt,
                                                      unsigned long long* __restrict__ newcnt,
                                                      const uint8_t* __restrict__ fail,
-                                                     unsigned long long* __restrict__ out /* [new groups, failed] */) {
+                                                     unsigned long long* __restrict__ out /* [new groups, failed] */,
+                                                     unsigned long long* __restrict__ hcnt,
+                                                     unsigned long long* __restrict__ hnew) {
   const int k = blockIdx.x * 256 + threadIdx.x;
   int64_t added = 0, failed = 0;
   if (plist ? k < nlist : k < P) {
@@ -921,10 +1316,12 @@ __global__ __launch_bounds__(256) void k_part_commit(int P, const int64_t* __res
         added = (int64_t)newcnt[p] - cnt[p];
         cnt[p] = (int64_t)newcnt[p];
         sel[p] ^= 1;
+        if (hcnt) hcnt[p] = hnew[p];
       } else {
         failed = 1;
       }
       newcnt[p] = 0;
+      if (hnew) hnew[p] = 0;
     }
   }
   added = wave_sum(added);
@@ -932,6 +1329,29 @@ __global__ __launch_bounds__(256) void k_part_commit(int P, const int64_t* __res
   if ((threadIdx.x & 63) == 0) {
     if (added) atomicAdd(&out[0], (unsigned long long)added);
     if (failed) atomicAdd(&out[1], (unsigned long long)failed);
+  }
+}
+
+// End-of-push counters in one place (one device-to-host copy per push): out[3 + k] = sum over
+// tiles of the per-tile counters k, out[3 + T_NPART] = closed rows, out[4 + T_NPART] = stream time.
+__global__ __launch_bounds__(256) void k_part_stats(const int64_t* __restrict__ tpart, int64_t nT,
+                                                    const unsigned long long* __restrict__ closed_n,
+                                                    const int64_t* __restrict__ stream_time,
+                                                    unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long acc[T_NPART];
+  if (threadIdx.x < T_NPART) acc[threadIdx.x] = 0;
+  __syncthreads();
+  for (int k = 0; k < T_NPART; k++) {
+    int64_t v = 0;
+    for (int64_t t = threadIdx.x; t < nT; t += 256) v += tpart[t * T_NPART + k];
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&acc[k], (unsigned long long)v);
+  }
+  __syncthreads();
+  if (threadIdx.x < T_NPART) out[3 + threadIdx.x] = acc[threadIdx.x];
+  if (threadIdx.x == 0) {
+    out[3 + T_NPART] = closed_n ? *closed_n : 0ULL;
+    out[4 + T_NPART] = (unsigned long long)*stream_time;
   }
 }
 
@@ -1050,6 +1470,35 @@ khip_status part_init(khip_agg* a, int64_t hint) {
   s.H = H;
   s.H_eff = H * 3 / 4;
   s.lds_bytes = (int)((((size_t)H * 4 + 15) & ~(size_t)15) + (size_t)H * 8 * used);
+  // k_part_merge layout: id u64 | u64 delta planes | rowtime u32 | u32 delta planes, sized so
+  // two workgroups share a CU; partitions are sized for whichever kernel holds fewer groups
+  {
+    int n64 = 0, n32 = 0;
+    for (int o = 0; o < a->ap.n_ops; o++) (a->ap.ops[o].kind == OP_INC || a->ap.ops[o].kind == OP_INC_VALID ? n32 : n64)++;
+    const int mentry = 8 + 8 * n64 + 4 + 4 * n32;
+    const int64_t mbudget = knob("KHIP_MERGE_LDS_KB", 78) * 1024;
+    int mH = (int)std::min<int64_t>(16384, mbudget / mentry) & ~63;
+    s.mH = mH;
+    int off = mH * 8;
+    for (int o = 0; o < a->ap.n_ops; o++)
+      if (!(a->ap.ops[o].kind == OP_INC || a->ap.ops[o].kind == OP_INC_VALID)) {
+        s.plane_off[o] = off;
+        s.plane_w64[o] = 1;
+        off += mH * 8;
+      }
+    s.rt_off = off;
+    off += mH * 4;
+    for (int o = 0; o < a->ap.n_ops; o++)
+      if (a->ap.ops[o].kind == OP_INC || a->ap.ops[o].kind == OP_INC_VALID) {
+        s.plane_off[o] = off;
+        s.plane_w64[o] = 0;
+        off += mH * 4;
+      }
+    s.m_lds = off;
+    for (int w = 0; w < 32; w++) s.word_op[w] = -1;
+    for (int o = 0; o < a->ap.n_ops; o++) s.word_op[a->ap.ops[o].word] = (int8_t)o;
+    if (mH >= 256) s.H_eff = std::min(s.H_eff, mH * 3 / 4);
+  }
   // partitions: at most ~H_eff/2 groups each at the hinted size
   const int64_t groups = std::max<int64_t>(hint, 1024);
   // at least 64 partitions: the packed identity then holds window ranges of up to 63
@@ -1084,7 +1533,15 @@ khip_status part_init(khip_agg* a, int64_t hint) {
   KHIP_TRY(s.newcnt.ensure(s.P * 8));
   KHIP_TRY(s.pbase.ensure((s.P + 1) * 8));
   KHIP_TRY(s.R.ensure((s.P + 1) * 8));
-  KHIP_TRY(s.ctr.ensure(64));
+  KHIP_TRY(s.ctr.ensure(128));
+  KHIP_TRY(s.hcnt.ensure(s.P * 8));
+  KHIP_TRY(s.hnew.ensure(s.P * 8));
+  KHIP_TRY(s.hclosed.ensure(8));
+  KHIP_TRY(s.pinfo.ensure(256));
+  KHIP_TRY_HIP(hipMemsetAsync(s.hcnt.p, 0, s.P * 8, a->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(s.hnew.p, 0, s.P * 8, a->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(s.hclosed.p, 0, 8, a->stream));
+  s.hvalid = true;
   for (int b = 0; b < 2; b++) KHIP_TRY(s.buf[b].ensure((size_t)s.P * s.cmax * a->sw * 8));
   KHIP_TRY_HIP(hipMemsetAsync(s.sel.p, 0, s.P, a->stream));
   KHIP_TRY_HIP(hipMemsetAsync(s.fail.p, 0, s.P, a->stream));
@@ -1095,7 +1552,8 @@ khip_status part_init(khip_agg* a, int64_t hint) {
 
 void part_release(khip_agg* a) {
   PartState& s = a->part;
-  DevBuf* bufs[] = {&s.srecA, &s.hcoarse, &s.scan_tmpB, &s.RB, &s.wr, &s.res, &s.closed, &s.closed_ctr, &s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist,
+  s.pinfo.release();
+  DevBuf* bufs[] = {&s.hcnt, &s.hnew, &s.hclosed, &s.srecA, &s.hcoarse, &s.scan_tmpB, &s.RB, &s.wr, &s.res, &s.closed, &s.closed_ctr, &s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist,
                     &s.tilemax, &s.tilemin,
                     &s.tileprefix, &s.tpart, &s.scan_tmp, &s.srec, &s.work,
                     &s.pbase, &s.R, &s.ctr, &s.counts};
@@ -1106,6 +1564,10 @@ khip_status part_reset(khip_agg* a) {
   PartState& s = a->part;
   s.closed_n = 0;
   s.res_fresh = true;
+  s.hvalid = true;
+  KHIP_TRY_HIP(hipMemsetAsync(s.hcnt.p, 0, s.P * 8, a->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(s.hnew.p, 0, s.P * 8, a->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(s.hclosed.p, 0, 8, a->stream));
   KHIP_TRY_HIP(hipMemsetAsync(s.cnt.p, 0, s.P * 8, a->stream));
   KHIP_TRY_HIP(hipMemsetAsync(s.newcnt.p, 0, s.P * 8, a->stream));
   KHIP_TRY_HIP(hipMemsetAsync(s.fail.p, 0, s.P, a->stream));
@@ -1197,6 +1659,12 @@ static khip_status part_split(khip_agg* a) {
   s.P = P2;
   s.log2P += 1;
   s.cmax = ncmax;
+  // per-partition HAVING counts do not survive the re-layout: the full scan serves HAVING
+  // counts until the next reset
+  KHIP_TRY(s.hcnt.ensure(P2 * 8));
+  KHIP_TRY(s.hnew.ensure(P2 * 8));
+  KHIP_TRY_HIP(hipMemsetAsync(s.hnew.p, 0, P2 * 8, a->stream));
+  s.hvalid = false;
   KHIP_TRY(s.pbase.ensure((s.P + 1) * 8));
   KHIP_TRY(s.R.ensure((s.P + 1) * 8));
   return KHIP_OK;
@@ -1278,6 +1746,18 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                      fbits, lvl2 ? s.hcoarse.as<uint32_t>() : (uint32_t*)nullptr);
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, a->stream, s.tilemax.as<int64_t>(), nT,
                      s.tileprefix.as<int64_t>(), a->stream_time.as<int64_t>());
+  // window range of the push (packed identity) and its event-time span → host: they pick the
+  // aggregate kernel (k_part_merge needs the identity and a span below 2^31 ms)
+  const PartAggParams q0 = part_params(a);
+  const int64_t close0 = (a->windowed && a->host_stream_time >= 0) ? a->host_stream_time - a->grace : INT64_MIN;
+  KHIP_TRY(s.wr.ensure(32));
+  KHIP_TRY(s.res.ensure(16));
+  hipLaunchKernelGGL(k_part_wrange, dim3(1), dim3(1024), 0, a->stream, s.tilemin.as<int64_t>(), s.tilemax.as<int64_t>(),
+                     nT, a->windowed, a->desc.size_ms, q0.adv, q0.fd, close0, s.log2P, s.res_fresh ? 1 : 0,
+                     (a->desc.flags & KHIP_FLAG_PART_CLAIM) ? 0 : 1, s.res.as<int64_t>(), s.wr.as<int64_t>());
+  s.res_fresh = false;
+  int64_t* pin = s.pinfo.as<int64_t>();
+  KHIP_TRY_HIP(hipMemcpyAsync(pin, s.wr.p, 32, hipMemcpyDeviceToHost, a->stream));
   // 2. offsets
   hipLaunchKernelGGL(k_part_colsum, dim3(ceil_div(P, 256), TC), dim3(256), 0, a->stream, s.hist.as<uint32_t>(), nT, P,
                      TC, s.scan_tmp.as<int64_t>());
@@ -1335,14 +1815,40 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   }
   ev_record_part(a, 2);
   // 4. aggregate partitions (+ retries)
-  const PartAggParams q0 = part_params(a);
-  const int64_t close0 = (a->windowed && a->host_stream_time >= 0) ? a->host_stream_time - a->grace : INT64_MIN;
-  KHIP_TRY(s.wr.ensure(16));
-  KHIP_TRY(s.res.ensure(16));
-  hipLaunchKernelGGL(k_part_wrange, dim3(1), dim3(1024), 0, a->stream, s.tilemin.as<int64_t>(), s.tilemax.as<int64_t>(),
-                     nT, a->windowed, a->desc.size_ms, q0.adv, q0.fd, close0, s.log2P, s.res_fresh ? 1 : 0,
-                     (a->desc.flags & KHIP_FLAG_PART_CLAIM) ? 0 : 1, s.res.as<int64_t>(), s.wr.as<int64_t>());
-  s.res_fresh = false;
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));  // pin[] (the kernels above keep the GPU busy meanwhile)
+  const bool idm = pin[1] != 0;
+  const int64_t tmin = pin[2], tmax = pin[3];
+  const bool merge = idm && s.mH >= 256 && (tmax < 0 || tmax - tmin < (1LL << 31) - 2) && knob("KHIP_MERGE", 1) != 0;
+  if (!merge) s.hvalid = false;  // k_part_agg does not maintain the HAVING counts
+  MergeParams mq{};
+  if (merge) {
+    mq.windowed = a->windowed;
+    mq.sw = a->sw;
+    mq.nwords = s.nwords;
+    mq.H = s.mH;
+    mq.rw = s.rw;
+    mq.meta_word = s.meta_word;
+    mq.log2P = s.log2P;
+    mq.n_ops = a->ap.n_ops;
+    mq.size = q0.size;
+    mq.adv = q0.adv;
+    mq.fd = q0.fd;
+    mq.tbase = tmax < 0 ? 0 : tmin;
+    for (int c = 0; c < MAX_COLS; c++) {
+      mq.col_word[c] = s.col_word[c];
+      mq.col_type[c] = a->ap.col_type[c];
+    }
+    for (int o = 0; o < a->ap.n_ops; o++) {
+      mq.ops[o] = a->ap.ops[o];
+      mq.plane_off[o] = s.plane_off[o];
+      mq.plane_w64[o] = s.plane_w64[o];
+    }
+    for (int w = 0; w < 32; w++) mq.word_op[w] = s.word_op[w];
+    mq.rt_off = s.rt_off;
+    mq.lds_bytes = s.m_lds;
+    mq.init = a->init;
+    mq.having = a->having;
+  }
   if (a->windowed) {  // worst case every live row closes in this push
     const int64_t live = a->occ - s.closed_n;
     if (s.closed_cap < s.closed_n + live) {
@@ -1386,25 +1892,42 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
       dbg = dbgbuf.as<unsigned long long>();
     }
     q.cmax = s.cmax;
+    mq.cmax = s.cmax;
     KHIP_TRY_HIP(hipMemsetAsync(s.ctr.p, 0, 24, a->stream));
     const uint32_t* wk = (pass == 0 && !subs0) ? nullptr : s.work.as<uint32_t>();
     const int64_t nwork = (pass == 0 && !subs0) ? P : (int64_t)work.size();
-    hipFuncSetAttribute((const void*)k_part_agg, hipFuncAttributeMaxDynamicSharedMemorySize, s.lds_bytes);
-    hipLaunchKernelGGL(k_part_agg, dim3(nwork), dim3(AG_THREADS), s.lds_bytes, a->stream, q, wk,
-                       s.pbase.as<int64_t>(), s.srec.as<uint64_t>(), pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(),
-                       s.buf[1].as<uint64_t>(), s.sel.as<uint8_t>(), s.cnt.as<int64_t>(),
-                       s.newcnt.as<unsigned long long>(), s.fail.as<uint8_t>(),
-                       s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
-                       s.closed_ctr.as<unsigned long long>(), s.wr.as<int64_t>(), dbg);
+    if (merge) {
+      hipFuncSetAttribute((const void*)k_part_merge, hipFuncAttributeMaxDynamicSharedMemorySize, s.m_lds);
+      hipLaunchKernelGGL(k_part_merge, dim3(nwork), dim3(MG_THREADS), s.m_lds, a->stream, mq, wk, s.pbase.as<int64_t>(),
+                         s.srec.as<uint64_t>(), pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
+                         s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
+                         s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
+                         s.closed_ctr.as<unsigned long long>(), s.wr.as<int64_t>(),
+                         s.hnew.as<unsigned long long>(), s.hclosed.as<unsigned long long>());
+    } else {
+      hipFuncSetAttribute((const void*)k_part_agg, hipFuncAttributeMaxDynamicSharedMemorySize, s.lds_bytes);
+      hipLaunchKernelGGL(k_part_agg, dim3(nwork), dim3(AG_THREADS), s.lds_bytes, a->stream, q, wk,
+                         s.pbase.as<int64_t>(), s.srec.as<uint64_t>(), pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(),
+                         s.buf[1].as<uint64_t>(), s.sel.as<uint8_t>(), s.cnt.as<int64_t>(),
+                         s.newcnt.as<unsigned long long>(), s.fail.as<uint8_t>(),
+                         s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
+                         s.closed_ctr.as<unsigned long long>(), s.wr.as<int64_t>(), dbg);
+    }
     const int nl = pass == 0 ? P : (int)plist.size();
     hipLaunchKernelGGL(k_part_commit, dim3(ceil_div(std::max(nl, 1), 256)), dim3(256), 0, a->stream, P,
                        s.pbase.as<int64_t>(), pass == 0 ? nullptr : s.work.as<uint32_t>() + work.size(), nl,
                        s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
-                       s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>());
+                       s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>(), s.hcnt.as<unsigned long long>(),
+                       s.hnew.as<unsigned long long>());
     KHIP_TRY_HIP(hipGetLastError());
-    if (pass == 0) ev_record_part(a, 3);
-    unsigned long long c2[3];
-    KHIP_TRY_HIP(hipMemcpyAsync(c2, s.ctr.p, 24, hipMemcpyDeviceToHost, a->stream));
+    if (pass == 0) {
+      ev_record_part(a, 3);
+      hipLaunchKernelGGL(k_part_stats, dim3(1), dim3(256), 0, a->stream, s.tpart.as<int64_t>(), nT,
+                         a->windowed ? s.closed_ctr.as<unsigned long long>() : (unsigned long long*)nullptr,
+                         a->stream_time.as<int64_t>(), s.ctr.as<unsigned long long>());
+    }
+    unsigned long long* c2 = s.pinfo.as<unsigned long long>() + 8;
+    KHIP_TRY_HIP(hipMemcpyAsync(c2, s.ctr.p, (pass == 0 ? 5 + T_NPART : 3) * 8, hipMemcpyDeviceToHost, a->stream));
     KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
     added_total += (int64_t)c2[0];
     if (dbg) agg_probe_report(dbgbuf, (int)((pass == 0 && !subs0) ? P : (int64_t)work.size()));
@@ -1434,18 +1957,16 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     KHIP_TRY_HIP(hipMemcpyAsync(s.work.p, both.data(), both.size() * 4, hipMemcpyHostToDevice, a->stream));
   }
   for (int p = 0; p < P; p++) s.psbits[p] = (uint8_t)std::max<int>(s.psbits[p], sbits[p]);
-  // 5. counters
+  // 5. counters (k_part_stats after pass 0: evictions only happen there)
+  const unsigned long long* st = s.pinfo.as<unsigned long long>() + 8;
   if (a->windowed) {
-    int64_t cn = 0;
-    KHIP_TRY_HIP(hipMemcpy(&cn, s.closed_ctr.p, 8, hipMemcpyDeviceToHost));
+    const int64_t cn = (int64_t)st[3 + T_NPART];
     added_total += cn - s.closed_n;  // evicted rows left the live regions but are still groups
     s.closed_n = cn;
   }
-  std::vector<int64_t> tp((size_t)nT * T_NPART);
-  KHIP_TRY_HIP(hipMemcpy(tp.data(), s.tpart.p, tp.size() * 8, hipMemcpyDeviceToHost));
-  int64_t c[T_NPART] = {0};
-  for (int64_t t = 0; t < nT; t++)
-    for (int k = 0; k < T_NPART; k++) c[k] += tp[t * T_NPART + k];
+  a->host_stream_time = (int64_t)st[4 + T_NPART];
+  int64_t c[T_NPART];
+  for (int k = 0; k < T_NPART; k++) c[k] = (int64_t)st[3 + k];
   tot[P_ACCEPTED] += c[T_ACCEPTED];
   tot[P_NULL_KEY] += c[T_NULL_KEY];
   tot[P_NULL_ROW] += c[T_NULL_ROW];
@@ -1454,6 +1975,36 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   tot[P_LATE] += c[T_LATE];
   tot[P_NEW] += added_total;
   return KHIP_OK;
+}
+
+__global__ __launch_bounds__(1024) void k_sum_counts(const unsigned long long* __restrict__ v, int64_t n,
+                                                     const unsigned long long* __restrict__ extra,
+                                                     unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long acc;
+  if (threadIdx.x == 0) acc = 0;
+  __syncthreads();
+  int64_t x = 0;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) x += (int64_t)v[i];
+  x = wave_sum(x);
+  if ((threadIdx.x & 63) == 0 && x) atomicAdd(&acc, (unsigned long long)x);
+  __syncthreads();
+  if (threadIdx.x == 0) *out = acc + *extra;
+}
+
+// The query's HAVING row count from the per-partition counts k_part_merge maintains (no scan of
+// the table).  Returns false when they are not valid (a push took a path that does not keep
+// them): the caller then scans.
+bool part_having_count(khip_agg* a, int64_t* n) {
+  PartState& s = a->part;
+  if (!s.hvalid || !a->having.active) return false;
+  hipLaunchKernelGGL(k_sum_counts, dim3(1), dim3(1024), 0, a->stream, s.hcnt.as<unsigned long long>(), s.P,
+                     s.hclosed.as<unsigned long long>(), s.ctr.as<unsigned long long>() + 15);
+  unsigned long long* h = s.pinfo.as<unsigned long long>() + 24;
+  if (hipMemcpyAsync(h, s.ctr.as<unsigned long long>() + 15, 8, hipMemcpyDeviceToHost, a->stream) != hipSuccess ||
+      hipStreamSynchronize(a->stream) != hipSuccess)
+    return false;
+  *n = (int64_t)*h;
+  return true;
 }
 
 // Rows passing `h` (all partitions) → rows (sw words each), or just the count.

@@ -168,6 +168,29 @@ def test_having_vs_oracle(prod, orc, having, engine):
     h.push(batches[0])
     assert h.count_rows(having) == o["n"]
     h.close()
+    # the query's own HAVING in the descriptor: the count the aggregate kernel maintains
+    h = abi.AggHandle(prod, abi.make_agg_desc(**dict(kw, flags=engine, having=having)))
+    h.push(batches[0])
+    assert h.count_rows(having) == o["n"]
+    h.close()
+
+
+@pytest.mark.parametrize("win", [1, 3, 4])
+def test_maintained_having_count_across_pushes(prod, orc, win, engine):
+    """HAVING counts kept per partition (and for evicted closed windows) across micro-batches
+    with late records and eviction, checked after every push against the oracle's table."""
+    rng = np.random.default_rng(50 + win)
+    having = {"agg": 0, "op": "GT", "value": 3}
+    kw = dict(WINDOWS[win], key_type="INT64", col_types=["INT32", "INT64", "DOUBLE", "DOUBLE"], aggs=ALL_AGGS,
+              capacity_hint=200_000)
+    g = abi.AggHandle(prod, abi.make_agg_desc(**dict(kw, flags=engine, having=having)))
+    o = abi.AggHandle(orc, abi.make_agg_desc(**kw))
+    for b in range(5):
+        batch = _random_batch(rng, 30_000, "INT64", 3000, 120_000, 20_000, t0=b * 100_000)
+        assert g.push(batch) == o.push(batch)
+        assert g.count_rows(having) == o.snapshot(having)["n"]
+    g.close()
+    o.close()
 
 
 def test_empty_and_all_null_batches(prod, orc, engine):
