@@ -884,9 +884,9 @@ struct MergeParams {
   int8_t plane_w64[MAX_OPS];   // 1: u64 plane, 0: u32 plane
   int32_t rt_off;              // byte offset of the rowtime plane
   int32_t lds_bytes;
-  int8_t word_op[32];  // row word → update op (-1: key / ws / rowtime / padding)
   InitWords init;
   HavingDev having;  // the query's HAVING (active = 0: none): rows passing it are counted
+  int32_t dbg;       // tuning build: KHIP_MERGE_DEBUG prints the delta table of touched partitions
 };
 
 __device__ __forceinline__ uint32_t mg_slot(uint64_t id, int H) {
@@ -905,17 +905,35 @@ __device__ __forceinline__ KLDS T* mg_plane(char* smem, int32_t off) {
   return (KLDS T*)((KLDS char*)smem + off);
 }
 
+// Per row word, copied to LDS at kernel start (row words are indexed at run time; the kernel
+// argument struct is only read at compile-time offsets): the word's update op kind (-1: none),
+// its delta plane's byte offset and width, and the initial value of a new group.
+struct MgOp {  // one update op, as the record phase needs it
+  int32_t kind;
+  int32_t col;
+  int32_t off;  // delta plane byte offset
+  int32_t cw;   // record word of the op's column
+  int32_t dbl;  // DOUBLE column (MIN/MAX on the total-order key)
+};
+
+struct MgWord {
+  int32_t kind;
+  int32_t off;
+  int32_t w64;
+  int32_t pad;
+  int64_t init;
+};
+
 // Word w (>= 3) of the merged row: resident row `old` (nullptr: a new group) ⊕ delta entry e.
-__device__ __forceinline__ uint64_t mg_word(const MergeParams& q, char* smem, int w, const uint64_t* old, int e) {
-  const int op_of_w = q.word_op[w];
-  if (op_of_w < 0) return old ? old[w] : (uint64_t)q.init.w[w];
-  const UpdOp op = q.ops[op_of_w];
+__device__ __forceinline__ uint64_t mg_word(const MgWord* tab, char* smem, int w, const uint64_t* old, int e) {
+  const MgWord t = tab[w];
+  if (t.kind < 0) return old ? old[w] : (uint64_t)t.init;
   uint64_t d;
-  if (q.plane_w64[op_of_w]) d = (uint64_t)mg_plane<int64_t>(smem, q.plane_off[op_of_w])[e];
-  else d = (uint64_t)mg_plane<uint32_t>(smem, q.plane_off[op_of_w])[e];
+  if (t.w64) d = (uint64_t)mg_plane<int64_t>(smem, t.off)[e];
+  else d = (uint64_t)mg_plane<uint32_t>(smem, t.off)[e];
   if (!old) return d;
   const uint64_t o = old[w];
-  switch (op.kind) {
+  switch (t.kind) {
     case OP_INC:
     case OP_INC_VALID:
     case OP_ADD_I64: return o + d;
@@ -965,7 +983,32 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
   __shared__ int lovf;
   __shared__ int wsum[MG_THREADS / 64];
   __shared__ unsigned long long lbase;
+  __shared__ MgWord wtab[32];
+  __shared__ MgOp otab[MAX_OPS];
   const int H = q.H;
+  if (threadIdx.x < q.n_ops) {
+    const int o = threadIdx.x;
+    MgOp t;
+    t.kind = q.ops[o].kind;
+    t.col = q.ops[o].col;
+    t.off = q.plane_off[o];
+    t.cw = q.col_word[q.ops[o].col];
+    t.dbl = q.col_type[q.ops[o].col] == KHIP_TYPE_DOUBLE;
+    otab[o] = t;
+  }
+  if (threadIdx.x < 32) {
+    const int w = threadIdx.x;
+    int o = -1;
+    for (int k = 0; k < q.n_ops; k++)
+      if (q.ops[k].word == w) o = k;
+    MgWord t;
+    t.kind = o < 0 ? -1 : q.ops[o].kind;
+    t.off = o < 0 ? 0 : q.plane_off[o];
+    t.w64 = o < 0 ? 0 : q.plane_w64[o];
+    t.pad = 0;
+    t.init = q.init.w[w];
+    wtab[w] = t;
+  }
   KLDS uint64_t* ids = mg_plane<uint64_t>(smem, 0);
   KLDS uint32_t* rt = mg_plane<uint32_t>(smem, q.rt_off);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1033,18 +1076,19 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
     __syncthreads();
   }
   // LDS init (the prefetched records are still in flight)
+  lds_barrier();  // otab / wtab
   for (int i = threadIdx.x; i < H; i += MG_THREADS) {
     ids[i] = EMPTY_ID;
     rt[i] = 0u;
   }
   for (int o = 0; o < q.n_ops; o++) {
-    const UpdOp op = q.ops[o];
-    if (q.plane_w64[o]) {
+    const MgOp op = otab[o];
+    if (op.kind != OP_INC && op.kind != OP_INC_VALID) {
       const int64_t v = op.kind == OP_MIN ? INT64_MAX : (op.kind == OP_MAX ? INT64_MIN : 0);
-      KLDS int64_t* pl = mg_plane<int64_t>(smem, q.plane_off[o]);
+      KLDS int64_t* pl = mg_plane<int64_t>(smem, op.off);
       for (int i = threadIdx.x; i < H; i += MG_THREADS) pl[i] = v;
     } else {
-      KLDS uint32_t* pl = mg_plane<uint32_t>(smem, q.plane_off[o]);
+      KLDS uint32_t* pl = mg_plane<uint32_t>(smem, op.off);
       for (int i = threadIdx.x; i < H; i += MG_THREADS) pl[i] = 0u;
     }
   }
@@ -1100,19 +1144,19 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
         }
         __hip_atomic_fetch_max(&rt[e], trel, WG_RLX);
         for (int o = 0; o < q.n_ops; o++) {
-          const UpdOp op = q.ops[o];
+          const MgOp op = otab[o];
           if (op.kind == OP_INC) {
-            __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, q.plane_off[o])[e], 1u, WG_RLX);
+            __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, op.off)[e], 1u, WG_RLX);
             continue;
           }
           if (!((vmask >> op.col) & 1u)) continue;
           if (op.kind == OP_INC_VALID) {
-            __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, q.plane_off[o])[e], 1u, WG_RLX);
+            __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, op.off)[e], 1u, WG_RLX);
             continue;
           }
-          const int cw = q.col_word[op.col];
+          const int cw = op.cw;
           const int64_t raw = cw == 3 ? w3 : (int64_t)srec[(uint64_t)gi * q.rw + cw];
-          KLDS int64_t* pl = mg_plane<int64_t>(smem, q.plane_off[o]);
+          KLDS int64_t* pl = mg_plane<int64_t>(smem, op.off);
           switch (op.kind) {
             case OP_ADD_I64: __hip_atomic_fetch_add((KLDS uint64_t*)&pl[e], (uint64_t)raw, WG_RLX); break;
             case OP_ADD_F64: {
@@ -1124,7 +1168,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
             case OP_MIN:
             case OP_MAX: {
               int64_t k = raw;
-              if (q.col_type[op.col] == KHIP_TYPE_DOUBLE) {
+              if (op.dbl) {
                 double d;
                 __builtin_memcpy(&d, &raw, 8);
                 k = f64_order_key(d);
@@ -1140,6 +1184,21 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
     }
   }
   __syncthreads();
+#ifdef KHIP_TUNING
+  if (q.dbg && threadIdx.x == 0 && rn > 0) {
+    for (int i = 0; i < H; i++)
+      if (ids[i] != EMPTY_ID) {
+        printf("[merge dbg] p %u e %d id %llx rt %u ops %d:", p, i, (unsigned long long)ids[i], rt[i], q.n_ops);
+        for (int o = 0; o < q.n_ops; o++)
+          printf(" o%d(k%d c%d w%d off%d w64 %d)=%llx", o, q.ops[o].kind, q.ops[o].col, q.ops[o].word, q.plane_off[o],
+                 q.plane_w64[o],
+                 q.plane_w64[o] ? (unsigned long long)mg_plane<int64_t>(smem, q.plane_off[o])[i]
+                                : (unsigned long long)mg_plane<uint32_t>(smem, q.plane_off[o])[i]);
+        printf(" rec0 %llx %llx ext %llx %llx\n", (unsigned long long)rec[0].x, (unsigned long long)rec[0].y,
+               (unsigned long long)ext[0].x, (unsigned long long)ext[0].y);
+      }
+  }
+#endif
   if (lovf) {
     if (threadIdx.x == 0) fail[p] |= 1;
     return;
@@ -1196,13 +1255,13 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
       }
       *(longlong2*)dst = make_longlong2((int64_t)row[0], (int64_t)row[1]);
       for (int w = 2; w < q.sw; w += 2) {
-        const uint64_t a = w == 2 ? w2 : (e >= 0 ? mg_word(q, smem, w, row, e) : row[w]);
-        const uint64_t c = e >= 0 ? mg_word(q, smem, w + 1, row, e) : row[w + 1];
+        const uint64_t a = w == 2 ? w2 : (e >= 0 ? mg_word(wtab, smem, w, row, e) : row[w]);
+        const uint64_t c = e >= 0 ? mg_word(wtab, smem, w + 1, row, e) : row[w + 1];
         *(longlong2*)(dst + w) = make_longlong2((int64_t)a, (int64_t)c);
       }
       if (q.having.active)
-        nh += having_ok_words(e >= 0 ? mg_word(q, smem, hv, row, e) : row[hv],
-                              hc < 0 ? 0 : (e >= 0 ? mg_word(q, smem, hc, row, e) : row[hc]), q.having);
+        nh += having_ok_words(e >= 0 ? mg_word(wtab, smem, hv, row, e) : row[hv],
+                              hc < 0 ? 0 : (e >= 0 ? mg_word(wtab, smem, hc, row, e) : row[hc]), q.having);
     }
     cur += __popcll(b);
   }
@@ -1217,11 +1276,19 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
       const int64_t ws = (((int64_t)(id & ((1ULL << q.log2P) - 1))) + wbase) * (q.windowed ? q.adv : 0);
       *(longlong2*)dst = make_longlong2(key_of_hash(hk), ws);
       for (int w = 2; w < q.sw; w += 2) {
-        const uint64_t a = w == 2 ? (uint64_t)(q.tbase + (int64_t)rt[e] - 1) : mg_word(q, smem, w, nullptr, e);
-        *(longlong2*)(dst + w) = make_longlong2((int64_t)a, (int64_t)mg_word(q, smem, w + 1, nullptr, e));
+        const uint64_t a = w == 2 ? (uint64_t)(q.tbase + (int64_t)rt[e] - 1) : mg_word(wtab, smem, w, nullptr, e);
+        *(longlong2*)(dst + w) = make_longlong2((int64_t)a, (int64_t)mg_word(wtab, smem, w + 1, nullptr, e));
       }
+#ifdef KHIP_TUNING
+      if (q.dbg)
+        printf("[merge out] p %u e %d sw %d wo3 %d wo4 %d mw3 %llx mw4 %llx init3 %lld dst %llx %llx %llx %llx %llx\n", p, e,
+               q.sw, wtab[3].kind, wtab[4].kind, (unsigned long long)mg_word(wtab, smem, 3, nullptr, e),
+               (unsigned long long)mg_word(wtab, smem, 4, nullptr, e), (long long)q.init.w[3],
+               (unsigned long long)dst[0], (unsigned long long)dst[1], (unsigned long long)dst[2],
+               (unsigned long long)dst[3], (unsigned long long)dst[4]);
+#endif
       if (q.having.active)
-        nh += having_ok_words(mg_word(q, smem, hv, nullptr, e), hc < 0 ? 0 : mg_word(q, smem, hc, nullptr, e),
+        nh += having_ok_words(mg_word(wtab, smem, hv, nullptr, e), hc < 0 ? 0 : mg_word(wtab, smem, hc, nullptr, e),
                               q.having);
     }
     cur += __popcll(b);
@@ -1843,11 +1910,11 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
       mq.plane_off[o] = s.plane_off[o];
       mq.plane_w64[o] = s.plane_w64[o];
     }
-    for (int w = 0; w < 32; w++) mq.word_op[w] = s.word_op[w];
     mq.rt_off = s.rt_off;
     mq.lds_bytes = s.m_lds;
     mq.init = a->init;
     mq.having = a->having;
+    mq.dbg = (int32_t)knob("KHIP_MERGE_DEBUG", 0);
   }
   if (a->windowed) {  // worst case every live row closes in this push
     const int64_t live = a->occ - s.closed_n;
