@@ -978,7 +978,10 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
     const uint8_t* __restrict__ sel, const int64_t* __restrict__ cnt, unsigned long long* __restrict__ newcnt,
     uint8_t* __restrict__ fail, unsigned long long* __restrict__ need, int64_t close0, uint64_t* __restrict__ closed,
     unsigned long long* __restrict__ closed_n, const int64_t* __restrict__ wr,
-    unsigned long long* __restrict__ hnew, unsigned long long* __restrict__ hclosed) {
+    unsigned long long* __restrict__ hnew, unsigned long long* __restrict__ hclosed,
+    unsigned long long* __restrict__ dbg) {
+#define MG_T(k) do { if (dbg && threadIdx.x == 0) dbg[blockIdx.x * 6 + (k)] = wall_clock64(); } while (0)
+  MG_T(0);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int lovf;
   __shared__ int wsum[MG_THREADS / 64];
@@ -1094,6 +1097,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
   }
   if (threadIdx.x == 0) lovf = 0;
   lds_barrier();
+  MG_T(1);
   // 1. this push's records
   for (int64_t l0 = threadIdx.x; l0 < rn; l0 += MG_AU * MG_THREADS) {
     if (*(volatile KLDS int*)&lovf) break;
@@ -1184,6 +1188,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
     }
   }
   __syncthreads();
+  MG_T(2);
 #ifdef KHIP_TUNING
   if (q.dbg && threadIdx.x == 0 && rn > 0) {
     for (int i = 0; i < H; i++)
@@ -1232,6 +1237,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
     }
     return;
   }
+  MG_T(3);
   // 4. write: lanes take ranks from ballots so consecutive lanes store consecutive rows; each
   //    wave owns a contiguous output range
   uint64_t* dst0 = (sel[p] ? buf0 : buf1) + (uint64_t)p * q.cmax * q.sw;
@@ -1297,6 +1303,13 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
     nh = (int)wave_sum(nh);
     if (lane == 0 && nh) atomicAdd(&hnew[p], (unsigned long long)nh);
   }
+  MG_T(4);
+  if (dbg) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    MG_T(5);
+  }
+#undef MG_T
 }
 
 // Window-index range of this push for the packed identity: the batch's windows plus the
@@ -1752,7 +1765,8 @@ static void agg_probe_report(DevBuf& b, int nb) {
     for (int k = 0; k < 5; k++) ph[k] += (double)(r[k + 1] - r[k]);
   }
   if (!m) return;
-  fprintf(stderr, "[agg probe] %d/%d wgs, span %.1f us, avg per wg (us): init %.2f resident %.2f records %.2f write %.2f drain %.2f\n",
+  fprintf(stderr, "[agg probe] %d/%d wgs, span %.1f us, avg per wg (us): phases %.2f %.2f %.2f %.2f %.2f "
+          "(k_part_agg: init resident records write drain; k_part_merge: init records mark+reserve write drain)\n",
           m, nb, (hi - lo) / 100.0, ph[0] / m / 100, ph[1] / m / 100, ph[2] / m / 100, ph[3] / m / 100, ph[4] / m / 100);
 }
 
@@ -1970,7 +1984,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                          s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
                          s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
                          s.closed_ctr.as<unsigned long long>(), s.wr.as<int64_t>(),
-                         s.hnew.as<unsigned long long>(), s.hclosed.as<unsigned long long>());
+                         s.hnew.as<unsigned long long>(), s.hclosed.as<unsigned long long>(), dbg);
     } else {
       hipFuncSetAttribute((const void*)k_part_agg, hipFuncAttributeMaxDynamicSharedMemorySize, s.lds_bytes);
       hipLaunchKernelGGL(k_part_agg, dim3(nwork), dim3(AG_THREADS), s.lds_bytes, a->stream, q, wk,
