@@ -96,9 +96,11 @@ __device__ __forceinline__ uint64_t ident_of(uint64_t hk, int64_t widx_rel, int 
   return (hk << log2P) | (uint64_t)widx_rel;
 }
 
-__device__ __forceinline__ uint32_t part_of(int64_t key, int log2P) {
-  return log2P == 0 ? 0u : (uint32_t)(key_hash(key) >> (64 - log2P));
+__device__ __forceinline__ uint32_t part_of_hk(uint64_t hk, int log2P) {
+  return log2P == 0 ? 0u : (uint32_t)(hk >> (64 - log2P));
 }
+
+__device__ __forceinline__ uint32_t part_of(int64_t key, int log2P) { return part_of_hk(key_hash(key), log2P); }
 
 __device__ __forceinline__ uint32_t slot_of(uint64_t hk, int64_t ws, int H) {
   return ((uint32_t)hk + (uint32_t)ws * 0x9E3779B1u) & (uint32_t)(H - 1);
@@ -245,9 +247,10 @@ __global__ __launch_bounds__(256) void k_part_colprefix(uint32_t* __restrict__ h
 __device__ __forceinline__ void scatter_one(int64_t key, int64_t x, int64_t jlo, int64_t i, int log2P, uint32_t* cur,
                                             uint64_t* __restrict__ srec, const RecLayout& L, const ColPtrs& cols,
                                             int n_cols, const ColTypes& ctypes, bool applied) {
-  const uint32_t pos = atomicAdd(&cur[part_of(key, log2P)], 1u);
+  const uint64_t hk = key_hash(key);
+  const uint32_t pos = atomicAdd(&cur[part_of_hk(hk, log2P)], 1u);
   uint64_t* r = srec + (uint64_t)pos * L.rw;
-  *(longlong2*)r = make_longlong2(key, applied ? x : -1);  // one 16-byte store
+  *(longlong2*)r = make_longlong2((int64_t)hk, applied ? x : -1);  // one 16-byte store: key hash, ts
   if (L.rw > 2) {  // then the rest of the record, 16 bytes at a time, contiguous
     uint32_t vm = 0;
     for (int c = 0; c < n_cols; c++)
@@ -321,7 +324,8 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
         } else {
           c_app += ok ? 1 : 0;
         }
-        pos[u] = atomicAdd(&cur[part_of(k[u], log2P)], ok ? 1u : 0u);
+        k[u] = (int64_t)key_hash(k[u]);  // records carry the key hash (key = its inverse)
+        pos[u] = atomicAdd(&cur[part_of_hk((uint64_t)k[u], log2P)], ok ? 1u : 0u);
         if (!ok) pos[u] = 0xFFFFFFFFu;
       }
 #pragma unroll
@@ -453,7 +457,7 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_refine(const uint64_t* __re
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const bool ok = i0 + (int64_t)u * PT_THREADS < hi;
-      const uint32_t f = part_of(r[u][0].x, log2P) & (uint32_t)(F - 1);
+      const uint32_t f = part_of_hk((uint64_t)r[u][0].x, log2P) & (uint32_t)(F - 1);
       pos[u] = atomicAdd(&cur[f], ok ? 1u : 0u);
       if (!ok) pos[u] = 0xFFFFFFFFu;
     }
@@ -689,8 +693,8 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
     for (int u = 0; u < AU; u++) {  // unrolled: rec[]/ext[] stay in registers (no scratch)
       const int64_t t = rec[u].y;
       if (t < 0) continue;  // every window late (or past the end)
-      const int64_t key = rec[u].x;
-      const uint64_t hk = key_hash(key);
+      const uint64_t hk = (uint64_t)rec[u].x;  // the scatter stores the key hash
+      const int64_t key = key_of_hash(hk);
       const int64_t gi = rbase + l0 + u * AG_THREADS;
       const uint32_t meta = q.meta_word == 2 ? (uint32_t)ext[u].x : 0u;
       const int64_t jlo = meta & 0xFFFFu;
@@ -972,6 +976,9 @@ __device__ __forceinline__ int mg_find(const MergeParams& q, const KLDS uint64_t
   return -1;
 }
 
+// CNT1: the query's only update is COUNT(*) (one u32 delta plane at word 3) — the record
+// phase and the write-out skip the generic op machinery (C1, C2).
+template <bool CNT1>
 __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
     MergeParams q, const uint32_t* __restrict__ work, const int64_t* __restrict__ pbase,
     const uint64_t* __restrict__ srec, int first, uint64_t* __restrict__ buf0, uint64_t* __restrict__ buf1,
@@ -1014,6 +1021,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
   }
   KLDS uint64_t* ids = mg_plane<uint64_t>(smem, 0);
   KLDS uint32_t* rt = mg_plane<uint32_t>(smem, q.rt_off);
+  KLDS uint32_t* cnt1 = mg_plane<uint32_t>(smem, q.plane_off[0]);  // CNT1: the COUNT(*) deltas
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr int NW = MG_THREADS / 64;
   uint32_t p;
@@ -1114,7 +1122,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
     for (int u = 0; u < MG_AU; u++) {
       const int64_t t = rec[u].y;
       if (t < 0) continue;  // every window late (or past the end)
-      const uint64_t hk = key_hash(rec[u].x);
+      const uint64_t hk = (uint64_t)rec[u].x;  // the scatter stores the key hash
       const int64_t gi = rbase + l0 + u * MG_THREADS;
       const uint32_t meta = q.meta_word == 2 ? (uint32_t)ext[u].x : 0u;
       const int64_t jlo = meta & 0xFFFFu;
@@ -1123,12 +1131,16 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
       const uint32_t trel = (uint32_t)(t - q.tbase + 1);
       int64_t widx = 0, wlast = 0;
       if (q.windowed) {
-        const int64_t lo = t - q.size + q.adv;
-        widx = (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), q.fd) + jlo;
         wlast = (int64_t)fast_udiv((uint64_t)t, q.fd);
+        if (q.size == q.adv) {
+          widx = wlast + jlo;  // TUMBLING: one window
+        } else {
+          const int64_t lo = t - q.size + q.adv;
+          widx = (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), q.fd) + jlo;
+        }
       }
       for (; widx <= wlast; widx++) {
-        if (!sub_ok(hk, widx * q.adv, sbits, sub)) continue;
+        if (sbits && !sub_ok(hk, widx * q.adv, sbits, sub)) continue;
         const uint64_t id = ident_of(hk, widx - wbase, q.log2P);
         uint32_t e = mg_slot(id, H);
         bool got = false;
@@ -1147,6 +1159,10 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
           break;
         }
         __hip_atomic_fetch_max(&rt[e], trel, WG_RLX);
+        if constexpr (CNT1) {
+          __hip_atomic_fetch_add(&cnt1[e], 1u, WG_RLX);
+          continue;
+        }
         for (int o = 0; o < q.n_ops; o++) {
           const MgOp op = otab[o];
           if (op.kind == OP_INC) {
@@ -1260,6 +1276,11 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
         w2 = t > (int64_t)w2 ? (uint64_t)t : w2;
       }
       *(longlong2*)dst = make_longlong2((int64_t)row[0], (int64_t)row[1]);
+      if constexpr (CNT1) {
+        const uint64_t c = row[3] + (e >= 0 ? (uint64_t)cnt1[e] : 0ULL);
+        *(longlong2*)(dst + 2) = make_longlong2((int64_t)w2, (int64_t)c);
+        if (q.having.active) nh += having_ok_words(c, 0, q.having);
+      } else {
       for (int w = 2; w < q.sw; w += 2) {
         const uint64_t a = w == 2 ? w2 : (e >= 0 ? mg_word(wtab, smem, w, row, e) : row[w]);
         const uint64_t c = e >= 0 ? mg_word(wtab, smem, w + 1, row, e) : row[w + 1];
@@ -1268,6 +1289,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
       if (q.having.active)
         nh += having_ok_words(e >= 0 ? mg_word(wtab, smem, hv, row, e) : row[hv],
                               hc < 0 ? 0 : (e >= 0 ? mg_word(wtab, smem, hc, row, e) : row[hc]), q.having);
+      }
     }
     cur += __popcll(b);
   }
@@ -1281,6 +1303,11 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
       const uint64_t hk = ((uint64_t)p << (64 - q.log2P)) | (id >> q.log2P);
       const int64_t ws = (((int64_t)(id & ((1ULL << q.log2P) - 1))) + wbase) * (q.windowed ? q.adv : 0);
       *(longlong2*)dst = make_longlong2(key_of_hash(hk), ws);
+      if constexpr (CNT1) {
+        const uint32_t c = cnt1[e];
+        *(longlong2*)(dst + 2) = make_longlong2(q.tbase + (int64_t)rt[e] - 1, (int64_t)c);
+        if (q.having.active) nh += having_ok_words(c, 0, q.having);
+      } else {
       for (int w = 2; w < q.sw; w += 2) {
         const uint64_t a = w == 2 ? (uint64_t)(q.tbase + (int64_t)rt[e] - 1) : mg_word(wtab, smem, w, nullptr, e);
         *(longlong2*)(dst + w) = make_longlong2((int64_t)a, (int64_t)mg_word(wtab, smem, w + 1, nullptr, e));
@@ -1296,6 +1323,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
       if (q.having.active)
         nh += having_ok_words(mg_word(wtab, smem, hv, nullptr, e), hc < 0 ? 0 : mg_word(wtab, smem, hc, nullptr, e),
                               q.having);
+      }
     }
     cur += __popcll(b);
   }
@@ -1978,8 +2006,11 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     const uint32_t* wk = (pass == 0 && !subs0) ? nullptr : s.work.as<uint32_t>();
     const int64_t nwork = (pass == 0 && !subs0) ? P : (int64_t)work.size();
     if (merge) {
-      hipFuncSetAttribute((const void*)k_part_merge, hipFuncAttributeMaxDynamicSharedMemorySize, s.m_lds);
-      hipLaunchKernelGGL(k_part_merge, dim3(nwork), dim3(MG_THREADS), s.m_lds, a->stream, mq, wk, s.pbase.as<int64_t>(),
+      // COUNT(*) alone: row = [key, ws, rowtime, count] (sw 4), one u32 delta plane
+      const bool cnt1 = a->ap.n_ops == 1 && a->ap.ops[0].kind == OP_INC && a->ap.ops[0].word == 3 && a->sw == 4;
+      auto mk = cnt1 ? k_part_merge<true> : k_part_merge<false>;
+      hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, s.m_lds);
+      hipLaunchKernelGGL(mk, dim3(nwork), dim3(MG_THREADS), s.m_lds, a->stream, mq, wk, s.pbase.as<int64_t>(),
                          s.srec.as<uint64_t>(), pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
                          s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
                          s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),

@@ -1,22 +1,18 @@
 #!/bin/bash
-# Fast iteration loop on the GPU box: parity tests, then a short bench (optionally with
-# the agg phase probe).  Each GPU step has its own time limit; a crash ends the script.
+# One iteration: fast GPU parity suite, the full-size tests selected by $FULL (pytest -k; empty = skip),
+# then tuning-build variants of the bench ($@, see gpu_variants2.sh).
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
-if [ -z "${SKIP_TESTS:-}" ]; then
-  timeout -k 10 300 python -u -m pytest tests -q -x -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1
-  rc=$?
-  tail -15 gpurun_out/gpu_tests.log
-  [ $rc -eq 0 ] || exit $rc
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+D=gpurun_out/${ITAG:-iter}
+mkdir -p $D
+export PYTHONUNBUFFERED=1
+timeout -k 10 400 python -u -m pytest tests -m "gpu and not slow" -x -q --timeout 120 --timeout-method thread \
+  > $D/gpu_fast.log 2>&1 || { echo "fast gpu tests failed"; tail -40 $D/gpu_fast.log; exit 1; }
+tail -1 $D/gpu_fast.log
+if [ -n "${FULL:-}" ]; then
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_fullsize.py -k "$FULL" -x -v --timeout 600 --timeout-method thread \
+    > $D/gpu_full.log 2>&1 || { echo "fullsize tests failed"; tail -40 $D/gpu_full.log; exit 1; }
+  grep -E "PASSED|FAILED" $D/gpu_full.log
 fi
-timeout -k 10 300 python bench.py ${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline} > gpurun_out/bench.log 2>&1 || { tail -20 gpurun_out/bench.log; exit 4; }
-grep -v "^{" gpurun_out/bench.log | tail -4
-python3 - <<'PY'
-import json
-d = json.loads(open("gpurun_out/bench.log").read().strip().splitlines()[-1])
-r = d["roofline"]
-print("value %.3e rec/s  ms/step %.3f  push %.3f ms  frac %.3f" % (d["value"], d["ms_per_step"], r.get("push_ms", 0), r["frac"]))
-for k, v in r.get("per_kernel", {}).items():
-    print("  %-16s %.3f ms" % (k, v["ms"]))
-PY
+[ $# -gt 0 ] && VTAG=${ITAG:-iter}/var bash scripts/gpu_variants2.sh "$@"
+exit 0
