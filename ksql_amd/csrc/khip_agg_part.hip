@@ -865,7 +865,6 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
 // A partition whose deltas overflow H writes nothing and is retried with 2x sub-passes (it
 // has already moved its closed rows in pass 0; retries skip them).
 constexpr int MG_THREADS = 512;
-constexpr int MG_AU = 8;
 constexpr uint32_t RT_MATCHED = 0x80000000u;
 
 struct MergeParams {
@@ -979,7 +978,7 @@ __device__ __forceinline__ int mg_find(const MergeParams& q, const KLDS uint64_t
 // CNT1: the query's only update is COUNT(*) (one u32 delta plane at word 3) — the record
 // phase and the write-out skip the generic op machinery (C1, C2).
 template <bool CNT1>
-__global__ __launch_bounds__(MG_THREADS) void k_part_merge(
+__global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
     MergeParams q, const uint32_t* __restrict__ work, const int64_t* __restrict__ pbase,
     const uint64_t* __restrict__ srec, int first, uint64_t* __restrict__ buf0, uint64_t* __restrict__ buf1,
     const uint8_t* __restrict__ sel, const int64_t* __restrict__ cnt, unsigned long long* __restrict__ newcnt,
@@ -1037,7 +1036,10 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
   const int64_t rbase = pbase[p], rn = pbase[p + 1] - rbase;
   if (rn == 0 && first) return;  // untouched partition: nothing to rewrite
   const int64_t wbase = wr[0];
-  const bool wide = q.rw > 2;
+  // CNT1 records are (key hash, ts) pairs with one window each; the generic path keeps fewer
+  // records in flight (more registers per record) to stay within 128 VGPRs (2 workgroups/CU)
+  constexpr int MG_AU = CNT1 ? 8 : 4;
+  const bool wide = !CNT1 && q.rw > 2;
   // records of the first chunk in flight before anything else
   longlong2 rec[MG_AU], ext[MG_AU];
 #pragma unroll
@@ -1088,7 +1090,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
   }
   // LDS init (the prefetched records are still in flight)
   lds_barrier();  // otab / wtab
-  for (int i = threadIdx.x; i < H; i += MG_THREADS) {
+  for (int i = threadIdx.x; i < H + 64; i += MG_THREADS) {  // + one dummy entry per lane
     ids[i] = EMPTY_ID;
     rt[i] = 0u;
   }
@@ -1106,7 +1108,12 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
   if (threadIdx.x == 0) lovf = 0;
   lds_barrier();
   MG_T(1);
-  // 1. this push's records
+  // 1. this push's records, AU per thread at a time.  Per window round j (TUMBLING: one) the
+  //    AU identities are computed first and their CASes issued back to back (AU LDS round
+  //    trips in flight, one wait); lanes whose home slot holds another group probe on in a
+  //    separate loop.  Inactive lanes (no record, late, other sub-pass, past the last window)
+  //    CAS their own dummy entry H + lane, so the common path has no branch around an LDS op.
+  const uint32_t dummy = (uint32_t)H + (uint32_t)lane;
   for (int64_t l0 = threadIdx.x; l0 < rn; l0 += MG_AU * MG_THREADS) {
     if (*(volatile KLDS int*)&lovf) break;
     if (l0 != threadIdx.x) {
@@ -1118,71 +1125,152 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
         ext[u] = (wide && li < rn) ? r[1] : make_longlong2(0, 0);
       }
     }
+    if constexpr (CNT1) {
+      // one window per record: w = ts / adv (TUMBLING) or 0 (no window); ts < 0: skip
+      uint64_t id[MG_AU], old[MG_AU];
+      uint32_t e[MG_AU];
+      bool pend[MG_AU];
 #pragma unroll
-    for (int u = 0; u < MG_AU; u++) {
-      const int64_t t = rec[u].y;
-      if (t < 0) continue;  // every window late (or past the end)
-      const uint64_t hk = (uint64_t)rec[u].x;  // the scatter stores the key hash
-      const int64_t gi = rbase + l0 + u * MG_THREADS;
-      const uint32_t meta = q.meta_word == 2 ? (uint32_t)ext[u].x : 0u;
-      const int64_t jlo = meta & 0xFFFFu;
-      const uint32_t vmask = meta >> 16;
-      const int64_t w3 = ext[u].y;
-      const uint32_t trel = (uint32_t)(t - q.tbase + 1);
-      int64_t widx = 0, wlast = 0;
-      if (q.windowed) {
-        wlast = (int64_t)fast_udiv((uint64_t)t, q.fd);
-        if (q.size == q.adv) {
-          widx = wlast + jlo;  // TUMBLING: one window
-        } else {
-          const int64_t lo = t - q.size + q.adv;
-          widx = (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), q.fd) + jlo;
-        }
+      for (int u = 0; u < MG_AU; u++) {
+        const int64_t t = rec[u].y;
+        const uint64_t hk = (uint64_t)rec[u].x;
+        const int64_t widx = q.windowed ? (int64_t)fast_udiv((uint64_t)(t < 0 ? 0 : t), q.fd) : 0;
+        const bool act = t >= 0 && (sbits == 0 || sub_ok(hk, widx * q.adv, sbits, sub));
+        id[u] = act ? ident_of(hk, widx - wbase, q.log2P) : EMPTY_ID;
+        e[u] = act ? mg_slot(id[u], H) : dummy;
       }
-      for (; widx <= wlast; widx++) {
-        if (sbits && !sub_ok(hk, widx * q.adv, sbits, sub)) continue;
-        const uint64_t id = ident_of(hk, widx - wbase, q.log2P);
-        uint32_t e = mg_slot(id, H);
-        bool got = false;
-        for (int probe = 0; probe < H; probe++) {
-          uint64_t old = EMPTY_ID;
-          __hip_atomic_compare_exchange_strong(&ids[e], &old, id, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (old == EMPTY_ID || old == id) {
-            got = true;
-            break;
-          }
-          e = e + 1 == (uint32_t)H ? 0u : e + 1;
-        }
-        if (!got) {
+#pragma unroll
+      for (int u = 0; u < MG_AU; u++) {
+        old[u] = EMPTY_ID;
+        __hip_atomic_compare_exchange_strong(&ids[e[u]], &old[u], id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+#pragma unroll
+      for (int u = 0; u < MG_AU; u++) pend[u] = old[u] != EMPTY_ID && old[u] != id[u];
+      for (int probes = 1;; probes++) {
+        bool anyp = false;
+#pragma unroll
+        for (int u = 0; u < MG_AU; u++) anyp |= pend[u];
+        if (!__ballot(anyp)) break;
+        if (probes >= H) {
           lovf = 1;
           break;
         }
-        __hip_atomic_fetch_max(&rt[e], trel, WG_RLX);
-        if constexpr (CNT1) {
-          __hip_atomic_fetch_add(&cnt1[e], 1u, WG_RLX);
-          continue;
+#pragma unroll
+        for (int u = 0; u < MG_AU; u++) {
+          if (!pend[u]) continue;
+          e[u] = e[u] + 1 == (uint32_t)H ? 0u : e[u] + 1;
+          uint64_t o2 = EMPTY_ID;
+          __hip_atomic_compare_exchange_strong(&ids[e[u]], &o2, id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+          pend[u] = o2 != EMPTY_ID && o2 != id[u];
         }
+      }
+#pragma unroll
+      for (int u = 0; u < MG_AU; u++) {
+        if (id[u] == EMPTY_ID || pend[u]) continue;
+        __hip_atomic_fetch_max(&rt[e[u]], (uint32_t)(rec[u].y - q.tbase + 1), WG_RLX);
+        __hip_atomic_fetch_add(&cnt1[e[u]], 1u, WG_RLX);
+      }
+      continue;
+    }
+    int64_t w0[MG_AU], wn[MG_AU];  // first applied window index, last window index
+    uint32_t trel[MG_AU];
+#pragma unroll
+    for (int u = 0; u < MG_AU; u++) {
+      const int64_t t = rec[u].y;
+      const uint32_t meta = q.meta_word == 2 ? (uint32_t)ext[u].x : 0u;
+      trel[u] = (uint32_t)(t - q.tbase + 1);
+      if (t < 0) {  // every window late (or past the end)
+        w0[u] = 1;
+        wn[u] = 0;
+      } else if (q.windowed) {
+        wn[u] = (int64_t)fast_udiv((uint64_t)t, q.fd);
+        if (q.size == q.adv) {
+          w0[u] = wn[u] + (int64_t)(meta & 0xFFFFu);  // TUMBLING: one window
+        } else {
+          const int64_t lo = t - q.size + q.adv;
+          w0[u] = (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), q.fd) + (int64_t)(meta & 0xFFFFu);
+        }
+      } else {
+        w0[u] = 0;
+        wn[u] = 0;
+      }
+    }
+    for (int64_t j = 0;; j++) {
+      bool any = false;
+      bool act[MG_AU];
+      uint64_t id[MG_AU];
+      uint32_t e[MG_AU];
+#pragma unroll
+      for (int u = 0; u < MG_AU; u++) {
+        const int64_t widx = w0[u] + j;
+        const uint64_t hk = (uint64_t)rec[u].x;  // the scatter stores the key hash
+        const bool has = widx <= wn[u];
+        any |= has;
+        act[u] = has && (sbits == 0 || sub_ok(hk, widx * q.adv, sbits, sub));
+        id[u] = act[u] ? ident_of(hk, widx - wbase, q.log2P) : EMPTY_ID;
+        e[u] = act[u] ? mg_slot(id[u], H) : dummy;
+      }
+      if (!__ballot(any)) break;
+      uint64_t old[MG_AU];
+#pragma unroll
+      for (int u = 0; u < MG_AU; u++) {
+        old[u] = EMPTY_ID;
+        __hip_atomic_compare_exchange_strong(&ids[e[u]], &old[u], id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      // collisions: probe on (linear, wrapping at H) until the group's slot or an empty one
+      bool pend[MG_AU];
+      int probes = 0;
+#pragma unroll
+      for (int u = 0; u < MG_AU; u++) pend[u] = act[u] && old[u] != EMPTY_ID && old[u] != id[u];
+      while (true) {
+        bool anyp = false;
+#pragma unroll
+        for (int u = 0; u < MG_AU; u++) anyp |= pend[u];
+        if (!__ballot(anyp)) break;
+        if (++probes >= H) {
+          lovf = 1;
+#pragma unroll
+          for (int u = 0; u < MG_AU; u++) act[u] = false;
+          break;
+        }
+#pragma unroll
+        for (int u = 0; u < MG_AU; u++) {
+          if (!pend[u]) continue;
+          e[u] = e[u] + 1 == (uint32_t)H ? 0u : e[u] + 1;
+          uint64_t o2 = EMPTY_ID;
+          __hip_atomic_compare_exchange_strong(&ids[e[u]], &o2, id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+          pend[u] = o2 != EMPTY_ID && o2 != id[u];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < MG_AU; u++) {
+        if (!act[u]) continue;
+        __hip_atomic_fetch_max(&rt[e[u]], trel[u], WG_RLX);
+        const uint32_t vmask = q.meta_word == 2 ? ((uint32_t)ext[u].x >> 16) : 0u;
+        const int64_t gi = rbase + l0 + u * MG_THREADS;
         for (int o = 0; o < q.n_ops; o++) {
           const MgOp op = otab[o];
           if (op.kind == OP_INC) {
-            __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, op.off)[e], 1u, WG_RLX);
+            __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, op.off)[e[u]], 1u, WG_RLX);
             continue;
           }
           if (!((vmask >> op.col) & 1u)) continue;
           if (op.kind == OP_INC_VALID) {
-            __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, op.off)[e], 1u, WG_RLX);
+            __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, op.off)[e[u]], 1u, WG_RLX);
             continue;
           }
-          const int cw = op.cw;
-          const int64_t raw = cw == 3 ? w3 : (int64_t)srec[(uint64_t)gi * q.rw + cw];
+          const int64_t raw = op.cw == 3 ? ext[u].y : (int64_t)srec[(uint64_t)gi * q.rw + op.cw];
           KLDS int64_t* pl = mg_plane<int64_t>(smem, op.off);
           switch (op.kind) {
-            case OP_ADD_I64: __hip_atomic_fetch_add((KLDS uint64_t*)&pl[e], (uint64_t)raw, WG_RLX); break;
+            case OP_ADD_I64: __hip_atomic_fetch_add((KLDS uint64_t*)&pl[e[u]], (uint64_t)raw, WG_RLX); break;
             case OP_ADD_F64: {
               double d;
               __builtin_memcpy(&d, &raw, 8);
-              __hip_atomic_fetch_add((KLDS double*)&pl[e], d, WG_RLX);
+              __hip_atomic_fetch_add((KLDS double*)&pl[e[u]], d, WG_RLX);
               break;
             }
             case OP_MIN:
@@ -1193,14 +1281,15 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
                 __builtin_memcpy(&d, &raw, 8);
                 k = f64_order_key(d);
               }
-              if (op.kind == OP_MIN) __hip_atomic_fetch_min(&pl[e], k, WG_RLX);
-              else __hip_atomic_fetch_max(&pl[e], k, WG_RLX);
+              if (op.kind == OP_MIN) __hip_atomic_fetch_min(&pl[e[u]], k, WG_RLX);
+              else __hip_atomic_fetch_max(&pl[e[u]], k, WG_RLX);
               break;
             }
             default: break;
           }
         }
       }
+      if (*(volatile KLDS int*)&lovf) break;
     }
   }
   __syncthreads();
@@ -1585,22 +1674,23 @@ khip_status part_init(khip_agg* a, int64_t hint) {
     for (int o = 0; o < a->ap.n_ops; o++) (a->ap.ops[o].kind == OP_INC || a->ap.ops[o].kind == OP_INC_VALID ? n32 : n64)++;
     const int mentry = 8 + 8 * n64 + 4 + 4 * n32;
     const int64_t mbudget = knob("KHIP_MERGE_LDS_KB", 78) * 1024;
-    int mH = (int)std::min<int64_t>(16384, mbudget / mentry) & ~63;
+    int mH = (int)std::min<int64_t>(16384, mbudget / mentry - 64) & ~63;
     s.mH = mH;
-    int off = mH * 8;
+    const int ms = mH + 64;  // plane stride: H entries + one dummy entry per lane
+    int off = ms * 8;
     for (int o = 0; o < a->ap.n_ops; o++)
       if (!(a->ap.ops[o].kind == OP_INC || a->ap.ops[o].kind == OP_INC_VALID)) {
         s.plane_off[o] = off;
         s.plane_w64[o] = 1;
-        off += mH * 8;
+        off += ms * 8;
       }
     s.rt_off = off;
-    off += mH * 4;
+    off += ms * 4;
     for (int o = 0; o < a->ap.n_ops; o++)
       if (a->ap.ops[o].kind == OP_INC || a->ap.ops[o].kind == OP_INC_VALID) {
         s.plane_off[o] = off;
         s.plane_w64[o] = 0;
-        off += mH * 4;
+        off += ms * 4;
       }
     s.m_lds = off;
     for (int w = 0; w < 32; w++) s.word_op[w] = -1;
@@ -2007,7 +2097,9 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     const int64_t nwork = (pass == 0 && !subs0) ? P : (int64_t)work.size();
     if (merge) {
       // COUNT(*) alone: row = [key, ws, rowtime, count] (sw 4), one u32 delta plane
-      const bool cnt1 = a->ap.n_ops == 1 && a->ap.ops[0].kind == OP_INC && a->ap.ops[0].word == 3 && a->sw == 4;
+      // and (key hash, ts) records with one window each (TUMBLING or no window: no meta word)
+      const bool cnt1 = a->ap.n_ops == 1 && a->ap.ops[0].kind == OP_INC && a->ap.ops[0].word == 3 && a->sw == 4 &&
+                        s.rw == 2 && a->desc.window_kind != KHIP_WINDOW_HOPPING;
       auto mk = cnt1 ? k_part_merge<true> : k_part_merge<false>;
       hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, s.m_lds);
       hipLaunchKernelGGL(mk, dim3(nwork), dim3(MG_THREADS), s.m_lds, a->stream, mq, wk, s.pbase.as<int64_t>(),
