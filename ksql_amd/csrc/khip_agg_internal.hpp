@@ -298,7 +298,7 @@ struct PartState {
   // two-level scatter: pass-A records, per-tile bucket histogram / offsets, bucket scans
   DevBuf srecA, hcoarse, scan_tmpB, RB;
   // k_part_merge (delta-only LDS): entries, LDS bytes, plane layout (khip_agg_part.hip)
-  int mH = 0, m_lds = 0, rt_off = 0;
+  int mH = 0, m_lds = 0, rt_off = 0, n_cu = 256;
   int32_t plane_off[MAX_OPS] = {};
   int8_t plane_w64[MAX_OPS] = {};
   int8_t word_op[32] = {};

@@ -864,7 +864,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
 //      instruction covers consecutive rows; count the rows passing the query's HAVING
 // A partition whose deltas overflow H writes nothing and is retried with 2x sub-passes (it
 // has already moved its closed rows in pass 0; retries skip them).
-constexpr int MG_THREADS = 512;
+constexpr int MG_THREADS = 1024;
 constexpr uint32_t RT_MATCHED = 0x80000000u;
 
 struct MergeParams {
@@ -975,26 +975,92 @@ __device__ __forceinline__ int mg_find(const MergeParams& q, const KLDS uint64_t
   return -1;
 }
 
-// CNT1: the query's only update is COUNT(*) (one u32 delta plane at word 3) — the record
-// phase and the write-out skip the generic op machinery (C1, C2).
+// One chunk of a partition's scattered records: AU per thread, rows l0 + tid + u * MG_THREADS.
+template <int AU>
+__device__ __forceinline__ void mg_load(longlong2 (&rec)[AU], longlong2 (&ext)[AU], const uint64_t* __restrict__ srec,
+                                        int64_t rbase, int64_t rn, int64_t l0, int rw, bool wide) {
+#pragma unroll
+  for (int u = 0; u < AU; u++) {
+    const int64_t li = l0 + threadIdx.x + (int64_t)u * MG_THREADS;
+    const longlong2* r = (const longlong2*)(srec + (uint64_t)(rbase + li) * rw);
+    rec[u] = li < rn ? r[0] : make_longlong2(0, -1);
+    if (wide) ext[u] = li < rn ? r[1] : make_longlong2(0, 0);
+  }
+}
+
+struct MgItem {
+  uint32_t p;
+  int sbits, sub;
+  int64_t rbase, rn;
+};
+
+__device__ __forceinline__ MgItem mg_item(const uint32_t* __restrict__ work, int64_t w,
+                                          const int64_t* __restrict__ pbase) {
+  MgItem it;
+  if (work) {
+    const uint32_t x = work[w];
+    it.p = x & 0xFFFFu;
+    it.sbits = (x >> 16) & 0xF;
+    it.sub = (int)(x >> 20);
+  } else {
+    it.p = (uint32_t)w;
+    it.sbits = 0;
+    it.sub = 0;
+  }
+  it.rbase = pbase[it.p];
+  it.rn = pbase[it.p + 1] - it.rbase;
+  return it;
+}
+
+// Reset delta entry e to its initial state (empty identity, no rowtime, op identities).
+__device__ __forceinline__ void mg_clear(char* smem, KLDS uint64_t* ids, KLDS uint32_t* rt, const MgOp* otab,
+                                         int n_ops, int e) {
+  ids[e] = EMPTY_ID;
+  rt[e] = 0u;
+  for (int o = 0; o < n_ops; o++) {
+    const MgOp op = otab[o];
+    if (op.kind == OP_INC || op.kind == OP_INC_VALID) mg_plane<uint32_t>(smem, op.off)[e] = 0u;
+    else mg_plane<int64_t>(smem, op.off)[e] = op.kind == OP_MIN ? INT64_MAX : (op.kind == OP_MAX ? INT64_MIN : 0);
+  }
+}
+
+// CNT1: the query's only update is COUNT(*) (one u32 delta plane at word 3) and its records are
+// (key hash, ts) pairs with one window each — the record phase and the write-out skip the
+// generic op machinery (C1, C2).
+//
+// Persistent: gridDim.x workgroups (one per CU) walk the work items w = blockIdx.x + k * gridDim.x.
+// The next item's first record chunk is loaded into registers before the current item's
+// resident-merge and write-out, and inside an item chunk c + 1 is loaded before chunk c is
+// applied, so HBM latency overlaps the LDS work; the write-out leaves every delta entry cleared
+// for the next item (no separate table init).
 template <bool CNT1>
-__global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
-    MergeParams q, const uint32_t* __restrict__ work, const int64_t* __restrict__ pbase,
+__global__ __launch_bounds__(MG_THREADS) void k_part_merge(
+    MergeParams q, const uint32_t* __restrict__ work, int64_t nwork, const int64_t* __restrict__ pbase,
     const uint64_t* __restrict__ srec, int first, uint64_t* __restrict__ buf0, uint64_t* __restrict__ buf1,
     const uint8_t* __restrict__ sel, const int64_t* __restrict__ cnt, unsigned long long* __restrict__ newcnt,
     uint8_t* __restrict__ fail, unsigned long long* __restrict__ need, int64_t close0, uint64_t* __restrict__ closed,
     unsigned long long* __restrict__ closed_n, const int64_t* __restrict__ wr,
     unsigned long long* __restrict__ hnew, unsigned long long* __restrict__ hclosed,
     unsigned long long* __restrict__ dbg) {
-#define MG_T(k) do { if (dbg && threadIdx.x == 0) dbg[blockIdx.x * 6 + (k)] = wall_clock64(); } while (0)
-  MG_T(0);
+#define MG_T(k) do { if (dbg && threadIdx.x == 0) atomicAdd(&dbg[(k)], (unsigned long long)(wall_clock64() - t_last)); t_last = wall_clock64(); } while (0)
+  unsigned long long t_last = wall_clock64();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int lovf;
   __shared__ int wsum[MG_THREADS / 64];
   __shared__ unsigned long long lbase;
   __shared__ MgWord wtab[32];
   __shared__ MgOp otab[MAX_OPS];
+  constexpr int AU = CNT1 ? 4 : 2;  // records per thread per chunk (two chunks in registers)
+  constexpr int NW = MG_THREADS / 64;
   const int H = q.H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t dummy = (uint32_t)H + (uint32_t)lane;
+  const bool wide = !CNT1 && q.rw > 2;
+  const int64_t wbase = wr[0];
+  const bool evict = q.windowed && close0 != INT64_MIN;
+  KLDS uint64_t* ids = mg_plane<uint64_t>(smem, 0);
+  KLDS uint32_t* rt = mg_plane<uint32_t>(smem, q.rt_off);
+  KLDS uint32_t* cnt1 = mg_plane<uint32_t>(smem, q.plane_off[0]);  // CNT1: the COUNT(*) deltas
   if (threadIdx.x < q.n_ops) {
     const int o = threadIdx.x;
     MgOp t;
@@ -1018,413 +1084,376 @@ __global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
     t.init = q.init.w[w];
     wtab[w] = t;
   }
-  KLDS uint64_t* ids = mg_plane<uint64_t>(smem, 0);
-  KLDS uint32_t* rt = mg_plane<uint32_t>(smem, q.rt_off);
-  KLDS uint32_t* cnt1 = mg_plane<uint32_t>(smem, q.plane_off[0]);  // CNT1: the COUNT(*) deltas
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  constexpr int NW = MG_THREADS / 64;
-  uint32_t p;
-  int sbits = 0, sub = 0;
-  if (work) {
-    const uint32_t w = work[blockIdx.x];
-    p = w & 0xFFFFu;
-    sbits = (w >> 16) & 0xF;
-    sub = (int)(w >> 20);
-  } else {
-    p = blockIdx.x;
+  int64_t w = blockIdx.x;
+  MgItem it{};
+  longlong2 rec[AU], ext[AU], nrec[AU], next[AU];
+  if (w < nwork) {
+    it = mg_item(work, w, pbase);
+    mg_load<AU>(rec, ext, srec, it.rbase, it.rn, 0, q.rw, wide);
   }
-  const int64_t rbase = pbase[p], rn = pbase[p + 1] - rbase;
-  if (rn == 0 && first) return;  // untouched partition: nothing to rewrite
-  const int64_t wbase = wr[0];
-  // CNT1 records are (key hash, ts) pairs with one window each; the generic path keeps fewer
-  // records in flight (more registers per record) to stay within 128 VGPRs (2 workgroups/CU)
-  constexpr int MG_AU = CNT1 ? 8 : 4;
-  const bool wide = !CNT1 && q.rw > 2;
-  // records of the first chunk in flight before anything else
-  longlong2 rec[MG_AU], ext[MG_AU];
+  if (threadIdx.x == 0) lovf = 0;
+  lds_barrier();  // otab / wtab / lovf
+  for (int i = threadIdx.x; i < H + 64; i += MG_THREADS) mg_clear(smem, ids, rt, otab, q.n_ops, i);
+  lds_barrier();
+  MG_T(0);
+  for (; w < nwork; w += gridDim.x) {
+    const uint32_t p = it.p;
+    const int sbits = it.sbits, sub = it.sub;
+    const int64_t rbase = it.rbase, rn = it.rn;
+    const int64_t wnext = w + gridDim.x;
+    MgItem nit{};
+    if (wnext < nwork) nit = mg_item(work, wnext, pbase);  // its loads are issued now, used later
+    if (rn == 0 && first) {  // untouched partition: nothing to rewrite
+      if (wnext < nwork) mg_load<AU>(rec, ext, srec, nit.rbase, nit.rn, 0, q.rw, wide);
+      it = nit;
+      continue;
+    }
+    const uint64_t* src = (sel[p] ? buf1 : buf0) + (uint64_t)p * q.cmax * q.sw;
+    const int64_t nrow = cnt[p];
+    // 0. closed resident rows → closed store (pass 0 only; retries skip them)
+    if (evict && first) {
+      int ne = 0, nh = 0;
+      for (int64_t r = threadIdx.x; r < nrow; r += MG_THREADS) {
+        const uint64_t* row = src + r * q.sw;
+        ne += ((int64_t)row[1] + q.size <= close0) && sub_ok(key_hash((int64_t)row[0]), (int64_t)row[1], sbits, sub);
+      }
+      int incl = ne;
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+      }
+      if (lane == 63) wsum[wave] = incl;
+      __syncthreads();
+      int before = 0, total = 0;
+      for (int k = 0; k < NW; k++) {
+        if (k < wave) before += wsum[k];
+        total += wsum[k];
+      }
+      if (threadIdx.x == 0) lbase = total ? atomicAdd(closed_n, (unsigned long long)total) : 0ULL;
+      __syncthreads();
+      uint64_t* dst = closed + (lbase + (uint64_t)(before + incl - ne)) * q.sw;
+      for (int64_t r = threadIdx.x; r < nrow; r += MG_THREADS) {
+        const uint64_t* row = src + r * q.sw;
+        if (!((int64_t)row[1] + q.size <= close0) ||
+            !sub_ok(key_hash((int64_t)row[0]), (int64_t)row[1], sbits, sub))
+          continue;
+        for (int k = 0; k < q.sw; k++) dst[k] = row[k];
+        dst += q.sw;
+        nh += having_ok(row, q.having) ? 1 : 0;
+      }
+      if (q.having.active) {
+        nh = (int)wave_sum(nh);
+        if (lane == 0 && nh) atomicAdd(hclosed, (unsigned long long)nh);
+      }
+      __syncthreads();
+    }
+    MG_T(1);
+    // 1. this item's records, chunk by chunk (chunk c + 1 in flight while c is applied)
+    for (int64_t l0 = 0; l0 < rn; l0 += (int64_t)AU * MG_THREADS) {
+      const bool more = l0 + (int64_t)AU * MG_THREADS < rn;
+      if (more) mg_load<AU>(nrec, next, srec, rbase, rn, l0 + (int64_t)AU * MG_THREADS, q.rw, wide);
+      if (*(volatile KLDS int*)&lovf) break;
+      if constexpr (CNT1) {
+        // one window per record: w = ts / adv (TUMBLING) or 0 (no window); ts < 0: skip.  The AU
+        // identities' CASes are issued back to back; collisions probe on afterwards.
+        uint64_t id[AU], old[AU];
+        uint32_t e[AU];
+        bool pend[AU];
 #pragma unroll
-  for (int u = 0; u < MG_AU; u++) {
-    const int64_t li = threadIdx.x + (int64_t)u * MG_THREADS;
-    const longlong2* r = (const longlong2*)(srec + (uint64_t)(rbase + li) * q.rw);
-    rec[u] = li < rn ? r[0] : make_longlong2(0, -1);
-    ext[u] = (wide && li < rn) ? r[1] : make_longlong2(0, 0);
-  }
-  const uint64_t* src = (sel[p] ? buf1 : buf0) + (uint64_t)p * q.cmax * q.sw;
-  const int64_t nrow = cnt[p];
-  const bool evict = q.windowed && close0 != INT64_MIN;
-  // 0. closed resident rows → closed store (pass 0 only; retries skip them)
-  if (evict && first) {
-    int ne = 0, nh = 0;
-    for (int64_t r = threadIdx.x; r < nrow; r += MG_THREADS) {
-      const uint64_t* row = src + r * q.sw;
-      ne += ((int64_t)row[1] + q.size <= close0) && sub_ok(key_hash((int64_t)row[0]), (int64_t)row[1], sbits, sub);
+        for (int u = 0; u < AU; u++) {
+          const int64_t t = rec[u].y;
+          const uint64_t hk = (uint64_t)rec[u].x;
+          const int64_t widx = q.windowed ? (int64_t)fast_udiv((uint64_t)(t < 0 ? 0 : t), q.fd) : 0;
+          const bool act = t >= 0 && (sbits == 0 || sub_ok(hk, widx * q.adv, sbits, sub));
+          id[u] = act ? ident_of(hk, widx - wbase, q.log2P) : EMPTY_ID;
+          e[u] = act ? mg_slot(id[u], H) : dummy;
+        }
+#pragma unroll
+        for (int u = 0; u < AU; u++) {
+          old[u] = EMPTY_ID;
+          __hip_atomic_compare_exchange_strong(&ids[e[u]], &old[u], id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+#pragma unroll
+        for (int u = 0; u < AU; u++) pend[u] = old[u] != EMPTY_ID && old[u] != id[u];
+        for (int probes = 1;; probes++) {
+          bool anyp = false;
+#pragma unroll
+          for (int u = 0; u < AU; u++) anyp |= pend[u];
+          if (!__ballot(anyp)) break;
+          if (probes >= H) {
+            lovf = 1;
+            break;
+          }
+#pragma unroll
+          for (int u = 0; u < AU; u++) {
+            if (!pend[u]) continue;
+            e[u] = e[u] + 1 == (uint32_t)H ? 0u : e[u] + 1;
+            uint64_t o2 = EMPTY_ID;
+            __hip_atomic_compare_exchange_strong(&ids[e[u]], &o2, id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+            pend[u] = o2 != EMPTY_ID && o2 != id[u];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < AU; u++) {
+          if (id[u] == EMPTY_ID || pend[u]) continue;
+          __hip_atomic_fetch_max(&rt[e[u]], (uint32_t)(rec[u].y - q.tbase + 1), WG_RLX);
+          __hip_atomic_fetch_add(&cnt1[e[u]], 1u, WG_RLX);
+        }
+      } else {
+        int64_t w0[AU], wn[AU];  // first applied window index, last window index
+        uint32_t trel[AU];
+#pragma unroll
+        for (int u = 0; u < AU; u++) {
+          const int64_t t = rec[u].y;
+          const uint32_t meta = q.meta_word == 2 ? (uint32_t)ext[u].x : 0u;
+          trel[u] = (uint32_t)(t - q.tbase + 1);
+          if (t < 0) {  // every window late (or past the end)
+            w0[u] = 1;
+            wn[u] = 0;
+          } else if (q.windowed) {
+            wn[u] = (int64_t)fast_udiv((uint64_t)t, q.fd);
+            if (q.size == q.adv) {
+              w0[u] = wn[u] + (int64_t)(meta & 0xFFFFu);  // TUMBLING: one window
+            } else {
+              const int64_t lo = t - q.size + q.adv;
+              w0[u] = (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), q.fd) + (int64_t)(meta & 0xFFFFu);
+            }
+          } else {
+            w0[u] = 0;
+            wn[u] = 0;
+          }
+        }
+        for (int64_t j = 0;; j++) {
+          bool any = false;
+          bool act[AU];
+          uint64_t id[AU];
+          uint32_t e[AU];
+#pragma unroll
+          for (int u = 0; u < AU; u++) {
+            const int64_t widx = w0[u] + j;
+            const uint64_t hk = (uint64_t)rec[u].x;  // the scatter stores the key hash
+            const bool has = widx <= wn[u];
+            any |= has;
+            act[u] = has && (sbits == 0 || sub_ok(hk, widx * q.adv, sbits, sub));
+            id[u] = act[u] ? ident_of(hk, widx - wbase, q.log2P) : EMPTY_ID;
+            e[u] = act[u] ? mg_slot(id[u], H) : dummy;
+          }
+          if (!__ballot(any)) break;
+          uint64_t old[AU];
+#pragma unroll
+          for (int u = 0; u < AU; u++) {
+            old[u] = EMPTY_ID;
+            __hip_atomic_compare_exchange_strong(&ids[e[u]], &old[u], id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          bool pend[AU];
+#pragma unroll
+          for (int u = 0; u < AU; u++) pend[u] = act[u] && old[u] != EMPTY_ID && old[u] != id[u];
+          for (int probes = 1;; probes++) {
+            bool anyp = false;
+#pragma unroll
+            for (int u = 0; u < AU; u++) anyp |= pend[u];
+            if (!__ballot(anyp)) break;
+            if (probes >= H) {
+              lovf = 1;
+#pragma unroll
+              for (int u = 0; u < AU; u++) act[u] = false;
+              break;
+            }
+#pragma unroll
+            for (int u = 0; u < AU; u++) {
+              if (!pend[u]) continue;
+              e[u] = e[u] + 1 == (uint32_t)H ? 0u : e[u] + 1;
+              uint64_t o2 = EMPTY_ID;
+              __hip_atomic_compare_exchange_strong(&ids[e[u]], &o2, id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+              pend[u] = o2 != EMPTY_ID && o2 != id[u];
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < AU; u++) {
+            if (!act[u]) continue;
+            __hip_atomic_fetch_max(&rt[e[u]], trel[u], WG_RLX);
+            const uint32_t vmask = q.meta_word == 2 ? ((uint32_t)ext[u].x >> 16) : 0u;
+            const int64_t gi = rbase + l0 + threadIdx.x + (int64_t)u * MG_THREADS;
+            for (int o = 0; o < q.n_ops; o++) {
+              const MgOp op = otab[o];
+              if (op.kind == OP_INC) {
+                __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, op.off)[e[u]], 1u, WG_RLX);
+                continue;
+              }
+              if (!((vmask >> op.col) & 1u)) continue;
+              if (op.kind == OP_INC_VALID) {
+                __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, op.off)[e[u]], 1u, WG_RLX);
+                continue;
+              }
+              const int64_t raw = op.cw == 3 ? ext[u].y : (int64_t)srec[(uint64_t)gi * q.rw + op.cw];
+              KLDS int64_t* pl = mg_plane<int64_t>(smem, op.off);
+              switch (op.kind) {
+                case OP_ADD_I64: __hip_atomic_fetch_add((KLDS uint64_t*)&pl[e[u]], (uint64_t)raw, WG_RLX); break;
+                case OP_ADD_F64: {
+                  double d;
+                  __builtin_memcpy(&d, &raw, 8);
+                  __hip_atomic_fetch_add((KLDS double*)&pl[e[u]], d, WG_RLX);
+                  break;
+                }
+                case OP_MIN:
+                case OP_MAX: {
+                  int64_t k = raw;
+                  if (op.dbl) {
+                    double d;
+                    __builtin_memcpy(&d, &raw, 8);
+                    k = f64_order_key(d);
+                  }
+                  if (op.kind == OP_MIN) __hip_atomic_fetch_min(&pl[e[u]], k, WG_RLX);
+                  else __hip_atomic_fetch_max(&pl[e[u]], k, WG_RLX);
+                  break;
+                }
+                default: break;
+              }
+            }
+          }
+          if (*(volatile KLDS int*)&lovf) break;
+        }
+      }
+      if (more) {
+#pragma unroll
+        for (int u = 0; u < AU; u++) {
+          rec[u] = nrec[u];
+          if (wide) ext[u] = next[u];
+        }
+      }
     }
-    int incl = ne;
-    for (int off = 1; off < 64; off <<= 1) {
-      const int y = __shfl_up(incl, off, 64);
-      if (lane >= off) incl += y;
-    }
-    if (lane == 63) wsum[wave] = incl;
     __syncthreads();
-    int before = 0, total = 0;
-    for (int w = 0; w < NW; w++) {
-      if (w < wave) before += wsum[w];
-      total += wsum[w];
+    MG_T(2);
+    // the next item's first chunk is in flight from here on
+    if (wnext < nwork) mg_load<AU>(rec, ext, srec, nit.rbase, nit.rn, 0, q.rw, wide);
+    if (lovf) {  // more groups than the table: retried with 2x sub-passes
+      if (threadIdx.x == 0) fail[p] |= 1;
+      for (int i = threadIdx.x; i < H; i += MG_THREADS) mg_clear(smem, ids, rt, otab, q.n_ops, i);
+      __syncthreads();
+      if (threadIdx.x == 0) lovf = 0;
+      __syncthreads();
+      it = nit;
+      continue;
     }
-    if (threadIdx.x == 0) lbase = total ? atomicAdd(closed_n, (unsigned long long)total) : 0ULL;
+    // 2. resident rows: mark the delta entries they absorb; count live rows
+    int n_mine = 0;
+    for (int64_t r0 = 0; r0 < nrow; r0 += MG_THREADS) {
+      const int64_t r = r0 + threadIdx.x;
+      if (r >= nrow) break;
+      const int e = mg_find(q, ids, src + r * q.sw, evict, close0, sbits, sub, wbase, H);
+      if (e >= 0) rt[e] |= RT_MATCHED;  // one resident row per identity: a plain store
+      n_mine += e != -2 ? 1 : 0;
+    }
     __syncthreads();
-    uint64_t* dst = closed + (lbase + (uint64_t)(before + incl - ne)) * q.sw;
-    for (int64_t r = threadIdx.x; r < nrow; r += MG_THREADS) {
-      const uint64_t* row = src + r * q.sw;
-      if (!((int64_t)row[1] + q.size <= close0) || !sub_ok(key_hash((int64_t)row[0]), (int64_t)row[1], sbits, sub))
-        continue;
-      for (int w = 0; w < q.sw; w++) dst[w] = row[w];
-      dst += q.sw;
-      nh += having_ok(row, q.having) ? 1 : 0;
+    for (int i = threadIdx.x; i < H; i += MG_THREADS) n_mine += (ids[i] != EMPTY_ID && !(rt[i] & RT_MATCHED)) ? 1 : 0;
+    // 3. per-wave row counts → the partition's region range (one atomic per work item)
+    const int wave_rows = (int)wave_sum(n_mine);
+    if (lane == 0) wsum[wave] = wave_rows;
+    __syncthreads();
+    int wave_before = 0, total = 0;
+    for (int k = 0; k < NW; k++) {
+      if (k < wave) wave_before += wsum[k];
+      total += wsum[k];
+    }
+    if (threadIdx.x == 0) lbase = total ? atomicAdd(&newcnt[p], (unsigned long long)total) : 0ULL;
+    __syncthreads();
+    MG_T(3);
+    if ((int64_t)(lbase + total) > q.cmax) {
+      if (threadIdx.x == 0) {
+        fail[p] |= 2;
+        atomicMax(need, (unsigned long long)(lbase + total));
+      }
+      for (int i = threadIdx.x; i < H; i += MG_THREADS) mg_clear(smem, ids, rt, otab, q.n_ops, i);
+      __syncthreads();
+      it = nit;
+      continue;
+    }
+    // 4. write: lanes take ranks from ballots so consecutive lanes store consecutive rows; each
+    //    wave owns a contiguous output range.  Delta entries are cleared once consumed.
+    uint64_t* dst0 = (sel[p] ? buf0 : buf1) + (uint64_t)p * q.cmax * q.sw;
+    uint64_t cur = lbase + (uint64_t)wave_before;
+    const uint64_t lt = (1ULL << lane) - 1;
+    const int hv = q.having.a.w_val, hc = q.having.a.w_cnt;
+    int nh = 0;
+    for (int64_t r0 = 0; r0 < nrow; r0 += MG_THREADS) {
+      const int64_t r = r0 + threadIdx.x;
+      const uint64_t* row = src + (r < nrow ? r : 0) * q.sw;
+      const int e = r < nrow ? mg_find(q, ids, row, evict, close0, sbits, sub, wbase, H) : -2;
+      const bool live = e != -2;
+      const uint64_t b = __ballot(live);
+      if (live) {
+        uint64_t* dst = dst0 + (cur + __popcll(b & lt)) * q.sw;
+        uint64_t w2 = row[2];
+        if (e >= 0) {
+          const uint32_t rr = rt[e] & ~RT_MATCHED;
+          const int64_t t = rr ? q.tbase + (int64_t)rr - 1 : INT64_MIN;
+          w2 = t > (int64_t)w2 ? (uint64_t)t : w2;
+        }
+        *(longlong2*)dst = make_longlong2((int64_t)row[0], (int64_t)row[1]);
+        if constexpr (CNT1) {
+          const uint64_t c = row[3] + (e >= 0 ? (uint64_t)cnt1[e] : 0ULL);
+          *(longlong2*)(dst + 2) = make_longlong2((int64_t)w2, (int64_t)c);
+          if (q.having.active) nh += having_ok_words(c, 0, q.having);
+        } else {
+          for (int k = 2; k < q.sw; k += 2) {
+            const uint64_t a = k == 2 ? w2 : (e >= 0 ? mg_word(wtab, smem, k, row, e) : row[k]);
+            const uint64_t c = e >= 0 ? mg_word(wtab, smem, k + 1, row, e) : row[k + 1];
+            *(longlong2*)(dst + k) = make_longlong2((int64_t)a, (int64_t)c);
+          }
+          if (q.having.active)
+            nh += having_ok_words(e >= 0 ? mg_word(wtab, smem, hv, row, e) : row[hv],
+                                  hc < 0 ? 0 : (e >= 0 ? mg_word(wtab, smem, hc, row, e) : row[hc]), q.having);
+        }
+      }
+      cur += __popcll(b);
+    }
+    __syncthreads();  // resident rows have read their entries: the loop below clears them all
+    for (int i0 = wave * 64; i0 < H; i0 += MG_THREADS) {  // delta entries, 64 per wave step
+      const int e = i0 + lane;
+      const uint64_t id = e < H ? ids[e] : EMPTY_ID;
+      const bool isnew = id != EMPTY_ID && !(rt[e] & RT_MATCHED);
+      const uint64_t b = __ballot(isnew);
+      if (isnew) {
+        uint64_t* dst = dst0 + (cur + __popcll(b & lt)) * q.sw;
+        const uint64_t hk = ((uint64_t)p << (64 - q.log2P)) | (id >> q.log2P);
+        const int64_t ws = (((int64_t)(id & ((1ULL << q.log2P) - 1))) + wbase) * (q.windowed ? q.adv : 0);
+        *(longlong2*)dst = make_longlong2(key_of_hash(hk), ws);
+        if constexpr (CNT1) {
+          const uint32_t c = cnt1[e];
+          *(longlong2*)(dst + 2) = make_longlong2(q.tbase + (int64_t)rt[e] - 1, (int64_t)c);
+          if (q.having.active) nh += having_ok_words(c, 0, q.having);
+        } else {
+          for (int k = 2; k < q.sw; k += 2) {
+            const uint64_t a = k == 2 ? (uint64_t)(q.tbase + (int64_t)rt[e] - 1) : mg_word(wtab, smem, k, nullptr, e);
+            *(longlong2*)(dst + k) = make_longlong2((int64_t)a, (int64_t)mg_word(wtab, smem, k + 1, nullptr, e));
+          }
+          if (q.having.active)
+            nh += having_ok_words(mg_word(wtab, smem, hv, nullptr, e), hc < 0 ? 0 : mg_word(wtab, smem, hc, nullptr, e),
+                                  q.having);
+        }
+      }
+      if (id != EMPTY_ID) {
+        if constexpr (CNT1) {
+          ids[e] = EMPTY_ID;
+          rt[e] = 0u;
+          cnt1[e] = 0u;
+        } else {
+          mg_clear(smem, ids, rt, otab, q.n_ops, e);
+        }
+      }
+      cur += __popcll(b);
     }
     if (q.having.active) {
       nh = (int)wave_sum(nh);
-      if (lane == 0 && nh) atomicAdd(hclosed, (unsigned long long)nh);
+      if (lane == 0 && nh) atomicAdd(&hnew[p], (unsigned long long)nh);
     }
-    __syncthreads();
-  }
-  // LDS init (the prefetched records are still in flight)
-  lds_barrier();  // otab / wtab
-  for (int i = threadIdx.x; i < H + 64; i += MG_THREADS) {  // + one dummy entry per lane
-    ids[i] = EMPTY_ID;
-    rt[i] = 0u;
-  }
-  for (int o = 0; o < q.n_ops; o++) {
-    const MgOp op = otab[o];
-    if (op.kind != OP_INC && op.kind != OP_INC_VALID) {
-      const int64_t v = op.kind == OP_MIN ? INT64_MAX : (op.kind == OP_MAX ? INT64_MIN : 0);
-      KLDS int64_t* pl = mg_plane<int64_t>(smem, op.off);
-      for (int i = threadIdx.x; i < H; i += MG_THREADS) pl[i] = v;
-    } else {
-      KLDS uint32_t* pl = mg_plane<uint32_t>(smem, op.off);
-      for (int i = threadIdx.x; i < H; i += MG_THREADS) pl[i] = 0u;
-    }
-  }
-  if (threadIdx.x == 0) lovf = 0;
-  lds_barrier();
-  MG_T(1);
-  // 1. this push's records, AU per thread at a time.  Per window round j (TUMBLING: one) the
-  //    AU identities are computed first and their CASes issued back to back (AU LDS round
-  //    trips in flight, one wait); lanes whose home slot holds another group probe on in a
-  //    separate loop.  Inactive lanes (no record, late, other sub-pass, past the last window)
-  //    CAS their own dummy entry H + lane, so the common path has no branch around an LDS op.
-  const uint32_t dummy = (uint32_t)H + (uint32_t)lane;
-  for (int64_t l0 = threadIdx.x; l0 < rn; l0 += MG_AU * MG_THREADS) {
-    if (*(volatile KLDS int*)&lovf) break;
-    if (l0 != threadIdx.x) {
-#pragma unroll
-      for (int u = 0; u < MG_AU; u++) {
-        const int64_t li = l0 + u * MG_THREADS;
-        const longlong2* r = (const longlong2*)(srec + (uint64_t)(rbase + li) * q.rw);
-        rec[u] = li < rn ? r[0] : make_longlong2(0, -1);
-        ext[u] = (wide && li < rn) ? r[1] : make_longlong2(0, 0);
-      }
-    }
-    if constexpr (CNT1) {
-      // one window per record: w = ts / adv (TUMBLING) or 0 (no window); ts < 0: skip
-      uint64_t id[MG_AU], old[MG_AU];
-      uint32_t e[MG_AU];
-      bool pend[MG_AU];
-#pragma unroll
-      for (int u = 0; u < MG_AU; u++) {
-        const int64_t t = rec[u].y;
-        const uint64_t hk = (uint64_t)rec[u].x;
-        const int64_t widx = q.windowed ? (int64_t)fast_udiv((uint64_t)(t < 0 ? 0 : t), q.fd) : 0;
-        const bool act = t >= 0 && (sbits == 0 || sub_ok(hk, widx * q.adv, sbits, sub));
-        id[u] = act ? ident_of(hk, widx - wbase, q.log2P) : EMPTY_ID;
-        e[u] = act ? mg_slot(id[u], H) : dummy;
-      }
-#pragma unroll
-      for (int u = 0; u < MG_AU; u++) {
-        old[u] = EMPTY_ID;
-        __hip_atomic_compare_exchange_strong(&ids[e[u]], &old[u], id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-#pragma unroll
-      for (int u = 0; u < MG_AU; u++) pend[u] = old[u] != EMPTY_ID && old[u] != id[u];
-      for (int probes = 1;; probes++) {
-        bool anyp = false;
-#pragma unroll
-        for (int u = 0; u < MG_AU; u++) anyp |= pend[u];
-        if (!__ballot(anyp)) break;
-        if (probes >= H) {
-          lovf = 1;
-          break;
-        }
-#pragma unroll
-        for (int u = 0; u < MG_AU; u++) {
-          if (!pend[u]) continue;
-          e[u] = e[u] + 1 == (uint32_t)H ? 0u : e[u] + 1;
-          uint64_t o2 = EMPTY_ID;
-          __hip_atomic_compare_exchange_strong(&ids[e[u]], &o2, id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-          pend[u] = o2 != EMPTY_ID && o2 != id[u];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < MG_AU; u++) {
-        if (id[u] == EMPTY_ID || pend[u]) continue;
-        __hip_atomic_fetch_max(&rt[e[u]], (uint32_t)(rec[u].y - q.tbase + 1), WG_RLX);
-        __hip_atomic_fetch_add(&cnt1[e[u]], 1u, WG_RLX);
-      }
-      continue;
-    }
-    int64_t w0[MG_AU], wn[MG_AU];  // first applied window index, last window index
-    uint32_t trel[MG_AU];
-#pragma unroll
-    for (int u = 0; u < MG_AU; u++) {
-      const int64_t t = rec[u].y;
-      const uint32_t meta = q.meta_word == 2 ? (uint32_t)ext[u].x : 0u;
-      trel[u] = (uint32_t)(t - q.tbase + 1);
-      if (t < 0) {  // every window late (or past the end)
-        w0[u] = 1;
-        wn[u] = 0;
-      } else if (q.windowed) {
-        wn[u] = (int64_t)fast_udiv((uint64_t)t, q.fd);
-        if (q.size == q.adv) {
-          w0[u] = wn[u] + (int64_t)(meta & 0xFFFFu);  // TUMBLING: one window
-        } else {
-          const int64_t lo = t - q.size + q.adv;
-          w0[u] = (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), q.fd) + (int64_t)(meta & 0xFFFFu);
-        }
-      } else {
-        w0[u] = 0;
-        wn[u] = 0;
-      }
-    }
-    for (int64_t j = 0;; j++) {
-      bool any = false;
-      bool act[MG_AU];
-      uint64_t id[MG_AU];
-      uint32_t e[MG_AU];
-#pragma unroll
-      for (int u = 0; u < MG_AU; u++) {
-        const int64_t widx = w0[u] + j;
-        const uint64_t hk = (uint64_t)rec[u].x;  // the scatter stores the key hash
-        const bool has = widx <= wn[u];
-        any |= has;
-        act[u] = has && (sbits == 0 || sub_ok(hk, widx * q.adv, sbits, sub));
-        id[u] = act[u] ? ident_of(hk, widx - wbase, q.log2P) : EMPTY_ID;
-        e[u] = act[u] ? mg_slot(id[u], H) : dummy;
-      }
-      if (!__ballot(any)) break;
-      uint64_t old[MG_AU];
-#pragma unroll
-      for (int u = 0; u < MG_AU; u++) {
-        old[u] = EMPTY_ID;
-        __hip_atomic_compare_exchange_strong(&ids[e[u]], &old[u], id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      // collisions: probe on (linear, wrapping at H) until the group's slot or an empty one
-      bool pend[MG_AU];
-      int probes = 0;
-#pragma unroll
-      for (int u = 0; u < MG_AU; u++) pend[u] = act[u] && old[u] != EMPTY_ID && old[u] != id[u];
-      while (true) {
-        bool anyp = false;
-#pragma unroll
-        for (int u = 0; u < MG_AU; u++) anyp |= pend[u];
-        if (!__ballot(anyp)) break;
-        if (++probes >= H) {
-          lovf = 1;
-#pragma unroll
-          for (int u = 0; u < MG_AU; u++) act[u] = false;
-          break;
-        }
-#pragma unroll
-        for (int u = 0; u < MG_AU; u++) {
-          if (!pend[u]) continue;
-          e[u] = e[u] + 1 == (uint32_t)H ? 0u : e[u] + 1;
-          uint64_t o2 = EMPTY_ID;
-          __hip_atomic_compare_exchange_strong(&ids[e[u]], &o2, id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-          pend[u] = o2 != EMPTY_ID && o2 != id[u];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < MG_AU; u++) {
-        if (!act[u]) continue;
-        __hip_atomic_fetch_max(&rt[e[u]], trel[u], WG_RLX);
-        const uint32_t vmask = q.meta_word == 2 ? ((uint32_t)ext[u].x >> 16) : 0u;
-        const int64_t gi = rbase + l0 + u * MG_THREADS;
-        for (int o = 0; o < q.n_ops; o++) {
-          const MgOp op = otab[o];
-          if (op.kind == OP_INC) {
-            __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, op.off)[e[u]], 1u, WG_RLX);
-            continue;
-          }
-          if (!((vmask >> op.col) & 1u)) continue;
-          if (op.kind == OP_INC_VALID) {
-            __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, op.off)[e[u]], 1u, WG_RLX);
-            continue;
-          }
-          const int64_t raw = op.cw == 3 ? ext[u].y : (int64_t)srec[(uint64_t)gi * q.rw + op.cw];
-          KLDS int64_t* pl = mg_plane<int64_t>(smem, op.off);
-          switch (op.kind) {
-            case OP_ADD_I64: __hip_atomic_fetch_add((KLDS uint64_t*)&pl[e[u]], (uint64_t)raw, WG_RLX); break;
-            case OP_ADD_F64: {
-              double d;
-              __builtin_memcpy(&d, &raw, 8);
-              __hip_atomic_fetch_add((KLDS double*)&pl[e[u]], d, WG_RLX);
-              break;
-            }
-            case OP_MIN:
-            case OP_MAX: {
-              int64_t k = raw;
-              if (op.dbl) {
-                double d;
-                __builtin_memcpy(&d, &raw, 8);
-                k = f64_order_key(d);
-              }
-              if (op.kind == OP_MIN) __hip_atomic_fetch_min(&pl[e[u]], k, WG_RLX);
-              else __hip_atomic_fetch_max(&pl[e[u]], k, WG_RLX);
-              break;
-            }
-            default: break;
-          }
-        }
-      }
-      if (*(volatile KLDS int*)&lovf) break;
-    }
-  }
-  __syncthreads();
-  MG_T(2);
-#ifdef KHIP_TUNING
-  if (q.dbg && threadIdx.x == 0 && rn > 0) {
-    for (int i = 0; i < H; i++)
-      if (ids[i] != EMPTY_ID) {
-        printf("[merge dbg] p %u e %d id %llx rt %u ops %d:", p, i, (unsigned long long)ids[i], rt[i], q.n_ops);
-        for (int o = 0; o < q.n_ops; o++)
-          printf(" o%d(k%d c%d w%d off%d w64 %d)=%llx", o, q.ops[o].kind, q.ops[o].col, q.ops[o].word, q.plane_off[o],
-                 q.plane_w64[o],
-                 q.plane_w64[o] ? (unsigned long long)mg_plane<int64_t>(smem, q.plane_off[o])[i]
-                                : (unsigned long long)mg_plane<uint32_t>(smem, q.plane_off[o])[i]);
-        printf(" rec0 %llx %llx ext %llx %llx\n", (unsigned long long)rec[0].x, (unsigned long long)rec[0].y,
-               (unsigned long long)ext[0].x, (unsigned long long)ext[0].y);
-      }
-  }
-#endif
-  if (lovf) {
-    if (threadIdx.x == 0) fail[p] |= 1;
-    return;
-  }
-  // 2. resident rows: mark the delta entries they absorb; count live rows
-  int n_mine = 0;
-  for (int64_t r0 = 0; r0 < nrow; r0 += MG_THREADS) {
-    const int64_t r = r0 + threadIdx.x;
-    if (r >= nrow) break;
-    const int e = mg_find(q, ids, src + r * q.sw, evict, close0, sbits, sub, wbase, H);
-    if (e >= 0) rt[e] |= RT_MATCHED;  // one resident row per identity: a plain store
-    n_mine += e != -2 ? 1 : 0;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < H; i += MG_THREADS) n_mine += (ids[i] != EMPTY_ID && !(rt[i] & RT_MATCHED)) ? 1 : 0;
-  // 3. per-wave row counts → the partition's region range (one atomic per work item)
-  const int wave_rows = (int)wave_sum(n_mine);
-  if (lane == 0) wsum[wave] = wave_rows;
-  __syncthreads();
-  int wave_before = 0, total = 0;
-  for (int w = 0; w < NW; w++) {
-    if (w < wave) wave_before += wsum[w];
-    total += wsum[w];
-  }
-  if (threadIdx.x == 0) lbase = total ? atomicAdd(&newcnt[p], (unsigned long long)total) : 0ULL;
-  __syncthreads();
-  if ((int64_t)(lbase + total) > q.cmax) {
-    if (threadIdx.x == 0) {
-      fail[p] |= 2;
-      atomicMax(need, (unsigned long long)(lbase + total));
-    }
-    return;
-  }
-  MG_T(3);
-  // 4. write: lanes take ranks from ballots so consecutive lanes store consecutive rows; each
-  //    wave owns a contiguous output range
-  uint64_t* dst0 = (sel[p] ? buf0 : buf1) + (uint64_t)p * q.cmax * q.sw;
-  uint64_t cur = lbase + (uint64_t)wave_before;
-  const uint64_t lt = (1ULL << lane) - 1;
-  const int hv = q.having.a.w_val, hc = q.having.a.w_cnt;
-  int nh = 0;
-  for (int64_t r0 = 0; r0 < nrow; r0 += MG_THREADS) {
-    const int64_t r = r0 + threadIdx.x;
-    const uint64_t* row = src + (r < nrow ? r : 0) * q.sw;
-    const int e = r < nrow ? mg_find(q, ids, row, evict, close0, sbits, sub, wbase, H) : -2;
-    const bool live = e != -2;
-    const uint64_t b = __ballot(live);
-    if (live) {
-      uint64_t* dst = dst0 + (cur + __popcll(b & lt)) * q.sw;
-      uint64_t w2 = row[2];
-      if (e >= 0) {
-        const uint32_t rr = rt[e] & ~RT_MATCHED;
-        const int64_t t = rr ? q.tbase + (int64_t)rr - 1 : INT64_MIN;
-        w2 = t > (int64_t)w2 ? (uint64_t)t : w2;
-      }
-      *(longlong2*)dst = make_longlong2((int64_t)row[0], (int64_t)row[1]);
-      if constexpr (CNT1) {
-        const uint64_t c = row[3] + (e >= 0 ? (uint64_t)cnt1[e] : 0ULL);
-        *(longlong2*)(dst + 2) = make_longlong2((int64_t)w2, (int64_t)c);
-        if (q.having.active) nh += having_ok_words(c, 0, q.having);
-      } else {
-      for (int w = 2; w < q.sw; w += 2) {
-        const uint64_t a = w == 2 ? w2 : (e >= 0 ? mg_word(wtab, smem, w, row, e) : row[w]);
-        const uint64_t c = e >= 0 ? mg_word(wtab, smem, w + 1, row, e) : row[w + 1];
-        *(longlong2*)(dst + w) = make_longlong2((int64_t)a, (int64_t)c);
-      }
-      if (q.having.active)
-        nh += having_ok_words(e >= 0 ? mg_word(wtab, smem, hv, row, e) : row[hv],
-                              hc < 0 ? 0 : (e >= 0 ? mg_word(wtab, smem, hc, row, e) : row[hc]), q.having);
-      }
-    }
-    cur += __popcll(b);
-  }
-  for (int i0 = wave * 64; i0 < H; i0 += MG_THREADS) {  // delta entries, 64 per wave step
-    const int e = i0 + lane;
-    const uint64_t id = e < H ? ids[e] : EMPTY_ID;
-    const bool isnew = id != EMPTY_ID && !(rt[e] & RT_MATCHED);
-    const uint64_t b = __ballot(isnew);
-    if (isnew) {
-      uint64_t* dst = dst0 + (cur + __popcll(b & lt)) * q.sw;
-      const uint64_t hk = ((uint64_t)p << (64 - q.log2P)) | (id >> q.log2P);
-      const int64_t ws = (((int64_t)(id & ((1ULL << q.log2P) - 1))) + wbase) * (q.windowed ? q.adv : 0);
-      *(longlong2*)dst = make_longlong2(key_of_hash(hk), ws);
-      if constexpr (CNT1) {
-        const uint32_t c = cnt1[e];
-        *(longlong2*)(dst + 2) = make_longlong2(q.tbase + (int64_t)rt[e] - 1, (int64_t)c);
-        if (q.having.active) nh += having_ok_words(c, 0, q.having);
-      } else {
-      for (int w = 2; w < q.sw; w += 2) {
-        const uint64_t a = w == 2 ? (uint64_t)(q.tbase + (int64_t)rt[e] - 1) : mg_word(wtab, smem, w, nullptr, e);
-        *(longlong2*)(dst + w) = make_longlong2((int64_t)a, (int64_t)mg_word(wtab, smem, w + 1, nullptr, e));
-      }
-#ifdef KHIP_TUNING
-      if (q.dbg)
-        printf("[merge out] p %u e %d sw %d wo3 %d wo4 %d mw3 %llx mw4 %llx init3 %lld dst %llx %llx %llx %llx %llx\n", p, e,
-               q.sw, wtab[3].kind, wtab[4].kind, (unsigned long long)mg_word(wtab, smem, 3, nullptr, e),
-               (unsigned long long)mg_word(wtab, smem, 4, nullptr, e), (long long)q.init.w[3],
-               (unsigned long long)dst[0], (unsigned long long)dst[1], (unsigned long long)dst[2],
-               (unsigned long long)dst[3], (unsigned long long)dst[4]);
-#endif
-      if (q.having.active)
-        nh += having_ok_words(mg_word(wtab, smem, hv, nullptr, e), hc < 0 ? 0 : mg_word(wtab, smem, hc, nullptr, e),
-                              q.having);
-      }
-    }
-    cur += __popcll(b);
-  }
-  if (q.having.active) {
-    nh = (int)wave_sum(nh);
-    if (lane == 0 && nh) atomicAdd(&hnew[p], (unsigned long long)nh);
-  }
-  MG_T(4);
-  if (dbg) {
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    MG_T(5);
+    __syncthreads();  // the table is clear for the next item
+    MG_T(4);
+    it = nit;
   }
 #undef MG_T
 }
@@ -1673,7 +1702,7 @@ khip_status part_init(khip_agg* a, int64_t hint) {
     int n64 = 0, n32 = 0;
     for (int o = 0; o < a->ap.n_ops; o++) (a->ap.ops[o].kind == OP_INC || a->ap.ops[o].kind == OP_INC_VALID ? n32 : n64)++;
     const int mentry = 8 + 8 * n64 + 4 + 4 * n32;
-    const int64_t mbudget = knob("KHIP_MERGE_LDS_KB", 78) * 1024;
+    const int64_t mbudget = knob("KHIP_MERGE_LDS_KB", 150) * 1024;  // one persistent workgroup per CU
     int mH = (int)std::min<int64_t>(16384, mbudget / mentry - 64) & ~63;
     s.mH = mH;
     const int ms = mH + 64;  // plane stride: H entries + one dummy entry per lane
@@ -1731,6 +1760,11 @@ khip_status part_init(khip_agg* a, int64_t hint) {
   KHIP_TRY(s.newcnt.ensure(s.P * 8));
   KHIP_TRY(s.pbase.ensure((s.P + 1) * 8));
   KHIP_TRY(s.R.ensure((s.P + 1) * 8));
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, a->device) == hipSuccess && ncu > 0)
+      s.n_cu = ncu;
+  }
   KHIP_TRY(s.ctr.ensure(128));
   KHIP_TRY(s.hcnt.ensure(s.P * 8));
   KHIP_TRY(s.hnew.ensure(s.P * 8));
@@ -2102,7 +2136,8 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                         s.rw == 2 && a->desc.window_kind != KHIP_WINDOW_HOPPING;
       auto mk = cnt1 ? k_part_merge<true> : k_part_merge<false>;
       hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, s.m_lds);
-      hipLaunchKernelGGL(mk, dim3(nwork), dim3(MG_THREADS), s.m_lds, a->stream, mq, wk, s.pbase.as<int64_t>(),
+      const int64_t grid = std::min<int64_t>(nwork, (int64_t)s.n_cu * knob("KHIP_MERGE_WG_PER_CU", 1));
+      hipLaunchKernelGGL(mk, dim3(grid), dim3(MG_THREADS), s.m_lds, a->stream, mq, wk, nwork, s.pbase.as<int64_t>(),
                          s.srec.as<uint64_t>(), pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
                          s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
                          s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
@@ -2134,7 +2169,16 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     KHIP_TRY_HIP(hipMemcpyAsync(c2, s.ctr.p, (pass == 0 ? 5 + T_NPART : 3) * 8, hipMemcpyDeviceToHost, a->stream));
     KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
     added_total += (int64_t)c2[0];
-    if (dbg) agg_probe_report(dbgbuf, (int)((pass == 0 && !subs0) ? P : (int64_t)work.size()));
+    if (dbg && merge) {  // k_part_merge: per-phase time summed over its persistent workgroups
+      unsigned long long ph[8] = {};
+      if (hipMemcpy(ph, dbgbuf.p, sizeof(ph), hipMemcpyDeviceToHost) == hipSuccess) {
+        const double g = (double)std::min<int64_t>(P, s.n_cu) * 100.0;  // 100 MHz ticks → us per workgroup
+        fprintf(stderr, "[merge probe] per workgroup (us): setup %.1f evict %.1f records %.1f mark+reserve %.1f write %.1f\n",
+                ph[0] / g, ph[1] / g, ph[2] / g, ph[3] / g, ph[4] / g);
+      }
+    } else if (dbg) {
+      agg_probe_report(dbgbuf, (int)((pass == 0 && !subs0) ? P : (int64_t)work.size()));
+    }
     if (c2[1] == 0) break;
     if (pass > 24) return fail(KHIP_E_DEVICE, "partitioned aggregation could not place the batch");
     // retry the failed partitions: LDS overflow → twice the sub-passes; region overflow → grow
