@@ -254,11 +254,13 @@ khip_status khip_agg_get(khip_agg* agg, const khip_pull* q, const khip_having* h
                          khip_snapshot* out);
 
 /* Count the rows that pass `having` entirely on the device (no copy-out).
- * having may be NULL (= total group count). */
+ * having may be NULL (= total group count).  When `having` is the descriptor's own HAVING,
+ * the count is the one the aggregate kernels maintain (returned without device work). */
 khip_status khip_agg_count_rows(khip_agg* agg, const khip_having* having,
                                 int64_t* n_rows);
 
-/* Drop all state (a fresh query instance); keeps the device allocation. */
+/* Drop all state (a fresh query instance); keeps the device allocation.  Asynchronous:
+ * queued on the handle's stream, ahead of every later call on the handle. */
 khip_status khip_agg_reset(khip_agg* agg);
 
 /* Block until all work queued on the handle has finished. */

@@ -463,23 +463,39 @@ __global__ __launch_bounds__(256) void k_dict_count(const uint64_t* __restrict__
   if (threadIdx.x == 0) bsum[blockIdx.x] = (int64_t)acc;
 }
 
-// Exclusive prefix sum of v[0..n) in place (single block); total added to *total.
+// Exclusive prefix sum of v[0..n) in place (single block); total added to *total.  Each thread
+// owns 16 consecutive elements of a 16K-element chunk: one wave scan and one barrier per chunk.
 __global__ __launch_bounds__(1024) void k_scan_excl(int64_t* __restrict__ v, int64_t n, int64_t* __restrict__ total) {
-  __shared__ int64_t lds[1024];
+  __shared__ int64_t wsum[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int64_t carry = 0;
-  for (int64_t b0 = 0; b0 < n; b0 += 1024) {
-    const int64_t b = b0 + threadIdx.x;
-    const int64_t x = b < n ? v[b] : 0;
-    lds[threadIdx.x] = x;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-      int64_t y = threadIdx.x >= off ? lds[threadIdx.x - off] : 0;
-      __syncthreads();
-      lds[threadIdx.x] += y;
-      __syncthreads();
+  for (int64_t b0 = 0; b0 < n; b0 += 1024 * 16) {
+    const int64_t base = b0 + (int64_t)threadIdx.x * 16;
+    int64_t x[16], s = 0;
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      x[u] = base + u < n ? v[base + u] : 0;
+      s += x[u];
     }
-    if (b < n) v[b] = carry + lds[threadIdx.x] - x;
-    carry += lds[1023];
+    int64_t incl = s;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int64_t y = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int64_t before = 0, tot = 0;
+    for (int k = 0; k < 16; k++) {
+      before += k < wave ? wsum[k] : 0;
+      tot += wsum[k];
+    }
+    int64_t run = carry + before + incl - s;
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      if (base + u < n) v[base + u] = run;
+      run += x[u];
+    }
+    carry += tot;
     __syncthreads();
   }
   if (threadIdx.x == 0) *total += carry;
@@ -1231,17 +1247,21 @@ khip_status khip_agg_reset(khip_agg* a) {
   clear_error();
   if (!a) return fail(KHIP_E_INVALID, "null argument");
   DeviceGuard g(a->device);
-  hipLaunchKernelGGL(k_init_table, dim3(grid_for(a->cap * a->sw, 256)), dim3(256), 0, a->stream,
-                     a->table.as<uint64_t>(), a->cap, a->sw, a->init);
-  int64_t m1 = -1;
-  KHIP_TRY_HIP(hipMemcpyAsync(a->stream_time.p, &m1, 8, hipMemcpyHostToDevice, a->stream));
-  if (a->engine == 0) KHIP_TRY(part_reset(a));
+  if (a->engine == 0) {
+    KHIP_TRY(part_reset(a));  // also the stream time
+  } else {
+    hipLaunchKernelGGL(k_init_table, dim3(grid_for(a->cap * a->sw, 256)), dim3(256), 0, a->stream,
+                       a->table.as<uint64_t>(), a->cap, a->sw, a->init);
+    int64_t m1 = -1;
+    KHIP_TRY_HIP(hipMemcpyAsync(a->stream_time.p, &m1, 8, hipMemcpyHostToDevice, a->stream));
+  }
   if (a->desc.key_type == KHIP_KEY_UTF8) {
     KHIP_TRY_HIP(hipMemsetAsync(a->dword.p, 0, a->dcap * 8, a->stream));
     a->docc = 0;
     a->arena_used = 0;
   }
-  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  // asynchronous on the handle's stream (every later call on the handle is ordered behind it)
+  KHIP_TRY_HIP(hipGetLastError());
   a->occ = 0;
   a->host_stream_time = -1;
   return KHIP_OK;

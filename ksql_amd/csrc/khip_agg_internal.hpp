@@ -303,9 +303,11 @@ struct PartState {
   int8_t plane_w64[MAX_OPS] = {};
   int8_t word_op[32] = {};
   // the query's HAVING maintained on the device: rows passing it per partition (hcnt; hnew =
-  // being written this push) and in the closed store (hclosed).  hvalid = false once a push
-  // took a path that does not maintain them (fallback kernel, split) until the next reset.
-  DevBuf hcnt, hnew, hclosed;
+  // being written this push), their sum (ctr[11]) and the closed store's (ctr[12]); having_total
+  // = both, as of the last push.  hvalid = false once a push took a path that does not maintain
+  // them (fallback kernel, split) until the next reset.
+  DevBuf hcnt, hnew;
+  int64_t having_total = 0;
   bool hvalid = true;
   HostBuf pinfo;  // pinned: push info (window range, event-time span) and end-of-push stats
 };

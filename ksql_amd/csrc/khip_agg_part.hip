@@ -214,18 +214,63 @@ __global__ __launch_bounds__(256) void k_part_colsum(const uint32_t* __restrict_
   csum[(int64_t)c * P + p] = s;
 }
 
-// in place: csum[c][p] → exclusive prefix over c; R[p] = column total
+// in place: csum[c][p] → exclusive prefix over c; R[p] = column total.  The chunk sums are
+// loaded 16 at a time before any store (the in-place stores would otherwise order every load
+// behind the previous store: TC dependent round trips per thread).
 __global__ __launch_bounds__(256) void k_part_colbase(int64_t* __restrict__ csum, int P, int TC,
                                                       int64_t* __restrict__ R) {
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= P) return;
   int64_t acc = 0;
-  for (int c = 0; c < TC; c++) {
-    const int64_t v = csum[(int64_t)c * P + p];
-    csum[(int64_t)c * P + p] = acc;
-    acc += v;
+  for (int c0 = 0; c0 < TC; c0 += 16) {
+    int64_t v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) v[u] = c0 + u < TC ? csum[(int64_t)(c0 + u) * P + p] : 0;
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      if (c0 + u < TC) csum[(int64_t)(c0 + u) * P + p] = acc;
+      acc += v[u];
+    }
   }
   R[p] = acc;
+}
+
+// v[0..n) → its exclusive prefix sum in place, v[n] = the total (one workgroup; each thread
+// owns 16 consecutive elements per 16K-element chunk: one wave scan + one barrier per chunk).
+__global__ __launch_bounds__(1024) void k_part_pscan(int64_t* __restrict__ v, int64_t n) {
+  __shared__ int64_t wsum[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int64_t carry = 0;
+  for (int64_t b0 = 0; b0 < n; b0 += 1024 * 16) {
+    const int64_t base = b0 + (int64_t)threadIdx.x * 16;
+    int64_t x[16], s = 0;
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      x[u] = base + u < n ? v[base + u] : 0;
+      s += x[u];
+    }
+    int64_t incl = s;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int64_t y = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int64_t before = 0, tot = 0;
+    for (int k = 0; k < 16; k++) {
+      before += k < wave ? wsum[k] : 0;
+      tot += wsum[k];
+    }
+    int64_t run = carry + before + incl - s;
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      if (base + u < n) v[base + u] = run;
+      run += x[u];
+    }
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) v[n] = carry;
 }
 
 // hist[t][p] → absolute output offset of (tile t, partition p)
@@ -244,11 +289,126 @@ __global__ __launch_bounds__(256) void k_part_colprefix(uint32_t* __restrict__ h
   }
 }
 
+// 12-byte (key hash, ts) record of the narrow layout (rw = 2) when k_part_merge runs: the key
+// hash, and ts relative to the push's earliest accepted ts (trel = ts - tbase + 1; 0 = no window
+// applied).  A quarter less traffic through the scatter, the refine and the merge's reads.
+struct R12 {
+  uint32_t lo, hi, trel;
+};
+
+__device__ __forceinline__ void r12_store(uint64_t* __restrict__ srec, uint64_t i, uint64_t hk, uint32_t trel) {
+  *(R12*)((char*)srec + i * 12) = R12{(uint32_t)hk, (uint32_t)(hk >> 32), trel};
+}
+
+// barrier without the vmcnt(0) that __syncthreads() implies: LDS writes are waited for, the
+// wave's outstanding global loads (prefetches) and stores stay in flight
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// LDS-staged scatter step (k_part_scatter's narrow fast path, k_part_refine of narrow records).
+// U records per thread (hk, pay, ok) go to bin (hk >> shift) & mask, whose next output position
+// is cur[bin].  Instead of every lane storing its record to its own bin's run (64 lines touched
+// per store instruction), the step's records are ranked per bin (LDS atomics), placed in LDS in
+// bin order, and written back out by consecutive threads: each bin's records of the step leave
+// as one contiguous run (~S / nb records) in whole-line, coalesced stores.
+//   out: 0 = (hk, pay) 16 bytes; 1 = R12 (pay = trel); 2 = R12 in, (hk, ts) 16 bytes out
+struct StageLds {
+  uint32_t* cur;    // [nb] next output record of each bin (global index)
+  uint32_t* cnt;    // [nb] records of the step per bin
+  uint32_t* sbase;  // [nb] the bin's first staged slot
+  uint32_t* gpos;   // [nb] output position of the bin's first record of the step
+  uint64_t* sk;     // [S] staged key hashes
+  int64_t* sp;      // [S] staged payloads
+  int* wsum;        // [16]
+};
+
+__device__ __forceinline__ uint32_t stage_bin(uint64_t hk, int shift, uint32_t mask) {
+  return shift >= 64 ? 0u : (uint32_t)(hk >> shift) & mask;
+}
+
+template <int U>
+__device__ __forceinline__ void stage_step(const uint64_t (&hk)[U], const int64_t (&pay)[U], const bool (&ok)[U],
+                                           int shift, uint32_t mask, int nb, const StageLds& L,
+                                           uint64_t* __restrict__ srec, int out, int64_t tbase) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  uint32_t rank[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) rank[u] = ok[u] ? atomicAdd(&L.cnt[stage_bin(hk[u], shift, mask)], 1u) : 0u;
+  lds_barrier();
+  // exclusive scan of the bin counts (nb <= PT_THREADS)
+  const uint32_t c = t < nb ? L.cnt[t] : 0u;
+  uint32_t incl = c;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) L.wsum[wave] = (int)incl;
+  lds_barrier();
+  uint32_t before = 0, tot = 0;
+  for (int k = 0; k < PT_THREADS / 64; k++) {
+    before += k < wave ? (uint32_t)L.wsum[k] : 0u;
+    tot += (uint32_t)L.wsum[k];
+  }
+  if (t < nb) {
+    L.sbase[t] = before + incl - c;
+    L.gpos[t] = L.cur[t];
+    L.cur[t] += c;
+    L.cnt[t] = 0u;
+  }
+  lds_barrier();
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if (!ok[u]) continue;
+    const uint32_t i = L.sbase[stage_bin(hk[u], shift, mask)] + rank[u];
+    L.sk[i] = hk[u];
+    L.sp[i] = pay[u];
+  }
+  lds_barrier();
+  for (uint32_t j = t; j < tot; j += PT_THREADS) {
+    const uint64_t h = L.sk[j];
+    const int64_t p = L.sp[j];
+    const uint32_t b = stage_bin(h, shift, mask);
+    const uint64_t dst = (uint64_t)L.gpos[b] + (j - L.sbase[b]);
+    if (out == 0) {
+      *(longlong2*)(srec + dst * 2) = make_longlong2((int64_t)h, p);
+    } else if (out == 1) {
+      r12_store(srec, dst, h, (uint32_t)p);
+    } else {
+      *(longlong2*)(srec + dst * 2) = make_longlong2((int64_t)h, p ? tbase + p - 1 : -1);
+    }
+  }
+  // the next step's first barrier (after its rank atomics) orders these LDS reads before any
+  // rewrite of sbase / gpos / the stage
+}
+
+// LDS carve-up for stage_step: nb bins, S staged records
+__host__ __device__ constexpr size_t stage_lds_bytes(int nb, int S) {
+  return ((size_t)nb * 16 + 15) / 16 * 16 + (size_t)S * 16;
+}
+
+__device__ __forceinline__ StageLds stage_carve(char* smem, int nb, int S, int* wsum) {
+  StageLds L;
+  L.cur = (uint32_t*)smem;
+  L.cnt = L.cur + nb;
+  L.sbase = L.cnt + nb;
+  L.gpos = L.sbase + nb;
+  L.sk = (uint64_t*)(smem + ((size_t)nb * 16 + 15) / 16 * 16);
+  L.sp = (int64_t*)(L.sk + S);
+  L.wsum = wsum;
+  return L;
+}
+
 __device__ __forceinline__ void scatter_one(int64_t key, int64_t x, int64_t jlo, int64_t i, int log2P, uint32_t* cur,
                                             uint64_t* __restrict__ srec, const RecLayout& L, const ColPtrs& cols,
-                                            int n_cols, const ColTypes& ctypes, bool applied) {
+                                            int n_cols, const ColTypes& ctypes, bool applied, bool r12,
+                                            int64_t tbase) {
   const uint64_t hk = key_hash(key);
   const uint32_t pos = atomicAdd(&cur[part_of_hk(hk, log2P)], 1u);
+  if (r12) {  // narrow layout only
+    r12_store(srec, pos, hk, applied ? (uint32_t)(x - tbase + 1) : 0u);
+    return;
+  }
   uint64_t* r = srec + (uint64_t)pos * L.rw;
   *(longlong2*)r = make_longlong2((int64_t)hk, applied ? x : -1);  // one 16-byte store: key hash, ts
   if (L.rw > 2) {  // then the rest of the record, 16 bytes at a time, contiguous
@@ -274,9 +434,13 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
     int pad, int64_t nT, const uint32_t* __restrict__ offs, const int64_t* __restrict__ pbase,
     const int64_t* __restrict__ tileprefix, const int64_t* __restrict__ tilemax,
     const int64_t* __restrict__ tilemin, int windowed, int64_t size, int64_t adv, FastDiv fd, int64_t grace,
-    RecLayout L, uint64_t* __restrict__ srec, int64_t dummy, int64_t* __restrict__ tpart) {
+    RecLayout L, uint64_t* __restrict__ srec, int64_t dummy, int64_t* __restrict__ tpart,
+    const int64_t* __restrict__ wr, int r12_ok, int stage) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint32_t* cur = (uint32_t*)smem;
+  __shared__ int wsum[PT_THREADS / 64];
+  const bool r12 = r12_ok && wr[4] != 0;  // k_part_merge runs: 12-byte records
+  const int64_t tbase = wr[5];
   __shared__ int64_t lmax[PT_THREADS / 64];
   __shared__ unsigned long long lc[2];
   const int P = 1 << log2P;
@@ -293,7 +457,53 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
   const int64_t smax = carry > tilemax[t] ? carry : tilemax[t];
   const int64_t tmin = tilemin[t];
   const bool fast = !windowed || tmin == INT64_MAX || first_window_start(tmin, size, adv) + size > smax - grace;
-  if (fast && NARROW) {
+  if (fast && NARROW && stage) {
+    // (key hash, ts) records through the LDS stage (stage_step), next step's loads in flight
+    constexpr int S = U * PT_THREADS;
+    const StageLds SL = stage_carve(smem, P, S, wsum);
+    for (int p = threadIdx.x; p < P; p += PT_THREADS) SL.cnt[p] = 0u;
+    lds_barrier();
+    int64_t x[U], k[U], nxx[U], nxk[U];
+    auto load_step = [&](int64_t i0, int64_t (&dx)[U], int64_t (&dk)[U]) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        int64_t i = i0 + (int64_t)u * PT_THREADS;
+        i = i < end ? i : end - 1;
+        dx[u] = ts[i];
+        dk[u] = keys[i];
+      }
+    };
+    // steps are uniform across the block (every thread runs every step: barriers inside)
+    int64_t s0 = base;
+    if (s0 < end) load_step(s0 + threadIdx.x, x, k);
+    for (; s0 < end; s0 += S) {
+      const int64_t i0 = s0 + threadIdx.x;
+      if (s0 + S < end) load_step(i0 + S, nxx, nxk);
+      uint64_t hk[U];
+      int64_t pay[U];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int64_t i = i0 + (int64_t)u * PT_THREADS;
+        ok[u] = i < end && x[u] >= 0 && bit_get(kv, i) && bit_get(rv, i);
+        if (windowed) {
+          const int64_t lo = x[u] - size + adv;
+          c_app += ok[u] ? (int64_t)fast_udiv((uint64_t)x[u], fd) - (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), fd) + 1
+                         : 0;
+        } else {
+          c_app += ok[u] ? 1 : 0;
+        }
+        hk[u] = key_hash(k[u]);  // records carry the key hash (key = its inverse)
+        pay[u] = r12 ? x[u] - tbase + 1 : x[u];
+      }
+      stage_step<U>(hk, pay, ok, log2P == 0 ? 64 : 64 - log2P, (uint32_t)(P - 1), P, SL, srec, r12 ? 1 : 0, tbase);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        x[u] = nxx[u];
+        k[u] = nxk[u];
+      }
+    }
+  } else if (fast && NARROW) {
     // 16-byte (key, ts) records: straight-line steps (no branch around a load or store, so
     // every wait is counted), next step's loads issued before this step's cursors/stores;
     // rejected or out-of-range lanes store to the dummy record
@@ -328,10 +538,18 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
         pos[u] = atomicAdd(&cur[part_of_hk((uint64_t)k[u], log2P)], ok ? 1u : 0u);
         if (!ok) pos[u] = 0xFFFFFFFFu;
       }
+      if (r12) {
 #pragma unroll
-      for (int u = 0; u < U; u++) {
-        const uint64_t dst = pos[u] == 0xFFFFFFFFu ? (uint64_t)dummy : (uint64_t)pos[u];
-        *(longlong2*)(srec + dst * 2) = make_longlong2(k[u], x[u]);
+        for (int u = 0; u < U; u++) {
+          const uint64_t dst = pos[u] == 0xFFFFFFFFu ? (uint64_t)dummy : (uint64_t)pos[u];
+          r12_store(srec, dst, (uint64_t)k[u], (uint32_t)(x[u] - tbase + 1));
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint64_t dst = pos[u] == 0xFFFFFFFFu ? (uint64_t)dummy : (uint64_t)pos[u];
+          *(longlong2*)(srec + dst * 2) = make_longlong2(k[u], x[u]);
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; u++) {
@@ -363,7 +581,7 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
             windowed ? (int64_t)fast_udiv((uint64_t)x[u], fd) - (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), fd) + 1
                      : 1;
         c_app += nwin;
-        scatter_one(k[u], x[u], 0, i, log2P, cur, srec, L, cols, n_cols, ctypes, true);
+        scatter_one(k[u], x[u], 0, i, log2P, cur, srec, L, cols, n_cols, ctypes, true, r12, tbase);
       }
     }
   } else {
@@ -388,7 +606,7 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
       }
       c_late += jlo;
       c_app += nwin - jlo;
-      scatter_one(keys[i], x, jlo, i, log2P, cur, srec, L, cols, n_cols, ctypes, nwin > jlo);
+      scatter_one(keys[i], x, jlo, i, log2P, cur, srec, L, cols, n_cols, ctypes, nwin > jlo, r12, tbase);
     }
   }
   c_app = wave_sum(c_app);
@@ -410,6 +628,116 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
   }
 }
 
+// One block's range [lo, hi) of bucket b → its partitions' runs (cursors in LDS).  N12: the
+// 12-byte narrow records (RW = 2 layout) k_part_scatter wrote for k_part_merge; out16: widen
+// them back to 16-byte (key hash, ts) records for the merge (tbase = the push's rowtime base).
+template <int RW, bool N12>
+__device__ __forceinline__ void refine_range(const uint64_t* __restrict__ srcA, uint32_t* cur, int64_t lo, int64_t hi,
+                                             int log2P, int F, int64_t dummy, uint64_t* __restrict__ srec, int mode,
+                                             bool out16, int64_t tbase) {
+  // Straight-line steps (no branch around a load, so the waits stay counted): U records
+  // per thread; the next step's loads are issued before this step's LDS cursors and
+  // stores; out-of-range lanes load a clamped index and store to the dummy record.
+  constexpr int U = RW <= 2 ? 8 : (RW <= 4 ? 4 : (RW <= 8 ? 2 : 1));  // ~64 VGPRs of records in flight
+  constexpr int H2 = N12 ? 1 : RW / 2;
+  longlong2 r[U][H2], nx[U][H2];
+  R12 r3[U], nx3[U];
+  auto load_step = [&](int64_t i0, longlong2 (&d)[U][H2], R12 (&d3)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      int64_t i = i0 + (int64_t)u * PT_THREADS;
+      i = i < hi ? i : hi - 1;
+      if constexpr (N12) {
+        d3[u] = *(const R12*)((const char*)srcA + (uint64_t)i * 12);
+      } else {
+#pragma unroll
+        for (int k = 0; k < H2; k++) d[u][k] = ((const longlong2*)(srcA + (uint64_t)i * RW))[k];
+      }
+    }
+  };
+  int64_t i0 = lo + threadIdx.x;
+  load_step(i0, r, r3);
+  for (; i0 < hi; i0 += U * PT_THREADS) {
+    const int64_t in = i0 + U * PT_THREADS;
+    if (in < hi) load_step(in, nx, nx3);
+    uint32_t pos[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const bool ok = i0 + (int64_t)u * PT_THREADS < hi;
+      const uint64_t hk = N12 ? ((uint64_t)r3[u].hi << 32 | r3[u].lo) : (uint64_t)r[u][0].x;
+      const uint32_t f = part_of_hk(hk, log2P) & (uint32_t)(F - 1);
+      pos[u] = atomicAdd(&cur[f], ok ? 1u : 0u);
+      if (!ok) pos[u] = 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      uint64_t dst = pos[u] == 0xFFFFFFFFu ? (uint64_t)dummy : (uint64_t)pos[u];
+      if (mode == 1) dst = pos[u] == 0xFFFFFFFFu ? (uint64_t)dummy : (uint64_t)(i0 + (int64_t)u * PT_THREADS);
+      if constexpr (N12) {
+        if (out16)
+          *(longlong2*)(srec + dst * 2) = make_longlong2((int64_t)((uint64_t)r3[u].hi << 32 | r3[u].lo),
+                                                         r3[u].trel ? tbase + (int64_t)r3[u].trel - 1 : -1);
+        else
+          *(R12*)((char*)srec + dst * 12) = r3[u];
+      } else {
+#pragma unroll
+        for (int k = 0; k < H2; k++) ((longlong2*)(srec + dst * RW))[k] = r[u][k];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if constexpr (N12) {
+        r3[u] = nx3[u];
+      } else {
+#pragma unroll
+        for (int k = 0; k < H2; k++) r[u][k] = nx[u][k];
+      }
+    }
+  }
+}
+
+// refine_range through the LDS stage (narrow records): out as in stage_step
+template <bool N12>
+__device__ __forceinline__ void refine_staged(const uint64_t* __restrict__ srcA, const StageLds& SL, int64_t lo,
+                                              int64_t hi, int log2P, int F, uint64_t* __restrict__ srec, int out,
+                                              int64_t tbase) {
+  constexpr int U = 8;
+  constexpr int S = U * PT_THREADS;
+  uint64_t hk[U], nhk[U];
+  int64_t pay[U], npay[U];
+  auto load_step = [&](int64_t i0, uint64_t (&dh)[U], int64_t (&dp)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      int64_t i = i0 + (int64_t)u * PT_THREADS;
+      i = i < hi ? i : hi - 1;
+      if constexpr (N12) {
+        const R12 v = *(const R12*)((const char*)srcA + (uint64_t)i * 12);
+        dh[u] = (uint64_t)v.hi << 32 | v.lo;
+        dp[u] = (int64_t)v.trel;
+      } else {
+        const longlong2 v = *(const longlong2*)(srcA + (uint64_t)i * 2);
+        dh[u] = (uint64_t)v.x;
+        dp[u] = v.y;
+      }
+    }
+  };
+  int64_t s0 = lo;
+  load_step(s0 + threadIdx.x, hk, pay);
+  for (; s0 < hi; s0 += S) {
+    const int64_t i0 = s0 + threadIdx.x;
+    if (s0 + S < hi) load_step(i0 + S, nhk, npay);
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) ok[u] = i0 + (int64_t)u * PT_THREADS < hi;
+    stage_step<U>(hk, pay, ok, 64 - log2P, (uint32_t)(F - 1), F, SL, srec, out, tbase);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      hk[u] = nhk[u];
+      pay[u] = npay[u];
+    }
+  }
+}
+
 // Two-level scatter, pass B: block (bucket b, tile group g) moves the records that pass A
 // (k_part_scatter over the B = P >> fbits buckets) put in bucket b for tiles [t0, t1) — one
 // contiguous range, since pass A lays each bucket out tile-major — to their partitions' final
@@ -421,58 +749,39 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_refine(const uint64_t* __re
                                                             const uint32_t* __restrict__ offs,
                                                             const int64_t* __restrict__ pbase, int64_t nT, int G,
                                                             int log2P, int fbits, int64_t dummy,
-                                                            uint64_t* __restrict__ srec, int mode) {
+                                                            uint64_t* __restrict__ srec, int mode,
+                                                            const int64_t* __restrict__ wr, int r12_ok, int stage) {
   __shared__ uint32_t cur[1 << 12];
   const int F = 1 << fbits, P = 1 << log2P, B = P >> fbits;
   const int64_t ng = (nT + G - 1) / G;
   const int b = (int)(blockIdx.x / ng);
   const int64_t g = blockIdx.x % ng;
   const int64_t t0 = g * G, t1 = t0 + G < nT ? t0 + G : nT;
+  if (RW == 2 && stage) {  // narrow records through the LDS stage
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ int wsum[PT_THREADS / 64];
+    const StageLds SL = stage_carve(smem, F, 8 * PT_THREADS, wsum);
+    for (int f = threadIdx.x; f < F; f += PT_THREADS) {
+      SL.cur[f] = offs[t0 * P + ((int64_t)b << fbits) + f];
+      SL.cnt[f] = 0u;
+    }
+    const int64_t lo = offA[t0 * B + b];
+    const int64_t hi = t1 < nT ? (int64_t)offA[t1 * B + b] : pbase[(int64_t)(b + 1) << fbits];
+    lds_barrier();
+    if (hi <= lo) return;
+    if (r12_ok && wr[4] != 0) refine_staged<true>(srcA, SL, lo, hi, log2P, F, srec, r12_ok == 2 ? 2 : 1, wr[5]);
+    else refine_staged<false>(srcA, SL, lo, hi, log2P, F, srec, 0, 0);
+    return;
+  }
   for (int f = threadIdx.x; f < F; f += PT_THREADS) cur[f] = offs[t0 * P + ((int64_t)b << fbits) + f];
   __syncthreads();
   const int64_t lo = offA[t0 * B + b];
   const int64_t hi = t1 < nT ? (int64_t)offA[t1 * B + b] : pbase[(int64_t)(b + 1) << fbits];
   if (hi <= lo) return;
-  // Straight-line steps (no branch around a load, so the waits stay counted): U records
-  // per thread; the next step's loads are issued before this step's LDS cursors and
-  // stores; out-of-range lanes load a clamped index and store to the dummy record.
-  constexpr int U = RW <= 2 ? 8 : (RW <= 4 ? 4 : (RW <= 8 ? 2 : 1));  // ~64 VGPRs of records in flight
-  constexpr int H2 = RW / 2;
-  longlong2 r[U][H2], nx[U][H2];
-  auto load_step = [&](int64_t i0, longlong2 (&d)[U][H2]) {
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      int64_t i = i0 + (int64_t)u * PT_THREADS;
-      i = i < hi ? i : hi - 1;
-#pragma unroll
-      for (int k = 0; k < H2; k++) d[u][k] = ((const longlong2*)(srcA + (uint64_t)i * RW))[k];
-    }
-  };
-  int64_t i0 = lo + threadIdx.x;
-  load_step(i0, r);
-  for (; i0 < hi; i0 += U * PT_THREADS) {
-    const int64_t in = i0 + U * PT_THREADS;
-    if (in < hi) load_step(in, nx);
-    uint32_t pos[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const bool ok = i0 + (int64_t)u * PT_THREADS < hi;
-      const uint32_t f = part_of_hk((uint64_t)r[u][0].x, log2P) & (uint32_t)(F - 1);
-      pos[u] = atomicAdd(&cur[f], ok ? 1u : 0u);
-      if (!ok) pos[u] = 0xFFFFFFFFu;
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      uint64_t dst = pos[u] == 0xFFFFFFFFu ? (uint64_t)dummy : (uint64_t)pos[u];
-      if (mode == 1) dst = pos[u] == 0xFFFFFFFFu ? (uint64_t)dummy : (uint64_t)(i0 + (int64_t)u * PT_THREADS);
-#pragma unroll
-      for (int k = 0; k < H2; k++) ((longlong2*)(srec + dst * RW))[k] = r[u][k];
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++)
-#pragma unroll
-      for (int k = 0; k < H2; k++) r[u][k] = nx[u][k];
-  }
+  if (RW == 2 && r12_ok && wr[4] != 0)
+    refine_range<RW, true>(srcA, cur, lo, hi, log2P, F, dummy, srec, mode, r12_ok == 2, wr[5]);
+  else
+    refine_range<RW, false>(srcA, cur, lo, hi, log2P, F, dummy, srec, mode, false, 0);
 }
 
 // ------------------------------------------------------------------ k_part_agg
@@ -864,7 +1173,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
 //      instruction covers consecutive rows; count the rows passing the query's HAVING
 // A partition whose deltas overflow H writes nothing and is retried with 2x sub-passes (it
 // has already moved its closed rows in pass 0; retries skip them).
-constexpr int MG_THREADS = 1024;
+constexpr int MG_THREADS = 512;  // two persistent workgroups per CU (one's LDS work hides the other's latency)
 constexpr uint32_t RT_MATCHED = 0x80000000u;
 
 struct MergeParams {
@@ -879,7 +1188,6 @@ struct MergeParams {
   int64_t size, adv;
   FastDiv fd;
   int64_t cmax;
-  int64_t tbase;  // rowtime planes hold ts - tbase + 1 (push span < 2^31 - 1)
   int8_t col_word[MAX_COLS];
   int32_t col_type[MAX_COLS];
   UpdOp ops[MAX_OPS];
@@ -890,6 +1198,7 @@ struct MergeParams {
   InitWords init;
   HavingDev having;  // the query's HAVING (active = 0: none): rows passing it are counted
   int32_t dbg;       // tuning build: KHIP_MERGE_DEBUG prints the delta table of touched partitions
+  int32_t r12;       // records are R12 (narrow layout; k_part_scatter / k_part_refine wrote them so)
 };
 
 __device__ __forceinline__ uint32_t mg_slot(uint64_t id, int H) {
@@ -897,11 +1206,6 @@ __device__ __forceinline__ uint32_t mg_slot(uint64_t id, int H) {
   return (uint32_t)(((uint64_t)h * (uint32_t)H) >> 32);
 }
 
-// barrier without the vmcnt(0) that __syncthreads() implies: LDS writes are waited for, the
-// wave's outstanding global loads (the record prefetch) stay in flight
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
 
 template <class T>
 __device__ __forceinline__ KLDS T* mg_plane(char* smem, int32_t off) {
@@ -976,9 +1280,24 @@ __device__ __forceinline__ int mg_find(const MergeParams& q, const KLDS uint64_t
 }
 
 // One chunk of a partition's scattered records: AU per thread, rows l0 + tid + u * MG_THREADS.
+// r12: 12-byte narrow records (key hash, trel) → (key hash, ts); trel 0 → ts -1 (no window)
 template <int AU>
 __device__ __forceinline__ void mg_load(longlong2 (&rec)[AU], longlong2 (&ext)[AU], const uint64_t* __restrict__ srec,
-                                        int64_t rbase, int64_t rn, int64_t l0, int rw, bool wide) {
+                                        int64_t rbase, int64_t rn, int64_t l0, int rw, bool wide, bool r12,
+                                        int64_t tbase) {
+  if (r12) {
+    R12 v[AU];
+#pragma unroll
+    for (int u = 0; u < AU; u++) {
+      const int64_t li = l0 + threadIdx.x + (int64_t)u * MG_THREADS;
+      v[u] = li < rn ? *(const R12*)((const char*)srec + (uint64_t)(rbase + li) * 12) : R12{0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < AU; u++)
+      rec[u] = make_longlong2((int64_t)((uint64_t)v[u].hi << 32 | v[u].lo),
+                              v[u].trel ? tbase + (int64_t)v[u].trel - 1 : -1);
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < AU; u++) {
     const int64_t li = l0 + threadIdx.x + (int64_t)u * MG_THREADS;
@@ -1028,13 +1347,15 @@ __device__ __forceinline__ void mg_clear(char* smem, KLDS uint64_t* ids, KLDS ui
 // (key hash, ts) pairs with one window each — the record phase and the write-out skip the
 // generic op machinery (C1, C2).
 //
-// Persistent: gridDim.x workgroups (one per CU) walk the work items w = blockIdx.x + k * gridDim.x.
+// Persistent: gridDim.x workgroups (two per CU) walk the work items w = blockIdx.x + k * gridDim.x.
+// Barriers inside the item loop wait for LDS only (lds_barrier): the write-out's row stores and
+// the next item's record prefetch stay in flight across them.
 // The next item's first record chunk is loaded into registers before the current item's
 // resident-merge and write-out, and inside an item chunk c + 1 is loaded before chunk c is
 // applied, so HBM latency overlaps the LDS work; the write-out leaves every delta entry cleared
 // for the next item (no separate table init).
 template <bool CNT1>
-__global__ __launch_bounds__(MG_THREADS) void k_part_merge(
+__global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
     MergeParams q, const uint32_t* __restrict__ work, int64_t nwork, const int64_t* __restrict__ pbase,
     const uint64_t* __restrict__ srec, int first, uint64_t* __restrict__ buf0, uint64_t* __restrict__ buf1,
     const uint8_t* __restrict__ sel, const int64_t* __restrict__ cnt, unsigned long long* __restrict__ newcnt,
@@ -1043,7 +1364,9 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
     unsigned long long* __restrict__ hnew, unsigned long long* __restrict__ hclosed,
     unsigned long long* __restrict__ dbg) {
 #define MG_T(k) do { if (dbg && threadIdx.x == 0) atomicAdd(&dbg[(k)], (unsigned long long)(wall_clock64() - t_last)); t_last = wall_clock64(); } while (0)
+  if (wr[4] == 0) return;  // k_part_wrange declined the merge path for this push
   unsigned long long t_last = wall_clock64();
+  const int64_t tbase = wr[5];
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int lovf;
   __shared__ int wsum[MG_THREADS / 64];
@@ -1056,6 +1379,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t dummy = (uint32_t)H + (uint32_t)lane;
   const bool wide = !CNT1 && q.rw > 2;
+  const bool r12 = q.r12 != 0;  // narrow records arrive in the 12-byte form
   const int64_t wbase = wr[0];
   const bool evict = q.windowed && close0 != INT64_MIN;
   KLDS uint64_t* ids = mg_plane<uint64_t>(smem, 0);
@@ -1089,7 +1413,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
   longlong2 rec[AU], ext[AU], nrec[AU], next[AU];
   if (w < nwork) {
     it = mg_item(work, w, pbase);
-    mg_load<AU>(rec, ext, srec, it.rbase, it.rn, 0, q.rw, wide);
+    mg_load<AU>(rec, ext, srec, it.rbase, it.rn, 0, q.rw, wide, r12, tbase);
   }
   if (threadIdx.x == 0) lovf = 0;
   lds_barrier();  // otab / wtab / lovf
@@ -1104,7 +1428,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
     MgItem nit{};
     if (wnext < nwork) nit = mg_item(work, wnext, pbase);  // its loads are issued now, used later
     if (rn == 0 && first) {  // untouched partition: nothing to rewrite
-      if (wnext < nwork) mg_load<AU>(rec, ext, srec, nit.rbase, nit.rn, 0, q.rw, wide);
+      if (wnext < nwork) mg_load<AU>(rec, ext, srec, nit.rbase, nit.rn, 0, q.rw, wide, r12, tbase);
       it = nit;
       continue;
     }
@@ -1123,14 +1447,14 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
         if (lane >= off) incl += y;
       }
       if (lane == 63) wsum[wave] = incl;
-      __syncthreads();
+      lds_barrier();
       int before = 0, total = 0;
       for (int k = 0; k < NW; k++) {
         if (k < wave) before += wsum[k];
         total += wsum[k];
       }
       if (threadIdx.x == 0) lbase = total ? atomicAdd(closed_n, (unsigned long long)total) : 0ULL;
-      __syncthreads();
+      lds_barrier();
       uint64_t* dst = closed + (lbase + (uint64_t)(before + incl - ne)) * q.sw;
       for (int64_t r = threadIdx.x; r < nrow; r += MG_THREADS) {
         const uint64_t* row = src + r * q.sw;
@@ -1145,13 +1469,13 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
         nh = (int)wave_sum(nh);
         if (lane == 0 && nh) atomicAdd(hclosed, (unsigned long long)nh);
       }
-      __syncthreads();
+      lds_barrier();
     }
     MG_T(1);
     // 1. this item's records, chunk by chunk (chunk c + 1 in flight while c is applied)
     for (int64_t l0 = 0; l0 < rn; l0 += (int64_t)AU * MG_THREADS) {
       const bool more = l0 + (int64_t)AU * MG_THREADS < rn;
-      if (more) mg_load<AU>(nrec, next, srec, rbase, rn, l0 + (int64_t)AU * MG_THREADS, q.rw, wide);
+      if (more) mg_load<AU>(nrec, next, srec, rbase, rn, l0 + (int64_t)AU * MG_THREADS, q.rw, wide, r12, tbase);
       if (*(volatile KLDS int*)&lovf) break;
       if constexpr (CNT1) {
         // one window per record: w = ts / adv (TUMBLING) or 0 (no window); ts < 0: skip.  The AU
@@ -1198,7 +1522,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
 #pragma unroll
         for (int u = 0; u < AU; u++) {
           if (id[u] == EMPTY_ID || pend[u]) continue;
-          __hip_atomic_fetch_max(&rt[e[u]], (uint32_t)(rec[u].y - q.tbase + 1), WG_RLX);
+          __hip_atomic_fetch_max(&rt[e[u]], (uint32_t)(rec[u].y - tbase + 1), WG_RLX);
           __hip_atomic_fetch_add(&cnt1[e[u]], 1u, WG_RLX);
         }
       } else {
@@ -1208,7 +1532,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
         for (int u = 0; u < AU; u++) {
           const int64_t t = rec[u].y;
           const uint32_t meta = q.meta_word == 2 ? (uint32_t)ext[u].x : 0u;
-          trel[u] = (uint32_t)(t - q.tbase + 1);
+          trel[u] = (uint32_t)(t - tbase + 1);
           if (t < 0) {  // every window late (or past the end)
             w0[u] = 1;
             wn[u] = 0;
@@ -1326,16 +1650,16 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     MG_T(2);
     // the next item's first chunk is in flight from here on
-    if (wnext < nwork) mg_load<AU>(rec, ext, srec, nit.rbase, nit.rn, 0, q.rw, wide);
+    if (wnext < nwork) mg_load<AU>(rec, ext, srec, nit.rbase, nit.rn, 0, q.rw, wide, r12, tbase);
     if (lovf) {  // more groups than the table: retried with 2x sub-passes
       if (threadIdx.x == 0) fail[p] |= 1;
       for (int i = threadIdx.x; i < H; i += MG_THREADS) mg_clear(smem, ids, rt, otab, q.n_ops, i);
-      __syncthreads();
+      lds_barrier();
       if (threadIdx.x == 0) lovf = 0;
-      __syncthreads();
+      lds_barrier();
       it = nit;
       continue;
     }
@@ -1348,19 +1672,26 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
       if (e >= 0) rt[e] |= RT_MATCHED;  // one resident row per identity: a plain store
       n_mine += e != -2 ? 1 : 0;
     }
-    __syncthreads();
+    lds_barrier();
     for (int i = threadIdx.x; i < H; i += MG_THREADS) n_mine += (ids[i] != EMPTY_ID && !(rt[i] & RT_MATCHED)) ? 1 : 0;
     // 3. per-wave row counts → the partition's region range (one atomic per work item)
     const int wave_rows = (int)wave_sum(n_mine);
     if (lane == 0) wsum[wave] = wave_rows;
-    __syncthreads();
+    lds_barrier();
     int wave_before = 0, total = 0;
     for (int k = 0; k < NW; k++) {
       if (k < wave) wave_before += wsum[k];
       total += wsum[k];
     }
-    if (threadIdx.x == 0) lbase = total ? atomicAdd(&newcnt[p], (unsigned long long)total) : 0ULL;
-    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (work) {  // sub-passes of one partition append to its region
+        lbase = total ? atomicAdd(&newcnt[p], (unsigned long long)total) : 0ULL;
+      } else {  // the partition's only work item: no atomic round trip
+        lbase = 0;
+        newcnt[p] = (unsigned long long)total;
+      }
+    }
+    lds_barrier();
     MG_T(3);
     if ((int64_t)(lbase + total) > q.cmax) {
       if (threadIdx.x == 0) {
@@ -1368,7 +1699,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
         atomicMax(need, (unsigned long long)(lbase + total));
       }
       for (int i = threadIdx.x; i < H; i += MG_THREADS) mg_clear(smem, ids, rt, otab, q.n_ops, i);
-      __syncthreads();
+      lds_barrier();
       it = nit;
       continue;
     }
@@ -1390,7 +1721,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
         uint64_t w2 = row[2];
         if (e >= 0) {
           const uint32_t rr = rt[e] & ~RT_MATCHED;
-          const int64_t t = rr ? q.tbase + (int64_t)rr - 1 : INT64_MIN;
+          const int64_t t = rr ? tbase + (int64_t)rr - 1 : INT64_MIN;
           w2 = t > (int64_t)w2 ? (uint64_t)t : w2;
         }
         *(longlong2*)dst = make_longlong2((int64_t)row[0], (int64_t)row[1]);
@@ -1411,7 +1742,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
       }
       cur += __popcll(b);
     }
-    __syncthreads();  // resident rows have read their entries: the loop below clears them all
+    lds_barrier();  // resident rows have read their entries: the loop below clears them all
     for (int i0 = wave * 64; i0 < H; i0 += MG_THREADS) {  // delta entries, 64 per wave step
       const int e = i0 + lane;
       const uint64_t id = e < H ? ids[e] : EMPTY_ID;
@@ -1424,11 +1755,11 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
         *(longlong2*)dst = make_longlong2(key_of_hash(hk), ws);
         if constexpr (CNT1) {
           const uint32_t c = cnt1[e];
-          *(longlong2*)(dst + 2) = make_longlong2(q.tbase + (int64_t)rt[e] - 1, (int64_t)c);
+          *(longlong2*)(dst + 2) = make_longlong2(tbase + (int64_t)rt[e] - 1, (int64_t)c);
           if (q.having.active) nh += having_ok_words(c, 0, q.having);
         } else {
           for (int k = 2; k < q.sw; k += 2) {
-            const uint64_t a = k == 2 ? (uint64_t)(q.tbase + (int64_t)rt[e] - 1) : mg_word(wtab, smem, k, nullptr, e);
+            const uint64_t a = k == 2 ? (uint64_t)(tbase + (int64_t)rt[e] - 1) : mg_word(wtab, smem, k, nullptr, e);
             *(longlong2*)(dst + k) = make_longlong2((int64_t)a, (int64_t)mg_word(wtab, smem, k + 1, nullptr, e));
           }
           if (q.having.active)
@@ -1451,7 +1782,7 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
       nh = (int)wave_sum(nh);
       if (lane == 0 && nh) atomicAdd(&hnew[p], (unsigned long long)nh);
     }
-    __syncthreads();  // the table is clear for the next item
+    lds_barrier();  // the table is clear for the next item
     MG_T(4);
     it = nit;
   }
@@ -1460,12 +1791,20 @@ __global__ __launch_bounds__(MG_THREADS) void k_part_merge(
 
 // Window-index range of this push for the packed identity: the batch's windows plus the
 // live resident ones (res = conservative [min, max] window index of resident rows; rows of
-// windows closed before this push are evicted before they are encoded).  wr = [wbase, ok].
+// windows closed before this push are evicted before they are encoded).
+// wr = [wbase, identity ok, tmin, tmax, k_part_merge runs, rowtime base].  The aggregate kernel
+// is chosen here, on the device, so the host never waits between the scatter and the aggregate:
+// k_part_merge needs the packed identity and an event-time span below 2^31 - 2 ms (u32 rowtime
+// deltas); when it declines, the host re-runs pass 0 with k_part_agg after the push's one sync.
+// Also zeroes the pass counters and publishes the closed-store row count (no host copies).
 __global__ __launch_bounds__(1024) void k_part_wrange(const int64_t* __restrict__ tilemin,
                                                       const int64_t* __restrict__ tilemax, int64_t nT, int windowed,
                                                       int64_t size, int64_t adv, FastDiv fd, int64_t close0,
-                                                      int log2P, int fresh, int allow, int64_t* __restrict__ res,
-                                                      int64_t* __restrict__ wr /* [wbase, ok, tmin, tmax] */) {
+                                                      int log2P, int fresh, int allow, int merge_allow,
+                                                      int64_t* __restrict__ res, int64_t* __restrict__ wr,
+                                                      unsigned long long* __restrict__ ctr,
+                                                      unsigned long long* __restrict__ closed_ctr,
+                                                      unsigned long long closed_n) {
   __shared__ int64_t smin[16], smax[16];
   int64_t mn = INT64_MAX, mx = -1;
   for (int64_t t = threadIdx.x; t < nT; t += 1024) {
@@ -1489,6 +1828,10 @@ __global__ __launch_bounds__(1024) void k_part_wrange(const int64_t* __restrict_
   }
   wr[2] = mn;  // event-time span of the accepted records (INT64_MAX / -1: none)
   wr[3] = mx;
+  wr[5] = mx < 0 ? 0 : mn;
+  const bool span_ok = mx < 0 || mx - mn < ((int64_t)1 << 31) - 2;
+  ctr[0] = ctr[1] = ctr[2] = 0ULL;
+  if (closed_ctr) *closed_ctr = closed_n;
   int64_t lo = INT64_MAX, hi = INT64_MIN;
   if (mx >= 0) {  // some accepted record
     if (windowed) {
@@ -1514,18 +1857,23 @@ __global__ __launch_bounds__(1024) void k_part_wrange(const int64_t* __restrict_
   if (lo > hi) {  // nothing live, nothing new
     wr[0] = 0;
     wr[1] = fits;
+    wr[4] = merge_allow && fits && span_ok;
     res[0] = INT64_MAX;
     res[1] = INT64_MIN;
     return;
   }
   wr[0] = lo;
   wr[1] = fits && hi - lo < ((int64_t)1 << log2P) - 1;
+  wr[4] = merge_allow && wr[1] && span_ok;
   res[0] = lo;
   res[1] = hi;
 }
 
 // Publish the partitions processed in this pass (all touched ones, or the retry list).
-__global__ __launch_bounds__(256) void k_part_commit(int P, const int64_t* __restrict__ pbase,
+// gate (k_part_merge's pass 0): nothing to publish when k_part_wrange declined the merge.
+// out[11] = rows passing the query's HAVING over all live partitions (maintained: += new - old).
+__global__ __launch_bounds__(256) void k_part_commit(const int64_t* __restrict__ gate, int P,
+                                                     const int64_t* __restrict__ pbase,
                                                      const uint32_t* __restrict__ plist, int nlist,
                                                      uint8_t* __restrict__ sel, int64_t* __restrict__ cnt,
                                                      unsigned long long* __restrict__ newcnt,
@@ -1533,8 +1881,9 @@ __global__ __launch_bounds__(256) void k_part_commit(int P, const int64_t* __res
                                                      unsigned long long* __restrict__ out /* [new groups, failed] */,
                                                      unsigned long long* __restrict__ hcnt,
                                                      unsigned long long* __restrict__ hnew) {
+  if (gate && gate[4] == 0) return;
   const int k = blockIdx.x * 256 + threadIdx.x;
-  int64_t added = 0, failed = 0;
+  int64_t added = 0, failed = 0, hdelta = 0;
   if (plist ? k < nlist : k < P) {
     const uint32_t p = plist ? plist[k] : (uint32_t)k;
     if (plist || pbase[p + 1] > pbase[p]) {
@@ -1542,7 +1891,10 @@ __global__ __launch_bounds__(256) void k_part_commit(int P, const int64_t* __res
         added = (int64_t)newcnt[p] - cnt[p];
         cnt[p] = (int64_t)newcnt[p];
         sel[p] ^= 1;
-        if (hcnt) hcnt[p] = hnew[p];
+        if (hcnt) {
+          hdelta = (int64_t)hnew[p] - (int64_t)hcnt[p];
+          hcnt[p] = hnew[p];
+        }
       } else {
         failed = 1;
       }
@@ -1552,9 +1904,11 @@ __global__ __launch_bounds__(256) void k_part_commit(int P, const int64_t* __res
   }
   added = wave_sum(added);
   failed = wave_sum(failed);
+  hdelta = wave_sum(hdelta);
   if ((threadIdx.x & 63) == 0) {
     if (added) atomicAdd(&out[0], (unsigned long long)added);
     if (failed) atomicAdd(&out[1], (unsigned long long)failed);
+    if (hdelta) atomicAdd(&out[11], (unsigned long long)hdelta);
   }
 }
 
@@ -1702,7 +2056,7 @@ khip_status part_init(khip_agg* a, int64_t hint) {
     int n64 = 0, n32 = 0;
     for (int o = 0; o < a->ap.n_ops; o++) (a->ap.ops[o].kind == OP_INC || a->ap.ops[o].kind == OP_INC_VALID ? n32 : n64)++;
     const int mentry = 8 + 8 * n64 + 4 + 4 * n32;
-    const int64_t mbudget = knob("KHIP_MERGE_LDS_KB", 150) * 1024;  // one persistent workgroup per CU
+    const int64_t mbudget = knob("KHIP_MERGE_LDS_KB", 76) * 1024;  // two persistent workgroups per CU
     int mH = (int)std::min<int64_t>(16384, mbudget / mentry - 64) & ~63;
     s.mH = mH;
     const int ms = mH + 64;  // plane stride: H entries + one dummy entry per lane
@@ -1768,11 +2122,11 @@ khip_status part_init(khip_agg* a, int64_t hint) {
   KHIP_TRY(s.ctr.ensure(128));
   KHIP_TRY(s.hcnt.ensure(s.P * 8));
   KHIP_TRY(s.hnew.ensure(s.P * 8));
-  KHIP_TRY(s.hclosed.ensure(8));
   KHIP_TRY(s.pinfo.ensure(256));
   KHIP_TRY_HIP(hipMemsetAsync(s.hcnt.p, 0, s.P * 8, a->stream));
   KHIP_TRY_HIP(hipMemsetAsync(s.hnew.p, 0, s.P * 8, a->stream));
-  KHIP_TRY_HIP(hipMemsetAsync(s.hclosed.p, 0, 8, a->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(s.ctr.p, 0, 128, a->stream));
+  s.having_total = 0;
   s.hvalid = true;
   for (int b = 0; b < 2; b++) KHIP_TRY(s.buf[b].ensure((size_t)s.P * s.cmax * a->sw * 8));
   KHIP_TRY_HIP(hipMemsetAsync(s.sel.p, 0, s.P, a->stream));
@@ -1785,11 +2139,29 @@ khip_status part_init(khip_agg* a, int64_t hint) {
 void part_release(khip_agg* a) {
   PartState& s = a->part;
   s.pinfo.release();
-  DevBuf* bufs[] = {&s.hcnt, &s.hnew, &s.hclosed, &s.srecA, &s.hcoarse, &s.scan_tmpB, &s.RB, &s.wr, &s.res, &s.closed, &s.closed_ctr, &s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist,
+  DevBuf* bufs[] = {&s.hcnt, &s.hnew, &s.srecA, &s.hcoarse, &s.scan_tmpB, &s.RB, &s.wr, &s.res, &s.closed, &s.closed_ctr, &s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist,
                     &s.tilemax, &s.tilemin,
                     &s.tileprefix, &s.tpart, &s.scan_tmp, &s.srec, &s.work,
                     &s.pbase, &s.R, &s.ctr, &s.counts};
   for (DevBuf* b : bufs) b->release();
+}
+
+// Empty every partition (one launch for all per-partition state, the counters and the stream time).
+__global__ __launch_bounds__(256) void k_part_reset(int64_t P, unsigned long long* __restrict__ hcnt,
+                                                    unsigned long long* __restrict__ hnew, int64_t* __restrict__ cnt,
+                                                    unsigned long long* __restrict__ newcnt, uint8_t* __restrict__ fail,
+                                                    unsigned long long* __restrict__ ctr,
+                                                    int64_t* __restrict__ stream_time) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p < P) {
+    hcnt[p] = 0;
+    hnew[p] = 0;
+    cnt[p] = 0;
+    newcnt[p] = 0;
+    fail[p] = 0;
+  }
+  if (p < 16) ctr[p] = 0;
+  if (p == 0) *stream_time = -1;
 }
 
 khip_status part_reset(khip_agg* a) {
@@ -1797,12 +2169,12 @@ khip_status part_reset(khip_agg* a) {
   s.closed_n = 0;
   s.res_fresh = true;
   s.hvalid = true;
-  KHIP_TRY_HIP(hipMemsetAsync(s.hcnt.p, 0, s.P * 8, a->stream));
-  KHIP_TRY_HIP(hipMemsetAsync(s.hnew.p, 0, s.P * 8, a->stream));
-  KHIP_TRY_HIP(hipMemsetAsync(s.hclosed.p, 0, 8, a->stream));
-  KHIP_TRY_HIP(hipMemsetAsync(s.cnt.p, 0, s.P * 8, a->stream));
-  KHIP_TRY_HIP(hipMemsetAsync(s.newcnt.p, 0, s.P * 8, a->stream));
-  KHIP_TRY_HIP(hipMemsetAsync(s.fail.p, 0, s.P, a->stream));
+  s.having_total = 0;
+  hipLaunchKernelGGL(k_part_reset, dim3(ceil_div(std::max<int64_t>(s.P, 16), 256)), dim3(256), 0, a->stream, s.P,
+                     s.hcnt.as<unsigned long long>(), s.hnew.as<unsigned long long>(), s.cnt.as<int64_t>(),
+                     s.newcnt.as<unsigned long long>(), s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>(),
+                     a->stream_time.as<int64_t>());
+  KHIP_TRY_HIP(hipGetLastError());
   return KHIP_OK;
 }
 
@@ -1983,23 +2355,25 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   // aggregate kernel (k_part_merge needs the identity and a span below 2^31 ms)
   const PartAggParams q0 = part_params(a);
   const int64_t close0 = (a->windowed && a->host_stream_time >= 0) ? a->host_stream_time - a->grace : INT64_MIN;
-  KHIP_TRY(s.wr.ensure(32));
+  KHIP_TRY(s.wr.ensure(64));
   KHIP_TRY(s.res.ensure(16));
+  KHIP_TRY(s.closed_ctr.ensure(8));
+  const bool merge_allow = s.mH >= 256 && knob("KHIP_MERGE", 1) != 0;
   hipLaunchKernelGGL(k_part_wrange, dim3(1), dim3(1024), 0, a->stream, s.tilemin.as<int64_t>(), s.tilemax.as<int64_t>(),
                      nT, a->windowed, a->desc.size_ms, q0.adv, q0.fd, close0, s.log2P, s.res_fresh ? 1 : 0,
-                     (a->desc.flags & KHIP_FLAG_PART_CLAIM) ? 0 : 1, s.res.as<int64_t>(), s.wr.as<int64_t>());
+                     (a->desc.flags & KHIP_FLAG_PART_CLAIM) ? 0 : 1, merge_allow ? 1 : 0, s.res.as<int64_t>(),
+                     s.wr.as<int64_t>(), s.ctr.as<unsigned long long>(),
+                     a->windowed ? s.closed_ctr.as<unsigned long long>() : (unsigned long long*)nullptr,
+                     (unsigned long long)s.closed_n);
   s.res_fresh = false;
-  int64_t* pin = s.pinfo.as<int64_t>();
-  KHIP_TRY_HIP(hipMemcpyAsync(pin, s.wr.p, 32, hipMemcpyDeviceToHost, a->stream));
+  int64_t* pin = s.pinfo.as<int64_t>();  // wr[0..6), read after the pass-0 sync
+  KHIP_TRY_HIP(hipMemcpyAsync(pin, s.wr.p, 48, hipMemcpyDeviceToHost, a->stream));
   // 2. offsets
   hipLaunchKernelGGL(k_part_colsum, dim3(ceil_div(P, 256), TC), dim3(256), 0, a->stream, s.hist.as<uint32_t>(), nT, P,
                      TC, s.scan_tmp.as<int64_t>());
   hipLaunchKernelGGL(k_part_colbase, dim3(ceil_div(P, 256)), dim3(256), 0, a->stream, s.scan_tmp.as<int64_t>(), P, TC,
-                     s.R.as<int64_t>());
-  KHIP_TRY_HIP(hipMemcpyAsync(s.pbase.p, s.R.p, P * 8, hipMemcpyDeviceToDevice, a->stream));
-  KHIP_TRY_HIP(hipMemsetAsync(s.pbase.as<int64_t>() + P, 0, 8, a->stream));
-  hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, a->stream, s.pbase.as<int64_t>(), (int64_t)P,
-                     s.pbase.as<int64_t>() + P);
+                     s.pbase.as<int64_t>());
+  hipLaunchKernelGGL(k_part_pscan, dim3(1), dim3(1024), 0, a->stream, s.pbase.as<int64_t>(), (int64_t)P);
   hipLaunchKernelGGL(k_part_colprefix, dim3(ceil_div(P, 256), TC), dim3(256), 0, a->stream, s.hist.as<uint32_t>(), nT,
                      P, TC, s.scan_tmp.as<int64_t>(), s.pbase.as<int64_t>(), 1);
   if (lvl2) {  // bucket b's region = its partitions' regions [pbase[b << fbits], pbase[(b + 1) << fbits])
@@ -2011,28 +2385,37 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                        nT, B, TC, s.scan_tmpB.as<int64_t>(), s.pbase.as<int64_t>(), 1 << fbits);
   }
   ev_record_part(a, 1);
-  // 3. scatter
-    const bool narrow = s.rw == 2;
+  // 3. scatter (12-byte records for k_part_merge when the layout is narrow: r12_ok, decided
+  //    on the device by wr[4])
+  const bool narrow = s.rw == 2;
+  const int64_t r12_mode = knob("KHIP_R12", 1);  // 1: 12-byte records end to end; 2: pass A only
+  const bool r12_ok = narrow && !pad && merge_allow && r12_mode != 0;
+  const bool r12_merge = r12_ok && (r12_mode == 1 || !lvl2);  // what k_part_merge reads
   const int U = (int)knob("KHIP_SCATTER_U", narrow ? 8 : 16);
   auto scat = narrow ? (U >= 16 ? k_part_scatter<16, true> : (U >= 8 ? k_part_scatter<8, true> : k_part_scatter<4, true>))
                      : (U >= 16 ? k_part_scatter<16, false> : (U >= 8 ? k_part_scatter<8, false> : k_part_scatter<4, false>));
-  if (!lvl2 && hist_lds > 64 * 1024)
-    hipFuncSetAttribute((const void*)scat, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hist_lds);
-  hipLaunchKernelGGL(scat, dim3(nT), dim3(PT_THREADS), lvl2 ? (size_t)B * 4 : hist_lds, a->stream, keys, ts, kv, rv,
+  // narrow records leave through the LDS stage (stage_step): bins = B buckets (two-level) or P
+  const int nbins = lvl2 ? B : P;
+  const int Ut = U >= 16 ? 16 : (U >= 8 ? 8 : 4);  // the instantiated records per thread per step
+  const bool stage = narrow && !pad && nbins <= PT_THREADS && Ut <= 8 && knob("KHIP_STAGE", 1) != 0;
+  const size_t scat_lds = stage ? stage_lds_bytes(nbins, Ut * PT_THREADS) : (lvl2 ? (size_t)B * 4 : hist_lds);
+  if (scat_lds > 64 * 1024)
+    hipFuncSetAttribute((const void*)scat, hipFuncAttributeMaxDynamicSharedMemorySize, (int)scat_lds);
+  hipLaunchKernelGGL(scat, dim3(nT), dim3(PT_THREADS), scat_lds, a->stream, keys, ts, kv, rv,
                      cols, a->desc.n_cols, ct, n, tile, s.log2P - fbits, pad, nT,
                      lvl2 ? s.hcoarse.as<uint32_t>() : s.hist.as<uint32_t>(), s.pbase.as<int64_t>(),
                      s.tileprefix.as<int64_t>(),
                      s.tilemax.as<int64_t>(), s.tilemin.as<int64_t>(), a->windowed, a->desc.size_ms,
                      a->windowed ? a->desc.advance_ms : 1, make_fastdiv(a->windowed ? a->desc.advance_ms : 1),
                      a->grace, L, lvl2 ? s.srecA.as<uint64_t>() : s.srec.as<uint64_t>(), ncap,
-                     s.tpart.as<int64_t>());
+                     s.tpart.as<int64_t>(), s.wr.as<int64_t>(), r12_ok ? 1 : 0, stage ? 1 : 0);
   KHIP_TRY_HIP(hipGetLastError());
   if (lvl2) {
     const int64_t per_blk = knob("KHIP_REFINE_RECS", 8192);  // measured: 8K records per block (1 KB runs) beat 32K
     const int G = (int)std::max<int64_t>(1, std::min<int64_t>(nT, per_blk * B / tile));
     const int64_t ng = ceil_div(nT, G);
     void (*ref)(const uint64_t*, const uint32_t*, const uint32_t*, const int64_t*, int64_t, int, int, int, int64_t,
-                uint64_t*, int);
+                uint64_t*, int, const int64_t*, int, int);
     switch (s.rw) {
       case 2: ref = k_part_refine<2>; break;
       case 4: ref = k_part_refine<4>; break;
@@ -2041,18 +2424,19 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
       case 10: ref = k_part_refine<10>; break;
       default: ref = k_part_refine<12>; break;
     }
-    hipLaunchKernelGGL(ref, dim3((unsigned)(B * ng)), dim3(PT_THREADS), 0, a->stream, s.srecA.as<uint64_t>(),
+    const bool rstage = s.rw == 2 && (1 << fbits) <= PT_THREADS && knob("KHIP_STAGE", 1) != 0;
+    const size_t ref_lds = rstage ? stage_lds_bytes(1 << fbits, 8 * PT_THREADS) : 0;
+    if (ref_lds) hipFuncSetAttribute((const void*)ref, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ref_lds);
+    hipLaunchKernelGGL(ref, dim3((unsigned)(B * ng)), dim3(PT_THREADS), ref_lds, a->stream, s.srecA.as<uint64_t>(),
                        s.hcoarse.as<uint32_t>(), s.hist.as<uint32_t>(), s.pbase.as<int64_t>(), nT, G, s.log2P, fbits,
-                       ncap, s.srec.as<uint64_t>(), (int)knob("KHIP_REFINE_MODE", 0));
+                       ncap, s.srec.as<uint64_t>(), (int)knob("KHIP_REFINE_MODE", 0), s.wr.as<int64_t>(),
+                       r12_ok ? (r12_merge ? 1 : 2) : 0, rstage ? 1 : 0);
     KHIP_TRY_HIP(hipGetLastError());
   }
   ev_record_part(a, 2);
-  // 4. aggregate partitions (+ retries)
-  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));  // pin[] (the kernels above keep the GPU busy meanwhile)
-  const bool idm = pin[1] != 0;
-  const int64_t tmin = pin[2], tmax = pin[3];
-  const bool merge = idm && s.mH >= 256 && (tmax < 0 || tmax - tmin < (1LL << 31) - 2) && knob("KHIP_MERGE", 1) != 0;
-  if (!merge) s.hvalid = false;  // k_part_agg does not maintain the HAVING counts
+  // 4. aggregate partitions (+ retries).  k_part_merge is launched speculatively (it and its
+  //    commit exit when k_part_wrange declined it); pass 0 is then redone with k_part_agg.
+  bool merge = merge_allow;
   MergeParams mq{};
   if (merge) {
     mq.windowed = a->windowed;
@@ -2066,7 +2450,6 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     mq.size = q0.size;
     mq.adv = q0.adv;
     mq.fd = q0.fd;
-    mq.tbase = tmax < 0 ? 0 : tmin;
     for (int c = 0; c < MAX_COLS; c++) {
       mq.col_word[c] = s.col_word[c];
       mq.col_type[c] = a->ap.col_type[c];
@@ -2081,6 +2464,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     mq.init = a->init;
     mq.having = a->having;
     mq.dbg = (int32_t)knob("KHIP_MERGE_DEBUG", 0);
+    mq.r12 = r12_merge ? 1 : 0;
   }
   if (a->windowed) {  // worst case every live row closes in this push
     const int64_t live = a->occ - s.closed_n;
@@ -2096,8 +2480,6 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
       nc.p = nullptr;
       s.closed_cap = ncap;
     }
-    KHIP_TRY(s.closed_ctr.ensure(8));
-    KHIP_TRY_HIP(hipMemcpyAsync(s.closed_ctr.p, &s.closed_n, 8, hipMemcpyHostToDevice, a->stream));
   }
   int64_t added_total = 0;
   std::vector<uint8_t> host_fail;
@@ -2126,7 +2508,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     }
     q.cmax = s.cmax;
     mq.cmax = s.cmax;
-    KHIP_TRY_HIP(hipMemsetAsync(s.ctr.p, 0, 24, a->stream));
+    if (pass > 0) KHIP_TRY_HIP(hipMemsetAsync(s.ctr.p, 0, 24, a->stream));  // pass 0: k_part_wrange
     const uint32_t* wk = (pass == 0 && !subs0) ? nullptr : s.work.as<uint32_t>();
     const int64_t nwork = (pass == 0 && !subs0) ? P : (int64_t)work.size();
     if (merge) {
@@ -2136,13 +2518,13 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                         s.rw == 2 && a->desc.window_kind != KHIP_WINDOW_HOPPING;
       auto mk = cnt1 ? k_part_merge<true> : k_part_merge<false>;
       hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, s.m_lds);
-      const int64_t grid = std::min<int64_t>(nwork, (int64_t)s.n_cu * knob("KHIP_MERGE_WG_PER_CU", 1));
+      const int64_t grid = std::min<int64_t>(nwork, (int64_t)s.n_cu * knob("KHIP_MERGE_WG_PER_CU", 2));
       hipLaunchKernelGGL(mk, dim3(grid), dim3(MG_THREADS), s.m_lds, a->stream, mq, wk, nwork, s.pbase.as<int64_t>(),
                          s.srec.as<uint64_t>(), pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
                          s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
                          s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
                          s.closed_ctr.as<unsigned long long>(), s.wr.as<int64_t>(),
-                         s.hnew.as<unsigned long long>(), s.hclosed.as<unsigned long long>(), dbg);
+                         s.hnew.as<unsigned long long>(), s.ctr.as<unsigned long long>() + 12, dbg);
     } else {
       hipFuncSetAttribute((const void*)k_part_agg, hipFuncAttributeMaxDynamicSharedMemorySize, s.lds_bytes);
       hipLaunchKernelGGL(k_part_agg, dim3(nwork), dim3(AG_THREADS), s.lds_bytes, a->stream, q, wk,
@@ -2153,7 +2535,8 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                          s.closed_ctr.as<unsigned long long>(), s.wr.as<int64_t>(), dbg);
     }
     const int nl = pass == 0 ? P : (int)plist.size();
-    hipLaunchKernelGGL(k_part_commit, dim3(ceil_div(std::max(nl, 1), 256)), dim3(256), 0, a->stream, P,
+    hipLaunchKernelGGL(k_part_commit, dim3(ceil_div(std::max(nl, 1), 256)), dim3(256), 0, a->stream,
+                       (merge && pass == 0) ? s.wr.as<int64_t>() : (const int64_t*)nullptr, P,
                        s.pbase.as<int64_t>(), pass == 0 ? nullptr : s.work.as<uint32_t>() + work.size(), nl,
                        s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
                        s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>(), s.hcnt.as<unsigned long long>(),
@@ -2166,8 +2549,14 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                          a->stream_time.as<int64_t>(), s.ctr.as<unsigned long long>());
     }
     unsigned long long* c2 = s.pinfo.as<unsigned long long>() + 8;
-    KHIP_TRY_HIP(hipMemcpyAsync(c2, s.ctr.p, (pass == 0 ? 5 + T_NPART : 3) * 8, hipMemcpyDeviceToHost, a->stream));
+    KHIP_TRY_HIP(hipMemcpyAsync(c2, s.ctr.p, 13 * 8, hipMemcpyDeviceToHost, a->stream));
     KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+    if (pass == 0 && merge && pin[4] == 0) {  // declined on the device: nothing was written
+      merge = false;
+      s.hvalid = false;  // k_part_agg does not maintain the HAVING counts
+      pass = -1;
+      continue;
+    }
     added_total += (int64_t)c2[0];
     if (dbg && merge) {  // k_part_merge: per-phase time summed over its persistent workgroups
       unsigned long long ph[8] = {};
@@ -2205,6 +2594,11 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     KHIP_TRY_HIP(hipMemcpyAsync(s.work.p, both.data(), both.size() * 4, hipMemcpyHostToDevice, a->stream));
   }
   for (int p = 0; p < P; p++) s.psbits[p] = (uint8_t)std::max<int>(s.psbits[p], sbits[p]);
+  if (!merge) s.hvalid = false;
+  {
+    const unsigned long long* hc = s.pinfo.as<unsigned long long>() + 8;
+    s.having_total = (int64_t)(hc[11] + hc[12]);  // live rows + closed rows passing HAVING
+  }
   // 5. counters (k_part_stats after pass 0: evictions only happen there)
   const unsigned long long* st = s.pinfo.as<unsigned long long>() + 8;
   if (a->windowed) {
@@ -2225,33 +2619,13 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   return KHIP_OK;
 }
 
-__global__ __launch_bounds__(1024) void k_sum_counts(const unsigned long long* __restrict__ v, int64_t n,
-                                                     const unsigned long long* __restrict__ extra,
-                                                     unsigned long long* __restrict__ out) {
-  __shared__ unsigned long long acc;
-  if (threadIdx.x == 0) acc = 0;
-  __syncthreads();
-  int64_t x = 0;
-  for (int64_t i = threadIdx.x; i < n; i += 1024) x += (int64_t)v[i];
-  x = wave_sum(x);
-  if ((threadIdx.x & 63) == 0 && x) atomicAdd(&acc, (unsigned long long)x);
-  __syncthreads();
-  if (threadIdx.x == 0) *out = acc + *extra;
-}
-
-// The query's HAVING row count from the per-partition counts k_part_merge maintains (no scan of
-// the table).  Returns false when they are not valid (a push took a path that does not keep
-// them): the caller then scans.
+// The query's HAVING row count from the counts k_part_merge / k_part_commit maintain on the
+// device (copied back with every push's counters): no kernel, no table scan.  Returns false
+// when they are not valid (a push took a path that does not keep them): the caller then scans.
 bool part_having_count(khip_agg* a, int64_t* n) {
   PartState& s = a->part;
   if (!s.hvalid || !a->having.active) return false;
-  hipLaunchKernelGGL(k_sum_counts, dim3(1), dim3(1024), 0, a->stream, s.hcnt.as<unsigned long long>(), s.P,
-                     s.hclosed.as<unsigned long long>(), s.ctr.as<unsigned long long>() + 15);
-  unsigned long long* h = s.pinfo.as<unsigned long long>() + 24;
-  if (hipMemcpyAsync(h, s.ctr.as<unsigned long long>() + 15, 8, hipMemcpyDeviceToHost, a->stream) != hipSuccess ||
-      hipStreamSynchronize(a->stream) != hipSuccess)
-    return false;
-  *n = (int64_t)*h;
+  *n = s.having_total;
   return true;
 }
 
