@@ -328,13 +328,13 @@ __device__ __forceinline__ uint32_t stage_bin(uint64_t hk, int shift, uint32_t m
 }
 
 template <int U>
-__device__ __forceinline__ void stage_step(const uint64_t (&hk)[U], const int64_t (&pay)[U], const bool (&ok)[U],
+__device__ __forceinline__ void stage_step(const int64_t (&hk)[U], const int64_t (&pay)[U], const bool (&ok)[U],
                                            int shift, uint32_t mask, int nb, const StageLds& L,
                                            uint64_t* __restrict__ srec, int out, int64_t tbase) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   uint32_t rank[U];
 #pragma unroll
-  for (int u = 0; u < U; u++) rank[u] = ok[u] ? atomicAdd(&L.cnt[stage_bin(hk[u], shift, mask)], 1u) : 0u;
+  for (int u = 0; u < U; u++) rank[u] = ok[u] ? atomicAdd(&L.cnt[stage_bin((uint64_t)hk[u], shift, mask)], 1u) : 0u;
   lds_barrier();
   // exclusive scan of the bin counts (nb <= PT_THREADS)
   const uint32_t c = t < nb ? L.cnt[t] : 0u;
@@ -360,8 +360,8 @@ __device__ __forceinline__ void stage_step(const uint64_t (&hk)[U], const int64_
 #pragma unroll
   for (int u = 0; u < U; u++) {
     if (!ok[u]) continue;
-    const uint32_t i = L.sbase[stage_bin(hk[u], shift, mask)] + rank[u];
-    L.sk[i] = hk[u];
+    const uint32_t i = L.sbase[stage_bin((uint64_t)hk[u], shift, mask)] + rank[u];
+    L.sk[i] = (uint64_t)hk[u];
     L.sp[i] = pay[u];
   }
   lds_barrier();
@@ -479,11 +479,9 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
     for (; s0 < end; s0 += S) {
       const int64_t i0 = s0 + threadIdx.x;
       if (s0 + S < end) load_step(i0 + S, nxx, nxk);
-      uint64_t hk[U];
-      int64_t pay[U];
       bool ok[U];
 #pragma unroll
-      for (int u = 0; u < U; u++) {
+      for (int u = 0; u < U; u++) {  // in place: k → key hash, x → payload
         const int64_t i = i0 + (int64_t)u * PT_THREADS;
         ok[u] = i < end && x[u] >= 0 && bit_get(kv, i) && bit_get(rv, i);
         if (windowed) {
@@ -493,10 +491,10 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
         } else {
           c_app += ok[u] ? 1 : 0;
         }
-        hk[u] = key_hash(k[u]);  // records carry the key hash (key = its inverse)
-        pay[u] = r12 ? x[u] - tbase + 1 : x[u];
+        k[u] = (int64_t)key_hash(k[u]);  // records carry the key hash (key = its inverse)
+        x[u] = r12 ? x[u] - tbase + 1 : x[u];
       }
-      stage_step<U>(hk, pay, ok, log2P == 0 ? 64 : 64 - log2P, (uint32_t)(P - 1), P, SL, srec, r12 ? 1 : 0, tbase);
+      stage_step<U>(k, x, ok, log2P == 0 ? 64 : 64 - log2P, (uint32_t)(P - 1), P, SL, srec, r12 ? 1 : 0, tbase);
 #pragma unroll
       for (int u = 0; u < U; u++) {
         x[u] = nxx[u];
@@ -697,26 +695,25 @@ __device__ __forceinline__ void refine_range(const uint64_t* __restrict__ srcA, 
 }
 
 // refine_range through the LDS stage (narrow records): out as in stage_step
-template <bool N12>
+template <bool N12, int U>
 __device__ __forceinline__ void refine_staged(const uint64_t* __restrict__ srcA, const StageLds& SL, int64_t lo,
                                               int64_t hi, int log2P, int F, uint64_t* __restrict__ srec, int out,
                                               int64_t tbase) {
-  constexpr int U = 8;
   constexpr int S = U * PT_THREADS;
-  uint64_t hk[U], nhk[U];
+  int64_t hk[U], nhk[U];
   int64_t pay[U], npay[U];
-  auto load_step = [&](int64_t i0, uint64_t (&dh)[U], int64_t (&dp)[U]) {
+  auto load_step = [&](int64_t i0, int64_t (&dh)[U], int64_t (&dp)[U]) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
       int64_t i = i0 + (int64_t)u * PT_THREADS;
       i = i < hi ? i : hi - 1;
       if constexpr (N12) {
         const R12 v = *(const R12*)((const char*)srcA + (uint64_t)i * 12);
-        dh[u] = (uint64_t)v.hi << 32 | v.lo;
+        dh[u] = (int64_t)((uint64_t)v.hi << 32 | v.lo);
         dp[u] = (int64_t)v.trel;
       } else {
         const longlong2 v = *(const longlong2*)(srcA + (uint64_t)i * 2);
-        dh[u] = (uint64_t)v.x;
+        dh[u] = v.x;
         dp[u] = v.y;
       }
     }
@@ -760,7 +757,7 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_refine(const uint64_t* __re
   if (RW == 2 && stage) {  // narrow records through the LDS stage
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int wsum[PT_THREADS / 64];
-    const StageLds SL = stage_carve(smem, F, 8 * PT_THREADS, wsum);
+    const StageLds SL = stage_carve(smem, F, stage * PT_THREADS, wsum);  // stage = records per thread
     for (int f = threadIdx.x; f < F; f += PT_THREADS) {
       SL.cur[f] = offs[t0 * P + ((int64_t)b << fbits) + f];
       SL.cnt[f] = 0u;
@@ -769,8 +766,14 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_refine(const uint64_t* __re
     const int64_t hi = t1 < nT ? (int64_t)offA[t1 * B + b] : pbase[(int64_t)(b + 1) << fbits];
     lds_barrier();
     if (hi <= lo) return;
-    if (r12_ok && wr[4] != 0) refine_staged<true>(srcA, SL, lo, hi, log2P, F, srec, r12_ok == 2 ? 2 : 1, wr[5]);
-    else refine_staged<false>(srcA, SL, lo, hi, log2P, F, srec, 0, 0);
+    const bool n12 = r12_ok && wr[4] != 0;
+    if (stage >= 8) {
+      if (n12) refine_staged<true, 8>(srcA, SL, lo, hi, log2P, F, srec, r12_ok == 2 ? 2 : 1, wr[5]);
+      else refine_staged<false, 8>(srcA, SL, lo, hi, log2P, F, srec, 0, 0);
+    } else {
+      if (n12) refine_staged<true, 4>(srcA, SL, lo, hi, log2P, F, srec, r12_ok == 2 ? 2 : 1, wr[5]);
+      else refine_staged<false, 4>(srcA, SL, lo, hi, log2P, F, srec, 0, 0);
+    }
     return;
   }
   for (int f = threadIdx.x; f < F; f += PT_THREADS) cur[f] = offs[t0 * P + ((int64_t)b << fbits) + f];
@@ -1173,7 +1176,9 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
 //      instruction covers consecutive rows; count the rows passing the query's HAVING
 // A partition whose deltas overflow H writes nothing and is retried with 2x sub-passes (it
 // has already moved its closed rows in pass 0; retries skip them).
-constexpr int MG_THREADS = 512;  // two persistent workgroups per CU (one's LDS work hides the other's latency)
+// k_part_merge workgroup size: 512 threads, two persistent workgroups per CU (one's global
+// round trips hidden by the other's LDS work; measured on C2: 256 x 4 needs 2^15 partitions
+// to fit its tables and loses more in the hist/refine than it gains)
 constexpr uint32_t RT_MATCHED = 0x80000000u;
 
 struct MergeParams {
@@ -1281,7 +1286,7 @@ __device__ __forceinline__ int mg_find(const MergeParams& q, const KLDS uint64_t
 
 // One chunk of a partition's scattered records: AU per thread, rows l0 + tid + u * MG_THREADS.
 // r12: 12-byte narrow records (key hash, trel) → (key hash, ts); trel 0 → ts -1 (no window)
-template <int AU>
+template <int AU, int NT>
 __device__ __forceinline__ void mg_load(longlong2 (&rec)[AU], longlong2 (&ext)[AU], const uint64_t* __restrict__ srec,
                                         int64_t rbase, int64_t rn, int64_t l0, int rw, bool wide, bool r12,
                                         int64_t tbase) {
@@ -1289,7 +1294,7 @@ __device__ __forceinline__ void mg_load(longlong2 (&rec)[AU], longlong2 (&ext)[A
     R12 v[AU];
 #pragma unroll
     for (int u = 0; u < AU; u++) {
-      const int64_t li = l0 + threadIdx.x + (int64_t)u * MG_THREADS;
+      const int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
       v[u] = li < rn ? *(const R12*)((const char*)srec + (uint64_t)(rbase + li) * 12) : R12{0u, 0u, 0u};
     }
 #pragma unroll
@@ -1300,7 +1305,7 @@ __device__ __forceinline__ void mg_load(longlong2 (&rec)[AU], longlong2 (&ext)[A
   }
 #pragma unroll
   for (int u = 0; u < AU; u++) {
-    const int64_t li = l0 + threadIdx.x + (int64_t)u * MG_THREADS;
+    const int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
     const longlong2* r = (const longlong2*)(srec + (uint64_t)(rbase + li) * rw);
     rec[u] = li < rn ? r[0] : make_longlong2(0, -1);
     if (wide) ext[u] = li < rn ? r[1] : make_longlong2(0, 0);
@@ -1354,8 +1359,8 @@ __device__ __forceinline__ void mg_clear(char* smem, KLDS uint64_t* ids, KLDS ui
 // resident-merge and write-out, and inside an item chunk c + 1 is loaded before chunk c is
 // applied, so HBM latency overlaps the LDS work; the write-out leaves every delta entry cleared
 // for the next item (no separate table init).
-template <bool CNT1>
-__global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
+template <bool CNT1, int NT>
+__global__ __launch_bounds__(NT, 4) void k_part_merge(
     MergeParams q, const uint32_t* __restrict__ work, int64_t nwork, const int64_t* __restrict__ pbase,
     const uint64_t* __restrict__ srec, int first, uint64_t* __restrict__ buf0, uint64_t* __restrict__ buf1,
     const uint8_t* __restrict__ sel, const int64_t* __restrict__ cnt, unsigned long long* __restrict__ newcnt,
@@ -1369,12 +1374,12 @@ __global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
   const int64_t tbase = wr[5];
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int lovf;
-  __shared__ int wsum[MG_THREADS / 64];
+  __shared__ int wsum[NT / 64];
   __shared__ unsigned long long lbase;
   __shared__ MgWord wtab[32];
   __shared__ MgOp otab[MAX_OPS];
   constexpr int AU = CNT1 ? 4 : 2;  // records per thread per chunk (two chunks in registers)
-  constexpr int NW = MG_THREADS / 64;
+  constexpr int NW = NT / 64;
   const int H = q.H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t dummy = (uint32_t)H + (uint32_t)lane;
@@ -1413,11 +1418,11 @@ __global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
   longlong2 rec[AU], ext[AU], nrec[AU], next[AU];
   if (w < nwork) {
     it = mg_item(work, w, pbase);
-    mg_load<AU>(rec, ext, srec, it.rbase, it.rn, 0, q.rw, wide, r12, tbase);
+    mg_load<AU, NT>(rec, ext, srec, it.rbase, it.rn, 0, q.rw, wide, r12, tbase);
   }
   if (threadIdx.x == 0) lovf = 0;
   lds_barrier();  // otab / wtab / lovf
-  for (int i = threadIdx.x; i < H + 64; i += MG_THREADS) mg_clear(smem, ids, rt, otab, q.n_ops, i);
+  for (int i = threadIdx.x; i < H + 64; i += NT) mg_clear(smem, ids, rt, otab, q.n_ops, i);
   lds_barrier();
   MG_T(0);
   for (; w < nwork; w += gridDim.x) {
@@ -1428,7 +1433,7 @@ __global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
     MgItem nit{};
     if (wnext < nwork) nit = mg_item(work, wnext, pbase);  // its loads are issued now, used later
     if (rn == 0 && first) {  // untouched partition: nothing to rewrite
-      if (wnext < nwork) mg_load<AU>(rec, ext, srec, nit.rbase, nit.rn, 0, q.rw, wide, r12, tbase);
+      if (wnext < nwork) mg_load<AU, NT>(rec, ext, srec, nit.rbase, nit.rn, 0, q.rw, wide, r12, tbase);
       it = nit;
       continue;
     }
@@ -1437,7 +1442,7 @@ __global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
     // 0. closed resident rows → closed store (pass 0 only; retries skip them)
     if (evict && first) {
       int ne = 0, nh = 0;
-      for (int64_t r = threadIdx.x; r < nrow; r += MG_THREADS) {
+      for (int64_t r = threadIdx.x; r < nrow; r += NT) {
         const uint64_t* row = src + r * q.sw;
         ne += ((int64_t)row[1] + q.size <= close0) && sub_ok(key_hash((int64_t)row[0]), (int64_t)row[1], sbits, sub);
       }
@@ -1456,7 +1461,7 @@ __global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
       if (threadIdx.x == 0) lbase = total ? atomicAdd(closed_n, (unsigned long long)total) : 0ULL;
       lds_barrier();
       uint64_t* dst = closed + (lbase + (uint64_t)(before + incl - ne)) * q.sw;
-      for (int64_t r = threadIdx.x; r < nrow; r += MG_THREADS) {
+      for (int64_t r = threadIdx.x; r < nrow; r += NT) {
         const uint64_t* row = src + r * q.sw;
         if (!((int64_t)row[1] + q.size <= close0) ||
             !sub_ok(key_hash((int64_t)row[0]), (int64_t)row[1], sbits, sub))
@@ -1473,9 +1478,9 @@ __global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
     }
     MG_T(1);
     // 1. this item's records, chunk by chunk (chunk c + 1 in flight while c is applied)
-    for (int64_t l0 = 0; l0 < rn; l0 += (int64_t)AU * MG_THREADS) {
-      const bool more = l0 + (int64_t)AU * MG_THREADS < rn;
-      if (more) mg_load<AU>(nrec, next, srec, rbase, rn, l0 + (int64_t)AU * MG_THREADS, q.rw, wide, r12, tbase);
+    for (int64_t l0 = 0; l0 < rn; l0 += (int64_t)AU * NT) {
+      const bool more = l0 + (int64_t)AU * NT < rn;
+      if (more) mg_load<AU, NT>(nrec, next, srec, rbase, rn, l0 + (int64_t)AU * NT, q.rw, wide, r12, tbase);
       if (*(volatile KLDS int*)&lovf) break;
       if constexpr (CNT1) {
         // one window per record: w = ts / adv (TUMBLING) or 0 (no window); ts < 0: skip.  The AU
@@ -1601,7 +1606,7 @@ __global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
             if (!act[u]) continue;
             __hip_atomic_fetch_max(&rt[e[u]], trel[u], WG_RLX);
             const uint32_t vmask = q.meta_word == 2 ? ((uint32_t)ext[u].x >> 16) : 0u;
-            const int64_t gi = rbase + l0 + threadIdx.x + (int64_t)u * MG_THREADS;
+            const int64_t gi = rbase + l0 + threadIdx.x + (int64_t)u * NT;
             for (int o = 0; o < q.n_ops; o++) {
               const MgOp op = otab[o];
               if (op.kind == OP_INC) {
@@ -1653,10 +1658,10 @@ __global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
     lds_barrier();
     MG_T(2);
     // the next item's first chunk is in flight from here on
-    if (wnext < nwork) mg_load<AU>(rec, ext, srec, nit.rbase, nit.rn, 0, q.rw, wide, r12, tbase);
+    if (wnext < nwork) mg_load<AU, NT>(rec, ext, srec, nit.rbase, nit.rn, 0, q.rw, wide, r12, tbase);
     if (lovf) {  // more groups than the table: retried with 2x sub-passes
       if (threadIdx.x == 0) fail[p] |= 1;
-      for (int i = threadIdx.x; i < H; i += MG_THREADS) mg_clear(smem, ids, rt, otab, q.n_ops, i);
+      for (int i = threadIdx.x; i < H; i += NT) mg_clear(smem, ids, rt, otab, q.n_ops, i);
       lds_barrier();
       if (threadIdx.x == 0) lovf = 0;
       lds_barrier();
@@ -1665,7 +1670,7 @@ __global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
     }
     // 2. resident rows: mark the delta entries they absorb; count live rows
     int n_mine = 0;
-    for (int64_t r0 = 0; r0 < nrow; r0 += MG_THREADS) {
+    for (int64_t r0 = 0; r0 < nrow; r0 += NT) {
       const int64_t r = r0 + threadIdx.x;
       if (r >= nrow) break;
       const int e = mg_find(q, ids, src + r * q.sw, evict, close0, sbits, sub, wbase, H);
@@ -1673,7 +1678,7 @@ __global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
       n_mine += e != -2 ? 1 : 0;
     }
     lds_barrier();
-    for (int i = threadIdx.x; i < H; i += MG_THREADS) n_mine += (ids[i] != EMPTY_ID && !(rt[i] & RT_MATCHED)) ? 1 : 0;
+    for (int i = threadIdx.x; i < H; i += NT) n_mine += (ids[i] != EMPTY_ID && !(rt[i] & RT_MATCHED)) ? 1 : 0;
     // 3. per-wave row counts → the partition's region range (one atomic per work item)
     const int wave_rows = (int)wave_sum(n_mine);
     if (lane == 0) wsum[wave] = wave_rows;
@@ -1698,7 +1703,7 @@ __global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
         fail[p] |= 2;
         atomicMax(need, (unsigned long long)(lbase + total));
       }
-      for (int i = threadIdx.x; i < H; i += MG_THREADS) mg_clear(smem, ids, rt, otab, q.n_ops, i);
+      for (int i = threadIdx.x; i < H; i += NT) mg_clear(smem, ids, rt, otab, q.n_ops, i);
       lds_barrier();
       it = nit;
       continue;
@@ -1710,7 +1715,7 @@ __global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
     const uint64_t lt = (1ULL << lane) - 1;
     const int hv = q.having.a.w_val, hc = q.having.a.w_cnt;
     int nh = 0;
-    for (int64_t r0 = 0; r0 < nrow; r0 += MG_THREADS) {
+    for (int64_t r0 = 0; r0 < nrow; r0 += NT) {
       const int64_t r = r0 + threadIdx.x;
       const uint64_t* row = src + (r < nrow ? r : 0) * q.sw;
       const int e = r < nrow ? mg_find(q, ids, row, evict, close0, sbits, sub, wbase, H) : -2;
@@ -1743,7 +1748,7 @@ __global__ __launch_bounds__(MG_THREADS, 4) void k_part_merge(
       cur += __popcll(b);
     }
     lds_barrier();  // resident rows have read their entries: the loop below clears them all
-    for (int i0 = wave * 64; i0 < H; i0 += MG_THREADS) {  // delta entries, 64 per wave step
+    for (int i0 = wave * 64; i0 < H; i0 += NT) {  // delta entries, 64 per wave step
       const int e = i0 + lane;
       const uint64_t id = e < H ? ids[e] : EMPTY_ID;
       const bool isnew = id != EMPTY_ID && !(rt[e] & RT_MATCHED);
@@ -2425,12 +2430,13 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
       default: ref = k_part_refine<12>; break;
     }
     const bool rstage = s.rw == 2 && (1 << fbits) <= PT_THREADS && knob("KHIP_STAGE", 1) != 0;
-    const size_t ref_lds = rstage ? stage_lds_bytes(1 << fbits, 8 * PT_THREADS) : 0;
+    const int ru = knob("KHIP_REFINE_U", 8) >= 8 ? 8 : 4;  // records per thread per staged step
+    const size_t ref_lds = rstage ? stage_lds_bytes(1 << fbits, ru * PT_THREADS) : 0;
     if (ref_lds) hipFuncSetAttribute((const void*)ref, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ref_lds);
     hipLaunchKernelGGL(ref, dim3((unsigned)(B * ng)), dim3(PT_THREADS), ref_lds, a->stream, s.srecA.as<uint64_t>(),
                        s.hcoarse.as<uint32_t>(), s.hist.as<uint32_t>(), s.pbase.as<int64_t>(), nT, G, s.log2P, fbits,
                        ncap, s.srec.as<uint64_t>(), (int)knob("KHIP_REFINE_MODE", 0), s.wr.as<int64_t>(),
-                       r12_ok ? (r12_merge ? 1 : 2) : 0, rstage ? 1 : 0);
+                       r12_ok ? (r12_merge ? 1 : 2) : 0, rstage ? ru : 0);
     KHIP_TRY_HIP(hipGetLastError());
   }
   ev_record_part(a, 2);
@@ -2516,10 +2522,12 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
       // and (key hash, ts) records with one window each (TUMBLING or no window: no meta word)
       const bool cnt1 = a->ap.n_ops == 1 && a->ap.ops[0].kind == OP_INC && a->ap.ops[0].word == 3 && a->sw == 4 &&
                         s.rw == 2 && a->desc.window_kind != KHIP_WINDOW_HOPPING;
-      auto mk = cnt1 ? k_part_merge<true> : k_part_merge<false>;
+      const int mt = (int)knob("KHIP_MERGE_THREADS", 512);
+      auto mk = mt >= 512 ? (cnt1 ? k_part_merge<true, 512> : k_part_merge<false, 512>)
+                          : (cnt1 ? k_part_merge<true, 256> : k_part_merge<false, 256>);
       hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, s.m_lds);
-      const int64_t grid = std::min<int64_t>(nwork, (int64_t)s.n_cu * knob("KHIP_MERGE_WG_PER_CU", 2));
-      hipLaunchKernelGGL(mk, dim3(grid), dim3(MG_THREADS), s.m_lds, a->stream, mq, wk, nwork, s.pbase.as<int64_t>(),
+      const int64_t grid = std::min<int64_t>(nwork, (int64_t)s.n_cu * knob("KHIP_MERGE_WG_PER_CU", mt >= 512 ? 2 : 4));
+      hipLaunchKernelGGL(mk, dim3(grid), dim3(mt >= 512 ? 512 : 256), s.m_lds, a->stream, mq, wk, nwork, s.pbase.as<int64_t>(),
                          s.srec.as<uint64_t>(), pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
                          s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
                          s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
