@@ -13,14 +13,49 @@ pieces of libksqldb_hip.so:
 
 The result feeds khip_agg_push exactly like a batch read back from the repartition topic:
 records from source rank 0 first, then rank 1, ..., each source's records in arrival order.
+
+The exchange is pluggable: `abi.Comm` (RCCL over xGMI, one process per GPU, the production
+path) or `GlooExchange` (any torch.distributed process group, rows staged through host memory:
+the CPU tests, and several ranks sharing one GPU, where RCCL refuses duplicate devices).
 """
 from . import abi
+
+
+class GlooExchange:
+    """The same two collective steps as abi.Comm.alltoall (counts, then rows laid out by source
+    rank) over a torch.distributed group, through host memory."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.nranks = dist.get_world_size(group)
+
+    def alltoall(self, send, send_counts, row_words):
+        import torch
+        dist = self.dist
+        if len(send_counts) != self.nranks:
+            raise ValueError("send_counts has %d entries, world is %d" % (len(send_counts), self.nranks))
+        sc = torch.tensor(list(send_counts), dtype=torch.int64)
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(rc, sc, group=self.group)
+        rcounts = [int(x) for x in rc.tolist()]
+        n_send = int(sc.sum())
+        dev = send.device if send is not None else torch.device("cpu")
+        hsend = (send[:n_send].to("cpu") if send is not None and n_send
+                 else torch.empty((0, row_words), dtype=torch.int64)).contiguous()
+        hrecv = torch.empty((sum(rcounts), row_words), dtype=torch.int64)
+        dist.all_to_all_single(hrecv.view(-1), hsend.view(-1), [c * row_words for c in rcounts],
+                               [int(c) * row_words for c in send_counts], group=self.group)
+        if hrecv.shape[0] == 0:
+            hrecv = torch.zeros((1, row_words), dtype=torch.int64)
+        return hrecv.to(dev), rcounts
 
 
 class Repartition:
     def __init__(self, lib, key_col, col_types, rank=0, world=1, comm=None, device=0):
         if world > 1 and comm is None:
-            raise ValueError("world > 1 needs an RCCL communicator (abi.Comm)")
+            raise ValueError("world > 1 needs an exchange (abi.Comm over RCCL, or GlooExchange)")
         self.world = world
         self.rank = rank
         self.comm = comm

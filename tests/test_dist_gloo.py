@@ -94,3 +94,93 @@ def test_key_sharded_union_equals_single_task():
     assert np.array_equal(cnt[order], ref["values"][0])
     assert np.array_equal(rt[order], ref["rowtime"])
     assert cnt.sum() == WORLD * N
+
+
+# ------------------------------------------------------------------ repartition across ranks
+# a non-key GROUP BY is one exchange step.  Each rank is one source task:
+# pack (the contract restated on the oracle's Kafka partitioner, tests/shuffle_ref.py) →
+# GlooExchange (the two collective steps abi.Comm runs over RCCL, here over gloo) → unpack →
+# aggregate (oracle).  Rank 0 checks what each task received and the union of the tables.
+
+SH_N = 20_000
+SH_COLS = ["INT64", "INT64"]  # region_id (the new key), amount
+
+
+def _shuffle_desc():
+    return abi.make_agg_desc(window_kind="TUMBLING", size_ms=60_000, key_type="INT64", col_types=SH_COLS,
+                             aggs=[("SUM", 1), ("COUNT_STAR", -1)])
+
+
+def _shuffle_worker(rank, port, q):
+    from shuffle_ref import expected_pack, expected_unpack
+    from ksql_amd.repartition import GlooExchange
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        orc = abi.load_oracle()
+        eid, ts, region, amount = synth.repartition_sum(0, SH_N, SH_N, rank=rank, world=WORLD, regions=300)
+        n = len(ts)
+        ones = np.ones(n, bool)
+        rows, counts = expected_pack(orc, 0, [region, amount], [ones, ones], ones, ts, WORLD)
+        ex = GlooExchange()
+        recv, rcounts = ex.alltoall(torch.from_numpy(rows), counts, rows.shape[1])
+        recv = recv[:sum(rcounts)].numpy()
+        key, rts, cols, valid = expected_unpack(recv, 0, SH_COLS)
+        h = abi.AggHandle(orc, _shuffle_desc())
+        h.push(abi.HostBatch(rts, keys=key, cols=cols, col_valid=valid))
+        s = h.snapshot()
+        h.close()
+        out = {"src": (region, ts, amount), "recv": recv, "rcounts": rcounts,
+               "snap": (s["key"], s["ws"], s["values"][0], s["values"][1], s["rowtime"])}
+        gathered = [None] * WORLD
+        dist.all_gather_object(gathered, out)
+        if rank == 0:
+            q.put(gathered)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_repartition_exchange_across_ranks():
+    from shuffle_ref import expected_pack, kafka_partition
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shuffle_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    g = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    orc = abi.load_oracle()
+    # task d receives source 0's rows for d, then source 1's, each in arrival order
+    packs = []
+    for s in range(WORLD):
+        region, ts, amount = g[s]["src"]
+        ones = np.ones(len(ts), bool)
+        packs.append(expected_pack(orc, 0, [region, amount], [ones, ones], ones, ts, WORLD))
+    for d in range(WORLD):
+        exp = np.concatenate([rows[sum(c[:d]):sum(c[:d + 1])] for rows, c in packs])
+        assert g[d]["rcounts"] == [c[d] for _, c in packs]
+        np.testing.assert_array_equal(g[d]["recv"], exp)
+        # every received key routes here
+        assert (kafka_partition(orc, g[d]["recv"][:, 0], 8, WORLD) == d).all()
+    # tasks own disjoint new keys; union of their tables == one task over every record
+    keys = [set(g[d]["snap"][0].tolist()) for d in range(WORLD)]
+    assert not (keys[0] & keys[1])
+    allr = np.concatenate([g[s]["src"][0] for s in range(WORLD)])
+    allt = np.concatenate([g[s]["src"][1] for s in range(WORLD)])
+    alla = np.concatenate([g[s]["src"][2] for s in range(WORLD)])
+    h = abi.AggHandle(orc, _shuffle_desc())
+    h.push(abi.HostBatch(allt, keys=allr, cols=[allr, alla]))
+    ref = h.snapshot()
+    h.close()
+    k, ws, sm, cn, rt = (np.concatenate([g[d]["snap"][i] for d in range(WORLD)]) for i in range(5))
+    o = np.lexsort((ws, k))
+    np.testing.assert_array_equal(k[o], ref["key"])
+    np.testing.assert_array_equal(ws[o], ref["ws"])
+    np.testing.assert_array_equal(sm[o], ref["values"][0])
+    np.testing.assert_array_equal(cn[o], ref["values"][1])
+    np.testing.assert_array_equal(rt[o], ref["rowtime"])
+    assert cn.sum() == WORLD * SH_N

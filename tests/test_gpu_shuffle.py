@@ -16,6 +16,7 @@ import torch
 
 from ksql_amd import abi, synth
 from ksql_amd.repartition import Repartition
+from shuffle_ref import expected_pack, kafka_partition
 
 pytestmark = pytest.mark.gpu
 
@@ -31,43 +32,7 @@ def orc():
 
 
 def _kafka_partition(orc, keys, width, n_parts):
-    keys = np.ascontiguousarray(keys, dtype=np.int64)
-    out = np.zeros(len(keys), np.int32)
-    orc.dll.oracle_kafka_partition(keys.ctypes.data, len(keys), width, n_parts, out.ctypes.data)
-    return out
-
-
-def _raw_i64(col):
-    if col.dtype == np.float64:
-        return col.view(np.int64)
-    return col.astype(np.int64)
-
-
-def expected_pack(orc, key_col, cols, col_valid, row_valid, ts, n_parts):
-    """Oracle-side restatement of khip_shuffle_pack: (rows int64 [m, 2+nc], counts)."""
-    n = len(ts)
-    width = 4 if cols[key_col].dtype == np.int32 else 8
-    ok = row_valid & col_valid[key_col] & (ts >= 0)
-    dest = _kafka_partition(orc, cols[key_col], width, n_parts)
-    nc = len(cols)
-    words = np.zeros((n, 2 + nc), np.int64)
-    words[:, 0] = cols[key_col].astype(np.int64)
-    words[:, 1] = ts
-    vm = np.zeros(n, np.int64)
-    w = 2
-    for c in range(nc):
-        vm |= (col_valid[c].astype(np.int64) << c)
-        if c == key_col:
-            continue
-        words[:, w] = np.where(col_valid[c], _raw_i64(cols[c]), 0)
-        w += 1
-    words[:, w] = vm
-    rows, counts = [], []
-    for d in range(n_parts):
-        sel = np.nonzero(ok & (dest == d))[0]  # arrival order
-        rows.append(words[sel])
-        counts.append(len(sel))
-    return np.concatenate(rows), counts
+    return kafka_partition(orc, keys, width, n_parts)
 
 
 def _random_source(n, key_type, seed, null_frac=0.05):
@@ -265,3 +230,77 @@ def test_rccl_single_rank_alltoall(prod):
     assert out.struct.n_rows == n
     comm.close()
     rp.close()
+
+
+# ---- two source tasks in two processes (both on cuda:0), rows exchanged over gloo ----------
+import os
+import socket
+
+import torch.multiprocessing as mp
+
+MP_WORLD = 2
+MP_N = 60_000
+
+
+def _mp_worker(rank, port, q):
+    import torch.distributed as dist
+    from ksql_amd.repartition import GlooExchange
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=MP_WORLD)
+    try:
+        torch.cuda.init()
+        prod = abi.load_product()
+        eid, ts, region, amount = synth.repartition_sum(0, MP_N, MP_N, xp="torch", device="cuda", rank=rank,
+                                                        world=MP_WORLD, regions=400)
+        rp = Repartition(prod, 0, ["INT64", "INT64"], rank=rank, world=MP_WORLD, comm=GlooExchange())
+        out = rp(abi.DeviceBatch(ts, cols=[region, amount]))
+        h = abi.AggHandle(prod, _agg_desc())
+        h.push(out)
+        s = h.snapshot()
+        h.close()
+        res = {"src": tuple(t.cpu().numpy() for t in (region, ts, amount)), "counts": rp.last_counts,
+               "snap": (s["key"], s["ws"], s["values"][0], s["values"][1], s["rowtime"])}
+        rp.close()
+        gathered = [None] * MP_WORLD
+        dist.all_gather_object(gathered, res)
+        if rank == 0:
+            q.put(gathered)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_process_repartition_gloo(orc):
+    """Product pack → exchange between two processes → product unpack → product aggregate, per
+    task equal to the oracle over the rows Kafka's partitioner routes to it (source order)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_mp_worker, args=(r, port, q)) for r in range(MP_WORLD)]
+    for p in procs:
+        p.start()
+    g = q.get(timeout=100)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for d in range(MP_WORLD):
+        rk, rts, ramt = [], [], []
+        for src in range(MP_WORLD):
+            region, ts, amount = g[src]["src"]
+            sel = _kafka_partition(orc, region, 8, MP_WORLD) == d
+            rk.append(region[sel]), rts.append(ts[sel]), ramt.append(amount[sel])
+        assert g[d]["counts"][1] == [g[src]["counts"][0][d] for src in range(MP_WORLD)]
+        rk, rts, ramt = np.concatenate(rk), np.concatenate(rts), np.concatenate(ramt)
+        ho = abi.AggHandle(orc, _agg_desc())
+        ho.push(abi.HostBatch(rts, keys=rk, cols=[rk, ramt]))
+        exp = ho.snapshot()
+        ho.close()
+        key, ws, sm, cn, rt = g[d]["snap"]
+        np.testing.assert_array_equal(key, exp["key"])
+        np.testing.assert_array_equal(ws, exp["ws"])
+        np.testing.assert_array_equal(sm, exp["values"][0])
+        np.testing.assert_array_equal(cn, exp["values"][1])
+        np.testing.assert_array_equal(rt, exp["rowtime"])
