@@ -223,7 +223,9 @@ khip_status khip_agg_result_type(const khip_agg_desc* desc, int32_t agg_index,
 khip_status khip_agg_push(khip_agg* agg, const khip_batch* batch,
                           khip_batch_stats* stats);
 
-/* Number of rows and key bytes the next snapshot will produce (no HAVING). */
+/* Number of rows and key bytes the next snapshot will produce (no HAVING).  Snapshots, pull
+ * queries and row counts read the window store: windows with start < obs - retention (obs =
+ * the largest window start put, i.e. floor(streamTime / advance) * advance) have expired. */
 khip_status khip_agg_snapshot_size(khip_agg* agg, int64_t* n_rows,
                                    int64_t* key_bytes);
 
@@ -252,6 +254,25 @@ typedef struct khip_pull {
  * over the HBM-resident state; only matching rows cross PCIe. */
 khip_status khip_agg_get(khip_agg* agg, const khip_pull* q, const khip_having* having,
                          khip_snapshot* out);
+
+/* ---- Emission (the aggregate's output topic: the table's changelog).
+ * One push = one commit of Kafka Streams' record cache (C/util/KsqlConstants.java:40-41): the
+ * rows a push emits are deduplicated per (key, window), carry their value after the push, and
+ * are sorted by (key, window start).  Pushing one record at a time reproduces the reference's
+ * cache-off output sequence exactly (QTT, tests/test_gpu_emit.py).
+ *   EMIT CHANGES (needs KHIP_FLAG_CHANGELOG): every (key, window) the push updated; with the
+ *     descriptor's HAVING (S/TableFilterBuilder.java:63-75) a row that no longer passes but did
+ *     before the push is a tombstone, one that passed neither before nor after is not emitted.
+ *   EMIT FINAL (S/StreamAggregateBuilder.java:282-285, EmitStrategy.onWindowClose): every window
+ *     the push closed (window end <= stream time - grace), emitted once with its final value
+ *     unless it had already expired from the window store (retention) at the record that closed
+ *     it, then filtered by the descriptor's HAVING.
+ * khip_agg_changes_size returns the row count and (UTF8) key bytes of the last push's rows;
+ * khip_agg_changes writes them in snapshot layout plus tombstone[n_rows] (1 = delete; may be
+ * NULL).  Valid until the next push or reset. */
+#define KHIP_FLAG_CHANGELOG 8
+khip_status khip_agg_changes_size(khip_agg* agg, int64_t* n_rows, int64_t* key_bytes);
+khip_status khip_agg_changes(khip_agg* agg, khip_snapshot* out, uint8_t* tombstone);
 
 /* Count the rows that pass `having` entirely on the device (no copy-out).
  * having may be NULL (= total group count).  When `having` is the descriptor's own HAVING,

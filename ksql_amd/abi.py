@@ -33,6 +33,7 @@ MEM_HOST, MEM_DEVICE = 0, 1
 FLAG_PROFILE = 1
 FLAG_ENGINE_ATOMIC = 2
 FLAG_PART_CLAIM = 4
+FLAG_CHANGELOG = 8
 RETENTION_DEFAULT = -1
 EMIT = {"CHANGES": 0, "FINAL": 1}
 NP_TYPE = {0: np.int32, 1: np.int64, 2: np.float64}
@@ -129,6 +130,8 @@ SIGS = {
     "agg_snapshot_size": ([_P, C.POINTER(i64), C.POINTER(i64)]),
     "agg_snapshot": ([_P, C.POINTER(Having), C.POINTER(Snapshot)]),
     "agg_destroy": ([_P]),
+    "agg_changes_size": ([_P, C.POINTER(i64), C.POINTER(i64)]),
+    "agg_changes": ([_P, C.POINTER(Snapshot), _P]),
     "table_create": ([C.POINTER(TableDesc), C.POINTER(_P)]),
     "table_upsert": ([_P, C.POINTER(Batch)]),
     "table_size": ([_P, C.POINTER(i64)]),
@@ -198,6 +201,10 @@ class Lib:
             self.dll.oracle_agg_snapshot_size_sharded.restype = i32
             self.dll.oracle_agg_snapshot_sharded.argtypes = [C.POINTER(_P), i32, C.POINTER(Having), C.POINTER(Snapshot)]
             self.dll.oracle_agg_snapshot_sharded.restype = i32
+            self.dll.oracle_agg_changes_size_sharded.argtypes = [C.POINTER(_P), i32, C.POINTER(i64), C.POINTER(i64)]
+            self.dll.oracle_agg_changes_size_sharded.restype = i32
+            self.dll.oracle_agg_changes_sharded.argtypes = [C.POINTER(_P), i32, C.POINTER(Snapshot), _P]
+            self.dll.oracle_agg_changes_sharded.restype = i32
 
     def check(self, status, what):
         if status != KHIP_OK:
@@ -353,6 +360,22 @@ class AggHandle:
         return self._materialize(having, lambda hv, s: self.lib.agg_snapshot(self.h, hv, s), "agg_snapshot",
                                  raw_keys=raw_keys)
 
+    def changes(self, raw_keys=False):
+        """Rows the last push emitted downstream (khip_agg_changes): snapshot layout sorted by
+        (key, ws), plus "tombstone" (bool per row: a HAVING delete)."""
+        return self._changes(self.lib.agg_changes_size, lambda s, t: self.lib.agg_changes(self.h, s, t), raw_keys)
+
+    def _changes(self, size_fn, call, raw_keys):
+        n, kb = i64(), i64()
+        self.lib.check(size_fn(self.h, C.byref(n), C.byref(kb)), "agg_changes_size")
+        cap = max(n.value, 1)
+        tomb = np.zeros(cap, np.uint8)
+        out, st, _ = self._materialize_into(None, lambda hv, s: call(s, tomb.ctypes.data), cap, max(kb.value, 1),
+                                            raw_keys)
+        self.lib.check(st, "agg_changes")
+        out["tombstone"] = tomb[:out["n"]].astype(bool)
+        return out
+
     def get(self, keys=None, ws=(None, None), we=(None, None), having=None):
         """Pull query (khip_agg_get): rows of `keys` (None = every key) whose WINDOWSTART and
         WINDOWEND lie in the closed bounds (None = unbounded), sorted by (key, ws)."""
@@ -491,6 +514,11 @@ class ShardedOracleAgg(AggHandle):
     def snapshot(self, having=None, raw_keys=False):
         return self._materialize(having, lambda hv, s: self._snap(self._hs, self.P, hv, s), "agg_snapshot_sharded",
                                  raw_keys=raw_keys)
+
+    def changes(self, raw_keys=False):
+        d = self.lib.dll
+        return self._changes(lambda h, n, kb: d.oracle_agg_changes_size_sharded(self._hs, self.P, n, kb),
+                             lambda s, t: d.oracle_agg_changes_sharded(self._hs, self.P, s, t), raw_keys)
 
     def _materialize(self, having, call, what, cap=None, raw_keys=False):
         if cap is None:

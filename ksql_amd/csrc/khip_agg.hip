@@ -79,6 +79,64 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(const int64_t* __restrict_
   if (threadIdx.x == 0) *stream_time = carry;
 }
 
+// EMIT FINAL (S/StreamAggregateBuilder.java:282-285, Kafka Streams EmitStrategy.onWindowClose):
+// with the emission check after every record, a window is emitted by the record whose stream
+// time first reaches ws + size + grace, unless the window store had already expired it there:
+// the store's observed time is then floor(M / adv) * adv (M = that record's stream time), so
+// the window is lost iff ws < floor(M / adv) * adv - retention.  That needs M to jump into a later
+// advance bucket in one record.  Per record (arrival order, accepted rows only; prefix = stream
+// time before each RPB block): a record that moves the stream time from Mp to M > Mp with
+// floor(M / adv) > floor(Mp / adv) loses the window starts in
+//   [Mp - size - grace + 1, min(M - size - grace, floor(M / adv) * adv - retention - 1)]
+// (rounded to multiples of adv); non-empty ranges are appended to lost[] as (lo, hi) pairs.
+__global__ __launch_bounds__(BLOCK) void k_emit_lost(const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
+                                                     const uint8_t* __restrict__ rv, int64_t n,
+                                                     const int64_t* __restrict__ prefix, int64_t size, int64_t adv,
+                                                     int64_t grace, int64_t retention, int64_t* __restrict__ lost,
+                                                     int64_t cap, unsigned long long* __restrict__ ctr) {
+  __shared__ int64_t lmax[BLOCK];
+  const int64_t i0 = (int64_t)blockIdx.x * RPB + (int64_t)threadIdx.x * ITEMS;
+  int64_t m = -1;
+  for (int k = 0; k < ITEMS; k++) {
+    const int64_t i = i0 + k;
+    if (i < n && bit_get(kv, i) && bit_get(rv, i) && ts[i] > m) m = ts[i];
+  }
+  lmax[threadIdx.x] = m;
+  __syncthreads();
+  for (int off = 1; off < BLOCK; off <<= 1) {  // inclusive prefix max over the block's threads
+    const int64_t y = threadIdx.x >= off ? lmax[threadIdx.x - off] : -1;
+    __syncthreads();
+    if (y > lmax[threadIdx.x]) lmax[threadIdx.x] = y;
+    __syncthreads();
+  }
+  int64_t mp = prefix[blockIdx.x];
+  if (threadIdx.x > 0 && lmax[threadIdx.x - 1] > mp) mp = lmax[threadIdx.x - 1];
+  const int64_t sg = size + grace;
+  for (int k = 0; k < ITEMS; k++) {
+    const int64_t i = i0 + k;
+    if (i >= n || !bit_get(kv, i) || !bit_get(rv, i)) continue;
+    const int64_t t = ts[i];
+    if (t <= mp) continue;
+    const int64_t bp = mp < 0 ? -1 : mp / adv, b = t / adv;
+    if (b > bp) {
+      int64_t lo = mp - sg + 1;
+      int64_t hi = t - sg;
+      const int64_t exp_hi = b * adv - retention - 1;
+      hi = hi < exp_hi ? hi : exp_hi;
+      lo = lo < 0 ? 0 : lo;
+      lo = (lo + adv - 1) / adv * adv;  // window starts are multiples of adv
+      if (lo <= hi) {
+        const unsigned long long slot = atomicAdd(ctr, 1ULL);
+        if ((int64_t)slot < cap) {
+          lost[2 * slot] = lo;
+          lost[2 * slot + 1] = hi;
+        }
+      }
+    }
+    mp = t;
+  }
+}
+
 // Find or claim the (key, ws) slot and apply the record's aggregate updates.
 // Claim reference: bit63 | fp15 << 48 | window index j << 36 | batch row (36 bits).
 __device__ __forceinline__ int upsert_apply(const ApplyParams& p, uint64_t* __restrict__ table,
@@ -686,6 +744,72 @@ static khip_status grow_dict(khip_agg* a, int64_t new_cap) {
   return KHIP_OK;
 }
 
+namespace khip {
+
+int64_t visible_from(const khip_agg* a) {
+  if (!a->windowed || a->host_stream_time < 0) return INT64_MIN;
+  const int64_t adv = a->desc.advance_ms;
+  return a->host_stream_time / adv * adv - a->retention;  // the store's observed time - retention
+}
+
+// EMIT FINAL: the window starts this batch closes after they expired (k_emit_lost), computed from
+// the batch alone before the engine runs; collected by finish_lost() after the push's sync.
+khip_status emit_final_lost(khip_agg* a, const int64_t* ts, const uint8_t* kv, const uint8_t* rv, int64_t n,
+                            int64_t, const int64_t*) {
+  const int64_t nb = ceil_div(n, RPB);
+  KHIP_TRY(a->blockmax.ensure(nb * 8));
+  KHIP_TRY(a->blockprefix.ensure(nb * 8 + 8));
+  KHIP_TRY(a->lostctr.ensure(16));
+  if (a->lost_cap == 0) {
+    a->lost_cap = 4096;
+    KHIP_TRY(a->lostbuf.ensure((size_t)a->lost_cap * 16));
+  }
+  int64_t* seed = a->blockprefix.as<int64_t>() + nb;  // stream time before the batch
+  KHIP_TRY(a->part.pinfo.ensure(512));
+  int64_t* hs = a->part.pinfo.as<int64_t>() + 24;
+  hs[0] = a->st_before;
+  KHIP_TRY_HIP(hipMemcpyAsync(seed, hs, 8, hipMemcpyHostToDevice, a->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(a->lostctr.p, 0, 8, a->stream));
+  hipLaunchKernelGGL(k_blockmax, dim3(nb), dim3(BLOCK), 0, a->stream, ts, kv, rv, n, a->blockmax.as<int64_t>());
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, a->stream, a->blockmax.as<int64_t>(), nb,
+                     a->blockprefix.as<int64_t>(), seed);
+  hipLaunchKernelGGL(k_emit_lost, dim3(nb), dim3(BLOCK), 0, a->stream, ts, kv, rv, n, a->blockprefix.as<int64_t>(),
+                     a->desc.size_ms, a->desc.advance_ms, a->grace, a->retention, a->lostbuf.as<int64_t>(), a->lost_cap,
+                     a->lostctr.as<unsigned long long>());
+  KHIP_TRY_HIP(hipGetLastError());
+  return KHIP_OK;
+}
+
+// After the push's sync: the lost ranges → host (sorted, merged); re-run with room if the
+// buffer overflowed (the batch is still valid: the caller owns it until the push returns).
+static khip_status finish_lost(khip_agg* a, const int64_t* ts, const uint8_t* kv, const uint8_t* rv, int64_t n) {
+  int64_t cnt = 0;
+  KHIP_TRY_HIP(hipMemcpy(&cnt, a->lostctr.p, 8, hipMemcpyDeviceToHost));
+  if (cnt > a->lost_cap) {
+    a->lost_cap = next_pow2(cnt);
+    a->lostbuf.release();
+    KHIP_TRY(a->lostbuf.ensure((size_t)a->lost_cap * 16));
+    KHIP_TRY(emit_final_lost(a, ts, kv, rv, n, 0, nullptr));
+    KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+    KHIP_TRY_HIP(hipMemcpy(&cnt, a->lostctr.p, 8, hipMemcpyDeviceToHost));
+  }
+  std::vector<std::pair<int64_t, int64_t>> r((size_t)cnt);
+  if (cnt) KHIP_TRY_HIP(hipMemcpy(r.data(), a->lostbuf.p, (size_t)cnt * 16, hipMemcpyDeviceToHost));
+  std::sort(r.begin(), r.end());
+  a->lost.clear();
+  for (auto& x : r) {
+    if (!a->lost.empty() && x.first <= a->lost.back() + 1) {
+      a->lost.back() = std::max(a->lost.back(), x.second);
+    } else {
+      a->lost.push_back(x.first);
+      a->lost.push_back(x.second);
+    }
+  }
+  return KHIP_OK;
+}
+
+}  // namespace khip
+
 extern "C" {
 
 khip_status khip_agg_result_type(const khip_agg_desc* d, int32_t i, int32_t* out) {
@@ -767,6 +891,13 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
   }
   a->profile = (d.flags & KHIP_FLAG_PROFILE) != 0;
   a->engine = (d.flags & KHIP_FLAG_ENGINE_ATOMIC) ? 1 : 0;
+  a->changelog = (d.flags & KHIP_FLAG_CHANGELOG) != 0 && d.emit == KHIP_EMIT_CHANGES;
+  if (a->windowed)
+    a->retention = d.retention_ms == KHIP_RETENTION_DEFAULT ? a->desc.size_ms + a->grace : d.retention_ms;
+  if (a->changelog && a->engine == 1) {
+    khip_agg_destroy(a);
+    return fail(KHIP_E_UNSUPPORTED, "EMIT CHANGES changelog needs the partitioned engine");
+  }
   if (a->profile)
     for (int e = 0; e < 8; e++) hipEventCreate(&a->ev[e]);
   int64_t cap = a->engine == 1 ? next_pow2(std::max<int64_t>(1024, d.capacity_hint > 0 ? d.capacity_hint * 2 : 1 << 16))
@@ -814,11 +945,18 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   DeviceGuard g(a->device);
   khip_batch_stats s{};
   s.rows_in = n;
-  if (n == 0) {
+  a->st_before = a->host_stream_time;
+  a->chg_ready = false;
+  a->lost.clear();
+  if (n == 0) {  // nothing changes, nothing closes
+    a->chg_ready = true;
+    a->chg_n = 0;
     s.stream_time = a->host_stream_time;
     if (stats) *stats = s;
     return KHIP_OK;
   }
+  if (a->changelog && n >= (1LL << 31)) return fail(KHIP_E_UNSUPPORTED, "changelog pushes above 2^31 rows");
+  const bool final_emit = a->desc.emit == KHIP_EMIT_FINAL;
   // ---- device pointers (stage host batches)
   const int64_t* keys = b->key_i64;
   const int64_t* ts = b->ts;
@@ -864,6 +1002,7 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   } else {
     return fail(KHIP_E_INVALID, "batch mem");
   }
+  if (final_emit) KHIP_TRY(emit_final_lost(a, ts, kv, rv, n, 0, nullptr));
   // ---- UTF8 keys → stable key ids
   const int64_t* hkeys = keys;
   if (utf8) {
@@ -999,6 +1138,13 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
     KHIP_TRY_HIP(hipMemcpyAsync(&a->host_stream_time, a->stream_time.p, 8, hipMemcpyDeviceToHost, a->stream));
     KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
   }
+  if (final_emit) KHIP_TRY(finish_lost(a, ts, kv, rv, n));
+  if (a->engine == 0 && a->windowed) {  // retention: drop expired windows from the closed store
+    HavingDev vis{};
+    vis.vis = 1;
+    vis.vis_from = visible_from(a);
+    if (vis.vis_from != INT64_MIN) KHIP_TRY(part_purge_closed(a, vis));
+  }
   s.rows_accepted = tot[P_ACCEPTED];
   s.dropped_null_key = tot[P_NULL_KEY];
   s.dropped_null_row = tot[P_NULL_ROW];
@@ -1010,10 +1156,25 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   return KHIP_OK;
 }
 
+// No row of the table has expired (retention) yet: every group counted in occ is visible.  The
+// partitioned engine purges its closed store after every push; its live rows satisfy
+// ws + size > (stream time before the last push) - grace, so they are all visible while that
+// bound is at or above the first visible window start.  The atomic engine keeps every row.
+static bool no_expired_live(const khip_agg* a) {
+  const int64_t vf = visible_from(a);
+  if (vf == INT64_MIN) return true;
+  if (a->engine != 0 || a->st_before < 0) return false;
+  return vf <= a->st_before - a->grace - a->desc.size_ms + 1;
+}
+
 static khip_status compact_rows(khip_agg* a, const khip_having* h, std::vector<uint64_t>* rows, int64_t* count,
                                 const HavingDev* pull = nullptr) {
   HavingDev hd{};
   if (pull) hd = *pull;
+  if (a->windowed && !hd.fin) {  // the store: expired windows are gone (retention)
+    hd.vis = 1;
+    hd.vis_from = visible_from(a);
+  }
   if (h) {
     if (h->agg_index < 0 || h->agg_index >= a->desc.n_aggs) return fail(KHIP_E_INVALID, "having agg index");
     if (h->op < KHIP_OP_GT || h->op > KHIP_OP_NE) return fail(KHIP_E_INVALID, "having op");
@@ -1058,7 +1219,7 @@ khip_status khip_agg_count_rows(khip_agg* a, const khip_having* h, int64_t* n) {
   if (h && a->engine == 0 && a->desc.has_having && h->agg_index == a->desc.having.agg_index &&
       h->op == a->desc.having.op && h->i64 == a->desc.having.i64 &&
       (h->f64 == a->desc.having.f64 || (h->f64 != h->f64 && a->desc.having.f64 != a->desc.having.f64)) &&
-      part_having_count(a, n))
+      no_expired_live(a) && part_having_count(a, n))
     return KHIP_OK;
   return compact_rows(a, h, nullptr, n);
 }
@@ -1067,7 +1228,10 @@ khip_status khip_agg_snapshot_size(khip_agg* a, int64_t* n_rows, int64_t* key_by
   clear_error();
   if (!a) return fail(KHIP_E_INVALID, "null argument");
   DeviceGuard g(a->device);
-  if (n_rows) *n_rows = a->occ;
+  if (n_rows) {
+    *n_rows = a->occ;
+    if (!no_expired_live(a)) KHIP_TRY(compact_rows(a, nullptr, nullptr, n_rows));
+  }
   if (key_bytes) {
     if (a->desc.key_type == KHIP_KEY_UTF8) {
       std::vector<uint64_t> rows;
@@ -1087,7 +1251,8 @@ khip_status khip_agg_snapshot_size(khip_agg* a, int64_t* n_rows, int64_t* key_by
 
 // Sort compacted rows by (key, window start) and write them to the caller's snapshot buffers
 // (ResultTransformer map() + WindowBoundsPopulator).
-static khip_status emit_snapshot(khip_agg* a, const std::vector<uint64_t>& rows, int64_t n, khip_snapshot* out) {
+static khip_status emit_snapshot(khip_agg* a, const std::vector<uint64_t>& rows, int64_t n, khip_snapshot* out,
+                                 const std::vector<uint8_t>* tomb_in = nullptr, uint8_t* tomb_out = nullptr) {
   const int sw = a->sw;
   const bool utf8 = a->desc.key_type == KHIP_KEY_UTF8;
   std::vector<uint8_t> arena;
@@ -1119,6 +1284,7 @@ static khip_status emit_snapshot(khip_agg* a, const std::vector<uint64_t>& rows,
   for (int64_t r = 0; r < n; r++) {
     const uint64_t* s = &rows[order[r] * sw];
     const int64_t key = (int64_t)s[0], ws = (int64_t)s[1];
+    if (tomb_out) tomb_out[r] = tomb_in ? (*tomb_in)[order[r]] : 0;
     if (utf8) {
       const int64_t len = klen(key);
       if (kb + len > out->key_bytes_capacity) return fail(KHIP_E_BUFFER, "snapshot key bytes capacity too small");
@@ -1243,10 +1409,72 @@ khip_status khip_agg_get(khip_agg* a, const khip_pull* q, const khip_having* h, 
   return emit_snapshot(a, rows, n, out);
 }
 
+// The rows the last push emitted (khip_agg_changes), computed once per push on first request.
+static khip_status compute_changes(khip_agg* a) {
+  if (a->chg_ready) return KHIP_OK;
+  a->chg_rows.clear();
+  a->chg_tomb.clear();
+  a->chg_n = 0;
+  if (a->desc.emit == KHIP_EMIT_FINAL) {
+    // windows closed by the push and still visible when they closed, passing HAVING
+    HavingDev fd{};
+    fd.fin = 1;
+    fd.fin_c0 = a->st_before - a->grace;
+    fd.fin_c1 = a->host_stream_time - a->grace;
+    fd.fin_size = a->desc.size_ms;
+    DevBuf dl;
+    if (!a->lost.empty()) {
+      KHIP_TRY(dl.ensure(a->lost.size() * 8));
+      KHIP_TRY_HIP(hipMemcpyAsync(dl.p, a->lost.data(), a->lost.size() * 8, hipMemcpyHostToDevice, a->stream));
+      fd.lost = dl.as<int64_t>();
+      fd.n_lost = (int32_t)(a->lost.size() / 2);
+    }
+    if (fd.fin_c1 > fd.fin_c0)
+      KHIP_TRY(compact_rows(a, a->desc.has_having ? &a->desc.having : nullptr, &a->chg_rows, &a->chg_n, &fd));
+    a->chg_tomb.assign((size_t)a->chg_n, 0);
+  } else if (a->changelog) {
+    KHIP_TRY(part_changes(a, &a->chg_rows, &a->chg_tomb, &a->chg_n));
+  } else {
+    return fail(KHIP_E_STATE, "handle created without KHIP_FLAG_CHANGELOG (EMIT CHANGES)");
+  }
+  a->chg_ready = true;
+  return KHIP_OK;
+}
+
+khip_status khip_agg_changes_size(khip_agg* a, int64_t* n_rows, int64_t* key_bytes) {
+  clear_error();
+  if (!a) return fail(KHIP_E_INVALID, "null argument");
+  DeviceGuard g(a->device);
+  KHIP_TRY(compute_changes(a));
+  if (n_rows) *n_rows = a->chg_n;
+  if (key_bytes) {
+    int64_t kb = 0;
+    if (a->desc.key_type == KHIP_KEY_UTF8 && a->chg_n) {
+      std::vector<uint8_t> arena(a->arena_used);
+      if (a->arena_used) KHIP_TRY_HIP(hipMemcpy(arena.data(), a->arena.p, a->arena_used, hipMemcpyDeviceToHost));
+      for (int64_t r = 0; r < a->chg_n; r++) kb += *(const int64_t*)(arena.data() + a->chg_rows[r * a->sw] + 8);
+    }
+    *key_bytes = kb;
+  }
+  return KHIP_OK;
+}
+
+khip_status khip_agg_changes(khip_agg* a, khip_snapshot* out, uint8_t* tombstone) {
+  clear_error();
+  if (!a || !out) return fail(KHIP_E_INVALID, "null argument");
+  DeviceGuard g(a->device);
+  KHIP_TRY(compute_changes(a));
+  return emit_snapshot(a, a->chg_rows, a->chg_n, out, &a->chg_tomb, tombstone);
+}
+
 khip_status khip_agg_reset(khip_agg* a) {
   clear_error();
   if (!a) return fail(KHIP_E_INVALID, "null argument");
   DeviceGuard g(a->device);
+  a->chg_ready = true;
+  a->chg_n = 0;
+  a->st_before = -1;
+  a->lost.clear();
   if (a->engine == 0) {
     KHIP_TRY(part_reset(a));  // also the stream time
   } else {
@@ -1295,7 +1523,7 @@ khip_status khip_agg_destroy(khip_agg* a) {
   DevBuf* bufs[] = {&a->table, &a->blockmax, &a->blockprefix, &a->partials, &a->resume, &a->counters,
                     &a->stream_time, &a->st_keys, &a->st_ts, &a->st_kv, &a->st_rv, &a->st_koff,
                     &a->st_kbytes, &a->kid, &a->khash, &a->dword, &a->dkid, &a->arena, &a->dict_bsum,
-                    &a->dict_fail};
+                    &a->dict_fail, &a->chg, &a->lostbuf, &a->lostctr};
   for (DevBuf* b : bufs) b->release();
   for (int c = 0; c < MAX_COLS; c++) {
     a->st_cols[c].release();

@@ -68,9 +68,39 @@ struct HavingDev {
   // partitioned engine, > 256 keys: keys grouped by partition (sorted within each), offsets P+1
   const int64_t* pkeys;
   const int64_t* pkoff;
+  // window store retention (RETENTION, default size + grace; S/StreamAggregateBuilder.java:293,
+  // 322,350): rows with ws < vis_from have expired from the store (windowed tables)
+  int32_t vis;
+  int64_t vis_from;
+  // EMIT FINAL (S/StreamAggregateBuilder.java:282-285): the windows that closed during the last
+  // push (ws + size in (fin_c0, fin_c1]) minus those that had already expired at the record
+  // that closed them (n_lost sorted disjoint ws ranges [lost[2i], lost[2i+1]])
+  int32_t fin;
+  int32_t n_lost;
+  int64_t fin_c0, fin_c1, fin_size;
+  const int64_t* lost;
 };
 
+// Retention and EMIT FINAL selection of a row [key, ws, ...] (no-ops unless h.vis / h.fin).
+__device__ __forceinline__ bool store_ok(const uint64_t* s, const HavingDev& h) {
+  const int64_t ws = (int64_t)s[1];
+  if (h.vis && ws < h.vis_from) return false;
+  if (h.fin) {
+    const int64_t end = ws + h.fin_size;
+    if (end <= h.fin_c0 || end > h.fin_c1) return false;
+    int lo = 0, hi = h.n_lost;  // first range starting after ws
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (h.lost[2 * mid] <= ws) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo > 0 && ws <= h.lost[2 * (lo - 1) + 1]) return false;
+  }
+  return true;
+}
+
 __device__ __forceinline__ bool pull_ok(const uint64_t* s, const HavingDev& h) {
+  if (!store_ok(s, h)) return false;
   if (!h.pull) return true;
   if (h.n_keys > 0) {
     const int64_t k = (int64_t)s[0];
@@ -299,6 +329,8 @@ struct PartState {
   DevBuf srecA, hcoarse, scan_tmpB, RB;
   // k_part_merge (delta-only LDS): entries, LDS bytes, plane layout (khip_agg_part.hip)
   int mH = 0, m_lds = 0, rt_off = 0, n_cu = 256;
+  int flag_off = 0;       // k_part_agg: LDS byte offset of the changelog flag plane
+  int64_t purged_to = INT64_MIN;  // closed store: expired rows (ws < purged_to) already dropped
   int32_t plane_off[MAX_OPS] = {};
   int8_t plane_w64[MAX_OPS] = {};
   int8_t word_op[32] = {};
@@ -350,7 +382,23 @@ struct khip_agg {
   int engine = 0;  // 0 partitioned (LDS-owned groups), 1 global-atomic
   khip::HavingDev having{};  // the query's HAVING (desc.has_having), maintained by the merge kernel
   khip::PartState part;
+  // ---- retention and emission (include/ksqldb_hip.h khip_agg_changes)
+  int64_t retention = 0;     // windowed: RETENTION or size + grace
+  bool changelog = false;    // KHIP_FLAG_CHANGELOG: keep the push's EMIT CHANGES rows
+  int64_t st_before = -1;    // stream time before the last push
+  DevBuf chg;                // partitioned engine: per row slot (P x cmax) emission flags, see CHG_*
+  DevBuf lostbuf, lostctr;   // EMIT FINAL: expired-at-close ws ranges found by the last push
+  int64_t lost_cap = 0;
+  std::vector<int64_t> lost; // sorted [lo, hi] pairs of the last push
+  bool chg_ready = false;    // changes of the last push computed (rows / tombstones below)
+  std::vector<uint64_t> chg_rows;
+  std::vector<uint8_t> chg_tomb;
+  int64_t chg_n = 0;
 };
+
+// Emission flags of a row written by the last push (khip_agg::chg): touched by one of its
+// records, HAVING held before the push, HAVING holds now (no HAVING: both set).
+constexpr uint8_t CHG_TOUCHED = 1, CHG_OLD = 2, CHG_NEW = 4;
 
 inline void ev_record(khip_agg* a, int i) {
   if (a->profile) (void)hipEventRecord(a->ev[i], a->stream);
@@ -370,6 +418,12 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                       const uint8_t* rv, const ColPtrs& cols, int64_t* tot);
 khip_status part_compact(khip_agg* a, const HavingDev& h, std::vector<uint64_t>* rows, int64_t* count);
 bool part_having_count(khip_agg* a, int64_t* n);
+khip_status part_changes(khip_agg* a, std::vector<uint64_t>* rows, std::vector<uint8_t>* tomb, int64_t* count);
+khip_status part_purge_closed(khip_agg* a, const HavingDev& vis);
+// the first visible window start after the last push (INT64_MIN: nothing expired)
+int64_t visible_from(const khip_agg* a);
+khip_status emit_final_lost(khip_agg* a, const int64_t* ts, const uint8_t* kv, const uint8_t* rv, int64_t n,
+                            int64_t tile, const int64_t* tile_prefix);
 }  // namespace khip
 
 

@@ -72,6 +72,11 @@ struct PartAggParams {
   int32_t col_type[MAX_COLS];
   UpdOp ops[MAX_OPS];
   InitWords init;
+  // changelog (khip_agg::changelog): byte offset of the LDS flag plane (H bytes: bit 0 touched,
+  // bit 1 HAVING held before the push) and the per-row-slot emission flags (CHG_*)
+  int32_t flag_off;
+  uint8_t* chg;
+  HavingDev having;
 };
 
 // Key hash: its top log2P bits pick the partition; inside a partition the LDS slot and the
@@ -902,6 +907,9 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
   } else {
     for (int i = threadIdx.x; i < H / 4; i += AG_THREADS) ((KLDS u32x4*)lref)[i] = u32x4{0u, 0u, 0u, 0u};
   }
+  lds_u32* lflag = q.flag_off ? (lds_u32*)(smem + q.flag_off) : nullptr;  // 4 entries per word
+  if (lflag)
+    for (int i = threadIdx.x; i < H / 4; i += AG_THREADS) lflag[i] = 0u;
   if (threadIdx.x == 0) lovf = 0;
   __syncthreads();
   AGG_T(1);
@@ -965,6 +973,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
         break;
       }
       for (int w = 2; w < q.nwords; w++) lw[w * H + e] = (int64_t)row[w];
+      if (lflag && having_ok(row, q.having)) __hip_atomic_fetch_or(&lflag[e >> 2], 2u << ((e & 3) * 8), WG_RLX);
       continue;
     }
     for (; probe < H; probe++) {
@@ -979,6 +988,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
       break;
     }
     for (int w = 0; w < q.nwords; w++) lw[w * H + e] = (int64_t)row[w];
+    if (lflag && having_ok(row, q.having)) __hip_atomic_fetch_or(&lflag[e >> 2], 2u << ((e & 3) * 8), WG_RLX);
   }
   if (dbg) {
     __builtin_amdgcn_s_waitcnt(0);
@@ -1040,6 +1050,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
             break;
           }
           if (!(q.dbg_mode & 1)) lds_apply(q, lw, H, (int)e, t, vmask, srec, gi, w3);
+          if (lflag) __hip_atomic_fetch_or(&lflag[e >> 2], 1u << ((e & 3) * 8), WG_RLX);
           continue;
         }
         const uint32_t fp = fp_of(hk, ws);
@@ -1091,6 +1102,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
           break;
         }
         if (!(q.dbg_mode & 1)) lds_apply(q, lw, H, (int)e, t, vmask, srec, gi, w3);
+        if (lflag) __hip_atomic_fetch_or(&lflag[e >> 2], 1u << ((e & 3) * 8), WG_RLX);
       }
     }
   }
@@ -1132,9 +1144,22 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
     }
     return;
   }
-  uint64_t* dst =
-      (sel[p] ? buf0 : buf1) + (uint64_t)p * q.cmax * q.sw + (lbase + (uint64_t)(before + incl - mine)) * q.sw;
+  const uint64_t row0 = lbase + (uint64_t)(before + incl - mine);  // this thread's first row
+  uint64_t* dst = (sel[p] ? buf0 : buf1) + (uint64_t)p * q.cmax * q.sw + row0 * q.sw;
+  uint8_t* cdst = lflag ? q.chg + (uint64_t)p * q.cmax + row0 : nullptr;
+  const int hv = q.having.a.w_val, hc = q.having.a.w_cnt;
   for (int e = e0; e < e1; e++) {
+    if (idm ? (uint64_t)lw[e] == EMPTY_ID : lref[e] == 0u) continue;
+    if (cdst) {  // emission flags of the row (CHG_*): HAVING on the entry's new words
+      const uint32_t f = (lflag[e >> 2] >> ((e & 3) * 8)) & 0xFFu;
+      uint8_t c = 0;
+      if (f & 1u) {
+        const bool now = !q.having.active ||
+                         having_ok_words((uint64_t)lw[hv * H + e], hc < 0 ? 0ULL : (uint64_t)lw[hc * H + e], q.having);
+        c = (uint8_t)(CHG_TOUCHED | ((f & 2u) || !q.having.active ? CHG_OLD : 0) | (now ? CHG_NEW : 0));
+      }
+      *cdst++ = c;
+    }
     if (idm) {
       const uint64_t id = (uint64_t)lw[e];
       if (id == EMPTY_ID) continue;
@@ -1204,6 +1229,7 @@ struct MergeParams {
   HavingDev having;  // the query's HAVING (active = 0: none): rows passing it are counted
   int32_t dbg;       // tuning build: KHIP_MERGE_DEBUG prints the delta table of touched partitions
   int32_t r12;       // records are R12 (narrow layout; k_part_scatter / k_part_refine wrote them so)
+  uint8_t* chg;      // changelog: per-row-slot emission flags (CHG_*), or null
 };
 
 __device__ __forceinline__ uint32_t mg_slot(uint64_t id, int H) {
@@ -1722,7 +1748,8 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
       const bool live = e != -2;
       const uint64_t b = __ballot(live);
       if (live) {
-        uint64_t* dst = dst0 + (cur + __popcll(b & lt)) * q.sw;
+        const uint64_t ri = cur + __popcll(b & lt);
+        uint64_t* dst = dst0 + ri * q.sw;
         uint64_t w2 = row[2];
         if (e >= 0) {
           const uint32_t rr = rt[e] & ~RT_MATCHED;
@@ -1730,19 +1757,28 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
           w2 = t > (int64_t)w2 ? (uint64_t)t : w2;
         }
         *(longlong2*)dst = make_longlong2((int64_t)row[0], (int64_t)row[1]);
+        bool now;
         if constexpr (CNT1) {
           const uint64_t c = row[3] + (e >= 0 ? (uint64_t)cnt1[e] : 0ULL);
           *(longlong2*)(dst + 2) = make_longlong2((int64_t)w2, (int64_t)c);
-          if (q.having.active) nh += having_ok_words(c, 0, q.having);
+          now = having_ok_words(c, 0, q.having);
         } else {
           for (int k = 2; k < q.sw; k += 2) {
             const uint64_t a = k == 2 ? w2 : (e >= 0 ? mg_word(wtab, smem, k, row, e) : row[k]);
             const uint64_t c = e >= 0 ? mg_word(wtab, smem, k + 1, row, e) : row[k + 1];
             *(longlong2*)(dst + k) = make_longlong2((int64_t)a, (int64_t)c);
           }
-          if (q.having.active)
-            nh += having_ok_words(e >= 0 ? mg_word(wtab, smem, hv, row, e) : row[hv],
-                                  hc < 0 ? 0 : (e >= 0 ? mg_word(wtab, smem, hc, row, e) : row[hc]), q.having);
+          now = !q.having.active ||
+                having_ok_words(e >= 0 ? mg_word(wtab, smem, hv, row, e) : row[hv],
+                                hc < 0 ? 0 : (e >= 0 ? mg_word(wtab, smem, hc, row, e) : row[hc]), q.having);
+        }
+        if (q.having.active) nh += now ? 1 : 0;
+        if (q.chg) {  // emission flags: touched rows, HAVING before (the old row) and after
+          uint8_t f = 0;
+          if (e >= 0)
+            f = (uint8_t)(CHG_TOUCHED | (having_ok_words(row[hv], hc < 0 ? 0ULL : row[hc], q.having) ? CHG_OLD : 0) |
+                          (now ? CHG_NEW : 0));
+          q.chg[(uint64_t)p * q.cmax + ri] = f;
         }
       }
       cur += __popcll(b);
@@ -1754,23 +1790,26 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
       const bool isnew = id != EMPTY_ID && !(rt[e] & RT_MATCHED);
       const uint64_t b = __ballot(isnew);
       if (isnew) {
-        uint64_t* dst = dst0 + (cur + __popcll(b & lt)) * q.sw;
+        const uint64_t ri = cur + __popcll(b & lt);
+        uint64_t* dst = dst0 + ri * q.sw;
         const uint64_t hk = ((uint64_t)p << (64 - q.log2P)) | (id >> q.log2P);
         const int64_t ws = (((int64_t)(id & ((1ULL << q.log2P) - 1))) + wbase) * (q.windowed ? q.adv : 0);
         *(longlong2*)dst = make_longlong2(key_of_hash(hk), ws);
+        bool now;
         if constexpr (CNT1) {
           const uint32_t c = cnt1[e];
           *(longlong2*)(dst + 2) = make_longlong2(tbase + (int64_t)rt[e] - 1, (int64_t)c);
-          if (q.having.active) nh += having_ok_words(c, 0, q.having);
+          now = having_ok_words(c, 0, q.having);
         } else {
           for (int k = 2; k < q.sw; k += 2) {
             const uint64_t a = k == 2 ? (uint64_t)(tbase + (int64_t)rt[e] - 1) : mg_word(wtab, smem, k, nullptr, e);
             *(longlong2*)(dst + k) = make_longlong2((int64_t)a, (int64_t)mg_word(wtab, smem, k + 1, nullptr, e));
           }
-          if (q.having.active)
-            nh += having_ok_words(mg_word(wtab, smem, hv, nullptr, e), hc < 0 ? 0 : mg_word(wtab, smem, hc, nullptr, e),
-                                  q.having);
+          now = !q.having.active || having_ok_words(mg_word(wtab, smem, hv, nullptr, e),
+                                                    hc < 0 ? 0 : mg_word(wtab, smem, hc, nullptr, e), q.having);
         }
+        if (q.having.active) nh += now ? 1 : 0;
+        if (q.chg) q.chg[(uint64_t)p * q.cmax + ri] = (uint8_t)(CHG_TOUCHED | (now ? CHG_NEW : 0));
       }
       if (id != EMPTY_ID) {
         if constexpr (CNT1) {
@@ -1951,6 +1990,12 @@ __global__ __launch_bounds__(256) void k_part_regrow(const uint64_t* __restrict_
   for (int64_t w = threadIdx.x; w < words; w += 256) dst[w] = src[w];
 }
 
+__global__ __launch_bounds__(256) void k_part_regrow_flags(const uint8_t* __restrict__ f, const int64_t* __restrict__ cnt,
+                                                           int64_t ocmax, uint8_t* __restrict__ nf, int64_t ncmax) {
+  const int64_t p = blockIdx.x;
+  for (int64_t r = threadIdx.x; r < cnt[p]; r += 256) nf[p * ncmax + r] = f[p * ocmax + r];
+}
+
 // Double the partition count: rows of partition p move to 2p / 2p+1 (next hash bit).
 // nb == nullptr: count only (ncnt = child row counts, used to size the new regions).
 __global__ __launch_bounds__(256) void k_part_split(const uint64_t* __restrict__ b0, const uint64_t* __restrict__ b1,
@@ -2030,6 +2075,51 @@ __global__ __launch_bounds__(256) void k_part_rows(const uint64_t* __restrict__ 
   if (threadIdx.x == 0 && counts) counts[p] = total;
 }
 
+// EMIT CHANGES (the record cache flushed at the push's commit, C/util/KsqlConstants.java:40-41):
+// per partition the last push's records reached, the rows it touched whose HAVING holds now
+// (emitted as rows) or held before the push (emitted as tombstones, S/TableFilterBuilder.java:
+// 63-75).  counts[p] (count pass) or rows at offs[p] + tombstone flags (write pass).
+__global__ __launch_bounds__(256) void k_part_chg(const uint64_t* __restrict__ b0, const uint64_t* __restrict__ b1,
+                                                  const uint8_t* __restrict__ sel, const int64_t* __restrict__ cnt,
+                                                  int64_t cmax, int sw, const int64_t* __restrict__ pbase,
+                                                  const uint8_t* __restrict__ chg, int64_t* __restrict__ counts,
+                                                  const int64_t* __restrict__ offs, uint64_t* __restrict__ out,
+                                                  uint8_t* __restrict__ otomb) {
+  __shared__ int lcnt[4];
+  const int64_t p = blockIdx.x;
+  if (pbase[p + 1] == pbase[p]) {  // no record of the push: its flags are stale
+    if (threadIdx.x == 0 && counts) counts[p] = 0;
+    return;
+  }
+  const uint64_t* src = (sel[p] ? b1 : b0) + (uint64_t)p * cmax * sw;
+  const uint8_t* fl = chg + (uint64_t)p * cmax;
+  const int64_t n = cnt[p];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int64_t total = 0;
+  const int64_t base = out ? offs[p] : 0;
+  for (int64_t r0 = 0; r0 < n; r0 += 256) {
+    const int64_t r = r0 + threadIdx.x;
+    const uint8_t f = r < n ? fl[r] : 0;
+    const bool take = (f & CHG_TOUCHED) && (f & (CHG_OLD | CHG_NEW));
+    const uint64_t bal = __ballot(take);
+    if (lane == 0) lcnt[wave] = __popcll(bal);
+    __syncthreads();
+    int before = __popcll(bal & ((1ULL << lane) - 1)), tot = 0;
+    for (int w = 0; w < 4; w++) {
+      if (w < wave) before += lcnt[w];
+      tot += lcnt[w];
+    }
+    if (take && out) {
+      const int64_t o = base + total + before;
+      for (int w = 0; w < sw; w++) out[o * sw + w] = src[r * sw + w];
+      otomb[o] = (f & CHG_NEW) ? 0 : 1;
+    }
+    total += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && counts) counts[p] = total;
+}
+
 // ------------------------------------------------------------------ host side
 
 static int part_ceil_log2(int64_t v) {
@@ -2055,6 +2145,10 @@ khip_status part_init(khip_agg* a, int64_t hint) {
   s.H = H;
   s.H_eff = H * 3 / 4;
   s.lds_bytes = (int)((((size_t)H * 4 + 15) & ~(size_t)15) + (size_t)H * 8 * used);
+  if (a->changelog) {  // k_part_agg's emission flag plane: one byte per entry
+    s.flag_off = s.lds_bytes;
+    s.lds_bytes += H;
+  }
   // k_part_merge layout: id u64 | u64 delta planes | rowtime u32 | u32 delta planes, sized so
   // two workgroups share a CU; partitions are sized for whichever kernel holds fewer groups
   {
@@ -2127,13 +2221,14 @@ khip_status part_init(khip_agg* a, int64_t hint) {
   KHIP_TRY(s.ctr.ensure(128));
   KHIP_TRY(s.hcnt.ensure(s.P * 8));
   KHIP_TRY(s.hnew.ensure(s.P * 8));
-  KHIP_TRY(s.pinfo.ensure(256));
+  KHIP_TRY(s.pinfo.ensure(512));
   KHIP_TRY_HIP(hipMemsetAsync(s.hcnt.p, 0, s.P * 8, a->stream));
   KHIP_TRY_HIP(hipMemsetAsync(s.hnew.p, 0, s.P * 8, a->stream));
   KHIP_TRY_HIP(hipMemsetAsync(s.ctr.p, 0, 128, a->stream));
   s.having_total = 0;
   s.hvalid = true;
   for (int b = 0; b < 2; b++) KHIP_TRY(s.buf[b].ensure((size_t)s.P * s.cmax * a->sw * 8));
+  if (a->changelog) KHIP_TRY(a->chg.ensure((size_t)s.P * s.cmax));
   KHIP_TRY_HIP(hipMemsetAsync(s.sel.p, 0, s.P, a->stream));
   KHIP_TRY_HIP(hipMemsetAsync(s.fail.p, 0, s.P, a->stream));
   KHIP_TRY_HIP(hipMemsetAsync(s.cnt.p, 0, s.P * 8, a->stream));
@@ -2172,6 +2267,7 @@ __global__ __launch_bounds__(256) void k_part_reset(int64_t P, unsigned long lon
 khip_status part_reset(khip_agg* a) {
   PartState& s = a->part;
   s.closed_n = 0;
+  s.purged_to = INT64_MIN;
   s.res_fresh = true;
   s.hvalid = true;
   s.having_total = 0;
@@ -2205,23 +2301,37 @@ static PartAggParams part_params(khip_agg* a) {
   for (int c = 0; c < MAX_COLS; c++) q.col_type[c] = a->ap.col_type[c];
   for (int o = 0; o < a->ap.n_ops; o++) q.ops[o] = a->ap.ops[o];
   q.init = a->init;
+  q.having = a->having;
+  q.flag_off = a->changelog ? s.flag_off : 0;
+  q.chg = a->changelog ? a->chg.as<uint8_t>() : nullptr;
   return q;
 }
 
 static khip_status part_regrow(khip_agg* a, int64_t ncmax) {
   PartState& s = a->part;
-  DevBuf nb[2];
+  DevBuf nb[2], nchg;
   for (int b = 0; b < 2; b++) KHIP_TRY(nb[b].ensure((size_t)s.P * ncmax * a->sw * 8));
   hipLaunchKernelGGL(k_part_regrow, dim3(s.P), dim3(256), 0, a->stream, s.buf[0].as<uint64_t>(),
                      s.buf[1].as<uint64_t>(), s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.cmax, nb[0].as<uint64_t>(),
                      ncmax, a->sw);
   KHIP_TRY_HIP(hipGetLastError());
+  if (a->changelog) {  // committed partitions keep this push's emission flags
+    KHIP_TRY(nchg.ensure((size_t)s.P * ncmax));
+    hipLaunchKernelGGL(k_part_regrow_flags, dim3(s.P), dim3(256), 0, a->stream, a->chg.as<uint8_t>(), s.cnt.as<int64_t>(),
+                       s.cmax, nchg.as<uint8_t>(), ncmax);
+    KHIP_TRY_HIP(hipGetLastError());
+  }
   KHIP_TRY_HIP(hipMemsetAsync(s.sel.p, 0, s.P, a->stream));
   KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
   for (int b = 0; b < 2; b++) {
     s.buf[b].release();
     s.buf[b] = nb[b];
     nb[b].p = nullptr;
+  }
+  if (a->changelog) {
+    a->chg.release();
+    a->chg = nchg;
+    nchg.p = nullptr;
   }
   s.cmax = ncmax;
   return KHIP_OK;
@@ -2268,6 +2378,10 @@ static khip_status part_split(khip_agg* a) {
   s.P = P2;
   s.log2P += 1;
   s.cmax = ncmax;
+  if (a->changelog) {  // rewritten by the push that follows (untouched partitions are not read)
+    a->chg.release();
+    KHIP_TRY(a->chg.ensure((size_t)P2 * ncmax));
+  }
   // per-partition HAVING counts do not survive the re-layout: the full scan serves HAVING
   // counts until the next reset
   KHIP_TRY(s.hcnt.ensure(P2 * 8));
@@ -2471,6 +2585,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     mq.having = a->having;
     mq.dbg = (int32_t)knob("KHIP_MERGE_DEBUG", 0);
     mq.r12 = r12_merge ? 1 : 0;
+    mq.chg = a->changelog ? a->chg.as<uint8_t>() : nullptr;
   }
   if (a->windowed) {  // worst case every live row closes in this push
     const int64_t live = a->occ - s.closed_n;
@@ -2514,6 +2629,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     }
     q.cmax = s.cmax;
     mq.cmax = s.cmax;
+    q.chg = mq.chg = a->changelog ? a->chg.as<uint8_t>() : nullptr;  // a retry's regrow moves them
     if (pass > 0) KHIP_TRY_HIP(hipMemsetAsync(s.ctr.p, 0, 24, a->stream));  // pass 0: k_part_wrange
     const uint32_t* wk = (pass == 0 && !subs0) ? nullptr : s.work.as<uint32_t>();
     const int64_t nwork = (pass == 0 && !subs0) ? P : (int64_t)work.size();
@@ -2712,6 +2828,86 @@ khip_status part_compact(khip_agg* a, const HavingDev& h_in, std::vector<uint64_
   if (n) KHIP_TRY_HIP(hipMemcpyAsync(rows->data(), out.p, (size_t)n * a->sw * 8, hipMemcpyDeviceToHost, a->stream));
   KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
   out.release();
+  return KHIP_OK;
+}
+
+khip_status part_changes(khip_agg* a, std::vector<uint64_t>* rows, std::vector<uint8_t>* tomb, int64_t* count) {
+  PartState& s = a->part;
+  const int P = (int)s.P;
+  KHIP_TRY(s.counts.ensure((P + 1) * 8));
+  hipLaunchKernelGGL(k_part_chg, dim3(P), dim3(256), 0, a->stream, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
+                     s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.cmax, a->sw, s.pbase.as<int64_t>(),
+                     a->chg.as<uint8_t>(), s.counts.as<int64_t>(), nullptr, nullptr, nullptr);
+  KHIP_TRY_HIP(hipMemsetAsync(s.counts.as<int64_t>() + P, 0, 8, a->stream));
+  hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, a->stream, s.counts.as<int64_t>(), (int64_t)P,
+                     s.counts.as<int64_t>() + P);
+  KHIP_TRY_HIP(hipGetLastError());
+  int64_t n = 0;
+  KHIP_TRY_HIP(hipMemcpyAsync(&n, s.counts.as<int64_t>() + P, 8, hipMemcpyDeviceToHost, a->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  *count = n;
+  DevBuf out, ot;
+  KHIP_TRY(out.ensure((size_t)std::max<int64_t>(n, 1) * a->sw * 8));
+  KHIP_TRY(ot.ensure((size_t)std::max<int64_t>(n, 1)));
+  hipLaunchKernelGGL(k_part_chg, dim3(P), dim3(256), 0, a->stream, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
+                     s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.cmax, a->sw, s.pbase.as<int64_t>(),
+                     a->chg.as<uint8_t>(), nullptr, s.counts.as<int64_t>(), out.as<uint64_t>(), ot.as<uint8_t>());
+  KHIP_TRY_HIP(hipGetLastError());
+  rows->resize((size_t)n * a->sw);
+  tomb->resize((size_t)n);
+  if (n) {
+    KHIP_TRY_HIP(hipMemcpyAsync(rows->data(), out.p, (size_t)n * a->sw * 8, hipMemcpyDeviceToHost, a->stream));
+    KHIP_TRY_HIP(hipMemcpyAsync(tomb->data(), ot.p, (size_t)n, hipMemcpyDeviceToHost, a->stream));
+  }
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  return KHIP_OK;
+}
+
+// Retention: drop the closed store's rows that expired from the window store (vis: h.vis_from),
+// keeping the maintained HAVING count of the closed rows (ctr[12]) and the group count in step.
+khip_status part_purge_closed(khip_agg* a, const HavingDev& vis) {
+  PartState& s = a->part;
+  if (s.closed_n == 0 || vis.vis_from <= s.purged_to) return KHIP_OK;
+  const int grid = (int)std::min<int64_t>(ceil_div(s.closed_n, 256), 4096);
+  DevBuf ctr;
+  KHIP_TRY(ctr.ensure(16));
+  KHIP_TRY_HIP(hipMemsetAsync(ctr.p, 0, 16, a->stream));
+  hipLaunchKernelGGL(k_compact, dim3(grid), dim3(256), 0, a->stream, s.closed.as<uint64_t>(), s.closed_n, a->sw, vis,
+                     (uint64_t*)nullptr, (int64_t)0, ctr.as<unsigned long long>());
+  HavingDev vh = vis;  // kept rows passing the query's HAVING
+  vh.active = a->having.active;
+  vh.op = a->having.op;
+  vh.a = a->having.a;
+  vh.i64 = a->having.i64;
+  vh.f64 = a->having.f64;
+  if (vh.active)
+    hipLaunchKernelGGL(k_compact, dim3(grid), dim3(256), 0, a->stream, s.closed.as<uint64_t>(), s.closed_n, a->sw, vh,
+                       (uint64_t*)nullptr, (int64_t)0, ctr.as<unsigned long long>() + 1);
+  KHIP_TRY_HIP(hipGetLastError());
+  int64_t kc[2] = {0, 0};
+  KHIP_TRY_HIP(hipMemcpyAsync(kc, ctr.p, 16, hipMemcpyDeviceToHost, a->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  s.purged_to = vis.vis_from;
+  const int64_t keep = kc[0];
+  if (keep == s.closed_n) return KHIP_OK;
+  DevBuf nc;
+  KHIP_TRY(nc.ensure((size_t)s.closed_cap * a->sw * 8));
+  KHIP_TRY_HIP(hipMemsetAsync(ctr.p, 0, 8, a->stream));
+  hipLaunchKernelGGL(k_compact, dim3(grid), dim3(256), 0, a->stream, s.closed.as<uint64_t>(), s.closed_n, a->sw, vis,
+                     nc.as<uint64_t>(), keep, ctr.as<unsigned long long>());
+  KHIP_TRY_HIP(hipGetLastError());
+  if (vh.active) {  // ctr[12]: closed rows passing HAVING
+    unsigned long long* hc = s.pinfo.as<unsigned long long>() + 40;
+    *hc = (unsigned long long)kc[1];
+    KHIP_TRY_HIP(hipMemcpyAsync(s.ctr.as<unsigned long long>() + 12, hc, 8, hipMemcpyHostToDevice, a->stream));
+    s.having_total += kc[1] - (int64_t)s.pinfo.as<unsigned long long>()[8 + 12];
+  }
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  s.closed.release();
+  s.closed = nc;
+  nc.p = nullptr;
+  a->occ -= s.closed_n - keep;
+  s.closed_n = keep;
   return KHIP_OK;
 }
 

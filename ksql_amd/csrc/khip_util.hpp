@@ -155,6 +155,9 @@ __host__ __device__ inline double f64_from_order_key(int64_t k) {
 __host__ __device__ inline int64_t grace_of(const khip_agg_desc& d) {
   if (d.window_kind == KHIP_WINDOW_NONE) return 0;
   if (d.grace_ms >= 0) return d.grace_ms;
+  // EMIT FINAL without GRACE PERIOD: the analyzer substitutes zero grace
+  // (ksqldb-engine/.../analyzer/RewrittenAnalysis.java:65,149-154)
+  if (d.emit == KHIP_EMIT_FINAL) return 0;
   int64_t g = 86400000LL - d.size_ms;
   return g > 0 ? g : 0;
 }

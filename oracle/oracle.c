@@ -23,7 +23,8 @@
  *     S/StreamAggregateBuilder.java:269-295,328-352).
  *  R4 late drop: window updated iff ws + size > streamTime - grace
  *     (grace: GRACE PERIOD or max(86400000 - size, 0), S/StreamAggregateBuilder.java
- *     :275-277,332-334).  Unwindowed aggregation (StreamAggregateBuilder.java:81-138)
+ *     :275-277,332-334); with EMIT FINAL and no GRACE PERIOD the analyzer sets 0
+ *     (E/analyzer/RewrittenAnalysis.java:65,149-154).  Unwindowed aggregation (StreamAggregateBuilder.java:81-138)
  *     has no windows and no late drop.
  *  R5 entry: created by the first applied record (KudafInitializer.apply,
  *     X/function/udaf/KudafInitializer.java:39-47), even if every aggregate input is
@@ -38,6 +39,20 @@
  *     min/MinKudaf.java:81; Double.compareTo: -0.0 < 0.0, NaN largest);
  *     AVG: {sum (wrapping for INT/BIGINT), count} and map = count==0 ? 0.0 :
  *     (double)sum / (double)count (E/function/udaf/average/AverageUdaf.java:104-128).
+ *  R9 retention (window store): a window is visible while ws >= obs - R, obs = the largest
+ *     window start put into the store (the store's observedStreamTime, Kafka 3.4 segmented
+ *     window stores), R = RETENTION or size + grace (X/runtime/MaterializedFactory.java:47 via
+ *     S/StreamAggregateBuilder.java:293,322,350).  Pinned by the EMIT FINAL QTT cases
+ *     (Q/suppress.json: expired windows are never emitted); snapshots and pull queries read
+ *     the store, so they apply it too.
+ *  R10 emission (one commit per push = the record cache flushed at commit,
+ *     C/util/KsqlConstants.java:40-41): EMIT CHANGES emits every (key, window) the push
+ *     updated with its new value; with HAVING (S/TableFilterBuilder.java:63-75) a row that
+ *     fails now but passed before the push is a tombstone, one that failed before and after
+ *     is not emitted (Q/having.json:7,25).  EMIT FINAL (S/StreamAggregateBuilder.java:282-285,
+ *     EmitStrategy.onWindowClose; Q/suppress.json) emits, once per push whose close time
+ *     (streamTime - grace) passed the last emitted one, the windows with start in
+ *     [max(0, lastClose - size), close - size] that are still visible (R9) and pass HAVING.
  *  R7 join: table keeps the latest non-null value per key, a null value deletes;
  *     stream records with null key / null value / negative ts are dropped; lookup
  *     against the table as of that point; INNER emits on hit, LEFT always
@@ -216,6 +231,9 @@ typedef struct {
   int64_t ws;
   int64_t rowtime;
   agg_state* st; /* n_aggs */
+  int64_t born_epoch;  /* push that created the entry                          */
+  int64_t touch_epoch; /* last push that updated it                            */
+  int old_pass;        /* HAVING before the push's first update (R10)          */
 } entry;
 
 struct oracle_agg {
@@ -229,6 +247,18 @@ struct oracle_agg {
   int64_t n, cap;
   int64_t* slots;
   int64_t nslots;
+  int64_t retention;  /* R9 (windowed)                                            */
+  int64_t obs_ws;     /* largest window start put (-1: none)                      */
+  int64_t epoch;      /* pushes so far                                            */
+  int64_t* touched;   /* entries the current push updated                         */
+  int64_t n_touched, cap_touched;
+  int64_t* chg;       /* the last push's emitted rows (entry index), sorted       */
+  uint8_t* chg_tomb;
+  int64_t n_chg, cap_chg;
+  int64_t st_before;  /* stream time before the current push                      */
+  int64_t* stmax;     /* the push's stream-time maxima, in arrival order           */
+  int64_t n_stmax, cap_stmax;
+  int own_stmax;      /* stmax is this handle's (0: borrowed from the sharded push)  */
 };
 
 static uint64_t entry_hash(int64_t key, int64_t ws) {
@@ -265,7 +295,34 @@ static entry* find_or_create(oracle_agg* a, int64_t key, int64_t ws) {
   x->ws = ws;
   x->rowtime = INT64_MIN;
   x->st = (agg_state*)calloc((size_t)(a->d.n_aggs > 0 ? a->d.n_aggs : 1), sizeof(agg_state));
+  x->born_epoch = a->epoch;
+  x->touch_epoch = -1;
+  x->old_pass = 0;
   return x;
+}
+
+static int having_pass(const oracle_agg* a, const khip_having* h, const entry* x);
+
+static const khip_having* query_having(const oracle_agg* a) {
+  return a->d.has_having ? &a->d.having : NULL;
+}
+
+/* R10: remember the entry's HAVING result before this push's first update to it. */
+static void touch(oracle_agg* a, entry* x) {
+  if (x->touch_epoch == a->epoch) return;
+  x->touch_epoch = a->epoch;
+  x->old_pass = x->born_epoch == a->epoch ? 0 : having_pass(a, query_having(a), x);
+  if (a->n_touched == a->cap_touched) {
+    a->cap_touched = a->cap_touched ? a->cap_touched * 2 : 1024;
+    a->touched = (int64_t*)realloc(a->touched, sizeof(int64_t) * a->cap_touched);
+  }
+  a->touched[a->n_touched++] = x - a->e;
+}
+
+/* R9: first visible window start (INT64_MIN: everything visible). */
+static int64_t visible_from(const oracle_agg* a) {
+  if (a->d.window_kind == KHIP_WINDOW_NONE || a->obs_ws < 0) return INT64_MIN;
+  return a->obs_ws - a->retention;
 }
 
 static int valid_desc(const khip_agg_desc* d) {
@@ -288,6 +345,9 @@ static int valid_desc(const khip_agg_desc* d) {
   }
   for (int c = 0; c < d->n_cols; c++)
     if (d->col_types[c] < KHIP_TYPE_INT32 || d->col_types[c] > KHIP_TYPE_DOUBLE) return 0;
+  if (d->emit != KHIP_EMIT_CHANGES && d->emit != KHIP_EMIT_FINAL) return 0;
+  if (d->emit == KHIP_EMIT_FINAL && d->window_kind == KHIP_WINDOW_NONE) return 0;
+  if (d->has_having && (d->having.agg_index < 0 || d->having.agg_index >= d->n_aggs)) return 0;
   return 1;
 }
 
@@ -304,12 +364,22 @@ khip_status oracle_agg_create(const khip_agg_desc* desc, oracle_agg** out) {
   if (desc->window_kind == KHIP_WINDOW_TUMBLING) a->d.advance_ms = desc->size_ms;
   if (desc->window_kind == KHIP_WINDOW_NONE) {
     a->grace = 0;
+  } else if (desc->grace_ms < 0 && desc->emit == KHIP_EMIT_FINAL) {
+    a->grace = 0; /* EMIT FINAL without GRACE PERIOD: the analyzer's zero grace (R4) */
   } else if (desc->grace_ms < 0) {
     int64_t g = ORACLE_DAY_MS - desc->size_ms;
     a->grace = g > 0 ? g : 0;
   } else {
     a->grace = desc->grace_ms;
   }
+  if (desc->window_kind != KHIP_WINDOW_NONE) {
+    const int64_t min_r = desc->size_ms + a->grace;
+    if (desc->retention_ms == KHIP_RETENTION_DEFAULT) a->retention = min_r;
+    else if (desc->retention_ms < min_r) { free(a->col_types); free(a->aggs); free(a); return KHIP_E_INVALID; }
+    else a->retention = desc->retention_ms;
+  }
+  a->obs_ws = -1;
+  a->own_stmax = 1;
   a->stream_time = -1;
   strdict_init(&a->dict);
   a->nslots = 1024;
@@ -373,6 +443,9 @@ static void apply_aggs(oracle_agg* a, entry* x, const khip_batch* b, int64_t r) 
   }
 }
 
+static void finish_push(oracle_agg* a);
+static void stmax_add(oracle_agg* a, int64_t st);
+
 khip_status oracle_agg_push(oracle_agg* a, const khip_batch* b, khip_batch_stats* stats) {
   if (!a || !b || b->mem != KHIP_MEM_HOST || b->n_rows < 0) return KHIP_E_INVALID;
   if (b->n_cols < a->d.n_cols) return KHIP_E_INVALID;
@@ -381,6 +454,10 @@ khip_status oracle_agg_push(oracle_agg* a, const khip_batch* b, khip_batch_stats
   s.rows_in = b->n_rows;
   const int windowed = a->d.window_kind != KHIP_WINDOW_NONE;
   const int64_t size = a->d.size_ms, adv = a->d.advance_ms;
+  a->epoch++;
+  a->n_touched = 0;
+  a->st_before = a->stream_time;
+  a->n_stmax = 0;
   for (int64_t r = 0; r < b->n_rows; r++) {
     if (!bit_get(b->key_valid, r)) { s.dropped_null_key++; continue; }
     if (!bit_get(b->row_valid, r)) { s.dropped_null_row++; continue; }
@@ -396,28 +473,35 @@ khip_status oracle_agg_push(oracle_agg* a, const khip_batch* b, khip_batch_stats
     }
     if (!windowed) {
       entry* x = find_or_create(a, key, 0);
+      touch(a, x);
       if (ts > x->rowtime) x->rowtime = ts;
       apply_aggs(a, x, b, r);
       s.windows_applied++;
       if (ts > a->stream_time) a->stream_time = ts;
       continue;
     }
-    if (ts > a->stream_time) a->stream_time = ts; /* R2: before the check */
+    if (ts > a->stream_time) { /* R2: before the check */
+      a->stream_time = ts;
+      stmax_add(a, ts);
+    }
     const int64_t close_time = a->stream_time - a->grace;
     int64_t lo = ts - size + adv;
     if (lo < 0) lo = 0;
     for (int64_t ws = (lo / adv) * adv; ws <= ts; ws += adv) {
       if (ws + size > close_time) {
         entry* x = find_or_create(a, key, ws);
+        touch(a, x);
         if (ts > x->rowtime) x->rowtime = ts;
         apply_aggs(a, x, b, r);
         s.windows_applied++;
+        if (ws > a->obs_ws) a->obs_ws = ws;
       } else {
         s.windows_late++;
       }
     }
   }
   s.stream_time = a->stream_time;
+  finish_push(a);
   if (stats) *stats = s;
   return KHIP_OK;
 }
@@ -503,15 +587,88 @@ static int cmp_entry(const void* pa, const void* pb, void* ctx) {
   return cmp_entry2(a, *(const entry* const*)pa, a, *(const entry* const*)pb);
 }
 
+static void stmax_add(oracle_agg* a, int64_t st) {
+  if (a->n_stmax == a->cap_stmax) {
+    a->cap_stmax = a->cap_stmax ? a->cap_stmax * 2 : 256;
+    a->stmax = (int64_t*)realloc(a->stmax, sizeof(int64_t) * a->cap_stmax);
+  }
+  a->stmax[a->n_stmax++] = st;
+}
+
+static void chg_add(oracle_agg* a, int64_t idx, uint8_t tomb) {
+  if (a->n_chg == a->cap_chg) {
+    a->cap_chg = a->cap_chg ? a->cap_chg * 2 : 1024;
+    a->chg = (int64_t*)realloc(a->chg, sizeof(int64_t) * a->cap_chg);
+    a->chg_tomb = (uint8_t*)realloc(a->chg_tomb, (size_t)a->cap_chg);
+  }
+  a->chg[a->n_chg] = idx;
+  a->chg_tomb[a->n_chg++] = tomb;
+}
+
+static int cmp_chg(const void* pa, const void* pb, void* ctx) {
+  const oracle_agg* a = (const oracle_agg*)ctx;
+  return cmp_entry2(a, &a->e[*(const int64_t*)pa], a, &a->e[*(const int64_t*)pb]);
+}
+
+/* R10: the rows this push emits (after the stream time of the push is known). */
+static void finish_push(oracle_agg* a) {
+  const khip_having* hv = query_having(a);
+  a->n_chg = 0;
+  if (a->d.emit == KHIP_EMIT_FINAL) {
+    /* Every window that closed during this push (streamTime - grace passed its end), emitted iff it
+     * was still visible (R9) at the record that closed it: with the emission check after every
+     * record (Q/suppress.json's emit interval 0), that record's stream time st* is the first
+     * maximum >= ws + size + grace, and the store's obs then is floor(st* / adv) * adv. */
+    const int64_t size = a->d.size_ms, adv = a->d.advance_ms;
+    const int64_t close0 = a->st_before - a->grace, close1 = a->stream_time - a->grace;
+    for (int64_t k = 0; close1 > close0 && k < a->n; k++) {
+      const entry* x = &a->e[k];
+      const int64_t end = x->ws + size;
+      if (end <= close0 || end > close1 || !having_pass(a, hv, x)) continue;
+      const int64_t T = end + a->grace;
+      int64_t lo = 0, hi = a->n_stmax - 1; /* first maximum >= T (the last one is >= T) */
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) / 2;
+        if (a->stmax[mid] >= T) hi = mid; else lo = mid + 1;
+      }
+      if (x->ws >= (a->stmax[lo] / adv) * adv - a->retention) chg_add(a, k, 0);
+    }
+  } else {
+    for (int64_t t = 0; t < a->n_touched; t++) {
+      const entry* x = &a->e[a->touched[t]];
+      if (having_pass(a, hv, x)) chg_add(a, a->touched[t], 0);
+      else if (x->old_pass) chg_add(a, a->touched[t], 1);
+    }
+  }
+  /* sort (key, ws); a row is a tombstone iff it fails HAVING (EMIT CHANGES) */
+  if (a->n_chg > 1) {
+    qsort_r(a->chg, (size_t)a->n_chg, sizeof(int64_t), cmp_chg, a);
+    for (int64_t k = 0; k < a->n_chg; k++)
+      a->chg_tomb[k] = (uint8_t)(a->d.emit == KHIP_EMIT_FINAL ? 0 : !having_pass(a, hv, &a->e[a->chg[k]]));
+  }
+}
+
 khip_status oracle_agg_snapshot_size(oracle_agg* a, int64_t* n_rows, int64_t* key_bytes) {
   if (!a) return KHIP_E_INVALID;
-  if (n_rows) *n_rows = a->n;
-  if (key_bytes) {
-    int64_t kb = 0;
-    if (a->d.key_type == KHIP_KEY_UTF8)
-      for (int64_t k = 0; k < a->n; k++) kb += a->dict.len[a->e[k].key];
-    *key_bytes = kb;
+  const int64_t vis = visible_from(a);
+  int64_t n = 0, kb = 0;
+  for (int64_t k = 0; k < a->n; k++) {
+    if (a->e[k].ws < vis) continue;
+    n++;
+    if (a->d.key_type == KHIP_KEY_UTF8) kb += a->dict.len[a->e[k].key];
   }
+  if (n_rows) *n_rows = n;
+  if (key_bytes) *key_bytes = kb;
+  return KHIP_OK;
+}
+
+khip_status oracle_agg_changes_size(oracle_agg* a, int64_t* n_rows, int64_t* key_bytes) {
+  if (!a) return KHIP_E_INVALID;
+  int64_t kb = 0;
+  if (a->d.key_type == KHIP_KEY_UTF8)
+    for (int64_t k = 0; k < a->n_chg; k++) kb += a->dict.len[a->e[a->chg[k]].key];
+  if (n_rows) *n_rows = a->n_chg;
+  if (key_bytes) *key_bytes = kb;
   return KHIP_OK;
 }
 
@@ -568,8 +725,9 @@ khip_status oracle_agg_snapshot(oracle_agg* a, const khip_having* h, khip_snapsh
   if (h && (h->agg_index < 0 || h->agg_index >= a->d.n_aggs)) return KHIP_E_INVALID;
   entry** order = (entry**)malloc(sizeof(entry*) * (a->n + 1));
   int64_t m = 0;
+  const int64_t vis = visible_from(a);
   for (int64_t k = 0; k < a->n; k++)
-    if (having_pass(a, h, &a->e[k])) order[m++] = &a->e[k];
+    if (a->e[k].ws >= vis && having_pass(a, h, &a->e[k])) order[m++] = &a->e[k];
   qsort_r(order, (size_t)m, sizeof(entry*), cmp_entry, a);
   owned_entry* rows = (owned_entry*)malloc(sizeof(owned_entry) * (m + 1));
   for (int64_t r = 0; r < m; r++) {
@@ -582,8 +740,25 @@ khip_status oracle_agg_snapshot(oracle_agg* a, const khip_having* h, khip_snapsh
   return st;
 }
 
+khip_status oracle_agg_changes(oracle_agg* a, khip_snapshot* out, uint8_t* tombstone) {
+  if (!a || !out) return KHIP_E_INVALID;
+  owned_entry* rows = (owned_entry*)malloc(sizeof(owned_entry) * (a->n_chg + 1));
+  for (int64_t r = 0; r < a->n_chg; r++) {
+    rows[r].a = a;
+    rows[r].x = &a->e[a->chg[r]];
+  }
+  khip_status st = write_rows(rows, a->n_chg, out);
+  if (st == KHIP_OK && tombstone && a->n_chg) memcpy(tombstone, a->chg_tomb, (size_t)a->n_chg);
+  free(rows);
+  return st;
+}
+
 khip_status oracle_agg_destroy(oracle_agg* a) {
   if (!a) return KHIP_OK;
+  free(a->touched);
+  free(a->chg);
+  free(a->chg_tomb);
+  if (a->own_stmax) free(a->stmax);
   for (int64_t k = 0; k < a->n; k++) free(a->e[k].st);
   free(a->e);
   free(a->slots);
@@ -641,6 +816,7 @@ static void* shard_run(void* arg) {
     }
     if (!windowed) {
       entry* x = find_or_create(a, key, 0);
+      touch(a, x);
       if (ts > x->rowtime) x->rowtime = ts;
       apply_aggs(a, x, b, r);
       j->applied++;
@@ -652,9 +828,11 @@ static void* shard_run(void* arg) {
     for (int64_t ws = (lo / adv) * adv; ws <= ts; ws += adv) {
       if (ws + size > close_time) {
         entry* x = find_or_create(a, key, ws);
+        touch(a, x);
         if (ts > x->rowtime) x->rowtime = ts;
         apply_aggs(a, x, b, r);
         j->applied++;
+        if (ws > a->obs_ws) a->obs_ws = ws;
       } else {
         j->late++;
       }
@@ -675,13 +853,18 @@ khip_status oracle_agg_push_sharded(oracle_agg** shards, int32_t P, const khip_b
   uint32_t* sh = (uint32_t*)malloc(sizeof(uint32_t) * (n + 1));
   int64_t* cnt = (int64_t*)calloc((size_t)P + 1, sizeof(int64_t));
   int64_t st = a0->stream_time;
+  const int64_t st_before = st;
+  a0->n_stmax = 0;
   for (int64_t r = 0; r < n; r++) { /* R1 drops and R2 stream time, sequential */
     sh[r] = UINT32_MAX;
     if (!bit_get(b->key_valid, r)) { s.dropped_null_key++; continue; }
     if (!bit_get(b->row_valid, r)) { s.dropped_null_row++; continue; }
     if (b->ts[r] < 0) { s.dropped_bad_ts++; continue; }
     s.rows_accepted++;
-    if (b->ts[r] > st) st = b->ts[r];
+    if (b->ts[r] > st) {
+      st = b->ts[r];
+      stmax_add(a0, st);
+    }
     st_after[r] = st;
     sh[r] = shard_of(a0, b, r, P);
     cnt[sh[r] + 1]++;
@@ -695,6 +878,8 @@ khip_status oracle_agg_push_sharded(oracle_agg** shards, int32_t P, const khip_b
   shard_job* jobs = (shard_job*)calloc((size_t)P, sizeof(shard_job));
   pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)P);
   for (int32_t p = 0; p < P; p++) {
+    shards[p]->epoch++;
+    shards[p]->n_touched = 0;
     jobs[p].a = shards[p];
     jobs[p].b = b;
     jobs[p].idx = idx + cnt[p];
@@ -708,6 +893,20 @@ khip_status oracle_agg_push_sharded(oracle_agg** shards, int32_t P, const khip_b
     s.windows_late += jobs[p].late;
     shards[p]->stream_time = st;
   }
+  int64_t obs = -1; /* one task, one window store: the largest window start over the shards */
+  for (int32_t p = 0; p < P; p++) obs = shards[p]->obs_ws > obs ? shards[p]->obs_ws : obs;
+  for (int32_t p = 0; p < P; p++) {
+    oracle_agg* sp = shards[p];
+    sp->obs_ws = obs;
+    sp->st_before = st_before;
+    if (p) { /* every shard reads the task's stream-time maxima */
+      if (sp->own_stmax) free(sp->stmax);
+      sp->own_stmax = 0;
+      sp->stmax = a0->stmax;
+      sp->n_stmax = a0->n_stmax;
+    }
+    finish_push(sp);
+  }
   s.stream_time = st;
   if (stats) *stats = s;
   free(jobs); free(th); free(fill); free(idx); free(cnt); free(sh); free(st_after);
@@ -718,7 +917,7 @@ khip_status oracle_agg_snapshot_size_sharded(oracle_agg** shards, int32_t P, int
   int64_t n = 0, kb = 0;
   for (int32_t p = 0; p < P; p++) {
     int64_t a = 0, k = 0;
-    oracle_agg_snapshot_size(shards[p], &a, &k);
+    oracle_agg_snapshot_size(shards[p], &a, &k);  /* R9 per shard: obs is shared */
     n += a;
     kb += k;
   }
@@ -730,6 +929,7 @@ khip_status oracle_agg_snapshot_size_sharded(oracle_agg** shards, int32_t P, int
 typedef struct {
   oracle_agg* a;
   const khip_having* h;
+  int changes; /* 1: the shard's last-push changes instead of its table */
   entry** order;
   int64_t m;
 } sort_job;
@@ -739,22 +939,27 @@ static void* sort_run(void* arg) {
   oracle_agg* a = j->a;
   j->order = (entry**)malloc(sizeof(entry*) * (a->n + 1));
   j->m = 0;
+  if (j->changes) { /* the push's emitted rows, already sorted */
+    for (int64_t k = 0; k < a->n_chg; k++) j->order[j->m++] = &a->e[a->chg[k]];
+    return NULL;
+  }
+  const int64_t vis = visible_from(a);
   for (int64_t k = 0; k < a->n; k++)
-    if (having_pass(a, j->h, &a->e[k])) j->order[j->m++] = &a->e[k];
+    if (a->e[k].ws >= vis && having_pass(a, j->h, &a->e[k])) j->order[j->m++] = &a->e[k];
   qsort_r(j->order, (size_t)j->m, sizeof(entry*), cmp_entry, a);
   return NULL;
 }
 
 /* Snapshot of the union of the shards: each shard sorted on its own thread, then a P-way
  * merge (binary heap of shard cursors) into (key, ws) order. */
-khip_status oracle_agg_snapshot_sharded(oracle_agg** shards, int32_t P, const khip_having* h, khip_snapshot* out) {
-  if (!shards || P < 1 || !out) return KHIP_E_INVALID;
-  if (h && (h->agg_index < 0 || h->agg_index >= shards[0]->d.n_aggs)) return KHIP_E_INVALID;
+static khip_status merge_sharded(oracle_agg** shards, int32_t P, const khip_having* h, int changes,
+                                 khip_snapshot* out, uint8_t* tombstone) {
   sort_job* jobs = (sort_job*)calloc((size_t)P, sizeof(sort_job));
   pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)P);
   for (int32_t p = 0; p < P; p++) {
     jobs[p].a = shards[p];
     jobs[p].h = h;
+    jobs[p].changes = changes;
     pthread_create(&th[p], NULL, sort_run, &jobs[p]);
   }
   int64_t m = 0;
@@ -795,9 +1000,37 @@ khip_status oracle_agg_snapshot_sharded(oracle_agg** shards, int32_t P, const kh
 #undef LESS
 #undef HEAD
   khip_status st = write_rows(rows, m, out);
+  if (st == KHIP_OK && tombstone) /* EMIT CHANGES: a change is a tombstone iff it fails HAVING */
+    for (int64_t r = 0; r < m; r++)
+      tombstone[r] = (uint8_t)(rows[r].a->d.emit == KHIP_EMIT_FINAL ? 0
+                                                                     : !having_pass(rows[r].a, query_having(rows[r].a), rows[r].x));
   for (int32_t p = 0; p < P; p++) free(jobs[p].order);
   free(rows); free(cur); free(heap); free(jobs); free(th);
   return st;
+}
+
+khip_status oracle_agg_snapshot_sharded(oracle_agg** shards, int32_t P, const khip_having* h, khip_snapshot* out) {
+  if (!shards || P < 1 || !out) return KHIP_E_INVALID;
+  if (h && (h->agg_index < 0 || h->agg_index >= shards[0]->d.n_aggs)) return KHIP_E_INVALID;
+  return merge_sharded(shards, P, h, 0, out, NULL);
+}
+
+khip_status oracle_agg_changes_size_sharded(oracle_agg** shards, int32_t P, int64_t* n_rows, int64_t* key_bytes) {
+  int64_t n = 0, kb = 0;
+  for (int32_t p = 0; p < P; p++) {
+    int64_t a = 0, k = 0;
+    oracle_agg_changes_size(shards[p], &a, &k);
+    n += a;
+    kb += k;
+  }
+  if (n_rows) *n_rows = n;
+  if (key_bytes) *key_bytes = kb;
+  return KHIP_OK;
+}
+
+khip_status oracle_agg_changes_sharded(oracle_agg** shards, int32_t P, khip_snapshot* out, uint8_t* tombstone) {
+  if (!shards || P < 1 || !out) return KHIP_E_INVALID;
+  return merge_sharded(shards, P, NULL, 1, out, tombstone);
 }
 
 /* --------------------------------------------------------------- join table */

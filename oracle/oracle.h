@@ -32,6 +32,11 @@ khip_status oracle_agg_snapshot(oracle_agg* agg, const khip_having* having,
                                 khip_snapshot* out);
 khip_status oracle_agg_destroy(oracle_agg* agg);
 
+/* Rows the last push emitted (R10), snapshot layout sorted by (key, ws); tombstone[r] = 1
+ * for a HAVING delete.  Mirrors khip_agg_changes_size / khip_agg_changes. */
+khip_status oracle_agg_changes_size(oracle_agg* agg, int64_t* n_rows, int64_t* key_bytes);
+khip_status oracle_agg_changes(oracle_agg* agg, khip_snapshot* out, uint8_t* tombstone);
+
 /* Key-sharded P-thread restatement (same results as oracle_agg_push over the batch): shards[]
  * are P handles created with the same descriptor and only ever pushed together. */
 khip_status oracle_agg_push_sharded(oracle_agg** shards, int32_t P, const khip_batch* batch,
@@ -40,6 +45,8 @@ khip_status oracle_agg_snapshot_size_sharded(oracle_agg** shards, int32_t P, int
                                              int64_t* key_bytes);
 khip_status oracle_agg_snapshot_sharded(oracle_agg** shards, int32_t P, const khip_having* having,
                                         khip_snapshot* out);
+khip_status oracle_agg_changes_size_sharded(oracle_agg** shards, int32_t P, int64_t* n_rows, int64_t* key_bytes);
+khip_status oracle_agg_changes_sharded(oracle_agg** shards, int32_t P, khip_snapshot* out, uint8_t* tombstone);
 
 khip_status oracle_table_create(const khip_table_desc* desc, oracle_table** out);
 khip_status oracle_table_upsert(oracle_table* t, const khip_batch* rows);

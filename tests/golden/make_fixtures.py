@@ -45,6 +45,9 @@ UNIT_MS = {"MILLISECOND": 1, "MILLISECONDS": 1, "SECOND": 1000, "SECONDS": 1000,
            "DAY": 86400000, "DAYS": 86400000}
 
 
+EMIT_INTERVAL = "ksql.streams.__emit.interval.ms.kstreams.windowed.aggregation__"
+
+
 class Skip(Exception):
     pass
 
@@ -124,7 +127,7 @@ def duration_ms(text):
 
 
 def parse_window(kind, body):
-    size = adv = grace = None
+    size = adv = grace = retention = None
     for part in split_top(body):
         p = part.strip()
         up = p.upper()
@@ -135,7 +138,7 @@ def parse_window(kind, body):
         elif up.startswith("GRACE PERIOD"):
             grace = duration_ms(p[12:])
         elif up.startswith("RETENTION"):
-            pass  # retention >= size + grace never drops more
+            retention = duration_ms(p[9:])
         else:
             raise Skip("window clause " + p)
     if size is None:
@@ -145,7 +148,7 @@ def parse_window(kind, body):
     if adv is None:
         raise Skip("hopping advance")
     return {"kind": kind, "size_ms": size, "advance_ms": adv,
-            "grace_ms": -1 if grace is None else grace}
+            "grace_ms": -1 if grace is None else grace, "retention_ms": -1 if retention is None else retention}
 
 
 AGG_RE = re.compile(r"(?is)^(COUNT|SUM|MIN|MAX|AVG)\s*\(\s*(.*?)\s*\)$")
@@ -249,9 +252,10 @@ def extract_agg(path, test, fmt_tag):
     src = parse_create_source(st[0], "STREAM")
     m = re.match(r"(?is)^\s*CREATE\s+TABLE\s+(\w+)\s+AS\s+SELECT\s+(.*?)\s+FROM\s+(\w+)(\s+\w+)?\s+"
                  r"(WINDOW\s+(TUMBLING|HOPPING)\s*\((.*?)\)\s+)?GROUP\s+BY\s+(.*?)"
-                 r"(\s+HAVING\s+(.*?))?\s*(EMIT\s+CHANGES)?\s*;?\s*$", st[1])
+                 r"(\s+HAVING\s+(.*?))?\s*(EMIT\s+(CHANGES|FINAL))?\s*;?\s*$", st[1])
     if not m:
         raise Skip("ctas shape")
+    emit = (m.group(12) or "CHANGES").upper()
     out_name = m.group(1).upper()
     if m.group(3).upper() != src["name"]:
         raise Skip("from")
@@ -347,7 +351,9 @@ def extract_agg(path, test, fmt_tag):
             row["cols"].append(v)
         rows.append(row)
 
-    # expected final state: last output per (key, window)
+    # expected output sequence (the table's changelog: one record per update, cache off) and
+    # final state: last output per (key, window)
+    outputs = []
     state = collections.OrderedDict()
     for o in test.get("outputs", []):
         if o.get("topic", "").upper() != out_name:
@@ -364,6 +370,7 @@ def extract_agg(path, test, fmt_tag):
         v = o.get("value")
         if v is None:
             state[(okey, ws)] = None
+            outputs.append({"key": okey, "ws": ws, "we": we, "rowtime": o.get("timestamp"), "tombstone": True})
             continue
         if isinstance(v, str):
             parts = v.split(",")
@@ -401,6 +408,7 @@ def extract_agg(path, test, fmt_tag):
                 present[oc["agg"]] = True
         state[(okey, ws)] = {"key": okey, "ws": ws, "we": we, "rowtime": o.get("timestamp"),
                              "values": aggv, "present": present}
+        outputs.append(dict(state[(okey, ws)], tombstone=False))
     expected = [v for v in state.values() if v is not None]
     expected.sort(key=lambda e: ((e["key"].encode() if isinstance(e["key"], str) else e["key"]), e["ws"]))
 
@@ -412,6 +420,8 @@ def extract_agg(path, test, fmt_tag):
             "size_ms": window["size_ms"] if window else 0,
             "advance_ms": window["advance_ms"] if window else 0,
             "grace_ms": window["grace_ms"] if window else -1,
+            "retention_ms": window["retention_ms"] if window else -1,
+            "emit": emit,
             "key_type": "UTF8" if gtype == "STRING" else "INT64",
             "col_types": col_types,
             "aggs": spec_aggs,
@@ -420,6 +430,7 @@ def extract_agg(path, test, fmt_tag):
         },
         "input": rows,
         "expected": expected,
+        "outputs": outputs,
     }
 
 
@@ -538,7 +549,9 @@ def main():
         except ValueError:
             continue
         for test in doc.get("tests", []):
-            if "expectedException" in test or test.get("properties"):
+            props = dict(test.get("properties") or {})
+            props.pop(EMIT_INTERVAL, None)  # 0 in every case that sets it: emit at every record
+            if "expectedException" in test or props:
                 continue
             for fmt_tag, t in expand_formats(test):
                 st = t.get("statements", [])

@@ -19,11 +19,14 @@ def load_cases(kind):
         return json.load(f)["cases"]
 
 
-def case_desc(case, device=0, flags=0):
+def case_desc(case, device=0, flags=0, changelog=True):
     d = case["desc"]
     return abi.make_agg_desc(d["window_kind"], d["key_type"], d["size_ms"], d["advance_ms"],
                              d["grace_ms"], d["col_types"],
-                             [(a["kind"], a["arg_col"]) for a in d["aggs"]], device=device, flags=flags)
+                             [(a["kind"], a["arg_col"]) for a in d["aggs"]], device=device,
+                             flags=flags | (abi.FLAG_CHANGELOG if changelog else 0),
+                             retention_ms=d.get("retention_ms", -1),
+                             emit=d.get("emit", "CHANGES"), having=d["having"])
 
 
 def case_batch(case, lo=0, hi=None):
@@ -45,9 +48,49 @@ def case_batch(case, lo=0, hi=None):
                          key_valid=key_valid, row_valid=row_valid, cols=cols, col_valid=cvalid)
 
 
-def run_agg_case(lib, case, split=None, device=0, flags=0):
-    """split: None = one batch; k = batches of k rows (exercises cross-batch state)."""
+def _rows_of(chg):
+    """khip_agg_changes output → list of row dicts (emission order)."""
+    out = []
+    for i in range(chg["n"]):
+        k = chg["key"][i]
+        out.append({"key": k if isinstance(k, str) else int(k), "ws": int(chg["ws"][i]), "we": int(chg["we"][i]),
+                    "rowtime": int(chg["rowtime"][i]), "tombstone": bool(chg["tombstone"][i]),
+                    "values": [v[i].item() for v in chg["values"]], "nulls": [bool(x[i]) for x in chg["nulls"]]})
+    return out
+
+
+def run_agg_outputs(lib, case, split=None, device=0, flags=0):
+    """The emitted changelog: pushes of `split` rows (None = one batch), the rows each push emits
+    (khip_agg_changes), concatenated in emission order."""
     h = abi.AggHandle(lib, case_desc(case, device, flags))
+    n = len(case["input"])
+    step = n if not split else split
+    rows = []
+    for lo in range(0, max(n, 1), max(step, 1)):
+        h.push(case_batch(case, lo, lo + step))
+        rows += _rows_of(h.changes())
+    h.close()
+    return rows
+
+
+def fold(rows):
+    """Changelog → final table (last row per (key, window), tombstones delete), snapshot layout."""
+    state = {}
+    for r in rows:
+        state[(r["key"], r["ws"])] = None if r["tombstone"] else r
+    live = sorted((r for r in state.values() if r is not None),
+                  key=lambda r: ((r["key"].encode() if isinstance(r["key"], str) else r["key"]), r["ws"]))
+    na = len(live[0]["values"]) if live else 0
+    return {"n": len(live), "key": [r["key"] for r in live], "ws": np.array([r["ws"] for r in live], np.int64),
+            "we": np.array([r["we"] for r in live], np.int64), "rowtime": np.array([r["rowtime"] for r in live], np.int64),
+            "values": [np.array([r["values"][a] for r in live]) for a in range(na)],
+            "nulls": [np.array([r["nulls"][a] for r in live], bool) for a in range(na)]}
+
+
+def run_agg_store(lib, case, split=None, device=0, flags=0):
+    """The window store after every record (khip_agg_snapshot with the query's HAVING): what a
+    pull query sees — retention applied, tombstoned rows absent."""
+    h = abi.AggHandle(lib, case_desc(case, device, flags, changelog=False))
     n = len(case["input"])
     step = n if not split else split
     for lo in range(0, max(n, 1), max(step, 1)):
@@ -55,6 +98,43 @@ def run_agg_case(lib, case, split=None, device=0, flags=0):
     snap = h.snapshot(case["desc"]["having"])
     h.close()
     return snap
+
+
+def run_agg_case(lib, case, split=None, device=0, flags=0):
+    """The final table the query emitted (fold of its changelog; the reference's expected final
+    state is the last output per (key, window)).  split: None = one batch; k = batches of k rows."""
+    return fold(run_agg_outputs(lib, case, split, device, flags))
+
+
+def compare_outputs(case, rows):
+    """Emitted rows vs the QTT expected output sequence, in order (1-row pushes = the reference's
+    cache-off, emit-every-record run).  Returns mismatch descriptions."""
+    exp = case["outputs"]
+    errs = []
+    if len(rows) != len(exp):
+        errs.append("output count %d != expected %d" % (len(rows), len(exp)))
+    for i, (r, e) in enumerate(zip(rows, exp)):
+        if r["key"] != e["key"] or r["ws"] != e["ws"] or r["we"] != e["we"]:
+            errs.append("out %d (%r,%d,%d) != (%r,%d,%d)" % (i, r["key"], r["ws"], r["we"], e["key"], e["ws"], e["we"]))
+            continue
+        if r["tombstone"] != e["tombstone"]:
+            errs.append("out %d tombstone %r != %r" % (i, r["tombstone"], e["tombstone"]))
+            continue
+        if e["rowtime"] is not None and r["rowtime"] != e["rowtime"]:
+            errs.append("out %d timestamp %d != %d" % (i, r["rowtime"], e["rowtime"]))
+        if e["tombstone"]:
+            continue
+        for a, (v, present) in enumerate(zip(e["values"], e["present"])):
+            if not present:
+                continue
+            if v is None:
+                if not r["nulls"][a]:
+                    errs.append("out %d agg %d expected null" % (i, a))
+            elif r["nulls"][a]:
+                errs.append("out %d agg %d unexpected null" % (i, a))
+            elif not _num_eq(r["values"][a], v):
+                errs.append("out %d agg %d %r != %r" % (i, a, r["values"][a], v))
+    return errs
 
 
 def _num_eq(a, b):

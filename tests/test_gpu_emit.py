@@ -1,0 +1,175 @@
+"""Emission and retention on the HIP path (khip_agg_changes, include/ksqldb_hip.h), against the
+oracle's rules R9 (retention) and R10 (emission), themselves pinned by the QTT goldens
+(test_oracle_golden.py: output sequences of having.json, suppress.json, ...).
+
+1. EMIT CHANGES: after every push, the rows the push emitted (deduplicated per (key, window),
+   sorted) and their tombstone flags equal the oracle's — random micro-batches with late
+   records, hopping fan-out, UTF-8 keys, HAVING on integer and DOUBLE aggregates, both
+   partitioned-engine claim modes (packed identity / claim protocol) and many partitions.
+2. EMIT FINAL: windows closed by each push, minus those that expired before the record that
+   closed them (stream-time jumps inside a push), both engines, default and explicit RETENTION.
+3. Retention: the window store (snapshot, pull query, row count) drops expired windows exactly
+   like the oracle's store, across pushes that evict and purge the closed store.
+"""
+import numpy as np
+import pytest
+
+from ksql_amd import abi
+from test_gpu_parity import ABS_SUM, ALL_AGGS, CNT_DBL, WINDOWS, _random_batch, assert_snap_equal
+
+pytestmark = pytest.mark.gpu
+
+COLS = ["INT32", "INT64", "DOUBLE", "DOUBLE"]
+
+
+@pytest.fixture(scope="module")
+def prod():
+    return abi.load_product()
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return abi.load_oracle()
+
+
+def _assert_changes_equal(g, o, desc):
+    assert_snap_equal(g, o, desc, ABS_SUM, CNT_DBL)
+    assert np.array_equal(g["tombstone"], o["tombstone"])
+
+
+def _batches(rng, nb, n, key_type, nkeys, span, disorder, jump=0):
+    out = []
+    t0 = 0
+    for b in range(nb):
+        out.append(_random_batch(rng, n, key_type, nkeys, span, disorder, t0=t0, neg_ts=0.005))
+        t0 += span * 3 // 4 + (jump if b % 2 else 0)
+    return out
+
+
+HAVINGS = [None, {"agg": 0, "op": "GT", "value": 3}, {"agg": 13, "op": "LE", "value": 10.5}]
+
+
+@pytest.mark.parametrize("engine", [0, abi.FLAG_PART_CLAIM])
+@pytest.mark.parametrize("having", range(len(HAVINGS)))
+@pytest.mark.parametrize("win", range(len(WINDOWS)))
+def test_changes_vs_oracle(prod, orc, win, having, engine):
+    rng = np.random.default_rng(300 + 10 * win + having)
+    hv = HAVINGS[having]
+    kw = dict(WINDOWS[win], key_type="INT64", col_types=COLS, aggs=ALL_AGGS, having=hv)
+    g = abi.AggHandle(prod, abi.make_agg_desc(**dict(kw, flags=engine | abi.FLAG_CHANGELOG)))
+    o = abi.AggHandle(orc, abi.make_agg_desc(**kw))
+    for batch in _batches(rng, 5, 6000, "INT64", 400, 120_000, 30_000):
+        assert g.push(batch) == o.push(batch)
+        gc, oc = g.changes(), o.changes()
+        assert gc["n"] > 0
+        _assert_changes_equal(gc, oc, g.desc)
+    assert_snap_equal(g.snapshot(hv), o.snapshot(hv), g.desc, ABS_SUM, CNT_DBL)
+    g.close()
+    o.close()
+
+
+def test_changes_utf8_and_many_partitions(prod, orc):
+    rng = np.random.default_rng(7)
+    hv = {"agg": 0, "op": "GE", "value": 2}
+    for key_type, hint, nkeys in (("UTF8", 0, 500), ("INT64", 30_000_000, 40_000)):
+        kw = dict(WINDOWS[3], key_type=key_type, col_types=COLS, aggs=ALL_AGGS, having=hv, capacity_hint=hint)
+        g = abi.AggHandle(prod, abi.make_agg_desc(**dict(kw, flags=abi.FLAG_CHANGELOG)))
+        o = abi.AggHandle(orc, abi.make_agg_desc(**kw))
+        for batch in _batches(rng, 3, 60_000, key_type, nkeys, 200_000, 20_000):
+            assert g.push(batch) == o.push(batch)
+            _assert_changes_equal(g.changes(), o.changes(), g.desc)
+        g.close()
+        o.close()
+
+
+def test_changes_one_record_pushes_match_sequence(prod, orc):
+    """Tiny pushes (1-3 records) exercise the cache-off sequence with tombstones."""
+    rng = np.random.default_rng(9)
+    hv = {"agg": 3, "op": "GT", "value": 0}  # SUM(BIGINT) > 0 flips back and forth
+    kw = dict(WINDOWS[4], key_type="INT64", col_types=COLS, aggs=ALL_AGGS, having=hv)
+    g = abi.AggHandle(prod, abi.make_agg_desc(**dict(kw, flags=abi.FLAG_CHANGELOG)))
+    o = abi.AggHandle(orc, abi.make_agg_desc(**kw))
+    big = _random_batch(rng, 300, "INT64", 5, 100_000, 20_000)
+    i = 0
+    tombs = 0
+    while i < 300:
+        k = int(rng.integers(1, 4))
+        sl = slice(i, min(i + k, 300))
+        b = abi.HostBatch(big.ts[sl], keys=big.keys[sl], cols=[c[sl] for c in big.cols],
+                          col_valid=[None if v is None else np.unpackbits(v, bitorder="little")[:300][sl].astype(bool)
+                                     for v in big.col_valid])
+        assert g.push(b) == o.push(b)
+        gc, oc = g.changes(), o.changes()
+        _assert_changes_equal(gc, oc, g.desc)
+        tombs += int(gc["tombstone"].sum())
+        i = sl.stop
+    assert tombs > 0
+    g.close()
+    o.close()
+
+
+@pytest.mark.parametrize("engine", [0, abi.FLAG_PART_CLAIM, abi.FLAG_ENGINE_ATOMIC])
+@pytest.mark.parametrize("retention", [-1, 200_000])
+@pytest.mark.parametrize("win", [2, 3, 4])
+def test_emit_final_vs_oracle(prod, orc, win, retention, engine):
+    """EMIT FINAL with stream-time jumps inside pushes (windows that expire before they close are
+    lost, as in Q/suppress.json 'tumbling windows'), HAVING on COUNT(*)."""
+    rng = np.random.default_rng(500 + win)
+    w = WINDOWS[win]
+    hv = {"agg": 0, "op": "GT", "value": 1}
+    kw = dict(w, key_type="INT64", col_types=COLS, aggs=ALL_AGGS, having=hv, emit="FINAL", retention_ms=retention)
+    g = abi.AggHandle(prod, abi.make_agg_desc(**dict(kw, flags=engine)))
+    o = abi.AggHandle(orc, abi.make_agg_desc(**kw))
+    emitted = 0
+    for b in range(6):
+        n = 5000
+        ts = b * 100_000 + np.sort(rng.integers(0, 80_000, n)) + rng.integers(0, 5_000, n)
+        jump = rng.random(n) < 0.002  # single records far ahead: close + expire in one step
+        ts = np.where(jump, ts + rng.integers(50_000, 400_000, n), ts)
+        ts = np.maximum.accumulate(ts) if b % 2 else ts
+        keys = rng.integers(0, 200, n)
+        cols = [rng.integers(-9, 9, n).astype(np.int32), rng.integers(-9, 9, n), rng.random(n), rng.random(n)]
+        batch = abi.HostBatch(ts, keys=keys, cols=cols)
+        assert g.push(batch) == o.push(batch)
+        gc, oc = g.changes(), o.changes()
+        _assert_changes_equal(gc, oc, g.desc)
+        emitted += gc["n"]
+    assert emitted > 0
+    assert_snap_equal(g.snapshot(), o.snapshot(), g.desc, ABS_SUM, CNT_DBL)
+    g.close()
+    o.close()
+
+
+@pytest.mark.parametrize("engine", [0, abi.FLAG_ENGINE_ATOMIC])
+@pytest.mark.parametrize("retention", [-1, 90_000])
+def test_retention_store_vs_oracle(prod, orc, retention, engine):
+    """The store after each push: snapshot, HAVING count, pull queries (keys + window bounds)."""
+    rng = np.random.default_rng(17)
+    hv = {"agg": 0, "op": "GT", "value": 2}
+    kw = dict(window_kind="HOPPING", size_ms=30_000, advance_ms=10_000, grace_ms=5_000, retention_ms=retention,
+              key_type="INT64", col_types=COLS, aggs=ALL_AGGS, having=hv, capacity_hint=20_000)
+    g = abi.AggHandle(prod, abi.make_agg_desc(**dict(kw, flags=engine)))
+    o = abi.AggHandle(orc, abi.make_agg_desc(**kw))
+    for batch in _batches(rng, 6, 8000, "INT64", 300, 100_000, 10_000, jump=150_000):
+        assert g.push(batch) == o.push(batch)
+        gs, os_ = g.snapshot(), o.snapshot()
+        assert_snap_equal(gs, os_, g.desc, ABS_SUM, CNT_DBL)
+        assert g.snapshot_size() == os_["n"]
+        assert g.count_rows(hv) == o.snapshot(hv)["n"]
+        keys = rng.choice(os_["key"], 10) if os_["n"] else np.array([1])
+        q = g.get(keys=keys)
+        sel = np.isin(os_["key"], keys)
+        assert np.array_equal(q["key"], os_["key"][sel]) and np.array_equal(q["ws"], os_["ws"][sel])
+    g.close()
+    o.close()
+
+
+def test_changes_need_the_flag(prod):
+    h = abi.AggHandle(prod, abi.make_agg_desc(**dict(WINDOWS[1], key_type="INT64", aggs=[("COUNT_STAR", -1)])))
+    h.push(abi.HostBatch(np.arange(10), keys=np.arange(10)))
+    with pytest.raises(abi.KsqlHipError):
+        h.changes()
+    h.close()
+    with pytest.raises(abi.KsqlHipError):  # the atomic engine keeps no EMIT CHANGES changelog
+        abi.AggHandle(prod, abi.make_agg_desc(**dict(WINDOWS[1], key_type="INT64", aggs=[("COUNT_STAR", -1)],
+                                                     flags=abi.FLAG_ENGINE_ATOMIC | abi.FLAG_CHANGELOG)))

@@ -40,11 +40,29 @@ def engine(request):
     return ENGINES[request.param]
 
 
+def _emits(case, engine):
+    """The global-atomic engine keeps no per-push changelog (EMIT CHANGES); EMIT FINAL it has."""
+    return engine != abi.FLAG_ENGINE_ATOMIC or case["desc"].get("emit") == "FINAL"
+
+
 @pytest.mark.parametrize("split", [None, 1, 3])
 @pytest.mark.parametrize("case", AGG_CASES, ids=["%s %s" % (c["source"], c["name"]) for c in AGG_CASES])
-def test_qtt_aggregate_golden(prod, case, split, engine):
-    snap = qtt.run_agg_case(prod, case, split, flags=engine)
-    assert qtt.compare_agg(case, snap) == []
+def test_qtt_aggregate_golden(prod, orc, case, split, engine):
+    """The final table the query emitted (fold of khip_agg_changes over the pushes) equals the
+    reference's (last output per (key, window)); and the window store equals the oracle's."""
+    if _emits(case, engine):
+        assert qtt.compare_agg(case, qtt.run_agg_case(prod, case, split, flags=engine)) == []
+    desc = qtt.case_desc(case)
+    assert_snap_equal(qtt.run_agg_store(prod, case, split, flags=engine), qtt.run_agg_store(orc, case, split), desc)
+
+
+@pytest.mark.parametrize("case", AGG_CASES, ids=["%s %s" % (c["source"], c["name"]) for c in AGG_CASES])
+def test_qtt_output_sequence(prod, case, engine):
+    """Every output record of the reference, in order (HAVING tombstones, EMIT FINAL), from
+    one-record pushes (the reference's cache-off run)."""
+    if not _emits(case, engine):
+        pytest.skip("EMIT CHANGES changelog: partitioned engine only")
+    assert qtt.compare_outputs(case, qtt.run_agg_outputs(prod, case, 1, flags=engine)) == []
 
 
 @pytest.mark.parametrize("case", JOIN_CASES, ids=["%s %s" % (c["source"], c["name"]) for c in JOIN_CASES])

@@ -33,6 +33,13 @@ def test_oracle_aggregate_golden(orc, case, split):
     assert qtt.compare_agg(case, qtt.run_agg_case(orc, case, split)) == []
 
 
+@pytest.mark.parametrize("case", AGG_CASES, ids=["%s %s" % (c["source"], c["name"]) for c in AGG_CASES])
+def test_oracle_output_sequence_golden(orc, case):
+    """Every output record the reference emits, in order: pushes of one record each are the
+    reference's cache-off, emit-at-every-record run (HAVING tombstones, EMIT FINAL)."""
+    assert qtt.compare_outputs(case, qtt.run_agg_outputs(orc, case, 1)) == []
+
+
 @pytest.mark.parametrize("case", JOIN_CASES, ids=["%s %s" % (c["source"], c["name"]) for c in JOIN_CASES])
 def test_oracle_join_golden(orc, case):
     assert qtt.compare_join(case, qtt.run_join_case(orc, case)) == []
