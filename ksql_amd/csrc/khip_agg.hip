@@ -749,7 +749,8 @@ namespace khip {
 int64_t visible_from(const khip_agg* a) {
   if (!a->windowed || a->host_stream_time < 0) return INT64_MIN;
   const int64_t adv = a->desc.advance_ms;
-  return a->host_stream_time / adv * adv - a->retention;  // the store's observed time - retention
+  const int64_t vf = a->host_stream_time / adv * adv - a->retention;  // the store's observed time - retention
+  return vf > 0 ? vf : INT64_MIN;  // window starts are >= 0: nothing has expired yet
 }
 
 // EMIT FINAL: the window starts this batch closes after they expired (k_emit_lost), computed from

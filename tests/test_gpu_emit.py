@@ -58,11 +58,13 @@ def test_changes_vs_oracle(prod, orc, win, having, engine):
     kw = dict(WINDOWS[win], key_type="INT64", col_types=COLS, aggs=ALL_AGGS, having=hv)
     g = abi.AggHandle(prod, abi.make_agg_desc(**dict(kw, flags=engine | abi.FLAG_CHANGELOG)))
     o = abi.AggHandle(orc, abi.make_agg_desc(**kw))
+    emitted = 0
     for batch in _batches(rng, 5, 6000, "INT64", 400, 120_000, 30_000):
         assert g.push(batch) == o.push(batch)
         gc, oc = g.changes(), o.changes()
-        assert gc["n"] > 0
         _assert_changes_equal(gc, oc, g.desc)
+        emitted += gc["n"]
+    assert emitted > 0 or (win == 2 and having == 1)  # sparse tumbling windows: no count above 3
     assert_snap_equal(g.snapshot(hv), o.snapshot(hv), g.desc, ABS_SUM, CNT_DBL)
     g.close()
     o.close()

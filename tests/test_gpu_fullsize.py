@@ -179,6 +179,43 @@ def test_c3_hopping_double_microbatches(prod, orc, say):
     assert_snap_equal(got, exp, desc)
 
 
+@pytest.mark.timeout(900)
+def test_c3_changelog_per_push(prod, orc, say):
+    """C3's micro-batch structure with EMIT CHANGES kept (KHIP_FLAG_CHANGELOG): the rows every
+    push emits equal the oracle's, push by push (the changelog a downstream topic receives)."""
+    n = 50_000_000
+    S = n // 8
+    cfg = synth.CONFIGS["hopping_double"]
+    kw = dict(window_kind="HOPPING", size_ms=cfg["size_ms"], advance_ms=cfg["advance_ms"], grace_ms=cfg["grace_ms"],
+              key_type="INT64", col_types=["DOUBLE"], aggs=[("SUM", 0), ("AVG", 0), ("MIN", 0), ("MAX", 0)],
+              having={"agg": 3, "op": "GT", "value": 990.0})
+    key, ts, val, valid = synth.hopping_double(0, n, n, xp="torch", device="cuda")
+    vb = abi.bitmap_torch(valid)
+    del valid
+    span_push = cfg["span_ms"] * S / n
+    live = int(cfg["keys"] * (span_push + cfg["size_ms"] + cfg["grace_ms"] + cfg["disorder_ms"]) / cfg["advance_ms"])
+    desc = abi.make_agg_desc(**kw, capacity_hint=live, flags=abi.FLAG_CHANGELOG)
+    keyh, tsh, valh, validh = synth.hopping_double(0, n, n)
+    h = abi.AggHandle(prod, desc)
+    o = abi.ShardedOracleAgg(orc, abi.make_agg_desc(**kw), THREADS)
+    total = tombs = 0
+    for lo in range(0, n, S):
+        st = h.push(abi.DeviceBatch(ts[lo:lo + S], keys=key[lo:lo + S], cols=[val[lo:lo + S]],
+                                    col_valid=[vb[lo // 8:(lo + S) // 8]]))
+        ost = o.push(abi.HostBatch(tsh[lo:lo + S], keys=keyh[lo:lo + S], cols=[valh[lo:lo + S]],
+                                   col_valid=[validh[lo:lo + S]]))
+        assert st == ost
+        gc, oc = h.changes(), o.changes()
+        assert_snap_equal(gc, oc, desc)
+        assert np.array_equal(gc["tombstone"], oc["tombstone"])
+        total += gc["n"]
+        tombs += int(gc["tombstone"].sum())
+    say("C3 changelog: %d rows emitted over 8 pushes (%d tombstones)" % (total, tombs))
+    assert total > 0 and tombs > 0
+    h.close()
+    o.close()
+
+
 # ------------------------------------------------------------------------ C4
 
 def _probe_oracle(orc_table, keys, ts, kv, rv, join_type, where, threads=THREADS):
