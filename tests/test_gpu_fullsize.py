@@ -188,7 +188,7 @@ def test_c3_changelog_per_push(prod, orc, say):
     cfg = synth.CONFIGS["hopping_double"]
     kw = dict(window_kind="HOPPING", size_ms=cfg["size_ms"], advance_ms=cfg["advance_ms"], grace_ms=cfg["grace_ms"],
               key_type="INT64", col_types=["DOUBLE"], aggs=[("SUM", 0), ("AVG", 0), ("MIN", 0), ("MAX", 0)],
-              having={"agg": 3, "op": "GT", "value": 990.0})
+              having={"agg": 1, "op": "GT", "value": 500.0})
     key, ts, val, valid = synth.hopping_double(0, n, n, xp="torch", device="cuda")
     vb = abi.bitmap_torch(valid)
     del valid
