@@ -22,6 +22,14 @@
 // Probe: one thread per stream row, coalesced key/ts loads, one slot line per probe;
 // output is row-aligned (selection bitmaps built with __ballot, 8 B per wave) so no
 // compaction pass is needed on the device path.
+//
+// Dense probe index (one INT/BIGINT value column, keys in a range at most 4x the live key
+// count, e.g. C4's users 1..1e8): cell[key - kmin] of W = 1/2/4/8 bytes, bit 0 live, bit 1
+// NULL value, bits 2.. value - vmin.  C4 is 1e8 one-byte cells (100 MB): it stays in the
+// 256 MB MALL, so the probes' random reads are cache hits instead of random 64 B HBM lines
+// into the 8.6 GB slot table.  Built from the slot table on the first probe after it became
+// eligible and kept in step by the upserts' winning rows (a key or value outside the index's
+// ranges drops it; the next probe rebuilds it over the new ranges).
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -115,17 +123,63 @@ __global__ __launch_bounds__(256) void k_upsert_finalize(uint64_t* __restrict__ 
   }
 }
 
+// Dense probe index parameters (active = 0: none).
+struct JDense {
+  int32_t active;
+  int32_t w;         // cell bytes: 1, 2, 4, 8
+  int64_t kmin, nkeys;  // cells for keys kmin .. kmin + nkeys - 1
+  int64_t vmin;
+  uint64_t vspan;    // values vmin .. vmin + vspan - 1 encodable
+  uint8_t* cells;
+  int* invalid;      // set when an upsert falls outside the ranges
+};
+
+__device__ __forceinline__ void dense_store(const JDense& d, int64_t idx, uint64_t cell) {
+  switch (d.w) {
+    case 1: d.cells[idx] = (uint8_t)cell; break;
+    case 2: ((uint16_t*)d.cells)[idx] = (uint16_t)cell; break;
+    case 4: ((uint32_t*)d.cells)[idx] = (uint32_t)cell; break;
+    default: ((uint64_t*)d.cells)[idx] = cell; break;
+  }
+}
+
+__device__ __forceinline__ uint64_t dense_load(const JDense& d, int64_t idx) {
+  switch (d.w) {
+    case 1: return d.cells[idx];
+    case 2: return ((const uint16_t*)d.cells)[idx];
+    case 4: return ((const uint32_t*)d.cells)[idx];
+    default: return ((const uint64_t*)d.cells)[idx];
+  }
+}
+
+// The cell of a live key (value word raw, NULL flag) — false if it does not fit the index.
+__device__ __forceinline__ bool dense_cell(const JDense& d, uint64_t raw, bool isnull, uint64_t* cell) {
+  if (isnull) {
+    *cell = 3;
+    return true;
+  }
+  const uint64_t off = (uint64_t)((int64_t)raw - d.vmin);
+  if ((int64_t)raw < d.vmin || off >= d.vspan) return false;
+  *cell = 1 | (off << 2);
+  return true;
+}
+
 __global__ __launch_bounds__(256) void k_upsert_apply(uint64_t* __restrict__ table, int sw,
                                                       const int64_t* __restrict__ slot_of,
-                                                      const uint8_t* __restrict__ rv, int64_t n, int ncols, const int32_t* __restrict__ types_dev, JCols cols) {
+                                                      const uint8_t* __restrict__ rv, int64_t n, int ncols, const int32_t* __restrict__ types_dev, JCols cols,
+                                                      JDense dn) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t slot = slot_of[i];
     if (slot < 0) continue;
     uint64_t* s = table + slot * (uint64_t)sw;
     if (s[2] != (uint64_t)(i + 1)) continue;  // not the last writer of this key
     s[2] = 0;  // only the winner matches: clearing cannot change another row's decision
+    const int64_t kidx = (int64_t)s[0] - dn.kmin;
+    const bool kin = dn.active && (int64_t)s[0] >= dn.kmin && kidx < dn.nkeys;
+    if (dn.active && !kin) *dn.invalid = 1;
     if (!bit_get(rv, i)) {
       s[1] = M_RESIDENT;  // tombstone: delete
+      if (kin) dense_store(dn, kidx, 0);
       continue;
     }
     uint64_t nullmask = 0;
@@ -141,6 +195,63 @@ __global__ __launch_bounds__(256) void k_upsert_apply(uint64_t* __restrict__ tab
       s[3 + c] = w;
     }
     s[1] = M_RESIDENT | M_LIVE | nullmask;
+    if (kin) {
+      uint64_t cell;
+      if (dense_cell(dn, s[3], nullmask & 1, &cell)) dense_store(dn, kidx, cell);
+      else *dn.invalid = 1;
+    }
+  }
+}
+
+// Ranges of the live slots: [kmin, kmax, vmin, vmax, live] (value over non-null values).
+__global__ __launch_bounds__(256) void k_table_ranges(const uint64_t* __restrict__ table, int64_t cap, int sw,
+                                                      unsigned long long* __restrict__ out) {
+  int64_t kmn = INT64_MAX, kmx = INT64_MIN, vmn = INT64_MAX, vmx = INT64_MIN, live = 0;
+  for (int64_t slot = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; slot < cap;
+       slot += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t* s = table + slot * (uint64_t)sw;
+    const uint64_t m = s[1];
+    if (!(m & M_LIVE)) continue;
+    const int64_t k = (int64_t)s[0];
+    kmn = k < kmn ? k : kmn;
+    kmx = k > kmx ? k : kmx;
+    live++;
+    if (!(m & 1)) {
+      const int64_t v = (int64_t)s[3];
+      vmn = v < vmn ? v : vmn;
+      vmx = v > vmx ? v : vmx;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const int64_t a = __shfl_xor(kmn, off, 64), b = __shfl_xor(kmx, off, 64), c = __shfl_xor(vmn, off, 64),
+                  d = __shfl_xor(vmx, off, 64);
+    kmn = a < kmn ? a : kmn;
+    kmx = b > kmx ? b : kmx;
+    vmn = c < vmn ? c : vmn;
+    vmx = d > vmx ? d : vmx;
+    live += __shfl_xor(live, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0 && live) {
+    // order-preserving unsigned view of the signed ranges for the 64-bit atomics
+    const uint64_t bias = 1ULL << 63;
+    atomicMin(&out[0], (unsigned long long)((uint64_t)kmn ^ bias));
+    atomicMax(&out[1], (unsigned long long)((uint64_t)kmx ^ bias));
+    atomicMin(&out[2], (unsigned long long)((uint64_t)vmn ^ bias));
+    atomicMax(&out[3], (unsigned long long)((uint64_t)vmx ^ bias));
+    atomicAdd(&out[4], (unsigned long long)live);
+  }
+}
+
+// Fill the dense index from the live slots (cells of absent keys were zeroed).
+__global__ __launch_bounds__(256) void k_dense_build(const uint64_t* __restrict__ table, int64_t cap, int sw, JDense dn) {
+  for (int64_t slot = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; slot < cap;
+       slot += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t* s = table + slot * (uint64_t)sw;
+    const uint64_t m = s[1];
+    if (!(m & M_LIVE)) continue;
+    uint64_t cell;
+    if (dense_cell(dn, s[3], m & 1, &cell)) dense_store(dn, (int64_t)s[0] - dn.kmin, cell);
+    else *dn.invalid = 1;
   }
 }
 
@@ -305,6 +416,61 @@ __global__ __launch_bounds__(256) void k_probe(const uint64_t* __restrict__ tabl
   if (n_emitted && lane == 0 && cnt) atomicAdd(n_emitted, (unsigned long long)cnt);
 }
 
+// Probe through the dense index: one random cell read (MALL-resident for C4) per stream row,
+// PR rows per thread issued before any is used; output identical to k_probe.
+template <int PR>
+__global__ __launch_bounds__(256) void k_probe_dense(JDense dn, const int64_t* __restrict__ keys,
+                                                     const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
+                                                     const uint8_t* __restrict__ rv, int64_t n, int inner, JWhere w,
+                                                     int32_t ctype, JOut out, unsigned long long* __restrict__ n_emitted) {
+  const int64_t base = (int64_t)blockIdx.x * 256 * PR;
+  const int lane = threadIdx.x & 63;
+  bool act[PR];
+  uint64_t cell[PR];
+#pragma unroll
+  for (int r = 0; r < PR; r++) {
+    const int64_t i = base + r * 256 + threadIdx.x;
+    const int64_t ic = i < n ? i : n - 1;
+    const int64_t k = keys[ic] - dn.kmin;
+    act[r] = i < n && ts[ic] >= 0 && bit_get(kv, ic) && bit_get(rv, ic);
+    const bool kin = keys[ic] >= dn.kmin && k < dn.nkeys;
+    cell[r] = kin ? dense_load(dn, k) : 0;
+  }
+  int cnt = 0;
+#pragma unroll
+  for (int r = 0; r < PR; r++) {
+    const int64_t i = base + r * 256 + threadIdx.x;
+    const bool hit = act[r] && (cell[r] & 1);
+    const bool isnull = !hit || (cell[r] & 2);
+    const uint64_t raw = isnull ? 0 : (uint64_t)(dn.vmin + (int64_t)(cell[r] >> 2));
+    bool emit = act[r] && (inner ? hit : true);
+    if (emit && w.active) emit = hit && where_ok_raw(raw, isnull ? 1ULL : 0ULL, w);
+    const uint64_t be = __ballot(emit), bh = __ballot(hit), bn = __ballot(i < n && isnull);
+    const int64_t wbase = i - lane;
+    if (lane == 0 && wbase < n) {
+      const int64_t nbytes = std::min<int64_t>(8, (n - wbase + 7) / 8);
+      if (nbytes == 8 && !(((uintptr_t)out.emit | (uintptr_t)out.matched | (uintptr_t)out.col_null[0]) & 7)) {
+        if (out.emit) *(uint64_t*)(out.emit + wbase / 8) = be;
+        if (out.matched) *(uint64_t*)(out.matched + wbase / 8) = bh;
+        if (out.col_null[0]) *(uint64_t*)(out.col_null[0] + wbase / 8) = bn;
+      } else {
+        for (int b = 0; b < nbytes; b++) {
+          if (out.emit) out.emit[wbase / 8 + b] = (uint8_t)(be >> (8 * b));
+          if (out.matched) out.matched[wbase / 8 + b] = (uint8_t)(bh >> (8 * b));
+          if (out.col_null[0]) out.col_null[0][wbase / 8 + b] = (uint8_t)(bn >> (8 * b));
+        }
+      }
+    }
+    if (i < n && out.col_data[0]) {
+      if (ctype == KHIP_TYPE_INT32) ((int32_t*)out.col_data[0])[i] = (int32_t)raw;
+      else ((uint64_t*)out.col_data[0])[i] = raw;
+    }
+    if (out.slot_out && i < n) out.slot_out[i] = emit ? (hit ? 1 : 0) : -1;
+    cnt += lane == 0 ? __popcll(be) : 0;
+  }
+  if (n_emitted && lane == 0 && cnt) atomicAdd(n_emitted, (unsigned long long)cnt);
+}
+
 __global__ __launch_bounds__(256) void k_table_rehash(const uint64_t* __restrict__ old, int64_t ocap,
                                                       uint64_t* __restrict__ nt, uint64_t nmask, int sw) {
   for (int64_t slot = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; slot < ocap;
@@ -350,7 +516,69 @@ struct khip_table {
   int64_t cap = 0;
   int64_t occ = 0;  // resident keys (live or deleted)
   DevBuf claimed;    // slots claimed by the current upsert batch
+  // dense probe index (JDense): in step with the slot table while dense_ok
+  bool dense_ok = false;
+  int64_t dense_eval_occ = -1;  // resident keys when eligibility was last evaluated (-1: never)
+  JDense dn{};
+  DevBuf dcells, dinvalid, drange;
 };
+
+// Build the dense probe index if the table qualifies: one INT/BIGINT value column, live keys
+// spanning at most 4x their count (or 2^20), values fitting a 1/2/4/8-byte cell.  Evaluated
+// again only after the table doubled since an unsuccessful try.
+static khip_status prepare_dense(khip_table* t) {
+  if (t->dense_ok || t->desc.n_cols != 1 || t->col_types[0] == KHIP_TYPE_DOUBLE || !knob("KHIP_PROBE_DENSE", 1))
+    return KHIP_OK;
+  if (t->dense_eval_occ >= 0 && t->occ < 2 * t->dense_eval_occ) return KHIP_OK;
+  t->dense_eval_occ = std::max<int64_t>(t->occ, 1);
+  KHIP_TRY(t->drange.ensure(64));
+  unsigned long long init[5] = {~0ULL, 0ULL, ~0ULL, 0ULL, 0ULL}, r[5];
+  unsigned long long* out = t->drange.as<unsigned long long>();
+  KHIP_TRY_HIP(hipMemcpyAsync(out, init, sizeof(init), hipMemcpyHostToDevice, t->stream));
+  hipLaunchKernelGGL(k_table_ranges, dim3(jgrid(t->cap, 4096)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->cap,
+                     t->sw, out);
+  KHIP_TRY_HIP(hipGetLastError());
+  KHIP_TRY_HIP(hipMemcpyAsync(r, out, sizeof(r), hipMemcpyDeviceToHost, t->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(t->stream));
+  const int64_t live = (int64_t)r[4];
+  if (live == 0) return KHIP_OK;
+  const uint64_t bias = 1ULL << 63;
+  const int64_t kmin = (int64_t)(r[0] ^ bias), kmax = (int64_t)(r[1] ^ bias);
+  int64_t vmin = (int64_t)(r[2] ^ bias), vmax = (int64_t)(r[3] ^ bias);
+  if (r[2] == ~0ULL) vmin = vmax = 0;  // every value NULL
+  const unsigned __int128 krange = (unsigned __int128)((__int128)kmax - (__int128)kmin) + 1;
+  if (krange > (unsigned __int128)std::max<int64_t>(4 * live, 1 << 20) || krange > ((unsigned __int128)1 << 34)) return KHIP_OK;
+  const unsigned __int128 vrange = (unsigned __int128)((__int128)vmax - (__int128)vmin) + 1;
+  int bits = 2;
+  while (bits < 64 && ((unsigned __int128)1 << (bits - 2)) < vrange) bits++;
+  if (((unsigned __int128)1 << (bits - 2)) < vrange) return KHIP_OK;
+  const int w = bits <= 8 ? 1 : (bits <= 16 ? 2 : (bits <= 32 ? 4 : 8));
+  // room for keys appended past the current maximum before the index must be rebuilt
+  const int64_t nkeys = (int64_t)krange + (int64_t)krange / 8 + 1024;
+  KHIP_TRY(t->dcells.ensure((size_t)nkeys * w));
+  KHIP_TRY(t->dinvalid.ensure(8));
+  KHIP_TRY_HIP(hipMemsetAsync(t->dcells.p, 0, (size_t)nkeys * w, t->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(t->dinvalid.p, 0, 8, t->stream));
+  JDense d{};
+  d.active = 1;
+  d.w = w;
+  d.kmin = kmin;
+  d.nkeys = nkeys;
+  d.vmin = vmin;
+  d.vspan = w == 8 ? (1ULL << 62) : (1ULL << (8 * w - 2));
+  d.cells = t->dcells.as<uint8_t>();
+  d.invalid = t->dinvalid.as<int>();
+  hipLaunchKernelGGL(k_dense_build, dim3(jgrid(t->cap, 8192)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->cap,
+                     t->sw, d);
+  KHIP_TRY_HIP(hipGetLastError());
+  int bad = 0;
+  KHIP_TRY_HIP(hipMemcpyAsync(&bad, t->dinvalid.p, 4, hipMemcpyDeviceToHost, t->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(t->stream));
+  if (bad) return KHIP_OK;
+  t->dn = d;
+  t->dense_ok = true;
+  return KHIP_OK;
+}
 
 static khip_status table_alloc(khip_table* t, DevBuf& buf, int64_t cap) {
   KHIP_TRY(buf.ensure((size_t)cap * t->sw * 8));
@@ -506,15 +734,21 @@ khip_status khip_table_upsert(khip_table* t, const khip_batch* b) {
   hipLaunchKernelGGL(k_upsert_finalize, dim3(jgrid(n)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->sw, keys,
                      t->claimed.as<int64_t>(), (const unsigned long long*)ctr);
   hipLaunchKernelGGL(k_upsert_apply, dim3(jgrid(n)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->sw,
-                     t->slot_of.as<int64_t>(), rv, n, t->desc.n_cols, t->types_dev.as<int32_t>(), cols);
+                     t->slot_of.as<int64_t>(), rv, n, t->desc.n_cols, t->types_dev.as<int32_t>(), cols,
+                     t->dense_ok ? t->dn : JDense{});
   KHIP_TRY_HIP(hipGetLastError());
   unsigned long long added = 0;
-  int failed = 0;
+  int failed = 0, dense_bad = 0;
   KHIP_TRY_HIP(hipMemcpyAsync(&added, ctr, 8, hipMemcpyDeviceToHost, t->stream));
   KHIP_TRY_HIP(hipMemcpyAsync(&failed, failp, 4, hipMemcpyDeviceToHost, t->stream));
+  if (t->dense_ok) KHIP_TRY_HIP(hipMemcpyAsync(&dense_bad, t->dinvalid.p, 4, hipMemcpyDeviceToHost, t->stream));
   KHIP_TRY_HIP(hipStreamSynchronize(t->stream));
   if (failed) return fail(KHIP_E_DEVICE, "table probe budget exhausted");
   t->occ += (int64_t)added;
+  if (dense_bad) {  // a key or value outside the index: rebuilt over the new ranges by the next probe
+    t->dense_ok = false;
+    t->dense_eval_occ = -1;
+  }
   return KHIP_OK;
 }
 
@@ -544,6 +778,19 @@ static khip_status probe_launch(khip_table* t, const khip_batch* b, int32_t join
   if (!ts) return fail(KHIP_E_INVALID, "missing timestamp column");
   JWhere jw;
   KHIP_TRY(make_where(t, w, &jw));
+  KHIP_TRY(prepare_dense(t));
+  if (t->dense_ok) {
+    // rows per thread: every cell read of a thread is issued before any is used (MLP); measured on
+    // C4 (1e9 probes, 100 MB of cells): 4 → 49 ms, 8 → 28 ms, 16 → 20 ms
+    const int dpr = (int)knob("KHIP_PROBE_DPR", 16);
+    auto dk = dpr >= 64 ? k_probe_dense<64>
+                        : (dpr >= 32 ? k_probe_dense<32> : (dpr >= 16 ? k_probe_dense<16> : k_probe_dense<8>));
+    const int pr = dpr >= 64 ? 64 : (dpr >= 32 ? 32 : (dpr >= 16 ? 16 : 8));
+    hipLaunchKernelGGL(dk, dim3(ceil_div(n, 256 * pr)), dim3(256), 0, t->stream, t->dn, keys, ts, kv, rv, n,
+                       join_type == KHIP_JOIN_INNER ? 1 : 0, jw, t->col_types[0], out, n_emitted);
+    KHIP_TRY_HIP(hipGetLastError());
+    return KHIP_OK;
+  }
   const int pr_env = (int)knob("KHIP_PROBE_PR", 4);  // measured: 4 > 8 > 16 > 1
   const int PR = pr_env >= 16 ? 16 : (pr_env >= 8 ? 8 : (pr_env >= 4 ? 4 : 1));
   auto kern = PR == 16 ? k_probe<16> : (PR == 8 ? k_probe<8> : (PR == 4 ? k_probe<4> : k_probe<1>));
@@ -661,7 +908,7 @@ khip_status khip_table_destroy(khip_table* t) {
   DeviceGuard g(t->device);
   if (t->stream) hipStreamSynchronize(t->stream);
   DevBuf* bufs[] = {&t->table, &t->types_dev, &t->slot_of, &t->claimed, &t->scratch, &t->st_keys, &t->st_ts, &t->st_kv,
-                    &t->st_rv, &t->out_emit, &t->out_matched, &t->out_slot};
+                    &t->st_rv, &t->out_emit, &t->out_matched, &t->out_slot, &t->dcells, &t->dinvalid, &t->drange};
   for (DevBuf* x : bufs) x->release();
   for (int c = 0; c < JMAX_COLS; c++) {
     t->st_cols[c].release();

@@ -363,3 +363,60 @@ def test_join_random_vs_oracle(prod, orc, join_type, where):
         for c in range(3):
             assert np.array_equal(a["nulls"][c], b["nulls"][c])
             assert np.array_equal(a["cols"][c][~a["nulls"][c]], b["cols"][c][~b["nulls"][c]])
+
+
+@pytest.mark.parametrize("ctype", ["INT32", "INT64"])
+def test_join_dense_index_vs_oracle(prod, orc, ctype):
+    """One value column with dense keys: the dense probe index (include/.. khip_join.hip) is built
+    on the first probe, kept in step by upserts (deletes, NULL values), dropped when a key or a
+    value leaves its ranges and rebuilt by the next probe — host and device probe outputs equal
+    the oracle's after every step."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(31 if ctype == "INT32" else 32)
+    tables = [abi.TableHandle(lib, [ctype], capacity_hint=64) for lib in (prod, orc)]
+    dt = np.int32 if ctype == "INT32" else np.int64
+    for step in range(8):
+        m = int(rng.integers(500, 3000))
+        keys = rng.integers(0, 5000, m)
+        vals = rng.integers(0, 3, m).astype(dt)
+        if step == 4:
+            keys[0] = 10**9  # a key far outside the index range: index dropped, then rebuilt
+        if step == 6:
+            vals[0] = dt(2**30) if ctype == "INT32" else dt(2**50)  # a value outside the cell width
+        rv = rng.random(m) > 0.1
+        cv = rng.random(m) > 0.05
+        for t in tables:
+            t.upsert(abi.HostBatch(np.zeros(m, np.int64), keys=keys, row_valid=rv, cols=[vals], col_valid=[cv]))
+        k = int(rng.integers(1000, 9000))
+        pk = rng.integers(-10, 5200, k)
+        pts = np.where(rng.random(k) < 0.01, -1, rng.integers(0, 10**6, k))
+        pkv, prv = rng.random(k) > 0.02, rng.random(k) > 0.02
+        where = {"col": 0, "op": "EQ", "i64": 2, "f64": 2.0} if step % 2 else None
+        for jt in ("LEFT", "INNER"):
+            g, o = (t.probe(abi.HostBatch(pts, keys=pk, key_valid=pkv, row_valid=prv), jt, where) for t in tables)
+            assert g["n"] == o["n"]
+            assert np.array_equal(g["stream_row"], o["stream_row"]) and np.array_equal(g["matched"], o["matched"])
+            assert np.array_equal(g["nulls"][0], o["nulls"][0])
+            assert np.array_equal(g["cols"][0][~g["nulls"][0]], o["cols"][0][~o["nulls"][0]])
+            # device probe: row-aligned bitmaps and column
+            dk, dts = torch.from_numpy(pk).cuda(), torch.from_numpy(pts).cuda()
+            kvb = abi.bitmap_torch(torch.from_numpy(pkv).cuda())
+            rvb = abi.bitmap_torch(torch.from_numpy(prv).cuda())
+            nb = (k + 7) // 8
+            emit = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+            matched = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+            col = torch.zeros(k, dtype=torch.int32 if ctype == "INT32" else torch.int64, device="cuda")
+            null = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+            n_emit = tables[0].probe_device(abi.DeviceBatch(dts, keys=dk, key_valid=kvb, row_valid=rvb), jt, where,
+                                            emit, matched, [col], [null])
+            assert n_emit == o["n"]
+            e = np.unpackbits(emit.cpu().numpy(), bitorder="little")[:k].astype(bool)
+            assert np.array_equal(np.nonzero(e)[0], o["stream_row"])
+            mt = np.unpackbits(matched.cpu().numpy(), bitorder="little")[:k].astype(bool)
+            assert np.array_equal(mt[o["stream_row"]], o["matched"].astype(bool))
+            nl = np.unpackbits(null.cpu().numpy(), bitorder="little")[:k].astype(bool)
+            assert np.array_equal(nl[o["stream_row"]], o["nulls"][0])
+            cv_ = col.cpu().numpy()[o["stream_row"]]
+            assert np.array_equal(cv_[~o["nulls"][0]], o["cols"][0][~o["nulls"][0]])
+    for t in tables:
+        t.close()
