@@ -53,6 +53,13 @@ typedef int32_t khip_status;
 #define KHIP_WINDOW_NONE 0
 #define KHIP_WINDOW_TUMBLING 1
 #define KHIP_WINDOW_HOPPING 2
+/* SESSION (gap = size_ms): X/windows/SessionWindowExpression.java, built by
+ * S/StreamAggregateBuilder.java:296-323 (SessionWindows + KudafAggregator.getMerger, X/function/
+ * udaf/KudafAggregator.java:87-111).  A record at ts joins (merges) every session of its key
+ * with end >= ts - gap and start <= ts + gap; it is late when the merged session ends before
+ * streamTime - grace - gap.  Rows are [key, aggs..., WINDOWSTART = session start, WINDOWEND =
+ * session end]; a merge emits tombstones for the sessions it replaced. */
+#define KHIP_WINDOW_SESSION 3
 
 /* Key types.  Group identity is equality of the serialized KAFKA key
  * (BIGINT = 8-byte value, STRING = UTF-8 bytes), SURVEY.md §8.0. */

@@ -23,7 +23,7 @@ ABI_VERSION = 2  # include/ksqldb_hip.h KHIP_ABI_VERSION the structs below mirro
 KHIP_OK = 0
 KHIP_E_BUFFER = -5
 
-WINDOW = {"NONE": 0, "TUMBLING": 1, "HOPPING": 2}
+WINDOW = {"NONE": 0, "TUMBLING": 1, "HOPPING": 2, "SESSION": 3}
 KEY = {"INT64": 0, "UTF8": 1}
 TYPE = {"INT32": 0, "INT64": 1, "DOUBLE": 2}
 AGG = {"COUNT_STAR": 0, "COUNT": 1, "SUM": 2, "MIN": 3, "MAX": 4, "AVG": 5}

@@ -53,6 +53,15 @@
  *     EmitStrategy.onWindowClose; Q/suppress.json) emits, once per push whose close time
  *     (streamTime - grace) passed the last emitted one, the windows with start in
  *     [max(0, lastClose - size), close - size] that are still visible (R9) and pass HAVING.
+ *  R11 SESSION windows (gap = size_ms; S/StreamAggregateBuilder.java:296-323, Kafka 3.4
+ *     KStreamSessionWindowAggregate): per record, the key's visible sessions (end >= streamTime
+ *     - retention, retention = gap + grace by default) with end >= ts - gap and start <= ts +
+ *     gap merge with [ts, ts] (aggregates combined by KudafAggregator.getMerger, X/function/
+ *     udaf/KudafAggregator.java:87-111: COUNT/SUM add, MIN/MAX compare, AVG adds both); the
+ *     record is late when the merged session ends before streamTime - grace - gap; otherwise the
+ *     merged-away sessions are deleted (tombstones) and the merged one is written with the
+ *     record applied.  Row time = session end.  Pinned by Q/session-windows.json:4,45 (late
+ *     drop and expiry with GRACE PERIOD); the default grace max(24h - gap, 0) is unpinned.
  *  R7 join: table keeps the latest non-null value per key, a null value deletes;
  *     stream records with null key / null value / negative ts are dropped; lookup
  *     against the table as of that point; INNER emits on hit, LEFT always
@@ -231,6 +240,8 @@ typedef struct {
   int64_t ws;
   int64_t rowtime;
   agg_state* st; /* n_aggs */
+  int64_t we;          /* SESSION: session end (time windows: ws + size)       */
+  int dead;            /* SESSION: merged away (kept for the push's tombstones) */
   int64_t born_epoch;  /* push that created the entry                          */
   int64_t touch_epoch; /* last push that updated it                            */
   int old_pass;        /* HAVING before the push's first update (R10)          */
@@ -256,6 +267,12 @@ struct oracle_agg {
   uint8_t* chg_tomb;
   int64_t n_chg, cap_chg;
   int64_t st_before;  /* stream time before the current push                      */
+  /* SESSION: per key, the indices of its live sessions (open addressing on the key) */
+  int64_t* sk_key;
+  int64_t** sk_list;
+  int64_t* sk_n;
+  int64_t* sk_cap;
+  int64_t sk_slots, sk_used;
   int64_t* stmax;     /* the push's stream-time maxima, in arrival order           */
   int64_t n_stmax, cap_stmax;
   int own_stmax;      /* stmax is this handle's (0: borrowed from the sharded push)  */
@@ -298,6 +315,8 @@ static entry* find_or_create(oracle_agg* a, int64_t key, int64_t ws) {
   x->born_epoch = a->epoch;
   x->touch_epoch = -1;
   x->old_pass = 0;
+  x->we = ws + a->d.size_ms;
+  x->dead = 0;
   return x;
 }
 
@@ -325,10 +344,18 @@ static int64_t visible_from(const oracle_agg* a) {
   return a->obs_ws - a->retention;
 }
 
+/* R9 for one entry: time windows by start, sessions by end (the session store's segment time). */
+static int entry_visible(const oracle_agg* a, const entry* x) {
+  if (x->dead) return 0;
+  const int64_t vis = visible_from(a);
+  return (a->d.window_kind == KHIP_WINDOW_SESSION ? x->we : x->ws) >= vis;
+}
+
 static int valid_desc(const khip_agg_desc* d) {
   if (d->window_kind != KHIP_WINDOW_NONE && d->window_kind != KHIP_WINDOW_TUMBLING &&
-      d->window_kind != KHIP_WINDOW_HOPPING)
+      d->window_kind != KHIP_WINDOW_HOPPING && d->window_kind != KHIP_WINDOW_SESSION)
     return 0;
+  if (d->window_kind == KHIP_WINDOW_SESSION && d->emit == KHIP_EMIT_FINAL) return 0;
   if (d->window_kind != KHIP_WINDOW_NONE) {
     if (d->size_ms <= 0) return 0;
     if (d->window_kind == KHIP_WINDOW_HOPPING &&
@@ -372,6 +399,7 @@ khip_status oracle_agg_create(const khip_agg_desc* desc, oracle_agg** out) {
   } else {
     a->grace = desc->grace_ms;
   }
+  if (desc->window_kind == KHIP_WINDOW_SESSION) a->d.advance_ms = 1;  /* obs = stream time itself */
   if (desc->window_kind != KHIP_WINDOW_NONE) {
     const int64_t min_r = desc->size_ms + a->grace;
     if (desc->retention_ms == KHIP_RETENTION_DEFAULT) a->retention = min_r;
@@ -446,6 +474,152 @@ static void apply_aggs(oracle_agg* a, entry* x, const khip_batch* b, int64_t r) 
 static void finish_push(oracle_agg* a);
 static void stmax_add(oracle_agg* a, int64_t st);
 
+/* ------------------------------------------------------------- SESSION windows (R11) */
+
+static int64_t* sk_lookup(oracle_agg* a, int64_t key) { /* the key's list slot (created) */
+  if (2 * (a->sk_used + 1) > a->sk_slots) {
+    const int64_t ns = a->sk_slots ? a->sk_slots * 2 : 1024;
+    int64_t* nk = (int64_t*)malloc(sizeof(int64_t) * ns);
+    int64_t** nl = (int64_t**)calloc((size_t)ns, sizeof(int64_t*));
+    int64_t* nn = (int64_t*)calloc((size_t)ns, sizeof(int64_t));
+    int64_t* nc = (int64_t*)calloc((size_t)ns, sizeof(int64_t));
+    char* used = (char*)calloc((size_t)ns, 1);
+    for (int64_t i = 0; i < a->sk_slots; i++) {
+      if (!a->sk_cap[i]) continue;
+      int64_t j = (int64_t)(mix64((uint64_t)a->sk_key[i]) & (uint64_t)(ns - 1));
+      while (used[j]) j = (j + 1) & (ns - 1);
+      used[j] = 1;
+      nk[j] = a->sk_key[i];
+      nl[j] = a->sk_list[i];
+      nn[j] = a->sk_n[i];
+      nc[j] = a->sk_cap[i];
+    }
+    free(used);
+    free(a->sk_key); free(a->sk_list); free(a->sk_n); free(a->sk_cap);
+    a->sk_key = nk; a->sk_list = nl; a->sk_n = nn; a->sk_cap = nc; a->sk_slots = ns;
+  }
+  int64_t j = (int64_t)(mix64((uint64_t)key) & (uint64_t)(a->sk_slots - 1));
+  while (a->sk_cap[j] && a->sk_key[j] != key) j = (j + 1) & (a->sk_slots - 1);
+  if (!a->sk_cap[j]) {
+    a->sk_key[j] = key;
+    a->sk_cap[j] = 4;
+    a->sk_n[j] = 0;
+    a->sk_list[j] = (int64_t*)malloc(sizeof(int64_t) * 4);
+    a->sk_used++;
+  }
+  return &a->sk_n[j];
+}
+
+static entry* new_entry(oracle_agg* a, int64_t key, int64_t ws, int64_t we) {
+  if (a->n == a->cap) {
+    a->cap = a->cap ? a->cap * 2 : 1024;
+    a->e = (entry*)realloc(a->e, sizeof(entry) * a->cap);
+  }
+  entry* x = &a->e[a->n++];
+  memset(x, 0, sizeof(*x));
+  x->key = key;
+  x->ws = ws;
+  x->we = we;
+  x->rowtime = INT64_MIN;
+  x->st = (agg_state*)calloc((size_t)(a->d.n_aggs > 0 ? a->d.n_aggs : 1), sizeof(agg_state));
+  x->born_epoch = a->epoch;
+  x->touch_epoch = -1;
+  return x;
+}
+
+/* KudafAggregator.getMerger (X/function/udaf/KudafAggregator.java:87-111): dst = merge(dst, src). */
+static void merge_state(oracle_agg* a, agg_state* dst, const agg_state* src) {
+  for (int i = 0; i < a->d.n_aggs; i++) {
+    const khip_agg_spec* sp = &a->aggs[i];
+    const int t = sp->kind == KHIP_AGG_COUNT_STAR ? KHIP_TYPE_INT64 : a->col_types[sp->arg_col];
+    agg_state* d = &dst[i];
+    const agg_state* x = &src[i];
+    switch (sp->kind) {
+      case KHIP_AGG_COUNT_STAR:
+      case KHIP_AGG_COUNT: d->i += x->i; break;
+      case KHIP_AGG_SUM:
+      case KHIP_AGG_AVG:
+        if (t == KHIP_TYPE_INT32) d->i = (int64_t)(int32_t)((uint32_t)(int32_t)d->i + (uint32_t)(int32_t)x->i);
+        else if (t == KHIP_TYPE_INT64) d->i = (int64_t)((uint64_t)d->i + (uint64_t)x->i);
+        else d->d = d->d + x->d;
+        d->cnt += x->cnt;
+        break;
+      case KHIP_AGG_MIN:
+      case KHIP_AGG_MAX: { /* BaseComparableKudaf.merge = aggregate(aggOne, aggTwo): ties keep aggTwo */
+        if (!x->has) break;
+        int take = !d->has;
+        if (!take) {
+          if (t == KHIP_TYPE_DOUBLE) {
+            const int c = java_double_compare(d->d, x->d);
+            take = sp->kind == KHIP_AGG_MAX ? !(c > 0) : !(c < 0);
+          } else {
+            take = sp->kind == KHIP_AGG_MAX ? !(d->i > x->i) : !(d->i < x->i);
+          }
+        }
+        if (take) *d = *x;
+        break;
+      }
+    }
+  }
+}
+
+/* One record of a SESSION aggregation (R11); st = the task's stream time after the record. */
+static void session_apply(oracle_agg* a, int64_t key, int64_t ts, int64_t st, const khip_batch* b, int64_t r,
+                          int64_t* applied, int64_t* late) {
+  const int64_t gap = a->d.size_ms;
+  const int64_t close = st - a->grace - gap, vis = st - a->retention;
+  const int64_t j = sk_lookup(a, key) - a->sk_n;
+  int64_t* L = a->sk_list[j];
+  int64_t n = a->sk_n[j];
+  int64_t mstart = ts, mend = ts, nover = 0, same = -1;
+  for (int64_t k = 0; k < n; k++) {
+    const entry* x = &a->e[L[k]];
+    if (x->we < vis) continue; /* expired from the session store: invisible */
+    if (x->we >= ts - gap && x->ws <= ts + gap) {
+      nover++;
+      if (x->ws < mstart) mstart = x->ws;
+      if (x->we > mend) mend = x->we;
+      if (x->ws == ts && x->we == ts) same = L[k];
+    }
+  }
+  if (mend < close) {
+    (*late)++;
+    return;
+  }
+  (*applied)++;
+  if (mstart == ts && mend == ts && same >= 0) { /* the session [ts, ts] itself: update in place */
+    entry* x = &a->e[same];
+    touch(a, x);
+    apply_aggs(a, x, b, r);
+    x->rowtime = x->we;
+    return;
+  }
+  entry* nx = new_entry(a, key, mstart, mend);
+  const int64_t ni = nx - a->e;
+  /* merge the overlapping sessions in store order (by end), delete them */
+  int64_t m = 0;
+  for (int64_t k = 0; k < n; k++) {
+    entry* x = &a->e[L[k]];
+    if (x->we >= vis && x->we >= ts - gap && x->ws <= ts + gap) {
+      touch(a, x);
+      merge_state(a, a->e[ni].st, x->st);
+      x->dead = 1;
+    } else {
+      L[m++] = L[k];
+    }
+  }
+  nx = &a->e[ni];
+  apply_aggs(a, nx, b, r);
+  nx->rowtime = mend;
+  touch(a, nx);
+  if (m == a->sk_cap[j]) {
+    a->sk_cap[j] *= 2;
+    a->sk_list[j] = (int64_t*)realloc(a->sk_list[j], sizeof(int64_t) * a->sk_cap[j]);
+  }
+  a->sk_list[j][m++] = ni;
+  a->sk_n[j] = m;
+}
+
 khip_status oracle_agg_push(oracle_agg* a, const khip_batch* b, khip_batch_stats* stats) {
   if (!a || !b || b->mem != KHIP_MEM_HOST || b->n_rows < 0) return KHIP_E_INVALID;
   if (b->n_cols < a->d.n_cols) return KHIP_E_INVALID;
@@ -478,6 +652,15 @@ khip_status oracle_agg_push(oracle_agg* a, const khip_batch* b, khip_batch_stats
       apply_aggs(a, x, b, r);
       s.windows_applied++;
       if (ts > a->stream_time) a->stream_time = ts;
+      continue;
+    }
+    if (a->d.window_kind == KHIP_WINDOW_SESSION) {
+      if (ts > a->stream_time) {
+        a->stream_time = ts;
+        stmax_add(a, ts);
+      }
+      session_apply(a, key, ts, a->stream_time, b, r, &s.windows_applied, &s.windows_late);
+      a->obs_ws = a->stream_time; /* every stream-time maximum is put into the session store */
       continue;
     }
     if (ts > a->stream_time) { /* R2: before the check */
@@ -582,6 +765,24 @@ static int cmp_entry2(const oracle_agg* ax, const entry* x, const oracle_agg* ay
   if (x->ws != y->ws) return x->ws < y->ws ? -1 : 1;
   return 0;
 }
+/* Order of a push's emitted rows: key, then (sessions) tombstones before rows, then window start
+ * and end — with one record per push this is the reference's own emission order. */
+static int cmp_row(const oracle_agg* ax, const entry* x, int tx, const oracle_agg* ay, const entry* y, int ty) {
+  if (ax->d.key_type == KHIP_KEY_INT64) {
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+  } else if (ax != ay || x->key != y->key) {
+    int64_t lx = ax->dict.len[x->key], ly = ay->dict.len[y->key];
+    int64_t m = lx < ly ? lx : ly;
+    int c = m ? memcmp(ax->dict.arena + ax->dict.off[x->key], ay->dict.arena + ay->dict.off[y->key], (size_t)m) : 0;
+    if (c) return c;
+    if (lx != ly) return lx < ly ? -1 : 1;
+  }
+  if (ax->d.window_kind == KHIP_WINDOW_SESSION && tx != ty) return tx ? -1 : 1;
+  if (x->ws != y->ws) return x->ws < y->ws ? -1 : 1;
+  if (x->we != y->we) return x->we < y->we ? -1 : 1;
+  return 0;
+}
+
 static int cmp_entry(const void* pa, const void* pb, void* ctx) {
   const oracle_agg* a = (const oracle_agg*)ctx;
   return cmp_entry2(a, *(const entry* const*)pa, a, *(const entry* const*)pb);
@@ -605,9 +806,10 @@ static void chg_add(oracle_agg* a, int64_t idx, uint8_t tomb) {
   a->chg_tomb[a->n_chg++] = tomb;
 }
 
-static int cmp_chg(const void* pa, const void* pb, void* ctx) {
+static int cmp_chg(const void* pa, const void* pb, void* ctx) { /* (entry << 1 | tombstone) */
   const oracle_agg* a = (const oracle_agg*)ctx;
-  return cmp_entry2(a, &a->e[*(const int64_t*)pa], a, &a->e[*(const int64_t*)pb]);
+  const int64_t u = *(const int64_t*)pa, v = *(const int64_t*)pb;
+  return cmp_row(a, &a->e[u >> 1], (int)(u & 1), a, &a->e[v >> 1], (int)(v & 1));
 }
 
 /* R10: the rows this push emits (after the stream time of the push is known). */
@@ -636,24 +838,30 @@ static void finish_push(oracle_agg* a) {
   } else {
     for (int64_t t = 0; t < a->n_touched; t++) {
       const entry* x = &a->e[a->touched[t]];
-      if (having_pass(a, hv, x)) chg_add(a, a->touched[t], 0);
-      else if (x->old_pass) chg_add(a, a->touched[t], 1);
+      if (x->dead) { /* a session merged away: deleted if it existed before the push */
+        if (x->born_epoch != a->epoch && x->old_pass) chg_add(a, a->touched[t], 1);
+      } else if (having_pass(a, hv, x)) {
+        chg_add(a, a->touched[t], 0);
+      } else if (x->old_pass) {
+        chg_add(a, a->touched[t], 1);
+      }
     }
   }
-  /* sort (key, ws); a row is a tombstone iff it fails HAVING (EMIT CHANGES) */
   if (a->n_chg > 1) {
+    for (int64_t k = 0; k < a->n_chg; k++) a->chg[k] = a->chg[k] << 1 | a->chg_tomb[k];
     qsort_r(a->chg, (size_t)a->n_chg, sizeof(int64_t), cmp_chg, a);
-    for (int64_t k = 0; k < a->n_chg; k++)
-      a->chg_tomb[k] = (uint8_t)(a->d.emit == KHIP_EMIT_FINAL ? 0 : !having_pass(a, hv, &a->e[a->chg[k]]));
+    for (int64_t k = 0; k < a->n_chg; k++) {
+      a->chg_tomb[k] = (uint8_t)(a->chg[k] & 1);
+      a->chg[k] >>= 1;
+    }
   }
 }
 
 khip_status oracle_agg_snapshot_size(oracle_agg* a, int64_t* n_rows, int64_t* key_bytes) {
   if (!a) return KHIP_E_INVALID;
-  const int64_t vis = visible_from(a);
   int64_t n = 0, kb = 0;
   for (int64_t k = 0; k < a->n; k++) {
-    if (a->e[k].ws < vis) continue;
+    if (!entry_visible(a, &a->e[k])) continue;
     n++;
     if (a->d.key_type == KHIP_KEY_UTF8) kb += a->dict.len[a->e[k].key];
   }
@@ -699,7 +907,7 @@ static khip_status write_rows(const owned_entry* rows, int64_t m, khip_snapshot*
       if (out->key_offsets) out->key_offsets[r + 1] = kb;
     }
     if (out->window_start) out->window_start[r] = windowed ? x->ws : 0;
-    if (out->window_end) out->window_end[r] = windowed ? x->ws + a->d.size_ms : 0;
+    if (out->window_end) out->window_end[r] = windowed ? x->we : 0;
     if (out->rowtime) out->rowtime[r] = x->rowtime;
     for (int i = 0; i < a->d.n_aggs; i++) {
       int64_t iv;
@@ -725,9 +933,8 @@ khip_status oracle_agg_snapshot(oracle_agg* a, const khip_having* h, khip_snapsh
   if (h && (h->agg_index < 0 || h->agg_index >= a->d.n_aggs)) return KHIP_E_INVALID;
   entry** order = (entry**)malloc(sizeof(entry*) * (a->n + 1));
   int64_t m = 0;
-  const int64_t vis = visible_from(a);
   for (int64_t k = 0; k < a->n; k++)
-    if (a->e[k].ws >= vis && having_pass(a, h, &a->e[k])) order[m++] = &a->e[k];
+    if (entry_visible(a, &a->e[k]) && having_pass(a, h, &a->e[k])) order[m++] = &a->e[k];
   qsort_r(order, (size_t)m, sizeof(entry*), cmp_entry, a);
   owned_entry* rows = (owned_entry*)malloc(sizeof(owned_entry) * (m + 1));
   for (int64_t r = 0; r < m; r++) {
@@ -759,6 +966,8 @@ khip_status oracle_agg_destroy(oracle_agg* a) {
   free(a->chg);
   free(a->chg_tomb);
   if (a->own_stmax) free(a->stmax);
+  for (int64_t i = 0; i < a->sk_slots; i++) free(a->sk_list[i]);
+  free(a->sk_key); free(a->sk_list); free(a->sk_n); free(a->sk_cap);
   for (int64_t k = 0; k < a->n; k++) free(a->e[k].st);
   free(a->e);
   free(a->slots);
@@ -820,6 +1029,10 @@ static void* shard_run(void* arg) {
       if (ts > x->rowtime) x->rowtime = ts;
       apply_aggs(a, x, b, r);
       j->applied++;
+      continue;
+    }
+    if (a->d.window_kind == KHIP_WINDOW_SESSION) {
+      session_apply(a, key, ts, j->st_after[r], b, r, &j->applied, &j->late);
       continue;
     }
     const int64_t close_time = j->st_after[r] - a->grace;
@@ -895,6 +1108,7 @@ khip_status oracle_agg_push_sharded(oracle_agg** shards, int32_t P, const khip_b
   }
   int64_t obs = -1; /* one task, one window store: the largest window start over the shards */
   for (int32_t p = 0; p < P; p++) obs = shards[p]->obs_ws > obs ? shards[p]->obs_ws : obs;
+  if (a0->d.window_kind == KHIP_WINDOW_SESSION) obs = st;
   for (int32_t p = 0; p < P; p++) {
     oracle_agg* sp = shards[p];
     sp->obs_ws = obs;
@@ -931,6 +1145,7 @@ typedef struct {
   const khip_having* h;
   int changes; /* 1: the shard's last-push changes instead of its table */
   entry** order;
+  uint8_t* tomb; /* changes: tombstone per order[] entry */
   int64_t m;
 } sort_job;
 
@@ -939,13 +1154,14 @@ static void* sort_run(void* arg) {
   oracle_agg* a = j->a;
   j->order = (entry**)malloc(sizeof(entry*) * (a->n + 1));
   j->m = 0;
+  j->tomb = NULL;
   if (j->changes) { /* the push's emitted rows, already sorted */
+    j->tomb = a->chg_tomb;
     for (int64_t k = 0; k < a->n_chg; k++) j->order[j->m++] = &a->e[a->chg[k]];
     return NULL;
   }
-  const int64_t vis = visible_from(a);
   for (int64_t k = 0; k < a->n; k++)
-    if (a->e[k].ws >= vis && having_pass(a, j->h, &a->e[k])) j->order[j->m++] = &a->e[k];
+    if (entry_visible(a, &a->e[k]) && having_pass(a, j->h, &a->e[k])) j->order[j->m++] = &a->e[k];
   qsort_r(j->order, (size_t)j->m, sizeof(entry*), cmp_entry, a);
   return NULL;
 }
@@ -972,7 +1188,8 @@ static khip_status merge_sharded(oracle_agg** shards, int32_t P, const khip_havi
   int32_t* heap = (int32_t*)malloc(sizeof(int32_t) * (size_t)P);
   int32_t hn = 0;
 #define HEAD(p) (jobs[p].order[cur[p]])
-#define LESS(p, q) (cmp_entry2(jobs[p].a, HEAD(p), jobs[q].a, HEAD(q)) < 0)
+#define TOMB(p) (jobs[p].tomb ? (int)jobs[p].tomb[cur[p]] : 0)
+#define LESS(p, q) (cmp_row(jobs[p].a, HEAD(p), TOMB(p), jobs[q].a, HEAD(q), TOMB(q)) < 0)
   for (int32_t p = 0; p < P; p++) {
     if (jobs[p].m == 0) continue;
     int32_t i = hn++;
@@ -982,10 +1199,12 @@ static khip_status merge_sharded(oracle_agg** shards, int32_t P, const khip_havi
       i = (i - 1) / 2;
     }
   }
+  uint8_t* mtomb = (uint8_t*)malloc((size_t)m + 1);
   for (int64_t r = 0; r < m; r++) {
     const int32_t p = heap[0];
     rows[r].a = jobs[p].a;
     rows[r].x = HEAD(p);
+    mtomb[r] = (uint8_t)TOMB(p);
     if (++cur[p] == jobs[p].m) heap[0] = heap[--hn];
     int32_t i = 0;
     for (;;) {
@@ -998,14 +1217,12 @@ static khip_status merge_sharded(oracle_agg** shards, int32_t P, const khip_havi
     }
   }
 #undef LESS
+#undef TOMB
 #undef HEAD
   khip_status st = write_rows(rows, m, out);
-  if (st == KHIP_OK && tombstone) /* EMIT CHANGES: a change is a tombstone iff it fails HAVING */
-    for (int64_t r = 0; r < m; r++)
-      tombstone[r] = (uint8_t)(rows[r].a->d.emit == KHIP_EMIT_FINAL ? 0
-                                                                     : !having_pass(rows[r].a, query_having(rows[r].a), rows[r].x));
+  if (st == KHIP_OK && tombstone && m) memcpy(tombstone, mtomb, (size_t)m);
   for (int32_t p = 0; p < P; p++) free(jobs[p].order);
-  free(rows); free(cur); free(heap); free(jobs); free(th);
+  free(rows); free(cur); free(heap); free(jobs); free(th); free(mtomb);
   return st;
 }
 

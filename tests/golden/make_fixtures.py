@@ -128,9 +128,12 @@ def duration_ms(text):
 
 def parse_window(kind, body):
     size = adv = grace = retention = None
-    for part in split_top(body):
+    for i, part in enumerate(split_top(body)):
         p = part.strip()
         up = p.upper()
+        if kind == "SESSION" and i == 0:  # WINDOW SESSION (<gap>, ...)
+            size = duration_ms(p)
+            continue
         if up.startswith("SIZE"):
             size = duration_ms(p[4:])
         elif up.startswith("ADVANCE BY"):
@@ -143,7 +146,7 @@ def parse_window(kind, body):
             raise Skip("window clause " + p)
     if size is None:
         raise Skip("window size")
-    if kind == "TUMBLING":
+    if kind in ("TUMBLING", "SESSION"):
         adv = size
     if adv is None:
         raise Skip("hopping advance")
@@ -251,11 +254,13 @@ def extract_agg(path, test, fmt_tag):
         raise Skip("statement count")
     src = parse_create_source(st[0], "STREAM")
     m = re.match(r"(?is)^\s*CREATE\s+TABLE\s+(\w+)\s+AS\s+SELECT\s+(.*?)\s+FROM\s+(\w+)(\s+\w+)?\s+"
-                 r"(WINDOW\s+(TUMBLING|HOPPING)\s*\((.*?)\)\s+)?GROUP\s+BY\s+(.*?)"
+                 r"(WINDOW\s+(TUMBLING|HOPPING|SESSION)\s*\((.*?)\)\s+)?GROUP\s+BY\s+(.*?)"
                  r"(\s+HAVING\s+(.*?))?\s*(EMIT\s+(CHANGES|FINAL))?\s*;?\s*$", st[1])
     if not m:
         raise Skip("ctas shape")
     emit = (m.group(12) or "CHANGES").upper()
+    if emit == "FINAL" and (m.group(6) or "").upper() == "SESSION":
+        raise Skip("session emit final")
     out_name = m.group(1).upper()
     if m.group(3).upper() != src["name"]:
         raise Skip("from")
