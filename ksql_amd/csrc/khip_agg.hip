@@ -826,8 +826,10 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
   clear_error();
   if (!desc || !out) return fail(KHIP_E_INVALID, "null argument");
   const khip_agg_desc& d = *desc;
-  if (d.window_kind < KHIP_WINDOW_NONE || d.window_kind > KHIP_WINDOW_HOPPING)
+  if (d.window_kind < KHIP_WINDOW_NONE || d.window_kind > KHIP_WINDOW_SESSION)
     return fail(KHIP_E_INVALID, "unknown window kind");
+  if (d.window_kind == KHIP_WINDOW_SESSION && d.emit == KHIP_EMIT_FINAL)
+    return fail(KHIP_E_UNSUPPORTED, "EMIT FINAL on SESSION windows");
   if (d.window_kind != KHIP_WINDOW_NONE) {
     if (d.size_ms <= 0) return fail(KHIP_E_INVALID, "window size must be > 0");
     if (d.window_kind == KHIP_WINDOW_HOPPING && (d.advance_ms <= 0 || d.advance_ms > d.size_ms))
@@ -864,7 +866,7 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
   a->aggs.assign(d.aggs, d.aggs + d.n_aggs);
   a->desc.col_types = a->col_types.data();
   a->desc.aggs = a->aggs.data();
-  if (d.window_kind == KHIP_WINDOW_TUMBLING) a->desc.advance_ms = d.size_ms;
+  if (d.window_kind == KHIP_WINDOW_TUMBLING || d.window_kind == KHIP_WINDOW_SESSION) a->desc.advance_ms = d.size_ms;
   a->windowed = d.window_kind != KHIP_WINDOW_NONE;
   a->grace = grace_of(a->desc);
   a->max_fanout = a->windowed ? (int)ceil_div(a->desc.size_ms, a->desc.advance_ms) : 1;
@@ -891,11 +893,11 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
     return fail(KHIP_E_DEVICE, "hipStreamCreate failed (no device?)");
   }
   a->profile = (d.flags & KHIP_FLAG_PROFILE) != 0;
-  a->engine = (d.flags & KHIP_FLAG_ENGINE_ATOMIC) ? 1 : 0;
+  a->engine = d.window_kind == KHIP_WINDOW_SESSION ? 2 : ((d.flags & KHIP_FLAG_ENGINE_ATOMIC) ? 1 : 0);
   a->changelog = (d.flags & KHIP_FLAG_CHANGELOG) != 0 && d.emit == KHIP_EMIT_CHANGES;
   if (a->windowed)
     a->retention = d.retention_ms == KHIP_RETENTION_DEFAULT ? a->desc.size_ms + a->grace : d.retention_ms;
-  if (a->changelog && a->engine == 1) {
+  if (a->changelog && a->engine == 1) {  // (SESSION windows keep their changelog themselves)
     khip_agg_destroy(a);
     return fail(KHIP_E_UNSUPPORTED, "EMIT CHANGES changelog needs the partitioned engine");
   }
@@ -1054,7 +1056,10 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
     ev_record(a, 2);
   }
   int64_t tot[NPART] = {0};
-  if (a->engine == 0) {
+  if (a->engine == 2) {
+    if (n >= (1LL << 31)) return fail(KHIP_E_UNSUPPORTED, "SESSION pushes above 2^31 rows");
+    KHIP_TRY(sess_push(a, n, keys, ts, kv, rv, cols, tot));
+  } else if (a->engine == 0) {
     // ---- partitioned engine, in slices of < 2^31 records (multiple of 8: bitmaps stay byte aligned)
     const int64_t slice = 1LL << 31;
     for (int64_t off = 0; off < n; off += slice) {
@@ -1135,7 +1140,7 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   a->times.apply_ms += apply_ms;
   a->times.finalize_ms += fin_ms;
   }
-  if (a->engine != 0) {  // the partitioned engine brought it back with its end-of-push counters
+  if (a->engine == 1) {  // the other engines brought it back with their end-of-push counters
     KHIP_TRY_HIP(hipMemcpyAsync(&a->host_stream_time, a->stream_time.p, 8, hipMemcpyDeviceToHost, a->stream));
     KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
   }
@@ -1162,6 +1167,7 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
 // ws + size > (stream time before the last push) - grace, so they are all visible while that
 // bound is at or above the first visible window start.  The atomic engine keeps every row.
 static bool no_expired_live(const khip_agg* a) {
+  if (a->engine == 2) return true;  // the session store drops expired sessions at every push
   const int64_t vf = visible_from(a);
   if (vf == INT64_MIN) return true;
   if (a->engine != 0 || a->st_before < 0) return false;
@@ -1172,10 +1178,11 @@ static khip_status compact_rows(khip_agg* a, const khip_having* h, std::vector<u
                                 const HavingDev* pull = nullptr) {
   HavingDev hd{};
   if (pull) hd = *pull;
-  if (a->windowed && !hd.fin) {  // the store: expired windows are gone (retention)
+  if (a->windowed && !hd.fin && a->engine != 2) {  // the store: expired windows are gone (retention)
     hd.vis = 1;
     hd.vis_from = visible_from(a);
   }
+  hd.session = a->engine == 2;
   if (h) {
     if (h->agg_index < 0 || h->agg_index >= a->desc.n_aggs) return fail(KHIP_E_INVALID, "having agg index");
     if (h->op < KHIP_OP_GT || h->op > KHIP_OP_NE) return fail(KHIP_E_INVALID, "having op");
@@ -1190,13 +1197,17 @@ static khip_status compact_rows(khip_agg* a, const khip_having* h, std::vector<u
     if (rows && *count > a->occ) return fail(KHIP_E_STATE, "group count bookkeeping mismatch");
     return KHIP_OK;
   }
+  // global-atomic table, or the SESSION store (a flat row array)
+  const uint64_t* src = a->engine == 2 ? a->sess.rows.as<uint64_t>() : a->table.as<uint64_t>();
+  const int64_t nsrc = a->engine == 2 ? a->sess.n : a->cap;
   DevBuf ctr, out;
   KHIP_TRY(ctr.ensure(8));
   KHIP_TRY_HIP(hipMemsetAsync(ctr.p, 0, 8, a->stream));
-  const int grid = grid_for(a->cap, 256, 4096);
+  const int grid = grid_for(std::max<int64_t>(nsrc, 1), 256, 4096);
   if (rows) KHIP_TRY(out.ensure((size_t)std::max<int64_t>(a->occ, 1) * a->sw * 8));
-  hipLaunchKernelGGL(k_compact, dim3(grid), dim3(256), 0, a->stream, a->table.as<uint64_t>(), a->cap, a->sw, hd,
-                     rows ? out.as<uint64_t>() : nullptr, std::max<int64_t>(a->occ, 1), ctr.as<unsigned long long>());
+  if (nsrc)
+    hipLaunchKernelGGL(k_compact, dim3(grid), dim3(256), 0, a->stream, src, nsrc, a->sw, hd,
+                       rows ? out.as<uint64_t>() : nullptr, std::max<int64_t>(a->occ, 1), ctr.as<unsigned long long>());
   KHIP_TRY_HIP(hipGetLastError());
   int64_t n = 0;
   KHIP_TRY_HIP(hipMemcpyAsync(&n, ctr.p, 8, hipMemcpyDeviceToHost, a->stream));
@@ -1265,6 +1276,7 @@ static khip_status emit_snapshot(khip_agg* a, const std::vector<uint64_t>& rows,
   auto klen = [&](int64_t kid) { return *(const int64_t*)(arena.data() + kid + 8); };
   std::vector<int64_t> order(n);
   std::iota(order.begin(), order.end(), 0);
+  const bool session = a->engine == 2;
   std::sort(order.begin(), order.end(), [&](int64_t x, int64_t y) {
     const int64_t kx = (int64_t)rows[x * sw], ky = (int64_t)rows[y * sw];
     if (kx != ky) {
@@ -1274,7 +1286,9 @@ static khip_status emit_snapshot(khip_agg* a, const std::vector<uint64_t>& rows,
       if (c) return c < 0;
       if (lx != ly) return lx < ly;
     }
-    return (int64_t)rows[x * sw + 1] < (int64_t)rows[y * sw + 1];
+    if (session && tomb_in && (*tomb_in)[x] != (*tomb_in)[y]) return (*tomb_in)[x] > (*tomb_in)[y];  // deletes first
+    if (rows[x * sw + 1] != rows[y * sw + 1]) return (int64_t)rows[x * sw + 1] < (int64_t)rows[y * sw + 1];
+    return (int64_t)rows[x * sw + 2] < (int64_t)rows[y * sw + 2];
   });
   if (n > out->capacity) {
     out->n_rows = n;
@@ -1296,7 +1310,7 @@ static khip_status emit_snapshot(khip_agg* a, const std::vector<uint64_t>& rows,
       out->key_i64[r] = key;
     }
     if (out->window_start) out->window_start[r] = a->windowed ? ws : 0;
-    if (out->window_end) out->window_end[r] = a->windowed ? ws + a->desc.size_ms : 0;
+    if (out->window_end) out->window_end[r] = a->windowed ? (session ? (int64_t)s[2] : ws + a->desc.size_ms) : 0;
     if (out->rowtime) out->rowtime[r] = (int64_t)s[2];
     for (int i = 0; i < a->desc.n_aggs; i++) {
       const AggOut& o = a->outs[i];
@@ -1433,6 +1447,8 @@ static khip_status compute_changes(khip_agg* a) {
     if (fd.fin_c1 > fd.fin_c0)
       KHIP_TRY(compact_rows(a, a->desc.has_having ? &a->desc.having : nullptr, &a->chg_rows, &a->chg_n, &fd));
     a->chg_tomb.assign((size_t)a->chg_n, 0);
+  } else if (a->changelog && a->engine == 2) {
+    KHIP_TRY(sess_changes(a, &a->chg_rows, &a->chg_tomb, &a->chg_n));
   } else if (a->changelog) {
     KHIP_TRY(part_changes(a, &a->chg_rows, &a->chg_tomb, &a->chg_n));
   } else {
@@ -1478,6 +1494,11 @@ khip_status khip_agg_reset(khip_agg* a) {
   a->lost.clear();
   if (a->engine == 0) {
     KHIP_TRY(part_reset(a));  // also the stream time
+  } else if (a->engine == 2) {
+    a->sess.n = 0;
+    a->sess.nchg = 0;
+    int64_t m1 = -1;
+    KHIP_TRY_HIP(hipMemcpyAsync(a->stream_time.p, &m1, 8, hipMemcpyHostToDevice, a->stream));
   } else {
     hipLaunchKernelGGL(k_init_table, dim3(grid_for(a->cap * a->sw, 256)), dim3(256), 0, a->stream,
                        a->table.as<uint64_t>(), a->cap, a->sw, a->init);
@@ -1531,6 +1552,7 @@ khip_status khip_agg_destroy(khip_agg* a) {
     a->st_cval[c].release();
   }
   part_release(a);
+  sess_release(a);
   for (int e = 0; e < 8; e++)
     if (a->ev[e]) hipEventDestroy(a->ev[e]);
   if (a->stream) hipStreamDestroy(a->stream);

@@ -79,6 +79,7 @@ struct HavingDev {
   int32_t n_lost;
   int64_t fin_c0, fin_c1, fin_size;
   const int64_t* lost;
+  int32_t session;  // SESSION rows: WINDOWEND is the row's own end (word 2), not ws + size
 };
 
 // Retention and EMIT FINAL selection of a row [key, ws, ...] (no-ops unless h.vis / h.fin).
@@ -113,7 +114,7 @@ __device__ __forceinline__ bool pull_ok(const uint64_t* s, const HavingDev& h) {
     if (lo >= h.n_keys || h.keys[lo] != k) return false;
   }
   if (h.pull_windowed) {
-    const int64_t ws = (int64_t)s[1], we = ws + h.size_ms;
+    const int64_t ws = (int64_t)s[1], we = h.session ? (int64_t)s[2] : ws + h.size_ms;
     if (ws < h.ws_lo || ws > h.ws_hi || we < h.we_lo || we > h.we_hi) return false;
   }
   return true;
@@ -278,7 +279,9 @@ __device__ __forceinline__ bool having_ok(const uint64_t* s, const HavingDev& h)
 }
 
 
-// kernels shared by both engines (defined in khip_agg.hip)
+// kernels shared by the engines (defined in khip_agg.hip)
+__global__ void k_blockmax(const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
+                           const uint8_t* __restrict__ rv, int64_t n, int64_t* __restrict__ blockmax);
 __global__ void k_scan_blocks(const int64_t* __restrict__ blockmax, int64_t nb, int64_t* __restrict__ prefix,
                               int64_t* __restrict__ stream_time);
 __global__ void k_scan_excl(int64_t* __restrict__ v, int64_t n, int64_t* __restrict__ total);
@@ -344,6 +347,16 @@ struct PartState {
   HostBuf pinfo;  // pinned: push info (window range, event-time span) and end-of-push stats
 };
 
+// SESSION engine state (khip_agg_session.hip): the session store sorted by (key, start) and
+// the per-push scratch.
+struct SessState {
+  DevBuf rows, rows2;  // store (n rows) and the next push's output
+  int64_t n = 0;
+  DevBuf skey, sidx, skey2, sidx2, st_after, ukeys, ucnt, nseg, useg, s0, cap, scap, fin, fin_pre;
+  DevBuf srow, sfl, trow, crow, ctomb, keep, keep_pre, ctr, tmp;
+  int64_t nchg = 0;    // changelog rows of the last push (crow / ctomb)
+};
+
 }  // namespace khip
 
 using namespace khip;
@@ -379,9 +392,10 @@ struct khip_agg {
   bool profile = false;
   hipEvent_t ev[8] = {};  // 0-4 atomic engine phases, 5-7 partitioned engine
   khip_kernel_times times{};
-  int engine = 0;  // 0 partitioned (LDS-owned groups), 1 global-atomic
+  int engine = 0;  // 0 partitioned (LDS-owned groups), 1 global-atomic, 2 SESSION store
   khip::HavingDev having{};  // the query's HAVING (desc.has_having), maintained by the merge kernel
   khip::PartState part;
+  khip::SessState sess;     // engine 2 (SESSION windows)
   // ---- retention and emission (include/ksqldb_hip.h khip_agg_changes)
   int64_t retention = 0;     // windowed: RETENTION or size + grace
   bool changelog = false;    // KHIP_FLAG_CHANGELOG: keep the push's EMIT CHANGES rows
@@ -420,6 +434,10 @@ khip_status part_compact(khip_agg* a, const HavingDev& h, std::vector<uint64_t>*
 bool part_having_count(khip_agg* a, int64_t* n);
 khip_status part_changes(khip_agg* a, std::vector<uint64_t>* rows, std::vector<uint8_t>* tomb, int64_t* count);
 khip_status part_purge_closed(khip_agg* a, const HavingDev& vis);
+khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
+                      const uint8_t* rv, const ColPtrs& cols, int64_t* tot);
+khip_status sess_changes(khip_agg* a, std::vector<uint64_t>* rows, std::vector<uint8_t>* tomb, int64_t* count);
+void sess_release(khip_agg* a);
 // the first visible window start after the last push (INT64_MIN: nothing expired)
 int64_t visible_from(const khip_agg* a);
 khip_status emit_final_lost(khip_agg* a, const int64_t* ts, const uint8_t* kv, const uint8_t* rv, int64_t n,

@@ -175,3 +175,60 @@ def test_changes_need_the_flag(prod):
     with pytest.raises(abi.KsqlHipError):  # the atomic engine keeps no EMIT CHANGES changelog
         abi.AggHandle(prod, abi.make_agg_desc(**dict(WINDOWS[1], key_type="INT64", aggs=[("COUNT_STAR", -1)],
                                                      flags=abi.FLAG_ENGINE_ATOMIC | abi.FLAG_CHANGELOG)))
+
+
+# ------------------------------------------------------------------ SESSION windows (R11)
+
+SESSIONS = [dict(window_kind="SESSION", size_ms=20_000, grace_ms=-1),
+            dict(window_kind="SESSION", size_ms=5_000, grace_ms=10_000),
+            dict(window_kind="SESSION", size_ms=30_000, grace_ms=0, retention_ms=100_000)]
+
+
+@pytest.mark.parametrize("key_type", ["INT64", "UTF8"])
+@pytest.mark.parametrize("having", [None, {"agg": 0, "op": "GT", "value": 2}])
+@pytest.mark.parametrize("win", range(len(SESSIONS)))
+def test_sessions_vs_oracle(prod, orc, win, having, key_type):
+    """Session merges (tombstones of merged-away sessions), late drops against
+    streamTime - grace - gap, expiry by session end; per-push changes, the store, pull queries."""
+    rng = np.random.default_rng(900 + 10 * win + (having is not None) + (5 if key_type == "UTF8" else 0))
+    kw = dict(SESSIONS[win], key_type=key_type, col_types=COLS, aggs=ALL_AGGS, having=having)
+    g = abi.AggHandle(prod, abi.make_agg_desc(**dict(kw, flags=abi.FLAG_CHANGELOG)))
+    o = abi.AggHandle(orc, abi.make_agg_desc(**kw))
+    tombs = 0
+    for batch in _batches(rng, 5, 5000, key_type, 200, 300_000, 60_000):
+        assert g.push(batch) == o.push(batch)
+        gc, oc = g.changes(), o.changes()
+        _assert_changes_equal(gc, oc, g.desc)
+        tombs += int(gc["tombstone"].sum())
+        gs, os_ = g.snapshot(having), o.snapshot(having)
+        assert_snap_equal(gs, os_, g.desc, ABS_SUM, CNT_DBL)
+        assert g.count_rows(having) == os_["n"]
+    assert tombs > 0 or win == 1
+    if key_type == "INT64":
+        s = o.snapshot()
+        keys = s["key"][::7][:20]
+        q = g.get(keys=keys, ws=(50_000, None))
+        sel = np.isin(s["key"], keys) & (s["ws"] >= 50_000)
+        assert np.array_equal(q["key"], s["key"][sel]) and np.array_equal(q["we"], s["we"][sel])
+    g.close()
+    o.close()
+
+
+def test_sessions_hot_key_and_big_batch(prod, orc):
+    """One key with many sessions and many records (sequential replay of a hot key), plus
+    100k keys in one push."""
+    rng = np.random.default_rng(4242)
+    kw = dict(SESSIONS[0], key_type="INT64", col_types=COLS, aggs=ALL_AGGS)
+    g = abi.AggHandle(prod, abi.make_agg_desc(**dict(kw, flags=abi.FLAG_CHANGELOG)))
+    o = abi.AggHandle(orc, abi.make_agg_desc(**kw))
+    n = 40_000
+    ts = np.sort(rng.integers(0, 4_000_000, n)) + rng.integers(0, 50_000, n)
+    keys = np.where(rng.random(n) < 0.3, 7, rng.integers(0, 100_000, n))
+    cols = [rng.integers(-9, 9, n).astype(np.int32), rng.integers(-9, 9, n), rng.random(n), rng.random(n)]
+    for lo in range(0, n, 20_000):
+        b = abi.HostBatch(ts[lo:lo + 20_000], keys=keys[lo:lo + 20_000], cols=[c[lo:lo + 20_000] for c in cols])
+        assert g.push(b) == o.push(b)
+        _assert_changes_equal(g.changes(), o.changes(), g.desc)
+    assert_snap_equal(g.snapshot(), o.snapshot(), g.desc, ABS_SUM, CNT_DBL)
+    g.close()
+    o.close()
