@@ -1,0 +1,321 @@
+// khip_numparse.hpp — Java-exact text → number conversions for the deserializers
+// (khip_serde.hip), usable on the device and on the host (the CPU tests compile this header
+// with g++ and check it against Python's correctly rounded float() / int()).
+//
+//   java_parse_int / java_parse_long   Integer.parseInt / Long.parseLong: optional sign, ASCII
+//                                      digits, no whitespace, overflow is an error
+//   java_parse_double                  Double.parseDouble: surrounding whitespace trimmed,
+//                                      sign, NaN / Infinity, decimal with optional exponent and
+//                                      f/F/d/D suffix (hexadecimal floats are rejected);
+//                                      correctly rounded (round half to even) by Eisel-Lemire
+//                                      (Lemire 2021; Mushtak & Lemire 2023: no fallback needed
+//                                      for an exact 64-bit mantissa), and for more than 19
+//                                      significant digits a big-integer comparison against the
+//                                      halfway point when w and w + 1 round differently.
+#pragma once
+
+#include <stdint.h>
+#include <string.h>
+
+#ifdef __HIPCC__
+#define KNP_HD __host__ __device__
+#else
+#define KNP_HD
+#endif
+
+namespace khip {
+namespace np {
+
+#ifdef __HIP_DEVICE_COMPILE__
+__constant__
+#endif
+static const uint64_t kPow5[] = {
+#include "khip_pow5.inc"
+};
+
+KNP_HD inline bool is_digit(uint8_t c) { return c >= '0' && c <= '9'; }
+
+// Integer.parseInt / Long.parseLong (ASCII digits; the JDK also accepts non-ASCII Unicode digits,
+// which never occur in these formats' numeric fields).
+KNP_HD inline bool java_parse_long(const uint8_t* p, int64_t n, int64_t* out) {
+  if (n <= 0) return false;
+  int64_t i = 0;
+  bool neg = false;
+  if (p[0] == '-' || p[0] == '+') {
+    neg = p[0] == '-';
+    i = 1;
+    if (n == 1) return false;
+  }
+  uint64_t v = 0;
+  const uint64_t lim = neg ? (uint64_t)1 << 63 : ((uint64_t)1 << 63) - 1;
+  for (; i < n; i++) {
+    if (!is_digit(p[i])) return false;
+    const uint64_t d = p[i] - '0';
+    if (v > (lim - d) / 10) return false;
+    v = v * 10 + d;
+  }
+  *out = neg ? (int64_t)(0 - v) : (int64_t)v;
+  return true;
+}
+
+KNP_HD inline bool java_parse_int(const uint8_t* p, int64_t n, int32_t* out) {
+  int64_t v;
+  if (!java_parse_long(p, n, &v)) return false;
+  if (v < -2147483648LL || v > 2147483647LL) return false;
+  *out = (int32_t)v;
+  return true;
+}
+
+KNP_HD inline uint64_t mul_hi64(uint64_t a, uint64_t b, uint64_t* lo) {
+  const unsigned __int128 r = (unsigned __int128)a * b;
+  *lo = (uint64_t)r;
+  return (uint64_t)(r >> 64);
+}
+
+KNP_HD inline int clz64(uint64_t x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __clzll((long long)x);
+#else
+  return __builtin_clzll(x);
+#endif
+}
+
+// Eisel-Lemire: w * 10^q (w != 0 exact) → binary64 bits, or false when q is outside the table.
+KNP_HD inline uint64_t eisel_lemire(int64_t q, uint64_t w) {
+  if (w == 0 || q < -342) return 0;
+  if (q > 308) return 0x7FF0000000000000ULL;
+  const int lz = clz64(w);
+  w <<= lz;
+  const int64_t idx = 2 * (q + 342);
+  uint64_t lo, hi = mul_hi64(w, kPow5[idx], &lo);
+  if ((hi & 0x1FF) == 0x1FF) {  // 55-bit precision not reached: add the table's low half
+    uint64_t lo2;
+    const uint64_t hi2 = mul_hi64(w, kPow5[idx + 1], &lo2);
+    const uint64_t nl = lo + hi2;
+    if (nl < lo) hi++;
+    lo = nl;
+  }
+  const int upper = (int)(hi >> 63);
+  const int shift = upper + 64 - 52 - 3;
+  uint64_t mant = hi >> shift;
+  int32_t p2 = (int32_t)((((152170 + 65536) * q) >> 16) + 63) + upper - lz + 1023;
+  if (p2 <= 0) {  // subnormal
+    if (-p2 + 1 >= 64) return 0;
+    mant >>= -p2 + 1;
+    mant += mant & 1;
+    mant >>= 1;
+    p2 = mant < ((uint64_t)1 << 52) ? 0 : 1;
+    return ((uint64_t)p2 << 52) | (mant & (((uint64_t)1 << 52) - 1));
+  }
+  if (lo <= 1 && q >= -4 && q <= 23 && (mant & 3) == 1 && (mant << shift) == hi) mant &= ~(uint64_t)1;  // exact tie
+  mant += mant & 1;
+  mant >>= 1;
+  if (mant >= ((uint64_t)2 << 52)) {
+    mant = (uint64_t)1 << 52;
+    p2++;
+  }
+  mant &= ~((uint64_t)1 << 52);
+  if (p2 >= 0x7FF) return 0x7FF0000000000000ULL;
+  return ((uint64_t)p2 << 52) | mant;
+}
+
+// ---- exact fallback: a small fixed-width big integer (little-endian 32-bit limbs)
+constexpr int BIG_LIMBS = 180;  // 5760 bits: 800 digits (2658 bits) x 2^1100 x 10^350
+struct Big {
+  uint32_t d[BIG_LIMBS];
+  int n;
+};
+KNP_HD inline void big_set(Big& b, uint32_t v) {
+  b.n = v ? 1 : 0;
+  b.d[0] = v;
+}
+KNP_HD inline bool big_mul_small(Big& b, uint32_t m, uint32_t add) {
+  uint64_t carry = add;
+  for (int i = 0; i < b.n; i++) {
+    const uint64_t t = (uint64_t)b.d[i] * m + carry;
+    b.d[i] = (uint32_t)t;
+    carry = t >> 32;
+  }
+  if (carry) {
+    if (b.n == BIG_LIMBS) return false;
+    b.d[b.n++] = (uint32_t)carry;
+  }
+  return true;
+}
+KNP_HD inline bool big_mul_pow(Big& b, uint32_t base, int64_t e) {  // b *= base^e (base 2, 5 or 10)
+  const uint32_t chunk = base == 2 ? (1u << 31) : (base == 5 ? 1220703125u /* 5^13 */ : 1000000000u);
+  const int step = base == 2 ? 31 : (base == 5 ? 13 : 9);
+  for (; e >= step; e -= step)
+    if (!big_mul_small(b, chunk, 0)) return false;
+  uint32_t r = 1;
+  for (; e > 0; e--) r *= base;
+  return big_mul_small(b, r, 0);
+}
+KNP_HD inline int big_cmp(const Big& a, const Big& b) {
+  if (a.n != b.n) return a.n < b.n ? -1 : 1;
+  for (int i = a.n - 1; i >= 0; i--)
+    if (a.d[i] != b.d[i]) return a.d[i] < b.d[i] ? -1 : 1;
+  return 0;
+}
+
+// digits[0..nd) (no leading zeros) x 10^e10 vs the value halfway above the double `bits`
+// (finite, positive): returns the correctly rounded bits among {bits, bits + 1}.
+KNP_HD inline bool round_by_halfway(const uint8_t* const* dp, const int64_t* dn, int nseg, int64_t e10, uint64_t bits,
+                                    uint64_t* out) {
+  // halfway h = (2m + 1) * 2^(e - 1), m the significand with the implicit bit, e its exponent
+  const int be = (int)(bits >> 52);
+  uint64_t m = bits & (((uint64_t)1 << 52) - 1);
+  int64_t e;
+  if (be == 0) {
+    e = -1074;
+  } else {
+    m |= (uint64_t)1 << 52;
+    e = be - 1075;
+  }
+  const uint64_t hm = 2 * m + 1;  // h = hm * 2^(e - 1)
+  Big L, R;
+  big_set(L, 0);
+  for (int s = 0; s < nseg; s++)
+    for (int64_t i = 0; i < dn[s]; i++)
+      if (!big_mul_small(L, 10, dp[s][i] - '0')) return false;
+  big_set(R, (uint32_t)hm);
+  if (hm >> 32) {
+    R.d[1] = (uint32_t)(hm >> 32);
+    R.n = 2;
+  }
+  if (e10 >= 0) {
+    if (!big_mul_pow(L, 10, e10)) return false;
+  } else if (!big_mul_pow(R, 10, -e10)) {
+    return false;
+  }
+  if (e - 1 >= 0) {
+    if (!big_mul_pow(R, 2, e - 1)) return false;
+  } else if (!big_mul_pow(L, 2, 1 - e)) {
+    return false;
+  }
+  const int c = big_cmp(L, R);
+  *out = (c > 0 || (c == 0 && (bits & 1))) ? bits + 1 : bits;
+  return true;
+}
+
+KNP_HD inline bool bytes_is(const uint8_t* p, int64_t n, const char* lit) {
+  int64_t k = 0;
+  for (; lit[k]; k++)
+    if (k >= n || p[k] != (uint8_t)lit[k]) return false;
+  return k == n;
+}
+
+constexpr int PD_OK = 0, PD_ERROR = 1, PD_NEED_BIG = 2;
+
+// Double.parseDouble over p[0..n) (java_text = false: a JSON number token, no trimming, no NaN /
+// Infinity / suffixes).  PD_ERROR = NumberFormatException; PD_NEED_BIG (big_ok = false) = more
+// than 19 significant digits whose rounding needs the big-integer comparison.
+KNP_HD inline int java_parse_double(const uint8_t* p, int64_t n, double* out, bool java_text = true,
+                                    bool big_ok = true) {
+  int64_t i = 0, j = n;
+  if (java_text) {  // String.trim(): code points <= ' '
+    while (i < j && p[i] <= ' ') i++;
+    while (j > i && p[j - 1] <= ' ') j--;
+  }
+  if (i >= j) return PD_ERROR;
+  bool neg = false;
+  if (p[i] == '-' || p[i] == '+') {
+    neg = p[i] == '-';
+    i++;
+  }
+  if (i >= j) return PD_ERROR;
+  uint64_t bits;
+  if (java_text && p[i] == 'N') {
+    if (!bytes_is(p + i, j - i, "NaN")) return PD_ERROR;
+    uint64_t nan = 0x7FF8000000000000ULL;
+    memcpy(out, &nan, 8);
+    return PD_OK;
+  }
+  if (java_text && p[i] == 'I') {
+    if (!bytes_is(p + i, j - i, "Infinity")) return PD_ERROR;
+    bits = 0x7FF0000000000000ULL | (neg ? (uint64_t)1 << 63 : 0);
+    memcpy(out, &bits, 8);
+    return PD_OK;
+  }
+  if (java_text && (p[j - 1] == 'd' || p[j - 1] == 'D' || p[j - 1] == 'f' || p[j - 1] == 'F')) j--;
+  // digits [int part][.frac part][e exp]
+  const int64_t i0 = i;
+  while (i < j && is_digit(p[i])) i++;
+  const int64_t int_end = i;
+  int64_t f0 = i, f1 = i;
+  if (i < j && p[i] == '.') {
+    i++;
+    f0 = i;
+    while (i < j && is_digit(p[i])) i++;
+    f1 = i;
+  }
+  if (int_end == i0 && f1 == f0) return PD_ERROR;  // no digit at all
+  int64_t exp10 = 0;
+  if (i < j && (p[i] == 'e' || p[i] == 'E')) {
+    i++;
+    bool eneg = false;
+    if (i < j && (p[i] == '-' || p[i] == '+')) {
+      eneg = p[i] == '-';
+      i++;
+    }
+    if (i >= j || !is_digit(p[i])) return PD_ERROR;
+    int64_t ev = 0;
+    for (; i < j && is_digit(p[i]); i++)
+      if (ev < 100000000) ev = ev * 10 + (p[i] - '0');
+    exp10 = eneg ? -ev : ev;
+  }
+  if (i != j) return PD_ERROR;
+  // significant digits: int part then fraction part, leading zeros dropped
+  const uint8_t* seg[2] = {p + i0, p + f0};
+  int64_t len[2] = {int_end - i0, f1 - f0};
+  int s0 = 0;
+  int64_t k0 = 0;
+  while (s0 < 2 && k0 >= len[s0]) { s0++; k0 = 0; }
+  while (s0 < 2) {  // skip leading zeros
+    if (seg[s0][k0] != '0') break;
+    if (++k0 >= len[s0]) { s0++; k0 = 0; }
+  }
+  if (s0 >= 2) {  // zero
+    bits = neg ? (uint64_t)1 << 63 : 0;
+    memcpy(out, &bits, 8);
+    return PD_OK;
+  }
+  // the decimal is 0.d1 d2 ... scaled: value = digits x 10^(exp10 + int digits after d1 - ...)
+  // count significant digits and the exponent of the last one
+  int64_t nd = 0;
+  uint64_t w = 0;
+  bool trunc = false;
+  for (int s = s0; s < 2; s++)
+    for (int64_t k = (s == s0 ? k0 : 0); k < len[s]; k++) {
+      if (nd < 19) w = w * 10 + (seg[s][k] - '0');
+      else if (seg[s][k] != '0') trunc = true;
+      nd++;
+    }
+  // exponent of the last significant digit: digits after the decimal point count negative
+  const int64_t frac_digits = len[1];
+  int64_t e_last = exp10 - frac_digits;  // value = all digits (as integer) x 10^e_last
+  const int64_t kept = nd < 19 ? nd : 19;
+  const int64_t q = e_last + (nd - kept);  // w x 10^q approximates the value (w = first 19 digits)
+  if (q + kept > 310) {
+    bits = 0x7FF0000000000000ULL;
+  } else if (q + kept < -343) {
+    bits = 0;
+  } else {
+    bits = eisel_lemire(q, w);
+    if (trunc) {
+      const uint64_t b2 = eisel_lemire(q, w + 1);
+      if (b2 != bits) {
+        if (!big_ok) return PD_NEED_BIG;
+        const uint8_t* dp[2] = {seg[s0] + k0, seg[s0 + (s0 == 0)] };
+        int64_t dn[2] = {len[s0] - k0, s0 == 0 ? len[1] : 0};
+        if (!round_by_halfway(dp, dn, s0 == 0 ? 2 : 1, e_last, bits, &bits)) return PD_ERROR;
+      }
+    }
+  }
+  if (neg) bits |= (uint64_t)1 << 63;
+  memcpy(out, &bits, 8);
+  return PD_OK;
+}
+
+}  // namespace np
+}  // namespace khip

@@ -1,0 +1,103 @@
+"""The deserializers' text → number conversions (ksql_amd/csrc/khip_numparse.hpp, compiled here
+for the host with g++ through tools/numparse_check.cpp) against Python's own parsers, which
+like Java's Double.parseDouble / Long.parseLong are exact: doubles correctly rounded (round
+half to even), including more than 19 significant digits (the big-integer halfway path),
+subnormals, overflow to infinity, ties; the Java syntax Double.parseDouble accepts (trimmed
+whitespace, sign, NaN, Infinity, f/d suffixes) and the strict integer syntax.  CPU only."""
+import os
+import random
+import struct
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def checker(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("np") / "npcheck")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-o", exe, os.path.join(REPO, "tools", "numparse_check.cpp")])
+
+    def run(lines):
+        out = subprocess.run([exe], input="\n".join(lines) + "\n", capture_output=True, text=True, check=True).stdout
+        return out.splitlines()
+    return run
+
+
+def bits(x):
+    return struct.unpack("<Q", struct.pack("<d", x))[0]
+
+
+def _random_decimals(rng, n):
+    out = []
+    for _ in range(n):
+        kind = rng.random()
+        if kind < 0.3:  # short decimals
+            s = "%d.%0*d" % (rng.randrange(10 ** rng.randrange(1, 8)), rng.randrange(1, 6), rng.randrange(10 ** 5))
+        elif kind < 0.5:  # long mantissas (> 19 digits)
+            s = str(rng.randrange(1, 10)) + "".join(str(rng.randrange(10)) for _ in range(rng.randrange(18, 40)))
+            s = s[:rng.randrange(1, len(s))] + "." + s[len(s) // 2:]
+        elif kind < 0.7:  # exponents over the whole range
+            s = "%d.%de%d" % (rng.randrange(1, 10), rng.randrange(10 ** 15), rng.randrange(-340, 310))
+        elif kind < 0.85:  # doubles printed exactly (ties and near-ties)
+            x = struct.unpack("<d", struct.pack("<Q", rng.randrange(1, 0x7FEFFFFFFFFFFFFF)))[0]
+            s = repr(x)
+            if rng.random() < 0.5:  # the exact halfway point to the next double, in decimal
+                from decimal import Decimal, getcontext
+                getcontext().prec = 800
+                nxt = struct.unpack("<d", struct.pack("<Q", bits(x) + 1))[0]
+                s = str((Decimal(x) + Decimal(nxt)) / 2)
+        else:  # subnormals / tiny
+            s = "%de-%d" % (rng.randrange(1, 10 ** rng.randrange(1, 20)), rng.randrange(300, 345))
+        if rng.random() < 0.2:
+            s = "-" + s
+        out.append(s)
+    return out
+
+
+def test_doubles_correctly_rounded(checker):
+    rng = random.Random(5)
+    vals = _random_decimals(rng, 6000) + ["0", "-0.0", "1e400", "-1e400", "1e-400", "4.9e-324", "2.4703282292062327e-324",
+                                          "2.4703282292062328e-324", "1.7976931348623157e308", "1.7976931348623158e308",
+                                          "9007199254740993", "0.1", "1e23", "8.98846567431158e307",
+                                          "2.2250738585072011e-308", "2.2250738585072012e-308", "." + "0" * 30 + "1"]
+    got = checker(["d " + v for v in vals])
+    for v, g in zip(vals, got):
+        assert g == "ok %d" % bits(float(v)), (v, g)
+
+
+def test_json_number_tokens(checker):
+    rng = random.Random(6)
+    vals = _random_decimals(rng, 1000)
+    got = checker(["j " + v for v in vals])
+    for v, g in zip(vals, got):
+        assert g == "ok %d" % bits(float(v)), (v, g)
+    # JSON tokens are not Java text: no trimming, no NaN / Infinity / suffixes
+    assert checker(["j NaN", "j  1", "j 1d", "j Infinity"]) == ["err"] * 4
+
+
+def test_java_double_syntax(checker):
+    cases = {" 1.5 ": 1.5, "\t-2e3\t": -2000.0, "+7": 7.0, "1d": 1.0, "2.5F": 2.5, "NaN": float("nan"),
+             "Infinity": float("inf"), "-Infinity": float("-inf"), ".5": 0.5, "5.": 5.0, "1e+2": 100.0}
+    got = checker(["d " + k for k in cases])
+    for (k, v), g in zip(cases.items(), got):
+        assert g == "ok %d" % bits(v), (k, g)
+    bad = ["", "abc", "1e", "--1", "1..2", ".", "e5", "0x1p3", "1,5", "nan", "infinity", "1 2"]
+    assert checker(["d " + b for b in bad]) == ["err"] * len(bad)
+
+
+def test_integers(checker):
+    rng = random.Random(7)
+    longs = [str(rng.randrange(-(1 << 63), 1 << 63)) for _ in range(2000)]
+    assert checker(["l " + v for v in longs]) == ["ok %d" % int(v) for v in longs]
+    edge = {"9223372036854775807": True, "-9223372036854775808": True, "9223372036854775808": False,
+            "-9223372036854775809": False, "+5": True, "-": False, "": False, " 1": False, "1 ": False,
+            "1.0": False, "0x10": False, "00012": True}
+    got = checker(["l " + k for k in edge])
+    for (k, ok), g in zip(edge.items(), got):
+        assert (g != "err") == ok, (k, g)
+        if ok:
+            assert g == "ok %d" % int(k)
+    ints = ["2147483647", "-2147483648", "2147483648", "-2147483649", "12", "-0"]
+    assert checker(["i " + v for v in ints]) == ["ok 2147483647", "ok -2147483648", "err", "err", "ok 12", "ok 0"]
