@@ -464,6 +464,67 @@ khip_status khip_comm_alltoall(khip_comm* c, const uint64_t* send, const int64_t
                                int32_t row_words);
 khip_status khip_comm_destroy(khip_comm* c);
 
+/* ------------------------------------------ deserialization (ksqldb-serde → device columns) */
+
+/* Formats (ksqldb-serde/src/main/java/io/confluent/ksql/serde/):
+ *   KAFKA      kafka/KafkaSerdeFactory.java:42-46 — Kafka's primitive serdes: INT = 4-byte and
+ *              BIGINT = 8-byte big-endian, DOUBLE = 8-byte big-endian IEEE 754, STRING = UTF-8;
+ *              one field per key / value (a wrong length is a SerializationException)
+ *   DELIMITED  delimited/KsqlDelimitedDeserializer.java — CSVFormat.DEFAULT with the configured
+ *              delimiter (RFC 4180 quoting), one field per column, empty field = NULL, numbers
+ *              by Integer.parseInt / Long.parseLong / Double.parseDouble
+ *   JSON       json/KsqlJsonDeserializer.java — one object per record; a column reads the field of
+ *              the same name, else the field whose upper-cased name matches (:273-300); JSON null
+ *              or a missing field = NULL; numbers coerced as JsonSerdeUtils.toInteger / toLong /
+ *              toDouble (Jackson intValue / asLong / doubleValue, or the Java parsers on strings)
+ * A record that fails to deserialize is dropped by the reference (processing log): here it gets a
+ * null key and a null value (every consumer drops it; a table upsert skips it) and is counted. */
+#define KHIP_FMT_NONE 0
+#define KHIP_FMT_KAFKA 1
+#define KHIP_FMT_DELIMITED 2
+#define KHIP_FMT_JSON 3
+#define KHIP_TYPE_STRING 3  /* VARCHAR: keys → UTF-8 key columns; value fields are only checked for
+                               NULL (an INT64 column of zeros + validity: what COUNT(col) reads)  */
+
+typedef struct khip_serde_desc {
+  int32_t key_format;              /* KHIP_FMT_NONE or KHIP_FMT_KAFKA                          */
+  int32_t key_type;                /* KHIP_TYPE_INT32 / INT64 (→ int64 keys) / STRING (→ UTF-8) */
+  int32_t value_format;            /* KHIP_FMT_KAFKA / DELIMITED / JSON                        */
+  int32_t n_fields;                /* value schema columns, in order                            */
+  const int32_t* field_types;      /* KHIP_TYPE_INT32 / INT64 / DOUBLE / STRING                 */
+  const char* const* field_names;  /* JSON: column names as ksqlDB stores them                  */
+  const int32_t* field_out;        /* output column of each field, or -1 (not read)            */
+  int32_t delimiter;               /* DELIMITED: the VALUE_DELIMITER byte (',')                 */
+  int32_t device;
+} khip_serde_desc;
+
+/* One batch of Kafka records as the consumer returns them (arrival order). */
+typedef struct khip_raw_batch {
+  int64_t n_rows;
+  int32_t mem;                   /* KHIP_MEM_HOST or KHIP_MEM_DEVICE                           */
+  const int64_t* ts;             /* record timestamps (ROWTIME)                                */
+  const int64_t* key_offsets;    /* n_rows + 1 offsets into key_bytes                          */
+  const uint8_t* key_bytes;
+  const uint8_t* key_valid;      /* bitmap, 0 = null key; NULL = all present                  */
+  const int64_t* value_offsets;  /* n_rows + 1 offsets into value_bytes                        */
+  const uint8_t* value_bytes;
+  const uint8_t* value_valid;    /* bitmap, 0 = null value (tombstone); NULL = all present     */
+} khip_raw_batch;
+
+typedef struct khip_serde khip_serde;
+
+/* GenericKeySerDe / GenericRowSerDe deserializers (ksqldb-serde/.../GenericKeySerDe.java,
+ * GenericRowSerDe.java) for one source topic's schema. */
+khip_status khip_serde_create(const khip_serde_desc* desc, khip_serde** out);
+
+/* Decode into device columns owned by the handle (valid until its next decode): *out becomes a
+ * KHIP_MEM_DEVICE batch (value columns = the fields with field_out >= 0) for khip_agg_push /
+ * khip_table_upsert / khip_table_probe_device.  UTF-8 keys of a device input point into the
+ * input's key bytes (keep the input alive while using *out).  *n_errors (may be NULL) receives
+ * the records that failed to deserialize. */
+khip_status khip_serde_decode(khip_serde* s, const khip_raw_batch* in, khip_batch* out, int64_t* n_errors);
+khip_status khip_serde_destroy(khip_serde* s);
+
 /* ------------------------------------------------------------ diagnostics */
 
 /* Thread-local message of the last failing call on this thread ("" if none). */

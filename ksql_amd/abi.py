@@ -121,6 +121,20 @@ class ShuffleDesc(C.Structure):
                 ("device", i32), ("flags", i32)]
 
 
+class SerdeDesc(C.Structure):
+    _fields_ = [("key_format", i32), ("key_type", i32), ("value_format", i32), ("n_fields", i32),
+                ("field_types", C.POINTER(i32)), ("field_names", C.POINTER(C.c_char_p)),
+                ("field_out", C.POINTER(i32)), ("delimiter", i32), ("device", i32)]
+
+
+class RawBatch(C.Structure):
+    _fields_ = [("n_rows", i64), ("mem", i32), ("ts", C.c_void_p), ("key_offsets", C.c_void_p),
+                ("key_bytes", C.c_void_p), ("key_valid", C.c_void_p), ("value_offsets", C.c_void_p),
+                ("value_bytes", C.c_void_p), ("value_valid", C.c_void_p)]
+
+
+FMT = {"NONE": 0, "KAFKA": 1, "DELIMITED": 2, "JSON": 3}
+TYPE_STRING = 3
 COMM_ID_BYTES = 128
 
 _P = C.c_void_p
@@ -158,6 +172,9 @@ PRODUCT_ONLY = {
     "comm_exchange_counts": ([_P, C.POINTER(i64), C.POINTER(i64)]),
     "comm_alltoall": ([_P, _P, C.POINTER(i64), _P, i64, C.POINTER(i64), i32]),
     "comm_destroy": ([_P]),
+    "serde_create": ([C.POINTER(SerdeDesc), C.POINTER(_P)]),
+    "serde_decode": ([_P, C.POINTER(RawBatch), C.POINTER(Batch), C.POINTER(i64)]),
+    "serde_destroy": ([_P]),
 }
 
 
@@ -705,3 +722,96 @@ class Comm:
             self.close()
         except Exception:
             pass
+
+
+class SerdeHandle:
+    """khip_serde_*: Kafka record bytes (KAFKA / DELIMITED / JSON) → a device batch."""
+
+    def __init__(self, lib, value_format, fields, key_type="INT64", key_format="KAFKA", delimiter=",",
+                 device=0):
+        """fields: [(name, type, out_col or -1)], type in INT32 / INT64 / DOUBLE / STRING."""
+        self.lib = lib
+        tmap = dict(TYPE, STRING=TYPE_STRING)
+        self._ft = (i32 * len(fields))(*[tmap[t] for _, t, _ in fields])
+        self._fn = (C.c_char_p * len(fields))(*[n.encode() for n, _, _ in fields])
+        self._fo = (i32 * len(fields))(*[o for _, _, o in fields])
+        self.n_out = max([o for _, _, o in fields] + [-1]) + 1
+        self.desc = SerdeDesc(FMT[key_format], tmap[key_type], FMT[value_format], len(fields), self._ft, self._fn,
+                              self._fo, ord(delimiter), device)
+        self.h = C.c_void_p()
+        lib.check(lib.serde_create(C.byref(self.desc), C.byref(self.h)), "serde_create")
+
+    def decode(self, ts, keys, values):
+        """ts: int64 array; keys / values: lists of bytes or None (host batch).  Returns (batch
+        object usable by AggHandle.push / TableHandle.upsert, n_errors)."""
+        n = len(ts)
+        keep = {}
+
+        def pack(items):
+            offs = np.zeros(n + 1, np.int64)
+            offs[1:] = np.cumsum([0 if x is None else len(x) for x in items])
+            data = np.frombuffer(b"".join(b"" if x is None else x for x in items) + b"\0", np.uint8).copy()
+            valid = bitmap([x is not None for x in items])
+            return offs, data, valid
+        ts = np.ascontiguousarray(ts, np.int64)
+        koff, kbytes, kval = pack(keys) if keys is not None else (None, None, None)
+        voff, vbytes, vval = pack(values)
+        keep.update(ts=ts, koff=koff, kbytes=kbytes, kval=kval, voff=voff, vbytes=vbytes, vval=vval)
+        raw = RawBatch(n, MEM_HOST, _ptr(ts), _ptr(koff), _ptr(kbytes), _ptr(kval), _ptr(voff), _ptr(vbytes),
+                       _ptr(vval))
+        out = Batch()
+        nerr = i64()
+        self.lib.check(self.lib.serde_decode(self.h, C.byref(raw), C.byref(out), C.byref(nerr)), "serde_decode")
+
+        class _Decoded:
+            pass
+        d = _Decoded()
+        d.struct = out
+        d._keep = keep
+        return d, nerr.value
+
+    def columns(self, decoded, out_types):
+        """Copy a decoded batch's columns back to the host (for tests): dict of numpy arrays."""
+        b = decoded.struct
+        n = b.n_rows
+        nb = (n + 7) // 8
+
+        def dget(ptr, count, dtype):
+            a = np.zeros(max(count, 1), dtype)
+            if count and ptr:
+                self.lib.check(_hip_copy(a, ptr, a.nbytes if count else 0), "copy")
+            return a[:count]
+        res = {"key_valid": np.unpackbits(dget(b.key_valid, nb, np.uint8), bitorder="little")[:n].astype(bool),
+               "row_valid": np.unpackbits(dget(b.row_valid, nb, np.uint8), bitorder="little")[:n].astype(bool)}
+        if b.key_i64:
+            res["key"] = dget(b.key_i64, n, np.int64)
+        cols, valid = [], []
+        for c, t in enumerate(out_types):
+            cols.append(dget(b.col_data[c], n, NP_TYPE[TYPE[t]] if t != "STRING" else np.int64))
+            valid.append(np.unpackbits(dget(b.col_valid[c], nb, np.uint8), bitorder="little")[:n].astype(bool))
+        res["cols"], res["valid"] = cols, valid
+        return res
+
+    def close(self):
+        if self.h:
+            self.lib.serde_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _hip_copy(dst, src_ptr, nbytes):
+    """Device → host copy through torch's HIP runtime (tests only)."""
+    import torch
+    t = torch.from_numpy(dst.view(np.uint8).reshape(-1))
+    if nbytes:
+        # wrap the device pointer as a torch tensor via the CUDA array interface
+        class _Dev:
+            __cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (int(src_ptr), True), "version": 2}
+        t[:nbytes].copy_(torch.as_tensor(_Dev(), device="cuda"))
+    return KHIP_OK
+

@@ -1,0 +1,691 @@
+// khip_serde.hip — deserialization of Kafka record bytes into device columns (gfx950).
+//
+// Replaces, for the hot path's source topics, the per-record GenericKeySerDe / GenericRowSerDe
+// deserializers (KAFKA, DELIMITED, JSON; include/ksqldb_hip.h "deserialization") that box every
+// record into a GenericKey / GenericRow before the aggregate or join sees it — the reference's
+// documented bottleneck (ksqldb-benchmark/README.md:7-9).
+//
+// Layout: the raw batch is the consumer's view — concatenated key / value bytes with n + 1
+// offsets and null bitmaps.  One thread decodes one record (records are tens to hundreds of
+// bytes; neighbouring threads read neighbouring bytes, so the loads stay cache friendly); each
+// wave assembles the validity bitmaps of its 64 records with ballots (one 8-byte store per
+// bitmap).  Numbers are converted exactly as Java does (khip_numparse.hpp); the rare double
+// with more than 19 significant digits whose rounding needs big-integer arithmetic is finished
+// by a second kernel (k_serde_fix) over just those fields, so the decode kernel keeps a small
+// stack.
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "khip_util.hpp"
+#include "khip_numparse.hpp"
+
+namespace khip {
+
+constexpr int SD_MAX_FIELDS = 32;
+constexpr int SD_NAME_BYTES = 64;
+
+struct SerdeParams {
+  int32_t key_format, key_type, value_format, n_fields, delimiter, n_out;
+  int32_t ftype[SD_MAX_FIELDS];
+  int32_t fout[SD_MAX_FIELDS];
+  int32_t name_len[SD_MAX_FIELDS];
+  uint8_t name[SD_MAX_FIELDS][SD_NAME_BYTES];
+};
+
+struct SerdeOut {
+  int64_t* key_i64;
+  uint8_t* key_valid;
+  uint8_t* row_valid;
+  void* col[SD_MAX_FIELDS];
+  uint8_t* col_valid[SD_MAX_FIELDS];
+  unsigned long long* n_err;
+  unsigned long long* n_fix;
+  int64_t* fix;  // (row, out column, byte offset, length | json flag << 32) per deferred double
+  int64_t fix_cap;
+};
+
+// a field's value as the decode loop found it
+struct Tok {
+  int32_t off, len;  // bytes (for strings: between the quotes)
+  int8_t kind;       // -1 absent, 0 null, 1 number, 2 string, 3 literal (true / false), 4 object / array
+  int8_t esc;        // string with escapes
+};
+
+__device__ __forceinline__ uint64_t be_load(const uint8_t* p, int n) {
+  uint64_t v = 0;
+  for (int i = 0; i < n; i++) v = v << 8 | p[i];
+  return v;
+}
+
+// (int) d and (long) d in Java: NaN → 0, saturating.
+__device__ __forceinline__ int64_t java_d2l(double d) {
+  if (d != d) return 0;
+  if (d >= 9.2233720368547758e18) return INT64_MAX;
+  if (d <= -9.2233720368547758e18) return INT64_MIN;
+  return (int64_t)d;
+}
+__device__ __forceinline__ int32_t java_d2i(double d) {
+  if (d != d) return 0;
+  if (d >= 2147483647.0) return INT32_MAX;
+  if (d <= -2147483648.0) return INT32_MIN;
+  return (int32_t)d;
+}
+
+__device__ __forceinline__ bool json_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+
+// Skip one JSON value starting at p[i] (i < n, not whitespace); returns the index after it or -1.
+__device__ int64_t json_skip(const uint8_t* p, int64_t i, int64_t n, Tok* t) {
+  const uint8_t c = p[i];
+  if (c == '"') {
+    int64_t j = i + 1;
+    int esc = 0;
+    while (j < n && p[j] != '"') {
+      if (p[j] == '\\') {
+        esc = 1;
+        j++;
+      }
+      j++;
+    }
+    if (j >= n) return -1;
+    t->kind = 2;
+    t->off = (int32_t)(i + 1);
+    t->len = (int32_t)(j - i - 1);
+    t->esc = (int8_t)esc;
+    return j + 1;
+  }
+  if (c == '{' || c == '[') {
+    int depth = 0;
+    int64_t j = i;
+    for (; j < n; j++) {
+      const uint8_t d = p[j];
+      if (d == '"') {
+        j++;
+        while (j < n && p[j] != '"') j += p[j] == '\\' ? 2 : 1;
+        if (j >= n) return -1;
+      } else if (d == '{' || d == '[') {
+        depth++;
+      } else if (d == '}' || d == ']') {
+        if (--depth == 0) break;
+      }
+    }
+    if (j >= n) return -1;
+    t->kind = 4;
+    t->off = (int32_t)i;
+    t->len = (int32_t)(j + 1 - i);
+    return j + 1;
+  }
+  if (c == 'n' || c == 't' || c == 'f') {
+    const char* lit = c == 'n' ? "null" : (c == 't' ? "true" : "false");
+    const int L = c == 'f' ? 5 : 4;
+    if (i + L > n) return -1;
+    for (int k = 0; k < L; k++)
+      if (p[i + k] != (uint8_t)lit[k]) return -1;
+    t->kind = c == 'n' ? 0 : 3;
+    t->off = (int32_t)i;
+    t->len = L;
+    return i + L;
+  }
+  // number: -?(0|[1-9]d*)(.d+)?([eE][+-]?d+)?  (Jackson's strict grammar)
+  int64_t j = i;
+  if (p[j] == '-') j++;
+  if (j >= n || !np::is_digit(p[j])) return -1;
+  if (p[j] == '0') {
+    j++;
+    if (j < n && np::is_digit(p[j])) return -1;  // leading zero
+  } else {
+    while (j < n && np::is_digit(p[j])) j++;
+  }
+  if (j < n && p[j] == '.') {
+    j++;
+    if (j >= n || !np::is_digit(p[j])) return -1;
+    while (j < n && np::is_digit(p[j])) j++;
+  }
+  if (j < n && (p[j] == 'e' || p[j] == 'E')) {
+    j++;
+    if (j < n && (p[j] == '+' || p[j] == '-')) j++;
+    if (j >= n || !np::is_digit(p[j])) return -1;
+    while (j < n && np::is_digit(p[j])) j++;
+  }
+  t->kind = 1;
+  t->off = (int32_t)i;
+  t->len = (int32_t)(j - i);
+  return j;
+}
+
+// JSON string unescape into buf (cap bytes); false on a bad escape or overflow.
+__device__ bool json_unescape(const uint8_t* p, int64_t n, uint8_t* buf, int cap, int* outn) {
+  int m = 0;
+  for (int64_t i = 0; i < n; i++) {
+    uint32_t c = p[i];
+    if (c == '\\') {
+      if (++i >= n) return false;
+      switch (p[i]) {
+        case '"': c = '"'; break;
+        case '\\': c = '\\'; break;
+        case '/': c = '/'; break;
+        case 'b': c = 8; break;
+        case 'f': c = 12; break;
+        case 'n': c = 10; break;
+        case 'r': c = 13; break;
+        case 't': c = 9; break;
+        case 'u': {
+          if (i + 4 >= n) return false;
+          uint32_t u = 0;
+          for (int k = 1; k <= 4; k++) {
+            const uint8_t h = p[i + k];
+            u = u * 16 + (h >= '0' && h <= '9' ? h - '0' : (h >= 'a' && h <= 'f' ? h - 'a' + 10 : (h >= 'A' && h <= 'F' ? h - 'A' + 10 : 99)));
+            if (u > 0xFFFF) return false;
+          }
+          i += 4;
+          if (u >= 0x80) return false;  // non-ASCII never forms a number; names are ASCII here
+          c = u;
+          break;
+        }
+        default: return false;
+      }
+    }
+    if (m >= cap) return false;
+    buf[m++] = (uint8_t)c;
+  }
+  *outn = m;
+  return true;
+}
+
+__device__ __forceinline__ uint8_t up(uint8_t c) { return c >= 'a' && c <= 'z' ? c - 32 : c; }
+
+// A numeric field (raw text p[0..n), json: a JSON number token, else Java text) → column.
+// Returns 0 ok, 1 error, 2 deferred (big-integer rounding).
+__device__ int put_number(const SerdeParams& q, int f, const uint8_t* p, int64_t n, bool json_num, void* col,
+                          int64_t row) {
+  const int t = q.ftype[f];
+  if (json_num) {
+    bool is_int = true;
+    for (int64_t k = 0; k < n; k++)
+      if (p[k] == '.' || p[k] == 'e' || p[k] == 'E') is_int = false;
+    if (is_int && t != KHIP_TYPE_DOUBLE) {  // intValue() / asLong(): the low 32 / 64 bits of the integer
+      uint64_t v = 0;
+      int64_t k = p[0] == '-' ? 1 : 0;
+      for (; k < n; k++) v = v * 10 + (p[k] - '0');
+      if (p[0] == '-') v = 0 - v;
+      if (!col) return 0;
+      if (t == KHIP_TYPE_INT32) ((int32_t*)col)[row] = (int32_t)(uint32_t)v;
+      else ((int64_t*)col)[row] = (int64_t)v;
+      return 0;
+    }
+    double d;
+    const int st = np::java_parse_double(p, n, &d, false, false);
+    if (st != np::PD_OK) return col || st == 1 ? st : 0;  // an unread field's exact rounding is moot
+    if (!col) return 0;
+    if (t == KHIP_TYPE_INT32) ((int32_t*)col)[row] = java_d2i(d);
+    else if (t == KHIP_TYPE_INT64) ((int64_t*)col)[row] = java_d2l(d);
+    else ((double*)col)[row] = d;
+    return 0;
+  }
+  if (t == KHIP_TYPE_INT32) {
+    int32_t v;
+    if (!np::java_parse_int(p, n, &v)) return 1;
+    if (col) ((int32_t*)col)[row] = v;
+  } else if (t == KHIP_TYPE_INT64) {
+    int64_t v;
+    if (!np::java_parse_long(p, n, &v)) return 1;
+    if (col) ((int64_t*)col)[row] = v;
+  } else {
+    double d;
+    const int st = np::java_parse_double(p, n, &d, true, false);
+    if (st != np::PD_OK) return col || st == 1 ? st : 0;
+    if (col) ((double*)col)[row] = d;
+  }
+  return 0;
+}
+
+__global__ __launch_bounds__(256) void k_serde_decode(SerdeParams q, int64_t n, const int64_t* __restrict__ koff,
+                                                      const uint8_t* __restrict__ kbytes, const uint8_t* __restrict__ kval,
+                                                      const int64_t* __restrict__ voff, const uint8_t* __restrict__ vbytes,
+                                                      const uint8_t* __restrict__ vval, SerdeOut o) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  bool ok = i < n;  // deserialized without error
+  bool key_ok = false, row_ok = false;
+  uint32_t fnull = 0;  // per output column: NULL
+  if (i < n) {
+    // ---- key (KAFKA format)
+    if (q.key_format == KHIP_FMT_NONE) {
+      key_ok = true;
+      if (o.key_i64) o.key_i64[i] = 0;
+    } else if (bit_get(kval, i)) {
+      const int64_t k0 = koff[i], kn = koff[i + 1] - k0;
+      if (q.key_type == KHIP_TYPE_INT64) {
+        if (kn == 8) o.key_i64[i] = (int64_t)be_load(kbytes + k0, 8);
+        else ok = false;
+      } else if (q.key_type == KHIP_TYPE_INT32) {
+        if (kn == 4) o.key_i64[i] = (int64_t)(int32_t)(uint32_t)be_load(kbytes + k0, 4);
+        else ok = false;
+      }
+      key_ok = true;  // STRING keys: the bytes themselves
+    }
+    // ---- value
+    row_ok = bit_get(vval, i);
+    if (ok && row_ok) {
+      const int64_t v0 = voff[i], vn = voff[i + 1] - v0;
+      const uint8_t* p = vbytes + v0;
+      for (int c = 0; c < q.n_out; c++) fnull |= 1u << c;
+      if (q.value_format == KHIP_FMT_KAFKA) {
+        const int f = 0;
+        const int c = q.fout[f];
+        const int t = q.ftype[f];
+        if (t == KHIP_TYPE_INT32 && vn != 4) ok = false;
+        else if ((t == KHIP_TYPE_INT64 || t == KHIP_TYPE_DOUBLE) && vn != 8) ok = false;
+        else if (c >= 0) {
+          fnull &= ~(1u << c);
+          if (t == KHIP_TYPE_INT32) ((int32_t*)o.col[c])[i] = (int32_t)(uint32_t)be_load(p, 4);
+          else if (t == KHIP_TYPE_STRING) ((int64_t*)o.col[c])[i] = 0;
+          else ((uint64_t*)o.col[c])[i] = be_load(p, 8);
+        }
+      } else if (q.value_format == KHIP_FMT_DELIMITED) {
+        // CSVFormat.DEFAULT: RFC 4180 fields, quote '"' (doubled inside), first record only
+        int64_t j = 0;
+        int f = 0;
+        bool more = vn > 0;
+        if (!more) ok = false;  // "No fields in record"
+        while (ok && more) {
+          int64_t s, e;
+          bool quoted = false, inner_quote = false;
+          if (j < vn && p[j] == '"') {
+            quoted = true;
+            int64_t k = j + 1;
+            while (true) {
+              if (k >= vn) { ok = false; break; }  // EOF inside an encapsulated token
+              if (p[k] == '"') {
+                if (k + 1 < vn && p[k + 1] == '"') { inner_quote = true; k += 2; continue; }
+                break;
+              }
+              k++;
+            }
+            if (!ok) break;
+            s = j + 1;
+            e = k;
+            j = k + 1;
+            if (j < vn && p[j] != q.delimiter && p[j] != '\n' && p[j] != '\r') { ok = false; break; }
+          } else {
+            s = j;
+            while (j < vn && p[j] != q.delimiter && p[j] != '\n' && p[j] != '\r') j++;
+            e = j;
+          }
+          more = j < vn && p[j] == q.delimiter;
+          j++;
+          if (f >= q.n_fields) { ok = false; break; }  // column count mismatch
+          const int c = q.fout[f];
+          if (e > s && q.ftype[f] != KHIP_TYPE_STRING) {  // every field parses (an unread one too)
+            const int st = inner_quote ? 1 : put_number(q, f, p + s, e - s, false, c >= 0 ? o.col[c] : nullptr, i);
+            if (st == 1) { ok = false; break; }
+            if (st == 2) {
+              const unsigned long long slot = atomicAdd(o.n_fix, 1ULL);
+              if ((int64_t)slot < o.fix_cap) {
+                o.fix[4 * slot] = i;
+                o.fix[4 * slot + 1] = c;
+                o.fix[4 * slot + 2] = v0 + s;
+                o.fix[4 * slot + 3] = e - s;
+              }
+            }
+            if (c >= 0) fnull &= ~(1u << c);
+          } else if (e > s && c >= 0) {  // a non-empty VARCHAR (empty field = NULL)
+            ((int64_t*)o.col[c])[i] = 0;
+            fnull &= ~(1u << c);
+          }
+          (void)quoted;
+          f++;
+        }
+        if (ok && f != q.n_fields) ok = false;
+      } else {  // JSON
+        int64_t j = 0;
+        while (j < vn && json_ws(p[j])) j++;
+        if (j >= vn || p[j] != '{') ok = false;
+        Tok ex[SD_MAX_FIELDS], ci[SD_MAX_FIELDS];
+        for (int f = 0; f < q.n_fields; f++) {
+          ex[f].kind = -1;
+          ci[f].kind = -1;
+        }
+        j++;
+        bool first = true;
+        while (ok) {
+          while (j < vn && json_ws(p[j])) j++;
+          if (j >= vn) { ok = false; break; }
+          if (p[j] == '}') { if (!first) ok = false; break; }  // "{}" only (trailing commas are errors)
+          first = false;
+          Tok kt;
+          const int64_t kend = p[j] == '"' ? json_skip(p, j, vn, &kt) : -1;
+          if (kend < 0) { ok = false; break; }
+          j = kend;
+          while (j < vn && json_ws(p[j])) j++;
+          if (j >= vn || p[j] != ':') { ok = false; break; }
+          j++;
+          while (j < vn && json_ws(p[j])) j++;
+          if (j >= vn) { ok = false; break; }
+          Tok vt;
+          vt.esc = 0;
+          const int64_t vend = json_skip(p, j, vn, &vt);
+          if (vend < 0) { ok = false; break; }
+          j = vend;
+          // field name: exact match wins, else the upper-cased name (last such field)
+          uint8_t nb[SD_NAME_BYTES];
+          int nl = 0;
+          const uint8_t* kp = p + kt.off;
+          if (kt.esc) {
+            if (!json_unescape(p + kt.off, kt.len, nb, SD_NAME_BYTES, &nl)) nl = -1;
+            kp = nb;
+          } else {
+            nl = kt.len <= SD_NAME_BYTES ? (int)kt.len : -1;
+          }
+          if (nl >= 0)
+            for (int f = 0; f < q.n_fields; f++) {
+              if (q.name_len[f] != nl) continue;
+              bool same = true, same_up = true;
+              for (int k = 0; k < nl; k++) {
+                same &= kp[k] == q.name[f][k];
+                same_up &= up(kp[k]) == q.name[f][k];
+              }
+              if (same) ex[f] = vt;
+              else if (same_up) ci[f] = vt;
+            }
+          while (j < vn && json_ws(p[j])) j++;
+          if (j < vn && p[j] == ',') { j++; continue; }
+          if (j < vn && p[j] == '}') break;
+          ok = false;
+        }
+        for (int f = 0; ok && f < q.n_fields; f++) {  // every schema field is coerced (:273-300)
+          const int c = q.fout[f];
+          const Tok t = ex[f].kind >= 0 ? ex[f] : ci[f];
+          if (t.kind <= 0) continue;  // missing or JSON null: NULL
+          if (q.ftype[f] == KHIP_TYPE_STRING) {  // asText(): any value is a non-null string
+            if (c >= 0) {
+              ((int64_t*)o.col[c])[i] = 0;
+              fnull &= ~(1u << c);
+            }
+            continue;
+          }
+          if (t.kind != 1 && t.kind != 2) { ok = false; break; }  // boolean / object / array
+          int st;
+          if (t.kind == 2) {  // a string: Integer.parseInt / Long.parseLong / Double.parseDouble
+            uint8_t sb[96];
+            int sn;
+            const uint8_t* sp = p + t.off;
+            int64_t sl = t.len;
+            if (t.esc) {
+              if (!json_unescape(p + t.off, t.len, sb, 96, &sn)) { ok = false; break; }
+              sp = sb;
+              sl = sn;
+            }
+            st = put_number(q, f, sp, sl, false, c >= 0 ? o.col[c] : nullptr, i);
+            if (st == 2 && t.esc) st = 1;  // escaped long decimals: not supported here
+          } else {
+            st = put_number(q, f, p + t.off, t.len, true, c >= 0 ? o.col[c] : nullptr, i);
+          }
+          if (st == 1) { ok = false; break; }
+          if (c < 0) continue;
+          if (st == 2) {
+            const unsigned long long slot = atomicAdd(o.n_fix, 1ULL);
+            if ((int64_t)slot < o.fix_cap) {
+              o.fix[4 * slot] = i;
+              o.fix[4 * slot + 1] = c;
+              o.fix[4 * slot + 2] = v0 + t.off;
+              o.fix[4 * slot + 3] = t.len | (t.kind == 1 ? (1LL << 32) : 0);
+            }
+          }
+          fnull &= ~(1u << c);
+        }
+      }
+    }
+  }
+  const bool err = i < n && !ok;
+  const uint64_t bk = __ballot(i < n && ok && key_ok), br = __ballot(i < n && ok && row_ok);
+  const int64_t wbase = i - lane;
+  if (lane == 0 && wbase < n) {
+    const int64_t nbytes = std::min<int64_t>(8, (n - wbase + 7) / 8);
+    for (int b = 0; b < nbytes; b++) {
+      o.key_valid[wbase / 8 + b] = (uint8_t)(bk >> (8 * b));
+      o.row_valid[wbase / 8 + b] = (uint8_t)(br >> (8 * b));
+    }
+  }
+  for (int c = 0; c < q.n_out; c++) {
+    const uint64_t bv = __ballot(i < n && ok && row_ok && !((fnull >> c) & 1));
+    if (lane == 0 && wbase < n) {
+      const int64_t nbytes = std::min<int64_t>(8, (n - wbase + 7) / 8);
+      for (int b = 0; b < nbytes; b++) o.col_valid[c][wbase / 8 + b] = (uint8_t)(bv >> (8 * b));
+    }
+  }
+  const uint64_t be = __ballot(err);
+  if (lane == 0 && be) atomicAdd(o.n_err, (unsigned long long)__popcll(be));
+}
+
+// The deferred doubles (more than 19 significant digits, rounding decided by big integers).
+__global__ __launch_bounds__(64) void k_serde_fix(const int64_t* __restrict__ fix, int64_t nfix,
+                                                  const uint8_t* __restrict__ vbytes, SerdeOut o,
+                                                  const SerdeParams q) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nfix) return;
+  const int64_t row = fix[4 * k], c = fix[4 * k + 1], off = fix[4 * k + 2];
+  const int64_t len = fix[4 * k + 3] & 0xFFFFFFFFLL;
+  const bool json_num = (fix[4 * k + 3] >> 32) & 1;
+  int f = 0;
+  while (f < q.n_fields && q.fout[f] != c) f++;
+  double d;
+  const int st = np::java_parse_double(vbytes + off, len, &d, !json_num, true);
+  if (st != np::PD_OK) {  // the record fails after all
+    atomicAnd((unsigned int*)(o.key_valid + (row >> 5) * 4), ~(1u << (row & 31)));
+    atomicAnd((unsigned int*)(o.row_valid + (row >> 5) * 4), ~(1u << (row & 31)));
+    atomicAdd(o.n_err, 1ULL);
+    return;
+  }
+  const int t = q.ftype[f];
+  if (t == KHIP_TYPE_INT32) ((int32_t*)o.col[c])[row] = java_d2i(d);
+  else if (t == KHIP_TYPE_INT64) ((int64_t*)o.col[c])[row] = java_d2l(d);
+  else ((double*)o.col[c])[row] = d;
+}
+
+}  // namespace khip
+
+using namespace khip;
+
+struct khip_serde {
+  khip_serde_desc desc{};
+  SerdeParams q{};
+  std::vector<int32_t> out_type;  // per output column: element type
+  int device = 0;
+  hipStream_t stream = nullptr;
+  DevBuf key_i64, key_valid, row_valid, cols[SD_MAX_FIELDS], cvalid[SD_MAX_FIELDS], ctr, fix;
+  DevBuf st_ts, st_koff, st_kbytes, st_kval, st_voff, st_vbytes, st_vval;
+  std::vector<const void*> col_ptrs;
+  std::vector<const uint8_t*> val_ptrs;
+  int64_t fix_cap = 0;
+};
+
+static khip_status sstage(khip_serde* s, DevBuf& b, const void* src, size_t bytes) {
+  KHIP_TRY(b.ensure(std::max<size_t>(bytes, 8)));
+  if (bytes) KHIP_TRY_HIP(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, s->stream));
+  return KHIP_OK;
+}
+
+extern "C" {
+
+khip_status khip_serde_create(const khip_serde_desc* d, khip_serde** out) {
+  clear_error();
+  if (!d || !out) return fail(KHIP_E_INVALID, "null argument");
+  if (d->key_format != KHIP_FMT_NONE && d->key_format != KHIP_FMT_KAFKA)
+    return fail(KHIP_E_UNSUPPORTED, "key format (KAFKA or none)");
+  if (d->key_format == KHIP_FMT_KAFKA && d->key_type != KHIP_TYPE_INT32 && d->key_type != KHIP_TYPE_INT64 &&
+      d->key_type != KHIP_TYPE_STRING)
+    return fail(KHIP_E_UNSUPPORTED, "key type");
+  if (d->value_format != KHIP_FMT_KAFKA && d->value_format != KHIP_FMT_DELIMITED && d->value_format != KHIP_FMT_JSON)
+    return fail(KHIP_E_UNSUPPORTED, "value format (KAFKA, DELIMITED, JSON)");
+  if (d->n_fields < 1 || d->n_fields > SD_MAX_FIELDS) return fail(KHIP_E_UNSUPPORTED, "1..32 value fields");
+  if (d->value_format == KHIP_FMT_KAFKA && d->n_fields != 1)
+    return fail(KHIP_E_INVALID, "the KAFKA format carries one field");
+  khip_serde* s = new khip_serde();
+  s->desc = *d;
+  SerdeParams& q = s->q;
+  q.key_format = d->key_format;
+  q.key_type = d->key_type;
+  q.value_format = d->value_format;
+  q.n_fields = d->n_fields;
+  q.delimiter = d->delimiter ? d->delimiter : ',';
+  int n_out = 0;
+  for (int f = 0; f < d->n_fields; f++) {
+    const int t = d->field_types[f];
+    if (t < KHIP_TYPE_INT32 || t > KHIP_TYPE_STRING) {
+      delete s;
+      return fail(KHIP_E_UNSUPPORTED, "field type");
+    }
+    q.ftype[f] = t;
+    q.fout[f] = d->field_out ? d->field_out[f] : f;
+    if (q.fout[f] >= 0) n_out = std::max(n_out, q.fout[f] + 1);
+    if (d->value_format == KHIP_FMT_JSON) {
+      const char* nm = d->field_names ? d->field_names[f] : nullptr;
+      const size_t L = nm ? strlen(nm) : 0;
+      if (!nm || L > SD_NAME_BYTES) {
+        delete s;
+        return fail(KHIP_E_INVALID, "JSON field names (<= 64 bytes) required");
+      }
+      q.name_len[f] = (int32_t)L;
+      memcpy(q.name[f], nm, L);
+    }
+  }
+  q.n_out = n_out;
+  s->out_type.assign(n_out, KHIP_TYPE_INT64);
+  for (int f = 0; f < d->n_fields; f++)
+    if (q.fout[f] >= 0) s->out_type[q.fout[f]] = q.ftype[f] == KHIP_TYPE_STRING ? KHIP_TYPE_INT64 : q.ftype[f];
+  s->device = d->device;
+  DeviceGuard g(s->device);
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamDefault) != hipSuccess) {
+    delete s;
+    return fail(KHIP_E_DEVICE, "hipStreamCreate failed (no device?)");
+  }
+  *out = s;
+  return KHIP_OK;
+}
+
+khip_status khip_serde_decode(khip_serde* s, const khip_raw_batch* in, khip_batch* out, int64_t* n_errors) {
+  clear_error();
+  if (!s || !in || !out) return fail(KHIP_E_INVALID, "null argument");
+  const int64_t n = in->n_rows;
+  if (n < 0 || !in->value_offsets || (n && !in->ts)) return fail(KHIP_E_INVALID, "raw batch shape");
+  if (s->q.key_format != KHIP_FMT_NONE && !in->key_offsets) return fail(KHIP_E_INVALID, "missing key offsets");
+  DeviceGuard g(s->device);
+  const SerdeParams& q = s->q;
+  const int64_t* ts = in->ts;
+  const int64_t *koff = in->key_offsets, *voff = in->value_offsets;
+  const uint8_t *kb = in->key_bytes, *kv = in->key_valid, *vb = in->value_bytes, *vv = in->value_valid;
+  const size_t bm = (size_t)(n + 7) / 8;
+  if (in->mem == KHIP_MEM_HOST) {
+    KHIP_TRY(sstage(s, s->st_ts, ts, n * 8));
+    ts = s->st_ts.as<int64_t>();
+    KHIP_TRY(sstage(s, s->st_voff, voff, (n + 1) * 8));
+    const int64_t vbytes = voff[n];
+    KHIP_TRY(sstage(s, s->st_vbytes, vb, (size_t)vbytes));
+    voff = s->st_voff.as<int64_t>();
+    vb = s->st_vbytes.as<uint8_t>();
+    if (vv) { KHIP_TRY(sstage(s, s->st_vval, vv, bm)); vv = s->st_vval.as<uint8_t>(); }
+    if (koff) {
+      const int64_t kbytes = koff[n];
+      KHIP_TRY(sstage(s, s->st_koff, koff, (n + 1) * 8));
+      KHIP_TRY(sstage(s, s->st_kbytes, kb, (size_t)kbytes));
+      koff = s->st_koff.as<int64_t>();
+      kb = s->st_kbytes.as<uint8_t>();
+    }
+    if (kv) { KHIP_TRY(sstage(s, s->st_kval, kv, bm)); kv = s->st_kval.as<uint8_t>(); }
+  } else if (in->mem != KHIP_MEM_DEVICE) {
+    return fail(KHIP_E_INVALID, "batch mem");
+  }
+  const size_t bm4 = ((size_t)(n + 31) / 32) * 4 + 8;  // word-aligned: k_serde_fix clears bits atomically
+  SerdeOut o{};
+  if (q.key_format == KHIP_FMT_NONE || q.key_type != KHIP_TYPE_STRING) {
+    KHIP_TRY(s->key_i64.ensure(std::max<int64_t>(n, 1) * 8));
+    o.key_i64 = s->key_i64.as<int64_t>();
+  }
+  KHIP_TRY(s->key_valid.ensure(bm4));
+  KHIP_TRY(s->row_valid.ensure(bm4));
+  o.key_valid = s->key_valid.as<uint8_t>();
+  o.row_valid = s->row_valid.as<uint8_t>();
+  for (int c = 0; c < q.n_out; c++) {
+    KHIP_TRY(s->cols[c].ensure(std::max<int64_t>(n, 1) * (s->out_type[c] == KHIP_TYPE_INT32 ? 4 : 8)));
+    KHIP_TRY(s->cvalid[c].ensure(bm4));
+    o.col[c] = s->cols[c].p;
+    o.col_valid[c] = s->cvalid[c].as<uint8_t>();
+  }
+  KHIP_TRY(s->ctr.ensure(16));
+  KHIP_TRY_HIP(hipMemsetAsync(s->ctr.p, 0, 16, s->stream));
+  o.n_err = s->ctr.as<unsigned long long>();
+  o.n_fix = o.n_err + 1;
+  if (s->fix_cap == 0) {
+    s->fix_cap = 1024;
+    KHIP_TRY(s->fix.ensure((size_t)s->fix_cap * 32));
+  }
+  o.fix = s->fix.as<int64_t>();
+  o.fix_cap = s->fix_cap;
+  unsigned long long c2[2] = {0, 0};
+  if (n > 0) {
+    for (int attempt = 0; attempt < 2; attempt++) {
+      hipLaunchKernelGGL(k_serde_decode, dim3(ceil_div(n, 256)), dim3(256), 0, s->stream, q, n, koff, kb, kv, voff, vb, vv,
+                         o);
+      KHIP_TRY_HIP(hipGetLastError());
+      KHIP_TRY_HIP(hipMemcpyAsync(c2, s->ctr.p, 16, hipMemcpyDeviceToHost, s->stream));
+      KHIP_TRY_HIP(hipStreamSynchronize(s->stream));
+      if ((int64_t)c2[1] <= s->fix_cap) break;
+      s->fix_cap = (int64_t)next_pow2(c2[1]);  // room for every deferred double, decode again
+      s->fix.release();
+      KHIP_TRY(s->fix.ensure((size_t)s->fix_cap * 32));
+      o.fix = s->fix.as<int64_t>();
+      o.fix_cap = s->fix_cap;
+      KHIP_TRY_HIP(hipMemsetAsync(s->ctr.p, 0, 16, s->stream));
+    }
+    if (c2[1]) {
+      hipLaunchKernelGGL(k_serde_fix, dim3(ceil_div((int64_t)c2[1], 64)), dim3(64), 0, s->stream, o.fix,
+                         (int64_t)c2[1], vb, o, q);
+      KHIP_TRY_HIP(hipGetLastError());
+      KHIP_TRY_HIP(hipMemcpyAsync(c2, s->ctr.p, 8, hipMemcpyDeviceToHost, s->stream));
+      KHIP_TRY_HIP(hipStreamSynchronize(s->stream));
+    }
+  }
+  if (n_errors) *n_errors = (int64_t)c2[0];
+  s->col_ptrs.assign(q.n_out, nullptr);
+  s->val_ptrs.assign(q.n_out, nullptr);
+  for (int c = 0; c < q.n_out; c++) {
+    s->col_ptrs[c] = s->cols[c].p;
+    s->val_ptrs[c] = s->cvalid[c].as<uint8_t>();
+  }
+  memset(out, 0, sizeof(*out));
+  out->n_rows = n;
+  out->mem = KHIP_MEM_DEVICE;
+  out->n_cols = q.n_out;
+  out->ts = ts;
+  out->key_valid = s->key_valid.as<uint8_t>();
+  out->row_valid = s->row_valid.as<uint8_t>();
+  if (q.key_format == KHIP_FMT_KAFKA && q.key_type == KHIP_TYPE_STRING) {
+    out->key_offsets = koff;
+    out->key_bytes = kb;
+  } else {
+    out->key_i64 = s->key_i64.as<int64_t>();
+  }
+  out->col_data = s->col_ptrs.data();
+  out->col_valid = s->val_ptrs.data();
+  return KHIP_OK;
+}
+
+khip_status khip_serde_destroy(khip_serde* s) {
+  if (!s) return KHIP_OK;
+  DeviceGuard g(s->device);
+  if (s->stream) hipStreamSynchronize(s->stream);
+  DevBuf* bufs[] = {&s->key_i64, &s->key_valid, &s->row_valid, &s->ctr, &s->fix, &s->st_ts, &s->st_koff,
+                    &s->st_kbytes, &s->st_kval, &s->st_voff, &s->st_vbytes, &s->st_vval};
+  for (DevBuf* b : bufs) b->release();
+  for (int c = 0; c < SD_MAX_FIELDS; c++) {
+    s->cols[c].release();
+    s->cvalid[c].release();
+  }
+  if (s->stream) hipStreamDestroy(s->stream);
+  delete s;
+  return KHIP_OK;
+}
+
+}  // extern "C"

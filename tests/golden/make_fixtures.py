@@ -336,6 +336,7 @@ def extract_agg(path, test, fmt_tag):
 
     topic = src["topic"]
     rows = []
+    raw_records = []
     for rec in test.get("inputs", []):
         if rec.get("topic") != topic:
             raise Skip("other input topic")
@@ -348,6 +349,7 @@ def extract_agg(path, test, fmt_tag):
             kval = None if rk is None else conv(gtype, rk)
         else:
             kval = None if val is None else val.get(gcol)
+        raw_records.append({"key": rk, "value": rec.get("value"), "ts": ts})
         row = {"key": kval, "row_valid": val is not None, "ts": ts, "cols": []}
         for c in used:
             v = None if val is None else val.get(c)
@@ -417,9 +419,19 @@ def extract_agg(path, test, fmt_tag):
     expected = [v for v in state.values() if v is not None]
     expected.sort(key=lambda e: ((e["key"].encode() if isinstance(e["key"], str) else e["key"]), e["ws"]))
 
+    # the serialized inputs (for the deserializer path): KAFKA key of the group column, the value
+    # in the source's format, every value column of the schema
+    raw = None
+    if by_key and src["format"] in ("JSON", "DELIMITED") and all(
+            c["type"] in ("INT32", "INT64", "DOUBLE", "STRING") for c in value_cols):
+        raw = {"format": src["format"], "key_type": gtype,
+               "fields": [{"name": c["name"], "type": c["type"],
+                           "out": used.index(c["name"]) if c["name"] in used else -1} for c in value_cols],
+               "records": raw_records}
     return {
         "name": test["name"] + (" [%s]" % fmt_tag if fmt_tag else ""),
         "source": "%s:%d" % (os.path.basename(path), find_line(path, test["name"])),
+        "raw": raw,
         "desc": {
             "window_kind": window["kind"] if window else "NONE",
             "size_ms": window["size_ms"] if window else 0,

@@ -1,0 +1,218 @@
+"""khip_serde_decode (KAFKA / DELIMITED / JSON record bytes → device columns) against the CPU
+restatement of ksqlDB's deserializers (tests/serde_ref.py), and end to end: the reference's own
+QTT inputs as raw record bytes → decode → aggregate → the reference's expected outputs."""
+import json
+import random
+import struct
+
+import numpy as np
+import pytest
+
+import qtt
+import serde_ref
+from ksql_amd import abi
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = [("ID", "INT64", -1), ("V32", "INT32", 0), ("V64", "INT64", 1), ("D", "DOUBLE", 2), ("NAME", "STRING", 3),
+          ("SKIPPED", "INT32", -1)]
+OUT_TYPES = ["INT32", "INT64", "DOUBLE", "STRING"]
+
+
+@pytest.fixture(scope="module")
+def prod():
+    return abi.load_product()
+
+
+def _num_text(rng, t):
+    r = rng.random()
+    if t == "DOUBLE":
+        if r < 0.3:
+            return repr(rng.uniform(-1e6, 1e6))
+        if r < 0.45:  # more than 19 significant digits (big-integer rounding path)
+            return str(rng.randrange(1, 10)) + "".join(str(rng.randrange(10)) for _ in range(rng.randrange(19, 30))) + \
+                "e" + str(rng.randrange(-320, 300))
+        if r < 0.55:
+            return rng.choice(["NaN", "Infinity", "-Infinity", " 1.5 ", "2.5e-310", "1e400", "7d", "abc", "1..2"])
+        return "%d.%d" % (rng.randrange(-10 ** 6, 10 ** 6), rng.randrange(1000))
+    bits = 32 if t == "INT32" else 64
+    if r < 0.7:
+        return str(rng.randrange(-(1 << (bits - 1)), 1 << (bits - 1)))
+    return rng.choice([str(1 << bits), "-0", "+5", " 3", "1.0", "x", "99999999999999999999"])
+
+
+def _delimited(rng):
+    parts = []
+    for name, t, _ in FIELDS:
+        if rng.random() < 0.08:
+            parts.append("")
+            continue
+        if t == "STRING":
+            s = rng.choice(["alice", "b,ob", 'q"uote', "", "x y"])
+            parts.append('"%s"' % s.replace('"', '""') if ("," in s or '"' in s or rng.random() < 0.2) else s)
+        else:
+            v = _num_text(rng, t)
+            parts.append('"%s"' % v if rng.random() < 0.1 else v)
+    if rng.random() < 0.03:
+        parts.append("extra")  # arity mismatch
+    if rng.random() < 0.03:
+        parts = parts[:-1]
+    line = ",".join(parts)
+    return (line + ("\n" if rng.random() < 0.05 else "")).encode()
+
+
+def _json(rng):
+    obj = []
+    for name, t, _ in FIELDS:
+        r = rng.random()
+        if r < 0.07:
+            continue  # missing
+        key = name if rng.random() < 0.7 else name.lower()
+        if r < 0.12:
+            val = "null"
+        elif t == "STRING":
+            val = json.dumps(rng.choice(["alice", "é", "a\"b"])) if rng.random() < 0.8 else rng.choice(["12", "true", "[1,2]"])
+        else:
+            k = rng.random()
+            if k < 0.5:
+                txt = _num_text(rng, t)
+                try:
+                    json.loads(txt)
+                    val = txt  # a JSON number token
+                except ValueError:
+                    val = json.dumps(txt)
+            elif k < 0.7:
+                val = json.dumps(_num_text(rng, t))  # numbers as strings
+            elif k < 0.8:
+                val = rng.choice(["true", "{\"a\":1}", "[1]"])
+            elif k < 0.9:
+                val = repr(rng.uniform(-3e9, 3e9))  # float token into an integer column
+            else:
+                val = str(rng.randrange(-(1 << 70), 1 << 70))  # BigInteger token
+        obj.append('"%s": %s' % (key, val))
+    if rng.random() < 0.1 and obj:
+        obj.append(obj[0])  # duplicate field: the last wins
+    body = "{" + ", ".join(obj) + "}"
+    if rng.random() < 0.03:
+        body = body[:-1]  # truncated
+    if rng.random() < 0.05:
+        body = "  " + body + "  trailing"
+    return body.encode()
+
+
+def _kafka_value(rng):
+    return struct.pack(">q", rng.randrange(-(1 << 63), 1 << 63)) if rng.random() < 0.95 else b"\x01\x02"
+
+
+def _records(rng, fmt, n):
+    keys, vals = [], []
+    for _ in range(n):
+        r = rng.random()
+        keys.append(None if r < 0.03 else (b"\x00\x01" if r < 0.05 else struct.pack(">q", rng.randrange(-1000, 1000))))
+        if rng.random() < 0.05:
+            vals.append(None)
+        elif fmt == "DELIMITED":
+            vals.append(_delimited(rng))
+        elif fmt == "JSON":
+            vals.append(_json(rng))
+        else:
+            vals.append(_kafka_value(rng))
+    return keys, vals
+
+
+def _check(got, exp, fields, out_types):
+    n = len(exp)
+    for i, (kv, key, rv, row) in enumerate(exp):
+        assert got["key_valid"][i] == kv, (i, kv)
+        assert got["row_valid"][i] == rv, i
+        if kv and key is not None and "key" in got:
+            assert got["key"][i] == key, i
+        if not rv or row is None:
+            continue
+        for name, t, c in fields:
+            if c < 0:
+                continue
+            v = row[name]
+            assert got["valid"][c][i] == (v is not None), (i, name, v)
+            if v is None or t == "STRING":
+                continue
+            g = got["cols"][c][i]
+            if t == "DOUBLE":
+                assert struct.pack("<d", g) == struct.pack("<d", v) or (np.isnan(g) and np.isnan(v)), (i, name, g, v)
+            else:
+                assert int(g) == v, (i, name, g, v)
+
+
+@pytest.mark.parametrize("fmt", ["DELIMITED", "JSON", "KAFKA"])
+def test_decode_vs_reference(prod, fmt):
+    rng = random.Random({"DELIMITED": 1, "JSON": 2, "KAFKA": 3}[fmt])
+    fields = FIELDS if fmt != "KAFKA" else [("V64", "INT64", 0)]
+    out_types = OUT_TYPES if fmt != "KAFKA" else ["INT64"]
+    sd = abi.SerdeHandle(prod, fmt, fields, key_type="INT64")
+    for n in (1, 63, 4000):
+        keys, vals = _records(rng, fmt, n)
+        ts = np.arange(n, dtype=np.int64)
+        d, nerr = sd.decode(ts, keys, vals)
+        exp, experr = serde_ref.decode(fmt, fields, "INT64", keys, vals)
+        assert nerr == experr
+        _check(sd.columns(d, out_types), exp, fields, out_types)
+    sd.close()
+
+
+def test_decode_string_keys_feed_aggregate(prod):
+    """UTF-8 keys straight from the records into the aggregate: COUNT(*) / SUM by card."""
+    rng = random.Random(9)
+    n = 5000
+    cards = ["4000%012d" % rng.randrange(300) for _ in range(n)]
+    amounts = [rng.randrange(-100, 100) for _ in range(n)]
+    vals = [("%d,%s" % (a, "x")).encode() for a in amounts]
+    sd = abi.SerdeHandle(prod, "DELIMITED", [("AMOUNT", "INT64", 0), ("TAG", "STRING", -1)], key_type="STRING")
+    ts = np.arange(n, dtype=np.int64) * 10
+    d, nerr = sd.decode(ts, [c.encode() for c in cards], vals)
+    assert nerr == 0
+    desc = abi.make_agg_desc(window_kind="TUMBLING", size_ms=20_000, key_type="UTF8", col_types=["INT64"],
+                             aggs=[("COUNT_STAR", -1), ("SUM", 0)])
+    g = abi.AggHandle(prod, desc)
+    g.push(d)
+    got = g.snapshot()
+    g.close()
+    o = abi.AggHandle(abi.load_oracle(), desc)
+    o.push(abi.HostBatch(ts, utf8_keys=cards, cols=[np.array(amounts, np.int64)]))
+    exp = o.snapshot()
+    o.close()
+    assert got["key"] == exp["key"]
+    assert np.array_equal(got["ws"], exp["ws"]) and np.array_equal(got["values"][1], exp["values"][1])
+    sd.close()
+
+
+# ---- QTT inputs as the raw record bytes the reference consumed
+
+RAW_CASES = [c for c in qtt.load_cases("agg") if c.get("raw")]
+
+
+@pytest.mark.parametrize("case", RAW_CASES, ids=["%s %s" % (c["source"], c["name"]) for c in RAW_CASES])
+def test_qtt_raw_records_end_to_end(prod, case):
+    """Serialized QTT inputs (DELIMITED / JSON values, KAFKA keys) → khip_serde_decode →
+    khip_agg_push (one record per push) → the reference's expected output sequence."""
+    raw = case["raw"]
+    fields = [(f["name"], f["type"], f["out"]) for f in raw["fields"]]
+    key_type = raw["key_type"]
+    sd = abi.SerdeHandle(prod, raw["format"], fields, key_type="STRING" if key_type == "STRING" else key_type)
+    h = abi.AggHandle(prod, qtt.case_desc(case))
+    rows = []
+    for rec in raw["records"]:
+        k = rec["key"]
+        if k is None:
+            kb = None
+        elif key_type == "STRING":
+            kb = k.encode()
+        else:
+            kb = struct.pack(">q" if key_type == "INT64" else ">i", int(k))
+        v = rec["value"]
+        vb = None if v is None else (v if isinstance(v, str) else json.dumps(v)).encode()
+        d, nerr = sd.decode(np.array([rec["ts"]], np.int64), [kb], [vb])
+        h.push(d)
+        rows += qtt._rows_of(h.changes())
+    h.close()
+    sd.close()
+    assert qtt.compare_outputs(case, rows) == []
