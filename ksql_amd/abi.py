@@ -811,7 +811,7 @@ def _hip_copy(dst, src_ptr, nbytes):
     if nbytes:
         # wrap the device pointer as a torch tensor via the CUDA array interface
         class _Dev:
-            __cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (int(src_ptr), True), "version": 2}
+            __cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (int(src_ptr), False), "version": 2}
         t[:nbytes].copy_(torch.as_tensor(_Dev(), device="cuda"))
     return KHIP_OK
 
