@@ -281,6 +281,38 @@ khip_status khip_agg_get(khip_agg* agg, const khip_pull* q, const khip_having* h
 khip_status khip_agg_changes_size(khip_agg* agg, int64_t* n_rows, int64_t* key_bytes);
 khip_status khip_agg_changes(khip_agg* agg, khip_snapshot* out, uint8_t* tombstone);
 
+/* ---- Table aggregation: CREATE TABLE .. AS SELECT .. FROM <TABLE> GROUP BY .. (KSPlanBuilder
+ * visitTableGroupBy + visitTableAggregate → S/TableGroupByBuilderBase.java:62-111,
+ * S/TableAggregateBuilder.java:54-108; Kafka Streams KTable.groupBy().aggregate(init, adder,
+ * subtractor), KTableAggregate).  Each source-table change (key k: old row → new row) undoes the
+ * old row from its group (KudafUndoAggregator, X/function/udaf/KudafUndoAggregator.java:29-55,
+ * TableUdaf.undo) and applies the new row to its group (KudafAggregator).  A group whose rows all
+ * left keeps its row (COUNT 0, Q/count.json "should count back to zero"); HAVING removes it.
+ * Only undoable aggregates are accepted: COUNT(*), COUNT, SUM, AVG (MIN/MAX on a table source is a
+ * KsqlException in the reference, E/structured/SchemaKGroupedTable.java:82-95 → KHIP_E_UNSUPPORTED).
+ * The handle is created with window_kind NONE and this flag; snapshots, pull queries and row counts
+ * work as for a stream aggregate. */
+#define KHIP_FLAG_TABLE_SOURCE 16
+
+/* The source table's PRIMARY KEY of each batch row (same memory kind as the batch). */
+typedef struct khip_table_src {
+  int32_t key_type;            /* KHIP_KEY_INT64 or KHIP_KEY_UTF8 (fixed by the first push)     */
+  int32_t reserved;
+  const int64_t* key_i64;
+  const int64_t* key_offsets;  /* UTF8: n_rows + 1 offsets into key_bytes                       */
+  const uint8_t* key_bytes;
+  const uint8_t* key_valid;    /* bitmap; a null PRIMARY KEY drops the record                   */
+} khip_table_src;
+
+/* Apply source-table changelog records in arrival order.  Batch rows: key = the row's GROUP BY
+ * value (key_valid 0 = NULL: the row joins no group, S/GroupByParamsFactory.java:92-100), row_valid
+ * 0 = tombstone (the key is deleted), ts = ROWTIME (< 0: dropped), value columns = the aggregate
+ * arguments.  Group row time = the largest ts of the records that added to or undid from it.
+ * stats: rows_accepted = source records applied, dropped_null_key = null PRIMARY KEY,
+ * windows_applied = aggregate updates (adds + undos). */
+khip_status khip_agg_push_table(khip_agg* agg, const khip_batch* batch, const khip_table_src* src,
+                                khip_batch_stats* stats);
+
 /* Count the rows that pass `having` entirely on the device (no copy-out).
  * having may be NULL (= total group count).  When `having` is the descriptor's own HAVING,
  * the count is the one the aggregate kernels maintain (returned without device work). */
@@ -328,7 +360,9 @@ khip_status khip_agg_destroy(khip_agg* agg);
 /* Table side: SourceBuilder.buildKTable (S/SourceBuilder.java:87-137) materializes
  * the latest non-null value per key; a null value deletes the key. */
 typedef struct khip_table_desc {
-  int32_t key_type;          /* KHIP_KEY_INT64                                        */
+  int32_t key_type;          /* KHIP_KEY_INT64, or KHIP_KEY_UTF8 (STRING keys: the batch's
+                                key_offsets/key_bytes, identity = byte equality; the
+                                stream batch probing it carries STRING keys too)      */
   int32_t n_cols;
   const int32_t* col_types;  /* KHIP_TYPE_* per table value column (VARCHAR columns are
                                 dictionary codes, KHIP_TYPE_INT32)                    */

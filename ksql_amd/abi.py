@@ -34,6 +34,7 @@ FLAG_PROFILE = 1
 FLAG_ENGINE_ATOMIC = 2
 FLAG_PART_CLAIM = 4
 FLAG_CHANGELOG = 8
+FLAG_TABLE_SOURCE = 16
 RETENTION_DEFAULT = -1
 EMIT = {"CHANGES": 0, "FINAL": 1}
 NP_TYPE = {0: np.int32, 1: np.int64, 2: np.float64}
@@ -105,6 +106,12 @@ class KernelTimes(C.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+class TableSrc(C.Structure):
+    """khip_table_src: the source table's PRIMARY KEY per batch row (table aggregation)."""
+    _fields_ = [("key_type", i32), ("reserved", i32), ("key_i64", C.c_void_p), ("key_offsets", C.c_void_p),
+                ("key_bytes", C.c_void_p), ("key_valid", C.c_void_p)]
+
+
 class JoinDevOut(C.Structure):
     _fields_ = [("emit", C.c_void_p), ("matched", C.c_void_p), ("col_data", C.POINTER(C.c_void_p)),
                 ("col_null", C.POINTER(C.c_void_p))]
@@ -141,6 +148,7 @@ _P = C.c_void_p
 SIGS = {
     "agg_create": ([C.POINTER(AggDesc), C.POINTER(_P)]),
     "agg_push": ([_P, C.POINTER(Batch), C.POINTER(BatchStats)]),
+    "agg_push_table": ([_P, C.POINTER(Batch), C.POINTER(TableSrc), C.POINTER(BatchStats)]),
     "agg_snapshot_size": ([_P, C.POINTER(i64), C.POINTER(i64)]),
     "agg_snapshot": ([_P, C.POINTER(Having), C.POINTER(Snapshot)]),
     "agg_destroy": ([_P]),
@@ -371,6 +379,34 @@ class AggHandle:
                                          C.byref(st) if stats else None), "agg_push")
         return st.as_dict() if stats else None
 
+    def push_table(self, batch, src_keys=None, src_utf8_keys=None, src_key_valid=None, stats=True):
+        """khip_agg_push_table (handle created with FLAG_TABLE_SOURCE): `batch` holds the rows'
+        GROUP BY keys / tombstones / ts / argument columns, src_* the source PRIMARY KEY of each row
+        (host memory, like `batch`)."""
+        n = batch.struct.n_rows
+        keep = []
+        if src_utf8_keys is not None:
+            enc = [b"" if k is None else (k.encode() if isinstance(k, str) else bytes(k)) for k in src_utf8_keys]
+            off = np.zeros(n + 1, dtype=np.int64)
+            off[1:] = np.cumsum([len(e) for e in enc])
+            kb = np.frombuffer(b"".join(enc) + b"\0", dtype=np.uint8).copy()
+            keep += [off, kb]
+            src = TableSrc(KEY["UTF8"], 0, None, off.ctypes.data, kb.ctypes.data, None)
+            if src_key_valid is None:
+                src_key_valid = [k is not None for k in src_utf8_keys]
+        else:
+            k = np.ascontiguousarray(src_keys, dtype=np.int64)
+            keep.append(k)
+            src = TableSrc(KEY["INT64"], 0, k.ctypes.data, None, None, None)
+        bm = None if src_key_valid is None else bitmap(src_key_valid)
+        if bm is not None:
+            keep.append(bm)
+            src.key_valid = bm.ctypes.data
+        st = BatchStats()
+        self.lib.check(self.lib.agg_push_table(self.h, C.byref(batch.struct), C.byref(src),
+                                               C.byref(st) if stats else None), "agg_push_table")
+        return st.as_dict() if stats else None
+
     def snapshot(self, having=None, raw_keys=False):
         """raw_keys: UTF8 keys as the columnar (key_offsets, key_bytes) arrays instead of a list of
         str (for tables of tens of millions of rows)."""
@@ -558,12 +594,12 @@ class ShardedOracleAgg(AggHandle):
 
 
 class TableHandle:
-    def __init__(self, lib, col_types, device=0, capacity_hint=0):
+    def __init__(self, lib, col_types, device=0, capacity_hint=0, key_type="INT64"):
         self.lib = lib
         self.col_types = [TYPE[t] if isinstance(t, str) else t for t in col_types]
         ct = (i32 * max(len(col_types), 1))(*self.col_types)
         self._ct = ct
-        self.desc = TableDesc(KEY["INT64"], len(col_types), ct, device, 0, capacity_hint)
+        self.desc = TableDesc(KEY[key_type], len(col_types), ct, device, 0, capacity_hint)
         self.h = C.c_void_p()
         lib.check(lib.table_create(C.byref(self.desc), C.byref(self.h)), "table_create")
 

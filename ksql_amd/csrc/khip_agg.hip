@@ -417,7 +417,7 @@ __global__ __launch_bounds__(256) void k_dict_lookup(uint64_t* __restrict__ dwor
                                                      int64_t* __restrict__ kid, int64_t* __restrict__ khash,
                                                      int* __restrict__ fail) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (!(bit_get(kv, i) && bit_get(rv, i) && ts[i] >= 0)) {
+    if (!(bit_get(kv, i) && bit_get(rv, i) && (ts == nullptr || ts[i] >= 0))) {
       kid[i] = 0;
       khash[i] = 0;
       continue;
@@ -624,6 +624,95 @@ static int grid_for(int64_t work, int per_block, int cap_blocks = 2048 * 8) {
   return (int)std::min<int64_t>(g, cap_blocks);
 }
 
+// ---- KeyDict (khip_dict.hpp)
+
+static khip_status dict_grow(KeyDict& d, hipStream_t s, int64_t new_cap) {
+  DevBuf nw, nk;
+  KHIP_TRY(nw.ensure((size_t)new_cap * 8));
+  KHIP_TRY(nk.ensure((size_t)new_cap * 8));
+  KHIP_TRY_HIP(hipMemsetAsync(nw.p, 0, (size_t)new_cap * 8, s));
+  if (d.dcap > 0 && d.docc > 0) {
+    hipLaunchKernelGGL(k_dict_rehash, dim3(grid_for(d.dcap, 256)), dim3(256), 0, s, d.dword.as<uint64_t>(),
+                       d.dkid.as<int64_t>(), d.dcap, nw.as<uint64_t>(), nk.as<int64_t>(), (uint64_t)(new_cap - 1),
+                       d.arena.as<uint8_t>());
+    KHIP_TRY_HIP(hipGetLastError());
+  }
+  KHIP_TRY_HIP(hipStreamSynchronize(s));
+  d.dword.release();
+  d.dkid.release();
+  d.dword = nw;
+  d.dkid = nk;
+  nw.p = nk.p = nullptr;
+  d.dcap = new_cap;
+  return KHIP_OK;
+}
+
+khip_status dict_init(KeyDict& d, hipStream_t s) {
+  KHIP_TRY(d.fail.ensure(8));
+  return dict_grow(d, s, 4096);
+}
+
+khip_status dict_map(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8_t* kbytes, int64_t key_bytes_total,
+                     const uint8_t* kv, const uint8_t* rv, const int64_t* ts, int64_t n, int64_t* kid, int64_t* khash) {
+  if (2 * (d.docc + n) > d.dcap) KHIP_TRY(dict_grow(d, s, next_pow2(4 * (d.docc + n))));
+  const int64_t need = d.arena_used + key_bytes_total + 16 * n + 16;
+  if ((size_t)need > d.arena.bytes) {
+    DevBuf na;
+    KHIP_TRY(na.ensure((size_t)std::max<int64_t>(need * 2, 1 << 20)));
+    if (d.arena_used) KHIP_TRY_HIP(hipMemcpyAsync(na.p, d.arena.p, d.arena_used, hipMemcpyDeviceToDevice, s));
+    KHIP_TRY_HIP(hipStreamSynchronize(s));
+    d.arena.release();
+    d.arena = na;
+    na.p = nullptr;
+  }
+  KHIP_TRY_HIP(hipMemsetAsync(d.fail.p, 0, 4, s));
+  hipLaunchKernelGGL(k_dict_lookup, dim3(grid_for(n, 256)), dim3(256), 0, s, d.dword.as<uint64_t>(),
+                     d.dkid.as<int64_t>(), (uint64_t)(d.dcap - 1), d.arena.as<uint8_t>(), koff, kbytes, kv, rv, ts, n,
+                     kid, khash, d.fail.as<int>());
+  const int64_t dnb = ceil_div(d.dcap, 256);
+  KHIP_TRY(d.bsum.ensure((dnb + 1) * 8));
+  hipLaunchKernelGGL(k_dict_count, dim3(dnb), dim3(256), 0, s, d.dword.as<uint64_t>(), d.dcap, koff,
+                     d.bsum.as<int64_t>());
+  int64_t* dtotal = d.bsum.as<int64_t>() + dnb;
+  KHIP_TRY_HIP(hipMemsetAsync(dtotal, 0, 8, s));
+  hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, d.bsum.as<int64_t>(), dnb, dtotal);
+  hipLaunchKernelGGL(k_dict_write, dim3(dnb), dim3(256), 0, s, d.dword.as<uint64_t>(), d.dkid.as<int64_t>(), d.dcap,
+                     d.bsum.as<int64_t>(), d.arena_used, d.arena.as<uint8_t>(), koff, kbytes, khash);
+  hipLaunchKernelGGL(k_kid_fixup, dim3(grid_for(n, 256)), dim3(256), 0, s, kid, n, d.dkid.as<int64_t>());
+  KHIP_TRY_HIP(hipGetLastError());
+  int64_t added = 0;
+  int failed = 0;
+  KHIP_TRY_HIP(hipMemcpyAsync(&added, dtotal, 8, hipMemcpyDeviceToHost, s));
+  KHIP_TRY_HIP(hipMemcpyAsync(&failed, d.fail.p, 4, hipMemcpyDeviceToHost, s));
+  KHIP_TRY_HIP(hipStreamSynchronize(s));
+  if (failed) return fail(KHIP_E_DEVICE, "key dictionary probe budget exhausted");
+  d.arena_used += added;
+  // occupancy over-estimated (every entry takes >= 16 arena bytes): growth is decided conservatively
+  d.docc = std::min<int64_t>(d.dcap, d.docc + std::min<int64_t>(n, added / 16));
+  return KHIP_OK;
+}
+
+khip_status dict_find(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8_t* kbytes, int64_t n, int64_t* kid) {
+  if (n <= 0) return KHIP_OK;
+  hipLaunchKernelGGL(k_dict_find, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, d.dword.as<uint64_t>(),
+                     d.dkid.as<int64_t>(), (uint64_t)(d.dcap - 1), d.arena.as<uint8_t>(), koff, kbytes, n, kid);
+  KHIP_TRY_HIP(hipGetLastError());
+  return KHIP_OK;
+}
+
+khip_status dict_clear(KeyDict& d, hipStream_t s) {
+  if (d.dcap) KHIP_TRY_HIP(hipMemsetAsync(d.dword.p, 0, d.dcap * 8, s));
+  d.docc = 0;
+  d.arena_used = 0;
+  return KHIP_OK;
+}
+
+void dict_release(KeyDict& d) {
+  DevBuf* bufs[] = {&d.dword, &d.dkid, &d.arena, &d.bsum, &d.fail};
+  for (DevBuf* b : bufs) b->release();
+  d.dcap = d.docc = d.arena_used = 0;
+}
+
 }  // namespace khip
 
 using namespace khip;
@@ -705,13 +794,13 @@ static khip_status init_table(khip_agg* a, DevBuf& buf, int64_t cap) {
   return KHIP_OK;
 }
 
-static khip_status grow_table(khip_agg* a, int64_t new_cap) {
+khip_status khip::agg_grow_table(khip_agg* a, int64_t new_cap) {
   DevBuf nt;
   KHIP_TRY(init_table(a, nt, new_cap));
   if (a->cap > 0 && a->occ > 0) {
     hipLaunchKernelGGL(k_rehash, dim3(grid_for(a->cap, 256)), dim3(256), 0, a->stream, a->table.as<uint64_t>(),
                        a->cap, nt.as<uint64_t>(), (uint64_t)(new_cap - 1), a->sw,
-                       a->desc.key_type == KHIP_KEY_UTF8 ? 1 : 0, a->arena.as<uint8_t>());
+                       a->desc.key_type == KHIP_KEY_UTF8 ? 1 : 0, a->dict.arena.as<uint8_t>());
     KHIP_TRY_HIP(hipGetLastError());
   }
   KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
@@ -723,26 +812,7 @@ static khip_status grow_table(khip_agg* a, int64_t new_cap) {
   return KHIP_OK;
 }
 
-static khip_status grow_dict(khip_agg* a, int64_t new_cap) {
-  DevBuf nw, nk;
-  KHIP_TRY(nw.ensure((size_t)new_cap * 8));
-  KHIP_TRY(nk.ensure((size_t)new_cap * 8));
-  KHIP_TRY_HIP(hipMemsetAsync(nw.p, 0, (size_t)new_cap * 8, a->stream));
-  if (a->dcap > 0 && a->docc > 0) {
-    hipLaunchKernelGGL(k_dict_rehash, dim3(grid_for(a->dcap, 256)), dim3(256), 0, a->stream, a->dword.as<uint64_t>(),
-                       a->dkid.as<int64_t>(), a->dcap, nw.as<uint64_t>(), nk.as<int64_t>(),
-                       (uint64_t)(new_cap - 1), a->arena.as<uint8_t>());
-    KHIP_TRY_HIP(hipGetLastError());
-  }
-  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
-  a->dword.release();
-  a->dkid.release();
-  a->dword = nw;
-  a->dkid = nk;
-  nw.p = nk.p = nullptr;
-  a->dcap = new_cap;
-  return KHIP_OK;
-}
+static khip_status grow_table(khip_agg* a, int64_t new_cap) { return agg_grow_table(a, new_cap); }
 
 namespace khip {
 
@@ -848,6 +918,13 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
       return fail(KHIP_E_INVALID, "aggregate argument column");
   }
   if (d.emit != KHIP_EMIT_CHANGES && d.emit != KHIP_EMIT_FINAL) return fail(KHIP_E_INVALID, "emit strategy");
+  if (d.flags & KHIP_FLAG_TABLE_SOURCE) {  // table aggregation: undoable aggregates, no windows
+    if (d.window_kind != KHIP_WINDOW_NONE) return fail(KHIP_E_UNSUPPORTED, "windowed aggregation of a table source");
+    for (int i = 0; i < d.n_aggs; i++)
+      if (d.aggs[i].kind == KHIP_AGG_MIN || d.aggs[i].kind == KHIP_AGG_MAX)  // E/structured/SchemaKGroupedTable.java:82-95
+        return fail(KHIP_E_UNSUPPORTED, "MIN/MAX cannot be applied to a table source, only to a stream source");
+    if (d.flags & KHIP_FLAG_CHANGELOG) return fail(KHIP_E_UNSUPPORTED, "changelog of a table-source aggregation");
+  }
   if (d.emit == KHIP_EMIT_FINAL && d.window_kind == KHIP_WINDOW_NONE)
     return fail(KHIP_E_INVALID, "EMIT FINAL needs a windowed aggregation");
   if (d.window_kind != KHIP_WINDOW_NONE && d.retention_ms != KHIP_RETENTION_DEFAULT) {
@@ -893,7 +970,9 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
     return fail(KHIP_E_DEVICE, "hipStreamCreate failed (no device?)");
   }
   a->profile = (d.flags & KHIP_FLAG_PROFILE) != 0;
-  a->engine = d.window_kind == KHIP_WINDOW_SESSION ? 2 : ((d.flags & KHIP_FLAG_ENGINE_ATOMIC) ? 1 : 0);
+  a->engine = d.window_kind == KHIP_WINDOW_SESSION ? 2
+              : (d.flags & KHIP_FLAG_TABLE_SOURCE) ? 3
+              : ((d.flags & KHIP_FLAG_ENGINE_ATOMIC) ? 1 : 0);
   a->changelog = (d.flags & KHIP_FLAG_CHANGELOG) != 0 && d.emit == KHIP_EMIT_CHANGES;
   if (a->windowed)
     a->retention = d.retention_ms == KHIP_RETENTION_DEFAULT ? a->desc.size_ms + a->grace : d.retention_ms;
@@ -903,7 +982,7 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
   }
   if (a->profile)
     for (int e = 0; e < 8; e++) hipEventCreate(&a->ev[e]);
-  int64_t cap = a->engine == 1 ? next_pow2(std::max<int64_t>(1024, d.capacity_hint > 0 ? d.capacity_hint * 2 : 1 << 16))
+  int64_t cap = (a->engine == 1 || a->engine == 3) ? next_pow2(std::max<int64_t>(1024, d.capacity_hint > 0 ? d.capacity_hint * 2 : 1 << 16))
                                 : 1024;
   if ((st = init_table(a, a->table, cap)) != KHIP_OK || (st = a->stream_time.ensure(8)) != KHIP_OK ||
       (st = a->counters.ensure(8 * NPART)) != KHIP_OK ||
@@ -915,7 +994,7 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
   int64_t m1 = -1;
   hipMemcpyAsync(a->stream_time.p, &m1, 8, hipMemcpyHostToDevice, a->stream);
   if (d.key_type == KHIP_KEY_UTF8) {
-    if ((st = grow_dict(a, 4096)) != KHIP_OK || (st = a->dict_fail.ensure(8)) != KHIP_OK) {
+    if ((st = dict_init(a->dict, a->stream)) != KHIP_OK) {
       khip_agg_destroy(a);
       return st;
     }
@@ -934,33 +1013,13 @@ static khip_status stage(khip_agg* a, DevBuf& buf, const void* src, size_t bytes
   return KHIP_OK;
 }
 
-khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* stats) {
-  clear_error();
-  if (!a || !b) return fail(KHIP_E_INVALID, "null argument");
-  if (b->n_rows < 0 || b->n_cols < a->desc.n_cols) return fail(KHIP_E_INVALID, "batch shape");
-  if (b->n_rows >= (1LL << 36)) return fail(KHIP_E_UNSUPPORTED, "batch larger than 2^36 rows");
+// The batch's device pointers: host batches are staged into the handle's buffers (asynchronously,
+// on its stream); UTF8 key byte totals of device batches are fetched (synchronise before use).
+static khip_status resolve_batch(khip_agg* a, const khip_batch* b, const int64_t** keys_o, const int64_t** ts_o,
+                                 const uint8_t** kv_o, const uint8_t** rv_o, const int64_t** koff_o,
+                                 const uint8_t** kbytes_o, ColPtrs* cols_o, int64_t* key_bytes_total_o) {
   const int64_t n = b->n_rows;
   const bool utf8 = a->desc.key_type == KHIP_KEY_UTF8;
-  if (!b->ts || (utf8 ? (!b->key_offsets || !b->key_bytes) : !b->key_i64))
-    if (n > 0) return fail(KHIP_E_INVALID, "missing key or timestamp column");
-  for (int c = 0; c < a->desc.n_cols; c++)
-    if (n > 0 && (!b->col_data || !b->col_data[c])) return fail(KHIP_E_INVALID, "missing value column");
-  DeviceGuard g(a->device);
-  khip_batch_stats s{};
-  s.rows_in = n;
-  a->st_before = a->host_stream_time;
-  a->chg_ready = false;
-  a->lost.clear();
-  if (n == 0) {  // nothing changes, nothing closes
-    a->chg_ready = true;
-    a->chg_n = 0;
-    s.stream_time = a->host_stream_time;
-    if (stats) *stats = s;
-    return KHIP_OK;
-  }
-  if (a->changelog && n >= (1LL << 31)) return fail(KHIP_E_UNSUPPORTED, "changelog pushes above 2^31 rows");
-  const bool final_emit = a->desc.emit == KHIP_EMIT_FINAL;
-  // ---- device pointers (stage host batches)
   const int64_t* keys = b->key_i64;
   const int64_t* ts = b->ts;
   const uint8_t* kv = b->key_valid;
@@ -1005,52 +1064,154 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   } else {
     return fail(KHIP_E_INVALID, "batch mem");
   }
+  *keys_o = keys;
+  *ts_o = ts;
+  *kv_o = kv;
+  *rv_o = rv;
+  *koff_o = koff;
+  *kbytes_o = kbytes;
+  *cols_o = cols;
+  *key_bytes_total_o = key_bytes_total;
+  return KHIP_OK;
+}
+
+khip_status khip_agg_push_table(khip_agg* a, const khip_batch* b, const khip_table_src* src,
+                                khip_batch_stats* stats) {
+  clear_error();
+  if (!a || !b || !src) return fail(KHIP_E_INVALID, "null argument");
+  if (a->engine != 3) return fail(KHIP_E_STATE, "handle not created with KHIP_FLAG_TABLE_SOURCE");
+  if (b->n_rows < 0 || b->n_cols < a->desc.n_cols) return fail(KHIP_E_INVALID, "batch shape");
+  if (src->key_type != KHIP_KEY_INT64 && src->key_type != KHIP_KEY_UTF8) return fail(KHIP_E_INVALID, "source key type");
+  TaggState& T = a->tagg;
+  if (T.key_type >= 0 && T.key_type != src->key_type) return fail(KHIP_E_INVALID, "source key type changed");
+  const int64_t n = b->n_rows;
+  const bool utf8 = a->desc.key_type == KHIP_KEY_UTF8, src_utf8 = src->key_type == KHIP_KEY_UTF8;
+  if (n > 0) {
+    if (!b->ts || (utf8 ? (!b->key_offsets || !b->key_bytes) : !b->key_i64))
+      return fail(KHIP_E_INVALID, "missing GROUP BY key or timestamp column");
+    if (src_utf8 ? (!src->key_offsets || !src->key_bytes) : !src->key_i64)
+      return fail(KHIP_E_INVALID, "missing source PRIMARY KEY column");
+    for (int c = 0; c < a->desc.n_cols; c++)
+      if (!b->col_data || !b->col_data[c]) return fail(KHIP_E_INVALID, "missing value column");
+  }
+  DeviceGuard g(a->device);
+  if (T.key_type < 0) {
+    if (src_utf8) KHIP_TRY(dict_init(T.dict, a->stream));
+    T.key_type = src->key_type;
+  }
+  khip_batch_stats s{};
+  s.rows_in = n;
+  a->chg_ready = false;
+  if (n == 0) {
+    s.stream_time = a->host_stream_time;
+    if (stats) *stats = s;
+    return KHIP_OK;
+  }
+  const int64_t* keys;
+  const int64_t* ts;
+  const uint8_t *kv, *rv;
+  const int64_t* koff;
+  const uint8_t* kbytes;
+  ColPtrs cols{};
+  int64_t key_bytes_total = 0;
+  KHIP_TRY(resolve_batch(a, b, &keys, &ts, &kv, &rv, &koff, &kbytes, &cols, &key_bytes_total));
+  // the source PRIMARY KEYs on the device
+  const int64_t* sk = src->key_i64;
+  const int64_t* skoff = src->key_offsets;
+  const uint8_t* skb = src->key_bytes;
+  const uint8_t* skv = src->key_valid;
+  int64_t src_bytes = 0;
+  if (b->mem == KHIP_MEM_HOST) {
+    const size_t bm = (size_t)(n + 7) / 8;
+    if (skv) { KHIP_TRY(stage(a, T.st_kv, skv, bm)); skv = T.st_kv.as<uint8_t>(); }
+    if (src_utf8) {
+      src_bytes = src->key_offsets[n];
+      KHIP_TRY(stage(a, T.st_koff, src->key_offsets, (n + 1) * 8));
+      KHIP_TRY(stage(a, T.st_kbytes, src->key_bytes, (size_t)std::max<int64_t>(src_bytes, 1)));
+      skoff = T.st_koff.as<int64_t>();
+      skb = T.st_kbytes.as<uint8_t>();
+    } else {
+      KHIP_TRY(stage(a, T.st_key, src->key_i64, n * 8));
+      sk = T.st_key.as<int64_t>();
+    }
+  } else if (src_utf8) {
+    KHIP_TRY_HIP(hipMemcpyAsync(&src_bytes, skoff + n, 8, hipMemcpyDeviceToHost, a->stream));
+  }
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));  // key byte totals of device batches
+  // GROUP BY keys → ids (UTF8: the group dictionary; rows that cannot add to a group are skipped)
+  const int64_t* hkeys = keys;
+  if (utf8) {
+    KHIP_TRY(a->kid.ensure(n * 8));
+    KHIP_TRY(a->khash.ensure(n * 8));
+    KHIP_TRY(dict_map(a->dict, a->stream, koff, kbytes, key_bytes_total, kv, rv, ts, n, a->kid.as<int64_t>(),
+                      a->khash.as<int64_t>()));
+    keys = a->kid.as<int64_t>();
+    hkeys = a->khash.as<int64_t>();
+  }
+  if (src_utf8) {
+    KHIP_TRY(T.sid.ensure(n * 8));
+    KHIP_TRY(T.shash.ensure(n * 8));
+    KHIP_TRY(dict_map(T.dict, a->stream, skoff, skb, src_bytes, skv, nullptr, ts, n, T.sid.as<int64_t>(),
+                      T.shash.as<int64_t>()));
+    sk = T.sid.as<int64_t>();
+  }
+  int64_t tot[NPART] = {0};
+  KHIP_TRY(tagg_push(a, n, keys, hkeys, kv, rv, ts, cols, sk, skv, tot));
+  s.rows_accepted = tot[P_ACCEPTED];
+  s.dropped_null_key = tot[P_NULL_KEY];
+  s.dropped_bad_ts = tot[P_BAD_TS];
+  s.windows_applied = tot[P_APPLIED];
+  s.stream_time = a->host_stream_time;
+  if (stats) *stats = s;
+  return KHIP_OK;
+}
+
+khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* stats) {
+  clear_error();
+  if (!a || !b) return fail(KHIP_E_INVALID, "null argument");
+  if (b->n_rows < 0 || b->n_cols < a->desc.n_cols) return fail(KHIP_E_INVALID, "batch shape");
+  if (b->n_rows >= (1LL << 36)) return fail(KHIP_E_UNSUPPORTED, "batch larger than 2^36 rows");
+  if (a->engine == 3) return fail(KHIP_E_STATE, "table-source aggregation: use khip_agg_push_table");
+  const int64_t n = b->n_rows;
+  const bool utf8 = a->desc.key_type == KHIP_KEY_UTF8;
+  if (!b->ts || (utf8 ? (!b->key_offsets || !b->key_bytes) : !b->key_i64))
+    if (n > 0) return fail(KHIP_E_INVALID, "missing key or timestamp column");
+  for (int c = 0; c < a->desc.n_cols; c++)
+    if (n > 0 && (!b->col_data || !b->col_data[c])) return fail(KHIP_E_INVALID, "missing value column");
+  DeviceGuard g(a->device);
+  khip_batch_stats s{};
+  s.rows_in = n;
+  a->st_before = a->host_stream_time;
+  a->chg_ready = false;
+  a->lost.clear();
+  if (n == 0) {  // nothing changes, nothing closes
+    a->chg_ready = true;
+    a->chg_n = 0;
+    s.stream_time = a->host_stream_time;
+    if (stats) *stats = s;
+    return KHIP_OK;
+  }
+  if (a->changelog && n >= (1LL << 31)) return fail(KHIP_E_UNSUPPORTED, "changelog pushes above 2^31 rows");
+  const bool final_emit = a->desc.emit == KHIP_EMIT_FINAL;
+  // ---- device pointers (stage host batches)
+  const int64_t* keys;
+  const int64_t* ts;
+  const uint8_t *kv, *rv;
+  const int64_t* koff;
+  const uint8_t* kbytes;
+  ColPtrs cols{};
+  int64_t key_bytes_total = 0;
+  KHIP_TRY(resolve_batch(a, b, &keys, &ts, &kv, &rv, &koff, &kbytes, &cols, &key_bytes_total));
   if (final_emit) KHIP_TRY(emit_final_lost(a, ts, kv, rv, n, 0, nullptr));
   // ---- UTF8 keys → stable key ids
   const int64_t* hkeys = keys;
   if (utf8) {
     KHIP_TRY_HIP(hipStreamSynchronize(a->stream));  // key_bytes_total for device batches
     ev_record(a, 1);
-    if (2 * (a->docc + n) > a->dcap) KHIP_TRY(grow_dict(a, next_pow2(4 * (a->docc + n))));
     KHIP_TRY(a->kid.ensure(n * 8));
     KHIP_TRY(a->khash.ensure(n * 8));
-    const int64_t need = a->arena_used + key_bytes_total + 16 * n + 16;
-    if ((size_t)need > a->arena.bytes) {
-      DevBuf na;
-      KHIP_TRY(na.ensure((size_t)std::max<int64_t>(need * 2, 1 << 20)));
-      if (a->arena_used) KHIP_TRY_HIP(hipMemcpyAsync(na.p, a->arena.p, a->arena_used, hipMemcpyDeviceToDevice, a->stream));
-      KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
-      a->arena.release();
-      a->arena = na;
-      na.p = nullptr;
-    }
-    KHIP_TRY_HIP(hipMemsetAsync(a->dict_fail.p, 0, 4, a->stream));
-    hipLaunchKernelGGL(k_dict_lookup, dim3(grid_for(n, 256)), dim3(256), 0, a->stream, a->dword.as<uint64_t>(),
-                       a->dkid.as<int64_t>(), (uint64_t)(a->dcap - 1), a->arena.as<uint8_t>(), koff, kbytes, kv,
-                       rv, ts, n, a->kid.as<int64_t>(), a->khash.as<int64_t>(), a->dict_fail.as<int>());
-    const int64_t dnb = ceil_div(a->dcap, 256);
-    KHIP_TRY(a->dict_bsum.ensure((dnb + 1) * 8));
-    hipLaunchKernelGGL(k_dict_count, dim3(dnb), dim3(256), 0, a->stream, a->dword.as<uint64_t>(), a->dcap, koff,
-                       a->dict_bsum.as<int64_t>());
-    int64_t* dtotal = a->dict_bsum.as<int64_t>() + dnb;
-    KHIP_TRY_HIP(hipMemsetAsync(dtotal, 0, 8, a->stream));
-    hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, a->stream, a->dict_bsum.as<int64_t>(), dnb, dtotal);
-    hipLaunchKernelGGL(k_dict_write, dim3(dnb), dim3(256), 0, a->stream, a->dword.as<uint64_t>(), a->dkid.as<int64_t>(),
-                       a->dcap, a->dict_bsum.as<int64_t>(), a->arena_used, a->arena.as<uint8_t>(), koff, kbytes,
-                       a->khash.as<int64_t>());
-    hipLaunchKernelGGL(k_kid_fixup, dim3(grid_for(n, 256)), dim3(256), 0, a->stream, a->kid.as<int64_t>(), n,
-                       a->dkid.as<int64_t>());
-    KHIP_TRY_HIP(hipGetLastError());
-    int64_t added = 0;
-    int failed = 0;
-    KHIP_TRY_HIP(hipMemcpyAsync(&added, dtotal, 8, hipMemcpyDeviceToHost, a->stream));
-    KHIP_TRY_HIP(hipMemcpyAsync(&failed, a->dict_fail.p, 4, hipMemcpyDeviceToHost, a->stream));
-    KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
-    if (failed) return fail(KHIP_E_DEVICE, "key dictionary probe budget exhausted");
-    a->arena_used += added;
-    // dictionary occupancy, over-estimated (every entry takes >= 16 arena bytes): growth is
-    // decided conservatively
-    a->docc = std::min<int64_t>(a->dcap, a->docc + std::min<int64_t>(n, added / 16));
+    KHIP_TRY(dict_map(a->dict, a->stream, koff, kbytes, key_bytes_total, kv, rv, ts, n, a->kid.as<int64_t>(),
+                      a->khash.as<int64_t>()));
     keys = a->kid.as<int64_t>();
     hkeys = a->khash.as<int64_t>();
     ev_record(a, 2);
@@ -1249,8 +1410,8 @@ khip_status khip_agg_snapshot_size(khip_agg* a, int64_t* n_rows, int64_t* key_by
       std::vector<uint64_t> rows;
       int64_t n = 0;
       KHIP_TRY(compact_rows(a, nullptr, &rows, &n));
-      std::vector<uint8_t> arena(a->arena_used);
-      if (a->arena_used) KHIP_TRY_HIP(hipMemcpy(arena.data(), a->arena.p, a->arena_used, hipMemcpyDeviceToHost));
+      std::vector<uint8_t> arena(a->dict.arena_used);
+      if (a->dict.arena_used) KHIP_TRY_HIP(hipMemcpy(arena.data(), a->dict.arena.p, a->dict.arena_used, hipMemcpyDeviceToHost));
       int64_t kb = 0;
       for (int64_t r = 0; r < n; r++) kb += *(const int64_t*)(arena.data() + rows[r * a->sw] + 8);
       *key_bytes = kb;
@@ -1269,8 +1430,8 @@ static khip_status emit_snapshot(khip_agg* a, const std::vector<uint64_t>& rows,
   const bool utf8 = a->desc.key_type == KHIP_KEY_UTF8;
   std::vector<uint8_t> arena;
   if (utf8) {
-    arena.resize(a->arena_used);
-    if (a->arena_used) KHIP_TRY_HIP(hipMemcpy(arena.data(), a->arena.p, a->arena_used, hipMemcpyDeviceToHost));
+    arena.resize(a->dict.arena_used);
+    if (a->dict.arena_used) KHIP_TRY_HIP(hipMemcpy(arena.data(), a->dict.arena.p, a->dict.arena_used, hipMemcpyDeviceToHost));
   }
   auto kptr = [&](int64_t kid) { return arena.data() + kid + 16; };
   auto klen = [&](int64_t kid) { return *(const int64_t*)(arena.data() + kid + 8); };
@@ -1387,17 +1548,14 @@ khip_status khip_agg_get(khip_agg* a, const khip_pull* q, const khip_having* h, 
     // key bytes → dictionary ids on the device (read-only probe); unseen keys match nothing
     const int64_t nk = q->n_keys, nb = q->key_offsets[nk];
     k.assign((size_t)nk, -1);
-    if (a->docc > 0 && a->dcap > 0) {
+    if (a->dict.docc > 0) {
       DevBuf doff, dbytes, dkid;
       KHIP_TRY(doff.ensure((size_t)(nk + 1) * 8));
       KHIP_TRY(dbytes.ensure((size_t)std::max<int64_t>(nb, 1)));
       KHIP_TRY(dkid.ensure((size_t)nk * 8));
       KHIP_TRY_HIP(hipMemcpyAsync(doff.p, q->key_offsets, (size_t)(nk + 1) * 8, hipMemcpyHostToDevice, a->stream));
       if (nb) KHIP_TRY_HIP(hipMemcpyAsync(dbytes.p, q->key_bytes, (size_t)nb, hipMemcpyHostToDevice, a->stream));
-      hipLaunchKernelGGL(k_dict_find, dim3(grid_for(nk, 256, 4096)), dim3(256), 0, a->stream, a->dword.as<uint64_t>(),
-                         a->dkid.as<int64_t>(), (uint64_t)(a->dcap - 1), a->arena.as<uint8_t>(), doff.as<int64_t>(),
-                         dbytes.as<uint8_t>(), nk, dkid.as<int64_t>());
-      KHIP_TRY_HIP(hipGetLastError());
+      KHIP_TRY(dict_find(a->dict, a->stream, doff.as<int64_t>(), dbytes.as<uint8_t>(), nk, dkid.as<int64_t>()));
       KHIP_TRY_HIP(hipMemcpyAsync(k.data(), dkid.p, (size_t)nk * 8, hipMemcpyDeviceToHost, a->stream));
       KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
     }
@@ -1467,8 +1625,8 @@ khip_status khip_agg_changes_size(khip_agg* a, int64_t* n_rows, int64_t* key_byt
   if (key_bytes) {
     int64_t kb = 0;
     if (a->desc.key_type == KHIP_KEY_UTF8 && a->chg_n) {
-      std::vector<uint8_t> arena(a->arena_used);
-      if (a->arena_used) KHIP_TRY_HIP(hipMemcpy(arena.data(), a->arena.p, a->arena_used, hipMemcpyDeviceToHost));
+      std::vector<uint8_t> arena(a->dict.arena_used);
+      if (a->dict.arena_used) KHIP_TRY_HIP(hipMemcpy(arena.data(), a->dict.arena.p, a->dict.arena_used, hipMemcpyDeviceToHost));
       for (int64_t r = 0; r < a->chg_n; r++) kb += *(const int64_t*)(arena.data() + a->chg_rows[r * a->sw] + 8);
     }
     *key_bytes = kb;
@@ -1504,11 +1662,10 @@ khip_status khip_agg_reset(khip_agg* a) {
                        a->table.as<uint64_t>(), a->cap, a->sw, a->init);
     int64_t m1 = -1;
     KHIP_TRY_HIP(hipMemcpyAsync(a->stream_time.p, &m1, 8, hipMemcpyHostToDevice, a->stream));
+    if (a->engine == 3) KHIP_TRY(tagg_reset(a));
   }
   if (a->desc.key_type == KHIP_KEY_UTF8) {
-    KHIP_TRY_HIP(hipMemsetAsync(a->dword.p, 0, a->dcap * 8, a->stream));
-    a->docc = 0;
-    a->arena_used = 0;
+    KHIP_TRY(dict_clear(a->dict, a->stream));
   }
   // asynchronous on the handle's stream (every later call on the handle is ordered behind it)
   KHIP_TRY_HIP(hipGetLastError());
@@ -1544,13 +1701,14 @@ khip_status khip_agg_destroy(khip_agg* a) {
   if (a->stream) hipStreamSynchronize(a->stream);
   DevBuf* bufs[] = {&a->table, &a->blockmax, &a->blockprefix, &a->partials, &a->resume, &a->counters,
                     &a->stream_time, &a->st_keys, &a->st_ts, &a->st_kv, &a->st_rv, &a->st_koff,
-                    &a->st_kbytes, &a->kid, &a->khash, &a->dword, &a->dkid, &a->arena, &a->dict_bsum,
-                    &a->dict_fail, &a->chg, &a->lostbuf, &a->lostctr};
+                    &a->st_kbytes, &a->kid, &a->khash, &a->chg, &a->lostbuf, &a->lostctr};
   for (DevBuf* b : bufs) b->release();
   for (int c = 0; c < MAX_COLS; c++) {
     a->st_cols[c].release();
     a->st_cval[c].release();
   }
+  dict_release(a->dict);
+  tagg_release(a);
   part_release(a);
   sess_release(a);
   for (int e = 0; e < 8; e++)

@@ -3,6 +3,7 @@
 
 #include <vector>
 
+#include "khip_dict.hpp"
 #include "khip_util.hpp"
 
 namespace khip {
@@ -349,6 +350,17 @@ struct PartState {
 
 // SESSION engine state (khip_agg_session.hip): the session store sorted by (key, start) and
 // the per-push scratch.
+// Table-aggregation state (khip_agg_table.hip, engine 3): the source table's current rows by
+// PRIMARY KEY id, HBM open addressing, TS_WORDS + n_cols u64 per slot (see the file header).
+struct TaggState {
+  DevBuf src;           // source-table slots
+  int64_t src_cap = 0, src_occ = 0;
+  int src_sw = 8;
+  int key_type = -1;    // source PRIMARY KEY type (fixed by the first push)
+  KeyDict dict;         // UTF8 PRIMARY KEYs → ids
+  DevBuf sid, skey, skey2, sidx, sidx2, tmp, ctr, claimed, st_koff, st_kbytes, st_kv, st_key, shash;
+};
+
 struct SessState {
   DevBuf rows, rows2;  // store (n rows) and the next push's output
   int64_t n = 0;
@@ -385,17 +397,18 @@ struct khip_agg {
   DevBuf kid, khash;  // UTF8
   int64_t resume_n = 0;
   // UTF8 dictionary
-  DevBuf dword, dkid, arena, dict_bsum, dict_fail;
-  int64_t dcap = 0, docc = 0, arena_used = 0;
+  KeyDict dict;
   int64_t host_stream_time = -1;
   // profiling (KHIP_FLAG_PROFILE)
   bool profile = false;
   hipEvent_t ev[8] = {};  // 0-4 atomic engine phases, 5-7 partitioned engine
   khip_kernel_times times{};
-  int engine = 0;  // 0 partitioned (LDS-owned groups), 1 global-atomic, 2 SESSION store
+  int engine = 0;  // 0 partitioned (LDS-owned groups), 1 global-atomic, 2 SESSION store, 3 table source
+                   // (the global-atomic table, updated by khip_agg_push_table)
   khip::HavingDev having{};  // the query's HAVING (desc.has_having), maintained by the merge kernel
   khip::PartState part;
   khip::SessState sess;     // engine 2 (SESSION windows)
+  khip::TaggState tagg;     // engine 3 (table source: KHIP_FLAG_TABLE_SOURCE)
   // ---- retention and emission (include/ksqldb_hip.h khip_agg_changes)
   int64_t retention = 0;     // windowed: RETENTION or size + grace
   bool changelog = false;    // KHIP_FLAG_CHANGELOG: keep the push's EMIT CHANGES rows
@@ -438,6 +451,17 @@ khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                       const uint8_t* rv, const ColPtrs& cols, int64_t* tot);
 khip_status sess_changes(khip_agg* a, std::vector<uint64_t>* rows, std::vector<uint8_t>* tomb, int64_t* count);
 void sess_release(khip_agg* a);
+// table source (khip_agg_table.hip): batch rows (group ids, group-key hashes, group validity kv,
+// tombstones rv, ts, argument columns) + device source PRIMARY KEY ids / validity
+khip_status tagg_push(khip_agg* a, int64_t n, const int64_t* gkeys, const int64_t* ghash, const uint8_t* kv,
+                      const uint8_t* rv, const int64_t* ts, const ColPtrs& cols, const int64_t* src_id,
+                      const uint8_t* src_kv, int64_t* tot);
+void tagg_release(khip_agg* a);
+khip_status tagg_reset(khip_agg* a);
+// the global-atomic table (khip_agg.hip), shared with engine 3
+khip_status agg_grow_table(khip_agg* a, int64_t new_cap);
+__global__ void k_finalize(uint64_t* __restrict__ table, int64_t cap, int sw, const int64_t* __restrict__ keys,
+                           const int64_t* __restrict__ ts, int windowed, int64_t size, int64_t adv);
 // the first visible window start after the last push (INT64_MIN: nothing expired)
 int64_t visible_from(const khip_agg* a);
 khip_status emit_final_lost(khip_agg* a, const int64_t* ts, const uint8_t* kv, const uint8_t* rv, int64_t n,

@@ -1,0 +1,439 @@
+// khip_agg_table.hip — table aggregation (CREATE TABLE .. AS SELECT .. FROM <TABLE> GROUP BY ..)
+// on MI355X (gfx950): engine 3 of khip_agg.
+//
+// Replaces, for one query task, KSPlanBuilder.visitTableGroupBy + visitTableAggregate
+// (S/TableGroupByBuilderBase.java:62-111, S/TableAggregateBuilder.java:54-108): Kafka Streams'
+// KTable.groupBy(mapper).aggregate(initializer, KudafAggregator, KudafUndoAggregator) — per
+// source-table change, the key's previous row is undone from its group (TableUdaf.undo,
+// X/function/udaf/KudafUndoAggregator.java:29-55) and the new row applied to its group.  Semantics
+// restated in oracle/oracle.c R12.
+//
+// Group state lives in the global-atomic engine's HBM table (khip_agg.hip: [key | claim ref,
+// ws = 0 | EMPTY, rowtime, state words]), so snapshots, pull queries, HAVING counts and growth
+// are that engine's.  The source table is a second open-addressing table keyed by PRIMARY KEY id:
+//   [0] key  [1] meta: 0 empty | bit63 claimed by this push (bits 0..39 = sorted position) |
+//                      bit62 resident
+//   [2] flags: bit0 live, bit1 GROUP BY value non-null, bits 8.. argument validity
+//   [3] group id  [4] group-key hash  [5..] argument words (raw 8 bytes)
+//
+// Per push (all on the handle's stream):
+//   k_tagg_keys    sort key = PRIMARY KEY id (UINT64_MAX for dropped rows), value = row; counts
+//   hipcub radix sort (stable: a key's rows keep their arrival order)
+//   k_tagg_apply   one thread per distinct PRIMARY KEY (segment leader): find-or-claim its source
+//                  slot (claim references the sorted position: no spin), then replay its rows in
+//                  order — undo the previous row (-1 / -x) from its group, apply the new row (+1 /
+//                  +x; the group is found or claimed with the atomic engine's reference CAS) —
+//                  and store the last row.  Group updates are agent-scope atomics; the row time
+//                  is an atomic max.  Integer state is exact (wrapping adds commute); DOUBLE sums
+//                  are order-dependent only by rounding.
+//   k_finalize     (khip_agg.hip) group claims → resident groups
+//   k_tagg_src_finalize  source claims → resident keys
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <vector>
+
+#include "khip_agg_internal.hpp"
+#include "khip_util.hpp"
+
+namespace khip {
+
+constexpr int TS_WORDS = 5;
+constexpr uint64_t TS_CLAIM = 1ULL << 63;
+constexpr uint64_t TS_RESIDENT = 1ULL << 62;
+constexpr uint64_t TF_LIVE = 1, TF_GVALID = 2;
+constexpr int TS_MAX_PROBE = 4096;
+
+enum { TC_ACCEPTED, TC_NULL_KEY, TC_BAD_TS, TC_UPDATES, TC_NEW_GROUPS, TC_NEW_KEYS, TC_FAILED, TC_N };
+
+__device__ __forceinline__ uint64_t src_hash(int64_t id) { return mix64((uint64_t)id ^ 0x3C6EF372FE94F82BULL); }
+
+__global__ __launch_bounds__(256) void k_tagg_keys(const int64_t* __restrict__ src_id, const uint8_t* __restrict__ src_kv,
+                                                   const int64_t* __restrict__ ts, int64_t n,
+                                                   uint64_t* __restrict__ skey, uint32_t* __restrict__ sidx,
+                                                   unsigned long long* __restrict__ ctr) {
+  int64_t acc = 0, nk = 0, bt = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const bool kv = bit_get(src_kv, i);
+    const bool ok = kv && ts[i] >= 0;
+    skey[i] = ok ? (uint64_t)src_id[i] : ~0ULL;
+    sidx[i] = (uint32_t)i;
+    acc += ok;
+    nk += !kv;
+    bt += kv && ts[i] < 0;
+  }
+  acc = wave_sum(acc);
+  nk = wave_sum(nk);
+  bt = wave_sum(bt);
+  if ((threadIdx.x & 63) == 0) {
+    if (acc) atomicAdd(&ctr[TC_ACCEPTED], (unsigned long long)acc);
+    if (nk) atomicAdd(&ctr[TC_NULL_KEY], (unsigned long long)nk);
+    if (bt) atomicAdd(&ctr[TC_BAD_TS], (unsigned long long)bt);
+  }
+}
+
+// One row's aggregate contribution: argument words + validity mask (bit c = column c non-null).
+struct TRow {
+  int64_t gid, ghash;
+  uint32_t flags;  // TF_* | valid mask << 8
+  int64_t w[MAX_COLS];
+};
+
+// Add (sign +1, may create the group; claim references batch row `row`) or undo (sign -1: the
+// group exists — resident, or claimed earlier in this push) one row's contribution.
+// Returns 0 on probe exhaustion, 1 on update, 2 on update of a newly claimed group.
+__device__ __forceinline__ int group_update(const ApplyParams& p, uint64_t* __restrict__ table, uint64_t mask,
+                                            const TRow& r, int sign, int64_t row, int64_t t,
+                                            const int64_t* __restrict__ gkeys) {
+  const uint64_t h = group_hash(r.ghash, 0);
+  const uint64_t fp = (h >> 49) & 0x7FFFULL;
+  const uint64_t myref = (1ULL << 63) | (fp << 48) | (uint64_t)row;
+  uint64_t slot = h & mask;
+  const int sw = p.slot_words;
+  for (int probe = 0; probe < MAX_PROBE; probe++) {
+    uint64_t* s = table + slot * (uint64_t)sw;
+    const int64_t w1 = (int64_t)ld_relaxed(&s[1]);
+    bool hit = false;
+    int isnew = 0;
+    if (w1 != EMPTY_WS) {
+      hit = (int64_t)s[0] == r.gid;
+    } else {
+      uint64_t w0 = ld_relaxed(s);
+      if (w0 == 0) {
+        if (sign < 0) return 0;  // an undo always finds its group
+        const uint64_t old = atomicCAS((unsigned long long*)s, 0ULL, (unsigned long long)myref);
+        if (old == 0) {
+          hit = true;
+          isnew = 1;
+        } else {
+          w0 = old;
+        }
+      }
+      if (!hit && ((w0 >> 48) & 0x7FFFULL) == fp) hit = gkeys[(int64_t)(w0 & ((1ULL << 36) - 1))] == r.gid;
+    }
+    if (hit) {
+      __hip_atomic_fetch_max((int64_t*)&s[2], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int o = 0; o < p.n_ops; o++) {
+        const UpdOp op = p.ops[o];
+        int64_t* w = (int64_t*)&s[op.word];
+        if (op.kind == OP_INC) {  // COUNT(*) = COUNT(ROWTIME): never null
+          __hip_atomic_fetch_add(w, (int64_t)sign, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          continue;
+        }
+        if (!((r.flags >> (8 + op.col)) & 1u)) continue;  // null argument: unchanged (undo too)
+        switch (op.kind) {
+          case OP_INC_VALID:
+            __hip_atomic_fetch_add(w, (int64_t)sign, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          case OP_ADD_I64: {  // INT / BIGINT: wrapping (INT truncated to 32 bits when read)
+            const uint64_t x = (uint64_t)r.w[op.col];
+            __hip_atomic_fetch_add((uint64_t*)w, sign > 0 ? x : (uint64_t)0 - x, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          case OP_ADD_F64: {
+            double d;
+            __builtin_memcpy(&d, &r.w[op.col], 8);
+            unsafeAtomicAdd((double*)w, sign > 0 ? d : -d);
+            break;
+          }
+          default:  // MIN / MAX are rejected at create (not undoable)
+            break;
+        }
+      }
+      return 1 + isnew;
+    }
+    slot = (slot + 1) & mask;
+  }
+  return 0;
+}
+
+struct TaggArgs {
+  ApplyParams p;
+  uint64_t* table;  // group table
+  uint64_t gmask;
+  uint64_t* src;    // source table
+  uint64_t smask;
+  int32_t ssw;
+  int32_t n_cols;
+  int32_t col_type[MAX_COLS];
+  int64_t n;
+};
+
+__device__ __forceinline__ int64_t load_word(const ColPtrs& c, int32_t type, int col, int64_t i) {
+  return type == KHIP_TYPE_INT32 ? (int64_t)((const int32_t*)c.data[col])[i] : ((const int64_t*)c.data[col])[i];
+}
+
+__global__ __launch_bounds__(256) void k_tagg_apply(TaggArgs A, const uint64_t* __restrict__ skey,
+                                                    const uint32_t* __restrict__ sidx, const int64_t* __restrict__ gkeys,
+                                                    const int64_t* __restrict__ ghash, const uint8_t* __restrict__ kv,
+                                                    const uint8_t* __restrict__ rv, const int64_t* __restrict__ ts,
+                                                    ColPtrs cols, const uint8_t* __restrict__ src_kv,
+                                                    int64_t* __restrict__ claimed, unsigned long long* __restrict__ ctr) {
+  int64_t upd = 0, newg = 0, newk = 0, failed = 0;
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < A.n; j += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = skey[j];
+    if (j > 0 && skey[j - 1] == k) continue;  // not the segment leader
+    int64_t end = j + 1;
+    while (end < A.n && skey[end] == k) end++;
+    // a segment of dropped rows only (UINT64_MAX that no accepted key shares)
+    bool any = false;
+    for (int64_t q = j; q < end && !any; q++) {
+      const int64_t r = sidx[q];
+      any = bit_get(src_kv, r) && ts[r] >= 0;
+    }
+    if (!any) continue;
+    const int64_t id = (int64_t)k;
+    // find or claim the key's source slot (only this thread holds this key)
+    uint64_t slot = src_hash(id) & A.smask;
+    uint64_t* s = nullptr;
+    bool fresh = false;
+    for (int probe = 0; probe < TS_MAX_PROBE; probe++) {
+      uint64_t* c = A.src + slot * (uint64_t)A.ssw;
+      uint64_t m = ld_relaxed(&c[1]);
+      if (m == 0) {
+        const uint64_t old = atomicCAS((unsigned long long*)&c[1], 0ULL, (unsigned long long)(TS_CLAIM | (uint64_t)j));
+        if (old == 0) {
+          s = c;
+          fresh = true;
+          break;
+        }
+        m = old;
+      }
+      // another key's claim of this push (compare by its sorted key) or a resident key
+      if (!(m & TS_CLAIM) && (int64_t)c[0] == id) {
+        s = c;
+        break;
+      }
+      slot = (slot + 1) & A.smask;
+    }
+    if (!s) {
+      failed++;
+      continue;
+    }
+    TRow prev{};
+    if (!fresh) {
+      prev.flags = (uint32_t)s[2];
+      prev.gid = (int64_t)s[3];
+      prev.ghash = (int64_t)s[4];
+      for (int c = 0; c < A.n_cols; c++) prev.w[c] = (int64_t)s[TS_WORDS + c];
+    } else {
+      claimed[atomicAdd(&ctr[TC_NEW_KEYS], 1ULL)] = (int64_t)slot;
+      newk++;
+    }
+    for (int64_t q = j; q < end; q++) {
+      const int64_t r = sidx[q];
+      const int64_t t = ts[r];
+      if (!bit_get(src_kv, r) || t < 0) continue;
+      if ((prev.flags & (TF_LIVE | TF_GVALID)) == (TF_LIVE | TF_GVALID)) {  // undo the previous row
+        const int u = group_update(A.p, A.table, A.gmask, prev, -1, r, t, gkeys);
+        if (u == 0) failed++;
+        upd++;
+      }
+      if (!bit_get(rv, r)) {  // tombstone: the key leaves the table
+        prev.flags = 0;
+        continue;
+      }
+      TRow cur{};
+      cur.flags = TF_LIVE;
+      if (bit_get(kv, r)) {
+        cur.flags |= TF_GVALID;
+        cur.gid = gkeys[r];
+        cur.ghash = ghash[r];
+      }
+      for (int c = 0; c < A.n_cols; c++) {
+        const bool v = bit_get(cols.valid[c], r);
+        cur.w[c] = v ? load_word(cols, A.col_type[c], c, r) : 0;
+        cur.flags |= (v ? 1u : 0u) << (8 + c);
+      }
+      if (cur.flags & TF_GVALID) {
+        const int u = group_update(A.p, A.table, A.gmask, cur, +1, r, t, gkeys);
+        if (u == 0) failed++;
+        newg += u == 2;
+        upd++;
+      }
+      prev = cur;
+    }
+    // the key's last row (or its deletion)
+    s[2] = prev.flags;
+    s[3] = (uint64_t)prev.gid;
+    s[4] = (uint64_t)prev.ghash;
+    for (int c = 0; c < A.n_cols; c++) s[TS_WORDS + c] = (uint64_t)prev.w[c];
+  }
+  upd = wave_sum(upd);
+  newg = wave_sum(newg);
+  failed = wave_sum(failed);
+  if ((threadIdx.x & 63) == 0) {
+    if (upd) atomicAdd(&ctr[TC_UPDATES], (unsigned long long)upd);
+    if (newg) atomicAdd(&ctr[TC_NEW_GROUPS], (unsigned long long)newg);
+    if (failed) atomicAdd(&ctr[TC_FAILED], (unsigned long long)failed);
+  }
+}
+
+// This push's source claims → resident keys (the claim holds the sorted position of the key).
+__global__ __launch_bounds__(256) void k_tagg_src_finalize(uint64_t* __restrict__ src, int ssw,
+                                                           const int64_t* __restrict__ claimed,
+                                                           const unsigned long long* __restrict__ n_claimed,
+                                                           const uint64_t* __restrict__ skey) {
+  const int64_t nc = (int64_t)*n_claimed;
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < nc; k += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t* s = src + (uint64_t)claimed[k] * (uint64_t)ssw;
+    const uint64_t m = s[1];
+    if (m & TS_CLAIM) {
+      s[0] = skey[(int64_t)(m & ((1ULL << 40) - 1))];
+      s[1] = TS_RESIDENT;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_tagg_src_rehash(const uint64_t* __restrict__ old, int64_t ocap,
+                                                         uint64_t* __restrict__ nt, uint64_t nmask, int ssw) {
+  for (int64_t slot = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; slot < ocap;
+       slot += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t* s = old + slot * (uint64_t)ssw;
+    if (!(s[1] & TS_RESIDENT)) continue;
+    if (!(s[2] & TF_LIVE)) continue;  // deleted keys are dropped on rehash
+    uint64_t d = src_hash((int64_t)s[0]) & nmask;
+    while (atomicCAS((unsigned long long*)&nt[d * ssw + 1], 0ULL, (unsigned long long)TS_RESIDENT) != 0ULL)
+      d = (d + 1) & nmask;
+    uint64_t* q = nt + d * (uint64_t)ssw;
+    q[0] = s[0];
+    for (int w = 2; w < ssw; w++) q[w] = s[w];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_tagg_src_count(const uint64_t* __restrict__ src, int64_t cap, int ssw,
+                                                        unsigned long long* __restrict__ n) {
+  int64_t c = 0;
+  for (int64_t slot = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; slot < cap;
+       slot += (int64_t)gridDim.x * blockDim.x)
+    c += (src[slot * (uint64_t)ssw + 1] & TS_RESIDENT) ? 1 : 0;
+  c = wave_sum(c);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(n, (unsigned long long)c);
+}
+
+static int tgrid(int64_t work, int cap_blocks = 8192) {
+  return (int)std::min<int64_t>(ceil_div(std::max<int64_t>(work, 1), 256), cap_blocks);
+}
+
+template <class F>
+static khip_status tcub(DevBuf& tmp, F&& f) {
+  size_t bytes = 0;
+  if (f(nullptr, bytes) != hipSuccess) return fail(KHIP_E_DEVICE, "hipcub size query failed");
+  KHIP_TRY(tmp.ensure(std::max<size_t>(bytes, 16)));
+  if (f(tmp.p, bytes) != hipSuccess) return fail(KHIP_E_DEVICE, "hipcub call failed");
+  return KHIP_OK;
+}
+
+static khip_status src_alloc(khip_agg* a, DevBuf& buf, int64_t cap) {
+  TaggState& T = a->tagg;
+  KHIP_TRY(buf.ensure((size_t)cap * T.src_sw * 8));
+  KHIP_TRY_HIP(hipMemsetAsync(buf.p, 0, (size_t)cap * T.src_sw * 8, a->stream));
+  return KHIP_OK;
+}
+
+// Grow the source table (deleted keys are dropped; the live ones re-inserted).
+static khip_status src_grow(khip_agg* a, int64_t new_cap) {
+  TaggState& T = a->tagg;
+  DevBuf nt;
+  KHIP_TRY(src_alloc(a, nt, new_cap));
+  if (T.src_cap > 0 && T.src_occ > 0) {
+    hipLaunchKernelGGL(k_tagg_src_rehash, dim3(tgrid(T.src_cap)), dim3(256), 0, a->stream, T.src.as<uint64_t>(),
+                       T.src_cap, nt.as<uint64_t>(), (uint64_t)(new_cap - 1), T.src_sw);
+    KHIP_TRY_HIP(hipGetLastError());
+  }
+  KHIP_TRY(T.ctr.ensure(TC_N * 8));
+  KHIP_TRY_HIP(hipMemsetAsync(T.ctr.p, 0, 8, a->stream));
+  hipLaunchKernelGGL(k_tagg_src_count, dim3(tgrid(new_cap, 2048)), dim3(256), 0, a->stream, nt.as<uint64_t>(), new_cap,
+                     T.src_sw, T.ctr.as<unsigned long long>());
+  unsigned long long occ = 0;
+  KHIP_TRY_HIP(hipMemcpyAsync(&occ, T.ctr.p, 8, hipMemcpyDeviceToHost, a->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  T.src.release();
+  T.src = nt;
+  nt.p = nullptr;
+  T.src_cap = new_cap;
+  T.src_occ = (int64_t)occ;
+  return KHIP_OK;
+}
+
+khip_status tagg_push(khip_agg* a, int64_t n, const int64_t* gkeys, const int64_t* ghash, const uint8_t* kv,
+                      const uint8_t* rv, const int64_t* ts, const ColPtrs& cols, const int64_t* src_id,
+                      const uint8_t* src_kv, int64_t* tot) {
+  TaggState& T = a->tagg;
+  hipStream_t st = a->stream;
+  if (n >= (1LL << 31)) return fail(KHIP_E_UNSUPPORTED, "table-source pushes above 2^31 rows");
+  T.src_sw = (int)next_pow2(std::max(8, TS_WORDS + a->desc.n_cols));
+  // capacity ahead of time: every row a new key / a new group at load <= 1/2 (a push cannot be
+  // resumed half-way: its undo/apply sequence is not idempotent)
+  if (T.src_cap == 0) KHIP_TRY(src_grow(a, next_pow2(std::max<int64_t>(1024, 2 * n))));
+  else if (2 * (T.src_occ + n) > T.src_cap) KHIP_TRY(src_grow(a, next_pow2(2 * (T.src_occ + n))));
+  if (2 * (a->occ + n) > a->cap) KHIP_TRY(agg_grow_table(a, next_pow2(2 * (a->occ + n))));
+  KHIP_TRY(T.skey.ensure(n * 8));
+  KHIP_TRY(T.skey2.ensure(n * 8));
+  KHIP_TRY(T.sidx.ensure(n * 4));
+  KHIP_TRY(T.sidx2.ensure(n * 4));
+  KHIP_TRY(T.claimed.ensure(n * 8));
+  KHIP_TRY(T.ctr.ensure(TC_N * 8));
+  unsigned long long* ctr = T.ctr.as<unsigned long long>();
+  KHIP_TRY_HIP(hipMemsetAsync(ctr, 0, TC_N * 8, st));
+  hipLaunchKernelGGL(k_tagg_keys, dim3(tgrid(n)), dim3(256), 0, st, src_id, src_kv, ts, n, T.skey.as<uint64_t>(),
+                     T.sidx.as<uint32_t>(), ctr);
+  KHIP_TRY_HIP(hipGetLastError());
+  uint64_t* kin = T.skey.as<uint64_t>();
+  uint64_t* kout = T.skey2.as<uint64_t>();
+  uint32_t* vin = T.sidx.as<uint32_t>();
+  uint32_t* vout = T.sidx2.as<uint32_t>();
+  const int ni = (int)n;
+  KHIP_TRY(tcub(T.tmp, [&](void* p, size_t& b) {
+    return hipcub::DeviceRadixSort::SortPairs(p, b, kin, kout, vin, vout, ni, 0, 64, st);
+  }));
+  TaggArgs A{};
+  A.p = a->ap;
+  A.table = a->table.as<uint64_t>();
+  A.gmask = (uint64_t)(a->cap - 1);
+  A.src = T.src.as<uint64_t>();
+  A.smask = (uint64_t)(T.src_cap - 1);
+  A.ssw = T.src_sw;
+  A.n_cols = a->desc.n_cols;
+  for (int c = 0; c < MAX_COLS; c++) A.col_type[c] = a->ap.col_type[c];
+  A.n = n;
+  hipLaunchKernelGGL(k_tagg_apply, dim3(tgrid(n, 16384)), dim3(256), 0, st, A, kout, vout, gkeys, ghash, kv, rv, ts,
+                     cols, src_kv, T.claimed.as<int64_t>(), ctr);
+  hipLaunchKernelGGL(k_finalize, dim3(tgrid(a->cap)), dim3(256), 0, st, a->table.as<uint64_t>(), a->cap, a->sw, gkeys,
+                     ts, 0, (int64_t)0, (int64_t)1);
+  hipLaunchKernelGGL(k_tagg_src_finalize, dim3(tgrid(n)), dim3(256), 0, st, T.src.as<uint64_t>(), T.src_sw,
+                     T.claimed.as<int64_t>(), (const unsigned long long*)&ctr[TC_NEW_KEYS], kout);
+  KHIP_TRY_HIP(hipGetLastError());
+  unsigned long long c[TC_N];
+  KHIP_TRY_HIP(hipMemcpyAsync(c, ctr, sizeof(c), hipMemcpyDeviceToHost, st));
+  KHIP_TRY_HIP(hipStreamSynchronize(st));
+  if (c[TC_FAILED]) return fail(KHIP_E_DEVICE, "table aggregation: hash table probe budget exhausted");
+  T.src_occ += (int64_t)c[TC_NEW_KEYS];
+  a->occ += (int64_t)c[TC_NEW_GROUPS];
+  tot[P_ACCEPTED] += (int64_t)c[TC_ACCEPTED];
+  tot[P_NULL_KEY] += (int64_t)c[TC_NULL_KEY];
+  tot[P_BAD_TS] += (int64_t)c[TC_BAD_TS];
+  tot[P_APPLIED] += (int64_t)c[TC_UPDATES];
+  tot[P_NEW] += (int64_t)c[TC_NEW_GROUPS];
+  return KHIP_OK;
+}
+
+khip_status tagg_reset(khip_agg* a) {
+  TaggState& T = a->tagg;
+  if (T.src_cap) KHIP_TRY_HIP(hipMemsetAsync(T.src.p, 0, (size_t)T.src_cap * T.src_sw * 8, a->stream));
+  T.src_occ = 0;
+  if (T.key_type == KHIP_KEY_UTF8) KHIP_TRY(dict_clear(T.dict, a->stream));
+  return KHIP_OK;
+}
+
+void tagg_release(khip_agg* a) {
+  TaggState& T = a->tagg;
+  DevBuf* bufs[] = {&T.src, &T.sid, &T.skey, &T.skey2, &T.sidx, &T.sidx2, &T.tmp, &T.ctr, &T.claimed,
+                    &T.st_koff, &T.st_kbytes, &T.st_kv, &T.st_key, &T.shash};
+  for (DevBuf* b : bufs) b->release();
+  dict_release(T.dict);
+  T.src_cap = T.src_occ = 0;
+}
+
+}  // namespace khip

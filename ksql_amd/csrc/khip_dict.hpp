@@ -1,0 +1,41 @@
+// khip_dict.hpp — the device dictionary of serialized STRING keys, shared by the aggregate
+// (UTF8 GROUP BY keys) and the stream-table join (STRING-keyed tables).
+//
+// Group / table identity in the reference is equality of the serialized KAFKA key bytes
+// (S/JoinParamsFactory.java:65-84 only requires both join sides' key types to
+// match).  The dictionary maps key bytes to a stable int64 id — the byte offset of the key's
+// entry in an append-only arena — so every downstream kernel works on 8-byte ids.
+//   dword[slot]: 0 empty | fresh claim: bit63 | fp22 << 40 | batch row (40 bits)
+//                        | resident:    bit62 | fp22 << 40
+//   arena entry at id o (8-aligned): [u64 hash][i64 len][bytes, padded to 8]
+// Kernels live in khip_agg.hip (k_dict_lookup / k_dict_count / k_dict_write / k_kid_fixup,
+// k_dict_find, k_dict_rehash).
+#pragma once
+#include "khip_util.hpp"
+
+namespace khip {
+
+struct KeyDict {
+  DevBuf dword, dkid, arena, bsum, fail;
+  int64_t dcap = 0, docc = 0, arena_used = 0;
+};
+
+// Allocate the first 4096 slots.
+khip_status dict_init(KeyDict& d, hipStream_t s);
+
+// Batch keys (device offsets[n+1] into device bytes) → ids, inserting unseen keys.  Rows that fail
+// kv, rv or ts >= 0 (each check skipped when its pointer is null) get id 0 and are not inserted.
+// kid[n] and khash[n] (the key's 64-bit hash) are device outputs.  key_bytes_total = koff[n].
+// Synchronises the stream.
+khip_status dict_map(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8_t* kbytes, int64_t key_bytes_total,
+                     const uint8_t* kv, const uint8_t* rv, const int64_t* ts, int64_t n, int64_t* kid, int64_t* khash);
+
+// Read-only probe: kid[i] = the id of key i, or -1 when it was never inserted.  Asynchronous.
+khip_status dict_find(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8_t* kbytes, int64_t n, int64_t* kid);
+
+// Forget every key (keeps the allocation).  Asynchronous.
+khip_status dict_clear(KeyDict& d, hipStream_t s);
+
+void dict_release(KeyDict& d);
+
+}  // namespace khip

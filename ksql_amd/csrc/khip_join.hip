@@ -30,11 +30,18 @@
 // into the 8.6 GB slot table.  Built from the slot table on the first probe after it became
 // eligible and kept in step by the upserts' winning rows (a key or value outside the index's
 // ranges drops it; the next probe rebuilds it over the new ranges).
+//
+// STRING-keyed tables (KHIP_KEY_UTF8): key bytes are mapped to stable ids by the device key
+// dictionary (khip_dict.hpp) — inserting on upsert, read-only on probe (an unseen key is -1,
+// which no slot holds) — and the slot table works on the ids.  Identity is byte equality of the
+// serialized KAFKA STRING key, as in the reference (S/JoinParamsFactory.java:65-84 requires the
+// two sides' key types to match; the lookup is a byte-keyed store get).
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
 
+#include "khip_dict.hpp"
 #include "khip_util.hpp"
 
 namespace khip {
@@ -521,13 +528,17 @@ struct khip_table {
   int64_t dense_eval_occ = -1;  // resident keys when eligibility was last evaluated (-1: never)
   JDense dn{};
   DevBuf dcells, dinvalid, drange;
+  // STRING keys
+  bool utf8 = false;
+  KeyDict dict;
+  DevBuf kid, khash, st_koff, st_kbytes;
 };
 
 // Build the dense probe index if the table qualifies: one INT/BIGINT value column, live keys
 // spanning at most 4x their count (or 2^20), values fitting a 1/2/4/8-byte cell.  Evaluated
 // again only after the table doubled since an unsuccessful try.
 static khip_status prepare_dense(khip_table* t) {
-  if (t->dense_ok || t->desc.n_cols != 1 || t->col_types[0] == KHIP_TYPE_DOUBLE || !knob("KHIP_PROBE_DENSE", 1))
+  if (t->dense_ok || t->utf8 || t->desc.n_cols != 1 || t->col_types[0] == KHIP_TYPE_DOUBLE || !knob("KHIP_PROBE_DENSE", 1))
     return KHIP_OK;
   if (t->dense_eval_occ >= 0 && t->occ < 2 * t->dense_eval_occ) return KHIP_OK;
   t->dense_eval_occ = std::max<int64_t>(t->occ, 1);
@@ -633,8 +644,10 @@ static khip_status jresolve(khip_table* t, const khip_batch* b, int ncols, const
     return KHIP_OK;
   }
   if (b->mem != KHIP_MEM_HOST) return fail(KHIP_E_INVALID, "batch mem");
-  KHIP_TRY(jstage(t, t->st_keys, b->key_i64, n * 8));
-  *keys = t->st_keys.as<int64_t>();
+  if (!t->utf8) {
+    KHIP_TRY(jstage(t, t->st_keys, b->key_i64, n * 8));
+    *keys = t->st_keys.as<int64_t>();
+  }
   if (b->ts) {
     KHIP_TRY(jstage(t, t->st_ts, b->ts, n * 8));
     *ts = t->st_ts.as<int64_t>();
@@ -651,6 +664,39 @@ static khip_status jresolve(khip_table* t, const khip_batch* b, int ncols, const
       cols->valid[c] = t->st_cval[c].as<uint8_t>();
     }
   }
+  return KHIP_OK;
+}
+
+// The batch's table keys on the device: the BIGINT/INT keys as given (jresolve), or the ids of
+// its STRING keys — inserted into the dictionary for an upsert, looked up read-only for a probe
+// (-1 = never upserted).
+static khip_status resolve_keys(khip_table* t, const khip_batch* b, bool upsert, const uint8_t* kv,
+                                const int64_t** keys) {
+  if (!t->utf8) return KHIP_OK;
+  const int64_t n = b->n_rows;
+  const int64_t* koff = b->key_offsets;
+  const uint8_t* kbytes = b->key_bytes;
+  int64_t nbytes = 0;
+  if (b->mem == KHIP_MEM_HOST) {
+    nbytes = b->key_offsets[n];
+    KHIP_TRY(jstage(t, t->st_koff, b->key_offsets, (size_t)(n + 1) * 8));
+    KHIP_TRY(jstage(t, t->st_kbytes, b->key_bytes, (size_t)nbytes));
+    KHIP_TRY(t->st_kbytes.ensure(8));
+    koff = t->st_koff.as<int64_t>();
+    kbytes = t->st_kbytes.as<uint8_t>();
+  } else if (upsert) {
+    KHIP_TRY_HIP(hipMemcpyAsync(&nbytes, koff + n, 8, hipMemcpyDeviceToHost, t->stream));
+    KHIP_TRY_HIP(hipStreamSynchronize(t->stream));
+  }
+  KHIP_TRY(t->kid.ensure((size_t)n * 8));
+  if (upsert) {
+    KHIP_TRY(t->khash.ensure((size_t)n * 8));
+    KHIP_TRY(dict_map(t->dict, t->stream, koff, kbytes, nbytes, kv, nullptr, nullptr, n, t->kid.as<int64_t>(),
+                      t->khash.as<int64_t>()));
+  } else {
+    KHIP_TRY(dict_find(t->dict, t->stream, koff, kbytes, n, t->kid.as<int64_t>()));
+  }
+  *keys = t->kid.as<int64_t>();
   return KHIP_OK;
 }
 
@@ -673,7 +719,8 @@ extern "C" {
 khip_status khip_table_create(const khip_table_desc* d, khip_table** out) {
   clear_error();
   if (!d || !out) return fail(KHIP_E_INVALID, "null argument");
-  if (d->key_type != KHIP_KEY_INT64) return fail(KHIP_E_UNSUPPORTED, "table keys must be INT/BIGINT");
+  if (d->key_type != KHIP_KEY_INT64 && d->key_type != KHIP_KEY_UTF8)
+    return fail(KHIP_E_UNSUPPORTED, "table keys must be INT/BIGINT or STRING");
   if (d->n_cols < 0 || d->n_cols > JMAX_COLS) return fail(KHIP_E_UNSUPPORTED, "at most 16 table columns");
   for (int c = 0; c < d->n_cols; c++)
     if (d->col_types[c] < KHIP_TYPE_INT32 || d->col_types[c] > KHIP_TYPE_DOUBLE)
@@ -683,6 +730,7 @@ khip_status khip_table_create(const khip_table_desc* d, khip_table** out) {
   t->col_types.assign(d->col_types, d->col_types + d->n_cols);
   t->desc.col_types = t->col_types.data();
   t->device = d->device;
+  t->utf8 = d->key_type == KHIP_KEY_UTF8;
   t->sw = (int)next_pow2(std::max(4, 3 + d->n_cols));
   DeviceGuard g(t->device);
   if (hipStreamCreateWithFlags(&t->stream, hipStreamDefault) != hipSuccess) {
@@ -693,7 +741,7 @@ khip_status khip_table_create(const khip_table_desc* d, khip_table** out) {
   khip_status st;
   if ((st = table_alloc(t, t->table, t->cap)) != KHIP_OK ||
       (st = t->types_dev.ensure(sizeof(int32_t) * JMAX_COLS)) != KHIP_OK ||
-      (st = t->scratch.ensure(64)) != KHIP_OK) {
+      (st = t->scratch.ensure(64)) != KHIP_OK || (t->utf8 && (st = dict_init(t->dict, t->stream)) != KHIP_OK)) {
     khip_table_destroy(t);
     return st;
   }
@@ -714,13 +762,14 @@ khip_status khip_table_upsert(khip_table* t, const khip_batch* b) {
   if (n < 0 || b->n_cols < t->desc.n_cols) return fail(KHIP_E_INVALID, "batch shape");
   if (n == 0) return KHIP_OK;
   if (n >= (1LL << 40)) return fail(KHIP_E_UNSUPPORTED, "upsert batch too large");
-  if (!b->key_i64) return fail(KHIP_E_INVALID, "missing key column");
+  if (t->utf8 ? (!b->key_offsets || !b->key_bytes) : !b->key_i64) return fail(KHIP_E_INVALID, "missing key column");
   DeviceGuard g(t->device);
   const int64_t* keys;
   const int64_t* ts;
   const uint8_t *kv, *rv;
   JCols cols;
   KHIP_TRY(jresolve(t, b, t->desc.n_cols, &keys, &ts, &kv, &rv, &cols));
+  KHIP_TRY(resolve_keys(t, b, true, kv, &keys));
   // keep the load factor <= 0.75 even if every row were a new key
   if (4 * (t->occ + n) > 3 * t->cap) KHIP_TRY(table_grow(t, next_pow2((4 * (t->occ + n) + 2) / 3)));
   KHIP_TRY(t->slot_of.ensure(n * 8));
@@ -776,6 +825,7 @@ static khip_status probe_launch(khip_table* t, const khip_batch* b, int32_t join
   JCols cols;
   KHIP_TRY(jresolve(t, b, 0, &keys, &ts, &kv, &rv, &cols));
   if (!ts) return fail(KHIP_E_INVALID, "missing timestamp column");
+  KHIP_TRY(resolve_keys(t, b, false, kv, &keys));
   JWhere jw;
   KHIP_TRY(make_where(t, w, &jw));
   KHIP_TRY(prepare_dense(t));
@@ -812,7 +862,8 @@ khip_status khip_table_probe(khip_table* t, const khip_batch* b, int32_t join_ty
     out->n_rows = 0;
     return KHIP_OK;
   }
-  if (!b->key_i64 || !b->ts) return fail(KHIP_E_INVALID, "missing key or timestamp column");
+  if ((t->utf8 ? (!b->key_offsets || !b->key_bytes) : !b->key_i64) || !b->ts)
+    return fail(KHIP_E_INVALID, "missing key or timestamp column");
   DeviceGuard g(t->device);
   const int nc = t->desc.n_cols;
   JOut o{};
@@ -872,7 +923,8 @@ khip_status khip_table_probe_device(khip_table* t, const khip_batch* b, int32_t 
     if (n_emitted) *n_emitted = 0;
     return KHIP_OK;
   }
-  if (!b->key_i64 || !b->ts) return fail(KHIP_E_INVALID, "missing key or timestamp column");
+  if ((t->utf8 ? (!b->key_offsets || !b->key_bytes) : !b->key_i64) || !b->ts)
+    return fail(KHIP_E_INVALID, "missing key or timestamp column");
   DeviceGuard g(t->device);
   JOut o{};
   o.emit = out->emit;
@@ -908,8 +960,10 @@ khip_status khip_table_destroy(khip_table* t) {
   DeviceGuard g(t->device);
   if (t->stream) hipStreamSynchronize(t->stream);
   DevBuf* bufs[] = {&t->table, &t->types_dev, &t->slot_of, &t->claimed, &t->scratch, &t->st_keys, &t->st_ts, &t->st_kv,
-                    &t->st_rv, &t->out_emit, &t->out_matched, &t->out_slot, &t->dcells, &t->dinvalid, &t->drange};
+                    &t->st_rv, &t->out_emit, &t->out_matched, &t->out_slot, &t->dcells, &t->dinvalid, &t->drange,
+                    &t->kid, &t->khash, &t->st_koff, &t->st_kbytes};
   for (DevBuf* x : bufs) x->release();
+  dict_release(t->dict);
   for (int c = 0; c < JMAX_COLS; c++) {
     t->st_cols[c].release();
     t->st_cval[c].release();

@@ -62,6 +62,15 @@
  *     merged-away sessions are deleted (tombstones) and the merged one is written with the
  *     record applied.  Row time = session end.  Pinned by Q/session-windows.json:4,45 (late
  *     drop and expiry with GRACE PERIOD); the default grace max(24h - gap, 0) is unpinned.
+ *  R12 table aggregation (S/TableAggregateBuilder.java:54-108 over S/TableGroupByBuilderBase.java
+ *     :62-111; Kafka 3.4 KTableRepartitionMap + KTableAggregate): the source table keeps the latest
+ *     row per PRIMARY KEY (a tombstone deletes it); each accepted record first undoes the key's
+ *     previous row from its group (TableUdaf.undo via KudafUndoAggregator, X/function/udaf/
+ *     KudafUndoAggregator.java:29-55: COUNT -1 if non-null, SUM subtracts (wrapping), AVG
+ *     {sum - x, count - 1}; E/function/udaf/count/CountKudaf.java:60-65, sum/*SumKudaf.java:44,
+ *     average/AverageUdaf.java:140-150) when that row had a non-null GROUP BY value, then applies
+ *     the new row to its group (created if absent).  Groups are never deleted (count back to zero,
+ *     Q/count.json); group row time = max ts of the records touching it.
  *  R7 join: table keeps the latest non-null value per key, a null value deletes;
  *     stream records with null key / null value / negative ts are dropped; lookup
  *     against the table as of that point; INNER emits on hit, LEFT always
@@ -79,6 +88,15 @@
 
 static int bit_get(const uint8_t* bm, int64_t i) {
   return bm == NULL ? 1 : (bm[i >> 3] >> (i & 7)) & 1;
+}
+
+#define KHIP_MAX_COLS_ORACLE 16
+
+static int64_t read_col_raw(const khip_batch* b, int c, int type, int64_t r) {
+  int64_t v = 0;
+  if (type == KHIP_TYPE_INT32) v = ((const int32_t*)b->col_data[c])[r];
+  else memcpy(&v, (const char*)b->col_data[c] + 8 * r, 8);
+  return v;
 }
 
 uint64_t oracle_splitmix64(uint64_t x) {
@@ -276,6 +294,18 @@ struct oracle_agg {
   int64_t* stmax;     /* the push's stream-time maxima, in arrival order           */
   int64_t n_stmax, cap_stmax;
   int own_stmax;      /* stmax is this handle's (0: borrowed from the sharded push)  */
+  /* R12 table source: the source table's current rows by PRIMARY KEY (id) */
+  int src_key_type;   /* -1 until the first push_table                            */
+  strdict src_dict;
+  int64_t* src_key;   /* per source row */
+  uint8_t* src_live;
+  uint8_t* src_gvalid;
+  int64_t* src_gkey;
+  int64_t* src_vals;  /* n_cols raw words per source row */
+  uint8_t* src_vvalid;
+  int64_t src_n, src_cap;
+  int64_t* src_slots;
+  int64_t src_nslots;
 };
 
 static uint64_t entry_hash(int64_t key, int64_t ws) {
@@ -375,6 +405,11 @@ static int valid_desc(const khip_agg_desc* d) {
   if (d->emit != KHIP_EMIT_CHANGES && d->emit != KHIP_EMIT_FINAL) return 0;
   if (d->emit == KHIP_EMIT_FINAL && d->window_kind == KHIP_WINDOW_NONE) return 0;
   if (d->has_having && (d->having.agg_index < 0 || d->having.agg_index >= d->n_aggs)) return 0;
+  if (d->flags & KHIP_FLAG_TABLE_SOURCE) { /* R12: unwindowed, undoable aggregates only */
+    if (d->window_kind != KHIP_WINDOW_NONE) return 0;
+    for (int i = 0; i < d->n_aggs; i++)
+      if (d->aggs[i].kind == KHIP_AGG_MIN || d->aggs[i].kind == KHIP_AGG_MAX) return 0;
+  }
   return 1;
 }
 
@@ -408,6 +443,7 @@ khip_status oracle_agg_create(const khip_agg_desc* desc, oracle_agg** out) {
   }
   a->obs_ws = -1;
   a->own_stmax = 1;
+  a->src_key_type = -1;
   a->stream_time = -1;
   strdict_init(&a->dict);
   a->nslots = 1024;
@@ -622,7 +658,7 @@ static void session_apply(oracle_agg* a, int64_t key, int64_t ts, int64_t st, co
 
 khip_status oracle_agg_push(oracle_agg* a, const khip_batch* b, khip_batch_stats* stats) {
   if (!a || !b || b->mem != KHIP_MEM_HOST || b->n_rows < 0) return KHIP_E_INVALID;
-  if (b->n_cols < a->d.n_cols) return KHIP_E_INVALID;
+  if (b->n_cols < a->d.n_cols || (a->d.flags & KHIP_FLAG_TABLE_SOURCE)) return KHIP_E_INVALID;
   khip_batch_stats s;
   memset(&s, 0, sizeof(s));
   s.rows_in = b->n_rows;
@@ -682,6 +718,148 @@ khip_status oracle_agg_push(oracle_agg* a, const khip_batch* b, khip_batch_stats
         s.windows_late++;
       }
     }
+  }
+  s.stream_time = a->stream_time;
+  finish_push(a);
+  if (stats) *stats = s;
+  return KHIP_OK;
+}
+
+/* ------------------------------------------------------------- table aggregation (R12) */
+
+/* Apply (sign +1: KudafAggregator.apply) or undo (sign -1: KudafUndoAggregator.apply) one row given
+ * as raw column words + validity. */
+static void table_row_aggs(oracle_agg* a, entry* x, const int64_t* raw, const uint8_t* valid, int sign) {
+  for (int i = 0; i < a->d.n_aggs; i++) {
+    const khip_agg_spec* sp = &a->aggs[i];
+    agg_state* st = &x->st[i];
+    if (sp->kind == KHIP_AGG_COUNT_STAR) { /* COUNT(ROWTIME): never null */
+      st->i = (int64_t)((uint64_t)st->i + (uint64_t)(int64_t)sign);
+      continue;
+    }
+    const int c = sp->arg_col, t = a->col_types[c];
+    if (!valid[c]) continue; /* null argument: aggregate unchanged (undo too) */
+    switch (sp->kind) {
+      case KHIP_AGG_COUNT: st->i += sign; break;
+      case KHIP_AGG_SUM:
+      case KHIP_AGG_AVG:
+        if (t == KHIP_TYPE_INT32) {
+          const uint32_t v = (uint32_t)(int32_t)raw[c];
+          st->i = (int64_t)(int32_t)(sign > 0 ? (uint32_t)(int32_t)st->i + v : (uint32_t)(int32_t)st->i - v);
+        } else if (t == KHIP_TYPE_INT64) {
+          st->i = (int64_t)(sign > 0 ? (uint64_t)st->i + (uint64_t)raw[c] : (uint64_t)st->i - (uint64_t)raw[c]);
+        } else {
+          double v;
+          memcpy(&v, &raw[c], 8);
+          st->d = sign > 0 ? st->d + v : st->d - v;
+        }
+        if (sp->kind == KHIP_AGG_AVG) st->cnt += sign;
+        break;
+      default:
+        break;
+    }
+  }
+}
+
+static int64_t src_find_or_add(oracle_agg* a, int64_t key) {
+  if (2 * (a->src_n + 1) > a->src_nslots) {
+    const int64_t ns = a->src_nslots ? a->src_nslots * 2 : 1024;
+    free(a->src_slots);
+    a->src_slots = (int64_t*)malloc(sizeof(int64_t) * ns);
+    for (int64_t i = 0; i < ns; i++) a->src_slots[i] = -1;
+    a->src_nslots = ns;
+    for (int64_t r = 0; r < a->src_n; r++) {
+      int64_t j = (int64_t)(mix64((uint64_t)a->src_key[r]) & (uint64_t)(ns - 1));
+      while (a->src_slots[j] >= 0) j = (j + 1) & (ns - 1);
+      a->src_slots[j] = r;
+    }
+  }
+  int64_t j = (int64_t)(mix64((uint64_t)key) & (uint64_t)(a->src_nslots - 1));
+  while (a->src_slots[j] >= 0) {
+    if (a->src_key[a->src_slots[j]] == key) return a->src_slots[j];
+    j = (j + 1) & (a->src_nslots - 1);
+  }
+  if (a->src_n == a->src_cap) {
+    const int nc = a->d.n_cols > 0 ? a->d.n_cols : 1;
+    a->src_cap = a->src_cap ? a->src_cap * 2 : 1024;
+    a->src_key = (int64_t*)realloc(a->src_key, sizeof(int64_t) * a->src_cap);
+    a->src_live = (uint8_t*)realloc(a->src_live, (size_t)a->src_cap);
+    a->src_gvalid = (uint8_t*)realloc(a->src_gvalid, (size_t)a->src_cap);
+    a->src_gkey = (int64_t*)realloc(a->src_gkey, sizeof(int64_t) * a->src_cap);
+    a->src_vals = (int64_t*)realloc(a->src_vals, sizeof(int64_t) * a->src_cap * nc);
+    a->src_vvalid = (uint8_t*)realloc(a->src_vvalid, (size_t)(a->src_cap * nc));
+  }
+  const int64_t r = a->src_n++;
+  a->src_key[r] = key;
+  a->src_live[r] = 0;
+  a->src_slots[j] = r;
+  return r;
+}
+
+khip_status oracle_agg_push_table(oracle_agg* a, const khip_batch* b, const khip_table_src* src,
+                                  khip_batch_stats* stats) {
+  if (!a || !b || !src || b->mem != KHIP_MEM_HOST || b->n_rows < 0) return KHIP_E_INVALID;
+  if (!(a->d.flags & KHIP_FLAG_TABLE_SOURCE) || b->n_cols < a->d.n_cols) return KHIP_E_INVALID;
+  if (src->key_type != KHIP_KEY_INT64 && src->key_type != KHIP_KEY_UTF8) return KHIP_E_INVALID;
+  if (a->src_key_type < 0) {
+    a->src_key_type = src->key_type;
+    strdict_init(&a->src_dict);
+  } else if (a->src_key_type != src->key_type) {
+    return KHIP_E_INVALID;
+  }
+  khip_batch_stats s;
+  memset(&s, 0, sizeof(s));
+  s.rows_in = b->n_rows;
+  a->epoch++;
+  a->n_touched = 0;
+  const int nc = a->d.n_cols > 0 ? a->d.n_cols : 1;
+  int64_t raw[KHIP_MAX_COLS_ORACLE];
+  uint8_t valid[KHIP_MAX_COLS_ORACLE];
+  for (int64_t r = 0; r < b->n_rows; r++) {
+    if (!bit_get(src->key_valid, r)) { s.dropped_null_key++; continue; }
+    const int64_t ts = b->ts[r];
+    if (ts < 0) { s.dropped_bad_ts++; continue; }
+    s.rows_accepted++;
+    const int64_t pk = src->key_type == KHIP_KEY_INT64
+                           ? src->key_i64[r]
+                           : strdict_intern(&a->src_dict, src->key_bytes + src->key_offsets[r],
+                                            src->key_offsets[r + 1] - src->key_offsets[r]);
+    const int64_t row = src_find_or_add(a, pk);
+    /* undo the key's previous row from its group */
+    if (a->src_live[row] && a->src_gvalid[row]) {
+      entry* x = find_or_create(a, a->src_gkey[row], 0);
+      touch(a, x);
+      if (ts > x->rowtime) x->rowtime = ts;
+      table_row_aggs(a, x, a->src_vals + row * nc, a->src_vvalid + row * nc, -1);
+      s.windows_applied++;
+    }
+    if (!bit_get(b->row_valid, r)) { /* tombstone: the key leaves the table */
+      a->src_live[row] = 0;
+      continue;
+    }
+    for (int c = 0; c < a->d.n_cols; c++) {
+      valid[c] = (uint8_t)bit_get(b->col_valid ? b->col_valid[c] : NULL, r);
+      raw[c] = valid[c] ? read_col_raw(b, c, a->col_types[c], r) : 0;
+    }
+    const int gvalid = bit_get(b->key_valid, r);
+    int64_t gkey = 0;
+    if (gvalid)
+      gkey = a->d.key_type == KHIP_KEY_INT64
+                 ? b->key_i64[r]
+                 : strdict_intern(&a->dict, b->key_bytes + b->key_offsets[r], b->key_offsets[r + 1] - b->key_offsets[r]);
+    a->src_live[row] = 1;
+    a->src_gvalid[row] = (uint8_t)gvalid;
+    a->src_gkey[row] = gkey;
+    memcpy(a->src_vals + row * nc, raw, sizeof(int64_t) * (size_t)a->d.n_cols);
+    memcpy(a->src_vvalid + row * nc, valid, (size_t)a->d.n_cols);
+    if (gvalid) {
+      entry* x = find_or_create(a, gkey, 0);
+      touch(a, x);
+      if (ts > x->rowtime) x->rowtime = ts;
+      table_row_aggs(a, x, raw, valid, +1);
+      s.windows_applied++;
+    }
+    if (ts > a->stream_time) a->stream_time = ts;
   }
   s.stream_time = a->stream_time;
   finish_push(a);
@@ -972,6 +1150,9 @@ khip_status oracle_agg_destroy(oracle_agg* a) {
   free(a->e);
   free(a->slots);
   strdict_free(&a->dict);
+  if (a->src_key_type >= 0) strdict_free(&a->src_dict);
+  free(a->src_key); free(a->src_live); free(a->src_gvalid); free(a->src_gkey); free(a->src_vals);
+  free(a->src_vvalid); free(a->src_slots);
   free(a->col_types);
   free(a->aggs);
   free(a);
@@ -1263,6 +1444,7 @@ struct oracle_table {
   int64_t* slots;    /* open addressing → row slot or -1 */
   int64_t nslots;
   int64_t nlive;
+  strdict dict;      /* KHIP_KEY_UTF8: key bytes → id (the id is the table key) */
 };
 
 static void table_rebuild(oracle_table* t, int64_t ns) {
@@ -1278,9 +1460,11 @@ static void table_rebuild(oracle_table* t, int64_t ns) {
 }
 
 khip_status oracle_table_create(const khip_table_desc* desc, oracle_table** out) {
-  if (!desc || !out || desc->key_type != KHIP_KEY_INT64 || desc->n_cols < 0) return KHIP_E_INVALID;
+  if (!desc || !out || desc->n_cols < 0) return KHIP_E_INVALID;
+  if (desc->key_type != KHIP_KEY_INT64 && desc->key_type != KHIP_KEY_UTF8) return KHIP_E_INVALID;
   oracle_table* t = (oracle_table*)calloc(1, sizeof(oracle_table));
   t->d = *desc;
+  strdict_init(&t->dict);
   t->col_types = (int32_t*)malloc(sizeof(int32_t) * (desc->n_cols + 1));
   memcpy(t->col_types, desc->col_types, sizeof(int32_t) * desc->n_cols);
   t->d.col_types = t->col_types;
@@ -1298,6 +1482,15 @@ static int64_t table_find(const oracle_table* t, int64_t key) {
   return -1;
 }
 
+/* Table key of batch row r: the BIGINT/INT key, or (STRING keys) the id of its UTF-8 bytes —
+ * byte equality, as KAFKA STRING keys compare (S/JoinParamsFactory.java:65-84 only requires
+ * both sides' key types to match). */
+static int64_t table_key(oracle_table* t, const khip_batch* b, int64_t r) {
+  if (t->d.key_type != KHIP_KEY_UTF8) return b->key_i64[r];
+  const int64_t o0 = b->key_offsets[r], o1 = b->key_offsets[r + 1];
+  return strdict_intern(&t->dict, b->key_bytes + o0, o1 - o0);
+}
+
 static int64_t read_raw(const khip_batch* b, int c, int type, int64_t r) {
   int64_t v = 0;
   if (type == KHIP_TYPE_INT32) v = ((const int32_t*)b->col_data[c])[r];
@@ -1310,7 +1503,7 @@ khip_status oracle_table_upsert(oracle_table* t, const khip_batch* b) {
   const int nc = t->d.n_cols;
   for (int64_t r = 0; r < b->n_rows; r++) {
     if (!bit_get(b->key_valid, r)) continue;
-    int64_t key = b->key_i64[r];
+    int64_t key = table_key(t, b, r);
     int64_t row = table_find(t, key);
     if (!bit_get(b->row_valid, r)) { /* tombstone */
       if (row >= 0 && t->live[row]) { t->live[row] = 0; t->nlive--; }
@@ -1383,7 +1576,7 @@ khip_status oracle_table_probe(oracle_table* t, const khip_batch* b, int32_t joi
   int64_t m = 0;
   for (int64_t r = 0; r < b->n_rows; r++) {
     if (!bit_get(b->key_valid, r) || !bit_get(b->row_valid, r) || b->ts[r] < 0) continue;
-    int64_t row = table_find(t, b->key_i64[r]);
+    int64_t row = table_find(t, table_key(t, b, r));
     if (row >= 0 && !t->live[row]) row = -1;
     if (join_type == KHIP_JOIN_INNER && row < 0) continue;
     if (!where_pass(t, w, row)) continue;
@@ -1410,6 +1603,7 @@ khip_status oracle_table_destroy(oracle_table* t) {
   if (!t) return KHIP_OK;
   free(t->keys); free(t->live); free(t->vals); free(t->nulls); free(t->slots);
   free(t->col_types);
+  strdict_free(&t->dict);
   free(t);
   return KHIP_OK;
 }

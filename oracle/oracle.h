@@ -31,6 +31,9 @@ khip_status oracle_agg_snapshot_size(oracle_agg* agg, int64_t* n_rows,
 khip_status oracle_agg_snapshot(oracle_agg* agg, const khip_having* having,
                                 khip_snapshot* out);
 khip_status oracle_agg_destroy(oracle_agg* agg);
+/* R12 table aggregation; mirrors khip_agg_push_table. */
+khip_status oracle_agg_push_table(oracle_agg* agg, const khip_batch* batch, const khip_table_src* src,
+                                  khip_batch_stats* stats);
 
 /* Rows the last push emitted (R10), snapshot layout sorted by (key, ws); tombstone[r] = 1
  * for a HAVING delete.  Mirrors khip_agg_changes_size / khip_agg_changes. */

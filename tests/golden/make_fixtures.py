@@ -252,7 +252,8 @@ def extract_agg(path, test, fmt_tag):
     st = test["statements"]
     if len(st) != 2:
         raise Skip("statement count")
-    src = parse_create_source(st[0], "STREAM")
+    table_source = re.match(r"(?i)\s*CREATE\s+TABLE", st[0]) is not None
+    src = parse_create_source(st[0], "TABLE" if table_source else "STREAM")
     m = re.match(r"(?is)^\s*CREATE\s+TABLE\s+(\w+)\s+AS\s+SELECT\s+(.*?)\s+FROM\s+(\w+)(\s+\w+)?\s+"
                  r"(WINDOW\s+(TUMBLING|HOPPING|SESSION)\s*\((.*?)\)\s+)?GROUP\s+BY\s+(.*?)"
                  r"(\s+HAVING\s+(.*?))?\s*(EMIT\s+(CHANGES|FINAL))?\s*;?\s*$", st[1])
@@ -265,6 +266,8 @@ def extract_agg(path, test, fmt_tag):
     if m.group(3).upper() != src["name"]:
         raise Skip("from")
     window = parse_window(m.group(6).upper(), m.group(7)) if m.group(5) else None
+    if table_source and window:
+        raise Skip("windowed table source")
     gb = split_top(m.group(8))
     if len(gb) != 1 or not re.match(r"^\(?\s*[\w`.]+\s*\)?$", gb[0]):
         raise Skip("group by shape")
@@ -280,6 +283,10 @@ def extract_agg(path, test, fmt_tag):
     by_key = colmap[gcol]["key"]
     if by_key and len(key_cols) != 1:
         raise Skip("multi key")
+    if table_source:
+        if len(key_cols) != 1 or key_cols[0]["type"] not in ("INT32", "INT64", "STRING"):
+            raise Skip("table source key")
+        pk_type = key_cols[0]["type"]
     vmap = {c["name"]: c for c in value_cols}
 
     aggs, outcols = [], []
@@ -298,6 +305,8 @@ def extract_agg(path, test, fmt_tag):
         a = parse_agg(e, vmap)
         if a is None:
             raise Skip("select item " + e)
+        if table_source and a["kind"] in ("MIN", "MAX"):
+            raise Skip("agg MIN/MAX on a table source")  # a KsqlException in the reference
         aggs.append(a)
         outcols.append({"src": "AGG", "agg": len(aggs) - 1, "name": alias})
     # unaliased columns get KSQL_COL_<i> names (i = position among unaliased items)
@@ -351,6 +360,8 @@ def extract_agg(path, test, fmt_tag):
             kval = None if val is None else val.get(gcol)
         raw_records.append({"key": rk, "value": rec.get("value"), "ts": ts})
         row = {"key": kval, "row_valid": val is not None, "ts": ts, "cols": []}
+        if table_source:
+            row["src_key"] = None if rk is None else conv(pk_type, rk)
         for c in used:
             v = None if val is None else val.get(c)
             if v is not None and vmap[c]["type"] not in ("INT32", "INT64", "DOUBLE"):
@@ -444,6 +455,8 @@ def extract_agg(path, test, fmt_tag):
             "aggs": spec_aggs,
             "having": having,
             "repartition": not by_key,
+            "table_source": table_source,
+            "src_key_type": ("UTF8" if pk_type == "STRING" else "INT64") if table_source else None,
         },
         "input": rows,
         "expected": expected,
@@ -455,8 +468,12 @@ def extract_join(path, test, fmt_tag):
     st = test["statements"]
     if len(st) != 3:
         raise Skip("statement count")
-    s = parse_create_source(st[0], "STREAM")
-    t = parse_create_source(st[1], "TABLE")
+    if re.match(r"(?i)\s*CREATE\s+TABLE", st[0]):  # table declared first
+        t = parse_create_source(st[0], "TABLE")
+        s = parse_create_source(st[1], "STREAM")
+    else:
+        s = parse_create_source(st[0], "STREAM")
+        t = parse_create_source(st[1], "TABLE")
     m = re.match(r"(?is)^\s*CREATE\s+STREAM\s+(\w+)\s+AS\s+SELECT\s+(.*?)\s+FROM\s+(\w+)(\s+(?!LEFT\b|JOIN\b|INNER\b)\w+)?\s+"
                  r"(LEFT\s+(?:OUTER\s+)?JOIN|INNER\s+JOIN|JOIN)\s+(\w+)(\s+\w+)?\s+ON\s+\(?\s*([\w`.]+)\s*=\s*([\w`.]+)\s*\)?"
                  r"(\s+WHERE\s+(.*?))?\s*(EMIT\s+CHANGES)?\s*;?\s*$", st[2])
@@ -471,8 +488,10 @@ def extract_join(path, test, fmt_tag):
     tkey = [c for c in t["cols"] if c["key"]]
     if len(skey) != 1 or len(tkey) != 1:
         raise Skip("join keys")
-    if skey[0]["type"] not in ("INT32", "INT64") or tkey[0]["type"] not in ("INT32", "INT64"):
+    if skey[0]["type"] not in ("INT32", "INT64", "STRING") or tkey[0]["type"] not in ("INT32", "INT64", "STRING"):
         raise Skip("join key type")
+    if (skey[0]["type"] == "STRING") != (tkey[0]["type"] == "STRING"):
+        raise Skip("join key types differ")
     lhs, rhs = m.group(8).upper().strip("`"), m.group(9).upper().strip("`")
 
     def side_col(ref):
@@ -548,6 +567,7 @@ def extract_join(path, test, fmt_tag):
         "name": test["name"] + (" [%s]" % fmt_tag if fmt_tag else ""),
         "source": "%s:%d" % (os.path.basename(path), find_line(path, test["name"])),
         "join_type": jt,
+        "key_type": "UTF8" if tkey[0]["type"] == "STRING" else "INT64",
         "stream_cols": svals,
         "table_cols": tvals,
         "select": sel,
@@ -558,7 +578,7 @@ def extract_join(path, test, fmt_tag):
 
 
 def main():
-    aggs, joins = [], []
+    aggs, taggs, joins = [], [], []
     skipped = collections.Counter()
     for path in sorted(glob.glob(os.path.join(QTT_DIR, "*.json"))):
         try:
@@ -574,17 +594,22 @@ def main():
                 st = t.get("statements", [])
                 try:
                     if len(st) == 2 and re.search(r"(?i)GROUP\s+BY", st[1]):
-                        aggs.append(extract_agg(path, t, fmt_tag))
-                    elif len(st) == 3 and re.search(r"(?i)\bJOIN\b", st[2]) and re.match(r"(?i)\s*CREATE\s+TABLE", st[1]) \
+                        c = extract_agg(path, t, fmt_tag)
+                        (taggs if c["desc"]["table_source"] else aggs).append(c)
+                    elif len(st) == 3 and re.search(r"(?i)\bJOIN\b", st[2]) \
+                            and sorted(re.match(r"(?i)\s*CREATE\s+(STREAM|TABLE)", x).group(1).upper()
+                                       for x in st[:2] if re.match(r"(?i)\s*CREATE\s+(STREAM|TABLE)", x)) == ["STREAM", "TABLE"] \
                             and re.match(r"(?i)\s*CREATE\s+STREAM", st[2]):
                         joins.append(extract_join(path, t, fmt_tag))
                 except Skip as e:
                     skipped[str(e).split(" ")[0]] += 1
     with open(os.path.join(OUT_DIR, "qtt_agg.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_fixtures.py", "cases": aggs}, f, indent=0, sort_keys=True)
+    with open(os.path.join(OUT_DIR, "qtt_tagg.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_fixtures.py", "cases": taggs}, f, indent=0, sort_keys=True)
     with open(os.path.join(OUT_DIR, "qtt_join.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_fixtures.py", "cases": joins}, f, indent=0, sort_keys=True)
-    print("aggregate cases:", len(aggs), "join cases:", len(joins))
+    print("aggregate cases:", len(aggs), "table-aggregate cases:", len(taggs), "join cases:", len(joins))
     print("skipped:", dict(skipped.most_common()))
 
 

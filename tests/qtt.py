@@ -106,6 +106,29 @@ def run_agg_case(lib, case, split=None, device=0, flags=0):
     return fold(run_agg_outputs(lib, case, split, device, flags))
 
 
+def run_tagg_case(lib, case, split=None, device=0):
+    """Table aggregation (khip_agg_push_table): the source table's changelog in pushes of `split`
+    rows, then the materialized table with the query's HAVING."""
+    d = case["desc"]
+    desc = abi.make_agg_desc(d["window_kind"], d["key_type"], 0, 0, -1, d["col_types"],
+                             [(a["kind"], a["arg_col"]) for a in d["aggs"]], device=device,
+                             flags=abi.FLAG_TABLE_SOURCE)
+    h = abi.AggHandle(lib, desc)
+    n = len(case["input"])
+    step = n if not split else split
+    for lo in range(0, max(n, 1), max(step, 1)):
+        rows = case["input"][lo:lo + step]
+        pk = [r["src_key"] for r in rows]
+        if d["src_key_type"] == "UTF8":
+            h.push_table(case_batch(case, lo, lo + step), src_utf8_keys=pk)
+        else:
+            h.push_table(case_batch(case, lo, lo + step), src_keys=[0 if k is None else k for k in pk],
+                         src_key_valid=[k is not None for k in pk])
+    snap = h.snapshot(d["having"])
+    h.close()
+    return snap
+
+
 def compare_outputs(case, rows):
     """Emitted rows vs the QTT expected output sequence, in order (1-row pushes = the reference's
     cache-off, emit-every-record run).  Returns mismatch descriptions."""
@@ -198,7 +221,8 @@ def run_join_case(lib, case, device=0):
 
     if case["where"] is not None and isinstance(case["where"]["value"], str):
         code(case["where"]["value"])
-    th = abi.TableHandle(lib, [_ctype(c["type"]) for c in tcols], device=device)
+    utf8 = case.get("key_type", "INT64") == "UTF8"
+    th = abi.TableHandle(lib, [_ctype(c["type"]) for c in tcols], device=device, key_type="UTF8" if utf8 else "INT64")
     where = None
     if case["where"] is not None:
         wc = [c["name"] for c in tcols].index(case["where"]["col"])
@@ -215,8 +239,11 @@ def run_join_case(lib, case, device=0):
             j += 1
         grp = events[i:j]
         ts = [e["ts"] for e in grp]
-        keys = [0 if e["key"] is None else int(e["key"]) for e in grp]
         kvalid = [e["key"] is not None for e in grp]
+        if utf8:  # STRING keys: serialized UTF-8 bytes
+            kargs = {"utf8_keys": [None if e["key"] is None else str(e["key"]) for e in grp]}
+        else:
+            kargs = {"keys": [0 if e["key"] is None else int(e["key"]) for e in grp]}
         rvalid = [e["value"] is not None for e in grp]
         if side == "T":
             cols, cval = [], []
@@ -228,9 +255,9 @@ def run_join_case(lib, case, device=0):
                     arr = np.array([0 if v is None else v for v in vals], abi.NP_TYPE[abi.TYPE[c["type"]]])
                 cols.append(arr)
                 cval.append([v is not None for v in vals])
-            th.upsert(abi.HostBatch(ts, keys=keys, key_valid=kvalid, row_valid=rvalid, cols=cols, col_valid=cval))
+            th.upsert(abi.HostBatch(ts, key_valid=kvalid, row_valid=rvalid, cols=cols, col_valid=cval, **kargs))
         else:
-            b = abi.HostBatch(ts, keys=keys, key_valid=kvalid, row_valid=rvalid)
+            b = abi.HostBatch(ts, key_valid=kvalid, row_valid=rvalid, **kargs)
             res = th.probe(b, case["join_type"], where)
             for r in range(res["n"]):
                 e = grp[int(res["stream_row"][r])]

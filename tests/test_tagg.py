@@ -1,0 +1,139 @@
+"""Table aggregation (CREATE TABLE .. AS SELECT .. FROM <TABLE> GROUP BY ..): khip_agg_push_table
+against the QTT table-source cases (tests/golden/qtt_tagg.json, extracted from count.json,
+average-udaf.json and group-by.json) and against the oracle's R12 restatement on random source-table
+changelogs (updates that move keys between groups, deletes, NULL GROUP BY values and arguments,
+repeated keys inside one push, INT wrap-around, STRING and BIGINT keys on both sides).
+
+Comparison: integers exact; DOUBLE SUM/AVG within 1e-12 relative to the sum of |x| the group's
+updates touched (the device applies a push's adds/undos with atomics, in no fixed order)."""
+import numpy as np
+import pytest
+
+import qtt
+from ksql_amd import abi
+
+CASES = qtt.load_cases("tagg")
+
+
+@pytest.fixture(scope="module")
+def prod():
+    return abi.load_product()
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return abi.load_oracle()
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["source"] for c in CASES])
+@pytest.mark.parametrize("split", [None, 1, 2])
+def test_oracle_tagg_golden(orc, case, split):
+    errs = qtt.compare_agg(case, qtt.run_tagg_case(orc, case, split))
+    assert not errs, errs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=[c["source"] for c in CASES])
+@pytest.mark.parametrize("split", [None, 1, 2])
+def test_tagg_golden(prod, case, split):
+    errs = qtt.compare_agg(case, qtt.run_tagg_case(prod, case, split))
+    assert not errs, errs
+
+
+def _changelog(rng, n, nsrc, ngroups, utf8_src, utf8_group):
+    pk = rng.integers(0, nsrc, n)
+    grp = rng.integers(0, ngroups, n)
+    gvalid = rng.random(n) > 0.05
+    rvalid = rng.random(n) > 0.12  # tombstones
+    ts = rng.integers(0, 10**6, n)
+    ts[rng.random(n) < 0.01] = -1
+    pkv = rng.random(n) > 0.01
+    c0 = rng.integers(-2**31, 2**31, n).astype(np.int32)  # INT: sums wrap
+    c1 = rng.integers(-10**15, 10**15, n)
+    c2 = rng.uniform(-100, 100, n)
+    cv = [rng.random(n) > 0.07 for _ in range(3)]
+    ka = {"utf8_keys": ["g%d" % g for g in grp]} if utf8_group else {"keys": grp}
+    b = abi.HostBatch(ts, key_valid=gvalid, row_valid=rvalid, cols=[c0, c1, c2], col_valid=cv, **ka)
+    sa = {"src_utf8_keys": ["pk-%d" % k if v else None for k, v in zip(pk, pkv)]} if utf8_src else \
+        {"src_keys": pk, "src_key_valid": pkv}
+    return b, sa, np.abs(c2)
+
+
+AGGS = [("COUNT_STAR", -1), ("COUNT", 0), ("SUM", 0), ("SUM", 1), ("SUM", 2), ("AVG", 2), ("AVG", 1), ("COUNT", 2)]
+
+
+def _run(lib, batches, utf8_group, having=None):
+    desc = abi.make_agg_desc("NONE", "UTF8" if utf8_group else "INT64", col_types=["INT32", "INT64", "DOUBLE"],
+                             aggs=AGGS, flags=abi.FLAG_TABLE_SOURCE)
+    h = abi.AggHandle(lib, desc)
+    stats = [h.push_table(b, **sa) for b, sa, _ in batches]
+    snap = h.snapshot(having)
+    h.close()
+    return snap, stats
+
+
+def _assert_same(g, o, scale):
+    assert g["n"] == o["n"]
+    assert list(g["key"]) == list(o["key"])
+    assert np.array_equal(g["rowtime"], o["rowtime"])
+    for a, (kind, col) in enumerate(AGGS):
+        assert np.array_equal(g["nulls"][a], o["nulls"][a]), a
+        if col == 2 and kind in ("SUM", "AVG"):
+            np.testing.assert_allclose(g["values"][a], o["values"][a], rtol=0, atol=1e-12 * scale)
+        elif kind == "AVG":  # AVG(BIGINT): (double)sum / count of exact integers
+            np.testing.assert_allclose(g["values"][a], o["values"][a], rtol=1e-15)
+        else:
+            assert np.array_equal(g["values"][a], o["values"][a]), (kind, col)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("utf8_src,utf8_group", [(False, False), (True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("pushes", [1, 5])
+def test_tagg_random_vs_oracle(prod, orc, utf8_src, utf8_group, pushes):
+    rng = np.random.default_rng(100 + 10 * pushes + 2 * utf8_src + utf8_group)
+    batches = [_changelog(rng, int(rng.integers(20000, 60000)), 8000, 300, utf8_src, utf8_group)
+               for _ in range(pushes)]
+    scale = sum(float(x.sum()) for _, _, x in batches) * 4  # every row can be added and undone twice
+    (g, gs), (o, os_) = (_run(lib, batches, utf8_group) for lib in (prod, orc))
+    for a, b in zip(gs, os_):
+        for f in ("rows_in", "rows_accepted", "dropped_null_key", "dropped_bad_ts", "windows_applied"):
+            assert a[f] == b[f], f
+    _assert_same(g, o, scale)
+    having = {"agg": 0, "op": "GT", "value": 0}  # HAVING COUNT(*) > 0: emptied groups disappear
+    (g, _), (o, _) = (_run(lib, batches, utf8_group, having) for lib in (prod, orc))
+    assert 0 < o["n"] <= 300
+    _assert_same(g, o, scale)
+
+
+@pytest.mark.gpu
+def test_tagg_many_updates_per_key(prod, orc):
+    """A handful of PRIMARY KEYs updated thousands of times inside one push: one device thread
+    replays each key's rows in arrival order."""
+    rng = np.random.default_rng(9)
+    batches = [_changelog(rng, 50000, 7, 20, False, False) for _ in range(2)]
+    scale = sum(float(x.sum()) for _, _, x in batches) * 4
+    (g, _), (o, _) = (_run(lib, batches, False) for lib in (prod, orc))
+    _assert_same(g, o, scale)
+
+
+@pytest.mark.gpu
+def test_tagg_reset_and_errors(prod, orc):
+    rng = np.random.default_rng(3)
+    b, sa, _ = _changelog(rng, 5000, 500, 50, False, False)
+    desc = abi.make_agg_desc("NONE", "INT64", col_types=["INT32", "INT64", "DOUBLE"], aggs=AGGS,
+                             flags=abi.FLAG_TABLE_SOURCE)
+    h = abi.AggHandle(prod, desc)
+    h.push_table(b, **sa)
+    first = h.snapshot()
+    with pytest.raises(abi.KsqlHipError):
+        h.push(b)  # a table-source handle takes source-table changes only
+    prod.check(prod.agg_reset(h.h), "agg_reset")
+    assert h.snapshot()["n"] == 0
+    h.push_table(b, **sa)
+    again = h.snapshot()
+    assert again["n"] == first["n"] and np.array_equal(again["values"][0], first["values"][0])
+    h.close()
+    for lib in (prod, orc):  # MIN/MAX are not undoable: rejected like the reference's KsqlException
+        bad = abi.make_agg_desc("NONE", "INT64", col_types=["INT64"], aggs=[("MIN", 0)], flags=abi.FLAG_TABLE_SOURCE)
+        with pytest.raises(abi.KsqlHipError):
+            abi.AggHandle(lib, bad)
