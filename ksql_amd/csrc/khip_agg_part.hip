@@ -1310,32 +1310,46 @@ __device__ __forceinline__ int mg_find(const MergeParams& q, const KLDS uint64_t
   return -1;
 }
 
-// One chunk of a partition's scattered records: AU per thread, rows l0 + tid + u * MG_THREADS.
-// r12: 12-byte narrow records (key hash, trel) → (key hash, ts); trel 0 → ts -1 (no window)
-template <int AU, int NT>
-__device__ __forceinline__ void mg_load(longlong2 (&rec)[AU], longlong2 (&ext)[AU], const uint64_t* __restrict__ srec,
-                                        int64_t rbase, int64_t rn, int64_t l0, int rw, bool wide, bool r12,
-                                        int64_t tbase) {
-  if (r12) {
-    R12 v[AU];
-#pragma unroll
-    for (int u = 0; u < AU; u++) {
-      const int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
-      v[u] = li < rn ? *(const R12*)((const char*)srec + (uint64_t)(rbase + li) * 12) : R12{0u, 0u, 0u};
-    }
-#pragma unroll
-    for (int u = 0; u < AU; u++)
-      rec[u] = make_longlong2((int64_t)((uint64_t)v[u].hi << 32 | v[u].lo),
-                              v[u].trel ? tbase + (int64_t)v[u].trel - 1 : -1);
-    return;
-  }
+// One chunk of a partition's scattered records, AU per thread (rows l0 + tid + u * NT), kept as
+// the raw words the load returns: converting them right after the load would make the wave wait for
+// it there — and, since vmcnt retires loads and stores in issue order, for every row store issued
+// before it.  Every lane loads (the index is clamped to the item's last record, so lanes past the
+// end re-read one line); mg_decode marks them invalid.
+struct MgRaw {
+  uint32_t w[4];  // R12: key hash lo, hi, trel; 16-byte record: key hash lo, hi, ts lo, hi
+};
+
+template <int AU, int NT, bool R12M>
+__device__ __forceinline__ void mg_load(MgRaw (&raw)[AU], longlong2 (&ext)[AU], const uint64_t* __restrict__ srec,
+                                        int64_t rbase, int64_t rn, int64_t l0, int rw, bool wide) {
 #pragma unroll
   for (int u = 0; u < AU; u++) {
     const int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
-    const longlong2* r = (const longlong2*)(srec + (uint64_t)(rbase + li) * rw);
-    rec[u] = li < rn ? r[0] : make_longlong2(0, -1);
-    if (wide) ext[u] = li < rn ? r[1] : make_longlong2(0, 0);
+    const uint64_t idx = (uint64_t)(rbase + (li < rn ? li : (rn > 0 ? rn - 1 : 0)));
+    if constexpr (R12M) {  // a compile-time choice: a run-time one merges both paths' registers,
+                           // which consumes the loaded words at the load
+      const R12 v = *(const R12*)((const char*)srec + idx * 12);
+      raw[u].w[0] = v.lo;
+      raw[u].w[1] = v.hi;
+      raw[u].w[2] = v.trel;
+      raw[u].w[3] = 0u;
+    } else {
+      const uint4 v = *(const uint4*)(srec + idx * rw);
+      raw[u].w[0] = v.x;
+      raw[u].w[1] = v.y;
+      raw[u].w[2] = v.z;
+      raw[u].w[3] = v.w;
+      if (wide) ext[u] = ((const longlong2*)(srec + idx * rw))[1];
+    }
   }
+}
+
+// (key hash, ts) of a raw record; ts = -1 for no window (R12 trel 0) or a lane past the item's end.
+template <bool R12M>
+__device__ __forceinline__ longlong2 mg_decode(const MgRaw& r, int64_t tbase, bool valid) {
+  const int64_t hk = (int64_t)((uint64_t)r.w[1] << 32 | r.w[0]);
+  const int64_t t = R12M ? (r.w[2] ? tbase + (int64_t)r.w[2] - 1 : -1) : (int64_t)((uint64_t)r.w[3] << 32 | r.w[2]);
+  return make_longlong2(hk, valid ? t : -1);
 }
 
 struct MgItem {
@@ -1385,7 +1399,7 @@ __device__ __forceinline__ void mg_clear(char* smem, KLDS uint64_t* ids, KLDS ui
 // resident-merge and write-out, and inside an item chunk c + 1 is loaded before chunk c is
 // applied, so HBM latency overlaps the LDS work; the write-out leaves every delta entry cleared
 // for the next item (no separate table init).
-template <bool CNT1, int NT>
+template <bool CNT1, int NT, bool R12M>
 __global__ __launch_bounds__(NT, 4) void k_part_merge(
     MergeParams q, const uint32_t* __restrict__ work, int64_t nwork, const int64_t* __restrict__ pbase,
     const uint64_t* __restrict__ srec, int first, uint64_t* __restrict__ buf0, uint64_t* __restrict__ buf1,
@@ -1410,7 +1424,7 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t dummy = (uint32_t)H + (uint32_t)lane;
   const bool wide = !CNT1 && q.rw > 2;
-  const bool r12 = q.r12 != 0;  // narrow records arrive in the 12-byte form
+  // R12M: narrow records arrive in the 12-byte form (q.r12)
   const int64_t wbase = wr[0];
   const bool evict = q.windowed && close0 != INT64_MIN;
   KLDS uint64_t* ids = mg_plane<uint64_t>(smem, 0);
@@ -1441,10 +1455,12 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
   }
   int64_t w = blockIdx.x;
   MgItem it{};
-  longlong2 rec[AU], ext[AU], nrec[AU], next[AU];
+  // two register sets: the records of chunk c + 1 are in flight while chunk c is applied
+  MgRaw rawA[AU], rawB[AU];
+  longlong2 extA[AU], extB[AU];
   if (w < nwork) {
     it = mg_item(work, w, pbase);
-    mg_load<AU, NT>(rec, ext, srec, it.rbase, it.rn, 0, q.rw, wide, r12, tbase);
+    mg_load<AU, NT, R12M>(rawA, extA, srec, it.rbase, it.rn, 0, q.rw, wide);
   }
   if (threadIdx.x == 0) lovf = 0;
   lds_barrier();  // otab / wtab / lovf
@@ -1459,7 +1475,7 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
     MgItem nit{};
     if (wnext < nwork) nit = mg_item(work, wnext, pbase);  // its loads are issued now, used later
     if (rn == 0 && first) {  // untouched partition: nothing to rewrite
-      if (wnext < nwork) mg_load<AU, NT>(rec, ext, srec, nit.rbase, nit.rn, 0, q.rw, wide, r12, tbase);
+      if (wnext < nwork) mg_load<AU, NT, R12M>(rawA, extA, srec, nit.rbase, nit.rn, 0, q.rw, wide);
       it = nit;
       continue;
     }
@@ -1503,11 +1519,13 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
       lds_barrier();
     }
     MG_T(1);
-    // 1. this item's records, chunk by chunk (chunk c + 1 in flight while c is applied)
-    for (int64_t l0 = 0; l0 < rn; l0 += (int64_t)AU * NT) {
-      const bool more = l0 + (int64_t)AU * NT < rn;
-      if (more) mg_load<AU, NT>(nrec, next, srec, rbase, rn, l0 + (int64_t)AU * NT, q.rw, wide, r12, tbase);
-      if (*(volatile KLDS int*)&lovf) break;
+    // 1. this item's records, two chunks per round: chunk c + 1 (set B) is loaded before chunk c
+    //    (set A, loaded before the previous item's write-out or in the last round) is applied, and
+    //    chunk c + 2 before chunk c + 1.  Loads are unconditional, so every wait is counted exactly.
+    auto apply_chunk = [&](const MgRaw (&raw)[AU], const longlong2 (&ext)[AU], int64_t l0) {
+      longlong2 rec[AU];
+#pragma unroll
+      for (int u = 0; u < AU; u++) rec[u] = mg_decode<R12M>(raw[u], tbase, l0 + threadIdx.x + (int64_t)u * NT < rn);
       if constexpr (CNT1) {
         // one window per record: w = ts / adv (TUMBLING) or 0 (no window); ts < 0: skip.  The AU
         // identities' CASes are issued back to back; collisions probe on afterwards.
@@ -1673,18 +1691,20 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
           if (*(volatile KLDS int*)&lovf) break;
         }
       }
-      if (more) {
-#pragma unroll
-        for (int u = 0; u < AU; u++) {
-          rec[u] = nrec[u];
-          if (wide) ext[u] = next[u];
-        }
-      }
+    };
+    const int64_t nch = (rn + (int64_t)AU * NT - 1) / ((int64_t)AU * NT);
+    for (int64_t c = 0; c < nch; c += 2) {
+      mg_load<AU, NT, R12M>(rawB, extB, srec, rbase, rn, (c + 1) * AU * NT, q.rw, wide);
+      apply_chunk(rawA, extA, c * AU * NT);
+      if (*(volatile KLDS int*)&lovf || c + 1 >= nch) break;
+      mg_load<AU, NT, R12M>(rawA, extA, srec, rbase, rn, (c + 2) * AU * NT, q.rw, wide);
+      apply_chunk(rawB, extB, (c + 1) * AU * NT);
+      if (*(volatile KLDS int*)&lovf) break;
     }
     lds_barrier();
     MG_T(2);
     // the next item's first chunk is in flight from here on
-    if (wnext < nwork) mg_load<AU, NT>(rec, ext, srec, nit.rbase, nit.rn, 0, q.rw, wide, r12, tbase);
+    if (wnext < nwork) mg_load<AU, NT, R12M>(rawA, extA, srec, nit.rbase, nit.rn, 0, q.rw, wide);
     if (lovf) {  // more groups than the table: retried with 2x sub-passes
       if (threadIdx.x == 0) fail[p] |= 1;
       for (int i = threadIdx.x; i < H; i += NT) mg_clear(smem, ids, rt, otab, q.n_ops, i);
@@ -2639,8 +2659,10 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
       const bool cnt1 = a->ap.n_ops == 1 && a->ap.ops[0].kind == OP_INC && a->ap.ops[0].word == 3 && a->sw == 4 &&
                         s.rw == 2 && a->desc.window_kind != KHIP_WINDOW_HOPPING;
       const int mt = (int)knob("KHIP_MERGE_THREADS", 512);
-      auto mk = mt >= 512 ? (cnt1 ? k_part_merge<true, 512> : k_part_merge<false, 512>)
-                          : (cnt1 ? k_part_merge<true, 256> : k_part_merge<false, 256>);
+      auto mk = mq.r12 ? (mt >= 512 ? (cnt1 ? k_part_merge<true, 512, true> : k_part_merge<false, 512, true>)
+                                    : (cnt1 ? k_part_merge<true, 256, true> : k_part_merge<false, 256, true>))
+                       : (mt >= 512 ? (cnt1 ? k_part_merge<true, 512, false> : k_part_merge<false, 512, false>)
+                                    : (cnt1 ? k_part_merge<true, 256, false> : k_part_merge<false, 256, false>));
       hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, s.m_lds);
       const int64_t grid = std::min<int64_t>(nwork, (int64_t)s.n_cu * knob("KHIP_MERGE_WG_PER_CU", mt >= 512 ? 2 : 4));
       hipLaunchKernelGGL(mk, dim3(grid), dim3(mt >= 512 ? 512 : 256), s.m_lds, a->stream, mq, wk, nwork, s.pbase.as<int64_t>(),
