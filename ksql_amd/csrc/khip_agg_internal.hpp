@@ -332,7 +332,7 @@ struct PartState {
   // two-level scatter: pass-A records, per-tile bucket histogram / offsets, bucket scans
   DevBuf srecA, hcoarse, scan_tmpB, RB;
   // k_part_merge (delta-only LDS): entries, LDS bytes, plane layout (khip_agg_part.hip)
-  int mH = 0, m_lds = 0, rt_off = 0, n_cu = 256;
+  int mH = 0, m_lds = 0, rt_off = 0, m_list_off = 0, n_cu = 256;
   int flag_off = 0;       // k_part_agg: LDS byte offset of the changelog flag plane
   int64_t purged_to = INT64_MIN;  // closed store: expired rows (ws < purged_to) already dropped
   int32_t plane_off[MAX_OPS] = {};

@@ -1205,6 +1205,9 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
 // round trips hidden by the other's LDS work; measured on C2: 256 x 4 needs 2^15 partitions
 // to fit its tables and loses more in the hist/refine than it gains)
 constexpr uint32_t RT_MATCHED = 0x80000000u;
+#ifndef KHIP_MG_AU_CNT1
+#define KHIP_MG_AU_CNT1 4  // k_part_merge COUNT(*) records per thread per chunk
+#endif
 
 struct MergeParams {
   int32_t windowed;
@@ -1230,7 +1233,22 @@ struct MergeParams {
   int32_t dbg;       // tuning build: KHIP_MERGE_DEBUG prints the delta table of touched partitions
   int32_t r12;       // records are R12 (narrow layout; k_part_scatter / k_part_refine wrote them so)
   uint8_t* chg;      // changelog: per-row-slot emission flags (CHG_*), or null
+  int32_t div32;     // windowed with adv <= 2^31: R12 window indices in 32-bit arithmetic (fd32)
+  FastDiv32 fd32;
+  int32_t list_off;  // byte offset of the LDS list of the entries the item's records claimed (u16 x H)
 };
+
+// Append the claimed entries of the wave's lanes to the item's list (one LDS atomic per wave);
+// called by every lane of the wave (convergent).
+__device__ __forceinline__ void mg_list_append(bool claimed, uint32_t e, KLDS uint16_t* nl, int* nnew) {
+  const uint64_t b = __ballot(claimed);
+  if (!b) return;
+  const int lane = threadIdx.x & 63, leader = __ffsll((long long)b) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(nnew, __popcll(b));
+  base = __shfl(base, leader, 64);
+  if (claimed) nl[base + __popcll(b & ((1ULL << lane) - 1))] = (uint16_t)e;
+}
 
 __device__ __forceinline__ uint32_t mg_slot(uint64_t id, int H) {
   const uint32_t h = ((uint32_t)id * 0x9E3779B1u) ^ (uint32_t)(id >> 32) * 0x85EBCA77u;
@@ -1356,10 +1374,15 @@ struct MgItem {
   uint32_t p;
   int sbits, sub;
   int64_t rbase, rn;
+  int64_t nrow;  // the partition's resident rows
+  bool sel;      // which ping-pong buffer holds them
 };
 
+// The work item's descriptor, read one item ahead with wave-uniform (scalar) loads: a vector
+// load here would, at its first use, wait for every store the previous item's write-out issued.
 __device__ __forceinline__ MgItem mg_item(const uint32_t* __restrict__ work, int64_t w,
-                                          const int64_t* __restrict__ pbase) {
+                                          const int64_t* __restrict__ pbase, const uint8_t* __restrict__ sel,
+                                          const int64_t* __restrict__ cnt) {
   MgItem it;
   if (work) {
     const uint32_t x = work[w];
@@ -1371,8 +1394,11 @@ __device__ __forceinline__ MgItem mg_item(const uint32_t* __restrict__ work, int
     it.sbits = 0;
     it.sub = 0;
   }
+  it.p = __builtin_amdgcn_readfirstlane(it.p);
   it.rbase = pbase[it.p];
   it.rn = pbase[it.p + 1] - it.rbase;
+  it.nrow = cnt[it.p];
+  it.sel = ((((const uint32_t*)sel)[it.p >> 2] >> (8 * (it.p & 3))) & 0xFFu) != 0;  // sel: P >= 64 bytes
   return it;
 }
 
@@ -1412,13 +1438,18 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
   if (wr[4] == 0) return;  // k_part_wrange declined the merge path for this push
   unsigned long long t_last = wall_clock64();
   const int64_t tbase = wr[5];
+  // R12 records: window index relative to wbase = qw0 + (r0 + trel - 1) / adv in 32-bit arithmetic
+  // (trel < 2^31, r0 < adv <= 2^31), with tbase = q0 * adv + r0 and qw0 = q0 - wbase
+  const int64_t q0 = q.windowed ? (int64_t)fast_udiv((uint64_t)tbase, q.fd) : 0;
+  const uint32_t r0 = (uint32_t)(tbase - q0 * q.adv);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int lovf;
+  __shared__ int nnew;  // entries claimed by the item's records (listed in nl)
   __shared__ int wsum[NT / 64];
   __shared__ unsigned long long lbase;
   __shared__ MgWord wtab[32];
   __shared__ MgOp otab[MAX_OPS];
-  constexpr int AU = CNT1 ? 4 : 2;  // records per thread per chunk (two chunks in registers)
+  constexpr int AU = CNT1 ? KHIP_MG_AU_CNT1 : 2;  // records per thread per chunk (two chunks in registers)
   constexpr int NW = NT / 64;
   const int H = q.H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1426,10 +1457,12 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
   const bool wide = !CNT1 && q.rw > 2;
   // R12M: narrow records arrive in the 12-byte form (q.r12)
   const int64_t wbase = wr[0];
+  const int64_t qw0 = q0 - wbase;
   const bool evict = q.windowed && close0 != INT64_MIN;
   KLDS uint64_t* ids = mg_plane<uint64_t>(smem, 0);
   KLDS uint32_t* rt = mg_plane<uint32_t>(smem, q.rt_off);
   KLDS uint32_t* cnt1 = mg_plane<uint32_t>(smem, q.plane_off[0]);  // CNT1: the COUNT(*) deltas
+  KLDS uint16_t* nl = mg_plane<uint16_t>(smem, q.list_off);
   if (threadIdx.x < q.n_ops) {
     const int o = threadIdx.x;
     MgOp t;
@@ -1459,11 +1492,14 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
   MgRaw rawA[AU], rawB[AU];
   longlong2 extA[AU], extB[AU];
   if (w < nwork) {
-    it = mg_item(work, w, pbase);
+    it = mg_item(work, w, pbase, sel, cnt);
     mg_load<AU, NT, R12M>(rawA, extA, srec, it.rbase, it.rn, 0, q.rw, wide);
   }
-  if (threadIdx.x == 0) lovf = 0;
-  lds_barrier();  // otab / wtab / lovf
+  if (threadIdx.x == 0) {
+    lovf = 0;
+    nnew = 0;
+  }
+  lds_barrier();  // otab / wtab / lovf / nnew
   for (int i = threadIdx.x; i < H + 64; i += NT) mg_clear(smem, ids, rt, otab, q.n_ops, i);
   lds_barrier();
   MG_T(0);
@@ -1473,14 +1509,14 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
     const int64_t rbase = it.rbase, rn = it.rn;
     const int64_t wnext = w + gridDim.x;
     MgItem nit{};
-    if (wnext < nwork) nit = mg_item(work, wnext, pbase);  // its loads are issued now, used later
+    if (wnext < nwork) nit = mg_item(work, wnext, pbase, sel, cnt);  // its loads are issued now, used later
     if (rn == 0 && first) {  // untouched partition: nothing to rewrite
       if (wnext < nwork) mg_load<AU, NT, R12M>(rawA, extA, srec, nit.rbase, nit.rn, 0, q.rw, wide);
       it = nit;
       continue;
     }
-    const uint64_t* src = (sel[p] ? buf1 : buf0) + (uint64_t)p * q.cmax * q.sw;
-    const int64_t nrow = cnt[p];
+    const uint64_t* src = (it.sel ? buf1 : buf0) + (uint64_t)p * q.cmax * q.sw;
+    const int64_t nrow = it.nrow;
     // 0. closed resident rows → closed store (pass 0 only; retries skip them)
     if (evict && first) {
       int ne = 0, nh = 0;
@@ -1536,9 +1572,15 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
         for (int u = 0; u < AU; u++) {
           const int64_t t = rec[u].y;
           const uint64_t hk = (uint64_t)rec[u].x;
-          const int64_t widx = q.windowed ? (int64_t)fast_udiv((uint64_t)(t < 0 ? 0 : t), q.fd) : 0;
-          const bool act = t >= 0 && (sbits == 0 || sub_ok(hk, widx * q.adv, sbits, sub));
-          id[u] = act ? ident_of(hk, widx - wbase, q.log2P) : EMPTY_ID;
+          int64_t wrel;  // window index - wbase
+          if (R12M && q.div32) {
+            const uint32_t trel = raw[u].w[2];
+            wrel = qw0 + (int64_t)fast_udiv32(r0 + trel - 1u, q.fd32);
+          } else {
+            wrel = (q.windowed ? (int64_t)fast_udiv((uint64_t)(t < 0 ? 0 : t), q.fd) : 0) - wbase;
+          }
+          const bool act = t >= 0 && (sbits == 0 || sub_ok(hk, (wrel + wbase) * q.adv, sbits, sub));
+          id[u] = act ? ident_of(hk, wrel, q.log2P) : EMPTY_ID;
           e[u] = act ? mg_slot(id[u], H) : dummy;
         }
 #pragma unroll
@@ -1548,7 +1590,10 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
         }
 #pragma unroll
-        for (int u = 0; u < AU; u++) pend[u] = old[u] != EMPTY_ID && old[u] != id[u];
+        for (int u = 0; u < AU; u++) {
+          pend[u] = old[u] != EMPTY_ID && old[u] != id[u];
+          mg_list_append(id[u] != EMPTY_ID && old[u] == EMPTY_ID, e[u], nl, &nnew);
+        }
         for (int probes = 1;; probes++) {
           bool anyp = false;
 #pragma unroll
@@ -1558,20 +1603,25 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
             lovf = 1;
             break;
           }
+          bool got[AU];
 #pragma unroll
           for (int u = 0; u < AU; u++) {
+            got[u] = false;
             if (!pend[u]) continue;
             e[u] = e[u] + 1 == (uint32_t)H ? 0u : e[u] + 1;
             uint64_t o2 = EMPTY_ID;
             __hip_atomic_compare_exchange_strong(&ids[e[u]], &o2, id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
             pend[u] = o2 != EMPTY_ID && o2 != id[u];
+            got[u] = o2 == EMPTY_ID;
           }
+#pragma unroll
+          for (int u = 0; u < AU; u++) mg_list_append(got[u], e[u], nl, &nnew);
         }
 #pragma unroll
         for (int u = 0; u < AU; u++) {
           if (id[u] == EMPTY_ID || pend[u]) continue;
-          __hip_atomic_fetch_max(&rt[e[u]], (uint32_t)(rec[u].y - tbase + 1), WG_RLX);
+          __hip_atomic_fetch_max(&rt[e[u]], R12M ? raw[u].w[2] : (uint32_t)(rec[u].y - tbase + 1), WG_RLX);
           __hip_atomic_fetch_add(&cnt1[e[u]], 1u, WG_RLX);
         }
       } else {
@@ -1623,7 +1673,10 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
           }
           bool pend[AU];
 #pragma unroll
-          for (int u = 0; u < AU; u++) pend[u] = act[u] && old[u] != EMPTY_ID && old[u] != id[u];
+          for (int u = 0; u < AU; u++) {
+            pend[u] = act[u] && old[u] != EMPTY_ID && old[u] != id[u];
+            mg_list_append(act[u] && old[u] == EMPTY_ID, e[u], nl, &nnew);
+          }
           for (int probes = 1;; probes++) {
             bool anyp = false;
 #pragma unroll
@@ -1635,15 +1688,20 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
               for (int u = 0; u < AU; u++) act[u] = false;
               break;
             }
+            bool got[AU];
 #pragma unroll
             for (int u = 0; u < AU; u++) {
+              got[u] = false;
               if (!pend[u]) continue;
               e[u] = e[u] + 1 == (uint32_t)H ? 0u : e[u] + 1;
               uint64_t o2 = EMPTY_ID;
               __hip_atomic_compare_exchange_strong(&ids[e[u]], &o2, id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
               pend[u] = o2 != EMPTY_ID && o2 != id[u];
+              got[u] = o2 == EMPTY_ID;
             }
+#pragma unroll
+            for (int u = 0; u < AU; u++) mg_list_append(got[u], e[u], nl, &nnew);
           }
 #pragma unroll
           for (int u = 0; u < AU; u++) {
@@ -1709,7 +1767,10 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
       if (threadIdx.x == 0) fail[p] |= 1;
       for (int i = threadIdx.x; i < H; i += NT) mg_clear(smem, ids, rt, otab, q.n_ops, i);
       lds_barrier();
-      if (threadIdx.x == 0) lovf = 0;
+      if (threadIdx.x == 0) {
+        lovf = 0;
+        nnew = 0;
+      }
       lds_barrier();
       it = nit;
       continue;
@@ -1724,7 +1785,8 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
       n_mine += e != -2 ? 1 : 0;
     }
     lds_barrier();
-    for (int i = threadIdx.x; i < H; i += NT) n_mine += (ids[i] != EMPTY_ID && !(rt[i] & RT_MATCHED)) ? 1 : 0;
+    const int nn = nnew;  // read by every thread here; reset after the next barrier
+    for (int i = threadIdx.x; i < nn; i += NT) n_mine += !(rt[nl[i]] & RT_MATCHED) ? 1 : 0;
     // 3. per-wave row counts → the partition's region range (one atomic per work item)
     const int wave_rows = (int)wave_sum(n_mine);
     if (lane == 0) wsum[wave] = wave_rows;
@@ -1748,6 +1810,7 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
       if (threadIdx.x == 0) {
         fail[p] |= 2;
         atomicMax(need, (unsigned long long)(lbase + total));
+        nnew = 0;
       }
       for (int i = threadIdx.x; i < H; i += NT) mg_clear(smem, ids, rt, otab, q.n_ops, i);
       lds_barrier();
@@ -1756,7 +1819,7 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
     }
     // 4. write: lanes take ranks from ballots so consecutive lanes store consecutive rows; each
     //    wave owns a contiguous output range.  Delta entries are cleared once consumed.
-    uint64_t* dst0 = (sel[p] ? buf0 : buf1) + (uint64_t)p * q.cmax * q.sw;
+    uint64_t* dst0 = (it.sel ? buf0 : buf1) + (uint64_t)p * q.cmax * q.sw;
     uint64_t cur = lbase + (uint64_t)wave_before;
     const uint64_t lt = (1ULL << lane) - 1;
     const int hv = q.having.a.w_val, hc = q.having.a.w_cnt;
@@ -1804,9 +1867,11 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
       cur += __popcll(b);
     }
     lds_barrier();  // resident rows have read their entries: the loop below clears them all
-    for (int i0 = wave * 64; i0 < H; i0 += NT) {  // delta entries, 64 per wave step
-      const int e = i0 + lane;
-      const uint64_t id = e < H ? ids[e] : EMPTY_ID;
+    if (threadIdx.x == 0) nnew = 0;  // every thread read it (nn) before the barrier above
+    for (int i0 = wave * 64; i0 < nn; i0 += NT) {  // the claimed entries, 64 per wave step
+      const int li = i0 + lane;
+      const int e = li < nn ? (int)nl[li] : H + lane;  // past the list: the lane's dummy entry
+      const uint64_t id = li < nn ? ids[e] : EMPTY_ID;
       const bool isnew = id != EMPTY_ID && !(rt[e] & RT_MATCHED);
       const uint64_t b = __ballot(isnew);
       if (isnew) {
@@ -2174,7 +2239,7 @@ khip_status part_init(khip_agg* a, int64_t hint) {
   {
     int n64 = 0, n32 = 0;
     for (int o = 0; o < a->ap.n_ops; o++) (a->ap.ops[o].kind == OP_INC || a->ap.ops[o].kind == OP_INC_VALID ? n32 : n64)++;
-    const int mentry = 8 + 8 * n64 + 4 + 4 * n32;
+    const int mentry = 8 + 8 * n64 + 4 + 4 * n32 + 2;  // + the u16 claimed-entry list
     const int64_t mbudget = knob("KHIP_MERGE_LDS_KB", 76) * 1024;  // two persistent workgroups per CU
     int mH = (int)std::min<int64_t>(16384, mbudget / mentry - 64) & ~63;
     s.mH = mH;
@@ -2194,6 +2259,8 @@ khip_status part_init(khip_agg* a, int64_t hint) {
         s.plane_w64[o] = 0;
         off += ms * 4;
       }
+    s.m_list_off = off;
+    off += (mH * 2 + 15) & ~15;
     s.m_lds = off;
     for (int w = 0; w < 32; w++) s.word_op[w] = -1;
     for (int o = 0; o < a->ap.n_ops; o++) s.word_op[a->ap.ops[o].word] = (int8_t)o;
@@ -2590,6 +2657,8 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     mq.size = q0.size;
     mq.adv = q0.adv;
     mq.fd = q0.fd;
+    mq.div32 = a->windowed && q0.adv <= (int64_t)1 << 31 ? 1 : 0;
+    mq.fd32 = make_fastdiv32((uint32_t)(mq.div32 ? q0.adv : 1));
     for (int c = 0; c < MAX_COLS; c++) {
       mq.col_word[c] = s.col_word[c];
       mq.col_type[c] = a->ap.col_type[c];
@@ -2600,6 +2669,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
       mq.plane_w64[o] = s.plane_w64[o];
     }
     mq.rt_off = s.rt_off;
+    mq.list_off = s.m_list_off;
     mq.lds_bytes = s.m_lds;
     mq.init = a->init;
     mq.having = a->having;

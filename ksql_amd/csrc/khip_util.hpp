@@ -199,6 +199,31 @@ __host__ __device__ inline uint64_t fast_udiv(uint64_t n, const FastDiv& f) {
   return (t + ((n - t) >> f.sh1)) >> f.sh2;
 }
 
+// 32-bit variant for dividends below 2^32 (window indices relative to a push's time base):
+// q = (hi32(m * n) + ((n - hi) >> sh1)) >> sh2, d in [1, 2^31].
+struct FastDiv32 {
+  uint32_t m, sh1, sh2;
+};
+
+inline FastDiv32 make_fastdiv32(uint32_t d) {
+  uint32_t l = 0;
+  while (l < 32 && (1ULL << l) < d) l++;
+  FastDiv32 f;
+  f.m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1);
+  f.sh1 = l < 1 ? l : 1;
+  f.sh2 = l > 1 ? l - 1 : 0;
+  return f;
+}
+
+__host__ __device__ inline uint32_t fast_udiv32(uint32_t n, const FastDiv32& f) {
+#ifdef __HIP_DEVICE_COMPILE__
+  const uint32_t t = __umulhi(f.m, n);
+#else
+  const uint32_t t = (uint32_t)(((uint64_t)f.m * n) >> 32);
+#endif
+  return (t + ((n - t) >> f.sh1)) >> f.sh2;
+}
+
 // first_window_start with the division by `adv` done through `fd` (= make_fastdiv(adv)).
 __host__ __device__ inline int64_t first_window_start_fd(int64_t ts, int64_t size, int64_t adv, const FastDiv& fd) {
   int64_t lo = ts - size + adv;
