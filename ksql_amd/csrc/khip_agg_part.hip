@@ -1208,6 +1208,9 @@ constexpr uint32_t RT_MATCHED = 0x80000000u;
 #ifndef KHIP_MG_AU_CNT1
 #define KHIP_MG_AU_CNT1 4  // k_part_merge COUNT(*) records per thread per chunk
 #endif
+#ifndef KHIP_MG_AU_GEN
+#define KHIP_MG_AU_GEN 2   // k_part_merge (other update sets) records per thread per chunk
+#endif
 
 struct MergeParams {
   int32_t windowed;
@@ -1236,6 +1239,7 @@ struct MergeParams {
   int32_t div32;     // windowed with adv <= 2^31: R12 window indices in 32-bit arithmetic (fd32)
   FastDiv32 fd32;
   int32_t list_off;  // byte offset of the LDS list of the entries the item's records claimed (u16 x H)
+  int32_t fan;       // most windows a record can fall in (ceil(size / advance); 1 without windows)
 };
 
 // Append the claimed entries of the wave's lanes to the item's list (one LDS atomic per wave);
@@ -1271,6 +1275,8 @@ struct MgOp {  // one update op, as the record phase needs it
   int32_t cw;   // record word of the op's column
   int32_t dbl;  // DOUBLE column (MIN/MAX on the total-order key)
 };
+
+constexpr int MG_FB = 6;  // k_part_merge: fan-outs up to this issue a record's window CASes together
 
 struct MgWord {
   int32_t kind;
@@ -1337,12 +1343,26 @@ struct MgRaw {
   uint32_t w[4];  // R12: key hash lo, hi, trel; 16-byte record: key hash lo, hi, ts lo, hi
 };
 
-template <int AU, int NT, bool R12M>
+// Record of chunk l0 taken by this thread's unit u.  STRIDE: a wave's 64 lanes take records
+// AU * NT / 64 apart (the whole chunk) instead of 64 consecutive ones: a partition's records are in
+// arrival order, and with few keys per partition consecutive records update the same (key, window)
+// entries — same-address LDS atomics that serialize (C3: 6 keys per partition, ~14 bank-conflict
+// cycles per LDS instruction with consecutive records).  Only items of at least one full chunk
+// stride (stride = rn >= AU * NT, uniform): in a smaller item every record is in one wave and the
+// lanes' same-address atomics apply in arrival order, as the reference's sequential DOUBLE sums do
+// (the QTT comparator's 1e-6 absolute tolerance on large sums needs that order).
+template <int AU, int NT, bool STRIDE>
+__device__ __forceinline__ int64_t mg_li(int64_t l0, int u, bool stride) {
+  if (STRIDE && stride) return l0 + (int64_t)(threadIdx.x & 63) * (AU * NT / 64) + (int64_t)(threadIdx.x >> 6) * AU + u;
+  return l0 + threadIdx.x + (int64_t)u * NT;
+}
+
+template <int AU, int NT, bool R12M, bool STRIDE>
 __device__ __forceinline__ void mg_load(MgRaw (&raw)[AU], longlong2 (&ext)[AU], const uint64_t* __restrict__ srec,
                                         int64_t rbase, int64_t rn, int64_t l0, int rw, bool wide) {
 #pragma unroll
   for (int u = 0; u < AU; u++) {
-    const int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
+    const int64_t li = mg_li<AU, NT, STRIDE>(l0, u, rn >= AU * NT);
     const uint64_t idx = (uint64_t)(rbase + (li < rn ? li : (rn > 0 ? rn - 1 : 0)));
     if constexpr (R12M) {  // a compile-time choice: a run-time one merges both paths' registers,
                            // which consumes the loaded words at the load
@@ -1449,7 +1469,7 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
   __shared__ unsigned long long lbase;
   __shared__ MgWord wtab[32];
   __shared__ MgOp otab[MAX_OPS];
-  constexpr int AU = CNT1 ? KHIP_MG_AU_CNT1 : 2;  // records per thread per chunk (two chunks in registers)
+  constexpr int AU = CNT1 ? KHIP_MG_AU_CNT1 : KHIP_MG_AU_GEN;  // records per thread per chunk (two chunks in registers)
   constexpr int NW = NT / 64;
   const int H = q.H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1493,13 +1513,34 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
   longlong2 extA[AU], extB[AU];
   if (w < nwork) {
     it = mg_item(work, w, pbase, sel, cnt);
-    mg_load<AU, NT, R12M>(rawA, extA, srec, it.rbase, it.rn, 0, q.rw, wide);
+    mg_load<AU, NT, R12M, !CNT1>(rawA, extA, srec, it.rbase, it.rn, 0, q.rw, wide);
   }
   if (threadIdx.x == 0) {
     lovf = 0;
     nnew = 0;
   }
   lds_barrier();  // otab / wtab / lovf / nnew
+  // One argument column (every op on it, plus COUNT(*)): the ops' plane offsets in wave-uniform
+  // registers, so a (record, window) update is straight-line code with no op-table reads (C3:
+  // COUNT / SUM / MIN / MAX of one DOUBLE).  -1 = op absent.  Other shapes walk otab.
+  int oc_star = -1, oc_cnt = -1, oc_sum = -1, oc_min = -1, oc_max = -1, oc_col = -1, oc_cw = 3, oc_f64 = 0;
+  bool onecol = true;
+  for (int o = 0; o < q.n_ops; o++) {
+    const MgOp t = otab[o];
+    if (t.kind == OP_INC) {
+      oc_star = t.off;
+      continue;
+    }
+    if (oc_col >= 0 && t.col != oc_col) onecol = false;
+    oc_col = t.col;
+    oc_cw = t.cw;
+    oc_f64 = t.dbl;
+    if (t.kind == OP_INC_VALID) oc_cnt = t.off;
+    else if (t.kind == OP_ADD_I64 || t.kind == OP_ADD_F64) oc_sum = t.off, oc_f64 = t.kind == OP_ADD_F64;
+    else if (t.kind == OP_MIN) oc_min = t.off;
+    else if (t.kind == OP_MAX) oc_max = t.off;
+  }
+  const bool dbl_col = oc_col >= 0 && q.col_type[oc_col < 0 ? 0 : oc_col] == KHIP_TYPE_DOUBLE;
   for (int i = threadIdx.x; i < H + 64; i += NT) mg_clear(smem, ids, rt, otab, q.n_ops, i);
   lds_barrier();
   MG_T(0);
@@ -1511,7 +1552,7 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
     MgItem nit{};
     if (wnext < nwork) nit = mg_item(work, wnext, pbase, sel, cnt);  // its loads are issued now, used later
     if (rn == 0 && first) {  // untouched partition: nothing to rewrite
-      if (wnext < nwork) mg_load<AU, NT, R12M>(rawA, extA, srec, nit.rbase, nit.rn, 0, q.rw, wide);
+      if (wnext < nwork) mg_load<AU, NT, R12M, !CNT1>(rawA, extA, srec, nit.rbase, nit.rn, 0, q.rw, wide);
       it = nit;
       continue;
     }
@@ -1561,7 +1602,7 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
     auto apply_chunk = [&](const MgRaw (&raw)[AU], const longlong2 (&ext)[AU], int64_t l0) {
       longlong2 rec[AU];
 #pragma unroll
-      for (int u = 0; u < AU; u++) rec[u] = mg_decode<R12M>(raw[u], tbase, l0 + threadIdx.x + (int64_t)u * NT < rn);
+      for (int u = 0; u < AU; u++) rec[u] = mg_decode<R12M>(raw[u], tbase, mg_li<AU, NT, !CNT1>(l0, u, rn >= AU * NT) < rn);
       if constexpr (CNT1) {
         // one window per record: w = ts / adv (TUMBLING) or 0 (no window); ts < 0: skip.  The AU
         // identities' CASes are issued back to back; collisions probe on afterwards.
@@ -1648,121 +1689,207 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
             wn[u] = 0;
           }
         }
-        for (int64_t j = 0;; j++) {
-          bool any = false;
-          bool act[AU];
-          uint64_t id[AU];
-          uint32_t e[AU];
-#pragma unroll
-          for (int u = 0; u < AU; u++) {
-            const int64_t widx = w0[u] + j;
-            const uint64_t hk = (uint64_t)rec[u].x;  // the scatter stores the key hash
-            const bool has = widx <= wn[u];
-            any |= has;
-            act[u] = has && (sbits == 0 || sub_ok(hk, widx * q.adv, sbits, sub));
-            id[u] = act[u] ? ident_of(hk, widx - wbase, q.log2P) : EMPTY_ID;
-            e[u] = act[u] ? mg_slot(id[u], H) : dummy;
-          }
-          if (!__ballot(any)) break;
-          uint64_t old[AU];
-#pragma unroll
-          for (int u = 0; u < AU; u++) {
-            old[u] = EMPTY_ID;
-            __hip_atomic_compare_exchange_strong(&ids[e[u]], &old[u], id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
-          bool pend[AU];
-#pragma unroll
-          for (int u = 0; u < AU; u++) {
-            pend[u] = act[u] && old[u] != EMPTY_ID && old[u] != id[u];
-            mg_list_append(act[u] && old[u] == EMPTY_ID, e[u], nl, &nnew);
-          }
-          for (int probes = 1;; probes++) {
-            bool anyp = false;
-#pragma unroll
-            for (int u = 0; u < AU; u++) anyp |= pend[u];
-            if (!__ballot(anyp)) break;
-            if (probes >= H) {
-              lovf = 1;
-#pragma unroll
-              for (int u = 0; u < AU; u++) act[u] = false;
-              break;
+        // one (record u, window) update into delta entry ent: row time, then the update ops
+        auto upd = [&](int u, uint32_t ent) {
+          __hip_atomic_fetch_max(&rt[ent], trel[u], WG_RLX);
+          const uint32_t vmask = q.meta_word == 2 ? ((uint32_t)ext[u].x >> 16) : 0u;
+          const int64_t gi = rbase + mg_li<AU, NT, !CNT1>(l0, u, rn >= AU * NT);
+          auto apply_op = [&](const MgOp op) {
+            if (op.kind == OP_INC) {
+              __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, op.off)[ent], 1u, WG_RLX);
+              return;
             }
-            bool got[AU];
-#pragma unroll
-            for (int u = 0; u < AU; u++) {
-              got[u] = false;
-              if (!pend[u]) continue;
-              e[u] = e[u] + 1 == (uint32_t)H ? 0u : e[u] + 1;
-              uint64_t o2 = EMPTY_ID;
-              __hip_atomic_compare_exchange_strong(&ids[e[u]], &o2, id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-              pend[u] = o2 != EMPTY_ID && o2 != id[u];
-              got[u] = o2 == EMPTY_ID;
+            if (!((vmask >> op.col) & 1u)) return;
+            if (op.kind == OP_INC_VALID) {
+              __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, op.off)[ent], 1u, WG_RLX);
+              return;
             }
-#pragma unroll
-            for (int u = 0; u < AU; u++) mg_list_append(got[u], e[u], nl, &nnew);
-          }
-#pragma unroll
-          for (int u = 0; u < AU; u++) {
-            if (!act[u]) continue;
-            __hip_atomic_fetch_max(&rt[e[u]], trel[u], WG_RLX);
-            const uint32_t vmask = q.meta_word == 2 ? ((uint32_t)ext[u].x >> 16) : 0u;
-            const int64_t gi = rbase + l0 + threadIdx.x + (int64_t)u * NT;
-            for (int o = 0; o < q.n_ops; o++) {
-              const MgOp op = otab[o];
-              if (op.kind == OP_INC) {
-                __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, op.off)[e[u]], 1u, WG_RLX);
-                continue;
+            const int64_t raw = op.cw == 3 ? ext[u].y : (int64_t)srec[(uint64_t)gi * q.rw + op.cw];
+            KLDS int64_t* pl = mg_plane<int64_t>(smem, op.off);
+            switch (op.kind) {
+              case OP_ADD_I64: __hip_atomic_fetch_add((KLDS uint64_t*)&pl[ent], (uint64_t)raw, WG_RLX); break;
+              case OP_ADD_F64: {
+                double d;
+                __builtin_memcpy(&d, &raw, 8);
+                __hip_atomic_fetch_add((KLDS double*)&pl[ent], d, WG_RLX);
+                break;
               }
-              if (!((vmask >> op.col) & 1u)) continue;
-              if (op.kind == OP_INC_VALID) {
-                __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, op.off)[e[u]], 1u, WG_RLX);
-                continue;
-              }
-              const int64_t raw = op.cw == 3 ? ext[u].y : (int64_t)srec[(uint64_t)gi * q.rw + op.cw];
-              KLDS int64_t* pl = mg_plane<int64_t>(smem, op.off);
-              switch (op.kind) {
-                case OP_ADD_I64: __hip_atomic_fetch_add((KLDS uint64_t*)&pl[e[u]], (uint64_t)raw, WG_RLX); break;
-                case OP_ADD_F64: {
+              case OP_MIN:
+              case OP_MAX: {
+                int64_t k = raw;
+                if (op.dbl) {
                   double d;
                   __builtin_memcpy(&d, &raw, 8);
-                  __hip_atomic_fetch_add((KLDS double*)&pl[e[u]], d, WG_RLX);
-                  break;
+                  k = f64_order_key(d);
                 }
-                case OP_MIN:
-                case OP_MAX: {
-                  int64_t k = raw;
-                  if (op.dbl) {
-                    double d;
-                    __builtin_memcpy(&d, &raw, 8);
-                    k = f64_order_key(d);
-                  }
-                  if (op.kind == OP_MIN) __hip_atomic_fetch_min(&pl[e[u]], k, WG_RLX);
-                  else __hip_atomic_fetch_max(&pl[e[u]], k, WG_RLX);
-                  break;
-                }
-                default: break;
+                if (op.kind == OP_MIN) __hip_atomic_fetch_min(&pl[ent], k, WG_RLX);
+                else __hip_atomic_fetch_max(&pl[ent], k, WG_RLX);
+                break;
+              }
+              default: break;
+            }
+          };
+          if (onecol) {
+            if (oc_star >= 0) __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, oc_star)[ent], 1u, WG_RLX);
+            if (oc_col >= 0 && ((vmask >> oc_col) & 1u)) {
+              if (oc_cnt >= 0) __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, oc_cnt)[ent], 1u, WG_RLX);
+              const int64_t raw = oc_cw == 3 ? ext[u].y : (int64_t)srec[(uint64_t)gi * q.rw + oc_cw];
+              double d;
+              __builtin_memcpy(&d, &raw, 8);
+              if (oc_sum >= 0) {
+                if (oc_f64) __hip_atomic_fetch_add(&mg_plane<double>(smem, oc_sum)[ent], d, WG_RLX);
+                else __hip_atomic_fetch_add(&mg_plane<uint64_t>(smem, oc_sum)[ent], (uint64_t)raw, WG_RLX);
+              }
+              const int64_t k = dbl_col ? f64_order_key(d) : raw;
+              if (oc_min >= 0) __hip_atomic_fetch_min(&mg_plane<int64_t>(smem, oc_min)[ent], k, WG_RLX);
+              if (oc_max >= 0) __hip_atomic_fetch_max(&mg_plane<int64_t>(smem, oc_max)[ent], k, WG_RLX);
+            }
+          } else {
+            for (int o = 0; o < q.n_ops; o++) apply_op(otab[o]);
+          }
+        };
+        if (q.fan <= MG_FB) {
+          // every window of a record at once: its identity CASes are in flight together, so a
+          // thread waits for LDS results once per record instead of once per window (LDS results
+          // return in order: a CAS's wait also covers every atomic issued before it)
+#pragma unroll
+          for (int u = 0; u < AU; u++) {
+            uint64_t id[MG_FB], old[MG_FB];
+            uint32_t e[MG_FB];
+            bool act[MG_FB], pend[MG_FB];
+            const uint64_t hk = (uint64_t)rec[u].x;
+#pragma unroll
+            for (int j = 0; j < MG_FB; j++) {
+              const int64_t widx = w0[u] + j;
+              act[j] = j < q.fan && widx <= wn[u] && (sbits == 0 || sub_ok(hk, widx * q.adv, sbits, sub));
+              id[j] = act[j] ? ident_of(hk, widx - wbase, q.log2P) : EMPTY_ID;
+              e[j] = act[j] ? mg_slot(id[j], H) : dummy;
+            }
+#pragma unroll
+            for (int j = 0; j < MG_FB; j++) {
+              if (j >= q.fan) break;
+              old[j] = EMPTY_ID;
+              __hip_atomic_compare_exchange_strong(&ids[e[j]], &old[j], id[j], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+#pragma unroll
+            for (int j = 0; j < MG_FB; j++) {
+              if (j >= q.fan) break;
+              pend[j] = act[j] && old[j] != EMPTY_ID && old[j] != id[j];
+              mg_list_append(act[j] && old[j] == EMPTY_ID, e[j], nl, &nnew);
+            }
+            for (int probes = 1;; probes++) {  // collisions: every pending window probes on together
+              bool anyp = false;
+#pragma unroll
+              for (int j = 0; j < MG_FB; j++) anyp |= j < q.fan && pend[j];
+              if (!__ballot(anyp)) break;
+              if (probes >= H) {
+                lovf = 1;
+#pragma unroll
+                for (int j = 0; j < MG_FB; j++) act[j] = false;
+                break;
+              }
+              bool got[MG_FB];
+#pragma unroll
+              for (int j = 0; j < MG_FB; j++) {
+                got[j] = false;
+                if (j >= q.fan || !pend[j]) continue;
+                e[j] = e[j] + 1 == (uint32_t)H ? 0u : e[j] + 1;
+                uint64_t o2 = EMPTY_ID;
+                __hip_atomic_compare_exchange_strong(&ids[e[j]], &o2, id[j], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+                pend[j] = o2 != EMPTY_ID && o2 != id[j];
+                got[j] = o2 == EMPTY_ID;
+              }
+#pragma unroll
+              for (int j = 0; j < MG_FB; j++) {
+                if (j >= q.fan) break;
+                mg_list_append(got[j], e[j], nl, &nnew);
               }
             }
+#pragma unroll
+            for (int j = 0; j < MG_FB; j++) {
+              if (j >= q.fan) break;
+              if (act[j]) upd(u, e[j]);
+            }
           }
-          if (*(volatile KLDS int*)&lovf) break;
+        } else {
+          for (int64_t j = 0;; j++) {
+            bool any = false;
+            bool act[AU];
+            uint64_t id[AU];
+            uint32_t e[AU];
+  #pragma unroll
+            for (int u = 0; u < AU; u++) {
+              const int64_t widx = w0[u] + j;
+              const uint64_t hk = (uint64_t)rec[u].x;  // the scatter stores the key hash
+              const bool has = widx <= wn[u];
+              any |= has;
+              act[u] = has && (sbits == 0 || sub_ok(hk, widx * q.adv, sbits, sub));
+              id[u] = act[u] ? ident_of(hk, widx - wbase, q.log2P) : EMPTY_ID;
+              e[u] = act[u] ? mg_slot(id[u], H) : dummy;
+            }
+            if (!__ballot(any)) break;
+            uint64_t old[AU];
+  #pragma unroll
+            for (int u = 0; u < AU; u++) {
+              old[u] = EMPTY_ID;
+              __hip_atomic_compare_exchange_strong(&ids[e[u]], &old[u], id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            bool pend[AU];
+  #pragma unroll
+            for (int u = 0; u < AU; u++) {
+              pend[u] = act[u] && old[u] != EMPTY_ID && old[u] != id[u];
+              mg_list_append(act[u] && old[u] == EMPTY_ID, e[u], nl, &nnew);
+            }
+            for (int probes = 1;; probes++) {
+              bool anyp = false;
+  #pragma unroll
+              for (int u = 0; u < AU; u++) anyp |= pend[u];
+              if (!__ballot(anyp)) break;
+              if (probes >= H) {
+                lovf = 1;
+  #pragma unroll
+                for (int u = 0; u < AU; u++) act[u] = false;
+                break;
+              }
+              bool got[AU];
+  #pragma unroll
+              for (int u = 0; u < AU; u++) {
+                got[u] = false;
+                if (!pend[u]) continue;
+                e[u] = e[u] + 1 == (uint32_t)H ? 0u : e[u] + 1;
+                uint64_t o2 = EMPTY_ID;
+                __hip_atomic_compare_exchange_strong(&ids[e[u]], &o2, id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+                pend[u] = o2 != EMPTY_ID && o2 != id[u];
+                got[u] = o2 == EMPTY_ID;
+              }
+  #pragma unroll
+              for (int u = 0; u < AU; u++) mg_list_append(got[u], e[u], nl, &nnew);
+            }
+  #pragma unroll
+            for (int u = 0; u < AU; u++)
+              if (act[u]) upd(u, e[u]);
+            if (*(volatile KLDS int*)&lovf) break;
+          }
         }
       }
     };
     const int64_t nch = (rn + (int64_t)AU * NT - 1) / ((int64_t)AU * NT);
     for (int64_t c = 0; c < nch; c += 2) {
-      mg_load<AU, NT, R12M>(rawB, extB, srec, rbase, rn, (c + 1) * AU * NT, q.rw, wide);
+      mg_load<AU, NT, R12M, !CNT1>(rawB, extB, srec, rbase, rn, (c + 1) * AU * NT, q.rw, wide);
       apply_chunk(rawA, extA, c * AU * NT);
       if (*(volatile KLDS int*)&lovf || c + 1 >= nch) break;
-      mg_load<AU, NT, R12M>(rawA, extA, srec, rbase, rn, (c + 2) * AU * NT, q.rw, wide);
+      mg_load<AU, NT, R12M, !CNT1>(rawA, extA, srec, rbase, rn, (c + 2) * AU * NT, q.rw, wide);
       apply_chunk(rawB, extB, (c + 1) * AU * NT);
       if (*(volatile KLDS int*)&lovf) break;
     }
     lds_barrier();
     MG_T(2);
     // the next item's first chunk is in flight from here on
-    if (wnext < nwork) mg_load<AU, NT, R12M>(rawA, extA, srec, nit.rbase, nit.rn, 0, q.rw, wide);
+    if (wnext < nwork) mg_load<AU, NT, R12M, !CNT1>(rawA, extA, srec, nit.rbase, nit.rn, 0, q.rw, wide);
     if (lovf) {  // more groups than the table: retried with 2x sub-passes
       if (threadIdx.x == 0) fail[p] |= 1;
       for (int i = threadIdx.x; i < H; i += NT) mg_clear(smem, ids, rt, otab, q.n_ops, i);
@@ -2670,6 +2797,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     }
     mq.rt_off = s.rt_off;
     mq.list_off = s.m_list_off;
+    mq.fan = a->windowed ? (int32_t)std::min<int64_t>((q0.size + q0.adv - 1) / q0.adv, 1 << 20) : 1;
     mq.lds_bytes = s.m_lds;
     mq.init = a->init;
     mq.having = a->having;

@@ -10,7 +10,7 @@ i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS" \
            "SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $grp -d $OUT/p$i -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extras > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 5; }
+  timeout -s KILL 120 rocprofv3 --pmc $grp -d $OUT/p$i -o run --output-format csv -- python3 bench.py ${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --no-extras} > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 5; }
   python3 tools/rocprof_summary.py pmc $OUT/p$i/run_counter_collection.csv "k_part_(merge|scatter|refine|hist)" >> $OUT/summary.txt
 done
 cat $OUT/summary.txt
