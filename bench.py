@@ -17,6 +17,11 @@ Other legs (--config), one JSON line each, same contract:
   hopping_double   configs[2]: 1e9 records, HOPPING 60 s / 10 s SUM/AVG/MIN/MAX(DOUBLE)
   clickstream_join configs[3]: 1e8-row users table in HBM, 1e9 clicks, LEFT JOIN + WHERE
   repartition_sum  configs[4]: GROUP BY a value column → pack → RCCL all-to-all → aggregate
+Legs for the rows SURVEY §8(f) ranks next (same contract, not BASELINE configs):
+  serde_json       C2's records as Kafka bytes (KAFKA BIGINT key, JSON value) → device columns
+  table_agg        CREATE TABLE .. AS SELECT region, COUNT(*), SUM(amount) FROM users GROUP BY region
+                   over a 1e8-row source-table changelog (updates move users between regions)
+  session          C2's records, COUNT(*) WINDOW SESSION (1 SECOND) GROUP BY card_number
 
 Multi-GPU: `--gpus N` (N > 1) without torchrun's environment relaunches this script under
 `torch.distributed.run` (one process per GPU, 127.0.0.1 rendezvous) before anything touches
@@ -63,7 +68,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", choices=["possible_fraud", "hourly_metrics", "hopping_double", "clickstream_join",
-                                         "repartition_sum"], default="possible_fraud",
+                                         "repartition_sum", "serde_json", "table_agg", "session"],
+                    default="possible_fraud",
                     help="possible_fraud = BASELINE configs[1] (the headline); hourly_metrics = configs[0]; "
                          "hopping_double = configs[2]; clickstream_join = configs[3]; repartition_sum = configs[4]")
     ap.add_argument("--records", type=int, default=None, help="records per GPU (default: the config's)")
@@ -226,6 +232,184 @@ def stream_copy_gbs(nbytes=1 << 31):
     return 2.0 * nbytes / (ms / 1000.0) / 1e9
 
 
+
+# ------------------------------------------------------------------ §8(f) legs
+
+def bench_serde_json(args, lib, rank, world, local):
+    """§8(f)1: deserialization of C2's records as the consumer returns them — KAFKA BIGINT key
+    (8 bytes big-endian card number) and a JSON value {"AMOUNT":<10 digits>} — into device
+    columns (khip_serde_decode).  One step = decode the whole device-resident raw batch."""
+    import torch
+    from ksql_amd import abi, synth
+    n = args.records or 100_000_000
+    card, ts = synth.possible_fraud(0, n, n, xp="torch", device="cuda", rank=rank, world=world, keys=args.keys)
+    kb = torch.stack([((card >> (8 * (7 - i))) & 0xFF).to(torch.uint8) for i in range(8)], dim=1).reshape(-1)
+    koff = torch.arange(0, 8 * (n + 1), 8, dtype=torch.int64, device="cuda")
+    amount = 1_000_000_000 + card % 999_999_937  # always 10 digits
+    head, tail = b'{"AMOUNT":', b"}"
+    w = len(head) + 10 + len(tail)
+    vb = torch.empty((n, w), dtype=torch.uint8, device="cuda")
+    vb[:, :len(head)] = torch.tensor(list(head), dtype=torch.uint8, device="cuda")
+    rem = amount.clone()
+    for i in range(9, -1, -1):
+        vb[:, len(head) + i] = (rem % 10 + 48).to(torch.uint8)
+        rem //= 10
+    vb[:, -1] = ord("}")
+    vb = vb.reshape(-1)
+    voff = torch.arange(0, w * (n + 1), w, dtype=torch.int64, device="cuda")
+    sd = abi.SerdeHandle(lib, "JSON", [("AMOUNT", "INT64", 0)], key_type="INT64", key_format="KAFKA", device=local)
+    torch.cuda.synchronize()
+
+    def step():
+        d, nerr = sd.decode_device(ts, koff, kb, voff, vb)
+        return nerr
+
+    for _ in range(max(args.warmup, 1)):
+        nerr = step()
+    assert nerr == 0, nerr
+    nerr, elapsed = timed_loop(step, args.steps, world)
+    sd.close()
+    if rank != 0:
+        return
+    ms_step = elapsed * 1000.0 / args.steps
+    bpr = 8 + w + 2 * 8 + 8 + 8  # key bytes + value bytes + 2 offsets read; key + value columns written
+    roof = roofline(bpr * n, ms_step, None, None, None, bpr, kernel="khip_serde_decode (k_serde_decode)")
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        import json as _json
+        m = 200_000
+        keys = [int(x).to_bytes(8, "big") for x in card[:m].cpu().numpy()]
+        vals = [bytes(v) for v in vb[: m * w].cpu().numpy().reshape(m, w)]
+        t0 = time.perf_counter()
+        out = [(int.from_bytes(k, "big", signed=True), _json.loads(v)["AMOUNT"]) for k, v in zip(keys, vals)]
+        dt = time.perf_counter() - t0
+        assert len(out) == m
+        cpu = {"value": m / dt, "unit": "records/s", "cores": 1, "kind": "port",
+               "sample": "%d of the records, CPython int.from_bytes + json.loads per record" % m,
+               "cpu": cpu_info(), "label": "CPU restatement of the KAFKA / JSON deserializers, not the JVM reference"}
+    line("records/sec, Kafka record bytes (KAFKA BIGINT key, JSON value) -> device columns",
+         world * n * args.steps / elapsed, world, args, ms_step, "u8",
+         "synthetic (C2's records serialized on the device), device-resident raw batch",
+         {"workload": "serde_json", "records_per_gpu": n, "key": "KAFKA BIGINT", "value": "JSON {\"AMOUNT\": BIGINT}",
+          "value_bytes": w, "errors": int(nerr), "parallelism": "records x%d" % world}, roof, cpu)
+
+
+def bench_table_agg(args, lib, rank, world, local):
+    """§8(f)4: CREATE TABLE by_region AS SELECT region, COUNT(*), SUM(amount) FROM users GROUP BY
+    region — a source table of 1e7 users whose changelog (1e8 rows, 5 % tombstones) moves users
+    between 1e5 regions; pushed as micro-batches of --slice rows (khip_agg_push_table).  One step =
+    a fresh query instance over the whole changelog."""
+    import torch
+    from ksql_amd import abi, synth
+    n = args.records or 100_000_000
+    users = 10_000_000 // world
+    S = max(8, min(args.slice, 1 << 24) // 8 * 8)
+    be = synth.backend("torch")
+    h0 = synth._stream(be, 7, 0, n, "cuda")
+    pk = (h0 % users).to(torch.int64)
+    region = ((h0 >> 24) % 100_000).to(torch.int64)
+    amount = ((h0 >> 40) % 2_000_001 - 1_000_000).to(torch.int64)
+    live = (h0 >> 60) != 0  # 1 in 16 rows: a tombstone
+    ts = torch.arange(n, dtype=torch.int64, device="cuda")
+    rv = abi.bitmap_torch(live)
+    batches = [(abi.DeviceBatch(ts[lo:min(lo + S, n)], keys=region[lo:min(lo + S, n)], row_valid=rv[lo // 8:],
+                                cols=[amount[lo:min(lo + S, n)]]), pk[lo:min(lo + S, n)]) for lo in range(0, n, S)]
+    desc = abi.make_agg_desc("NONE", "INT64", col_types=["INT64"], aggs=[("COUNT_STAR", -1), ("SUM", 0)],
+                             device=local, capacity_hint=200_000, flags=abi.FLAG_TABLE_SOURCE)
+    h = abi.AggHandle(lib, desc)
+    torch.cuda.synchronize()
+
+    def push_dev(b, k):
+        src = abi.TableSrc(abi.KEY["INT64"], 0, k.data_ptr(), None, None, None)
+        st = abi.BatchStats()
+        lib.check(lib.agg_push_table(h.h, abi.C.byref(b.struct), abi.C.byref(src), abi.C.byref(st)), "agg_push_table")
+        return st.rows_accepted
+
+    def step():
+        lib.check(lib.agg_reset(h.h), "agg_reset")
+        return sum(push_dev(b, k) for b, k in batches)
+
+    for _ in range(max(args.warmup, 1)):
+        acc = step()
+    acc, elapsed = timed_loop(step, args.steps, world)
+    groups = h.count_rows(None)
+    h.close()
+    if rank != 0:
+        return
+    ms_step = elapsed * 1000.0 / args.steps
+    bpr = 32 + 2 * 48 + 2 * 2 * 32  # row in (pk, region, ts, amount) + source-row RMW + undo and apply group RMWs
+    roof = roofline(bpr * n, ms_step, None, None, None, bpr,
+                    kernel="khip_agg_push_table (k_tagg_keys + radix sort + k_tagg_apply + finalize)")
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        orc = abi.load_oracle()
+        m = 2_000_000
+        hb = abi.HostBatch(ts[:m].cpu().numpy(), keys=region[:m].cpu().numpy(), row_valid=live[:m].cpu().numpy(),
+                           cols=[amount[:m].cpu().numpy()])
+        ho = abi.AggHandle(orc, abi.make_agg_desc("NONE", "INT64", col_types=["INT64"],
+                                                  aggs=[("COUNT_STAR", -1), ("SUM", 0)], flags=abi.FLAG_TABLE_SOURCE))
+        t0 = time.perf_counter()
+        ho.push_table(hb, src_keys=pk[:m].cpu().numpy(), stats=False)
+        dt = time.perf_counter() - t0
+        ho.close()
+        cpu = {"value": m / dt, "unit": "records/s", "cores": 1, "kind": "port",
+               "sample": "first %d changelog rows, oracle_agg_push_table (R12)" % m, "cpu": cpu_info(),
+               "label": CPU_LABEL}
+    line("records/sec, table aggregation (source-table changelog rows, undo + apply)",
+         world * n * args.steps / elapsed, world, args, ms_step, "int64",
+         "synthetic (splitmix64), device-resident changelog",
+         {"workload": "table_agg", "records_per_gpu": n, "source_keys": users, "regions": 100_000,
+          "micro_batch": S, "groups_per_gpu": int(groups), "rows_accepted": int(acc), "parallelism": "key-hash shards x%d" % world}, roof, cpu)
+
+
+def bench_session(args, lib, rank, world, local):
+    """§8(f)4: C2's records with SESSION windows: SELECT card_number, COUNT(*) ... WINDOW SESSION
+    (1 SECOND) GROUP BY card_number (khip_agg session engine).  One step = a fresh query instance
+    over the 100M device-resident records."""
+    import torch
+    from ksql_amd import abi, synth
+    n = args.records or 100_000_000
+    card, ts = synth.possible_fraud(0, n, n, xp="torch", device="cuda", rank=rank, world=world, keys=args.keys)
+    batch = abi.DeviceBatch(ts, keys=card)
+    kw = dict(window_kind="SESSION", size_ms=1000, key_type="INT64", aggs=[("COUNT_STAR", -1)])
+    h = abi.AggHandle(lib, abi.make_agg_desc(**kw, device=local, capacity_hint=3 * args.keys))
+    torch.cuda.synchronize()
+
+    def step():
+        h.reset()
+        return h.push(batch)
+
+    for _ in range(max(args.warmup, 1)):
+        st = step()
+    assert st["rows_accepted"] == n, st
+    st, elapsed = timed_loop(step, args.steps, world)
+    groups = h.count_rows(None)
+    h.close()
+    if rank != 0:
+        return
+    ms_step = elapsed * 1000.0 / args.steps
+    bpr = 16 + 2 * 32  # key + ts in, one session-row RMW
+    roof = roofline(bpr * n, ms_step, None, None, None, bpr,
+                    kernel="khip_agg_push, SESSION engine (sort + one thread per key + store rebuild)")
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        orc = abi.load_oracle()
+        m = 4_000_000
+        c2, t2 = synth.possible_fraud(0, m, n, keys=args.keys)
+        ho = abi.AggHandle(orc, abi.make_agg_desc(**kw))
+        t0 = time.perf_counter()
+        ho.push(abi.HostBatch(t2, keys=c2), stats=False)
+        dt = time.perf_counter() - t0
+        ho.close()
+        cpu = {"value": m / dt, "unit": "records/s", "cores": 1, "kind": "port",
+               "sample": "first %d of the records, oracle R11" % m, "cpu": cpu_info(), "label": CPU_LABEL}
+    line("records/sec, SESSION-windowed GROUP BY (COUNT(*) WINDOW SESSION 1 SECOND GROUP BY card_number)",
+         world * n * args.steps / elapsed, world, args, ms_step, "int64",
+         "synthetic (splitmix64, ksql_amd/synth.py possible_fraud), device-resident columnar batch",
+         {"workload": "session", "records_per_gpu": n, "keys_per_gpu": args.keys, "window": "SESSION 1 s",
+          "sessions_per_gpu": int(groups), "windows_late": int(st["windows_late"]),
+          "parallelism": "key-hash shards x%d" % world}, roof, cpu)
+
 # ------------------------------------------------------------------ main
 
 def main():
@@ -248,7 +432,8 @@ def main():
     lib = abi.load_product()
     legs = {"possible_fraud": bench_possible_fraud, "hourly_metrics": bench_hourly_metrics,
             "hopping_double": bench_hopping_double, "clickstream_join": bench_join,
-            "repartition_sum": bench_repartition}
+            "repartition_sum": bench_repartition, "serde_json": bench_serde_json, "table_agg": bench_table_agg,
+            "session": bench_session}
     legs[args.config](args, lib, rank, world, local)
     if world > 1:
         dist.destroy_process_group()

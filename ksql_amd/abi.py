@@ -806,6 +806,24 @@ class SerdeHandle:
         d._keep = keep
         return d, nerr.value
 
+    def decode_device(self, ts, key_offsets, key_bytes, value_offsets, value_bytes, key_valid=None,
+                      value_valid=None):
+        """Device raw batch (torch tensors, caller-owned and kept alive while the result is used)
+        → (decoded batch, n_errors)."""
+        p = lambda t: None if t is None else t.data_ptr()
+        raw = RawBatch(int(ts.numel()), MEM_DEVICE, p(ts), p(key_offsets), p(key_bytes), p(key_valid),
+                       p(value_offsets), p(value_bytes), p(value_valid))
+        out = Batch()
+        nerr = i64()
+        self.lib.check(self.lib.serde_decode(self.h, C.byref(raw), C.byref(out), C.byref(nerr)), "serde_decode")
+
+        class _Decoded:
+            pass
+        d = _Decoded()
+        d.struct = out
+        d._keep = (ts, key_offsets, key_bytes, value_offsets, value_bytes, key_valid, value_valid)
+        return d, nerr.value
+
     def columns(self, decoded, out_types):
         """Copy a decoded batch's columns back to the host (for tests): dict of numpy arrays."""
         b = decoded.struct
