@@ -10,9 +10,12 @@
 // key are disjoint, so sorted by start they are also sorted by end.
 //
 // Per push (all on the handle's stream):
-//   k_blockmax / k_scan_blocks   stream time before each 2048-record block
-//   k_sess_prep                  per record: accepted?, stream time after it; (key, row) pairs
-//   radix sort (hipcub, stable)  records grouped by key, arrival order kept inside a key
+//   k_sess_range / k_scan_blocks stream time before each 2048-record block; the key range
+//   k_sess_prep                  per record: accepted?, stream time after it (packed with ts);
+//                                (key - kmin, row) pairs
+//   radix sort (hipcub, stable)  records grouped by key, arrival order kept inside a key; only
+//                                the bits of the push's key range are sorted
+//   k_sess_gather                the packed (ts, stream time) records in sorted order
 //   run-length encode            one segment per batch key
 //   k_sess_bounds                the key's store range (binary search), scratch capacity
 //   k_sess_apply                 ONE THREAD PER KEY replays the key's records in arrival order
@@ -43,53 +46,208 @@ struct SessParams {
   int64_t gap, grace, retention;
 };
 
-// Per record: accepted (valid key and value, ts >= 0), the task's stream time after it (in-block
-// running max seeded with the block prefix), and the (key, row) pair to sort; drop counters.
+// Accepted records (valid key and value, ts >= 0): per-block ts maximum (for the stream-time
+// prefix), and the key range of the push (min / max as order-preserving unsigned words,
+// atomic-max'd: ctr[C_KMINN] = max of ~u, ctr[C_KMAX] = max of u, ctr[C_KACC] = accepted).
+// Coalesced: element k of thread t is base + k * BLOCK + t.
+constexpr int C_KMINN = 20, C_KMAX = 21, C_KACC = 22;
+
+__device__ __forceinline__ uint64_t key_ord(int64_t k) { return (uint64_t)k ^ (1ULL << 63); }
+
+__device__ __forceinline__ bool sess_ok(const uint8_t* kv, const uint8_t* rv, const int64_t* ts, int64_t i,
+                                        int64_t* t) {
+  *t = ts[i];
+  return bit_get(kv, i) && bit_get(rv, i) && *t >= 0;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_sess_range(const int64_t* __restrict__ keys, const int64_t* __restrict__ ts,
+                                                      const uint8_t* __restrict__ kv, const uint8_t* __restrict__ rv,
+                                                      int64_t n, int64_t* __restrict__ blockmax,
+                                                      ulonglong2* __restrict__ blockkr, int64_t* __restrict__ blockacc) {
+  __shared__ int64_t lds[BLOCK / 64];
+  __shared__ uint64_t lk[2][BLOCK / 64];
+  __shared__ int64_t la[BLOCK / 64];
+  const int64_t base = (int64_t)blockIdx.x * RPB;
+  int64_t m = -1;
+  uint64_t kmn = 0, kmx = 0;
+  int64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < ITEMS; k++) {
+    const int64_t i = base + k * BLOCK + threadIdx.x;
+    int64_t t;
+    if (i < n && sess_ok(kv, rv, ts, i, &t)) {
+      m = t > m ? t : m;
+      const uint64_t u = key_ord(keys[i]);
+      kmn = ~u > kmn ? ~u : kmn;
+      kmx = u > kmx ? u : kmx;
+      acc++;
+    }
+  }
+  int64_t tot;
+  block_incl_max(m, lds, &tot);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t a = __shfl_xor(kmn, off, 64), b = __shfl_xor(kmx, off, 64);
+    kmn = a > kmn ? a : kmn;
+    kmx = b > kmx ? b : kmx;
+  }
+  acc = wave_sum(acc);
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    lk[0][wave] = kmn;
+    lk[1][wave] = kmx;
+    la[wave] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < BLOCK / 64; w++) {
+      kmn = lk[0][w] > kmn ? lk[0][w] : kmn;
+      kmx = lk[1][w] > kmx ? lk[1][w] : kmx;
+      acc += la[w];
+    }
+    blockmax[blockIdx.x] = tot;
+    blockkr[blockIdx.x] = make_ulonglong2(kmn, kmx);
+    blockacc[blockIdx.x] = acc;
+  }
+}
+
+// The per-block key ranges → ctr[C_KMINN], ctr[C_KMAX], ctr[C_KACC] (one workgroup).
+__global__ __launch_bounds__(1024) void k_sess_range_reduce(const ulonglong2* __restrict__ blockkr,
+                                                            const int64_t* __restrict__ blockacc, int64_t nb,
+                                                            unsigned long long* __restrict__ ctr) {
+  __shared__ uint64_t l[3][1024 / 64];
+  uint64_t kmn = 0, kmx = 0;
+  int64_t acc = 0;
+  for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) {
+    const ulonglong2 v = blockkr[b];
+    kmn = v.x > kmn ? v.x : kmn;
+    kmx = v.y > kmx ? v.y : kmx;
+    acc += blockacc[b];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t a = __shfl_xor(kmn, off, 64), b = __shfl_xor(kmx, off, 64);
+    kmn = a > kmn ? a : kmn;
+    kmx = b > kmx ? b : kmx;
+  }
+  acc = wave_sum(acc);
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    l[0][wave] = kmn;
+    l[1][wave] = kmx;
+    l[2][wave] = (uint64_t)acc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); w++) {
+      kmn = l[0][w] > kmn ? l[0][w] : kmn;
+      kmx = l[1][w] > kmx ? l[1][w] : kmx;
+      acc += (int64_t)l[2][w];
+    }
+    ctr[C_KMINN] = kmn;
+    ctr[C_KMAX] = kmx;
+    ctr[C_KACC] = (unsigned long long)acc;
+  }
+}
+
+// Per record (coalesced): the task's stream time after it (block prefix, then the block's running
+// max), the packed replay record {ts or -1 when dropped, stream time after}, and the (key - kmin,
+// row) pair to sort (dropped rows get the sentinel `drop`, which sorts last); drop counters.
 __global__ __launch_bounds__(BLOCK) void k_sess_prep(const int64_t* __restrict__ keys, const int64_t* __restrict__ ts,
                                                      const uint8_t* __restrict__ kv, const uint8_t* __restrict__ rv,
-                                                     int64_t n, const int64_t* __restrict__ prefix,
-                                                     int64_t* __restrict__ skey, int64_t* __restrict__ sidx,
-                                                     int64_t* __restrict__ st_after,
-                                                     unsigned long long* __restrict__ ctr) {
-  __shared__ int64_t lmax[BLOCK];
-  const int64_t i0 = (int64_t)blockIdx.x * RPB + (int64_t)threadIdx.x * ITEMS;
-  int64_t m = -1;
+                                                     int64_t n, const int64_t* __restrict__ prefix, int64_t kmin,
+                                                     uint64_t drop, uint64_t* __restrict__ skey,
+                                                     uint32_t* __restrict__ sidx, longlong2* __restrict__ rec,
+                                                     int64_t* __restrict__ blockcnt) {
+  // wave w owns records [base + w * 64 * ITEMS, +64 * ITEMS), read 64 at a time (coalesced); the
+  // running max is a wave scan per step, the earlier waves' maxima join after one block barrier
+  __shared__ int64_t wmax[BLOCK / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * RPB + (int64_t)wave * 64 * ITEMS + lane;
+  int64_t stv[ITEMS], tv[ITEMS];
+  int64_t carry = -1;
   int nk = 0, nr = 0, nt = 0, na = 0;
+#pragma unroll
   for (int k = 0; k < ITEMS; k++) {
-    const int64_t i = i0 + k;
-    if (i >= n) break;
-    if (!bit_get(kv, i)) { nk++; continue; }
-    if (!bit_get(rv, i)) { nr++; continue; }
-    if (ts[i] < 0) { nt++; continue; }
-    na++;
-    m = ts[i] > m ? ts[i] : m;
+    const int64_t i = base + k * 64;
+    int64_t t = -1;
+    bool ok = false;
+    if (i < n) {
+      t = ts[i];
+      const bool a = bit_get(kv, i), b = bit_get(rv, i);
+      ok = a && b && t >= 0;
+      nk += !a;
+      nr += a && !b;
+      nt += a && b && t < 0;
+      na += ok;
+    }
+    tv[k] = ok ? t : -1;
+    int64_t incl = wave_incl_max(tv[k]);
+    incl = incl > carry ? incl : carry;
+    stv[k] = incl;
+    carry = __shfl(incl, 63, 64);
   }
-  lmax[threadIdx.x] = m;
+  if (lane == 0) wmax[wave] = carry;
   __syncthreads();
-  for (int off = 1; off < BLOCK; off <<= 1) {
-    const int64_t y = threadIdx.x >= off ? lmax[threadIdx.x - off] : -1;
-    __syncthreads();
-    if (y > lmax[threadIdx.x]) lmax[threadIdx.x] = y;
-    __syncthreads();
-  }
-  int64_t st = prefix[blockIdx.x];
-  if (threadIdx.x > 0 && lmax[threadIdx.x - 1] > st) st = lmax[threadIdx.x - 1];
+  int64_t pre = prefix[blockIdx.x];
+  for (int w = 0; w < wave; w++) pre = wmax[w] > pre ? wmax[w] : pre;
+#pragma unroll
   for (int k = 0; k < ITEMS; k++) {
-    const int64_t i = i0 + k;
-    if (i >= n) break;
-    const bool ok = bit_get(kv, i) && bit_get(rv, i) && ts[i] >= 0;
-    if (ok && ts[i] > st) st = ts[i];
-    st_after[i] = st;
-    skey[i] = ok ? keys[i] : INT64_MAX;  // dropped rows sort last (skipped by the replay)
-    sidx[i] = i;
+    const int64_t i = base + k * 64;
+    if (i < n) {
+      const bool ok = tv[k] >= 0;
+      skey[i] = ok ? (uint64_t)keys[i] - (uint64_t)kmin : drop;
+      if (sidx) sidx[i] = (uint32_t)i;
+      rec[i] = make_longlong2(tv[k], stv[k] > pre ? stv[k] : pre);
+    }
   }
-  const int64_t s0 = wave_sum(nk), s1 = wave_sum(nr), s2 = wave_sum(nt), s3 = wave_sum(na);
-  if ((threadIdx.x & 63) == 0) {
-    if (s0) atomicAdd(&ctr[P_NULL_KEY], (unsigned long long)s0);
-    if (s1) atomicAdd(&ctr[P_NULL_ROW], (unsigned long long)s1);
-    if (s2) atomicAdd(&ctr[P_BAD_TS], (unsigned long long)s2);
-    if (s3) atomicAdd(&ctr[P_ACCEPTED], (unsigned long long)s3);
+  // drop counters: one row of 4 per block (summed by k_sess_cnt_reduce; same-address atomics
+  // from every wave would serialize)
+  __shared__ int64_t wc[BLOCK / 64][4];
+  const int64_t c4[4] = {wave_sum(nk), wave_sum(nr), wave_sum(nt), wave_sum(na)};
+  if (lane < 4) wc[wave][lane] = c4[lane];
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    int64_t v = 0;
+    for (int w = 0; w < BLOCK / 64; w++) v += wc[w][threadIdx.x];
+    blockcnt[blockIdx.x * 4 + threadIdx.x] = v;
   }
+}
+
+// Per-block drop counters → ctr[P_NULL_KEY, P_NULL_ROW, P_BAD_TS, P_ACCEPTED] (one workgroup).
+__global__ __launch_bounds__(1024) void k_sess_cnt_reduce(const int64_t* __restrict__ blockcnt, int64_t nb,
+                                                          unsigned long long* __restrict__ ctr) {
+  __shared__ int64_t l[4][1024 / 64];
+  int64_t v[4] = {0, 0, 0, 0};
+  for (int64_t b = threadIdx.x; b < nb; b += blockDim.x)
+    for (int k = 0; k < 4; k++) v[k] += blockcnt[b * 4 + k];
+  const int wave = threadIdx.x >> 6;
+  for (int k = 0; k < 4; k++) {
+    const int64_t x = wave_sum(v[k]);
+    if ((threadIdx.x & 63) == 0) l[k][wave] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    int64_t x = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); w++) x += l[threadIdx.x][w];
+    const int slot[4] = {P_NULL_KEY, P_NULL_ROW, P_BAD_TS, P_ACCEPTED};
+    ctr[slot[threadIdx.x]] += (unsigned long long)x;
+  }
+}
+
+// Replay records in sorted order: g[r] = rec[sidx[r]] (the random reads leave the per-key chain).
+__global__ __launch_bounds__(256) void k_sess_gather(const uint32_t* __restrict__ sidx, const longlong2* __restrict__ rec,
+                                                     int64_t n, longlong2* __restrict__ g) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+    g[r] = rec[sidx[r]];
+}
+
+__global__ void k_sess_setn(int* __restrict__ p, int v) { *p = v; }
+
+// Run-length-encoded keys back to absolute keys.
+__global__ __launch_bounds__(256) void k_sess_ukeys(int64_t* __restrict__ ukeys, const int* __restrict__ nseg, int64_t kmin) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j < *nseg) ukeys[j] = (int64_t)((uint64_t)ukeys[j] + (uint64_t)kmin);
 }
 
 __device__ __forceinline__ int64_t lower_key(const uint64_t* __restrict__ rows, int sw, int64_t n, int64_t key) {
@@ -196,45 +354,28 @@ __device__ __forceinline__ void row_copy(uint64_t* d, const uint64_t* s, int sw)
   for (int w = 0; w < sw; w++) d[w] = s[w];
 }
 
-// One thread per batch key: replay its records (arrival order) against its sessions.
-// scratch rows / flags at base = scap[j]; removed original sessions go to trow at the same base.
-// Outputs: fin[j] = sessions left after expiry (compacted at base), chg rows appended to the
-// changelog buffer, applied / late counters.
-__global__ __launch_bounds__(64) void k_sess_apply(SessParams q, const uint64_t* __restrict__ store,
-                                                   const int64_t* __restrict__ ukeys, const int* __restrict__ ucnt,
-                                                   const int64_t* __restrict__ useg, const int* __restrict__ nseg,
-                                                   const int64_t* __restrict__ s0, const int64_t* __restrict__ cap,
-                                                   const int64_t* __restrict__ scap, const int64_t* __restrict__ sidx,
-                                                   const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
-                                                   const uint8_t* __restrict__ rv, ColPtrs cols,
-                                                   const int64_t* __restrict__ st_after,
-                                                   const int64_t* __restrict__ st_end, uint64_t* __restrict__ srow,
-                                                   uint8_t* __restrict__ sfl, uint64_t* __restrict__ trow,
-                                                   int64_t* __restrict__ fin, uint64_t* __restrict__ crow,
-                                                   uint8_t* __restrict__ ctomb, unsigned long long* __restrict__ ctr,
-                                                   int keep_changes) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= *nseg) return;
+// One batch key: replay its records (arrival order) against its sessions.  R / F: the key's
+// scratch rows and flags (LDS or HBM), T: removed original sessions (HBM), orig: its store rows.
+// Returns the sessions left after expiry (compacted at R); chg rows appended to the changelog.
+__device__ __forceinline__ int64_t sess_replay(const SessParams& q, int64_t key, const uint64_t* orig, int64_t norig,
+                                               const longlong2* g, const uint32_t* sidx, int64_t nrec,
+                                               uint64_t* R, uint8_t* F, uint64_t* T, const ColPtrs& cols,
+                                               int64_t vis_end, uint64_t* __restrict__ crow,
+                                               uint8_t* __restrict__ ctomb, unsigned long long* __restrict__ ctr,
+                                               int keep_changes, int64_t& applied, int64_t& late) {
   const int sw = q.sw;
-  const int64_t key = ukeys[j];
-  const int64_t base = scap[j];
-  uint64_t* R = srow + base * sw;
-  uint8_t* F = sfl + base;
-  uint64_t* T = trow + base * sw;
-  const int64_t norig = cap[j] - ucnt[j];
   int64_t m = 0, nt = 0;
   for (int64_t k = 0; k < norig; k++) {  // the key's sessions, sorted by start (and end)
-    const uint64_t* src = store + (s0[j] + k) * sw;
+    const uint64_t* src = orig + k * sw;
     row_copy(R + m * sw, src, sw);
     F[m] = SF_ORIG | (having_ok(src, q.having) ? SF_OLDP : 0);
     m++;
   }
-  int64_t applied = 0, late = 0;
-  const int64_t r0 = useg[j], r1 = r0 + ucnt[j];
-  for (int64_t r = r0; r < r1; r++) {
-    const int64_t i = sidx[r];
-    if (!bit_get(kv, i) || !bit_get(rv, i) || ts[i] < 0) continue;
-    const int64_t t = ts[i], st = st_after[i];
+  for (int64_t r = 0; r < nrec; r++) {
+    const longlong2 gr = g[r];
+    const int64_t t = gr.x, st = gr.y;
+    if (t < 0) continue;  // dropped (only where the sentinel shares the last key's segment)
+    const int64_t i = q.ap.n_cols ? (int64_t)sidx[r] : 0;
     const int64_t vis = st - q.retention, close = st - q.grace - q.gap;
     // overlapping run: visible sessions with end >= t - gap and start <= t + gap
     const int64_t from = t - q.gap > vis ? t - q.gap : vis;
@@ -261,26 +402,28 @@ __global__ __launch_bounds__(64) void k_sess_apply(SessParams q, const uint64_t*
       F[lo] |= SF_TOUCHED;
       continue;
     }
-    uint64_t acc[32];
-    acc[0] = (uint64_t)key;
-    acc[1] = (uint64_t)ms;
-    acc[2] = (uint64_t)me;
-    for (int w = 3; w < sw; w++) acc[w] = (uint64_t)q.init.w[w];
-    for (int64_t k = lo; k < hi; k++) {  // store order (by end), merged into the initial row
-      sess_merge(q, acc, R + k * sw);
-      if (F[k] & SF_ORIG) {  // existed before the push: its deletion is emitted
+    // the merged-away sessions that existed before the push: their deletions are emitted
+    for (int64_t k = lo; k < hi; k++) {
+      if (F[k] & SF_ORIG) {
         row_copy(T + nt * sw, R + k * sw, sw);
         T[nt * sw + 0] = (uint64_t)F[k];  // flags ride in the key word (the key is known)
         nt++;
       }
     }
+    // merged row, in place at lo: the first overlapped session, the later ones merged into it in
+    // store order (by end) — or the initial row for a new session
+    uint64_t* M = R + lo * sw;
+    if (hi > lo) {
+      for (int64_t k = lo + 1; k < hi; k++) sess_merge(q, M, R + k * sw);
+    }
     const int64_t removed = hi - lo;
-    if (removed == 0) {  // a new session: shift the later ones right
+    if (removed == 0) {  // a new session: shift the later ones right, initial row at lo
       for (int64_t k = m; k > lo; k--) {
         row_copy(R + k * sw, R + (k - 1) * sw, sw);
         F[k] = F[k - 1];
       }
       m++;
+      for (int w = 3; w < sw; w++) M[w] = (uint64_t)q.init.w[w];
     } else if (removed > 1) {  // close the gap left by the merged sessions
       for (int64_t k = hi; k < m; k++) {
         row_copy(R + (k - removed + 1) * sw, R + k * sw, sw);
@@ -288,7 +431,9 @@ __global__ __launch_bounds__(64) void k_sess_apply(SessParams q, const uint64_t*
       }
       m -= removed - 1;
     }
-    row_copy(R + lo * sw, acc, sw);
+    M[0] = (uint64_t)key;
+    M[1] = (uint64_t)ms;
+    M[2] = (uint64_t)me;
     F[lo] = SF_TOUCHED;
     sess_apply_record(q, R + lo * sw, cols, i);
   }
@@ -315,16 +460,79 @@ __global__ __launch_bounds__(64) void k_sess_apply(SessParams q, const uint64_t*
     }
   }
   // expired sessions leave the store (end < stream time after the push - retention)
-  const int64_t vis_end = *st_end - q.retention;
   int64_t kept = 0;
   for (int64_t k = 0; k < m; k++) {
     if ((int64_t)R[k * sw + 2] < vis_end) continue;
     if (kept != k) row_copy(R + kept * sw, R + k * sw, sw);
     kept++;
   }
-  fin[j] = kept;
-  if (applied) atomicAdd(&ctr[P_APPLIED], (unsigned long long)applied);
-  if (late) atomicAdd(&ctr[P_LATE], (unsigned long long)late);
+  return kept;
+}
+
+// Scratch budget of one wave's keys in LDS (records 16 B, rows sw words + 1 flag byte each);
+// waves whose keys need more replay in HBM scratch.
+constexpr int SESS_LDS = 40960;
+
+// One wave per 64 batch keys, one lane per key.  The wave's records (one contiguous range of the
+// sorted records) and its keys' scratch rows are staged in LDS when they fit, so the per-key
+// sequential replay runs against LDS; the keys' final rows then leave with coalesced stores.
+__global__ __launch_bounds__(64) void k_sess_apply(SessParams q, const uint64_t* __restrict__ store,
+                                                   const int64_t* __restrict__ ukeys, const int* __restrict__ ucnt,
+                                                   const int64_t* __restrict__ useg, const int* __restrict__ nseg,
+                                                   const int64_t* __restrict__ s0, const int64_t* __restrict__ cap,
+                                                   const int64_t* __restrict__ scap, const uint32_t* __restrict__ sidx,
+                                                   const longlong2* __restrict__ g, ColPtrs cols,
+                                                   const int64_t* __restrict__ st_end, uint64_t* __restrict__ srow,
+                                                   uint8_t* __restrict__ sfl, uint64_t* __restrict__ trow,
+                                                   int64_t* __restrict__ fin, uint64_t* __restrict__ crow,
+                                                   uint8_t* __restrict__ ctomb, unsigned long long* __restrict__ ctr,
+                                                   int keep_changes, int64_t nseg_eff) {
+  __shared__ uint64_t lds[SESS_LDS / 8];
+  const int lane = threadIdx.x;
+  const int64_t j0 = (int64_t)blockIdx.x * 64, j = j0 + lane;
+  const int64_t jl = (nseg_eff - 1 < j0 + 63) ? nseg_eff - 1 : j0 + 63;
+  const int sw = q.sw;
+  const int64_t R0 = useg[j0], R1 = useg[jl] + ucnt[jl];
+  const int64_t C0 = scap[j0], C1 = scap[jl] + cap[jl];
+  const int64_t need = (R1 - R0) * 16 + (C1 - C0) * (sw * 8 + 1);
+  const bool in_lds = need <= SESS_LDS;
+  const int64_t vis_end = *st_end - q.retention;
+  int64_t applied = 0, late = 0, kept = 0;
+  const bool mine = j < nseg_eff;
+  if (in_lds) {
+    longlong2* lrec = (longlong2*)lds;
+    uint64_t* lrow = lds + 2 * (R1 - R0);
+    uint8_t* lfl = (uint8_t*)(lrow + (C1 - C0) * sw);
+    for (int64_t x = lane; x < R1 - R0; x += 64) lrec[x] = g[R0 + x];
+    __syncthreads();
+    if (mine) {
+      const int64_t base = scap[j], r0 = useg[j];
+      kept = sess_replay(q, ukeys[j], store + s0[j] * sw, cap[j] - ucnt[j], lrec + (r0 - R0), sidx ? sidx + r0 : nullptr,
+                         ucnt[j], lrow + (base - C0) * sw, lfl + (base - C0), trow + base * sw, cols, vis_end, crow,
+                         ctomb, ctr, keep_changes, applied, late);
+      fin[j] = kept;
+    }
+    __syncthreads();
+    // the keys' final rows → HBM scratch (at scap), one key at a time across the wave's lanes
+    const int64_t off = mine ? scap[j] - C0 : 0, words = mine ? kept * sw : 0;
+    const int nk = (int)(jl - j0 + 1);
+    for (int k = 0; k < nk; k++) {
+      const int64_t o = __shfl(off, k, 64), w = __shfl(words, k, 64);
+      for (int64_t x = lane; x < w; x += 64) srow[(C0 + o) * sw + x] = lrow[o * sw + x];
+    }
+  } else if (mine) {
+    const int64_t base = scap[j], r0 = useg[j];
+    kept = sess_replay(q, ukeys[j], store + s0[j] * sw, cap[j] - ucnt[j], g + r0, sidx ? sidx + r0 : nullptr, ucnt[j],
+                       srow + base * sw, sfl + base, trow + base * sw, cols, vis_end, crow, ctomb, ctr, keep_changes,
+                       applied, late);
+    fin[j] = kept;
+  }
+  applied = wave_sum(applied);
+  late = wave_sum(late);
+  if (lane == 0) {
+    if (applied) atomicAdd(&ctr[P_APPLIED], (unsigned long long)applied);
+    if (late) atomicAdd(&ctr[P_LATE], (unsigned long long)late);
+  }
 }
 
 // Store rows that survive untouched: key not in the batch and not expired.
@@ -357,20 +565,32 @@ __global__ __launch_bounds__(256) void k_sess_scatter_store(const uint64_t* __re
   row_copy(out + ((int64_t)keep_pre[i] + fin_pre[p]) * sw, s, sw);
 }
 
-__global__ __launch_bounds__(64) void k_sess_scatter_seg(const uint64_t* __restrict__ store, int64_t ns, int sw,
-                                                         const int* __restrict__ keep_pre,
-                                                         const int* __restrict__ keep, const int64_t* __restrict__ ukeys,
-                                                         const int* __restrict__ nseg, const int64_t* __restrict__ fin,
-                                                         const int64_t* __restrict__ fin_pre,
-                                                         const int64_t* __restrict__ scap,
-                                                         const uint64_t* __restrict__ srow, uint64_t* __restrict__ out) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= *nseg) return;
-  const int64_t a = lower_key(store, sw, ns, ukeys[j]);
-  const int64_t kept_before = a < ns ? (int64_t)keep_pre[a] : (ns ? (int64_t)keep_pre[ns - 1] + keep[ns - 1] : 0);
-  uint64_t* d = out + (kept_before + fin_pre[j]) * sw;
-  const uint64_t* s = srow + scap[j] * sw;
-  for (int64_t k = 0; k < fin[j] * sw; k++) d[k] = s[k];
+// The rewritten keys' sessions into the new store: one wave per 64 batch keys, the key's rows
+// copied by the wave's lanes (coalesced) instead of by one thread.
+__global__ __launch_bounds__(256) void k_sess_scatter_seg(const uint64_t* __restrict__ store, int64_t ns, int sw,
+                                                          const int* __restrict__ keep_pre,
+                                                          const int* __restrict__ keep, const int64_t* __restrict__ ukeys,
+                                                          int64_t nseg, const int64_t* __restrict__ fin,
+                                                          const int64_t* __restrict__ fin_pre,
+                                                          const int64_t* __restrict__ scap,
+                                                          const uint64_t* __restrict__ srow, uint64_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j0 = ((int64_t)blockIdx.x * 256 + (threadIdx.x & ~63));
+  if (j0 >= nseg) return;
+  int64_t dst = 0, src = 0, words = 0;
+  const int64_t jl = j0 + lane;
+  if (jl < nseg) {
+    const int64_t a = ns ? lower_key(store, sw, ns, ukeys[jl]) : 0;
+    const int64_t kept_before = a < ns ? (int64_t)keep_pre[a] : (ns ? (int64_t)keep_pre[ns - 1] + keep[ns - 1] : 0);
+    dst = (kept_before + fin_pre[jl]) * sw;
+    src = scap[jl] * sw;
+    words = fin[jl] * sw;
+  }
+  const int nk = (int)(nseg - j0 < 64 ? nseg - j0 : 64);
+  for (int k = 0; k < nk; k++) {
+    const int64_t d = __shfl(dst, k, 64), s = __shfl(src, k, 64), w = __shfl(words, k, 64);
+    for (int64_t x = lane; x < w; x += 64) out[d + x] = srow[s + x];
+  }
 }
 
 // ------------------------------------------------------------------ host side
@@ -395,49 +615,97 @@ khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   KHIP_TRY(a->blockprefix.ensure(nb * 8));
   KHIP_TRY(S.ctr.ensure(32 * 8));
   KHIP_TRY_HIP(hipMemsetAsync(S.ctr.p, 0, 32 * 8, st));
-  hipLaunchKernelGGL(k_blockmax, dim3(nb), dim3(BLOCK), 0, st, ts, kv, rv, n, a->blockmax.as<int64_t>());
+  KHIP_TRY(S.blockkr.ensure(nb * 32));
+  hipLaunchKernelGGL(k_sess_range, dim3(nb), dim3(BLOCK), 0, st, keys, ts, kv, rv, n, a->blockmax.as<int64_t>(),
+                     S.blockkr.as<ulonglong2>(), (int64_t*)(S.blockkr.as<char>() + nb * 16));
+  hipLaunchKernelGGL(k_sess_range_reduce, dim3(1), dim3(1024), 0, st, S.blockkr.as<ulonglong2>(),
+                     (const int64_t*)(S.blockkr.as<char>() + nb * 16), nb, S.ctr.as<unsigned long long>());
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, st, a->blockmax.as<int64_t>(), nb,
                      a->blockprefix.as<int64_t>(), a->stream_time.as<int64_t>());
+  // the push's key range: the sort runs over (key - kmin) and only the bits that range needs
+  unsigned long long kr[3] = {0, 0, 0};
+  KHIP_TRY_HIP(hipMemcpyAsync(kr, S.ctr.as<unsigned long long>() + C_KMINN, sizeof(kr), hipMemcpyDeviceToHost, st));
+  KHIP_TRY_HIP(hipStreamSynchronize(st));
+  int64_t kmin = 0;
+  uint64_t range = 0;
+  if (kr[2]) {
+    kmin = (int64_t)(~(uint64_t)kr[0] ^ (1ULL << 63));
+    const int64_t kmax = (int64_t)((uint64_t)kr[1] ^ (1ULL << 63));
+    range = (uint64_t)kmax - (uint64_t)kmin;
+  }
+  const bool sentinel = range != ~0ULL;  // dropped rows get a key of their own (range + 1)
+  const uint64_t drop = sentinel ? range + 1 : range;
+  const int end_bit = drop ? 64 - __builtin_clzll(drop) : 1;
+  // without argument columns the replay needs only (ts, stream time after): those 16 bytes ride
+  // through the sort as the value; with columns the value is the row index and a gather pass
+  // brings the packed records into sorted order
+  const bool by_idx = a->desc.n_cols > 0;
   KHIP_TRY(S.skey.ensure(n * 8));
-  KHIP_TRY(S.sidx.ensure(n * 8));
   KHIP_TRY(S.skey2.ensure(n * 8));
-  KHIP_TRY(S.sidx2.ensure(n * 8));
-  KHIP_TRY(S.st_after.ensure(n * 8));
-  hipLaunchKernelGGL(k_sess_prep, dim3(nb), dim3(BLOCK), 0, st, keys, ts, kv, rv, n, a->blockprefix.as<int64_t>(),
-                     S.skey.as<int64_t>(), S.sidx.as<int64_t>(), S.st_after.as<int64_t>(),
+  KHIP_TRY(S.st_after.ensure(n * 16));
+  KHIP_TRY(S.gath.ensure(n * 16));
+  if (by_idx) {
+    KHIP_TRY(S.sidx.ensure(n * 4));
+    KHIP_TRY(S.sidx2.ensure(n * 4));
+  }
+  hipLaunchKernelGGL(k_sess_prep, dim3(nb), dim3(BLOCK), 0, st, keys, ts, kv, rv, n, a->blockprefix.as<int64_t>(), kmin,
+                     drop, S.skey.as<uint64_t>(), by_idx ? S.sidx.as<uint32_t>() : nullptr, S.st_after.as<longlong2>(),
+                     (int64_t*)S.blockkr.p);
+  hipLaunchKernelGGL(k_sess_cnt_reduce, dim3(1), dim3(1024), 0, st, (const int64_t*)S.blockkr.p, nb,
                      S.ctr.as<unsigned long long>());
   KHIP_TRY_HIP(hipGetLastError());
   // group by key, arrival order kept within a key (LSD radix sort is stable)
   const int ni = (int)n;
-  int64_t* k_in = S.skey.as<int64_t>();
-  int64_t* k_out = S.skey2.as<int64_t>();
-  int64_t* v_in = S.sidx.as<int64_t>();
-  int64_t* v_out = S.sidx2.as<int64_t>();
-  KHIP_TRY(cub_call(S.tmp, st, [&](void* p, size_t& b) {
-    return hipcub::DeviceRadixSort::SortPairs(p, b, k_in, k_out, v_in, v_out, ni, 0, 64, st);
-  }));
+  uint64_t* k_in = S.skey.as<uint64_t>();
+  uint64_t* k_out = S.skey2.as<uint64_t>();
+  uint32_t* v_out = by_idx ? S.sidx2.as<uint32_t>() : nullptr;
+  if (by_idx) {
+    uint32_t* v_in = S.sidx.as<uint32_t>();
+    KHIP_TRY(cub_call(S.tmp, st, [&](void* p, size_t& b) {
+      return hipcub::DeviceRadixSort::SortPairs(p, b, k_in, k_out, v_in, v_out, ni, 0, end_bit, st);
+    }));
+    hipLaunchKernelGGL(k_sess_gather, dim3((int)std::min<int64_t>(ceil_div(n, 256), 16384)), dim3(256), 0, st, v_out,
+                       S.st_after.as<longlong2>(), n, S.gath.as<longlong2>());
+  } else {
+    longlong2* r_in = S.st_after.as<longlong2>();
+    longlong2* r_out = S.gath.as<longlong2>();
+    KHIP_TRY(cub_call(S.tmp, st, [&](void* p, size_t& b) {
+      return hipcub::DeviceRadixSort::SortPairs(p, b, k_in, k_out, r_in, r_out, ni, 0, end_bit, st);
+    }));
+  }
   KHIP_TRY(S.ukeys.ensure(n * 8));
   KHIP_TRY(S.ucnt.ensure(n * 4));
   KHIP_TRY(S.nseg.ensure(16));
   KHIP_TRY(cub_call(S.tmp, st, [&](void* p, size_t& b) {
-    return hipcub::DeviceRunLengthEncode::Encode(p, b, k_out, S.ukeys.as<int64_t>(), S.ucnt.as<int>(), S.nseg.as<int>(),
+    return hipcub::DeviceRunLengthEncode::Encode(p, b, k_out, S.ukeys.as<uint64_t>(), S.ucnt.as<int>(), S.nseg.as<int>(),
                                                  ni, st);
   }));
   int nseg = 0;
   KHIP_TRY_HIP(hipMemcpyAsync(&nseg, S.nseg.p, 4, hipMemcpyDeviceToHost, st));
   KHIP_TRY_HIP(hipStreamSynchronize(st));
+  uint64_t last = 0;
+  if (nseg > 0) {
+    KHIP_TRY_HIP(hipMemcpyAsync(&last, S.ukeys.as<uint64_t>() + nseg - 1, 8, hipMemcpyDeviceToHost, st));
+    KHIP_TRY_HIP(hipStreamSynchronize(st));
+    if (sentinel && last == drop) nseg--;  // the dropped rows' segment is not a key
+  }
+  if (nseg > 0)
+    hipLaunchKernelGGL(k_sess_ukeys, dim3(ceil_div(nseg, 256)), dim3(256), 0, st, S.ukeys.as<int64_t>(),
+                       S.nseg.as<int>(), kmin);
   KHIP_TRY(S.useg.ensure((size_t)(nseg + 1) * 8));
   KHIP_TRY(S.s0.ensure((size_t)(nseg + 1) * 8));
   KHIP_TRY(S.cap.ensure((size_t)(nseg + 1) * 8));
   KHIP_TRY(S.scap.ensure((size_t)(nseg + 1) * 8));
   KHIP_TRY(S.fin.ensure((size_t)(nseg + 1) * 8));
   KHIP_TRY(S.fin_pre.ensure((size_t)(nseg + 1) * 8));
+  hipLaunchKernelGGL(k_sess_setn, dim3(1), dim3(1), 0, st, S.nseg.as<int>(), nseg);
   KHIP_TRY(cub_call(S.tmp, st, [&](void* p, size_t& b) {
     return hipcub::DeviceScan::ExclusiveSum(p, b, S.ucnt.as<int>(), S.useg.as<int64_t>(), nseg, st);
   }));
   const uint64_t* store = S.rows.as<uint64_t>();
   const int64_t ns = S.n;
-  hipLaunchKernelGGL(k_sess_bounds, dim3(ceil_div(nseg, 256)), dim3(256), 0, st, store, ns, sw, S.ukeys.as<int64_t>(),
+  if (nseg > 0)
+    hipLaunchKernelGGL(k_sess_bounds, dim3(ceil_div(nseg, 256)), dim3(256), 0, st, store, ns, sw, S.ukeys.as<int64_t>(),
                      S.ucnt.as<int>(), S.nseg.as<int>(), S.s0.as<int64_t>(), S.cap.as<int64_t>());
   KHIP_TRY(cub_call(S.tmp, st, [&](void* p, size_t& b) {
     return hipcub::DeviceScan::ExclusiveSum(p, b, S.cap.as<int64_t>(), S.scap.as<int64_t>(), nseg, st);
@@ -459,12 +727,14 @@ khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   q.gap = a->desc.size_ms;
   q.grace = a->grace;
   q.retention = a->retention;
-  hipLaunchKernelGGL(k_sess_apply, dim3(ceil_div(nseg, 64)), dim3(64), 0, st, q, store, S.ukeys.as<int64_t>(),
+  if (nseg > 0)
+    hipLaunchKernelGGL(k_sess_apply, dim3(ceil_div(nseg, 64)), dim3(64), 0, st, q, store, S.ukeys.as<int64_t>(),
                      S.ucnt.as<int>(), S.useg.as<int64_t>(), S.nseg.as<int>(), S.s0.as<int64_t>(), S.cap.as<int64_t>(),
-                     S.scap.as<int64_t>(), v_out, ts, kv, rv, cols, S.st_after.as<int64_t>(),
+                     S.scap.as<int64_t>(), v_out, S.gath.as<longlong2>(), cols,
                      a->stream_time.as<int64_t>(), S.srow.as<uint64_t>(), S.sfl.as<uint8_t>(), S.trow.as<uint64_t>(),
                      S.fin.as<int64_t>(), keep_changes ? S.crow.as<uint64_t>() : nullptr,
-                     keep_changes ? S.ctomb.as<uint8_t>() : nullptr, S.ctr.as<unsigned long long>(), keep_changes ? 1 : 0);
+                     keep_changes ? S.ctomb.as<uint8_t>() : nullptr, S.ctr.as<unsigned long long>(), keep_changes ? 1 : 0,
+                     (int64_t)nseg);
   KHIP_TRY_HIP(hipGetLastError());
   // the new store
   KHIP_TRY(S.keep.ensure((size_t)(ns + 1) * 4));
@@ -496,8 +766,9 @@ khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     hipLaunchKernelGGL(k_sess_scatter_store, dim3(ceil_div(ns, 256)), dim3(256), 0, st, store, ns, sw, S.keep.as<int>(),
                        S.keep_pre.as<int>(), S.ukeys.as<int64_t>(), S.nseg.as<int>(), S.fin_pre.as<int64_t>(),
                        S.rows2.as<uint64_t>());
-  hipLaunchKernelGGL(k_sess_scatter_seg, dim3(ceil_div(nseg, 64)), dim3(64), 0, st, store, ns, sw, S.keep_pre.as<int>(),
-                     S.keep.as<int>(), S.ukeys.as<int64_t>(), S.nseg.as<int>(), S.fin.as<int64_t>(),
+  if (nseg > 0)
+    hipLaunchKernelGGL(k_sess_scatter_seg, dim3(ceil_div(nseg, 256)), dim3(256), 0, st, store, ns, sw, S.keep_pre.as<int>(),
+                     S.keep.as<int>(), S.ukeys.as<int64_t>(), (int64_t)nseg, S.fin.as<int64_t>(),
                      S.fin_pre.as<int64_t>(), S.scap.as<int64_t>(), S.srow.as<uint64_t>(), S.rows2.as<uint64_t>());
   KHIP_TRY_HIP(hipGetLastError());
   unsigned long long c[32];
@@ -534,7 +805,7 @@ khip_status sess_changes(khip_agg* a, std::vector<uint64_t>* rows, std::vector<u
 
 void sess_release(khip_agg* a) {
   SessState& S = a->sess;
-  DevBuf* bufs[] = {&S.rows, &S.rows2, &S.skey, &S.sidx, &S.skey2, &S.sidx2, &S.st_after, &S.ukeys, &S.ucnt, &S.nseg,
+  DevBuf* bufs[] = {&S.rows, &S.rows2, &S.skey, &S.sidx, &S.skey2, &S.sidx2, &S.st_after, &S.gath, &S.blockkr, &S.ukeys, &S.ucnt, &S.nseg,
                     &S.useg, &S.s0, &S.cap, &S.scap, &S.fin, &S.fin_pre, &S.srow, &S.sfl, &S.trow, &S.crow, &S.ctomb,
                     &S.keep, &S.keep_pre, &S.ctr, &S.tmp};
   for (DevBuf* b : bufs) b->release();

@@ -26,7 +26,7 @@
 //                  and store the last row.  Group updates are agent-scope atomics; the row time
 //                  is an atomic max.  Integer state is exact (wrapping adds commute); DOUBLE sums
 //                  are order-dependent only by rounding.
-//   k_finalize     (khip_agg.hip) group claims → resident groups
+//   k_tagg_grp_finalize  this push's group claims → resident groups (the claimed slots only)
 //   k_tagg_src_finalize  source claims → resident keys
 #include <hipcub/hipcub.hpp>
 
@@ -44,7 +44,7 @@ constexpr uint64_t TS_RESIDENT = 1ULL << 62;
 constexpr uint64_t TF_LIVE = 1, TF_GVALID = 2;
 constexpr int TS_MAX_PROBE = 4096;
 
-enum { TC_ACCEPTED, TC_NULL_KEY, TC_BAD_TS, TC_UPDATES, TC_NEW_GROUPS, TC_NEW_KEYS, TC_FAILED, TC_N };
+enum { TC_ACCEPTED, TC_NULL_KEY, TC_BAD_TS, TC_UPDATES, TC_NEW_GROUPS, TC_NEW_KEYS, TC_FAILED, TC_GLIST, TC_N };
 
 __device__ __forceinline__ uint64_t src_hash(int64_t id) { return mix64((uint64_t)id ^ 0x3C6EF372FE94F82BULL); }
 
@@ -84,7 +84,8 @@ struct TRow {
 // Returns 0 on probe exhaustion, 1 on update, 2 on update of a newly claimed group.
 __device__ __forceinline__ int group_update(const ApplyParams& p, uint64_t* __restrict__ table, uint64_t mask,
                                             const TRow& r, int sign, int64_t row, int64_t t,
-                                            const int64_t* __restrict__ gkeys) {
+                                            const int64_t* __restrict__ gkeys, int64_t* __restrict__ glist,
+                                            unsigned long long* __restrict__ ctr) {
   const uint64_t h = group_hash(r.ghash, 0);
   const uint64_t fp = (h >> 49) & 0x7FFFULL;
   const uint64_t myref = (1ULL << 63) | (fp << 48) | (uint64_t)row;
@@ -105,6 +106,7 @@ __device__ __forceinline__ int group_update(const ApplyParams& p, uint64_t* __re
         if (old == 0) {
           hit = true;
           isnew = 1;
+          glist[atomicAdd(&ctr[TC_GLIST], 1ULL)] = (int64_t)slot;  // finalized by k_tagg_grp_finalize
         } else {
           w0 = old;
         }
@@ -158,6 +160,7 @@ struct TaggArgs {
   int32_t n_cols;
   int32_t col_type[MAX_COLS];
   int64_t n;
+  int64_t* glist;   // group slots claimed by this push
 };
 
 __device__ __forceinline__ int64_t load_word(const ColPtrs& c, int32_t type, int col, int64_t i) {
@@ -170,8 +173,15 @@ __global__ __launch_bounds__(256) void k_tagg_apply(TaggArgs A, const uint64_t* 
                                                     const uint8_t* __restrict__ rv, const int64_t* __restrict__ ts,
                                                     ColPtrs cols, const uint8_t* __restrict__ src_kv,
                                                     int64_t* __restrict__ claimed, unsigned long long* __restrict__ ctr) {
-  int64_t upd = 0, newg = 0, newk = 0, failed = 0;
-  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < A.n; j += (int64_t)gridDim.x * blockDim.x) {
+  int64_t upd = 0, newg = 0, failed = 0;
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = lane ? (~0ULL >> (64 - lane)) : 0ULL;
+  // every lane of a wave runs the same iterations: new source slots are listed with one counter
+  // add per wave (a returning same-address atomic per new key would serialize)
+  for (int64_t j0 = blockIdx.x * (int64_t)blockDim.x; j0 < A.n; j0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = j0 + threadIdx.x;
+    int64_t fresh_slot = -1;
+    if (j < A.n) do {  // `continue` below leaves this record's body
     const uint64_t k = skey[j];
     if (j > 0 && skey[j - 1] == k) continue;  // not the segment leader
     int64_t end = j + 1;
@@ -218,15 +228,14 @@ __global__ __launch_bounds__(256) void k_tagg_apply(TaggArgs A, const uint64_t* 
       prev.ghash = (int64_t)s[4];
       for (int c = 0; c < A.n_cols; c++) prev.w[c] = (int64_t)s[TS_WORDS + c];
     } else {
-      claimed[atomicAdd(&ctr[TC_NEW_KEYS], 1ULL)] = (int64_t)slot;
-      newk++;
+      fresh_slot = (int64_t)slot;
     }
     for (int64_t q = j; q < end; q++) {
       const int64_t r = sidx[q];
       const int64_t t = ts[r];
       if (!bit_get(src_kv, r) || t < 0) continue;
       if ((prev.flags & (TF_LIVE | TF_GVALID)) == (TF_LIVE | TF_GVALID)) {  // undo the previous row
-        const int u = group_update(A.p, A.table, A.gmask, prev, -1, r, t, gkeys);
+        const int u = group_update(A.p, A.table, A.gmask, prev, -1, r, t, gkeys, A.glist, ctr);
         if (u == 0) failed++;
         upd++;
       }
@@ -247,7 +256,7 @@ __global__ __launch_bounds__(256) void k_tagg_apply(TaggArgs A, const uint64_t* 
         cur.flags |= (v ? 1u : 0u) << (8 + c);
       }
       if (cur.flags & TF_GVALID) {
-        const int u = group_update(A.p, A.table, A.gmask, cur, +1, r, t, gkeys);
+        const int u = group_update(A.p, A.table, A.gmask, cur, +1, r, t, gkeys, A.glist, ctr);
         if (u == 0) failed++;
         newg += u == 2;
         upd++;
@@ -259,6 +268,15 @@ __global__ __launch_bounds__(256) void k_tagg_apply(TaggArgs A, const uint64_t* 
     s[3] = (uint64_t)prev.gid;
     s[4] = (uint64_t)prev.ghash;
     for (int c = 0; c < A.n_cols; c++) s[TS_WORDS + c] = (uint64_t)prev.w[c];
+    } while (0);
+    const uint64_t mk = __ballot(fresh_slot >= 0);
+    if (mk) {
+      const int first = __ffsll((unsigned long long)mk) - 1;
+      unsigned long long x0 = 0;
+      if (lane == first) x0 = atomicAdd(&ctr[TC_NEW_KEYS], (unsigned long long)__popcll(mk));
+      x0 = __shfl(x0, first, 64);
+      if (fresh_slot >= 0) claimed[(int64_t)x0 + __popcll(mk & below)] = fresh_slot;
+    }
   }
   upd = wave_sum(upd);
   newg = wave_sum(newg);
@@ -267,6 +285,23 @@ __global__ __launch_bounds__(256) void k_tagg_apply(TaggArgs A, const uint64_t* 
     if (upd) atomicAdd(&ctr[TC_UPDATES], (unsigned long long)upd);
     if (newg) atomicAdd(&ctr[TC_NEW_GROUPS], (unsigned long long)newg);
     if (failed) atomicAdd(&ctr[TC_FAILED], (unsigned long long)failed);
+  }
+}
+
+// This push's group claims → resident groups (key word from the claiming row, ws = 0): only the
+// claimed slots are visited, not the table.
+__global__ __launch_bounds__(256) void k_tagg_grp_finalize(uint64_t* __restrict__ table, int sw,
+                                                           const int64_t* __restrict__ list,
+                                                           const unsigned long long* __restrict__ n_list,
+                                                           const int64_t* __restrict__ gkeys) {
+  const int64_t nc = (int64_t)*n_list;
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < nc; k += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t* s = table + (uint64_t)list[k] * (uint64_t)sw;
+    const uint64_t w0 = s[0];
+    if ((int64_t)s[1] == EMPTY_WS && w0 != 0) {
+      s[0] = (uint64_t)gkeys[(int64_t)(w0 & ((1ULL << 36) - 1))];
+      s[1] = 0;
+    }
   }
 }
 
@@ -374,6 +409,7 @@ khip_status tagg_push(khip_agg* a, int64_t n, const int64_t* gkeys, const int64_
   KHIP_TRY(T.sidx.ensure(n * 4));
   KHIP_TRY(T.sidx2.ensure(n * 4));
   KHIP_TRY(T.claimed.ensure(n * 8));
+  KHIP_TRY(T.gclaimed.ensure(n * 8));
   KHIP_TRY(T.ctr.ensure(TC_N * 8));
   unsigned long long* ctr = T.ctr.as<unsigned long long>();
   KHIP_TRY_HIP(hipMemsetAsync(ctr, 0, TC_N * 8, st));
@@ -398,10 +434,11 @@ khip_status tagg_push(khip_agg* a, int64_t n, const int64_t* gkeys, const int64_
   A.n_cols = a->desc.n_cols;
   for (int c = 0; c < MAX_COLS; c++) A.col_type[c] = a->ap.col_type[c];
   A.n = n;
+  A.glist = T.gclaimed.as<int64_t>();
   hipLaunchKernelGGL(k_tagg_apply, dim3(tgrid(n, 16384)), dim3(256), 0, st, A, kout, vout, gkeys, ghash, kv, rv, ts,
                      cols, src_kv, T.claimed.as<int64_t>(), ctr);
-  hipLaunchKernelGGL(k_finalize, dim3(tgrid(a->cap)), dim3(256), 0, st, a->table.as<uint64_t>(), a->cap, a->sw, gkeys,
-                     ts, 0, (int64_t)0, (int64_t)1);
+  hipLaunchKernelGGL(k_tagg_grp_finalize, dim3(tgrid(n, 1024)), dim3(256), 0, st, a->table.as<uint64_t>(), a->sw,
+                     T.gclaimed.as<int64_t>(), (const unsigned long long*)&ctr[TC_GLIST], gkeys);
   hipLaunchKernelGGL(k_tagg_src_finalize, dim3(tgrid(n)), dim3(256), 0, st, T.src.as<uint64_t>(), T.src_sw,
                      T.claimed.as<int64_t>(), (const unsigned long long*)&ctr[TC_NEW_KEYS], kout);
   KHIP_TRY_HIP(hipGetLastError());
@@ -429,7 +466,7 @@ khip_status tagg_reset(khip_agg* a) {
 
 void tagg_release(khip_agg* a) {
   TaggState& T = a->tagg;
-  DevBuf* bufs[] = {&T.src, &T.sid, &T.skey, &T.skey2, &T.sidx, &T.sidx2, &T.tmp, &T.ctr, &T.claimed,
+  DevBuf* bufs[] = {&T.src, &T.sid, &T.skey, &T.skey2, &T.sidx, &T.sidx2, &T.tmp, &T.ctr, &T.claimed, &T.gclaimed,
                     &T.st_koff, &T.st_kbytes, &T.st_kv, &T.st_key, &T.shash};
   for (DevBuf* b : bufs) b->release();
   dict_release(T.dict);

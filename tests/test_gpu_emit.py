@@ -232,3 +232,53 @@ def test_sessions_hot_key_and_big_batch(prod, orc):
     assert_snap_equal(g.snapshot(), o.snapshot(), g.desc, ABS_SUM, CNT_DBL)
     g.close()
     o.close()
+
+
+def test_sessions_bench_shape_vs_oracle(prod, orc):
+    """bench.py --config session's shape (C2's records, COUNT(*) WINDOW SESSION (1 SECOND)) at
+    4M records / 400k card numbers in two pushes: the store, row count and drop counters equal
+    the oracle's."""
+    from ksql_amd import synth
+    n, keys = 4_000_000, 400_000
+    card, ts = synth.possible_fraud(0, n, n, keys=keys)
+    kw = dict(window_kind="SESSION", size_ms=1000, key_type="INT64", aggs=[("COUNT_STAR", -1)])
+    g = abi.AggHandle(prod, abi.make_agg_desc(**dict(kw, capacity_hint=3 * keys)))
+    o = abi.AggHandle(orc, abi.make_agg_desc(**kw))
+    for lo in (0, n // 2):
+        b = abi.HostBatch(ts[lo:lo + n // 2], keys=card[lo:lo + n // 2])
+        assert g.push(b) == o.push(b)
+    s = o.snapshot()
+    assert_snap_equal(g.snapshot(), s, g.desc, ABS_SUM, CNT_DBL)
+    assert g.count_rows(None) == s["n"]
+    g.close()
+    o.close()
+
+
+def test_sessions_key_range_edges(prod, orc):
+    """The session sort runs over key - kmin on the bits of the push's key range: keys at both
+    ends of BIGINT (the full 64-bit range, no sentinel key for dropped rows), a push whose
+    records are all dropped, a single-key push, dropped rows mixed with the largest key."""
+    kw = dict(SESSIONS[0], key_type="INT64", col_types=COLS, aggs=ALL_AGGS)
+    g = abi.AggHandle(prod, abi.make_agg_desc(**dict(kw, flags=abi.FLAG_CHANGELOG)))
+    o = abi.AggHandle(orc, abi.make_agg_desc(**kw))
+    rng = np.random.default_rng(77)
+    lo64, hi64 = np.iinfo(np.int64).min, np.iinfo(np.int64).max
+
+    def batch(keys, ts, key_valid=None):
+        m = len(keys)
+        cols = [rng.integers(-9, 9, m).astype(np.int32), rng.integers(-9, 9, m), rng.random(m), rng.random(m)]
+        return abi.HostBatch(np.asarray(ts, np.int64), keys=np.asarray(keys, np.int64), key_valid=key_valid, cols=cols)
+
+    pushes = [
+        batch([lo64, hi64, 0, lo64, hi64, -1, 1], [10, 20, 30, 40, 50, -5, 60]),
+        batch([5, 6, 7], [100, 110, 120], key_valid=[False, False, False]),
+        batch([hi64] * 5, [200, 30_000, 30_100, 90_000, 95_000]),
+        batch([hi64, 3, hi64, 4], [96_000, 96_500, 97_000, -1], key_valid=[True, False, True, True]),
+        batch([lo64 + 1, lo64 + 2, lo64 + 1], [98_000, 98_000, 99_000]),
+    ]
+    for b in pushes:
+        assert g.push(b) == o.push(b)
+        _assert_changes_equal(g.changes(), o.changes(), g.desc)
+        assert_snap_equal(g.snapshot(), o.snapshot(), g.desc, ABS_SUM, CNT_DBL)
+    g.close()
+    o.close()
