@@ -240,12 +240,61 @@ __device__ int put_number(const SerdeParams& q, int f, const uint8_t* p, int64_t
   return 0;
 }
 
+// Stage the bytes [b0, b1) of `base` (one wave's records: the offsets are monotone) into the
+// wave's LDS buffer with dword loads (coalesced); the record parsers then read LDS instead of
+// issuing one global byte load per character.  Returns false (nothing staged) when the range does
+// not fit.  lds byte of global byte x = buf + (x - *shift).
+template <int WORDS>
+__device__ __forceinline__ bool stage_bytes(uint32_t* buf, const uint8_t* base, int64_t b0, int64_t b1, int lane,
+                                            int64_t* shift) {
+  const uintptr_t ua = ((uintptr_t)(base + b0)) & ~(uintptr_t)3;
+  const uintptr_t ue = (uintptr_t)(base + b1);
+  const int64_t words = (int64_t)((ue - ua + 3) >> 2);
+  if (b1 <= b0 || words > WORDS) return false;
+  for (int64_t x = lane; x < words; x += 64) {
+    const uintptr_t a = ua + 4 * (uintptr_t)x;
+    uint32_t w;
+    if (a >= (uintptr_t)(base + b0) && a + 4 <= ue) {
+      w = *(const uint32_t*)a;
+    } else {  // the range's partial first / last dword: only its bytes inside [b0, b1)
+      w = 0;
+      for (int k = 0; k < 4; k++) {
+        const uintptr_t ak = a + k;
+        if (ak >= (uintptr_t)(base + b0) && ak < ue) w |= (uint32_t)(*(const uint8_t*)ak) << (8 * k);
+      }
+    }
+    buf[x] = w;
+  }
+  *shift = (int64_t)(ua - (uintptr_t)base);
+  return true;
+}
+
+constexpr int SERDE_VWORDS = 1024;  // 4 KB of value bytes per wave (64 records of <= 64 bytes)
+constexpr int SERDE_KWORDS = 256;   // 1 KB of key bytes per wave
+
+// MAXF: compile-time bound on the schema's field count: the JSON field-token arrays (private
+// memory) shrink to the schema (4 for the common narrow schemas; 32 otherwise).
+template <int MAXF>
 __global__ __launch_bounds__(256) void k_serde_decode(SerdeParams q, int64_t n, const int64_t* __restrict__ koff,
                                                       const uint8_t* __restrict__ kbytes, const uint8_t* __restrict__ kval,
                                                       const int64_t* __restrict__ voff, const uint8_t* __restrict__ vbytes,
                                                       const uint8_t* __restrict__ vval, SerdeOut o) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ uint32_t vst[4][SERDE_VWORDS];
+  __shared__ uint32_t kst[4][SERDE_KWORDS];
+  const int64_t w0 = i - lane, wl = (n - 1 < w0 + 63) ? n - 1 : w0 + 63;
+  int64_t vshift = 0, kshift = 0;
+  bool vstaged = false, kstaged = false;
+  if (w0 < n) {
+    vstaged = stage_bytes<SERDE_VWORDS>(vst[wave], vbytes, voff[w0], voff[wl + 1], lane, &vshift);
+    if (q.key_format != KHIP_FMT_NONE && kbytes)
+      kstaged = stage_bytes<SERDE_KWORDS>(kst[wave], kbytes, koff[w0], koff[wl + 1], lane, &kshift);
+  }
+  __syncthreads();
+  // byte x of the record bytes: staged ? LDS[x - shift] : global[x]
+  auto vat = [&](int64_t x) { return vstaged ? (const uint8_t*)vst[wave] + (x - vshift) : vbytes + x; };
+  auto kat = [&](int64_t x) { return kstaged ? (const uint8_t*)kst[wave] + (x - kshift) : kbytes + x; };
   bool ok = i < n;  // deserialized without error
   bool key_ok = false, row_ok = false;
   uint32_t fnull = 0;  // per output column: NULL
@@ -257,10 +306,10 @@ __global__ __launch_bounds__(256) void k_serde_decode(SerdeParams q, int64_t n, 
     } else if (bit_get(kval, i)) {
       const int64_t k0 = koff[i], kn = koff[i + 1] - k0;
       if (q.key_type == KHIP_TYPE_INT64) {
-        if (kn == 8) o.key_i64[i] = (int64_t)be_load(kbytes + k0, 8);
+        if (kn == 8) o.key_i64[i] = (int64_t)be_load(kat(k0), 8);
         else ok = false;
       } else if (q.key_type == KHIP_TYPE_INT32) {
-        if (kn == 4) o.key_i64[i] = (int64_t)(int32_t)(uint32_t)be_load(kbytes + k0, 4);
+        if (kn == 4) o.key_i64[i] = (int64_t)(int32_t)(uint32_t)be_load(kat(k0), 4);
         else ok = false;
       }
       key_ok = true;  // STRING keys: the bytes themselves
@@ -269,7 +318,7 @@ __global__ __launch_bounds__(256) void k_serde_decode(SerdeParams q, int64_t n, 
     row_ok = bit_get(vval, i);
     if (ok && row_ok) {
       const int64_t v0 = voff[i], vn = voff[i + 1] - v0;
-      const uint8_t* p = vbytes + v0;
+      const uint8_t* p = vat(v0);
       for (int c = 0; c < q.n_out; c++) fnull |= 1u << c;
       if (q.value_format == KHIP_FMT_KAFKA) {
         const int f = 0;
@@ -342,7 +391,7 @@ __global__ __launch_bounds__(256) void k_serde_decode(SerdeParams q, int64_t n, 
         int64_t j = 0;
         while (j < vn && json_ws(p[j])) j++;
         if (j >= vn || p[j] != '{') ok = false;
-        Tok ex[SD_MAX_FIELDS], ci[SD_MAX_FIELDS];
+        Tok ex[MAXF], ci[MAXF];
         for (int f = 0; f < q.n_fields; f++) {
           ex[f].kind = -1;
           ci[f].kind = -1;
@@ -378,17 +427,19 @@ __global__ __launch_bounds__(256) void k_serde_decode(SerdeParams q, int64_t n, 
           } else {
             nl = kt.len <= SD_NAME_BYTES ? (int)kt.len : -1;
           }
-          if (nl >= 0)
+          if (nl >= 0) {
             for (int f = 0; f < q.n_fields; f++) {
-              if (q.name_len[f] != nl) continue;
-              bool same = true, same_up = true;
-              for (int k = 0; k < nl; k++) {
-                same &= kp[k] == q.name[f][k];
-                same_up &= up(kp[k]) == q.name[f][k];
+              if (q.name_len[f] == nl) {
+                bool same = true, same_up = true;
+                for (int k = 0; k < nl; k++) {
+                  same &= kp[k] == q.name[f][k];
+                  same_up &= up(kp[k]) == q.name[f][k];
+                }
+                if (same) ex[f] = vt;
+                else if (same_up) ci[f] = vt;
               }
-              if (same) ex[f] = vt;
-              else if (same_up) ci[f] = vt;
             }
+          }
           while (j < vn && json_ws(p[j])) j++;
           if (j < vn && p[j] == ',') { j++; continue; }
           if (j < vn && p[j] == '}') break;
@@ -626,8 +677,12 @@ khip_status khip_serde_decode(khip_serde* s, const khip_raw_batch* in, khip_batc
   unsigned long long c2[2] = {0, 0};
   if (n > 0) {
     for (int attempt = 0; attempt < 2; attempt++) {
-      hipLaunchKernelGGL(k_serde_decode, dim3(ceil_div(n, 256)), dim3(256), 0, s->stream, q, n, koff, kb, kv, voff, vb, vv,
-                         o);
+      if (q.n_fields <= 4)
+        hipLaunchKernelGGL(k_serde_decode<4>, dim3(ceil_div(n, 256)), dim3(256), 0, s->stream, q, n, koff, kb, kv, voff, vb,
+                           vv, o);
+      else
+        hipLaunchKernelGGL(k_serde_decode<SD_MAX_FIELDS>, dim3(ceil_div(n, 256)), dim3(256), 0, s->stream, q, n, koff, kb,
+                           kv, voff, vb, vv, o);
       KHIP_TRY_HIP(hipGetLastError());
       KHIP_TRY_HIP(hipMemcpyAsync(c2, s->ctr.p, 16, hipMemcpyDeviceToHost, s->stream));
       KHIP_TRY_HIP(hipStreamSynchronize(s->stream));

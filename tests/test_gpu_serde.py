@@ -216,3 +216,49 @@ def test_qtt_raw_records_end_to_end(prod, case):
     h.close()
     sd.close()
     assert qtt.compare_outputs(case, rows) == []
+
+
+@pytest.mark.parametrize("narrow", [False, True])
+@pytest.mark.parametrize("fmt", ["DELIMITED", "JSON"])
+def test_decode_device_batches_staged_and_long(prod, fmt, narrow):
+    """khip_serde_decode on a device-resident raw batch (bench.py's serde_json path): the
+    kernel stages each wave's record bytes in LDS when they fit (unaligned record offsets, partial
+    first/last dwords) and reads HBM directly when a wave's records are too long (padding makes
+    every 7th wave's records exceed the stage).  narrow: a 4-field schema (the kernel variant
+    whose field-token arrays live in registers)."""
+    torch = pytest.importorskip("torch")
+    fields = FIELDS[1:5] if narrow else FIELDS
+    rng = random.Random({"DELIMITED": 11, "JSON": 12}[fmt])
+    n = 3000
+    keys, vals = _records(rng, fmt, n)
+    if fmt == "JSON":
+        vals = [v if (v is None or (i // 64) % 7) else v[:1] + b" " * 90 + v[1:] for i, v in enumerate(vals)]
+    else:
+        vals = [v if (v is None or (i // 64) % 7) else v + b"\r\n" + b"x" * 90 for i, v in enumerate(vals)]
+    if narrow and fmt == "DELIMITED":  # the narrow schema's records: fields 1..4 of each row
+        vals = [v if v is None else _narrow_delimited(v) for v in vals]
+    exp, experr = serde_ref.decode(fmt, fields, "INT64", keys, vals)
+
+    def pack(items):
+        offs = np.zeros(n + 1, np.int64)
+        offs[1:] = np.cumsum([0 if x is None else len(x) for x in items])
+        data = np.frombuffer(b"".join(b"" if x is None else x for x in items) + b"\0", np.uint8).copy()
+        valid = np.array([x is not None for x in items])
+        return offs, data, valid
+    koff, kb, kvld = pack(keys)
+    voff, vb, vvld = pack(vals)
+    dev = lambda a: torch.from_numpy(a).cuda()
+    ts = dev(np.arange(n, dtype=np.int64))
+    sd = abi.SerdeHandle(prod, fmt, fields, key_type="INT64")
+    d, nerr = sd.decode_device(ts, dev(koff), dev(kb), dev(voff), dev(vb), key_valid=dev(abi.bitmap(kvld)),
+                               value_valid=dev(abi.bitmap(vvld)))
+    assert nerr == experr
+    _check(sd.columns(d, OUT_TYPES), exp, fields, OUT_TYPES)
+    sd.close()
+
+
+def _narrow_delimited(v):
+    """Drop a DELIMITED record's first and last field (the ID / SKIPPED columns) when it is a plain
+    6-field row; other records (quoted, malformed) stay as they are: errors on both sides."""
+    parts = v.split(b",")
+    return b",".join(parts[1:5]) if len(parts) == 6 and b'"' not in v and b"\n" not in v else v
