@@ -273,7 +273,8 @@ def bench_serde_json(args, lib, rank, world, local):
         return
     ms_step = elapsed * 1000.0 / args.steps
     bpr = 8 + w + 2 * 8 + 8 + 8  # key bytes + value bytes + 2 offsets read; key + value columns written
-    roof = roofline(bpr * n, ms_step, None, None, None, bpr, kernel="khip_serde_decode (k_serde_decode)")
+    roof = roofline(bpr * n, ms_step, None, None, load_traffic(args.traffic_json, "serde_json", n), bpr,
+                    kernel="khip_serde_decode (k_serde_decode)")
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         import json as _json
@@ -338,7 +339,7 @@ def bench_table_agg(args, lib, rank, world, local):
         return
     ms_step = elapsed * 1000.0 / args.steps
     bpr = 32 + 2 * 48 + 2 * 2 * 32  # row in (pk, region, ts, amount) + source-row RMW + undo and apply group RMWs
-    roof = roofline(bpr * n, ms_step, None, None, None, bpr,
+    roof = roofline(bpr * n, ms_step, None, None, load_traffic(args.traffic_json, "table_agg", n), bpr,
                     kernel="khip_agg_push_table (k_tagg_keys + radix sort + k_tagg_apply + finalize)")
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
@@ -389,8 +390,8 @@ def bench_session(args, lib, rank, world, local):
         return
     ms_step = elapsed * 1000.0 / args.steps
     bpr = 16 + 2 * 32  # key + ts in, one session-row RMW
-    roof = roofline(bpr * n, ms_step, None, None, None, bpr,
-                    kernel="khip_agg_push, SESSION engine (sort + one thread per key + store rebuild)")
+    roof = roofline(bpr * n, ms_step, None, None, load_traffic(args.traffic_json, "session", n), bpr,
+                    kernel="khip_agg_push, SESSION engine (key-range sort + LDS per-key replay + store rebuild)")
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         orc = abi.load_oracle()
