@@ -1211,6 +1211,9 @@ constexpr uint32_t RT_MATCHED = 0x80000000u;
 #ifndef KHIP_MG_AU_GEN
 #define KHIP_MG_AU_GEN 2   // k_part_merge (other update sets) records per thread per chunk
 #endif
+#ifndef KHIP_MG_AU_GEN_WIDE
+#define KHIP_MG_AU_GEN_WIDE 2  // the same with 16-byte (+ argument word) records
+#endif
 
 struct MergeParams {
   int32_t windowed;
@@ -1469,7 +1472,7 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
   __shared__ unsigned long long lbase;
   __shared__ MgWord wtab[32];
   __shared__ MgOp otab[MAX_OPS];
-  constexpr int AU = CNT1 ? KHIP_MG_AU_CNT1 : KHIP_MG_AU_GEN;  // records per thread per chunk (two chunks in registers)
+  constexpr int AU = CNT1 ? KHIP_MG_AU_CNT1 : (R12M ? KHIP_MG_AU_GEN : KHIP_MG_AU_GEN_WIDE);  // records per thread per chunk (two chunks in registers)
   constexpr int NW = NT / 64;
   const int H = q.H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;

@@ -73,22 +73,38 @@ __global__ __launch_bounds__(256) void k_tagg_keys(const int64_t* __restrict__ s
 }
 
 // One row's aggregate contribution: argument words + validity mask (bit c = column c non-null).
+// NC (the handle's argument column count) is a template parameter: the words stay in registers
+// (a run-time bound would index them dynamically and put every row in scratch memory).
+template <int NC>
 struct TRow {
   int64_t gid, ghash;
   uint32_t flags;  // TF_* | valid mask << 8
-  int64_t w[MAX_COLS];
+  int64_t w[NC > 0 ? NC : 1];
 };
 
-// Add (sign +1, may create the group; claim references batch row `row`) or undo (sign -1: the
-// group exists — resident, or claimed earlier in this push) one row's contribution.
+// r.w[col] for a run-time col without dynamic register indexing
+template <int NC>
+__device__ __forceinline__ int64_t wpick(const TRow<NC>& r, int col) {
+  int64_t v = 0;
+#pragma unroll
+  for (int c = 0; c < NC; c++) v = c == col ? r.w[c] : v;
+  return v;
+}
+
+// One group's net change from one source key's changes in this push: + `add`'s contribution, −
+// `sub`'s (either may be null; both null = a touch: the row time only — a group an intermediate
+// row of the key passed through, whose +x / −x cancel).  The group is found, or claimed when
+// claim_row >= 0 (the claim references that batch row, whose GROUP BY key is the group's).
 // Returns 0 on probe exhaustion, 1 on update, 2 on update of a newly claimed group.
-__device__ __forceinline__ int group_update(const ApplyParams& p, uint64_t* __restrict__ table, uint64_t mask,
-                                            const TRow& r, int sign, int64_t row, int64_t t,
-                                            const int64_t* __restrict__ gkeys, int64_t* __restrict__ glist,
-                                            unsigned long long* __restrict__ ctr) {
-  const uint64_t h = group_hash(r.ghash, 0);
+template <int NC>
+__device__ __forceinline__ int group_net(const ApplyParams& p, uint64_t* __restrict__ table, uint64_t mask,
+                                         int64_t gid, int64_t ghash, bool has_add, const TRow<NC>& add, bool has_sub,
+                                         const TRow<NC>& sub, int64_t t,
+                                         int64_t claim_row, const int64_t* __restrict__ gkeys,
+                                         int64_t* __restrict__ glist, unsigned long long* __restrict__ ctr) {
+  const uint64_t h = group_hash(ghash, 0);
   const uint64_t fp = (h >> 49) & 0x7FFFULL;
-  const uint64_t myref = (1ULL << 63) | (fp << 48) | (uint64_t)row;
+  const uint64_t myref = (1ULL << 63) | (fp << 48) | (uint64_t)(claim_row < 0 ? 0 : claim_row);
   uint64_t slot = h & mask;
   const int sw = p.slot_words;
   for (int probe = 0; probe < MAX_PROBE; probe++) {
@@ -97,11 +113,11 @@ __device__ __forceinline__ int group_update(const ApplyParams& p, uint64_t* __re
     bool hit = false;
     int isnew = 0;
     if (w1 != EMPTY_WS) {
-      hit = (int64_t)s[0] == r.gid;
+      hit = (int64_t)s[0] == gid;
     } else {
       uint64_t w0 = ld_relaxed(s);
       if (w0 == 0) {
-        if (sign < 0) return 0;  // an undo always finds its group
+        if (claim_row < 0) return 0;  // an undo always finds its group
         const uint64_t old = atomicCAS((unsigned long long*)s, 0ULL, (unsigned long long)myref);
         if (old == 0) {
           hit = true;
@@ -111,32 +127,33 @@ __device__ __forceinline__ int group_update(const ApplyParams& p, uint64_t* __re
           w0 = old;
         }
       }
-      if (!hit && ((w0 >> 48) & 0x7FFFULL) == fp) hit = gkeys[(int64_t)(w0 & ((1ULL << 36) - 1))] == r.gid;
+      if (!hit && ((w0 >> 48) & 0x7FFFULL) == fp) hit = gkeys[(int64_t)(w0 & ((1ULL << 36) - 1))] == gid;
     }
     if (hit) {
       __hip_atomic_fetch_max((int64_t*)&s[2], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (int o = 0; o < p.n_ops; o++) {
         const UpdOp op = p.ops[o];
         int64_t* w = (int64_t*)&s[op.word];
-        if (op.kind == OP_INC) {  // COUNT(*) = COUNT(ROWTIME): never null
-          __hip_atomic_fetch_add(w, (int64_t)sign, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          continue;
-        }
-        if (!((r.flags >> (8 + op.col)) & 1u)) continue;  // null argument: unchanged (undo too)
+        const bool va = has_add && (op.kind == OP_INC || ((add.flags >> (8 + op.col)) & 1u));
+        const bool vs = has_sub && (op.kind == OP_INC || ((sub.flags >> (8 + op.col)) & 1u));
+        if (!va && !vs) continue;  // null arguments (undo too): unchanged
         switch (op.kind) {
-          case OP_INC_VALID:
-            __hip_atomic_fetch_add(w, (int64_t)sign, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          case OP_INC:        // COUNT(*) = COUNT(ROWTIME): never null
+          case OP_INC_VALID: {
+            const int64_t d = (int64_t)va - (int64_t)vs;
+            if (d) __hip_atomic_fetch_add(w, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
+          }
           case OP_ADD_I64: {  // INT / BIGINT: wrapping (INT truncated to 32 bits when read)
-            const uint64_t x = (uint64_t)r.w[op.col];
-            __hip_atomic_fetch_add((uint64_t*)w, sign > 0 ? x : (uint64_t)0 - x, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t d = (va ? (uint64_t)wpick(add, op.col) : 0) - (vs ? (uint64_t)wpick(sub, op.col) : 0);
+            if (d) __hip_atomic_fetch_add((uint64_t*)w, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
           }
           case OP_ADD_F64: {
-            double d;
-            __builtin_memcpy(&d, &r.w[op.col], 8);
-            unsafeAtomicAdd((double*)w, sign > 0 ? d : -d);
+            double x = 0, y = 0;
+            if (va) x = __longlong_as_double(wpick(add, op.col));
+            if (vs) y = __longlong_as_double(wpick(sub, op.col));
+            unsafeAtomicAdd((double*)w, va && vs ? x - y : (va ? x : -y));
             break;
           }
           default:  // MIN / MAX are rejected at create (not undoable)
@@ -167,6 +184,7 @@ __device__ __forceinline__ int64_t load_word(const ColPtrs& c, int32_t type, int
   return type == KHIP_TYPE_INT32 ? (int64_t)((const int32_t*)c.data[col])[i] : ((const int64_t*)c.data[col])[i];
 }
 
+template <int NC>
 __global__ __launch_bounds__(256) void k_tagg_apply(TaggArgs A, const uint64_t* __restrict__ skey,
                                                     const uint32_t* __restrict__ sidx, const int64_t* __restrict__ gkeys,
                                                     const int64_t* __restrict__ ghash, const uint8_t* __restrict__ kv,
@@ -221,53 +239,90 @@ __global__ __launch_bounds__(256) void k_tagg_apply(TaggArgs A, const uint64_t* 
       failed++;
       continue;
     }
-    TRow prev{};
+    TRow<NC> prev{};
     if (!fresh) {
       prev.flags = (uint32_t)s[2];
       prev.gid = (int64_t)s[3];
       prev.ghash = (int64_t)s[4];
-      for (int c = 0; c < A.n_cols; c++) prev.w[c] = (int64_t)s[TS_WORDS + c];
+      _Pragma("unroll") for (int c = 0; c < NC; c++) prev.w[c] = (int64_t)s[TS_WORDS + c];
     } else {
       fresh_slot = (int64_t)slot;
     }
+    // Replay the key's changes in arrival order.  Every change undoes the previous row from its
+    // group and applies the new one; over the push these telescope: the stored row A0 is undone
+    // once (at the first change's time), the last row applied once (at its time), and every
+    // intermediate row's +x / −x cancel — its group only takes the row time (and exists: a group
+    // a row passed through stays, with its count back where it was).  Integer state is exact;
+    // DOUBLE sums differ from the one-by-one order only by rounding.  `upd` counts the
+    // undo/apply operations of the one-by-one replay (the push's statistics).
+    const TRow<NC> a0 = prev;  // the stored row
+    const bool a0_live = (a0.flags & (TF_LIVE | TF_GVALID)) == (TF_LIVE | TF_GVALID);
+    bool first = true;
+    int64_t t_first = 0, t_app = 0, r_app = -1;  // time / row of the current row's apply
     for (int64_t q = j; q < end; q++) {
       const int64_t r = sidx[q];
       const int64_t t = ts[r];
       if (!bit_get(src_kv, r) || t < 0) continue;
       if ((prev.flags & (TF_LIVE | TF_GVALID)) == (TF_LIVE | TF_GVALID)) {  // undo the previous row
-        const int u = group_update(A.p, A.table, A.gmask, prev, -1, r, t, gkeys, A.glist, ctr);
-        if (u == 0) failed++;
+        if (!first) {  // an intermediate row: its group's row time is max(apply, undo)
+          const int u = group_net<NC>(A.p, A.table, A.gmask, prev.gid, prev.ghash, false, prev, false, prev,
+                                      t > t_app ? t : t_app, r_app, gkeys, A.glist, ctr);
+          if (u == 0) failed++;
+          newg += u == 2;
+        }
         upd++;
       }
+      if (first) t_first = t;
+      first = false;
+      r_app = -1;
       if (!bit_get(rv, r)) {  // tombstone: the key leaves the table
         prev.flags = 0;
         continue;
       }
-      TRow cur{};
+      TRow<NC> cur{};
       cur.flags = TF_LIVE;
       if (bit_get(kv, r)) {
         cur.flags |= TF_GVALID;
         cur.gid = gkeys[r];
         cur.ghash = ghash[r];
       }
-      for (int c = 0; c < A.n_cols; c++) {
+      _Pragma("unroll") for (int c = 0; c < NC; c++) {
         const bool v = bit_get(cols.valid[c], r);
         cur.w[c] = v ? load_word(cols, A.col_type[c], c, r) : 0;
         cur.flags |= (v ? 1u : 0u) << (8 + c);
       }
       if (cur.flags & TF_GVALID) {
-        const int u = group_update(A.p, A.table, A.gmask, cur, +1, r, t, gkeys, A.glist, ctr);
-        if (u == 0) failed++;
-        newg += u == 2;
         upd++;
+        t_app = t;
+        r_app = r;
       }
       prev = cur;
+    }
+    const bool last_live = r_app >= 0;  // the last row is live with a GROUP BY value (applied)
+    if (!first) {
+      if (a0_live && last_live && a0.gid == prev.gid) {  // one group: net (last − stored)
+        const int u = group_net<NC>(A.p, A.table, A.gmask, prev.gid, prev.ghash, true, prev, true, a0,
+                                    t_app > t_first ? t_app : t_first, r_app, gkeys, A.glist, ctr);
+        if (u == 0) failed++;
+        newg += u == 2;
+      } else {
+        if (a0_live) {
+          const int u = group_net<NC>(A.p, A.table, A.gmask, a0.gid, a0.ghash, false, a0, true, a0, t_first, -1, gkeys, A.glist, ctr);
+          if (u == 0) failed++;
+        }
+        if (last_live) {
+          const int u = group_net<NC>(A.p, A.table, A.gmask, prev.gid, prev.ghash, true, prev, false, prev, t_app, r_app, gkeys,
+                                      A.glist, ctr);
+          if (u == 0) failed++;
+          newg += u == 2;
+        }
+      }
     }
     // the key's last row (or its deletion)
     s[2] = prev.flags;
     s[3] = (uint64_t)prev.gid;
     s[4] = (uint64_t)prev.ghash;
-    for (int c = 0; c < A.n_cols; c++) s[TS_WORDS + c] = (uint64_t)prev.w[c];
+    _Pragma("unroll") for (int c = 0; c < NC; c++) s[TS_WORDS + c] = (uint64_t)prev.w[c];
     } while (0);
     const uint64_t mk = __ballot(fresh_slot >= 0);
     if (mk) {
@@ -435,8 +490,13 @@ khip_status tagg_push(khip_agg* a, int64_t n, const int64_t* gkeys, const int64_
   for (int c = 0; c < MAX_COLS; c++) A.col_type[c] = a->ap.col_type[c];
   A.n = n;
   A.glist = T.gclaimed.as<int64_t>();
-  hipLaunchKernelGGL(k_tagg_apply, dim3(tgrid(n, 16384)), dim3(256), 0, st, A, kout, vout, gkeys, ghash, kv, rv, ts,
-                     cols, src_kv, T.claimed.as<int64_t>(), ctr);
+  static void (*const kapply[MAX_COLS + 1])(TaggArgs, const uint64_t*, const uint32_t*, const int64_t*, const int64_t*,
+                                            const uint8_t*, const uint8_t*, const int64_t*, ColPtrs, const uint8_t*,
+                                            int64_t*, unsigned long long*) = {
+      k_tagg_apply<0>, k_tagg_apply<1>, k_tagg_apply<2>, k_tagg_apply<3>, k_tagg_apply<4>,
+      k_tagg_apply<5>, k_tagg_apply<6>, k_tagg_apply<7>, k_tagg_apply<8>};
+  hipLaunchKernelGGL(kapply[A.n_cols], dim3(tgrid(n, 16384)), dim3(256), 0, st, A, kout, vout, gkeys, ghash, kv, rv,
+                     ts, cols, src_kv, T.claimed.as<int64_t>(), ctr);
   hipLaunchKernelGGL(k_tagg_grp_finalize, dim3(tgrid(n, 1024)), dim3(256), 0, st, a->table.as<uint64_t>(), a->sw,
                      T.gclaimed.as<int64_t>(), (const unsigned long long*)&ctr[TC_GLIST], gkeys);
   hipLaunchKernelGGL(k_tagg_src_finalize, dim3(tgrid(n)), dim3(256), 0, st, T.src.as<uint64_t>(), T.src_sw,

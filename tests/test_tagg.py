@@ -5,7 +5,8 @@ changelogs (updates that move keys between groups, deletes, NULL GROUP BY values
 repeated keys inside one push, INT wrap-around, STRING and BIGINT keys on both sides).
 
 Comparison: integers exact; DOUBLE SUM/AVG within 1e-12 relative to the sum of |x| the group's
-updates touched (the device applies a push's adds/undos with atomics, in no fixed order)."""
+updates touched (the device applies a push's adds/undos with atomics, in no fixed order, and nets
+each source key's changes inside one push: an intermediate row's +x / -x are not applied)."""
 import numpy as np
 import pytest
 
