@@ -358,7 +358,7 @@ struct TaggState {
   int src_sw = 8;
   int key_type = -1;    // source PRIMARY KEY type (fixed by the first push)
   KeyDict dict;         // UTF8 PRIMARY KEYs → ids
-  DevBuf sid, skey, skey2, sidx, sidx2, tmp, ctr, claimed, gclaimed, st_koff, st_kbytes, st_kv, st_key, shash;
+  DevBuf sid, skey, skey2, sidx, sidx2, tmp, ctr, claimed, gclaimed, blk, st_koff, st_kbytes, st_kv, st_key, shash;
 };
 
 struct SessState {

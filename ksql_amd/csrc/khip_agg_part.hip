@@ -2728,11 +2728,11 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   const bool r12_ok = narrow && !pad && merge_allow && r12_mode != 0;
   const bool r12_merge = r12_ok && (r12_mode == 1 || !lvl2);  // what k_part_merge reads
   const int U = (int)knob("KHIP_SCATTER_U", narrow ? 8 : 16);
-  auto scat = narrow ? (U >= 16 ? k_part_scatter<16, true> : (U >= 8 ? k_part_scatter<8, true> : k_part_scatter<4, true>))
+  auto scat = narrow ? (U >= 16 ? k_part_scatter<16, true> : (U >= 8 ? k_part_scatter<8, true> : (U >= 6 ? k_part_scatter<6, true> : k_part_scatter<4, true>)))
                      : (U >= 16 ? k_part_scatter<16, false> : (U >= 8 ? k_part_scatter<8, false> : k_part_scatter<4, false>));
   // narrow records leave through the LDS stage (stage_step): bins = B buckets (two-level) or P
   const int nbins = lvl2 ? B : P;
-  const int Ut = U >= 16 ? 16 : (U >= 8 ? 8 : 4);  // the instantiated records per thread per step
+  const int Ut = U >= 16 ? 16 : (U >= 8 ? 8 : (narrow && U >= 6 ? 6 : 4));  // the instantiated records per thread per step
   const bool stage = narrow && !pad && nbins <= PT_THREADS && Ut <= 8 && knob("KHIP_STAGE", 1) != 0;
   const size_t scat_lds = stage ? stage_lds_bytes(nbins, Ut * PT_THREADS) : (lvl2 ? (size_t)B * 4 : hist_lds);
   if (scat_lds > 64 * 1024)

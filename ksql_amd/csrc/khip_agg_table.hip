@@ -17,8 +17,9 @@
 //   [3] group id  [4] group-key hash  [5..] argument words (raw 8 bytes)
 //
 // Per push (all on the handle's stream):
-//   k_tagg_keys    sort key = PRIMARY KEY id (UINT64_MAX for dropped rows), value = row; counts
-//   hipcub radix sort (stable: a key's rows keep their arrival order)
+//   k_tagg_range   the push's PRIMARY KEY range (per-block partials, one reducing workgroup)
+//   k_tagg_keys    sort key = PRIMARY KEY id − kmin (dropped rows sort last), value = row; counts
+//   hipcub radix sort over the range's bits only (stable: a key's rows keep their arrival order)
 //   k_tagg_apply   one thread per distinct PRIMARY KEY (segment leader): find-or-claim its source
 //                  slot (claim references the sorted position: no spin), then replay its rows in
 //                  order — undo the previous row (-1 / -x) from its group, apply the new row (+1 /
@@ -44,31 +45,103 @@ constexpr uint64_t TS_RESIDENT = 1ULL << 62;
 constexpr uint64_t TF_LIVE = 1, TF_GVALID = 2;
 constexpr int TS_MAX_PROBE = 4096;
 
-enum { TC_ACCEPTED, TC_NULL_KEY, TC_BAD_TS, TC_UPDATES, TC_NEW_GROUPS, TC_NEW_KEYS, TC_FAILED, TC_GLIST, TC_N };
+enum { TC_ACCEPTED, TC_NULL_KEY, TC_BAD_TS, TC_UPDATES, TC_NEW_GROUPS, TC_NEW_KEYS, TC_FAILED, TC_GLIST, TC_KMINN, TC_KMAX,
+       TC_KACC, TC_N };
 
 __device__ __forceinline__ uint64_t src_hash(int64_t id) { return mix64((uint64_t)id ^ 0x3C6EF372FE94F82BULL); }
 
+__device__ __forceinline__ uint64_t id_ord(int64_t k) { return (uint64_t)k ^ (1ULL << 63); }
+
+// The accepted rows' PRIMARY KEY range (order-preserving words: min as max of ~u), per block.
+__global__ __launch_bounds__(256) void k_tagg_range(const int64_t* __restrict__ src_id, const uint8_t* __restrict__ src_kv,
+                                                    const int64_t* __restrict__ ts, int64_t n,
+                                                    ulonglong2* __restrict__ blk) {
+  __shared__ uint64_t l[2][4];
+  uint64_t mn = 0, mx = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (bit_get(src_kv, i) && ts[i] >= 0) {
+      const uint64_t u = id_ord(src_id[i]);
+      mn = ~u > mn ? ~u : mn;
+      mx = u > mx ? u : mx;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
+    mn = a > mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    l[0][wave] = mn;
+    l[1][wave] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; w++) {
+      mn = l[0][w] > mn ? l[0][w] : mn;
+      mx = l[1][w] > mx ? l[1][w] : mx;
+    }
+    blk[blockIdx.x] = make_ulonglong2(mn, mx);
+  }
+}
+
+// Per-block ranges → ctr[TC_KMINN] / ctr[TC_KMAX] (one workgroup; 0 / 0 when nothing accepted).
+__global__ __launch_bounds__(256) void k_tagg_range_reduce(const ulonglong2* __restrict__ blk, int nb,
+                                                           unsigned long long* __restrict__ ctr) {
+  __shared__ uint64_t l[2][4];
+  uint64_t mn = 0, mx = 0;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    mn = blk[b].x > mn ? blk[b].x : mn;
+    mx = blk[b].y > mx ? blk[b].y : mx;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
+    mn = a > mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    l[0][wave] = mn;
+    l[1][wave] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; w++) {
+      mn = l[0][w] > mn ? l[0][w] : mn;
+      mx = l[1][w] > mx ? l[1][w] : mx;
+    }
+    ctr[TC_KMINN] = mn;
+    ctr[TC_KMAX] = mx;
+  }
+}
+
+// Sort key = PRIMARY KEY id − kmin (dropped rows: `drop`, which sorts last), value = row; counts.
 __global__ __launch_bounds__(256) void k_tagg_keys(const int64_t* __restrict__ src_id, const uint8_t* __restrict__ src_kv,
-                                                   const int64_t* __restrict__ ts, int64_t n,
+                                                   const int64_t* __restrict__ ts, int64_t n, int64_t kmin, uint64_t drop,
                                                    uint64_t* __restrict__ skey, uint32_t* __restrict__ sidx,
                                                    unsigned long long* __restrict__ ctr) {
   int64_t acc = 0, nk = 0, bt = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const bool kv = bit_get(src_kv, i);
     const bool ok = kv && ts[i] >= 0;
-    skey[i] = ok ? (uint64_t)src_id[i] : ~0ULL;
+    skey[i] = ok ? (uint64_t)src_id[i] - (uint64_t)kmin : drop;
     sidx[i] = (uint32_t)i;
     acc += ok;
     nk += !kv;
     bt += kv && ts[i] < 0;
   }
-  acc = wave_sum(acc);
-  nk = wave_sum(nk);
-  bt = wave_sum(bt);
-  if ((threadIdx.x & 63) == 0) {
-    if (acc) atomicAdd(&ctr[TC_ACCEPTED], (unsigned long long)acc);
-    if (nk) atomicAdd(&ctr[TC_NULL_KEY], (unsigned long long)nk);
-    if (bt) atomicAdd(&ctr[TC_BAD_TS], (unsigned long long)bt);
+  // one add per block and counter (same-address adds from every wave would serialize)
+  __shared__ int64_t lc[3][4];
+  const int64_t c3[3] = {wave_sum(acc), wave_sum(nk), wave_sum(bt)};
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane < 3) lc[lane][wave] = c3[lane];
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const int64_t v = lc[threadIdx.x][0] + lc[threadIdx.x][1] + lc[threadIdx.x][2] + lc[threadIdx.x][3];
+    const int slot[3] = {TC_ACCEPTED, TC_NULL_KEY, TC_BAD_TS};
+    if (v) atomicAdd(&ctr[slot[threadIdx.x]], (unsigned long long)v);
   }
 }
 
@@ -178,6 +251,7 @@ struct TaggArgs {
   int32_t col_type[MAX_COLS];
   int64_t n;
   int64_t* glist;   // group slots claimed by this push
+  int64_t kmin;     // sort keys are PRIMARY KEY id − kmin
 };
 
 __device__ __forceinline__ int64_t load_word(const ColPtrs& c, int32_t type, int col, int64_t i) {
@@ -211,7 +285,7 @@ __global__ __launch_bounds__(256) void k_tagg_apply(TaggArgs A, const uint64_t* 
       any = bit_get(src_kv, r) && ts[r] >= 0;
     }
     if (!any) continue;
-    const int64_t id = (int64_t)k;
+    const int64_t id = (int64_t)(k + (uint64_t)A.kmin);
     // find or claim the key's source slot (only this thread holds this key)
     uint64_t slot = src_hash(id) & A.smask;
     uint64_t* s = nullptr;
@@ -333,13 +407,15 @@ __global__ __launch_bounds__(256) void k_tagg_apply(TaggArgs A, const uint64_t* 
       if (fresh_slot >= 0) claimed[(int64_t)x0 + __popcll(mk & below)] = fresh_slot;
     }
   }
-  upd = wave_sum(upd);
-  newg = wave_sum(newg);
-  failed = wave_sum(failed);
-  if ((threadIdx.x & 63) == 0) {
-    if (upd) atomicAdd(&ctr[TC_UPDATES], (unsigned long long)upd);
-    if (newg) atomicAdd(&ctr[TC_NEW_GROUPS], (unsigned long long)newg);
-    if (failed) atomicAdd(&ctr[TC_FAILED], (unsigned long long)failed);
+  __shared__ int64_t lc[3][4];  // one add per block and counter
+  const int64_t c3[3] = {wave_sum(upd), wave_sum(newg), wave_sum(failed)};
+  const int wave = threadIdx.x >> 6;
+  if (lane < 3) lc[lane][wave] = c3[lane];
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const int64_t v = lc[threadIdx.x][0] + lc[threadIdx.x][1] + lc[threadIdx.x][2] + lc[threadIdx.x][3];
+    const int slot[3] = {TC_UPDATES, TC_NEW_GROUPS, TC_FAILED};
+    if (v) atomicAdd(&ctr[slot[threadIdx.x]], (unsigned long long)v);
   }
 }
 
@@ -364,13 +440,13 @@ __global__ __launch_bounds__(256) void k_tagg_grp_finalize(uint64_t* __restrict_
 __global__ __launch_bounds__(256) void k_tagg_src_finalize(uint64_t* __restrict__ src, int ssw,
                                                            const int64_t* __restrict__ claimed,
                                                            const unsigned long long* __restrict__ n_claimed,
-                                                           const uint64_t* __restrict__ skey) {
+                                                           const uint64_t* __restrict__ skey, int64_t kmin) {
   const int64_t nc = (int64_t)*n_claimed;
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < nc; k += (int64_t)gridDim.x * blockDim.x) {
     uint64_t* s = src + (uint64_t)claimed[k] * (uint64_t)ssw;
     const uint64_t m = s[1];
     if (m & TS_CLAIM) {
-      s[0] = skey[(int64_t)(m & ((1ULL << 40) - 1))];
+      s[0] = skey[(int64_t)(m & ((1ULL << 40) - 1))] + (uint64_t)kmin;
       s[1] = TS_RESIDENT;
     }
   }
@@ -468,8 +544,24 @@ khip_status tagg_push(khip_agg* a, int64_t n, const int64_t* gkeys, const int64_
   KHIP_TRY(T.ctr.ensure(TC_N * 8));
   unsigned long long* ctr = T.ctr.as<unsigned long long>();
   KHIP_TRY_HIP(hipMemsetAsync(ctr, 0, TC_N * 8, st));
-  hipLaunchKernelGGL(k_tagg_keys, dim3(tgrid(n)), dim3(256), 0, st, src_id, src_kv, ts, n, T.skey.as<uint64_t>(),
-                     T.sidx.as<uint32_t>(), ctr);
+  // the push's PRIMARY KEY range: the sort runs over (id − kmin) and only the bits that range needs
+  const int rb = tgrid(n);
+  KHIP_TRY(T.blk.ensure((size_t)rb * 16));
+  hipLaunchKernelGGL(k_tagg_range, dim3(rb), dim3(256), 0, st, src_id, src_kv, ts, n, T.blk.as<ulonglong2>());
+  hipLaunchKernelGGL(k_tagg_range_reduce, dim3(1), dim3(256), 0, st, T.blk.as<ulonglong2>(), rb, ctr);
+  unsigned long long kr[2] = {0, 0};
+  KHIP_TRY_HIP(hipMemcpyAsync(kr, ctr + TC_KMINN, sizeof(kr), hipMemcpyDeviceToHost, st));
+  KHIP_TRY_HIP(hipStreamSynchronize(st));
+  int64_t kmin = 0;
+  uint64_t range = 0;
+  if (kr[0] | kr[1]) {  // some row accepted (both words are 0 only when none was)
+    kmin = (int64_t)(~(uint64_t)kr[0] ^ (1ULL << 63));
+    range = (uint64_t)(int64_t)((uint64_t)kr[1] ^ (1ULL << 63)) - (uint64_t)kmin;
+  }
+  const uint64_t drop = range != ~0ULL ? range + 1 : range;  // full 64-bit range: dropped rows share
+  const int end_bit = drop ? 64 - __builtin_clzll(drop) : 1;  // the last key's segment (rows re-checked)
+  hipLaunchKernelGGL(k_tagg_keys, dim3(tgrid(n)), dim3(256), 0, st, src_id, src_kv, ts, n, kmin, drop,
+                     T.skey.as<uint64_t>(), T.sidx.as<uint32_t>(), ctr);
   KHIP_TRY_HIP(hipGetLastError());
   uint64_t* kin = T.skey.as<uint64_t>();
   uint64_t* kout = T.skey2.as<uint64_t>();
@@ -477,7 +569,7 @@ khip_status tagg_push(khip_agg* a, int64_t n, const int64_t* gkeys, const int64_
   uint32_t* vout = T.sidx2.as<uint32_t>();
   const int ni = (int)n;
   KHIP_TRY(tcub(T.tmp, [&](void* p, size_t& b) {
-    return hipcub::DeviceRadixSort::SortPairs(p, b, kin, kout, vin, vout, ni, 0, 64, st);
+    return hipcub::DeviceRadixSort::SortPairs(p, b, kin, kout, vin, vout, ni, 0, end_bit, st);
   }));
   TaggArgs A{};
   A.p = a->ap;
@@ -490,6 +582,7 @@ khip_status tagg_push(khip_agg* a, int64_t n, const int64_t* gkeys, const int64_
   for (int c = 0; c < MAX_COLS; c++) A.col_type[c] = a->ap.col_type[c];
   A.n = n;
   A.glist = T.gclaimed.as<int64_t>();
+  A.kmin = kmin;
   static void (*const kapply[MAX_COLS + 1])(TaggArgs, const uint64_t*, const uint32_t*, const int64_t*, const int64_t*,
                                             const uint8_t*, const uint8_t*, const int64_t*, ColPtrs, const uint8_t*,
                                             int64_t*, unsigned long long*) = {
@@ -500,7 +593,7 @@ khip_status tagg_push(khip_agg* a, int64_t n, const int64_t* gkeys, const int64_
   hipLaunchKernelGGL(k_tagg_grp_finalize, dim3(tgrid(n, 1024)), dim3(256), 0, st, a->table.as<uint64_t>(), a->sw,
                      T.gclaimed.as<int64_t>(), (const unsigned long long*)&ctr[TC_GLIST], gkeys);
   hipLaunchKernelGGL(k_tagg_src_finalize, dim3(tgrid(n)), dim3(256), 0, st, T.src.as<uint64_t>(), T.src_sw,
-                     T.claimed.as<int64_t>(), (const unsigned long long*)&ctr[TC_NEW_KEYS], kout);
+                     T.claimed.as<int64_t>(), (const unsigned long long*)&ctr[TC_NEW_KEYS], kout, kmin);
   KHIP_TRY_HIP(hipGetLastError());
   unsigned long long c[TC_N];
   KHIP_TRY_HIP(hipMemcpyAsync(c, ctr, sizeof(c), hipMemcpyDeviceToHost, st));

@@ -138,3 +138,30 @@ def test_tagg_reset_and_errors(prod, orc):
         bad = abi.make_agg_desc("NONE", "INT64", col_types=["INT64"], aggs=[("MIN", 0)], flags=abi.FLAG_TABLE_SOURCE)
         with pytest.raises(abi.KsqlHipError):
             abi.AggHandle(lib, bad)
+
+
+@pytest.mark.gpu
+def test_tagg_key_range_edges(prod, orc):
+    """The PRIMARY KEY sort runs over id − kmin on the bits of the push's key range: keys at both
+    ends of BIGINT (the full 64-bit range: no sentinel for dropped rows), a push with every row
+    dropped, negative keys, one key updated across pushes."""
+    lo, hi = np.iinfo(np.int64).min, np.iinfo(np.int64).max
+
+    def batch(pk, grp, ts, pkv=None, rv=None):
+        m = len(pk)
+        b = abi.HostBatch(np.asarray(ts, np.int64), keys=np.asarray(grp, np.int64),
+                          row_valid=rv if rv is not None else [True] * m,
+                          cols=[np.arange(m, dtype=np.int32), np.arange(m, dtype=np.int64) * 7, np.linspace(0, 1, m)])
+        return b, {"src_keys": np.asarray(pk, np.int64), "src_key_valid": pkv}, np.ones(m)
+
+    batches = [
+        batch([lo, hi, 0, lo, -5, hi], [1, 2, 3, 2, 1, 1], [1, 2, 3, 4, 5, 6]),
+        batch([1, 2, 3], [1, 1, 1], [7, 8, 9], pkv=[False, False, False]),
+        batch([-5, -6, -5, -7], [4, 4, 5, 4], [10, -1, 12, 13], rv=[True, True, False, True]),
+        batch([hi, hi, lo], [3, 1, 1], [14, 15, 16], pkv=[True, False, True]),
+    ]
+    (g, gs), (o, os_) = (_run(lib, batches, False) for lib in (prod, orc))
+    for a, b in zip(gs, os_):
+        for f in ("rows_in", "rows_accepted", "dropped_null_key", "dropped_bad_ts", "windows_applied"):
+            assert a[f] == b[f], f
+    _assert_same(g, o, 100.0)
