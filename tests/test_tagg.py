@@ -165,3 +165,51 @@ def test_tagg_key_range_edges(prod, orc):
         for f in ("rows_in", "rows_accepted", "dropped_null_key", "dropped_bad_ts", "windows_applied"):
             assert a[f] == b[f], f
     _assert_same(g, o, 100.0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ncols", [0, 1, 2])
+@pytest.mark.parametrize("utf8_src", [False, True])
+def test_tagg_narrow_rows_vs_oracle(prod, orc, ncols, utf8_src):
+    """Narrow handles (0-2 argument columns, INT and DOUBLE; each column count is its own replay
+    kernel instantiation) against the oracle, BIGINT and STRING PRIMARY KEYs."""
+    rng = np.random.default_rng(500 + 10 * ncols + utf8_src)
+    types = ["INT32", "DOUBLE"][:ncols]
+    aggs = [("COUNT_STAR", -1)] + [a for c in range(ncols) for a in (("SUM", c), ("COUNT", c), ("AVG", c))]
+    batches, scale = [], 0.0
+    for _ in range(4):
+        n = int(rng.integers(20000, 50000))
+        pk = rng.integers(0, 6000, n)
+        grp = rng.integers(0, 200, n)
+        ts = rng.integers(0, 10**6, n)
+        ts[rng.random(n) < 0.01] = -1
+        cols = [rng.integers(-2**31, 2**31, n).astype(np.int32), rng.uniform(-100, 100, n)][:ncols]
+        cv = [rng.random(n) > 0.07 for _ in range(ncols)]
+        b = abi.HostBatch(ts, keys=grp, key_valid=rng.random(n) > 0.05, row_valid=rng.random(n) > 0.12, cols=cols,
+                          col_valid=cv)
+        pkv = rng.random(n) > 0.01
+        sa = {"src_utf8_keys": ["pk-%d" % k if v else None for k, v in zip(pk, pkv)]} if utf8_src else \
+            {"src_keys": pk, "src_key_valid": pkv}
+        batches.append((b, sa))
+        if ncols == 2:
+            scale += float(np.abs(cols[1]).sum()) * 4
+    res = []
+    for lib in (prod, orc):
+        h = abi.AggHandle(lib, abi.make_agg_desc("NONE", "INT64", col_types=types, aggs=aggs, flags=abi.FLAG_TABLE_SOURCE))
+        st = [h.push_table(b, **sa) for b, sa in batches]
+        res.append((h.snapshot(), st))
+        h.close()
+    (g, gs), (o, os_) = res
+    for a, b in zip(gs, os_):
+        for f in ("rows_in", "rows_accepted", "dropped_null_key", "dropped_bad_ts", "windows_applied"):
+            assert a[f] == b[f], f
+    assert g["n"] == o["n"] and list(g["key"]) == list(o["key"])
+    assert np.array_equal(g["rowtime"], o["rowtime"])
+    for a, (kind, col) in enumerate(aggs):
+        assert np.array_equal(g["nulls"][a], o["nulls"][a]), a
+        if col >= 0 and types[col] == "DOUBLE" and kind in ("SUM", "AVG"):
+            np.testing.assert_allclose(g["values"][a], o["values"][a], rtol=0, atol=1e-12 * scale)
+        elif kind == "AVG":
+            np.testing.assert_allclose(g["values"][a], o["values"][a], rtol=1e-15)
+        else:
+            assert np.array_equal(g["values"][a], o["values"][a]), (kind, col)
