@@ -471,7 +471,10 @@ __device__ __forceinline__ int64_t sess_replay(const SessParams& q, int64_t key,
 
 // Scratch budget of one wave's keys in LDS (records 16 B, rows sw words + 1 flag byte each);
 // waves whose keys need more replay in HBM scratch.
-constexpr int SESS_LDS = 40960;
+#ifndef KHIP_SESS_LDS
+#define KHIP_SESS_LDS 40960
+#endif
+constexpr int SESS_LDS = KHIP_SESS_LDS;
 
 // One wave per 64 batch keys, one lane per key.  The wave's records (one contiguous range of the
 // sorted records) and its keys' scratch rows are staged in LDS when they fit, so the per-key
