@@ -596,8 +596,8 @@ def bench_hourly_metrics(args, lib, rank, world, local):
     ms_step = elapsed * 1000.0 / args.steps
     bpr = float(kb.size) / n + 8 + 8 + 2 * 32  # key bytes + offset + ts + 2 x S_slot(32)
     phase = push_phases(kt, kt["apply_launches"])
-    roof = roofline(bpr * n, ms_step, sum(phase.values()), None, None, bpr,
-                    kernel="khip_agg_push (UTF8 dictionary + partitioned aggregate) + row count",
+    roof = roofline(bpr * n, ms_step, sum(phase.values()), None, load_traffic(args.traffic_json, "hourly_metrics", n),
+                    bpr, kernel="khip_agg_push (UTF8 dictionary + partitioned aggregate) + row count",
                     extra={"note": "1M records: launch/latency-bound, not HBM-bound"})
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
