@@ -684,17 +684,24 @@ def bench_hopping_double(args, lib, rank, world, local):
         return
     ms_step = elapsed * 1000.0 / args.steps
     phase = {k: kt[k] / args.steps for k in ("stream_time_ms", "partition_ms", "apply_ms", "finalize_ms")}
-    # what the kernels actually stream per record (LDS fan-out: one record in, F window
-    # updates in LDS): hist 16 + scatter 24 read / 32 write + agg 32 + resident rows in and out
-    moved = 16 + 24 + 32 + 32 + 2 * 64.0 * groups / n
+    # what the kernels actually move per record (the engine fans the F windows out in LDS): the
+    # committed PMC counter bytes of this configuration when present; otherwise the model of the
+    # passes (32-byte records: hist 16 read, scatter 24 read + 32 write, refine 32 + 32, merge 32
+    # read, resident rows read and written once per push)
+    traffic = load_traffic(args.traffic_json, "hopping_double", n)
+    moved_model = 16 + 24 + 32 + 32 + 32 + 32 + 2 * 64.0 * groups / n * len(batches)
+    moved = traffic / n if traffic else moved_model
     roof = roofline(BYTES_PER_RECORD_C3 * n, ms_step, sum(phase.values()), None,
-                    load_traffic(args.traffic_json, "hopping_double", n), BYTES_PER_RECORD_C3,
+                    traffic, BYTES_PER_RECORD_C3,
                     kernel="khip_agg_push (all kernels of every micro-batch push) + row count",
                     extra={"algorithmic_equivalent": True,
                            "note": "SURVEY §8(d)'s 696 B/record assumes one HBM slot RMW per (record, window); "
                                    "the engine fans the 6 windows out in LDS, so frac here is an "
-                                   "algorithmic-equivalent rate, not HBM bandwidth: see streamed_* and traffic",
+                                   "algorithmic-equivalent rate, not HBM bandwidth: streamed_frac (counter "
+                                   "bytes / time) is the bandwidth figure",
                            "streamed_bytes_per_record": moved,
+                           "streamed_basis": "PMC counter bytes (profiles/traffic.json)" if traffic else
+                                             "model of the passes (no counter record for this size)",
                            "streamed_frac": moved * n / (ms_step / 1000.0) / 1e9 / HBM_PEAK_GBS,
                            "phase_ms_per_step": phase, "stream_copy_GBps": stream_copy_gbs()})
     cpu = None

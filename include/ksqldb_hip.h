@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KHIP_ABI_VERSION 2
+#define KHIP_ABI_VERSION 3
 
 typedef int32_t khip_status;
 #define KHIP_OK 0
@@ -511,25 +511,50 @@ khip_status khip_comm_destroy(khip_comm* c);
  *              the same name, else the field whose upper-cased name matches (:273-300); JSON null
  *              or a missing field = NULL; numbers coerced as JsonSerdeUtils.toInteger / toLong /
  *              toDouble (Jackson intValue / asLong / doubleValue, or the Java parsers on strings)
+ *   AVRO       avro/KsqlAvroSerdeFactory.java:130-144 (Confluent's KafkaAvroDeserializer through
+ *              connect/KsqlConnectDeserializer) — Confluent wire format: magic byte 0, 4-byte
+ *              big-endian schema id, then the Avro binary encoding of the WRITER schema's record
+ *              (zig-zag varint int / long, little-endian float / double, long-length-prefixed
+ *              string / bytes, a varint branch index for a union [null, T] or [T, null]).  Writer
+ *              fields land in the column of the same name, else of the upper-cased name
+ *              (connect/ConnectDataTranslator.java:290-318); a writer type the column's type does
+ *              not accept (validateSchema :123-146: BIGINT ← int / long, INT ← int, DOUBLE ← float /
+ *              double, STRING ← any primitive) fails every record; missing columns are NULL.
  * A record that fails to deserialize is dropped by the reference (processing log): here it gets a
  * null key and a null value (every consumer drops it; a table upsert skips it) and is counted. */
 #define KHIP_FMT_NONE 0
 #define KHIP_FMT_KAFKA 1
 #define KHIP_FMT_DELIMITED 2
 #define KHIP_FMT_JSON 3
+#define KHIP_FMT_AVRO 4
+/* Avro writer-schema field types (primitive; unions of null and one of them via avro_field_union) */
+#define KHIP_AVRO_BOOLEAN 1
+#define KHIP_AVRO_INT 2
+#define KHIP_AVRO_LONG 3
+#define KHIP_AVRO_FLOAT 4
+#define KHIP_AVRO_DOUBLE 5
+#define KHIP_AVRO_STRING 6
+#define KHIP_AVRO_BYTES 7
 #define KHIP_TYPE_STRING 3  /* VARCHAR: keys → UTF-8 key columns; value fields are only checked for
                                NULL (an INT64 column of zeros + validity: what COUNT(col) reads)  */
 
 typedef struct khip_serde_desc {
   int32_t key_format;              /* KHIP_FMT_NONE or KHIP_FMT_KAFKA                          */
   int32_t key_type;                /* KHIP_TYPE_INT32 / INT64 (→ int64 keys) / STRING (→ UTF-8) */
-  int32_t value_format;            /* KHIP_FMT_KAFKA / DELIMITED / JSON                        */
+  int32_t value_format;            /* KHIP_FMT_KAFKA / DELIMITED / JSON / AVRO                 */
   int32_t n_fields;                /* value schema columns, in order                            */
   const int32_t* field_types;      /* KHIP_TYPE_INT32 / INT64 / DOUBLE / STRING                 */
-  const char* const* field_names;  /* JSON: column names as ksqlDB stores them                  */
+  const char* const* field_names;  /* JSON / AVRO: column names as ksqlDB stores them           */
   const int32_t* field_out;        /* output column of each field, or -1 (not read)            */
   int32_t delimiter;               /* DELIMITED: the VALUE_DELIMITER byte (',')                 */
   int32_t device;
+  /* AVRO: the writer schema (a record of avro_n_fields fields, in writer order) registered under
+   * avro_schema_id (-1: accept any id; a different id is a deserialization error) */
+  int32_t avro_schema_id;
+  int32_t avro_n_fields;
+  const char* const* avro_field_names;
+  const int32_t* avro_field_types;  /* KHIP_AVRO_*                                               */
+  const int32_t* avro_field_union;  /* 0: plain; 1: ["null", T]; 2: [T, "null"]                  */
 } khip_serde_desc;
 
 /* One batch of Kafka records as the consumer returns them (arrival order). */

@@ -19,7 +19,7 @@ PRODUCT_LIB = os.path.join(REPO, "ksql_amd", "libksqldb_hip_tune.so" if os.envir
                            else "libksqldb_hip.so")
 ORACLE_LIB = os.path.join(REPO, "oracle", "liboracle.so")
 
-ABI_VERSION = 2  # include/ksqldb_hip.h KHIP_ABI_VERSION the structs below mirror
+ABI_VERSION = 3  # include/ksqldb_hip.h KHIP_ABI_VERSION the structs below mirror
 KHIP_OK = 0
 KHIP_E_BUFFER = -5
 
@@ -131,7 +131,9 @@ class ShuffleDesc(C.Structure):
 class SerdeDesc(C.Structure):
     _fields_ = [("key_format", i32), ("key_type", i32), ("value_format", i32), ("n_fields", i32),
                 ("field_types", C.POINTER(i32)), ("field_names", C.POINTER(C.c_char_p)),
-                ("field_out", C.POINTER(i32)), ("delimiter", i32), ("device", i32)]
+                ("field_out", C.POINTER(i32)), ("delimiter", i32), ("device", i32),
+                ("avro_schema_id", i32), ("avro_n_fields", i32), ("avro_field_names", C.POINTER(C.c_char_p)),
+                ("avro_field_types", C.POINTER(i32)), ("avro_field_union", C.POINTER(i32))]
 
 
 class RawBatch(C.Structure):
@@ -140,7 +142,8 @@ class RawBatch(C.Structure):
                 ("value_bytes", C.c_void_p), ("value_valid", C.c_void_p)]
 
 
-FMT = {"NONE": 0, "KAFKA": 1, "DELIMITED": 2, "JSON": 3}
+FMT = {"NONE": 0, "KAFKA": 1, "DELIMITED": 2, "JSON": 3, "AVRO": 4}
+AVRO_TYPE = {"boolean": 1, "int": 2, "long": 3, "float": 4, "double": 5, "string": 6, "bytes": 7}
 TYPE_STRING = 3
 COMM_ID_BYTES = 128
 
@@ -761,19 +764,27 @@ class Comm:
 
 
 class SerdeHandle:
-    """khip_serde_*: Kafka record bytes (KAFKA / DELIMITED / JSON) → a device batch."""
+    """khip_serde_*: Kafka record bytes (KAFKA / DELIMITED / JSON / AVRO) → a device batch."""
 
     def __init__(self, lib, value_format, fields, key_type="INT64", key_format="KAFKA", delimiter=",",
-                 device=0):
-        """fields: [(name, type, out_col or -1)], type in INT32 / INT64 / DOUBLE / STRING."""
+                 device=0, avro_schema=None, avro_schema_id=-1):
+        """fields: [(name, type, out_col or -1)], type in INT32 / INT64 / DOUBLE / STRING.
+        avro_schema (AVRO): the writer record's fields [(name, avro type, union)], avro type in
+        boolean / int / long / float / double / string / bytes, union 0 (plain), 1 (["null", T]) or
+        2 ([T, "null"]); registered under avro_schema_id (-1: any id)."""
         self.lib = lib
         tmap = dict(TYPE, STRING=TYPE_STRING)
         self._ft = (i32 * len(fields))(*[tmap[t] for _, t, _ in fields])
         self._fn = (C.c_char_p * len(fields))(*[n.encode() for n, _, _ in fields])
         self._fo = (i32 * len(fields))(*[o for _, _, o in fields])
         self.n_out = max([o for _, _, o in fields] + [-1]) + 1
+        aw = avro_schema or []
+        self._an = (C.c_char_p * max(len(aw), 1))(*[n.encode() for n, _, _ in aw])
+        self._at = (i32 * max(len(aw), 1))(*[AVRO_TYPE[t] for _, t, _ in aw])
+        self._au = (i32 * max(len(aw), 1))(*[u for _, _, u in aw])
         self.desc = SerdeDesc(FMT[key_format], tmap[key_type], FMT[value_format], len(fields), self._ft, self._fn,
-                              self._fo, ord(delimiter), device)
+                              self._fo, ord(delimiter), device, avro_schema_id, len(aw), self._an, self._at,
+                              self._au)
         self.h = C.c_void_p()
         lib.check(lib.serde_create(C.byref(self.desc), C.byref(self.h)), "serde_create")
 

@@ -2048,6 +2048,402 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
 #undef MG_T
 }
 
+// ------------------------------------------------------------------ k_part_merge_c1
+// The COUNT(*) merge over 12-byte records (C1, C2: TUMBLING or no window, one u32 count), written
+// for its instruction count.  k_part_merge<true, 512, true> issued ~200 VALU instructions per
+// record (64-bit identities and slots, a claimed-entry list with a ballot and an LDS atomic per
+// record, the generic sub-pass / op machinery): on C2 its VALU issue alone was ~60 % of its time
+// (SQ_INSTS_VALU 3.2e8 per push, profiles/r03/).  Here every per-record step is 32-bit:
+//   identity  lo = key hash bits 0..31, hi = (key hash bits 32..63 << log2P) | window index - wbase
+//             (the partition's top log2P hash bits are implied): one 64-bit LDS CAS
+//   slot      (hash lo + window * 0x9E3779B1) >> (32 - log2H), H a power of two, linear probing
+//   state     u32 rowtime delta (ts - tbase + 1; bit 31: matched by a resident row), u32 count
+// The write-out scans the table (each wave a contiguous 1/NW of it, ballots kept in scalar
+// registers between the count and the write) instead of keeping a list of claimed entries.
+// LDS = (H + 64) x 16 B: ids | rowtime | count, the 64 per-lane dummy entries absorb the inactive
+// lanes' CASes.  Phases, the persistent item loop, retries and HAVING / changelog bookkeeping are
+// k_part_merge's (the contract is the same; k_part_commit publishes the result).
+constexpr uint32_t C1_GOLD = 0x9E3779B1u;
+
+// k_part_merge_c1's parameters: only what it reads (a large by-value argument struct keeps its
+// fields live in scalar registers across the item loop; the spills cost VALU moves)
+struct C1Params {
+  int32_t log2P, log2H, sw, hv_active, hv_op;
+  int64_t size, adv, cmax, hv_i64;
+  FastDiv fd;
+  FastDiv32 fd32;
+  uint8_t* chg;  // changelog: per-row-slot emission flags (CHG_*), or null
+};
+
+// HAVING on the COUNT(*) word (the query's only aggregate)
+__device__ __forceinline__ bool c1_having(const C1Params& q, uint64_t c) {
+  const int64_t v = (int64_t)c;
+  switch (q.hv_op) {
+    case KHIP_OP_GT: return v > q.hv_i64;
+    case KHIP_OP_GE: return v >= q.hv_i64;
+    case KHIP_OP_LT: return v < q.hv_i64;
+    case KHIP_OP_LE: return v <= q.hv_i64;
+    case KHIP_OP_EQ: return v == q.hv_i64;
+    case KHIP_OP_NE: return v != q.hv_i64;
+  }
+  return true;
+}
+
+__device__ __forceinline__ int c1_find(const KLDS uint64_t* ids, uint64_t id, uint32_t e, int H) {
+  for (int probe = 0; probe < H; probe++) {
+    const uint64_t v = ids[e];
+    if (v == id) return (int)e;
+    if (v == EMPTY_ID) return -1;
+    e = (e + 1) & (uint32_t)(H - 1);
+  }
+  return -1;
+}
+
+template <int NT, int AU>
+__global__ __launch_bounds__(NT, 4) void k_part_merge_c1(
+    C1Params q, const uint32_t* __restrict__ work, int64_t nwork, const int64_t* __restrict__ pbase,
+    const uint64_t* __restrict__ srec, int first, uint64_t* __restrict__ buf0, uint64_t* __restrict__ buf1,
+    const uint8_t* __restrict__ sel, const int64_t* __restrict__ cnt, unsigned long long* __restrict__ newcnt,
+    uint8_t* __restrict__ fail, unsigned long long* __restrict__ need, int64_t close0, uint64_t* __restrict__ closed,
+    unsigned long long* __restrict__ closed_n, const int64_t* __restrict__ wr, unsigned long long* __restrict__ hnew,
+    unsigned long long* __restrict__ hclosed, unsigned long long* __restrict__ dbg) {
+  if (wr[4] == 0) return;  // k_part_wrange declined the merge path for this push
+  // dbg (KHIP_AGG_PROBE): wall-clock time per phase summed over the workgroups (thread 0's view)
+  unsigned long long t_last = dbg ? wall_clock64() : 0ULL;
+#define C1_T(k)                                                                        \
+  do {                                                                                 \
+    if (dbg && threadIdx.x == 0) {                                                     \
+      const unsigned long long now = wall_clock64();                                   \
+      atomicAdd(&dbg[(k)], now - t_last);                                              \
+      t_last = now;                                                                    \
+    }                                                                                  \
+  } while (0)
+  constexpr int NW = NT / 64;
+  const int log2H = q.log2H;
+  const int H = 1 << log2H;
+  const int EPW = H / NW;  // entries per wave in the write-out scan (a multiple of 64)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  KLDS uint64_t* ids = mg_plane<uint64_t>(smem, 0);
+  KLDS uint32_t* rt = mg_plane<uint32_t>(smem, (H + 64) * 8);
+  KLDS uint32_t* ct = mg_plane<uint32_t>(smem, (H + 64) * 12);
+  __shared__ int lovf;
+  __shared__ int wsum[NW];
+  __shared__ unsigned long long lbase;
+  const int64_t tbase = wr[5], wbase = wr[0];
+  const int64_t q0 = (int64_t)fast_udiv((uint64_t)tbase, q.fd);
+  const uint32_t r0 = (uint32_t)(tbase - q0 * q.adv);
+  const uint32_t qw0 = (uint32_t)(q0 - wbase);
+  const int log2P = q.log2P;
+  const uint32_t wmask = (1u << log2P) - 1u;
+  const bool evict = close0 != INT64_MIN;
+  const uint32_t dummy = (uint32_t)H + (uint32_t)lane;
+  for (int i = threadIdx.x; i < H + 64; i += NT) {
+    ids[i] = EMPTY_ID;
+    rt[i] = 0u;
+    ct[i] = 0u;
+  }
+  if (threadIdx.x == 0) lovf = 0;
+  // window index of a record relative to wbase (the packed identity's low log2P bits); the host
+  // launches this kernel only for windowed queries with adv <= 2^31 (q.div32)
+  const FastDiv32 fd32 = q.fd32;
+  auto wrel_of = [&](uint32_t trel) -> uint32_t { return qw0 + fast_udiv32(r0 + trel - 1u, fd32); };
+  // the identity and home slot of a resident row
+  auto row_id = [&](const uint64_t* row, uint64_t* id, uint32_t* e) {
+    const uint64_t hk = key_hash((int64_t)row[0]);
+    const uint32_t w = (uint32_t)((int64_t)fast_udiv((uint64_t)row[1], q.fd) - wbase);
+    const uint32_t lo = (uint32_t)hk;
+    *id = ((uint64_t)(((uint32_t)(hk >> 32) << log2P) | w) << 32) | lo;
+    *e = (lo + w * C1_GOLD) >> (32 - log2H);
+  };
+  // two register sets of records: chunk c + 1 in flight while chunk c is applied.  Every load is
+  // unconditional (indices clamped to the item's last record; an empty item reads record rbase,
+  // which exists: srec has a spare record), so the compiler counts the loads in flight exactly on
+  // every path and each wait covers only the set about to be applied.  A record stays
+  // the (lo, hi, trel) triple the load returns (a uint3: the load writes the registers the apply
+  // reads; splitting it into per-field arrays made the compiler copy — and so wait for — each load
+  // right after issuing it)
+  uint3 ra[AU], rb[AU];
+  auto load = [&](uint3 (&x)[AU], int64_t rbase, int64_t rn, int64_t l0) {
+    const uint32_t* base = (const uint32_t*)srec + (uint64_t)rbase * 3;
+#pragma unroll
+    for (int u = 0; u < AU; u++) {
+      const int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
+      const uint32_t* r = base + (uint64_t)(li < rn ? li : (rn > 0 ? rn - 1 : 0)) * 3;
+      // three dword loads, not one dwordx3: a 3-register tuple must start at an even register, and
+      // the re-aligning copy would wait for the load right after issuing it
+      x[u].x = __builtin_nontemporal_load(r);
+      x[u].y = __builtin_nontemporal_load(r + 1);
+      x[u].z = __builtin_nontemporal_load(r + 2);
+    }
+  };
+  int64_t w = blockIdx.x;
+  MgItem it{};
+  if (w < nwork) it = mg_item(work, w, pbase, sel, cnt);
+  load(ra, it.rbase, it.rn, 0);
+  lds_barrier();
+  for (; w < nwork; w += gridDim.x) {
+    const uint32_t p = it.p;
+    const int sbits = it.sbits, sub = it.sub;
+    const int64_t rbase = it.rbase, rn = it.rn;
+    const int64_t wnext = w + gridDim.x;
+    MgItem nit = it;  // past the last item: harmless reloads of this one
+    if (wnext < nwork) nit = mg_item(work, wnext, pbase, sel, cnt);
+    if (rn == 0 && first) {  // untouched partition: nothing to rewrite
+      load(ra, nit.rbase, nit.rn, 0);
+      it = nit;
+      continue;
+    }
+    const uint64_t* src = (it.sel ? buf1 : buf0) + (uint64_t)p * q.cmax * q.sw;
+    const int64_t nrow = it.nrow;
+    // 0. closed resident rows → closed store (pass 0 only; retries skip them)
+    if (evict && first) {
+      int ne = 0, nh = 0;
+      for (int64_t r = threadIdx.x; r < nrow; r += NT) {
+        const uint64_t* row = src + r * q.sw;
+        ne += ((int64_t)row[1] + q.size <= close0) && sub_ok(key_hash((int64_t)row[0]), (int64_t)row[1], sbits, sub);
+      }
+      int incl = ne;
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+      }
+      if (lane == 63) wsum[wave] = incl;
+      lds_barrier();
+      int before = 0, total = 0;
+      for (int k = 0; k < NW; k++) {
+        if (k < wave) before += wsum[k];
+        total += wsum[k];
+      }
+      if (threadIdx.x == 0) lbase = total ? atomicAdd(closed_n, (unsigned long long)total) : 0ULL;
+      lds_barrier();
+      uint64_t* dst = closed + (lbase + (uint64_t)(before + incl - ne)) * q.sw;
+      for (int64_t r = threadIdx.x; r < nrow; r += NT) {
+        const uint64_t* row = src + r * q.sw;
+        if (!((int64_t)row[1] + q.size <= close0) || !sub_ok(key_hash((int64_t)row[0]), (int64_t)row[1], sbits, sub))
+          continue;
+        for (int k = 0; k < q.sw; k++) dst[k] = row[k];
+        dst += q.sw;
+        nh += q.hv_active && c1_having(q, row[3]) ? 1 : 0;
+      }
+      if (q.hv_active) {
+        nh = (int)wave_sum(nh);
+        if (lane == 0 && nh) atomicAdd(hclosed, (unsigned long long)nh);
+      }
+      lds_barrier();
+    }
+    C1_T(0);
+    // 1. records → delta entries
+    auto apply = [&](const uint3 (&x)[AU], int64_t l0) {
+      uint64_t id[AU], old[AU];
+      uint32_t e[AU];
+      bool pend[AU];
+#pragma unroll
+      for (int u = 0; u < AU; u++) {
+        const int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
+        const uint32_t trel = x[u].z;
+        const uint32_t wi = wrel_of(trel);
+        bool act = li < rn && trel != 0u;
+        if (sbits) act = act && sub_ok(((uint64_t)x[u].y << 32) | x[u].x, ((int64_t)wi + wbase) * q.adv, sbits, sub);
+        id[u] = act ? ((uint64_t)((x[u].y << log2P) | wi) << 32) | x[u].x : EMPTY_ID;
+        e[u] = act ? (x[u].x + wi * C1_GOLD) >> (32 - log2H) : dummy;
+      }
+#pragma unroll
+      for (int u = 0; u < AU; u++) {
+        old[u] = EMPTY_ID;
+        __hip_atomic_compare_exchange_strong(&ids[e[u]], &old[u], id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+#pragma unroll
+      for (int u = 0; u < AU; u++) pend[u] = old[u] != EMPTY_ID && old[u] != id[u];
+      for (int probes = 1;; probes++) {  // collisions: every pending record probes on together
+        bool anyp = false;
+#pragma unroll
+        for (int u = 0; u < AU; u++) anyp |= pend[u];
+        if (!__ballot(anyp)) break;
+        if (probes >= H) {
+          lovf = 1;
+#pragma unroll
+          for (int u = 0; u < AU; u++)
+            if (pend[u]) id[u] = EMPTY_ID;
+          break;
+        }
+#pragma unroll
+        for (int u = 0; u < AU; u++) {
+          if (!pend[u]) continue;
+          e[u] = (e[u] + 1) & (uint32_t)(H - 1);
+          uint64_t o2 = EMPTY_ID;
+          __hip_atomic_compare_exchange_strong(&ids[e[u]], &o2, id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+          pend[u] = o2 != EMPTY_ID && o2 != id[u];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < AU; u++) {
+        if (id[u] == EMPTY_ID) continue;
+        __hip_atomic_fetch_max(&rt[e[u]], x[u].z, WG_RLX);
+        __hip_atomic_fetch_add(&ct[e[u]], 1u, WG_RLX);
+      }
+    };
+    const int64_t nch = (rn + (int64_t)AU * NT - 1) / ((int64_t)AU * NT);
+    for (int64_t c = 0; c < nch; c += 2) {
+      load(rb, rbase, rn, (c + 1) * AU * NT);
+      apply(ra, c * AU * NT);
+      if (c + 1 >= nch || *(volatile KLDS int*)&lovf) break;
+      load(ra, rbase, rn, (c + 2) * AU * NT);
+      apply(rb, (c + 1) * AU * NT);
+      if (*(volatile KLDS int*)&lovf) break;
+    }
+    lds_barrier();
+    C1_T(1);
+    // the next item's first chunk is in flight from here on
+    load(ra, nit.rbase, nit.rn, 0);
+    if (lovf) {  // more groups than the table: retried with 2x sub-passes
+      if (threadIdx.x == 0) fail[p] |= 1;
+      for (int i = threadIdx.x; i < H; i += NT) {
+        ids[i] = EMPTY_ID;
+        rt[i] = 0u;
+        ct[i] = 0u;
+      }
+      lds_barrier();
+      if (threadIdx.x == 0) lovf = 0;
+      lds_barrier();
+      it = nit;
+      continue;
+    }
+    // 2. resident rows: mark the delta entries they absorb; count live rows
+    int n_mine = 0;
+    for (int64_t r = threadIdx.x; r < nrow; r += NT) {
+      const uint64_t* row = src + r * q.sw;
+      if (evict && (int64_t)row[1] + q.size <= close0) continue;
+      if (sbits && !sub_ok(key_hash((int64_t)row[0]), (int64_t)row[1], sbits, sub)) continue;
+      uint64_t id;
+      uint32_t e0;
+      row_id(row, &id, &e0);
+      const int e = c1_find(ids, id, e0, H);
+      if (e >= 0) rt[e] |= RT_MATCHED;  // one resident row per identity: a plain store
+      n_mine++;
+    }
+    lds_barrier();
+    // the wave's share of the table: new (unmatched) entries, one ballot per 64 entries
+    const int ebase = wave * EPW;
+    int nnew = 0;
+    for (int k = 0; k < EPW; k += 64) {
+      const int e = ebase + k + lane;
+      const bool isnew = ids[e] != EMPTY_ID && !(rt[e] & RT_MATCHED);
+      nnew += (int)__popcll(__ballot(isnew));
+    }
+    // 3. per-wave row counts → the partition's region range (one atomic per work item)
+    const int wave_rows = (int)wave_sum(n_mine) + nnew;
+    if (lane == 0) wsum[wave] = wave_rows;
+    lds_barrier();
+    int wave_before = 0, total = 0;
+    for (int k = 0; k < NW; k++) {
+      if (k < wave) wave_before += wsum[k];
+      total += wsum[k];
+    }
+    if (threadIdx.x == 0) {
+      if (work) {  // sub-passes of one partition append to its region
+        lbase = total ? atomicAdd(&newcnt[p], (unsigned long long)total) : 0ULL;
+      } else {  // the partition's only work item: no atomic round trip
+        lbase = 0;
+        newcnt[p] = (unsigned long long)total;
+      }
+    }
+    lds_barrier();
+    if ((int64_t)(lbase + total) > q.cmax) {
+      if (threadIdx.x == 0) {
+        fail[p] |= 2;
+        atomicMax(need, (unsigned long long)(lbase + total));
+      }
+      for (int i = threadIdx.x; i < H; i += NT) {
+        ids[i] = EMPTY_ID;
+        rt[i] = 0u;
+        ct[i] = 0u;
+      }
+      lds_barrier();
+      it = nit;
+      continue;
+    }
+    C1_T(2);
+    // 4. write: resident rows (merged), then the wave's new entries; lanes take ranks from ballots
+    //    so each store instruction covers consecutive rows
+    uint64_t* dst0 = (it.sel ? buf0 : buf1) + (uint64_t)p * q.cmax * q.sw;
+    uint64_t cur = lbase + (uint64_t)wave_before;
+    const uint64_t lt = (1ULL << lane) - 1;
+    int nh = 0;
+    for (int64_t r0 = wave * 64; r0 < nrow; r0 += NT) {
+      const int64_t r = r0 + lane;
+      const uint64_t* row = src + (r < nrow ? r : 0) * q.sw;
+      bool live = r < nrow && !(evict && (int64_t)row[1] + q.size <= close0);
+      if (live && sbits) live = sub_ok(key_hash((int64_t)row[0]), (int64_t)row[1], sbits, sub);
+      int e = -1;
+      if (live) {
+        uint64_t id;
+        uint32_t e0;
+        row_id(row, &id, &e0);
+        e = c1_find(ids, id, e0, H);
+      }
+      const uint64_t b = __ballot(live);
+      if (live) {
+        const uint64_t ri = cur + __popcll(b & lt);
+        uint64_t* dst = dst0 + ri * q.sw;
+        uint64_t w2 = row[2], c = row[3];
+        if (e >= 0) {
+          const int64_t t = tbase + (int64_t)(rt[e] & ~RT_MATCHED) - 1;
+          w2 = t > (int64_t)w2 ? (uint64_t)t : w2;
+          c += ct[e];
+        }
+        *(longlong2*)dst = make_longlong2((int64_t)row[0], (int64_t)row[1]);
+        *(longlong2*)(dst + 2) = make_longlong2((int64_t)w2, (int64_t)c);
+        const bool now = !q.hv_active || c1_having(q, c);
+        nh += q.hv_active && now ? 1 : 0;
+        if (q.chg)
+          q.chg[(uint64_t)p * q.cmax + ri] =
+              e >= 0 ? (uint8_t)(CHG_TOUCHED | (!q.hv_active || c1_having(q, row[3]) ? CHG_OLD : 0) | (now ? CHG_NEW : 0))
+                     : (uint8_t)0;
+      }
+      cur += __popcll(b);
+    }
+    lds_barrier();  // every wave's resident rows have read their entries: the scan below clears them
+    const uint64_t hkp = (uint64_t)p << (32 - log2P);
+    for (int k = 0; k < EPW; k += 64) {
+      const int e = ebase + k + lane;
+      const uint64_t id = ids[e];
+      const uint32_t rv = rt[e];
+      const bool isnew = id != EMPTY_ID && !(rv & RT_MATCHED);
+      const uint64_t b = __ballot(isnew);
+      if (isnew) {
+        const uint64_t ri = cur + __popcll(b & lt);
+        uint64_t* dst = dst0 + ri * q.sw;
+        const uint32_t ih = (uint32_t)(id >> 32);
+        const uint64_t hk = ((hkp | (ih >> log2P)) << 32) | (uint32_t)id;
+        const int64_t ws = ((int64_t)(ih & wmask) + wbase) * q.adv;
+        const uint32_t c = ct[e];
+        *(longlong2*)dst = make_longlong2(key_of_hash(hk), ws);
+        *(longlong2*)(dst + 2) = make_longlong2(tbase + (int64_t)rv - 1, (int64_t)c);
+        const bool now = !q.hv_active || c1_having(q, c);
+        nh += q.hv_active && now ? 1 : 0;
+        if (q.chg) q.chg[(uint64_t)p * q.cmax + ri] = (uint8_t)(CHG_TOUCHED | (now ? CHG_NEW : 0));
+      }
+      if (id != EMPTY_ID) {  // every entry of the wave's share leaves cleared for the next item
+        ids[e] = EMPTY_ID;
+        rt[e] = 0u;
+        ct[e] = 0u;
+      }
+      cur += __popcll(b);
+    }
+    if (q.hv_active) {
+      nh = (int)wave_sum(nh);
+      if (lane == 0 && nh) atomicAdd(&hnew[p], (unsigned long long)nh);
+    }
+    lds_barrier();  // the table is clear for the next item
+    C1_T(3);
+    it = nit;
+  }
+#undef C1_T
+}
+
 // Window-index range of this push for the packed identity: the batch's windows plus the
 // live resident ones (res = conservative [min, max] window index of resident rows; rows of
 // windows closed before this push are evicted before they are encoded).
@@ -2840,6 +3236,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   const bool probe = knob("KHIP_AGG_PROBE", 0) != 0;
   DevBuf dbgbuf;
   unsigned long long* dbg = nullptr;
+  bool c1_ran = false;
   for (int pass = 0;; pass++) {
     PartAggParams q = q0;
     dbg = nullptr;
@@ -2860,6 +3257,34 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
       const bool cnt1 = a->ap.n_ops == 1 && a->ap.ops[0].kind == OP_INC && a->ap.ops[0].word == 3 && a->sw == 4 &&
                         s.rw == 2 && a->desc.window_kind != KHIP_WINDOW_HOPPING;
       const int mt = (int)knob("KHIP_MERGE_THREADS", 512);
+      const int c1h = (int)knob("KHIP_C1_LOG2H", 12);
+      c1_ran = cnt1 && mq.r12 && mq.windowed && mq.div32 && mt >= 512 && knob("KHIP_MERGE_C1", 1) != 0;
+      if (c1_ran) {  // the lean COUNT(*) merge
+        const int au = (int)knob("KHIP_C1_AU", 6);
+        auto mk = au >= 8 ? k_part_merge_c1<512, 8> : (au >= 6 ? k_part_merge_c1<512, 6> : k_part_merge_c1<512, 4>);
+        const int lds = ((1 << c1h) + 64) * 16;
+        hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        const int64_t grid = std::min<int64_t>(nwork, (int64_t)s.n_cu * knob("KHIP_MERGE_WG_PER_CU", 2));
+        C1Params cq{};
+        cq.log2P = mq.log2P;
+        cq.log2H = c1h;
+        cq.sw = mq.sw;
+        cq.size = mq.size;
+        cq.adv = mq.adv;
+        cq.cmax = mq.cmax;
+        cq.fd = mq.fd;
+        cq.fd32 = mq.fd32;
+        cq.chg = mq.chg;
+        cq.hv_active = a->having.active;
+        cq.hv_op = a->having.op;
+        cq.hv_i64 = a->having.i64;
+        hipLaunchKernelGGL(mk, dim3(grid), dim3(512), lds, a->stream, cq, wk, nwork, s.pbase.as<int64_t>(),
+                           s.srec.as<uint64_t>(), pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
+                           s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
+                           s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
+                           s.closed_ctr.as<unsigned long long>(), s.wr.as<int64_t>(),
+                           s.hnew.as<unsigned long long>(), s.ctr.as<unsigned long long>() + 12, dbg);
+      } else {
       auto mk = mq.r12 ? (mt >= 512 ? (cnt1 ? k_part_merge<true, 512, true> : k_part_merge<false, 512, true>)
                                     : (cnt1 ? k_part_merge<true, 256, true> : k_part_merge<false, 256, true>))
                        : (mt >= 512 ? (cnt1 ? k_part_merge<true, 512, false> : k_part_merge<false, 512, false>)
@@ -2872,6 +3297,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                          s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
                          s.closed_ctr.as<unsigned long long>(), s.wr.as<int64_t>(),
                          s.hnew.as<unsigned long long>(), s.ctr.as<unsigned long long>() + 12, dbg);
+      }
     } else {
       hipFuncSetAttribute((const void*)k_part_agg, hipFuncAttributeMaxDynamicSharedMemorySize, s.lds_bytes);
       hipLaunchKernelGGL(k_part_agg, dim3(nwork), dim3(AG_THREADS), s.lds_bytes, a->stream, q, wk,
@@ -2908,9 +3334,13 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     if (dbg && merge) {  // k_part_merge: per-phase time summed over its persistent workgroups
       unsigned long long ph[8] = {};
       if (hipMemcpy(ph, dbgbuf.p, sizeof(ph), hipMemcpyDeviceToHost) == hipSuccess) {
-        const double g = (double)std::min<int64_t>(P, s.n_cu) * 100.0;  // 100 MHz ticks → us per workgroup
-        fprintf(stderr, "[merge probe] per workgroup (us): setup %.1f evict %.1f records %.1f mark+reserve %.1f write %.1f\n",
-                ph[0] / g, ph[1] / g, ph[2] / g, ph[3] / g, ph[4] / g);
+        const double g = (double)std::min<int64_t>(P, 2 * s.n_cu) * 100.0;  // 100 MHz ticks → us per workgroup
+        if (c1_ran)
+          fprintf(stderr, "[merge c1 probe] per workgroup (us): item start+evict %.1f records %.1f mark+count+reserve %.1f "
+                  "write %.1f\n", ph[0] / g, ph[1] / g, ph[2] / g, ph[3] / g);
+        else
+          fprintf(stderr, "[merge probe] per workgroup (us): setup %.1f evict %.1f records %.1f mark+reserve %.1f write %.1f\n",
+                  ph[0] / g, ph[1] / g, ph[2] / g, ph[3] / g, ph[4] / g);
       }
     } else if (dbg) {
       agg_probe_report(dbgbuf, (int)((pass == 0 && !subs0) ? P : (int64_t)work.size()));

@@ -46,74 +46,90 @@ constexpr uint64_t TF_LIVE = 1, TF_GVALID = 2;
 constexpr int TS_MAX_PROBE = 4096;
 
 enum { TC_ACCEPTED, TC_NULL_KEY, TC_BAD_TS, TC_UPDATES, TC_NEW_GROUPS, TC_NEW_KEYS, TC_FAILED, TC_GLIST, TC_KMINN, TC_KMAX,
-       TC_KACC, TC_N };
+       TC_KACC, TC_TSMAX, TC_N };
 
 __device__ __forceinline__ uint64_t src_hash(int64_t id) { return mix64((uint64_t)id ^ 0x3C6EF372FE94F82BULL); }
 
 __device__ __forceinline__ uint64_t id_ord(int64_t k) { return (uint64_t)k ^ (1ULL << 63); }
 
-// The accepted rows' PRIMARY KEY range (order-preserving words: min as max of ~u), per block.
+// The accepted rows' PRIMARY KEY range (order-preserving words: min as max of ~u) and the largest
+// timestamp of the accepted non-tombstone rows (the stream time the push reaches; stored +1, so 0
+// = none), per block.
 __global__ __launch_bounds__(256) void k_tagg_range(const int64_t* __restrict__ src_id, const uint8_t* __restrict__ src_kv,
-                                                    const int64_t* __restrict__ ts, int64_t n,
-                                                    ulonglong2* __restrict__ blk) {
-  __shared__ uint64_t l[2][4];
-  uint64_t mn = 0, mx = 0;
+                                                    const uint8_t* __restrict__ rv, const int64_t* __restrict__ ts,
+                                                    int64_t n, ulonglong2* __restrict__ blk,
+                                                    unsigned long long* __restrict__ blkts) {
+  __shared__ uint64_t l[3][4];
+  uint64_t mn = 0, mx = 0, tmx = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (bit_get(src_kv, i) && ts[i] >= 0) {
+    const int64_t t = ts[i];
+    if (bit_get(src_kv, i) && t >= 0) {
       const uint64_t u = id_ord(src_id[i]);
       mn = ~u > mn ? ~u : mn;
       mx = u > mx ? u : mx;
+      if (bit_get(rv, i)) tmx = (uint64_t)t + 1 > tmx ? (uint64_t)t + 1 : tmx;
     }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
-    const uint64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
+    const uint64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64), c = __shfl_xor(tmx, off, 64);
     mn = a > mn ? a : mn;
     mx = b > mx ? b : mx;
+    tmx = c > tmx ? c : tmx;
   }
   const int wave = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
     l[0][wave] = mn;
     l[1][wave] = mx;
+    l[2][wave] = tmx;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int w = 1; w < 4; w++) {
       mn = l[0][w] > mn ? l[0][w] : mn;
       mx = l[1][w] > mx ? l[1][w] : mx;
+      tmx = l[2][w] > tmx ? l[2][w] : tmx;
     }
     blk[blockIdx.x] = make_ulonglong2(mn, mx);
+    blkts[blockIdx.x] = tmx;
   }
 }
 
-// Per-block ranges → ctr[TC_KMINN] / ctr[TC_KMAX] (one workgroup; 0 / 0 when nothing accepted).
-__global__ __launch_bounds__(256) void k_tagg_range_reduce(const ulonglong2* __restrict__ blk, int nb,
+// Per-block ranges → ctr[TC_KMINN] / ctr[TC_KMAX] (one workgroup; 0 / 0 when nothing accepted) and
+// ctr[TC_TSMAX] (largest accepted row timestamp + 1, 0: none).
+__global__ __launch_bounds__(256) void k_tagg_range_reduce(const ulonglong2* __restrict__ blk,
+                                                           const unsigned long long* __restrict__ blkts, int nb,
                                                            unsigned long long* __restrict__ ctr) {
-  __shared__ uint64_t l[2][4];
-  uint64_t mn = 0, mx = 0;
+  __shared__ uint64_t l[3][4];
+  uint64_t mn = 0, mx = 0, tmx = 0;
   for (int b = threadIdx.x; b < nb; b += blockDim.x) {
     mn = blk[b].x > mn ? blk[b].x : mn;
     mx = blk[b].y > mx ? blk[b].y : mx;
+    tmx = blkts[b] > tmx ? blkts[b] : tmx;
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
-    const uint64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
+    const uint64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64), c = __shfl_xor(tmx, off, 64);
     mn = a > mn ? a : mn;
     mx = b > mx ? b : mx;
+    tmx = c > tmx ? c : tmx;
   }
   const int wave = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
     l[0][wave] = mn;
     l[1][wave] = mx;
+    l[2][wave] = tmx;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int w = 1; w < 4; w++) {
       mn = l[0][w] > mn ? l[0][w] : mn;
       mx = l[1][w] > mx ? l[1][w] : mx;
+      tmx = l[2][w] > tmx ? l[2][w] : tmx;
     }
     ctr[TC_KMINN] = mn;
     ctr[TC_KMAX] = mx;
+    ctr[TC_TSMAX] = tmx;
   }
 }
 
@@ -546,9 +562,10 @@ khip_status tagg_push(khip_agg* a, int64_t n, const int64_t* gkeys, const int64_
   KHIP_TRY_HIP(hipMemsetAsync(ctr, 0, TC_N * 8, st));
   // the push's PRIMARY KEY range: the sort runs over (id − kmin) and only the bits that range needs
   const int rb = tgrid(n);
-  KHIP_TRY(T.blk.ensure((size_t)rb * 16));
-  hipLaunchKernelGGL(k_tagg_range, dim3(rb), dim3(256), 0, st, src_id, src_kv, ts, n, T.blk.as<ulonglong2>());
-  hipLaunchKernelGGL(k_tagg_range_reduce, dim3(1), dim3(256), 0, st, T.blk.as<ulonglong2>(), rb, ctr);
+  KHIP_TRY(T.blk.ensure((size_t)rb * 24));
+  unsigned long long* blkts = (unsigned long long*)(T.blk.as<ulonglong2>() + rb);
+  hipLaunchKernelGGL(k_tagg_range, dim3(rb), dim3(256), 0, st, src_id, src_kv, rv, ts, n, T.blk.as<ulonglong2>(), blkts);
+  hipLaunchKernelGGL(k_tagg_range_reduce, dim3(1), dim3(256), 0, st, T.blk.as<ulonglong2>(), blkts, rb, ctr);
   unsigned long long kr[2] = {0, 0};
   KHIP_TRY_HIP(hipMemcpyAsync(kr, ctr + TC_KMINN, sizeof(kr), hipMemcpyDeviceToHost, st));
   KHIP_TRY_HIP(hipStreamSynchronize(st));
@@ -601,6 +618,11 @@ khip_status tagg_push(khip_agg* a, int64_t n, const int64_t* gkeys, const int64_
   if (c[TC_FAILED]) return fail(KHIP_E_DEVICE, "table aggregation: hash table probe budget exhausted");
   T.src_occ += (int64_t)c[TC_NEW_KEYS];
   a->occ += (int64_t)c[TC_NEW_GROUPS];
+  if (c[TC_TSMAX] && (int64_t)c[TC_TSMAX] - 1 > a->host_stream_time) {  // the oracle's stream time (oracle.c:862)
+    a->host_stream_time = (int64_t)c[TC_TSMAX] - 1;
+    KHIP_TRY_HIP(hipMemcpyAsync(a->stream_time.p, &a->host_stream_time, 8, hipMemcpyHostToDevice, st));
+    KHIP_TRY_HIP(hipStreamSynchronize(st));
+  }
   tot[P_ACCEPTED] += (int64_t)c[TC_ACCEPTED];
   tot[P_NULL_KEY] += (int64_t)c[TC_NULL_KEY];
   tot[P_BAD_TS] += (int64_t)c[TC_BAD_TS];

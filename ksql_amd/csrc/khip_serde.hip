@@ -1,7 +1,7 @@
 // khip_serde.hip — deserialization of Kafka record bytes into device columns (gfx950).
 //
 // Replaces, for the hot path's source topics, the per-record GenericKeySerDe / GenericRowSerDe
-// deserializers (KAFKA, DELIMITED, JSON; include/ksqldb_hip.h "deserialization") that box every
+// deserializers (KAFKA, DELIMITED, JSON, AVRO; include/ksqldb_hip.h "deserialization") that box every
 // record into a GenericKey / GenericRow before the aggregate or join sees it — the reference's
 // documented bottleneck (ksqldb-benchmark/README.md:7-9).
 //
@@ -32,6 +32,10 @@ struct SerdeParams {
   int32_t fout[SD_MAX_FIELDS];
   int32_t name_len[SD_MAX_FIELDS];
   uint8_t name[SD_MAX_FIELDS][SD_NAME_BYTES];
+  // AVRO: the writer schema's fields in order: type (KHIP_AVRO_*), union (0 plain, 1 [null, T],
+  // 2 [T, null]) and the ksql field (column schema index) it lands in, or -1
+  int32_t avro_id, avro_nw, avro_incompat;
+  int8_t aw_type[SD_MAX_FIELDS], aw_union[SD_MAX_FIELDS], aw_field[SD_MAX_FIELDS];
 };
 
 struct SerdeOut {
@@ -71,6 +75,32 @@ __device__ __forceinline__ int32_t java_d2i(double d) {
   if (d >= 2147483647.0) return INT32_MAX;
   if (d <= -2147483648.0) return INT32_MIN;
   return (int32_t)d;
+}
+
+// Avro binary varint (BinaryDecoder.readInt / readLong): at most maxb bytes (5 / 10), the last one
+// without a continuation bit ("Invalid int / long encoding" otherwise); bits past 64 are dropped
+// (readInt's past 32 by the caller's truncation); the zig-zag decoding is the caller's.
+__device__ __forceinline__ bool avro_varint(const uint8_t* p, int64_t n, int64_t* j, int maxb, uint64_t* out) {
+  uint64_t v = 0;
+  for (int k = 0; k < maxb; k++) {
+    if (*j >= n) return false;  // EOFException
+    const uint8_t b = p[(*j)++];
+    v |= (uint64_t)(b & 0x7F) << (7 * k);
+    if (!(b & 0x80)) {
+      *out = v;
+      return true;
+    }
+  }
+  return false;
+}
+
+__device__ __forceinline__ int64_t zz64(uint64_t v) { return (int64_t)(v >> 1) ^ -(int64_t)(v & 1); }
+__device__ __forceinline__ int32_t zz32(uint32_t v) { return (int32_t)(v >> 1) ^ -(int32_t)(v & 1); }
+
+__device__ __forceinline__ uint64_t le_load(const uint8_t* p, int n) {
+  uint64_t v = 0;
+  for (int i = n - 1; i >= 0; i--) v = v << 8 | p[i];
+  return v;
 }
 
 __device__ __forceinline__ bool json_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
@@ -195,6 +225,50 @@ __device__ bool json_unescape(const uint8_t* p, int64_t n, uint8_t* buf, int cap
 
 __device__ __forceinline__ uint8_t up(uint8_t c) { return c >= 'a' && c <= 'z' ? c - 32 : c; }
 
+// Jackson reads a JSON number token with a fraction or an exponent as a BigDecimal
+// (USE_BIG_DECIMAL_FOR_FLOATS, KsqlJsonDeserializer.java:68-70); JsonSerdeUtils.toInteger /
+// toLong (:95-121) then take intValue() / asLong(): the integer part truncated toward zero, its
+// low 32 / 64 bits.  Computed exactly from the digits: D x 10^s with s >= 64 is a multiple of 2^64;
+// s < 0 drops the last -s digits.  false: the token is not a number BigDecimal accepts (its
+// exponent must fit an int).
+__device__ bool json_bigdec_low64(const uint8_t* p, int64_t n, uint64_t* out) {
+  int64_t k = 0;
+  const bool neg = n > 0 && p[0] == '-';
+  if (neg) k++;
+  const int64_t i0 = k;
+  while (k < n && p[k] >= '0' && p[k] <= '9') k++;
+  const int64_t i1 = k;
+  int64_t f0 = k, f1 = k;
+  if (k < n && p[k] == '.') {
+    f0 = ++k;
+    while (k < n && p[k] >= '0' && p[k] <= '9') k++;
+    f1 = k;
+  }
+  if (i1 == i0 && f1 == f0) return false;
+  int64_t e = 0;
+  if (k < n && (p[k] == 'e' || p[k] == 'E')) {
+    k++;
+    bool en = false;
+    if (k < n && (p[k] == '+' || p[k] == '-')) en = p[k++] == '-';
+    if (k >= n) return false;
+    for (; k < n && p[k] >= '0' && p[k] <= '9'; k++) {
+      e = e * 10 + (p[k] - '0');
+      if (e > 0x7FFFFFFFLL) return false;  // BigDecimal: exponent overflow
+    }
+    if (en) e = -e;
+  }
+  if (k != n) return false;
+  const int64_t nint = i1 - i0, nfrac = f1 - f0;
+  const int64_t s = e - nfrac;  // value = D x 10^s, D = the int digits then the fraction digits
+  const int64_t keep = s >= 0 ? nint + nfrac : nint + nfrac + s;
+  uint64_t v = 0;
+  for (int64_t j = 0; j < keep; j++) v = v * 10 + (uint64_t)(p[j < nint ? i0 + j : f0 + (j - nint)] - '0');
+  if (s >= 64) v = 0;
+  for (int64_t j = 0; j < s && j < 64; j++) v *= 10;
+  *out = neg ? 0 - v : v;
+  return true;
+}
+
 // A numeric field (raw text p[0..n), json: a JSON number token, else Java text) → column.
 // Returns 0 ok, 1 error, 2 deferred (big-integer rounding).
 __device__ int put_number(const SerdeParams& q, int f, const uint8_t* p, int64_t n, bool json_num, void* col,
@@ -209,6 +283,14 @@ __device__ int put_number(const SerdeParams& q, int f, const uint8_t* p, int64_t
       int64_t k = p[0] == '-' ? 1 : 0;
       for (; k < n; k++) v = v * 10 + (p[k] - '0');
       if (p[0] == '-') v = 0 - v;
+      if (!col) return 0;
+      if (t == KHIP_TYPE_INT32) ((int32_t*)col)[row] = (int32_t)(uint32_t)v;
+      else ((int64_t*)col)[row] = (int64_t)v;
+      return 0;
+    }
+    if (t != KHIP_TYPE_DOUBLE) {  // BigDecimal → intValue() / longValue()
+      uint64_t v;
+      if (!json_bigdec_low64(p, n, &v)) return 1;
       if (!col) return 0;
       if (t == KHIP_TYPE_INT32) ((int32_t*)col)[row] = (int32_t)(uint32_t)v;
       else ((int64_t*)col)[row] = (int64_t)v;
@@ -387,6 +469,76 @@ __global__ __launch_bounds__(256) void k_serde_decode(SerdeParams q, int64_t n, 
           f++;
         }
         if (ok && f != q.n_fields) ok = false;
+      } else if (q.value_format == KHIP_FMT_AVRO) {
+        // Confluent wire format: magic 0, 4-byte big-endian schema id, the writer record's fields in
+        // order; each lands in its ksql column (by name, resolved at create) or is skipped
+        if (vn < 5 || p[0] != 0 || q.avro_incompat) ok = false;
+        else if (q.avro_id >= 0 && (int32_t)(uint32_t)be_load(p + 1, 4) != q.avro_id) ok = false;
+        int64_t j = 5;
+        for (int w = 0; ok && w < q.avro_nw; w++) {
+          bool isnull = false;
+          if (q.aw_union[w]) {  // readIndex() = readInt()
+            uint64_t br;
+            if (!avro_varint(p, vn, &j, 5, &br)) { ok = false; break; }
+            const int32_t idx = zz32((uint32_t)br);
+            if (idx != 0 && idx != 1) { ok = false; break; }  // no such union branch
+            isnull = idx == q.aw_union[w] - 1;
+          }
+          const int f = q.aw_field[w];
+          const int c = f >= 0 ? q.fout[f] : -1;
+          if (isnull) {
+            if (c >= 0) fnull |= 1u << c;  // a later field of the same column overwrites
+            continue;
+          }
+          uint64_t bits = 0;  // the value as the column stores it
+          switch (q.aw_type[w]) {
+            case KHIP_AVRO_BOOLEAN:
+              if (j >= vn) { ok = false; break; }
+              bits = p[j++] == 1;
+              break;
+            case KHIP_AVRO_INT: {
+              uint64_t v;
+              if (!avro_varint(p, vn, &j, 5, &v)) { ok = false; break; }
+              bits = (uint64_t)(int64_t)zz32((uint32_t)v);
+              break;
+            }
+            case KHIP_AVRO_LONG: {
+              uint64_t v;
+              if (!avro_varint(p, vn, &j, 10, &v)) { ok = false; break; }
+              bits = (uint64_t)zz64(v);
+              break;
+            }
+            case KHIP_AVRO_FLOAT: {
+              if (vn - j < 4) { ok = false; break; }
+              const uint32_t u = (uint32_t)le_load(p + j, 4);
+              j += 4;
+              float fv;
+              __builtin_memcpy(&fv, &u, 4);
+              const double dv = (double)fv;  // Number.doubleValue() of a Float
+              __builtin_memcpy(&bits, &dv, 8);
+              break;
+            }
+            case KHIP_AVRO_DOUBLE:
+              if (vn - j < 8) { ok = false; break; }
+              bits = le_load(p + j, 8);
+              j += 8;
+              break;
+            default: {  // STRING / BYTES: long length, then the bytes
+              uint64_t v;
+              if (!avro_varint(p, vn, &j, 10, &v)) { ok = false; break; }
+              const int64_t len = zz64(v);
+              if (len < 0 || len > vn - j) { ok = false; break; }  // negative length / EOF
+              j += len;
+              break;
+            }
+          }
+          if (!ok || c < 0) continue;
+          fnull &= ~(1u << c);
+          const int t = q.ftype[f];
+          if (t == KHIP_TYPE_INT32) ((int32_t*)o.col[c])[i] = (int32_t)bits;
+          else if (t == KHIP_TYPE_STRING) ((int64_t*)o.col[c])[i] = 0;  // String.valueOf(any primitive)
+          else ((uint64_t*)o.col[c])[i] = bits;  // BIGINT (int widened) / DOUBLE (float widened)
+        }
       } else {  // JSON
         int64_t j = 0;
         while (j < vn && json_ws(p[j])) j++;
@@ -568,8 +720,13 @@ khip_status khip_serde_create(const khip_serde_desc* d, khip_serde** out) {
   if (d->key_format == KHIP_FMT_KAFKA && d->key_type != KHIP_TYPE_INT32 && d->key_type != KHIP_TYPE_INT64 &&
       d->key_type != KHIP_TYPE_STRING)
     return fail(KHIP_E_UNSUPPORTED, "key type");
-  if (d->value_format != KHIP_FMT_KAFKA && d->value_format != KHIP_FMT_DELIMITED && d->value_format != KHIP_FMT_JSON)
-    return fail(KHIP_E_UNSUPPORTED, "value format (KAFKA, DELIMITED, JSON)");
+  if (d->value_format != KHIP_FMT_KAFKA && d->value_format != KHIP_FMT_DELIMITED && d->value_format != KHIP_FMT_JSON &&
+      d->value_format != KHIP_FMT_AVRO)
+    return fail(KHIP_E_UNSUPPORTED, "value format (KAFKA, DELIMITED, JSON, AVRO)");
+  if (d->value_format == KHIP_FMT_AVRO &&
+      (d->avro_n_fields < 0 || d->avro_n_fields > SD_MAX_FIELDS || (d->avro_n_fields && (!d->avro_field_names ||
+                                                                                     !d->avro_field_types))))
+    return fail(KHIP_E_INVALID, "AVRO writer schema: 0..32 fields with names and types");
   if (d->n_fields < 1 || d->n_fields > SD_MAX_FIELDS) return fail(KHIP_E_UNSUPPORTED, "1..32 value fields");
   if (d->value_format == KHIP_FMT_KAFKA && d->n_fields != 1)
     return fail(KHIP_E_INVALID, "the KAFKA format carries one field");
@@ -591,15 +748,52 @@ khip_status khip_serde_create(const khip_serde_desc* d, khip_serde** out) {
     q.ftype[f] = t;
     q.fout[f] = d->field_out ? d->field_out[f] : f;
     if (q.fout[f] >= 0) n_out = std::max(n_out, q.fout[f] + 1);
-    if (d->value_format == KHIP_FMT_JSON) {
+    if (d->value_format == KHIP_FMT_JSON || d->value_format == KHIP_FMT_AVRO) {
       const char* nm = d->field_names ? d->field_names[f] : nullptr;
       const size_t L = nm ? strlen(nm) : 0;
       if (!nm || L > SD_NAME_BYTES) {
         delete s;
-        return fail(KHIP_E_INVALID, "JSON field names (<= 64 bytes) required");
+        return fail(KHIP_E_INVALID, "JSON / AVRO field names (<= 64 bytes) required");
       }
       q.name_len[f] = (int32_t)L;
       memcpy(q.name[f], nm, L);
+    }
+  }
+  if (d->value_format == KHIP_FMT_AVRO) {
+    // writer field → ksql field: the field of the same name, else of the upper-cased name
+    // (ConnectDataTranslator.toKsqlStruct: Java's toUpperCase; ASCII letters here); validateSchema
+    // (:123-146) runs on every mapped field of every record, so one incompatible type fails them all
+    q.avro_id = d->avro_schema_id;
+    q.avro_nw = d->avro_n_fields;
+    q.avro_incompat = 0;
+    for (int w = 0; w < d->avro_n_fields; w++) {
+      const int at = d->avro_field_types[w];
+      const int un = d->avro_field_union ? d->avro_field_union[w] : 0;
+      const char* wn = d->avro_field_names[w];
+      if (at < KHIP_AVRO_BOOLEAN || at > KHIP_AVRO_BYTES || un < 0 || un > 2 || !wn) {
+        delete s;
+        return fail(KHIP_E_UNSUPPORTED, "AVRO writer field: primitive type, plain or a union with null");
+      }
+      std::string up(wn);
+      for (char& ch : up)
+        if (ch >= 'a' && ch <= 'z') ch = (char)(ch - 32);
+      int fx = -1, fu = -1;
+      for (int f = 0; f < d->n_fields; f++) {
+        const std::string kn(d->field_names[f]);
+        if (kn == wn && fx < 0) fx = f;
+        if (kn == up && fu < 0) fu = f;
+      }
+      const int f = fx >= 0 ? fx : fu;
+      q.aw_type[w] = (int8_t)at;
+      q.aw_union[w] = (int8_t)un;
+      q.aw_field[w] = (int8_t)f;
+      if (f < 0) continue;
+      const int kt = d->field_types[f];
+      const bool okt = kt == KHIP_TYPE_STRING ? at != KHIP_AVRO_BYTES
+                       : kt == KHIP_TYPE_INT64 ? (at == KHIP_AVRO_INT || at == KHIP_AVRO_LONG)
+                       : kt == KHIP_TYPE_INT32 ? at == KHIP_AVRO_INT
+                                               : (at == KHIP_AVRO_FLOAT || at == KHIP_AVRO_DOUBLE);
+      if (!okt) q.avro_incompat = 1;
     }
   }
   q.n_out = n_out;

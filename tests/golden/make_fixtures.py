@@ -17,7 +17,7 @@ the final per-(key, window) table state is the LAST output per (key, window)
 The extractor recognises the statement shapes this path implements and skips the
 rest (reported on stdout):
 
-  aggregate:  CREATE STREAM s (cols) WITH (...value_format=JSON|AVRO|DELIMITED...);
+  aggregate:  CREATE STREAM s (cols) WITH (...value_format=JSON|AVRO|DELIMITED|JSON_SR|PROTOBUF...);
               CREATE TABLE t AS SELECT <group col>, <aggs | WINDOWSTART | WINDOWEND>
               FROM s [WINDOW TUMBLING|HOPPING (...)] GROUP BY <one column>
               [HAVING <agg> <op> <number>];
@@ -39,7 +39,15 @@ OUT_DIR = os.path.dirname(os.path.abspath(__file__))
 
 TYPE_MAP = {"INT": "INT32", "INTEGER": "INT32", "BIGINT": "INT64", "DOUBLE": "DOUBLE",
             "STRING": "STRING", "VARCHAR": "STRING", "BOOLEAN": "BOOLEAN"}
-SUPPORTED_FORMATS = {"JSON", "AVRO", "DELIMITED"}
+# value formats whose QTT input records are written as JSON objects (DELIMITED: as text); the
+# columnar path replays them all, the raw-record (deserializer) path covers JSON, DELIMITED and AVRO
+SUPPORTED_FORMATS = {"JSON", "AVRO", "DELIMITED", "JSON_SR", "PROTOBUF", "PROTOBUF_NOSR"}
+RAW_FORMATS = ("JSON", "DELIMITED", "AVRO")
+# proto3 without wrappers has no NULL: the PROTOBUF serializer writes a null field as its type's
+# default and the deserializer reads an absent field as it (0, 0.0, ""); such cases carry
+# "null_as_default" and the comparators read the build's NULLs in an output the same way
+PROTO_FORMATS = ("PROTOBUF", "PROTOBUF_NOSR")
+TYPE_DEFAULT = {"INT32": 0, "INT64": 0, "DOUBLE": 0.0, "STRING": "", "BOOLEAN": False}
 UNIT_MS = {"MILLISECOND": 1, "MILLISECONDS": 1, "SECOND": 1000, "SECONDS": 1000,
            "MINUTE": 60000, "MINUTES": 60000, "HOUR": 3600000, "HOURS": 3600000,
            "DAY": 86400000, "DAYS": 86400000}
@@ -200,6 +208,8 @@ def parse_value(fmt, value, value_cols):
     out = {}
     for c in value_cols:
         v = lower.get(c["name"])
+        if v is None and fmt in PROTO_FORMATS:
+            v = TYPE_DEFAULT.get(c["type"])
         out[c["name"]] = None if v is None else conv(c["type"], v)
     return out
 
@@ -433,7 +443,7 @@ def extract_agg(path, test, fmt_tag):
     # the serialized inputs (for the deserializer path): KAFKA key of the group column, the value
     # in the source's format, every value column of the schema
     raw = None
-    if by_key and src["format"] in ("JSON", "DELIMITED") and all(
+    if by_key and src["format"] in RAW_FORMATS and all(
             c["type"] in ("INT32", "INT64", "DOUBLE", "STRING") for c in value_cols):
         raw = {"format": src["format"], "key_type": gtype,
                "fields": [{"name": c["name"], "type": c["type"],
@@ -442,6 +452,7 @@ def extract_agg(path, test, fmt_tag):
     return {
         "name": test["name"] + (" [%s]" % fmt_tag if fmt_tag else ""),
         "source": "%s:%d" % (os.path.basename(path), find_line(path, test["name"])),
+        "null_as_default": src["format"] in PROTO_FORMATS,
         "raw": raw,
         "desc": {
             "window_kind": window["kind"] if window else "NONE",
@@ -566,6 +577,7 @@ def extract_join(path, test, fmt_tag):
     return {
         "name": test["name"] + (" [%s]" % fmt_tag if fmt_tag else ""),
         "source": "%s:%d" % (os.path.basename(path), find_line(path, test["name"])),
+        "null_as_default": s["format"] in PROTO_FORMATS or t["format"] in PROTO_FORMATS,
         "join_type": jt,
         "key_type": "UTF8" if tkey[0]["type"] == "STRING" else "INT64",
         "stream_cols": svals,

@@ -10,13 +10,36 @@ small batches): the checker of khip_serde_decode.
   JSON       ksqldb-serde/.../json/KsqlJsonDeserializer.java:149-300 + JsonSerdeUtils.java:95-136
              (Jackson tree: the field of the same name, else the upper-cased one; intValue() /
              asLong() / doubleValue() of numbers, the Java parsers of strings; booleans, objects
-             and arrays are coercion errors for numbers)
+             and arrays are coercion errors for numbers).  The mapper enables
+             USE_BIG_DECIMAL_FOR_FLOATS (KsqlJsonDeserializer.java:68-70): a token with a fraction or
+             an exponent is a BigDecimal, whose intValue() / longValue() truncate toward zero and
+             keep the low 32 / 64 bits of the integer part (no saturation, no rounding through a
+             double); doubleValue() is the correctly rounded double.
 Python's float() is correctly rounded like Double.parseDouble for decimal text.
 """
+import decimal
 import json
 import math
 import re
 import struct
+
+
+class JDec(str):
+    """A JSON number token with a fraction or an exponent (Jackson: BigDecimal), kept as text."""
+
+
+def bigdec_low_bits(tok, bits):
+    """BigDecimal(tok).intValue() (bits 32) / longValue() (bits 64): integer part, low bits."""
+    d = decimal.Decimal(tok)  # exact: the constructor does not round
+    sign, digits, exp = d.as_tuple()
+    if exp >= 64:  # 10^exp is a multiple of 2^64
+        v = 0
+    elif exp >= 0:
+        v = int("".join(map(str, digits)) or "0") * 10 ** exp
+    else:
+        keep = len(digits) + exp
+        v = int("".join(map(str, digits[:keep]))) if keep > 0 else 0
+    return wrap(-v if sign else v, bits)
 
 INT_RE = re.compile(r"^[+-]?[0-9]+$")
 DBL_RE = re.compile(r"^[+-]?(NaN|Infinity|([0-9]+\.?[0-9]*|\.[0-9]+)([eE][+-]?[0-9]+)?[fFdD]?)$")
@@ -150,7 +173,8 @@ def decode_value(fmt, fields, raw, delim=","):
         pairs_seen.append(pairs)
         return pairs
     try:
-        obj, _ = json.JSONDecoder(object_pairs_hook=hook, parse_constant=bad_const).raw_decode(text)
+        obj, _ = json.JSONDecoder(object_pairs_hook=hook, parse_constant=bad_const,
+                                  parse_float=JDec).raw_decode(text)
     except ValueError as e:
         raise Err(str(e))
     if not isinstance(obj, list) or not pairs_seen or obj is not pairs_seen[-1]:
@@ -170,12 +194,15 @@ def decode_value(fmt, fields, raw, delim=","):
             continue
         if isinstance(v, bool) or isinstance(v, list):  # booleans, objects (pair lists), arrays
             raise Err("coercion")
-        if isinstance(v, str):
+        if isinstance(v, JDec):  # BigDecimal
+            out[name] = bigdec_low_bits(v, 32) if t == "INT32" else (bigdec_low_bits(v, 64) if t == "INT64"
+                                                                      else float(v))
+        elif isinstance(v, str):
             out[name] = coerce_text(v, t)
         elif isinstance(v, int):
             out[name] = wrap(v, 32) if t == "INT32" else (wrap(v, 64) if t == "INT64" else float(v))
         else:
-            out[name] = java_d2i(v, 32) if t == "INT32" else (java_d2i(v, 64) if t == "INT64" else v)
+            raise Err("unexpected JSON value")
     return out
 
 

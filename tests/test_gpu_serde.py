@@ -8,6 +8,7 @@ import struct
 import numpy as np
 import pytest
 
+import avro_ref
 import qtt
 import serde_ref
 from ksql_amd import abi
@@ -85,8 +86,8 @@ def _json(rng):
                 val = json.dumps(_num_text(rng, t))  # numbers as strings
             elif k < 0.8:
                 val = rng.choice(["true", "{\"a\":1}", "[1]"])
-            elif k < 0.9:
-                val = repr(rng.uniform(-3e9, 3e9))  # float token into an integer column
+            elif k < 0.9:  # float token into an integer column (BigDecimal truncation)
+                val = repr(rng.uniform(-3e9, 3e9)) if rng.random() < 0.6 else rng.choice(DECIMAL_TOKENS)
             else:
                 val = str(rng.randrange(-(1 << 70), 1 << 70))  # BigInteger token
         obj.append('"%s": %s' % (key, val))
@@ -98,6 +99,30 @@ def _json(rng):
     if rng.random() < 0.05:
         body = "  " + body + "  trailing"
     return body.encode()
+
+
+# JSON float tokens (Jackson BigDecimal) whose int / long value differs from a saturating double
+# conversion: above 2^31, above 2^53 (digits a double loses), 1e20 (low 64 bits), huge exponents
+DECIMAL_TOKENS = ["3000000000.5", "-3000000000.5", "1e20", "-1e20", "9007199254740993.7", "1.5e300", "-0.9",
+                  "123456789012345678901234.9", "4.2E1", "1e-5", "0.0", "-0e0", "18446744073709551617.25",
+                  "2147483648.0", "-2147483649.99", "1E+19", "12345678901234567890e-3"]
+
+
+def test_json_decimal_into_integer_columns(prod):
+    """USE_BIG_DECIMAL_FOR_FLOATS (KsqlJsonDeserializer.java:68-70): intValue() / longValue() of a
+    BigDecimal keep the low bits of the truncated integer part, exactly."""
+    fields = [("V32", "INT32", 0), ("V64", "INT64", 1), ("D", "DOUBLE", 2)]
+    vals = [('{"V32": %s, "V64": %s, "D": %s}' % (t, t, t)).encode() for t in DECIMAL_TOKENS]
+    keys = [struct.pack(">q", i) for i in range(len(vals))]
+    sd = abi.SerdeHandle(prod, "JSON", fields, key_type="INT64")
+    d, nerr = sd.decode(np.arange(len(vals), dtype=np.int64), keys, vals)
+    exp, experr = serde_ref.decode("JSON", fields, "INT64", keys, vals)
+    assert nerr == experr == 0
+    got = sd.columns(d, ["INT32", "INT64", "DOUBLE"])
+    _check(got, exp, fields, ["INT32", "INT64", "DOUBLE"])
+    assert int(got["cols"][0][0]) == -1294967296 and int(got["cols"][1][2]) == 7766279631452241920
+    assert int(got["cols"][1][4]) == 9007199254740993
+    sd.close()
 
 
 def _kafka_value(rng):
@@ -197,7 +222,9 @@ def test_qtt_raw_records_end_to_end(prod, case):
     raw = case["raw"]
     fields = [(f["name"], f["type"], f["out"]) for f in raw["fields"]]
     key_type = raw["key_type"]
-    sd = abi.SerdeHandle(prod, raw["format"], fields, key_type="STRING" if key_type == "STRING" else key_type)
+    writer = avro_ref.ksql_writer_schema(fields) if raw["format"] == "AVRO" else None
+    sd = abi.SerdeHandle(prod, raw["format"], fields, key_type="STRING" if key_type == "STRING" else key_type,
+                         avro_schema=writer)
     h = abi.AggHandle(prod, qtt.case_desc(case))
     rows = []
     for rec in raw["records"]:
@@ -209,13 +236,36 @@ def test_qtt_raw_records_end_to_end(prod, case):
         else:
             kb = struct.pack(">q" if key_type == "INT64" else ">i", int(k))
         v = rec["value"]
-        vb = None if v is None else (v if isinstance(v, str) else json.dumps(v)).encode()
+        if v is None:
+            vb = None
+        elif writer:  # the QTT harness serializes the spec's JSON object with the source's AVRO schema
+            vb = avro_ref.encode(writer, _avro_spec(v, fields))
+        else:
+            vb = (v if isinstance(v, str) else json.dumps(v)).encode()
         d, nerr = sd.decode(np.array([rec["ts"]], np.int64), [kb], [vb])
         h.push(d)
         rows += qtt._rows_of(h.changes())
     h.close()
     sd.close()
     assert qtt.compare_outputs(case, rows) == []
+
+
+def _avro_spec(value, fields):
+    """A QTT input value (JSON object) as the Avro record of the source's schema: the field of the
+    column's name (any case), coerced to the column's type."""
+    up = {k.upper(): x for k, x in value.items()}
+    rec = {}
+    for name, t, _ in fields:
+        x = up.get(name)
+        if x is None:
+            rec[name] = None
+        elif t == "STRING":
+            rec[name] = x if isinstance(x, str) else json.dumps(x)
+        elif t == "DOUBLE":
+            rec[name] = float(x)
+        else:
+            rec[name] = int(x)
+    return rec
 
 
 @pytest.mark.parametrize("narrow", [False, True])
@@ -262,3 +312,81 @@ def _narrow_delimited(v):
     6-field row; other records (quoted, malformed) stay as they are: errors on both sides."""
     parts = v.split(b",")
     return b",".join(parts[1:5]) if len(parts) == 6 and b'"' not in v and b"\n" not in v else v
+
+
+# ---- AVRO (Confluent wire format + Avro binary of the writer schema; tests/avro_ref.py)
+
+AVRO_FIELDS = [("ID", "INT64", -1), ("V32", "INT32", 0), ("V64", "INT64", 1), ("D", "DOUBLE", 2), ("NAME", "STRING", 3),
+               ("F", "DOUBLE", 4), ("W", "INT64", 5)]
+# the writer's record: lower-case names matched through upper-casing, a float into a DOUBLE column,
+# an int into a BIGINT column, both union orders, plain fields, fields no column reads
+AVRO_WRITER = [("id", "long", 1), ("extra", "string", 1), ("V32", "int", 2), ("v64", "long", 0), ("D", "double", 1),
+               ("flag", "boolean", 0), ("NAME", "boolean", 1), ("F", "float", 1), ("w", "int", 1),
+               ("blob", "bytes", 0)]
+
+
+def _avro_record(rng):
+    rec = {"id": rng.randrange(-(1 << 63), 1 << 63), "extra": rng.choice([None, "", "xyz", "é" * 40]),
+           "V32": rng.randrange(-(1 << 31), 1 << 31), "v64": rng.randrange(-(1 << 63), 1 << 63),
+           "D": rng.choice([rng.uniform(-1e9, 1e9), float("nan"), -0.0, 1e-310]), "flag": rng.random() < 0.5,
+           "NAME": rng.random() < 0.5, "F": rng.uniform(-1e6, 1e6), "w": rng.randrange(-(1 << 31), 1 << 31),
+           "blob": bytes(rng.randrange(256) for _ in range(rng.randrange(0, 20)))}
+    for k in ("id", "extra", "V32", "D", "NAME", "F", "w"):
+        if rng.random() < 0.1:
+            rec[k] = None
+    return rec
+
+
+def _avro_corrupt(rng, b):
+    k = rng.randrange(7)
+    if k == 0:
+        return b"\x01" + b[1:]  # unknown magic byte
+    if k == 1:
+        return b[:rng.randrange(0, len(b))]  # truncated
+    if k == 2:
+        return b[:5] + b"\x04" + b[6:]  # union branch index 2
+    if k == 3:
+        return b[:5] + b"\x02" + b"\xff" * 10 + b"\x01"  # long varint over 10 bytes
+    if k == 4:
+        return b[:1] + b"\x00\x00\x00\x09" + b[5:]  # another schema id
+    if k == 5:
+        return b + b"trailing bytes"  # ignored: not an error
+    return b"\x00"  # shorter than the header
+
+
+def test_avro_decode_vs_reference(prod):
+    rng = random.Random(21)
+    fields = AVRO_FIELDS
+    out_types = ["INT32", "INT64", "DOUBLE", "STRING", "DOUBLE", "INT64"]
+    sd = abi.SerdeHandle(prod, "AVRO", fields, key_type="INT64", avro_schema=AVRO_WRITER, avro_schema_id=7)
+    for n in (1, 64, 5000):
+        keys, vals = [], []
+        for _ in range(n):
+            r = rng.random()
+            keys.append(None if r < 0.03 else struct.pack(">q", rng.randrange(-1000, 1000)))
+            if rng.random() < 0.05:
+                vals.append(None)
+                continue
+            b = avro_ref.encode(AVRO_WRITER, _avro_record(rng), schema_id=7)
+            vals.append(_avro_corrupt(rng, b) if rng.random() < 0.1 else b)
+        ts = np.arange(n, dtype=np.int64)
+        d, nerr = sd.decode(ts, keys, vals)
+        exp, experr = avro_ref.decode(fields, AVRO_WRITER, "INT64", keys, vals, schema_id=7)
+        assert nerr == experr
+        _check(sd.columns(d, out_types), exp, fields, out_types)
+    sd.close()
+
+
+def test_avro_incompatible_writer_type_fails_every_record(prod):
+    """validateSchema (ConnectDataTranslator.java:123-146): a long field for an INT column fails
+    each record, even where that field is null; null values (tombstones) stay null."""
+    fields = [("A", "INT32", 0), ("B", "INT64", 1)]
+    writer = [("A", "long", 1), ("B", "long", 1)]
+    vals = [avro_ref.encode(writer, {"A": None, "B": 5}), None, avro_ref.encode(writer, {"A": 3, "B": 4})]
+    keys = [struct.pack(">q", i) for i in range(3)]
+    sd = abi.SerdeHandle(prod, "AVRO", fields, key_type="INT64", avro_schema=writer)
+    d, nerr = sd.decode(np.arange(3, dtype=np.int64), keys, vals)
+    exp, experr = avro_ref.decode(fields, writer, "INT64", keys, vals)
+    assert nerr == experr == 2
+    _check(sd.columns(d, ["INT32", "INT64"]), exp, fields, ["INT32", "INT64"])
+    sd.close()

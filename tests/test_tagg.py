@@ -97,7 +97,7 @@ def test_tagg_random_vs_oracle(prod, orc, utf8_src, utf8_group, pushes):
     scale = sum(float(x.sum()) for _, _, x in batches) * 4  # every row can be added and undone twice
     (g, gs), (o, os_) = (_run(lib, batches, utf8_group) for lib in (prod, orc))
     for a, b in zip(gs, os_):
-        for f in ("rows_in", "rows_accepted", "dropped_null_key", "dropped_bad_ts", "windows_applied"):
+        for f in ("rows_in", "rows_accepted", "dropped_null_key", "dropped_bad_ts", "windows_applied", "stream_time"):
             assert a[f] == b[f], f
     _assert_same(g, o, scale)
     having = {"agg": 0, "op": "GT", "value": 0}  # HAVING COUNT(*) > 0: emptied groups disappear
@@ -162,7 +162,7 @@ def test_tagg_key_range_edges(prod, orc):
     ]
     (g, gs), (o, os_) = (_run(lib, batches, False) for lib in (prod, orc))
     for a, b in zip(gs, os_):
-        for f in ("rows_in", "rows_accepted", "dropped_null_key", "dropped_bad_ts", "windows_applied"):
+        for f in ("rows_in", "rows_accepted", "dropped_null_key", "dropped_bad_ts", "windows_applied", "stream_time"):
             assert a[f] == b[f], f
     _assert_same(g, o, 100.0)
 
@@ -201,7 +201,7 @@ def test_tagg_narrow_rows_vs_oracle(prod, orc, ncols, utf8_src):
         h.close()
     (g, gs), (o, os_) = res
     for a, b in zip(gs, os_):
-        for f in ("rows_in", "rows_accepted", "dropped_null_key", "dropped_bad_ts", "windows_applied"):
+        for f in ("rows_in", "rows_accepted", "dropped_null_key", "dropped_bad_ts", "windows_applied", "stream_time"):
             assert a[f] == b[f], f
     assert g["n"] == o["n"] and list(g["key"]) == list(o["key"])
     assert np.array_equal(g["rowtime"], o["rowtime"])
