@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KHIP_ABI_VERSION 3
+#define KHIP_ABI_VERSION 4
 
 typedef int32_t khip_status;
 #define KHIP_OK 0
@@ -583,6 +583,102 @@ khip_status khip_serde_create(const khip_serde_desc* desc, khip_serde** out);
  * the records that failed to deserialize. */
 khip_status khip_serde_decode(khip_serde* s, const khip_raw_batch* in, khip_batch* out, int64_t* n_errors);
 khip_status khip_serde_destroy(khip_serde* s);
+
+/* ---------------------------------------------- serialization (device columns → record bytes) */
+
+/* The output side of GenericKeySerDe / GenericRowSerDe for a sink topic (ksqldb-serde/src/main/
+ * java/io/confluent/ksql/serde/GenericKeySerDe.java:95-117, GenericRowSerDe.java), run on the
+ * device over columnar rows:
+ *   key    the inner key in key_format — KAFKA (kafka/KafkaSerdeFactory.java:42-46: INT 4-byte /
+ *          BIGINT 8-byte big-endian, DOUBLE 8-byte IEEE big-endian, STRING UTF-8; one column),
+ *          JSON (one column unwrapped = the bare JSON value; several = an object in column order),
+ *          DELIMITED (the CSV record of the columns) — then, for a windowed table, Kafka Streams'
+ *          TimeWindowedSerializer (inner ++ 8-byte big-endian window start) or
+ *          SessionWindowedSerializer (inner ++ 8-byte big-endian window end ++ window start).
+ *   value  JSON: Kafka Connect JsonConverter with schemas off (json/KsqlJsonSerdeFactory.java:
+ *          158-161) → compact object in column order; DELIMITED: KsqlDelimitedSerializer
+ *          (delimited/KsqlDelimitedSerializer.java:59-71; commons-csv 1.4 MINIMAL quoting, null =
+ *          empty field); KAFKA: the single column's primitive bytes (a NULL column = a null value).
+ *          A tombstone row (the row left the table / a HAVING delete) has a null value.
+ * Numbers print as Long.toString / Double.toString (JDK 19+ shortest-decimal specification;
+ * non-finite doubles as the JSON strings "NaN" / "Infinity" / "-Infinity", Jackson's default).
+ * Group identity in the reference is equality of the serialized key, so the bytes
+ * khip_sink_key builds from several GROUP BY columns are also the composite key the aggregate
+ * groups by (a KHIP_KEY_UTF8 handle). */
+#define KHIP_SINK_MAX_COLS 32
+#define KHIP_SINK_SRC_WS (-2)   /* value column source: WINDOWSTART                            */
+#define KHIP_SINK_SRC_WE (-3)   /* value column source: WINDOWEND                              */
+
+typedef struct khip_sink_desc {
+  int32_t key_format;              /* KHIP_FMT_KAFKA / JSON / DELIMITED                          */
+  int32_t n_key_cols;              /* 1..KHIP_SINK_MAX_COLS (KAFKA: 1)                            */
+  const int32_t* key_types;        /* KHIP_TYPE_INT32 / INT64 / DOUBLE / STRING                   */
+  const char* const* key_names;    /* JSON object field names (several key columns)              */
+  int32_t window_kind;             /* KHIP_WINDOW_*: the table's window (NONE: plain key)        */
+  int32_t value_format;            /* KHIP_FMT_KAFKA / JSON / DELIMITED                          */
+  int32_t n_value_cols;            /* 0..KHIP_SINK_MAX_COLS (KAFKA: 1)                            */
+  const int32_t* value_types;      /* KHIP_TYPE_INT32 / INT64 / DOUBLE                            */
+  const char* const* value_names;  /* JSON field names, in output column order                   */
+  const int32_t* value_src;        /* rows column index, or KHIP_SINK_SRC_WS / KHIP_SINK_SRC_WE   */
+  int32_t delimiter;               /* DELIMITED: the delimiter byte (0 = ',')                     */
+  int32_t device;
+} khip_sink_desc;
+
+typedef struct khip_sink khip_sink;
+
+khip_status khip_sink_create(const khip_sink_desc* desc, khip_sink** out);
+
+/* One GROUP BY column of a batch (same memory kind as the batch). */
+typedef struct khip_key_col {
+  const void* data;         /* INT32 / INT64 / DOUBLE: n_rows elements                            */
+  const int64_t* offsets;   /* STRING: n_rows + 1 offsets into bytes                              */
+  const uint8_t* bytes;
+  const uint8_t* valid;     /* bitmap, NULL = all valid                                          */
+} khip_key_col;
+
+/* GROUP BY columns → the serialized inner key of every row (GroupByParamsFactory.ExpressionGrouper,
+ * S/GroupByParamsFactory.java:137-150): key column i is cols[i], of type desc.key_types[i].  A row
+ * with any NULL key column gets a null key (the reference drops it, :92-100).  *out = the input
+ * batch with its key replaced by these bytes (KHIP_KEY_UTF8 layout, in the batch's memory kind,
+ * owned by the handle and valid until its next call); ts, validity and value columns are the
+ * input's. */
+khip_status khip_sink_key(khip_sink* s, const khip_batch* in, const khip_key_col* cols, khip_batch* out);
+
+/* Rows in khip_snapshot layout (what khip_agg_changes / khip_agg_snapshot write). */
+typedef struct khip_sink_rows {
+  int64_t n_rows;
+  int32_t mem;                     /* KHIP_MEM_HOST or KHIP_MEM_DEVICE (every pointer below)     */
+  int32_t key_serialized;          /* 1: key_offsets/key_bytes hold the serialized inner key      */
+  const int64_t* key_i64;          /* one INT32 / INT64 key column                                */
+  const int64_t* key_offsets;      /* STRING key column or serialized keys: n_rows + 1 offsets    */
+  const uint8_t* key_bytes;
+  const int64_t* window_start;
+  const int64_t* window_end;
+  const void* const* col_data;     /* the value sources (agg results); element type from desc     */
+  const uint8_t* const* col_null;  /* 1 byte per row, 1 = NULL (entries may be NULL)             */
+  const uint8_t* tombstone;        /* 1 byte per row, 1 = delete → null value (may be NULL)      */
+} khip_sink_rows;
+
+typedef struct khip_sink_out {
+  int32_t mem;                     /* where the buffers below live                                */
+  int32_t reserved;
+  int64_t key_capacity;            /* bytes                                                       */
+  int64_t value_capacity;          /* bytes                                                       */
+  int64_t* key_offsets;            /* n_rows + 1 (from 0)                                         */
+  uint8_t* key_bytes;
+  int64_t* value_offsets;          /* n_rows + 1 (from 0)                                         */
+  uint8_t* value_bytes;
+  uint8_t* value_null;             /* 1 byte per row: 1 = null value (tombstone)                  */
+  int64_t key_len;                 /* out: key bytes written (needed, on KHIP_E_BUFFER)           */
+  int64_t value_len;               /* out: value bytes written (needed, on KHIP_E_BUFFER)         */
+} khip_sink_out;
+
+/* Serialize rows into sink records (key bytes, value bytes or null).  The encoding runs on the
+ * device; host rows are staged in and host outputs copied back.  On KHIP_E_BUFFER nothing is
+ * written except key_len / value_len. */
+khip_status khip_sink_encode(khip_sink* s, const khip_sink_rows* rows, khip_sink_out* out);
+khip_status khip_sink_sync(khip_sink* s);
+khip_status khip_sink_destroy(khip_sink* s);
 
 /* ------------------------------------------------------------ diagnostics */
 

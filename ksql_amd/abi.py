@@ -19,7 +19,7 @@ PRODUCT_LIB = os.path.join(REPO, "ksql_amd", "libksqldb_hip_tune.so" if os.envir
                            else "libksqldb_hip.so")
 ORACLE_LIB = os.path.join(REPO, "oracle", "liboracle.so")
 
-ABI_VERSION = 3  # include/ksqldb_hip.h KHIP_ABI_VERSION the structs below mirror
+ABI_VERSION = 4  # include/ksqldb_hip.h KHIP_ABI_VERSION the structs below mirror
 KHIP_OK = 0
 KHIP_E_BUFFER = -5
 
@@ -142,7 +142,32 @@ class RawBatch(C.Structure):
                 ("value_bytes", C.c_void_p), ("value_valid", C.c_void_p)]
 
 
+class SinkDesc(C.Structure):
+    _fields_ = [("key_format", i32), ("n_key_cols", i32), ("key_types", C.POINTER(i32)),
+                ("key_names", C.POINTER(C.c_char_p)), ("window_kind", i32), ("value_format", i32),
+                ("n_value_cols", i32), ("value_types", C.POINTER(i32)), ("value_names", C.POINTER(C.c_char_p)),
+                ("value_src", C.POINTER(i32)), ("delimiter", i32), ("device", i32)]
+
+
+class KeyCol(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("offsets", C.c_void_p), ("bytes", C.c_void_p), ("valid", C.c_void_p)]
+
+
+class SinkRows(C.Structure):
+    _fields_ = [("n_rows", i64), ("mem", i32), ("key_serialized", i32), ("key_i64", C.c_void_p),
+                ("key_offsets", C.c_void_p), ("key_bytes", C.c_void_p), ("window_start", C.c_void_p),
+                ("window_end", C.c_void_p), ("col_data", C.POINTER(C.c_void_p)), ("col_null", C.POINTER(C.c_void_p)),
+                ("tombstone", C.c_void_p)]
+
+
+class SinkOut(C.Structure):
+    _fields_ = [("mem", i32), ("reserved", i32), ("key_capacity", i64), ("value_capacity", i64),
+                ("key_offsets", C.c_void_p), ("key_bytes", C.c_void_p), ("value_offsets", C.c_void_p),
+                ("value_bytes", C.c_void_p), ("value_null", C.c_void_p), ("key_len", i64), ("value_len", i64)]
+
+
 FMT = {"NONE": 0, "KAFKA": 1, "DELIMITED": 2, "JSON": 3, "AVRO": 4}
+SINK_SRC = {"WS": -2, "WE": -3}
 AVRO_TYPE = {"boolean": 1, "int": 2, "long": 3, "float": 4, "double": 5, "string": 6, "bytes": 7}
 TYPE_STRING = 3
 COMM_ID_BYTES = 128
@@ -186,6 +211,11 @@ PRODUCT_ONLY = {
     "serde_create": ([C.POINTER(SerdeDesc), C.POINTER(_P)]),
     "serde_decode": ([_P, C.POINTER(RawBatch), C.POINTER(Batch), C.POINTER(i64)]),
     "serde_destroy": ([_P]),
+    "sink_create": ([C.POINTER(SinkDesc), C.POINTER(_P)]),
+    "sink_key": ([_P, C.POINTER(Batch), C.POINTER(KeyCol), C.POINTER(Batch)]),
+    "sink_encode": ([_P, C.POINTER(SinkRows), C.POINTER(SinkOut)]),
+    "sink_sync": ([_P]),
+    "sink_destroy": ([_P]),
 }
 
 
@@ -860,6 +890,151 @@ class SerdeHandle:
     def close(self):
         if self.h:
             self.lib.serde_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class SinkHandle:
+    """khip_sink_*: columnar rows → sink record bytes (windowed key, value or null), and GROUP BY
+    columns → the serialized composite key."""
+
+    def __init__(self, lib, key_format, key_cols, value_format, value_cols, window_kind="NONE", delimiter=",",
+                 device=0):
+        """key_cols: [(name, type)]; value_cols: [(name, type, src)] with src a rows column index or
+        "WS" / "WE"; types INT32 / INT64 / DOUBLE / STRING (keys)."""
+        self.lib = lib
+        tmap = dict(TYPE, STRING=TYPE_STRING)
+        nk, nv = len(key_cols), len(value_cols)
+        self._kt = (i32 * max(nk, 1))(*[tmap[t] for _, t in key_cols])
+        self._kn = (C.c_char_p * max(nk, 1))(*[n.encode() for n, _ in key_cols])
+        self._vt = (i32 * max(nv, 1))(*[tmap[t] for _, t, _ in value_cols])
+        self._vn = (C.c_char_p * max(nv, 1))(*[n.encode() for n, _, _ in value_cols])
+        self._vs = (i32 * max(nv, 1))(*[SINK_SRC[s] if isinstance(s, str) else s for _, _, s in value_cols])
+        self.key_cols, self.value_cols = key_cols, value_cols
+        self.desc = SinkDesc(FMT[key_format], nk, self._kt, self._kn, WINDOW[window_kind], FMT[value_format], nv,
+                             self._vt, self._vn, self._vs, ord(delimiter), device)
+        self.h = C.c_void_p()
+        lib.check(lib.sink_create(C.byref(self.desc), C.byref(self.h)), "sink_create")
+
+    def key(self, batch, cols):
+        """batch: a HostBatch (host columns) or any batch object with .struct; cols: per key column
+        a numpy array (INT32 / INT64 / DOUBLE; or (array, bool validity)) or a list of str / bytes /
+        None (STRING), host
+        memory, or a dict {"data" | "offsets" + "bytes", "valid"} of device pointers for a device
+        batch.  Returns a batch object whose key is the serialized key (UTF-8 key layout, usable by
+        AggHandle.push on a UTF8 handle); NULL in any column = a null key."""
+        keep = []
+        kc = (KeyCol * len(cols))()
+        for i, c in enumerate(cols):
+            if isinstance(c, dict):
+                kc[i] = KeyCol(c.get("data"), c.get("offsets"), c.get("bytes"), c.get("valid"))
+                continue
+            if isinstance(c, tuple):  # (numpy array, bool validity)
+                a = np.ascontiguousarray(c[0])
+                vb = bitmap(c[1])
+                keep += [a, vb]
+                kc[i].data, kc[i].valid = a.ctypes.data, _ptr(vb)
+                continue
+            if isinstance(c, np.ndarray):
+                a = np.ascontiguousarray(c)
+                keep.append(a)
+                kc[i].data = a.ctypes.data
+                continue
+            enc = [None if x is None else (x.encode() if isinstance(x, str) else bytes(x)) for x in c]
+            offs = np.zeros(len(enc) + 1, np.int64)
+            offs[1:] = np.cumsum([0 if e is None else len(e) for e in enc]) if enc else []
+            data = np.frombuffer(b"".join(e or b"" for e in enc) + b"\0", np.uint8).copy()
+            vb = bitmap([e is not None for e in enc])
+            keep += [offs, data, vb]
+            kc[i].offsets, kc[i].bytes, kc[i].valid = offs.ctypes.data, data.ctypes.data, _ptr(vb)
+        out = Batch()
+        self.lib.check(self.lib.sink_key(self.h, C.byref(batch.struct), kc, C.byref(out)), "sink_key")
+
+        class _Keyed:
+            pass
+        k = _Keyed()
+        k.struct = out
+        k._keep = (batch, kc, keep)
+        return k
+
+    def key_bytes(self, keyed):
+        """Host copy of a keyed host batch's keys: list of bytes or None (null key)."""
+        b = keyed.struct
+        n = b.n_rows
+        offs = np.ctypeslib.as_array(C.cast(b.key_offsets, C.POINTER(i64)), shape=(n + 1,))
+        tot = int(offs[n]) if n else 0
+        data = bytes(np.ctypeslib.as_array(C.cast(b.key_bytes, C.POINTER(C.c_uint8)), shape=(max(tot, 1),))[:tot])
+        nb = (n + 7) // 8
+        valid = np.unpackbits(np.ctypeslib.as_array(C.cast(b.key_valid, C.POINTER(C.c_uint8)), shape=(max(nb, 1),)),
+                              bitorder="little")[:n].astype(bool)
+        return [data[offs[i]:offs[i + 1]] if valid[i] else None for i in range(n)]
+
+    def encode(self, snap, tombstone=None, key_serialized=False):
+        """snap: a snapshot dict (AggHandle.snapshot() / changes() layout: key or key_bytes/key_offsets,
+        ws, we, values, nulls); host rows.  Returns (keys, values): lists of bytes / None."""
+        n = int(snap["n"])
+        keep = []
+
+        def arr(a, dtype):
+            a = np.ascontiguousarray(a, dtype)
+            keep.append(a)
+            return a.ctypes.data
+        rows = SinkRows()
+        rows.n_rows = n
+        rows.mem = MEM_HOST
+        rows.key_serialized = 1 if key_serialized else 0
+        if snap.get("key_offsets") is None and len(snap.get("key", [])) and isinstance(snap["key"][0], (str, bytes)):
+            enc = [k.encode("utf-8", "surrogateescape") if isinstance(k, str) else k for k in snap["key"]]
+            snap = dict(snap, key_offsets=np.concatenate([[0], np.cumsum([len(e) for e in enc])]).astype(np.int64),
+                        key_bytes=np.frombuffer(b"".join(enc) or b"\0", np.uint8)[:sum(len(e) for e in enc)])
+        if snap.get("key_offsets") is not None:
+            rows.key_offsets = arr(snap["key_offsets"], np.int64)
+            rows.key_bytes = arr(np.concatenate([np.asarray(snap["key_bytes"], np.uint8), np.zeros(1, np.uint8)]), np.uint8)
+        else:
+            rows.key_i64 = arr(snap["key"], np.int64)
+        rows.window_start = arr(snap["ws"], np.int64)
+        rows.window_end = arr(snap["we"], np.int64)
+        vals = snap.get("values", [])
+        nulls = snap.get("nulls", [])
+        cd = (C.c_void_p * max(len(vals), 1))()
+        cn = (C.c_void_p * max(len(vals), 1))()
+        for j, v in enumerate(vals):
+            v = np.asarray(v)
+            cd[j] = arr(v, v.dtype)
+            cn[j] = arr(np.asarray(nulls[j], np.uint8), np.uint8) if j < len(nulls) and nulls[j] is not None else None
+        rows.col_data = cd
+        rows.col_null = cn
+        if tombstone is not None:
+            rows.tombstone = arr(np.asarray(tombstone, np.uint8), np.uint8)
+        out = SinkOut()
+        out.mem = MEM_HOST
+        koff = np.zeros(n + 1, np.int64)
+        voff = np.zeros(n + 1, np.int64)
+        vnull = np.zeros(max(n, 1), np.uint8)
+        out.key_offsets, out.value_offsets, out.value_null = koff.ctypes.data, voff.ctypes.data, vnull.ctypes.data
+        st = self.lib.sink_encode(self.h, C.byref(rows), C.byref(out))
+        if st == KHIP_E_BUFFER:
+            kb = np.zeros(max(out.key_len, 1), np.uint8)
+            vb = np.zeros(max(out.value_len, 1), np.uint8)
+            out.key_capacity, out.value_capacity = out.key_len, out.value_len
+            out.key_bytes, out.value_bytes = kb.ctypes.data, vb.ctypes.data
+            st = self.lib.sink_encode(self.h, C.byref(rows), C.byref(out))
+        else:
+            kb = vb = np.zeros(1, np.uint8)
+        self.lib.check(st, "sink_encode")
+        kbs, vbs = kb.tobytes(), vb.tobytes()
+        keys = [kbs[koff[i]:koff[i + 1]] for i in range(n)]
+        values = [None if vnull[i] else vbs[voff[i]:voff[i + 1]] for i in range(n)]
+        return keys, values
+
+    def close(self):
+        if self.h:
+            self.lib.sink_destroy(self.h)
             self.h = C.c_void_p()
 
     def __del__(self):

@@ -34,6 +34,9 @@ import os
 import re
 import sys
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import sink_ref  # noqa: E402  (test infrastructure: the composite-key serializer)
+
 QTT_DIR = "/root/reference/ksqldb-functional-tests/src/test/resources/query-validation-tests"
 OUT_DIR = os.path.dirname(os.path.abspath(__file__))
 
@@ -43,6 +46,7 @@ TYPE_MAP = {"INT": "INT32", "INTEGER": "INT32", "BIGINT": "INT64", "DOUBLE": "DO
 # columnar path replays them all, the raw-record (deserializer) path covers JSON, DELIMITED and AVRO
 SUPPORTED_FORMATS = {"JSON", "AVRO", "DELIMITED", "JSON_SR", "PROTOBUF", "PROTOBUF_NOSR"}
 RAW_FORMATS = ("JSON", "DELIMITED", "AVRO")
+SINK_FORMATS = ("JSON", "DELIMITED", "KAFKA")  # what khip_sink_encode writes
 # proto3 without wrappers has no NULL: the PROTOBUF serializer writes a null field as its type's
 # default and the deserializer reads an absent field as it (0, 0.0, ""); such cases carry
 # "null_as_default" and the comparators read the build's NULLs in an output the same way
@@ -123,8 +127,9 @@ def parse_create_source(stmt, kind):
     if "window_type" in props:
         raise Skip("windowed source")
     cols = parse_columns(m.group(2))
+    kfmt = (props.get("key_format") or props.get("format") or "KAFKA").upper()
     return {"name": m.group(1).upper(), "cols": cols, "topic": props.get("kafka_topic"),
-            "format": fmt}
+            "format": fmt, "key_format": kfmt}
 
 
 def duration_ms(text):
@@ -279,24 +284,51 @@ def extract_agg(path, test, fmt_tag):
     if table_source and window:
         raise Skip("windowed table source")
     gb = split_top(m.group(8))
-    if len(gb) != 1 or not re.match(r"^\(?\s*[\w`.]+\s*\)?$", gb[0]):
-        raise Skip("group by shape")
-    gcol = unq(gb[0].strip("() "))
+    gcols = []
+    for g in gb:
+        if not re.match(r"^\(?\s*[\w`.]+\s*\)?$", g):
+            raise Skip("group by shape")
+        gcols.append(unq(g.strip("() ")))
     colmap = {c["name"]: c for c in src["cols"]}
-    if gcol not in colmap:
-        raise Skip("group col")
+    for g in gcols:
+        if g not in colmap:
+            raise Skip("group col")
     key_cols = [c for c in src["cols"] if c["key"]]
     value_cols = [c for c in src["cols"] if not c["key"]]
-    gtype = colmap[gcol]["type"]
-    if gtype not in ("INT32", "INT64", "STRING"):
-        raise Skip("group type " + gtype)
-    by_key = colmap[gcol]["key"]
-    if by_key and len(key_cols) != 1:
-        raise Skip("multi key")
+    gtypes = [colmap[g]["type"] for g in gcols]
+    for t in gtypes:
+        if t not in ("INT32", "INT64", "STRING"):
+            raise Skip("group type " + t)
+    # several GROUP BY columns: the group key is the serialized multi-column key (its identity in
+    # the reference is the serialized bytes), built on the device by khip_sink_key
+    composite = len(gcols) > 1
+    if composite:
+        if src["key_format"] not in ("JSON", "DELIMITED"):
+            raise Skip("multi-col key format " + src["key_format"])
+        if table_source:
+            raise Skip("composite_table source")
+    gcol, gtype = gcols[0], gtypes[0]
+    by_key = not composite and colmap[gcol]["key"] and len(key_cols) == 1
     if table_source:
         if len(key_cols) != 1 or key_cols[0]["type"] not in ("INT32", "INT64", "STRING"):
             raise Skip("table source key")
         pk_type = key_cols[0]["type"]
+
+    def col_value(name, rk, val):
+        c = colmap[name]
+        if not c["key"]:
+            return None if val is None else val.get(name)
+        if len(key_cols) == 1:
+            return None if rk is None else conv(c["type"], rk)
+        if not isinstance(rk, dict):
+            return None
+        v = {k.upper(): x for k, x in rk.items()}.get(name)
+        return None if v is None else conv(c["type"], v)
+
+    def composite_key(vals):
+        if any(v is None for v in vals):
+            return None
+        return sink_ref.encode_key(src["key_format"], list(zip(gcols, gtypes)), vals).decode()
     vmap = {c["name"]: c for c in value_cols}
 
     aggs, outcols = [], []
@@ -304,8 +336,8 @@ def extract_agg(path, test, fmt_tag):
         am = re.match(r"(?is)^(.*?)\s+AS\s+`?(\w+)`?$", item)
         expr, alias = (am.group(1), am.group(2).upper()) if am else (item, None)
         e = expr.strip()
-        if unq(e) == gcol and re.match(r"^[\w`.]+$", e):
-            continue  # the group-by column: becomes the key
+        if unq(e) in gcols and re.match(r"^[\w`.]+$", e):
+            continue  # a group-by column: part of the key
         if re.match(r"(?i)^[\w`]*\.?WINDOWSTART$", e):
             outcols.append({"src": "WS", "name": alias})
             continue
@@ -364,12 +396,12 @@ def extract_agg(path, test, fmt_tag):
         ts = rec.get("timestamp", 0)
         val = parse_value(src["format"], rec.get("value"), value_cols)
         rk = rec.get("key")
-        if by_key:
-            kval = None if rk is None else conv(gtype, rk)
-        else:
-            kval = None if val is None else val.get(gcol)
+        gvals = [col_value(g, rk, val) for g in gcols]
+        kval = composite_key(gvals) if composite else gvals[0]
         raw_records.append({"key": rk, "value": rec.get("value"), "ts": ts})
         row = {"key": kval, "row_valid": val is not None, "ts": ts, "cols": []}
+        if composite:
+            row["gvals"] = gvals
         if table_source:
             row["src_key"] = None if rk is None else conv(pk_type, rk)
         for c in used:
@@ -389,7 +421,13 @@ def extract_agg(path, test, fmt_tag):
         okey = o.get("key")
         if okey is None:
             raise Skip("null output key")
-        okey = conv(gtype, okey)
+        if composite:
+            if not isinstance(okey, dict):
+                raise Skip("composite_output key")
+            ok = {k.upper(): x for k, x in okey.items()}
+            okey = composite_key([None if ok.get(g) is None else conv(t, ok.get(g)) for g, t in zip(gcols, gtypes)])
+        else:
+            okey = conv(gtype, okey)
         w = o.get("window")
         if window and not w:
             raise Skip("missing window")
@@ -398,7 +436,8 @@ def extract_agg(path, test, fmt_tag):
         v = o.get("value")
         if v is None:
             state[(okey, ws)] = None
-            outputs.append({"key": okey, "ws": ws, "we": we, "rowtime": o.get("timestamp"), "tombstone": True})
+            outputs.append({"key": okey, "ws": ws, "we": we, "rowtime": o.get("timestamp"), "tombstone": True,
+                            "raw_key": o.get("key"), "raw_value": None})
             continue
         if isinstance(v, str):
             parts = v.split(",")
@@ -436,7 +475,7 @@ def extract_agg(path, test, fmt_tag):
                 present[oc["agg"]] = True
         state[(okey, ws)] = {"key": okey, "ws": ws, "we": we, "rowtime": o.get("timestamp"),
                              "values": aggv, "present": present}
-        outputs.append(dict(state[(okey, ws)], tombstone=False))
+        outputs.append(dict(state[(okey, ws)], tombstone=False, raw_key=o.get("key"), raw_value=v))
     expected = [v for v in state.values() if v is not None]
     expected.sort(key=lambda e: ((e["key"].encode() if isinstance(e["key"], str) else e["key"]), e["ws"]))
 
@@ -449,11 +488,20 @@ def extract_agg(path, test, fmt_tag):
                "fields": [{"name": c["name"], "type": c["type"],
                            "out": used.index(c["name"]) if c["name"] in used else -1} for c in value_cols],
                "records": raw_records}
+    # the sink topic's serializers (the CTAS inherits the source's formats): key columns, value
+    # columns in output order with where each comes from; byte-level parity covers the formats the
+    # device serializer writes
+    sink = None
+    if src["format"] in SINK_FORMATS and src["key_format"] in SINK_FORMATS and not table_source:
+        sink = {"key_format": src["key_format"], "value_format": src["format"],
+                "key_cols": [[g, t] for g, t in zip(gcols, gtypes)],
+                "value_cols": [{"name": oc["name"], "src": oc["src"], "agg": oc.get("agg")} for oc in outcols]}
     return {
         "name": test["name"] + (" [%s]" % fmt_tag if fmt_tag else ""),
         "source": "%s:%d" % (os.path.basename(path), find_line(path, test["name"])),
         "null_as_default": src["format"] in PROTO_FORMATS,
         "raw": raw,
+        "sink": sink,
         "desc": {
             "window_kind": window["kind"] if window else "NONE",
             "size_ms": window["size_ms"] if window else 0,
@@ -461,7 +509,9 @@ def extract_agg(path, test, fmt_tag):
             "grace_ms": window["grace_ms"] if window else -1,
             "retention_ms": window["retention_ms"] if window else -1,
             "emit": emit,
-            "key_type": "UTF8" if gtype == "STRING" else "INT64",
+            "key_type": "UTF8" if composite or gtype == "STRING" else "INT64",
+            "group": {"key_format": src["key_format"], "cols": [[g, t] for g, t in zip(gcols, gtypes)]}
+            if composite else None,
             "col_types": col_types,
             "aggs": spec_aggs,
             "having": having,
