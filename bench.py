@@ -82,6 +82,11 @@ def parse():
     ap.add_argument("--slice", type=int, default=1 << 27, help="hopping_double: records per micro-batch push")
     ap.add_argument("--users", type=int, default=100_000_000, help="clickstream_join: table rows")
     ap.add_argument("--no-extras", action="store_true", help="skip the PCIe-inclusive and pull-query side numbers")
+    ap.add_argument("--exchange", choices=["rccl", "gloo"], default="rccl",
+                    help="repartition_sum at N > 1: RCCL all-to-all over xGMI (production), or the same two "
+                         "collective steps over a gloo process group through host memory (rehearsal)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="every rank on cuda:0 (with --exchange gloo: an N-rank rehearsal on a 1-GPU box)")
     return ap.parse_args()
 
 
@@ -134,11 +139,19 @@ def sized_run(run, m0, target_s, m_max):
     return m0, dt
 
 
-def cpu_baseline_block(single, par, P, unit, sample):
-    return {"value": par[0] / par[1], "unit": unit, "cores": P, "kind": "port", "sample": sample % (par[0], P),
-            "single_thread": {"value": single[0] / single[1], "cores": 1, "records": single[0],
-                              "seconds": single[1]},
-            "parallel_seconds": par[1], "cpu": cpu_info(), "label": CPU_LABEL}
+KS_THREADS = 4  # ksqlDB's default Kafka Streams threads per query (C/util/KsqlConstants.java:42)
+
+
+def cpu_baseline_block(single, par, P, unit, sample, ks=None):
+    """single / ks / par: (records, seconds) at 1, KS_THREADS and P threads.  P is this job's CPU
+    share (16 on the GPU box, whose nproc counts the whole host)."""
+    b = {"value": par[0] / par[1], "unit": unit, "cores": P, "kind": "port", "sample": sample % (par[0], P),
+         "single_thread": {"value": single[0] / single[1], "cores": 1, "records": single[0],
+                           "seconds": single[1]},
+         "parallel_seconds": par[1], "cpu": cpu_info(), "label": CPU_LABEL}
+    if ks is not None:
+        b["ksql_default_threads"] = {"value": ks[0] / ks[1], "cores": KS_THREADS, "records": ks[0], "seconds": ks[1]}
+    return b
 
 
 def load_traffic(path, config, n, variant=""):
@@ -167,7 +180,8 @@ def max_over_ranks(elapsed, world):
     import torch
     import torch.distributed as dist
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dev = "cpu" if dist.get_backend() == "gloo" else "cuda"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed
@@ -427,8 +441,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    if args.one_device:
+        if args.exchange != "gloo":
+            raise SystemExit("bench.py: --one-device needs --exchange gloo (RCCL refuses two ranks on one GPU)")
+        local = 0
     torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 and args.exchange == "gloo":
+        dist.init_process_group("gloo")
+    elif world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     lib = abi.load_product()
     legs = {"possible_fraud": bench_possible_fraud, "hourly_metrics": bench_hourly_metrics,
@@ -559,8 +579,9 @@ def cpu_baseline_agg(gen, utf8, kw, target_s, m_max, sample):
         return dt
 
     single = sized_run(lambda m: run(m, 1), 500_000, target_s, m_max)
+    ks = sized_run(lambda m: run(m, KS_THREADS), 1_000_000, target_s, m_max)
     par = sized_run(lambda m: run(m, P), 1_000_000, target_s, m_max)
-    return cpu_baseline_block(single, par, P, "records/s", sample)
+    return cpu_baseline_block(single, par, P, "records/s", sample, ks)
 
 
 # ------------------------------------------------------------------ C1 hourly_metrics
@@ -628,12 +649,12 @@ def cpu_baseline_hourly(n, target_s):
         return time.perf_counter() - t0
 
     out = []
-    for shards in (1, P):
+    for shards in (1, P, KS_THREADS):
         dt = run(shards, 1)
         reps = max(1, int(target_s / max(dt, 1e-3)))
         out.append((n * reps, run(shards, reps)))
     return cpu_baseline_block(out[0], out[1], P, "records/s",
-                              "%d records (the 1M-record hourly_metrics run, repeated), %d key-hash shards")
+                              "%d records (the 1M-record hourly_metrics run, repeated), %d key-hash shards", out[2])
 
 
 # ------------------------------------------------------------------ C3 hopping_double
@@ -826,10 +847,11 @@ def cpu_baseline_join(users, target_s):
         return time.perf_counter() - t0
 
     single = sized_run(lambda m: run(m, 1), 1_000_000, target_s, 50_000_000)
+    ks = sized_run(lambda m: run(m, KS_THREADS), 2_000_000, target_s, 100_000_000)
     par = sized_run(lambda m: run(m, P), 2_000_000, target_s, 100_000_000)
     t.close()
     return cpu_baseline_block(single, par, P, "records/s",
-                              "%%d clicks probed against a %d-row users table, %%d threads" % U)
+                              "%%d clicks probed against a %d-row users table, %%d threads" % U, ks)
 
 
 # ------------------------------------------------------------------ C5 repartition_sum
@@ -851,8 +873,11 @@ def bench_repartition(args, lib, rank, world, local):
     eid, ts, region, amount = synth.repartition_sum(0, n, n, xp="torch", device="cuda", rank=rank, world=world)
     torch.cuda.synchronize()
     src = abi.DeviceBatch(ts, cols=[region, amount])
+    from ksql_amd.repartition import GlooExchange
     comm = None
-    if world > 1:
+    if world > 1 and args.exchange == "gloo":
+        comm = GlooExchange()
+    elif world > 1:
         obj = [abi.comm_unique_id(lib) if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         comm = abi.Comm(lib, world, rank, obj[0], local)
@@ -896,7 +921,7 @@ def bench_repartition(args, lib, rank, world, local):
     h.close()
     rp.close()
     if comm is not None:
-        comm.close()
+        getattr(comm, "close", lambda: None)()
     if rank != 0:
         return
     ms_step = elapsed * 1000.0 / args.steps
@@ -912,7 +937,8 @@ def bench_repartition(args, lib, rank, world, local):
          world * n * args.steps / elapsed, world, args, ms_step, "int64",
          "synthetic (splitmix64, ksql_amd/synth.py repartition_sum), device-resident columnar batch",
          {"workload": "repartition_sum", "records_per_gpu": n, "regions": 1_000_000, "window": "TUMBLING 1 MINUTE",
-          "parallelism": "repartition all-to-all x%d" % world, "rows_received_rank0": m, "groups_rank0": int(rows)},
+          "parallelism": "repartition all-to-all x%d" % world, "exchange": args.exchange if world > 1 else None,
+          "rows_received_rank0": m, "groups_rank0": int(rows)},
          roof, cpu)
 
 
@@ -951,10 +977,11 @@ def cpu_baseline_repartition(n_total, target_s):
         return dt
 
     single = sized_run(lambda m: run(m, 1), 1_000_000, target_s, 40_000_000)
+    ks = sized_run(lambda m: run(m, KS_THREADS), 2_000_000, target_s, 80_000_000)
     par = sized_run(lambda m: run(m, P), 2_000_000, target_s, 80_000_000)
     return cpu_baseline_block(single, par, P, "records/s",
                               "first %%d of rank 0's %d repartition_sum records: partitioner + aggregate, %%d threads"
-                              % n_total)
+                              % n_total, ks)
 
 
 if __name__ == "__main__":

@@ -82,3 +82,33 @@ def test_result_types():
         out.append(t.value)
     assert out == [1, 0, 2, 2, 1]
     assert abi.result_types(desc) == out
+
+
+def test_comm_argument_validation_cpu():
+    """khip_comm_* reject bad arguments before touching a device or RCCL (no GPU needed)."""
+    lib = abi.load_product()
+    idb = (C.c_uint8 * abi.COMM_ID_BYTES)()
+    h = C.c_void_p()
+    assert lib.comm_init(0, 0, idb, 0, C.byref(h)) == -1      # no ranks
+    assert lib.comm_init(2, 2, idb, 0, C.byref(h)) == -1      # rank outside the world
+    assert lib.comm_init(2, -1, idb, 0, C.byref(h)) == -1
+    assert lib.comm_init(2, 0, None, 0, C.byref(h)) == -1     # no unique id
+    assert lib.comm_init(2, 0, idb, 0, None) == -1
+    assert b"communicator" in lib.dll.khip_last_error()
+    sc = (abi.i64 * 2)(1, 2)
+    assert lib.comm_exchange_counts(None, sc, sc) == -1
+    assert lib.comm_alltoall(None, None, sc, None, 0, sc, 3) == -1
+    assert lib.comm_destroy(None) == 0
+
+
+def test_sink_argument_validation_cpu():
+    """khip_sink_create rejects descriptors the reference would not build (no GPU needed)."""
+    lib = abi.load_product()
+    with pytest.raises(abi.KsqlHipError):
+        abi.SinkHandle(lib, "KAFKA", [("A", "INT32"), ("B", "INT32")], "JSON", [])  # KAFKA key: one column
+    with pytest.raises(abi.KsqlHipError):
+        abi.SinkHandle(lib, "JSON", [("A", "INT32")], "KAFKA", [("X", "INT64", 0), ("Y", "INT64", 1)])
+    with pytest.raises(abi.KsqlHipError):
+        abi.SinkHandle(lib, "AVRO", [("A", "INT32")], "JSON", [])
+    with pytest.raises(abi.KsqlHipError):
+        abi.SinkHandle(lib, "JSON", [("A", "INT32")], "JSON", [("WS", "DOUBLE", "WS")])  # WINDOWSTART is BIGINT

@@ -304,3 +304,42 @@ def test_two_process_repartition_gloo(orc):
         np.testing.assert_array_equal(sm, exp["values"][0])
         np.testing.assert_array_equal(cn, exp["values"][1])
         np.testing.assert_array_equal(rt, exp["rowtime"])
+
+
+def test_rccl_error_paths_single_rank(prod):
+    """khip_comm_* argument validation and the capacity check that runs before any group opens
+    (a capacity error there must not leave a half-open group: the next call still works)."""
+    uid = abi.comm_unique_id(prod)
+    c = abi.Comm(prod, 1, 0, uid, 0)
+    sc = (abi.i64 * 1)(5)
+    rc = (abi.i64 * 1)(5)
+    recv = torch.empty((4, 3), dtype=torch.int64, device="cuda")
+    send = torch.arange(15, dtype=torch.int64, device="cuda").reshape(5, 3)
+    st = prod.comm_alltoall(c.h, send.data_ptr(), sc, recv.data_ptr(), 4, rc, 3)
+    assert st == abi.KHIP_E_BUFFER, st
+    assert prod.comm_alltoall(None, send.data_ptr(), sc, recv.data_ptr(), 4, rc, 3) == -1
+    assert prod.comm_alltoall(c.h, send.data_ptr(), sc, recv.data_ptr(), 4, rc, 0) == -1
+    assert prod.comm_exchange_counts(c.h, None, rc) == -1
+    out, counts = c.alltoall(send, [5], 3)  # the communicator is still usable
+    assert counts == [5] and torch.equal(out[:5], send)
+    c.close()
+
+
+def test_bench_repartition_two_ranks_one_gpu_gloo():
+    """bench.py's own repartition step loop at N = 2 (both ranks on this GPU, the exchange over a
+    gloo group): the multi-rank branches of the leg, the barrier and the max-over-ranks timing."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--config", "repartition_sum", "--gpus", "2",
+                        "--exchange", "gloo", "--one-device", "--records", "2000000", "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline"], cwd=repo, env=env, capture_output=True, text=True, timeout=220)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["exchange"] == "gloo"
+    assert d["value"] > 0 and d["config"]["rows_received_rank0"] > 0
