@@ -68,7 +68,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", choices=["possible_fraud", "hourly_metrics", "hopping_double", "clickstream_join",
-                                         "repartition_sum", "serde_json", "table_agg", "session"],
+                                         "repartition_sum", "serde_json", "serde_avro", "sink_json", "table_agg",
+                                         "session"],
                     default="possible_fraud",
                     help="possible_fraud = BASELINE configs[1] (the headline); hourly_metrics = configs[0]; "
                          "hopping_double = configs[2]; clickstream_join = configs[3]; repartition_sum = configs[4]")
@@ -81,6 +82,9 @@ def parse():
     ap.add_argument("--engine", choices=["part", "atomic"], default="part")
     ap.add_argument("--slice", type=int, default=1 << 27, help="hopping_double: records per micro-batch push")
     ap.add_argument("--users", type=int, default=100_000_000, help="clickstream_join: table rows")
+    ap.add_argument("--sparse-ids", action="store_true",
+                    help="clickstream_join: user ids spread over 2^40 (a bijection of 1..U), so the dense "
+                         "direct-map index is ineligible and the hash-probe kernel runs")
     ap.add_argument("--no-extras", action="store_true", help="skip the PCIe-inclusive and pull-query side numbers")
     ap.add_argument("--exchange", choices=["rccl", "gloo"], default="rccl",
                     help="repartition_sum at N > 1: RCCL all-to-all over xGMI (production), or the same two "
@@ -309,6 +313,134 @@ def bench_serde_json(args, lib, rank, world, local):
           "value_bytes": w, "errors": int(nerr), "parallelism": "records x%d" % world}, roof, cpu)
 
 
+def bench_serde_avro(args, lib, rank, world, local):
+    """§8(f)1: the same records in the reference's example-data format — KAFKA BIGINT key and an
+    AVRO value in the Confluent wire format (magic byte 0, 4-byte schema id, the Avro binary record
+    {AMOUNT: long} as a zig-zag varint) — into device columns (khip_serde_decode, KHIP_FMT_AVRO)."""
+    import torch
+    from ksql_amd import abi, synth
+    n = args.records or 100_000_000
+    card, ts = synth.possible_fraud(0, n, n, xp="torch", device="cuda", rank=rank, world=world, keys=args.keys)
+    kb = torch.stack([((card >> (8 * (7 - i))) & 0xFF).to(torch.uint8) for i in range(8)], dim=1).reshape(-1)
+    koff = torch.arange(0, 8 * (n + 1), 8, dtype=torch.int64, device="cuda")
+    amount = 1_000_000_000 + card % 999_999_937  # zig-zag 2e9..4e9: always 5 varint bytes
+    zz = amount * 2
+    w = 5 + 5
+    vb = torch.zeros((n, w), dtype=torch.uint8, device="cuda")
+    vb[:, 4] = 1  # schema id 1, big-endian
+    for i in range(5):
+        vb[:, 5 + i] = (((zz >> (7 * i)) & 0x7F) | (0x80 if i < 4 else 0)).to(torch.uint8)
+    vb = vb.reshape(-1)
+    voff = torch.arange(0, w * (n + 1), w, dtype=torch.int64, device="cuda")
+    sd = abi.SerdeHandle(lib, "AVRO", [("AMOUNT", "INT64", 0)], key_type="INT64", key_format="KAFKA", device=local,
+                         avro_schema=[("AMOUNT", "long", 0)], avro_schema_id=1)
+    torch.cuda.synchronize()
+
+    def step():
+        d, nerr = sd.decode_device(ts, koff, kb, voff, vb)
+        return nerr
+
+    for _ in range(max(args.warmup, 1)):
+        nerr = step()
+    assert nerr == 0, nerr
+    nerr, elapsed = timed_loop(step, args.steps, world)
+    sd.close()
+    if rank != 0:
+        return
+    ms_step = elapsed * 1000.0 / args.steps
+    bpr = 8 + w + 2 * 8 + 8 + 8  # key bytes + value bytes + 2 offsets read; key + value columns written
+    roof = roofline(bpr * n, ms_step, None, None, load_traffic(args.traffic_json, "serde_avro", n), bpr,
+                    kernel="khip_serde_decode (k_serde_decode, AVRO)")
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        m = 200_000
+        keys = [int(x).to_bytes(8, "big") for x in card[:m].cpu().numpy()]
+        vals = [bytes(v) for v in vb[: m * w].cpu().numpy().reshape(m, w)]
+
+        def avro_long(b):  # the wire header, then BinaryDecoder.readLong
+            assert b[0] == 0 and int.from_bytes(b[1:5], "big") == 1
+            v, sh, j = 0, 0, 5
+            while True:
+                x = b[j]
+                v |= (x & 0x7F) << sh
+                j += 1
+                sh += 7
+                if not x & 0x80:
+                    break
+            return (v >> 1) ^ -(v & 1)
+        t0 = time.perf_counter()
+        out = [(int.from_bytes(k, "big", signed=True), avro_long(v)) for k, v in zip(keys, vals)]
+        dt = time.perf_counter() - t0
+        assert len(out) == m and out[0][1] == int(amount[0])
+        cpu = {"value": m / dt, "unit": "records/s", "cores": 1, "kind": "port",
+               "sample": "%d of the records, CPython per-record wire header + zig-zag varint" % m,
+               "cpu": cpu_info(), "label": "CPU restatement of the KAFKA / AVRO deserializers, not the JVM reference"}
+    line("records/sec, Kafka record bytes (KAFKA BIGINT key, AVRO value) -> device columns",
+         world * n * args.steps / elapsed, world, args, ms_step, "u8",
+         "synthetic (C2's records serialized on the device, Confluent wire format), device-resident raw batch",
+         {"workload": "serde_avro", "records_per_gpu": n, "key": "KAFKA BIGINT", "value": "AVRO {AMOUNT: long}",
+          "value_bytes": w, "errors": int(nerr), "parallelism": "records x%d" % world}, roof, cpu)
+
+
+def bench_sink_json(args, lib, rank, world, local):
+    """§8(f)2: C2's changelog as sink records — one row per (card number, 5 s window): a
+    TimeWindowed KAFKA BIGINT key (8-byte key + 8-byte window start) and a JSON value
+    {"KSQL_COL_0":<count>} (khip_sink_encode, device rows → device record bytes).  One step =
+    encode --records rows (default 22M, C2's group count)."""
+    import torch
+    from ksql_amd import abi, synth
+    n = args.records or 22_000_000
+    be = synth.backend("torch")
+    h0 = synth._stream(be, 8, 0, n, "cuda")
+    key = (h0 % 10_000_000).to(torch.int64)
+    ws = ((h0 >> 24) % 3).to(torch.int64) * 5000
+    we = ws + 5000
+    cnt = ((h0 >> 40) % 30 + 1).to(torch.int64)
+    nul = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    s = abi.SinkHandle(lib, "KAFKA", [("CARD_NUMBER", "INT64")], "JSON", [("KSQL_COL_0", "INT64", 0)],
+                       window_kind="TUMBLING", device=local)
+    rows = abi.SinkRows()
+    rows.n_rows, rows.mem, rows.key_serialized = n, abi.MEM_DEVICE, 0
+    rows.key_i64, rows.window_start, rows.window_end = key.data_ptr(), ws.data_ptr(), we.data_ptr()
+    cd = (abi.C.c_void_p * 1)(cnt.data_ptr())
+    cn = (abi.C.c_void_p * 1)(nul.data_ptr())
+    rows.col_data, rows.col_null = cd, cn
+    kcap, vcap = 16 * n, 40 * n
+    koff = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    voff = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    kbytes = torch.empty(kcap, dtype=torch.uint8, device="cuda")
+    vbytes = torch.empty(vcap, dtype=torch.uint8, device="cuda")
+    vnull = torch.empty(n, dtype=torch.uint8, device="cuda")
+    out = abi.SinkOut()
+    out.mem, out.key_capacity, out.value_capacity = abi.MEM_DEVICE, kcap, vcap
+    out.key_offsets, out.key_bytes = koff.data_ptr(), kbytes.data_ptr()
+    out.value_offsets, out.value_bytes, out.value_null = voff.data_ptr(), vbytes.data_ptr(), vnull.data_ptr()
+    torch.cuda.synchronize()
+
+    def step():
+        lib.check(lib.sink_encode(s.h, abi.C.byref(rows), abi.C.byref(out)), "sink_encode")
+        return out.key_len, out.value_len
+
+    for _ in range(max(args.warmup, 1)):
+        kl, vl = step()
+    assert kl == 16 * n, kl
+    (kl, vl), elapsed = timed_loop(step, args.steps, world)
+    s.close()
+    if rank != 0:
+        return
+    ms_step = elapsed * 1000.0 / args.steps
+    # rows read (key, ws, we, count, null flag) + record bytes and offsets written
+    bpr = 8 + 8 + 8 + 8 + 1 + 16 + vl / n + 2 * 8 + 1
+    roof = roofline(bpr * n, ms_step, None, None, load_traffic(args.traffic_json, "sink_json", n), bpr,
+                    kernel="khip_sink_encode (k_sink_measure + scans + k_sink_write)")
+    line("records/sec, changelog rows -> sink records (TimeWindowed KAFKA BIGINT key, JSON value)",
+         world * n * args.steps / elapsed, world, args, ms_step, "u8",
+         "synthetic C2-shaped changelog rows (splitmix64), device-resident columns",
+         {"workload": "sink_json", "rows_per_gpu": n, "key": "KAFKA BIGINT + 8-byte window start",
+          "value": "JSON {\"KSQL_COL_0\": BIGINT}", "value_bytes_per_row": vl / n,
+          "parallelism": "rows x%d" % world}, roof, None)
+
+
 def bench_table_agg(args, lib, rank, world, local):
     """§8(f)4: CREATE TABLE by_region AS SELECT region, COUNT(*), SUM(amount) FROM users GROUP BY
     region — a source table of 1e7 users whose changelog (1e8 rows, 5 % tombstones) moves users
@@ -453,7 +585,8 @@ def main():
     lib = abi.load_product()
     legs = {"possible_fraud": bench_possible_fraud, "hourly_metrics": bench_hourly_metrics,
             "hopping_double": bench_hopping_double, "clickstream_join": bench_join,
-            "repartition_sum": bench_repartition, "serde_json": bench_serde_json, "table_agg": bench_table_agg,
+            "repartition_sum": bench_repartition, "serde_json": bench_serde_json, "serde_avro": bench_serde_avro,
+            "sink_json": bench_sink_json, "table_agg": bench_table_agg,
             "session": bench_session}
     legs[args.config](args, lib, rank, world, local)
     if world > 1:
@@ -774,6 +907,8 @@ def bench_join(args, lib, rank, world, local):
     n = args.records or 1_000_000_000
     U = args.users
     uid, level = synth.users_table(0, U, xp="torch", device="cuda")
+    if args.sparse_ids:
+        uid = synth.sparse_ids(uid)
     level = level.to(torch.int32)
     t = abi.TableHandle(lib, ["INT32"], device=local, capacity_hint=U)
     tb = abi.DeviceBatch(torch.zeros(U, dtype=torch.int64, device="cuda"), keys=uid, cols=[level])
@@ -784,6 +919,8 @@ def bench_join(args, lib, rank, world, local):
     build_s = time.perf_counter() - t0
     del tb, uid, level
     cu, cts = synth.clicks(0, n, U, xp="torch", device="cuda", seed_clicks=5 + 1000 * rank)
+    if args.sparse_ids:
+        cu = synth.sparse_ids(cu)
     batch = abi.DeviceBatch(cts, keys=cu)
     nb = (n + 7) // 8 + 8
     emit = torch.empty(nb, dtype=torch.uint8, device="cuda")
@@ -811,17 +948,18 @@ def bench_join(args, lib, rank, world, local):
                            "random_gather_rows_per_s": random_gather_rows_per_s(info["table_bytes"])})
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline_join(U, args.cpu_seconds)
+        cpu = cpu_baseline_join(U, args.cpu_seconds, args.sparse_ids)
     line("stream records/sec, stream-table LEFT JOIN (clickstream x users WHERE level = 'Platinum')",
          world * n * args.steps / elapsed, world, args, ms_step, "int64",
          "synthetic (splitmix64, ksql_amd/synth.py users_table/clicks), device-resident columnar batch",
-         {"workload": "clickstream_join", "table_rows": U, "clicks_per_gpu": n, "table_build_s": build_s,
+         {"workload": "clickstream_join", "user_ids": "sparse over 2^40 (hash probe)" if args.sparse_ids else
+          "1..U (dense direct-map index)", "table_rows": U, "clicks_per_gpu": n, "table_build_s": build_s,
           "table_build_rows_per_s": U / build_s, "emitted_rows_per_gpu": int(rows),
           "parallelism": "replicated table x%d" % world},
          roof, cpu)
 
 
-def cpu_baseline_join(users, target_s):
+def cpu_baseline_join(users, target_s, sparse=False):
     """Oracle stream-table LEFT JOIN WHERE level = 'Platinum': a users table of min(users, 1e7)
     rows built first (untimed), then clicks over the same 1.1x id span probed against it —
     1 thread, and P threads over P chunks of the stream (the table is read-only)."""
@@ -830,12 +968,16 @@ def cpu_baseline_join(users, target_s):
     P = cpu_threads()
     U = min(users, 10_000_000)
     uid, level = synth.users_table(0, U)
+    if sparse:
+        uid = synth.sparse_ids(uid)
     t = abi.TableHandle(orc, ["INT32"], capacity_hint=U)
     t.upsert(abi.HostBatch(np.zeros(U, np.int64), keys=uid, cols=[level.astype(np.int32)]))
     where = {"col": 0, "op": "EQ", "i64": synth.LEVELS.index("Platinum")}
 
     def run(m, threads):
         cu, cts = synth.clicks(0, m, U, seed_clicks=5)
+        if sparse:
+            cu = synth.sparse_ids(cu)
         bounds = np.linspace(0, m, threads + 1).astype(np.int64)
         bs = [abi.HostBatch(cts[bounds[k]:bounds[k + 1]], keys=cu[bounds[k]:bounds[k + 1]]) for k in range(threads)]
         th = [threading.Thread(target=t.probe, args=(bs[k], "LEFT", where)) for k in range(threads)]

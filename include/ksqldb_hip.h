@@ -265,7 +265,11 @@ khip_status khip_agg_get(khip_agg* agg, const khip_pull* q, const khip_having* h
 /* ---- Emission (the aggregate's output topic: the table's changelog).
  * One push = one commit of Kafka Streams' record cache (C/util/KsqlConstants.java:40-41): the
  * rows a push emits are deduplicated per (key, window), carry their value after the push, and
- * are sorted by (key, window start).  Pushing one record at a time reproduces the reference's
+ * are sorted by (key, window start).  SESSION windows are the exception: a record that lands in an
+ * existing session [s, e] replaces it, and the push emits the tombstone of the old session and the
+ * rewritten session as two rows — even when the rewritten one has the same (s, e) — delete first
+ * (Kafka Streams' session store removes the merged sessions and puts the new one; the reference's
+ * cache-off output has the same two records).  Pushing one record at a time reproduces the reference's
  * cache-off output sequence exactly (QTT, tests/test_gpu_emit.py).
  *   EMIT CHANGES (needs KHIP_FLAG_CHANGELOG): every (key, window) the push updated; with the
  *     descriptor's HAVING (S/TableFilterBuilder.java:63-75) a row that no longer passes but did

@@ -312,6 +312,7 @@ struct PartState {
   DevBuf buf[2];          // region storage: P x cmax rows x sw words, double buffered
   DevBuf sel, cnt, newcnt, fail;  // per partition: buffer select, rows, rows being written, flags
   DevBuf hist, tilemax, tilemin, tileprefix, tpart, scan_tmp;
+  DevBuf tilekr;  // per tile: largest key, ~smallest key (R8 records)
   // scattered records, AoS, rw u64 words each: key, ts (-1 = no window applied),
   // [meta = jlo | validity << 16, if meta_word = 2], [the referenced value columns], pad to even
   DevBuf srec;

@@ -136,11 +136,13 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_hist(const int64_t* __restr
                                                           int log2P, int pad, int64_t nT, uint32_t* __restrict__ hist,
                                                           int64_t* __restrict__ tilemax, int64_t* __restrict__ tilemin,
                                                           int64_t* __restrict__ tpart, int fbits,
-                                                          uint32_t* __restrict__ hcoarse) {
+                                                          uint32_t* __restrict__ hcoarse,
+                                                          int64_t* __restrict__ tilekr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint32_t* lh = (uint32_t*)smem;
   __shared__ int64_t lmax[PT_THREADS / 64];
   __shared__ int64_t lmin[PT_THREADS / 64];
+  __shared__ int64_t lkr[2][PT_THREADS / 64];
   __shared__ unsigned long long lc[4];
   const int P = 1 << log2P;
   const int64_t t = tile_of(blockIdx.x, nT);
@@ -148,6 +150,7 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_hist(const int64_t* __restr
   if (threadIdx.x < 4) lc[threadIdx.x] = 0;
   __syncthreads();
   int64_t m = -1, mn = INT64_MAX, c_acc = 0, c_nk = 0, c_nr = 0, c_bt = 0;
+  int64_t kmx = INT64_MIN, kmxn = INT64_MIN;  // accepted keys: max of key and of ~key (= ~min)
   const int64_t base = t * tile;
   const int64_t end = base + tile < n ? base + tile : n;
   for (int64_t i0 = base + threadIdx.x; i0 < end; i0 += 4 * PT_THREADS) {
@@ -170,6 +173,8 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_hist(const int64_t* __restr
       c_acc++;
       m = x[u] > m ? x[u] : m;
       mn = x[u] < mn ? x[u] : mn;
+      kmx = k[u] > kmx ? k[u] : kmx;
+      kmxn = ~k[u] > kmxn ? ~k[u] : kmxn;
       atomicAdd(&lh[part_of(k[u], log2P)], 1u);
     }
   }
@@ -177,6 +182,17 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_hist(const int64_t* __restr
   block_incl_max(m, lmax, &tot);
   int64_t totmin;
   block_incl_max(-mn, lmin, &totmin);  // min via max of negation (mn >= 0 or INT64_MAX)
+  if (tilekr) {  // the tile's key range (R8 records: keys relative to the push's smallest)
+    for (int off = 32; off > 0; off >>= 1) {
+      const int64_t a = __shfl_xor(kmx, off, 64), b = __shfl_xor(kmxn, off, 64);
+      kmx = a > kmx ? a : kmx;
+      kmxn = b > kmxn ? b : kmxn;
+    }
+    if ((threadIdx.x & 63) == 0) {
+      lkr[0][threadIdx.x >> 6] = kmx;
+      lkr[1][threadIdx.x >> 6] = kmxn;
+    }
+  }
   c_acc = wave_sum(c_acc); c_nk = wave_sum(c_nk); c_nr = wave_sum(c_nr); c_bt = wave_sum(c_bt);
   if ((threadIdx.x & 63) == 0) {
     if (c_acc) atomicAdd(&lc[0], (unsigned long long)c_acc);
@@ -199,6 +215,15 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_hist(const int64_t* __restr
   if (threadIdx.x == 0) {
     tilemax[t] = tot;
     tilemin[t] = -totmin;
+    if (tilekr) {
+      int64_t a = INT64_MIN, b = INT64_MIN;
+      for (int w = 0; w < PT_THREADS / 64; w++) {
+        a = lkr[0][w] > a ? lkr[0][w] : a;
+        b = lkr[1][w] > b ? lkr[1][w] : b;
+      }
+      tilekr[2 * t] = a;      // INT64_MIN: no accepted record
+      tilekr[2 * t + 1] = b;  // ~(smallest key)
+    }
     int64_t* tp = tpart + t * T_NPART;
     tp[T_ACCEPTED] = (int64_t)lc[0];
     tp[T_NULL_KEY] = (int64_t)lc[1];
@@ -317,7 +342,8 @@ __device__ __forceinline__ void lds_barrier() {
 // per store instruction), the step's records are ranked per bin (LDS atomics), placed in LDS in
 // bin order, and written back out by consecutive threads: each bin's records of the step leave
 // as one contiguous run (~S / nb records) in whole-line, coalesced stores.
-//   out: 0 = (hk, pay) 16 bytes; 1 = R12 (pay = trel); 2 = R12 in, (hk, ts) 16 bytes out
+//   out: 0 = (hk, pay) 16 bytes; 1 = R12 (pay = trel); 2 = R12 in, (hk, ts) 16 bytes out;
+//        3 = R8 (pay = the 8-byte record)
 struct StageLds {
   uint32_t* cur;    // [nb] next output record of each bin (global index)
   uint32_t* cnt;    // [nb] records of the step per bin
@@ -375,7 +401,9 @@ __device__ __forceinline__ void stage_step(const int64_t (&hk)[U], const int64_t
     const int64_t p = L.sp[j];
     const uint32_t b = stage_bin(h, shift, mask);
     const uint64_t dst = (uint64_t)L.gpos[b] + (j - L.sbase[b]);
-    if (out == 0) {
+    if (out == 3) {  // R8: the payload is the record
+      srec[dst] = (uint64_t)p;
+    } else if (out == 0) {
       *(longlong2*)(srec + dst * 2) = make_longlong2((int64_t)h, p);
     } else if (out == 1) {
       r12_store(srec, dst, h, (uint32_t)p);
@@ -385,6 +413,49 @@ __device__ __forceinline__ void stage_step(const int64_t (&hk)[U], const int64_t
   }
   // the next step's first barrier (after its rank atomics) orders these LDS reads before any
   // rewrite of sbase / gpos / the stage
+}
+
+// stage_step for self-contained 8-byte records (R8): only the record is staged (8 bytes per record
+// instead of 16: a step of U = 8 records per thread fits twice in a CU's LDS, so two workgroups
+// overlap one's barriers with the other's loads); the write-out recomputes each staged record's
+// bin with binof.  L.sp holds U * PT_THREADS records.
+template <int U, class BinOf>
+__device__ __forceinline__ void stage_step8(const int64_t (&rec)[U], const uint32_t (&bin)[U], const bool (&ok)[U],
+                                            int nb, const StageLds& L, uint64_t* __restrict__ srec, BinOf binof) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  uint32_t rank[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) rank[u] = ok[u] ? atomicAdd(&L.cnt[bin[u]], 1u) : 0u;
+  lds_barrier();
+  const uint32_t c = t < nb ? L.cnt[t] : 0u;
+  uint32_t incl = c;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) L.wsum[wave] = (int)incl;
+  lds_barrier();
+  uint32_t before = 0, tot = 0;
+  for (int k = 0; k < PT_THREADS / 64; k++) {
+    before += k < wave ? (uint32_t)L.wsum[k] : 0u;
+    tot += (uint32_t)L.wsum[k];
+  }
+  if (t < nb) {
+    L.sbase[t] = before + incl - c;
+    L.gpos[t] = L.cur[t];
+    L.cur[t] += c;
+    L.cnt[t] = 0u;
+  }
+  lds_barrier();
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    if (ok[u]) L.sp[L.sbase[bin[u]] + rank[u]] = rec[u];
+  lds_barrier();
+  for (uint32_t j = t; j < tot; j += PT_THREADS) {
+    const int64_t p = L.sp[j];
+    const uint32_t b = binof(p);
+    srec[(uint64_t)L.gpos[b] + (j - L.sbase[b])] = (uint64_t)p;
+  }
 }
 
 // LDS carve-up for stage_step: nb bins, S staged records
@@ -407,9 +478,13 @@ __device__ __forceinline__ StageLds stage_carve(char* smem, int nb, int S, int* 
 __device__ __forceinline__ void scatter_one(int64_t key, int64_t x, int64_t jlo, int64_t i, int log2P, uint32_t* cur,
                                             uint64_t* __restrict__ srec, const RecLayout& L, const ColPtrs& cols,
                                             int n_cols, const ColTypes& ctypes, bool applied, bool r12,
-                                            int64_t tbase) {
+                                            int64_t tbase, int r8tb, int64_t kbase) {
   const uint64_t hk = key_hash(key);
   const uint32_t pos = atomicAdd(&cur[part_of_hk(hk, log2P)], 1u);
+  if (r12 && r8tb) {  // R8: (key - kbase) << tb | trel
+    srec[pos] = ((uint64_t)(key - kbase) << r8tb) | (applied ? (uint64_t)(x - tbase + 1) : 0ULL);
+    return;
+  }
   if (r12) {  // narrow layout only
     r12_store(srec, pos, hk, applied ? (uint32_t)(x - tbase + 1) : 0u);
     return;
@@ -446,6 +521,8 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
   __shared__ int wsum[PT_THREADS / 64];
   const bool r12 = r12_ok && wr[4] != 0;  // k_part_merge runs: 12-byte records
   const int64_t tbase = wr[5];
+  const int r8tb = r12 ? (int)wr[7] : 0;    // ... or 8-byte ones (k_part_wrange)
+  const int64_t kbase = wr[6];
   __shared__ int64_t lmax[PT_THREADS / 64];
   __shared__ unsigned long long lc[2];
   const int P = 1 << log2P;
@@ -465,9 +542,15 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
   if (fast && NARROW && stage) {
     // (key hash, ts) records through the LDS stage (stage_step), next step's loads in flight
     constexpr int S = U * PT_THREADS;
-    const StageLds SL = stage_carve(smem, P, S, wsum);
+    // the host sized the stage for S 8-byte records: R8 steps use it whole (stage_step8), the
+    // 12/16-byte records go through it in two half steps of 16-byte (hash, payload) pairs
+    const StageLds SL = stage_carve(smem, P, S / 2, wsum);
+    StageLds SL8 = SL;
+    SL8.sp = (int64_t*)SL.sk;
     for (int p = threadIdx.x; p < P; p += PT_THREADS) SL.cnt[p] = 0u;
     lds_barrier();
+    const int shift = log2P == 0 ? 64 : 64 - log2P;
+    const uint32_t bmask = (uint32_t)(P - 1);
     int64_t x[U], k[U], nxx[U], nxk[U];
     auto load_step = [&](int64_t i0, int64_t (&dx)[U], int64_t (&dk)[U]) {
 #pragma unroll
@@ -496,10 +579,32 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
         } else {
           c_app += ok[u] ? 1 : 0;
         }
+        x[u] = r8tb ? (int64_t)(((uint64_t)(k[u] - kbase) << r8tb) | (uint64_t)(x[u] - tbase + 1))
+                    : (r12 ? x[u] - tbase + 1 : x[u]);
         k[u] = (int64_t)key_hash(k[u]);  // records carry the key hash (key = its inverse)
-        x[u] = r12 ? x[u] - tbase + 1 : x[u];
       }
-      stage_step<U>(k, x, ok, log2P == 0 ? 64 : 64 - log2P, (uint32_t)(P - 1), P, SL, srec, r12 ? 1 : 0, tbase);
+      if (r8tb) {
+        uint32_t bin[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) bin[u] = stage_bin((uint64_t)k[u], shift, bmask);
+        stage_step8<U>(x, bin, ok, P, SL8, srec, [&](int64_t p) {
+          return stage_bin(key_hash(kbase + (int64_t)((uint64_t)p >> r8tb)), shift, bmask);
+        });
+      } else {
+        constexpr int H = U / 2;
+        int64_t kh[H], xh[H];
+        bool okh[H];
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+#pragma unroll
+          for (int u = 0; u < H; u++) {
+            kh[u] = k[half * H + u];
+            xh[u] = x[half * H + u];
+            okh[u] = ok[half * H + u];
+          }
+          stage_step<H>(kh, xh, okh, shift, bmask, P, SL, srec, r12 ? 1 : 0, tbase);
+        }
+      }
 #pragma unroll
       for (int u = 0; u < U; u++) {
         x[u] = nxx[u];
@@ -537,11 +642,15 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
         } else {
           c_app += ok ? 1 : 0;
         }
+        if (r8tb) x[u] = (int64_t)(((uint64_t)(k[u] - kbase) << r8tb) | (uint64_t)(x[u] - tbase + 1));
         k[u] = (int64_t)key_hash(k[u]);  // records carry the key hash (key = its inverse)
         pos[u] = atomicAdd(&cur[part_of_hk((uint64_t)k[u], log2P)], ok ? 1u : 0u);
         if (!ok) pos[u] = 0xFFFFFFFFu;
       }
-      if (r12) {
+      if (r8tb) {
+#pragma unroll
+        for (int u = 0; u < U; u++) srec[pos[u] == 0xFFFFFFFFu ? (uint64_t)dummy : (uint64_t)pos[u]] = (uint64_t)x[u];
+      } else if (r12) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
           const uint64_t dst = pos[u] == 0xFFFFFFFFu ? (uint64_t)dummy : (uint64_t)pos[u];
@@ -584,7 +693,7 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
             windowed ? (int64_t)fast_udiv((uint64_t)x[u], fd) - (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), fd) + 1
                      : 1;
         c_app += nwin;
-        scatter_one(k[u], x[u], 0, i, log2P, cur, srec, L, cols, n_cols, ctypes, true, r12, tbase);
+        scatter_one(k[u], x[u], 0, i, log2P, cur, srec, L, cols, n_cols, ctypes, true, r12, tbase, r8tb, kbase);
       }
     }
   } else {
@@ -609,7 +718,7 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
       }
       c_late += jlo;
       c_app += nwin - jlo;
-      scatter_one(keys[i], x, jlo, i, log2P, cur, srec, L, cols, n_cols, ctypes, nwin > jlo, r12, tbase);
+      scatter_one(keys[i], x, jlo, i, log2P, cur, srec, L, cols, n_cols, ctypes, nwin > jlo, r12, tbase, r8tb, kbase);
     }
   }
   c_app = wave_sum(c_app);
@@ -740,6 +849,54 @@ __device__ __forceinline__ void refine_staged(const uint64_t* __restrict__ srcA,
   }
 }
 
+// R8 records (8 bytes: (key - kbase) << tb | trel) of one block's range → their partitions,
+// through the LDS stage (staged) or straight to each partition's cursor
+template <int U>
+__device__ __forceinline__ void refine_r8(const uint64_t* __restrict__ srcA, const StageLds* SL, uint32_t* cur,
+                                          int64_t lo, int64_t hi, int log2P, int F, uint64_t* __restrict__ srec,
+                                          int tb, int64_t kbase, int64_t dummy) {
+  constexpr int S = U * PT_THREADS;
+  int64_t hk[U], pay[U], npay[U];
+  auto load_step = [&](int64_t i0, int64_t (&dp)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      int64_t i = i0 + (int64_t)u * PT_THREADS;
+      i = i < hi ? i : hi - 1;
+      dp[u] = (int64_t)__builtin_nontemporal_load(srcA + i);
+    }
+  };
+  int64_t s0 = lo;
+  load_step(s0 + threadIdx.x, pay);
+  for (; s0 < hi; s0 += S) {
+    const int64_t i0 = s0 + threadIdx.x;
+    if (s0 + S < hi) load_step(i0 + S, npay);
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      ok[u] = i0 + (int64_t)u * PT_THREADS < hi;
+      hk[u] = (int64_t)key_hash(kbase + (int64_t)((uint64_t)pay[u] >> tb));
+    }
+    if (SL) {
+      uint32_t bin[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) bin[u] = stage_bin((uint64_t)hk[u], 64 - log2P, (uint32_t)(F - 1));
+      StageLds SL8 = *SL;
+      SL8.sp = (int64_t*)SL->sk;
+      stage_step8<U>(pay, bin, ok, F, SL8, srec, [&](int64_t p) {
+        return stage_bin(key_hash(kbase + (int64_t)((uint64_t)p >> tb)), 64 - log2P, (uint32_t)(F - 1));
+      });
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint32_t pos = atomicAdd(&cur[part_of_hk((uint64_t)hk[u], log2P) & (uint32_t)(F - 1)], ok[u] ? 1u : 0u);
+        srec[ok[u] ? (uint64_t)pos : (uint64_t)dummy] = (uint64_t)pay[u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) pay[u] = npay[u];
+  }
+}
+
 // Two-level scatter, pass B: block (bucket b, tile group g) moves the records that pass A
 // (k_part_scatter over the B = P >> fbits buckets) put in bucket b for tiles [t0, t1) — one
 // contiguous range, since pass A lays each bucket out tile-major — to their partitions' final
@@ -762,7 +919,9 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_refine(const uint64_t* __re
   if (RW == 2 && stage) {  // narrow records through the LDS stage
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int wsum[PT_THREADS / 64];
-    const StageLds SL = stage_carve(smem, F, stage * PT_THREADS, wsum);  // stage = records per thread
+    // the stage holds stage * PT_THREADS 8-byte records (stage = records per thread): R8 steps use
+    // it whole, the 12/16-byte records half as many 16-byte pairs per step
+    const StageLds SL = stage_carve(smem, F, stage * PT_THREADS / 2, wsum);
     for (int f = threadIdx.x; f < F; f += PT_THREADS) {
       SL.cur[f] = offs[t0 * P + ((int64_t)b << fbits) + f];
       SL.cnt[f] = 0u;
@@ -772,12 +931,17 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_refine(const uint64_t* __re
     lds_barrier();
     if (hi <= lo) return;
     const bool n12 = r12_ok && wr[4] != 0;
+    if (n12 && wr[7]) {
+      if (stage >= 8) refine_r8<8>(srcA, &SL, nullptr, lo, hi, log2P, F, srec, (int)wr[7], wr[6], dummy);
+      else refine_r8<4>(srcA, &SL, nullptr, lo, hi, log2P, F, srec, (int)wr[7], wr[6], dummy);
+      return;
+    }
     if (stage >= 8) {
-      if (n12) refine_staged<true, 8>(srcA, SL, lo, hi, log2P, F, srec, r12_ok == 2 ? 2 : 1, wr[5]);
-      else refine_staged<false, 8>(srcA, SL, lo, hi, log2P, F, srec, 0, 0);
-    } else {
       if (n12) refine_staged<true, 4>(srcA, SL, lo, hi, log2P, F, srec, r12_ok == 2 ? 2 : 1, wr[5]);
       else refine_staged<false, 4>(srcA, SL, lo, hi, log2P, F, srec, 0, 0);
+    } else {
+      if (n12) refine_staged<true, 2>(srcA, SL, lo, hi, log2P, F, srec, r12_ok == 2 ? 2 : 1, wr[5]);
+      else refine_staged<false, 2>(srcA, SL, lo, hi, log2P, F, srec, 0, 0);
     }
     return;
   }
@@ -786,7 +950,9 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_refine(const uint64_t* __re
   const int64_t lo = offA[t0 * B + b];
   const int64_t hi = t1 < nT ? (int64_t)offA[t1 * B + b] : pbase[(int64_t)(b + 1) << fbits];
   if (hi <= lo) return;
-  if (RW == 2 && r12_ok && wr[4] != 0)
+  if (RW == 2 && r12_ok && wr[4] != 0 && wr[7])
+    refine_r8<8>(srcA, nullptr, cur, lo, hi, log2P, F, srec, (int)wr[7], wr[6], dummy);
+  else if (RW == 2 && r12_ok && wr[4] != 0)
     refine_range<RW, true>(srcA, cur, lo, hi, log2P, F, dummy, srec, mode, r12_ok == 2, wr[5]);
   else
     refine_range<RW, false>(srcA, cur, lo, hi, log2P, F, dummy, srec, mode, false, 0);
@@ -2163,8 +2329,24 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge_c1(
   // the (lo, hi, trel) triple the load returns (a uint3: the load writes the registers the apply
   // reads; splitting it into per-field arrays made the compiler copy — and so wait for — each load
   // right after issuing it)
+  // R8 records (k_part_wrange chose them for this push): one 8-byte word, (key - kbase) << r8tb |
+  // trel; the key hash is recomputed here
+  const int r8tb = (int)wr[7];
+  const int64_t kbase = wr[6];
+  const uint64_t r8mask = r8tb ? (~0ULL >> (64 - r8tb)) : 0ULL;
   uint3 ra[AU], rb[AU];
   auto load = [&](uint3 (&x)[AU], int64_t rbase, int64_t rn, int64_t l0) {
+    if (r8tb) {
+      const uint32_t* base = (const uint32_t*)srec + (uint64_t)rbase * 2;
+#pragma unroll
+      for (int u = 0; u < AU; u++) {
+        const int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
+        const uint32_t* r = base + (uint64_t)(li < rn ? li : (rn > 0 ? rn - 1 : 0)) * 2;
+        x[u].x = __builtin_nontemporal_load(r);
+        x[u].y = __builtin_nontemporal_load(r + 1);
+      }
+      return;
+    }
     const uint32_t* base = (const uint32_t*)srec + (uint64_t)rbase * 3;
 #pragma unroll
     for (int u = 0; u < AU; u++) {
@@ -2234,10 +2416,21 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge_c1(
     }
     C1_T(0);
     // 1. records → delta entries
-    auto apply = [&](const uint3 (&x)[AU], int64_t l0) {
+    auto apply = [&](const uint3 (&xr)[AU], int64_t l0) {
       uint64_t id[AU], old[AU];
       uint32_t e[AU];
       bool pend[AU];
+      uint3 x[AU];
+#pragma unroll
+      for (int u = 0; u < AU; u++) {
+        if (r8tb) {  // (lo, hi) of the key hash, trel
+          const uint64_t v = ((uint64_t)xr[u].y << 32) | xr[u].x;
+          const uint64_t hk = key_hash(kbase + (int64_t)(v >> r8tb));
+          x[u] = make_uint3((uint32_t)hk, (uint32_t)(hk >> 32), (uint32_t)(v & r8mask));
+        } else {
+          x[u] = xr[u];
+        }
+      }
 #pragma unroll
       for (int u = 0; u < AU; u++) {
         const int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
@@ -2459,32 +2652,59 @@ __global__ __launch_bounds__(1024) void k_part_wrange(const int64_t* __restrict_
                                                       int64_t* __restrict__ res, int64_t* __restrict__ wr,
                                                       unsigned long long* __restrict__ ctr,
                                                       unsigned long long* __restrict__ closed_ctr,
-                                                      unsigned long long closed_n) {
-  __shared__ int64_t smin[16], smax[16];
-  int64_t mn = INT64_MAX, mx = -1;
+                                                      unsigned long long closed_n,
+                                                      const int64_t* __restrict__ tilekr, int r8_allow) {
+  __shared__ int64_t smin[16], smax[16], skx[16], skn[16];
+  int64_t mn = INT64_MAX, mx = -1, kx = INT64_MIN, kn = INT64_MIN;
   for (int64_t t = threadIdx.x; t < nT; t += 1024) {
     mn = tilemin[t] < mn ? tilemin[t] : mn;
     mx = tilemax[t] > mx ? tilemax[t] : mx;
+    if (tilekr) {
+      kx = tilekr[2 * t] > kx ? tilekr[2 * t] : kx;
+      kn = tilekr[2 * t + 1] > kn ? tilekr[2 * t + 1] : kn;
+    }
   }
   for (int off = 32; off > 0; off >>= 1) {
     const int64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
+    const int64_t c = __shfl_xor(kx, off, 64), d = __shfl_xor(kn, off, 64);
     mn = a < mn ? a : mn;
     mx = b > mx ? b : mx;
+    kx = c > kx ? c : kx;
+    kn = d > kn ? d : kn;
   }
   if ((threadIdx.x & 63) == 0) {
     smin[threadIdx.x >> 6] = mn;
     smax[threadIdx.x >> 6] = mx;
+    skx[threadIdx.x >> 6] = kx;
+    skn[threadIdx.x >> 6] = kn;
   }
   __syncthreads();
   if (threadIdx.x) return;
   for (int w = 0; w < 16; w++) {
     mn = smin[w] < mn ? smin[w] : mn;
     mx = smax[w] > mx ? smax[w] : mx;
+    kx = skx[w] > kx ? skx[w] : kx;
+    kn = skn[w] > kn ? skn[w] : kn;
   }
   wr[2] = mn;  // event-time span of the accepted records (INT64_MAX / -1: none)
   wr[3] = mx;
   wr[5] = mx < 0 ? 0 : mn;
   const bool span_ok = mx < 0 || mx - mn < ((int64_t)1 << 31) - 2;
+  // R8 records (8 bytes: key - kbase above the rowtime delta) when the push's key range and
+  // event-time span fit one word together: wr[6] = kbase, wr[7] = rowtime-delta bits (0: R12)
+  wr[6] = 0;
+  wr[7] = 0;
+  if (r8_allow && tilekr && mx >= 0 && span_ok) {
+    const int64_t kmin = ~kn;
+    const uint64_t krange = (uint64_t)kx - (uint64_t)kmin;
+    const uint64_t trange = (uint64_t)(mx - mn + 1);  // trel in [0, mx - mn + 1]
+    const int kb = krange ? 64 - __clzll((long long)krange) : 0;
+    const int tb = 64 - __clzll((long long)trange);
+    if (kb + tb <= 64) {
+      wr[6] = kmin;
+      wr[7] = tb;
+    }
+  }
   ctr[0] = ctr[1] = ctr[2] = 0ULL;
   if (closed_ctr) *closed_ctr = closed_n;
   int64_t lo = INT64_MAX, hi = INT64_MIN;
@@ -2853,7 +3073,7 @@ void part_release(khip_agg* a) {
   PartState& s = a->part;
   s.pinfo.release();
   DevBuf* bufs[] = {&s.hcnt, &s.hnew, &s.srecA, &s.hcoarse, &s.scan_tmpB, &s.RB, &s.wr, &s.res, &s.closed, &s.closed_ctr, &s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist,
-                    &s.tilemax, &s.tilemin,
+                    &s.tilemax, &s.tilemin, &s.tilekr,
                     &s.tileprefix, &s.tpart, &s.scan_tmp, &s.srec, &s.work,
                     &s.pbase, &s.R, &s.ctr, &s.counts};
   for (DevBuf* b : bufs) b->release();
@@ -3041,6 +3261,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   KHIP_TRY(s.hist.ensure((size_t)nT * P * 4));
   KHIP_TRY(s.tilemax.ensure(nT * 8));
   KHIP_TRY(s.tilemin.ensure(nT * 8));
+  KHIP_TRY(s.tilekr.ensure(nT * 16));
   KHIP_TRY(s.tileprefix.ensure(nT * 8));
   KHIP_TRY(s.tpart.ensure(nT * 8 * T_NPART));
   KHIP_TRY(s.scan_tmp.ensure((size_t)TC * P * 8));
@@ -3080,7 +3301,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   hipLaunchKernelGGL(k_part_hist, dim3(nT), dim3(PT_THREADS), hist_lds, a->stream, keys, ts, kv, rv, n, tile, s.log2P,
                      pad, nT,
                      s.hist.as<uint32_t>(), s.tilemax.as<int64_t>(), s.tilemin.as<int64_t>(), s.tpart.as<int64_t>(),
-                     fbits, lvl2 ? s.hcoarse.as<uint32_t>() : (uint32_t*)nullptr);
+                     fbits, lvl2 ? s.hcoarse.as<uint32_t>() : (uint32_t*)nullptr, s.tilekr.as<int64_t>());
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, a->stream, s.tilemax.as<int64_t>(), nT,
                      s.tileprefix.as<int64_t>(), a->stream_time.as<int64_t>());
   // window range of the push (packed identity) and its event-time span → host: they pick the
@@ -3091,12 +3312,25 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   KHIP_TRY(s.res.ensure(16));
   KHIP_TRY(s.closed_ctr.ensure(8));
   const bool merge_allow = s.mH >= 256 && knob("KHIP_MERGE", 1) != 0;
+  // which merge kernel pass 0 runs (host-known): the lean COUNT(*) merge reads R8 records too
+  const bool narrow = s.rw == 2;
+  const int64_t r12_mode = knob("KHIP_R12", 1);  // 1: 12-byte records end to end; 2: pass A only
+  const bool r12_ok = narrow && !pad && merge_allow && r12_mode != 0;
+  const bool r12_merge = r12_ok && (r12_mode == 1 || !lvl2);  // what k_part_merge reads
+  // COUNT(*) alone: row = [key, ws, rowtime, count] (sw 4), one u32 delta plane
+  // and (key hash, ts) records with one window each (TUMBLING or no window: no meta word)
+  const bool cnt1 = a->ap.n_ops == 1 && a->ap.ops[0].kind == OP_INC && a->ap.ops[0].word == 3 && a->sw == 4 &&
+                    s.rw == 2 && a->desc.window_kind != KHIP_WINDOW_HOPPING;
+  const int mt = (int)knob("KHIP_MERGE_THREADS", 512);
+  const bool c1_plan = cnt1 && r12_merge && a->windowed && q0.adv <= (int64_t)1 << 31 && mt >= 512 &&
+                       knob("KHIP_MERGE_C1", 1) != 0;
+  const bool r8_allow = c1_plan && knob("KHIP_R8", 1) != 0;
   hipLaunchKernelGGL(k_part_wrange, dim3(1), dim3(1024), 0, a->stream, s.tilemin.as<int64_t>(), s.tilemax.as<int64_t>(),
                      nT, a->windowed, a->desc.size_ms, q0.adv, q0.fd, close0, s.log2P, s.res_fresh ? 1 : 0,
                      (a->desc.flags & KHIP_FLAG_PART_CLAIM) ? 0 : 1, merge_allow ? 1 : 0, s.res.as<int64_t>(),
                      s.wr.as<int64_t>(), s.ctr.as<unsigned long long>(),
                      a->windowed ? s.closed_ctr.as<unsigned long long>() : (unsigned long long*)nullptr,
-                     (unsigned long long)s.closed_n);
+                     (unsigned long long)s.closed_n, s.tilekr.as<int64_t>(), r8_allow ? 1 : 0);
   s.res_fresh = false;
   int64_t* pin = s.pinfo.as<int64_t>();  // wr[0..6), read after the pass-0 sync
   KHIP_TRY_HIP(hipMemcpyAsync(pin, s.wr.p, 48, hipMemcpyDeviceToHost, a->stream));
@@ -3119,10 +3353,6 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   ev_record_part(a, 1);
   // 3. scatter (12-byte records for k_part_merge when the layout is narrow: r12_ok, decided
   //    on the device by wr[4])
-  const bool narrow = s.rw == 2;
-  const int64_t r12_mode = knob("KHIP_R12", 1);  // 1: 12-byte records end to end; 2: pass A only
-  const bool r12_ok = narrow && !pad && merge_allow && r12_mode != 0;
-  const bool r12_merge = r12_ok && (r12_mode == 1 || !lvl2);  // what k_part_merge reads
   const int U = (int)knob("KHIP_SCATTER_U", narrow ? 8 : 16);
   auto scat = narrow ? (U >= 16 ? k_part_scatter<16, true> : (U >= 8 ? k_part_scatter<8, true> : (U >= 6 ? k_part_scatter<6, true> : k_part_scatter<4, true>)))
                      : (U >= 16 ? k_part_scatter<16, false> : (U >= 8 ? k_part_scatter<8, false> : k_part_scatter<4, false>));
@@ -3130,7 +3360,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   const int nbins = lvl2 ? B : P;
   const int Ut = U >= 16 ? 16 : (U >= 8 ? 8 : (narrow && U >= 6 ? 6 : 4));  // the instantiated records per thread per step
   const bool stage = narrow && !pad && nbins <= PT_THREADS && Ut <= 8 && knob("KHIP_STAGE", 1) != 0;
-  const size_t scat_lds = stage ? stage_lds_bytes(nbins, Ut * PT_THREADS) : (lvl2 ? (size_t)B * 4 : hist_lds);
+  const size_t scat_lds = stage ? stage_lds_bytes(nbins, Ut * PT_THREADS / 2) : (lvl2 ? (size_t)B * 4 : hist_lds);
   if (scat_lds > 64 * 1024)
     hipFuncSetAttribute((const void*)scat, hipFuncAttributeMaxDynamicSharedMemorySize, (int)scat_lds);
   hipLaunchKernelGGL(scat, dim3(nT), dim3(PT_THREADS), scat_lds, a->stream, keys, ts, kv, rv,
@@ -3158,7 +3388,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     }
     const bool rstage = s.rw == 2 && (1 << fbits) <= PT_THREADS && knob("KHIP_STAGE", 1) != 0;
     const int ru = knob("KHIP_REFINE_U", 8) >= 8 ? 8 : 4;  // records per thread per staged step
-    const size_t ref_lds = rstage ? stage_lds_bytes(1 << fbits, ru * PT_THREADS) : 0;
+    const size_t ref_lds = rstage ? stage_lds_bytes(1 << fbits, ru * PT_THREADS / 2) : 0;
     if (ref_lds) hipFuncSetAttribute((const void*)ref, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ref_lds);
     hipLaunchKernelGGL(ref, dim3((unsigned)(B * ng)), dim3(PT_THREADS), ref_lds, a->stream, s.srecA.as<uint64_t>(),
                        s.hcoarse.as<uint32_t>(), s.hist.as<uint32_t>(), s.pbase.as<int64_t>(), nT, G, s.log2P, fbits,
@@ -3252,13 +3482,8 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     const uint32_t* wk = (pass == 0 && !subs0) ? nullptr : s.work.as<uint32_t>();
     const int64_t nwork = (pass == 0 && !subs0) ? P : (int64_t)work.size();
     if (merge) {
-      // COUNT(*) alone: row = [key, ws, rowtime, count] (sw 4), one u32 delta plane
-      // and (key hash, ts) records with one window each (TUMBLING or no window: no meta word)
-      const bool cnt1 = a->ap.n_ops == 1 && a->ap.ops[0].kind == OP_INC && a->ap.ops[0].word == 3 && a->sw == 4 &&
-                        s.rw == 2 && a->desc.window_kind != KHIP_WINDOW_HOPPING;
-      const int mt = (int)knob("KHIP_MERGE_THREADS", 512);
       const int c1h = (int)knob("KHIP_C1_LOG2H", 12);
-      c1_ran = cnt1 && mq.r12 && mq.windowed && mq.div32 && mt >= 512 && knob("KHIP_MERGE_C1", 1) != 0;
+      c1_ran = c1_plan;
       if (c1_ran) {  // the lean COUNT(*) merge
         const int au = (int)knob("KHIP_C1_AU", 6);
         auto mk = au >= 8 ? k_part_merge_c1<512, 8> : (au >= 6 ? k_part_merge_c1<512, 6> : k_part_merge_c1<512, 4>);

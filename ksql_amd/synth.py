@@ -221,6 +221,20 @@ def clicks(lo, hi, users, xp="numpy", device=None, seed_clicks=5, miss_factor=1.
     return uid, ts
 
 
+SPARSE_MULT = 0x9E3779B97F4A7C15  # odd: id -> id * M mod 2^40 is a bijection of [0, 2^40)
+
+
+def sparse_ids(uid):
+    """User ids 1..U spread over [0, 2^40) (clickstream_join --sparse-ids): no dense index."""
+    if hasattr(uid, "dtype") and str(uid.dtype).startswith("torch"):
+        import torch
+        m = torch.tensor(SPARSE_MULT - (1 << 64), dtype=torch.int64, device=uid.device)  # wraps like uint64
+        return (uid * m) & ((1 << 40) - 1)
+    import numpy as np
+    with np.errstate(over="ignore"):
+        return ((np.asarray(uid, np.uint64) * np.uint64(SPARSE_MULT)) & np.uint64((1 << 40) - 1)).astype(np.int64)
+
+
 def repartition_sum(lo, hi, n, xp="numpy", device=None, rank=0, world=1, regions=1_000_000, seed=6,
                     span_ms=3_600_000, disorder_ms=1_000):
     """C5 source partition `rank`: (event_id key, ts, region_id BIGINT, amount BIGINT)."""

@@ -179,6 +179,42 @@ def test_c3_hopping_double_microbatches(prod, orc, say):
     assert_snap_equal(got, exp, desc)
 
 
+@pytest.mark.timeout(1100)
+def test_c3_bench_push_size(prod, orc, say):
+    """The timed configuration itself: bench.py's hopping_double pushes (2^27-record event-time
+    micro-batches of the 1e9-record workload, its capacity hint), two of them — the first two pushes
+    of a bench step, bit-exact integer state and DOUBLE within tolerance against the oracle."""
+    n_total = 1_000_000_000
+    S = 1 << 27
+    m = 2 * S
+    cfg = synth.CONFIGS["hopping_double"]
+    kw = dict(window_kind="HOPPING", size_ms=cfg["size_ms"], advance_ms=cfg["advance_ms"], grace_ms=cfg["grace_ms"],
+              key_type="INT64", col_types=["DOUBLE"], aggs=[("SUM", 0), ("AVG", 0), ("MIN", 0), ("MAX", 0)])
+    key, ts, val, valid = synth.hopping_double(0, m, n_total, xp="torch", device="cuda")
+    vb = abi.bitmap_torch(valid)
+    del valid
+    span_push = cfg["span_ms"] * S / n_total  # bench.py:bench_hopping_double's live-group hint
+    live = int(cfg["keys"] * (span_push + cfg["size_ms"] + cfg["grace_ms"] + cfg["disorder_ms"]) / cfg["advance_ms"])
+    desc = abi.make_agg_desc(**kw, capacity_hint=live)
+    h = abi.AggHandle(prod, desc)
+    stats = [h.push(abi.DeviceBatch(ts[lo:lo + S], keys=key[lo:lo + S], cols=[val[lo:lo + S]],
+                                    col_valid=[vb[lo // 8:(lo + S) // 8]])) for lo in range(0, m, S)]
+    got = h.snapshot()
+    h.close()
+    del key, ts, val, vb
+    say("C3 at the bench's push size: %d groups after %d pushes of %d records" % (got["n"], len(stats), S))
+    keyh, tsh, valh, validh = synth.hopping_double(0, m, n_total)
+    o = abi.ShardedOracleAgg(orc, abi.make_agg_desc(**kw), THREADS)
+    ostats = [o.push(abi.HostBatch(tsh[lo:lo + S], keys=keyh[lo:lo + S], cols=[valh[lo:lo + S]],
+                                   col_valid=[validh[lo:lo + S]])) for lo in range(0, m, S)]
+    del keyh, tsh, valh, validh
+    exp = o.snapshot()
+    o.close()
+    assert stats == ostats
+    assert sum(s["rows_accepted"] for s in stats) == m
+    assert_snap_equal(got, exp, desc)
+
+
 @pytest.mark.timeout(900)
 def test_c3_changelog_per_push(prod, orc, say):
     """C3's micro-batch structure with EMIT CHANGES kept (KHIP_FLAG_CHANGELOG): the rows every
@@ -326,14 +362,20 @@ def test_c4_probe_device_vs_oracle(prod, orc, join_type, where):
 
 
 @pytest.mark.timeout(900)
-def test_c4_clickstream_probe_device_full(prod, orc, say):
+@pytest.mark.parametrize("sparse", [False, True], ids=["dense-ids", "sparse-ids"])
+def test_c4_clickstream_probe_device_full(prod, orc, say, sparse):
     """The bench's C4 step (LEFT JOIN users WHERE level = 'Platinum', one INT32 level column)
-    on a 1e7-row users table and 1e8 + 37 clicks."""
+    on a 1e7-row users table and 1e8 + 37 clicks: user ids 1..U (the dense direct-map index) and
+    spread over 2^40 (bench.py --sparse-ids: the hash-probe kernel)."""
     U, n = 10_000_000, 100_000_037
     uid, level = synth.users_table(0, U)
+    if sparse:
+        uid = synth.sparse_ids(uid)
     b = abi.HostBatch(np.zeros(U, np.int64), keys=uid, cols=[level.astype(np.int32)])
     tp, to = _table_pair(prod, orc, ["INT32"], [b], U)
     cu, cts = synth.clicks(0, n, U, seed_clicks=5)
+    if sparse:
+        cu = synth.sparse_ids(cu)
     where = {"col": 0, "op": "EQ", "i64": synth.LEVELS.index("Platinum")}
     say("C4 table built, probing %d clicks" % n)
     _check_probe_device(tp, to, cu, cts, None, None, "LEFT", where, ["INT32"])

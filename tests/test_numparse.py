@@ -101,3 +101,12 @@ def test_integers(checker):
             assert g == "ok %d" % int(k)
     ints = ["2147483647", "-2147483648", "2147483648", "-2147483649", "12", "-0"]
     assert checker(["i " + v for v in ints]) == ["ok 2147483647", "ok -2147483648", "err", "err", "ok 12", "ok 0"]
+
+
+def test_known_differences(checker):
+    """Pinned on purpose (khip_numparse.hpp header): inputs Java parses and this path reports as
+    errors — a hex float, and a value whose halfway comparison needs ~1,700 or more digits."""
+    halfway = "1.00000000000000011102230246251565404236316680908203125"  # 1 + 2^-53 exactly
+    assert float(halfway + "0" * 2000 + "1") == 1.0000000000000002  # Java / Python: rounds up
+    assert checker(["d 0x1p3", "d " + halfway + "0" * 2000 + "1"]) == ["err", "err"]
+    assert checker(["d " + halfway + "0" * 1300 + "1"]) == ["ok %d" % bits(1.0000000000000002)]  # within the bound
