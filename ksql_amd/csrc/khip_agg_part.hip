@@ -2489,7 +2489,8 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge_c1(
     }
     lds_barrier();
     C1_T(1);
-    // the next item's first chunk is in flight from here on
+    // the next item's first chunk is in flight from here on (its second one too was measured
+    // slower: the count phase then waits behind those loads)
     load(ra, nit.rbase, nit.rn, 0);
     if (lovf) {  // more groups than the table: retried with 2x sub-passes
       if (threadIdx.x == 0) fail[p] |= 1;
