@@ -737,7 +737,9 @@ khip_status khip_table_create(const khip_table_desc* d, khip_table** out) {
     delete t;
     return fail(KHIP_E_DEVICE, "hipStreamCreate failed (no device?)");
   }
-  t->cap = next_pow2(std::max<int64_t>(1024, d->capacity_hint > 0 ? (d->capacity_hint * 4 + 2) / 3 : 1 << 16));
+  // load factor <= 1/2: with linear probing a hit then costs ~1.5 slot reads and a miss ~2.5
+  // (at 3/4 it was 2.5 and 8.5: dependent random HBM reads, the probe kernel's latency chain)
+  t->cap = next_pow2(std::max<int64_t>(1024, d->capacity_hint > 0 ? d->capacity_hint * 2 : 1 << 16));
   khip_status st;
   if ((st = table_alloc(t, t->table, t->cap)) != KHIP_OK ||
       (st = t->types_dev.ensure(sizeof(int32_t) * JMAX_COLS)) != KHIP_OK ||
@@ -770,8 +772,8 @@ khip_status khip_table_upsert(khip_table* t, const khip_batch* b) {
   JCols cols;
   KHIP_TRY(jresolve(t, b, t->desc.n_cols, &keys, &ts, &kv, &rv, &cols));
   KHIP_TRY(resolve_keys(t, b, true, kv, &keys));
-  // keep the load factor <= 0.75 even if every row were a new key
-  if (4 * (t->occ + n) > 3 * t->cap) KHIP_TRY(table_grow(t, next_pow2((4 * (t->occ + n) + 2) / 3)));
+  // keep the load factor <= 1/2 even if every row were a new key
+  if (2 * (t->occ + n) > t->cap) KHIP_TRY(table_grow(t, next_pow2(2 * (t->occ + n))));
   KHIP_TRY(t->slot_of.ensure(n * 8));
   KHIP_TRY(t->claimed.ensure(n * 8));
   unsigned long long* ctr = t->scratch.as<unsigned long long>();
