@@ -469,10 +469,12 @@ __device__ __forceinline__ int64_t sess_replay(const SessParams& q, int64_t key,
   return kept;
 }
 
-// Scratch budget of one wave's keys in LDS (records 16 B, rows sw words + 1 flag byte each);
-// waves whose keys need more replay in HBM scratch.
+// Scratch budget of one wave's keys in LDS (rows of sw words + 1 flag byte each); waves whose
+// keys need more replay in HBM scratch.  The records are read from HBM by each lane (a key's
+// records are contiguous, and the wave's keys are neighbours: their lines are shared through L1),
+// so the LDS holds only the rows and six waves fit a CU.
 #ifndef KHIP_SESS_LDS
-#define KHIP_SESS_LDS 40960
+#define KHIP_SESS_LDS 24576
 #endif
 constexpr int SESS_LDS = KHIP_SESS_LDS;
 
@@ -495,22 +497,20 @@ __global__ __launch_bounds__(64) void k_sess_apply(SessParams q, const uint64_t*
   const int64_t j0 = (int64_t)blockIdx.x * 64, j = j0 + lane;
   const int64_t jl = (nseg_eff - 1 < j0 + 63) ? nseg_eff - 1 : j0 + 63;
   const int sw = q.sw;
-  const int64_t R0 = useg[j0], R1 = useg[jl] + ucnt[jl];
+  const int64_t R1 = useg[jl] + ucnt[jl];
   const int64_t C0 = scap[j0], C1 = scap[jl] + cap[jl];
-  const int64_t need = (R1 - R0) * 16 + (C1 - C0) * (sw * 8 + 1);
+  const int64_t need = (C1 - C0) * (sw * 8 + 1);
   const bool in_lds = need <= SESS_LDS;
   const int64_t vis_end = *st_end - q.retention;
   int64_t applied = 0, late = 0, kept = 0;
   const bool mine = j < nseg_eff;
+  (void)R1;
   if (in_lds) {
-    longlong2* lrec = (longlong2*)lds;
-    uint64_t* lrow = lds + 2 * (R1 - R0);
+    uint64_t* lrow = lds;
     uint8_t* lfl = (uint8_t*)(lrow + (C1 - C0) * sw);
-    for (int64_t x = lane; x < R1 - R0; x += 64) lrec[x] = g[R0 + x];
-    __syncthreads();
     if (mine) {
       const int64_t base = scap[j], r0 = useg[j];
-      kept = sess_replay(q, ukeys[j], store + s0[j] * sw, cap[j] - ucnt[j], lrec + (r0 - R0), sidx ? sidx + r0 : nullptr,
+      kept = sess_replay(q, ukeys[j], store + s0[j] * sw, cap[j] - ucnt[j], g + r0, sidx ? sidx + r0 : nullptr,
                          ucnt[j], lrow + (base - C0) * sw, lfl + (base - C0), trow + base * sw, cols, vis_end, crow,
                          ctomb, ctr, keep_changes, applied, late);
       fin[j] = kept;
