@@ -359,14 +359,14 @@ struct TaggState {
   int src_sw = 8;
   int key_type = -1;    // source PRIMARY KEY type (fixed by the first push)
   KeyDict dict;         // UTF8 PRIMARY KEYs → ids
-  DevBuf sid, skey, skey2, sidx, sidx2, tmp, ctr, claimed, gclaimed, blk, st_koff, st_kbytes, st_kv, st_key, shash;
+  DevBuf sid, skey, skey2, sidx, sidx2, tmp, tmp2, ctr, claimed, gclaimed, blk, st_koff, st_kbytes, st_kv, st_key, shash;
 };
 
 struct SessState {
   DevBuf rows, rows2;  // store (n rows) and the next push's output
   int64_t n = 0;
   DevBuf skey, sidx, skey2, sidx2, st_after, ukeys, ucnt, nseg, useg, s0, cap, scap, fin, fin_pre;
-  DevBuf srow, sfl, trow, crow, ctomb, keep, keep_pre, ctr, tmp, gath, blockkr;
+  DevBuf srow, sfl, trow, crow, ctomb, keep, keep_pre, ctr, tmp, tmp2, gath, blockkr;
   int64_t nchg = 0;    // changelog rows of the last push (crow / ctomb)
 };
 

@@ -11,11 +11,13 @@
 //
 // Per push (all on the handle's stream):
 //   k_sess_range / k_scan_blocks stream time before each 2048-record block; the key range
-//   k_sess_prep                  per record: accepted?, stream time after it (packed with ts);
-//                                (key - kmin, row) pairs
-//   radix sort (hipcub, stable)  records grouped by key, arrival order kept inside a key; only
+//   k_sess_prep                  per record: accepted?, stream time after it, packed with ts into
+//                                8 bytes relative to the push's time base (16 when the push spans
+//                                2^32 ms); (key - kmin, record) pairs
+//   radix sort (khip_sort.hpp)   records grouped by key, arrival order kept inside a key; only
 //                                the bits of the push's key range are sorted
-//   k_sess_gather                the packed (ts, stream time) records in sorted order
+//   k_sess_gather                (argument columns or 16-byte records: the sort carries row
+//                                indices) the records in sorted order
 //   run-length encode            one segment per batch key
 //   k_sess_bounds                the key's store range (binary search), scratch capacity
 //   k_sess_apply                 ONE THREAD PER KEY replays the key's records in arrival order
@@ -25,7 +27,6 @@
 //                                tombstones of merged-away sessions)
 //   k_sess_keep / k_sess_scatter the new store = untouched keys' sessions (minus expired) merged
 //                                in key order with the rewritten keys' sessions
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <vector>
@@ -33,6 +34,7 @@
 #include "khip_util.hpp"
 
 #include "khip_agg_internal.hpp"
+#include "khip_sort.hpp"
 
 namespace khip {
 
@@ -50,7 +52,7 @@ struct SessParams {
 // prefix), and the key range of the push (min / max as order-preserving unsigned words,
 // atomic-max'd: ctr[C_KMINN] = max of ~u, ctr[C_KMAX] = max of u, ctr[C_KACC] = accepted).
 // Coalesced: element k of thread t is base + k * BLOCK + t.
-constexpr int C_KMINN = 20, C_KMAX = 21, C_KACC = 22;
+constexpr int C_KMINN = 20, C_KMAX = 21, C_KACC = 22, C_TBASE = 23;
 
 __device__ __forceinline__ uint64_t key_ord(int64_t k) { return (uint64_t)k ^ (1ULL << 63); }
 
@@ -63,12 +65,13 @@ __device__ __forceinline__ bool sess_ok(const uint8_t* kv, const uint8_t* rv, co
 __global__ __launch_bounds__(BLOCK) void k_sess_range(const int64_t* __restrict__ keys, const int64_t* __restrict__ ts,
                                                       const uint8_t* __restrict__ kv, const uint8_t* __restrict__ rv,
                                                       int64_t n, int64_t* __restrict__ blockmax,
-                                                      ulonglong2* __restrict__ blockkr, int64_t* __restrict__ blockacc) {
+                                                      ulonglong2* __restrict__ blockkr, int64_t* __restrict__ blockacc,
+                                                      int64_t* __restrict__ blocktmin) {
   __shared__ int64_t lds[BLOCK / 64];
-  __shared__ uint64_t lk[2][BLOCK / 64];
+  __shared__ uint64_t lk[3][BLOCK / 64];
   __shared__ int64_t la[BLOCK / 64];
   const int64_t base = (int64_t)blockIdx.x * RPB;
-  int64_t m = -1;
+  int64_t m = -1, tmn = INT64_MAX;
   uint64_t kmn = 0, kmx = 0;
   int64_t acc = 0;
 #pragma unroll
@@ -77,6 +80,7 @@ __global__ __launch_bounds__(BLOCK) void k_sess_range(const int64_t* __restrict_
     int64_t t;
     if (i < n && sess_ok(kv, rv, ts, i, &t)) {
       m = t > m ? t : m;
+      tmn = t < tmn ? t : tmn;
       const uint64_t u = key_ord(keys[i]);
       kmn = ~u > kmn ? ~u : kmn;
       kmx = u > kmx ? u : kmx;
@@ -88,14 +92,17 @@ __global__ __launch_bounds__(BLOCK) void k_sess_range(const int64_t* __restrict_
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const uint64_t a = __shfl_xor(kmn, off, 64), b = __shfl_xor(kmx, off, 64);
+    const int64_t c = __shfl_xor(tmn, off, 64);
     kmn = a > kmn ? a : kmn;
     kmx = b > kmx ? b : kmx;
+    tmn = c < tmn ? c : tmn;
   }
   acc = wave_sum(acc);
   const int wave = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
     lk[0][wave] = kmn;
     lk[1][wave] = kmx;
+    lk[2][wave] = (uint64_t)tmn;
     la[wave] = acc;
   }
   __syncthreads();
@@ -103,32 +110,42 @@ __global__ __launch_bounds__(BLOCK) void k_sess_range(const int64_t* __restrict_
     for (int w = 1; w < BLOCK / 64; w++) {
       kmn = lk[0][w] > kmn ? lk[0][w] : kmn;
       kmx = lk[1][w] > kmx ? lk[1][w] : kmx;
+      tmn = (int64_t)lk[2][w] < tmn ? (int64_t)lk[2][w] : tmn;
       acc += la[w];
     }
     blockmax[blockIdx.x] = tot;
     blockkr[blockIdx.x] = make_ulonglong2(kmn, kmx);
     blockacc[blockIdx.x] = acc;
+    blocktmin[blockIdx.x] = tmn;
   }
 }
 
-// The per-block key ranges → ctr[C_KMINN], ctr[C_KMAX], ctr[C_KACC] (one workgroup).
+// The per-block key ranges → ctr[C_KMINN], ctr[C_KMAX], ctr[C_KACC]; ctr[C_TBASE] = the base of
+// the push's packed replay records: the smallest accepted ts, or the stream time before the push
+// when that is smaller and set (every stream time a record of the push sees is -1 or >= it).
+// Runs before k_scan_blocks advances *stream_time (one workgroup).
 __global__ __launch_bounds__(1024) void k_sess_range_reduce(const ulonglong2* __restrict__ blockkr,
-                                                            const int64_t* __restrict__ blockacc, int64_t nb,
+                                                            const int64_t* __restrict__ blockacc,
+                                                            const int64_t* __restrict__ blocktmin, int64_t nb,
+                                                            const int64_t* __restrict__ stream_time,
                                                             unsigned long long* __restrict__ ctr) {
-  __shared__ uint64_t l[3][1024 / 64];
+  __shared__ uint64_t l[4][1024 / 64];
   uint64_t kmn = 0, kmx = 0;
-  int64_t acc = 0;
+  int64_t acc = 0, tmn = INT64_MAX;
   for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) {
     const ulonglong2 v = blockkr[b];
     kmn = v.x > kmn ? v.x : kmn;
     kmx = v.y > kmx ? v.y : kmx;
     acc += blockacc[b];
+    tmn = blocktmin[b] < tmn ? blocktmin[b] : tmn;
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const uint64_t a = __shfl_xor(kmn, off, 64), b = __shfl_xor(kmx, off, 64);
+    const int64_t c = __shfl_xor(tmn, off, 64);
     kmn = a > kmn ? a : kmn;
     kmx = b > kmx ? b : kmx;
+    tmn = c < tmn ? c : tmn;
   }
   acc = wave_sum(acc);
   const int wave = threadIdx.x >> 6;
@@ -136,6 +153,7 @@ __global__ __launch_bounds__(1024) void k_sess_range_reduce(const ulonglong2* __
     l[0][wave] = kmn;
     l[1][wave] = kmx;
     l[2][wave] = (uint64_t)acc;
+    l[3][wave] = (uint64_t)tmn;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -143,11 +161,27 @@ __global__ __launch_bounds__(1024) void k_sess_range_reduce(const ulonglong2* __
       kmn = l[0][w] > kmn ? l[0][w] : kmn;
       kmx = l[1][w] > kmx ? l[1][w] : kmx;
       acc += (int64_t)l[2][w];
+      tmn = (int64_t)l[3][w] < tmn ? (int64_t)l[3][w] : tmn;
     }
+    const int64_t p = *stream_time;
+    if (p >= 0 && p < tmn) tmn = p;
     ctr[C_KMINN] = kmn;
     ctr[C_KMAX] = kmx;
     ctr[C_KACC] = (unsigned long long)acc;
+    ctr[C_TBASE] = (unsigned long long)(tmn == INT64_MAX ? 0 : tmn);
   }
+}
+
+// Packed 8-byte replay record: (stream time after - tbase + 1) << 32 | (ts - tbase + 1), each half
+// 0 for -1 (a dropped record / no stream time yet); used when the push's times span < 2^32 - 1.
+__device__ __forceinline__ uint64_t rec_pack(int64_t t, int64_t st, int64_t tbase) {
+  const uint64_t lo = t >= 0 ? (uint64_t)(t - tbase + 1) : 0, hi = st >= 0 ? (uint64_t)(st - tbase + 1) : 0;
+  return (hi << 32) | lo;
+}
+__device__ __forceinline__ void rec_unpack(uint64_t r, int64_t tbase, int64_t& t, int64_t& st) {
+  const uint32_t lo = (uint32_t)r, hi = (uint32_t)(r >> 32);
+  t = lo ? tbase + (int64_t)lo - 1 : -1;
+  st = hi ? tbase + (int64_t)hi - 1 : -1;
 }
 
 // Per record (coalesced): the task's stream time after it (block prefix, then the block's running
@@ -158,6 +192,7 @@ __global__ __launch_bounds__(BLOCK) void k_sess_prep(const int64_t* __restrict__
                                                      int64_t n, const int64_t* __restrict__ prefix, int64_t kmin,
                                                      uint64_t drop, uint64_t* __restrict__ skey,
                                                      uint32_t* __restrict__ sidx, longlong2* __restrict__ rec,
+                                                     uint64_t* __restrict__ rec8, int64_t tbase,
                                                      int64_t* __restrict__ blockcnt) {
   // wave w owns records [base + w * 64 * ITEMS, +64 * ITEMS), read 64 at a time (coalesced); the
   // running max is a wave scan per step, the earlier waves' maxima join after one block barrier
@@ -198,7 +233,9 @@ __global__ __launch_bounds__(BLOCK) void k_sess_prep(const int64_t* __restrict__
       const bool ok = tv[k] >= 0;
       skey[i] = ok ? (uint64_t)keys[i] - (uint64_t)kmin : drop;
       if (sidx) sidx[i] = (uint32_t)i;
-      rec[i] = make_longlong2(tv[k], stv[k] > pre ? stv[k] : pre);
+      const int64_t sa = stv[k] > pre ? stv[k] : pre;
+      if (rec8) rec8[i] = rec_pack(tv[k], sa, tbase);
+      else rec[i] = make_longlong2(tv[k], sa);
     }
   }
   // drop counters: one row of 4 per block (summed by k_sess_cnt_reduce; same-address atomics
@@ -236,8 +273,9 @@ __global__ __launch_bounds__(1024) void k_sess_cnt_reduce(const int64_t* __restr
 }
 
 // Replay records in sorted order: g[r] = rec[sidx[r]] (the random reads leave the per-key chain).
-__global__ __launch_bounds__(256) void k_sess_gather(const uint32_t* __restrict__ sidx, const longlong2* __restrict__ rec,
-                                                     int64_t n, longlong2* __restrict__ g) {
+template <class R>
+__global__ __launch_bounds__(256) void k_sess_gather(const uint32_t* __restrict__ sidx, const R* __restrict__ rec,
+                                                     int64_t n, R* __restrict__ g) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
     g[r] = rec[sidx[r]];
 }
@@ -358,7 +396,8 @@ __device__ __forceinline__ void row_copy(uint64_t* d, const uint64_t* s, int sw)
 // scratch rows and flags (LDS or HBM), T: removed original sessions (HBM), orig: its store rows.
 // Returns the sessions left after expiry (compacted at R); chg rows appended to the changelog.
 __device__ __forceinline__ int64_t sess_replay(const SessParams& q, int64_t key, const uint64_t* orig, int64_t norig,
-                                               const longlong2* g, const uint32_t* sidx, int64_t nrec,
+                                               const longlong2* g, const uint64_t* g8, int64_t tbase,
+                                               const uint32_t* sidx, int64_t nrec,
                                                uint64_t* R, uint8_t* F, uint64_t* T, const ColPtrs& cols,
                                                int64_t vis_end, uint64_t* __restrict__ crow,
                                                uint8_t* __restrict__ ctomb, unsigned long long* __restrict__ ctr,
@@ -372,8 +411,14 @@ __device__ __forceinline__ int64_t sess_replay(const SessParams& q, int64_t key,
     m++;
   }
   for (int64_t r = 0; r < nrec; r++) {
-    const longlong2 gr = g[r];
-    const int64_t t = gr.x, st = gr.y;
+    int64_t t, st;
+    if (g8) {
+      rec_unpack(g8[r], tbase, t, st);
+    } else {
+      const longlong2 gr = g[r];
+      t = gr.x;
+      st = gr.y;
+    }
     if (t < 0) continue;  // dropped (only where the sentinel shares the last key's segment)
     const int64_t i = q.ap.n_cols ? (int64_t)sidx[r] : 0;
     const int64_t vis = st - q.retention, close = st - q.grace - q.gap;
@@ -486,7 +531,8 @@ __global__ __launch_bounds__(64) void k_sess_apply(SessParams q, const uint64_t*
                                                    const int64_t* __restrict__ useg, const int* __restrict__ nseg,
                                                    const int64_t* __restrict__ s0, const int64_t* __restrict__ cap,
                                                    const int64_t* __restrict__ scap, const uint32_t* __restrict__ sidx,
-                                                   const longlong2* __restrict__ g, ColPtrs cols,
+                                                   const longlong2* __restrict__ g, const uint64_t* __restrict__ g8,
+                                                   int64_t tbase, ColPtrs cols,
                                                    const int64_t* __restrict__ st_end, uint64_t* __restrict__ srow,
                                                    uint8_t* __restrict__ sfl, uint64_t* __restrict__ trow,
                                                    int64_t* __restrict__ fin, uint64_t* __restrict__ crow,
@@ -510,7 +556,8 @@ __global__ __launch_bounds__(64) void k_sess_apply(SessParams q, const uint64_t*
     uint8_t* lfl = (uint8_t*)(lrow + (C1 - C0) * sw);
     if (mine) {
       const int64_t base = scap[j], r0 = useg[j];
-      kept = sess_replay(q, ukeys[j], store + s0[j] * sw, cap[j] - ucnt[j], g + r0, sidx ? sidx + r0 : nullptr,
+      kept = sess_replay(q, ukeys[j], store + s0[j] * sw, cap[j] - ucnt[j], g ? g + r0 : nullptr, g8 ? g8 + r0 : nullptr, tbase,
+                         sidx ? sidx + r0 : nullptr,
                          ucnt[j], lrow + (base - C0) * sw, lfl + (base - C0), trow + base * sw, cols, vis_end, crow,
                          ctomb, ctr, keep_changes, applied, late);
       fin[j] = kept;
@@ -525,7 +572,8 @@ __global__ __launch_bounds__(64) void k_sess_apply(SessParams q, const uint64_t*
     }
   } else if (mine) {
     const int64_t base = scap[j], r0 = useg[j];
-    kept = sess_replay(q, ukeys[j], store + s0[j] * sw, cap[j] - ucnt[j], g + r0, sidx ? sidx + r0 : nullptr, ucnt[j],
+    kept = sess_replay(q, ukeys[j], store + s0[j] * sw, cap[j] - ucnt[j], g ? g + r0 : nullptr, g8 ? g8 + r0 : nullptr, tbase,
+                         sidx ? sidx + r0 : nullptr, ucnt[j],
                        srow + base * sw, sfl + base, trow + base * sw, cols, vis_end, crow, ctomb, ctr, keep_changes,
                        applied, late);
     fin[j] = kept;
@@ -598,16 +646,6 @@ __global__ __launch_bounds__(256) void k_sess_scatter_seg(const uint64_t* __rest
 
 // ------------------------------------------------------------------ host side
 
-template <class F>
-static khip_status cub_call(DevBuf& tmp, hipStream_t st, F&& f) {
-  size_t bytes = 0;
-  if (f(nullptr, bytes) != hipSuccess) return fail(KHIP_E_DEVICE, "hipcub size query failed");
-  KHIP_TRY(tmp.ensure(std::max<size_t>(bytes, 16)));
-  if (f(tmp.p, bytes) != hipSuccess) return fail(KHIP_E_DEVICE, "hipcub call failed");
-  (void)st;
-  return KHIP_OK;
-}
-
 khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
                       const uint8_t* rv, const ColPtrs& cols, int64_t* tot) {
   SessState& S = a->sess;
@@ -619,16 +657,23 @@ khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   KHIP_TRY(S.ctr.ensure(32 * 8));
   KHIP_TRY_HIP(hipMemsetAsync(S.ctr.p, 0, 32 * 8, st));
   KHIP_TRY(S.blockkr.ensure(nb * 32));
+  int64_t* blockacc = (int64_t*)(S.blockkr.as<char>() + nb * 16);
+  int64_t* blocktmin = (int64_t*)(S.blockkr.as<char>() + nb * 24);
   hipLaunchKernelGGL(k_sess_range, dim3(nb), dim3(BLOCK), 0, st, keys, ts, kv, rv, n, a->blockmax.as<int64_t>(),
-                     S.blockkr.as<ulonglong2>(), (int64_t*)(S.blockkr.as<char>() + nb * 16));
-  hipLaunchKernelGGL(k_sess_range_reduce, dim3(1), dim3(1024), 0, st, S.blockkr.as<ulonglong2>(),
-                     (const int64_t*)(S.blockkr.as<char>() + nb * 16), nb, S.ctr.as<unsigned long long>());
+                     S.blockkr.as<ulonglong2>(), blockacc, blocktmin);
+  hipLaunchKernelGGL(k_sess_range_reduce, dim3(1), dim3(1024), 0, st, S.blockkr.as<ulonglong2>(), blockacc, blocktmin,
+                     nb, a->stream_time.as<int64_t>(), S.ctr.as<unsigned long long>());
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, st, a->blockmax.as<int64_t>(), nb,
                      a->blockprefix.as<int64_t>(), a->stream_time.as<int64_t>());
-  // the push's key range: the sort runs over (key - kmin) and only the bits that range needs
-  unsigned long long kr[3] = {0, 0, 0};
+  // the push's key range: the sort runs over (key - kmin) and only the bits that range needs;
+  // its time base and the stream time after it: packed 8-byte replay records when the span fits
+  unsigned long long kr[4] = {0, 0, 0, 0};
+  int64_t st_after_push = -1;
   KHIP_TRY_HIP(hipMemcpyAsync(kr, S.ctr.as<unsigned long long>() + C_KMINN, sizeof(kr), hipMemcpyDeviceToHost, st));
+  KHIP_TRY_HIP(hipMemcpyAsync(&st_after_push, a->stream_time.p, 8, hipMemcpyDeviceToHost, st));
   KHIP_TRY_HIP(hipStreamSynchronize(st));
+  const int64_t tbase = (int64_t)kr[3];
+  const bool packed = st_after_push < 0 || (uint64_t)(st_after_push - tbase) < 0xFFFFFFF0ULL;
   int64_t kmin = 0;
   uint64_t range = 0;
   if (kr[2]) {
@@ -639,10 +684,10 @@ khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   const bool sentinel = range != ~0ULL;  // dropped rows get a key of their own (range + 1)
   const uint64_t drop = sentinel ? range + 1 : range;
   const int end_bit = drop ? 64 - __builtin_clzll(drop) : 1;
-  // without argument columns the replay needs only (ts, stream time after): those 16 bytes ride
-  // through the sort as the value; with columns the value is the row index and a gather pass
-  // brings the packed records into sorted order
-  const bool by_idx = a->desc.n_cols > 0;
+  // Packed records without argument columns ride through the sort as its 8-byte value.  With
+  // columns (or 16-byte records) the sort carries 4-byte row indices and one gather brings the
+  // records into sorted order (a 16-byte value would cost the sort more than the gather).
+  const bool by_idx = !packed || a->desc.n_cols > 0;
   KHIP_TRY(S.skey.ensure(n * 8));
   KHIP_TRY(S.skey2.ensure(n * 8));
   KHIP_TRY(S.st_after.ensure(n * 16));
@@ -652,40 +697,40 @@ khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     KHIP_TRY(S.sidx2.ensure(n * 4));
   }
   hipLaunchKernelGGL(k_sess_prep, dim3(nb), dim3(BLOCK), 0, st, keys, ts, kv, rv, n, a->blockprefix.as<int64_t>(), kmin,
-                     drop, S.skey.as<uint64_t>(), by_idx ? S.sidx.as<uint32_t>() : nullptr, S.st_after.as<longlong2>(),
+                     drop, S.skey.as<uint64_t>(), by_idx ? S.sidx.as<uint32_t>() : nullptr,
+                     packed ? nullptr : S.st_after.as<longlong2>(), packed ? S.st_after.as<uint64_t>() : nullptr, tbase,
                      (int64_t*)S.blockkr.p);
   hipLaunchKernelGGL(k_sess_cnt_reduce, dim3(1), dim3(1024), 0, st, (const int64_t*)S.blockkr.p, nb,
                      S.ctr.as<unsigned long long>());
   KHIP_TRY_HIP(hipGetLastError());
   // group by key, arrival order kept within a key (LSD radix sort is stable)
-  const int ni = (int)n;
   uint64_t* k_in = S.skey.as<uint64_t>();
   uint64_t* k_out = S.skey2.as<uint64_t>();
   uint32_t* v_out = by_idx ? S.sidx2.as<uint32_t>() : nullptr;
+  const dim3 ggrid((int)std::min<int64_t>(ceil_div(n, 256), 16384));
   if (by_idx) {
     uint32_t* v_in = S.sidx.as<uint32_t>();
-    KHIP_TRY(cub_call(S.tmp, st, [&](void* p, size_t& b) {
-      return hipcub::DeviceRadixSort::SortPairs(p, b, k_in, k_out, v_in, v_out, ni, 0, end_bit, st);
-    }));
-    hipLaunchKernelGGL(k_sess_gather, dim3((int)std::min<int64_t>(ceil_div(n, 256), 16384)), dim3(256), 0, st, v_out,
-                       S.st_after.as<longlong2>(), n, S.gath.as<longlong2>());
+    KHIP_TRY(ksort::sort_pairs<uint32_t>(st, S.tmp, S.tmp2, k_in, k_out, v_in, v_out, n, end_bit));
+    if (packed) {
+      auto kg = k_sess_gather<uint64_t>;
+      hipLaunchKernelGGL(kg, ggrid, dim3(256), 0, st, v_out, S.st_after.as<uint64_t>(), n, S.gath.as<uint64_t>());
+    } else {
+      auto kg = k_sess_gather<longlong2>;
+      hipLaunchKernelGGL(kg, ggrid, dim3(256), 0, st, v_out, S.st_after.as<longlong2>(), n, S.gath.as<longlong2>());
+    }
   } else {
-    longlong2* r_in = S.st_after.as<longlong2>();
-    longlong2* r_out = S.gath.as<longlong2>();
-    KHIP_TRY(cub_call(S.tmp, st, [&](void* p, size_t& b) {
-      return hipcub::DeviceRadixSort::SortPairs(p, b, k_in, k_out, r_in, r_out, ni, 0, end_bit, st);
-    }));
+    KHIP_TRY(ksort::sort_pairs<uint64_t>(st, S.tmp, S.tmp2, k_in, k_out, S.st_after.as<uint64_t>(),
+                                         S.gath.as<uint64_t>(), n, end_bit));
   }
   KHIP_TRY(S.ukeys.ensure(n * 8));
   KHIP_TRY(S.ucnt.ensure(n * 4));
   KHIP_TRY(S.nseg.ensure(16));
-  KHIP_TRY(cub_call(S.tmp, st, [&](void* p, size_t& b) {
-    return hipcub::DeviceRunLengthEncode::Encode(p, b, k_out, S.ukeys.as<uint64_t>(), S.ucnt.as<int>(), S.nseg.as<int>(),
-                                                 ni, st);
-  }));
-  int nseg = 0;
-  KHIP_TRY_HIP(hipMemcpyAsync(&nseg, S.nseg.p, 4, hipMemcpyDeviceToHost, st));
-  KHIP_TRY_HIP(hipStreamSynchronize(st));
+  KHIP_TRY(S.useg.ensure((size_t)(n + 1) * 8));
+  // key segments: unique keys, counts and starts (useg = the counts' exclusive prefix)
+  int64_t nseg64 = 0;
+  KHIP_TRY(ksort::rle_sorted(st, S.tmp, k_out, n, S.ukeys.as<uint64_t>(), S.ucnt.as<int>(), S.useg.as<int64_t>(),
+                             S.nseg.as<int>(), &nseg64));
+  int nseg = (int)nseg64;
   uint64_t last = 0;
   if (nseg > 0) {
     KHIP_TRY_HIP(hipMemcpyAsync(&last, S.ukeys.as<uint64_t>() + nseg - 1, 8, hipMemcpyDeviceToHost, st));
@@ -695,24 +740,19 @@ khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   if (nseg > 0)
     hipLaunchKernelGGL(k_sess_ukeys, dim3(ceil_div(nseg, 256)), dim3(256), 0, st, S.ukeys.as<int64_t>(),
                        S.nseg.as<int>(), kmin);
-  KHIP_TRY(S.useg.ensure((size_t)(nseg + 1) * 8));
   KHIP_TRY(S.s0.ensure((size_t)(nseg + 1) * 8));
   KHIP_TRY(S.cap.ensure((size_t)(nseg + 1) * 8));
   KHIP_TRY(S.scap.ensure((size_t)(nseg + 1) * 8));
   KHIP_TRY(S.fin.ensure((size_t)(nseg + 1) * 8));
   KHIP_TRY(S.fin_pre.ensure((size_t)(nseg + 1) * 8));
   hipLaunchKernelGGL(k_sess_setn, dim3(1), dim3(1), 0, st, S.nseg.as<int>(), nseg);
-  KHIP_TRY(cub_call(S.tmp, st, [&](void* p, size_t& b) {
-    return hipcub::DeviceScan::ExclusiveSum(p, b, S.ucnt.as<int>(), S.useg.as<int64_t>(), nseg, st);
-  }));
   const uint64_t* store = S.rows.as<uint64_t>();
   const int64_t ns = S.n;
   if (nseg > 0)
     hipLaunchKernelGGL(k_sess_bounds, dim3(ceil_div(nseg, 256)), dim3(256), 0, st, store, ns, sw, S.ukeys.as<int64_t>(),
                      S.ucnt.as<int>(), S.nseg.as<int>(), S.s0.as<int64_t>(), S.cap.as<int64_t>());
-  KHIP_TRY(cub_call(S.tmp, st, [&](void* p, size_t& b) {
-    return hipcub::DeviceScan::ExclusiveSum(p, b, S.cap.as<int64_t>(), S.scap.as<int64_t>(), nseg, st);
-  }));
+  KHIP_TRY((ksort::scan_excl<int64_t, int64_t>(st, S.tmp, S.cap.as<int64_t>(), S.scap.as<int64_t>(), nseg, false,
+                                                 nullptr)));
   const int64_t scr = ns + n;  // total scratch rows >= sum of capacities
   KHIP_TRY(S.srow.ensure((size_t)scr * sw * 8));
   KHIP_TRY(S.sfl.ensure((size_t)scr));
@@ -733,7 +773,8 @@ khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   if (nseg > 0)
     hipLaunchKernelGGL(k_sess_apply, dim3(ceil_div(nseg, 64)), dim3(64), 0, st, q, store, S.ukeys.as<int64_t>(),
                      S.ucnt.as<int>(), S.useg.as<int64_t>(), S.nseg.as<int>(), S.s0.as<int64_t>(), S.cap.as<int64_t>(),
-                     S.scap.as<int64_t>(), v_out, S.gath.as<longlong2>(), cols,
+                     S.scap.as<int64_t>(), v_out, packed ? nullptr : S.gath.as<longlong2>(),
+                     packed ? S.gath.as<uint64_t>() : nullptr, tbase, cols,
                      a->stream_time.as<int64_t>(), S.srow.as<uint64_t>(), S.sfl.as<uint8_t>(), S.trow.as<uint64_t>(),
                      S.fin.as<int64_t>(), keep_changes ? S.crow.as<uint64_t>() : nullptr,
                      keep_changes ? S.ctomb.as<uint8_t>() : nullptr, S.ctr.as<unsigned long long>(), keep_changes ? 1 : 0,
@@ -745,15 +786,12 @@ khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   if (ns) {
     hipLaunchKernelGGL(k_sess_keep, dim3(ceil_div(ns, 256)), dim3(256), 0, st, store, ns, sw, S.ukeys.as<int64_t>(),
                        S.nseg.as<int>(), a->stream_time.as<int64_t>(), a->retention, S.keep.as<int>());
-    KHIP_TRY(cub_call(S.tmp, st, [&](void* p, size_t& b) {
-      return hipcub::DeviceScan::ExclusiveSum(p, b, S.keep.as<int>(), S.keep_pre.as<int>(), (int)ns, st);
-    }));
+    KHIP_TRY((ksort::scan_excl<int, int>(st, S.tmp, S.keep.as<int>(), S.keep_pre.as<int>(), ns, false, nullptr)));
   }
   // fin_pre[nseg] = total rewritten rows (inclusive end) via a scan over nseg + 1 entries
   KHIP_TRY_HIP(hipMemsetAsync(S.fin.as<int64_t>() + nseg, 0, 8, st));
-  KHIP_TRY(cub_call(S.tmp, st, [&](void* p, size_t& b) {
-    return hipcub::DeviceScan::ExclusiveSum(p, b, S.fin.as<int64_t>(), S.fin_pre.as<int64_t>(), nseg + 1, st);
-  }));
+  KHIP_TRY((ksort::scan_excl<int64_t, int64_t>(st, S.tmp, S.fin.as<int64_t>(), S.fin_pre.as<int64_t>(), nseg + 1, false,
+                                                 nullptr)));
   int64_t tail[2] = {0, 0};
   int kept_tail[2] = {0, 0};
   KHIP_TRY_HIP(hipMemcpyAsync(&tail[0], S.fin_pre.as<int64_t>() + nseg, 8, hipMemcpyDeviceToHost, st));

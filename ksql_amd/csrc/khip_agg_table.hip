@@ -19,7 +19,7 @@
 // Per push (all on the handle's stream):
 //   k_tagg_range   the push's PRIMARY KEY range (per-block partials, one reducing workgroup)
 //   k_tagg_keys    sort key = PRIMARY KEY id − kmin (dropped rows sort last), value = row; counts
-//   hipcub radix sort over the range's bits only (stable: a key's rows keep their arrival order)
+//   radix sort over the range's bits only (khip_sort.hpp; stable: a key's rows keep their arrival order)
 //   k_tagg_apply   one thread per distinct PRIMARY KEY (segment leader): find-or-claim its source
 //                  slot (claim references the sorted position: no spin), then replay its rows in
 //                  order — undo the previous row (-1 / -x) from its group, apply the new row (+1 /
@@ -29,12 +29,11 @@
 //                  are order-dependent only by rounding.
 //   k_tagg_grp_finalize  this push's group claims → resident groups (the claimed slots only)
 //   k_tagg_src_finalize  source claims → resident keys
-#include <hipcub/hipcub.hpp>
-
 #include <algorithm>
 #include <vector>
 
 #include "khip_agg_internal.hpp"
+#include "khip_sort.hpp"
 #include "khip_util.hpp"
 
 namespace khip {
@@ -498,15 +497,6 @@ static int tgrid(int64_t work, int cap_blocks = 8192) {
   return (int)std::min<int64_t>(ceil_div(std::max<int64_t>(work, 1), 256), cap_blocks);
 }
 
-template <class F>
-static khip_status tcub(DevBuf& tmp, F&& f) {
-  size_t bytes = 0;
-  if (f(nullptr, bytes) != hipSuccess) return fail(KHIP_E_DEVICE, "hipcub size query failed");
-  KHIP_TRY(tmp.ensure(std::max<size_t>(bytes, 16)));
-  if (f(tmp.p, bytes) != hipSuccess) return fail(KHIP_E_DEVICE, "hipcub call failed");
-  return KHIP_OK;
-}
-
 static khip_status src_alloc(khip_agg* a, DevBuf& buf, int64_t cap) {
   TaggState& T = a->tagg;
   KHIP_TRY(buf.ensure((size_t)cap * T.src_sw * 8));
@@ -584,10 +574,7 @@ khip_status tagg_push(khip_agg* a, int64_t n, const int64_t* gkeys, const int64_
   uint64_t* kout = T.skey2.as<uint64_t>();
   uint32_t* vin = T.sidx.as<uint32_t>();
   uint32_t* vout = T.sidx2.as<uint32_t>();
-  const int ni = (int)n;
-  KHIP_TRY(tcub(T.tmp, [&](void* p, size_t& b) {
-    return hipcub::DeviceRadixSort::SortPairs(p, b, kin, kout, vin, vout, ni, 0, end_bit, st);
-  }));
+  KHIP_TRY(ksort::sort_pairs<uint32_t>(st, T.tmp, T.tmp2, kin, kout, vin, vout, n, end_bit));
   TaggArgs A{};
   A.p = a->ap;
   A.table = a->table.as<uint64_t>();

@@ -282,3 +282,44 @@ def test_sessions_key_range_edges(prod, orc):
         assert_snap_equal(g.snapshot(), o.snapshot(), g.desc, ABS_SUM, CNT_DBL)
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("count_only", [True, False])
+def test_sessions_time_span_edges(prod, orc, count_only):
+    """Replay records are packed to 8 bytes relative to the push's time base (smallest accepted ts,
+    or the stream time before the push when smaller) when the push's times span < 2^32 - 16 ms,
+    and kept at 16 bytes otherwise: pushes on both sides of that boundary, a push entirely below
+    the stream time (late), dropped rows before the first accepted one, with and without argument
+    columns (the sort carries the packed record itself, or row indices and a gather)."""
+    rng = np.random.default_rng(78)
+    aggs = [("COUNT_STAR", -1)] if count_only else ALL_AGGS
+    kw = dict(window_kind="SESSION", size_ms=5_000, grace_ms=2 ** 40, key_type="INT64",
+              col_types=[] if count_only else COLS, aggs=aggs)
+    g = abi.AggHandle(prod, abi.make_agg_desc(**dict(kw, flags=abi.FLAG_CHANGELOG)))
+    o = abi.AggHandle(orc, abi.make_agg_desc(**kw))
+    edge = 2 ** 32 - 17
+
+    def batch(ts, keys=None, key_valid=None):
+        ts = np.asarray(ts, np.int64)
+        m = len(ts)
+        keys = rng.integers(0, 6, m) if keys is None else np.asarray(keys, np.int64)
+        cols = [] if count_only else [rng.integers(-9, 9, m).astype(np.int32), rng.integers(-9, 9, m),
+                                        rng.random(m), rng.random(m)]
+        return abi.HostBatch(ts, keys=keys, key_valid=key_valid, cols=cols)
+
+    base = 1_000_000
+    pushes = [
+        batch([base + 5, base, base + 3, -1, base + 7000]),                     # packed, base = tmin
+        batch([base + 1000, base + edge - 1000, base + 2000]),                   # span just inside
+        batch([base, base + edge + 1000, base + 10]),                            # span just outside
+        batch(rng.integers(base, base + 3 * 2 ** 32, 3000)),                     # wide, many records
+        batch([7, 3, 9, 5, 1]),                                                  # all below stream time
+        batch([base + 3 * 2 ** 32 + 1, base + 3 * 2 ** 32 + 9], key_valid=[False, True]),  # dropped first
+        batch(rng.integers(base + 3 * 2 ** 32, base + 3 * 2 ** 32 + 60_000, 2000)),
+    ]
+    for b in pushes:
+        assert g.push(b) == o.push(b)
+        _assert_changes_equal(g.changes(), o.changes(), g.desc)
+        assert_snap_equal(g.snapshot(), o.snapshot(), g.desc, ABS_SUM, CNT_DBL)
+    g.close()
+    o.close()
