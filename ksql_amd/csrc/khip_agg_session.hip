@@ -514,6 +514,32 @@ __device__ __forceinline__ int64_t sess_replay(const SessParams& q, int64_t key,
   return kept;
 }
 
+// The wave's keys' row runs copied with every lane busy: lane k's run is `words` words from
+// src + soff to dst + doff; the runs are laid end to end and each word finds its run by a binary
+// search over the lanes' inclusive prefix (consecutive words of a run: consecutive addresses).
+__device__ __forceinline__ void wave_copy_runs(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst,
+                                               int64_t soff, int64_t doff, int64_t words) {
+  const int lane = threadIdx.x & 63;
+  int64_t incl = words;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  const int64_t W = __shfl(incl, 63, 64);
+  for (int64_t x0 = 0; x0 < W; x0 += 64) {  // uniform trip count: every lane takes part in the shuffles
+    const int64_t x = x0 + lane;
+    int lo = 0;
+#pragma unroll
+    for (int step = 32; step; step >>= 1)
+      if (__shfl(incl, lo + step - 1, 64) <= x) lo += step;
+    lo = lo > 63 ? 63 : lo;
+    const int64_t e = __shfl(incl, lo, 64) - __shfl(words, lo, 64);
+    const int64_t so = __shfl(soff, lo, 64), d = __shfl(doff, lo, 64);
+    if (x < W) dst[d + (x - e)] = src[so + (x - e)];
+  }
+}
+
 // Scratch budget of one wave's keys in LDS (rows of sw words + 1 flag byte each); waves whose
 // keys need more replay in HBM scratch.  The records are read from HBM by each lane (a key's
 // records are contiguous, and the wave's keys are neighbours: their lines are shared through L1),
@@ -563,13 +589,9 @@ __global__ __launch_bounds__(64) void k_sess_apply(SessParams q, const uint64_t*
       fin[j] = kept;
     }
     __syncthreads();
-    // the keys' final rows → HBM scratch (at scap), one key at a time across the wave's lanes
-    const int64_t off = mine ? scap[j] - C0 : 0, words = mine ? kept * sw : 0;
-    const int nk = (int)(jl - j0 + 1);
-    for (int k = 0; k < nk; k++) {
-      const int64_t o = __shfl(off, k, 64), w = __shfl(words, k, 64);
-      for (int64_t x = lane; x < w; x += 64) srow[(C0 + o) * sw + x] = lrow[o * sw + x];
-    }
+    // the keys' final rows → HBM scratch (at scap), the wave's runs flattened over its lanes
+    const int64_t off = mine ? scap[j] - C0 : 0;
+    wave_copy_runs(lrow, srow, off * sw, (C0 + off) * sw, mine ? kept * sw : 0);
   } else if (mine) {
     const int64_t base = scap[j], r0 = useg[j];
     kept = sess_replay(q, ukeys[j], store + s0[j] * sw, cap[j] - ucnt[j], g ? g + r0 : nullptr, g8 ? g8 + r0 : nullptr, tbase,
@@ -616,8 +638,8 @@ __global__ __launch_bounds__(256) void k_sess_scatter_store(const uint64_t* __re
   row_copy(out + ((int64_t)keep_pre[i] + fin_pre[p]) * sw, s, sw);
 }
 
-// The rewritten keys' sessions into the new store: one wave per 64 batch keys, the key's rows
-// copied by the wave's lanes (coalesced) instead of by one thread.
+// The rewritten keys' sessions into the new store: one wave per 64 batch keys, their row runs
+// copied with every lane of the wave busy (wave_copy_runs).
 __global__ __launch_bounds__(256) void k_sess_scatter_seg(const uint64_t* __restrict__ store, int64_t ns, int sw,
                                                           const int* __restrict__ keep_pre,
                                                           const int* __restrict__ keep, const int64_t* __restrict__ ukeys,
@@ -637,11 +659,7 @@ __global__ __launch_bounds__(256) void k_sess_scatter_seg(const uint64_t* __rest
     src = scap[jl] * sw;
     words = fin[jl] * sw;
   }
-  const int nk = (int)(nseg - j0 < 64 ? nseg - j0 : 64);
-  for (int k = 0; k < nk; k++) {
-    const int64_t d = __shfl(dst, k, 64), s = __shfl(src, k, 64), w = __shfl(words, k, 64);
-    for (int64_t x = lane; x < w; x += 64) out[d + x] = srow[s + x];
-  }
+  wave_copy_runs(srow, out, src, dst, words);
 }
 
 // ------------------------------------------------------------------ host side

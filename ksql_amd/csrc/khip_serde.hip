@@ -20,6 +20,7 @@
 
 #include "khip_util.hpp"
 #include "khip_numparse.hpp"
+#include "khip_upper.inc"
 
 namespace khip {
 
@@ -184,11 +185,133 @@ __device__ int64_t json_skip(const uint8_t* p, int64_t i, int64_t n, Tok* t) {
   return j;
 }
 
+// Case-insensitive field names: Java's String.toUpperCase() (default, non-tr/az/lt locale: the
+// full unconditional Unicode mapping, e.g. "straße" → "STRASSE", "ǆ" → "Ǆ"), through the table
+// tools/gen_upper.py generates (khip_upper.inc: the non-ASCII code points that change).
+__constant__ uint32_t kUpperDev[KHIP_UPPER_N * 4] = KHIP_UPPER_TABLE;
+static const uint32_t kUpperHost[KHIP_UPPER_N * 4] = KHIP_UPPER_TABLE;
+
+__host__ __device__ inline uint8_t up(uint8_t c) { return c >= 'a' && c <= 'z' ? c - 32 : c; }
+
+// One UTF-8 code point at s[i..n): its length, or 0 when the bytes are not well-formed.
+__host__ __device__ inline int utf8_dec(const uint8_t* s, int n, int i, uint32_t* cp) {
+  const uint8_t c = s[i];
+  int l = c >= 0xF0 ? 4 : c >= 0xE0 ? 3 : c >= 0xC0 ? 2 : 0;
+  if (!l || c >= 0xF8 || i + l > n) return 0;
+  uint32_t v = c & (0x7F >> l);
+  for (int k = 1; k < l; k++) {
+    if ((s[i + k] & 0xC0) != 0x80) return 0;
+    v = (v << 6) | (s[i + k] & 0x3F);
+  }
+  if ((l == 2 && v < 0x80) || (l == 3 && v < 0x800) || (l == 4 && (v < 0x10000 || v > 0x10FFFF))) return 0;
+  if (v >= 0xD800 && v < 0xE000) return 0;
+  *cp = v;
+  return l;
+}
+
+__host__ __device__ inline int utf8_enc(uint32_t cp, uint8_t* o) {
+  if (cp < 0x80) { o[0] = (uint8_t)cp; return 1; }
+  if (cp < 0x800) { o[0] = (uint8_t)(0xC0 | (cp >> 6)); o[1] = (uint8_t)(0x80 | (cp & 0x3F)); return 2; }
+  if (cp < 0x10000) {
+    o[0] = (uint8_t)(0xE0 | (cp >> 12));
+    o[1] = (uint8_t)(0x80 | ((cp >> 6) & 0x3F));
+    o[2] = (uint8_t)(0x80 | (cp & 0x3F));
+    return 3;
+  }
+  o[0] = (uint8_t)(0xF0 | (cp >> 18));
+  o[1] = (uint8_t)(0x80 | ((cp >> 12) & 0x3F));
+  o[2] = (uint8_t)(0x80 | ((cp >> 6) & 0x3F));
+  o[3] = (uint8_t)(0x80 | (cp & 0x3F));
+  return 4;
+}
+
+// Upper-case mapping of a non-ASCII code point: up to three code points (unused = 0).
+__host__ __device__ inline void upper_cp(const uint32_t* tab, uint32_t cp, uint32_t m[3]) {
+  int lo = 0, hi = KHIP_UPPER_N;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (tab[mid * 4] < cp) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo < KHIP_UPPER_N && tab[lo * 4] == cp) {
+    m[0] = tab[lo * 4 + 1];
+    m[1] = tab[lo * 4 + 2];
+    m[2] = tab[lo * 4 + 3];
+  } else {
+    m[0] = cp;
+    m[1] = m[2] = 0;
+  }
+}
+
+// toUpperCase(a) == b, byte for byte (a, b UTF-8; a malformed a matches nothing).
+__host__ __device__ inline bool upper_equals(const uint32_t* tab, const uint8_t* a, int na, const uint8_t* b, int nb) {
+  int j = 0;
+  for (int i = 0; i < na;) {
+    if (a[i] < 0x80) {
+      if (j >= nb || b[j] != up(a[i])) return false;
+      i++;
+      j++;
+      continue;
+    }
+    uint32_t cp, m[3];
+    const int l = utf8_dec(a, na, i, &cp);
+    if (!l) return false;
+    i += l;
+    upper_cp(tab, cp, m);
+    for (int k = 0; k < 3 && (k == 0 || m[k]); k++) {
+      uint8_t e[4];
+      const int el = utf8_enc(m[k], e);
+      for (int x = 0; x < el; x++, j++)
+        if (j >= nb || b[j] != e[x]) return false;
+    }
+  }
+  return j == nb;
+}
+
+static std::string upper_utf8_host(const char* s) {
+  const int n = (int)strlen(s);
+  const uint8_t* a = (const uint8_t*)s;
+  std::string out;
+  for (int i = 0; i < n;) {
+    if (a[i] < 0x80) {
+      out.push_back((char)up(a[i++]));
+      continue;
+    }
+    uint32_t cp, m[3];
+    const int l = utf8_dec(a, n, i, &cp);
+    if (!l) {  // malformed: kept as is (matches no ksql field name upper-cased by Java)
+      out.push_back((char)a[i++]);
+      continue;
+    }
+    i += l;
+    upper_cp(kUpperHost, cp, m);
+    for (int k = 0; k < 3 && (k == 0 || m[k]); k++) {
+      uint8_t e[4];
+      out.append((const char*)e, (size_t)utf8_enc(m[k], e));
+    }
+  }
+  return out;
+}
+
+__device__ __forceinline__ bool hex4(const uint8_t* p, int64_t n, int64_t i, uint32_t* u) {
+  if (i + 4 > n) return false;
+  uint32_t v = 0;
+  for (int k = 0; k < 4; k++) {
+    const uint8_t h = p[i + k];
+    const int d = h >= '0' && h <= '9' ? h - '0' : (h >= 'a' && h <= 'f' ? h - 'a' + 10 : (h >= 'A' && h <= 'F' ? h - 'A' + 10 : -1));
+    if (d < 0) return false;
+    v = v * 16 + (uint32_t)d;
+  }
+  *u = v;
+  return true;
+}
+
 // JSON string unescape into buf (cap bytes); false on a bad escape or overflow.
 __device__ bool json_unescape(const uint8_t* p, int64_t n, uint8_t* buf, int cap, int* outn) {
   int m = 0;
   for (int64_t i = 0; i < n; i++) {
     uint32_t c = p[i];
+    bool cp = false;  // c is a code point from a \\u escape (else one raw byte)
     if (c == '\\') {
       if (++i >= n) return false;
       switch (p[i]) {
@@ -201,29 +324,40 @@ __device__ bool json_unescape(const uint8_t* p, int64_t n, uint8_t* buf, int cap
         case 'r': c = 13; break;
         case 't': c = 9; break;
         case 'u': {
-          if (i + 4 >= n) return false;
-          uint32_t u = 0;
-          for (int k = 1; k <= 4; k++) {
-            const uint8_t h = p[i + k];
-            u = u * 16 + (h >= '0' && h <= '9' ? h - '0' : (h >= 'a' && h <= 'f' ? h - 'a' + 10 : (h >= 'A' && h <= 'F' ? h - 'A' + 10 : 99)));
-            if (u > 0xFFFF) return false;
-          }
+          uint32_t u;
+          if (!hex4(p, n, i + 1, &u)) return false;
           i += 4;
-          if (u >= 0x80) return false;  // non-ASCII never forms a number; names are ASCII here
+          if (u >= 0xD800 && u < 0xDC00) {  // a surrogate pair → one supplementary code point
+            uint32_t lo;
+            if (i + 2 >= n || p[i + 1] != '\\' || p[i + 2] != 'u' || !hex4(p, n, i + 3, &lo) || lo < 0xDC00 ||
+                lo >= 0xE000)
+              return false;  // a lone surrogate (matches no UTF-8 name, forms no number)
+            i += 6;
+            u = 0x10000 + ((u - 0xD800) << 10) + (lo - 0xDC00);
+          } else if (u >= 0xDC00 && u < 0xE000) {
+            return false;
+          }
           c = u;
+          cp = true;
           break;
         }
         default: return false;
       }
     }
-    if (m >= cap) return false;
-    buf[m++] = (uint8_t)c;
+    if (!cp || c < 0x80) {
+      if (m >= cap) return false;
+      buf[m++] = (uint8_t)c;
+    } else {  // \u escapes of non-ASCII code points, as UTF-8 (raw bytes >= 0x80 pass through above)
+      uint8_t e[4];
+      const int el = utf8_enc(c, e);
+      if (m + el > cap) return false;
+      for (int k = 0; k < el; k++) buf[m++] = e[k];
+    }
   }
   *outn = m;
   return true;
 }
 
-__device__ __forceinline__ uint8_t up(uint8_t c) { return c >= 'a' && c <= 'z' ? c - 32 : c; }
 
 // Jackson reads a JSON number token with a fraction or an exponent as a BigDecimal
 // (USE_BIG_DECIMAL_FOR_FLOATS, KsqlJsonDeserializer.java:68-70); JsonSerdeUtils.toInteger /
@@ -569,7 +703,8 @@ __global__ __launch_bounds__(256) void k_serde_decode(SerdeParams q, int64_t n, 
           const int64_t vend = json_skip(p, j, vn, &vt);
           if (vend < 0) { ok = false; break; }
           j = vend;
-          // field name: exact match wins, else the upper-cased name (last such field)
+          // field name: exact match wins, else the upper-cased name (last such field; Unicode
+          // upper case as Java's toUpperCase, KsqlJsonDeserializer.java:301-306)
           uint8_t nb[SD_NAME_BYTES];
           int nl = 0;
           const uint8_t* kp = p + kt.off;
@@ -581,15 +716,10 @@ __global__ __launch_bounds__(256) void k_serde_decode(SerdeParams q, int64_t n, 
           }
           if (nl >= 0) {
             for (int f = 0; f < q.n_fields; f++) {
-              if (q.name_len[f] == nl) {
-                bool same = true, same_up = true;
-                for (int k = 0; k < nl; k++) {
-                  same &= kp[k] == q.name[f][k];
-                  same_up &= up(kp[k]) == q.name[f][k];
-                }
-                if (same) ex[f] = vt;
-                else if (same_up) ci[f] = vt;
-              }
+              bool same = q.name_len[f] == nl;
+              for (int k = 0; same && k < nl; k++) same = kp[k] == q.name[f][k];
+              if (same) ex[f] = vt;
+              else if (upper_equals(kUpperDev, kp, nl, q.name[f], q.name_len[f])) ci[f] = vt;
             }
           }
           while (j < vn && json_ws(p[j])) j++;
@@ -761,7 +891,7 @@ khip_status khip_serde_create(const khip_serde_desc* d, khip_serde** out) {
   }
   if (d->value_format == KHIP_FMT_AVRO) {
     // writer field → ksql field: the field of the same name, else of the upper-cased name
-    // (ConnectDataTranslator.toKsqlStruct: Java's toUpperCase; ASCII letters here); validateSchema
+    // (ConnectDataTranslator.toKsqlStruct: Java's toUpperCase, Unicode as above); validateSchema
     // (:123-146) runs on every mapped field of every record, so one incompatible type fails them all
     q.avro_id = d->avro_schema_id;
     q.avro_nw = d->avro_n_fields;
@@ -774,9 +904,7 @@ khip_status khip_serde_create(const khip_serde_desc* d, khip_serde** out) {
         delete s;
         return fail(KHIP_E_UNSUPPORTED, "AVRO writer field: primitive type, plain or a union with null");
       }
-      std::string up(wn);
-      for (char& ch : up)
-        if (ch >= 'a' && ch <= 'z') ch = (char)(ch - 32);
+      const std::string up = upper_utf8_host(wn);  // (Avro names are ASCII; same rule as JSON)
       int fx = -1, fu = -1;
       for (int f = 0; f < d->n_fields; f++) {
         const std::string kn(d->field_names[f]);

@@ -390,3 +390,41 @@ def test_avro_incompatible_writer_type_fails_every_record(prod):
     assert nerr == experr == 2
     _check(sd.columns(d, ["INT32", "INT64"]), exp, fields, ["INT32", "INT64"])
     sd.close()
+
+
+# ---- case-insensitive field names beyond ASCII (Java's String.toUpperCase: full Unicode mapping)
+
+UNI_FIELDS = [("STRASSE", "INT64", 0), ("ǄX", "INT64", 1), ("ΣΊΣΥΦΟΣ", "INT64", 2), ("CAFÉ", "DOUBLE", 3),
+              ("𐐀B", "INT64", 4), ("FFʼN", "INT32", 5)]
+UNI_NAMES = {"STRASSE": ["STRASSE", "straße", "Strasse", "STRAßE", "strasse"],
+             "ǄX": ["ǄX", "ǆx", "ǅX", "ǆX"], "ΣΊΣΥΦΟΣ": ["ΣΊΣΥΦΟΣ", "σίσυφος", "Σίσυφος", "σίσυφοσ"],
+             "CAFÉ": ["CAFÉ", "café", "Café", "cafe"], "𐐀B": ["𐐀B", "𐐨b", "𐐨B"], "FFʼN": ["FFʼN", "ﬀŉ", "ffŉ"]}
+
+
+def test_json_field_names_unicode_upper_case(prod):
+    """A JSON field matches its column exactly, else through toUpperCase (KsqlJsonDeserializer.java:
+    301-306): "straße" → STRASSE, "ǆx" → ǄX, Greek final sigma, "ﬀŉ" → FFʼN (length-changing maps),
+    a supplementary-plane letter; "cafe" is not "CAFÉ".  Checked against tests/serde_ref.py, whose
+    matching is Python's str.upper() (the same unconditional Unicode mapping)."""
+    rng = random.Random(31)
+    vals = []
+    for i in range(300):
+        parts = []
+        for name, t, _ in UNI_FIELDS:
+            if rng.random() < 0.15:
+                continue
+            v = "%.3f" % rng.uniform(-9, 9) if t == "DOUBLE" else str(rng.randrange(-1000, 1000))
+            parts.append('%s: %s' % (json.dumps(rng.choice(UNI_NAMES[name]), ensure_ascii=rng.random() < 0.3), v))
+        rng.shuffle(parts)
+        vals.append(("{" + ", ".join(parts) + "}").encode())
+    keys = [struct.pack(">q", i) for i in range(len(vals))]
+    out_types = ["INT64", "INT64", "INT64", "DOUBLE", "INT64", "INT32"]
+    sd = abi.SerdeHandle(prod, "JSON", UNI_FIELDS, key_type="INT64")
+    d, nerr = sd.decode(np.arange(len(vals), dtype=np.int64), keys, vals)
+    exp, experr = serde_ref.decode("JSON", UNI_FIELDS, "INT64", keys, vals)
+    assert nerr == experr == 0
+    got = sd.columns(d, out_types)
+    _check(got, exp, UNI_FIELDS, out_types)
+    assert got["valid"][0].any() and not all(got["valid"][3])  # matches through upper case; "cafe" misses
+    sd.close()
+
