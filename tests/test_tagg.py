@@ -168,6 +168,33 @@ def test_tagg_key_range_edges(prod, orc):
 
 
 @pytest.mark.gpu
+def test_tagg_group_capacity_growth(prod, orc):
+    """The group table grows ahead of a push by min(rows, span of the push's GROUP BY keys) new
+    groups (8 slots per group): pushes whose groups are mostly new — a narrow span with many rows,
+    a wide random span, distinct dense keys with both BIGINT extremes — from a tiny initial table."""
+    rng = np.random.default_rng(11)
+    lo, hi = np.iinfo(np.int64).min, np.iinfo(np.int64).max
+    batches = []
+    for p in range(12):
+        m = 3000
+        if p % 3 == 0:
+            grp = 100_000 * p + rng.integers(0, 500, m)
+        elif p % 3 == 1:
+            grp = rng.integers(lo, hi, m)
+        else:
+            grp = np.concatenate([[lo, hi], 1_000_000 * p + np.arange(m - 2)])
+        c2 = rng.normal(size=m)
+        b = abi.HostBatch(np.arange(m, dtype=np.int64) + p * m, keys=np.asarray(grp, np.int64),
+                          row_valid=rng.random(m) > 0.05,
+                          cols=[rng.integers(-9, 9, m).astype(np.int32), rng.integers(-9, 9, m), c2])
+        batches.append((b, {"src_keys": rng.integers(0, 5000, m)}, np.abs(c2)))
+    scale = sum(float(x.sum()) for _, _, x in batches) * 4
+    (g, _), (o, _) = (_run(lib, batches, False) for lib in (prod, orc))
+    assert o["n"] > 10_000
+    _assert_same(g, o, scale)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("ncols", [0, 1, 2])
 @pytest.mark.parametrize("utf8_src", [False, True])
 def test_tagg_narrow_rows_vs_oracle(prod, orc, ncols, utf8_src):
