@@ -433,12 +433,28 @@ def bench_sink_json(args, lib, rank, world, local):
     bpr = 8 + 8 + 8 + 8 + 1 + 16 + vl / n + 2 * 8 + 1
     roof = roofline(bpr * n, ms_step, None, None, load_traffic(args.traffic_json, "sink_json", n), bpr,
                     kernel="khip_sink_encode (k_sink_measure + scans + k_sink_write)")
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        # the CPU restatement of the serializers (tests/sink_ref.py) on a bounded sample
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import sink_ref
+        m = min(n, 2_000_000)
+        kk, ww, cc = (x[:m].cpu().numpy().tolist() for x in (key, ws, cnt))
+        kc, vc = [("CARD_NUMBER", "INT64")], [("KSQL_COL_0", "INT64")]
+        t0 = time.perf_counter()
+        recs = [(sink_ref.encode_key("KAFKA", kc, [k]) + sink_ref.window_suffix("TUMBLING", w, w + 5000),
+                 sink_ref.encode_value("JSON", vc, [c])) for k, w, c in zip(kk, ww, cc)]
+        dt = time.perf_counter() - t0
+        assert len(recs[0][0]) == 16
+        cpu = {"value": m / dt, "unit": "records/s", "cores": 1, "kind": "port",
+               "sample": "%d of the rows, tests/sink_ref.py per row (CPython)" % m, "cpu": cpu_info(),
+               "label": "CPU restatement of the KAFKA key / JSON value serializers, not the JVM reference"}
     line("records/sec, changelog rows -> sink records (TimeWindowed KAFKA BIGINT key, JSON value)",
          world * n * args.steps / elapsed, world, args, ms_step, "u8",
          "synthetic C2-shaped changelog rows (splitmix64), device-resident columns",
          {"workload": "sink_json", "rows_per_gpu": n, "key": "KAFKA BIGINT + 8-byte window start",
           "value": "JSON {\"KSQL_COL_0\": BIGINT}", "value_bytes_per_row": vl / n,
-          "parallelism": "rows x%d" % world}, roof, None)
+          "parallelism": "rows x%d" % world}, roof, cpu)
 
 
 def bench_table_agg(args, lib, rank, world, local):
@@ -942,7 +958,7 @@ def bench_join(args, lib, rank, world, local):
     if rank != 0:
         return
     ms_step = elapsed * 1000.0 / args.steps
-    roof = roofline(BYTES_PER_PROBE_C4 * n, ms_step, None, None, load_traffic(args.traffic_json, "clickstream_join", n),
+    roof = roofline(BYTES_PER_PROBE_C4 * n, ms_step, None, None, load_traffic(args.traffic_json, "clickstream_join" + ("_sparse_ids" if args.sparse_ids else ""), n),
                     BYTES_PER_PROBE_C4, kernel="khip_table_probe_device (probe kernels) + emitted count",
                     extra={"stream_copy_GBps": stream_copy_gbs(), "table": info,
                            "random_gather_rows_per_s": random_gather_rows_per_s(info["table_bytes"])})

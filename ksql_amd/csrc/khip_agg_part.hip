@@ -1409,6 +1409,7 @@ struct MergeParams {
   FastDiv32 fd32;
   int32_t list_off;  // byte offset of the LDS list of the entries the item's records claimed (u16 x H)
   int32_t fan;       // most windows a record can fall in (ceil(size / advance); 1 without windows)
+  int32_t pane;      // HOPPING with size % advance == 0 and fan <= MG_FB: pane aggregation allowed
 };
 
 // Append the claimed entries of the wave's lanes to the item's list (one LDS atomic per wave);
@@ -1710,6 +1711,12 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
     else if (t.kind == OP_MAX) oc_max = t.off;
   }
   const bool dbl_col = oc_col >= 0 && q.col_type[oc_col < 0 ? 0 : oc_col] == KHIP_TYPE_DOUBLE;
+  // Panes (HOPPING, size a multiple of the advance): a record whose windows are all open updates
+  // ONE entry — its pane, the advance-long slice it falls in, identity (key, slice index + PB) —
+  // instead of its F windows; after the records, each pane is folded into its F windows (F updates
+  // per pane instead of per record).  Items of at least one full chunk stride without sub-passes.
+  const bool panes_ok = !CNT1 && q.pane && wr[8] != 0;
+  const int64_t PB = panes_ok ? ((int64_t)1 << (q.log2P - 1)) : 0;
   for (int i = threadIdx.x; i < H + 64; i += NT) mg_clear(smem, ids, rt, otab, q.n_ops, i);
   lds_barrier();
   MG_T(0);
@@ -1717,6 +1724,7 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
     const uint32_t p = it.p;
     const int sbits = it.sbits, sub = it.sub;
     const int64_t rbase = it.rbase, rn = it.rn;
+    const bool pmode = panes_ok && sbits == 0 && rn >= (int64_t)AU * NT;
     const int64_t wnext = w + gridDim.x;
     MgItem nit{};
     if (wnext < nwork) nit = mg_item(work, wnext, pbase, sel, cnt);  // its loads are issued now, used later
@@ -1927,11 +1935,18 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
             uint32_t e[MG_FB];
             bool act[MG_FB], pend[MG_FB];
             const uint64_t hk = (uint64_t)rec[u].x;
+            // every window open (no late offset): the record's pane instead of its windows
+            const bool pr = pmode && (q.meta_word != 2 || ((uint32_t)ext[u].x & 0xFFFFu) == 0u);
 #pragma unroll
             for (int j = 0; j < MG_FB; j++) {
               const int64_t widx = w0[u] + j;
-              act[j] = j < q.fan && widx <= wn[u] && (sbits == 0 || sub_ok(hk, widx * q.adv, sbits, sub));
-              id[j] = act[j] ? ident_of(hk, widx - wbase, q.log2P) : EMPTY_ID;
+              if (pr) {
+                act[j] = j == 0 && w0[u] <= wn[u];
+                id[j] = act[j] ? ident_of(hk, wn[u] - wbase + PB, q.log2P) : EMPTY_ID;
+              } else {
+                act[j] = j < q.fan && widx <= wn[u] && (sbits == 0 || sub_ok(hk, widx * q.adv, sbits, sub));
+                id[j] = act[j] ? ident_of(hk, widx - wbase, q.log2P) : EMPTY_ID;
+              }
               e[j] = act[j] ? mg_slot(id[j], H) : dummy;
             }
 #pragma unroll
@@ -2059,6 +2074,98 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
     MG_T(2);
     // the next item's first chunk is in flight from here on
     if (wnext < nwork) mg_load<AU, NT, R12M, !CNT1>(rawA, extA, srec, nit.rbase, nit.rn, 0, q.rw, wide);
+    if constexpr (!CNT1) {
+      if (pmode && !lovf) {
+        // 1b. fold: each pane into its F windows, whose entries are found or claimed as a record's
+        const int nn0 = nnew;
+        lds_barrier();  // every thread has read nn0 before the fold lists its windows
+        for (int i0 = 0; i0 < nn0; i0 += NT) {  // uniform trip count: the probe loop is convergent
+          const int li = i0 + threadIdx.x;
+          const int pe = li < nn0 ? (int)nl[li] : -1;
+          const uint64_t pid = pe >= 0 ? ids[pe] : EMPTY_ID;
+          const int64_t rel = (int64_t)(pid & ((1ULL << q.log2P) - 1));
+          const bool isp = pid != EMPTY_ID && rel >= PB;
+          const int64_t pw = rel - PB + wbase;  // the pane's slice index = the index of its last window
+          const uint64_t hk = ((uint64_t)p << (64 - q.log2P)) | (pid >> q.log2P);
+          uint64_t id[MG_FB], old[MG_FB];
+          uint32_t e[MG_FB];
+          bool act[MG_FB], pend[MG_FB];
+#pragma unroll
+          for (int j = 0; j < MG_FB; j++) {
+            act[j] = isp && j < q.fan && pw - j >= 0;
+            id[j] = act[j] ? ident_of(hk, pw - j - wbase, q.log2P) : EMPTY_ID;
+            e[j] = act[j] ? mg_slot(id[j], H) : dummy;
+          }
+#pragma unroll
+          for (int j = 0; j < MG_FB; j++) {
+            old[j] = EMPTY_ID;
+            __hip_atomic_compare_exchange_strong(&ids[e[j]], &old[j], id[j], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+#pragma unroll
+          for (int j = 0; j < MG_FB; j++) {
+            pend[j] = act[j] && old[j] != EMPTY_ID && old[j] != id[j];
+            mg_list_append(act[j] && old[j] == EMPTY_ID, e[j], nl, &nnew);
+          }
+          for (int probes = 1;; probes++) {
+            bool anyp = false;
+#pragma unroll
+            for (int j = 0; j < MG_FB; j++) anyp |= pend[j];
+            if (!__ballot(anyp)) break;
+            if (probes >= H) {
+              lovf = 1;
+#pragma unroll
+              for (int j = 0; j < MG_FB; j++) act[j] = false;
+              break;
+            }
+            bool got[MG_FB];
+#pragma unroll
+            for (int j = 0; j < MG_FB; j++) {
+              got[j] = false;
+              if (!pend[j]) continue;
+              e[j] = e[j] + 1 == (uint32_t)H ? 0u : e[j] + 1;
+              uint64_t o2 = EMPTY_ID;
+              __hip_atomic_compare_exchange_strong(&ids[e[j]], &o2, id[j], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+              pend[j] = o2 != EMPTY_ID && o2 != id[j];
+              got[j] = o2 == EMPTY_ID;
+            }
+#pragma unroll
+            for (int j = 0; j < MG_FB; j++) mg_list_append(got[j], e[j], nl, &nnew);
+          }
+          if (!isp) continue;
+          const uint32_t prt = rt[pe];
+#pragma unroll
+          for (int j = 0; j < MG_FB; j++) {
+            if (!act[j]) continue;
+            const uint32_t we = e[j];
+            __hip_atomic_fetch_max(&rt[we], prt, WG_RLX);
+            for (int o = 0; o < q.n_ops; o++) {
+              const MgOp op = otab[o];
+              if (op.kind == OP_INC || op.kind == OP_INC_VALID) {
+                __hip_atomic_fetch_add(&mg_plane<uint32_t>(smem, op.off)[we], mg_plane<uint32_t>(smem, op.off)[pe], WG_RLX);
+                continue;
+              }
+              KLDS int64_t* pl = mg_plane<int64_t>(smem, op.off);
+              const int64_t v = pl[pe];
+              switch (op.kind) {
+                case OP_ADD_I64: __hip_atomic_fetch_add((KLDS uint64_t*)&pl[we], (uint64_t)v, WG_RLX); break;
+                case OP_ADD_F64: {
+                  double d;
+                  __builtin_memcpy(&d, &v, 8);
+                  __hip_atomic_fetch_add((KLDS double*)&pl[we], d, WG_RLX);
+                  break;
+                }
+                case OP_MIN: __hip_atomic_fetch_min(&pl[we], v, WG_RLX); break;
+                case OP_MAX: __hip_atomic_fetch_max(&pl[we], v, WG_RLX); break;
+                default: break;
+              }
+            }
+          }
+        }
+        lds_barrier();
+      }
+    }
     if (lovf) {  // more groups than the table: retried with 2x sub-passes
       if (threadIdx.x == 0) fail[p] |= 1;
       for (int i = threadIdx.x; i < H; i += NT) mg_clear(smem, ids, rt, otab, q.n_ops, i);
@@ -2082,7 +2189,9 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
     }
     lds_barrier();
     const int nn = nnew;  // read by every thread here; reset after the next barrier
-    for (int i = threadIdx.x; i < nn; i += NT) n_mine += !(rt[nl[i]] & RT_MATCHED) ? 1 : 0;
+    // (pane entries are not rows)
+    for (int i = threadIdx.x; i < nn; i += NT)
+      n_mine += !(rt[nl[i]] & RT_MATCHED) && !(PB && (int64_t)(ids[nl[i]] & ((1ULL << q.log2P) - 1)) >= PB) ? 1 : 0;
     // 3. per-wave row counts → the partition's region range (one atomic per work item)
     const int wave_rows = (int)wave_sum(n_mine);
     if (lane == 0) wsum[wave] = wave_rows;
@@ -2168,7 +2277,8 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge(
       const int li = i0 + lane;
       const int e = li < nn ? (int)nl[li] : H + lane;  // past the list: the lane's dummy entry
       const uint64_t id = li < nn ? ids[e] : EMPTY_ID;
-      const bool isnew = id != EMPTY_ID && !(rt[e] & RT_MATCHED);
+      const bool isnew = id != EMPTY_ID && !(rt[e] & RT_MATCHED) &&
+                         !(PB && (int64_t)(id & ((1ULL << q.log2P) - 1)) >= PB);  // panes are not rows
       const uint64_t b = __ballot(isnew);
       if (isnew) {
         const uint64_t ri = cur + __popcll(b & lt);
@@ -2734,12 +2844,15 @@ __global__ __launch_bounds__(1024) void k_part_wrange(const int64_t* __restrict_
     wr[0] = 0;
     wr[1] = fits;
     wr[4] = merge_allow && fits && span_ok;
+    wr[8] = 0;
     res[0] = INT64_MAX;
     res[1] = INT64_MIN;
     return;
   }
   wr[0] = lo;
   wr[1] = fits && hi - lo < ((int64_t)1 << log2P) - 1;
+  // panes (k_part_merge): pane identities use window indices offset by 2^(log2P - 1)
+  wr[8] = fits && log2P >= 2 && hi - lo < ((int64_t)1 << (log2P - 1)) - 1;
   wr[4] = merge_allow && wr[1] && span_ok;
   res[0] = lo;
   res[1] = hi;
@@ -3309,7 +3422,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   // aggregate kernel (k_part_merge needs the identity and a span below 2^31 ms)
   const PartAggParams q0 = part_params(a);
   const int64_t close0 = (a->windowed && a->host_stream_time >= 0) ? a->host_stream_time - a->grace : INT64_MIN;
-  KHIP_TRY(s.wr.ensure(64));
+  KHIP_TRY(s.wr.ensure(128));
   KHIP_TRY(s.res.ensure(16));
   KHIP_TRY(s.closed_ctr.ensure(8));
   const bool merge_allow = s.mH >= 256 && knob("KHIP_MERGE", 1) != 0;
@@ -3428,6 +3541,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     mq.rt_off = s.rt_off;
     mq.list_off = s.m_list_off;
     mq.fan = a->windowed ? (int32_t)std::min<int64_t>((q0.size + q0.adv - 1) / q0.adv, 1 << 20) : 1;
+    mq.pane = a->windowed && mq.fan > 1 && mq.fan <= MG_FB && q0.size % q0.adv == 0 && knob("KHIP_PANES", 1) ? 1 : 0;
     mq.lds_bytes = s.m_lds;
     mq.init = a->init;
     mq.having = a->having;

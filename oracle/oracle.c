@@ -67,7 +67,7 @@
  *     row per PRIMARY KEY (a tombstone deletes it); each accepted record first undoes the key's
  *     previous row from its group (TableUdaf.undo via KudafUndoAggregator, X/function/udaf/
  *     KudafUndoAggregator.java:29-55: COUNT -1 if non-null, SUM subtracts (wrapping), AVG
- *     {sum - x, count - 1}; E/function/udaf/count/CountKudaf.java:60-65, sum/*SumKudaf.java:44,
+ *     {sum - x, count - 1}; E/function/udaf/count/CountKudaf.java:60-65, sum/(Integer,Long,Double)SumKudaf.java:44,
  *     average/AverageUdaf.java:140-150) when that row had a non-null GROUP BY value, then applies
  *     the new row to its group (created if absent).  Groups are never deleted (count back to zero,
  *     Q/count.json); group row time = max ts of the records touching it.
@@ -1364,7 +1364,7 @@ static khip_status merge_sharded(oracle_agg** shards, int32_t P, const khip_havi
     pthread_join(th[p], NULL);
     m += jobs[p].m;
   }
-  owned_entry* rows = (owned_entry*)malloc(sizeof(owned_entry) * (m + 1));
+  owned_entry* rows = (owned_entry*)calloc((size_t)(m + 1), sizeof(owned_entry));
   int64_t* cur = (int64_t*)calloc((size_t)P, sizeof(int64_t));
   int32_t* heap = (int32_t*)malloc(sizeof(int32_t) * (size_t)P);
   int32_t hn = 0;
