@@ -463,6 +463,59 @@ __host__ __device__ constexpr size_t stage_lds_bytes(int nb, int S) {
   return ((size_t)nb * 16 + 15) / 16 * 16 + (size_t)S * 16;
 }
 
+// stage_step for 32-byte records (rw = 4: key hash, ts, and two more words — meta and one value
+// column, or two values): staged as two 16-byte halves (L.sk/L.sp hold words 0/1, L.sk + S /
+// L.sp + S words 2/3: the carve-up of stage_lds_bytes(nb, 2 * S)), written out per bin as whole
+// 32-byte records in consecutive, coalesced stores.
+template <int U>
+__device__ __forceinline__ void stage_step_w(const int64_t (&hk)[U], const int64_t (&ts)[U], const int64_t (&w2)[U],
+                                             const int64_t (&w3)[U], const bool (&ok)[U], int shift, uint32_t mask,
+                                             int nb, const StageLds& L, uint64_t* __restrict__ srec) {
+  constexpr int S = U * PT_THREADS;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  uint32_t rank[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) rank[u] = ok[u] ? atomicAdd(&L.cnt[stage_bin((uint64_t)hk[u], shift, mask)], 1u) : 0u;
+  lds_barrier();
+  const uint32_t c = t < nb ? L.cnt[t] : 0u;
+  uint32_t incl = c;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) L.wsum[wave] = (int)incl;
+  lds_barrier();
+  uint32_t before = 0, tot = 0;
+  for (int k = 0; k < PT_THREADS / 64; k++) {
+    before += k < wave ? (uint32_t)L.wsum[k] : 0u;
+    tot += (uint32_t)L.wsum[k];
+  }
+  if (t < nb) {
+    L.sbase[t] = before + incl - c;
+    L.gpos[t] = L.cur[t];
+    L.cur[t] += c;
+    L.cnt[t] = 0u;
+  }
+  lds_barrier();
+  longlong2* lo = (longlong2*)L.sk;  // [S] words 0, 1
+  longlong2* hi = lo + S;             // [S] words 2, 3
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if (!ok[u]) continue;
+    const uint32_t i = L.sbase[stage_bin((uint64_t)hk[u], shift, mask)] + rank[u];
+    lo[i] = make_longlong2(hk[u], ts[u]);
+    hi[i] = make_longlong2(w2[u], w3[u]);
+  }
+  lds_barrier();
+  for (uint32_t j = t; j < tot; j += PT_THREADS) {
+    const longlong2 a = lo[j], b = hi[j];
+    const uint32_t bn = stage_bin((uint64_t)a.x, shift, mask);
+    uint64_t* r = srec + ((uint64_t)L.gpos[bn] + (j - L.sbase[bn])) * 4;
+    *(longlong2*)r = a;
+    *(longlong2*)(r + 2) = b;
+  }
+}
+
 __device__ __forceinline__ StageLds stage_carve(char* smem, int nb, int S, int* wsum) {
   StageLds L;
   L.cur = (uint32_t*)smem;
@@ -667,6 +720,64 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
       for (int u = 0; u < U; u++) {
         x[u] = nxx[u];
         k[u] = nxk[u];
+      }
+    }
+  } else if (fast && !NARROW && stage && L.rw == 4) {
+    // 32-byte records through the LDS stage (stage_step_w): each bin's records of a step leave
+    // as one contiguous run of whole records instead of one scattered record per lane; the next
+    // step's key / ts / value loads are in flight during this step's barriers
+    constexpr int WU = U >= 16 ? 4 : 2;
+    constexpr int S = WU * PT_THREADS;
+    const StageLds SL = stage_carve(smem, P, 2 * S, wsum);
+    for (int p = threadIdx.x; p < P; p += PT_THREADS) SL.cnt[p] = 0u;
+    lds_barrier();
+    const int shift = log2P == 0 ? 64 : 64 - log2P;
+    const uint32_t bmask = (uint32_t)(P - 1);
+    const int c2 = L.word_col[2], c3 = L.word_col[3];
+    int64_t x[WU], k[WU], v2[WU], v3[WU], nx[WU], nk[WU], nv2[WU], nv3[WU];
+    auto load_step = [&](int64_t i0, int64_t (&dx)[WU], int64_t (&dk)[WU], int64_t (&d2)[WU], int64_t (&d3)[WU]) {
+#pragma unroll
+      for (int u = 0; u < WU; u++) {
+        int64_t i = i0 + (int64_t)u * PT_THREADS;
+        i = i < end ? i : end - 1;
+        dx[u] = ts[i];
+        dk[u] = keys[i];
+        d2[u] = c2 >= 0 ? load_col_raw(cols, ctypes.t[c2], c2, i) : 0;
+        d3[u] = c3 >= 0 ? load_col_raw(cols, ctypes.t[c3], c3, i) : 0;
+      }
+    };
+    if (base < end) load_step(base + threadIdx.x, x, k, v2, v3);
+    for (int64_t s0 = base; s0 < end; s0 += S) {  // uniform across the block: barriers inside
+      const int64_t i0 = s0 + threadIdx.x;
+      if (s0 + S < end) load_step(i0 + S, nx, nk, nv2, nv3);
+      int64_t hk[WU], w2[WU], w3[WU];
+      bool ok[WU];
+#pragma unroll
+      for (int u = 0; u < WU; u++) {
+        const int64_t i = i0 + (int64_t)u * PT_THREADS;
+        const int64_t ic = i < end ? i : end - 1;
+        ok[u] = i < end && x[u] >= 0 && bit_get(kv, ic) && bit_get(rv, ic);
+        uint32_t vm = 0;
+        for (int c = 0; c < n_cols; c++)
+          if ((L.vcols >> c) & 1u) vm |= (bit_get(cols.valid[c], ic) ? 1u : 0u) << c;
+        w2[u] = L.meta_word == 2 ? (int64_t)(vm << 16) : v2[u];
+        w3[u] = L.meta_word == 3 ? (int64_t)(vm << 16) : v3[u];
+        if (windowed) {
+          const int64_t lo = x[u] - size + adv;
+          c_app += ok[u] ? (int64_t)fast_udiv((uint64_t)x[u], fd) - (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), fd) + 1
+                         : 0;
+        } else {
+          c_app += ok[u] ? 1 : 0;
+        }
+        hk[u] = (int64_t)key_hash(k[u]);
+      }
+      stage_step_w<WU>(hk, x, w2, w3, ok, shift, bmask, P, SL, srec);
+#pragma unroll
+      for (int u = 0; u < WU; u++) {
+        x[u] = nx[u];
+        k[u] = nk[u];
+        v2[u] = nv2[u];
+        v3[u] = nv3[u];
       }
     }
   } else if (fast) {
@@ -3474,7 +3585,12 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   const int nbins = lvl2 ? B : P;
   const int Ut = U >= 16 ? 16 : (U >= 8 ? 8 : (narrow && U >= 6 ? 6 : 4));  // the instantiated records per thread per step
   const bool stage = narrow && !pad && nbins <= PT_THREADS && Ut <= 8 && knob("KHIP_STAGE", 1) != 0;
-  const size_t scat_lds = stage ? stage_lds_bytes(nbins, Ut * PT_THREADS / 2) : (lvl2 ? (size_t)B * 4 : hist_lds);
+  // 32-byte records (key hash, ts, meta / value words) through the LDS stage too (2 x 1024 per step)
+  const bool wstage = !narrow && s.rw == 4 && !pad && nbins <= PT_THREADS && knob("KHIP_WSTAGE", 1) != 0;
+  const int wu = Ut >= 16 ? 4 : 2;  // k_part_scatter's WU: staged 32-byte records per thread per step
+  const size_t scat_lds = stage ? stage_lds_bytes(nbins, Ut * PT_THREADS / 2)
+                                : (wstage ? stage_lds_bytes(nbins, 2 * wu * PT_THREADS)
+                                          : (lvl2 ? (size_t)B * 4 : hist_lds));
   if (scat_lds > 64 * 1024)
     hipFuncSetAttribute((const void*)scat, hipFuncAttributeMaxDynamicSharedMemorySize, (int)scat_lds);
   hipLaunchKernelGGL(scat, dim3(nT), dim3(PT_THREADS), scat_lds, a->stream, keys, ts, kv, rv,
@@ -3484,7 +3600,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                      s.tilemax.as<int64_t>(), s.tilemin.as<int64_t>(), a->windowed, a->desc.size_ms,
                      a->windowed ? a->desc.advance_ms : 1, make_fastdiv(a->windowed ? a->desc.advance_ms : 1),
                      a->grace, L, lvl2 ? s.srecA.as<uint64_t>() : s.srec.as<uint64_t>(), ncap,
-                     s.tpart.as<int64_t>(), s.wr.as<int64_t>(), r12_ok ? 1 : 0, stage ? 1 : 0);
+                     s.tpart.as<int64_t>(), s.wr.as<int64_t>(), r12_ok ? 1 : 0, (stage || wstage) ? 1 : 0);
   KHIP_TRY_HIP(hipGetLastError());
   if (lvl2) {
     const int64_t per_blk = knob("KHIP_REFINE_RECS", 8192);  // measured: 8K records per block (1 KB runs) beat 32K
