@@ -960,6 +960,46 @@ __device__ __forceinline__ void refine_staged(const uint64_t* __restrict__ srcA,
   }
 }
 
+// refine_range for 32-byte records (RW = 4) through the LDS stage (stage_step_w), next step's
+// loads in flight
+template <int U>
+__device__ __forceinline__ void refine_staged_w(const uint64_t* __restrict__ srcA, const StageLds& SL, int64_t lo,
+                                                int64_t hi, int log2P, int F, uint64_t* __restrict__ srec) {
+  constexpr int S = U * PT_THREADS;
+  longlong2 a[U], b[U], na[U], nb[U];
+  auto load_step = [&](int64_t i0, longlong2 (&da)[U], longlong2 (&db)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      int64_t i = i0 + (int64_t)u * PT_THREADS;
+      i = i < hi ? i : hi - 1;
+      da[u] = ((const longlong2*)(srcA + (uint64_t)i * 4))[0];
+      db[u] = ((const longlong2*)(srcA + (uint64_t)i * 4))[1];
+    }
+  };
+  int64_t s0 = lo;
+  load_step(s0 + threadIdx.x, a, b);
+  for (; s0 < hi; s0 += S) {
+    const int64_t i0 = s0 + threadIdx.x;
+    if (s0 + S < hi) load_step(i0 + S, na, nb);
+    int64_t hk[U], ts[U], w2[U], w3[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      ok[u] = i0 + (int64_t)u * PT_THREADS < hi;
+      hk[u] = a[u].x;
+      ts[u] = a[u].y;
+      w2[u] = b[u].x;
+      w3[u] = b[u].y;
+    }
+    stage_step_w<U>(hk, ts, w2, w3, ok, 64 - log2P, (uint32_t)(F - 1), F, SL, srec);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      a[u] = na[u];
+      b[u] = nb[u];
+    }
+  }
+}
+
 // R8 records (8 bytes: (key - kbase) << tb | trel) of one block's range → their partitions,
 // through the LDS stage (staged) or straight to each partition's cursor
 template <int U>
@@ -1054,6 +1094,22 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_refine(const uint64_t* __re
       if (n12) refine_staged<true, 2>(srcA, SL, lo, hi, log2P, F, srec, r12_ok == 2 ? 2 : 1, wr[5]);
       else refine_staged<false, 2>(srcA, SL, lo, hi, log2P, F, srec, 0, 0);
     }
+    return;
+  }
+  if (RW == 4 && stage) {  // 32-byte records through the LDS stage (stage = records per thread per step)
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ int wsum[PT_THREADS / 64];
+    const StageLds SL = stage_carve(smem, F, 2 * stage * PT_THREADS, wsum);
+    for (int f = threadIdx.x; f < F; f += PT_THREADS) {
+      SL.cur[f] = offs[t0 * P + ((int64_t)b << fbits) + f];
+      SL.cnt[f] = 0u;
+    }
+    const int64_t lo = offA[t0 * B + b];
+    const int64_t hi = t1 < nT ? (int64_t)offA[t1 * B + b] : pbase[(int64_t)(b + 1) << fbits];
+    lds_barrier();
+    if (hi <= lo) return;
+    if (stage >= 4) refine_staged_w<4>(srcA, SL, lo, hi, log2P, F, srec);
+    else refine_staged_w<2>(srcA, SL, lo, hi, log2P, F, srec);
     return;
   }
   for (int f = threadIdx.x; f < F; f += PT_THREADS) cur[f] = offs[t0 * P + ((int64_t)b << fbits) + f];
@@ -3617,13 +3673,16 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
       default: ref = k_part_refine<12>; break;
     }
     const bool rstage = s.rw == 2 && (1 << fbits) <= PT_THREADS && knob("KHIP_STAGE", 1) != 0;
-    const int ru = knob("KHIP_REFINE_U", 8) >= 8 ? 8 : 4;  // records per thread per staged step
-    const size_t ref_lds = rstage ? stage_lds_bytes(1 << fbits, ru * PT_THREADS / 2) : 0;
+    const bool rwstage = s.rw == 4 && (1 << fbits) <= PT_THREADS && knob("KHIP_WSTAGE", 1) != 0;
+    const int ru = rwstage ? (knob("KHIP_REFINE_WU", 4) >= 4 ? 4 : 2)  // 32-byte records per thread per step
+                           : (knob("KHIP_REFINE_U", 8) >= 8 ? 8 : 4);   // records per thread per staged step
+    const size_t ref_lds = rstage ? stage_lds_bytes(1 << fbits, ru * PT_THREADS / 2)
+                                  : (rwstage ? stage_lds_bytes(1 << fbits, 2 * ru * PT_THREADS) : 0);
     if (ref_lds) hipFuncSetAttribute((const void*)ref, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ref_lds);
     hipLaunchKernelGGL(ref, dim3((unsigned)(B * ng)), dim3(PT_THREADS), ref_lds, a->stream, s.srecA.as<uint64_t>(),
                        s.hcoarse.as<uint32_t>(), s.hist.as<uint32_t>(), s.pbase.as<int64_t>(), nT, G, s.log2P, fbits,
                        ncap, s.srec.as<uint64_t>(), (int)knob("KHIP_REFINE_MODE", 0), s.wr.as<int64_t>(),
-                       r12_ok ? (r12_merge ? 1 : 2) : 0, rstage ? ru : 0);
+                       r12_ok ? (r12_merge ? 1 : 2) : 0, (rstage || rwstage) ? ru : 0);
     KHIP_TRY_HIP(hipGetLastError());
   }
   ev_record_part(a, 2);
