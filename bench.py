@@ -861,18 +861,17 @@ def bench_hopping_double(args, lib, rank, world, local):
     traffic = load_traffic(args.traffic_json, "hopping_double", n)
     moved_model = 16 + 24 + 32 + 32 + 32 + 32 + 2 * 64.0 * groups / n * len(batches)
     moved = traffic / n if traffic else moved_model
-    roof = roofline(BYTES_PER_RECORD_C3 * n, ms_step, sum(phase.values()), None,
-                    traffic, BYTES_PER_RECORD_C3,
+    # frac over the bytes the passes stream (counter bytes when committed for this size, else the
+    # model): SURVEY §8(d)'s 696 B/record assumes one HBM slot read-modify-write per (record,
+    # window), which the engine never does (windows fan out in LDS, panes fold them), so a rate
+    # over it is reported beside frac, not as frac
+    roof = roofline(moved * n, ms_step, sum(phase.values()), None, traffic, moved,
                     kernel="khip_agg_push (all kernels of every micro-batch push) + row count",
-                    extra={"algorithmic_equivalent": True,
-                           "note": "SURVEY §8(d)'s 696 B/record assumes one HBM slot RMW per (record, window); "
-                                   "the engine fans the 6 windows out in LDS, so frac here is an "
-                                   "algorithmic-equivalent rate, not HBM bandwidth: streamed_frac (counter "
-                                   "bytes / time) is the bandwidth figure",
-                           "streamed_bytes_per_record": moved,
-                           "streamed_basis": "PMC counter bytes (profiles/traffic.json)" if traffic else
-                                             "model of the passes (no counter record for this size)",
-                           "streamed_frac": moved * n / (ms_step / 1000.0) / 1e9 / HBM_PEAK_GBS,
+                    extra={"basis": "streamed bytes per record (" + ("PMC counter bytes, profiles/traffic.json"
+                                    if traffic else "model of the passes: no counter record for this size") +
+                                    ") / ms_per_step (wall, barrier to barrier)",
+                           "survey_algorithmic_bytes_per_record": BYTES_PER_RECORD_C3,
+                           "survey_equivalent_frac": BYTES_PER_RECORD_C3 * n / (ms_step / 1000.0) / 1e9 / HBM_PEAK_GBS,
                            "phase_ms_per_step": phase, "stream_copy_GBps": stream_copy_gbs()})
     cpu = None
     if world == 1 and not args.no_cpu_baseline:

@@ -20,7 +20,7 @@ python3 tools/rocprof_summary.py stats $OUT/trace/run_kernel_stats.csv > $OUT/ke
 head -14 $OUT/kernel_stats.md
 timeout -s KILL 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 $B > $OUT/fetch.log 2>&1 || { tail -20 $OUT/fetch.log; exit 6; }
 timeout -s KILL 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 $B > $OUT/write.log 2>&1 || { tail -20 $OUT/write.log; exit 7; }
-N=$(python3 -c "import json,sys; d=json.loads([l for l in open('$OUT/trace.log') if l.startswith('{')][-1]); c=d['config']; print(c.get('records_per_gpu') or c.get('clicks_per_gpu'))")
+N=$(python3 -c "import json,sys; d=json.loads([l for l in open('$OUT/trace.log') if l.startswith('{')][-1]); c=d['config']; print(c.get('records_per_gpu') or c.get('clicks_per_gpu') or c.get('rows_per_gpu'))")
 python3 tools/pmc_traffic.py $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv $N $((S+W)) $OUT/traffic.json $CFG${SUF:+_$SUF}
 if [ "${SQ:-0}" = 1 ]; then
   timeout -s KILL 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS -d $OUT/sq -o run --output-format csv -- python3 $B > $OUT/sq.log 2>&1 || { tail -20 $OUT/sq.log; exit 8; }
