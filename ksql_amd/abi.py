@@ -15,8 +15,9 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # KSQL_AMD_LIB_VARIANT=tune loads the tuning build (same HIP kernels, KHIP_* knobs read from the
 # environment; ksql_amd/Makefile TUNING=1) for GPU parameter sweeps.  Both are the HIP library.
-PRODUCT_LIB = os.path.join(REPO, "ksql_amd", "libksqldb_hip_tune.so" if os.environ.get("KSQL_AMD_LIB_VARIANT") == "tune"
-                           else "libksqldb_hip.so")
+# (any other name V loads libksqldb_hip_V.so: a build kept for an A/B inside one GPU call).
+_VARIANT = os.environ.get("KSQL_AMD_LIB_VARIANT", "")
+PRODUCT_LIB = os.path.join(REPO, "ksql_amd", "libksqldb_hip_%s.so" % _VARIANT if _VARIANT else "libksqldb_hip.so")
 ORACLE_LIB = os.path.join(REPO, "oracle", "liboracle.so")
 
 ABI_VERSION = 4  # include/ksqldb_hip.h KHIP_ABI_VERSION the structs below mirror

@@ -31,6 +31,7 @@
 namespace khip {
 
 constexpr int PT_THREADS = 1024;
+constexpr int R8_NT = 512;  // k_part_scatter_r8 / k_part_refine_r8 workgroup size (two per CU)
 constexpr int PT_ITEMS = 64;  // default records per thread per tile (KHIP_TILE_ITEMS overrides)
 constexpr int AG_THREADS = 1024;
 constexpr uint32_t L_CLAIM = 1u;
@@ -568,7 +569,7 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
     const int64_t* __restrict__ tileprefix, const int64_t* __restrict__ tilemax,
     const int64_t* __restrict__ tilemin, int windowed, int64_t size, int64_t adv, FastDiv fd, int64_t grace,
     RecLayout L, uint64_t* __restrict__ srec, int64_t dummy, int64_t* __restrict__ tpart,
-    const int64_t* __restrict__ wr, int r12_ok, int stage) {
+    const int64_t* __restrict__ wr, int r12_ok, int stage, int skip_r8) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint32_t* cur = (uint32_t*)smem;
   __shared__ int wsum[PT_THREADS / 64];
@@ -592,6 +593,7 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
   const int64_t smax = carry > tilemax[t] ? carry : tilemax[t];
   const int64_t tmin = tilemin[t];
   const bool fast = !windowed || tmin == INT64_MAX || first_window_start(tmin, size, adv) + size > smax - grace;
+  if (NARROW && skip_r8 && fast && stage && r8tb) return;  // k_part_scatter_r8's tile
   if (fast && NARROW && stage) {
     // (key hash, ts) records through the LDS stage (stage_step), next step's loads in flight
     constexpr int S = U * PT_THREADS;
@@ -614,7 +616,12 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
         dk[u] = keys[i];
       }
     };
-    // steps are uniform across the block (every thread runs every step: barriers inside)
+    // steps are uniform across the block (every thread runs every step: barriers inside).  The
+    // R8 and the 12/16-byte step loops are separate loops (R8C: compile-time), so the registers
+    // of one are not allocated around the other (one shared loop spilled the next step's
+    // prefetched records to scratch every step)
+    auto run = [&](auto r8c) {
+      constexpr bool R8C = decltype(r8c)::value;
     int64_t s0 = base;
     if (s0 < end) load_step(s0 + threadIdx.x, x, k);
     for (; s0 < end; s0 += S) {
@@ -632,11 +639,11 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
         } else {
           c_app += ok[u] ? 1 : 0;
         }
-        x[u] = r8tb ? (int64_t)(((uint64_t)(k[u] - kbase) << r8tb) | (uint64_t)(x[u] - tbase + 1))
-                    : (r12 ? x[u] - tbase + 1 : x[u]);
+        x[u] = R8C ? (int64_t)(((uint64_t)(k[u] - kbase) << r8tb) | (uint64_t)(x[u] - tbase + 1))
+                   : (r12 ? x[u] - tbase + 1 : x[u]);
         k[u] = (int64_t)key_hash(k[u]);  // records carry the key hash (key = its inverse)
       }
-      if (r8tb) {
+      if constexpr (R8C) {
         uint32_t bin[U];
 #pragma unroll
         for (int u = 0; u < U; u++) bin[u] = stage_bin((uint64_t)k[u], shift, bmask);
@@ -664,6 +671,11 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
         k[u] = nxk[u];
       }
     }
+    };
+    if (r8tb)
+      run(std::true_type{});
+    else
+      run(std::false_type{});
   } else if (fast && NARROW) {
     // 16-byte (key, ts) records: straight-line steps (no branch around a load or store, so
     // every wait is counted), next step's loads issued before this step's cursors/stores;
@@ -1060,13 +1072,15 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_refine(const uint64_t* __re
                                                             const int64_t* __restrict__ pbase, int64_t nT, int G,
                                                             int log2P, int fbits, int64_t dummy,
                                                             uint64_t* __restrict__ srec, int mode,
-                                                            const int64_t* __restrict__ wr, int r12_ok, int stage) {
+                                                            const int64_t* __restrict__ wr, int r12_ok, int stage,
+                                                            int skip_r8) {
   __shared__ uint32_t cur[1 << 12];
   const int F = 1 << fbits, P = 1 << log2P, B = P >> fbits;
   const int64_t ng = (nT + G - 1) / G;
   const int b = (int)(blockIdx.x / ng);
   const int64_t g = blockIdx.x % ng;
   const int64_t t0 = g * G, t1 = t0 + G < nT ? t0 + G : nT;
+  if (RW == 2 && stage && skip_r8 && r12_ok && wr[4] != 0 && wr[7]) return;  // k_part_refine_r8's
   if (RW == 2 && stage) {  // narrow records through the LDS stage
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int wsum[PT_THREADS / 64];
@@ -1123,6 +1137,223 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_refine(const uint64_t* __re
     refine_range<RW, true>(srcA, cur, lo, hi, log2P, F, dummy, srec, mode, r12_ok == 2, wr[5]);
   else
     refine_range<RW, false>(srcA, cur, lo, hi, log2P, F, dummy, srec, mode, false, 0);
+}
+
+// ------------------------------------------------------------------ R8 scatter / refine
+// The R8 (8-byte record) steps of k_part_scatter and k_part_refine as kernels of their own, of NT
+// threads: register allocation sees only this path (inside the general kernels the other record
+// layouts' loops put it at the 128-VGPR cap with the next step's prefetched records spilled to
+// scratch, one 1024-thread workgroup per CU), and two NT = 512 workgroups share a CU, so one's
+// four stage barriers per step overlap the other's loads and stores.  Each staged record keeps
+// its bin beside it in LDS (u16), so the write-out does not hash the key again.
+struct StageR8 {
+  uint32_t* cur;    // [nb] next output record of each bin
+  uint32_t* cnt;    // [nb] records of the step per bin
+  uint32_t* sbase;  // [nb] the bin's first staged slot
+  uint32_t* gpos;   // [nb] output position of the bin's first record of the step
+  int64_t* sp;      // [S] staged records
+  uint16_t* sbin;   // [S] their bins
+  int* wsum;        // [NT / 64]
+};
+
+__host__ __device__ constexpr size_t stage_r8_lds_bytes(int nb, int S) {
+  return (size_t)nb * 16 + (size_t)S * 8 + ((size_t)S * 2 + 15) / 16 * 16;
+}
+
+__device__ __forceinline__ StageR8 stage_r8_carve(char* smem, int nb, int S, int* wsum) {
+  StageR8 L;
+  L.cur = (uint32_t*)smem;
+  L.cnt = L.cur + nb;
+  L.sbase = L.cnt + nb;
+  L.gpos = L.sbase + nb;
+  L.sp = (int64_t*)(smem + (size_t)nb * 16);
+  L.sbin = (uint16_t*)(L.sp + S);
+  L.wsum = wsum;
+  return L;
+}
+
+// One step: U records per thread (ok = present) → rank per bin, bin-ordered in LDS, written out
+// per bin as one contiguous run by consecutive threads.  nb <= NT.
+template <int U, int NT>
+__device__ __forceinline__ void stage_step_r8(const int64_t (&rec)[U], const uint32_t (&bin)[U], const bool (&ok)[U],
+                                              int nb, const StageR8& L, uint64_t* __restrict__ srec) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  uint32_t rank[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) rank[u] = ok[u] ? atomicAdd(&L.cnt[bin[u]], 1u) : 0u;
+  lds_barrier();
+  const uint32_t c = t < nb ? L.cnt[t] : 0u;
+  uint32_t incl = c;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) L.wsum[wave] = (int)incl;
+  lds_barrier();
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < NT / 64; k++) {
+    before += k < wave ? (uint32_t)L.wsum[k] : 0u;
+    tot += (uint32_t)L.wsum[k];
+  }
+  if (t < nb) {
+    L.sbase[t] = before + incl - c;
+    L.gpos[t] = L.cur[t];
+    L.cur[t] += c;
+    L.cnt[t] = 0u;
+  }
+  lds_barrier();
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    if (ok[u]) {
+      const uint32_t i = L.sbase[bin[u]] + rank[u];
+      L.sp[i] = rec[u];
+      L.sbin[i] = (uint16_t)bin[u];
+    }
+  lds_barrier();
+  for (uint32_t j = t; j < tot; j += NT) {
+    const uint32_t b = L.sbin[j];
+    srec[(uint64_t)L.gpos[b] + (j - L.sbase[b])] = (uint64_t)L.sp[j];
+  }
+  // the next step's first barrier (after its rank atomics) orders these LDS reads before any
+  // rewrite of sbase / gpos / the stage
+}
+
+// Pass A for a push whose records are R8 (wr[4] && wr[7], decided on the device by
+// k_part_wrange): the tiles with no late record (k_part_scatter's `fast` test); k_part_scatter
+// (skip_r8) takes the others.  Same output as k_part_scatter's staged R8 path.
+template <int U, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_part_scatter_r8(
+    const int64_t* __restrict__ keys, const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
+    const uint8_t* __restrict__ rv, int64_t n, int64_t tile, int log2P, int64_t nT, const uint32_t* __restrict__ offs,
+    const int64_t* __restrict__ tileprefix, const int64_t* __restrict__ tilemax, const int64_t* __restrict__ tilemin,
+    int windowed, int64_t size, int64_t adv, FastDiv fd, int64_t grace, uint64_t* __restrict__ srec,
+    int64_t* __restrict__ tpart, const int64_t* __restrict__ wr) {
+  if (wr[4] == 0 || wr[7] == 0) return;
+  const int64_t t = tile_of(blockIdx.x, nT);
+  const int64_t carry = tileprefix[t];
+  const int64_t smax = carry > tilemax[t] ? carry : tilemax[t];
+  const int64_t tmin = tilemin[t];
+  const bool fast = !windowed || tmin == INT64_MAX || first_window_start(tmin, size, adv) + size > smax - grace;
+  if (!fast) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int wsum[NT / 64];
+  __shared__ unsigned long long lc;
+  constexpr int S = U * NT;
+  const int P = 1 << log2P;
+  const StageR8 L = stage_r8_carve(smem, P, S, wsum);
+  for (int p = threadIdx.x; p < P; p += NT) {
+    L.cur[p] = offs[t * P + p];
+    L.cnt[p] = 0u;
+  }
+  if (threadIdx.x == 0) lc = 0;
+  const int tb = (int)wr[7];
+  const int64_t tbase = wr[5], kbase = wr[6];
+  const int shift = log2P == 0 ? 64 : 64 - log2P;
+  const uint32_t bmask = (uint32_t)(P - 1);
+  const int64_t base = t * tile;
+  const int64_t end = base + tile < n ? base + tile : n;
+  int64_t c_app = 0;
+  int64_t x[U], k[U];
+  auto load_step = [&](int64_t i0, int64_t (&dx)[U], int64_t (&dk)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      int64_t i = i0 + (int64_t)u * NT;
+      i = i < end ? i : end - 1;
+      dx[u] = ts[i];
+      dk[u] = keys[i];
+    }
+  };
+  lds_barrier();
+  int64_t s0 = base;
+  if (s0 < end) load_step(s0 + threadIdx.x, x, k);
+  for (; s0 < end; s0 += S) {  // uniform across the block: barriers inside
+    const int64_t i0 = s0 + threadIdx.x;
+    bool ok[U];
+    uint32_t bin[U];
+    int64_t rec[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t i = i0 + (int64_t)u * NT;
+      ok[u] = i < end && x[u] >= 0 && bit_get(kv, i) && bit_get(rv, i);
+      if (windowed) {
+        const int64_t lo = x[u] - size + adv;
+        c_app += ok[u] ? (int64_t)fast_udiv((uint64_t)x[u], fd) - (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), fd) + 1
+                       : 0;
+      } else {
+        c_app += ok[u] ? 1 : 0;
+      }
+      bin[u] = stage_bin(key_hash(k[u]), shift, bmask);
+      rec[u] = (int64_t)(((uint64_t)(k[u] - kbase) << tb) | (uint64_t)(x[u] - tbase + 1));
+    }
+    // the next step's loads go into x / k (dead now) and stay in flight through this step's stage
+    if (s0 + S < end) load_step(i0 + S, x, k);
+    stage_step_r8<U, NT>(rec, bin, ok, P, L, srec);
+  }
+  c_app = wave_sum(c_app);
+  if ((threadIdx.x & 63) == 0 && c_app) atomicAdd(&lc, (unsigned long long)c_app);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    tpart[t * T_NPART + T_APPLIED] = (int64_t)lc;
+    tpart[t * T_NPART + T_LATE] = 0;
+  }
+}
+
+// Pass B of R8 records (k_part_refine's staged R8 path): block (bucket b, tile group g).
+template <int U, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_part_refine_r8(const uint64_t* __restrict__ srcA,
+                                                          const uint32_t* __restrict__ offA,
+                                                          const uint32_t* __restrict__ offs,
+                                                          const int64_t* __restrict__ pbase, int64_t nT, int G,
+                                                          int log2P, int fbits, uint64_t* __restrict__ srec,
+                                                          const int64_t* __restrict__ wr) {
+  if (wr[4] == 0 || wr[7] == 0) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int wsum[NT / 64];
+  constexpr int S = U * NT;
+  const int F = 1 << fbits, P = 1 << log2P, B = P >> fbits;
+  const int64_t ng = (nT + G - 1) / G;
+  const int b = (int)(blockIdx.x / ng);
+  const int64_t g = blockIdx.x % ng;
+  const int64_t t0 = g * G, t1 = t0 + G < nT ? t0 + G : nT;
+  const StageR8 L = stage_r8_carve(smem, F, S, wsum);
+  for (int f = threadIdx.x; f < F; f += NT) {
+    L.cur[f] = offs[t0 * P + ((int64_t)b << fbits) + f];
+    L.cnt[f] = 0u;
+  }
+  const int64_t lo = offA[t0 * B + b];
+  const int64_t hi = t1 < nT ? (int64_t)offA[t1 * B + b] : pbase[(int64_t)(b + 1) << fbits];
+  lds_barrier();
+  if (hi <= lo) return;
+  const int tb = (int)wr[7];
+  const int64_t kbase = wr[6];
+  const int shift = 64 - log2P;
+  const uint32_t fmask = (uint32_t)(F - 1);
+  int64_t pay[U], npay[U];
+  auto load_step = [&](int64_t i0, int64_t (&dp)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      int64_t i = i0 + (int64_t)u * NT;
+      i = i < hi ? i : hi - 1;
+      dp[u] = (int64_t)__builtin_nontemporal_load(srcA + i);
+    }
+  };
+  int64_t s0 = lo;
+  load_step(s0 + threadIdx.x, pay);
+  for (; s0 < hi; s0 += S) {  // uniform across the block: barriers inside
+    const int64_t i0 = s0 + threadIdx.x;
+    if (s0 + S < hi) load_step(i0 + S, npay);
+    bool ok[U];
+    uint32_t bin[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      ok[u] = i0 + (int64_t)u * NT < hi;
+      bin[u] = stage_bin(key_hash(kbase + (int64_t)((uint64_t)pay[u] >> tb)), shift, fmask);
+    }
+    stage_step_r8<U, NT>(pay, bin, ok, F, L, srec);
+#pragma unroll
+    for (int u = 0; u < U; u++) pay[u] = npay[u];
+  }
 }
 
 // ------------------------------------------------------------------ k_part_agg
@@ -3644,6 +3875,9 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   // 32-byte records (key hash, ts, meta / value words) through the LDS stage too (2 x 1024 per step)
   const bool wstage = !narrow && s.rw == 4 && !pad && nbins <= PT_THREADS && knob("KHIP_WSTAGE", 1) != 0;
   const int wu = Ut >= 16 ? 4 : 2;  // k_part_scatter's WU: staged 32-byte records per thread per step
+  // R8 records (decided on the device) through k_part_scatter_r8 / k_part_refine_r8
+  const bool r8k = r8_allow && stage && Ut == 8 && nbins <= R8_NT && (!lvl2 || (1 << fbits) <= R8_NT) &&
+                   knob("KHIP_R8K", 1) != 0;
   const size_t scat_lds = stage ? stage_lds_bytes(nbins, Ut * PT_THREADS / 2)
                                 : (wstage ? stage_lds_bytes(nbins, 2 * wu * PT_THREADS)
                                           : (lvl2 ? (size_t)B * 4 : hist_lds));
@@ -3656,14 +3890,26 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                      s.tilemax.as<int64_t>(), s.tilemin.as<int64_t>(), a->windowed, a->desc.size_ms,
                      a->windowed ? a->desc.advance_ms : 1, make_fastdiv(a->windowed ? a->desc.advance_ms : 1),
                      a->grace, L, lvl2 ? s.srecA.as<uint64_t>() : s.srec.as<uint64_t>(), ncap,
-                     s.tpart.as<int64_t>(), s.wr.as<int64_t>(), r12_ok ? 1 : 0, (stage || wstage) ? 1 : 0);
+                     s.tpart.as<int64_t>(), s.wr.as<int64_t>(), r12_ok ? 1 : 0, (stage || wstage) ? 1 : 0, r8k ? 1 : 0);
   KHIP_TRY_HIP(hipGetLastError());
+  if (r8k) {  // the R8 tiles (exits at once unless k_part_wrange chose R8)
+    auto s8 = k_part_scatter_r8<8, R8_NT>;
+    const size_t s8_lds = stage_r8_lds_bytes(nbins, 8 * R8_NT);
+    if (s8_lds > 64 * 1024) hipFuncSetAttribute((const void*)s8, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s8_lds);
+    hipLaunchKernelGGL(s8, dim3(nT), dim3(R8_NT), s8_lds, a->stream, keys, ts, kv, rv, n, tile, s.log2P - fbits, nT,
+                       lvl2 ? s.hcoarse.as<uint32_t>() : s.hist.as<uint32_t>(), s.tileprefix.as<int64_t>(),
+                       s.tilemax.as<int64_t>(), s.tilemin.as<int64_t>(), a->windowed, a->desc.size_ms,
+                       a->windowed ? a->desc.advance_ms : 1, make_fastdiv(a->windowed ? a->desc.advance_ms : 1),
+                       a->grace, lvl2 ? s.srecA.as<uint64_t>() : s.srec.as<uint64_t>(), s.tpart.as<int64_t>(),
+                       s.wr.as<int64_t>());
+    KHIP_TRY_HIP(hipGetLastError());
+  }
   if (lvl2) {
     const int64_t per_blk = knob("KHIP_REFINE_RECS", 8192);  // measured: 8K records per block (1 KB runs) beat 32K
     const int G = (int)std::max<int64_t>(1, std::min<int64_t>(nT, per_blk * B / tile));
     const int64_t ng = ceil_div(nT, G);
     void (*ref)(const uint64_t*, const uint32_t*, const uint32_t*, const int64_t*, int64_t, int, int, int, int64_t,
-                uint64_t*, int, const int64_t*, int, int);
+                uint64_t*, int, const int64_t*, int, int, int);
     switch (s.rw) {
       case 2: ref = k_part_refine<2>; break;
       case 4: ref = k_part_refine<4>; break;
@@ -3682,8 +3928,17 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     hipLaunchKernelGGL(ref, dim3((unsigned)(B * ng)), dim3(PT_THREADS), ref_lds, a->stream, s.srecA.as<uint64_t>(),
                        s.hcoarse.as<uint32_t>(), s.hist.as<uint32_t>(), s.pbase.as<int64_t>(), nT, G, s.log2P, fbits,
                        ncap, s.srec.as<uint64_t>(), (int)knob("KHIP_REFINE_MODE", 0), s.wr.as<int64_t>(),
-                       r12_ok ? (r12_merge ? 1 : 2) : 0, (rstage || rwstage) ? ru : 0);
+                       r12_ok ? (r12_merge ? 1 : 2) : 0, (rstage || rwstage) ? ru : 0, (r8k && rstage) ? 1 : 0);
     KHIP_TRY_HIP(hipGetLastError());
+    if (r8k && rstage) {
+      auto r8 = k_part_refine_r8<8, R8_NT>;
+      const size_t r8_lds = stage_r8_lds_bytes(1 << fbits, 8 * R8_NT);
+      if (r8_lds > 64 * 1024) hipFuncSetAttribute((const void*)r8, hipFuncAttributeMaxDynamicSharedMemorySize, (int)r8_lds);
+      hipLaunchKernelGGL(r8, dim3((unsigned)(B * ng)), dim3(R8_NT), r8_lds, a->stream, s.srecA.as<uint64_t>(),
+                         s.hcoarse.as<uint32_t>(), s.hist.as<uint32_t>(), s.pbase.as<int64_t>(), nT, G, s.log2P, fbits,
+                         s.srec.as<uint64_t>(), s.wr.as<int64_t>());
+      KHIP_TRY_HIP(hipGetLastError());
+    }
   }
   ev_record_part(a, 2);
   // 4. aggregate partitions (+ retries).  k_part_merge is launched speculatively (it and its
