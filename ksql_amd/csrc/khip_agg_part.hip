@@ -2773,7 +2773,10 @@ __device__ __forceinline__ int c1_find(const KLDS uint64_t* ids, uint64_t id, ui
   return -1;
 }
 
-template <int NT, int AU>
+// RM: the record layout this instantiation reads (0: R12, 1: R8); the host launches both and the
+// one that does not match k_part_wrange's choice (wr[7]) exits at once.  One instantiation with
+// both layouts spilled the prefetched records to scratch (a spill waits for its load).
+template <int NT, int AU, int RM>
 __global__ __launch_bounds__(NT, 4) void k_part_merge_c1(
     C1Params q, const uint32_t* __restrict__ work, int64_t nwork, const int64_t* __restrict__ pbase,
     const uint64_t* __restrict__ srec, int first, uint64_t* __restrict__ buf0, uint64_t* __restrict__ buf1,
@@ -2782,6 +2785,7 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge_c1(
     unsigned long long* __restrict__ closed_n, const int64_t* __restrict__ wr, unsigned long long* __restrict__ hnew,
     unsigned long long* __restrict__ hclosed, unsigned long long* __restrict__ dbg) {
   if (wr[4] == 0) return;  // k_part_wrange declined the merge path for this push
+  if ((wr[7] != 0) != (RM == 1)) return;  // the other record layout's instantiation
   // dbg (KHIP_AGG_PROBE): wall-clock time per phase summed over the workgroups (thread 0's view)
   unsigned long long t_last = dbg ? wall_clock64() : 0ULL;
 #define C1_T(k)                                                                        \
@@ -2839,12 +2843,12 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge_c1(
   // right after issuing it)
   // R8 records (k_part_wrange chose them for this push): one 8-byte word, (key - kbase) << r8tb |
   // trel; the key hash is recomputed here
-  const int r8tb = (int)wr[7];
+  const int r8tb = RM == 1 ? (int)wr[7] : 0;
   const int64_t kbase = wr[6];
   const uint64_t r8mask = r8tb ? (~0ULL >> (64 - r8tb)) : 0ULL;
   uint3 ra[AU], rb[AU];
   auto load = [&](uint3 (&x)[AU], int64_t rbase, int64_t rn, int64_t l0) {
-    if (r8tb) {
+    if constexpr (RM == 1) {
       const uint32_t* base = (const uint32_t*)srec + (uint64_t)rbase * 2;
 #pragma unroll
       for (int u = 0; u < AU; u++) {
@@ -2931,7 +2935,7 @@ __global__ __launch_bounds__(NT, 4) void k_part_merge_c1(
       uint3 x[AU];
 #pragma unroll
       for (int u = 0; u < AU; u++) {
-        if (r8tb) {  // (lo, hi) of the key hash, trel
+        if constexpr (RM == 1) {  // (lo, hi) of the key hash, trel
           const uint64_t v = ((uint64_t)xr[u].y << 32) | xr[u].x;
           const uint64_t hk = key_hash(kbase + (int64_t)(v >> r8tb));
           x[u] = make_uint3((uint32_t)hk, (uint32_t)(hk >> 32), (uint32_t)(v & r8mask));
@@ -4031,8 +4035,11 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
       c1_ran = c1_plan;
       if (c1_ran) {  // the lean COUNT(*) merge
         const int au = (int)knob("KHIP_C1_AU", 6);
-        auto mk = au >= 8 ? k_part_merge_c1<512, 8> : (au >= 6 ? k_part_merge_c1<512, 6> : k_part_merge_c1<512, 4>);
         const int lds = ((1 << c1h) + 64) * 16;
+        // both record layouts' instantiations (R8 only when k_part_wrange may choose it)
+        for (int rm = r8_allow ? 1 : 0; rm >= 0; rm--) {
+        auto mk = rm ? (au >= 8 ? k_part_merge_c1<512, 8, 1> : (au >= 6 ? k_part_merge_c1<512, 6, 1> : k_part_merge_c1<512, 4, 1>))
+                     : (au >= 8 ? k_part_merge_c1<512, 8, 0> : (au >= 6 ? k_part_merge_c1<512, 6, 0> : k_part_merge_c1<512, 4, 0>));
         hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         const int64_t grid = std::min<int64_t>(nwork, (int64_t)s.n_cu * knob("KHIP_MERGE_WG_PER_CU", 2));
         C1Params cq{};
@@ -4054,6 +4061,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                            s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
                            s.closed_ctr.as<unsigned long long>(), s.wr.as<int64_t>(),
                            s.hnew.as<unsigned long long>(), s.ctr.as<unsigned long long>() + 12, dbg);
+        }
       } else {
       auto mk = mq.r12 ? (mt >= 512 ? (cnt1 ? k_part_merge<true, 512, true> : k_part_merge<false, 512, true>)
                                     : (cnt1 ? k_part_merge<true, 256, true> : k_part_merge<false, 256, true>))

@@ -200,6 +200,7 @@ __device__ __forceinline__ int group_net(const ApplyParams& p, uint64_t* __restr
   for (int probe = 0; probe < MAX_PROBE; probe++) {
     uint64_t* s = table + slot * (uint64_t)sw;
     const int64_t w1 = (int64_t)ld_relaxed(&s[1]);
+    const int64_t w2 = (int64_t)ld_relaxed(&s[2]);  // row time, loaded beside the slot's state
     bool hit = false;
     int isnew = 0;
     if (w1 != EMPTY_WS) {
@@ -220,7 +221,9 @@ __device__ __forceinline__ int group_net(const ApplyParams& p, uint64_t* __restr
       if (!hit && ((w0 >> 48) & 0x7FFFULL) == fp) hit = gkeys[(int64_t)(w0 & ((1ULL << 36) - 1))] == gid;
     }
     if (hit) {
-      __hip_atomic_fetch_max((int64_t*)&s[2], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // the row time only grows: no atomic when the slot already holds t or later (a stale or
+      // pre-claim read is only ever lower, and then the atomic runs)
+      if (isnew || w2 < t) __hip_atomic_fetch_max((int64_t*)&s[2], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (int o = 0; o < p.n_ops; o++) {
         const UpdOp op = p.ops[o];
         int64_t* w = (int64_t*)&s[op.word];
