@@ -2013,8 +2013,11 @@ __device__ __forceinline__ void mg_clear(char* smem, KLDS uint64_t* ids, KLDS ui
 // resident-merge and write-out, and inside an item chunk c + 1 is loaded before chunk c is
 // applied, so HBM latency overlaps the LDS work; the write-out leaves every delta entry cleared
 // for the next item (no separate table init).
+#ifndef KHIP_MG_WPE
+#define KHIP_MG_WPE 4  // k_part_merge: minimum waves per SIMD (4: <= 128 VGPRs, two 512-thread workgroups per CU)
+#endif
 template <bool CNT1, int NT, bool R12M>
-__global__ __launch_bounds__(NT, 4) void k_part_merge(
+__global__ __launch_bounds__(NT, KHIP_MG_WPE) void k_part_merge(
     MergeParams q, const uint32_t* __restrict__ work, int64_t nwork, const int64_t* __restrict__ pbase,
     const uint64_t* __restrict__ srec, int first, uint64_t* __restrict__ buf0, uint64_t* __restrict__ buf1,
     const uint8_t* __restrict__ sel, const int64_t* __restrict__ cnt, unsigned long long* __restrict__ newcnt,
@@ -3896,9 +3899,10 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                      a->grace, L, lvl2 ? s.srecA.as<uint64_t>() : s.srec.as<uint64_t>(), ncap,
                      s.tpart.as<int64_t>(), s.wr.as<int64_t>(), r12_ok ? 1 : 0, (stage || wstage) ? 1 : 0, r8k ? 1 : 0);
   KHIP_TRY_HIP(hipGetLastError());
+  const int r8u = knob("KHIP_R8_U", 8) >= 8 ? 8 : 4;  // R8 records per thread per staged step
   if (r8k) {  // the R8 tiles (exits at once unless k_part_wrange chose R8)
-    auto s8 = k_part_scatter_r8<8, R8_NT>;
-    const size_t s8_lds = stage_r8_lds_bytes(nbins, 8 * R8_NT);
+    auto s8 = r8u == 8 ? k_part_scatter_r8<8, R8_NT> : k_part_scatter_r8<4, R8_NT>;
+    const size_t s8_lds = stage_r8_lds_bytes(nbins, r8u * R8_NT);
     if (s8_lds > 64 * 1024) hipFuncSetAttribute((const void*)s8, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s8_lds);
     hipLaunchKernelGGL(s8, dim3(nT), dim3(R8_NT), s8_lds, a->stream, keys, ts, kv, rv, n, tile, s.log2P - fbits, nT,
                        lvl2 ? s.hcoarse.as<uint32_t>() : s.hist.as<uint32_t>(), s.tileprefix.as<int64_t>(),
@@ -3935,8 +3939,8 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                        r12_ok ? (r12_merge ? 1 : 2) : 0, (rstage || rwstage) ? ru : 0, (r8k && rstage) ? 1 : 0);
     KHIP_TRY_HIP(hipGetLastError());
     if (r8k && rstage) {
-      auto r8 = k_part_refine_r8<8, R8_NT>;
-      const size_t r8_lds = stage_r8_lds_bytes(1 << fbits, 8 * R8_NT);
+      auto r8 = r8u == 8 ? k_part_refine_r8<8, R8_NT> : k_part_refine_r8<4, R8_NT>;
+      const size_t r8_lds = stage_r8_lds_bytes(1 << fbits, r8u * R8_NT);
       if (r8_lds > 64 * 1024) hipFuncSetAttribute((const void*)r8, hipFuncAttributeMaxDynamicSharedMemorySize, (int)r8_lds);
       hipLaunchKernelGGL(r8, dim3((unsigned)(B * ng)), dim3(R8_NT), r8_lds, a->stream, s.srecA.as<uint64_t>(),
                          s.hcoarse.as<uint32_t>(), s.hist.as<uint32_t>(), s.pbase.as<int64_t>(), nT, G, s.log2P, fbits,
@@ -4068,7 +4072,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                        : (mt >= 512 ? (cnt1 ? k_part_merge<true, 512, false> : k_part_merge<false, 512, false>)
                                     : (cnt1 ? k_part_merge<true, 256, false> : k_part_merge<false, 256, false>));
       hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, s.m_lds);
-      const int64_t grid = std::min<int64_t>(nwork, (int64_t)s.n_cu * knob("KHIP_MERGE_WG_PER_CU", mt >= 512 ? 2 : 4));
+      const int64_t grid = std::min<int64_t>(nwork, (int64_t)s.n_cu * knob("KHIP_MERGE_WG_PER_CU", mt >= 512 ? KHIP_MG_WPE / 2 : KHIP_MG_WPE));
       hipLaunchKernelGGL(mk, dim3(grid), dim3(mt >= 512 ? 512 : 256), s.m_lds, a->stream, mq, wk, nwork, s.pbase.as<int64_t>(),
                          s.srec.as<uint64_t>(), pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
                          s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
