@@ -32,6 +32,7 @@ namespace khip {
 
 constexpr int PT_THREADS = 1024;
 constexpr int R8_NT = 512;  // k_part_scatter_r8 / k_part_refine_r8 workgroup size (two per CU)
+constexpr int W_NT = 512;   // k_part_scatter_w workgroup size (two per CU)
 constexpr int PT_ITEMS = 64;  // default records per thread per tile (KHIP_TILE_ITEMS overrides)
 constexpr int AG_THREADS = 1024;
 constexpr uint32_t L_CLAIM = 1u;
@@ -468,11 +469,11 @@ __host__ __device__ constexpr size_t stage_lds_bytes(int nb, int S) {
 // column, or two values): staged as two 16-byte halves (L.sk/L.sp hold words 0/1, L.sk + S /
 // L.sp + S words 2/3: the carve-up of stage_lds_bytes(nb, 2 * S)), written out per bin as whole
 // 32-byte records in consecutive, coalesced stores.
-template <int U>
+template <int U, int NT = PT_THREADS>
 __device__ __forceinline__ void stage_step_w(const int64_t (&hk)[U], const int64_t (&ts)[U], const int64_t (&w2)[U],
                                              const int64_t (&w3)[U], const bool (&ok)[U], int shift, uint32_t mask,
                                              int nb, const StageLds& L, uint64_t* __restrict__ srec) {
-  constexpr int S = U * PT_THREADS;
+  constexpr int S = U * NT;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   uint32_t rank[U];
 #pragma unroll
@@ -487,7 +488,7 @@ __device__ __forceinline__ void stage_step_w(const int64_t (&hk)[U], const int64
   if (lane == 63) L.wsum[wave] = (int)incl;
   lds_barrier();
   uint32_t before = 0, tot = 0;
-  for (int k = 0; k < PT_THREADS / 64; k++) {
+  for (int k = 0; k < NT / 64; k++) {
     before += k < wave ? (uint32_t)L.wsum[k] : 0u;
     tot += (uint32_t)L.wsum[k];
   }
@@ -508,7 +509,7 @@ __device__ __forceinline__ void stage_step_w(const int64_t (&hk)[U], const int64
     hi[i] = make_longlong2(w2[u], w3[u]);
   }
   lds_barrier();
-  for (uint32_t j = t; j < tot; j += PT_THREADS) {
+  for (uint32_t j = t; j < tot; j += NT) {
     const longlong2 a = lo[j], b = hi[j];
     const uint32_t bn = stage_bin((uint64_t)a.x, shift, mask);
     uint64_t* r = srec + ((uint64_t)L.gpos[bn] + (j - L.sbase[bn])) * 4;
@@ -593,7 +594,7 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
   const int64_t smax = carry > tilemax[t] ? carry : tilemax[t];
   const int64_t tmin = tilemin[t];
   const bool fast = !windowed || tmin == INT64_MAX || first_window_start(tmin, size, adv) + size > smax - grace;
-  if (NARROW && skip_r8 && fast && stage && r8tb) return;  // k_part_scatter_r8's tile
+  if (skip_r8 && fast && stage && (NARROW ? r8tb != 0 : L.rw == 4)) return;  // k_part_scatter_r8 / _w's tile
   if (fast && NARROW && stage) {
     // (key hash, ts) records through the LDS stage (stage_step), next step's loads in flight
     constexpr int S = U * PT_THREADS;
@@ -974,15 +975,15 @@ __device__ __forceinline__ void refine_staged(const uint64_t* __restrict__ srcA,
 
 // refine_range for 32-byte records (RW = 4) through the LDS stage (stage_step_w), next step's
 // loads in flight
-template <int U>
+template <int U, int NT = PT_THREADS>
 __device__ __forceinline__ void refine_staged_w(const uint64_t* __restrict__ srcA, const StageLds& SL, int64_t lo,
                                                 int64_t hi, int log2P, int F, uint64_t* __restrict__ srec) {
-  constexpr int S = U * PT_THREADS;
+  constexpr int S = U * NT;
   longlong2 a[U], b[U], na[U], nb[U];
   auto load_step = [&](int64_t i0, longlong2 (&da)[U], longlong2 (&db)[U]) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      int64_t i = i0 + (int64_t)u * PT_THREADS;
+      int64_t i = i0 + (int64_t)u * NT;
       i = i < hi ? i : hi - 1;
       da[u] = ((const longlong2*)(srcA + (uint64_t)i * 4))[0];
       db[u] = ((const longlong2*)(srcA + (uint64_t)i * 4))[1];
@@ -997,13 +998,13 @@ __device__ __forceinline__ void refine_staged_w(const uint64_t* __restrict__ src
     bool ok[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      ok[u] = i0 + (int64_t)u * PT_THREADS < hi;
+      ok[u] = i0 + (int64_t)u * NT < hi;
       hk[u] = a[u].x;
       ts[u] = a[u].y;
       w2[u] = b[u].x;
       w3[u] = b[u].y;
     }
-    stage_step_w<U>(hk, ts, w2, w3, ok, 64 - log2P, (uint32_t)(F - 1), F, SL, srec);
+    stage_step_w<U, NT>(hk, ts, w2, w3, ok, 64 - log2P, (uint32_t)(F - 1), F, SL, srec);
 #pragma unroll
     for (int u = 0; u < U; u++) {
       a[u] = na[u];
@@ -1353,6 +1354,98 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     stage_step_r8<U, NT>(pay, bin, ok, F, L, srec);
 #pragma unroll
     for (int u = 0; u < U; u++) pay[u] = npay[u];
+  }
+}
+
+// ------------------------------------------------------------------ wide scatter / refine
+// The 32-byte-record (rw = 4: key hash, ts, meta / value words; C3) staged steps of k_part_scatter
+// as a kernel of its own, of NT = 512 threads, two workgroups per CU — the same change as the R8
+// kernels above — for the tiles with no late record (the host launches k_part_scatter with skip
+// set for the rest).  C3: 1956 → 1815 µs per push.  The same split of the wide refine pass was
+// slower (1784 → 1989 µs; profiles/r03/ab/wide_kernels.txt) and is not kept.
+template <int WU, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_part_scatter_w(
+    const int64_t* __restrict__ keys, const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
+    const uint8_t* __restrict__ rv, ColPtrs cols, int n_cols, ColTypes ctypes, int64_t n, int64_t tile, int log2P,
+    int64_t nT, const uint32_t* __restrict__ offs, const int64_t* __restrict__ tileprefix,
+    const int64_t* __restrict__ tilemax, const int64_t* __restrict__ tilemin, int windowed, int64_t size, int64_t adv,
+    FastDiv fd, int64_t grace, RecLayout L, uint64_t* __restrict__ srec, int64_t* __restrict__ tpart) {
+  const int64_t t = tile_of(blockIdx.x, nT);
+  const int64_t carry = tileprefix[t];
+  const int64_t smax = carry > tilemax[t] ? carry : tilemax[t];
+  const int64_t tmin = tilemin[t];
+  const bool fast = !windowed || tmin == INT64_MAX || first_window_start(tmin, size, adv) + size > smax - grace;
+  if (!fast) return;  // k_part_scatter's tile
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int wsum[NT / 64];
+  __shared__ unsigned long long lc;
+  constexpr int S = WU * NT;
+  const int P = 1 << log2P;
+  const StageLds SL = stage_carve(smem, P, 2 * S, wsum);
+  for (int p = threadIdx.x; p < P; p += NT) {
+    SL.cur[p] = offs[t * P + p];
+    SL.cnt[p] = 0u;
+  }
+  if (threadIdx.x == 0) lc = 0;
+  lds_barrier();
+  const int shift = log2P == 0 ? 64 : 64 - log2P;
+  const uint32_t bmask = (uint32_t)(P - 1);
+  const int c2 = L.word_col[2], c3 = L.word_col[3];
+  const int64_t base = t * tile;
+  const int64_t end = base + tile < n ? base + tile : n;
+  int64_t c_app = 0;
+  int64_t x[WU], k[WU], v2[WU], v3[WU], nx[WU], nk[WU], nv2[WU], nv3[WU];
+  auto load_step = [&](int64_t i0, int64_t (&dx)[WU], int64_t (&dk)[WU], int64_t (&d2)[WU], int64_t (&d3)[WU]) {
+#pragma unroll
+    for (int u = 0; u < WU; u++) {
+      int64_t i = i0 + (int64_t)u * NT;
+      i = i < end ? i : end - 1;
+      dx[u] = ts[i];
+      dk[u] = keys[i];
+      d2[u] = c2 >= 0 ? load_col_raw(cols, ctypes.t[c2], c2, i) : 0;
+      d3[u] = c3 >= 0 ? load_col_raw(cols, ctypes.t[c3], c3, i) : 0;
+    }
+  };
+  if (base < end) load_step(base + threadIdx.x, x, k, v2, v3);
+  for (int64_t s0 = base; s0 < end; s0 += S) {  // uniform across the block: barriers inside
+    const int64_t i0 = s0 + threadIdx.x;
+    if (s0 + S < end) load_step(i0 + S, nx, nk, nv2, nv3);
+    int64_t hk[WU], w2[WU], w3[WU];
+    bool ok[WU];
+#pragma unroll
+    for (int u = 0; u < WU; u++) {
+      const int64_t i = i0 + (int64_t)u * NT;
+      const int64_t ic = i < end ? i : end - 1;
+      ok[u] = i < end && x[u] >= 0 && bit_get(kv, ic) && bit_get(rv, ic);
+      uint32_t vm = 0;
+      for (int c = 0; c < n_cols; c++)
+        if ((L.vcols >> c) & 1u) vm |= (bit_get(cols.valid[c], ic) ? 1u : 0u) << c;
+      w2[u] = L.meta_word == 2 ? (int64_t)(vm << 16) : v2[u];
+      w3[u] = L.meta_word == 3 ? (int64_t)(vm << 16) : v3[u];
+      if (windowed) {
+        const int64_t lo = x[u] - size + adv;
+        c_app += ok[u] ? (int64_t)fast_udiv((uint64_t)x[u], fd) - (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), fd) + 1
+                       : 0;
+      } else {
+        c_app += ok[u] ? 1 : 0;
+      }
+      hk[u] = (int64_t)key_hash(k[u]);
+    }
+    stage_step_w<WU, NT>(hk, x, w2, w3, ok, shift, bmask, P, SL, srec);
+#pragma unroll
+    for (int u = 0; u < WU; u++) {
+      x[u] = nx[u];
+      k[u] = nk[u];
+      v2[u] = nv2[u];
+      v3[u] = nv3[u];
+    }
+  }
+  c_app = wave_sum(c_app);
+  if ((threadIdx.x & 63) == 0 && c_app) atomicAdd(&lc, (unsigned long long)c_app);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    tpart[t * T_NPART + T_APPLIED] = (int64_t)lc;
+    tpart[t * T_NPART + T_LATE] = 0;
   }
 }
 
@@ -3885,6 +3978,8 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   // R8 records (decided on the device) through k_part_scatter_r8 / k_part_refine_r8
   const bool r8k = r8_allow && stage && Ut == 8 && nbins <= R8_NT && (!lvl2 || (1 << fbits) <= R8_NT) &&
                    knob("KHIP_R8K", 1) != 0;
+  // 32-byte records through k_part_scatter_w (host-known)
+  const bool wk = wstage && nbins <= W_NT && knob("KHIP_WK", 1) != 0;
   const size_t scat_lds = stage ? stage_lds_bytes(nbins, Ut * PT_THREADS / 2)
                                 : (wstage ? stage_lds_bytes(nbins, 2 * wu * PT_THREADS)
                                           : (lvl2 ? (size_t)B * 4 : hist_lds));
@@ -3897,8 +3992,21 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                      s.tilemax.as<int64_t>(), s.tilemin.as<int64_t>(), a->windowed, a->desc.size_ms,
                      a->windowed ? a->desc.advance_ms : 1, make_fastdiv(a->windowed ? a->desc.advance_ms : 1),
                      a->grace, L, lvl2 ? s.srecA.as<uint64_t>() : s.srec.as<uint64_t>(), ncap,
-                     s.tpart.as<int64_t>(), s.wr.as<int64_t>(), r12_ok ? 1 : 0, (stage || wstage) ? 1 : 0, r8k ? 1 : 0);
+                     s.tpart.as<int64_t>(), s.wr.as<int64_t>(), r12_ok ? 1 : 0, (stage || wstage) ? 1 : 0,
+                     (r8k || wk) ? 1 : 0);
   KHIP_TRY_HIP(hipGetLastError());
+  if (wk) {  // the wide staged tiles
+    auto sw_ = wu >= 4 ? k_part_scatter_w<4, W_NT> : k_part_scatter_w<2, W_NT>;
+    const size_t sw_lds = stage_lds_bytes(nbins, 2 * wu * W_NT);
+    if (sw_lds > 64 * 1024) hipFuncSetAttribute((const void*)sw_, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sw_lds);
+    hipLaunchKernelGGL(sw_, dim3(nT), dim3(W_NT), sw_lds, a->stream, keys, ts, kv, rv, cols, a->desc.n_cols, ct, n, tile,
+                       s.log2P - fbits, nT, lvl2 ? s.hcoarse.as<uint32_t>() : s.hist.as<uint32_t>(),
+                       s.tileprefix.as<int64_t>(), s.tilemax.as<int64_t>(), s.tilemin.as<int64_t>(), a->windowed,
+                       a->desc.size_ms, a->windowed ? a->desc.advance_ms : 1,
+                       make_fastdiv(a->windowed ? a->desc.advance_ms : 1), a->grace, L,
+                       lvl2 ? s.srecA.as<uint64_t>() : s.srec.as<uint64_t>(), s.tpart.as<int64_t>());
+    KHIP_TRY_HIP(hipGetLastError());
+  }
   const int r8u = knob("KHIP_R8_U", 8) >= 8 ? 8 : 4;  // R8 records per thread per staged step
   if (r8k) {  // the R8 tiles (exits at once unless k_part_wrange chose R8)
     auto s8 = r8u == 8 ? k_part_scatter_r8<8, R8_NT> : k_part_scatter_r8<4, R8_NT>;
