@@ -36,7 +36,7 @@ OUTSIDE_STEP = ("k_upsert_claim", "k_upsert_finalize", "k_upsert_apply", "k_tabl
 
 
 # wide coalesced streaming readers (16-B-per-lane loads of contiguous runs): FETCH_SIZE x 2
-STREAMING = ("k_part_hist", "k_part_scatter", "k_part_refine", "k_part_merge", "k_part_merge_c1", "k_part_agg",
+STREAMING = ("k_part_hist", "k_part_scatter", "k_part_scatter_r8", "k_part_scatter_w", "k_part_refine", "k_part_refine_r8", "k_part_merge", "k_part_merge_c1", "k_part_agg",
              "k_part_colsum", "k_part_colbase", "k_part_colprefix", "k_part_pscan", "k_scan_blocks", "k_part_rows",
              "k_part_chg", "k_part_stats", "k_part_wrange", "k_part_commit", "k_part_reset", "k_part_tsrange",
              "k_shuf_hist", "k_shuf_pack", "k_shuf_unpack", "k_shuf_colsum", "k_shuf_prefix", "k_init_table")
