@@ -1067,21 +1067,17 @@ __device__ __forceinline__ void refine_r8(const uint64_t* __restrict__ srcA, con
 // runs (cursors = the fine offsets of tile t0).  Every partition's run per group is G tiles
 // long, so the stores combine into whole lines where pass A alone would leave ~64-byte runs.
 template <int RW>
-__global__ __launch_bounds__(PT_THREADS) void k_part_refine(const uint64_t* __restrict__ srcA,
-                                                            const uint32_t* __restrict__ offA,
-                                                            const uint32_t* __restrict__ offs,
-                                                            const int64_t* __restrict__ pbase, int64_t nT, int G,
-                                                            int log2P, int fbits, int64_t dummy,
-                                                            uint64_t* __restrict__ srec, int mode,
-                                                            const int64_t* __restrict__ wr, int r12_ok, int stage,
-                                                            int skip_r8) {
+__device__ __forceinline__ void refine_block(int64_t vb, const uint64_t* __restrict__ srcA,
+                                             const uint32_t* __restrict__ offA, const uint32_t* __restrict__ offs,
+                                             const int64_t* __restrict__ pbase, int64_t nT, int G, int log2P,
+                                             int fbits, int64_t dummy, uint64_t* __restrict__ srec, int mode,
+                                             const int64_t* __restrict__ wr, int r12_ok, int stage) {
   __shared__ uint32_t cur[1 << 12];
   const int F = 1 << fbits, P = 1 << log2P, B = P >> fbits;
   const int64_t ng = (nT + G - 1) / G;
-  const int b = (int)(blockIdx.x / ng);
-  const int64_t g = blockIdx.x % ng;
+  const int b = (int)(vb / ng);
+  const int64_t g = vb % ng;
   const int64_t t0 = g * G, t1 = t0 + G < nT ? t0 + G : nT;
-  if (RW == 2 && stage && skip_r8 && r12_ok && wr[4] != 0 && wr[7]) return;  // k_part_refine_r8's
   if (RW == 2 && stage) {  // narrow records through the LDS stage
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int wsum[PT_THREADS / 64];
@@ -1138,6 +1134,30 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_refine(const uint64_t* __re
     refine_range<RW, true>(srcA, cur, lo, hi, log2P, F, dummy, srec, mode, r12_ok == 2, wr[5]);
   else
     refine_range<RW, false>(srcA, cur, lo, hi, log2P, F, dummy, srec, mode, false, 0);
+}
+
+// Blocks (bucket, tile group) = vb in [0, B * ng).  Narrow records: grid-strided, and the host
+// launches a grid of two workgroups per CU when k_part_refine_r8 may take the push instead
+// (skip_r8), so that when it does, this launch costs ~500 exiting workgroups instead of ~12K.
+template <int RW>
+__global__ __launch_bounds__(PT_THREADS) void k_part_refine(const uint64_t* __restrict__ srcA,
+                                                            const uint32_t* __restrict__ offA,
+                                                            const uint32_t* __restrict__ offs,
+                                                            const int64_t* __restrict__ pbase, int64_t nT, int G,
+                                                            int log2P, int fbits, int64_t dummy,
+                                                            uint64_t* __restrict__ srec, int mode,
+                                                            const int64_t* __restrict__ wr, int r12_ok, int stage,
+                                                            int skip_r8) {
+  if (RW == 2 && stage && skip_r8 && r12_ok && wr[4] != 0 && wr[7]) return;  // k_part_refine_r8's
+  if constexpr (RW == 2) {
+    const int64_t nblk = (int64_t)((1 << log2P) >> fbits) * ((nT + G - 1) / G);
+    for (int64_t vb = blockIdx.x; vb < nblk; vb += gridDim.x) {
+      refine_block<RW>(vb, srcA, offA, offs, pbase, nT, G, log2P, fbits, dummy, srec, mode, wr, r12_ok, stage);
+      __syncthreads();  // the block's LDS (cursors, stage) is reused by the next one
+    }
+  } else {  // wide records (no R8 alternative): one block per workgroup (the loop cost registers)
+    refine_block<RW>(blockIdx.x, srcA, offA, offs, pbase, nT, G, log2P, fbits, dummy, srec, mode, wr, r12_ok, stage);
+  }
 }
 
 // ------------------------------------------------------------------ R8 scatter / refine
@@ -4041,7 +4061,8 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     const size_t ref_lds = rstage ? stage_lds_bytes(1 << fbits, ru * PT_THREADS / 2)
                                   : (rwstage ? stage_lds_bytes(1 << fbits, 2 * ru * PT_THREADS) : 0);
     if (ref_lds) hipFuncSetAttribute((const void*)ref, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ref_lds);
-    hipLaunchKernelGGL(ref, dim3((unsigned)(B * ng)), dim3(PT_THREADS), ref_lds, a->stream, s.srecA.as<uint64_t>(),
+    const int64_t ref_grid = (r8k && rstage) ? std::min<int64_t>(B * ng, 2 * s.n_cu) : B * ng;
+    hipLaunchKernelGGL(ref, dim3((unsigned)ref_grid), dim3(PT_THREADS), ref_lds, a->stream, s.srecA.as<uint64_t>(),
                        s.hcoarse.as<uint32_t>(), s.hist.as<uint32_t>(), s.pbase.as<int64_t>(), nT, G, s.log2P, fbits,
                        ncap, s.srec.as<uint64_t>(), (int)knob("KHIP_REFINE_MODE", 0), s.wr.as<int64_t>(),
                        r12_ok ? (r12_merge ? 1 : 2) : 0, (rstage || rwstage) ? ru : 0, (r8k && rstage) ? 1 : 0);

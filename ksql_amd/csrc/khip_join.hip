@@ -362,6 +362,10 @@ __global__ __launch_bounds__(256) void k_probe(const uint64_t* __restrict__ tabl
       uint64_t m = (uint64_t)h0[r].y;
       int64_t k0 = h0[r].x;
       uint64_t c0 = (uint64_t)h1[r].y, sl = slot[r];
+      // c0 opaque (a register, not "a load of h1[r].y"): otherwise the compiler sinks c0's load to
+      // the hit through a pointer phi (home slot word in the private h1 array | probed slot), which
+      // keeps h1 in scratch — each home-slot word stored right after its load, a wait per probe
+      asm volatile("" : "+v"(c0));
       // linear probing past the home slot (a minority of rows)
       for (int probe = 0; probe < JMAX_PROBE; probe++) {
         if (m == 0) break;
