@@ -854,22 +854,30 @@ def bench_hopping_double(args, lib, rank, world, local):
         return
     ms_step = elapsed * 1000.0 / args.steps
     phase = {k: kt[k] / args.steps for k in ("stream_time_ms", "partition_ms", "apply_ms", "finalize_ms")}
-    # what the kernels actually move per record (the engine fans the F windows out in LDS): the
-    # committed PMC counter bytes of this configuration when present; otherwise the model of the
-    # passes (32-byte records: hist 16 read, scatter 24 read + 32 write, refine 32 + 32, merge 32
-    # read, resident rows read and written once per push)
+    # frac over the ALGORITHMIC FLOOR of the step: every input column read once (W_in = key 8 + ts 8
+    # + value 8 + validity 1/8 = 24.125 B/record) plus, per push, one read-modify-write of the live
+    # (key, window) rows (S_slot = key 8 + ws 8 + sum/count/min/max 32 + rowtime 8 = 56 B, read and
+    # written: 112 B).  Live rows per push = the windows the push's span, size, grace and disorder
+    # keep open per key, at most the step's groups.  The counter bytes the kernels move stay in
+    # `traffic` (their rate over the wall time is `streamed_frac`: utilisation, not efficiency);
+    # SURVEY §8(d)'s 696 B/record (one HBM slot read-modify-write per (record, window), which the
+    # engine never does: windows fan out in LDS, panes fold them) gives `survey_equivalent_frac`.
     traffic = load_traffic(args.traffic_json, "hopping_double", n)
+    floor_rec = 24.125
+    live_rows = min(groups, live)
+    floor_bytes = floor_rec * n + len(batches) * live_rows * 2 * 56.0
     moved_model = 16 + 24 + 32 + 32 + 32 + 32 + 2 * 64.0 * groups / n * len(batches)
     moved = traffic / n if traffic else moved_model
-    # frac over the bytes the passes stream (counter bytes when committed for this size, else the
-    # model): SURVEY §8(d)'s 696 B/record assumes one HBM slot read-modify-write per (record,
-    # window), which the engine never does (windows fan out in LDS, panes fold them), so a rate
-    # over it is reported beside frac, not as frac
-    roof = roofline(moved * n, ms_step, sum(phase.values()), None, traffic, moved,
+    roof = roofline(floor_bytes, ms_step, sum(phase.values()), None, traffic, floor_bytes / n,
                     kernel="khip_agg_push (all kernels of every micro-batch push) + row count",
-                    extra={"basis": "streamed bytes per record (" + ("PMC counter bytes, profiles/traffic.json"
-                                    if traffic else "model of the passes: no counter record for this size") +
-                                    ") / ms_per_step (wall, barrier to barrier)",
+                    extra={"basis": "algorithmic floor (input columns once + one read-modify-write of the live rows "
+                                    "per push, %.3f B/record) / ms_per_step (wall, barrier to barrier)"
+                                    % (floor_bytes / n),
+                           "live_rows_per_push": live_rows, "pushes": len(batches),
+                           "streamed_bytes_per_record": moved,
+                           "streamed_basis": "PMC counter bytes, profiles/traffic.json" if traffic else
+                                             "model of the passes: no counter record for this size",
+                           "streamed_frac": moved * n / (ms_step / 1000.0) / 1e9 / HBM_PEAK_GBS,
                            "survey_algorithmic_bytes_per_record": BYTES_PER_RECORD_C3,
                            "survey_equivalent_frac": BYTES_PER_RECORD_C3 * n / (ms_step / 1000.0) / 1e9 / HBM_PEAK_GBS,
                            "phase_ms_per_step": phase, "stream_copy_GBps": stream_copy_gbs()})

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KHIP_ABI_VERSION 4
+#define KHIP_ABI_VERSION 5
 
 typedef int32_t khip_status;
 #define KHIP_OK 0
@@ -123,6 +123,13 @@ typedef struct khip_batch {
                                  (S/timestamp/LoggingTimestampExtractor.java:72-84)    */
   const void* const* col_data;      /* n_cols column pointers (element type per desc) */
   const uint8_t* const* col_valid;  /* n_cols bitmaps (entries may be NULL)           */
+  /* ABI 5: stream-time domains (khip_agg_desc.time_domain; both NULL for KHIP_TIME_TASK) */
+  const int32_t* partition;   /* KHIP_TIME_PARTITION: the row's Kafka partition, 0..n_partitions-1.
+                                 Rows of one partition form one contiguous run (a consumer poll's
+                                 records per TopicPartition, concatenated)                       */
+  const int64_t* stream_time; /* KHIP_TIME_SUPPLIED: the stream time observed at the row over the
+                                 global arrival order (khip_stream_time_scan upstream, before the
+                                 rows were routed to this handle); >= ts for accepted rows       */
 } khip_batch;
 
 /* Per-batch counters (the Kafka Streams dropped-records / late sensors). */
@@ -138,6 +145,27 @@ typedef struct khip_batch_stats {
 } khip_batch_stats;
 
 /* --------------------------------------------------------- windowed aggregate */
+
+/* Stream-time domains (late drop compares a window's end with streamTime - grace).
+ * TASK: one stream time per handle — one Kafka Streams task (KStreamWindowAggregate's
+ *   observedStreamTime, S/StreamAggregateBuilder.java:287-294), the reference's behaviour when the
+ *   handle serves one input partition, and TopologyTestDriver's when it sees every record
+ *   (F/tools/TestExecutorUtil.java:123-126).
+ * PARTITION: the handle serves n_partitions Kafka partitions, one task each (one task per input
+ *   partition, C/util/KsqlConstants.java:42): each partition has its own stream time, set by the
+ *   batch's `partition` column.  The GROUP BY key must determine the partition (co-partitioned
+ *   input, as groupByKey requires), so the tasks' stores are disjoint and one table holds them.
+ *   Closed windows are evicted by the smallest partition stream time; snapshot retention and
+ *   EMIT FINAL are not offered in this domain (KHIP_E_UNSUPPORTED).
+ * SUPPLIED: one GLOBAL stream time over several handles (ranks): each row carries the stream
+ *   time observed at it over the global arrival order (`stream_time` column), computed where the
+ *   rows were read, before routing: rank r scans its contiguous arrival chunk with
+ *   khip_stream_time_scan seeded with max(global stream time before the batch, the maxima of the
+ *   chunks of ranks < r) — an all-gather of one int64 per rank.  The union of the ranks' tables
+ *   then equals one task over the whole stream. */
+#define KHIP_TIME_TASK 0
+#define KHIP_TIME_PARTITION 1
+#define KHIP_TIME_SUPPLIED 2
 
 /* Window store retention (WINDOW ... RETENTION, X/windows/KsqlWindowExpression.java:26-54, passed to
  * the store by S/StreamAggregateBuilder.java:293,322,350 → X/runtime/MaterializedFactory.java:47).
@@ -188,6 +216,9 @@ typedef struct khip_agg_desc {
                                the aggregate); the library then keeps its row count and
                                changelog tombstones up to date as records arrive          */
   khip_having having;
+  /* ABI 5 */
+  int32_t time_domain;      /* KHIP_TIME_TASK (0), KHIP_TIME_PARTITION, KHIP_TIME_SUPPLIED      */
+  int32_t n_partitions;     /* KHIP_TIME_PARTITION: partitions the handle serves (<= 65536)     */
 } khip_agg_desc;
 
 typedef struct khip_agg khip_agg;
@@ -229,6 +260,14 @@ khip_status khip_agg_result_type(const khip_agg_desc* desc, int32_t agg_index,
  * before the device work completes). */
 khip_status khip_agg_push(khip_agg* agg, const khip_batch* batch,
                           khip_batch_stats* stats);
+
+/* ABI 5.  The stream time observed at each row of `batch` in arrival order, starting from `seed`
+ * (-1: none): out[i] = max(seed, ts of the accepted rows 0..i) — rows with a null key, a null
+ * value or ts < 0 never reach the aggregate and do not advance it.  *out_max = the value after the
+ * last row.  `out` is in the batch's memory (host or device).  The upstream half of
+ * KHIP_TIME_SUPPLIED (see above); the handle only provides the device and stream. */
+khip_status khip_stream_time_scan(khip_agg* agg, const khip_batch* batch, int64_t seed, int64_t* out,
+                                  int64_t* out_max);
 
 /* Number of rows and key bytes the next snapshot will produce (no HAVING).  Snapshots, pull
  * queries and row counts read the window store: windows with start < obs - retention (obs =
@@ -350,6 +389,9 @@ typedef struct khip_kernel_times {
   double finalize_ms;    /* atomic engine: k_finalize + counter reduction             */
   int64_t apply_launches;
   int64_t records;       /* records covered by those apply launches (first passes)    */
+  int64_t c1_pushes;     /* ABI 5: pushes the windowed COUNT(*) pipeline took           */
+  int64_t c1_declined;   /* ABI 5: pushes it declined (late records possible, wide
+                            ts span or key range): the general path ran instead        */
 } khip_kernel_times;
 
 khip_status khip_agg_kernel_times(khip_agg* agg, khip_kernel_times* out, int32_t reset);

@@ -20,7 +20,7 @@ _VARIANT = os.environ.get("KSQL_AMD_LIB_VARIANT", "")
 PRODUCT_LIB = os.path.join(REPO, "ksql_amd", "libksqldb_hip_%s.so" % _VARIANT if _VARIANT else "libksqldb_hip.so")
 ORACLE_LIB = os.path.join(REPO, "oracle", "liboracle.so")
 
-ABI_VERSION = 4  # include/ksqldb_hip.h KHIP_ABI_VERSION the structs below mirror
+ABI_VERSION = 5  # include/ksqldb_hip.h KHIP_ABI_VERSION the structs below mirror
 KHIP_OK = 0
 KHIP_E_BUFFER = -5
 
@@ -38,6 +38,7 @@ FLAG_CHANGELOG = 8
 FLAG_TABLE_SOURCE = 16
 RETENTION_DEFAULT = -1
 EMIT = {"CHANGES": 0, "FINAL": 1}
+TIME = {"TASK": 0, "PARTITION": 1, "SUPPLIED": 2}  # ABI 5 stream-time domains
 NP_TYPE = {0: np.int32, 1: np.int64, 2: np.float64}
 
 i32, i64, u8p = C.c_int32, C.c_int64, C.POINTER(C.c_uint8)
@@ -47,7 +48,9 @@ class Batch(C.Structure):
     _fields_ = [("n_rows", i64), ("mem", i32), ("n_cols", i32),
                 ("key_i64", C.c_void_p), ("key_offsets", C.c_void_p), ("key_bytes", C.c_void_p),
                 ("key_valid", C.c_void_p), ("row_valid", C.c_void_p), ("ts", C.c_void_p),
-                ("col_data", C.POINTER(C.c_void_p)), ("col_valid", C.POINTER(C.c_void_p))]
+                ("col_data", C.POINTER(C.c_void_p)), ("col_valid", C.POINTER(C.c_void_p)),
+                # ABI 5: stream-time domains
+                ("partition", C.c_void_p), ("stream_time", C.c_void_p)]
 
 
 class BatchStats(C.Structure):
@@ -73,7 +76,9 @@ class AggDesc(C.Structure):
                 ("n_aggs", i32), ("aggs", C.POINTER(AggSpec)), ("device", i32), ("flags", i32),
                 ("capacity_hint", i64),
                 # ABI 2
-                ("retention_ms", i64), ("emit", i32), ("has_having", i32), ("having", Having)]
+                ("retention_ms", i64), ("emit", i32), ("has_having", i32), ("having", Having),
+                # ABI 5
+                ("time_domain", i32), ("n_partitions", i32)]
 
 
 class Snapshot(C.Structure):
@@ -101,7 +106,8 @@ class Where(C.Structure):
 class KernelTimes(C.Structure):
     _fields_ = [("stream_time_ms", C.c_double), ("dict_ms", C.c_double), ("partition_ms", C.c_double),
                 ("apply_ms", C.c_double),
-                ("finalize_ms", C.c_double), ("apply_launches", i64), ("records", i64)]
+                ("finalize_ms", C.c_double), ("apply_launches", i64), ("records", i64),
+                ("c1_pushes", i64), ("c1_declined", i64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -197,6 +203,7 @@ PRODUCT_ONLY = {
     "agg_sync": ([_P]),
     "agg_stream": ([_P, C.POINTER(_P)]),
     "agg_kernel_times": ([_P, C.POINTER(KernelTimes), i32]),
+    "stream_time_scan": ([_P, C.POINTER(Batch), i64, _P, C.POINTER(i64)]),
     "table_probe_device": ([_P, C.POINTER(Batch), i32, C.POINTER(Where), C.POINTER(JoinDevOut), C.POINTER(i64)]),
     "table_sync": ([_P]),
     "shuffle_create": ([C.POINTER(ShuffleDesc), C.POINTER(_P)]),
@@ -309,9 +316,10 @@ class HostBatch:
     """Owns numpy arrays for one host batch and the ctypes struct pointing at them."""
 
     def __init__(self, ts, keys=None, key_valid=None, row_valid=None, cols=(), col_valid=(),
-                 utf8_keys=None, key_offsets=None, key_bytes=None):
+                 utf8_keys=None, key_offsets=None, key_bytes=None, partition=None, stream_time=None):
         """utf8_keys: a list of str/bytes (None → b""), or the columnar form key_offsets
-        (int64, n+1) + key_bytes (uint8)."""
+        (int64, n+1) + key_bytes (uint8).  partition (int32) / stream_time (int64): the ABI 5
+        stream-time domain columns (TIME["PARTITION"] / TIME["SUPPLIED"])."""
         self.ts = np.ascontiguousarray(ts, dtype=np.int64)
         n = len(self.ts)
         self.keys = None if keys is None else np.ascontiguousarray(keys, dtype=np.int64)
@@ -330,9 +338,11 @@ class HostBatch:
         nc = len(self.cols)
         self._cd = (C.c_void_p * max(nc, 1))(*[_ptr(c) for c in self.cols])
         self._cv = (C.c_void_p * max(nc, 1))(*[_ptr(v) for v in self.col_valid])
+        self.partition = None if partition is None else np.ascontiguousarray(partition, dtype=np.int32)
+        self.stream_time = None if stream_time is None else np.ascontiguousarray(stream_time, dtype=np.int64)
         self.struct = Batch(n, MEM_HOST, nc, _ptr(self.keys), _ptr(self.key_offsets),
                             _ptr(self.key_bytes), _ptr(self.key_valid), _ptr(self.row_valid),
-                            _ptr(self.ts), self._cd, self._cv)
+                            _ptr(self.ts), self._cd, self._cv, _ptr(self.partition), _ptr(self.stream_time))
 
 
 def having_struct(having):
@@ -343,8 +353,9 @@ def having_struct(having):
 
 def make_agg_desc(window_kind="NONE", key_type="INT64", size_ms=0, advance_ms=0, grace_ms=-1,
                   col_types=(), aggs=(), device=0, capacity_hint=0, flags=0, retention_ms=RETENTION_DEFAULT,
-                  emit="CHANGES", having=None):
-    """having: the query's HAVING ({"agg", "op", "value"}), maintained by the library (ABI 2)."""
+                  emit="CHANGES", having=None, time_domain="TASK", n_partitions=0):
+    """having: the query's HAVING ({"agg", "op", "value"}), maintained by the library (ABI 2).
+    time_domain / n_partitions: the stream-time domain (ABI 5; include/ksqldb_hip.h KHIP_TIME_*)."""
     ct = (i32 * max(len(col_types), 1))(*[TYPE[t] if isinstance(t, str) else t for t in col_types])
     sp = (AggSpec * max(len(aggs), 1))(*[AggSpec(AGG[k] if isinstance(k, str) else k, c) for k, c in aggs])
     d = AggDesc(WINDOW[window_kind] if isinstance(window_kind, str) else window_kind,
@@ -352,7 +363,8 @@ def make_agg_desc(window_kind="NONE", key_type="INT64", size_ms=0, advance_ms=0,
                 size_ms, advance_ms if advance_ms else size_ms, grace_ms, len(col_types), ct,
                 len(aggs), sp, device, flags, capacity_hint, retention_ms,
                 EMIT[emit] if isinstance(emit, str) else emit, 0 if having is None else 1,
-                Having() if having is None else having_struct(having))
+                Having() if having is None else having_struct(having),
+                TIME[time_domain] if isinstance(time_domain, str) else time_domain, n_partitions)
     d._keep = (ct, sp)
     return d
 
@@ -374,15 +386,16 @@ class DeviceBatch:
     """A khip_batch over device tensors (torch) — the caller keeps the tensors alive."""
 
     def __init__(self, ts, keys=None, key_valid=None, row_valid=None, cols=(), col_valid=(),
-                 key_offsets=None, key_bytes=None):
-        self._keep = [ts, keys, key_valid, row_valid, key_offsets, key_bytes] + list(cols) + list(col_valid)
+                 key_offsets=None, key_bytes=None, partition=None, stream_time=None):
+        self._keep = [ts, keys, key_valid, row_valid, key_offsets, key_bytes, partition, stream_time] + \
+            list(cols) + list(col_valid)
         p = lambda t: None if t is None else t.data_ptr()
         nc = len(cols)
         cv = list(col_valid) + [None] * (nc - len(col_valid))
         self._cd = (C.c_void_p * max(nc, 1))(*[p(c) for c in cols])
         self._cv = (C.c_void_p * max(nc, 1))(*[p(v) for v in cv])
         self.struct = Batch(int(ts.numel()), MEM_DEVICE, nc, p(keys), p(key_offsets), p(key_bytes),
-                            p(key_valid), p(row_valid), p(ts), self._cd, self._cv)
+                            p(key_valid), p(row_valid), p(ts), self._cd, self._cv, p(partition), p(stream_time))
 
 
 def bitmap_torch(valid_bool):
@@ -535,6 +548,21 @@ class AggHandle:
         else:
             out["key"] = arrays["key"][:m]
         return out, KHIP_OK, m
+
+    def stream_time_scan(self, batch, seed=-1, out=None):
+        """khip_stream_time_scan (ABI 5): the stream time observed at each row of `batch` starting
+        from `seed`.  Host batch → (int64 array, max); device batch → `out` (an int64 device tensor
+        of n_rows) is filled and (out, max) returned."""
+        n = int(batch.struct.n_rows)
+        mx = i64()
+        if batch.struct.mem == MEM_HOST:
+            res = np.zeros(max(n, 1), np.int64)
+            self.lib.check(self.lib.stream_time_scan(self.h, C.byref(batch.struct), seed, res.ctypes.data, C.byref(mx)),
+                           "stream_time_scan")
+            return res[:n], mx.value
+        self.lib.check(self.lib.stream_time_scan(self.h, C.byref(batch.struct), seed, out.data_ptr(), C.byref(mx)),
+                       "stream_time_scan")
+        return out, mx.value
 
     def kernel_times(self, reset=False):
         kt = KernelTimes()

@@ -40,7 +40,8 @@ namespace khip {
 __global__ __launch_bounds__(BLOCK) void k_blockmax(const int64_t* __restrict__ ts,
                                                     const uint8_t* __restrict__ kv,
                                                     const uint8_t* __restrict__ rv, int64_t n,
-                                                    int64_t* __restrict__ blockmax) {
+                                                    int64_t* __restrict__ blockmax,
+                                                    const int64_t* __restrict__ st_at) {
   __shared__ int64_t lds[BLOCK / 64];
   const int64_t base = (int64_t)blockIdx.x * RPB;
   int64_t m = -1;
@@ -48,7 +49,8 @@ __global__ __launch_bounds__(BLOCK) void k_blockmax(const int64_t* __restrict__ 
   for (int k = 0; k < ITEMS; k++) {
     const int64_t i = base + k * BLOCK + threadIdx.x;
     if (i < n && bit_get(kv, i) && bit_get(rv, i)) {
-      const int64_t t = ts[i];
+      // ABI 5 domains: the row's given stream time (an upper bound of its ts), else its ts
+      const int64_t t = ts[i] < 0 ? -1 : (st_at ? st_at[i] : ts[i]);
       m = t > m ? t : m;
     }
   }
@@ -233,7 +235,8 @@ __global__ __launch_bounds__(BLOCK) void k_apply(ApplyParams p, const int64_t* _
                                                  const int64_t* __restrict__ blockprefix, int64_t n,
                                                  uint64_t* __restrict__ table, uint64_t mask,
                                                  int32_t* __restrict__ resume,
-                                                 int64_t* __restrict__ partials, int resume_mode) {
+                                                 int64_t* __restrict__ partials, int resume_mode,
+                                                 const int64_t* __restrict__ st_at) {
   __shared__ int64_t lds_scan[BLOCK / 64];
   __shared__ unsigned long long lds_cnt[NPART];
   if (threadIdx.x < NPART) lds_cnt[threadIdx.x] = 0;
@@ -251,9 +254,10 @@ __global__ __launch_bounds__(BLOCK) void k_apply(ApplyParams p, const int64_t* _
     const bool valid = kval && rval && t >= 0;
     int64_t tot;
     const int64_t incl = block_incl_max(valid ? t : -1, lds_scan, &tot);
-    const int64_t st = incl > carry ? incl : carry;  // stream time after this record
+    int64_t st = incl > carry ? incl : carry;  // stream time after this record
     carry = tot > carry ? tot : carry;
     if (!in) continue;
+    if (st_at) st = st_at[i];  // ABI 5 domains: given per row
     int64_t j0 = 0;
     if (resume_mode) {
       j0 = resume[i];
@@ -841,7 +845,8 @@ khip_status emit_final_lost(khip_agg* a, const int64_t* ts, const uint8_t* kv, c
   hs[0] = a->st_before;
   KHIP_TRY_HIP(hipMemcpyAsync(seed, hs, 8, hipMemcpyHostToDevice, a->stream));
   KHIP_TRY_HIP(hipMemsetAsync(a->lostctr.p, 0, 8, a->stream));
-  hipLaunchKernelGGL(k_blockmax, dim3(nb), dim3(BLOCK), 0, a->stream, ts, kv, rv, n, a->blockmax.as<int64_t>());
+  hipLaunchKernelGGL(k_blockmax, dim3(nb), dim3(BLOCK), 0, a->stream, ts, kv, rv, n, a->blockmax.as<int64_t>(),
+                     (const int64_t*)nullptr);
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, a->stream, a->blockmax.as<int64_t>(), nb,
                      a->blockprefix.as<int64_t>(), seed);
   hipLaunchKernelGGL(k_emit_lost, dim3(nb), dim3(BLOCK), 0, a->stream, ts, kv, rv, n, a->blockprefix.as<int64_t>(),
@@ -933,6 +938,16 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
     if (d.retention_ms < 0 || d.retention_ms < d.size_ms + g)
       return fail(KHIP_E_INVALID, "retention must be at least window size + grace");
   }
+  if (d.time_domain < KHIP_TIME_TASK || d.time_domain > KHIP_TIME_SUPPLIED) return fail(KHIP_E_INVALID, "time domain");
+  if (d.time_domain != KHIP_TIME_TASK) {
+    if (d.window_kind == KHIP_WINDOW_SESSION) return fail(KHIP_E_UNSUPPORTED, "stream-time domains on SESSION windows");
+    if (d.flags & KHIP_FLAG_TABLE_SOURCE) return fail(KHIP_E_UNSUPPORTED, "stream-time domains of a table source");
+    if (d.emit == KHIP_EMIT_FINAL) return fail(KHIP_E_UNSUPPORTED, "EMIT FINAL with a stream-time domain");
+    if (d.time_domain == KHIP_TIME_PARTITION && d.retention_ms != KHIP_RETENTION_DEFAULT)
+      return fail(KHIP_E_UNSUPPORTED, "RETENTION with per-partition stream times");
+    if (d.time_domain == KHIP_TIME_PARTITION && (d.n_partitions < 1 || d.n_partitions > 65536))
+      return fail(KHIP_E_INVALID, "n_partitions must be in [1, 65536]");
+  }
   if (d.has_having) {
     if (d.having.agg_index < 0 || d.having.agg_index >= d.n_aggs) return fail(KHIP_E_INVALID, "having agg index");
     if (d.having.op < KHIP_OP_GT || d.having.op > KHIP_OP_NE) return fail(KHIP_E_INVALID, "having op");
@@ -993,6 +1008,14 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
   a->cap = cap;
   int64_t m1 = -1;
   hipMemcpyAsync(a->stream_time.p, &m1, 8, hipMemcpyHostToDevice, a->stream);
+  if (d.time_domain == KHIP_TIME_PARTITION) {  // every partition's stream time: none yet
+    if ((st = a->pst.ensure((size_t)d.n_partitions * 8)) != KHIP_OK ||
+        (st = a->pst2.ensure((size_t)d.n_partitions * 8)) != KHIP_OK) {
+      khip_agg_destroy(a);
+      return st;
+    }
+    hipMemsetAsync(a->pst.p, 0xFF, (size_t)d.n_partitions * 8, a->stream);
+  }
   if (d.key_type == KHIP_KEY_UTF8) {
     if ((st = dict_init(a->dict, a->stream)) != KHIP_OK) {
       khip_agg_destroy(a);
@@ -1203,6 +1226,27 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   int64_t key_bytes_total = 0;
   KHIP_TRY(resolve_batch(a, b, &keys, &ts, &kv, &rv, &koff, &kbytes, &cols, &key_bytes_total));
   if (final_emit) KHIP_TRY(emit_final_lost(a, ts, kv, rv, n, 0, nullptr));
+  // ---- ABI 5 stream-time domains: the stream time observed at every row
+  const int64_t* st_at = nullptr;
+  if (a->desc.time_domain == KHIP_TIME_SUPPLIED) {
+    if (!b->stream_time) return fail(KHIP_E_INVALID, "KHIP_TIME_SUPPLIED: the batch has no stream_time column");
+    if (b->mem == KHIP_MEM_HOST) {
+      KHIP_TRY(stage(a, a->st_col, b->stream_time, n * 8));
+      st_at = a->st_col.as<int64_t>();
+    } else {
+      st_at = b->stream_time;
+    }
+  } else if (a->desc.time_domain == KHIP_TIME_PARTITION) {
+    if (!b->partition) return fail(KHIP_E_INVALID, "KHIP_TIME_PARTITION: the batch has no partition column");
+    const int32_t* part = b->partition;
+    if (b->mem == KHIP_MEM_HOST) {
+      KHIP_TRY(stage(a, a->st_part, b->partition, n * 4));
+      part = a->st_part.as<int32_t>();
+    }
+    KHIP_TRY(a->st_col.ensure((size_t)n * 8));
+    KHIP_TRY(stream_time_column(a, ts, kv, rv, part, n, -1, a->st_col.as<int64_t>(), nullptr));
+    st_at = a->st_col.as<int64_t>();
+  }
   // ---- UTF8 keys → stable key ids
   const int64_t* hkeys = keys;
   if (utf8) {
@@ -1231,7 +1275,7 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
         if (cs.valid[c]) cs.valid[c] += off / 8;
       }
       KHIP_TRY(part_push(a, m, keys + off, ts + off, kv ? kv + off / 8 : nullptr, rv ? rv + off / 8 : nullptr, cs,
-                         tot));
+                         tot, st_at ? st_at + off : nullptr));
     }
     a->occ += tot[P_NEW];
     if (a->profile) {  // events of the last slice
@@ -1256,7 +1300,8 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   KHIP_TRY_HIP(hipMemsetAsync(a->counters.p, 0, 8 * NPART, a->stream));
   // ---- stream time before each block (atomic engine)
   ev_record(a, 0);
-  hipLaunchKernelGGL(k_blockmax, dim3(nb), dim3(BLOCK), 0, a->stream, ts, kv, rv, n, a->blockmax.as<int64_t>());
+  hipLaunchKernelGGL(k_blockmax, dim3(nb), dim3(BLOCK), 0, a->stream, ts, kv, rv, n, a->blockmax.as<int64_t>(),
+                     st_at);
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, a->stream, a->blockmax.as<int64_t>(), nb,
                      a->blockprefix.as<int64_t>(), a->stream_time.as<int64_t>());
   KHIP_TRY_HIP(hipGetLastError());
@@ -1270,7 +1315,7 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
     ev_record(a, 3);
     hipLaunchKernelGGL(k_apply, dim3(nb), dim3(BLOCK), 0, a->stream, a->ap, hkeys, keys, ts, kv, rv, cols,
                        a->blockprefix.as<int64_t>(), n, a->table.as<uint64_t>(), (uint64_t)(a->cap - 1),
-                       a->resume.as<int32_t>(), a->partials.as<int64_t>(), pass > 0 ? 1 : 0);
+                       a->resume.as<int32_t>(), a->partials.as<int64_t>(), pass > 0 ? 1 : 0, st_at);
     ev_record(a, 4);
     hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(256), 0, a->stream, a->partials.as<int64_t>(), nb, NPART,
                        a->counters.as<int64_t>());
@@ -1305,6 +1350,8 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
     KHIP_TRY_HIP(hipMemcpyAsync(&a->host_stream_time, a->stream_time.p, 8, hipMemcpyDeviceToHost, a->stream));
     KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
   }
+  // one task per partition: the handle's stream time (closing windows, retention) is the slowest's
+  if (a->desc.time_domain == KHIP_TIME_PARTITION) KHIP_TRY(stream_time_partition_min(a));
   if (final_emit) KHIP_TRY(finish_lost(a, ts, kv, rv, n));
   if (a->engine == 0 && a->windowed) {  // retention: drop expired windows from the closed store
     HavingDev vis{};
@@ -1320,6 +1367,37 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   s.windows_late = tot[P_LATE];
   s.stream_time = a->host_stream_time;
   if (stats) *stats = s;
+  return KHIP_OK;
+}
+
+khip_status khip_stream_time_scan(khip_agg* a, const khip_batch* b, int64_t seed, int64_t* out, int64_t* out_max) {
+  clear_error();
+  if (!a || !b || !out_max || (b->n_rows > 0 && (!out || !b->ts))) return fail(KHIP_E_INVALID, "null argument");
+  if (b->n_rows < 0) return fail(KHIP_E_INVALID, "batch shape");
+  DeviceGuard g(a->device);
+  const int64_t n = b->n_rows;
+  *out_max = seed < -1 ? -1 : seed;
+  if (n == 0) return KHIP_OK;
+  const int64_t* ts = b->ts;
+  const uint8_t *kv = b->key_valid, *rv = b->row_valid;
+  int64_t* dst = out;
+  const size_t bm = (size_t)(n + 7) / 8;
+  if (b->mem == KHIP_MEM_HOST) {
+    KHIP_TRY(stage(a, a->st_ts, b->ts, n * 8));
+    ts = a->st_ts.as<int64_t>();
+    if (kv) { KHIP_TRY(stage(a, a->st_kv, kv, bm)); kv = a->st_kv.as<uint8_t>(); }
+    if (rv) { KHIP_TRY(stage(a, a->st_rv, rv, bm)); rv = a->st_rv.as<uint8_t>(); }
+    KHIP_TRY(a->st_col.ensure((size_t)n * 8));
+    dst = a->st_col.as<int64_t>();
+  } else if (b->mem != KHIP_MEM_DEVICE) {
+    return fail(KHIP_E_INVALID, "batch mem");
+  }
+  KHIP_TRY(a->st_seen.ensure(8));
+  int64_t* last = a->st_seen.as<int64_t>();
+  KHIP_TRY(stream_time_column(a, ts, kv, rv, nullptr, n, seed < -1 ? -1 : seed, dst, last));
+  if (b->mem == KHIP_MEM_HOST) KHIP_TRY_HIP(hipMemcpyAsync(out, dst, (size_t)n * 8, hipMemcpyDeviceToHost, a->stream));
+  KHIP_TRY_HIP(hipMemcpyAsync(out_max, last, 8, hipMemcpyDeviceToHost, a->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
   return KHIP_OK;
 }
 
@@ -1667,6 +1745,8 @@ khip_status khip_agg_reset(khip_agg* a) {
   if (a->desc.key_type == KHIP_KEY_UTF8) {
     KHIP_TRY(dict_clear(a->dict, a->stream));
   }
+  if (a->desc.time_domain == KHIP_TIME_PARTITION)
+    KHIP_TRY_HIP(hipMemsetAsync(a->pst.p, 0xFF, (size_t)a->desc.n_partitions * 8, a->stream));
   // asynchronous on the handle's stream (every later call on the handle is ordered behind it)
   KHIP_TRY_HIP(hipGetLastError());
   a->occ = 0;

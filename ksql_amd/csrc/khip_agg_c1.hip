@@ -1,0 +1,1160 @@
+// khip_agg_c1.hip — the windowed COUNT(*) pipeline of the partitioned engine (C2's query:
+// `SELECT k, COUNT(*) ... WINDOW TUMBLING ... GROUP BY k [HAVING ...]`).
+//
+// Same contract as part_push's general path (khip_agg_part.hip) — per record (SURVEY §8.0,
+// Kafka Streams' KStreamWindowAggregate as called from S/StreamAggregateBuilder.java:287-294):
+// stream time, TimeWindows.windowsFor, late drop, store update, row time = max ts — but the input
+// is read once for the records and once (keys only) for the bucket offsets, and every record
+// moves as 8 bytes:
+//
+//   k_c1_hist     keys only: per 64K-record tile, a histogram over the B coarse buckets (top bits
+//                 of the key hash) and the key range (global atomics)
+//   (k_part_colsum / colbase / pscan / colprefix over B columns: each (tile, bucket) run's offset)
+//   k_c1_scatter  keys, ts, validity: every record → its bucket's run as (key - kmin, ts - T0),
+//                 two int32s; invalid records (null key / row, ts < 0) as sentinels; per step of
+//                 4096 records the largest and smallest accepted ts, per tile the counters.
+//                 Optimistic: no record is assumed late.
+//   k_c1_check    one workgroup: stream time before each 4096-record step (exclusive prefix
+//                 max), and the push is ACCEPTED only if no step can hold a late record (the
+//                 general path's `fast` test per step), every ts fits ts - T0 in 31 bits and the
+//                 key range fits 32 bits; otherwise nothing was written and the host runs the
+//                 general path.
+//                 Also the window range, the group-identity width and the refine's chunk list.
+//   k_c1_refine   per 8K-record chunk of a bucket: sentinels dropped, records counting-sorted by
+//                 their partition inside the bucket (LDS), written back contiguously; the chunk's
+//                 per-partition offsets (u16) go to a segment table
+//   k_c1_merge    persistent workgroups, one partition per item: the partition's records are its
+//                 segments of the bucket's chunks; (key - kmin, window) → a 32-bit identity when
+//                 it fits (no key hash on the record path), LDS identity CAS + u32 row-time max +
+//                 u32 count, claimed entries listed (the write-out walks the list, not the table);
+//                 resident rows merged, closed rows evicted, HAVING counts and changelog flags
+//                 maintained exactly as k_part_merge_c1 does (k_part_commit publishes)
+//
+// Algorithmic bytes per record: 8 (hist) + 16 + 8 (scatter) + 8 + 8 (refine) + 8 (merge read)
+// + the table rows written (32 B per group) — against 16 + 24 + 16 + 8 + rows for the general
+// path (DESIGN.md §(d)).
+#include <algorithm>
+#include <vector>
+
+#include "khip_part.hpp"
+
+namespace khip {
+
+constexpr int C1_TILE = 65536;   // records per hist / scatter tile (the general path's tile)
+constexpr int C1_NT = 512;       // workgroup size of every kernel here
+constexpr int C1_CH = 8192;      // refine chunk (records), 16 per thread
+constexpr int C1_SEGMAX = 512;   // chunks of one bucket the merge can hold (4M records)
+constexpr uint32_t C1_SENT = 0x80000000u;  // low word of a sentinel record (ts - T0 never is)
+
+// c1info (int64) slots
+enum {
+  CI_KMIN = 0,   // atomics (k_c1_hist), reset by k_c1_check for the next push
+  CI_KMAX = 1,
+  CI_TFAIL = 2,  // some accepted ts - T0 outside int32 (k_c1_scatter)
+  CI_T0 = 3,     // time base (k_c1_hist block 0)
+  CI_GATE = 4,   // accepted (k_part_commit reads gate[4])
+  CI_WBASE = 5,  // smallest window index (records and live resident rows)
+  CI_WBITS = 6,
+  CI_ID32 = 7,   // identity mode: 1 = u32 (krel << wbits | wrel), 0 = u64 (krel << 32 | wrel)
+  CI_TMIN = 8,   // smallest accepted ts (row-time deltas are relative to it)
+  CI_TMAX = 9,
+  CI_KBITS = 10,
+  CI_NCHUNK = 11,  // refine work items
+  CI_KMINC = 12,   // kmin copied for the refine / merge
+  CI_WHI = 13,     // largest relative window index
+  CI_KRANGE = 14,
+  CI_N = 16
+};
+
+__device__ __forceinline__ int bits_of(uint64_t v) { return v ? 64 - __clzll((long long)v) : 0; }
+
+// ------------------------------------------------------------------ k_c1_hist
+// Keys only (8 B/record): the tile's bucket histogram and key range.  Every record i < n counts
+// (k_c1_scatter writes a sentinel for the invalid ones), so no validity or ts is read here.
+template <bool VEC>
+__global__ __launch_bounds__(C1_NT) void k_c1_hist(const int64_t* __restrict__ keys, const int64_t* __restrict__ ts,
+                                                   int64_t n, int64_t nT, int log2B, uint32_t* __restrict__ hist,
+                                                   int64_t* __restrict__ ci, const int64_t* __restrict__ stream_time) {
+  __shared__ uint32_t lh[512];
+  __shared__ int64_t lk[2][C1_NT / 64];
+  const int B = 1 << log2B;
+  const int64_t t = tile_of(blockIdx.x, nT);
+  for (int b = threadIdx.x; b < B; b += C1_NT) lh[b] = 0;
+  __syncthreads();
+  const int64_t base = t * C1_TILE;
+  const int64_t end = base + C1_TILE < n ? base + C1_TILE : n;
+  const int shift = 64 - log2B;
+  int64_t kmx = INT64_MIN, kmxn = INT64_MIN;  // max of key and of ~key (= ~min)
+  auto one = [&](int64_t k) {
+    kmx = k > kmx ? k : kmx;
+    kmxn = ~k > kmxn ? ~k : kmxn;
+    atomicAdd(&lh[log2B == 0 ? 0u : (uint32_t)(key_hash(k) >> shift)], 1u);
+  };
+  if constexpr (VEC) {  // 16-byte loads: pairs of keys (keys is 16-byte aligned, base is even)
+    const longlong2* kp = (const longlong2*)(keys + base);
+    const int64_t npair = (end - base + 1) >> 1;
+    for (int64_t j0 = threadIdx.x; j0 < npair; j0 += 8 * C1_NT) {
+      longlong2 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int64_t j = j0 + (int64_t)u * C1_NT;
+        v[u] = j < npair ? kp[j] : make_longlong2(0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int64_t j = j0 + (int64_t)u * C1_NT;
+        if (j >= npair) continue;
+        one(v[u].x);
+        if (base + 2 * j + 1 < end) one(v[u].y);
+      }
+    }
+  } else {
+    for (int64_t i0 = base + threadIdx.x; i0 < end; i0 += 8 * C1_NT) {
+      int64_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int64_t i = i0 + (int64_t)u * C1_NT;
+        v[u] = i < end ? keys[i] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (i0 + (int64_t)u * C1_NT < end) one(v[u]);
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const int64_t a = __shfl_xor(kmx, off, 64), b = __shfl_xor(kmxn, off, 64);
+    kmx = a > kmx ? a : kmx;
+    kmxn = b > kmxn ? b : kmxn;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    lk[0][threadIdx.x >> 6] = kmx;
+    lk[1][threadIdx.x >> 6] = kmxn;
+  }
+  __syncthreads();
+  uint32_t* hrow = hist + t * (int64_t)B;
+  for (int b = threadIdx.x; b < B; b += C1_NT) hrow[b] = lh[b];
+  if (threadIdx.x == 0) {
+    int64_t a = INT64_MIN, c = INT64_MIN;
+    for (int w = 0; w < C1_NT / 64; w++) {
+      a = lk[0][w] > a ? lk[0][w] : a;
+      c = lk[1][w] > c ? lk[1][w] : c;
+    }
+    if (end > base) {
+      atomicMax((long long*)&ci[CI_KMAX], (long long)a);
+      atomicMin((long long*)&ci[CI_KMIN], (long long)~c);
+    }
+    if (blockIdx.x == 0) {  // time base: the stream time before the push, else the first ts
+      const int64_t st0 = *stream_time;
+      const int64_t t0 = n > 0 ? ts[0] : 0;
+      ci[CI_T0] = st0 >= 0 ? st0 : (t0 > 0 ? t0 : 0);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ k_c1_scatter
+// Records of tile t → their bucket's run (offs[t][b] from the column prefix).  8-byte record:
+// (key - kmin) << 32 | (uint32)(ts - T0); invalid records keep their key word (their bucket is the
+// key's) with the sentinel low word.  Same staged step as k_part_scatter_r8.
+template <int U, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_c1_scatter(
+    const int64_t* __restrict__ keys, const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
+    const uint8_t* __restrict__ rv, int64_t n, int64_t nT, int log2B, const uint32_t* __restrict__ offs,
+    uint64_t* __restrict__ srec, int64_t* __restrict__ stepstat, int64_t* __restrict__ tpart,
+    int64_t* __restrict__ ci, const int64_t* __restrict__ st_at) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int wsum[NT / 64];
+  __shared__ unsigned long long lc[4];
+  __shared__ int64_t lt[2][2][NT / 64];  // [step parity][max | min][wave]
+  __shared__ int lfail;
+  constexpr int S = U * NT;
+  const int B = 1 << log2B;
+  const int64_t t = tile_of(blockIdx.x, nT);
+  const StageR8 L = stage_r8_carve(smem, B, S, wsum);
+  for (int b = threadIdx.x; b < B; b += NT) {
+    L.cur[b] = offs[t * B + b];
+    L.cnt[b] = 0u;
+  }
+  if (threadIdx.x < 4) lc[threadIdx.x] = 0;
+  if (threadIdx.x == 0) lfail = 0;
+  const int64_t kmin = ci[CI_KMIN], T0 = ci[CI_T0];
+  const int shift = log2B == 0 ? 64 : 64 - log2B;
+  const uint32_t bmask = (uint32_t)(B - 1);
+  const int64_t base = t * C1_TILE;
+  const int64_t end = base + C1_TILE < n ? base + C1_TILE : n;
+  int64_t c_acc = 0, c_nk = 0, c_nr = 0, c_bt = 0;
+  bool tfail = false;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int64_t x[U], k[U];
+  auto load_step = [&](int64_t i0, int64_t (&dx)[U], int64_t (&dk)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      int64_t i = i0 + (int64_t)u * NT;
+      i = i < end ? i : end - 1;
+      dx[u] = ts[i];
+      dk[u] = keys[i];
+    }
+  };
+  lds_barrier();
+  int64_t s0 = base;
+  if (s0 < end) load_step(s0 + threadIdx.x, x, k);
+  for (int st = 0; s0 < end; s0 += S, st++) {  // uniform across the block: barriers inside
+    const int64_t i0 = s0 + threadIdx.x;
+    bool ok[U];
+    uint32_t bin[U];
+    int64_t rec[U];
+    int64_t tmx = -1, tmn = INT64_MAX;  // this step's accepted ts range (k_c1_check's late test)
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t i = i0 + (int64_t)u * NT;
+      ok[u] = i < end;
+      const bool kok = bit_get(kv, ok[u] ? i : base), rok = bit_get(rv, ok[u] ? i : base);
+      const bool valid = ok[u] && kok && rok && x[u] >= 0;
+      c_nk += ok[u] && !kok;
+      c_nr += ok[u] && kok && !rok;
+      c_bt += ok[u] && kok && rok && x[u] < 0;
+      c_acc += valid;
+      const int64_t sx = st_at ? st_at[ok[u] ? i : base] : x[u];  // ABI 5 domains: the given stream time
+      tmx = valid && sx > tmx ? sx : tmx;
+      tmn = valid && x[u] < tmn ? x[u] : tmn;
+      const int64_t d = x[u] - T0;
+      tfail |= valid && (d <= (int64_t)INT32_MIN || d > (int64_t)INT32_MAX);
+      bin[u] = stage_bin(key_hash(k[u]), shift, bmask);
+      rec[u] = (int64_t)(((uint64_t)(k[u] - kmin) << 32) | (valid ? (uint64_t)(uint32_t)d : (uint64_t)C1_SENT));
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      const int64_t a = __shfl_xor(tmx, off, 64), b = __shfl_xor(tmn, off, 64);
+      tmx = a > tmx ? a : tmx;
+      tmn = b < tmn ? b : tmn;
+    }
+    if (lane == 0) {
+      lt[st & 1][0][wave] = tmx;
+      lt[st & 1][1][wave] = tmn;
+    }
+    // the next step's loads go into x / k (dead now) and stay in flight through this step's stage
+    if (s0 + S < end) load_step(i0 + S, x, k);
+    stage_step_r8<U, NT>(rec, bin, ok, B, L, srec);
+    if (threadIdx.x == 0) {  // the stage's barriers ordered every wave's lt write before this
+      int64_t a = -1, b = INT64_MAX;
+#pragma unroll
+      for (int w = 0; w < NT / 64; w++) {
+        a = lt[st & 1][0][w] > a ? lt[st & 1][0][w] : a;
+        b = lt[st & 1][1][w] < b ? lt[st & 1][1][w] : b;
+      }
+      const int64_t g = (s0 / S) * 2;  // global step index (records [g/2 * S, +S))
+      stepstat[g] = a;
+      stepstat[g + 1] = b;
+    }
+  }
+  c_acc = wave_sum(c_acc);
+  c_nk = wave_sum(c_nk);
+  c_nr = wave_sum(c_nr);
+  c_bt = wave_sum(c_bt);
+  if ((threadIdx.x & 63) == 0) {
+    if (c_acc) atomicAdd(&lc[0], (unsigned long long)c_acc);
+    if (c_nk) atomicAdd(&lc[1], (unsigned long long)c_nk);
+    if (c_nr) atomicAdd(&lc[2], (unsigned long long)c_nr);
+    if (c_bt) atomicAdd(&lc[3], (unsigned long long)c_bt);
+  }
+  if (tfail) lfail = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t* tp = tpart + t * T_NPART;
+    tp[T_ACCEPTED] = (int64_t)lc[0];
+    tp[T_NULL_KEY] = (int64_t)lc[1];
+    tp[T_NULL_ROW] = (int64_t)lc[2];
+    tp[T_BAD_TS] = (int64_t)lc[3];
+    tp[T_APPLIED] = (int64_t)lc[0];  // TUMBLING: one window per accepted record, none late (checked)
+    tp[T_LATE] = 0;
+    if (lfail) atomicOr((unsigned long long*)&ci[CI_TFAIL], 1ULL);
+  }
+}
+
+// ------------------------------------------------------------------ k_c1_check
+// One workgroup.  Accept the push when no scatter step (4096 consecutive records) can hold a late
+// record: the step's earliest window outlives the largest stream time the step reaches,
+// max(stream time before the step, the step's max ts) - grace (the general path's per-tile `fast`
+// test at step granularity; S/StreamAggregateBuilder.java:272-277 for the grace).
+// Accepted: publish the stream time, the window range (k_part_wrange's rules, resident rows
+// included), the identity width and the refine's chunk list (cstart); reset the counters the
+// merge and commit use.  Declined: nothing persistent is touched.
+__global__ __launch_bounds__(1024) void k_c1_check(
+    const int64_t* __restrict__ stepstat, int64_t nS, int64_t size, int64_t adv, FastDiv fd, int64_t grace,
+    int64_t close0, int fresh, int log2B, const int64_t* __restrict__ bb, int* __restrict__ cstart,
+    int64_t* __restrict__ ci, int64_t* __restrict__ stream_time, int64_t* __restrict__ res,
+    unsigned long long* __restrict__ ctr, unsigned long long* __restrict__ closed_ctr, unsigned long long closed_n) {
+  __shared__ int64_t wmx[16];
+  __shared__ int64_t red[4][16];
+  __shared__ int lslow;
+  __shared__ int lnch[512 + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x == 0) lslow = 0;
+  const int64_t st0 = *stream_time;
+  // thread j owns steps [j K, (j + 1) K): its maximum, the block's exclusive prefix of those, then
+  // a sequential walk with the running stream time
+  const int64_t K = (nS + 1023) / 1024;
+  const int64_t g0 = threadIdx.x * K, g1 = g0 + K < nS ? g0 + K : nS;
+  int64_t m = -1;
+  for (int64_t g = g0; g < g1; g++) m = stepstat[2 * g] > m ? stepstat[2 * g] : m;
+  const int64_t incl = wave_incl_max(m);
+  if (lane == 63) wmx[wave] = incl;
+  __syncthreads();
+  int64_t pre = st0;
+  for (int w = 0; w < wave; w++) pre = wmx[w] > pre ? wmx[w] : pre;
+  const int64_t excl = __shfl_up(incl, 1, 64);
+  int64_t run = lane == 0 ? pre : (excl > pre ? excl : pre);  // stream time before step g0
+  int64_t gmn = INT64_MAX, gmx = -1;
+  bool slow = false;
+  for (int64_t g = g0; g < g1; g++) {
+    const int64_t mx = stepstat[2 * g], mn = stepstat[2 * g + 1];
+    if (mn != INT64_MAX) {
+      const int64_t smax = run > mx ? run : mx;
+      slow |= !(first_window_start(mn, size, adv) + size > smax - grace);
+      gmn = mn < gmn ? mn : gmn;
+    }
+    run = mx > run ? mx : run;
+    gmx = mx > gmx ? mx : gmx;
+  }
+  if (slow) lslow = 1;
+  for (int off = 32; off > 0; off >>= 1) {
+    const int64_t a = __shfl_xor(gmn, off, 64), b = __shfl_xor(gmx, off, 64);
+    gmn = a < gmn ? a : gmn;
+    gmx = b > gmx ? b : gmx;
+  }
+  if (lane == 0) {
+    red[0][wave] = gmn;
+    red[1][wave] = gmx;
+  }
+  // chunks per bucket → cstart (exclusive prefix), largest bucket's chunk count
+  const int B = 1 << log2B;
+  for (int b = threadIdx.x; b < B; b += 1024) lnch[b] = (int)((bb[b + 1] - bb[b] + C1_CH - 1) / C1_CH);
+  __syncthreads();
+  if (threadIdx.x) return;
+  for (int w = 0; w < 16; w++) {
+    gmn = red[0][w] < gmn ? red[0][w] : gmn;
+    gmx = red[1][w] > gmx ? red[1][w] : gmx;
+  }
+  int acc = 0, mxc = 0;
+  for (int b = 0; b < B; b++) {
+    cstart[b] = acc;
+    acc += lnch[b];
+    mxc = lnch[b] > mxc ? lnch[b] : mxc;
+  }
+  cstart[B] = acc;
+  const int64_t kmin = ci[CI_KMIN], kmax = ci[CI_KMAX];
+  ci[CI_KMIN] = INT64_MAX;  // ready for the next push's atomics
+  ci[CI_KMAX] = INT64_MIN;
+  const bool tfail = ci[CI_TFAIL] != 0;
+  ci[CI_TFAIL] = 0;
+  bool ok = !lslow && !tfail && mxc <= C1_SEGMAX && kmax >= kmin;
+  const uint64_t krange = ok ? (uint64_t)kmax - (uint64_t)kmin : 0;
+  ok = ok && krange < 0xFFFFFFFFull;
+  // window range of this push's records and of the live resident rows (k_part_wrange)
+  int64_t lo = INT64_MAX, hi = INT64_MIN;
+  if (gmx >= 0) {
+    const int64_t l = gmn - size + adv;
+    lo = (int64_t)fast_udiv((uint64_t)(l > 0 ? l : 0), fd);
+    hi = (int64_t)fast_udiv((uint64_t)gmx, fd);
+  }
+  if (!fresh) {
+    int64_t rlo = res[0];
+    const int64_t rhi = res[1];
+    if (close0 != INT64_MIN && rlo != INT64_MAX) {  // live: ws > close0 - size
+      const int64_t c = close0 - size;
+      const int64_t lb = c >= 0 ? (int64_t)fast_udiv((uint64_t)c, fd) + 1 : 0;
+      rlo = rlo > lb ? rlo : lb;
+    }
+    lo = rlo < lo ? rlo : lo;
+    hi = rhi > hi ? rhi : hi;
+  }
+  const bool none = lo > hi;  // nothing live, nothing new
+  if (none) lo = hi = 0;
+  ok = ok && (uint64_t)(hi - lo) < 0xFFFFFFFEull;
+  const int wbits = bits_of((uint64_t)(hi - lo)), kbits = bits_of(krange);
+  ci[CI_GATE] = ok ? 1 : 0;
+  if (!ok) return;
+  ci[CI_WBASE] = lo;
+  ci[CI_WHI] = hi - lo;
+  ci[CI_WBITS] = wbits;
+  ci[CI_KBITS] = kbits;
+  ci[CI_KRANGE] = (int64_t)krange;
+  ci[CI_ID32] = kbits + wbits <= 31 ? 1 : 0;
+  ci[CI_TMIN] = gmx >= 0 ? gmn : 0;
+  ci[CI_TMAX] = gmx;
+  ci[CI_NCHUNK] = acc;
+  ci[CI_KMINC] = kmin;
+  *stream_time = gmx > st0 ? gmx : st0;
+  res[0] = none ? INT64_MAX : lo;
+  res[1] = none ? INT64_MIN : hi;
+  ctr[0] = ctr[1] = ctr[2] = 0ULL;
+  if (closed_ctr) *closed_ctr = closed_n;
+}
+
+// ------------------------------------------------------------------ k_c1_refine
+// Work item w = chunk c of bucket b (cstart): its records are counting-sorted by partition
+// inside the bucket (F = 2^fbits bins) in LDS and written back to the same positions of the
+// output; seg[w][f] (u16) = partition f's first record in the chunk, seg[w][F] = valid records.
+template <int U, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_c1_refine(
+    const uint64_t* __restrict__ srcA, const int64_t* __restrict__ bb, const int* __restrict__ cstart, int log2B,
+    int log2P, int fbits, uint64_t* __restrict__ srec, uint16_t* __restrict__ seg, const int64_t* __restrict__ ci) {
+  if (ci[CI_GATE] == 0) return;
+  const int w = blockIdx.x;
+  if (w >= (int)ci[CI_NCHUNK]) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int lb;
+  __shared__ int wsum[NT / 64];
+  constexpr int S = U * NT;
+  static_assert(S == C1_CH, "refine chunk");
+  const int F = 1 << fbits, B = 1 << log2B;
+  uint32_t* cnt = (uint32_t*)smem;
+  uint32_t* sbase = cnt + F;
+  uint64_t* stage = (uint64_t*)(smem + (size_t)F * 8);
+  for (int f = threadIdx.x; f < F; f += NT) cnt[f] = 0u;
+  if (threadIdx.x == 0) lb = -1;
+  __syncthreads();
+  for (int b = threadIdx.x; b < B; b += NT)
+    if (cstart[b] <= w && w < cstart[b + 1]) lb = b;
+  __syncthreads();
+  const int b = lb;
+  if (b < 0) return;  // (cannot happen: w < cstart[B])
+  const int64_t lo = bb[b] + (int64_t)(w - cstart[b]) * C1_CH;
+  const int64_t bend = bb[b + 1];
+  const int len = (int)(bend - lo < C1_CH ? bend - lo : C1_CH);
+  const int64_t kmin = ci[CI_KMINC];
+  const int shift = 64 - log2P;
+  uint64_t r[U];
+  uint32_t f[U], rank[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const int j = threadIdx.x + u * NT;
+    r[u] = __builtin_nontemporal_load(srcA + lo + (j < len ? j : len - 1));
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const int j = threadIdx.x + u * NT;
+    const bool v = j < len && (uint32_t)r[u] != C1_SENT;
+    f[u] = (uint32_t)(key_hash(kmin + (int64_t)(r[u] >> 32)) >> shift) & (uint32_t)(F - 1);
+    rank[u] = v ? atomicAdd(&cnt[f[u]], 1u) : 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  // exclusive scan of the F counts (F <= NT)
+  {
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t c = t < F ? cnt[t] : 0u;
+    uint32_t incl = c;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = (int)incl;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < NT / 64; k++) {
+      before += k < wave ? (uint32_t)wsum[k] : 0u;
+      tot += (uint32_t)wsum[k];
+    }
+    if (t < F) {
+      sbase[t] = before + incl - c;
+      seg[(int64_t)w * (F + 1) + t] = (uint16_t)(before + incl - c);
+    }
+    if (t == 0) seg[(int64_t)w * (F + 1) + F] = (uint16_t)tot;
+    if (t == 0) wsum[0] = (int)tot;  // read after the next barrier
+  }
+  __syncthreads();
+  const int nv = wsum[0];
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    if (rank[u] != 0xFFFFFFFFu) stage[sbase[f[u]] + rank[u]] = r[u];
+  __syncthreads();
+  for (int j = threadIdx.x; j < nv; j += NT) srec[lo + j] = stage[j];
+}
+
+// ------------------------------------------------------------------ k_c1_merge
+struct C1Q {
+  int32_t log2P, fbits, log2H, sw, hv_active, hv_op, hmax;
+  int64_t size, adv, cmax, hv_i64;
+  FastDiv fd;
+  uint8_t* chg;  // changelog: per-row-slot emission flags (CHG_*), or null
+};
+
+__device__ __forceinline__ bool c1q_having(const C1Q& q, uint64_t c) {
+  const int64_t v = (int64_t)c;
+  switch (q.hv_op) {
+    case KHIP_OP_GT: return v > q.hv_i64;
+    case KHIP_OP_GE: return v >= q.hv_i64;
+    case KHIP_OP_LT: return v < q.hv_i64;
+    case KHIP_OP_LE: return v <= q.hv_i64;
+    case KHIP_OP_EQ: return v == q.hv_i64;
+    case KHIP_OP_NE: return v != q.hv_i64;
+  }
+  return true;
+}
+
+// identity → 32-bit hash (slot = its top log2H bits; sub-pass = bits of a remix)
+template <class ID>
+__device__ __forceinline__ uint32_t c1_hash(ID id) {
+  if constexpr (sizeof(ID) == 4) return (uint32_t)id * 0x9E3779B1u;
+  else return ((uint32_t)id * 0x9E3779B1u) ^ ((uint32_t)(id >> 32) * 0x85EBCA77u);
+}
+__device__ __forceinline__ uint32_t c1_sub(uint32_t h, int sbits) {
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  return (h >> 12) & ((1u << sbits) - 1u);
+}
+
+template <class ID>
+__device__ __forceinline__ int c1_find_id(const KLDS ID* ids, ID id, uint32_t e, int H) {
+  for (int probe = 0; probe < H; probe++) {
+    const ID v = ids[e];
+    if (v == id) return (int)e;
+    if (v == (ID)~(ID)0) return -1;
+    e = (e + 1) & (uint32_t)(H - 1);
+  }
+  return -1;
+}
+
+// Work item: p (work == nullptr: item w is partition w) or work[w] = p | sbits << 16 | sub << 20
+// (a retry with 2^sbits sub-passes).  LDS: ids ID[H + 64] | rt u32[H + 64] | ct u32[H + 64] |
+// list u16[H] | segment prefix u32[SEGMAX + 1] | segment bases i32[SEGMAX] (n < 2^31).
+template <int NT, int AU, class ID>
+__global__ __launch_bounds__(NT, 4) void k_c1_merge(
+    C1Q q, const uint32_t* __restrict__ work, int64_t nwork, const int64_t* __restrict__ bb,
+    const int* __restrict__ cstart, const uint16_t* __restrict__ seg, const uint64_t* __restrict__ srec, int first,
+    uint64_t* __restrict__ buf0, uint64_t* __restrict__ buf1, const uint8_t* __restrict__ sel,
+    const int64_t* __restrict__ cnt, unsigned long long* __restrict__ newcnt, uint8_t* __restrict__ fail,
+    unsigned long long* __restrict__ need, int64_t close0, uint64_t* __restrict__ closed,
+    unsigned long long* __restrict__ closed_n, const int64_t* __restrict__ ci, unsigned long long* __restrict__ hnew,
+    unsigned long long* __restrict__ hclosed, uint32_t* __restrict__ prn) {
+  if (ci[CI_GATE] == 0) return;
+  if ((ci[CI_ID32] != 0) != (sizeof(ID) == 4)) return;  // the other identity width's instantiation
+  constexpr int NW = NT / 64;
+  constexpr ID EMPTY = (ID)~(ID)0;
+  const int log2H = q.log2H;
+  const int H = 1 << log2H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  KLDS ID* ids = (KLDS ID*)(KLDS char*)smem;
+  KLDS uint32_t* rt = (KLDS uint32_t*)((KLDS char*)smem + (size_t)(H + 64) * sizeof(ID));
+  KLDS uint32_t* ct = rt + (H + 64);
+  KLDS uint16_t* list = (KLDS uint16_t*)(ct + (H + 64));
+  KLDS uint32_t* spre = (KLDS uint32_t*)((KLDS char*)list + (((size_t)H * 2 + 15) & ~(size_t)15));
+  KLDS int32_t* sbs = (KLDS int32_t*)((KLDS char*)spre + (size_t)(C1_SEGMAX + 4) * 4);
+  __shared__ int lovf, nnew;
+  __shared__ int wsum[NW];
+  __shared__ unsigned long long lbase;
+  const int F = 1 << q.fbits;
+  const int64_t wbase = ci[CI_WBASE], whi = ci[CI_WHI], T0 = ci[CI_T0], tmin = ci[CI_TMIN];
+  const int wbits = (int)ci[CI_WBITS];
+  const int64_t kmin = ci[CI_KMINC];
+  const uint64_t krange = (uint64_t)ci[CI_KRANGE];
+  const int32_t tmin32 = (int32_t)(tmin - T0);
+  const bool evict = close0 != INT64_MIN;
+  const uint32_t dummy = (uint32_t)H + (uint32_t)lane;
+  for (int i = threadIdx.x; i < H + 64; i += NT) {
+    ids[i] = EMPTY;
+    rt[i] = 0u;
+    ct[i] = 0u;
+  }
+  if (threadIdx.x == 0) {
+    lovf = 0;
+    nnew = 0;
+  }
+  // identity of a resident row (false: no record of this push can match it) and its sub-pass hash
+  auto row_id = [&](const uint64_t* row, ID* id, uint32_t* h) -> bool {
+    const uint64_t krel = (uint64_t)((int64_t)row[0] - kmin);
+    const int64_t wi = (int64_t)fast_udiv((uint64_t)row[1], q.fd) - wbase;
+    if (krel > krange || wi < 0 || wi > whi) {
+      *h = (uint32_t)(key_hash((int64_t)row[0]) >> 32) ^ (uint32_t)row[1];
+      return false;
+    }
+    if constexpr (sizeof(ID) == 4) *id = (ID)(((uint32_t)krel << wbits) | (uint32_t)wi);
+    else *id = (ID)((krel << 32) | (uint64_t)wi);
+    *h = c1_hash<ID>(*id);
+    return true;
+  };
+  for (int64_t w = blockIdx.x; w < nwork; w += gridDim.x) {
+    uint32_t p;
+    int sbits = 0, sub = 0;
+    if (work) {
+      const uint32_t x = work[w];
+      p = x & 0xFFFFu;
+      sbits = (x >> 16) & 0xF;
+      sub = (int)(x >> 20);
+    } else {
+      p = (uint32_t)w;
+    }
+    p = __builtin_amdgcn_readfirstlane(p);
+    const int b = (int)(p >> q.fbits), f = (int)(p & (uint32_t)(F - 1));
+    const int cs = cstart[b];
+    int nseg = cstart[b + 1] - cs;
+    if (nseg < 0 || nseg > C1_SEGMAX) nseg = 0;  // (k_c1_check guarantees 0 <= nseg <= SEGMAX)
+    const int64_t nrow = cnt[p];
+    const bool isel = ((((const uint32_t*)sel)[p >> 2] >> (8 * (p & 3))) & 0xFFu) != 0;
+    // 0. the item's segments: prefix of their lengths, and each one's base (record = sbs[s] + li)
+    {
+      int len0 = 0, len1 = 0;
+      int64_t base0 = 0, base1 = 0;
+      const int k0 = threadIdx.x * 2;
+      if (k0 < nseg) {
+        const uint16_t* sg = seg + (int64_t)(cs + k0) * (F + 1) + f;
+        const int o0 = sg[0];
+        len0 = (int)sg[1] - o0;
+        base0 = bb[b] + (int64_t)k0 * C1_CH + o0;
+      }
+      if (k0 + 1 < nseg) {
+        const uint16_t* sg = seg + (int64_t)(cs + k0 + 1) * (F + 1) + f;
+        const int o0 = sg[0];
+        len1 = (int)sg[1] - o0;
+        base1 = bb[b] + (int64_t)(k0 + 1) * C1_CH + o0;
+      }
+      const int s = len0 + len1;
+      int incl = s;
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+      }
+      if (lane == 63) wsum[wave] = incl;
+      __syncthreads();
+      int before = 0;
+      for (int k = 0; k < NW; k++) before += k < wave ? wsum[k] : 0;
+      const int ex = before + incl - s;
+      if (k0 < nseg) {
+        spre[k0] = (uint32_t)ex;
+        sbs[k0] = (int32_t)(base0 - ex);
+      }
+      if (k0 + 1 < nseg) {
+        spre[k0 + 1] = (uint32_t)(ex + len0);
+        sbs[k0 + 1] = (int32_t)(base1 - (ex + len0));
+      }
+      if (k0 < nseg && k0 + 2 >= nseg) spre[nseg] = (uint32_t)(ex + s);  // the total
+      if (nseg == 0 && threadIdx.x == 0) spre[0] = 0u;
+      __syncthreads();
+    }
+    const int64_t rn = spre[nseg];
+    if (first && threadIdx.x == 0) prn[p] = (uint32_t)rn;
+    if (rn == 0 && first) {  // untouched partition: nothing to rewrite
+      __syncthreads();
+      continue;
+    }
+    const uint64_t* src = (isel ? buf1 : buf0) + (uint64_t)p * q.cmax * q.sw;
+    // 0b. closed resident rows → closed store (pass 0 only; retries skip them)
+    if (evict && first) {
+      int ne = 0, nh = 0;
+      for (int64_t r = threadIdx.x; r < nrow; r += NT) {
+        const uint64_t* row = src + r * q.sw;
+        ID id;
+        uint32_t h;
+        row_id(row, &id, &h);
+        ne += ((int64_t)row[1] + q.size <= close0) && (sbits == 0 || (int)c1_sub(h, sbits) == sub);
+      }
+      int incl = ne;
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+      }
+      if (lane == 63) wsum[wave] = incl;
+      __syncthreads();
+      int before = 0, total = 0;
+      for (int k = 0; k < NW; k++) {
+        if (k < wave) before += wsum[k];
+        total += wsum[k];
+      }
+      if (threadIdx.x == 0) lbase = total ? atomicAdd(closed_n, (unsigned long long)total) : 0ULL;
+      __syncthreads();
+      uint64_t* dst = closed + (lbase + (uint64_t)(before + incl - ne)) * q.sw;
+      for (int64_t r = threadIdx.x; r < nrow; r += NT) {
+        const uint64_t* row = src + r * q.sw;
+        ID id;
+        uint32_t h;
+        row_id(row, &id, &h);
+        if (!((int64_t)row[1] + q.size <= close0) || !(sbits == 0 || (int)c1_sub(h, sbits) == sub)) continue;
+        for (int k = 0; k < q.sw; k++) dst[k] = row[k];
+        dst += q.sw;
+        nh += q.hv_active && c1q_having(q, row[3]) ? 1 : 0;
+      }
+      if (q.hv_active) {
+        nh = (int)wave_sum(nh);
+        if (lane == 0 && nh) atomicAdd(hclosed, (unsigned long long)nh);
+      }
+      __syncthreads();
+    }
+    // 1. records → delta entries, two register sets (chunk c + 1 in flight while c is applied)
+    uint64_t ra[AU], rb[AU];
+    auto load = [&](uint64_t (&x)[AU], int64_t l0) {
+#pragma unroll
+      for (int u = 0; u < AU; u++) {
+        int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
+        li = li < rn ? li : rn - 1;
+        int lo = 0, hi = nseg;  // the last segment starting at or before li
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if ((int64_t)spre[mid] <= li) lo = mid;
+          else hi = mid;
+        }
+        x[u] = __builtin_nontemporal_load(srec + (int64_t)sbs[lo] + li);
+      }
+    };
+    auto apply = [&](const uint64_t (&xr)[AU], int64_t l0) {
+      ID id[AU];
+      uint32_t e[AU], tr[AU];
+      bool pend[AU], claimed[AU];
+#pragma unroll
+      for (int u = 0; u < AU; u++) {
+        const int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
+        const uint64_t v = xr[u];
+        const int32_t t32 = (int32_t)(uint32_t)v;
+        const uint64_t krel = v >> 32;
+        const uint64_t wi = fast_udiv((uint64_t)(T0 + (int64_t)t32), q.fd) - (uint64_t)wbase;
+        ID x;
+        if constexpr (sizeof(ID) == 4) x = (ID)(((uint32_t)krel << wbits) | (uint32_t)wi);
+        else x = (ID)((krel << 32) | wi);
+        const uint32_t h = c1_hash<ID>(x);
+        bool act = li < rn;
+        if (sbits) act = act && (int)c1_sub(h, sbits) == sub;
+        id[u] = act ? x : EMPTY;
+        e[u] = act ? h >> (32 - log2H) : dummy;
+        tr[u] = (uint32_t)(t32 - tmin32) + 1u;
+      }
+#pragma unroll
+      for (int u = 0; u < AU; u++) {
+        ID old = EMPTY;
+        __hip_atomic_compare_exchange_strong(&ids[e[u]], &old, id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        claimed[u] = id[u] != EMPTY && old == EMPTY;
+        pend[u] = old != EMPTY && old != id[u];
+      }
+      for (int probes = 1;; probes++) {  // collisions: every pending record probes on together
+        bool anyp = false;
+#pragma unroll
+        for (int u = 0; u < AU; u++) anyp |= pend[u];
+        if (!__ballot(anyp)) break;
+        if (probes >= H) {
+          lovf = 1;
+#pragma unroll
+          for (int u = 0; u < AU; u++)
+            if (pend[u]) id[u] = EMPTY;
+          break;
+        }
+#pragma unroll
+        for (int u = 0; u < AU; u++) {
+          if (!pend[u]) continue;
+          e[u] = (e[u] + 1) & (uint32_t)(H - 1);
+          ID o2 = EMPTY;
+          __hip_atomic_compare_exchange_strong(&ids[e[u]], &o2, id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+          claimed[u] = o2 == EMPTY;
+          pend[u] = o2 != EMPTY && o2 != id[u];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < AU; u++) mg_list_append(claimed[u] && id[u] != EMPTY, e[u], list, &nnew);
+#pragma unroll
+      for (int u = 0; u < AU; u++) {
+        if (id[u] == EMPTY) continue;
+        __hip_atomic_fetch_max(&rt[e[u]], tr[u], WG_RLX);
+        __hip_atomic_fetch_add(&ct[e[u]], 1u, WG_RLX);
+      }
+    };
+    const int64_t nch = (rn + (int64_t)AU * NT - 1) / ((int64_t)AU * NT);
+    if (rn > 0) {
+      load(ra, 0);
+      for (int64_t c = 0; c < nch; c += 2) {
+        if (c + 1 < nch) load(rb, (c + 1) * AU * NT);
+        apply(ra, c * AU * NT);
+        if (c + 1 >= nch || *(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
+        if (c + 2 < nch) load(ra, (c + 2) * AU * NT);
+        apply(rb, (c + 1) * AU * NT);
+        if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
+      }
+    }
+    __syncthreads();
+    const int nl = nnew < H ? nnew : H;
+    if (lovf || nnew > q.hmax) {  // more groups than the table takes: retried with 2x sub-passes
+      if (threadIdx.x == 0) fail[p] |= 1;
+      for (int i = threadIdx.x; i < nl; i += NT) {
+        const uint32_t e = list[i];
+        ids[e] = EMPTY;
+        rt[e] = 0u;
+        ct[e] = 0u;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        lovf = 0;
+        nnew = 0;
+      }
+      __syncthreads();
+      continue;
+    }
+    // 2. resident rows: mark the delta entries they absorb; count live rows
+    int n_mine = 0;
+    for (int64_t r = threadIdx.x; r < nrow; r += NT) {
+      const uint64_t* row = src + r * q.sw;
+      if (evict && (int64_t)row[1] + q.size <= close0) continue;
+      ID id;
+      uint32_t h;
+      const bool has = row_id(row, &id, &h);
+      if (sbits && (int)c1_sub(h, sbits) != sub) continue;
+      if (has) {
+        const int e = c1_find_id<ID>(ids, id, h >> (32 - log2H), H);
+        if (e >= 0) rt[e] |= RT_MATCHED;  // one resident row per identity: a plain store
+      }
+      n_mine++;
+    }
+    __syncthreads();
+    // the wave's share of the list: new (unmatched) entries
+    const int per = ((nl + NW - 1) / NW + 63) & ~63;
+    const int lb0 = wave * per, lb1 = lb0 + per < nl ? lb0 + per : nl;
+    int nnw = 0;
+    for (int k = lb0; k < lb1; k += 64) {
+      const int i = k + lane;
+      const bool isnew = i < lb1 && !(rt[list[i]] & RT_MATCHED);
+      nnw += (int)__popcll(__ballot(isnew));
+    }
+    // 3. per-wave row counts → the partition's region range (one atomic per work item)
+    const int wave_rows = (int)wave_sum(n_mine) + nnw;
+    if (lane == 0) wsum[wave] = wave_rows;
+    __syncthreads();
+    int wave_before = 0, total = 0;
+    for (int k = 0; k < NW; k++) {
+      if (k < wave) wave_before += wsum[k];
+      total += wsum[k];
+    }
+    if (threadIdx.x == 0) {
+      if (work) lbase = total ? atomicAdd(&newcnt[p], (unsigned long long)total) : 0ULL;
+      else {
+        lbase = 0;
+        newcnt[p] = (unsigned long long)total;
+      }
+    }
+    __syncthreads();
+    if ((int64_t)(lbase + total) > q.cmax) {
+      if (threadIdx.x == 0) {
+        fail[p] |= 2;
+        atomicMax(need, (unsigned long long)(lbase + total));
+      }
+      for (int i = threadIdx.x; i < nl; i += NT) {
+        const uint32_t e = list[i];
+        ids[e] = EMPTY;
+        rt[e] = 0u;
+        ct[e] = 0u;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) nnew = 0;
+      __syncthreads();
+      continue;
+    }
+    // 4. write: resident rows (merged), then the wave's new entries (ballot ranks: consecutive rows)
+    uint64_t* dst0 = (isel ? buf0 : buf1) + (uint64_t)p * q.cmax * q.sw;
+    uint64_t cur = lbase + (uint64_t)wave_before;
+    const uint64_t lt = (1ULL << lane) - 1;
+    int nh = 0;
+    for (int64_t r0 = wave * 64; r0 < nrow; r0 += NT) {
+      const int64_t r = r0 + lane;
+      const uint64_t* row = src + (r < nrow ? r : 0) * q.sw;
+      bool live = r < nrow && !(evict && (int64_t)row[1] + q.size <= close0);
+      int e = -1;
+      if (live) {
+        ID id;
+        uint32_t h;
+        const bool has = row_id(row, &id, &h);
+        if (sbits) live = (int)c1_sub(h, sbits) == sub;
+        if (live && has) e = c1_find_id<ID>(ids, id, h >> (32 - log2H), H);
+      }
+      const uint64_t bl = __ballot(live);
+      if (live) {
+        const uint64_t ri = cur + __popcll(bl & lt);
+        uint64_t* dst = dst0 + ri * q.sw;
+        uint64_t w2 = row[2], c = row[3];
+        if (e >= 0) {
+          const int64_t t = tmin + (int64_t)(rt[e] & ~RT_MATCHED) - 1;
+          w2 = t > (int64_t)w2 ? (uint64_t)t : w2;
+          c += ct[e];
+        }
+        *(longlong2*)dst = make_longlong2((int64_t)row[0], (int64_t)row[1]);
+        *(longlong2*)(dst + 2) = make_longlong2((int64_t)w2, (int64_t)c);
+        const bool now = !q.hv_active || c1q_having(q, c);
+        nh += q.hv_active && now ? 1 : 0;
+        if (q.chg)
+          q.chg[(uint64_t)p * q.cmax + ri] =
+              e >= 0 ? (uint8_t)(CHG_TOUCHED | (!q.hv_active || c1q_having(q, row[3]) ? CHG_OLD : 0) | (now ? CHG_NEW : 0))
+                     : (uint8_t)0;
+      }
+      cur += __popcll(bl);
+    }
+    __syncthreads();  // every wave's resident rows have read their entries: the list walk clears them
+    const uint32_t wmask = wbits ? (1u << wbits) - 1u : 0u;
+    for (int k = lb0; k < lb1; k += 64) {
+      const int i = k + lane;
+      const uint32_t e = i < lb1 ? list[i] : dummy;
+      const uint32_t rv = rt[e];
+      const bool isnew = i < lb1 && !(rv & RT_MATCHED);
+      const uint64_t bl = __ballot(isnew);
+      if (isnew) {
+        const uint64_t ri = cur + __popcll(bl & lt);
+        uint64_t* dst = dst0 + ri * q.sw;
+        const ID id = ids[e];
+        int64_t krel, wi;
+        if constexpr (sizeof(ID) == 4) {
+          krel = (int64_t)((uint32_t)id >> wbits);
+          wi = (int64_t)((uint32_t)id & wmask);
+        } else {
+          krel = (int64_t)((uint64_t)id >> 32);
+          wi = (int64_t)((uint64_t)id & 0xFFFFFFFFull);
+        }
+        const uint32_t c = ct[e];
+        *(longlong2*)dst = make_longlong2(kmin + krel, (wbase + wi) * q.adv);
+        *(longlong2*)(dst + 2) = make_longlong2(tmin + (int64_t)rv - 1, (int64_t)c);
+        const bool now = !q.hv_active || c1q_having(q, c);
+        nh += q.hv_active && now ? 1 : 0;
+        if (q.chg) q.chg[(uint64_t)p * q.cmax + ri] = (uint8_t)(CHG_TOUCHED | (now ? CHG_NEW : 0));
+      }
+      if (i < lb1) {  // every listed entry leaves cleared for the next item
+        ids[e] = EMPTY;
+        rt[e] = 0u;
+        ct[e] = 0u;
+      }
+      cur += __popcll(bl);
+    }
+    if (q.hv_active) {
+      nh = (int)wave_sum(nh);
+      if (lane == 0 && nh) atomicAdd(&hnew[p], (unsigned long long)nh);
+    }
+    __syncthreads();  // the table is clear for the next item
+    if (threadIdx.x == 0) nnew = 0;
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ host side
+
+size_t c1_merge_lds(int log2H, int idw) {
+  const size_t H = (size_t)1 << log2H;
+  return (H + 64) * (idw + 8) + ((H * 2 + 15) & ~(size_t)15) + (C1_SEGMAX + 4) * 4 + C1_SEGMAX * 4;
+}
+
+// Whether the COUNT(*) pipeline may take this push (the general path's c1 plan, TUMBLING, the
+// two-level partition layout).  The push may still be declined on the device (k_c1_check).
+bool c1_eligible(khip_agg* a, int64_t n) {
+  PartState& s = a->part;
+  const bool cnt1 = a->ap.n_ops == 1 && a->ap.ops[0].kind == OP_INC && a->ap.ops[0].word == 3 && a->sw == 4 &&
+                    s.rw == 2;
+  return cnt1 && a->windowed && a->desc.window_kind == KHIP_WINDOW_TUMBLING && s.log2P >= 11 && s.log2P <= 16 &&
+         s.mH >= 256 && a->desc.advance_ms <= ((int64_t)1 << 31) && !(a->desc.flags & KHIP_FLAG_PART_CLAIM) &&
+         n > 0 && n < ((int64_t)1 << 31) && knob("KHIP_C1P", 1) != 0 && knob("KHIP_PAD", 0) == 0 &&
+         knob("KHIP_MERGE", 1) != 0 && knob("KHIP_SCATTER2", 1) != 0;
+}
+
+// Returns KHIP_OK with *declined = true when k_c1_check declined the push (nothing persistent was
+// touched: the caller runs the general path on the same batch).
+khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
+                    const uint8_t* rv, int64_t* tot, bool* declined, const int64_t* st_at) {
+  PartState& s = a->part;
+  *declined = false;
+  const int P = (int)s.P;
+  const int fbits = s.log2P - s.log2P / 2;
+  const int log2B = s.log2P - fbits;
+  const int B = 1 << log2B, F = 1 << fbits;
+  const int64_t nT = ceil_div(n, C1_TILE);
+  const int TC = (int)std::min<int64_t>(nT, 64);
+  const int64_t nchunk_max = ceil_div(n, C1_CH) + B;
+  KHIP_TRY(s.c1hist.ensure((size_t)nT * B * 4));
+  KHIP_TRY(s.c1bb.ensure((size_t)(B + 1) * 8));
+  const size_t seg_bytes = ((size_t)nchunk_max * (F + 1) * 2 + 255) & ~(size_t)255;  // cstart 256-B aligned
+  KHIP_TRY(s.c1seg.ensure(seg_bytes + (size_t)(B + 1) * 4));
+  const int64_t nS = ceil_div(n, 8 * C1_NT);  // k_c1_scatter steps (8 records per thread)
+  KHIP_TRY(s.tilemax.ensure(nS * 16));      // per step: accepted ts max, min
+  KHIP_TRY(s.tpart.ensure(nT * 8 * T_NPART));
+  KHIP_TRY(s.scan_tmpB.ensure((size_t)TC * B * 8));
+  KHIP_TRY(s.prn.ensure((size_t)P * 4));
+  KHIP_TRY(s.res.ensure(16));
+  KHIP_TRY(s.closed_ctr.ensure(8));
+  if (s.scat_cap < n) {
+    KHIP_TRY(s.srec.ensure((size_t)(n + 1) * s.rw * 8));
+    s.scat_cap = n;
+  }
+  KHIP_TRY(s.srecA.ensure((size_t)(n + 1) * s.rw * 8));
+  if (!s.c1info.p) {
+    KHIP_TRY(s.c1info.ensure(CI_N * 8));
+    int64_t init[CI_N] = {};
+    init[CI_KMIN] = INT64_MAX;
+    init[CI_KMAX] = INT64_MIN;
+    KHIP_TRY_HIP(hipMemcpy(s.c1info.p, init, sizeof(init), hipMemcpyHostToDevice));
+  }
+  int64_t* ci = s.c1info.as<int64_t>();
+  int* cstart = (int*)(s.c1seg.as<char>() + seg_bytes);
+  uint16_t* seg = s.c1seg.as<uint16_t>();
+  const int64_t adv = a->desc.advance_ms;
+  const FastDiv fd = make_fastdiv(adv);
+  const int64_t close0 = a->host_stream_time >= 0 ? a->host_stream_time - a->grace : INT64_MIN;
+  if (s.closed_cap < s.closed_n + (a->occ - s.closed_n)) {  // worst case every live row closes in this push
+    const int64_t live = a->occ - s.closed_n;
+    const int64_t ncap = next_pow2(std::max<int64_t>(1024, s.closed_n + live));
+    DevBuf nc;
+    KHIP_TRY(nc.ensure((size_t)ncap * a->sw * 8));
+    if (s.closed_n)
+      KHIP_TRY_HIP(hipMemcpyAsync(nc.p, s.closed.p, (size_t)s.closed_n * a->sw * 8, hipMemcpyDeviceToDevice, a->stream));
+    KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+    s.closed.release();
+    s.closed = nc;
+    nc.p = nullptr;
+    s.closed_cap = ncap;
+  }
+  // 1. bucket histogram (keys only) → 2. (tile, bucket) offsets
+  ev_record_part(a, 0);
+  const bool vec = ((uintptr_t)keys & 15) == 0;
+  hipLaunchKernelGGL(vec ? k_c1_hist<true> : k_c1_hist<false>, dim3(nT), dim3(C1_NT), 0, a->stream, keys, ts, n, nT,
+                     log2B, s.c1hist.as<uint32_t>(), ci, a->stream_time.as<int64_t>());
+  hipLaunchKernelGGL(k_part_colsum, dim3(ceil_div(B, 256), TC), dim3(256), 0, a->stream, s.c1hist.as<uint32_t>(), nT, B,
+                     TC, s.scan_tmpB.as<int64_t>());
+  hipLaunchKernelGGL(k_part_colbase, dim3(ceil_div(B, 256)), dim3(256), 0, a->stream, s.scan_tmpB.as<int64_t>(), B, TC,
+                     s.c1bb.as<int64_t>());
+  hipLaunchKernelGGL(k_part_pscan, dim3(1), dim3(1024), 0, a->stream, s.c1bb.as<int64_t>(), (int64_t)B);
+  hipLaunchKernelGGL(k_part_colprefix, dim3(ceil_div(B, 256), TC), dim3(256), 0, a->stream, s.c1hist.as<uint32_t>(), nT,
+                     B, TC, s.scan_tmpB.as<int64_t>(), s.c1bb.as<int64_t>(), 1);
+  ev_record_part(a, 1);
+  // 3. records → buckets
+  {
+    constexpr int U = 8;
+    const size_t lds = stage_r8_lds_bytes(B, U * C1_NT);
+    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)k_c1_scatter<U, C1_NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((k_c1_scatter<U, C1_NT>), dim3(nT), dim3(C1_NT), lds, a->stream, keys, ts, kv, rv, n, nT, log2B,
+                       s.c1hist.as<uint32_t>(), s.srecA.as<uint64_t>(), s.tilemax.as<int64_t>(), s.tpart.as<int64_t>(),
+                       ci, st_at);
+    KHIP_TRY_HIP(hipGetLastError());
+  }
+  // 4. accept or decline
+  hipLaunchKernelGGL(k_c1_check, dim3(1), dim3(1024), 0, a->stream, s.tilemax.as<int64_t>(), nS,
+                     a->desc.size_ms, adv, fd, a->grace, close0, s.res_fresh ? 1 : 0, log2B,
+                     s.c1bb.as<int64_t>(), cstart, ci, a->stream_time.as<int64_t>(), s.res.as<int64_t>(),
+                     s.ctr.as<unsigned long long>(), s.closed_ctr.as<unsigned long long>(),
+                     (unsigned long long)s.closed_n);
+  // 5. refine: chunks → partition-sorted, segment table
+  {
+    constexpr int U = C1_CH / C1_NT;
+    const size_t lds = (size_t)F * 8 + (size_t)C1_CH * 8;
+    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)k_c1_refine<U, C1_NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((k_c1_refine<U, C1_NT>), dim3((unsigned)nchunk_max), dim3(C1_NT), lds, a->stream,
+                       s.srecA.as<uint64_t>(), s.c1bb.as<int64_t>(), cstart, log2B, s.log2P, fbits,
+                       s.srec.as<uint64_t>(), seg, ci);
+    KHIP_TRY_HIP(hipGetLastError());
+  }
+  ev_record_part(a, 2);
+  // 6. merge partitions (+ retries), as part_push's pass loop
+  const int log2H = (int)knob("KHIP_C1_LOG2H", 12);
+  C1Q cq{};
+  cq.log2P = s.log2P;
+  cq.fbits = fbits;
+  cq.log2H = log2H;
+  cq.sw = a->sw;
+  cq.hv_active = a->having.active;
+  cq.hv_op = a->having.op;
+  cq.hv_i64 = a->having.i64;
+  cq.hmax = (int)((int64_t)(1 << log2H) * 3 / 4);
+  cq.size = a->desc.size_ms;
+  cq.adv = adv;
+  cq.fd = fd;
+  int64_t added_total = 0;
+  std::vector<int> sbits(s.psbits.begin(), s.psbits.end());
+  std::vector<uint32_t> plist, work;
+  bool subs0 = false;
+  for (int p = 0; p < P && !subs0; p++) subs0 = sbits[p] > 0;
+  if (subs0) {
+    for (int p = 0; p < P; p++)
+      for (int k = 0; k < (1 << sbits[p]); k++) work.push_back((uint32_t)p | ((uint32_t)sbits[p] << 16) | ((uint32_t)k << 20));
+    KHIP_TRY(s.work.ensure(work.size() * 4));
+    KHIP_TRY_HIP(hipMemcpyAsync(s.work.p, work.data(), work.size() * 4, hipMemcpyHostToDevice, a->stream));
+  }
+  const int au = (int)knob("KHIP_C1_AU", 6);
+  std::vector<uint8_t> host_fail;
+  for (int pass = 0;; pass++) {
+    cq.cmax = s.cmax;
+    cq.chg = a->changelog ? a->chg.as<uint8_t>() : nullptr;
+    if (pass > 0) KHIP_TRY_HIP(hipMemsetAsync(s.ctr.p, 0, 24, a->stream));
+    const uint32_t* wk = (pass == 0 && !subs0) ? nullptr : s.work.as<uint32_t>();
+    const int64_t nwork = (pass == 0 && !subs0) ? P : (int64_t)work.size();
+    const int64_t grid = std::min<int64_t>(nwork, (int64_t)s.n_cu * knob("KHIP_MERGE_WG_PER_CU", 2));
+    // both identity widths are launched: the one k_c1_check did not choose exits at once
+    for (int idw = 0; idw < 2; idw++) {
+      auto mk = idw == 0 ? (au >= 8 ? k_c1_merge<512, 8, uint32_t> : (au >= 6 ? k_c1_merge<512, 6, uint32_t> : k_c1_merge<512, 4, uint32_t>))
+                         : k_c1_merge<512, 4, uint64_t>;
+      const size_t lds = c1_merge_lds(log2H, idw == 0 ? 4 : 8);
+      hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(mk, dim3(grid), dim3(512), lds, a->stream, cq, wk, nwork, s.c1bb.as<int64_t>(), cstart, seg,
+                         s.srec.as<uint64_t>(), pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
+                         s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
+                         s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
+                         s.closed_ctr.as<unsigned long long>(), ci,
+                         s.hnew.as<unsigned long long>(), s.ctr.as<unsigned long long>() + 12, s.prn.as<uint32_t>());
+    }
+    KHIP_TRY_HIP(hipGetLastError());
+    const int nl = pass == 0 ? P : (int)plist.size();
+    hipLaunchKernelGGL(k_part_commit, dim3(ceil_div(std::max(nl, 1), 256)), dim3(256), 0, a->stream,
+                       pass == 0 ? (const int64_t*)ci : (const int64_t*)nullptr, P, s.pbase.as<int64_t>(),
+                       s.prn.as<uint32_t>(), pass == 0 ? nullptr : s.work.as<uint32_t>() + work.size(), nl,
+                       s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
+                       s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>(), s.hcnt.as<unsigned long long>(),
+                       s.hnew.as<unsigned long long>());
+    KHIP_TRY_HIP(hipGetLastError());
+    if (pass == 0) {
+      ev_record_part(a, 3);
+      hipLaunchKernelGGL(k_part_stats, dim3(1), dim3(256), 0, a->stream, s.tpart.as<int64_t>(), nT,
+                         s.closed_ctr.as<unsigned long long>(), a->stream_time.as<int64_t>(),
+                         s.ctr.as<unsigned long long>());
+      KHIP_TRY_HIP(hipMemcpyAsync(s.pinfo.as<int64_t>() + 32, ci, CI_N * 8, hipMemcpyDeviceToHost, a->stream));
+    }
+    unsigned long long* c2 = s.pinfo.as<unsigned long long>() + 8;
+    KHIP_TRY_HIP(hipMemcpyAsync(c2, s.ctr.p, 13 * 8, hipMemcpyDeviceToHost, a->stream));
+    KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+    if (pass == 0 && s.pinfo.as<int64_t>()[32 + CI_GATE] == 0) {  // declined: nothing was written
+      *declined = true;
+      return KHIP_OK;
+    }
+    added_total += (int64_t)c2[0];
+    if (c2[1] == 0) break;
+    if (pass > 24) return fail(KHIP_E_DEVICE, "partitioned aggregation could not place the batch");
+    host_fail.resize(P);
+    KHIP_TRY_HIP(hipMemcpy(host_fail.data(), s.fail.p, P, hipMemcpyDeviceToHost));
+    KHIP_TRY_HIP(hipMemsetAsync(s.fail.p, 0, P, a->stream));
+    bool grow = false;
+    plist.clear();
+    work.clear();
+    for (int p = 0; p < P; p++) {
+      if (!host_fail[p]) continue;
+      if (host_fail[p] & 1) sbits[p] = sbits[p] + 1;
+      if (host_fail[p] & 2) grow = true;
+      plist.push_back((uint32_t)p);
+      if (sbits[p] > 12) return fail(KHIP_E_DEVICE, "partition needs more than 4096 sub-passes (extreme key skew)");
+      for (int k = 0; k < (1 << sbits[p]); k++) work.push_back((uint32_t)p | ((uint32_t)sbits[p] << 16) | ((uint32_t)k << 20));
+    }
+    if (grow) KHIP_TRY(part_regrow(a, next_pow2(std::max<int64_t>(s.cmax * 2, (int64_t)c2[2] * 5 / 4 + 64))));
+    std::vector<uint32_t> both(work);
+    both.insert(both.end(), plist.begin(), plist.end());
+    KHIP_TRY(s.work.ensure(both.size() * 4));
+    KHIP_TRY_HIP(hipMemcpyAsync(s.work.p, both.data(), both.size() * 4, hipMemcpyHostToDevice, a->stream));
+  }
+  for (int p = 0; p < P; p++) s.psbits[p] = (uint8_t)std::max<int>(s.psbits[p], sbits[p]);
+  s.res_fresh = false;
+  s.last_c1 = true;
+  {
+    const unsigned long long* hc = s.pinfo.as<unsigned long long>() + 8;
+    s.having_total = (int64_t)(hc[11] + hc[12]);
+  }
+  const unsigned long long* st = s.pinfo.as<unsigned long long>() + 8;
+  const int64_t cn = (int64_t)st[3 + T_NPART];
+  added_total += cn - s.closed_n;  // evicted rows left the live regions but are still groups
+  s.closed_n = cn;
+  a->host_stream_time = (int64_t)st[4 + T_NPART];
+  int64_t c[T_NPART];
+  for (int k = 0; k < T_NPART; k++) c[k] = (int64_t)st[3 + k];
+  tot[P_ACCEPTED] += c[T_ACCEPTED];
+  tot[P_NULL_KEY] += c[T_NULL_KEY];
+  tot[P_NULL_ROW] += c[T_NULL_ROW];
+  tot[P_BAD_TS] += c[T_BAD_TS];
+  tot[P_APPLIED] += c[T_APPLIED];
+  tot[P_LATE] += c[T_LATE];
+  tot[P_NEW] += added_total;
+  return KHIP_OK;
+}
+
+}  // namespace khip

@@ -282,7 +282,8 @@ __device__ __forceinline__ bool having_ok(const uint64_t* s, const HavingDev& h)
 
 // kernels shared by the engines (defined in khip_agg.hip)
 __global__ void k_blockmax(const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
-                           const uint8_t* __restrict__ rv, int64_t n, int64_t* __restrict__ blockmax);
+                           const uint8_t* __restrict__ rv, int64_t n, int64_t* __restrict__ blockmax,
+                           const int64_t* __restrict__ st_at);
 __global__ void k_scan_blocks(const int64_t* __restrict__ blockmax, int64_t nb, int64_t* __restrict__ prefix,
                               int64_t* __restrict__ stream_time);
 __global__ void k_scan_excl(int64_t* __restrict__ v, int64_t n, int64_t* __restrict__ total);
@@ -347,6 +348,12 @@ struct PartState {
   int64_t having_total = 0;
   bool hvalid = true;
   HostBuf pinfo;  // pinned: push info (window range, event-time span) and end-of-push stats
+  // COUNT(*) pipeline (khip_agg_c1.hip): per-tile bucket counts / offsets, bucket bases, the
+  // refine's per-chunk partition offsets, records of each partition in the last push (prn), and
+  // whether the last push took that pipeline (k_part_chg then reads prn instead of pbase)
+  DevBuf c1hist, c1bb, c1seg, c1info, prn;
+  bool last_c1 = false;
+  int c1_skip = 0;  // pushes left before the pipeline is tried again after a declined push
 };
 
 // SESSION engine state (khip_agg_session.hip): the session store sorted by (key, start) and
@@ -422,6 +429,9 @@ struct khip_agg {
   std::vector<uint64_t> chg_rows;
   std::vector<uint8_t> chg_tomb;
   int64_t chg_n = 0;
+  // ---- stream-time domains (ABI 5, khip_stream_time.hip): per-partition stream times (pst,
+  // pst2 = the next batch's), the push's per-row stream time, scan scratch, staged partition ids
+  DevBuf pst, pst2, st_col, st_agg, st_seen, st_part;
 };
 
 // Emission flags of a row written by the last push (khip_agg::chg): touched by one of its
@@ -442,8 +452,9 @@ namespace khip {
 khip_status part_init(khip_agg* a, int64_t hint);
 void part_release(khip_agg* a);
 khip_status part_reset(khip_agg* a);
+// st_at: per-row stream time (ABI 5 domains other than TASK), or null (computed per handle)
 khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
-                      const uint8_t* rv, const ColPtrs& cols, int64_t* tot);
+                      const uint8_t* rv, const ColPtrs& cols, int64_t* tot, const int64_t* st_at);
 khip_status part_compact(khip_agg* a, const HavingDev& h, std::vector<uint64_t>* rows, int64_t* count);
 bool part_having_count(khip_agg* a, int64_t* n);
 khip_status part_changes(khip_agg* a, std::vector<uint64_t>* rows, std::vector<uint8_t>* tomb, int64_t* count);
@@ -467,6 +478,11 @@ __global__ void k_finalize(uint64_t* __restrict__ table, int64_t cap, int sw, co
 int64_t visible_from(const khip_agg* a);
 khip_status emit_final_lost(khip_agg* a, const int64_t* ts, const uint8_t* kv, const uint8_t* rv, int64_t n,
                             int64_t tile, const int64_t* tile_prefix);
+// khip_stream_time.hip: the per-row stream time column (one seeded segment, or the partition runs
+// of `part` seeded with / updating a->pst), and the PARTITION domain's handle stream time
+khip_status stream_time_column(khip_agg* a, const int64_t* ts, const uint8_t* kv, const uint8_t* rv,
+                               const int32_t* part, int64_t n, int64_t seed, int64_t* st, int64_t* last);
+khip_status stream_time_partition_min(khip_agg* a);
 }  // namespace khip
 
 

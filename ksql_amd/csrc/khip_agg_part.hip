@@ -27,6 +27,7 @@
 #include <cstdlib>
 
 #include "khip_agg_internal.hpp"
+#include "khip_part.hpp"
 
 namespace khip {
 
@@ -42,7 +43,6 @@ constexpr int SPLIT_P_LOG2 = 14;  // growth by splitting stops here (more partit
                                   // scatter more than they save the LDS aggregate)
 constexpr int TC_MAX = 64;      // tile chunks for the column prefix
 
-enum { T_ACCEPTED, T_NULL_KEY, T_NULL_ROW, T_BAD_TS, T_APPLIED, T_LATE, T_NPART };
 
 struct ColTypes {
   int32_t t[MAX_COLS];
@@ -81,33 +81,14 @@ struct PartAggParams {
   HavingDev having;
 };
 
-// Key hash: its top log2P bits pick the partition; inside a partition the LDS slot and the
-// sub-pass of a (key, windowStart) group mix its low bits with ws (cheap 32-bit math).
-__device__ __forceinline__ uint64_t key_hash(int64_t key) { return mix64((uint64_t)key ^ 0x6A09E667F3BCC908ULL); }
-
-// inverse of key_hash (mix64 is a bijection): key = unmix64(hk) ^ C
-__device__ __forceinline__ int64_t key_of_hash(uint64_t h) {
-  h ^= h >> 33;
-  h *= 0x9cb4b2f8129337dbULL;  // inverse of 0xc4ceb9fe1a85ec53 mod 2^64
-  h ^= h >> 33;
-  h *= 0x4f74430c22a54005ULL;  // inverse of 0xff51afd7ed558ccd mod 2^64
-  h ^= h >> 33;
-  return (int64_t)(h ^ 0x6A09E667F3BCC908ULL);
-}
 
 // Packed group identity (identity-CAS mode): inside partition p the top log2P bits of the
 // key hash are p, so (hk << log2P) keeps the key exactly; the low log2P bits hold the
 // window index relative to wbase (< 2^log2P - 1, so an identity is never EMPTY_ID).
-constexpr uint64_t EMPTY_ID = ~0ULL;
 __device__ __forceinline__ uint64_t ident_of(uint64_t hk, int64_t widx_rel, int log2P) {
   return (hk << log2P) | (uint64_t)widx_rel;
 }
 
-__device__ __forceinline__ uint32_t part_of_hk(uint64_t hk, int log2P) {
-  return log2P == 0 ? 0u : (uint32_t)(hk >> (64 - log2P));
-}
-
-__device__ __forceinline__ uint32_t part_of(int64_t key, int log2P) { return part_of_hk(key_hash(key), log2P); }
 
 __device__ __forceinline__ uint32_t slot_of(uint64_t hk, int64_t ws, int H) {
   return ((uint32_t)hk + (uint32_t)ws * 0x9E3779B1u) & (uint32_t)(H - 1);
@@ -124,12 +105,6 @@ __device__ __forceinline__ bool sub_ok(uint64_t hk, int64_t ws, int sbits, int s
   return sbits == 0 || (int)((((uint32_t)(hk >> 16) + (uint32_t)ws * 0x85EBCA77u) >> 20) & ((1u << sbits) - 1)) == sub;
 }
 
-__device__ __forceinline__ int64_t tile_of(int64_t b, int64_t nT) {
-  // blocks b, b+8, b+16 ... share an XCD (round-robin dispatch): give each XCD a contiguous
-  // run of tiles so consecutive tiles' writes to one partition combine in that XCD's L2
-  const int64_t per = nT / 8, rem = nT % 8, x = b % 8, k = b / 8;
-  return x * per + (x < rem ? x : rem) + k;
-}
 
 __global__ __launch_bounds__(PT_THREADS) void k_part_hist(const int64_t* __restrict__ keys,
                                                           const int64_t* __restrict__ ts,
@@ -139,7 +114,8 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_hist(const int64_t* __restr
                                                           int64_t* __restrict__ tilemax, int64_t* __restrict__ tilemin,
                                                           int64_t* __restrict__ tpart, int fbits,
                                                           uint32_t* __restrict__ hcoarse,
-                                                          int64_t* __restrict__ tilekr) {
+                                                          int64_t* __restrict__ tilekr,
+                                                          const int64_t* __restrict__ st_at) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint32_t* lh = (uint32_t*)smem;
   __shared__ int64_t lmax[PT_THREADS / 64];
@@ -173,7 +149,8 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_hist(const int64_t* __restr
       if (!bit_get(rv, i)) { c_nr++; continue; }
       if (x[u] < 0) { c_bt++; continue; }
       c_acc++;
-      m = x[u] > m ? x[u] : m;
+      const int64_t sx = st_at ? st_at[i] : x[u];  // ABI 5 domains: the row's given stream time
+      m = sx > m ? sx : m;
       mn = x[u] < mn ? x[u] : mn;
       kmx = k[u] > kmx ? k[u] : kmx;
       kmxn = ~k[u] > kmxn ? ~k[u] : kmxn;
@@ -332,11 +309,6 @@ __device__ __forceinline__ void r12_store(uint64_t* __restrict__ srec, uint64_t 
   *(R12*)((char*)srec + i * 12) = R12{(uint32_t)hk, (uint32_t)(hk >> 32), trel};
 }
 
-// barrier without the vmcnt(0) that __syncthreads() implies: LDS writes are waited for, the
-// wave's outstanding global loads (prefetches) and stores stay in flight
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
 
 // LDS-staged scatter step (k_part_scatter's narrow fast path, k_part_refine of narrow records).
 // U records per thread (hk, pay, ok) go to bin (hk >> shift) & mask, whose next output position
@@ -356,9 +328,6 @@ struct StageLds {
   int* wsum;        // [16]
 };
 
-__device__ __forceinline__ uint32_t stage_bin(uint64_t hk, int shift, uint32_t mask) {
-  return shift >= 64 ? 0u : (uint32_t)(hk >> shift) & mask;
-}
 
 template <int U>
 __device__ __forceinline__ void stage_step(const int64_t (&hk)[U], const int64_t (&pay)[U], const bool (&ok)[U],
@@ -570,7 +539,7 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
     const int64_t* __restrict__ tileprefix, const int64_t* __restrict__ tilemax,
     const int64_t* __restrict__ tilemin, int windowed, int64_t size, int64_t adv, FastDiv fd, int64_t grace,
     RecLayout L, uint64_t* __restrict__ srec, int64_t dummy, int64_t* __restrict__ tpart,
-    const int64_t* __restrict__ wr, int r12_ok, int stage, int skip_r8) {
+    const int64_t* __restrict__ wr, int r12_ok, int stage, int skip_r8, const int64_t* __restrict__ st_at) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint32_t* cur = (uint32_t*)smem;
   __shared__ int wsum[PT_THREADS / 64];
@@ -828,9 +797,10 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_scatter(
       const bool valid = in && bit_get(kv, i) && bit_get(rv, i) && x >= 0;
       int64_t tot;
       const int64_t incl = block_incl_max(valid ? x : -1, lmax, &tot);
-      const int64_t st = incl > carry ? incl : carry;
+      int64_t st = incl > carry ? incl : carry;
       carry = tot > carry ? tot : carry;
       if (!valid) continue;
+      if (st_at) st = st_at[i];  // ABI 5 domains: given per row
       int64_t jlo = 0, nwin = 1;
       if (windowed) {
         const int64_t ws0 = first_window_start_fd(x, size, adv, fd);
@@ -1167,78 +1137,6 @@ __global__ __launch_bounds__(PT_THREADS) void k_part_refine(const uint64_t* __re
 // scratch, one 1024-thread workgroup per CU), and two NT = 512 workgroups share a CU, so one's
 // four stage barriers per step overlap the other's loads and stores.  Each staged record keeps
 // its bin beside it in LDS (u16), so the write-out does not hash the key again.
-struct StageR8 {
-  uint32_t* cur;    // [nb] next output record of each bin
-  uint32_t* cnt;    // [nb] records of the step per bin
-  uint32_t* sbase;  // [nb] the bin's first staged slot
-  uint32_t* gpos;   // [nb] output position of the bin's first record of the step
-  int64_t* sp;      // [S] staged records
-  uint16_t* sbin;   // [S] their bins
-  int* wsum;        // [NT / 64]
-};
-
-__host__ __device__ constexpr size_t stage_r8_lds_bytes(int nb, int S) {
-  return (size_t)nb * 16 + (size_t)S * 8 + ((size_t)S * 2 + 15) / 16 * 16;
-}
-
-__device__ __forceinline__ StageR8 stage_r8_carve(char* smem, int nb, int S, int* wsum) {
-  StageR8 L;
-  L.cur = (uint32_t*)smem;
-  L.cnt = L.cur + nb;
-  L.sbase = L.cnt + nb;
-  L.gpos = L.sbase + nb;
-  L.sp = (int64_t*)(smem + (size_t)nb * 16);
-  L.sbin = (uint16_t*)(L.sp + S);
-  L.wsum = wsum;
-  return L;
-}
-
-// One step: U records per thread (ok = present) → rank per bin, bin-ordered in LDS, written out
-// per bin as one contiguous run by consecutive threads.  nb <= NT.
-template <int U, int NT>
-__device__ __forceinline__ void stage_step_r8(const int64_t (&rec)[U], const uint32_t (&bin)[U], const bool (&ok)[U],
-                                              int nb, const StageR8& L, uint64_t* __restrict__ srec) {
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  uint32_t rank[U];
-#pragma unroll
-  for (int u = 0; u < U; u++) rank[u] = ok[u] ? atomicAdd(&L.cnt[bin[u]], 1u) : 0u;
-  lds_barrier();
-  const uint32_t c = t < nb ? L.cnt[t] : 0u;
-  uint32_t incl = c;
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += y;
-  }
-  if (lane == 63) L.wsum[wave] = (int)incl;
-  lds_barrier();
-  uint32_t before = 0, tot = 0;
-#pragma unroll
-  for (int k = 0; k < NT / 64; k++) {
-    before += k < wave ? (uint32_t)L.wsum[k] : 0u;
-    tot += (uint32_t)L.wsum[k];
-  }
-  if (t < nb) {
-    L.sbase[t] = before + incl - c;
-    L.gpos[t] = L.cur[t];
-    L.cur[t] += c;
-    L.cnt[t] = 0u;
-  }
-  lds_barrier();
-#pragma unroll
-  for (int u = 0; u < U; u++)
-    if (ok[u]) {
-      const uint32_t i = L.sbase[bin[u]] + rank[u];
-      L.sp[i] = rec[u];
-      L.sbin[i] = (uint16_t)bin[u];
-    }
-  lds_barrier();
-  for (uint32_t j = t; j < tot; j += NT) {
-    const uint32_t b = L.sbin[j];
-    srec[(uint64_t)L.gpos[b] + (j - L.sbase[b])] = (uint64_t)L.sp[j];
-  }
-  // the next step's first barrier (after its rank atomics) orders these LDS reads before any
-  // rewrite of sbase / gpos / the stage
-}
 
 // Pass A for a push whose records are R8 (wr[4] && wr[7], decided on the device by
 // k_part_wrange): the tiles with no late record (k_part_scatter's `fast` test); k_part_scatter
@@ -1474,11 +1372,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 // p | sub_bits << 16 | sub << 20  (retry with 2^sub_bits sub-passes, sub_bits <= 12).
 // LDS: lref u32[H] | words i64[nwords][H]  (word 0 key, 1 ws, 2 rowtime, 3.. state)
 
-#define KLDS __attribute__((address_space(3)))
-typedef KLDS uint32_t lds_u32;
-typedef KLDS int64_t lds_i64;
-typedef KLDS double lds_f64;
-#define WG_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP
 
 __device__ __forceinline__ void lds_apply(const PartAggParams& q, lds_i64* lw, int H, int e, int64_t t,
                                           uint32_t vmask, const uint64_t* __restrict__ srec, int64_t gi, int64_t w3) {
@@ -1881,7 +1774,6 @@ __global__ __launch_bounds__(AG_THREADS) void k_part_agg(PartAggParams q, const 
 // k_part_merge workgroup size: 512 threads, two persistent workgroups per CU (one's global
 // round trips hidden by the other's LDS work; measured on C2: 256 x 4 needs 2^15 partitions
 // to fit its tables and loses more in the hist/refine than it gains)
-constexpr uint32_t RT_MATCHED = 0x80000000u;
 #ifndef KHIP_MG_AU_CNT1
 #define KHIP_MG_AU_CNT1 4  // k_part_merge COUNT(*) records per thread per chunk
 #endif
@@ -1923,17 +1815,6 @@ struct MergeParams {
   int32_t pane;      // HOPPING with size % advance == 0 and fan <= MG_FB: pane aggregation allowed
 };
 
-// Append the claimed entries of the wave's lanes to the item's list (one LDS atomic per wave);
-// called by every lane of the wave (convergent).
-__device__ __forceinline__ void mg_list_append(bool claimed, uint32_t e, KLDS uint16_t* nl, int* nnew) {
-  const uint64_t b = __ballot(claimed);
-  if (!b) return;
-  const int lane = threadIdx.x & 63, leader = __ffsll((long long)b) - 1;
-  int base = 0;
-  if (lane == leader) base = atomicAdd(nnew, __popcll(b));
-  base = __shfl(base, leader, 64);
-  if (claimed) nl[base + __popcll(b & ((1ULL << lane) - 1))] = (uint16_t)e;
-}
 
 __device__ __forceinline__ uint32_t mg_slot(uint64_t id, int H) {
   const uint32_t h = ((uint32_t)id * 0x9E3779B1u) ^ (uint32_t)(id >> 32) * 0x85EBCA77u;
@@ -2853,7 +2734,6 @@ __global__ __launch_bounds__(NT, KHIP_MG_WPE) void k_part_merge(
 // LDS = (H + 64) x 16 B: ids | rowtime | count, the 64 per-lane dummy entries absorb the inactive
 // lanes' CASes.  Phases, the persistent item loop, retries and HAVING / changelog bookkeeping are
 // k_part_merge's (the contract is the same; k_part_commit publishes the result).
-constexpr uint32_t C1_GOLD = 0x9E3779B1u;
 
 // k_part_merge_c1's parameters: only what it reads (a large by-value argument struct keeps its
 // fields live in scalar registers across the item loop; the spills cost VALU moves)
@@ -3381,6 +3261,7 @@ __global__ __launch_bounds__(1024) void k_part_wrange(const int64_t* __restrict_
 // out[11] = rows passing the query's HAVING over all live partitions (maintained: += new - old).
 __global__ __launch_bounds__(256) void k_part_commit(const int64_t* __restrict__ gate, int P,
                                                      const int64_t* __restrict__ pbase,
+                                                     const uint32_t* __restrict__ prn,
                                                      const uint32_t* __restrict__ plist, int nlist,
                                                      uint8_t* __restrict__ sel, int64_t* __restrict__ cnt,
                                                      unsigned long long* __restrict__ newcnt,
@@ -3393,7 +3274,7 @@ __global__ __launch_bounds__(256) void k_part_commit(const int64_t* __restrict__
   int64_t added = 0, failed = 0, hdelta = 0;
   if (plist ? k < nlist : k < P) {
     const uint32_t p = plist ? plist[k] : (uint32_t)k;
-    if (plist || pbase[p + 1] > pbase[p]) {
+    if (plist || (prn ? prn[p] != 0 : pbase[p + 1] > pbase[p])) {
       if (fail[p] == 0) {
         added = (int64_t)newcnt[p] - cnt[p];
         cnt[p] = (int64_t)newcnt[p];
@@ -3545,12 +3426,13 @@ __global__ __launch_bounds__(256) void k_part_rows(const uint64_t* __restrict__ 
 __global__ __launch_bounds__(256) void k_part_chg(const uint64_t* __restrict__ b0, const uint64_t* __restrict__ b1,
                                                   const uint8_t* __restrict__ sel, const int64_t* __restrict__ cnt,
                                                   int64_t cmax, int sw, const int64_t* __restrict__ pbase,
+                                                  const uint32_t* __restrict__ prn,
                                                   const uint8_t* __restrict__ chg, int64_t* __restrict__ counts,
                                                   const int64_t* __restrict__ offs, uint64_t* __restrict__ out,
                                                   uint8_t* __restrict__ otomb) {
   __shared__ int lcnt[4];
   const int64_t p = blockIdx.x;
-  if (pbase[p + 1] == pbase[p]) {  // no record of the push: its flags are stale
+  if (prn ? prn[p] == 0 : pbase[p + 1] == pbase[p]) {  // no record of the push: its flags are stale
     if (threadIdx.x == 0 && counts) counts[p] = 0;
     return;
   }
@@ -3707,6 +3589,7 @@ void part_release(khip_agg* a) {
   DevBuf* bufs[] = {&s.hcnt, &s.hnew, &s.srecA, &s.hcoarse, &s.scan_tmpB, &s.RB, &s.wr, &s.res, &s.closed, &s.closed_ctr, &s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist,
                     &s.tilemax, &s.tilemin, &s.tilekr,
                     &s.tileprefix, &s.tpart, &s.scan_tmp, &s.srec, &s.work,
+                    &s.c1hist, &s.c1bb, &s.c1seg, &s.c1info, &s.prn,
                     &s.pbase, &s.R, &s.ctr, &s.counts};
   for (DevBuf* b : bufs) b->release();
 }
@@ -3736,6 +3619,8 @@ khip_status part_reset(khip_agg* a) {
   s.res_fresh = true;
   s.hvalid = true;
   s.having_total = 0;
+  s.last_c1 = false;
+  s.c1_skip = 0;
   hipLaunchKernelGGL(k_part_reset, dim3(ceil_div(std::max<int64_t>(s.P, 16), 256)), dim3(256), 0, a->stream, s.P,
                      s.hcnt.as<unsigned long long>(), s.hnew.as<unsigned long long>(), s.cnt.as<int64_t>(),
                      s.newcnt.as<unsigned long long>(), s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>(),
@@ -3772,7 +3657,7 @@ static PartAggParams part_params(khip_agg* a) {
   return q;
 }
 
-static khip_status part_regrow(khip_agg* a, int64_t ncmax) {
+khip_status part_regrow(khip_agg* a, int64_t ncmax) {
   PartState& s = a->part;
   DevBuf nb[2], nchg;
   for (int b = 0; b < 2; b++) KHIP_TRY(nb[b].ensure((size_t)s.P * ncmax * a->sw * 8));
@@ -3880,11 +3765,24 @@ static void agg_probe_report(DevBuf& b, int nb) {
 
 // One push slice (n < 2^31).  tot[] receives the P_* counters.
 khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
-                      const uint8_t* rv, const ColPtrs& cols, int64_t* tot) {
+                      const uint8_t* rv, const ColPtrs& cols, int64_t* tot, const int64_t* st_at) {
   PartState& s = a->part;
   // keep the resident groups per partition well inside the LDS table (split = exact re-layout)
   // live groups only: closed (evicted) windows live in the flat store, not in the LDS tables
   while (s.log2P < SPLIT_P_LOG2 && a->occ - s.closed_n > s.P * (int64_t)s.H_eff / 2) KHIP_TRY(part_split(a));
+  // the windowed COUNT(*) pipeline (khip_agg_c1.hip) when it applies; a push it declines (a tile
+  // that may hold late records, a ts span or key range too wide) runs the general path below, and
+  // the next few pushes go straight there
+  s.last_c1 = false;
+  if (s.c1_skip > 0) {
+    s.c1_skip--;
+  } else if (c1_eligible(a, n)) {
+    bool declined = false;
+    KHIP_TRY(c1_push(a, n, keys, ts, kv, rv, tot, &declined, st_at));
+    if (a->profile) (declined ? a->times.c1_declined : a->times.c1_pushes)++;
+    if (!declined) return KHIP_OK;
+    s.c1_skip = 8;
+  }
   const int P = (int)s.P;
   const int64_t tile = (int64_t)PT_THREADS * knob("KHIP_TILE_ITEMS", PT_ITEMS);
   const int pad = (int)knob("KHIP_PAD", 0);
@@ -3933,7 +3831,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   hipLaunchKernelGGL(k_part_hist, dim3(nT), dim3(PT_THREADS), hist_lds, a->stream, keys, ts, kv, rv, n, tile, s.log2P,
                      pad, nT,
                      s.hist.as<uint32_t>(), s.tilemax.as<int64_t>(), s.tilemin.as<int64_t>(), s.tpart.as<int64_t>(),
-                     fbits, lvl2 ? s.hcoarse.as<uint32_t>() : (uint32_t*)nullptr, s.tilekr.as<int64_t>());
+                     fbits, lvl2 ? s.hcoarse.as<uint32_t>() : (uint32_t*)nullptr, s.tilekr.as<int64_t>(), st_at);
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, a->stream, s.tilemax.as<int64_t>(), nT,
                      s.tileprefix.as<int64_t>(), a->stream_time.as<int64_t>());
   // window range of the push (packed identity) and its event-time span → host: they pick the
@@ -4013,7 +3911,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
                      a->windowed ? a->desc.advance_ms : 1, make_fastdiv(a->windowed ? a->desc.advance_ms : 1),
                      a->grace, L, lvl2 ? s.srecA.as<uint64_t>() : s.srec.as<uint64_t>(), ncap,
                      s.tpart.as<int64_t>(), s.wr.as<int64_t>(), r12_ok ? 1 : 0, (stage || wstage) ? 1 : 0,
-                     (r8k || wk) ? 1 : 0);
+                     (r8k || wk) ? 1 : 0, st_at);
   KHIP_TRY_HIP(hipGetLastError());
   if (wk) {  // the wide staged tiles
     auto sw_ = wu >= 4 ? k_part_scatter_w<4, W_NT> : k_part_scatter_w<2, W_NT>;
@@ -4221,7 +4119,8 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     const int nl = pass == 0 ? P : (int)plist.size();
     hipLaunchKernelGGL(k_part_commit, dim3(ceil_div(std::max(nl, 1), 256)), dim3(256), 0, a->stream,
                        (merge && pass == 0) ? s.wr.as<int64_t>() : (const int64_t*)nullptr, P,
-                       s.pbase.as<int64_t>(), pass == 0 ? nullptr : s.work.as<uint32_t>() + work.size(), nl,
+                       s.pbase.as<int64_t>(), (const uint32_t*)nullptr,
+                       pass == 0 ? nullptr : s.work.as<uint32_t>() + work.size(), nl,
                        s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
                        s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>(), s.hcnt.as<unsigned long long>(),
                        s.hnew.as<unsigned long long>());
@@ -4401,7 +4300,7 @@ khip_status part_changes(khip_agg* a, std::vector<uint64_t>* rows, std::vector<u
   KHIP_TRY(s.counts.ensure((P + 1) * 8));
   hipLaunchKernelGGL(k_part_chg, dim3(P), dim3(256), 0, a->stream, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
                      s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.cmax, a->sw, s.pbase.as<int64_t>(),
-                     a->chg.as<uint8_t>(), s.counts.as<int64_t>(), nullptr, nullptr, nullptr);
+                     s.last_c1 ? s.prn.as<uint32_t>() : (const uint32_t*)nullptr, a->chg.as<uint8_t>(), s.counts.as<int64_t>(), nullptr, nullptr, nullptr);
   KHIP_TRY_HIP(hipMemsetAsync(s.counts.as<int64_t>() + P, 0, 8, a->stream));
   hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, a->stream, s.counts.as<int64_t>(), (int64_t)P,
                      s.counts.as<int64_t>() + P);
@@ -4415,7 +4314,7 @@ khip_status part_changes(khip_agg* a, std::vector<uint64_t>* rows, std::vector<u
   KHIP_TRY(ot.ensure((size_t)std::max<int64_t>(n, 1)));
   hipLaunchKernelGGL(k_part_chg, dim3(P), dim3(256), 0, a->stream, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
                      s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.cmax, a->sw, s.pbase.as<int64_t>(),
-                     a->chg.as<uint8_t>(), nullptr, s.counts.as<int64_t>(), out.as<uint64_t>(), ot.as<uint8_t>());
+                     s.last_c1 ? s.prn.as<uint32_t>() : (const uint32_t*)nullptr, a->chg.as<uint8_t>(), nullptr, s.counts.as<int64_t>(), out.as<uint64_t>(), ot.as<uint8_t>());
   KHIP_TRY_HIP(hipGetLastError());
   rows->resize((size_t)n * a->sw);
   tomb->resize((size_t)n);

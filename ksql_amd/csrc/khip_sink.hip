@@ -802,6 +802,11 @@ khip_status khip_sink_encode(khip_sink* s, const khip_sink_rows* rows, khip_sink
     return fail(KHIP_E_INVALID, "row key arrays");
   int ncol = 0;
   int ctype[SK_MAX];
+  bool used[SK_MAX];  // columns some value column reads: only those are staged or passed on
+  for (int c = 0; c < SK_MAX; c++) {
+    ctype[c] = KHIP_TYPE_INT64;
+    used[c] = false;
+  }
   for (int c = 0; c < q.n_val; c++) {
     const int src = q.vsrc[c];
     if (src == KHIP_SINK_SRC_WS && n && !rows->window_start) return fail(KHIP_E_INVALID, "WINDOWSTART source");
@@ -810,6 +815,7 @@ khip_status khip_sink_encode(khip_sink* s, const khip_sink_rows* rows, khip_sink
       if (n && (!rows->col_data || !rows->col_data[src])) return fail(KHIP_E_INVALID, "value source column");
       ncol = std::max(ncol, src + 1);
       ctype[src] = q.vtype[c];
+      used[src] = true;
     }
   }
   DeviceGuard g(s->device);
@@ -822,8 +828,8 @@ khip_status khip_sink_encode(khip_sink* s, const khip_sink_rows* rows, khip_sink
   r.we = rows->window_end;
   r.tomb = rows->tombstone;
   for (int c = 0; c < ncol; c++) {
-    r.col[c] = rows->col_data ? rows->col_data[c] : nullptr;
-    r.cnull[c] = rows->col_null ? rows->col_null[c] : nullptr;
+    r.col[c] = used[c] && rows->col_data ? rows->col_data[c] : nullptr;
+    r.cnull[c] = used[c] && rows->col_null ? rows->col_null[c] : nullptr;
   }
   if (rows->mem == KHIP_MEM_HOST && n) {
     const void* p;
@@ -843,7 +849,7 @@ khip_status khip_sink_encode(khip_sink* s, const khip_sink_rows* rows, khip_sink
     KHIP_TRY(sk_stage(s, s->st_tomb, rows->tombstone, (size_t)n, &p));
     r.tomb = (const uint8_t*)p;
     for (int c = 0; c < ncol; c++) {
-      if (!rows->col_data[c]) continue;
+      if (!used[c] || !rows->col_data[c]) continue;
       KHIP_TRY(sk_stage(s, s->st_col[c], rows->col_data[c], (size_t)n * (ctype[c] == KHIP_TYPE_INT32 ? 4 : 8), &p));
       r.col[c] = p;
       KHIP_TRY(sk_stage(s, s->st_null[c], rows->col_null ? rows->col_null[c] : nullptr, (size_t)n, &p));

@@ -1,0 +1,170 @@
+"""The boundary's struct layouts, pinned three ways (CPU only, gcc).
+
+include/ksqldb_hip.h is the contract; two bindings restate its structs by hand:
+- ksql_amd/abi.py (ctypes), which every test and bench.py call through;
+- INTEGRATION.md §2 (the Java Panama FFM StructLayouts a maintainer adds to ksqlDB).
+A field added, removed, reordered or retyped in one of them and not the others would make the
+caller read or write the wrong bytes.  This test parses every `typedef struct` of the header,
+compiles a C program printing sizeof / alignof / offsetof of each field, and checks
+1. every ctypes structure against its C struct: the same field names in the same order, the same
+   offsets and the same size;
+2. every FFM StructLayout against its C struct: the same field names in order, offsets from the
+   layout's own element sizes and explicit padding (FFM does not pad on its own), and a size
+   that differs from sizeof only by the struct's trailing padding.
+"""
+import ctypes as C
+import json
+import os
+import re
+import subprocess
+
+import pytest
+
+from ksql_amd import abi
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "ksqldb_hip.h")
+
+CTYPES = {  # abi.py class → header struct
+    "khip_batch": abi.Batch,
+    "khip_batch_stats": abi.BatchStats,
+    "khip_agg_spec": abi.AggSpec,
+    "khip_having": abi.Having,
+    "khip_agg_desc": abi.AggDesc,
+    "khip_snapshot": abi.Snapshot,
+    "khip_pull": abi.Pull,
+    "khip_table_desc": abi.TableDesc,
+    "khip_where": abi.Where,
+    "khip_kernel_times": abi.KernelTimes,
+    "khip_table_src": abi.TableSrc,
+    "khip_join_dev_out": abi.JoinDevOut,
+    "khip_join_out": abi.JoinOut,
+    "khip_shuffle_desc": abi.ShuffleDesc,
+    "khip_serde_desc": abi.SerdeDesc,
+    "khip_raw_batch": abi.RawBatch,
+    "khip_sink_desc": abi.SinkDesc,
+    "khip_key_col": abi.KeyCol,
+    "khip_sink_rows": abi.SinkRows,
+    "khip_sink_out": abi.SinkOut,
+}
+
+JAVA = {  # INTEGRATION.md StructLayout → header struct
+    "AGG_SPEC": "khip_agg_spec",
+    "HAVING": "khip_having",
+    "AGG_DESC": "khip_agg_desc",
+    "BATCH": "khip_batch",
+    "TABLE_SRC": "khip_table_src",
+    "STATS": "khip_batch_stats",
+    "SINK_DESC": "khip_sink_desc",
+    "KEY_COL": "khip_key_col",
+    "SINK_ROWS": "khip_sink_rows",
+    "SINK_OUT": "khip_sink_out",
+}
+
+
+def parse_header():
+    """{struct: [field, ...]} for every `typedef struct NAME { ... } NAME;` of the header."""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    out = {}
+    for m in re.finditer(r"typedef\s+struct\s+(\w+)\s*\{(.*?)\}\s*(\w+)\s*;", src, flags=re.S):
+        assert m.group(1) == m.group(3), m.group(1)
+        fields = []
+        for decl in m.group(2).split(";"):
+            decl = " ".join(decl.split())
+            if not decl:
+                continue
+            # "type d1, d2": the first declarator carries the type
+            parts = [p.strip() for p in decl.split(",")]
+            for p in parts:
+                p = re.sub(r"\[[^\]]*\]", "", p)
+                name = re.findall(r"[A-Za-z_]\w*", p)[-1]
+                fields.append(name)
+        out[m.group(1)] = fields
+    return out
+
+
+@pytest.fixture(scope="module")
+def c_layout(tmp_path_factory):
+    structs = parse_header()
+    assert len(structs) >= 20, sorted(structs)
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "ksqldb_hip.h"', "int main(void) {",
+             '  printf("{");']
+    for i, (s, fields) in enumerate(sorted(structs.items())):
+        sep = "," if i else ""
+        lines.append('  printf("%s\\"%s\\": {\\"size\\": %%zu, \\"align\\": %%zu, \\"fields\\": [", sizeof(%s), _Alignof(%s));'
+                     % (sep, s, s, s))
+        for j, f in enumerate(fields):
+            fsep = "," if j else ""
+            lines.append('  printf("%s[\\"%s\\", %%zu, %%zu]", offsetof(%s, %s), sizeof(((%s*)0)->%s));'
+                         % (fsep, f, s, f, s, f))
+        lines.append('  printf("]}");')
+    lines += ['  printf("}\\n");', "  return 0;", "}"]
+    d = tmp_path_factory.mktemp("layout")
+    c = d / "layout.c"
+    c.write_text("\n".join(lines) + "\n")
+    exe = d / "layout"
+    subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(REPO, "include"), str(c),
+                           "-o", str(exe)])
+    return json.loads(subprocess.check_output([str(exe)]).decode())
+
+
+def test_header_structs_all_bound(c_layout):
+    """Every struct of the header has a ctypes mirror (a new struct must get one)."""
+    assert sorted(c_layout) == sorted(CTYPES), set(c_layout) ^ set(CTYPES)
+
+
+@pytest.mark.parametrize("name", sorted(CTYPES))
+def test_ctypes_matches_header(c_layout, name):
+    lay = c_layout[name]
+    cls = CTYPES[name]
+    names = [f[0] for f in cls._fields_]
+    assert names == [f[0] for f in lay["fields"]], (name, names)
+    for fname, off, size in lay["fields"]:
+        field = getattr(cls, fname)
+        assert field.offset == off, (name, fname, field.offset, off)
+        assert field.size == size, (name, fname, field.size, size)
+    assert C.sizeof(cls) == lay["size"], (name, C.sizeof(cls), lay["size"])
+
+
+def parse_java():
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    sizes = {"JAVA_INT": 4, "JAVA_LONG": 8, "JAVA_DOUBLE": 8, "ADDRESS": 8, "JAVA_BYTE": 1, "JAVA_SHORT": 2}
+    layouts = {}
+    for m in re.finditer(r"StructLayout\s+(\w+)\s*=\s*MemoryLayout\.structLayout\((.*?)\);", text, flags=re.S):
+        name, body = m.group(1), m.group(2)
+        off = 0
+        fields = []
+        for tok in re.finditer(r"MemoryLayout\.paddingLayout\((\d+)\)|(\w+)\.withName\(\"(\w+)\"\)", body):
+            if tok.group(1):
+                off += int(tok.group(1))
+                continue
+            kind, fname = tok.group(2), tok.group(3)
+            if kind in sizes:
+                size = sizes[kind]
+            else:  # a nested layout defined above
+                size = layouts[kind]["size"]
+            fields.append((fname, off, size))
+            off += size
+        layouts[name] = {"fields": fields, "size": off}
+    return layouts
+
+
+def test_java_layouts_listed():
+    assert sorted(parse_java()) == sorted(JAVA)
+
+
+@pytest.mark.parametrize("jname", sorted(JAVA))
+def test_java_layout_matches_header(c_layout, jname):
+    lay = c_layout[JAVA[jname]]
+    jl = parse_java()[jname]
+    assert [f[0] for f in jl["fields"]] == [f[0] for f in lay["fields"]], jname
+    for (fname, joff, jsize), (_, off, size) in zip(jl["fields"], lay["fields"]):
+        assert (joff, jsize) == (off, size), (jname, fname, joff, jsize, off, size)
+    tail = lay["size"] - jl["size"]
+    assert 0 <= tail < lay["align"], (jname, jl["size"], lay["size"])
+
+
+def test_integration_states_the_abi_version():
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    assert "khip_abi_version() == %d" % abi.ABI_VERSION in text

@@ -114,6 +114,25 @@ def test_value_null_kafka_and_empty(prod):
     s.close()
 
 
+@pytest.mark.parametrize("vfmt", ["JSON", "DELIMITED"])
+def test_value_sources_with_gap(prod, vfmt):
+    """Value columns read rows columns 0 and 2; column 1 (an INT32 column no value column reads,
+    n * 4 bytes of host memory) sits in the gap and must not be staged or read."""
+    rng = np.random.default_rng(5)
+    n = 5000
+    a = rng.integers(-2**40, 2**40, n, dtype=np.int64)
+    gap = rng.integers(-2**31, 2**31 - 1, n, dtype=np.int64).astype(np.int32)
+    b = rng.uniform(-1e6, 1e6, n)
+    bn = rng.random(n) < 0.1
+    s = abi.SinkHandle(prod, "KAFKA", [("K", "INT64")], vfmt, [("A", "INT64", 0), ("B", "DOUBLE", 2)])
+    kb, vb = s.encode(_rows(n, keys=np.arange(n, dtype=np.int64), values=[a, gap, b],
+                            nulls=[np.zeros(n, bool), np.zeros(n, bool), bn]))
+    for i in range(n):
+        exp = sink_ref.encode_value(vfmt, [("A", "INT64"), ("B", "DOUBLE")], [int(a[i]), None if bn[i] else float(b[i])])
+        assert vb[i] == exp, (i, vb[i], exp)
+    s.close()
+
+
 @pytest.mark.parametrize("kfmt", ["JSON", "DELIMITED"])
 @pytest.mark.parametrize("device", [False, True])
 def test_composite_keys(prod, kfmt, device):

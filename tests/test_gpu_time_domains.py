@@ -1,0 +1,319 @@
+"""Stream-time domains (ABI 5, include/ksqldb_hip.h KHIP_TIME_*) on the HIP path, against the oracle.
+
+The reference keeps one observedStreamTime per Kafka Streams task (KStreamWindowAggregate, as
+called from S/StreamAggregateBuilder.java:287-294), one task per input partition
+(C/util/KsqlConstants.java:42); TopologyTestDriver runs one task over every record in arrival
+order (F/tools/TestExecutorUtil.java:123-126).  The cases use late-heavy data (small grace,
+disorder across window boundaries) so that the domain decides which records are dropped:
+
+- PARTITION: one handle serving P partitions (rows of partition p = one run per batch, keys
+  co-partitioned: key % P == p) equals P independent oracle tasks, one per partition — the
+  union of their tables, their summed counters; the handle's stream time is the slowest task's.
+  Partitions advance at different event-time rates, so one shared stream time would drop the
+  slow partitions' records.  Both engines; the COUNT(*) pipeline on a late-free variant.
+- SUPPLIED (the GLOBAL domain across ranks): a global stream of micro-batches, each split into
+  contiguous arrival chunks, one per rank; rank r scans its chunk (khip_stream_time_scan) seeded
+  with the exclusive prefix max of the earlier ranks' chunk maxima, routes rows to the key owner
+  with their stream time, and each owner pushes them.  The union of the owners' tables equals ONE
+  oracle task over the whole stream.  Emulated in one process, and for real with two processes
+  over gloo on this one GPU (the product library in both ranks).
+- khip_stream_time_scan itself against numpy, and the batch validation errors.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from ksql_amd import abi
+from test_gpu_parity import assert_snap_equal
+
+pytestmark = pytest.mark.gpu
+
+AGGS = [("COUNT_STAR", -1), ("SUM", 0), ("MAX", 0)]
+
+
+@pytest.fixture(scope="module")
+def prod():
+    return abi.load_product()
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return abi.load_oracle()
+
+
+def _desc(window="TUMBLING", size=5000, adv=0, grace=1000, flags=0, aggs=AGGS, **kw):
+    return abi.make_agg_desc(window_kind=window, size_ms=size, advance_ms=adv or size, grace_ms=grace,
+                             col_types=["INT64"], aggs=aggs, flags=flags, capacity_hint=1 << 20, **kw)
+
+
+def _union(snaps, desc):
+    """Snapshots of disjoint-key tasks → one snapshot sorted by (key, ws)."""
+    keys = np.concatenate([s["key"] for s in snaps])
+    ws = np.concatenate([s["ws"] for s in snaps])
+    order = np.lexsort((ws, keys))
+    out = {"n": int(len(keys)), "key": keys[order], "ws": ws[order],
+           "we": np.concatenate([s["we"] for s in snaps])[order],
+           "rowtime": np.concatenate([s["rowtime"] for s in snaps])[order],
+           "values": [np.concatenate([s["values"][a] for s in snaps])[order] for a in range(desc.n_aggs)],
+           "nulls": [np.concatenate([s["nulls"][a] for s in snaps])[order] for a in range(desc.n_aggs)]}
+    return out
+
+
+def _partition_batches(rng, P, nb, per, keys_per_part, rate_skew=True, disorder=3000):
+    """nb batches; in each, partition p's rows are one run (partitions in a random order), keys
+    with key % P == p, event time advancing at a per-partition rate (partition p lags p * 20 s)."""
+    batches = []
+    t0 = np.zeros(P, np.int64)
+    for b in range(nb):
+        order = rng.permutation(P)
+        ks, ts, vs, ps = [], [], [], []
+        for p in order:
+            n = int(rng.integers(per // 2, per * 3 // 2))
+            k = rng.integers(0, keys_per_part, n) * P + p
+            span = 30_000
+            t = t0[p] + (np.arange(n) * span) // n + rng.integers(0, disorder, n)
+            t0[p] += span
+            ks.append(k)
+            ts.append(t + (200_000 - p * 20_000 if rate_skew else 0))
+            vs.append(rng.integers(-1000, 1000, n))
+            ps.append(np.full(n, p, np.int32))
+        batches.append((np.concatenate(ks), np.concatenate(ts), np.concatenate(vs), np.concatenate(ps)))
+    return batches
+
+
+@pytest.mark.parametrize("engine", ["part", "atomic"])
+@pytest.mark.parametrize("window", ["TUMBLING", "HOPPING"])
+def test_partition_domain_matches_independent_tasks(prod, orc, engine, window):
+    rng = np.random.default_rng(11 + (engine == "atomic") + 2 * (window == "HOPPING"))
+    P = 4
+    batches = _partition_batches(rng, P, nb=3, per=40_000, keys_per_part=3000)
+    kw = dict(window=window, adv=2500 if window == "HOPPING" else 0)
+    flags = abi.FLAG_ENGINE_ATOMIC if engine == "atomic" else 0
+    gd = _desc(time_domain="PARTITION", n_partitions=P, flags=flags, **kw)
+    g = abi.AggHandle(prod, gd)
+    tasks = [abi.AggHandle(orc, _desc(**kw)) for _ in range(P)]
+    late = 0
+    for k, t, v, p in batches:
+        gs = g.push(abi.HostBatch(t, keys=k, cols=[v], partition=p))
+        os_ = [tasks[q].push(abi.HostBatch(t[p == q], keys=k[p == q], cols=[v[p == q]])) for q in range(P)]
+        for f in ("rows_accepted", "windows_applied", "windows_late", "dropped_null_key", "dropped_bad_ts"):
+            assert gs[f] == sum(o[f] for o in os_), (f, gs[f], [o[f] for o in os_])
+        assert gs["stream_time"] == min(o["stream_time"] for o in os_)
+        late += gs["windows_late"]
+    assert late > 0  # the domain mattered: some records were late in their own task
+    assert_snap_equal(g.snapshot(), _union([h.snapshot() for h in tasks], gd), gd)
+    g.close()
+    for h in tasks:
+        h.close()
+
+
+def test_partition_domain_one_shared_stream_time_differs(prod, orc):
+    """The same data through one TASK-domain handle drops more (the fast partition's stream time
+    closes the slow partitions' windows): the PARTITION result above is not a coincidence."""
+    rng = np.random.default_rng(11)
+    P = 4
+    batches = _partition_batches(rng, P, nb=3, per=40_000, keys_per_part=3000)
+    g = abi.AggHandle(prod, _desc())
+    o = abi.AggHandle(orc, _desc())
+    for k, t, v, p in batches:
+        gs = g.push(abi.HostBatch(t, keys=k, cols=[v]))
+        assert gs == o.push(abi.HostBatch(t, keys=k, cols=[v]))
+    assert gs["windows_late"] > 0
+    g.close()
+    o.close()
+
+
+def test_partition_domain_count_pipeline(prod, orc):
+    """COUNT(*) TUMBLING without late records (default grace): the COUNT(*) pipeline takes the
+    pushes with the per-row stream times."""
+    rng = np.random.default_rng(13)
+    P = 8
+    batches = _partition_batches(rng, P, nb=2, per=60_000, keys_per_part=5000, disorder=500)
+    aggs = [("COUNT_STAR", -1)]
+    gd = abi.make_agg_desc(window_kind="TUMBLING", size_ms=5000, aggs=aggs, capacity_hint=1 << 22,
+                           flags=abi.FLAG_PROFILE, time_domain="PARTITION", n_partitions=P)
+    g = abi.AggHandle(prod, gd)
+    tasks = [abi.AggHandle(orc, abi.make_agg_desc(window_kind="TUMBLING", size_ms=5000, aggs=aggs)) for _ in range(P)]
+    for k, t, v, p in batches:
+        gs = g.push(abi.HostBatch(t, keys=k, partition=p))
+        os_ = [tasks[q].push(abi.HostBatch(t[p == q], keys=k[p == q])) for q in range(P)]
+        assert gs["windows_applied"] == sum(o["windows_applied"] for o in os_)
+        assert gs["stream_time"] == min(o["stream_time"] for o in os_)
+    assert_snap_equal(g.snapshot(), _union([h.snapshot() for h in tasks], gd), gd)
+    kt = g.kernel_times()
+    assert kt["c1_pushes"] == 2, kt
+    g.close()
+    for h in tasks:
+        h.close()
+
+
+def test_partition_domain_rejects_bad_batches(prod):
+    g = abi.AggHandle(prod, _desc(time_domain="PARTITION", n_partitions=2))
+    k = np.arange(10, dtype=np.int64)
+    t = np.arange(10, dtype=np.int64) * 100
+    v = np.zeros(10, np.int64)
+    with pytest.raises(abi.KsqlHipError, match="no partition column"):
+        g.push(abi.HostBatch(t, keys=k, cols=[v]))
+    with pytest.raises(abi.KsqlHipError, match="contiguous run"):
+        g.push(abi.HostBatch(t, keys=k, cols=[v], partition=np.array([0, 0, 1, 1, 0, 0, 1, 1, 1, 1], np.int32)))
+    with pytest.raises(abi.KsqlHipError, match="outside"):
+        g.push(abi.HostBatch(t, keys=k, cols=[v], partition=np.full(10, 2, np.int32)))
+    g.close()
+    with pytest.raises(abi.KsqlHipError):
+        abi.AggHandle(prod, _desc(time_domain="PARTITION", n_partitions=0))
+    with pytest.raises(abi.KsqlHipError):
+        abi.AggHandle(prod, abi.make_agg_desc(window_kind="SESSION", size_ms=1000, aggs=[("COUNT_STAR", -1)],
+                                              time_domain="SUPPLIED"))
+
+
+def _np_stream_time(ts, valid, seed):
+    v = np.where(valid & (ts >= 0), ts, -1)
+    return np.maximum.accumulate(np.concatenate([[seed], v]))[1:]
+
+
+@pytest.mark.parametrize("n", [1, 4095, 4097, 1_000_003])
+def test_stream_time_scan(prod, n):
+    rng = np.random.default_rng(n)
+    ts = rng.integers(0, 10**9, n)
+    ts[rng.random(n) < 0.01] = -5
+    kv = rng.random(n) > 0.03
+    seed = int(rng.integers(-1, 10**8))
+    h = abi.AggHandle(prod, _desc())
+    out, mx = h.stream_time_scan(abi.HostBatch(ts, keys=np.zeros(n, np.int64), key_valid=kv), seed)
+    ref = _np_stream_time(ts, kv, seed)
+    assert np.array_equal(out, ref)
+    assert mx == ref[-1]
+    h.close()
+
+
+def _global_stream(rng, nb, per, keys):
+    """Late-heavy global stream: per batch (keys, ts, value)."""
+    out = []
+    t0 = 0
+    for b in range(nb):
+        n = per
+        k = rng.integers(0, keys, n)
+        t = t0 + (np.arange(n) * 40_000) // n + rng.integers(0, 6000, n)
+        t0 += 40_000
+        out.append((k, t, rng.integers(-100, 100, n)))
+    return out
+
+
+def _route_supplied(prod_handles, scan_handle, stream, world):
+    """The ranks' work for each micro-batch: scan its chunk with the earlier ranks' maxima as seed,
+    route every row to its key's owner with its stream time, the owner pushes.  Returns the owners'
+    summed late counts."""
+    gst = -1
+    late = 0
+    for k, t, v in stream:
+        n = len(t)
+        bounds = [n * r // world for r in range(world + 1)]
+        chunks, maxima = [], []
+        for r in range(world):  # chunk maxima first (the all-gather)
+            lo, hi = bounds[r], bounds[r + 1]
+            _, mx = scan_handle.stream_time_scan(abi.HostBatch(t[lo:hi], keys=k[lo:hi]), -1)
+            maxima.append(mx)
+        for r in range(world):
+            lo, hi = bounds[r], bounds[r + 1]
+            seed = max([gst] + maxima[:r])
+            st, _ = scan_handle.stream_time_scan(abi.HostBatch(t[lo:hi], keys=k[lo:hi]), seed)
+            chunks.append((k[lo:hi], t[lo:hi], v[lo:hi], st))
+        gst = max([gst] + maxima)
+        for owner in range(world):
+            parts = [(ck[ck % world == owner], ct[ck % world == owner], cv[ck % world == owner], cs[ck % world == owner])
+                     for ck, ct, cv, cs in chunks]
+            kk, tt, vv, ss = (np.concatenate([p[i] for p in parts]) for i in range(4))
+            st = prod_handles[owner].push(abi.HostBatch(tt, keys=kk, cols=[vv], stream_time=ss))
+            late += st["windows_late"]
+            assert st["stream_time"] <= gst
+    return late
+
+
+@pytest.mark.parametrize("engine", ["part", "atomic"])
+def test_supplied_domain_union_equals_one_task(prod, orc, engine):
+    rng = np.random.default_rng(21)
+    world = 2
+    stream = _global_stream(rng, nb=4, per=60_000, keys=4000)
+    flags = abi.FLAG_ENGINE_ATOMIC if engine == "atomic" else 0
+    gd = _desc(time_domain="SUPPLIED", flags=flags)
+    hs = [abi.AggHandle(prod, gd) for _ in range(world)]
+    late = _route_supplied(hs, hs[0], stream, world)
+    o = abi.AggHandle(orc, _desc())
+    olate = sum(o.push(abi.HostBatch(t, keys=k, cols=[v]))["windows_late"] for k, t, v in stream)
+    assert late == olate and late > 0
+    assert_snap_equal(_union([h.snapshot() for h in hs], gd), o.snapshot(), gd)
+    for h in hs + [o]:
+        h.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _gloo_rank(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        prod = abi.load_product()
+        h = abi.AggHandle(prod, _desc(time_domain="SUPPLIED"))
+        rng = np.random.default_rng(21)  # every rank generates the same global stream, keeps its chunk
+        stream = _global_stream(rng, nb=4, per=60_000, keys=4000)
+        gst = -1
+        late = 0
+        for k, t, v in stream:
+            n = len(t)
+            lo, hi = n * rank // world, n * (rank + 1) // world
+            ck, ct, cv = k[lo:hi], t[lo:hi], v[lo:hi]
+            _, mx = h.stream_time_scan(abi.HostBatch(ct, keys=ck), -1)
+            maxima = torch.zeros(world, dtype=torch.int64)
+            dist.all_gather_into_tensor(maxima, torch.tensor([mx], dtype=torch.int64))
+            maxima = maxima.tolist()
+            st, _ = h.stream_time_scan(abi.HostBatch(ct, keys=ck), max([gst] + maxima[:rank]))
+            gst = max([gst] + maxima)
+            out = [(ck[ck % world == d], ct[ck % world == d], cv[ck % world == d], st[ck % world == d])
+                   for d in range(world)]
+            got = [None] * world
+            dist.all_gather_object(got, out)
+            mine = [got[src][rank] for src in range(world)]  # rows routed to this rank, by source rank
+            kk, tt, vv, ss = (np.concatenate([m[i] for m in mine]) for i in range(4))
+            late += h.push(abi.HostBatch(tt, keys=kk, cols=[vv], stream_time=ss))["windows_late"]
+        s = h.snapshot()
+        h.close()
+        res = [None] * world
+        dist.all_gather_object(res, (s, late))
+        if rank == 0:
+            q.put(res)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_supplied_domain_two_processes_gloo_one_gpu(orc):
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(21)
+    stream = _global_stream(rng, nb=4, per=60_000, keys=4000)
+    o = abi.AggHandle(orc, _desc())
+    olate = sum(o.push(abi.HostBatch(t, keys=k, cols=[v]))["windows_late"] for k, t, v in stream)
+    gd = _desc()
+    assert sum(r[1] for r in res) == olate > 0
+    assert_snap_equal(_union([r[0] for r in res], gd), o.snapshot(), gd)
+    o.close()
