@@ -76,6 +76,9 @@ def parse():
     ap.add_argument("--records", type=int, default=None, help="records per GPU (default: the config's)")
     ap.add_argument("--keys", type=int, default=10_000_000, help="possible_fraud: card numbers per GPU")
     ap.add_argument("--utf8", action="store_true", help="possible_fraud: VARCHAR card numbers (16 bytes)")
+    ap.add_argument("--sparse-keys", action="store_true",
+                    help="possible_fraud: card numbers spread over [0, 2^53) by a bijection of the dense ids "
+                         "(the key range does not fit 32 bits)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target CPU baseline sample time per run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
@@ -612,6 +615,7 @@ def main():
 
 # ------------------------------------------------------------------ C2 possible_fraud
 
+SPARSE_MULT = 0x5DEECE66D  # --sparse-keys: odd, so id -> id * SPARSE_MULT mod 2^64 is a bijection
 BYTES_PER_RECORD_C2 = 80  # W_in 16 + F(1) x 2 x S_slot(32)
 BYTES_PER_RECORD_C2_UTF8 = 16 + 8 + 8 + 64  # key bytes 16 + offset 8 + ts 8 + 2 x S_slot(32)
 
@@ -621,6 +625,8 @@ def bench_possible_fraud(args, lib, rank, world, local):
     from ksql_amd import abi, synth
     n = args.records or 100_000_000
     card, ts = synth.possible_fraud(0, n, n, xp="torch", device="cuda", rank=rank, world=world, keys=args.keys)
+    if args.sparse_keys:  # a bijection on [0, 2^53): odd multiplier mod 2^64, then the low 53 bits
+        card = (card * SPARSE_MULT) & ((1 << 53) - 1)
     if args.utf8:
         offs, kbytes = synth.card_utf8(card, xp="torch")
         batch = abi.DeviceBatch(ts, key_offsets=offs, key_bytes=kbytes)
@@ -675,15 +681,24 @@ def bench_possible_fraud(args, lib, rank, world, local):
     phase = push_phases(kt, kt["apply_launches"])
     push_ms = sum(phase.values())
     bpr = BYTES_PER_RECORD_C2_UTF8 if args.utf8 else BYTES_PER_RECORD_C2
-    own = {"stream_time_ms": 16, "dict_ms": 32, "partition_ms": 32, "apply_ms": 16 + 32.0 * groups / n,
-           "finalize_ms": 0}
+    c1 = kt.get("c1_pushes", 0) > 0
+    if c1:  # the COUNT(*) pipeline: keys-only histogram; scatter + refine of 8-byte (12 wide) records
+        wide = args.sparse_keys
+        own = {"stream_time_ms": 8, "dict_ms": 32, "partition_ms": (16 + 12 + 12 + 12) if wide else (16 + 8 + 8 + 8),
+               "apply_ms": (12 if wide else 8) + 32.0 * groups / n, "finalize_ms": 0}
+    else:
+        own = {"stream_time_ms": 16, "dict_ms": 32, "partition_ms": 32, "apply_ms": 16 + 32.0 * groups / n,
+               "finalize_ms": 0}
     per_kernel = {k: {"ms": phase[k], "bytes_per_record": own[k],
                       "GB/s": own[k] * n / (phase[k] / 1000.0) / 1e9} for k in phase if phase[k] > 0}
-    variant = "_utf8" if args.utf8 else ""
+    variant = "_utf8" if args.utf8 else ("_sparse" if args.sparse_keys else "")
     traffic = load_traffic(args.traffic_json, "possible_fraud" + ("_atomic" if args.engine == "atomic" else ""), n,
                            variant)
     roof = roofline(bpr * n, ms_step, push_ms, per_kernel, traffic, bpr,
-                    kernel="khip_agg_push (k_part_hist + scans + k_part_scatter + k_part_agg + commit) + HAVING count")
+                    kernel=("khip_agg_push (COUNT(*) pipeline: k_c1_hist + offsets + k_c1_scatter + k_c1_check + "
+                            "k_c1_refine + k_c1_merge + commit) + HAVING count") if c1 else
+                           "khip_agg_push (k_part_hist + scans + k_part_scatter + k_part_refine + k_part_merge + "
+                           "commit) + HAVING count")
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_agg(
@@ -693,7 +708,8 @@ def bench_possible_fraud(args, lib, rank, world, local):
     line("records/sec, windowed GROUP BY (COUNT(*) TUMBLING 5 s GROUP BY card_number HAVING > 3)",
          world * n * args.steps / elapsed, world, args, ms_step, "int64",
          "synthetic (splitmix64, ksql_amd/synth.py), device-resident columnar batch",
-         {"workload": "possible_fraud", "key": "VARCHAR(16) card_number" if args.utf8 else "BIGINT card_number",
+         {"workload": "possible_fraud", "key": ("VARCHAR(16) card_number" if args.utf8 else "BIGINT card_number") +
+                                                 (" spread over 2^53" if args.sparse_keys else ""),
           "records_per_gpu": n, "keys_per_gpu": args.keys, "window": "TUMBLING 5s, grace default",
           "having": "COUNT(*) > 3", "groups_per_gpu": groups, "having_rows_per_gpu": int(rows),
           "parallelism": "key-hash shards x%d" % world},

@@ -63,7 +63,10 @@ enum {
   CI_KMINC = 12,   // kmin copied for the refine / merge
   CI_WHI = 13,     // largest relative window index
   CI_KRANGE = 14,
-  CI_N = 16
+  CI_WIDE = 15,    // records of this push: 1 = key hash + u32 ts words (the key range is too wide)
+  CI_REASON = 16,  // declined: 1 = the key range needs the wide records (the host retries with them)
+  CI_FITS = 17,    // the key range fits the compact records (a wide push tells the host)
+  CI_N = 24
 };
 
 __device__ __forceinline__ int bits_of(uint64_t v) { return v ? 64 - __clzll((long long)v) : 0; }
@@ -155,26 +158,80 @@ __global__ __launch_bounds__(C1_NT) void k_c1_hist(const int64_t* __restrict__ k
 // Records of tile t → their bucket's run (offs[t][b] from the column prefix).  8-byte record:
 // (key - kmin) << 32 | (uint32)(ts - T0); invalid records keep their key word (their bucket is the
 // key's) with the sentinel low word.  Same staged step as k_part_scatter_r8.
+// WIDE (the key range does not fit 32 bits): the record is the 64-bit key hash (key = its inverse)
+// and ts - T0 goes to a parallel u32 array (srecT), staged beside it.
 template <int U, int NT>
+__device__ __forceinline__ void stage_step_c1w(const int64_t (&rec)[U], const uint32_t (&t32)[U], const uint32_t (&bin)[U],
+                                               const bool (&ok)[U], int nb, const StageR8& L, uint32_t* lt32,
+                                               uint64_t* __restrict__ srec, uint32_t* __restrict__ srecT) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  uint32_t rank[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) rank[u] = ok[u] ? atomicAdd(&L.cnt[bin[u]], 1u) : 0u;
+  lds_barrier();
+  const uint32_t c = t < nb ? L.cnt[t] : 0u;
+  uint32_t incl = c;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) L.wsum[wave] = (int)incl;
+  lds_barrier();
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < NT / 64; k++) {
+    before += k < wave ? (uint32_t)L.wsum[k] : 0u;
+    tot += (uint32_t)L.wsum[k];
+  }
+  if (t < nb) {
+    L.sbase[t] = before + incl - c;
+    L.gpos[t] = L.cur[t];
+    L.cur[t] += c;
+    L.cnt[t] = 0u;
+  }
+  lds_barrier();
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    if (ok[u]) {
+      const uint32_t i = L.sbase[bin[u]] + rank[u];
+      L.sp[i] = rec[u];
+      lt32[i] = t32[u];
+      L.sbin[i] = (uint16_t)bin[u];
+    }
+  lds_barrier();
+  for (uint32_t j = t; j < tot; j += NT) {
+    const uint32_t b = L.sbin[j];
+    const uint64_t pos = (uint64_t)L.gpos[b] + (j - L.sbase[b]);
+    srec[pos] = (uint64_t)L.sp[j];
+    srecT[pos] = lt32[j];
+  }
+}
+
+template <int U, int NT, bool WIDE, bool ST>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_c1_scatter(
     const int64_t* __restrict__ keys, const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
     const uint8_t* __restrict__ rv, int64_t n, int64_t nT, int log2B, const uint32_t* __restrict__ offs,
     uint64_t* __restrict__ srec, int64_t* __restrict__ stepstat, int64_t* __restrict__ tpart,
-    int64_t* __restrict__ ci, const int64_t* __restrict__ st_at) {
+    int64_t* __restrict__ ci, const int64_t* __restrict__ st_at, uint32_t* __restrict__ srecT) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int wsum[NT / 64];
   __shared__ unsigned long long lc[4];
-  __shared__ int64_t lt[2][2][NT / 64];  // [step parity][max | min][wave]
+  __shared__ long long lt[2][2];  // [step parity][max | min] of the step's accepted ts (LDS atomics)
   __shared__ int lfail;
   constexpr int S = U * NT;
   const int B = 1 << log2B;
   const int64_t t = tile_of(blockIdx.x, nT);
   const StageR8 L = stage_r8_carve(smem, B, S, wsum);
+  uint32_t* lt32 = (uint32_t*)(smem + stage_r8_lds_bytes(B, S));  // WIDE: the staged ts - T0
   for (int b = threadIdx.x; b < B; b += NT) {
     L.cur[b] = offs[t * B + b];
     L.cnt[b] = 0u;
   }
   if (threadIdx.x < 4) lc[threadIdx.x] = 0;
+  if (threadIdx.x < 2) {
+    lt[threadIdx.x][0] = -1;
+    lt[threadIdx.x][1] = INT64_MAX;
+  }
   if (threadIdx.x == 0) lfail = 0;
   const int64_t kmin = ci[CI_KMIN], T0 = ci[CI_T0];
   const int shift = log2B == 0 ? 64 : 64 - log2B;
@@ -183,7 +240,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const int64_t end = base + C1_TILE < n ? base + C1_TILE : n;
   int64_t c_acc = 0, c_nk = 0, c_nr = 0, c_bt = 0;
   bool tfail = false;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int64_t x[U], k[U];
   auto load_step = [&](int64_t i0, int64_t (&dx)[U], int64_t (&dk)[U]) {
 #pragma unroll
@@ -200,7 +256,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   for (int st = 0; s0 < end; s0 += S, st++) {  // uniform across the block: barriers inside
     const int64_t i0 = s0 + threadIdx.x;
     bool ok[U];
-    uint32_t bin[U];
+    uint32_t bin[U], t32[U];
     int64_t rec[U];
     int64_t tmx = -1, tmn = INT64_MAX;  // this step's accepted ts range (k_c1_check's late test)
 #pragma unroll
@@ -213,36 +269,30 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
       c_nr += ok[u] && kok && !rok;
       c_bt += ok[u] && kok && rok && x[u] < 0;
       c_acc += valid;
-      const int64_t sx = st_at ? st_at[ok[u] ? i : base] : x[u];  // ABI 5 domains: the given stream time
+      const int64_t sx = ST ? st_at[ok[u] ? i : base] : x[u];  // ABI 5 domains: the given stream time
       tmx = valid && sx > tmx ? sx : tmx;
       tmn = valid && x[u] < tmn ? x[u] : tmn;
       const int64_t d = x[u] - T0;
       tfail |= valid && (d <= (int64_t)INT32_MIN || d > (int64_t)INT32_MAX);
-      bin[u] = stage_bin(key_hash(k[u]), shift, bmask);
-      rec[u] = (int64_t)(((uint64_t)(k[u] - kmin) << 32) | (valid ? (uint64_t)(uint32_t)d : (uint64_t)C1_SENT));
+      const uint64_t hk = key_hash(k[u]);
+      bin[u] = stage_bin(hk, shift, bmask);
+      t32[u] = valid ? (uint32_t)d : C1_SENT;
+      rec[u] = WIDE ? (int64_t)hk : (int64_t)(((uint64_t)(k[u] - kmin) << 32) | (uint64_t)t32[u]);
     }
-    for (int off = 32; off > 0; off >>= 1) {
-      const int64_t a = __shfl_xor(tmx, off, 64), b = __shfl_xor(tmn, off, 64);
-      tmx = a > tmx ? a : tmx;
-      tmn = b < tmn ? b : tmn;
-    }
-    if (lane == 0) {
-      lt[st & 1][0][wave] = tmx;
-      lt[st & 1][1][wave] = tmn;
+    if (tmx >= 0) {
+      atomicMax(&lt[st & 1][0], (long long)tmx);
+      atomicMin(&lt[st & 1][1], (long long)tmn);
     }
     // the next step's loads go into x / k (dead now) and stay in flight through this step's stage
     if (s0 + S < end) load_step(i0 + S, x, k);
-    stage_step_r8<U, NT>(rec, bin, ok, B, L, srec);
-    if (threadIdx.x == 0) {  // the stage's barriers ordered every wave's lt write before this
-      int64_t a = -1, b = INT64_MAX;
-#pragma unroll
-      for (int w = 0; w < NT / 64; w++) {
-        a = lt[st & 1][0][w] > a ? lt[st & 1][0][w] : a;
-        b = lt[st & 1][1][w] < b ? lt[st & 1][1][w] : b;
-      }
+    if constexpr (WIDE) stage_step_c1w<U, NT>(rec, t32, bin, ok, B, L, lt32, srec, srecT);
+    else stage_step_r8<U, NT>(rec, bin, ok, B, L, srec);
+    if (threadIdx.x == 0) {  // the stage's barriers ordered every wave's lt atomics before this
       const int64_t g = (s0 / S) * 2;  // global step index (records [g/2 * S, +S))
-      stepstat[g] = a;
-      stepstat[g + 1] = b;
+      stepstat[g] = lt[st & 1][0];
+      stepstat[g + 1] = lt[st & 1][1];
+      lt[st & 1][0] = -1;  // for step st + 2 (its atomics come after step st + 1's barriers)
+      lt[st & 1][1] = INT64_MAX;
     }
   }
   c_acc = wave_sum(c_acc);
@@ -279,7 +329,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 // merge and commit use.  Declined: nothing persistent is touched.
 __global__ __launch_bounds__(1024) void k_c1_check(
     const int64_t* __restrict__ stepstat, int64_t nS, int64_t size, int64_t adv, FastDiv fd, int64_t grace,
-    int64_t close0, int fresh, int log2B, const int64_t* __restrict__ bb, int* __restrict__ cstart,
+    int64_t close0, int fresh, int log2B, int log2P, int wide, const int64_t* __restrict__ bb, int* __restrict__ cstart,
     int64_t* __restrict__ ci, int64_t* __restrict__ stream_time, int64_t* __restrict__ res,
     unsigned long long* __restrict__ ctr, unsigned long long* __restrict__ closed_ctr, unsigned long long closed_n) {
   __shared__ int64_t wmx[16];
@@ -346,8 +396,11 @@ __global__ __launch_bounds__(1024) void k_c1_check(
   const bool tfail = ci[CI_TFAIL] != 0;
   ci[CI_TFAIL] = 0;
   bool ok = !lslow && !tfail && mxc <= C1_SEGMAX && kmax >= kmin;
-  const uint64_t krange = ok ? (uint64_t)kmax - (uint64_t)kmin : 0;
-  ok = ok && krange < 0xFFFFFFFFull;
+  const uint64_t krange = kmax >= kmin ? (uint64_t)kmax - (uint64_t)kmin : 0;
+  const bool fits = krange < 0xFFFFFFFFull;
+  ci[CI_FITS] = fits ? 1 : 0;
+  ci[CI_REASON] = ok && !wide && !fits ? 1 : 0;
+  ok = ok && (wide || fits);
   // window range of this push's records and of the live resident rows (k_part_wrange)
   int64_t lo = INT64_MAX, hi = INT64_MIN;
   if (gmx >= 0) {
@@ -368,7 +421,7 @@ __global__ __launch_bounds__(1024) void k_c1_check(
   }
   const bool none = lo > hi;  // nothing live, nothing new
   if (none) lo = hi = 0;
-  ok = ok && (uint64_t)(hi - lo) < 0xFFFFFFFEull;
+  ok = ok && (uint64_t)(hi - lo) < (wide ? ((uint64_t)1 << log2P) - 1 : 0xFFFFFFFEull);
   const int wbits = bits_of((uint64_t)(hi - lo)), kbits = bits_of(krange);
   ci[CI_GATE] = ok ? 1 : 0;
   if (!ok) return;
@@ -377,7 +430,8 @@ __global__ __launch_bounds__(1024) void k_c1_check(
   ci[CI_WBITS] = wbits;
   ci[CI_KBITS] = kbits;
   ci[CI_KRANGE] = (int64_t)krange;
-  ci[CI_ID32] = kbits + wbits <= 31 ? 1 : 0;
+  ci[CI_ID32] = !wide && kbits + wbits <= 31 ? 1 : 0;
+  ci[CI_WIDE] = wide;
   ci[CI_TMIN] = gmx >= 0 ? gmn : 0;
   ci[CI_TMAX] = gmx;
   ci[CI_NCHUNK] = acc;
@@ -393,15 +447,18 @@ __global__ __launch_bounds__(1024) void k_c1_check(
 // Work item w = chunk c of bucket b (cstart): its records are counting-sorted by partition
 // inside the bucket (F = 2^fbits bins) in LDS and written back to the same positions of the
 // output; seg[w][f] (u16) = partition f's first record in the chunk, seg[w][F] = valid records.
-template <int U, int NT>
+// WIDE: records are key hashes (srcA / srec) with ts - T0 in parallel u32 arrays (srcAT / srecT);
+// the two are staged one after the other through the same LDS.
+template <int U, int NT, bool WIDE>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_c1_refine(
     const uint64_t* __restrict__ srcA, const int64_t* __restrict__ bb, const int* __restrict__ cstart, int log2B,
-    int log2P, int fbits, uint64_t* __restrict__ srec, uint16_t* __restrict__ seg, const int64_t* __restrict__ ci) {
+    int log2P, int fbits, uint64_t* __restrict__ srec, uint16_t* __restrict__ seg, const int64_t* __restrict__ ci,
+    const uint32_t* __restrict__ srcAT, uint32_t* __restrict__ srecT) {
   if (ci[CI_GATE] == 0) return;
   const int w = blockIdx.x;
   if (w >= (int)ci[CI_NCHUNK]) return;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ int lb;
+  __shared__ int lb, lnv;
   __shared__ int wsum[NT / 64];
   constexpr int S = U * NT;
   static_assert(S == C1_CH, "refine chunk");
@@ -423,17 +480,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const int64_t kmin = ci[CI_KMINC];
   const int shift = 64 - log2P;
   uint64_t r[U];
-  uint32_t f[U], rank[U];
+  uint32_t f[U], rank[U], t32[U];
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const int j = threadIdx.x + u * NT;
-    r[u] = __builtin_nontemporal_load(srcA + lo + (j < len ? j : len - 1));
+    const int jj = j < len ? j : len - 1;
+    r[u] = __builtin_nontemporal_load(srcA + lo + jj);
+    if constexpr (WIDE) t32[u] = __builtin_nontemporal_load(srcAT + lo + jj);
   }
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const int j = threadIdx.x + u * NT;
-    const bool v = j < len && (uint32_t)r[u] != C1_SENT;
-    f[u] = (uint32_t)(key_hash(kmin + (int64_t)(r[u] >> 32)) >> shift) & (uint32_t)(F - 1);
+    const bool v = j < len && (WIDE ? t32[u] : (uint32_t)r[u]) != C1_SENT;
+    f[u] = WIDE ? (uint32_t)(r[u] >> shift) & (uint32_t)(F - 1)
+                : (uint32_t)(key_hash(kmin + (int64_t)(r[u] >> 32)) >> shift) & (uint32_t)(F - 1);
     rank[u] = v ? atomicAdd(&cnt[f[u]], 1u) : 0xFFFFFFFFu;
   }
   __syncthreads();
@@ -458,16 +518,27 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
       sbase[t] = before + incl - c;
       seg[(int64_t)w * (F + 1) + t] = (uint16_t)(before + incl - c);
     }
-    if (t == 0) seg[(int64_t)w * (F + 1) + F] = (uint16_t)tot;
-    if (t == 0) wsum[0] = (int)tot;  // read after the next barrier
+    if (t == 0) {
+      seg[(int64_t)w * (F + 1) + F] = (uint16_t)tot;
+      lnv = (int)tot;
+    }
   }
   __syncthreads();
-  const int nv = wsum[0];
+  const int nv = lnv;
 #pragma unroll
   for (int u = 0; u < U; u++)
     if (rank[u] != 0xFFFFFFFFu) stage[sbase[f[u]] + rank[u]] = r[u];
   __syncthreads();
   for (int j = threadIdx.x; j < nv; j += NT) srec[lo + j] = stage[j];
+  if constexpr (WIDE) {  // the ts words through the same LDS
+    __syncthreads();
+    uint32_t* stage32 = (uint32_t*)stage;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (rank[u] != 0xFFFFFFFFu) stage32[sbase[f[u]] + rank[u]] = t32[u];
+    __syncthreads();
+    for (int j = threadIdx.x; j < nv; j += NT) srecT[lo + j] = stage32[j];
+  }
 }
 
 // ------------------------------------------------------------------ k_c1_merge
@@ -517,7 +588,7 @@ __device__ __forceinline__ int c1_find_id(const KLDS ID* ids, ID id, uint32_t e,
 // Work item: p (work == nullptr: item w is partition w) or work[w] = p | sbits << 16 | sub << 20
 // (a retry with 2^sbits sub-passes).  LDS: ids ID[H + 64] | rt u32[H + 64] | ct u32[H + 64] |
 // list u16[H] | segment prefix u32[SEGMAX + 1] | segment bases i32[SEGMAX] (n < 2^31).
-template <int NT, int AU, class ID>
+template <int NT, int AU, class ID, bool WIDE>
 __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     C1Q q, const uint32_t* __restrict__ work, int64_t nwork, const int64_t* __restrict__ bb,
     const int* __restrict__ cstart, const uint16_t* __restrict__ seg, const uint64_t* __restrict__ srec, int first,
@@ -525,9 +596,11 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     const int64_t* __restrict__ cnt, unsigned long long* __restrict__ newcnt, uint8_t* __restrict__ fail,
     unsigned long long* __restrict__ need, int64_t close0, uint64_t* __restrict__ closed,
     unsigned long long* __restrict__ closed_n, const int64_t* __restrict__ ci, unsigned long long* __restrict__ hnew,
-    unsigned long long* __restrict__ hclosed, uint32_t* __restrict__ prn) {
+    unsigned long long* __restrict__ hclosed, uint32_t* __restrict__ prn, const uint32_t* __restrict__ srecT) {
   if (ci[CI_GATE] == 0) return;
-  if ((ci[CI_ID32] != 0) != (sizeof(ID) == 4)) return;  // the other identity width's instantiation
+  if ((ci[CI_WIDE] != 0) != WIDE) return;                            // the other record format's
+  if (!WIDE && (ci[CI_ID32] != 0) != (sizeof(ID) == 4)) return;     // the other identity width's
+  static_assert(!WIDE || sizeof(ID) == 8, "wide records use 64-bit identities");
   constexpr int NW = NT / 64;
   constexpr ID EMPTY = (ID)~(ID)0;
   const int log2H = q.log2H;
@@ -562,8 +635,17 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
   }
   // identity of a resident row (false: no record of this push can match it) and its sub-pass hash
   auto row_id = [&](const uint64_t* row, ID* id, uint32_t* h) -> bool {
-    const uint64_t krel = (uint64_t)((int64_t)row[0] - kmin);
     const int64_t wi = (int64_t)fast_udiv((uint64_t)row[1], q.fd) - wbase;
+    if constexpr (WIDE) {  // (key hash without its partition bits) << log2P | window
+      if (wi < 0 || wi > whi) {
+        *h = (uint32_t)(key_hash((int64_t)row[0]) >> 32) ^ (uint32_t)row[1];
+        return false;
+      }
+      *id = (ID)((key_hash((int64_t)row[0]) << q.log2P) | (uint64_t)wi);
+      *h = c1_hash<ID>(*id);
+      return true;
+    }
+    const uint64_t krel = (uint64_t)((int64_t)row[0] - kmin);
     if (krel > krange || wi < 0 || wi > whi) {
       *h = (uint32_t)(key_hash((int64_t)row[0]) >> 32) ^ (uint32_t)row[1];
       return false;
@@ -573,7 +655,15 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     *h = c1_hash<ID>(*id);
     return true;
   };
-  for (int64_t w = blockIdx.x; w < nwork; w += gridDim.x) {
+  // item w's descriptor, and its segments in LDS (prefix of their lengths, each one's base:
+  // record li = srec[sbs[s] + li]); called by the whole workgroup (barriers inside)
+  struct It {
+    uint32_t p;
+    int sbits, sub, nseg;
+    int64_t rn, nrow;
+    bool isel;
+  };
+  auto prep = [&](int64_t w, It& it) {
     uint32_t p;
     int sbits = 0, sub = 0;
     if (work) {
@@ -589,52 +679,92 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     const int cs = cstart[b];
     int nseg = cstart[b + 1] - cs;
     if (nseg < 0 || nseg > C1_SEGMAX) nseg = 0;  // (k_c1_check guarantees 0 <= nseg <= SEGMAX)
-    const int64_t nrow = cnt[p];
-    const bool isel = ((((const uint32_t*)sel)[p >> 2] >> (8 * (p & 3))) & 0xFFu) != 0;
-    // 0. the item's segments: prefix of their lengths, and each one's base (record = sbs[s] + li)
-    {
-      int len0 = 0, len1 = 0;
-      int64_t base0 = 0, base1 = 0;
-      const int k0 = threadIdx.x * 2;
-      if (k0 < nseg) {
-        const uint16_t* sg = seg + (int64_t)(cs + k0) * (F + 1) + f;
-        const int o0 = sg[0];
-        len0 = (int)sg[1] - o0;
-        base0 = bb[b] + (int64_t)k0 * C1_CH + o0;
-      }
-      if (k0 + 1 < nseg) {
-        const uint16_t* sg = seg + (int64_t)(cs + k0 + 1) * (F + 1) + f;
-        const int o0 = sg[0];
-        len1 = (int)sg[1] - o0;
-        base1 = bb[b] + (int64_t)(k0 + 1) * C1_CH + o0;
-      }
-      const int s = len0 + len1;
-      int incl = s;
-      for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
-      }
-      if (lane == 63) wsum[wave] = incl;
-      __syncthreads();
-      int before = 0;
-      for (int k = 0; k < NW; k++) before += k < wave ? wsum[k] : 0;
-      const int ex = before + incl - s;
-      if (k0 < nseg) {
-        spre[k0] = (uint32_t)ex;
-        sbs[k0] = (int32_t)(base0 - ex);
-      }
-      if (k0 + 1 < nseg) {
-        spre[k0 + 1] = (uint32_t)(ex + len0);
-        sbs[k0 + 1] = (int32_t)(base1 - (ex + len0));
-      }
-      if (k0 < nseg && k0 + 2 >= nseg) spre[nseg] = (uint32_t)(ex + s);  // the total
-      if (nseg == 0 && threadIdx.x == 0) spre[0] = 0u;
-      __syncthreads();
+    it.p = p;
+    it.sbits = sbits;
+    it.sub = sub;
+    it.nseg = nseg;
+    it.nrow = cnt[p];
+    it.isel = ((((const uint32_t*)sel)[p >> 2] >> (8 * (p & 3))) & 0xFFu) != 0;
+    int len0 = 0, len1 = 0;
+    int64_t base0 = 0, base1 = 0;
+    const int k0 = threadIdx.x * 2;
+    if (k0 < nseg) {
+      const uint16_t* sg = seg + (int64_t)(cs + k0) * (F + 1) + f;
+      const int o0 = sg[0];
+      len0 = (int)sg[1] - o0;
+      base0 = bb[b] + (int64_t)k0 * C1_CH + o0;
     }
-    const int64_t rn = spre[nseg];
+    if (k0 + 1 < nseg) {
+      const uint16_t* sg = seg + (int64_t)(cs + k0 + 1) * (F + 1) + f;
+      const int o0 = sg[0];
+      len1 = (int)sg[1] - o0;
+      base1 = bb[b] + (int64_t)(k0 + 1) * C1_CH + o0;
+    }
+    const int s = len0 + len1;
+    int incl = s;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int before = 0;
+    for (int k = 0; k < NW; k++) before += k < wave ? wsum[k] : 0;
+    const int ex = before + incl - s;
+    if (k0 < nseg) {
+      spre[k0] = (uint32_t)ex;
+      sbs[k0] = (int32_t)(base0 - ex);
+    }
+    if (k0 + 1 < nseg) {
+      spre[k0 + 1] = (uint32_t)(ex + len0);
+      sbs[k0 + 1] = (int32_t)(base1 - (ex + len0));
+    }
+    if (k0 < nseg && k0 + 2 >= nseg) spre[nseg] = (uint32_t)(ex + s);  // the total
+    if (nseg == 0 && threadIdx.x == 0) spre[0] = 0u;
+    __syncthreads();
+    it.rn = spre[nseg];
+  };
+  uint64_t ra[AU], rb[AU];
+  uint32_t ta[AU], tb[AU];  // WIDE: the records' ts words
+  // records li = l0 + thread + u NT of the item whose segments are in LDS (indices clamped to the
+  // last record: every load is unconditional, so the waits stay counted)
+  auto load = [&](uint64_t (&x)[AU], uint32_t (&tx)[AU], int64_t l0, int64_t rn, int nseg) {
+#pragma unroll
+    for (int u = 0; u < AU; u++) {
+      int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
+      li = li < rn ? li : rn - 1;
+      int lo = 0, hi = nseg;  // the last segment starting at or before li
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if ((int64_t)spre[mid] <= li) lo = mid;
+        else hi = mid;
+      }
+      const int64_t at = (int64_t)sbs[lo] + li;
+      x[u] = __builtin_nontemporal_load(srec + at);
+      if constexpr (WIDE) tx[u] = __builtin_nontemporal_load(srecT + at);
+    }
+  };
+  // the first item, and its first chunk in flight; each item prepares the next one (segments and
+  // first chunk) as soon as its own records are in the table, so those loads overlap its
+  // resident-row, count and write-out phases
+  It nx{};
+  if (blockIdx.x < nwork) {
+    prep(blockIdx.x, nx);
+    if (nx.rn > 0) load(ra, ta, 0, nx.rn, nx.nseg);
+  }
+  for (int64_t w = blockIdx.x; w < nwork; w += gridDim.x) {
+    const It it = nx;
+    const uint32_t p = it.p;
+    const int sbits = it.sbits, sub = it.sub, nseg = it.nseg;
+    const int64_t rn = it.rn, nrow = it.nrow;
+    const bool isel = it.isel;
+    const int64_t wn = w + gridDim.x;
     if (first && threadIdx.x == 0) prn[p] = (uint32_t)rn;
     if (rn == 0 && first) {  // untouched partition: nothing to rewrite
-      __syncthreads();
+      if (wn < nwork) {
+        prep(wn, nx);
+        if (nx.rn > 0) load(ra, ta, 0, nx.rn, nx.nseg);
+      }
       continue;
     }
     const uint64_t* src = (isel ? buf1 : buf0) + (uint64_t)p * q.cmax * q.sw;
@@ -679,23 +809,9 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       }
       __syncthreads();
     }
-    // 1. records → delta entries, two register sets (chunk c + 1 in flight while c is applied)
-    uint64_t ra[AU], rb[AU];
-    auto load = [&](uint64_t (&x)[AU], int64_t l0) {
-#pragma unroll
-      for (int u = 0; u < AU; u++) {
-        int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
-        li = li < rn ? li : rn - 1;
-        int lo = 0, hi = nseg;  // the last segment starting at or before li
-        while (hi - lo > 1) {
-          const int mid = (lo + hi) >> 1;
-          if ((int64_t)spre[mid] <= li) lo = mid;
-          else hi = mid;
-        }
-        x[u] = __builtin_nontemporal_load(srec + (int64_t)sbs[lo] + li);
-      }
-    };
-    auto apply = [&](const uint64_t (&xr)[AU], int64_t l0) {
+    // 1. records → delta entries, two register sets (chunk c + 1 in flight while c is applied;
+    //    chunk 0 was loaded with the item's segments)
+    auto apply = [&](const uint64_t (&xr)[AU], const uint32_t (&txr)[AU], int64_t l0) {
       ID id[AU];
       uint32_t e[AU], tr[AU];
       bool pend[AU], claimed[AU];
@@ -703,11 +819,12 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       for (int u = 0; u < AU; u++) {
         const int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
         const uint64_t v = xr[u];
-        const int32_t t32 = (int32_t)(uint32_t)v;
+        const int32_t t32 = WIDE ? (int32_t)txr[u] : (int32_t)(uint32_t)v;
         const uint64_t krel = v >> 32;
         const uint64_t wi = fast_udiv((uint64_t)(T0 + (int64_t)t32), q.fd) - (uint64_t)wbase;
         ID x;
-        if constexpr (sizeof(ID) == 4) x = (ID)(((uint32_t)krel << wbits) | (uint32_t)wi);
+        if constexpr (WIDE) x = (ID)((v << q.log2P) | wi);  // v = the key hash
+        else if constexpr (sizeof(ID) == 4) x = (ID)(((uint32_t)krel << wbits) | (uint32_t)wi);
         else x = (ID)((krel << 32) | wi);
         const uint32_t h = c1_hash<ID>(x);
         bool act = li < rn;
@@ -758,17 +875,22 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     };
     const int64_t nch = (rn + (int64_t)AU * NT - 1) / ((int64_t)AU * NT);
     if (rn > 0) {
-      load(ra, 0);
       for (int64_t c = 0; c < nch; c += 2) {
-        if (c + 1 < nch) load(rb, (c + 1) * AU * NT);
-        apply(ra, c * AU * NT);
+        if (c + 1 < nch) load(rb, tb, (c + 1) * AU * NT, rn, nseg);
+        apply(ra, ta, c * AU * NT);
         if (c + 1 >= nch || *(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
-        if (c + 2 < nch) load(ra, (c + 2) * AU * NT);
-        apply(rb, (c + 1) * AU * NT);
+        if (c + 2 < nch) load(ra, ta, (c + 2) * AU * NT, rn, nseg);
+        apply(rb, tb, (c + 1) * AU * NT);
         if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
       }
     }
     __syncthreads();
+    // the item's records are in the table (its segments are no longer read): the next item's
+    // segments and first chunk now
+    if (wn < nwork) {
+      prep(wn, nx);
+      if (nx.rn > 0) load(ra, ta, 0, nx.rn, nx.nseg);
+    }
     const int nl = nnew < H ? nnew : H;
     if (lovf || nnew > q.hmax) {  // more groups than the table takes: retried with 2x sub-passes
       if (threadIdx.x == 0) fail[p] |= 1;
@@ -894,16 +1016,19 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
         const uint64_t ri = cur + __popcll(bl & lt);
         uint64_t* dst = dst0 + ri * q.sw;
         const ID id = ids[e];
-        int64_t krel, wi;
-        if constexpr (sizeof(ID) == 4) {
-          krel = (int64_t)((uint32_t)id >> wbits);
+        int64_t key, wi;
+        if constexpr (WIDE) {  // the partition's bits above the identity's key-hash bits
+          wi = (int64_t)((uint64_t)id & (((uint64_t)1 << q.log2P) - 1));
+          key = key_of_hash(((uint64_t)p << (64 - q.log2P)) | ((uint64_t)id >> q.log2P));
+        } else if constexpr (sizeof(ID) == 4) {
+          key = kmin + (int64_t)((uint32_t)id >> wbits);
           wi = (int64_t)((uint32_t)id & wmask);
         } else {
-          krel = (int64_t)((uint64_t)id >> 32);
+          key = kmin + (int64_t)((uint64_t)id >> 32);
           wi = (int64_t)((uint64_t)id & 0xFFFFFFFFull);
         }
         const uint32_t c = ct[e];
-        *(longlong2*)dst = make_longlong2(kmin + krel, (wbase + wi) * q.adv);
+        *(longlong2*)dst = make_longlong2(key, (wbase + wi) * q.adv);
         *(longlong2*)(dst + 2) = make_longlong2(tmin + (int64_t)rv - 1, (int64_t)c);
         const bool now = !q.hv_active || c1q_having(q, c);
         nh += q.hv_active && now ? 1 : 0;
@@ -948,9 +1073,10 @@ bool c1_eligible(khip_agg* a, int64_t n) {
 // Returns KHIP_OK with *declined = true when k_c1_check declined the push (nothing persistent was
 // touched: the caller runs the general path on the same batch).
 khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
-                    const uint8_t* rv, int64_t* tot, bool* declined, const int64_t* st_at) {
+                    const uint8_t* rv, int64_t* tot, bool* declined, const int64_t* st_at, bool* retry_wide) {
   PartState& s = a->part;
   *declined = false;
+  *retry_wide = false;
   const int P = (int)s.P;
   const int fbits = s.log2P - s.log2P / 2;
   const int log2B = s.log2P - fbits;
@@ -1013,30 +1139,38 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
   hipLaunchKernelGGL(k_part_colprefix, dim3(ceil_div(B, 256), TC), dim3(256), 0, a->stream, s.c1hist.as<uint32_t>(), nT,
                      B, TC, s.scan_tmpB.as<int64_t>(), s.c1bb.as<int64_t>(), 1);
   ev_record_part(a, 1);
+  // wide records (key hash + u32 ts words) when the key range did not fit 32 bits last time: the
+  // host predicts the format, k_c1_check declines a compact push whose keys do not fit
+  const bool wide = s.c1_wide;
+  uint32_t* srecAT = (uint32_t*)(s.srecA.as<uint64_t>() + n + 1);  // WIDE ts words (12 B/record in all)
+  uint32_t* srecT = (uint32_t*)(s.srec.as<uint64_t>() + n + 1);
   // 3. records → buckets
   {
     constexpr int U = 8;
-    const size_t lds = stage_r8_lds_bytes(B, U * C1_NT);
-    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)k_c1_scatter<U, C1_NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((k_c1_scatter<U, C1_NT>), dim3(nT), dim3(C1_NT), lds, a->stream, keys, ts, kv, rv, n, nT, log2B,
+    auto sk = wide ? (st_at ? k_c1_scatter<U, C1_NT, true, true> : k_c1_scatter<U, C1_NT, true, false>)
+                   : (st_at ? k_c1_scatter<U, C1_NT, false, true> : k_c1_scatter<U, C1_NT, false, false>);
+    const size_t lds = stage_r8_lds_bytes(B, U * C1_NT) + (wide ? (size_t)U * C1_NT * 4 : 0);
+    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)sk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(sk, dim3(nT), dim3(C1_NT), lds, a->stream, keys, ts, kv, rv, n, nT, log2B,
                        s.c1hist.as<uint32_t>(), s.srecA.as<uint64_t>(), s.tilemax.as<int64_t>(), s.tpart.as<int64_t>(),
-                       ci, st_at);
+                       ci, st_at, srecAT);
     KHIP_TRY_HIP(hipGetLastError());
   }
   // 4. accept or decline
   hipLaunchKernelGGL(k_c1_check, dim3(1), dim3(1024), 0, a->stream, s.tilemax.as<int64_t>(), nS,
-                     a->desc.size_ms, adv, fd, a->grace, close0, s.res_fresh ? 1 : 0, log2B,
+                     a->desc.size_ms, adv, fd, a->grace, close0, s.res_fresh ? 1 : 0, log2B, s.log2P, wide ? 1 : 0,
                      s.c1bb.as<int64_t>(), cstart, ci, a->stream_time.as<int64_t>(), s.res.as<int64_t>(),
                      s.ctr.as<unsigned long long>(), s.closed_ctr.as<unsigned long long>(),
                      (unsigned long long)s.closed_n);
   // 5. refine: chunks → partition-sorted, segment table
   {
     constexpr int U = C1_CH / C1_NT;
+    auto rk = wide ? k_c1_refine<U, C1_NT, true> : k_c1_refine<U, C1_NT, false>;
     const size_t lds = (size_t)F * 8 + (size_t)C1_CH * 8;
-    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)k_c1_refine<U, C1_NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((k_c1_refine<U, C1_NT>), dim3((unsigned)nchunk_max), dim3(C1_NT), lds, a->stream,
+    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)rk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(rk, dim3((unsigned)nchunk_max), dim3(C1_NT), lds, a->stream,
                        s.srecA.as<uint64_t>(), s.c1bb.as<int64_t>(), cstart, log2B, s.log2P, fbits,
-                       s.srec.as<uint64_t>(), seg, ci);
+                       s.srec.as<uint64_t>(), seg, ci, (const uint32_t*)srecAT, srecT);
     KHIP_TRY_HIP(hipGetLastError());
   }
   ev_record_part(a, 2);
@@ -1074,10 +1208,13 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     const uint32_t* wk = (pass == 0 && !subs0) ? nullptr : s.work.as<uint32_t>();
     const int64_t nwork = (pass == 0 && !subs0) ? P : (int64_t)work.size();
     const int64_t grid = std::min<int64_t>(nwork, (int64_t)s.n_cu * knob("KHIP_MERGE_WG_PER_CU", 2));
-    // both identity widths are launched: the one k_c1_check did not choose exits at once
-    for (int idw = 0; idw < 2; idw++) {
-      auto mk = idw == 0 ? (au >= 8 ? k_c1_merge<512, 8, uint32_t> : (au >= 6 ? k_c1_merge<512, 6, uint32_t> : k_c1_merge<512, 4, uint32_t>))
-                         : k_c1_merge<512, 4, uint64_t>;
+    // compact records: both identity widths are launched, the one k_c1_check did not choose exits
+    // at once; wide records: 64-bit identities
+    for (int idw = wide ? 1 : 0; idw < 2; idw++) {
+      auto mk = wide ? k_c1_merge<512, 4, uint64_t, true>
+                     : (idw == 0 ? (au >= 8 ? k_c1_merge<512, 8, uint32_t, false>
+                                            : (au >= 6 ? k_c1_merge<512, 6, uint32_t, false> : k_c1_merge<512, 4, uint32_t, false>))
+                                 : k_c1_merge<512, 4, uint64_t, false>);
       const size_t lds = c1_merge_lds(log2H, idw == 0 ? 4 : 8);
       hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(mk, dim3(grid), dim3(512), lds, a->stream, cq, wk, nwork, s.c1bb.as<int64_t>(), cstart, seg,
@@ -1085,7 +1222,8 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
                          s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
                          s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
                          s.closed_ctr.as<unsigned long long>(), ci,
-                         s.hnew.as<unsigned long long>(), s.ctr.as<unsigned long long>() + 12, s.prn.as<uint32_t>());
+                         s.hnew.as<unsigned long long>(), s.ctr.as<unsigned long long>() + 12, s.prn.as<uint32_t>(),
+                         (const uint32_t*)srecT);
     }
     KHIP_TRY_HIP(hipGetLastError());
     const int nl = pass == 0 ? P : (int)plist.size();
@@ -1106,10 +1244,14 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     unsigned long long* c2 = s.pinfo.as<unsigned long long>() + 8;
     KHIP_TRY_HIP(hipMemcpyAsync(c2, s.ctr.p, 13 * 8, hipMemcpyDeviceToHost, a->stream));
     KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
-    if (pass == 0 && s.pinfo.as<int64_t>()[32 + CI_GATE] == 0) {  // declined: nothing was written
+    const int64_t* hci = s.pinfo.as<int64_t>() + 32;
+    if (pass == 0 && hci[CI_GATE] == 0) {  // declined: nothing was written
       *declined = true;
+      *retry_wide = hci[CI_REASON] == 1;  // only the record format was wrong
+      if (*retry_wide) s.c1_wide = true;
       return KHIP_OK;
     }
+    if (pass == 0 && wide && hci[CI_FITS]) s.c1_wide = false;  // compact records fit again next time
     added_total += (int64_t)c2[0];
     if (c2[1] == 0) break;
     if (pass > 24) return fail(KHIP_E_DEVICE, "partitioned aggregation could not place the batch");

@@ -3620,7 +3620,7 @@ khip_status part_reset(khip_agg* a) {
   s.hvalid = true;
   s.having_total = 0;
   s.last_c1 = false;
-  s.c1_skip = 0;
+  s.c1_skip = 0;  // (c1_wide, a prediction about the keys, stays)
   hipLaunchKernelGGL(k_part_reset, dim3(ceil_div(std::max<int64_t>(s.P, 16), 256)), dim3(256), 0, a->stream, s.P,
                      s.hcnt.as<unsigned long long>(), s.hnew.as<unsigned long long>(), s.cnt.as<int64_t>(),
                      s.newcnt.as<unsigned long long>(), s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>(),
@@ -3777,8 +3777,10 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   if (s.c1_skip > 0) {
     s.c1_skip--;
   } else if (c1_eligible(a, n)) {
-    bool declined = false;
-    KHIP_TRY(c1_push(a, n, keys, ts, kv, rv, tot, &declined, st_at));
+    bool declined = false, retry_wide = false;
+    KHIP_TRY(c1_push(a, n, keys, ts, kv, rv, tot, &declined, st_at, &retry_wide));
+    if (declined && retry_wide)  // the keys needed the wide records: this push again with them
+      KHIP_TRY(c1_push(a, n, keys, ts, kv, rv, tot, &declined, st_at, &retry_wide));
     if (a->profile) (declined ? a->times.c1_declined : a->times.c1_pushes)++;
     if (!declined) return KHIP_OK;
     s.c1_skip = 8;

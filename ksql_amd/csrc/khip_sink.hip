@@ -11,7 +11,10 @@
 // block-local scan plus carry), then k_sink_write writes each record at its offset.  Doubles print
 // through the Schubfach shortest-decimal algorithm (R. Giulietti 2020; java.lang.Double.toString
 // since JDK 19) with the 126-bit powers of ten of tools/gen_dtoa.py, so every digit is computed
-// exactly with 64-bit integer arithmetic.
+// exactly with 64-bit integer arithmetic.  Byte parity of DOUBLE text therefore assumes the
+// reference runs on JDK 19 or later: JDK <= 18's FloatingDecimal prints longer digit strings for
+// some values (tests/sink_ref.py lists them); on such a JVM the values still parse to the same
+// double, but the bytes differ (DESIGN.md §(c), unpinned).
 #include <algorithm>
 #include <cstring>
 #include <string>

@@ -62,8 +62,13 @@ C2_HAVING = {"agg": 0, "op": "GT", "value": 3}
 C2_N, C2_KEYS = 100_000_000, 10_000_000
 
 
-def _c2_oracle(orc, key_type, say):
+SPARSE_MULT = 0x5DEECE66D  # bench.py --sparse-keys: id -> (id * SPARSE_MULT) mod 2^53, a bijection
+
+
+def _c2_oracle(orc, key_type, say, sparse=False):
     card, ts = synth.possible_fraud(0, C2_N, C2_N, keys=C2_KEYS)
+    if sparse:
+        card = (card * SPARSE_MULT) & ((1 << 53) - 1)
     o = abi.ShardedOracleAgg(orc, abi.make_agg_desc(key_type=key_type, **C2_DESC), THREADS)
     if key_type == "UTF8":
         offs, kb = synth.card_utf8(card)
@@ -96,6 +101,30 @@ def test_c2_possible_fraud_full(prod, orc, say):
     assert n_having == int((exp["values"][0] > 3).sum())
     # the counts the round-1 bench line printed are the oracle's
     assert (exp["n"], n_having) == (22_054_808, 14_333_273)
+
+
+@pytest.mark.timeout(900)
+def test_c2_possible_fraud_sparse_full(prod, orc, say):
+    """bench.py --sparse-keys: the same records with the card ids spread over 2^53 (the COUNT(*)
+    pipeline's wide records: 64-bit key hashes)."""
+    card, ts = synth.possible_fraud(0, C2_N, C2_N, xp="torch", device="cuda", keys=C2_KEYS)
+    card = (card * SPARSE_MULT) & ((1 << 53) - 1)
+    desc = abi.make_agg_desc(key_type="INT64", capacity_hint=min(3 * C2_KEYS, 2 * C2_N), flags=abi.FLAG_PROFILE,
+                             **C2_DESC)
+    h = abi.AggHandle(prod, desc)
+    st = h.push(abi.DeviceBatch(ts, keys=card))
+    n_having = h.count_rows(C2_HAVING)
+    got = h.snapshot()
+    kt = h.kernel_times()
+    h.close()
+    del card, ts
+    say("C2 sparse product: %d groups, %d HAVING rows" % (got["n"], n_having))
+    ost, exp = _c2_oracle(orc, "INT64", say, sparse=True)
+    assert st == ost
+    assert_snap_equal(got, exp, desc)
+    assert n_having == int((exp["values"][0] > 3).sum())
+    assert (exp["n"], n_having) == (22_054_808, 14_333_273)  # a bijection of the keys: the same table shape
+    assert kt["c1_pushes"] == 1, kt
 
 
 @pytest.mark.timeout(900)
