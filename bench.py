@@ -1070,16 +1070,19 @@ def bench_repartition(args, lib, rank, world, local):
     phases = {"pack": 0.0, "exchange_unpack": 0.0, "aggregate": 0.0}
     state = {"timed": False, "m": 0}
 
+    # sized for every source row: khip_shuffle_pack's counts and scatter in one call
+    send_buf = torch.empty((n, rp.shuffle.row_words), dtype=torch.int64, device=torch.device("cuda", local))
+
     def step():
         t0 = time.perf_counter()
-        send, counts = rp.shuffle.pack(src)
+        send, counts = rp.shuffle.pack(src, send=send_buf)
         t1 = time.perf_counter()
         if world > 1:
             recv, rc = comm.alltoall(send, counts, rp.shuffle.row_words)
         else:
             recv, rc = send, counts
         m = int(sum(rc))
-        key, kts, cols, valid = rp.shuffle.unpack(recv, m)
+        key, kts, cols, valid = rp.shuffle.unpack(recv, m, key_as_col=True)  # region = the key
         t2 = time.perf_counter()
         h.reset()
         st = h.push(abi.DeviceBatch(kts, keys=key, cols=cols, col_valid=valid))

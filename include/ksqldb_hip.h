@@ -155,8 +155,10 @@ typedef struct khip_batch_stats {
  *   partition, C/util/KsqlConstants.java:42): each partition has its own stream time, set by the
  *   batch's `partition` column.  The GROUP BY key must determine the partition (co-partitioned
  *   input, as groupByKey requires), so the tasks' stores are disjoint and one table holds them.
- *   Closed windows are evicted by the smallest partition stream time; snapshot retention and
- *   EMIT FINAL are not offered in this domain (KHIP_E_UNSUPPORTED).
+ *   Closed windows are evicted by the smallest partition stream time; retention and EMIT FINAL
+ *   are not offered in this domain (KHIP_E_UNSUPPORTED for a RETENTION or EMIT FINAL
+ *   descriptor; snapshots, pull queries and row counts see every window, as tasks whose
+ *   retention covers the whole stream would).
  * SUPPLIED: one GLOBAL stream time over several handles (ranks): each row carries the stream
  *   time observed at it over the global arrival order (`stream_time` column), computed where the
  *   rows were read, before routing: rank r scans its contiguous arrival chunk with
@@ -513,8 +515,13 @@ khip_status khip_shuffle_pack(khip_shuffle* s, const khip_batch* in, uint64_t* s
 
 /* Packed rows (device) → columnar device arrays owned by the caller: key[n], ts[n],
  * col_data[c][n] (8-byte raw for every column type except INT32 = 4 bytes) and
- * col_valid[c] bitmaps ((n+7)/8 bytes; may be NULL).  The result is a khip_batch whose
- * records are the received rows in (source, arrival) order. */
+ * col_valid[c] bitmaps ((n+7)/8 bytes; may be NULL).  A NULL col_data[c] / col_valid[c]
+ * entry skips that column / bitmap (e.g. the GROUP BY column, which is the key and valid by
+ * construction).  The result is a khip_batch whose records are the received rows in
+ * (source, arrival) order.
+ * Capacity: khip_shuffle_pack's `send` may be sized for every batch row (n_rows x row words):
+ * then one call computes the counts and scatters (a smaller buffer returns KHIP_E_BUFFER with
+ * the counts, and the caller calls again). */
 khip_status khip_shuffle_unpack(khip_shuffle* s, const uint64_t* rows, int64_t n, int64_t* key,
                                 int64_t* ts, void* const* col_data, uint8_t* const* col_valid);
 

@@ -754,20 +754,25 @@ class ShuffleHandle:
         self.lib.check(st, "shuffle_pack")
         return send, list(counts)
 
-    def unpack(self, rows, n):
-        """Packed rows → (key, ts, cols, col_valid bitmaps) device tensors."""
+    def unpack(self, rows, n, key_as_col=False):
+        """Packed rows → (key, ts, cols, col_valid bitmaps) device tensors.  key_as_col: the
+        GROUP BY column is not written again (it IS the key: cols[key_col] is the key tensor,
+        valid by construction — pack drops NULL keys — so its bitmap is None)."""
         import torch
         dev = torch.device("cuda", self.device)
         key = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
         ts = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
         tdt = {0: torch.int32, 1: torch.int64, 2: torch.float64}
-        cols = [torch.empty(max(n, 1), dtype=tdt[t], device=dev) for t in self.col_types]
-        valid = [torch.empty(max((n + 7) // 8, 1), dtype=torch.uint8, device=dev) for _ in self.col_types]
-        cd = (C.c_void_p * len(cols))(*[c.data_ptr() for c in cols])
-        cv = (C.c_void_p * len(cols))(*[v.data_ptr() for v in valid])
+        kc = self.desc.key_col if key_as_col and self.col_types[self.desc.key_col] == TYPE["INT64"] else -1
+        cols = [key if c == kc else torch.empty(max(n, 1), dtype=tdt[t], device=dev)
+                for c, t in enumerate(self.col_types)]
+        valid = [None if c == kc else torch.empty(max((n + 7) // 8, 1), dtype=torch.uint8, device=dev)
+                 for c in range(len(self.col_types))]
+        cd = (C.c_void_p * len(cols))(*[None if c == kc else x.data_ptr() for c, x in enumerate(cols)])
+        cv = (C.c_void_p * len(cols))(*[None if v is None else v.data_ptr() for v in valid])
         self.lib.check(self.lib.shuffle_unpack(self.h, None if rows is None else rows.data_ptr(), n,
                                                key.data_ptr(), ts.data_ptr(), cd, cv), "shuffle_unpack")
-        return key[:n], ts[:n], [c[:n] for c in cols], [v[:(n + 7) // 8] for v in valid]
+        return key[:n], ts[:n], [c[:n] for c in cols], [None if v is None else v[:(n + 7) // 8] for v in valid]
 
     def close(self):
         if self.h:

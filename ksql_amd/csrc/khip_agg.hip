@@ -733,7 +733,9 @@ static khip_status plan_state(khip_agg* a) {
       continue;
     }
     const int c = s.arg_col;
-    if (w_cnt[c] < 0) w_cnt[c] = word++;
+    // the column's non-null count: COUNT(col), AVG's divisor, MIN/MAX's null test.  SUM alone needs
+    // none (SUM over only NULLs is 0, SumKudaf's initial value): its rows stay 32 bytes
+    if (s.kind != KHIP_AGG_SUM && w_cnt[c] < 0) w_cnt[c] = word++;
     if ((s.kind == KHIP_AGG_SUM || s.kind == KHIP_AGG_AVG) && w_sum[c] < 0) w_sum[c] = word++;
     if (s.kind == KHIP_AGG_MIN && w_min[c] < 0) w_min[c] = word++;
     if (s.kind == KHIP_AGG_MAX && w_max[c] < 0) w_max[c] = word++;
@@ -822,6 +824,9 @@ namespace khip {
 
 int64_t visible_from(const khip_agg* a) {
   if (!a->windowed || a->host_stream_time < 0) return INT64_MIN;
+  // PARTITION: every task's store would expire by its own stream time, which needs each row's
+  // partition; the handle keeps every window visible instead (retention is not offered there)
+  if (a->desc.time_domain == KHIP_TIME_PARTITION) return INT64_MIN;
   const int64_t adv = a->desc.advance_ms;
   const int64_t vf = a->host_stream_time / adv * adv - a->retention;  // the store's observed time - retention
   return vf > 0 ? vf : INT64_MIN;  // window starts are >= 0: nothing has expired yet
@@ -1466,6 +1471,11 @@ khip_status khip_agg_count_rows(khip_agg* a, const khip_having* h, int64_t* n) {
   clear_error();
   if (!a || !n) return fail(KHIP_E_INVALID, "null argument");
   DeviceGuard g(a->device);
+  // every row while none has expired: the group count every engine maintains, no table scan
+  if (!h && no_expired_live(a)) {
+    *n = a->occ;
+    return KHIP_OK;
+  }
   // the query's own HAVING: counts maintained by the aggregate kernel, no table scan
   if (h && a->engine == 0 && a->desc.has_having && h->agg_index == a->desc.having.agg_index &&
       h->op == a->desc.having.op && h->i64 == a->desc.having.i64 &&

@@ -34,6 +34,7 @@
 // + the table rows written (32 B per group) — against 16 + 24 + 16 + 8 + rows for the general
 // path (DESIGN.md §(d)).
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "khip_part.hpp"
@@ -44,6 +45,8 @@ constexpr int C1_TILE = 65536;   // records per hist / scatter tile (the general
 constexpr int C1_NT = 512;       // workgroup size of every kernel here
 constexpr int C1_CH = 8192;      // refine chunk (records), 16 per thread
 constexpr int C1_SEGMAX = 512;   // chunks of one bucket the merge can hold (4M records)
+constexpr int C1_SEGB = 7;       // the merge's segment lookup: one entry per 128 records of an item
+constexpr int C1_SEGOF = 512;    // ... for items of up to 64K records (larger ones binary-search)
 constexpr uint32_t C1_SENT = 0x80000000u;  // low word of a sentinel record (ts - T0 never is)
 
 // c1info (int64) slots
@@ -216,7 +219,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int wsum[NT / 64];
   __shared__ unsigned long long lc[4];
-  __shared__ long long lt[2][2];  // [step parity][max | min] of the step's accepted ts (LDS atomics)
+  __shared__ int lt[2][2];  // [step parity][max | min] of the step's accepted ts - T0 (LDS atomics)
   __shared__ int lfail;
   constexpr int S = U * NT;
   const int B = 1 << log2B;
@@ -229,8 +232,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   }
   if (threadIdx.x < 4) lc[threadIdx.x] = 0;
   if (threadIdx.x < 2) {
-    lt[threadIdx.x][0] = -1;
-    lt[threadIdx.x][1] = INT64_MAX;
+    lt[threadIdx.x][0] = INT32_MIN;
+    lt[threadIdx.x][1] = INT32_MAX;
   }
   if (threadIdx.x == 0) lfail = 0;
   const int64_t kmin = ci[CI_KMIN], T0 = ci[CI_T0];
@@ -238,7 +241,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const uint32_t bmask = (uint32_t)(B - 1);
   const int64_t base = t * C1_TILE;
   const int64_t end = base + C1_TILE < n ? base + C1_TILE : n;
-  int64_t c_acc = 0, c_nk = 0, c_nr = 0, c_bt = 0;
+  int c_acc = 0, c_nk = 0, c_nr = 0, c_bt = 0;  // < 2^16 per tile
   bool tfail = false;
   int64_t x[U], k[U];
   auto load_step = [&](int64_t i0, int64_t (&dx)[U], int64_t (&dk)[U]) {
@@ -250,15 +253,28 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
       dk[u] = keys[i];
     }
   };
+  // step st's (records [sb, sb + S)) ts range → stepstat; its LDS slots reset for step st + 2
+  auto publish = [&](int64_t sb, int st) {
+    const int64_t g = (sb / S) * 2;  // global step index
+    const int mx = lt[st & 1][0], mn = lt[st & 1][1];
+    stepstat[g] = mx == INT32_MIN ? -1 : T0 + mx;  // none accepted: -1, INT64_MAX
+    stepstat[g + 1] = mx == INT32_MIN ? INT64_MAX : T0 + mn;
+    lt[st & 1][0] = INT32_MIN;
+    lt[st & 1][1] = INT32_MAX;
+  };
   lds_barrier();
   int64_t s0 = base;
+  int st_last = -1;
   if (s0 < end) load_step(s0 + threadIdx.x, x, k);
   for (int st = 0; s0 < end; s0 += S, st++) {  // uniform across the block: barriers inside
+    st_last = st;
     const int64_t i0 = s0 + threadIdx.x;
     bool ok[U];
     uint32_t bin[U], t32[U];
     int64_t rec[U];
-    int64_t tmx = -1, tmn = INT64_MAX;  // this step's accepted ts range (k_c1_check's late test)
+    // this step's accepted ts range, relative to T0 (k_c1_check's late test): 32-bit, every
+    // accepted ts - T0 and stream time - T0 fits (else tfail declines the push)
+    int tmx = INT32_MIN, tmn = INT32_MAX;
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int64_t i = i0 + (int64_t)u * NT;
@@ -270,31 +286,41 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
       c_bt += ok[u] && kok && rok && x[u] < 0;
       c_acc += valid;
       const int64_t sx = ST ? st_at[ok[u] ? i : base] : x[u];  // ABI 5 domains: the given stream time
-      tmx = valid && sx > tmx ? sx : tmx;
-      tmn = valid && x[u] < tmn ? x[u] : tmn;
       const int64_t d = x[u] - T0;
       tfail |= valid && (d <= (int64_t)INT32_MIN || d > (int64_t)INT32_MAX);
+      if constexpr (ST) {
+        const int64_t ds = sx - T0;
+        tfail |= valid && (ds <= (int64_t)INT32_MIN || ds > (int64_t)INT32_MAX);
+        tmx = valid && (int)ds > tmx ? (int)ds : tmx;
+      } else {
+        tmx = valid && (int)d > tmx ? (int)d : tmx;
+      }
+      tmn = valid && (int)d < tmn ? (int)d : tmn;
       const uint64_t hk = key_hash(k[u]);
       bin[u] = stage_bin(hk, shift, bmask);
       t32[u] = valid ? (uint32_t)d : C1_SENT;
       rec[u] = WIDE ? (int64_t)hk : (int64_t)(((uint64_t)(k[u] - kmin) << 32) | (uint64_t)t32[u]);
     }
-    if (tmx >= 0) {
-      atomicMax(&lt[st & 1][0], (long long)tmx);
-      atomicMin(&lt[st & 1][1], (long long)tmn);
-    }
     // the next step's loads go into x / k (dead now) and stay in flight through this step's stage
     if (s0 + S < end) load_step(i0 + S, x, k);
     if constexpr (WIDE) stage_step_c1w<U, NT>(rec, t32, bin, ok, B, L, lt32, srec, srecT);
     else stage_step_r8<U, NT>(rec, bin, ok, B, L, srec);
-    if (threadIdx.x == 0) {  // the stage's barriers ordered every wave's lt atomics before this
-      const int64_t g = (s0 / S) * 2;  // global step index (records [g/2 * S, +S))
-      stepstat[g] = lt[st & 1][0];
-      stepstat[g + 1] = lt[st & 1][1];
-      lt[st & 1][0] = -1;  // for step st + 2 (its atomics come after step st + 1's barriers)
-      lt[st & 1][1] = INT64_MAX;
+    // the step's ts range: the wave's first (one LDS atomic per wave, not 64 to one address),
+    // after the stage so that its registers are free; published by thread 0 one step later
+    // (after the next stage's barriers), the last step's after the loop
+    for (int off = 32; off > 0; off >>= 1) {
+      const int a = __shfl_xor(tmx, off, 64), b = __shfl_xor(tmn, off, 64);
+      tmx = a > tmx ? a : tmx;
+      tmn = b < tmn ? b : tmn;
     }
+    if ((threadIdx.x & 63) == 0 && tmx != INT32_MIN) {
+      atomicMax(&lt[st & 1][0], tmx);
+      atomicMin(&lt[st & 1][1], tmn);
+    }
+    if (threadIdx.x == 0 && st > 0) publish(s0 - S, st - 1);
   }
+  __syncthreads();
+  if (threadIdx.x == 0 && s0 > base) publish(s0 - S, st_last);
   c_acc = wave_sum(c_acc);
   c_nk = wave_sum(c_nk);
   c_nr = wave_sum(c_nr);
@@ -329,7 +355,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 // merge and commit use.  Declined: nothing persistent is touched.
 __global__ __launch_bounds__(1024) void k_c1_check(
     const int64_t* __restrict__ stepstat, int64_t nS, int64_t size, int64_t adv, FastDiv fd, int64_t grace,
-    int64_t close0, int fresh, int log2B, int log2P, int wide, const int64_t* __restrict__ bb, int* __restrict__ cstart,
+    int64_t close0, int fresh, int log2B, int log2P, int wide, int ch, int kbmax, int pbits, const int64_t* __restrict__ bb,
+    int* __restrict__ cstart,
     int64_t* __restrict__ ci, int64_t* __restrict__ stream_time, int64_t* __restrict__ res,
     unsigned long long* __restrict__ ctr, unsigned long long* __restrict__ closed_ctr, unsigned long long closed_n) {
   __shared__ int64_t wmx[16];
@@ -376,7 +403,7 @@ __global__ __launch_bounds__(1024) void k_c1_check(
   }
   // chunks per bucket → cstart (exclusive prefix), largest bucket's chunk count
   const int B = 1 << log2B;
-  for (int b = threadIdx.x; b < B; b += 1024) lnch[b] = (int)((bb[b + 1] - bb[b] + C1_CH - 1) / C1_CH);
+  for (int b = threadIdx.x; b < B; b += 1024) lnch[b] = (int)((bb[b + 1] - bb[b] + ch - 1) / ch);
   __syncthreads();
   if (threadIdx.x) return;
   for (int w = 0; w < 16; w++) {
@@ -397,7 +424,7 @@ __global__ __launch_bounds__(1024) void k_c1_check(
   ci[CI_TFAIL] = 0;
   bool ok = !lslow && !tfail && mxc <= C1_SEGMAX && kmax >= kmin;
   const uint64_t krange = kmax >= kmin ? (uint64_t)kmax - (uint64_t)kmin : 0;
-  const bool fits = krange < 0xFFFFFFFFull;
+  const bool fits = krange < ((1ULL << kbmax) - 1);  // compact records: 32 key bits (value records 31)
   ci[CI_FITS] = fits ? 1 : 0;
   ci[CI_REASON] = ok && !wide && !fits ? 1 : 0;
   ok = ok && (wide || fits);
@@ -421,7 +448,7 @@ __global__ __launch_bounds__(1024) void k_c1_check(
   }
   const bool none = lo > hi;  // nothing live, nothing new
   if (none) lo = hi = 0;
-  ok = ok && (uint64_t)(hi - lo) < (wide ? ((uint64_t)1 << log2P) - 1 : 0xFFFFFFFEull);
+  ok = ok && (uint64_t)(hi - lo) < (wide ? ((uint64_t)1 << log2P) - 1 : (pbits ? 0x7FFFFFFEull : 0xFFFFFFFEull));
   const int wbits = bits_of((uint64_t)(hi - lo)), kbits = bits_of(krange);
   ci[CI_GATE] = ok ? 1 : 0;
   if (!ok) return;
@@ -430,7 +457,7 @@ __global__ __launch_bounds__(1024) void k_c1_check(
   ci[CI_WBITS] = wbits;
   ci[CI_KBITS] = kbits;
   ci[CI_KRANGE] = (int64_t)krange;
-  ci[CI_ID32] = !wide && kbits + wbits <= 31 ? 1 : 0;
+  ci[CI_ID32] = !wide && kbits + wbits + pbits <= 31 ? 1 : 0;  // pbits: the pane flag
   ci[CI_WIDE] = wide;
   ci[CI_TMIN] = gmx >= 0 ? gmn : 0;
   ci[CI_TMAX] = gmx;
@@ -546,6 +573,7 @@ struct C1Q {
   int32_t log2P, fbits, log2H, sw, hv_active, hv_op, hmax;
   int64_t size, adv, cmax, hv_i64;
   FastDiv fd;
+  FastDiv32 fd32;
   uint8_t* chg;  // changelog: per-row-slot emission flags (CHG_*), or null
 };
 
@@ -613,6 +641,9 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
   KLDS uint16_t* list = (KLDS uint16_t*)(ct + (H + 64));
   KLDS uint32_t* spre = (KLDS uint32_t*)((KLDS char*)list + (((size_t)H * 2 + 15) & ~(size_t)15));
   KLDS int32_t* sbs = (KLDS int32_t*)((KLDS char*)spre + (size_t)(C1_SEGMAX + 4) * 4);
+  KLDS int64_t* lbb = (KLDS int64_t*)(sbs + C1_SEGMAX);  // [B + 1] bucket bases
+  KLDS int32_t* lcs = (KLDS int32_t*)(lbb + (1 << (q.log2P - q.fbits)) + 1);  // [B + 1] chunk starts
+  KLDS uint16_t* segof = (KLDS uint16_t*)(lcs + (1 << (q.log2P - q.fbits)) + 2);  // [C1_SEGOF] block → segment
   __shared__ int lovf, nnew;
   __shared__ int wsum[NW];
   __shared__ unsigned long long lbase;
@@ -622,6 +653,9 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
   const int64_t kmin = ci[CI_KMINC];
   const uint64_t krange = (uint64_t)ci[CI_KRANGE];
   const int32_t tmin32 = (int32_t)(tmin - T0);
+  const int64_t wstart = wbase * q.adv;  // the first window's start: every record ts >= it
+  const bool r32 = ci[CI_TMAX] - wstart < ((int64_t)1 << 32);
+  const uint32_t tsh32 = (uint32_t)(T0 - wstart);  // ts - wstart = (uint32) t32 + tsh32
   const bool evict = close0 != INT64_MIN;
   const uint32_t dummy = (uint32_t)H + (uint32_t)lane;
   for (int i = threadIdx.x; i < H + 64; i += NT) {
@@ -656,14 +690,24 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     return true;
   };
   // item w's descriptor, and its segments in LDS (prefix of their lengths, each one's base:
-  // record li = srec[sbs[s] + li]); called by the whole workgroup (barriers inside)
+  // record li = srec[sbs[s] + li]).  fetch issues the global loads only (the raw words stay in
+  // registers, nothing waits on them): it runs for item w + grid at the start of item w, so the
+  // loads are in flight through w's records.  prep (the whole workgroup, barriers inside) turns
+  // them into the LDS segment table once w's records are in the table.
+  struct Pre {
+    uint32_t p;
+    int sbits, sub, nseg;
+    int64_t nrow, bb0;
+    uint32_t selw;
+    uint16_t s00, s01, s10, s11;  // seg[k0][f], seg[k0][f + 1], seg[k0 + 1][f], seg[k0 + 1][f + 1]
+  };
   struct It {
     uint32_t p;
     int sbits, sub, nseg;
     int64_t rn, nrow;
     bool isel;
   };
-  auto prep = [&](int64_t w, It& it) {
+  auto fetch = [&](int64_t w, Pre& r) {
     uint32_t p;
     int sbits = 0, sub = 0;
     if (work) {
@@ -676,30 +720,42 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     }
     p = __builtin_amdgcn_readfirstlane(p);
     const int b = (int)(p >> q.fbits), f = (int)(p & (uint32_t)(F - 1));
-    const int cs = cstart[b];
-    int nseg = cstart[b + 1] - cs;
+    const int cs = lcs[b];
+    int nseg = lcs[b + 1] - cs;
     if (nseg < 0 || nseg > C1_SEGMAX) nseg = 0;  // (k_c1_check guarantees 0 <= nseg <= SEGMAX)
-    it.p = p;
-    it.sbits = sbits;
-    it.sub = sub;
-    it.nseg = nseg;
-    it.nrow = cnt[p];
-    it.isel = ((((const uint32_t*)sel)[p >> 2] >> (8 * (p & 3))) & 0xFFu) != 0;
-    int len0 = 0, len1 = 0;
-    int64_t base0 = 0, base1 = 0;
+    r.p = p;
+    r.sbits = sbits;
+    r.sub = sub;
+    r.nseg = nseg;
+    r.nrow = cnt[p];
+    r.selw = ((const uint32_t*)sel)[p >> 2];
+    r.bb0 = lbb[b];
     const int k0 = threadIdx.x * 2;
+    r.s00 = r.s01 = r.s10 = r.s11 = 0;
     if (k0 < nseg) {
       const uint16_t* sg = seg + (int64_t)(cs + k0) * (F + 1) + f;
-      const int o0 = sg[0];
-      len0 = (int)sg[1] - o0;
-      base0 = bb[b] + (int64_t)k0 * C1_CH + o0;
+      r.s00 = sg[0];
+      r.s01 = sg[1];
     }
     if (k0 + 1 < nseg) {
       const uint16_t* sg = seg + (int64_t)(cs + k0 + 1) * (F + 1) + f;
-      const int o0 = sg[0];
-      len1 = (int)sg[1] - o0;
-      base1 = bb[b] + (int64_t)(k0 + 1) * C1_CH + o0;
+      r.s10 = sg[0];
+      r.s11 = sg[1];
     }
+  };
+  auto prep = [&](const Pre& r, It& it) {
+    const int nseg = r.nseg;
+    it.p = r.p;
+    it.sbits = r.sbits;
+    it.sub = r.sub;
+    it.nseg = nseg;
+    it.nrow = r.nrow;
+    it.isel = ((r.selw >> (8 * (r.p & 3))) & 0xFFu) != 0;
+    const int k0 = threadIdx.x * 2;
+    const int len0 = k0 < nseg ? (int)r.s01 - (int)r.s00 : 0;
+    const int len1 = k0 + 1 < nseg ? (int)r.s11 - (int)r.s10 : 0;
+    const int64_t base0 = r.bb0 + (int64_t)k0 * C1_CH + r.s00;
+    const int64_t base1 = r.bb0 + (int64_t)(k0 + 1) * C1_CH + r.s10;
     const int s = len0 + len1;
     int incl = s;
     for (int off = 1; off < 64; off <<= 1) {
@@ -707,7 +763,7 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       if (lane >= off) incl += y;
     }
     if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
+    lds_barrier();
     int before = 0;
     for (int k = 0; k < NW; k++) before += k < wave ? wsum[k] : 0;
     const int ex = before + incl - s;
@@ -719,9 +775,14 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       spre[k0 + 1] = (uint32_t)(ex + len0);
       sbs[k0 + 1] = (int32_t)(base1 - (ex + len0));
     }
+    // segment lookup: block j (records [128 j, 128 j + 128)) starts in segment segof[j]
+    for (int bj = (ex + 127) >> C1_SEGB, be = (ex + len0 + 127) >> C1_SEGB; bj < be && bj < C1_SEGOF; bj++)
+      segof[bj] = (uint16_t)k0;
+    for (int bj = (ex + len0 + 127) >> C1_SEGB, be = (ex + s + 127) >> C1_SEGB; bj < be && bj < C1_SEGOF; bj++)
+      segof[bj] = (uint16_t)(k0 + 1);
     if (k0 < nseg && k0 + 2 >= nseg) spre[nseg] = (uint32_t)(ex + s);  // the total
     if (nseg == 0 && threadIdx.x == 0) spre[0] = 0u;
-    __syncthreads();
+    lds_barrier();
     it.rn = spre[nseg];
   };
   uint64_t ra[AU], rb[AU];
@@ -733,24 +794,44 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     for (int u = 0; u < AU; u++) {
       int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
       li = li < rn ? li : rn - 1;
-      int lo = 0, hi = nseg;  // the last segment starting at or before li
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if ((int64_t)spre[mid] <= li) lo = mid;
-        else hi = mid;
+      int lo = 0;  // the last segment starting at or before li
+      if (rn <= ((int64_t)C1_SEGOF << C1_SEGB)) {  // from the block's segment, a step or two on
+        lo = segof[li >> C1_SEGB];
+        while (lo + 1 < nseg && (int64_t)spre[lo + 1] <= li) lo++;
+      } else {
+        int hi = nseg;
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if ((int64_t)spre[mid] <= li) lo = mid;
+          else hi = mid;
+        }
       }
       const int64_t at = (int64_t)sbs[lo] + li;
       x[u] = __builtin_nontemporal_load(srec + at);
       if constexpr (WIDE) tx[u] = __builtin_nontemporal_load(srecT + at);
     }
   };
-  // the first item, and its first chunk in flight; each item prepares the next one (segments and
-  // first chunk) as soon as its own records are in the table, so those loads overlap its
+  // the item's first two chunks (register sets A and B): a chunk is always two chunks ahead of
+  // the one being applied
+  auto load01 = [&](const It& x) {
+    if (x.rn > 0) load(ra, ta, 0, x.rn, x.nseg);
+    if (x.rn > (int64_t)AU * NT) load(rb, tb, (int64_t)AU * NT, x.rn, x.nseg);
+  };
+  // the bucket table (chunk starts, bucket bases) in LDS for every descriptor
+  for (int k = threadIdx.x; k <= (1 << (q.log2P - q.fbits)); k += NT) {
+    lcs[k] = cstart[k];
+    lbb[k] = bb[k];
+  }
+  lds_barrier();
+  // the first item, and its first chunks in flight; each item prepares the next one (segments and
+  // first chunks) as soon as its own records are in the table, so those loads overlap its
   // resident-row, count and write-out phases
+  Pre pr{};
   It nx{};
   if (blockIdx.x < nwork) {
-    prep(blockIdx.x, nx);
-    if (nx.rn > 0) load(ra, ta, 0, nx.rn, nx.nseg);
+    fetch(blockIdx.x, pr);
+    prep(pr, nx);
+    load01(nx);
   }
   for (int64_t w = blockIdx.x; w < nwork; w += gridDim.x) {
     const It it = nx;
@@ -759,11 +840,12 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     const int64_t rn = it.rn, nrow = it.nrow;
     const bool isel = it.isel;
     const int64_t wn = w + gridDim.x;
+    if (wn < nwork) fetch(wn, pr);
     if (first && threadIdx.x == 0) prn[p] = (uint32_t)rn;
     if (rn == 0 && first) {  // untouched partition: nothing to rewrite
       if (wn < nwork) {
-        prep(wn, nx);
-        if (nx.rn > 0) load(ra, ta, 0, nx.rn, nx.nseg);
+        prep(pr, nx);
+        load01(nx);
       }
       continue;
     }
@@ -784,14 +866,14 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
         if (lane >= off) incl += y;
       }
       if (lane == 63) wsum[wave] = incl;
-      __syncthreads();
+      lds_barrier();
       int before = 0, total = 0;
       for (int k = 0; k < NW; k++) {
         if (k < wave) before += wsum[k];
         total += wsum[k];
       }
       if (threadIdx.x == 0) lbase = total ? atomicAdd(closed_n, (unsigned long long)total) : 0ULL;
-      __syncthreads();
+      lds_barrier();
       uint64_t* dst = closed + (lbase + (uint64_t)(before + incl - ne)) * q.sw;
       for (int64_t r = threadIdx.x; r < nrow; r += NT) {
         const uint64_t* row = src + r * q.sw;
@@ -807,11 +889,13 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
         nh = (int)wave_sum(nh);
         if (lane == 0 && nh) atomicAdd(hclosed, (unsigned long long)nh);
       }
-      __syncthreads();
+      lds_barrier();
     }
     // 1. records → delta entries, two register sets (chunk c + 1 in flight while c is applied;
     //    chunk 0 was loaded with the item's segments)
-    auto apply = [&](const uint64_t (&xr)[AU], const uint32_t (&txr)[AU], int64_t l0) {
+    // R32: the push's record times relative to the first window's start fit 32 bits (a 32-bit
+    // window division instead of the 64-bit one)
+    auto apply = [&](const uint64_t (&xr)[AU], const uint32_t (&txr)[AU], int64_t l0, auto R32) {
       ID id[AU];
       uint32_t e[AU], tr[AU];
       bool pend[AU], claimed[AU];
@@ -821,7 +905,9 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
         const uint64_t v = xr[u];
         const int32_t t32 = WIDE ? (int32_t)txr[u] : (int32_t)(uint32_t)v;
         const uint64_t krel = v >> 32;
-        const uint64_t wi = fast_udiv((uint64_t)(T0 + (int64_t)t32), q.fd) - (uint64_t)wbase;
+        uint64_t wi;
+        if constexpr (decltype(R32)::value) wi = fast_udiv32((uint32_t)t32 + tsh32, q.fd32);
+        else wi = fast_udiv((uint64_t)(T0 + (int64_t)t32), q.fd) - (uint64_t)wbase;
         ID x;
         if constexpr (WIDE) x = (ID)((v << q.log2P) | wi);  // v = the key hash
         else if constexpr (sizeof(ID) == 4) x = (ID)(((uint32_t)krel << wbits) | (uint32_t)wi);
@@ -864,8 +950,12 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
           pend[u] = o2 != EMPTY && o2 != id[u];
         }
       }
+      {
+        bool cl[AU];
 #pragma unroll
-      for (int u = 0; u < AU; u++) mg_list_append(claimed[u] && id[u] != EMPTY, e[u], list, &nnew);
+        for (int u = 0; u < AU; u++) cl[u] = claimed[u] && id[u] != EMPTY;
+        mg_list_append_n<AU>(cl, e, list, &nnew);
+      }
 #pragma unroll
       for (int u = 0; u < AU; u++) {
         if (id[u] == EMPTY) continue;
@@ -874,22 +964,25 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       }
     };
     const int64_t nch = (rn + (int64_t)AU * NT - 1) / ((int64_t)AU * NT);
-    if (rn > 0) {
+    if (rn > 0) {  // chunks 0 and 1 are in flight (load01); each set is reloaded once applied
       for (int64_t c = 0; c < nch; c += 2) {
-        if (c + 1 < nch) load(rb, tb, (c + 1) * AU * NT, rn, nseg);
-        apply(ra, ta, c * AU * NT);
-        if (c + 1 >= nch || *(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
-        if (c + 2 < nch) load(ra, ta, (c + 2) * AU * NT, rn, nseg);
-        apply(rb, tb, (c + 1) * AU * NT);
+        if (r32) apply(ra, ta, c * AU * NT, std::true_type{});
+        else apply(ra, ta, c * AU * NT, std::false_type{});
         if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
+        if (c + 2 < nch) load(ra, ta, (c + 2) * AU * NT, rn, nseg);
+        if (c + 1 >= nch) break;
+        if (r32) apply(rb, tb, (c + 1) * AU * NT, std::true_type{});
+        else apply(rb, tb, (c + 1) * AU * NT, std::false_type{});
+        if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
+        if (c + 3 < nch) load(rb, tb, (c + 3) * AU * NT, rn, nseg);
       }
     }
-    __syncthreads();
+    lds_barrier();
     // the item's records are in the table (its segments are no longer read): the next item's
-    // segments and first chunk now
+    // segments and first chunks now
     if (wn < nwork) {
-      prep(wn, nx);
-      if (nx.rn > 0) load(ra, ta, 0, nx.rn, nx.nseg);
+      prep(pr, nx);
+      load01(nx);
     }
     const int nl = nnew < H ? nnew : H;
     if (lovf || nnew > q.hmax) {  // more groups than the table takes: retried with 2x sub-passes
@@ -900,12 +993,12 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
         rt[e] = 0u;
         ct[e] = 0u;
       }
-      __syncthreads();
+      lds_barrier();
       if (threadIdx.x == 0) {
         lovf = 0;
         nnew = 0;
       }
-      __syncthreads();
+      lds_barrier();
       continue;
     }
     // 2. resident rows: mark the delta entries they absorb; count live rows
@@ -923,7 +1016,7 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       }
       n_mine++;
     }
-    __syncthreads();
+    lds_barrier();
     // the wave's share of the list: new (unmatched) entries
     const int per = ((nl + NW - 1) / NW + 63) & ~63;
     const int lb0 = wave * per, lb1 = lb0 + per < nl ? lb0 + per : nl;
@@ -936,7 +1029,7 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     // 3. per-wave row counts → the partition's region range (one atomic per work item)
     const int wave_rows = (int)wave_sum(n_mine) + nnw;
     if (lane == 0) wsum[wave] = wave_rows;
-    __syncthreads();
+    lds_barrier();
     int wave_before = 0, total = 0;
     for (int k = 0; k < NW; k++) {
       if (k < wave) wave_before += wsum[k];
@@ -949,7 +1042,7 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
         newcnt[p] = (unsigned long long)total;
       }
     }
-    __syncthreads();
+    lds_barrier();
     if ((int64_t)(lbase + total) > q.cmax) {
       if (threadIdx.x == 0) {
         fail[p] |= 2;
@@ -961,9 +1054,9 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
         rt[e] = 0u;
         ct[e] = 0u;
       }
-      __syncthreads();
+      lds_barrier();
       if (threadIdx.x == 0) nnew = 0;
-      __syncthreads();
+      lds_barrier();
       continue;
     }
     // 4. write: resident rows (merged), then the wave's new entries (ballot ranks: consecutive rows)
@@ -1004,7 +1097,7 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       }
       cur += __popcll(bl);
     }
-    __syncthreads();  // every wave's resident rows have read their entries: the list walk clears them
+    lds_barrier();  // every wave's resident rows have read their entries: the list walk clears them
     const uint32_t wmask = wbits ? (1u << wbits) - 1u : 0u;
     for (int k = lb0; k < lb1; k += 64) {
       const int i = k + lane;
@@ -1045,17 +1138,981 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       nh = (int)wave_sum(nh);
       if (lane == 0 && nh) atomicAdd(&hnew[p], (unsigned long long)nh);
     }
-    __syncthreads();  // the table is clear for the next item
+    lds_barrier();  // the table is clear for the next item
     if (threadIdx.x == 0) nnew = 0;
+    lds_barrier();
+  }
+}
+
+// ------------------------------------------------------------------ value records (c1v)
+// The same pipeline for a query whose aggregates all read ONE argument column (COUNT(col), SUM,
+// AVG, MIN, MAX, with or without COUNT(*)): records are 16 bytes, {(key - kmin) << 32 |
+// (uint32)(ts - T0), bit 63 = the argument is not NULL; the argument's bits (INT sign-extended,
+// BIGINT, DOUBLE raw)}, so the key range must fit 31 bits.  HOPPING windows whose size is a
+// multiple of the advance go through panes: a record updates ONE entry, its pane (key, ts /
+// advance), and after the records every pane is folded into its F windows — F updates per pane,
+// not per record.  TUMBLING is the F = 1 case (the pane is the window).
+constexpr int C1V_CH = 4096;  // refine chunk of 16-byte records (64 KB of LDS stage)
+constexpr int C1V_MAXW = 8;   // row words (key, ws, rowtime + at most 5 state words)
+
+typedef uint64_t c1v_u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ ulonglong2 ld_nt2(const ulonglong2* p) {  // streaming 16-byte load
+  const c1v_u2 v = __builtin_nontemporal_load((const c1v_u2*)p);
+  return make_ulonglong2(v.x, v.y);
+}
+
+struct C1VCol {
+  const void* data;
+  const uint8_t* valid;
+  int32_t type;
+};
+
+// LDS stage of one scatter step of 16-byte records: per bin its output cursor, step count, staged
+// base and output position, then the staged records and their bins.
+template <int U, int NT>
+__device__ __forceinline__ void stage_step_v(const ulonglong2 (&rec)[U], const uint32_t (&bin)[U], const bool (&ok)[U],
+                                             int nb, uint32_t* cur, uint32_t* cnt, uint32_t* sbase, uint32_t* gpos,
+                                             ulonglong2* sp, uint16_t* sbin, int* wsum, ulonglong2* __restrict__ srec) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  uint32_t rank[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) rank[u] = ok[u] ? atomicAdd(&cnt[bin[u]], 1u) : 0u;
+  lds_barrier();
+  const uint32_t c = t < nb ? cnt[t] : 0u;
+  uint32_t incl = c;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) wsum[wave] = (int)incl;
+  lds_barrier();
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < NT / 64; k++) {
+    before += k < wave ? (uint32_t)wsum[k] : 0u;
+    tot += (uint32_t)wsum[k];
+  }
+  if (t < nb) {
+    sbase[t] = before + incl - c;
+    gpos[t] = cur[t];
+    cur[t] += c;
+    cnt[t] = 0u;
+  }
+  lds_barrier();
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    if (ok[u]) {
+      const uint32_t i = sbase[bin[u]] + rank[u];
+      sp[i] = rec[u];
+      sbin[i] = (uint16_t)bin[u];
+    }
+  lds_barrier();
+  for (uint32_t j = t; j < tot; j += NT) {
+    const uint32_t b = sbin[j];
+    srec[(uint64_t)gpos[b] + (j - sbase[b])] = sp[j];
+  }
+}
+
+__host__ __device__ constexpr size_t c1v_stage_lds(int nb, int S) {
+  return (size_t)nb * 16 + (size_t)S * 16 + ((size_t)S * 2 + 15) / 16 * 16;
+}
+
+// Records of tile t → their bucket's run, as k_c1_scatter, 16 bytes each.  HOP: the windows
+// applied per accepted record (windowsFor's count) for the batch statistics.
+template <int U, int NT, bool ST>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_c1v_scatter(
+    const int64_t* __restrict__ keys, const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
+    const uint8_t* __restrict__ rv, C1VCol vc, int64_t n, int64_t nT, int log2B, const uint32_t* __restrict__ offs,
+    ulonglong2* __restrict__ srec, int64_t* __restrict__ stepstat, int64_t* __restrict__ tpart,
+    int64_t* __restrict__ ci, const int64_t* __restrict__ st_at, int64_t size, int64_t adv, FastDiv fd, int hop) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int wsum[NT / 64];
+  __shared__ unsigned long long lc[5];
+  __shared__ int lt[2][2];
+  __shared__ int lfail;
+  constexpr int S = U * NT;
+  const int B = 1 << log2B;
+  const int64_t t = tile_of(blockIdx.x, nT);
+  uint32_t* cur = (uint32_t*)smem;
+  uint32_t* cnt = cur + B;
+  uint32_t* sbase = cnt + B;
+  uint32_t* gpos = sbase + B;
+  ulonglong2* sp = (ulonglong2*)(smem + (size_t)B * 16);
+  uint16_t* sbin = (uint16_t*)(sp + S);
+  for (int b = threadIdx.x; b < B; b += NT) {
+    cur[b] = offs[t * B + b];
+    cnt[b] = 0u;
+  }
+  if (threadIdx.x < 5) lc[threadIdx.x] = 0;
+  if (threadIdx.x < 2) {
+    lt[threadIdx.x][0] = INT32_MIN;
+    lt[threadIdx.x][1] = INT32_MAX;
+  }
+  if (threadIdx.x == 0) lfail = 0;
+  const int64_t kmin = ci[CI_KMIN], T0 = ci[CI_T0];
+  const int shift = log2B == 0 ? 64 : 64 - log2B;
+  const uint32_t bmask = (uint32_t)(B - 1);
+  const int64_t base = t * C1_TILE;
+  const int64_t end = base + C1_TILE < n ? base + C1_TILE : n;
+  int c_acc = 0, c_nk = 0, c_nr = 0, c_bt = 0, c_app = 0;
+  bool tfail = false;
+  int64_t x[U], k[U], v[U];
+  auto load_step = [&](int64_t i0) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      int64_t i = i0 + (int64_t)u * NT;
+      i = i < end ? i : end - 1;
+      x[u] = ts[i];
+      k[u] = keys[i];
+      v[u] = vc.type == KHIP_TYPE_INT32 ? (int64_t)((const int32_t*)vc.data)[i] : ((const int64_t*)vc.data)[i];
+    }
+  };
+  auto publish = [&](int64_t sb, int st) {
+    const int64_t g = (sb / S) * 2;
+    const int mx = lt[st & 1][0], mn = lt[st & 1][1];
+    stepstat[g] = mx == INT32_MIN ? -1 : T0 + mx;
+    stepstat[g + 1] = mx == INT32_MIN ? INT64_MAX : T0 + mn;
+    lt[st & 1][0] = INT32_MIN;
+    lt[st & 1][1] = INT32_MAX;
+  };
+  lds_barrier();
+  int64_t s0 = base;
+  int st_last = -1;
+  if (s0 < end) load_step(s0 + threadIdx.x);
+  for (int st = 0; s0 < end; s0 += S, st++) {
+    st_last = st;
+    const int64_t i0 = s0 + threadIdx.x;
+    bool ok[U];
+    uint32_t bin[U];
+    ulonglong2 rec[U];
+    int tmx = INT32_MIN, tmn = INT32_MAX;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t i = i0 + (int64_t)u * NT;
+      ok[u] = i < end;
+      const int64_t ii = ok[u] ? i : base;
+      const bool kok = bit_get(kv, ii), rok = bit_get(rv, ii), vok = bit_get(vc.valid, ii);
+      const bool valid = ok[u] && kok && rok && x[u] >= 0;
+      c_nk += ok[u] && !kok;
+      c_nr += ok[u] && kok && !rok;
+      c_bt += ok[u] && kok && rok && x[u] < 0;
+      c_acc += valid;
+      const int64_t d = x[u] - T0;
+      tfail |= valid && (d <= (int64_t)INT32_MIN || d > (int64_t)INT32_MAX);
+      if constexpr (ST) {
+        const int64_t ds = st_at[ii] - T0;
+        tfail |= valid && (ds <= (int64_t)INT32_MIN || ds > (int64_t)INT32_MAX);
+        tmx = valid && (int)ds > tmx ? (int)ds : tmx;
+      } else {
+        tmx = valid && (int)d > tmx ? (int)d : tmx;
+      }
+      tmn = valid && (int)d < tmn ? (int)d : tmn;
+      if (hop && valid) {  // windowsFor: starts in (ts - size, ts], multiples of adv, >= 0
+        const int64_t lo = x[u] - size + adv;
+        c_app += (int)((int64_t)fast_udiv((uint64_t)x[u], fd) - (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), fd) + 1);
+      }
+      bin[u] = stage_bin(key_hash(k[u]), shift, bmask);
+      const uint64_t w0 = ((uint64_t)(k[u] - kmin) << 32) | (uint64_t)(valid ? (uint32_t)d : C1_SENT);
+      rec[u] = make_ulonglong2(w0 | (vok ? (1ULL << 63) : 0ULL), (uint64_t)v[u]);
+    }
+    if (s0 + S < end) load_step(i0 + S);
+    stage_step_v<U, NT>(rec, bin, ok, B, cur, cnt, sbase, gpos, sp, sbin, wsum, srec);
+    for (int off = 32; off > 0; off >>= 1) {
+      const int a = __shfl_xor(tmx, off, 64), b = __shfl_xor(tmn, off, 64);
+      tmx = a > tmx ? a : tmx;
+      tmn = b < tmn ? b : tmn;
+    }
+    if ((threadIdx.x & 63) == 0 && tmx != INT32_MIN) {
+      atomicMax(&lt[st & 1][0], tmx);
+      atomicMin(&lt[st & 1][1], tmn);
+    }
+    if (threadIdx.x == 0 && st > 0) publish(s0 - S, st - 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && s0 > base) publish(s0 - S, st_last);
+  c_acc = wave_sum(c_acc);
+  c_nk = wave_sum(c_nk);
+  c_nr = wave_sum(c_nr);
+  c_bt = wave_sum(c_bt);
+  c_app = wave_sum(c_app);
+  if ((threadIdx.x & 63) == 0) {
+    if (c_acc) atomicAdd(&lc[0], (unsigned long long)c_acc);
+    if (c_nk) atomicAdd(&lc[1], (unsigned long long)c_nk);
+    if (c_nr) atomicAdd(&lc[2], (unsigned long long)c_nr);
+    if (c_bt) atomicAdd(&lc[3], (unsigned long long)c_bt);
+    if (c_app) atomicAdd(&lc[4], (unsigned long long)c_app);
+  }
+  if (tfail) lfail = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t* tp = tpart + t * T_NPART;
+    tp[T_ACCEPTED] = (int64_t)lc[0];
+    tp[T_NULL_KEY] = (int64_t)lc[1];
+    tp[T_NULL_ROW] = (int64_t)lc[2];
+    tp[T_BAD_TS] = (int64_t)lc[3];
+    tp[T_APPLIED] = hop ? (int64_t)lc[4] : (int64_t)lc[0];  // none late (checked)
+    tp[T_LATE] = 0;
+    if (lfail) atomicOr((unsigned long long*)&ci[CI_TFAIL], 1ULL);
+  }
+}
+
+// Chunk w of its bucket (C1V_CH records): sentinels dropped, counting-sorted by partition,
+// written back in place; the segment table as k_c1_refine's.
+template <int U, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_c1v_refine(
+    const ulonglong2* __restrict__ srcA, const int64_t* __restrict__ bb, const int* __restrict__ cstart, int log2B,
+    int log2P, int fbits, ulonglong2* __restrict__ srec, uint16_t* __restrict__ seg, const int64_t* __restrict__ ci) {
+  if (ci[CI_GATE] == 0) return;
+  const int w = blockIdx.x;
+  if (w >= (int)ci[CI_NCHUNK]) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int lb, lnv;
+  __shared__ int wsum[NT / 64];
+  constexpr int CH = U * NT;
+  static_assert(CH == C1V_CH, "refine chunk");
+  const int F = 1 << fbits, B = 1 << log2B;
+  uint32_t* cnt = (uint32_t*)smem;
+  uint32_t* sbase = cnt + F;
+  ulonglong2* stage = (ulonglong2*)(smem + (((size_t)F * 8 + 15) & ~(size_t)15));
+  for (int f = threadIdx.x; f < F; f += NT) cnt[f] = 0u;
+  if (threadIdx.x == 0) lb = -1;
+  __syncthreads();
+  for (int b = threadIdx.x; b < B; b += NT)
+    if (cstart[b] <= w && w < cstart[b + 1]) lb = b;
+  __syncthreads();
+  const int b = lb;
+  if (b < 0) return;
+  const int64_t lo = bb[b] + (int64_t)(w - cstart[b]) * CH;
+  const int64_t bend = bb[b + 1];
+  const int len = (int)(bend - lo < CH ? bend - lo : CH);
+  const int64_t kmin = ci[CI_KMINC];
+  const int shift = 64 - log2P;
+  ulonglong2 r[U];
+  uint32_t f[U], rank[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const int j = threadIdx.x + u * NT;
+    const int jj = j < len ? j : len - 1;
+    r[u] = ld_nt2(srcA + lo + jj);
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const int j = threadIdx.x + u * NT;
+    const bool v = j < len && (uint32_t)r[u].x != C1_SENT;
+    f[u] = (uint32_t)(key_hash(kmin + (int64_t)((r[u].x >> 32) & 0x7FFFFFFFull)) >> shift) & (uint32_t)(F - 1);
+    rank[u] = v ? atomicAdd(&cnt[f[u]], 1u) : 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  {
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t c = t < F ? cnt[t] : 0u;
+    uint32_t incl = c;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = (int)incl;
     __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < NT / 64; k++) {
+      before += k < wave ? (uint32_t)wsum[k] : 0u;
+      tot += (uint32_t)wsum[k];
+    }
+    if (t < F) {
+      sbase[t] = before + incl - c;
+      seg[(int64_t)w * (F + 1) + t] = (uint16_t)(before + incl - c);
+    }
+    if (t == 0) {
+      seg[(int64_t)w * (F + 1) + F] = (uint16_t)tot;
+      lnv = (int)tot;
+    }
+  }
+  __syncthreads();
+  const int nv = lnv;
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    if (rank[u] != 0xFFFFFFFFu) stage[sbase[f[u]] + rank[u]] = r[u];
+  __syncthreads();
+  for (int j = threadIdx.x; j < nv; j += NT) srec[lo + j] = stage[j];
+}
+
+// Merge parameters of the value pipeline.  LDS: ids ID[H + 64] | 8-byte planes (sum, min, max,
+// present ones) | u32 planes (row time, COUNT(*), non-null count) | list u16[H] | segment prefix
+// | segment bases | bucket bases | chunk starts (byte offsets below, from c1v_layout).
+struct C1VQ {
+  int32_t log2P, fbits, log2H, sw, hmax, f64, fan;
+  int32_t off_sum, off_min, off_max, off_rt, off_star, off_cnt, off_list, off_spre;
+  int32_t word_op[C1V_MAXW];  // kind of the update op writing row word k (-1: none)
+  int64_t size, adv, cmax;
+  FastDiv fd;
+  FastDiv32 fd32;
+  uint64_t init[C1V_MAXW];
+  HavingDev having;
+  uint8_t* chg;
+};
+
+template <class T>
+__device__ __forceinline__ KLDS T* c1v_plane(char* smem, int off) {
+  return (KLDS T*)((KLDS char*)smem + off);
+}
+
+// Row words r[3..sw) of a (key, window) combined with delta entry e (resident row, or the initial
+// words for a new one).  Unrolled over the words: r stays in registers.
+__device__ __forceinline__ void c1v_combine(const C1VQ& q, char* smem, int e, uint64_t (&r)[C1V_MAXW]) {
+#pragma unroll
+  for (int k = 3; k < C1V_MAXW; k++) {
+    if (k >= q.sw) break;
+    switch (q.word_op[k]) {
+      case OP_INC: r[k] += c1v_plane<uint32_t>(smem, q.off_star)[e]; break;
+      case OP_INC_VALID: r[k] += c1v_plane<uint32_t>(smem, q.off_cnt)[e]; break;
+      case OP_ADD_I64: r[k] += c1v_plane<uint64_t>(smem, q.off_sum)[e]; break;
+      case OP_ADD_F64: {
+        double a, b = c1v_plane<double>(smem, q.off_sum)[e];
+        __builtin_memcpy(&a, &r[k], 8);
+        a += b;
+        __builtin_memcpy(&r[k], &a, 8);
+        break;
+      }
+      case OP_MIN: {
+        const int64_t m = c1v_plane<int64_t>(smem, q.off_min)[e];
+        if (m < (int64_t)r[k]) r[k] = (uint64_t)m;
+        break;
+      }
+      case OP_MAX: {
+        const int64_t m = c1v_plane<int64_t>(smem, q.off_max)[e];
+        if (m > (int64_t)r[k]) r[k] = (uint64_t)m;
+        break;
+      }
+      default: break;
+    }
+  }
+}
+
+__device__ __forceinline__ bool c1v_having(const C1VQ& q, const uint64_t (&r)[C1V_MAXW]) {
+  if (!q.having.active) return true;
+  uint64_t val = 0, cntw = 0;
+#pragma unroll
+  for (int k = 3; k < C1V_MAXW; k++) {
+    if (k == q.having.a.w_val) val = r[k];
+    if (k == q.having.a.w_cnt) cntw = r[k];
+  }
+  return having_ok_words(val, cntw, q.having);
+}
+
+// Clear delta entry e for the next item.
+__device__ __forceinline__ void c1v_clear(const C1VQ& q, char* smem, int e) {
+  c1v_plane<uint32_t>(smem, q.off_rt)[e] = 0u;
+  if (q.off_star >= 0) c1v_plane<uint32_t>(smem, q.off_star)[e] = 0u;
+  if (q.off_cnt >= 0) c1v_plane<uint32_t>(smem, q.off_cnt)[e] = 0u;
+  if (q.off_sum >= 0) c1v_plane<uint64_t>(smem, q.off_sum)[e] = 0ULL;
+  if (q.off_min >= 0) c1v_plane<int64_t>(smem, q.off_min)[e] = INT64_MAX;
+  if (q.off_max >= 0) c1v_plane<int64_t>(smem, q.off_max)[e] = INT64_MIN;
+}
+
+// One (record or pane) contribution into delta entry e: row time, then the update planes.
+// vok: the argument is not NULL; val: its bits (a pane: cs / cv its counts, val its sum, mn / mx
+// its order keys).
+__device__ __forceinline__ void c1v_add(const C1VQ& q, char* smem, uint32_t e, uint32_t tr, uint32_t cs, uint32_t cv,
+                                        uint64_t sum, int64_t mn, int64_t mx) {
+  __hip_atomic_fetch_max(&c1v_plane<uint32_t>(smem, q.off_rt)[e], tr, WG_RLX);
+  if (q.off_star >= 0 && cs) __hip_atomic_fetch_add(&c1v_plane<uint32_t>(smem, q.off_star)[e], cs, WG_RLX);
+  if (cv) {
+    if (q.off_cnt >= 0) __hip_atomic_fetch_add(&c1v_plane<uint32_t>(smem, q.off_cnt)[e], cv, WG_RLX);
+    if (q.off_sum >= 0) {
+      if (q.f64) {
+        double d;
+        __builtin_memcpy(&d, &sum, 8);
+        __hip_atomic_fetch_add(&c1v_plane<double>(smem, q.off_sum)[e], d, WG_RLX);
+      } else {
+        __hip_atomic_fetch_add(&c1v_plane<uint64_t>(smem, q.off_sum)[e], sum, WG_RLX);
+      }
+    }
+    if (q.off_min >= 0) __hip_atomic_fetch_min(&c1v_plane<int64_t>(smem, q.off_min)[e], mn, WG_RLX);
+    if (q.off_max >= 0) __hip_atomic_fetch_max(&c1v_plane<int64_t>(smem, q.off_max)[e], mx, WG_RLX);
+  }
+}
+
+// identity of (krel, relative window or pane index): u32 krel << (wbits + PB) | pane << wbits | wi,
+// u64 krel << 32 | pane << 31 | wi
+template <class ID, bool PANES>
+__device__ __forceinline__ ID c1v_id(uint64_t krel, uint64_t wi, bool pane, int wbits) {
+  if constexpr (sizeof(ID) == 4)
+    return (ID)(((uint32_t)krel << (wbits + (PANES ? 1 : 0))) | ((PANES && pane) ? (1u << wbits) : 0u) | (uint32_t)wi);
+  else
+    return (ID)((krel << 32) | ((PANES && pane) ? (1ULL << 31) : 0ULL) | wi);
+}
+template <class ID, bool PANES>
+__device__ __forceinline__ bool c1v_is_pane(ID id, int wbits) {
+  if constexpr (!PANES) return false;
+  if constexpr (sizeof(ID) == 4) return ((uint32_t)id >> wbits) & 1u;
+  else return ((uint64_t)id >> 31) & 1ULL;
+}
+
+// WPE: waves per SIMD the register budget allows (4: <= 128 VGPRs, two workgroups per CU; 2:
+// <= 256, one)
+template <int NT, int AU, class ID, bool PANES, int WPE>
+__global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
+    const C1VQ* __restrict__ qp, const uint32_t* __restrict__ work, int64_t nwork, const int64_t* __restrict__ bb,
+    const int* __restrict__ cstart, const uint16_t* __restrict__ seg, const ulonglong2* __restrict__ srec, int first,
+    uint64_t* __restrict__ buf0, uint64_t* __restrict__ buf1, const uint8_t* __restrict__ sel,
+    const int64_t* __restrict__ cnt, unsigned long long* __restrict__ newcnt, uint8_t* __restrict__ fail,
+    unsigned long long* __restrict__ need, int64_t close0, uint64_t* __restrict__ closed,
+    unsigned long long* __restrict__ closed_n, const int64_t* __restrict__ ci, unsigned long long* __restrict__ hnew,
+    unsigned long long* __restrict__ hclosed, uint32_t* __restrict__ prn) {
+  if (ci[CI_GATE] == 0) return;
+  if ((ci[CI_ID32] != 0) != (sizeof(ID) == 4)) return;  // the other identity width's
+  const C1VQ& q = *qp;  // in device memory: its fields are loaded where used (SGPR pressure)
+  constexpr int NW = NT / 64;
+  constexpr ID EMPTY = (ID)~(ID)0;
+  const int log2H = q.log2H;
+  const int H = 1 << log2H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  KLDS ID* ids = (KLDS ID*)(KLDS char*)smem;
+  KLDS uint32_t* rt = c1v_plane<uint32_t>(smem, q.off_rt);
+  KLDS uint16_t* list = c1v_plane<uint16_t>(smem, q.off_list);
+  KLDS uint32_t* spre = c1v_plane<uint32_t>(smem, q.off_spre);
+  KLDS int32_t* sbs = (KLDS int32_t*)(spre + (C1_SEGMAX + 4));
+  KLDS int64_t* lbb = (KLDS int64_t*)(sbs + C1_SEGMAX);
+  KLDS int32_t* lcs = (KLDS int32_t*)(lbb + (1 << (q.log2P - q.fbits)) + 1);
+  KLDS uint16_t* segof = (KLDS uint16_t*)(lcs + (1 << (q.log2P - q.fbits)) + 2);
+  __shared__ int lovf, nnew;
+  __shared__ int wsum[NW];
+  __shared__ unsigned long long lbase;
+  const int F = 1 << q.fbits;
+  const int64_t wbase = ci[CI_WBASE], whi = ci[CI_WHI], T0 = ci[CI_T0], tmin = ci[CI_TMIN];
+  const int wbits = (int)ci[CI_WBITS];
+  const int64_t kmin = ci[CI_KMINC];
+  const uint64_t krange = (uint64_t)ci[CI_KRANGE];
+  const int32_t tmin32 = (int32_t)(tmin - T0);
+  const int64_t wstart = wbase * q.adv;
+  const bool r32 = ci[CI_TMAX] - wstart < ((int64_t)1 << 32);
+  const uint32_t tsh32 = (uint32_t)(T0 - wstart);
+  const bool evict = close0 != INT64_MIN;
+  const uint32_t dummy = (uint32_t)H + (uint32_t)lane;
+  for (int i = threadIdx.x; i < H + 64; i += NT) {
+    ids[i] = EMPTY;
+    c1v_clear(q, smem, i);
+  }
+  if (threadIdx.x == 0) {
+    lovf = 0;
+    nnew = 0;
+  }
+  // identity and slot hash of a resident row (false: no record of this push can match it).
+  // Sub-passes split a partition by KEY (subh): a pane and its windows stay in one sub-pass.
+  auto row_id = [&](const uint64_t* row, ID* id, uint32_t* h) -> bool {
+    const int64_t wi = (int64_t)fast_udiv((uint64_t)row[1], q.fd) - wbase;
+    const uint64_t krel = (uint64_t)((int64_t)row[0] - kmin);
+    if (krel > krange || wi < 0 || wi > whi) return false;
+    *id = c1v_id<ID, PANES>(krel, (uint64_t)wi, false, wbits);
+    *h = c1_hash<ID>(*id);
+    return true;
+  };
+  auto subh = [&](int64_t key) -> uint32_t { return (uint32_t)(uint64_t)(key - kmin) * 0x9E3779B1u; };
+  // probe for id from its home slot; claims it if absent (listed); -1 when the table is full
+  auto claim = [&](ID id, bool act) -> int {
+    uint32_t e = act ? c1_hash<ID>(id) >> (32 - log2H) : dummy;
+    ID old = EMPTY;
+    __hip_atomic_compare_exchange_strong(&ids[e], &old, act ? id : EMPTY, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+    bool got = act && old == EMPTY;
+    bool pend = act && old != EMPTY && old != id;
+    for (int probes = 1;; probes++) {
+      if (!__ballot(pend)) break;
+      if (probes >= H) {  // the table is full: the item is retried (claimed entries stay listed)
+        if (pend) {
+          lovf = 1;
+          act = false;
+        }
+        pend = false;
+        break;
+      }
+      if (pend) {
+        e = (e + 1) & (uint32_t)(H - 1);
+        ID o2 = EMPTY;
+        __hip_atomic_compare_exchange_strong(&ids[e], &o2, id, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        got = o2 == EMPTY;
+        pend = o2 != EMPTY && o2 != id;
+      }
+    }
+    mg_list_append(act && got, e, list, &nnew);
+    return act ? (int)e : -1;
+  };
+  struct Pre {
+    uint32_t p;
+    int sbits, sub, nseg;
+    int64_t nrow, bb0;
+    uint32_t selw;
+    uint16_t s00, s01, s10, s11;
+  };
+  struct It {
+    uint32_t p;
+    int sbits, sub, nseg;
+    int64_t rn, nrow;
+    bool isel;
+  };
+  auto fetch = [&](int64_t w, Pre& r) {
+    uint32_t p;
+    int sbits = 0, sub = 0;
+    if (work) {
+      const uint32_t x = work[w];
+      p = x & 0xFFFFu;
+      sbits = (x >> 16) & 0xF;
+      sub = (int)(x >> 20);
+    } else {
+      p = (uint32_t)w;
+    }
+    p = __builtin_amdgcn_readfirstlane(p);
+    const int b = (int)(p >> q.fbits), f = (int)(p & (uint32_t)(F - 1));
+    const int cs = lcs[b];
+    int nseg = lcs[b + 1] - cs;
+    if (nseg < 0 || nseg > C1_SEGMAX) nseg = 0;
+    r.p = p;
+    r.sbits = sbits;
+    r.sub = sub;
+    r.nseg = nseg;
+    r.nrow = cnt[p];
+    r.selw = ((const uint32_t*)sel)[p >> 2];
+    r.bb0 = lbb[b];
+    const int k0 = threadIdx.x * 2;
+    r.s00 = r.s01 = r.s10 = r.s11 = 0;
+    if (k0 < nseg) {
+      const uint16_t* sg = seg + (int64_t)(cs + k0) * (F + 1) + f;
+      r.s00 = sg[0];
+      r.s01 = sg[1];
+    }
+    if (k0 + 1 < nseg) {
+      const uint16_t* sg = seg + (int64_t)(cs + k0 + 1) * (F + 1) + f;
+      r.s10 = sg[0];
+      r.s11 = sg[1];
+    }
+  };
+  auto prep = [&](const Pre& r, It& it) {
+    const int nseg = r.nseg;
+    it.p = r.p;
+    it.sbits = r.sbits;
+    it.sub = r.sub;
+    it.nseg = nseg;
+    it.nrow = r.nrow;
+    it.isel = ((r.selw >> (8 * (r.p & 3))) & 0xFFu) != 0;
+    const int k0 = threadIdx.x * 2;
+    const int len0 = k0 < nseg ? (int)r.s01 - (int)r.s00 : 0;
+    const int len1 = k0 + 1 < nseg ? (int)r.s11 - (int)r.s10 : 0;
+    const int64_t base0 = r.bb0 + (int64_t)k0 * C1V_CH + r.s00;
+    const int64_t base1 = r.bb0 + (int64_t)(k0 + 1) * C1V_CH + r.s10;
+    const int s = len0 + len1;
+    int incl = s;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    lds_barrier();
+    int before = 0;
+    for (int k = 0; k < NW; k++) before += k < wave ? wsum[k] : 0;
+    const int ex = before + incl - s;
+    if (k0 < nseg) {
+      spre[k0] = (uint32_t)ex;
+      sbs[k0] = (int32_t)(base0 - ex);
+    }
+    if (k0 + 1 < nseg) {
+      spre[k0 + 1] = (uint32_t)(ex + len0);
+      sbs[k0 + 1] = (int32_t)(base1 - (ex + len0));
+    }
+    // segment lookup: block j (records [128 j, 128 j + 128)) starts in segment segof[j]
+    for (int bj = (ex + 127) >> C1_SEGB, be = (ex + len0 + 127) >> C1_SEGB; bj < be && bj < C1_SEGOF; bj++)
+      segof[bj] = (uint16_t)k0;
+    for (int bj = (ex + len0 + 127) >> C1_SEGB, be = (ex + s + 127) >> C1_SEGB; bj < be && bj < C1_SEGOF; bj++)
+      segof[bj] = (uint16_t)(k0 + 1);
+    if (k0 < nseg && k0 + 2 >= nseg) spre[nseg] = (uint32_t)(ex + s);
+    if (nseg == 0 && threadIdx.x == 0) spre[0] = 0u;
+    lds_barrier();
+    it.rn = spre[nseg];
+  };
+  ulonglong2 ra[AU], rb[AU];
+  auto load = [&](ulonglong2 (&x)[AU], int64_t l0, int64_t rn, int nseg) {
+#pragma unroll
+    for (int u = 0; u < AU; u++) {
+      int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
+      li = li < rn ? li : rn - 1;
+      int lo = 0;  // the last segment starting at or before li
+      if (rn <= ((int64_t)C1_SEGOF << C1_SEGB)) {  // from the block's segment, a step or two on
+        lo = segof[li >> C1_SEGB];
+        while (lo + 1 < nseg && (int64_t)spre[lo + 1] <= li) lo++;
+      } else {
+        int hi = nseg;
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if ((int64_t)spre[mid] <= li) lo = mid;
+          else hi = mid;
+        }
+      }
+      x[u] = ld_nt2(srec + ((int64_t)sbs[lo] + li));
+    }
+  };
+  auto load01 = [&](const It& x) {
+    if (x.rn > 0) load(ra, 0, x.rn, x.nseg);
+    if (x.rn > (int64_t)AU * NT) load(rb, (int64_t)AU * NT, x.rn, x.nseg);
+  };
+  for (int k = threadIdx.x; k <= (1 << (q.log2P - q.fbits)); k += NT) {
+    lcs[k] = cstart[k];
+    lbb[k] = bb[k];
+  }
+  lds_barrier();
+  Pre pr{};
+  It nx{};
+  if (blockIdx.x < nwork) {
+    fetch(blockIdx.x, pr);
+    prep(pr, nx);
+    load01(nx);
+  }
+  for (int64_t w = blockIdx.x; w < nwork; w += gridDim.x) {
+    const It it = nx;
+    const uint32_t p = it.p;
+    const int sbits = it.sbits, sub = it.sub, nseg = it.nseg;
+    const int64_t rn = it.rn, nrow = it.nrow;
+    const bool isel = it.isel;
+    const int64_t wn = w + gridDim.x;
+    if (wn < nwork) fetch(wn, pr);
+    if (first && threadIdx.x == 0) prn[p] = (uint32_t)rn;
+    if (rn == 0 && first) {
+      if (wn < nwork) {
+        prep(pr, nx);
+        load01(nx);
+      }
+      continue;
+    }
+    const uint64_t* src = (isel ? buf1 : buf0) + (uint64_t)p * q.cmax * q.sw;
+    // 0. closed resident rows → closed store (pass 0 only)
+    if (evict && first) {
+      int ne = 0, nh = 0;
+      for (int64_t r = threadIdx.x; r < nrow; r += NT) {
+        const uint64_t* row = src + r * q.sw;
+        ne += ((int64_t)row[1] + q.size <= close0) && (sbits == 0 || (int)c1_sub(subh((int64_t)row[0]), sbits) == sub);
+      }
+      int incl = ne;
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+      }
+      if (lane == 63) wsum[wave] = incl;
+      lds_barrier();
+      int before = 0, total = 0;
+      for (int k = 0; k < NW; k++) {
+        if (k < wave) before += wsum[k];
+        total += wsum[k];
+      }
+      if (threadIdx.x == 0) lbase = total ? atomicAdd(closed_n, (unsigned long long)total) : 0ULL;
+      lds_barrier();
+      uint64_t* dst = closed + (lbase + (uint64_t)(before + incl - ne)) * q.sw;
+      for (int64_t r = threadIdx.x; r < nrow; r += NT) {
+        const uint64_t* row = src + r * q.sw;
+        if (!((int64_t)row[1] + q.size <= close0) || !(sbits == 0 || (int)c1_sub(subh((int64_t)row[0]), sbits) == sub))
+          continue;
+        for (int k = 0; k < q.sw; k++) dst[k] = row[k];
+        dst += q.sw;
+        nh += having_ok(row, q.having) ? 1 : 0;
+      }
+      if (q.having.active) {
+        nh = (int)wave_sum(nh);
+        if (lane == 0 && nh) atomicAdd(hclosed, (unsigned long long)nh);
+      }
+      lds_barrier();
+    }
+    // 1. records → their pane (window) entries: the AU identities' CASes back to back, then the
+    //    collisions probe on together (as k_c1_merge)
+    auto apply = [&](const ulonglong2 (&xr)[AU], int64_t l0, auto R32) {
+      ID id[AU];
+      uint32_t e[AU];
+      bool pend[AU], claimed[AU];
+#pragma unroll
+      for (int u = 0; u < AU; u++) {
+        const int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
+        const uint64_t w0 = xr[u].x;
+        const uint64_t krel = (w0 >> 32) & 0x7FFFFFFFull;
+        uint64_t wi;
+        if constexpr (decltype(R32)::value) wi = fast_udiv32((uint32_t)w0 + tsh32, q.fd32);
+        else wi = fast_udiv((uint64_t)(T0 + (int64_t)(int32_t)(uint32_t)w0), q.fd) - (uint64_t)wbase;
+        const ID x = c1v_id<ID, PANES>(krel, wi, PANES, wbits);
+        bool act = li < rn;
+        if (sbits) act = act && (int)c1_sub((uint32_t)krel * 0x9E3779B1u, sbits) == sub;
+        id[u] = act ? x : EMPTY;
+        e[u] = act ? c1_hash<ID>(x) >> (32 - log2H) : dummy;
+      }
+#pragma unroll
+      for (int u = 0; u < AU; u++) {
+        ID old = EMPTY;
+        __hip_atomic_compare_exchange_strong(&ids[e[u]], &old, id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        claimed[u] = id[u] != EMPTY && old == EMPTY;
+        pend[u] = old != EMPTY && old != id[u];
+      }
+      for (int probes = 1;; probes++) {
+        bool anyp = false;
+#pragma unroll
+        for (int u = 0; u < AU; u++) anyp |= pend[u];
+        if (!__ballot(anyp)) break;
+        if (probes >= H) {
+          lovf = 1;
+#pragma unroll
+          for (int u = 0; u < AU; u++)
+            if (pend[u]) id[u] = EMPTY;
+          break;
+        }
+#pragma unroll
+        for (int u = 0; u < AU; u++) {
+          if (!pend[u]) continue;
+          e[u] = (e[u] + 1) & (uint32_t)(H - 1);
+          ID o2 = EMPTY;
+          __hip_atomic_compare_exchange_strong(&ids[e[u]], &o2, id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+          claimed[u] = o2 == EMPTY;
+          pend[u] = o2 != EMPTY && o2 != id[u];
+        }
+      }
+      {
+        bool cl[AU];
+#pragma unroll
+        for (int u = 0; u < AU; u++) cl[u] = claimed[u] && id[u] != EMPTY;
+        mg_list_append_n<AU>(cl, e, list, &nnew);
+      }
+#pragma unroll
+      for (int u = 0; u < AU; u++) {
+        if (id[u] == EMPTY) continue;
+        const uint64_t w0 = xr[u].x;
+        int64_t ok_ = (int64_t)xr[u].y;
+        if (q.f64 && (q.off_min >= 0 || q.off_max >= 0)) {
+          double d;
+          __builtin_memcpy(&d, &xr[u].y, 8);
+          ok_ = f64_order_key(d);
+        }
+        c1v_add(q, smem, e[u], (uint32_t)((int32_t)(uint32_t)w0 - tmin32) + 1u, 1u, (w0 >> 63) ? 1u : 0u, xr[u].y, ok_,
+                ok_);
+      }
+    };
+    const int64_t nch = (rn + (int64_t)AU * NT - 1) / ((int64_t)AU * NT);
+    if (rn > 0) {
+      for (int64_t c = 0; c < nch; c += 2) {
+        if (r32) apply(ra, c * AU * NT, std::true_type{});
+        else apply(ra, c * AU * NT, std::false_type{});
+        if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
+        if (c + 2 < nch) load(ra, (c + 2) * AU * NT, rn, nseg);
+        if (c + 1 >= nch) break;
+        if (r32) apply(rb, (c + 1) * AU * NT, std::true_type{});
+        else apply(rb, (c + 1) * AU * NT, std::false_type{});
+        if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
+        if (c + 3 < nch) load(rb, (c + 3) * AU * NT, rn, nseg);
+      }
+    }
+    lds_barrier();
+    if (wn < nwork) {
+      prep(pr, nx);
+      load01(nx);
+    }
+    // 1b. panes → their windows (the window entries are claimed as a record's would be)
+    if (PANES && q.fan > 1 && !lovf && nnew <= q.hmax) {
+      const int nn0 = nnew;
+      lds_barrier();  // every thread has read nn0 before the fold lists windows
+      for (int i0 = 0; i0 < nn0; i0 += NT) {  // uniform trip count: claim's ballots converge
+        const int li = i0 + threadIdx.x;
+        const int pe = li < nn0 ? (int)list[li] : 0;
+        const ID pid = li < nn0 ? ids[pe] : EMPTY;
+        const bool isp = li < nn0 && pid != EMPTY && c1v_is_pane<ID, PANES>(pid, wbits);
+        uint64_t krel, pw;
+        if constexpr (sizeof(ID) == 4) {
+          krel = (uint64_t)((uint32_t)pid >> (wbits + 1));
+          pw = (uint64_t)((uint32_t)pid & ((1u << wbits) - 1u));
+          if (wbits == 0) pw = 0;
+        } else {
+          krel = (uint64_t)pid >> 32;
+          pw = (uint64_t)pid & 0x7FFFFFFFull;
+        }
+        const uint32_t prt = isp ? rt[pe] : 0u;
+        const uint32_t pcs = isp && q.off_star >= 0 ? c1v_plane<uint32_t>(smem, q.off_star)[pe] : 0u;
+        const uint32_t pcv = isp && q.off_cnt >= 0 ? c1v_plane<uint32_t>(smem, q.off_cnt)[pe] : (isp ? 1u : 0u);
+        const uint64_t psum = isp && q.off_sum >= 0 ? c1v_plane<uint64_t>(smem, q.off_sum)[pe] : 0ULL;
+        const int64_t pmn = isp && q.off_min >= 0 ? c1v_plane<int64_t>(smem, q.off_min)[pe] : INT64_MAX;
+        const int64_t pmx = isp && q.off_max >= 0 ? c1v_plane<int64_t>(smem, q.off_max)[pe] : INT64_MIN;
+        for (int j = 0; j < q.fan; j++) {
+          // window pw - j (its start is >= 0: windowsFor never returns a negative start)
+          const bool act = isp && (int64_t)pw - j + wbase >= 0 && (int64_t)pw - j >= 0;
+          const int e = claim(c1v_id<ID, PANES>(krel, pw - (uint64_t)j, false, wbits), act);
+          if (e >= 0) c1v_add(q, smem, (uint32_t)e, prt, pcs, pcv, psum, pmn, pmx);
+        }
+      }
+      lds_barrier();
+    }
+    const int nl = nnew < H ? nnew : H;
+    if (lovf || nnew > q.hmax) {
+      if (threadIdx.x == 0) fail[p] |= 1;
+      for (int i = threadIdx.x; i < nl; i += NT) {
+        const uint32_t e = list[i];
+        ids[e] = EMPTY;
+        c1v_clear(q, smem, (int)e);
+      }
+      lds_barrier();
+      if (threadIdx.x == 0) {
+        lovf = 0;
+        nnew = 0;
+      }
+      lds_barrier();
+      continue;
+    }
+    // 2. resident rows: mark the delta entries they absorb; count live rows
+    int n_mine = 0;
+    for (int64_t r = threadIdx.x; r < nrow; r += NT) {
+      const uint64_t* row = src + r * q.sw;
+      if (evict && (int64_t)row[1] + q.size <= close0) continue;
+      if (sbits && (int)c1_sub(subh((int64_t)row[0]), sbits) != sub) continue;
+      ID id;
+      uint32_t h;
+      const bool has = row_id(row, &id, &h);
+      if (has) {
+        const int e = c1_find_id<ID>(ids, id, h >> (32 - log2H), H);
+        if (e >= 0) rt[e] |= RT_MATCHED;
+      }
+      n_mine++;
+    }
+    lds_barrier();
+    const int per = ((nl + NW - 1) / NW + 63) & ~63;
+    const int lb0 = wave * per, lb1 = lb0 + per < nl ? lb0 + per : nl;
+    int nnw = 0;
+    for (int k = lb0; k < lb1; k += 64) {
+      const int i = k + lane;
+      const uint32_t e = i < lb1 ? list[i] : dummy;
+      const bool isnew = i < lb1 && !(rt[e] & RT_MATCHED) && !c1v_is_pane<ID, PANES>(ids[e], wbits);
+      nnw += (int)__popcll(__ballot(isnew));
+    }
+    // 3. the partition's region range
+    const int wave_rows = (int)wave_sum(n_mine) + nnw;
+    if (lane == 0) wsum[wave] = wave_rows;
+    lds_barrier();
+    int wave_before = 0, total = 0;
+    for (int k = 0; k < NW; k++) {
+      if (k < wave) wave_before += wsum[k];
+      total += wsum[k];
+    }
+    if (threadIdx.x == 0) {
+      if (work) lbase = total ? atomicAdd(&newcnt[p], (unsigned long long)total) : 0ULL;
+      else {
+        lbase = 0;
+        newcnt[p] = (unsigned long long)total;
+      }
+    }
+    lds_barrier();
+    if ((int64_t)(lbase + total) > q.cmax) {
+      if (threadIdx.x == 0) {
+        fail[p] |= 2;
+        atomicMax(need, (unsigned long long)(lbase + total));
+      }
+      for (int i = threadIdx.x; i < nl; i += NT) {
+        const uint32_t e = list[i];
+        ids[e] = EMPTY;
+        c1v_clear(q, smem, (int)e);
+      }
+      lds_barrier();
+      if (threadIdx.x == 0) nnew = 0;
+      lds_barrier();
+      continue;
+    }
+    // 4. write: resident rows (merged), then the wave's new window entries
+    uint64_t* dst0 = (isel ? buf0 : buf1) + (uint64_t)p * q.cmax * q.sw;
+    uint64_t cur = lbase + (uint64_t)wave_before;
+    const uint64_t lt = (1ULL << lane) - 1;
+    int nh = 0;
+    for (int64_t r0 = wave * 64; r0 < nrow; r0 += NT) {
+      const int64_t r = r0 + lane;
+      const uint64_t* row = src + (r < nrow ? r : 0) * q.sw;
+      bool live = r < nrow && !(evict && (int64_t)row[1] + q.size <= close0);
+      int e = -1;
+      if (live) {
+        if (sbits) live = (int)c1_sub(subh((int64_t)row[0]), sbits) == sub;
+        ID id;
+        uint32_t h;
+        if (live && row_id(row, &id, &h)) e = c1_find_id<ID>(ids, id, h >> (32 - log2H), H);
+      }
+      const uint64_t bl = __ballot(live);
+      if (live) {
+        const uint64_t ri = cur + __popcll(bl & lt);
+        uint64_t* dst = dst0 + ri * q.sw;
+        uint64_t rr[C1V_MAXW];
+#pragma unroll
+        for (int k = 0; k < C1V_MAXW; k++) rr[k] = k < q.sw ? row[k] : 0ULL;
+        const bool was = c1v_having(q, rr);
+        if (e >= 0) {
+          const int64_t t = tmin + (int64_t)(rt[e] & ~RT_MATCHED) - 1;
+          rr[2] = t > (int64_t)rr[2] ? (uint64_t)t : rr[2];
+          c1v_combine(q, smem, e, rr);
+        }
+#pragma unroll
+        for (int k = 0; k < C1V_MAXW; k++)
+          if (k < q.sw) dst[k] = rr[k];
+        const bool now = c1v_having(q, rr);
+        nh += q.having.active && now ? 1 : 0;
+        if (q.chg)
+          q.chg[(uint64_t)p * q.cmax + ri] =
+              e >= 0 ? (uint8_t)(CHG_TOUCHED | (was ? CHG_OLD : 0) | (now ? CHG_NEW : 0)) : (uint8_t)0;
+      }
+      cur += __popcll(bl);
+    }
+    lds_barrier();
+    const uint32_t wmask = wbits ? (1u << wbits) - 1u : 0u;
+    for (int k = lb0; k < lb1; k += 64) {
+      const int i = k + lane;
+      const uint32_t e = i < lb1 ? list[i] : dummy;
+      const uint32_t rv = rt[e];
+      const ID id = ids[e];
+      const bool isnew = i < lb1 && !(rv & RT_MATCHED) && !c1v_is_pane<ID, PANES>(id, wbits);
+      const uint64_t bl = __ballot(isnew);
+      if (isnew) {
+        const uint64_t ri = cur + __popcll(bl & lt);
+        uint64_t* dst = dst0 + ri * q.sw;
+        int64_t key, wi;
+        if constexpr (sizeof(ID) == 4) {
+          key = kmin + (int64_t)((uint32_t)id >> (wbits + (PANES ? 1 : 0)));
+          wi = (int64_t)((uint32_t)id & wmask);
+        } else {
+          key = kmin + (int64_t)((uint64_t)id >> 32);
+          wi = (int64_t)((uint64_t)id & 0x7FFFFFFFull);
+        }
+        uint64_t rr[C1V_MAXW];
+#pragma unroll
+        for (int k = 0; k < C1V_MAXW; k++) rr[k] = q.init[k];
+        rr[0] = (uint64_t)key;
+        rr[1] = (uint64_t)((wbase + wi) * q.adv);
+        rr[2] = (uint64_t)(tmin + (int64_t)rv - 1);
+        c1v_combine(q, smem, (int)e, rr);
+#pragma unroll
+        for (int k = 0; k < C1V_MAXW; k++)
+          if (k < q.sw) dst[k] = rr[k];
+        const bool now = c1v_having(q, rr);
+        nh += q.having.active && now ? 1 : 0;
+        if (q.chg) q.chg[(uint64_t)p * q.cmax + ri] = (uint8_t)(CHG_TOUCHED | (now ? CHG_NEW : 0));
+      }
+      if (i < lb1) {
+        ids[e] = EMPTY;
+        c1v_clear(q, smem, (int)e);
+      }
+      cur += __popcll(bl);
+    }
+    if (q.having.active) {
+      nh = (int)wave_sum(nh);
+      if (lane == 0 && nh) atomicAdd(&hnew[p], (unsigned long long)nh);
+    }
+    lds_barrier();
+    if (threadIdx.x == 0) nnew = 0;
+    lds_barrier();
   }
 }
 
 // ------------------------------------------------------------------ host side
 
-size_t c1_merge_lds(int log2H, int idw) {
-  const size_t H = (size_t)1 << log2H;
-  return (H + 64) * (idw + 8) + ((H * 2 + 15) & ~(size_t)15) + (C1_SEGMAX + 4) * 4 + C1_SEGMAX * 4;
+size_t c1_merge_lds(int log2H, int idw, int log2B) {
+  const size_t H = (size_t)1 << log2H, B = (size_t)1 << log2B;
+  return (H + 64) * (idw + 8) + ((H * 2 + 15) & ~(size_t)15) + (C1_SEGMAX + 4) * 4 + C1_SEGMAX * 4 + (B + 1) * 12 + 8 +
+         C1_SEGOF * 2;
 }
 
 // Whether the COUNT(*) pipeline may take this push (the general path's c1 plan, TUMBLING, the
@@ -1070,25 +2127,98 @@ bool c1_eligible(khip_agg* a, int64_t n) {
          knob("KHIP_MERGE", 1) != 0 && knob("KHIP_SCATTER2", 1) != 0;
 }
 
+// The value pipeline: every update op reads one argument column (or is COUNT(*)), at most one op
+// per kind, TUMBLING or HOPPING with size a multiple of the advance (panes), rows of <= 8 words.
+// *col = the argument column.
+bool c1v_eligible(khip_agg* a, int64_t n, int* col) {
+  PartState& s = a->part;
+  if (!a->windowed || a->sw > C1V_MAXW || a->ap.n_ops < 1 || s.rw < 2) return false;
+  const int64_t size = a->desc.size_ms, adv = a->desc.advance_ms;
+  if (a->desc.window_kind == KHIP_WINDOW_HOPPING) {
+    if (size % adv != 0 || size / adv > 16) return false;
+  } else if (a->desc.window_kind != KHIP_WINDOW_TUMBLING) {
+    return false;
+  }
+  int c = -1, seen = 0;
+  for (int o = 0; o < a->ap.n_ops; o++) {
+    const UpdOp op = a->ap.ops[o];
+    if (op.kind < OP_INC || op.kind > OP_MAX || op.word < 3 || op.word >= a->sw) return false;
+    const int bit = op.kind == OP_ADD_F64 ? (1 << OP_ADD_I64) : (1 << op.kind);
+    if (seen & bit) return false;
+    seen |= bit;
+    if (op.kind == OP_INC) continue;
+    if (c >= 0 && op.col != c) return false;
+    c = op.col;
+  }
+  if (c < 0) return false;  // COUNT(*) alone: the COUNT(*) pipeline's
+  const int t = a->ap.col_type[c];
+  if (t != KHIP_TYPE_INT32 && t != KHIP_TYPE_INT64 && t != KHIP_TYPE_DOUBLE) return false;
+  *col = c;
+  return s.log2P >= 11 && s.log2P <= 16 && s.mH >= 256 && adv <= ((int64_t)1 << 31) &&
+         !(a->desc.flags & KHIP_FLAG_PART_CLAIM) && n > 0 && n < ((int64_t)1 << 31) && knob("KHIP_C1V", 1) != 0 &&
+         knob("KHIP_PAD", 0) == 0 && knob("KHIP_MERGE", 1) != 0 && knob("KHIP_SCATTER2", 1) != 0;
+}
+
+// LDS layout of k_c1v_merge (byte offsets into q); returns the bytes.
+static size_t c1v_layout(khip_agg* a, int log2H, int idw, int log2B, C1VQ* q) {
+  const size_t E = ((size_t)1 << log2H) + 64, H = (size_t)1 << log2H, B = (size_t)1 << log2B;
+  size_t off = E * idw;
+  off = (off + 7) & ~(size_t)7;
+  q->off_sum = q->off_min = q->off_max = q->off_star = q->off_cnt = -1;
+  for (int o = 0; o < a->ap.n_ops; o++) {
+    const int k = a->ap.ops[o].kind;
+    if (k == OP_ADD_I64 || k == OP_ADD_F64) q->off_sum = 1;
+    if (k == OP_MIN) q->off_min = 1;
+    if (k == OP_MAX) q->off_max = 1;
+    if (k == OP_INC) q->off_star = 1;
+    if (k == OP_INC_VALID) q->off_cnt = 1;
+  }
+  auto place = [&](int32_t* f, size_t bytes) {
+    if (*f < 0) return;
+    *f = (int32_t)off;
+    off += E * bytes;
+  };
+  place(&q->off_sum, 8);
+  place(&q->off_min, 8);
+  place(&q->off_max, 8);
+  q->off_rt = (int32_t)off;
+  off += E * 4;
+  place(&q->off_star, 4);
+  place(&q->off_cnt, 4);
+  off = (off + 15) & ~(size_t)15;
+  q->off_list = (int32_t)off;
+  off += (H * 2 + 15) & ~(size_t)15;
+  q->off_spre = (int32_t)off;
+  off += (C1_SEGMAX + 4) * 4 + C1_SEGMAX * 4 + (B + 1) * 12 + 8 + C1_SEGOF * 2;
+  return off;
+}
+
 // Returns KHIP_OK with *declined = true when k_c1_check declined the push (nothing persistent was
 // touched: the caller runs the general path on the same batch).
+// cols != nullptr: the value pipeline over argument column vcol (c1v_eligible).
 khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
-                    const uint8_t* rv, int64_t* tot, bool* declined, const int64_t* st_at, bool* retry_wide) {
+                    const uint8_t* rv, int64_t* tot, bool* declined, const int64_t* st_at, bool* retry_wide,
+                    const ColPtrs* cols, int vcol) {
   PartState& s = a->part;
   *declined = false;
   *retry_wide = false;
+  const bool val = cols != nullptr;
+  const bool panes = val && a->desc.window_kind == KHIP_WINDOW_HOPPING;
+  const int pbits = panes ? 1 : 0;
+  const int CH = val ? C1V_CH : C1_CH;
+  constexpr int UV = 4;  // value scatter: records per thread per step
   const int P = (int)s.P;
   const int fbits = s.log2P - s.log2P / 2;
   const int log2B = s.log2P - fbits;
   const int B = 1 << log2B, F = 1 << fbits;
   const int64_t nT = ceil_div(n, C1_TILE);
   const int TC = (int)std::min<int64_t>(nT, 64);
-  const int64_t nchunk_max = ceil_div(n, C1_CH) + B;
+  const int64_t nchunk_max = ceil_div(n, CH) + B;
   KHIP_TRY(s.c1hist.ensure((size_t)nT * B * 4));
   KHIP_TRY(s.c1bb.ensure((size_t)(B + 1) * 8));
   const size_t seg_bytes = ((size_t)nchunk_max * (F + 1) * 2 + 255) & ~(size_t)255;  // cstart 256-B aligned
   KHIP_TRY(s.c1seg.ensure(seg_bytes + (size_t)(B + 1) * 4));
-  const int64_t nS = ceil_div(n, 8 * C1_NT);  // k_c1_scatter steps (8 records per thread)
+  const int64_t nS = ceil_div(n, (val ? UV : 8) * C1_NT);  // scatter steps
   KHIP_TRY(s.tilemax.ensure(nS * 16));      // per step: accepted ts max, min
   KHIP_TRY(s.tpart.ensure(nT * 8 * T_NPART));
   KHIP_TRY(s.scan_tmpB.ensure((size_t)TC * B * 8));
@@ -1099,7 +2229,8 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     KHIP_TRY(s.srec.ensure((size_t)(n + 1) * s.rw * 8));
     s.scat_cap = n;
   }
-  KHIP_TRY(s.srecA.ensure((size_t)(n + 1) * s.rw * 8));
+  KHIP_TRY(s.srec.ensure((size_t)(n + 1) * 16));  // (s.rw >= 2: no-ops)
+  KHIP_TRY(s.srecA.ensure((size_t)(n + 1) * std::max(s.rw, 2) * 8));
   if (!s.c1info.p) {
     KHIP_TRY(s.c1info.ensure(CI_N * 8));
     int64_t init[CI_N] = {};
@@ -1141,11 +2272,20 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
   ev_record_part(a, 1);
   // wide records (key hash + u32 ts words) when the key range did not fit 32 bits last time: the
   // host predicts the format, k_c1_check declines a compact push whose keys do not fit
-  const bool wide = s.c1_wide;
+  const bool wide = !val && s.c1_wide;
   uint32_t* srecAT = (uint32_t*)(s.srecA.as<uint64_t>() + n + 1);  // WIDE ts words (12 B/record in all)
   uint32_t* srecT = (uint32_t*)(s.srec.as<uint64_t>() + n + 1);
   // 3. records → buckets
-  {
+  if (val) {
+    const C1VCol vc{cols->data[vcol], cols->valid[vcol], a->ap.col_type[vcol]};
+    auto sk = st_at ? k_c1v_scatter<UV, C1_NT, true> : k_c1v_scatter<UV, C1_NT, false>;
+    const size_t lds = c1v_stage_lds(B, UV * C1_NT);
+    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)sk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(sk, dim3(nT), dim3(C1_NT), lds, a->stream, keys, ts, kv, rv, vc, n, nT, log2B,
+                       s.c1hist.as<uint32_t>(), (ulonglong2*)s.srecA.p, s.tilemax.as<int64_t>(), s.tpart.as<int64_t>(),
+                       ci, st_at, a->desc.size_ms, adv, fd, a->desc.size_ms != adv ? 1 : 0);
+    KHIP_TRY_HIP(hipGetLastError());
+  } else {
     constexpr int U = 8;
     auto sk = wide ? (st_at ? k_c1_scatter<U, C1_NT, true, true> : k_c1_scatter<U, C1_NT, true, false>)
                    : (st_at ? k_c1_scatter<U, C1_NT, false, true> : k_c1_scatter<U, C1_NT, false, false>);
@@ -1159,11 +2299,18 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
   // 4. accept or decline
   hipLaunchKernelGGL(k_c1_check, dim3(1), dim3(1024), 0, a->stream, s.tilemax.as<int64_t>(), nS,
                      a->desc.size_ms, adv, fd, a->grace, close0, s.res_fresh ? 1 : 0, log2B, s.log2P, wide ? 1 : 0,
-                     s.c1bb.as<int64_t>(), cstart, ci, a->stream_time.as<int64_t>(), s.res.as<int64_t>(),
+                     val ? C1V_CH : C1_CH, val ? 31 : 32, pbits, s.c1bb.as<int64_t>(), cstart, ci, a->stream_time.as<int64_t>(), s.res.as<int64_t>(),
                      s.ctr.as<unsigned long long>(), s.closed_ctr.as<unsigned long long>(),
                      (unsigned long long)s.closed_n);
   // 5. refine: chunks → partition-sorted, segment table
-  {
+  if (val) {
+    auto rk = k_c1v_refine<C1V_CH / C1_NT, C1_NT>;
+    const size_t lds = (((size_t)F * 8 + 15) & ~(size_t)15) + (size_t)C1V_CH * 16;
+    hipFuncSetAttribute((const void*)rk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(rk, dim3((unsigned)nchunk_max), dim3(C1_NT), lds, a->stream, (const ulonglong2*)s.srecA.p,
+                       s.c1bb.as<int64_t>(), cstart, log2B, s.log2P, fbits, (ulonglong2*)s.srec.p, seg, ci);
+    KHIP_TRY_HIP(hipGetLastError());
+  } else {
     constexpr int U = C1_CH / C1_NT;
     auto rk = wide ? k_c1_refine<U, C1_NT, true> : k_c1_refine<U, C1_NT, false>;
     const size_t lds = (size_t)F * 8 + (size_t)C1_CH * 8;
@@ -1188,6 +2335,38 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
   cq.size = a->desc.size_ms;
   cq.adv = adv;
   cq.fd = fd;
+  cq.fd32 = make_fastdiv32((uint32_t)adv);
+  // the value pipeline's merge: the largest table (up to 2^12 entries) whose LDS lets two
+  // workgroups share a CU
+  C1VQ vq0{};
+  int v_log2H = 12;
+  bool v_big = false;
+  if (val) {
+    while (v_log2H > 9 && c1v_layout(a, v_log2H, 8, log2B, &vq0) > 78 * 1024) v_log2H--;
+    v_log2H = (int)knob("KHIP_C1V_LOG2H", v_log2H);
+    v_big = knob("KHIP_C1V_AU", 2) >= 4;
+    vq0.log2P = s.log2P;
+    vq0.fbits = fbits;
+    vq0.log2H = v_log2H;
+    vq0.sw = a->sw;
+    vq0.hmax = (int)((int64_t)(1 << v_log2H) * 3 / 4);
+    vq0.fan = (int)(a->desc.size_ms / adv);
+    vq0.f64 = 0;
+    for (int k = 0; k < C1V_MAXW; k++) {
+      vq0.word_op[k] = -1;
+      vq0.init[k] = (uint64_t)a->init.w[k];
+    }
+    for (int o = 0; o < a->ap.n_ops; o++) {
+      vq0.word_op[a->ap.ops[o].word] = a->ap.ops[o].kind;
+      if (a->ap.ops[o].kind == OP_ADD_F64) vq0.f64 = 1;
+    }
+    if (a->ap.col_type[vcol] == KHIP_TYPE_DOUBLE) vq0.f64 = 1;
+    vq0.size = a->desc.size_ms;
+    vq0.adv = adv;
+    vq0.fd = fd;
+    vq0.fd32 = make_fastdiv32((uint32_t)adv);
+    vq0.having = a->having;
+  }
   int64_t added_total = 0;
   std::vector<int> sbits(s.psbits.begin(), s.psbits.end());
   std::vector<uint32_t> plist, work;
@@ -1199,7 +2378,6 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     KHIP_TRY(s.work.ensure(work.size() * 4));
     KHIP_TRY_HIP(hipMemcpyAsync(s.work.p, work.data(), work.size() * 4, hipMemcpyHostToDevice, a->stream));
   }
-  const int au = (int)knob("KHIP_C1_AU", 6);
   std::vector<uint8_t> host_fail;
   for (int pass = 0;; pass++) {
     cq.cmax = s.cmax;
@@ -1210,12 +2388,31 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     const int64_t grid = std::min<int64_t>(nwork, (int64_t)s.n_cu * knob("KHIP_MERGE_WG_PER_CU", 2));
     // compact records: both identity widths are launched, the one k_c1_check did not choose exits
     // at once; wide records: 64-bit identities
-    for (int idw = wide ? 1 : 0; idw < 2; idw++) {
-      auto mk = wide ? k_c1_merge<512, 4, uint64_t, true>
-                     : (idw == 0 ? (au >= 8 ? k_c1_merge<512, 8, uint32_t, false>
-                                            : (au >= 6 ? k_c1_merge<512, 6, uint32_t, false> : k_c1_merge<512, 4, uint32_t, false>))
-                                 : k_c1_merge<512, 4, uint64_t, false>);
-      const size_t lds = c1_merge_lds(log2H, idw == 0 ? 4 : 8);
+    for (int idw = wide ? 1 : 0; idw < 2 && val; idw++) {
+      C1VQ vq = vq0;
+      const size_t lds = c1v_layout(a, v_log2H, idw == 0 ? 4 : 8, log2B, &vq);
+      vq.cmax = s.cmax;
+      vq.chg = a->changelog ? a->chg.as<uint8_t>() : nullptr;
+      // AU 2 at <= 128 VGPRs (two workgroups per CU) or AU 4 at <= 256 (one)
+      auto mk = v_big ? (panes ? (idw == 0 ? k_c1v_merge<512, 4, uint32_t, true, 2> : k_c1v_merge<512, 4, uint64_t, true, 2>)
+                               : (idw == 0 ? k_c1v_merge<512, 4, uint32_t, false, 2> : k_c1v_merge<512, 4, uint64_t, false, 2>))
+                      : (panes ? (idw == 0 ? k_c1v_merge<512, 2, uint32_t, true, 4> : k_c1v_merge<512, 2, uint64_t, true, 4>)
+                               : (idw == 0 ? k_c1v_merge<512, 2, uint32_t, false, 4> : k_c1v_merge<512, 2, uint64_t, false, 4>));
+      hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      KHIP_TRY(s.c1vq.ensure(sizeof(C1VQ)));
+      KHIP_TRY_HIP(hipMemcpyAsync(s.c1vq.p, &vq, sizeof(C1VQ), hipMemcpyHostToDevice, a->stream));
+      const int64_t vgrid = std::min<int64_t>(nwork, (int64_t)s.n_cu * (v_big ? 1 : 2));
+      hipLaunchKernelGGL(mk, dim3(vgrid), dim3(512), lds, a->stream, s.c1vq.as<C1VQ>(), wk, nwork, s.c1bb.as<int64_t>(), cstart, seg,
+                         (const ulonglong2*)s.srec.p, pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
+                         s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
+                         s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
+                         s.closed_ctr.as<unsigned long long>(), ci,
+                         s.hnew.as<unsigned long long>(), s.ctr.as<unsigned long long>() + 12, s.prn.as<uint32_t>());
+    }
+    for (int idw = wide ? 1 : 0; idw < 2 && !val; idw++) {
+      auto mk = wide ? k_c1_merge<512, 3, uint64_t, true>
+                     : (idw == 0 ? k_c1_merge<512, 4, uint32_t, false> : k_c1_merge<512, 4, uint64_t, false>);
+      const size_t lds = c1_merge_lds(log2H, idw == 0 ? 4 : 8, log2B);
       hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(mk, dim3(grid), dim3(512), lds, a->stream, cq, wk, nwork, s.c1bb.as<int64_t>(), cstart, seg,
                          s.srec.as<uint64_t>(), pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
@@ -1247,7 +2444,7 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     const int64_t* hci = s.pinfo.as<int64_t>() + 32;
     if (pass == 0 && hci[CI_GATE] == 0) {  // declined: nothing was written
       *declined = true;
-      *retry_wide = hci[CI_REASON] == 1;  // only the record format was wrong
+      *retry_wide = !val && hci[CI_REASON] == 1;  // only the record format was wrong
       if (*retry_wide) s.c1_wide = true;
       return KHIP_OK;
     }

@@ -354,6 +354,7 @@ struct PartState {
   DevBuf c1hist, c1bb, c1seg, c1info, prn;
   bool last_c1 = false;
   int c1_skip = 0;  // pushes left before the pipeline is tried again after a declined push
+  DevBuf c1vq;  // the value pipeline's merge parameters (device copy)
   bool c1_wide = false;  // the pipeline's record format for the next push (key range past 32 bits)
 };
 

@@ -3774,13 +3774,16 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   // that may hold late records, a ts span or key range too wide) runs the general path below, and
   // the next few pushes go straight there
   s.last_c1 = false;
+  int vcol = -1;
   if (s.c1_skip > 0) {
     s.c1_skip--;
-  } else if (c1_eligible(a, n)) {
+  } else if (c1_eligible(a, n) || c1v_eligible(a, n, &vcol)) {
+    // COUNT(*) alone: 8-byte records; one argument column: 16-byte value records
+    const ColPtrs* vc = vcol >= 0 ? &cols : nullptr;
     bool declined = false, retry_wide = false;
-    KHIP_TRY(c1_push(a, n, keys, ts, kv, rv, tot, &declined, st_at, &retry_wide));
+    KHIP_TRY(c1_push(a, n, keys, ts, kv, rv, tot, &declined, st_at, &retry_wide, vc, vcol));
     if (declined && retry_wide)  // the keys needed the wide records: this push again with them
-      KHIP_TRY(c1_push(a, n, keys, ts, kv, rv, tot, &declined, st_at, &retry_wide));
+      KHIP_TRY(c1_push(a, n, keys, ts, kv, rv, tot, &declined, st_at, &retry_wide, vc, vcol));
     if (a->profile) (declined ? a->times.c1_declined : a->times.c1_pushes)++;
     if (!declined) return KHIP_OK;
     s.c1_skip = 8;

@@ -63,6 +63,30 @@ __device__ __forceinline__ void mg_list_append(bool claimed, uint32_t e, KLDS ui
   if (claimed) nl[base + __popcll(b & ((1ULL << lane) - 1))] = (uint16_t)e;
 }
 
+// mg_list_append for AU entries per lane at once: one LDS atomic per wave for all of them.
+template <int AU>
+__device__ __forceinline__ void mg_list_append_n(const bool (&claimed)[AU], const uint32_t (&e)[AU], KLDS uint16_t* nl,
+                                                 int* nnew) {
+  uint64_t b[AU];
+  int tot = 0;
+#pragma unroll
+  for (int u = 0; u < AU; u++) {
+    b[u] = __ballot(claimed[u]);
+    tot += __popcll(b[u]);
+  }
+  if (!tot) return;
+  const int lane = threadIdx.x & 63;
+  int base = 0;
+  if (lane == 0) base = atomicAdd(nnew, tot);
+  base = __shfl(base, 0, 64);
+  const uint64_t lt = (1ULL << lane) - 1;
+#pragma unroll
+  for (int u = 0; u < AU; u++) {
+    if (claimed[u]) nl[base + __popcll(b[u] & lt)] = (uint16_t)e[u];
+    base += __popcll(b[u]);
+  }
+}
+
 constexpr uint32_t C1_GOLD = 0x9E3779B1u;
 
 __device__ __forceinline__ uint32_t stage_bin(uint64_t hk, int shift, uint32_t mask) {
@@ -150,8 +174,10 @@ __global__ void k_part_stats(const int64_t* __restrict__ tpart, int64_t nT, cons
 khip_status part_regrow(khip_agg* a, int64_t ncmax);
 // khip_agg_c1.hip: the windowed COUNT(*) pipeline (declined = the general path must run)
 bool c1_eligible(khip_agg* a, int64_t n);
+bool c1v_eligible(khip_agg* a, int64_t n, int* col);
 khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
-                    const uint8_t* rv, int64_t* tot, bool* declined, const int64_t* st_at, bool* retry_wide);
+                    const uint8_t* rv, int64_t* tot, bool* declined, const int64_t* st_at, bool* retry_wide,
+                    const ColPtrs* cols = nullptr, int vcol = -1);
 __global__ void k_part_commit(const int64_t* __restrict__ gate, int P, const int64_t* __restrict__ pbase,
                               const uint32_t* __restrict__ prn, const uint32_t* __restrict__ plist, int nlist,
                               uint8_t* __restrict__ sel, int64_t* __restrict__ cnt,

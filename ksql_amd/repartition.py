@@ -61,10 +61,18 @@ class Repartition:
         self.comm = comm
         self.shuffle = abi.ShuffleHandle(lib, world, key_col, col_types, device)
         self.last_counts = None
+        self._send = None
 
     def __call__(self, batch):
         """Device batch (source partition) → (DeviceBatch of this task's rows, tensors)."""
-        send, counts = self.shuffle.pack(batch)
+        import torch
+        n = max(int(batch.struct.n_rows), 1)
+        # a send buffer for every row the batch holds, kept across calls: one pack launch
+        # sequence per call (no count-only pass to size the buffer)
+        if self._send is None or self._send.shape[0] < n:
+            self._send = torch.empty((n, self.shuffle.row_words), dtype=torch.int64,
+                                     device=torch.device("cuda", self.shuffle.device))
+        send, counts = self.shuffle.pack(batch, send=self._send)
         if self.world == 1:
             recv, rcounts = send, counts
         else:

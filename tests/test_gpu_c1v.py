@@ -1,0 +1,171 @@
+"""The value-record pipeline (ksql_amd/csrc/khip_agg_c1.hip, k_c1v_*) against the oracle.
+
+A push whose aggregates all read ONE argument column (COUNT(col), SUM, AVG, MIN, MAX, with or
+without COUNT(*)) over TUMBLING or HOPPING windows (size a multiple of the advance) moves 16-byte
+records — (key - kmin, ts - T0, the argument's null flag) + the argument's bits — through the
+COUNT(*) pipeline's histogram / scatter / refine, and a merge whose LDS table holds per-entry
+planes for the ops present; HOPPING goes through panes (one entry per (key, ts / advance), folded
+into its F windows after the records).  Declined like the COUNT(*) pipeline (a step that may hold a
+late record, a ts span past 2^31 ms) and also when the key range does not fit 31 bits; the
+general path then runs the same batch.  Every case checks the final table, every push's batch
+statistics (windows applied included: HOPPING counts windowsFor per record), the HAVING count
+and, where asked, the per-push changelog against the oracle (the sequential restatement of
+KStreamWindowAggregate, S/StreamAggregateBuilder.java:287-294, and the Kudaf aggregators), and
+which path each push took (khip_kernel_times c1_pushes / c1_declined).
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+from ksql_amd import abi
+from test_gpu_parity import assert_snap_equal
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def prod():
+    return abi.load_product()
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return abi.load_oracle()
+
+
+SHAPES = {
+    # C5's query: SUM(amount) of a BIGINT
+    "sum_i64": (["INT64"], [("SUM", 0)]),
+    # C3's: SUM/AVG/MIN/MAX of a DOUBLE (non-negative values: the SUM bound is relative)
+    "c3_f64": (["DOUBLE"], [("SUM", 0), ("AVG", 0), ("MIN", 0), ("MAX", 0)]),
+    # every op kind on an INT column, with COUNT(*)
+    "all_i32": (["INT32"], [("COUNT_STAR", -1), ("COUNT", 0), ("SUM", 0), ("MIN", 0), ("MAX", 0), ("AVG", 0)]),
+    # MIN / MAX of a DOUBLE with negative values (the order key), COUNT(col)
+    "minmax_f64": (["DOUBLE"], [("MIN", 0), ("MAX", 0), ("COUNT", 0)]),
+}
+
+WINDOWS = {
+    "tumbling": dict(window_kind="TUMBLING", size_ms=5000),
+    "hop3": dict(window_kind="HOPPING", size_ms=6000, advance_ms=2000, grace_ms=30_000),
+    "hop6": dict(window_kind="HOPPING", size_ms=60_000, advance_ms=10_000, grace_ms=60_000),
+    "hop3_g0": dict(window_kind="HOPPING", size_ms=6000, advance_ms=2000, grace_ms=0),
+}
+MAIN_WINDOWS = ["tumbling", "hop3", "hop6"]
+
+
+def _values(rng, n, shape):
+    t = SHAPES[shape][0][0]
+    if t == "INT32":
+        v = rng.integers(-2**31, 2**31, n).astype(np.int32)
+    elif t == "INT64":
+        v = rng.integers(-2**62, 2**62, n) * rng.integers(-1, 2, n)  # SUM wraps
+    elif shape == "c3_f64":
+        v = rng.uniform(0, 1e3, n)
+    else:
+        v = rng.uniform(-1e3, 1e3, n) * np.where(rng.random(n) < 0.01, 1e200, 1.0)
+        v[rng.random(n) < 0.002] = -0.0
+    return v
+
+
+def _batches(rng, shape, nb, n, keys, span, disorder=500, kbase=0, null_frac=0.03, utf8=False):
+    out = []
+    for b in range(nb):
+        k = kbase + rng.integers(0, keys, n)
+        ts = b * span + (np.arange(n) * span) // n + rng.integers(0, disorder, n)
+        v = _values(rng, n, shape)
+        vv = rng.random(n) > null_frac
+        if utf8:
+            out.append(abi.HostBatch(ts, utf8_keys=["u%d" % x for x in k], cols=[v], col_valid=[vv]))
+        else:
+            out.append(abi.HostBatch(ts, keys=k, cols=[v], col_valid=[vv]))
+    return out
+
+
+def _desc(shape, win, hint, flags=0, having=None, key_type="INT64"):
+    types, aggs = SHAPES[shape]
+    return abi.make_agg_desc(key_type=key_type, col_types=types, aggs=aggs, capacity_hint=hint, flags=flags,
+                             having=having, **WINDOWS[win])
+
+
+def _run(prod, orc, shape, win, batches, hint, changes=False, having=None, key_type="INT64"):
+    flags = abi.FLAG_CHANGELOG if changes else 0
+    gd = _desc(shape, win, hint, flags | abi.FLAG_PROFILE, having, key_type)
+    od = _desc(shape, win, hint, flags, having, key_type)
+    g, o = abi.AggHandle(prod, gd), abi.AggHandle(orc, od)
+    for b in batches:
+        gs, os_ = g.push(b), o.push(b)
+        assert gs == os_, (gs, os_)
+        if changes:
+            gc, oc = g.changes(), o.changes()
+            assert_snap_equal(gc, oc, gd)
+            assert np.array_equal(gc["tombstone"], oc["tombstone"])
+    assert_snap_equal(g.snapshot(), o.snapshot(), gd)
+    if having is not None:
+        assert g.count_rows(having) == o.snapshot(having)["n"]
+    assert g.count_rows(None) == o.snapshot()["n"]
+    kt = g.kernel_times()
+    g.close()
+    o.close()
+    return kt
+
+
+@pytest.mark.parametrize("win", MAIN_WINDOWS)
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_c1v_vs_oracle(prod, orc, shape, win):
+    """Three pushes (resident rows merged; HOPPING windows spanning pushes), nulls in the argument."""
+    rng = np.random.default_rng(zlib.crc32((shape + win).encode()))
+    span = 40_000 if win != "hop6" else 200_000
+    batches = _batches(rng, shape, 3, 600_000, 60_000, span)
+    kt = _run(prod, orc, shape, win, batches, hint=3_000_000)
+    assert kt["c1_pushes"] == 3 and kt["c1_declined"] == 0, kt
+
+
+@pytest.mark.parametrize("win", ["tumbling", "hop3"])
+def test_c1v_changelog_having(prod, orc, win):
+    """EMIT CHANGES per push with a HAVING on SUM (tombstones when a window's sum leaves it)."""
+    rng = np.random.default_rng(5)
+    batches = _batches(rng, "sum_i64", 3, 400_000, 30_000, 30_000)
+    having = {"agg": 0, "op": "GT", "value": 0}
+    kt = _run(prod, orc, "sum_i64", win, batches, hint=2_000_000, changes=True, having=having)
+    assert kt["c1_pushes"] == 3, kt
+
+
+def test_c1v_c3_shape_having_avg(prod, orc):
+    """C3's aggregate list with a HAVING on AVG (a DOUBLE result), HOPPING 60 s / 10 s."""
+    rng = np.random.default_rng(6)
+    batches = _batches(rng, "c3_f64", 2, 800_000, 20_000, 300_000)
+    having = {"agg": 1, "op": "GE", "value": 500.0}
+    kt = _run(prod, orc, "c3_f64", "hop6", batches, hint=2_000_000, having=having)
+    assert kt["c1_pushes"] == 2, kt
+
+
+def test_c1v_utf8_keys(prod, orc):
+    rng = np.random.default_rng(7)
+    batches = _batches(rng, "sum_i64", 2, 300_000, 40_000, 30_000, utf8=True)
+    kt = _run(prod, orc, "sum_i64", "tumbling", batches, hint=2_000_000, key_type="UTF8")
+    assert kt["c1_pushes"] == 2, kt
+
+
+def test_c1v_declines(prod, orc):
+    """Late records (grace 0, disorder across window ends) and a key range past 31 bits: the
+    general path runs those pushes, with the same results."""
+    rng = np.random.default_rng(8)
+    late = _batches(rng, "sum_i64", 2, 200_000, 20_000, 30_000, disorder=8000)
+    kt = _run(prod, orc, "sum_i64", "hop3_g0", late, hint=2_000_000)
+    assert kt["c1_declined"] >= 1, kt
+    wide = _batches(rng, "c3_f64", 1, 200_000, 20_000, 30_000, kbase=0)
+    k = wide[0].keys.copy()
+    k[::2] += 1 << 40
+    b = abi.HostBatch(wide[0].ts, keys=k, cols=[_values(rng, len(k), "c3_f64")])
+    kt = _run(prod, orc, "c3_f64", "tumbling", [b], hint=2_000_000)
+    assert kt["c1_declined"] == 1 and kt["c1_pushes"] == 0, kt
+
+
+def test_c1v_many_groups_subpasses(prod, orc):
+    """More groups per partition than the merge's table takes at the hinted size: sub-pass
+    retries (split by key, so a pane and its windows stay together) and region growth."""
+    rng = np.random.default_rng(9)
+    batches = _batches(rng, "all_i32", 2, 1_000_000, 900_000, 20_000)
+    kt = _run(prod, orc, "all_i32", "hop3", batches, hint=1 << 16)
+    assert kt["c1_pushes"] >= 1, kt

@@ -9,8 +9,13 @@ COUNT(*) TUMBLING + HAVING workload against the oracle (table, batch statistics,
 - KHIP_R8_U=4: R8 staged steps of 4 records per thread;
 - KHIP_SCATTER2=0: one-level scatter (no refine pass);
 - KHIP_R8=0: 12-byte (R12) records where R8 would fit;
-- KHIP_C1_AU=4 / KHIP_C1_LOG2H=13: the pipeline's merge with fewer records per thread per chunk,
-  and with a twice larger LDS table.
+- KHIP_C1P=0 + KHIP_C1_AU=4: the general path's COUNT(*) merge with fewer records per thread;
+- KHIP_C1_LOG2H=13 / 11: the pipeline's merge with a twice larger LDS table, and with a twice
+  smaller one (partitions overflow it: the sub-pass retries);
+- KHIP_C1V=0: value aggregates through the general path instead of the value-record pipeline;
+  KHIP_C1V_AU=4: its merge at 4 records per thread per chunk (<= 256 VGPRs, one workgroup per
+  CU); KHIP_C1V_LOG2H=9: a small LDS table (sub-pass retries, split by key).
+Each case runs COUNT(*) TUMBLING + HAVING and SUM / MIN / MAX of a BIGINT over HOPPING (panes).
 Dense and sparse key ranges, several pushes (resident rows), late records (the pipeline declines).
 """
 import os
@@ -31,8 +36,12 @@ KNOBS = [
     {"KHIP_C1P": "0", "KHIP_R8_U": "4"},
     {"KHIP_C1P": "0", "KHIP_SCATTER2": "0"},
     {"KHIP_C1P": "0", "KHIP_R8": "0"},
-    {"KHIP_C1_AU": "4"},
+    {"KHIP_C1P": "0", "KHIP_C1_AU": "4"},
     {"KHIP_C1_LOG2H": "13"},
+    {"KHIP_C1_LOG2H": "11"},
+    {"KHIP_C1V": "0"},
+    {"KHIP_C1V_AU": "4"},
+    {"KHIP_C1V_LOG2H": "9"},
 ]
 
 
@@ -58,18 +67,24 @@ def _check():
             if case == "late":
                 ts[rng.random(n) < 0.02] -= 15_000
             t0 += 20_000
-            batches.append(abi.HostBatch(ts, keys=k))
-        kw = dict(window_kind="TUMBLING", size_ms=5000, grace_ms=2000 if case == "late" else -1,
-                  aggs=[("COUNT_STAR", -1)], having=having, capacity_hint=1 << 22)
-        gd, od = abi.make_agg_desc(**kw), abi.make_agg_desc(**kw)
-        g, o = abi.AggHandle(prod, gd), abi.AggHandle(orc, od)
-        for b in batches:
-            gs, os_ = g.push(b), o.push(b)
-            assert gs == os_, (case, gs, os_)
-        assert_snap_equal(g.snapshot(), o.snapshot(), gd)
-        assert g.count_rows(having) == o.snapshot(having)["n"], case
-        g.close()
-        o.close()
+            v = rng.integers(-1000, 1000, n)
+            batches.append(abi.HostBatch(ts, keys=k, cols=[v], col_valid=[rng.random(n) > 0.02]))
+        grace = 2000 if case == "late" else -1
+        kws = [dict(window_kind="TUMBLING", size_ms=5000, grace_ms=grace, aggs=[("COUNT_STAR", -1)], having=having,
+                    capacity_hint=1 << 22),
+               dict(window_kind="HOPPING", size_ms=6000, advance_ms=2000, grace_ms=grace, col_types=["INT64"],
+                    aggs=[("SUM", 0), ("MIN", 0), ("MAX", 0)], having={"agg": 0, "op": "GT", "value": 0},
+                    capacity_hint=1 << 22)]
+        for kw in kws:
+            gd, od = abi.make_agg_desc(**kw), abi.make_agg_desc(**kw)
+            g, o = abi.AggHandle(prod, gd), abi.AggHandle(orc, od)
+            for b in batches:
+                gs, os_ = g.push(b), o.push(b)
+                assert gs == os_, (case, gs, os_)
+            assert_snap_equal(g.snapshot(), o.snapshot(), gd)
+            assert g.count_rows(kw["having"]) == o.snapshot(kw["having"])["n"], case
+            g.close()
+            o.close()
     print("OK")
 
 

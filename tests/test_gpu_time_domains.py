@@ -93,7 +93,8 @@ def test_partition_domain_matches_independent_tasks(prod, orc, engine, window):
     flags = abi.FLAG_ENGINE_ATOMIC if engine == "atomic" else 0
     gd = _desc(time_domain="PARTITION", n_partitions=P, flags=flags, **kw)
     g = abi.AggHandle(prod, gd)
-    tasks = [abi.AggHandle(orc, _desc(**kw)) for _ in range(P)]
+    # the handle keeps every window visible (no retention in this domain): so do the tasks
+    tasks = [abi.AggHandle(orc, _desc(retention_ms=1 << 40, **kw)) for _ in range(P)]
     late = 0
     for k, t, v, p in batches:
         gs = g.push(abi.HostBatch(t, keys=k, cols=[v], partition=p))
