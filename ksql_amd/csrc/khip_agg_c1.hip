@@ -242,7 +242,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const int64_t base = t * C1_TILE;
   const int64_t end = base + C1_TILE < n ? base + C1_TILE : n;
   int c_acc = 0, c_nk = 0, c_nr = 0, c_bt = 0;  // < 2^16 per tile
-  bool tfail = false;
   int64_t x[U], k[U];
   auto load_step = [&](int64_t i0, int64_t (&dx)[U], int64_t (&dk)[U]) {
 #pragma unroll
@@ -287,10 +286,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
       c_acc += valid;
       const int64_t sx = ST ? st_at[ok[u] ? i : base] : x[u];  // ABI 5 domains: the given stream time
       const int64_t d = x[u] - T0;
-      tfail |= valid && (d <= (int64_t)INT32_MIN || d > (int64_t)INT32_MAX);
+      if (valid && (d <= (int64_t)INT32_MIN || d > (int64_t)INT32_MAX)) lfail = 1;  // rare: an LDS flag, not a loop-carried mask
       if constexpr (ST) {
         const int64_t ds = sx - T0;
-        tfail |= valid && (ds <= (int64_t)INT32_MIN || ds > (int64_t)INT32_MAX);
+        if (valid && (ds <= (int64_t)INT32_MIN || ds > (int64_t)INT32_MAX)) lfail = 1;
         tmx = valid && (int)ds > tmx ? (int)ds : tmx;
       } else {
         tmx = valid && (int)d > tmx ? (int)d : tmx;
@@ -331,7 +330,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (c_nr) atomicAdd(&lc[2], (unsigned long long)c_nr);
     if (c_bt) atomicAdd(&lc[3], (unsigned long long)c_bt);
   }
-  if (tfail) lfail = 1;
   __syncthreads();
   if (threadIdx.x == 0) {
     int64_t* tp = tpart + t * T_NPART;
@@ -1255,7 +1253,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const int64_t base = t * C1_TILE;
   const int64_t end = base + C1_TILE < n ? base + C1_TILE : n;
   int c_acc = 0, c_nk = 0, c_nr = 0, c_bt = 0, c_app = 0;
-  bool tfail = false;
   int64_t x[U], k[U], v[U];
   auto load_step = [&](int64_t i0) {
 #pragma unroll
@@ -1298,10 +1295,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
       c_bt += ok[u] && kok && rok && x[u] < 0;
       c_acc += valid;
       const int64_t d = x[u] - T0;
-      tfail |= valid && (d <= (int64_t)INT32_MIN || d > (int64_t)INT32_MAX);
+      if (valid && (d <= (int64_t)INT32_MIN || d > (int64_t)INT32_MAX)) lfail = 1;  // rare: an LDS flag, not a loop-carried mask
       if constexpr (ST) {
         const int64_t ds = st_at[ii] - T0;
-        tfail |= valid && (ds <= (int64_t)INT32_MIN || ds > (int64_t)INT32_MAX);
+        if (valid && (ds <= (int64_t)INT32_MIN || ds > (int64_t)INT32_MAX)) lfail = 1;
         tmx = valid && (int)ds > tmx ? (int)ds : tmx;
       } else {
         tmx = valid && (int)d > tmx ? (int)d : tmx;
@@ -1342,7 +1339,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (c_bt) atomicAdd(&lc[3], (unsigned long long)c_bt);
     if (c_app) atomicAdd(&lc[4], (unsigned long long)c_app);
   }
-  if (tfail) lfail = 1;
   __syncthreads();
   if (threadIdx.x == 0) {
     int64_t* tp = tpart + t * T_NPART;
@@ -1457,70 +1453,107 @@ __device__ __forceinline__ KLDS T* c1v_plane(char* smem, int off) {
   return (KLDS T*)((KLDS char*)smem + off);
 }
 
-// Row words r[3..sw) of a (key, window) combined with delta entry e (resident row, or the initial
-// words for a new one).  Unrolled over the words: r stays in registers.
-__device__ __forceinline__ void c1v_combine(const C1VQ& q, char* smem, int e, uint64_t (&r)[C1V_MAXW]) {
-#pragma unroll
-  for (int k = 3; k < C1V_MAXW; k++) {
-    if (k >= q.sw) break;
-    switch (q.word_op[k]) {
-      case OP_INC: r[k] += c1v_plane<uint32_t>(smem, q.off_star)[e]; break;
-      case OP_INC_VALID: r[k] += c1v_plane<uint32_t>(smem, q.off_cnt)[e]; break;
-      case OP_ADD_I64: r[k] += c1v_plane<uint64_t>(smem, q.off_sum)[e]; break;
-      case OP_ADD_F64: {
+// Plane masks: a merge instantiation specialised for the planes a query has (PM != 0, the
+// benchmarks' shapes), or PM = 0 reading them from the parameters (every other shape).
+constexpr int PM_STAR = 1, PM_CNT = 2, PM_SUM = 4, PM_MIN = 8, PM_MAX = 16, PM_F64 = 32, PM_SPEC = 64;
+constexpr int PM_C5 = PM_SPEC | PM_SUM;                                   // SUM(BIGINT)
+constexpr int PM_C3 = PM_SPEC | PM_CNT | PM_SUM | PM_MIN | PM_MAX | PM_F64;  // SUM/AVG/MIN/MAX(DOUBLE)
+template <int PM>
+struct C1VP {
+  const C1VQ& q;
+  __device__ __forceinline__ bool star() const { return PM ? (PM & PM_STAR) != 0 : q.off_star >= 0; }
+  __device__ __forceinline__ bool cnt() const { return PM ? (PM & PM_CNT) != 0 : q.off_cnt >= 0; }
+  __device__ __forceinline__ bool sum() const { return PM ? (PM & PM_SUM) != 0 : q.off_sum >= 0; }
+  __device__ __forceinline__ bool mn() const { return PM ? (PM & PM_MIN) != 0 : q.off_min >= 0; }
+  __device__ __forceinline__ bool mx() const { return PM ? (PM & PM_MAX) != 0 : q.off_max >= 0; }
+  __device__ __forceinline__ bool f64() const { return PM ? (PM & PM_F64) != 0 : q.f64 != 0; }
+};
+
+// Row word k (k >= 3) of a (key, window) combined with delta entry e: the word's update op
+// applied to the entry's plane.
+template <int PM>
+__device__ __forceinline__ uint64_t c1v_word(const C1VQ& q, char* smem, int e, int k, uint64_t w) {
+  const C1VP<PM> v{q};
+  switch (q.word_op[k]) {
+    case OP_INC: return v.star() ? w + c1v_plane<uint32_t>(smem, q.off_star)[e] : w;
+    case OP_INC_VALID: return v.cnt() ? w + c1v_plane<uint32_t>(smem, q.off_cnt)[e] : w;
+    case OP_ADD_I64: return v.sum() && !v.f64() ? w + c1v_plane<uint64_t>(smem, q.off_sum)[e] : w;
+    case OP_ADD_F64:
+      if (v.sum() && v.f64()) {
         double a, b = c1v_plane<double>(smem, q.off_sum)[e];
-        __builtin_memcpy(&a, &r[k], 8);
+        __builtin_memcpy(&a, &w, 8);
         a += b;
-        __builtin_memcpy(&r[k], &a, 8);
-        break;
+        __builtin_memcpy(&w, &a, 8);
       }
-      case OP_MIN: {
+      return w;
+    case OP_MIN:
+      if (v.mn()) {
         const int64_t m = c1v_plane<int64_t>(smem, q.off_min)[e];
-        if (m < (int64_t)r[k]) r[k] = (uint64_t)m;
-        break;
+        if (m < (int64_t)w) w = (uint64_t)m;
       }
-      case OP_MAX: {
+      return w;
+    case OP_MAX:
+      if (v.mx()) {
         const int64_t m = c1v_plane<int64_t>(smem, q.off_max)[e];
-        if (m > (int64_t)r[k]) r[k] = (uint64_t)m;
-        break;
+        if (m > (int64_t)w) w = (uint64_t)m;
       }
-      default: break;
-    }
+      return w;
+    default: return w;
   }
 }
 
-__device__ __forceinline__ bool c1v_having(const C1VQ& q, const uint64_t (&r)[C1V_MAXW]) {
-  if (!q.having.active) return true;
-  uint64_t val = 0, cntw = 0;
+// Write one row word by word (no row array in registers: the write-out runs while the next
+// item's record chunks are in flight), from the resident row (src) or, src == nullptr, from the
+// initial words + key / window start / row time; e >= 0: combined with delta entry e (rtabs =
+// its row time).  *was / *now: the HAVING before and after.
+template <int PM>
+__device__ __forceinline__ void c1v_emit(const C1VQ& q, char* smem, uint64_t* __restrict__ dst,
+                                         const uint64_t* __restrict__ src, int e, int64_t key, int64_t ws, int64_t rtabs,
+                                         bool* was, bool* now) {
+  const int hv = q.having.a.w_val, hc = q.having.a.w_cnt;
+  uint64_t ov = 0, oc = 0, nv = 0, nc = 0;
 #pragma unroll
-  for (int k = 3; k < C1V_MAXW; k++) {
-    if (k == q.having.a.w_val) val = r[k];
-    if (k == q.having.a.w_cnt) cntw = r[k];
+  for (int k = 0; k < C1V_MAXW; k++) {
+    if (k >= q.sw) break;
+    uint64_t w = src ? src[k] : (k == 0 ? (uint64_t)key : k == 1 ? (uint64_t)ws : k == 2 ? (uint64_t)rtabs : q.init[k]);
+    if (k == hv) ov = w;
+    if (k == hc) oc = w;
+    if (e >= 0) {
+      if (k == 2 && src) w = rtabs > (int64_t)w ? (uint64_t)rtabs : w;
+      if (k >= 3) w = c1v_word<PM>(q, smem, e, k, w);
+    }
+    if (k == hv) nv = w;
+    if (k == hc) nc = w;
+    dst[k] = w;
   }
-  return having_ok_words(val, cntw, q.having);
+  *was = q.having.active ? having_ok_words(ov, oc, q.having) : true;
+  *now = q.having.active ? having_ok_words(nv, nc, q.having) : true;
 }
 
 // Clear delta entry e for the next item.
+template <int PM>
 __device__ __forceinline__ void c1v_clear(const C1VQ& q, char* smem, int e) {
+  const C1VP<PM> v{q};
   c1v_plane<uint32_t>(smem, q.off_rt)[e] = 0u;
-  if (q.off_star >= 0) c1v_plane<uint32_t>(smem, q.off_star)[e] = 0u;
-  if (q.off_cnt >= 0) c1v_plane<uint32_t>(smem, q.off_cnt)[e] = 0u;
-  if (q.off_sum >= 0) c1v_plane<uint64_t>(smem, q.off_sum)[e] = 0ULL;
-  if (q.off_min >= 0) c1v_plane<int64_t>(smem, q.off_min)[e] = INT64_MAX;
-  if (q.off_max >= 0) c1v_plane<int64_t>(smem, q.off_max)[e] = INT64_MIN;
+  if (v.star()) c1v_plane<uint32_t>(smem, q.off_star)[e] = 0u;
+  if (v.cnt()) c1v_plane<uint32_t>(smem, q.off_cnt)[e] = 0u;
+  if (v.sum()) c1v_plane<uint64_t>(smem, q.off_sum)[e] = 0ULL;
+  if (v.mn()) c1v_plane<int64_t>(smem, q.off_min)[e] = INT64_MAX;
+  if (v.mx()) c1v_plane<int64_t>(smem, q.off_max)[e] = INT64_MIN;
 }
 
 // One (record or pane) contribution into delta entry e: row time, then the update planes.
-// vok: the argument is not NULL; val: its bits (a pane: cs / cv its counts, val its sum, mn / mx
-// its order keys).
+// cv: the argument's non-null count (a record: 0 / 1), sum its bits (sum), mn / mx its order keys.
+template <int PM>
 __device__ __forceinline__ void c1v_add(const C1VQ& q, char* smem, uint32_t e, uint32_t tr, uint32_t cs, uint32_t cv,
                                         uint64_t sum, int64_t mn, int64_t mx) {
+  const C1VP<PM> v{q};
   __hip_atomic_fetch_max(&c1v_plane<uint32_t>(smem, q.off_rt)[e], tr, WG_RLX);
-  if (q.off_star >= 0 && cs) __hip_atomic_fetch_add(&c1v_plane<uint32_t>(smem, q.off_star)[e], cs, WG_RLX);
+  if (v.star() && cs) __hip_atomic_fetch_add(&c1v_plane<uint32_t>(smem, q.off_star)[e], cs, WG_RLX);
   if (cv) {
-    if (q.off_cnt >= 0) __hip_atomic_fetch_add(&c1v_plane<uint32_t>(smem, q.off_cnt)[e], cv, WG_RLX);
-    if (q.off_sum >= 0) {
-      if (q.f64) {
+    if (v.cnt()) __hip_atomic_fetch_add(&c1v_plane<uint32_t>(smem, q.off_cnt)[e], cv, WG_RLX);
+    if (v.sum()) {
+      if (v.f64()) {
         double d;
         __builtin_memcpy(&d, &sum, 8);
         __hip_atomic_fetch_add(&c1v_plane<double>(smem, q.off_sum)[e], d, WG_RLX);
@@ -1528,8 +1561,8 @@ __device__ __forceinline__ void c1v_add(const C1VQ& q, char* smem, uint32_t e, u
         __hip_atomic_fetch_add(&c1v_plane<uint64_t>(smem, q.off_sum)[e], sum, WG_RLX);
       }
     }
-    if (q.off_min >= 0) __hip_atomic_fetch_min(&c1v_plane<int64_t>(smem, q.off_min)[e], mn, WG_RLX);
-    if (q.off_max >= 0) __hip_atomic_fetch_max(&c1v_plane<int64_t>(smem, q.off_max)[e], mx, WG_RLX);
+    if (v.mn()) __hip_atomic_fetch_min(&c1v_plane<int64_t>(smem, q.off_min)[e], mn, WG_RLX);
+    if (v.mx()) __hip_atomic_fetch_max(&c1v_plane<int64_t>(smem, q.off_max)[e], mx, WG_RLX);
   }
 }
 
@@ -1551,7 +1584,7 @@ __device__ __forceinline__ bool c1v_is_pane(ID id, int wbits) {
 
 // WPE: waves per SIMD the register budget allows (4: <= 128 VGPRs, two workgroups per CU; 2:
 // <= 256, one)
-template <int NT, int AU, class ID, bool PANES, int WPE>
+template <int NT, int AU, class ID, bool PANES, int WPE, int PM>
 __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
     const C1VQ* __restrict__ qp, const uint32_t* __restrict__ work, int64_t nwork, const int64_t* __restrict__ bb,
     const int* __restrict__ cstart, const uint16_t* __restrict__ seg, const ulonglong2* __restrict__ srec, int first,
@@ -1593,7 +1626,7 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
   const uint32_t dummy = (uint32_t)H + (uint32_t)lane;
   for (int i = threadIdx.x; i < H + 64; i += NT) {
     ids[i] = EMPTY;
-    c1v_clear(q, smem, i);
+    c1v_clear<PM>(q, smem, i);
   }
   if (threadIdx.x == 0) {
     lovf = 0;
@@ -1883,12 +1916,12 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
         if (id[u] == EMPTY) continue;
         const uint64_t w0 = xr[u].x;
         int64_t ok_ = (int64_t)xr[u].y;
-        if (q.f64 && (q.off_min >= 0 || q.off_max >= 0)) {
+        if (C1VP<PM>{q}.f64() && (C1VP<PM>{q}.mn() || C1VP<PM>{q}.mx())) {
           double d;
           __builtin_memcpy(&d, &xr[u].y, 8);
           ok_ = f64_order_key(d);
         }
-        c1v_add(q, smem, e[u], (uint32_t)((int32_t)(uint32_t)w0 - tmin32) + 1u, 1u, (w0 >> 63) ? 1u : 0u, xr[u].y, ok_,
+        c1v_add<PM>(q, smem, e[u], (uint32_t)((int32_t)(uint32_t)w0 - tmin32) + 1u, 1u, (w0 >> 63) ? 1u : 0u, xr[u].y, ok_,
                 ok_);
       }
     };
@@ -1930,16 +1963,17 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
           pw = (uint64_t)pid & 0x7FFFFFFFull;
         }
         const uint32_t prt = isp ? rt[pe] : 0u;
-        const uint32_t pcs = isp && q.off_star >= 0 ? c1v_plane<uint32_t>(smem, q.off_star)[pe] : 0u;
-        const uint32_t pcv = isp && q.off_cnt >= 0 ? c1v_plane<uint32_t>(smem, q.off_cnt)[pe] : (isp ? 1u : 0u);
-        const uint64_t psum = isp && q.off_sum >= 0 ? c1v_plane<uint64_t>(smem, q.off_sum)[pe] : 0ULL;
-        const int64_t pmn = isp && q.off_min >= 0 ? c1v_plane<int64_t>(smem, q.off_min)[pe] : INT64_MAX;
-        const int64_t pmx = isp && q.off_max >= 0 ? c1v_plane<int64_t>(smem, q.off_max)[pe] : INT64_MIN;
+        const C1VP<PM> pv{q};
+        const uint32_t pcs = isp && pv.star() ? c1v_plane<uint32_t>(smem, q.off_star)[pe] : 0u;
+        const uint32_t pcv = isp && pv.cnt() ? c1v_plane<uint32_t>(smem, q.off_cnt)[pe] : (isp ? 1u : 0u);
+        const uint64_t psum = isp && pv.sum() ? c1v_plane<uint64_t>(smem, q.off_sum)[pe] : 0ULL;
+        const int64_t pmn = isp && pv.mn() ? c1v_plane<int64_t>(smem, q.off_min)[pe] : INT64_MAX;
+        const int64_t pmx = isp && pv.mx() ? c1v_plane<int64_t>(smem, q.off_max)[pe] : INT64_MIN;
         for (int j = 0; j < q.fan; j++) {
           // window pw - j (its start is >= 0: windowsFor never returns a negative start)
           const bool act = isp && (int64_t)pw - j + wbase >= 0 && (int64_t)pw - j >= 0;
           const int e = claim(c1v_id<ID, PANES>(krel, pw - (uint64_t)j, false, wbits), act);
-          if (e >= 0) c1v_add(q, smem, (uint32_t)e, prt, pcs, pcv, psum, pmn, pmx);
+          if (e >= 0) c1v_add<PM>(q, smem, (uint32_t)e, prt, pcs, pcv, psum, pmn, pmx);
         }
       }
       lds_barrier();
@@ -1950,7 +1984,7 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       for (int i = threadIdx.x; i < nl; i += NT) {
         const uint32_t e = list[i];
         ids[e] = EMPTY;
-        c1v_clear(q, smem, (int)e);
+        c1v_clear<PM>(q, smem, (int)e);
       }
       lds_barrier();
       if (threadIdx.x == 0) {
@@ -2010,7 +2044,7 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       for (int i = threadIdx.x; i < nl; i += NT) {
         const uint32_t e = list[i];
         ids[e] = EMPTY;
-        c1v_clear(q, smem, (int)e);
+        c1v_clear<PM>(q, smem, (int)e);
       }
       lds_barrier();
       if (threadIdx.x == 0) nnew = 0;
@@ -2037,19 +2071,9 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       if (live) {
         const uint64_t ri = cur + __popcll(bl & lt);
         uint64_t* dst = dst0 + ri * q.sw;
-        uint64_t rr[C1V_MAXW];
-#pragma unroll
-        for (int k = 0; k < C1V_MAXW; k++) rr[k] = k < q.sw ? row[k] : 0ULL;
-        const bool was = c1v_having(q, rr);
-        if (e >= 0) {
-          const int64_t t = tmin + (int64_t)(rt[e] & ~RT_MATCHED) - 1;
-          rr[2] = t > (int64_t)rr[2] ? (uint64_t)t : rr[2];
-          c1v_combine(q, smem, e, rr);
-        }
-#pragma unroll
-        for (int k = 0; k < C1V_MAXW; k++)
-          if (k < q.sw) dst[k] = rr[k];
-        const bool now = c1v_having(q, rr);
+        bool was, now;
+        const int64_t t = e >= 0 ? tmin + (int64_t)(rt[e] & ~RT_MATCHED) - 1 : 0;
+        c1v_emit<PM>(q, smem, dst, row, e, 0, 0, t, &was, &now);
         nh += q.having.active && now ? 1 : 0;
         if (q.chg)
           q.chg[(uint64_t)p * q.cmax + ri] =
@@ -2077,23 +2101,14 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
           key = kmin + (int64_t)((uint64_t)id >> 32);
           wi = (int64_t)((uint64_t)id & 0x7FFFFFFFull);
         }
-        uint64_t rr[C1V_MAXW];
-#pragma unroll
-        for (int k = 0; k < C1V_MAXW; k++) rr[k] = q.init[k];
-        rr[0] = (uint64_t)key;
-        rr[1] = (uint64_t)((wbase + wi) * q.adv);
-        rr[2] = (uint64_t)(tmin + (int64_t)rv - 1);
-        c1v_combine(q, smem, (int)e, rr);
-#pragma unroll
-        for (int k = 0; k < C1V_MAXW; k++)
-          if (k < q.sw) dst[k] = rr[k];
-        const bool now = c1v_having(q, rr);
+        bool was, now;
+        c1v_emit<PM>(q, smem, dst, nullptr, (int)e, key, (wbase + wi) * q.adv, tmin + (int64_t)rv - 1, &was, &now);
         nh += q.having.active && now ? 1 : 0;
         if (q.chg) q.chg[(uint64_t)p * q.cmax + ri] = (uint8_t)(CHG_TOUCHED | (now ? CHG_NEW : 0));
       }
       if (i < lb1) {
         ids[e] = EMPTY;
-        c1v_clear(q, smem, (int)e);
+        c1v_clear<PM>(q, smem, (int)e);
       }
       cur += __popcll(bl);
     }
@@ -2340,11 +2355,11 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
   // workgroups share a CU
   C1VQ vq0{};
   int v_log2H = 12;
-  bool v_big = false;
+  int v_pm = 0;  // the plane mask when a specialised merge exists for it
   if (val) {
     while (v_log2H > 9 && c1v_layout(a, v_log2H, 8, log2B, &vq0) > 78 * 1024) v_log2H--;
     v_log2H = (int)knob("KHIP_C1V_LOG2H", v_log2H);
-    v_big = knob("KHIP_C1V_AU", 2) >= 4;
+
     vq0.log2P = s.log2P;
     vq0.fbits = fbits;
     vq0.log2H = v_log2H;
@@ -2361,6 +2376,12 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
       if (a->ap.ops[o].kind == OP_ADD_F64) vq0.f64 = 1;
     }
     if (a->ap.col_type[vcol] == KHIP_TYPE_DOUBLE) vq0.f64 = 1;
+    for (int o = 0; o < a->ap.n_ops; o++) {
+      const int k = a->ap.ops[o].kind;
+      v_pm |= k == OP_INC ? PM_STAR : k == OP_INC_VALID ? PM_CNT : k == OP_MIN ? PM_MIN : k == OP_MAX ? PM_MAX : PM_SUM;
+    }
+    v_pm |= PM_SPEC | (vq0.f64 ? PM_F64 : 0);
+    if ((v_pm != PM_C5 && v_pm != PM_C3) || knob("KHIP_C1V_SPEC", 1) == 0) v_pm = 0;
     vq0.size = a->desc.size_ms;
     vq0.adv = adv;
     vq0.fd = fd;
@@ -2393,15 +2414,19 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
       const size_t lds = c1v_layout(a, v_log2H, idw == 0 ? 4 : 8, log2B, &vq);
       vq.cmax = s.cmax;
       vq.chg = a->changelog ? a->chg.as<uint8_t>() : nullptr;
-      // AU 2 at <= 128 VGPRs (two workgroups per CU) or AU 4 at <= 256 (one)
-      auto mk = v_big ? (panes ? (idw == 0 ? k_c1v_merge<512, 4, uint32_t, true, 2> : k_c1v_merge<512, 4, uint64_t, true, 2>)
-                               : (idw == 0 ? k_c1v_merge<512, 4, uint32_t, false, 2> : k_c1v_merge<512, 4, uint64_t, false, 2>))
-                      : (panes ? (idw == 0 ? k_c1v_merge<512, 2, uint32_t, true, 4> : k_c1v_merge<512, 2, uint64_t, true, 4>)
-                               : (idw == 0 ? k_c1v_merge<512, 2, uint32_t, false, 4> : k_c1v_merge<512, 2, uint64_t, false, 4>));
+      // the benchmarks' plane shapes have instantiations of their own (PM_C5, PM_C3), every other
+      // one reads the planes from the parameters; AU 2 at <= 128 VGPRs (two workgroups per CU)
+      auto pick = [&](auto pmc) {
+        constexpr int PMv = decltype(pmc)::value;
+        return panes ? (idw == 0 ? k_c1v_merge<512, 2, uint32_t, true, 4, PMv> : k_c1v_merge<512, 2, uint64_t, true, 4, PMv>)
+                     : (idw == 0 ? k_c1v_merge<512, 2, uint32_t, false, 4, PMv> : k_c1v_merge<512, 2, uint64_t, false, 4, PMv>);
+      };
+      auto mk = v_pm == PM_C5 ? pick(std::integral_constant<int, PM_C5>{})
+                              : (v_pm == PM_C3 ? pick(std::integral_constant<int, PM_C3>{}) : pick(std::integral_constant<int, 0>{}));
       hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       KHIP_TRY(s.c1vq.ensure(sizeof(C1VQ)));
       KHIP_TRY_HIP(hipMemcpyAsync(s.c1vq.p, &vq, sizeof(C1VQ), hipMemcpyHostToDevice, a->stream));
-      const int64_t vgrid = std::min<int64_t>(nwork, (int64_t)s.n_cu * (v_big ? 1 : 2));
+      const int64_t vgrid = std::min<int64_t>(nwork, (int64_t)s.n_cu * 2);
       hipLaunchKernelGGL(mk, dim3(vgrid), dim3(512), lds, a->stream, s.c1vq.as<C1VQ>(), wk, nwork, s.c1bb.as<int64_t>(), cstart, seg,
                          (const ulonglong2*)s.srec.p, pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
                          s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),

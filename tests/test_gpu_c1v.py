@@ -160,6 +160,13 @@ def test_c1v_declines(prod, orc):
     b = abi.HostBatch(wide[0].ts, keys=k, cols=[_values(rng, len(k), "c3_f64")])
     kt = _run(prod, orc, "c3_f64", "tumbling", [b], hint=2_000_000)
     assert kt["c1_declined"] == 1 and kt["c1_pushes"] == 0, kt
+    # a ts span past 2^31 ms at the end of the batch (the last tile only)
+    span = _batches(rng, "sum_i64", 1, 300_000, 20_000, 30_000)[0]
+    ts = span.ts.copy()
+    ts[-1000:] += 1 << 32
+    b = abi.HostBatch(ts, keys=span.keys, cols=[_values(rng, len(ts), "sum_i64")])
+    kt = _run(prod, orc, "sum_i64", "hop3", [b], hint=2_000_000)
+    assert kt["c1_declined"] == 1 and kt["c1_pushes"] == 0, kt
 
 
 def test_c1v_many_groups_subpasses(prod, orc):

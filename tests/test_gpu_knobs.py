@@ -13,9 +13,9 @@ COUNT(*) TUMBLING + HAVING workload against the oracle (table, batch statistics,
 - KHIP_C1_LOG2H=13 / 11: the pipeline's merge with a twice larger LDS table, and with a twice
   smaller one (partitions overflow it: the sub-pass retries);
 - KHIP_C1V=0: value aggregates through the general path instead of the value-record pipeline;
-  KHIP_C1V_AU=4: its merge at 4 records per thread per chunk (<= 256 VGPRs, one workgroup per
-  CU); KHIP_C1V_LOG2H=9: a small LDS table (sub-pass retries, split by key).
-Each case runs COUNT(*) TUMBLING + HAVING and SUM / MIN / MAX of a BIGINT over HOPPING (panes).
+  KHIP_C1V_SPEC=0: its merge without the plane-shape specialisation (SUM(BIGINT) here);
+  KHIP_C1V_LOG2H=9: a small LDS table (sub-pass retries, split by key).
+Each case runs COUNT(*) TUMBLING + HAVING and SUM of a BIGINT + HAVING over HOPPING (panes).
 Dense and sparse key ranges, several pushes (resident rows), late records (the pipeline declines).
 """
 import os
@@ -40,7 +40,7 @@ KNOBS = [
     {"KHIP_C1_LOG2H": "13"},
     {"KHIP_C1_LOG2H": "11"},
     {"KHIP_C1V": "0"},
-    {"KHIP_C1V_AU": "4"},
+    {"KHIP_C1V_SPEC": "0"},
     {"KHIP_C1V_LOG2H": "9"},
 ]
 
@@ -73,7 +73,7 @@ def _check():
         kws = [dict(window_kind="TUMBLING", size_ms=5000, grace_ms=grace, aggs=[("COUNT_STAR", -1)], having=having,
                     capacity_hint=1 << 22),
                dict(window_kind="HOPPING", size_ms=6000, advance_ms=2000, grace_ms=grace, col_types=["INT64"],
-                    aggs=[("SUM", 0), ("MIN", 0), ("MAX", 0)], having={"agg": 0, "op": "GT", "value": 0},
+                    aggs=[("SUM", 0)], having={"agg": 0, "op": "GT", "value": 0},
                     capacity_hint=1 << 22)]
         for kw in kws:
             gd, od = abi.make_agg_desc(**kw), abi.make_agg_desc(**kw)
