@@ -975,8 +975,9 @@ def bench_join(args, lib, rank, world, local):
     for _ in range(max(args.warmup, 1)):
         rows = step()
     rows, elapsed = timed_loop(step, args.steps, world)
-    # khip_table_create: cap = next_pow2(2 x hint) slots of 32 bytes (one INT32 column)
-    info = {"table_bytes": (1 << max(10, (2 * U - 1).bit_length())) * 32}
+    # khip_table_create: cap = next_pow2(2 x hint) slots of 16 bytes (one INT column: the compact
+    # layout, the value inside the meta word); a probe's first read is its 32-byte home pair
+    info = {"table_bytes": (1 << max(10, (2 * U - 1).bit_length())) * 16, "slot_bytes": 16, "home_read_bytes": 32}
     t.close()
     if rank != 0:
         return

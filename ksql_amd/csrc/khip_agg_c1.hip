@@ -34,6 +34,7 @@
 // + the table rows written (32 B per group) — against 16 + 24 + 16 + 8 + rows for the general
 // path (DESIGN.md §(d)).
 #include <algorithm>
+#include <cstdio>
 #include <type_traits>
 #include <vector>
 
@@ -73,6 +74,15 @@ enum {
 };
 
 __device__ __forceinline__ int bits_of(uint64_t v) { return v ? 64 - __clzll((long long)v) : 0; }
+
+// A c1info word another kernel produced (atomics of k_c1_hist / k_c1_scatter, stores of
+// k_c1_check): read with a device-coherent vector load, never through the scalar cache.
+__device__ __forceinline__ int64_t ci_ld(const int64_t* ci, int k) {
+  const uint64_t v = (uint64_t)__hip_atomic_load(&ci[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // uniform: back into scalar registers
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 
 // ------------------------------------------------------------------ k_c1_hist
 // Keys only (8 B/record): the tile's bucket histogram and key range.  Every record i < n counts
@@ -214,8 +224,9 @@ template <int U, int NT, bool WIDE, bool ST>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_c1_scatter(
     const int64_t* __restrict__ keys, const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
     const uint8_t* __restrict__ rv, int64_t n, int64_t nT, int log2B, const uint32_t* __restrict__ offs,
-    uint64_t* __restrict__ srec, int64_t* __restrict__ stepstat, int64_t* __restrict__ tpart,
-    int64_t* __restrict__ ci, const int64_t* __restrict__ st_at, uint32_t* __restrict__ srecT) {
+    uint64_t* __restrict__ srec, int64_t* __restrict__ tilestat, int64_t* __restrict__ tpart,
+    int64_t* __restrict__ ci, const int64_t* __restrict__ st_at, uint32_t* __restrict__ srecT, int64_t size, int64_t adv,
+    FastDiv fd, int64_t grace) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int wsum[NT / 64];
   __shared__ unsigned long long lc[4];
@@ -236,7 +247,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     lt[threadIdx.x][1] = INT32_MAX;
   }
   if (threadIdx.x == 0) lfail = 0;
-  const int64_t kmin = ci[CI_KMIN], T0 = ci[CI_T0];
+  const int64_t kmin = ci_ld(ci, CI_KMIN), T0 = ci_ld(ci, CI_T0);
   const int shift = log2B == 0 ? 64 : 64 - log2B;
   const uint32_t bmask = (uint32_t)(B - 1);
   const int64_t base = t * C1_TILE;
@@ -252,12 +263,25 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
       dk[u] = keys[i];
     }
   };
-  // step st's (records [sb, sb + S)) ts range → stepstat; its LDS slots reset for step st + 2
-  auto publish = [&](int64_t sb, int st) {
-    const int64_t g = (sb / S) * 2;  // global step index
+  // Thread 0 folds each step's accepted-ts range (LDS slots lt[st & 1], reset for step st + 2)
+  // into the tile's late-record summary for k_c1_check: the stream-time maximum, the smallest ts,
+  // the largest stream time every step stays below (bound: the step's earliest window still
+  // open, S/StreamAggregateBuilder.java:272-277) and whether the tile's own running maximum
+  // already passes a step's bound.  The check then needs only the stream time carried INTO the
+  // tile: carry <= bound (and ok) <=> no record of the tile is late.
+  int64_t t_rmax = -1, t_min = INT64_MAX, t_bound = INT64_MAX;
+  bool t_ok = true;
+  auto publish = [&](int64_t, int st) {
     const int mx = lt[st & 1][0], mn = lt[st & 1][1];
-    stepstat[g] = mx == INT32_MIN ? -1 : T0 + mx;  // none accepted: -1, INT64_MAX
-    stepstat[g + 1] = mx == INT32_MIN ? INT64_MAX : T0 + mn;
+    if (mx != INT32_MIN) {
+      const int64_t smx = T0 + mx, smn = T0 + mn;
+      t_rmax = smx > t_rmax ? smx : t_rmax;
+      t_min = smn < t_min ? smn : t_min;
+      const int64_t fw = first_window_start_fd(smn, size, adv, fd) + size;
+      const int64_t b = grace > ((int64_t)1 << 61) ? INT64_MAX : fw + grace - 1;
+      t_bound = b < t_bound ? b : t_bound;
+      t_ok = t_ok && t_rmax <= b;
+    }
     lt[st & 1][0] = INT32_MIN;
     lt[st & 1][1] = INT32_MAX;
   };
@@ -286,7 +310,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
       c_acc += valid;
       const int64_t sx = ST ? st_at[ok[u] ? i : base] : x[u];  // ABI 5 domains: the given stream time
       const int64_t d = x[u] - T0;
-      if (valid && (d <= (int64_t)INT32_MIN || d > (int64_t)INT32_MAX)) lfail = 1;  // rare: an LDS flag, not a loop-carried mask
+      if (valid && (d <= (int64_t)INT32_MIN || d > (int64_t)INT32_MAX)) {  // rare: an LDS flag, not a loop-carried mask
+        lfail = 1;
+#ifdef KHIP_TUNING
+        if (ci[CI_N - 1] == 1 && (threadIdx.x & 63) == 0) printf("[c1 scatter] t %ld i %ld x %ld T0 %ld\n", (long)t, (long)i, (long)x[u], (long)T0);
+#endif
+      }
       if constexpr (ST) {
         const int64_t ds = sx - T0;
         if (valid && (ds <= (int64_t)INT32_MIN || ds > (int64_t)INT32_MAX)) lfail = 1;
@@ -340,6 +369,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     tp[T_APPLIED] = (int64_t)lc[0];  // TUMBLING: one window per accepted record, none late (checked)
     tp[T_LATE] = 0;
     if (lfail) atomicOr((unsigned long long*)&ci[CI_TFAIL], 1ULL);
+    int64_t* ts4 = tilestat + t * 4;
+    ts4[0] = t_rmax;
+    ts4[1] = t_min;
+    ts4[2] = t_bound;
+    ts4[3] = t_ok ? 1 : 0;
   }
 }
 
@@ -352,7 +386,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 // included), the identity width and the refine's chunk list (cstart); reset the counters the
 // merge and commit use.  Declined: nothing persistent is touched.
 __global__ __launch_bounds__(1024) void k_c1_check(
-    const int64_t* __restrict__ stepstat, int64_t nS, int64_t size, int64_t adv, FastDiv fd, int64_t grace,
+    const int64_t* __restrict__ tilestat, int64_t nT, int64_t size, int64_t adv, FastDiv fd, int64_t grace,
     int64_t close0, int fresh, int log2B, int log2P, int wide, int ch, int kbmax, int pbits, const int64_t* __restrict__ bb,
     int* __restrict__ cstart,
     int64_t* __restrict__ ci, int64_t* __restrict__ stream_time, int64_t* __restrict__ res,
@@ -364,26 +398,26 @@ __global__ __launch_bounds__(1024) void k_c1_check(
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (threadIdx.x == 0) lslow = 0;
   const int64_t st0 = *stream_time;
-  // thread j owns steps [j K, (j + 1) K): its maximum, the block's exclusive prefix of those, then
-  // a sequential walk with the running stream time
-  const int64_t K = (nS + 1023) / 1024;
-  const int64_t g0 = threadIdx.x * K, g1 = g0 + K < nS ? g0 + K : nS;
+  // thread j owns tiles [j K, (j + 1) K): their stream-time maximum, the block's exclusive prefix
+  // of those (the stream time carried into each tile), then each tile's summary (k_c1_scatter)
+  const int64_t K = (nT + 1023) / 1024;
+  const int64_t g0 = threadIdx.x * K, g1 = g0 + K < nT ? g0 + K : nT;
   int64_t m = -1;
-  for (int64_t g = g0; g < g1; g++) m = stepstat[2 * g] > m ? stepstat[2 * g] : m;
+  for (int64_t g = g0; g < g1; g++) m = tilestat[4 * g] > m ? tilestat[4 * g] : m;
   const int64_t incl = wave_incl_max(m);
   if (lane == 63) wmx[wave] = incl;
   __syncthreads();
   int64_t pre = st0;
   for (int w = 0; w < wave; w++) pre = wmx[w] > pre ? wmx[w] : pre;
   const int64_t excl = __shfl_up(incl, 1, 64);
-  int64_t run = lane == 0 ? pre : (excl > pre ? excl : pre);  // stream time before step g0
+  int64_t run = lane == 0 ? pre : (excl > pre ? excl : pre);  // stream time before tile g0
   int64_t gmn = INT64_MAX, gmx = -1;
   bool slow = false;
   for (int64_t g = g0; g < g1; g++) {
-    const int64_t mx = stepstat[2 * g], mn = stepstat[2 * g + 1];
+    const int64_t* t4 = tilestat + 4 * g;
+    const int64_t mx = t4[0], mn = t4[1];
     if (mn != INT64_MAX) {
-      const int64_t smax = run > mx ? run : mx;
-      slow |= !(first_window_start(mn, size, adv) + size > smax - grace);
+      slow |= t4[3] == 0 || run > t4[2];  // a record of the tile may be late
       gmn = mn < gmn ? mn : gmn;
     }
     run = mx > run ? mx : run;
@@ -415,12 +449,17 @@ __global__ __launch_bounds__(1024) void k_c1_check(
     mxc = lnch[b] > mxc ? lnch[b] : mxc;
   }
   cstart[B] = acc;
-  const int64_t kmin = ci[CI_KMIN], kmax = ci[CI_KMAX];
+  const int64_t kmin = ci_ld(ci, CI_KMIN), kmax = ci_ld(ci, CI_KMAX);
+  const bool tfail = ci_ld(ci, CI_TFAIL) != 0;
   ci[CI_KMIN] = INT64_MAX;  // ready for the next push's atomics
   ci[CI_KMAX] = INT64_MIN;
-  const bool tfail = ci[CI_TFAIL] != 0;
   ci[CI_TFAIL] = 0;
   bool ok = !lslow && !tfail && mxc <= C1_SEGMAX && kmax >= kmin;
+#ifdef KHIP_TUNING
+  if (ci[CI_N - 1] == 1)  // debug (tuning build, KHIP_C1_DEBUG=1): the decision's inputs
+    printf("[c1 check] tfail %d slow %d mxc %d kmin %ld kmax %ld gmn %ld gmx %ld T0 %ld st0 %ld nT %ld\n", (int)tfail,
+           (int)lslow, mxc, (long)kmin, (long)kmax, (long)gmn, (long)gmx, (long)ci[CI_T0], (long)st0, (long)nT);
+#endif
   const uint64_t krange = kmax >= kmin ? (uint64_t)kmax - (uint64_t)kmin : 0;
   const bool fits = krange < ((1ULL << kbmax) - 1);  // compact records: 32 key bits (value records 31)
   ci[CI_FITS] = fits ? 1 : 0;
@@ -479,9 +518,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const uint64_t* __restrict__ srcA, const int64_t* __restrict__ bb, const int* __restrict__ cstart, int log2B,
     int log2P, int fbits, uint64_t* __restrict__ srec, uint16_t* __restrict__ seg, const int64_t* __restrict__ ci,
     const uint32_t* __restrict__ srcAT, uint32_t* __restrict__ srecT) {
-  if (ci[CI_GATE] == 0) return;
+  if (ci_ld(ci, CI_GATE) == 0) return;
   const int w = blockIdx.x;
-  if (w >= (int)ci[CI_NCHUNK]) return;
+  if (w >= (int)ci_ld(ci, CI_NCHUNK)) return;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int lb, lnv;
   __shared__ int wsum[NT / 64];
@@ -502,7 +541,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const int64_t lo = bb[b] + (int64_t)(w - cstart[b]) * C1_CH;
   const int64_t bend = bb[b + 1];
   const int len = (int)(bend - lo < C1_CH ? bend - lo : C1_CH);
-  const int64_t kmin = ci[CI_KMINC];
+  const int64_t kmin = ci_ld(ci, CI_KMINC);
   const int shift = 64 - log2P;
   uint64_t r[U];
   uint32_t f[U], rank[U], t32[U];
@@ -566,6 +605,26 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   }
 }
 
+// KHIP_AGG_PROBE (tuning build): wall-clock time per merge phase summed over the persistent
+// workgroups (thread 0's view): 0 item start + eviction, 1 records, 2 pane fold, 3 mark + count
+// + reserve, 4 write-out.  dbg == nullptr in every other run.
+#ifdef KHIP_TUNING
+#define C1M_T(k)                                                                        \
+  do {                                                                                  \
+    if (dbg && threadIdx.x == 0) {                                                      \
+      const unsigned long long now_ = wall_clock64();                                   \
+      atomicAdd(&dbg[(k)], now_ - t_last);                                              \
+      t_last = now_;                                                                    \
+    }                                                                                   \
+  } while (0)
+#define C1M_T0 unsigned long long t_last = dbg ? wall_clock64() : 0ULL
+#else  // the release build carries no probe (its registers would cost the merge)
+#define C1M_T(k) \
+  do {           \
+  } while (0)
+#define C1M_T0 (void)dbg
+#endif
+
 // ------------------------------------------------------------------ k_c1_merge
 struct C1Q {
   int32_t log2P, fbits, log2H, sw, hv_active, hv_op, hmax;
@@ -622,10 +681,11 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     const int64_t* __restrict__ cnt, unsigned long long* __restrict__ newcnt, uint8_t* __restrict__ fail,
     unsigned long long* __restrict__ need, int64_t close0, uint64_t* __restrict__ closed,
     unsigned long long* __restrict__ closed_n, const int64_t* __restrict__ ci, unsigned long long* __restrict__ hnew,
-    unsigned long long* __restrict__ hclosed, uint32_t* __restrict__ prn, const uint32_t* __restrict__ srecT) {
-  if (ci[CI_GATE] == 0) return;
-  if ((ci[CI_WIDE] != 0) != WIDE) return;                            // the other record format's
-  if (!WIDE && (ci[CI_ID32] != 0) != (sizeof(ID) == 4)) return;     // the other identity width's
+    unsigned long long* __restrict__ hclosed, uint32_t* __restrict__ prn, const uint32_t* __restrict__ srecT,
+    unsigned long long* __restrict__ dbg) {
+  if (ci_ld(ci, CI_GATE) == 0) return;
+  if ((ci_ld(ci, CI_WIDE) != 0) != WIDE) return;                            // the other record format's
+  if (!WIDE && (ci_ld(ci, CI_ID32) != 0) != (sizeof(ID) == 4)) return;     // the other identity width's
   static_assert(!WIDE || sizeof(ID) == 8, "wide records use 64-bit identities");
   constexpr int NW = NT / 64;
   constexpr ID EMPTY = (ID)~(ID)0;
@@ -646,15 +706,16 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
   __shared__ int wsum[NW];
   __shared__ unsigned long long lbase;
   const int F = 1 << q.fbits;
-  const int64_t wbase = ci[CI_WBASE], whi = ci[CI_WHI], T0 = ci[CI_T0], tmin = ci[CI_TMIN];
-  const int wbits = (int)ci[CI_WBITS];
-  const int64_t kmin = ci[CI_KMINC];
-  const uint64_t krange = (uint64_t)ci[CI_KRANGE];
+  const int64_t wbase = ci_ld(ci, CI_WBASE), whi = ci_ld(ci, CI_WHI), T0 = ci_ld(ci, CI_T0), tmin = ci_ld(ci, CI_TMIN);
+  const int wbits = (int)ci_ld(ci, CI_WBITS);
+  const int64_t kmin = ci_ld(ci, CI_KMINC);
+  const uint64_t krange = (uint64_t)ci_ld(ci, CI_KRANGE);
   const int32_t tmin32 = (int32_t)(tmin - T0);
   const int64_t wstart = wbase * q.adv;  // the first window's start: every record ts >= it
-  const bool r32 = ci[CI_TMAX] - wstart < ((int64_t)1 << 32);
+  const bool r32 = ci_ld(ci, CI_TMAX) - wstart < ((int64_t)1 << 32);
   const uint32_t tsh32 = (uint32_t)(T0 - wstart);  // ts - wstart = (uint32) t32 + tsh32
   const bool evict = close0 != INT64_MIN;
+  C1M_T0;
   const uint32_t dummy = (uint32_t)H + (uint32_t)lane;
   for (int i = threadIdx.x; i < H + 64; i += NT) {
     ids[i] = EMPTY;
@@ -889,6 +950,7 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       }
       lds_barrier();
     }
+    C1M_T(0);
     // 1. records → delta entries, two register sets (chunk c + 1 in flight while c is applied;
     //    chunk 0 was loaded with the item's segments)
     // R32: the push's record times relative to the first window's start fit 32 bits (a 32-bit
@@ -982,6 +1044,7 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       prep(pr, nx);
       load01(nx);
     }
+    C1M_T(1);
     const int nl = nnew < H ? nnew : H;
     if (lovf || nnew > q.hmax) {  // more groups than the table takes: retried with 2x sub-passes
       if (threadIdx.x == 0) fail[p] |= 1;
@@ -1057,6 +1120,7 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       lds_barrier();
       continue;
     }
+    C1M_T(3);
     // 4. write: resident rows (merged), then the wave's new entries (ballot ranks: consecutive rows)
     uint64_t* dst0 = (isel ? buf0 : buf1) + (uint64_t)p * q.cmax * q.sw;
     uint64_t cur = lbase + (uint64_t)wave_before;
@@ -1137,6 +1201,7 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       if (lane == 0 && nh) atomicAdd(&hnew[p], (unsigned long long)nh);
     }
     lds_barrier();  // the table is clear for the next item
+    C1M_T(4);
     if (threadIdx.x == 0) nnew = 0;
     lds_barrier();
   }
@@ -1221,8 +1286,9 @@ template <int U, int NT, bool ST>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_c1v_scatter(
     const int64_t* __restrict__ keys, const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
     const uint8_t* __restrict__ rv, C1VCol vc, int64_t n, int64_t nT, int log2B, const uint32_t* __restrict__ offs,
-    ulonglong2* __restrict__ srec, int64_t* __restrict__ stepstat, int64_t* __restrict__ tpart,
-    int64_t* __restrict__ ci, const int64_t* __restrict__ st_at, int64_t size, int64_t adv, FastDiv fd, int hop) {
+    ulonglong2* __restrict__ srec, int64_t* __restrict__ tilestat, int64_t* __restrict__ tpart,
+    int64_t* __restrict__ ci, const int64_t* __restrict__ st_at, int64_t size, int64_t adv, FastDiv fd, int hop,
+    int64_t grace) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int wsum[NT / 64];
   __shared__ unsigned long long lc[5];
@@ -1247,7 +1313,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     lt[threadIdx.x][1] = INT32_MAX;
   }
   if (threadIdx.x == 0) lfail = 0;
-  const int64_t kmin = ci[CI_KMIN], T0 = ci[CI_T0];
+  const int64_t kmin = ci_ld(ci, CI_KMIN), T0 = ci_ld(ci, CI_T0);
   const int shift = log2B == 0 ? 64 : 64 - log2B;
   const uint32_t bmask = (uint32_t)(B - 1);
   const int64_t base = t * C1_TILE;
@@ -1264,11 +1330,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
       v[u] = vc.type == KHIP_TYPE_INT32 ? (int64_t)((const int32_t*)vc.data)[i] : ((const int64_t*)vc.data)[i];
     }
   };
-  auto publish = [&](int64_t sb, int st) {
-    const int64_t g = (sb / S) * 2;
+  int64_t t_rmax = -1, t_min = INT64_MAX, t_bound = INT64_MAX;  // the tile's summary (k_c1_scatter)
+  bool t_ok = true;
+  auto publish = [&](int64_t, int st) {
     const int mx = lt[st & 1][0], mn = lt[st & 1][1];
-    stepstat[g] = mx == INT32_MIN ? -1 : T0 + mx;
-    stepstat[g + 1] = mx == INT32_MIN ? INT64_MAX : T0 + mn;
+    if (mx != INT32_MIN) {
+      const int64_t smx = T0 + mx, smn = T0 + mn;
+      t_rmax = smx > t_rmax ? smx : t_rmax;
+      t_min = smn < t_min ? smn : t_min;
+      const int64_t fw = first_window_start_fd(smn, size, adv, fd) + size;
+      const int64_t b = grace > ((int64_t)1 << 61) ? INT64_MAX : fw + grace - 1;
+      t_bound = b < t_bound ? b : t_bound;
+      t_ok = t_ok && t_rmax <= b;
+    }
     lt[st & 1][0] = INT32_MIN;
     lt[st & 1][1] = INT32_MAX;
   };
@@ -1295,7 +1369,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
       c_bt += ok[u] && kok && rok && x[u] < 0;
       c_acc += valid;
       const int64_t d = x[u] - T0;
-      if (valid && (d <= (int64_t)INT32_MIN || d > (int64_t)INT32_MAX)) lfail = 1;  // rare: an LDS flag, not a loop-carried mask
+      if (valid && (d <= (int64_t)INT32_MIN || d > (int64_t)INT32_MAX)) {  // rare: an LDS flag, not a loop-carried mask
+        lfail = 1;
+#ifdef KHIP_TUNING
+        if (ci[CI_N - 1] == 1 && (threadIdx.x & 63) == 0) printf("[c1 scatter] t %ld i %ld x %ld T0 %ld\n", (long)t, (long)i, (long)x[u], (long)T0);
+#endif
+      }
       if constexpr (ST) {
         const int64_t ds = st_at[ii] - T0;
         if (valid && (ds <= (int64_t)INT32_MIN || ds > (int64_t)INT32_MAX)) lfail = 1;
@@ -1349,6 +1428,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     tp[T_APPLIED] = hop ? (int64_t)lc[4] : (int64_t)lc[0];  // none late (checked)
     tp[T_LATE] = 0;
     if (lfail) atomicOr((unsigned long long*)&ci[CI_TFAIL], 1ULL);
+    int64_t* ts4 = tilestat + t * 4;
+    ts4[0] = t_rmax;
+    ts4[1] = t_min;
+    ts4[2] = t_bound;
+    ts4[3] = t_ok ? 1 : 0;
   }
 }
 
@@ -1358,9 +1442,9 @@ template <int U, int NT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_c1v_refine(
     const ulonglong2* __restrict__ srcA, const int64_t* __restrict__ bb, const int* __restrict__ cstart, int log2B,
     int log2P, int fbits, ulonglong2* __restrict__ srec, uint16_t* __restrict__ seg, const int64_t* __restrict__ ci) {
-  if (ci[CI_GATE] == 0) return;
+  if (ci_ld(ci, CI_GATE) == 0) return;
   const int w = blockIdx.x;
-  if (w >= (int)ci[CI_NCHUNK]) return;
+  if (w >= (int)ci_ld(ci, CI_NCHUNK)) return;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int lb, lnv;
   __shared__ int wsum[NT / 64];
@@ -1381,7 +1465,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const int64_t lo = bb[b] + (int64_t)(w - cstart[b]) * CH;
   const int64_t bend = bb[b + 1];
   const int len = (int)(bend - lo < CH ? bend - lo : CH);
-  const int64_t kmin = ci[CI_KMINC];
+  const int64_t kmin = ci_ld(ci, CI_KMINC);
   const int shift = 64 - log2P;
   ulonglong2 r[U];
   uint32_t f[U], rank[U];
@@ -1592,9 +1676,9 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
     const int64_t* __restrict__ cnt, unsigned long long* __restrict__ newcnt, uint8_t* __restrict__ fail,
     unsigned long long* __restrict__ need, int64_t close0, uint64_t* __restrict__ closed,
     unsigned long long* __restrict__ closed_n, const int64_t* __restrict__ ci, unsigned long long* __restrict__ hnew,
-    unsigned long long* __restrict__ hclosed, uint32_t* __restrict__ prn) {
-  if (ci[CI_GATE] == 0) return;
-  if ((ci[CI_ID32] != 0) != (sizeof(ID) == 4)) return;  // the other identity width's
+    unsigned long long* __restrict__ hclosed, uint32_t* __restrict__ prn, unsigned long long* __restrict__ dbg) {
+  if (ci_ld(ci, CI_GATE) == 0) return;
+  if ((ci_ld(ci, CI_ID32) != 0) != (sizeof(ID) == 4)) return;  // the other identity width's
   const C1VQ& q = *qp;  // in device memory: its fields are loaded where used (SGPR pressure)
   constexpr int NW = NT / 64;
   constexpr ID EMPTY = (ID)~(ID)0;
@@ -1614,15 +1698,16 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
   __shared__ int wsum[NW];
   __shared__ unsigned long long lbase;
   const int F = 1 << q.fbits;
-  const int64_t wbase = ci[CI_WBASE], whi = ci[CI_WHI], T0 = ci[CI_T0], tmin = ci[CI_TMIN];
-  const int wbits = (int)ci[CI_WBITS];
-  const int64_t kmin = ci[CI_KMINC];
-  const uint64_t krange = (uint64_t)ci[CI_KRANGE];
+  const int64_t wbase = ci_ld(ci, CI_WBASE), whi = ci_ld(ci, CI_WHI), T0 = ci_ld(ci, CI_T0), tmin = ci_ld(ci, CI_TMIN);
+  const int wbits = (int)ci_ld(ci, CI_WBITS);
+  const int64_t kmin = ci_ld(ci, CI_KMINC);
+  const uint64_t krange = (uint64_t)ci_ld(ci, CI_KRANGE);
   const int32_t tmin32 = (int32_t)(tmin - T0);
   const int64_t wstart = wbase * q.adv;
-  const bool r32 = ci[CI_TMAX] - wstart < ((int64_t)1 << 32);
+  const bool r32 = ci_ld(ci, CI_TMAX) - wstart < ((int64_t)1 << 32);
   const uint32_t tsh32 = (uint32_t)(T0 - wstart);
   const bool evict = close0 != INT64_MIN;
+  C1M_T0;
   const uint32_t dummy = (uint32_t)H + (uint32_t)lane;
   for (int i = threadIdx.x; i < H + 64; i += NT) {
     ids[i] = EMPTY;
@@ -1854,6 +1939,7 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       }
       lds_barrier();
     }
+    C1M_T(0);
     // 1. records → their pane (window) entries: the AU identities' CASes back to back, then the
     //    collisions probe on together (as k_c1_merge)
     auto apply = [&](const ulonglong2 (&xr)[AU], int64_t l0, auto R32) {
@@ -1944,6 +2030,7 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       prep(pr, nx);
       load01(nx);
     }
+    C1M_T(1);
     // 1b. panes → their windows (the window entries are claimed as a record's would be)
     if (PANES && q.fan > 1 && !lovf && nnew <= q.hmax) {
       const int nn0 = nnew;
@@ -1978,6 +2065,7 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       }
       lds_barrier();
     }
+    C1M_T(2);
     const int nl = nnew < H ? nnew : H;
     if (lovf || nnew > q.hmax) {
       if (threadIdx.x == 0) fail[p] |= 1;
@@ -2051,6 +2139,7 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       lds_barrier();
       continue;
     }
+    C1M_T(3);
     // 4. write: resident rows (merged), then the wave's new window entries
     uint64_t* dst0 = (isel ? buf0 : buf1) + (uint64_t)p * q.cmax * q.sw;
     uint64_t cur = lbase + (uint64_t)wave_before;
@@ -2117,6 +2206,7 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       if (lane == 0 && nh) atomicAdd(&hnew[p], (unsigned long long)nh);
     }
     lds_barrier();
+    C1M_T(4);
     if (threadIdx.x == 0) nnew = 0;
     lds_barrier();
   }
@@ -2233,8 +2323,7 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
   KHIP_TRY(s.c1bb.ensure((size_t)(B + 1) * 8));
   const size_t seg_bytes = ((size_t)nchunk_max * (F + 1) * 2 + 255) & ~(size_t)255;  // cstart 256-B aligned
   KHIP_TRY(s.c1seg.ensure(seg_bytes + (size_t)(B + 1) * 4));
-  const int64_t nS = ceil_div(n, (val ? UV : 8) * C1_NT);  // scatter steps
-  KHIP_TRY(s.tilemax.ensure(nS * 16));      // per step: accepted ts max, min
+  KHIP_TRY(s.tilemax.ensure(nT * 32));  // per tile: stream-time max, smallest ts, late bound, ok
   KHIP_TRY(s.tpart.ensure(nT * 8 * T_NPART));
   KHIP_TRY(s.scan_tmpB.ensure((size_t)TC * B * 8));
   KHIP_TRY(s.prn.ensure((size_t)P * 4));
@@ -2254,6 +2343,13 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     KHIP_TRY_HIP(hipMemcpy(s.c1info.p, init, sizeof(init), hipMemcpyHostToDevice));
   }
   int64_t* ci = s.c1info.as<int64_t>();
+#ifdef KHIP_TUNING
+  {
+    const int64_t dbg = knob("KHIP_C1_DEBUG", 0);
+    KHIP_TRY_HIP(hipMemcpyAsync(ci + CI_N - 1, &dbg, 8, hipMemcpyHostToDevice, a->stream));
+    KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  }
+#endif
   int* cstart = (int*)(s.c1seg.as<char>() + seg_bytes);
   uint16_t* seg = s.c1seg.as<uint16_t>();
   const int64_t adv = a->desc.advance_ms;
@@ -2298,7 +2394,7 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     if (lds > 64 * 1024) hipFuncSetAttribute((const void*)sk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(sk, dim3(nT), dim3(C1_NT), lds, a->stream, keys, ts, kv, rv, vc, n, nT, log2B,
                        s.c1hist.as<uint32_t>(), (ulonglong2*)s.srecA.p, s.tilemax.as<int64_t>(), s.tpart.as<int64_t>(),
-                       ci, st_at, a->desc.size_ms, adv, fd, a->desc.size_ms != adv ? 1 : 0);
+                       ci, st_at, a->desc.size_ms, adv, fd, a->desc.size_ms != adv ? 1 : 0, a->grace);
     KHIP_TRY_HIP(hipGetLastError());
   } else {
     constexpr int U = 8;
@@ -2308,11 +2404,11 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     if (lds > 64 * 1024) hipFuncSetAttribute((const void*)sk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(sk, dim3(nT), dim3(C1_NT), lds, a->stream, keys, ts, kv, rv, n, nT, log2B,
                        s.c1hist.as<uint32_t>(), s.srecA.as<uint64_t>(), s.tilemax.as<int64_t>(), s.tpart.as<int64_t>(),
-                       ci, st_at, srecAT);
+                       ci, st_at, srecAT, a->desc.size_ms, adv, fd, a->grace);
     KHIP_TRY_HIP(hipGetLastError());
   }
   // 4. accept or decline
-  hipLaunchKernelGGL(k_c1_check, dim3(1), dim3(1024), 0, a->stream, s.tilemax.as<int64_t>(), nS,
+  hipLaunchKernelGGL(k_c1_check, dim3(1), dim3(1024), 0, a->stream, s.tilemax.as<int64_t>(), nT,
                      a->desc.size_ms, adv, fd, a->grace, close0, s.res_fresh ? 1 : 0, log2B, s.log2P, wide ? 1 : 0,
                      val ? C1V_CH : C1_CH, val ? 31 : 32, pbits, s.c1bb.as<int64_t>(), cstart, ci, a->stream_time.as<int64_t>(), s.res.as<int64_t>(),
                      s.ctr.as<unsigned long long>(), s.closed_ctr.as<unsigned long long>(),
@@ -2400,7 +2496,14 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     KHIP_TRY_HIP(hipMemcpyAsync(s.work.p, work.data(), work.size() * 4, hipMemcpyHostToDevice, a->stream));
   }
   std::vector<uint8_t> host_fail;
+  const bool probe = knob("KHIP_AGG_PROBE", 0) != 0;
+  DevBuf dbgbuf;
+  if (probe) {
+    KHIP_TRY(dbgbuf.ensure(64));
+    KHIP_TRY_HIP(hipMemsetAsync(dbgbuf.p, 0, 64, a->stream));
+  }
   for (int pass = 0;; pass++) {
+    unsigned long long* dbg = probe && pass == 0 ? dbgbuf.as<unsigned long long>() : nullptr;
     cq.cmax = s.cmax;
     cq.chg = a->changelog ? a->chg.as<uint8_t>() : nullptr;
     if (pass > 0) KHIP_TRY_HIP(hipMemsetAsync(s.ctr.p, 0, 24, a->stream));
@@ -2432,7 +2535,7 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
                          s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
                          s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
                          s.closed_ctr.as<unsigned long long>(), ci,
-                         s.hnew.as<unsigned long long>(), s.ctr.as<unsigned long long>() + 12, s.prn.as<uint32_t>());
+                         s.hnew.as<unsigned long long>(), s.ctr.as<unsigned long long>() + 12, s.prn.as<uint32_t>(), dbg);
     }
     for (int idw = wide ? 1 : 0; idw < 2 && !val; idw++) {
       auto mk = wide ? k_c1_merge<512, 3, uint64_t, true>
@@ -2445,7 +2548,7 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
                          s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
                          s.closed_ctr.as<unsigned long long>(), ci,
                          s.hnew.as<unsigned long long>(), s.ctr.as<unsigned long long>() + 12, s.prn.as<uint32_t>(),
-                         (const uint32_t*)srecT);
+                         (const uint32_t*)srecT, dbg);
     }
     KHIP_TRY_HIP(hipGetLastError());
     const int nl = pass == 0 ? P : (int)plist.size();
@@ -2474,6 +2577,15 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
       return KHIP_OK;
     }
     if (pass == 0 && wide && hci[CI_FITS]) s.c1_wide = false;  // compact records fit again next time
+    if (dbg) {
+      unsigned long long ph[8] = {};
+      if (hipMemcpy(ph, dbgbuf.p, sizeof(ph), hipMemcpyDeviceToHost) == hipSuccess) {
+        const double g = (double)std::min<int64_t>(P, 2 * s.n_cu) * 100.0;  // 100 MHz ticks → us per workgroup
+        fprintf(stderr, "[%s merge probe] per workgroup (us): start+evict %.1f records %.1f fold %.1f "
+                "mark+count+reserve %.1f write %.1f\n", val ? "c1v" : "c1", ph[0] / g, ph[1] / g, ph[2] / g, ph[3] / g,
+                ph[4] / g);
+      }
+    }
     added_total += (int64_t)c2[0];
     if (c2[1] == 0) break;
     if (pass > 24) return fail(KHIP_E_DEVICE, "partitioned aggregation could not place the batch");

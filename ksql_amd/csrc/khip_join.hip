@@ -10,7 +10,9 @@
 //   meta: bit63 = claimed by this upsert batch (bits 0..39 = batch row),
 //         bit62 = resident (key valid), bit61 = live (has a value; 0 = deleted),
 //         bits 0..31 = null mask of the right columns (when resident).
-//   For a table of 1 payload column a slot is 32 B: one probe touches one line.
+//   COMPACT (one INT payload column, e.g. C4's level): 16-byte slots [0] key [1] meta with the
+//   value in bits 0..31 and its NULL flag in bit 32; the last-writer tags live in a separate
+//   array (read only by the upserts), so a probe's home pair is one 32-byte read.
 //
 // Upsert (arrival order, last writer wins, tombstone deletes):
 //   k_upsert_claim   find-or-claim each key's slot (CAS on meta, claim references the
@@ -72,17 +74,30 @@ __device__ __forceinline__ uint64_t jld(const uint64_t* p) {
 
 __device__ __forceinline__ uint64_t key_hash(int64_t k) { return mix64((uint64_t)k ^ 0x2545F4914F6CDD1DULL); }
 
+// A key's home slot: always the first of an aligned PAIR of slots (64 bytes for one payload
+// column), so one probe's first read brings two slots of its linear-probe sequence — at the
+// tables' load factor (<= 1/2) nearly every lookup ends inside its home pair.
+__device__ __forceinline__ uint64_t home_slot(int64_t k, uint64_t mask) { return key_hash(k) & mask & ~1ULL; }
+
+// Payload column c of a slot and its NULL flag, in either layout (cmp: COMPACT).
+__device__ __forceinline__ uint64_t slot_col(const uint64_t* s, uint64_t meta, int c, bool cmp) {
+  return cmp ? (uint64_t)(int64_t)(int32_t)(uint32_t)meta : s[3 + c];
+}
+__device__ __forceinline__ bool slot_null(uint64_t meta, int c, bool cmp) {
+  return cmp ? ((meta >> 32) & 1ULL) != 0 : ((meta >> c) & 1ULL) != 0;
+}
+
 __global__ __launch_bounds__(256) void k_upsert_claim(uint64_t* __restrict__ table, uint64_t mask, int sw,
                                                       const int64_t* __restrict__ keys,
                                                       const uint8_t* __restrict__ kv, int64_t n,
                                                       int64_t* __restrict__ slot_of, int* __restrict__ fail,
                                                       unsigned long long* __restrict__ new_keys,
-                                                      int64_t* __restrict__ claimed) {
+                                                      int64_t* __restrict__ claimed, uint64_t* __restrict__ tags) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     slot_of[i] = -1;
     if (!bit_get(kv, i)) continue;
     const int64_t key = keys[i];
-    uint64_t slot = key_hash(key) & mask;
+    uint64_t slot = home_slot(key, mask);
     const uint64_t claim = M_CLAIM | (uint64_t)i;
     bool done = false;
     for (int probe = 0; probe < JMAX_PROBE && !done; probe++) {
@@ -106,7 +121,7 @@ __global__ __launch_bounds__(256) void k_upsert_claim(uint64_t* __restrict__ tab
       }
       if (done) {
         slot_of[i] = (int64_t)slot;
-        atomicMax((unsigned long long*)&s[2], (unsigned long long)(i + 1));
+        atomicMax((unsigned long long*)(tags ? &tags[slot] : &s[2]), (unsigned long long)(i + 1));
       } else {
         slot = (slot + 1) & mask;
       }
@@ -174,19 +189,31 @@ __device__ __forceinline__ bool dense_cell(const JDense& d, uint64_t raw, bool i
 __global__ __launch_bounds__(256) void k_upsert_apply(uint64_t* __restrict__ table, int sw,
                                                       const int64_t* __restrict__ slot_of,
                                                       const uint8_t* __restrict__ rv, int64_t n, int ncols, const int32_t* __restrict__ types_dev, JCols cols,
-                                                      JDense dn) {
+                                                      JDense dn, uint64_t* __restrict__ tags) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t slot = slot_of[i];
     if (slot < 0) continue;
     uint64_t* s = table + slot * (uint64_t)sw;
-    if (s[2] != (uint64_t)(i + 1)) continue;  // not the last writer of this key
-    s[2] = 0;  // only the winner matches: clearing cannot change another row's decision
+    uint64_t* tg = tags ? &tags[slot] : &s[2];
+    if (*tg != (uint64_t)(i + 1)) continue;  // not the last writer of this key
+    *tg = 0;  // only the winner matches: clearing cannot change another row's decision
     const int64_t kidx = (int64_t)s[0] - dn.kmin;
     const bool kin = dn.active && (int64_t)s[0] >= dn.kmin && kidx < dn.nkeys;
     if (dn.active && !kin) *dn.invalid = 1;
     if (!bit_get(rv, i)) {
       s[1] = M_RESIDENT;  // tombstone: delete
       if (kin) dense_store(dn, kidx, 0);
+      continue;
+    }
+    if (tags) {  // COMPACT: the INT value in the meta word
+      const bool v = bit_get(cols.valid[0], i);
+      const int32_t x = v ? ((const int32_t*)cols.data[0])[i] : 0;
+      s[1] = M_RESIDENT | M_LIVE | (v ? (uint64_t)(uint32_t)x : (1ULL << 32));
+      if (kin) {
+        uint64_t cell;
+        if (dense_cell(dn, (uint64_t)(int64_t)x, !v, &cell)) dense_store(dn, kidx, cell);
+        else *dn.invalid = 1;
+      }
       continue;
     }
     uint64_t nullmask = 0;
@@ -212,7 +239,7 @@ __global__ __launch_bounds__(256) void k_upsert_apply(uint64_t* __restrict__ tab
 
 // Ranges of the live slots: [kmin, kmax, vmin, vmax, live] (value over non-null values).
 __global__ __launch_bounds__(256) void k_table_ranges(const uint64_t* __restrict__ table, int64_t cap, int sw,
-                                                      unsigned long long* __restrict__ out) {
+                                                      unsigned long long* __restrict__ out, int cmp) {
   int64_t kmn = INT64_MAX, kmx = INT64_MIN, vmn = INT64_MAX, vmx = INT64_MIN, live = 0;
   for (int64_t slot = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; slot < cap;
        slot += (int64_t)gridDim.x * blockDim.x) {
@@ -223,8 +250,8 @@ __global__ __launch_bounds__(256) void k_table_ranges(const uint64_t* __restrict
     kmn = k < kmn ? k : kmn;
     kmx = k > kmx ? k : kmx;
     live++;
-    if (!(m & 1)) {
-      const int64_t v = (int64_t)s[3];
+    if (!slot_null(m, 0, cmp)) {
+      const int64_t v = (int64_t)slot_col(s, m, 0, cmp);
       vmn = v < vmn ? v : vmn;
       vmx = v > vmx ? v : vmx;
     }
@@ -250,14 +277,15 @@ __global__ __launch_bounds__(256) void k_table_ranges(const uint64_t* __restrict
 }
 
 // Fill the dense index from the live slots (cells of absent keys were zeroed).
-__global__ __launch_bounds__(256) void k_dense_build(const uint64_t* __restrict__ table, int64_t cap, int sw, JDense dn) {
+__global__ __launch_bounds__(256) void k_dense_build(const uint64_t* __restrict__ table, int64_t cap, int sw, JDense dn,
+                                                     int cmp) {
   for (int64_t slot = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; slot < cap;
        slot += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t* s = table + slot * (uint64_t)sw;
     const uint64_t m = s[1];
     if (!(m & M_LIVE)) continue;
     uint64_t cell;
-    if (dense_cell(dn, s[3], m & 1, &cell)) dense_store(dn, (int64_t)s[0] - dn.kmin, cell);
+    if (dense_cell(dn, slot_col(s, m, 0, cmp), slot_null(m, 0, cmp), &cell)) dense_store(dn, (int64_t)s[0] - dn.kmin, cell);
     else *dn.invalid = 1;
   }
 }
@@ -295,9 +323,9 @@ struct JOut {
   int64_t* slot_out;  // host path: -1 not emitted, 0 emitted miss, slot + 1 emitted hit
 };
 
-__device__ __forceinline__ bool where_ok_raw(uint64_t raw, uint64_t meta, const JWhere& w) {
+__device__ __forceinline__ bool where_ok_raw(uint64_t raw, uint64_t meta, const JWhere& w, bool cmp = false) {
   if (!w.active) return true;
-  if (meta & (1ULL << w.col)) return false;  // NULL never satisfies
+  if (slot_null(meta, w.col, cmp)) return false;  // NULL never satisfies
   int c;
   if (w.type == KHIP_TYPE_DOUBLE) {
     double d;
@@ -324,7 +352,7 @@ __device__ __forceinline__ bool where_ok_raw(uint64_t raw, uint64_t meta, const 
 // PR rows (32 bytes: key, meta, tag, first column — one line) is loaded before any is
 // examined, so a wave keeps 4 x PR independent HBM reads in flight: the table is far larger
 // than the caches and every probe is a random line, so the kernel is latency/MLP-bound.
-template <int PR>
+template <int PR, bool CMP>
 __global__ __launch_bounds__(256) void k_probe(const uint64_t* __restrict__ table, uint64_t mask, int sw,
                                                const int64_t* __restrict__ keys, const int64_t* __restrict__ ts,
                                                const uint8_t* __restrict__ kv, const uint8_t* __restrict__ rv,
@@ -336,7 +364,8 @@ __global__ __launch_bounds__(256) void k_probe(const uint64_t* __restrict__ tabl
   int64_t key[PR];
   bool act[PR];
   uint64_t slot[PR];
-  longlong2 h0[PR], h1[PR];
+  longlong2 h0[PR], g0[PR];  // (key, meta) of the home pair's two slots
+  uint64_t c0a[PR], c0b[PR];  // their first payload words
 #pragma unroll
   for (int r = 0; r < PR; r++) {
     const int64_t i = base + r * 256 + threadIdx.x;
@@ -346,10 +375,17 @@ __global__ __launch_bounds__(256) void k_probe(const uint64_t* __restrict__ tabl
   }
 #pragma unroll
   for (int r = 0; r < PR; r++) {
-    slot[r] = key_hash(key[r]) & mask;
-    const longlong2* sp = (const longlong2*)(table + slot[r] * (uint64_t)sw);
-    h0[r] = sp[0];
-    h1[r] = sp[1];
+    slot[r] = home_slot(key[r], mask);
+    const uint64_t* sp = table + slot[r] * (uint64_t)sw;
+    h0[r] = *(const longlong2*)sp;
+    g0[r] = *(const longlong2*)(sp + sw);
+    if constexpr (CMP) {  // the value is in the meta word: the pair is one 32-byte read
+      c0a[r] = (uint64_t)h0[r].y;
+      c0b[r] = (uint64_t)g0[r].y;
+    } else {
+      c0a[r] = sp[3];
+      c0b[r] = sp[sw + 3];
+    }
   }
   int cnt = 0;
 #pragma unroll
@@ -361,12 +397,13 @@ __global__ __launch_bounds__(256) void k_probe(const uint64_t* __restrict__ tabl
     if (act[r]) {
       uint64_t m = (uint64_t)h0[r].y;
       int64_t k0 = h0[r].x;
-      uint64_t c0 = (uint64_t)h1[r].y, sl = slot[r];
-      // c0 opaque (a register, not "a load of h1[r].y"): otherwise the compiler sinks c0's load to
-      // the hit through a pointer phi (home slot word in the private h1 array | probed slot), which
-      // keeps h1 in scratch — each home-slot word stored right after its load, a wait per probe
-      asm volatile("" : "+v"(c0));
-      // linear probing past the home slot (a minority of rows)
+      uint64_t c0 = c0a[r], c1 = c0b[r], sl = slot[r];
+      // c0 / c1 opaque (registers, not "loads of c0a / c0b"): otherwise the compiler sinks the
+      // loads to the hit through a pointer phi (a home-pair word in a private array | a probed
+      // slot), which keeps the array in scratch — each word stored right after its load, a wait
+      // per probe
+      asm volatile("" : "+v"(c0), "+v"(c1));
+      // the home pair's second slot from registers; linear probing past the pair (rare)
       for (int probe = 0; probe < JMAX_PROBE; probe++) {
         if (m == 0) break;
         if (k0 == key[r]) {
@@ -374,19 +411,25 @@ __global__ __launch_bounds__(256) void k_probe(const uint64_t* __restrict__ tabl
             hit = true;
             found = (int64_t)sl;
             meta = m;
-            v0 = c0;
+            v0 = CMP ? (uint64_t)(int64_t)(int32_t)(uint32_t)c0 : c0;
           }
           break;
         }
         sl = (sl + 1) & mask;
-        const uint64_t* s = table + sl * (uint64_t)sw;
-        k0 = (int64_t)s[0];
-        m = s[1];
-        c0 = s[3];
+        if (probe == 0) {
+          k0 = g0[r].x;
+          m = (uint64_t)g0[r].y;
+          c0 = c1;
+        } else {
+          const uint64_t* s = table + sl * (uint64_t)sw;
+          k0 = (int64_t)s[0];
+          m = s[1];
+          c0 = CMP ? m : s[3];
+        }
       }
       emit = inner ? hit : true;
       if (emit && w.active)
-        emit = hit && where_ok_raw(w.col == 0 ? v0 : table[found * (uint64_t)sw + 3 + w.col], meta, w);
+        emit = hit && where_ok_raw(w.col == 0 ? v0 : table[found * (uint64_t)sw + 3 + w.col], meta, w, CMP);
     }
     const uint64_t be = __ballot(emit), bh = __ballot(hit);
     const int64_t wbase = i - lane;
@@ -405,7 +448,7 @@ __global__ __launch_bounds__(256) void k_probe(const uint64_t* __restrict__ tabl
     }
     for (int c = 0; c < ncols; c++) {
       // rows past the batch end keep a 0 bit (the bitmap's last byte is partial when n % 8 != 0)
-      const bool isnull = i < n && (!hit || (meta & (1ULL << c)));
+      const bool isnull = i < n && (!hit || slot_null(meta, c, CMP));
       const uint64_t bn = __ballot(isnull);
       if (out.col_null[c] && lane == 0 && wbase < n) {
         const int64_t nbytes = std::min<int64_t>(8, (n - wbase + 7) / 8);
@@ -483,16 +526,17 @@ __global__ __launch_bounds__(256) void k_probe_dense(JDense dn, const int64_t* _
 }
 
 __global__ __launch_bounds__(256) void k_table_rehash(const uint64_t* __restrict__ old, int64_t ocap,
-                                                      uint64_t* __restrict__ nt, uint64_t nmask, int sw) {
+                                                      uint64_t* __restrict__ nt, uint64_t nmask, int sw, int cmp) {
   for (int64_t slot = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; slot < ocap;
        slot += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t* s = old + slot * (uint64_t)sw;
     const uint64_t m = s[1];
     if (!(m & M_LIVE)) continue;  // deleted keys are dropped on rehash
-    uint64_t d = key_hash((int64_t)s[0]) & nmask;
+    uint64_t d = home_slot((int64_t)s[0], nmask);
     while (atomicCAS((unsigned long long*)&nt[d * sw + 1], 0ULL, (unsigned long long)m) != 0ULL) d = (d + 1) & nmask;
     uint64_t* q = nt + d * (uint64_t)sw;
     q[0] = s[0];
+    if (cmp) continue;  // COMPACT: key + meta (value inside); the tags array is zero
     q[2] = 0;
     for (int w = 3; w < sw; w++) q[w] = s[w];
   }
@@ -522,6 +566,8 @@ struct khip_table {
   int device = 0;
   hipStream_t stream = nullptr;
   int sw = 4;
+  bool compact = false;  // 16-byte slots (one INT payload column), last-writer tags beside
+  DevBuf tags;
   DevBuf table, types_dev, slot_of, scratch, st_keys, st_ts, st_kv, st_rv, st_cols[JMAX_COLS],
       st_cval[JMAX_COLS], out_emit, out_matched, out_cols[JMAX_COLS], out_nulls[JMAX_COLS], out_slot;
   int64_t cap = 0;
@@ -551,7 +597,7 @@ static khip_status prepare_dense(khip_table* t) {
   unsigned long long* out = t->drange.as<unsigned long long>();
   KHIP_TRY_HIP(hipMemcpyAsync(out, init, sizeof(init), hipMemcpyHostToDevice, t->stream));
   hipLaunchKernelGGL(k_table_ranges, dim3(jgrid(t->cap, 4096)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->cap,
-                     t->sw, out);
+                     t->sw, out, t->compact ? 1 : 0);
   KHIP_TRY_HIP(hipGetLastError());
   KHIP_TRY_HIP(hipMemcpyAsync(r, out, sizeof(r), hipMemcpyDeviceToHost, t->stream));
   KHIP_TRY_HIP(hipStreamSynchronize(t->stream));
@@ -584,7 +630,7 @@ static khip_status prepare_dense(khip_table* t) {
   d.cells = t->dcells.as<uint8_t>();
   d.invalid = t->dinvalid.as<int>();
   hipLaunchKernelGGL(k_dense_build, dim3(jgrid(t->cap, 8192)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->cap,
-                     t->sw, d);
+                     t->sw, d, t->compact ? 1 : 0);
   KHIP_TRY_HIP(hipGetLastError());
   int bad = 0;
   KHIP_TRY_HIP(hipMemcpyAsync(&bad, t->dinvalid.p, 4, hipMemcpyDeviceToHost, t->stream));
@@ -598,6 +644,11 @@ static khip_status prepare_dense(khip_table* t) {
 static khip_status table_alloc(khip_table* t, DevBuf& buf, int64_t cap) {
   KHIP_TRY(buf.ensure((size_t)cap * t->sw * 8));
   KHIP_TRY_HIP(hipMemsetAsync(buf.p, 0, (size_t)cap * t->sw * 8, t->stream));
+  if (t->compact) {  // the last-writer tags, one per slot (zero between upserts)
+    t->tags.release();
+    KHIP_TRY(t->tags.ensure((size_t)cap * 8));
+    KHIP_TRY_HIP(hipMemsetAsync(t->tags.p, 0, (size_t)cap * 8, t->stream));
+  }
   return KHIP_OK;
 }
 
@@ -605,7 +656,7 @@ static khip_status table_grow(khip_table* t, int64_t new_cap) {
   DevBuf nt;
   KHIP_TRY(table_alloc(t, nt, new_cap));
   hipLaunchKernelGGL(k_table_rehash, dim3(jgrid(t->cap)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->cap,
-                     nt.as<uint64_t>(), (uint64_t)(new_cap - 1), t->sw);
+                     nt.as<uint64_t>(), (uint64_t)(new_cap - 1), t->sw, t->compact ? 1 : 0);
   KHIP_TRY_HIP(hipGetLastError());
   unsigned long long* ctr;
   KHIP_TRY(t->scratch.ensure(64));
@@ -735,7 +786,10 @@ khip_status khip_table_create(const khip_table_desc* d, khip_table** out) {
   t->desc.col_types = t->col_types.data();
   t->device = d->device;
   t->utf8 = d->key_type == KHIP_KEY_UTF8;
-  t->sw = (int)next_pow2(std::max(4, 3 + d->n_cols));
+  // one INT payload column: 16-byte slots (the value inside the meta word); else
+  // [key, meta, tag, columns...] rounded up to a power of two
+  t->compact = d->n_cols == 1 && d->col_types[0] == KHIP_TYPE_INT32 && knob("KHIP_JOIN_COMPACT", 1) != 0;
+  t->sw = t->compact ? 2 : (int)next_pow2(std::max(4, 3 + d->n_cols));
   DeviceGuard g(t->device);
   if (hipStreamCreateWithFlags(&t->stream, hipStreamDefault) != hipSuccess) {
     delete t;
@@ -785,12 +839,12 @@ khip_status khip_table_upsert(khip_table* t, const khip_batch* b) {
   KHIP_TRY_HIP(hipMemsetAsync(t->scratch.p, 0, 64, t->stream));
   hipLaunchKernelGGL(k_upsert_claim, dim3(jgrid(n)), dim3(256), 0, t->stream, t->table.as<uint64_t>(),
                      (uint64_t)(t->cap - 1), t->sw, keys, kv, n, t->slot_of.as<int64_t>(), failp, ctr,
-                     t->claimed.as<int64_t>());
+                     t->claimed.as<int64_t>(), t->compact ? t->tags.as<uint64_t>() : (uint64_t*)nullptr);
   hipLaunchKernelGGL(k_upsert_finalize, dim3(jgrid(n)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->sw, keys,
                      t->claimed.as<int64_t>(), (const unsigned long long*)ctr);
   hipLaunchKernelGGL(k_upsert_apply, dim3(jgrid(n)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->sw,
                      t->slot_of.as<int64_t>(), rv, n, t->desc.n_cols, t->types_dev.as<int32_t>(), cols,
-                     t->dense_ok ? t->dn : JDense{});
+                     t->dense_ok ? t->dn : JDense{}, t->compact ? t->tags.as<uint64_t>() : (uint64_t*)nullptr);
   KHIP_TRY_HIP(hipGetLastError());
   unsigned long long added = 0;
   int failed = 0, dense_bad = 0;
@@ -849,7 +903,8 @@ static khip_status probe_launch(khip_table* t, const khip_batch* b, int32_t join
   }
   const int pr_env = (int)knob("KHIP_PROBE_PR", 4);  // measured: 4 > 8 > 16 > 1
   const int PR = pr_env >= 16 ? 16 : (pr_env >= 8 ? 8 : (pr_env >= 4 ? 4 : 1));
-  auto kern = PR == 16 ? k_probe<16> : (PR == 8 ? k_probe<8> : (PR == 4 ? k_probe<4> : k_probe<1>));
+  auto kern = t->compact ? (PR == 16 ? k_probe<16, true> : (PR == 8 ? k_probe<8, true> : (PR == 4 ? k_probe<4, true> : k_probe<1, true>)))
+                         : (PR == 16 ? k_probe<16, false> : (PR == 8 ? k_probe<8, false> : (PR == 4 ? k_probe<4, false> : k_probe<1, false>)));
   hipLaunchKernelGGL(kern, dim3(ceil_div(n, 256 * PR)), dim3(256), 0, t->stream, t->table.as<uint64_t>(),
                      (uint64_t)(t->cap - 1), t->sw, keys, ts, kv, rv, n, join_type == KHIP_JOIN_INNER ? 1 : 0, jw,
                      t->desc.n_cols, t->types_dev.as<int32_t>(), out, n_emitted);

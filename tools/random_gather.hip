@@ -1,6 +1,6 @@
 // random_gather.hip — the random-access ceiling a hash probe runs against (C4's general path).
 //
-// Reads `n` uniformly random `W`-byte words (W = 8, 16, 32) from a table of `bytes`, each thread
+// Reads `n` uniformly random `W`-byte words (W = 8 .. 128, W-aligned) from a table of `bytes`, each thread
 // issuing R independent loads before using any (memory-level parallelism), and reports loads/s.
 // Table sizes span the MALL (256 MB) to C4's 8.6 GB slot table; the keys are a splitmix64 stream
 // hashed to slots, as k_probe does.  Build: hipcc -O3 --offload-arch=gfx950 -o random_gather
@@ -79,6 +79,9 @@ int main() {
     printf("%llu,16,16,%.4g\n", (unsigned long long)bytes, run<16, 16>(table, bytes / 16, n, sink));
     printf("%llu,32,4,%.4g\n", (unsigned long long)bytes, run<32, 4>(table, bytes / 32, n, sink));
     printf("%llu,32,8,%.4g\n", (unsigned long long)bytes, run<32, 8>(table, bytes / 32, n, sink));
+    printf("%llu,64,2,%.4g\n", (unsigned long long)bytes, run<64, 2>(table, bytes / 64, n, sink));
+    printf("%llu,64,4,%.4g\n", (unsigned long long)bytes, run<64, 4>(table, bytes / 64, n, sink));
+    printf("%llu,128,2,%.4g\n", (unsigned long long)bytes, run<128, 2>(table, bytes / 128, n, sink));
     fflush(stdout);
     hipFree(table);
   }
