@@ -473,6 +473,8 @@ def bench_table_agg(args, lib, rank, world, local):
     be = synth.backend("torch")
     h0 = synth._stream(be, 7, 0, n, "cuda")
     pk = (h0 % users).to(torch.int64)
+    if args.sparse_ids:  # the same users under ids spread over 2^40 (synth.sparse_ids, as C4's)
+        pk = synth.sparse_ids(pk)
     region = ((h0 >> 24) % 100_000).to(torch.int64)
     amount = ((h0 >> 40) % 2_000_001 - 1_000_000).to(torch.int64)
     live = (h0 >> 60) != 0  # 1 in 16 rows: a tombstone
@@ -503,7 +505,7 @@ def bench_table_agg(args, lib, rank, world, local):
     if rank != 0:
         return
     ms_step = elapsed * 1000.0 / args.steps
-    bpr = 32 + 2 * 48 + 2 * 2 * 32  # row in (pk, region, ts, amount) + source-row RMW + undo and apply group RMWs
+    bpr = 32 + 2 * 32 + 2 * 2 * 32  # row in (pk, region, ts, amount) + 32-B source-row RMW + undo and apply group RMWs
     roof = roofline(bpr * n, ms_step, None, None, load_traffic(args.traffic_json, "table_agg", n), bpr,
                     kernel="khip_agg_push_table (k_tagg_keys + radix sort + k_tagg_apply + finalize)")
     cpu = None
@@ -525,6 +527,7 @@ def bench_table_agg(args, lib, rank, world, local):
          world * n * args.steps / elapsed, world, args, ms_step, "int64",
          "synthetic (splitmix64), device-resident changelog",
          {"workload": "table_agg", "records_per_gpu": n, "source_keys": users, "regions": 100_000,
+          "source_ids": "sparse over 2^40 (hash layout)" if args.sparse_ids else "dense 0..users (dense layout)",
           "micro_batch": S, "groups_per_gpu": int(groups), "rows_accepted": int(acc), "parallelism": "key-hash shards x%d" % world}, roof, cpu)
 
 

@@ -367,8 +367,10 @@ struct TaggState {
   int64_t src_cap = 0, src_occ = 0;
   int src_sw = 8;
   int key_type = -1;    // source PRIMARY KEY type (fixed by the first push)
+  bool dense = false;   // source slots by id − dbase (khip_agg_table.hip src_prepare), else hashed
+  int64_t dbase = 0;
   KeyDict dict;         // UTF8 PRIMARY KEYs → ids
-  DevBuf sid, skey, skey2, sidx, sidx2, tmp, tmp2, ctr, claimed, gclaimed, blk, st_koff, st_kbytes, st_kv, st_key, shash;
+  DevBuf sid, skey, skey2, sidx, sidx2, rec, tmp, tmp2, ctr, claimed, gclaimed, blk, st_koff, st_kbytes, st_kv, st_key, shash;
 };
 
 struct SessState {

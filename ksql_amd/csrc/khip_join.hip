@@ -901,7 +901,7 @@ static khip_status probe_launch(khip_table* t, const khip_batch* b, int32_t join
     KHIP_TRY_HIP(hipGetLastError());
     return KHIP_OK;
   }
-  const int pr_env = (int)knob("KHIP_PROBE_PR", 4);  // measured: 4 > 8 > 16 > 1
+  const int pr_env = (int)knob("KHIP_PROBE_PR", 8);  // measured with 16-byte slots: 8 > 4, 16 (profiles/r04/)
   const int PR = pr_env >= 16 ? 16 : (pr_env >= 8 ? 8 : (pr_env >= 4 ? 4 : 1));
   auto kern = t->compact ? (PR == 16 ? k_probe<16, true> : (PR == 8 ? k_probe<8, true> : (PR == 4 ? k_probe<4, true> : k_probe<1, true>)))
                          : (PR == 16 ? k_probe<16, false> : (PR == 8 ? k_probe<8, false> : (PR == 4 ? k_probe<4, false> : k_probe<1, false>)));

@@ -24,3 +24,4 @@ KSQL_AMD_LIB_VARIANT=tune KHIP_PROBE_PR=8 run c4s_pr8 300 python3 bench.py --con
 run knobs 600 python -u -m pytest -q --timeout 300 --timeout-method thread tests/test_gpu_knobs.py
 cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extras > $R/$O/prof.log 2>&1; echo "prof rc=$?"
 cd $R && python3 tools/rocprof_summary.py stats $O/prof/run_kernel_stats.csv > $O/c2_stats.md; grep -E "k_c1|k_part|k_scan" $O/c2_stats.md
+cd $R && run ratomic 150 ./tools/random_atomic && cat $O/ratomic.log

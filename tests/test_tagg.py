@@ -5,8 +5,13 @@ changelogs (updates that move keys between groups, deletes, NULL GROUP BY values
 repeated keys inside one push, INT wrap-around, STRING and BIGINT keys on both sides).
 
 Comparison: integers exact; DOUBLE SUM/AVG within 1e-12 relative to the sum of |x| the group's
-updates touched (the device applies a push's adds/undos with atomics, in no fixed order, and nets
-each source key's changes inside one push: an intermediate row's +x / -x are not applied)."""
+updates touched (the device folds a push's adds/undos per group in no fixed order — LDS atomics on
+the delta path, agent-scope atomics on the atomic path — and nets each source key's changes inside
+one push: an intermediate row's +x / -x are not applied)."""
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 
@@ -240,3 +245,54 @@ def test_tagg_narrow_rows_vs_oracle(prod, orc, ncols, utf8_src):
             np.testing.assert_allclose(g["values"][a], o["values"][a], rtol=1e-15)
         else:
             assert np.array_equal(g["values"][a], o["values"][a]), (kind, col)
+
+
+@pytest.mark.gpu
+def test_tagg_source_layout_transitions(prod, orc):
+    """The source table's dense layout (slot = id − base) grows its window when a push's ids fall
+    below or above it, and moves to the hash layout when the ids spread past the dense bound; keys
+    updated and deleted before each move must be found after it."""
+    rng = np.random.default_rng(21)
+    ranges = [(1000, 2000), (500, 3000), (400, 2600), None, (0, 3000), (2**40, 2**40 + 50)]
+    batches = []
+    for p, r in enumerate(ranges):
+        n = 20000
+        if r is None:  # far ids mixed with old ones: the dense window would be too large
+            pk = np.where(rng.random(n) < 0.3, rng.integers(10**12, 10**12 + 10**6, n), rng.integers(400, 3000, n))
+        else:
+            pk = rng.integers(r[0], r[1], n)
+        b, sa, x = _changelog(rng, n, 1, 300, False, False)
+        sa = {"src_keys": pk, "src_key_valid": sa["src_key_valid"]}
+        batches.append((b, sa, x))
+    scale = sum(float(x.sum()) for _, _, x in batches) * 4
+    (g, gs), (o, os_) = (_run(lib, batches, False) for lib in (prod, orc))
+    for a, b in zip(gs, os_):
+        for f in ("rows_in", "rows_accepted", "dropped_null_key", "dropped_bad_ts", "windows_applied", "stream_time"):
+            assert a[f] == b[f], f
+    _assert_same(g, o, scale)
+
+
+@pytest.mark.gpu
+def test_tagg_hash_layout_tuning_build():
+    """KHIP_TAGG_DENSE=0 on the tuning build: the hash layout for every source table (the layout
+    sparse and STRING PRIMARY KEYs take) on the dense-id workloads, against the oracle."""
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, KSQL_AMD_LIB_VARIANT="tune", KHIP_TAGG_DENSE="0",
+               PYTHONPATH=os.pathsep.join([repo, os.environ.get("PYTHONPATH", "")]))
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child"], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def _child():
+    prod, orc = abi.load_product(), abi.load_oracle()
+    assert prod.path.endswith("libksqldb_hip_tune.so"), prod.path
+    for utf8_group in (False, True):
+        test_tagg_random_vs_oracle(prod, orc, False, utf8_group, 5)
+    test_tagg_many_updates_per_key(prod, orc)
+    test_tagg_group_capacity_growth(prod, orc)
+    print("OK")
+
+
+if __name__ == "__main__" and "--child" in sys.argv:
+    _child()
