@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     ap.add_argument("--engine", choices=["part", "atomic"], default="part")
+    ap.add_argument("--unpack", action="store_true",
+                    help="repartition_sum: unpack the received rows to columns, then khip_agg_push")
     ap.add_argument("--slice", type=int, default=1 << 27, help="hopping_double: records per micro-batch push")
     ap.add_argument("--users", type=int, default=100_000_000, help="clickstream_join: table rows")
     ap.add_argument("--sparse-ids", action="store_true",
@@ -1047,7 +1049,8 @@ BYTES_PER_RECORD_C5 = 136  # read 24 + pack 24 + recv 24 + 2 x
 def bench_repartition(args, lib, rank, world, local):
     """configs[4]: GROUP BY region_id (a value column) forces the repartition.  One step per rank:
     khip_shuffle_pack (Kafka partitioner) → RCCL count exchange + all-to-all over xGMI (N > 1) →
-    khip_shuffle_unpack → SUM(amount) TUMBLING 1 MINUTE push → row count.  Weak scaling: every
+    khip_agg_push_shuffled (the received rows read where they lie; --unpack: khip_shuffle_unpack +
+    khip_agg_push) → SUM(amount) TUMBLING 1 MINUTE → row count.  Weak scaling: every
     rank owns one source partition of --records records (1e9 node-wide at N = 8 with 125M)."""
     import torch
     import torch.distributed as dist
@@ -1071,7 +1074,7 @@ def bench_repartition(args, lib, rank, world, local):
                              aggs=[("SUM", 1)], device=local, capacity_hint=60 * 1_000_000 // max(world, 1),
                              flags=abi.FLAG_PROFILE)
     h = abi.AggHandle(lib, desc)
-    phases = {"pack": 0.0, "exchange_unpack": 0.0, "aggregate": 0.0}
+    phases = {"pack": 0.0, "exchange": 0.0, "aggregate": 0.0}
     state = {"timed": False, "m": 0}
 
     # sized for every source row: khip_shuffle_pack's counts and scatter in one call
@@ -1086,15 +1089,18 @@ def bench_repartition(args, lib, rank, world, local):
         else:
             recv, rc = send, counts
         m = int(sum(rc))
-        key, kts, cols, valid = rp.shuffle.unpack(recv, m, key_as_col=True)  # region = the key
         t2 = time.perf_counter()
         h.reset()
-        st = h.push(abi.DeviceBatch(kts, keys=key, cols=cols, col_valid=valid))
+        if args.unpack:  # the columnar route: khip_shuffle_unpack, then khip_agg_push
+            key, kts, cols, valid = rp.shuffle.unpack(recv, m, key_as_col=True)  # region = the key
+            st = h.push(abi.DeviceBatch(kts, keys=key, cols=cols, col_valid=valid))
+        else:  # the received rows read where they lie (khip_agg_push_shuffled)
+            st = h.push_shuffled(rp.shuffle, recv, m)
         rows = h.count_rows(None)
         t3 = time.perf_counter()
         if state["timed"]:
             phases["pack"] += t1 - t0
-            phases["exchange_unpack"] += t2 - t1
+            phases["exchange"] += t2 - t1
             phases["aggregate"] += t3 - t2
         state["m"] = m
         return st, rows, m
@@ -1116,7 +1122,7 @@ def bench_repartition(args, lib, rank, world, local):
     per = {k: v * 1000.0 / args.steps for k, v in phases.items()}
     push_ms = sum(push_phases(kt, kt["apply_launches"]).values())
     roof = roofline(BYTES_PER_RECORD_C5 * n, ms_step, None, None, load_traffic(args.traffic_json, "repartition_sum", n),
-                    BYTES_PER_RECORD_C5, kernel="whole step: pack + all-to-all + unpack + khip_agg_push + row count",
+                    BYTES_PER_RECORD_C5, kernel="whole step: pack + all-to-all + khip_agg_push_shuffled (or unpack + khip_agg_push) + row count",
                     extra={"phase_ms": per, "push_device_ms": push_ms})
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
@@ -1126,7 +1132,8 @@ def bench_repartition(args, lib, rank, world, local):
          "synthetic (splitmix64, ksql_amd/synth.py repartition_sum), device-resident columnar batch",
          {"workload": "repartition_sum", "records_per_gpu": n, "regions": 1_000_000, "window": "TUMBLING 1 MINUTE",
           "parallelism": "repartition all-to-all x%d" % world, "exchange": args.exchange if world > 1 else None,
-          "rows_received_rank0": m, "groups_rank0": int(rows)},
+          "rows_received_rank0": m, "groups_rank0": int(rows),
+          "aggregate_input": "columns (khip_shuffle_unpack)" if args.unpack else "shuffled rows (khip_agg_push_shuffled)"},
          roof, cpu)
 
 

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KHIP_ABI_VERSION 5
+#define KHIP_ABI_VERSION 6
 
 typedef int32_t khip_status;
 #define KHIP_OK 0
@@ -524,6 +524,18 @@ khip_status khip_shuffle_pack(khip_shuffle* s, const khip_batch* in, uint64_t* s
  * the counts, and the caller calls again). */
 khip_status khip_shuffle_unpack(khip_shuffle* s, const uint64_t* rows, int64_t n, int64_t* key,
                                 int64_t* ts, void* const* col_data, uint8_t* const* col_valid);
+
+/* ABI 6.  Received rows straight into the aggregation that reads the repartition topic (the
+ * non-key GROUP BY's aggregate, S/StreamGroupByBuilderBase.java:101-103 → StreamAggregateBuilder),
+ * without materialising them as columns first: the same effect and statistics as khip_agg_push of
+ * khip_shuffle_unpack's batch (key = the shuffle's key column, every row valid).  `agg`'s columns
+ * must be the shuffle's columns (count and types) and its GROUP BY key an integer (the new key).
+ * `rows` (device, n rows of khip_shuffle_row_words words) stays the caller's.  Pushes the value
+ * pipeline takes read the rows where they lie; every other push unpacks them into the handle's
+ * staging columns and runs as a device batch.  Replaces khip_shuffle_unpack + khip_agg_push at the
+ * reference's repartition source (S/StreamGroupByBuilderBase.java:101-103). */
+khip_status khip_agg_push_shuffled(khip_agg* agg, const khip_shuffle* s, const uint64_t* rows, int64_t n,
+                                   khip_batch_stats* stats);
 
 khip_status khip_shuffle_sync(khip_shuffle* s);
 khip_status khip_shuffle_destroy(khip_shuffle* s);

@@ -20,7 +20,7 @@ _VARIANT = os.environ.get("KSQL_AMD_LIB_VARIANT", "")
 PRODUCT_LIB = os.path.join(REPO, "ksql_amd", "libksqldb_hip_%s.so" % _VARIANT if _VARIANT else "libksqldb_hip.so")
 ORACLE_LIB = os.path.join(REPO, "oracle", "liboracle.so")
 
-ABI_VERSION = 5  # include/ksqldb_hip.h KHIP_ABI_VERSION the structs below mirror
+ABI_VERSION = 6  # include/ksqldb_hip.h KHIP_ABI_VERSION the structs below mirror
 KHIP_OK = 0
 KHIP_E_BUFFER = -5
 
@@ -209,6 +209,7 @@ PRODUCT_ONLY = {
     "shuffle_create": ([C.POINTER(ShuffleDesc), C.POINTER(_P)]),
     "shuffle_pack": ([_P, C.POINTER(Batch), _P, i64, C.POINTER(i64)]),
     "shuffle_unpack": ([_P, _P, i64, _P, _P, C.POINTER(_P), C.POINTER(_P)]),
+    "agg_push_shuffled": ([_P, _P, _P, i64, C.POINTER(BatchStats)]),
     "shuffle_sync": ([_P]),
     "shuffle_destroy": ([_P]),
     "comm_unique_id": ([C.POINTER(C.c_uint8)]),
@@ -424,6 +425,14 @@ class AggHandle:
         st = BatchStats()
         self.lib.check(self.lib.agg_push(self.h, C.byref(batch.struct if hasattr(batch, "struct") else batch),
                                          C.byref(st) if stats else None), "agg_push")
+        return st.as_dict() if stats else None
+
+    def push_shuffled(self, shuffle, rows, n, stats=True):
+        """khip_agg_push_shuffled (ABI 6): `n` rows a ShuffleHandle packed / received (a device tensor
+        [>= n, row_words]) into this aggregation, without unpacking them to columns first."""
+        st = BatchStats()
+        self.lib.check(self.lib.agg_push_shuffled(self.h, shuffle.h, None if rows is None else rows.data_ptr(), n,
+                                                  C.byref(st) if stats else None), "agg_push_shuffled")
         return st.as_dict() if stats else None
 
     def push_table(self, batch, src_keys=None, src_utf8_keys=None, src_key_valid=None, stats=True):

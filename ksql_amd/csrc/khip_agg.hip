@@ -1103,6 +1103,86 @@ static khip_status resolve_batch(khip_agg* a, const khip_batch* b, const int64_t
   return KHIP_OK;
 }
 
+// ABI 6.  Received shuffle rows into the aggregation: the value pipeline reads them where they lie
+// (khip_agg_c1.hip, RowsIn); any other push unpacks them into the handle's staging columns and runs
+// as a device batch.  Same results and statistics as khip_agg_push of the unpacked batch.
+khip_status khip_agg_push_shuffled(khip_agg* a, const khip_shuffle* sh, const uint64_t* rows, int64_t n,
+                                   khip_batch_stats* stats) {
+  clear_error();
+  if (!a || !sh || (n > 0 && !rows)) return fail(KHIP_E_INVALID, "null argument");
+  if (n < 0) return fail(KHIP_E_INVALID, "row count");
+  int kc = 0, nc = 0;
+  const int32_t* types = nullptr;
+  shuffle_layout(sh, &kc, &nc, &types);
+  if (nc != a->desc.n_cols) return fail(KHIP_E_INVALID, "the shuffle's columns are not the aggregation's");
+  for (int c = 0; c < nc; c++)
+    if (types[c] != a->col_types[c]) return fail(KHIP_E_INVALID, "the shuffle's column types are not the aggregation's");
+  if (a->desc.key_type == KHIP_KEY_UTF8) return fail(KHIP_E_UNSUPPORTED, "shuffled rows carry an integer GROUP BY key");
+  if (a->engine == 3) return fail(KHIP_E_STATE, "table-source aggregation: use khip_agg_push_table");
+  const int rw = 2 + nc;
+  DeviceGuard g(a->device);
+  if (n > 0 && n < (1LL << 31) && a->engine == 0 && a->desc.time_domain == KHIP_TIME_TASK &&
+      a->desc.emit != KHIP_EMIT_FINAL) {
+    khip_batch_stats s{};
+    s.rows_in = n;
+    a->st_before = a->host_stream_time;
+    a->chg_ready = false;
+    a->lost.clear();
+    int64_t tot[NPART] = {0};
+    bool done = false;
+    KHIP_TRY(part_push_rows(a, n, RowsIn{rows, rw, 0, 0}, kc, tot, &done));
+    if (done) {
+      a->occ += tot[P_NEW];
+      if (a->profile) {
+        a->times.stream_time_ms += ev_ms(a, 3, 4);
+        a->times.partition_ms += ev_ms(a, 4, 5);
+        a->times.apply_ms += ev_ms(a, 5, 6);
+        a->times.records += n;
+        a->times.apply_launches++;
+      }
+      if (a->windowed) {  // retention: drop expired windows from the closed store
+        HavingDev vis{};
+        vis.vis = 1;
+        vis.vis_from = visible_from(a);
+        if (vis.vis_from != INT64_MIN) KHIP_TRY(part_purge_closed(a, vis));
+      }
+      s.rows_accepted = tot[P_ACCEPTED];
+      s.dropped_null_key = tot[P_NULL_KEY];
+      s.dropped_null_row = tot[P_NULL_ROW];
+      s.dropped_bad_ts = tot[P_BAD_TS];
+      s.windows_applied = tot[P_APPLIED];
+      s.windows_late = tot[P_LATE];
+      s.stream_time = a->host_stream_time;
+      if (stats) *stats = s;
+      return KHIP_OK;
+    }
+  }
+  // the rows as columns (the staging buffers: a device batch never uses them)
+  const size_t bm = (size_t)(n + 7) / 8;
+  KHIP_TRY(a->st_keys.ensure((size_t)std::max<int64_t>(n, 1) * 8));
+  KHIP_TRY(a->st_ts.ensure((size_t)std::max<int64_t>(n, 1) * 8));
+  void* cd[MAX_COLS] = {};
+  uint8_t* cv[MAX_COLS] = {};
+  for (int c = 0; c < nc; c++) {
+    KHIP_TRY(a->st_cols[c].ensure((size_t)std::max<int64_t>(n, 1) * 8));
+    KHIP_TRY(a->st_cval[c].ensure(std::max<size_t>(bm, 1)));
+    cd[c] = a->st_cols[c].p;
+    cv[c] = a->st_cval[c].as<uint8_t>();
+  }
+  if (n > 0)
+    KHIP_TRY(khip_shuffle_unpack(const_cast<khip_shuffle*>(sh), rows, n, a->st_keys.as<int64_t>(), a->st_ts.as<int64_t>(),
+                                 cd, cv));
+  khip_batch b{};
+  b.mem = KHIP_MEM_DEVICE;
+  b.n_rows = n;
+  b.n_cols = nc;
+  b.key_i64 = a->st_keys.as<int64_t>();
+  b.ts = a->st_ts.as<int64_t>();
+  b.col_data = (const void* const*)cd;
+  b.col_valid = (const uint8_t* const*)cv;
+  return khip_agg_push(a, &b, stats);
+}
+
 khip_status khip_agg_push_table(khip_agg* a, const khip_batch* b, const khip_table_src* src,
                                 khip_batch_stats* stats) {
   clear_error();

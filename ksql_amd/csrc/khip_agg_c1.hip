@@ -4,25 +4,25 @@
 // Same contract as part_push's general path (khip_agg_part.hip) — per record (SURVEY §8.0,
 // Kafka Streams' KStreamWindowAggregate as called from S/StreamAggregateBuilder.java:287-294):
 // stream time, TimeWindows.windowsFor, late drop, store update, row time = max ts — but the input
-// is read once for the records and once (keys only) for the bucket offsets, and every record
-// moves as 8 bytes:
+// is read once, and every record moves as 8 bytes:
 //
-//   k_c1_hist     keys only: per 64K-record tile, a histogram over the B coarse buckets (top bits
-//                 of the key hash) and the key range (global atomics)
-//   (k_part_colsum / colbase / pscan / colprefix over B columns: each (tile, bucket) run's offset)
-//   k_c1_scatter  keys, ts, validity: every record → its bucket's run as (key - kmin, ts - T0),
-//                 two int32s; invalid records (null key / row, ts < 0) as sentinels; per step of
-//                 4096 records the largest and smallest accepted ts, per tile the counters.
+//   k_c1_scatter  keys, ts, validity: every record → (key - kb, ts - T0), two int32s; invalid
+//                 records (null key / row, ts < 0) as sentinels; each 4096-record step leaves as
+//                 one run in bucket order (B coarse buckets: top bits of the key hash) with its
+//                 per-bucket counts (the step-run layout: no histogram pass ahead of it); per step
+//                 the largest and smallest accepted ts, per tile the counters and the key range.
 //                 Optimistic: no record is assumed late.
+//   (scan_excl over the [bucket][step] counts: each run's place in its bucket; k_c1_bases)
 //   k_c1_check    one workgroup: stream time before each 4096-record step (exclusive prefix
 //                 max), and the push is ACCEPTED only if no step can hold a late record (the
 //                 general path's `fast` test per step), every ts fits ts - T0 in 31 bits and the
-//                 key range fits 32 bits; otherwise nothing was written and the host runs the
-//                 general path.
+//                 keys fit 32 bits above the base kb; otherwise nothing was written and the host
+//                 runs the general path (or the same push with kb = the key minimum).
 //                 Also the window range, the group-identity width and the refine's chunk list.
-//   k_c1_refine   per 8K-record chunk of a bucket: sentinels dropped, records counting-sorted by
-//                 their partition inside the bucket (LDS), written back contiguously; the chunk's
-//                 per-partition offsets (u16) go to a segment table
+//   k_c1_refine   per 8K-record chunk of a bucket, read from its step runs: sentinels dropped,
+//                 keys rebased to the key minimum, records counting-sorted by their partition
+//                 inside the bucket (LDS), written bucket-contiguously; the chunk's per-partition
+//                 offsets (u16) go to a segment table
 //   k_c1_merge    persistent workgroups, one partition per item: the partition's records are its
 //                 segments of the bucket's chunks; (key - kmin, window) → a 32-bit identity when
 //                 it fits (no key hash on the record path), LDS identity CAS + u32 row-time max +
@@ -30,7 +30,7 @@
 //                 resident rows merged, closed rows evicted, HAVING counts and changelog flags
 //                 maintained exactly as k_part_merge_c1 does (k_part_commit publishes)
 //
-// Algorithmic bytes per record: 8 (hist) + 16 + 8 (scatter) + 8 + 8 (refine) + 8 (merge read)
+// Algorithmic bytes per record: 16 + 8 (scatter) + 8 + 8 (refine) + 8 (merge read)
 // + the table rows written (32 B per group) — against 16 + 24 + 16 + 8 + rows for the general
 // path (DESIGN.md §(d)).
 #include <algorithm>
@@ -39,6 +39,7 @@
 #include <vector>
 
 #include "khip_part.hpp"
+#include "khip_sort.hpp"
 
 namespace khip {
 
@@ -52,10 +53,10 @@ constexpr uint32_t C1_SENT = 0x80000000u;  // low word of a sentinel record (ts 
 
 // c1info (int64) slots
 enum {
-  CI_KMIN = 0,   // atomics (k_c1_hist), reset by k_c1_check for the next push
+  CI_KMIN = 0,   // atomics (the scatters), reset by k_c1_check for the next push
   CI_KMAX = 1,
   CI_TFAIL = 2,  // some accepted ts - T0 outside int32 (k_c1_scatter)
-  CI_T0 = 3,     // time base (k_c1_hist block 0)
+  CI_T0 = 3,     // time base (the scatters' block 0)
   CI_GATE = 4,   // accepted (k_part_commit reads gate[4])
   CI_WBASE = 5,  // smallest window index (records and live resident rows)
   CI_WBITS = 6,
@@ -70,12 +71,15 @@ enum {
   CI_WIDE = 15,    // records of this push: 1 = key hash + u32 ts words (the key range is too wide)
   CI_REASON = 16,  // declined: 1 = the key range needs the wide records (the host retries with them)
   CI_FITS = 17,    // the key range fits the compact records (a wide push tells the host)
+  CI_KBASE = 18,   // the key base of this push's records (the scatters)
+  CI_KSHIFT = 19,  // kmin - kbase: the refines rebase the records to the key minimum
+  CI_KFAIL = 20,   // some key fell outside the records' key field above kbase (the scatters)
   CI_N = 24
 };
 
 __device__ __forceinline__ int bits_of(uint64_t v) { return v ? 64 - __clzll((long long)v) : 0; }
 
-// A c1info word another kernel produced (atomics of k_c1_hist / k_c1_scatter, stores of
+// A c1info word another kernel produced (atomics / stores of the scatters, stores of
 // k_c1_check): read with a device-coherent vector load, never through the scalar cache.
 __device__ __forceinline__ int64_t ci_ld(const int64_t* ci, int k) {
   const uint64_t v = (uint64_t)__hip_atomic_load(&ci[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -84,175 +88,168 @@ __device__ __forceinline__ int64_t ci_ld(const int64_t* ci, int k) {
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-// ------------------------------------------------------------------ k_c1_hist
-// Keys only (8 B/record): the tile's bucket histogram and key range.  Every record i < n counts
-// (k_c1_scatter writes a sentinel for the invalid ones), so no validity or ts is read here.
-template <bool VEC>
-__global__ __launch_bounds__(C1_NT) void k_c1_hist(const int64_t* __restrict__ keys, const int64_t* __restrict__ ts,
-                                                   int64_t n, int64_t nT, int log2B, uint32_t* __restrict__ hist,
-                                                   int64_t* __restrict__ ci, const int64_t* __restrict__ stream_time) {
-  __shared__ uint32_t lh[512];
-  __shared__ int64_t lk[2][C1_NT / 64];
-  const int B = 1 << log2B;
-  const int64_t t = tile_of(blockIdx.x, nT);
-  for (int b = threadIdx.x; b < B; b += C1_NT) lh[b] = 0;
-  __syncthreads();
-  const int64_t base = t * C1_TILE;
-  const int64_t end = base + C1_TILE < n ? base + C1_TILE : n;
-  const int shift = 64 - log2B;
-  int64_t kmx = INT64_MIN, kmxn = INT64_MIN;  // max of key and of ~key (= ~min)
-  auto one = [&](int64_t k) {
-    kmx = k > kmx ? k : kmx;
-    kmxn = ~k > kmxn ? ~k : kmxn;
-    atomicAdd(&lh[log2B == 0 ? 0u : (uint32_t)(key_hash(k) >> shift)], 1u);
-  };
-  if constexpr (VEC) {  // 16-byte loads: pairs of keys (keys is 16-byte aligned, base is even)
-    const longlong2* kp = (const longlong2*)(keys + base);
-    const int64_t npair = (end - base + 1) >> 1;
-    for (int64_t j0 = threadIdx.x; j0 < npair; j0 += 8 * C1_NT) {
-      longlong2 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int64_t j = j0 + (int64_t)u * C1_NT;
-        v[u] = j < npair ? kp[j] : make_longlong2(0, 0);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int64_t j = j0 + (int64_t)u * C1_NT;
-        if (j >= npair) continue;
-        one(v[u].x);
-        if (base + 2 * j + 1 < end) one(v[u].y);
-      }
-    }
-  } else {
-    for (int64_t i0 = base + threadIdx.x; i0 < end; i0 += 8 * C1_NT) {
-      int64_t v[8];
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int64_t i = i0 + (int64_t)u * C1_NT;
-        v[u] = i < end ? keys[i] : 0;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; u++)
-        if (i0 + (int64_t)u * C1_NT < end) one(v[u]);
-    }
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    const int64_t a = __shfl_xor(kmx, off, 64), b = __shfl_xor(kmxn, off, 64);
-    kmx = a > kmx ? a : kmx;
-    kmxn = b > kmxn ? b : kmxn;
-  }
-  if ((threadIdx.x & 63) == 0) {
-    lk[0][threadIdx.x >> 6] = kmx;
-    lk[1][threadIdx.x >> 6] = kmxn;
-  }
-  __syncthreads();
-  uint32_t* hrow = hist + t * (int64_t)B;
-  for (int b = threadIdx.x; b < B; b += C1_NT) hrow[b] = lh[b];
-  if (threadIdx.x == 0) {
-    int64_t a = INT64_MIN, c = INT64_MIN;
-    for (int w = 0; w < C1_NT / 64; w++) {
-      a = lk[0][w] > a ? lk[0][w] : a;
-      c = lk[1][w] > c ? lk[1][w] : c;
-    }
-    if (end > base) {
-      atomicMax((long long*)&ci[CI_KMAX], (long long)a);
-      atomicMin((long long*)&ci[CI_KMIN], (long long)~c);
-    }
-    if (blockIdx.x == 0) {  // time base: the stream time before the push, else the first ts
-      const int64_t st0 = *stream_time;
-      const int64_t t0 = n > 0 ? ts[0] : 0;
-      ci[CI_T0] = st0 >= 0 ? st0 : (t0 > 0 ? t0 : 0);
-    }
-  }
-}
-
-// ------------------------------------------------------------------ k_c1_scatter
-// Records of tile t → their bucket's run (offs[t][b] from the column prefix).  8-byte record:
-// (key - kmin) << 32 | (uint32)(ts - T0); invalid records keep their key word (their bucket is the
-// key's) with the sentinel low word.  Same staged step as k_part_scatter_r8.
-// WIDE (the key range does not fit 32 bits): the record is the 64-bit key hash (key = its inverse)
-// and ts - T0 goes to a parallel u32 array (srecT), staged beside it.
-template <int U, int NT>
-__device__ __forceinline__ void stage_step_c1w(const int64_t (&rec)[U], const uint32_t (&t32)[U], const uint32_t (&bin)[U],
-                                               const bool (&ok)[U], int nb, const StageR8& L, uint32_t* lt32,
-                                               uint64_t* __restrict__ srec, uint32_t* __restrict__ srecT) {
+// ------------------------------------------------------------------ step-run layout
+// The scatters write no bucket-contiguous output (that needs every tile's bucket counts first: a
+// histogram pass over the keys): each step of S records leaves as ONE contiguous run of S records
+// in bucket order at out[gs * S], and its per-bucket count / offset go to rcnt[b][gs] / roff[b][gs]
+// (bucket-major).  The exclusive scan of rcnt gives each (bucket, step) run's place in the bucket's
+// order (rpos); the refine reads a bucket's chunk from its step runs.  The key range, the time base
+// and the bucket counts are all learned in the one read of the input.
+template <int U, int NT, class R, bool W>
+__device__ __forceinline__ uint32_t stage_step_runs(const R (&rec)[U], const uint32_t (&t32)[U], const uint32_t (&bin)[U],
+                                                const bool (&ok)[U], int nb, uint32_t* cnt, uint32_t* sbase, int* wsum,
+                                                R* sp, uint32_t* lt32, R* __restrict__ out, uint32_t* __restrict__ outT,
+                                                int64_t gs, int64_t nSt, uint32_t* __restrict__ rcnt,
+                                                uint16_t* __restrict__ roff) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   uint32_t rank[U];
 #pragma unroll
-  for (int u = 0; u < U; u++) rank[u] = ok[u] ? atomicAdd(&L.cnt[bin[u]], 1u) : 0u;
+  for (int u = 0; u < U; u++) rank[u] = ok[u] ? atomicAdd(&cnt[bin[u]], 1u) : 0u;
   lds_barrier();
-  const uint32_t c = t < nb ? L.cnt[t] : 0u;
+  const uint32_t c = t < nb ? cnt[t] : 0u;
   uint32_t incl = c;
   for (int off = 1; off < 64; off <<= 1) {
     const uint32_t y = __shfl_up(incl, off, 64);
     if (lane >= off) incl += y;
   }
-  if (lane == 63) L.wsum[wave] = (int)incl;
+  if (lane == 63) wsum[wave] = (int)incl;
   lds_barrier();
   uint32_t before = 0, tot = 0;
 #pragma unroll
   for (int k = 0; k < NT / 64; k++) {
-    before += k < wave ? (uint32_t)L.wsum[k] : 0u;
-    tot += (uint32_t)L.wsum[k];
+    before += k < wave ? (uint32_t)wsum[k] : 0u;
+    tot += (uint32_t)wsum[k];
   }
   if (t < nb) {
-    L.sbase[t] = before + incl - c;
-    L.gpos[t] = L.cur[t];
-    L.cur[t] += c;
-    L.cnt[t] = 0u;
+    sbase[t] = before + incl - c;
+    rcnt[(int64_t)t * nSt + gs] = c;
+    roff[(int64_t)t * nSt + gs] = (uint16_t)(before + incl - c);
+    cnt[t] = 0u;
   }
   lds_barrier();
 #pragma unroll
   for (int u = 0; u < U; u++)
     if (ok[u]) {
-      const uint32_t i = L.sbase[bin[u]] + rank[u];
-      L.sp[i] = rec[u];
-      lt32[i] = t32[u];
-      L.sbin[i] = (uint16_t)bin[u];
+      const uint32_t i = sbase[bin[u]] + rank[u];
+      sp[i] = rec[u];
+      if (W) lt32[i] = t32[u];
     }
   lds_barrier();
-  for (uint32_t j = t; j < tot; j += NT) {
-    const uint32_t b = L.sbin[j];
-    const uint64_t pos = (uint64_t)L.gpos[b] + (j - L.sbase[b]);
-    srec[pos] = (uint64_t)L.sp[j];
-    srecT[pos] = lt32[j];
+  R* o = out + gs * (int64_t)(U * NT);
+  for (uint32_t j = t; j < tot; j += NT) o[j] = sp[j];
+  if (W) {
+    uint32_t* oT = outT + gs * (int64_t)(U * NT);
+    for (uint32_t j = t; j < tot; j += NT) oT[j] = lt32[j];
+  }
+  // the next step's first barrier (after its rank atomics) orders these LDS reads before any
+  // rewrite of sbase / the stage
+  return tot;
+}
+
+// The step's staged key offsets (key - kb, kbits wide, above bit 32 of the record's first word)
+// → the workgroup's LDS minimum / maximum (one atomic pair per wave); registers only for the step.
+template <int NT, class R>
+__device__ __forceinline__ void step_krange(const R* sp, uint32_t tot, uint32_t kmask, uint32_t* lkr) {
+  uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+  for (uint32_t j = threadIdx.x; j < tot; j += NT) {
+    uint64_t w;
+    if constexpr (sizeof(R) == 16) w = ((const ulonglong2*)sp)[j].x;
+    else w = (uint64_t)((const int64_t*)sp)[j];
+    const uint32_t kr = (uint32_t)(w >> 32) & kmask;
+    mn = kr < mn ? kr : mn;
+    mx = kr > mx ? kr : mx;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if ((threadIdx.x & 63) == 0 && mx >= mn) {
+    atomicMin(&lkr[0], mn);
+    atomicMax(&lkr[1], mx);
   }
 }
 
+// LDS of a step-run scatter: per bucket its step count and staged base, the staged records (and
+// their ts words when W).
+__host__ __device__ constexpr size_t run_stage_lds(int nb, int S, int rec_bytes, bool w) {
+  return (size_t)nb * 8 + (size_t)S * rec_bytes + (w ? (size_t)S * 4 : 0);
+}
+
+// The time base, the key base and the tile's key range — shared by both scatters.  T0: the stream
+// time before the push, else the first ts (k_c1_check's 31-bit ts test is relative to it).  kb:
+// the host's base (the last push's key minimum less a margin), else keys[0] − half the key field;
+// the records hold (key − kb), and k_c1_check rebases them to the push's key minimum (CI_KSHIFT)
+// or declines when some key falls outside the field.
+__device__ __forceinline__ void run_bases(const int64_t* __restrict__ keys, const int64_t* __restrict__ ts, int64_t n,
+                                          const int64_t* __restrict__ stream_time, int64_t kb_in, int has_kb,
+                                          int kfield, int64_t* ci, int64_t* T0, int64_t* kb) {
+  const int64_t st0 = *stream_time;
+  const int64_t t0 = n > 0 ? ts[0] : 0;
+  *T0 = st0 >= 0 ? st0 : (t0 > 0 ? t0 : 0);
+  *kb = has_kb ? kb_in : (int64_t)((uint64_t)keys[0] - (1ULL << (kfield - 1)));
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    ci[CI_T0] = *T0;
+    ci[CI_KBASE] = *kb;
+  }
+}
+
+// The workgroup's key range → CI_KMIN / CI_KMAX atomics (kb + the staged offsets' extremes), and
+// CI_KFAIL when some key fell outside the record's key field above kb (thread 0, after the loop).
+__device__ __forceinline__ void run_krange(const uint32_t* lkr, int kfail, int64_t kb, int64_t* ci) {
+  if (lkr[1] >= lkr[0]) {
+    atomicMin((long long*)&ci[CI_KMIN], (long long)((uint64_t)kb + lkr[0]));
+    atomicMax((long long*)&ci[CI_KMAX], (long long)((uint64_t)kb + lkr[1]));
+  }
+  if (kfail) atomicOr((unsigned long long*)&ci[CI_KFAIL], 1ULL);
+}
+
+// ------------------------------------------------------------------ k_c1_scatter
+// Records of tile t → step runs.  8-byte record: (key - kb) << 32 | (uint32)(ts - T0); invalid
+// records keep their key word (their bucket is the key's) with the sentinel low word.
+// WIDE (the key range does not fit 32 bits): the record is the 64-bit key hash (key = its inverse)
+// and ts - T0 goes to a parallel u32 array (srecT), staged beside it.
 template <int U, int NT, bool WIDE, bool ST>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_c1_scatter(
     const int64_t* __restrict__ keys, const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
-    const uint8_t* __restrict__ rv, int64_t n, int64_t nT, int log2B, const uint32_t* __restrict__ offs,
-    uint64_t* __restrict__ srec, int64_t* __restrict__ tilestat, int64_t* __restrict__ tpart,
-    int64_t* __restrict__ ci, const int64_t* __restrict__ st_at, uint32_t* __restrict__ srecT, int64_t size, int64_t adv,
-    FastDiv fd, int64_t grace) {
+    const uint8_t* __restrict__ rv, int64_t n, int64_t nT, int log2B, uint32_t* __restrict__ rcnt,
+    uint16_t* __restrict__ roff, int64_t nSt, uint64_t* __restrict__ srec, int64_t* __restrict__ tilestat,
+    int64_t* __restrict__ tpart, int64_t* __restrict__ ci, const int64_t* __restrict__ st_at,
+    uint32_t* __restrict__ srecT, int64_t size, int64_t adv, FastDiv fd, int64_t grace,
+    const int64_t* __restrict__ stream_time, int64_t kb_in, int has_kb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int wsum[NT / 64];
   __shared__ unsigned long long lc[4];
   __shared__ int lt[2][2];  // [step parity][max | min] of the step's accepted ts - T0 (LDS atomics)
-  __shared__ int lfail;
+  __shared__ int lfail, lkfail;
+  __shared__ uint32_t lkr[2];  // min / max of the staged key offsets (not WIDE)
   constexpr int S = U * NT;
+  constexpr int SPT = C1_TILE / S;
   const int B = 1 << log2B;
   const int64_t t = tile_of(blockIdx.x, nT);
-  const StageR8 L = stage_r8_carve(smem, B, S, wsum);
-  uint32_t* lt32 = (uint32_t*)(smem + stage_r8_lds_bytes(B, S));  // WIDE: the staged ts - T0
-  for (int b = threadIdx.x; b < B; b += NT) {
-    L.cur[b] = offs[t * B + b];
-    L.cnt[b] = 0u;
-  }
+  uint32_t* cnt = (uint32_t*)smem;
+  uint32_t* sbase = cnt + B;
+  int64_t* sp = (int64_t*)(smem + (size_t)B * 8);
+  uint32_t* lt32 = (uint32_t*)(sp + S);  // WIDE: the staged ts - T0
+  for (int b = threadIdx.x; b < B; b += NT) cnt[b] = 0u;
   if (threadIdx.x < 4) lc[threadIdx.x] = 0;
   if (threadIdx.x < 2) {
     lt[threadIdx.x][0] = INT32_MIN;
     lt[threadIdx.x][1] = INT32_MAX;
   }
-  if (threadIdx.x == 0) lfail = 0;
-  const int64_t kmin = ci_ld(ci, CI_KMIN), T0 = ci_ld(ci, CI_T0);
+  if (threadIdx.x == 0) {
+    lfail = lkfail = 0;
+    lkr[0] = 0xFFFFFFFFu;
+    lkr[1] = 0u;
+  }
+  int64_t T0, kb;
+  run_bases(keys, ts, n, stream_time, kb_in, has_kb, 32, ci, &T0, &kb);
   const int shift = log2B == 0 ? 64 : 64 - log2B;
   const uint32_t bmask = (uint32_t)(B - 1);
   const int64_t base = t * C1_TILE;
   const int64_t end = base + C1_TILE < n ? base + C1_TILE : n;
   int c_acc = 0, c_nk = 0, c_nr = 0, c_bt = 0;  // < 2^16 per tile
+  uint32_t kor = 0u;
   int64_t x[U], k[U];
   auto load_step = [&](int64_t i0, int64_t (&dx)[U], int64_t (&dk)[U]) {
 #pragma unroll
@@ -327,12 +324,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
       const uint64_t hk = key_hash(k[u]);
       bin[u] = stage_bin(hk, shift, bmask);
       t32[u] = valid ? (uint32_t)d : C1_SENT;
-      rec[u] = WIDE ? (int64_t)hk : (int64_t)(((uint64_t)(k[u] - kmin) << 32) | (uint64_t)t32[u]);
+      const uint64_t kd = (uint64_t)k[u] - (uint64_t)kb;
+      if (!WIDE) kor |= ok[u] ? (uint32_t)(kd >> 32) : 0u;  // nonzero: a key outside the field above kb
+      rec[u] = WIDE ? (int64_t)hk : (int64_t)((kd << 32) | (uint64_t)t32[u]);
     }
     // the next step's loads go into x / k (dead now) and stay in flight through this step's stage
     if (s0 + S < end) load_step(i0 + S, x, k);
-    if constexpr (WIDE) stage_step_c1w<U, NT>(rec, t32, bin, ok, B, L, lt32, srec, srecT);
-    else stage_step_r8<U, NT>(rec, bin, ok, B, L, srec);
+    const uint32_t tot = stage_step_runs<U, NT, int64_t, WIDE>(rec, t32, bin, ok, B, cnt, sbase, wsum, sp, lt32,
+                                                               (int64_t*)srec, srecT, t * SPT + st, nSt, rcnt, roff);
+    if (!WIDE) step_krange<NT, int64_t>(sp, tot, 0xFFFFFFFFu, lkr);
     // the step's ts range: the wave's first (one LDS atomic per wave, not 64 to one address),
     // after the stage so that its registers are free; published by thread 0 one step later
     // (after the next stage's barriers), the last step's after the loop
@@ -347,8 +347,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
     if (threadIdx.x == 0 && st > 0) publish(s0 - S, st - 1);
   }
+  // the last tile's steps past the input: empty runs
+  for (int st = st_last + 1; st < SPT; st++)
+    for (int b = threadIdx.x; b < B; b += NT) rcnt[(int64_t)b * nSt + t * SPT + st] = 0u;
+  if (!WIDE && kor) lkfail = 1;
   __syncthreads();
   if (threadIdx.x == 0 && s0 > base) publish(s0 - S, st_last);
+  if (!WIDE && threadIdx.x == 0) run_krange(lkr, lkfail, kb, ci);
   c_acc = wave_sum(c_acc);
   c_nk = wave_sum(c_nk);
   c_nr = wave_sum(c_nr);
@@ -375,6 +380,86 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     ts4[2] = t_bound;
     ts4[3] = t_ok ? 1 : 0;
   }
+}
+
+// The exact key range of a push (the host's fallback when a key fell outside the key field; keys
+// every `stride` words):
+// out[0] = max of ~key (= ~min), out[1] = max of key (both start at INT64_MIN).
+__global__ __launch_bounds__(256) void k_c1_krange(const int64_t* __restrict__ keys, int64_t stride, int64_t n,
+                                                   long long* __restrict__ out) {
+  int64_t mx = INT64_MIN, mxn = INT64_MIN;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = keys[i * stride];
+    mx = k > mx ? k : mx;
+    mxn = ~k > mxn ? ~k : mxn;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const int64_t a = __shfl_xor(mx, off, 64), b = __shfl_xor(mxn, off, 64);
+    mx = a > mx ? a : mx;
+    mxn = b > mxn ? b : mxn;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(&out[0], (long long)mxn);
+    atomicMax(&out[1], (long long)mx);
+  }
+}
+
+// Bucket bases from the scanned run counts: bb[b] = rpos[b][0], bb[B] = the total.
+__global__ __launch_bounds__(256) void k_c1_bases(const uint32_t* __restrict__ rpos, int64_t nSt, int B,
+                                                  int64_t* __restrict__ bb) {
+  for (int b = threadIdx.x; b <= B; b += blockDim.x) bb[b] = (int64_t)rpos[(int64_t)b * nSt];
+}
+
+// Refine work item w → its bucket (cstart), its first step s0 and run count R (cinfo[2w],
+// [2w + 1]): one thread per item, binary searches over cstart and the bucket's scanned run
+// positions — so a refine workgroup starts with one round of table loads, not the searches.
+__global__ __launch_bounds__(256) void k_c1_chunks(const int* __restrict__ cstart, int B, const int64_t* __restrict__ bb,
+                                                   const uint32_t* __restrict__ rpos, int64_t nSt, int ch,
+                                                   const int64_t* __restrict__ ci, uint32_t* __restrict__ cinfo) {
+  if (ci_ld(ci, CI_GATE) == 0) return;
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= (int)ci_ld(ci, CI_NCHUNK)) return;
+  int a = 0, e = B;  // the last bucket with cstart[b] <= w, in [a, e)
+  while (e - a > 1) {
+    const int m = (a + e) >> 1;
+    if (cstart[m] <= w) a = m;
+    else e = m;
+  }
+  const int b = a;
+  const int64_t lo = bb[b] + (int64_t)(w - cstart[b]) * ch;
+  const int64_t len = bb[b + 1] - lo < ch ? bb[b + 1] - lo : ch;
+  const uint32_t* rp = rpos + (int64_t)b * nSt;
+  int64_t sa = 0, se = nSt;  // s0: the last step whose run starts at or before lo
+  while (se - sa > 1) {
+    const int64_t m = (sa + se) >> 1;
+    if ((int64_t)rp[m] <= lo) sa = m;
+    else se = m;
+  }
+  int64_t ta = sa, te = nSt;  // the first step after s0 whose run starts at or past lo + len (or nSt)
+  while (te - ta > 1) {
+    const int64_t m = (ta + te) >> 1;
+    if ((int64_t)rp[m] < lo + len) ta = m;
+    else te = m;
+  }
+  cinfo[2 * w] = (uint32_t)sa;
+  cinfo[2 * w + 1] = (uint32_t)(te - sa);
+}
+
+// The chunk's source positions: map[j] = where the chunk's record j lies in the step runs (u32 per
+// record, in the refine's not yet used stage).  One thread per run of the chunk (cinfo): one round
+// of loads of its position / end / step offset, then the run's slice of the map.
+__device__ __forceinline__ void chunk_map(const uint32_t* __restrict__ rp, const uint16_t* __restrict__ ro,
+                                          const uint32_t* __restrict__ cinfo, int w, int64_t S, int64_t lo, int len,
+                                          uint32_t* map) {
+  const int64_t s0 = cinfo[2 * w];
+  const int R = (int)cinfo[2 * w + 1];
+  for (int k = threadIdx.x; k < R; k += blockDim.x) {
+    const int64_t s = s0 + k, p = (int64_t)rp[s], pe = (int64_t)rp[s + 1];  // rp[nSt] = the next bucket's start
+    const int64_t a = p > lo ? p : lo, e = pe < lo + len ? pe : lo + len;
+    const uint32_t src = (uint32_t)(s * S + (int64_t)ro[s] + (a - p));
+    for (int64_t x = a; x < e; x++) map[x - lo] = src + (uint32_t)(x - a);
+  }
+  __syncthreads();
 }
 
 // ------------------------------------------------------------------ k_c1_check
@@ -450,20 +535,28 @@ __global__ __launch_bounds__(1024) void k_c1_check(
   }
   cstart[B] = acc;
   const int64_t kmin = ci_ld(ci, CI_KMIN), kmax = ci_ld(ci, CI_KMAX);
-  const bool tfail = ci_ld(ci, CI_TFAIL) != 0;
+  const bool tfail = ci_ld(ci, CI_TFAIL) != 0, kfail = ci_ld(ci, CI_KFAIL) != 0;
   ci[CI_KMIN] = INT64_MAX;  // ready for the next push's atomics
   ci[CI_KMAX] = INT64_MIN;
   ci[CI_TFAIL] = 0;
-  bool ok = !lslow && !tfail && mxc <= C1_SEGMAX && kmax >= kmin;
+  ci[CI_KFAIL] = 0;
+  // (wide records: the scatter tracks no key range)
+  bool ok = !lslow && !tfail && mxc <= C1_SEGMAX && (wide || kmax >= kmin);
 #ifdef KHIP_TUNING
   if (ci[CI_N - 1] == 1)  // debug (tuning build, KHIP_C1_DEBUG=1): the decision's inputs
     printf("[c1 check] tfail %d slow %d mxc %d kmin %ld kmax %ld gmn %ld gmx %ld T0 %ld st0 %ld nT %ld\n", (int)tfail,
            (int)lslow, mxc, (long)kmin, (long)kmax, (long)gmn, (long)gmx, (long)ci[CI_T0], (long)st0, (long)nT);
 #endif
+  // compact records: every key within the key field above the push's base kb (the scatters wrote
+  // key - kb; kfail: some key was not — the host then learns the true range and re-runs the push
+  // with kb = kmin, or with wide records), and the range within 32 key bits (value records 31)
   const uint64_t krange = kmax >= kmin ? (uint64_t)kmax - (uint64_t)kmin : 0;
-  const bool fits = krange < ((1ULL << kbmax) - 1);  // compact records: 32 key bits (value records 31)
+  const bool fits = !wide && !kfail && krange < ((1ULL << kbmax) - 1);
+  const int64_t kb = ci_ld(ci, CI_KBASE);
   ci[CI_FITS] = fits ? 1 : 0;
-  ci[CI_REASON] = ok && !wide && !fits ? 1 : 0;
+  ci[CI_REASON] = ok && !wide && kfail ? 2 : (ok && !wide && !fits ? 1 : 0);
+  ci[CI_KMINC] = kmin;
+  ci[CI_KSHIFT] = (int64_t)((uint64_t)kmin - (uint64_t)kb);
   ok = ok && (wide || fits);
   // window range of this push's records and of the live resident rows (k_part_wrange)
   int64_t lo = INT64_MAX, hi = INT64_MIN;
@@ -499,7 +592,6 @@ __global__ __launch_bounds__(1024) void k_c1_check(
   ci[CI_TMIN] = gmx >= 0 ? gmn : 0;
   ci[CI_TMAX] = gmx;
   ci[CI_NCHUNK] = acc;
-  ci[CI_KMINC] = kmin;
   *stream_time = gmx > st0 ? gmx : st0;
   res[0] = none ? INT64_MAX : lo;
   res[1] = none ? INT64_MIN : hi;
@@ -517,15 +609,15 @@ template <int U, int NT, bool WIDE>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_c1_refine(
     const uint64_t* __restrict__ srcA, const int64_t* __restrict__ bb, const int* __restrict__ cstart, int log2B,
     int log2P, int fbits, uint64_t* __restrict__ srec, uint16_t* __restrict__ seg, const int64_t* __restrict__ ci,
-    const uint32_t* __restrict__ srcAT, uint32_t* __restrict__ srecT) {
+    const uint32_t* __restrict__ srcAT, uint32_t* __restrict__ srecT, const uint32_t* __restrict__ rpos,
+    const uint16_t* __restrict__ roff, int64_t nSt, int64_t S, const uint32_t* __restrict__ cinfo) {
   if (ci_ld(ci, CI_GATE) == 0) return;
   const int w = blockIdx.x;
   if (w >= (int)ci_ld(ci, CI_NCHUNK)) return;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int lb, lnv;
   __shared__ int wsum[NT / 64];
-  constexpr int S = U * NT;
-  static_assert(S == C1_CH, "refine chunk");
+  static_assert(U * NT == C1_CH, "refine chunk");
   const int F = 1 << fbits, B = 1 << log2B;
   uint32_t* cnt = (uint32_t*)smem;
   uint32_t* sbase = cnt + F;
@@ -542,15 +634,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const int64_t bend = bb[b + 1];
   const int len = (int)(bend - lo < C1_CH ? bend - lo : C1_CH);
   const int64_t kmin = ci_ld(ci, CI_KMINC);
+  const uint64_t kshift = WIDE ? 0 : (uint64_t)ci_ld(ci, CI_KSHIFT) << 32;  // records hold key - kb
   const int shift = 64 - log2P;
+  // where the chunk's records lie in the step runs (a map in the not yet used stage)
+  const uint32_t* rp = rpos + (int64_t)b * nSt;
+  const uint16_t* ro = roff + (int64_t)b * nSt;
+  chunk_map(rp, ro, cinfo, w, S, lo, len, (uint32_t*)stage);
   uint64_t r[U];
   uint32_t f[U], rank[U], t32[U];
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const int j = threadIdx.x + u * NT;
-    const int jj = j < len ? j : len - 1;
-    r[u] = __builtin_nontemporal_load(srcA + lo + jj);
-    if constexpr (WIDE) t32[u] = __builtin_nontemporal_load(srcAT + lo + jj);
+    const uint32_t src = ((const uint32_t*)stage)[j < len ? j : len - 1];
+    r[u] = __builtin_nontemporal_load(srcA + src) - kshift;
+    if constexpr (WIDE) t32[u] = __builtin_nontemporal_load(srcAT + src);
   }
 #pragma unroll
   for (int u = 0; u < U; u++) {
@@ -1230,104 +1327,68 @@ struct C1VCol {
   int32_t type;
 };
 
-// LDS stage of one scatter step of 16-byte records: per bin its output cursor, step count, staged
-// base and output position, then the staged records and their bins.
-template <int U, int NT>
-__device__ __forceinline__ void stage_step_v(const ulonglong2 (&rec)[U], const uint32_t (&bin)[U], const bool (&ok)[U],
-                                             int nb, uint32_t* cur, uint32_t* cnt, uint32_t* sbase, uint32_t* gpos,
-                                             ulonglong2* sp, uint16_t* sbin, int* wsum, ulonglong2* __restrict__ srec) {
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  uint32_t rank[U];
-#pragma unroll
-  for (int u = 0; u < U; u++) rank[u] = ok[u] ? atomicAdd(&cnt[bin[u]], 1u) : 0u;
-  lds_barrier();
-  const uint32_t c = t < nb ? cnt[t] : 0u;
-  uint32_t incl = c;
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += y;
-  }
-  if (lane == 63) wsum[wave] = (int)incl;
-  lds_barrier();
-  uint32_t before = 0, tot = 0;
-#pragma unroll
-  for (int k = 0; k < NT / 64; k++) {
-    before += k < wave ? (uint32_t)wsum[k] : 0u;
-    tot += (uint32_t)wsum[k];
-  }
-  if (t < nb) {
-    sbase[t] = before + incl - c;
-    gpos[t] = cur[t];
-    cur[t] += c;
-    cnt[t] = 0u;
-  }
-  lds_barrier();
-#pragma unroll
-  for (int u = 0; u < U; u++)
-    if (ok[u]) {
-      const uint32_t i = sbase[bin[u]] + rank[u];
-      sp[i] = rec[u];
-      sbin[i] = (uint16_t)bin[u];
-    }
-  lds_barrier();
-  for (uint32_t j = t; j < tot; j += NT) {
-    const uint32_t b = sbin[j];
-    srec[(uint64_t)gpos[b] + (j - sbase[b])] = sp[j];
-  }
-}
 
-__host__ __device__ constexpr size_t c1v_stage_lds(int nb, int S) {
-  return (size_t)nb * 16 + (size_t)S * 16 + ((size_t)S * 2 + 15) / 16 * 16;
-}
-
-// Records of tile t → their bucket's run, as k_c1_scatter, 16 bytes each.  HOP: the windows
+// Records of tile t → step runs, as k_c1_scatter, 16 bytes each (key - kb in 31 bits, the
+// argument's non-null flag in bit 63).  HOP: the windows
 // applied per accepted record (windowsFor's count) for the batch statistics.
-template <int U, int NT, bool ST>
+template <int U, int NT, bool ST, bool ROWS>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_c1v_scatter(
     const int64_t* __restrict__ keys, const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
-    const uint8_t* __restrict__ rv, C1VCol vc, int64_t n, int64_t nT, int log2B, const uint32_t* __restrict__ offs,
-    ulonglong2* __restrict__ srec, int64_t* __restrict__ tilestat, int64_t* __restrict__ tpart,
-    int64_t* __restrict__ ci, const int64_t* __restrict__ st_at, int64_t size, int64_t adv, FastDiv fd, int hop,
-    int64_t grace) {
+    const uint8_t* __restrict__ rv, C1VCol vc, RowsIn ri, int64_t n, int64_t nT, int log2B, uint32_t* __restrict__ rcnt,
+    uint16_t* __restrict__ roff, int64_t nSt, ulonglong2* __restrict__ srec, int64_t* __restrict__ tilestat,
+    int64_t* __restrict__ tpart, int64_t* __restrict__ ci, const int64_t* __restrict__ st_at, int64_t size, int64_t adv,
+    FastDiv fd, int hop, int64_t grace, const int64_t* __restrict__ stream_time, int64_t kb_in, int has_kb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int wsum[NT / 64];
   __shared__ unsigned long long lc[5];
   __shared__ int lt[2][2];
-  __shared__ int lfail;
+  __shared__ int lfail, lkfail;
+  __shared__ uint32_t lkr[2];  // min / max of the staged key offsets
   constexpr int S = U * NT;
+  constexpr int SPT = C1_TILE / S;
   const int B = 1 << log2B;
   const int64_t t = tile_of(blockIdx.x, nT);
-  uint32_t* cur = (uint32_t*)smem;
-  uint32_t* cnt = cur + B;
+  uint32_t* cnt = (uint32_t*)smem;
   uint32_t* sbase = cnt + B;
-  uint32_t* gpos = sbase + B;
-  ulonglong2* sp = (ulonglong2*)(smem + (size_t)B * 16);
-  uint16_t* sbin = (uint16_t*)(sp + S);
-  for (int b = threadIdx.x; b < B; b += NT) {
-    cur[b] = offs[t * B + b];
-    cnt[b] = 0u;
-  }
+  ulonglong2* sp = (ulonglong2*)(smem + (size_t)B * 8);  // B >= 32: 16-byte aligned
+  for (int b = threadIdx.x; b < B; b += NT) cnt[b] = 0u;
   if (threadIdx.x < 5) lc[threadIdx.x] = 0;
   if (threadIdx.x < 2) {
     lt[threadIdx.x][0] = INT32_MIN;
     lt[threadIdx.x][1] = INT32_MAX;
   }
-  if (threadIdx.x == 0) lfail = 0;
-  const int64_t kmin = ci_ld(ci, CI_KMIN), T0 = ci_ld(ci, CI_T0);
+  if (threadIdx.x == 0) {
+    lfail = lkfail = 0;
+    lkr[0] = 0xFFFFFFFFu;
+    lkr[1] = 0u;
+  }
+  int64_t T0, kb;
+  if constexpr (ROWS) run_bases((const int64_t*)ri.rows, (const int64_t*)ri.rows + 1, n, stream_time, kb_in, has_kb, 31, ci, &T0, &kb);
+  else run_bases(keys, ts, n, stream_time, kb_in, has_kb, 31, ci, &T0, &kb);
   const int shift = log2B == 0 ? 64 : 64 - log2B;
   const uint32_t bmask = (uint32_t)(B - 1);
   const int64_t base = t * C1_TILE;
   const int64_t end = base + C1_TILE < n ? base + C1_TILE : n;
   int c_acc = 0, c_nk = 0, c_nr = 0, c_bt = 0, c_app = 0;
+  uint32_t kor = 0u;
   int64_t x[U], k[U], v[U];
+  uint32_t vm[ROWS ? U : 1];  // ROWS: the rows' validity words (low half)
   auto load_step = [&](int64_t i0) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
       int64_t i = i0 + (int64_t)u * NT;
       i = i < end ? i : end - 1;
-      x[u] = ts[i];
-      k[u] = keys[i];
-      v[u] = vc.type == KHIP_TYPE_INT32 ? (int64_t)((const int32_t*)vc.data)[i] : ((const int64_t*)vc.data)[i];
+      if constexpr (ROWS) {
+        const uint64_t* r = ri.rows + i * (int64_t)ri.rw;
+        k[u] = (int64_t)r[0];
+        x[u] = (int64_t)r[1];
+        v[u] = (int64_t)r[ri.vword];
+        vm[u] = (uint32_t)r[ri.rw - 1];
+      } else {
+        x[u] = ts[i];
+        k[u] = keys[i];
+        v[u] = vc.type == KHIP_TYPE_INT32 ? (int64_t)((const int32_t*)vc.data)[i] : ((const int64_t*)vc.data)[i];
+      }
     }
   };
   int64_t t_rmax = -1, t_min = INT64_MAX, t_bound = INT64_MAX;  // the tile's summary (k_c1_scatter)
@@ -1362,7 +1423,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
       const int64_t i = i0 + (int64_t)u * NT;
       ok[u] = i < end;
       const int64_t ii = ok[u] ? i : base;
-      const bool kok = bit_get(kv, ii), rok = bit_get(rv, ii), vok = bit_get(vc.valid, ii);
+      const bool kok = ROWS || bit_get(kv, ii), rok = ROWS || bit_get(rv, ii);
+      const bool vok = ROWS ? ((vm[ROWS ? u : 0] >> ri.vbit) & 1u) != 0 : bit_get(vc.valid, ii);
       const bool valid = ok[u] && kok && rok && x[u] >= 0;
       c_nk += ok[u] && !kok;
       c_nr += ok[u] && kok && !rok;
@@ -1388,11 +1450,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         c_app += (int)((int64_t)fast_udiv((uint64_t)x[u], fd) - (int64_t)fast_udiv((uint64_t)(lo > 0 ? lo : 0), fd) + 1);
       }
       bin[u] = stage_bin(key_hash(k[u]), shift, bmask);
-      const uint64_t w0 = ((uint64_t)(k[u] - kmin) << 32) | (uint64_t)(valid ? (uint32_t)d : C1_SENT);
+      const uint64_t kd = (uint64_t)k[u] - (uint64_t)kb;
+      kor |= ok[u] ? (uint32_t)(kd >> 31) : 0u;  // nonzero: a key outside the 31-bit field above kb
+      const uint64_t w0 = ((kd & 0x7FFFFFFFull) << 32) | (uint64_t)(valid ? (uint32_t)d : C1_SENT);
       rec[u] = make_ulonglong2(w0 | (vok ? (1ULL << 63) : 0ULL), (uint64_t)v[u]);
     }
     if (s0 + S < end) load_step(i0 + S);
-    stage_step_v<U, NT>(rec, bin, ok, B, cur, cnt, sbase, gpos, sp, sbin, wsum, srec);
+    uint32_t t32u[U];  // (no ts words: 16-byte records carry the ts)
+    const uint32_t tot = stage_step_runs<U, NT, ulonglong2, false>(rec, t32u, bin, ok, B, cnt, sbase, wsum, sp, nullptr,
+                                                                   srec, nullptr, t * SPT + st, nSt, rcnt, roff);
+    step_krange<NT, ulonglong2>(sp, tot, 0x7FFFFFFFu, lkr);
     for (int off = 32; off > 0; off >>= 1) {
       const int a = __shfl_xor(tmx, off, 64), b = __shfl_xor(tmn, off, 64);
       tmx = a > tmx ? a : tmx;
@@ -1404,8 +1471,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
     if (threadIdx.x == 0 && st > 0) publish(s0 - S, st - 1);
   }
+  for (int st = st_last + 1; st < SPT; st++)  // the last tile's steps past the input: empty runs
+    for (int b = threadIdx.x; b < B; b += NT) rcnt[(int64_t)b * nSt + t * SPT + st] = 0u;
+  if (kor) lkfail = 1;
   __syncthreads();
   if (threadIdx.x == 0 && s0 > base) publish(s0 - S, st_last);
+  if (threadIdx.x == 0) run_krange(lkr, lkfail, kb, ci);
   c_acc = wave_sum(c_acc);
   c_nk = wave_sum(c_nk);
   c_nr = wave_sum(c_nr);
@@ -1441,7 +1512,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 template <int U, int NT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_c1v_refine(
     const ulonglong2* __restrict__ srcA, const int64_t* __restrict__ bb, const int* __restrict__ cstart, int log2B,
-    int log2P, int fbits, ulonglong2* __restrict__ srec, uint16_t* __restrict__ seg, const int64_t* __restrict__ ci) {
+    int log2P, int fbits, ulonglong2* __restrict__ srec, uint16_t* __restrict__ seg, const int64_t* __restrict__ ci,
+    const uint32_t* __restrict__ rpos, const uint16_t* __restrict__ roff, int64_t nSt, int64_t S,
+    const uint32_t* __restrict__ cinfo) {
   if (ci_ld(ci, CI_GATE) == 0) return;
   const int w = blockIdx.x;
   if (w >= (int)ci_ld(ci, CI_NCHUNK)) return;
@@ -1466,14 +1539,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const int64_t bend = bb[b + 1];
   const int len = (int)(bend - lo < CH ? bend - lo : CH);
   const int64_t kmin = ci_ld(ci, CI_KMINC);
+  const uint64_t kshift = (uint64_t)ci_ld(ci, CI_KSHIFT) << 32;  // records hold key - kb
   const int shift = 64 - log2P;
+  // where the chunk's records lie in the step runs (a map in the not yet used stage)
+  const uint32_t* rp = rpos + (int64_t)b * nSt;
+  const uint16_t* ro = roff + (int64_t)b * nSt;
+  chunk_map(rp, ro, cinfo, w, S, lo, len, (uint32_t*)stage);
   ulonglong2 r[U];
   uint32_t f[U], rank[U];
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const int j = threadIdx.x + u * NT;
-    const int jj = j < len ? j : len - 1;
-    r[u] = ld_nt2(srcA + lo + jj);
+    const uint32_t src = ((const uint32_t*)stage)[j < len ? j : len - 1];
+    r[u] = ld_nt2(srcA + src);
+    r[u].x -= kshift;
   }
 #pragma unroll
   for (int u = 0; u < U; u++) {
@@ -2303,11 +2382,11 @@ static size_t c1v_layout(khip_agg* a, int log2H, int idw, int log2B, C1VQ* q) {
 // cols != nullptr: the value pipeline over argument column vcol (c1v_eligible).
 khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
                     const uint8_t* rv, int64_t* tot, bool* declined, const int64_t* st_at, bool* retry_wide,
-                    const ColPtrs* cols, int vcol) {
+                    const ColPtrs* cols, int vcol, const RowsIn* rows) {
   PartState& s = a->part;
   *declined = false;
   *retry_wide = false;
-  const bool val = cols != nullptr;
+  const bool val = cols != nullptr || rows != nullptr;
   const bool panes = val && a->desc.window_kind == KHIP_WINDOW_HOPPING;
   const int pbits = panes ? 1 : 0;
   const int CH = val ? C1V_CH : C1_CH;
@@ -2317,15 +2396,17 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
   const int log2B = s.log2P - fbits;
   const int B = 1 << log2B, F = 1 << fbits;
   const int64_t nT = ceil_div(n, C1_TILE);
-  const int TC = (int)std::min<int64_t>(nT, 64);
+  const int64_t S = val ? (int64_t)UV * C1_NT : (int64_t)8 * C1_NT;  // scatter step (records)
+  const int64_t nSt = nT * (C1_TILE / S);                             // steps (runs per bucket)
   const int64_t nchunk_max = ceil_div(n, CH) + B;
-  KHIP_TRY(s.c1hist.ensure((size_t)nT * B * 4));
+  KHIP_TRY(s.c1rc.ensure((size_t)B * nSt * 4));
+  KHIP_TRY(s.c1rp.ensure(((size_t)B * nSt + 1) * 4));
+  KHIP_TRY(s.c1ro.ensure((size_t)B * nSt * 2));
   KHIP_TRY(s.c1bb.ensure((size_t)(B + 1) * 8));
   const size_t seg_bytes = ((size_t)nchunk_max * (F + 1) * 2 + 255) & ~(size_t)255;  // cstart 256-B aligned
   KHIP_TRY(s.c1seg.ensure(seg_bytes + (size_t)(B + 1) * 4));
   KHIP_TRY(s.tilemax.ensure(nT * 32));  // per tile: stream-time max, smallest ts, late bound, ok
   KHIP_TRY(s.tpart.ensure(nT * 8 * T_NPART));
-  KHIP_TRY(s.scan_tmpB.ensure((size_t)TC * B * 8));
   KHIP_TRY(s.prn.ensure((size_t)P * 4));
   KHIP_TRY(s.res.ensure(16));
   KHIP_TRY(s.closed_ctr.ensure(8));
@@ -2368,58 +2449,63 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     nc.p = nullptr;
     s.closed_cap = ncap;
   }
-  // 1. bucket histogram (keys only) → 2. (tile, bucket) offsets
-  ev_record_part(a, 0);
-  const bool vec = ((uintptr_t)keys & 15) == 0;
-  hipLaunchKernelGGL(vec ? k_c1_hist<true> : k_c1_hist<false>, dim3(nT), dim3(C1_NT), 0, a->stream, keys, ts, n, nT,
-                     log2B, s.c1hist.as<uint32_t>(), ci, a->stream_time.as<int64_t>());
-  hipLaunchKernelGGL(k_part_colsum, dim3(ceil_div(B, 256), TC), dim3(256), 0, a->stream, s.c1hist.as<uint32_t>(), nT, B,
-                     TC, s.scan_tmpB.as<int64_t>());
-  hipLaunchKernelGGL(k_part_colbase, dim3(ceil_div(B, 256)), dim3(256), 0, a->stream, s.scan_tmpB.as<int64_t>(), B, TC,
-                     s.c1bb.as<int64_t>());
-  hipLaunchKernelGGL(k_part_pscan, dim3(1), dim3(1024), 0, a->stream, s.c1bb.as<int64_t>(), (int64_t)B);
-  hipLaunchKernelGGL(k_part_colprefix, dim3(ceil_div(B, 256), TC), dim3(256), 0, a->stream, s.c1hist.as<uint32_t>(), nT,
-                     B, TC, s.scan_tmpB.as<int64_t>(), s.c1bb.as<int64_t>(), 1);
-  ev_record_part(a, 1);
   // wide records (key hash + u32 ts words) when the key range did not fit 32 bits last time: the
   // host predicts the format, k_c1_check declines a compact push whose keys do not fit
   const bool wide = !val && s.c1_wide;
   uint32_t* srecAT = (uint32_t*)(s.srecA.as<uint64_t>() + n + 1);  // WIDE ts words (12 B/record in all)
   uint32_t* srecT = (uint32_t*)(s.srec.as<uint64_t>() + n + 1);
-  // 3. records → buckets
+  uint32_t* rc = s.c1rc.as<uint32_t>();
+  uint32_t* rp = s.c1rp.as<uint32_t>();
+  uint16_t* ro = s.c1ro.as<uint16_t>();
+  const int has_kb = s.c1_kb_valid ? 1 : 0;
+  // 1. records → step runs (the key range, time base and bucket counts in the same read)
+  ev_record_part(a, 0);
   if (val) {
-    const C1VCol vc{cols->data[vcol], cols->valid[vcol], a->ap.col_type[vcol]};
-    auto sk = st_at ? k_c1v_scatter<UV, C1_NT, true> : k_c1v_scatter<UV, C1_NT, false>;
-    const size_t lds = c1v_stage_lds(B, UV * C1_NT);
+    const C1VCol vc{rows ? nullptr : cols->data[vcol], rows ? nullptr : cols->valid[vcol], a->ap.col_type[vcol]};
+    const RowsIn ri = rows ? *rows : RowsIn{};
+    auto sk = rows ? k_c1v_scatter<UV, C1_NT, false, true>
+                   : (st_at ? k_c1v_scatter<UV, C1_NT, true, false> : k_c1v_scatter<UV, C1_NT, false, false>);
+    const size_t lds = run_stage_lds(B, UV * C1_NT, 16, false);
     if (lds > 64 * 1024) hipFuncSetAttribute((const void*)sk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(sk, dim3(nT), dim3(C1_NT), lds, a->stream, keys, ts, kv, rv, vc, n, nT, log2B,
-                       s.c1hist.as<uint32_t>(), (ulonglong2*)s.srecA.p, s.tilemax.as<int64_t>(), s.tpart.as<int64_t>(),
-                       ci, st_at, a->desc.size_ms, adv, fd, a->desc.size_ms != adv ? 1 : 0, a->grace);
+    hipLaunchKernelGGL(sk, dim3(nT), dim3(C1_NT), lds, a->stream, keys, ts, kv, rv, vc, ri, n, nT, log2B, rc, ro, nSt,
+                       (ulonglong2*)s.srecA.p, s.tilemax.as<int64_t>(), s.tpart.as<int64_t>(), ci, st_at,
+                       a->desc.size_ms, adv, fd, a->desc.size_ms != adv ? 1 : 0, a->grace,
+                       (const int64_t*)a->stream_time.as<int64_t>(), s.c1_kbase, has_kb);
     KHIP_TRY_HIP(hipGetLastError());
   } else {
     constexpr int U = 8;
     auto sk = wide ? (st_at ? k_c1_scatter<U, C1_NT, true, true> : k_c1_scatter<U, C1_NT, true, false>)
                    : (st_at ? k_c1_scatter<U, C1_NT, false, true> : k_c1_scatter<U, C1_NT, false, false>);
-    const size_t lds = stage_r8_lds_bytes(B, U * C1_NT) + (wide ? (size_t)U * C1_NT * 4 : 0);
+    const size_t lds = run_stage_lds(B, U * C1_NT, 8, wide);
     if (lds > 64 * 1024) hipFuncSetAttribute((const void*)sk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(sk, dim3(nT), dim3(C1_NT), lds, a->stream, keys, ts, kv, rv, n, nT, log2B,
-                       s.c1hist.as<uint32_t>(), s.srecA.as<uint64_t>(), s.tilemax.as<int64_t>(), s.tpart.as<int64_t>(),
-                       ci, st_at, srecAT, a->desc.size_ms, adv, fd, a->grace);
+    hipLaunchKernelGGL(sk, dim3(nT), dim3(C1_NT), lds, a->stream, keys, ts, kv, rv, n, nT, log2B, rc, ro, nSt,
+                       s.srecA.as<uint64_t>(), s.tilemax.as<int64_t>(), s.tpart.as<int64_t>(), ci, st_at, srecAT,
+                       a->desc.size_ms, adv, fd, a->grace, (const int64_t*)a->stream_time.as<int64_t>(), s.c1_kbase,
+                       has_kb);
     KHIP_TRY_HIP(hipGetLastError());
   }
+  // 2. each (bucket, step) run's place in its bucket's order; the bucket bases
+  KHIP_TRY((ksort::scan_excl<uint32_t, uint32_t>(a->stream, s.c1scan, rc, rp, (int64_t)B * nSt, true, nullptr)));
+  hipLaunchKernelGGL(k_c1_bases, dim3(1), dim3(256), 0, a->stream, (const uint32_t*)rp, nSt, B, s.c1bb.as<int64_t>());
+  ev_record_part(a, 1);
   // 4. accept or decline
   hipLaunchKernelGGL(k_c1_check, dim3(1), dim3(1024), 0, a->stream, s.tilemax.as<int64_t>(), nT,
                      a->desc.size_ms, adv, fd, a->grace, close0, s.res_fresh ? 1 : 0, log2B, s.log2P, wide ? 1 : 0,
                      val ? C1V_CH : C1_CH, val ? 31 : 32, pbits, s.c1bb.as<int64_t>(), cstart, ci, a->stream_time.as<int64_t>(), s.res.as<int64_t>(),
                      s.ctr.as<unsigned long long>(), s.closed_ctr.as<unsigned long long>(),
                      (unsigned long long)s.closed_n);
-  // 5. refine: chunks → partition-sorted, segment table
+  // 5. refine: each chunk's step runs (k_c1_chunks), chunks → partition-sorted, segment table
+  KHIP_TRY(s.c1ci.ensure((size_t)nchunk_max * 8));
+  hipLaunchKernelGGL(k_c1_chunks, dim3((unsigned)ceil_div(nchunk_max, 256)), dim3(256), 0, a->stream, (const int*)cstart, B,
+                     (const int64_t*)s.c1bb.as<int64_t>(), (const uint32_t*)rp, nSt, CH, (const int64_t*)ci,
+                     s.c1ci.as<uint32_t>());
   if (val) {
     auto rk = k_c1v_refine<C1V_CH / C1_NT, C1_NT>;
     const size_t lds = (((size_t)F * 8 + 15) & ~(size_t)15) + (size_t)C1V_CH * 16;
     hipFuncSetAttribute((const void*)rk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(rk, dim3((unsigned)nchunk_max), dim3(C1_NT), lds, a->stream, (const ulonglong2*)s.srecA.p,
-                       s.c1bb.as<int64_t>(), cstart, log2B, s.log2P, fbits, (ulonglong2*)s.srec.p, seg, ci);
+                       s.c1bb.as<int64_t>(), cstart, log2B, s.log2P, fbits, (ulonglong2*)s.srec.p, seg, ci,
+                       (const uint32_t*)rp, (const uint16_t*)ro, nSt, S, (const uint32_t*)s.c1ci.as<uint32_t>());
     KHIP_TRY_HIP(hipGetLastError());
   } else {
     constexpr int U = C1_CH / C1_NT;
@@ -2428,7 +2514,8 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     if (lds > 64 * 1024) hipFuncSetAttribute((const void*)rk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(rk, dim3((unsigned)nchunk_max), dim3(C1_NT), lds, a->stream,
                        s.srecA.as<uint64_t>(), s.c1bb.as<int64_t>(), cstart, log2B, s.log2P, fbits,
-                       s.srec.as<uint64_t>(), seg, ci, (const uint32_t*)srecAT, srecT);
+                       s.srec.as<uint64_t>(), seg, ci, (const uint32_t*)srecAT, srecT, (const uint32_t*)rp,
+                       (const uint16_t*)ro, nSt, S, (const uint32_t*)s.c1ci.as<uint32_t>());
     KHIP_TRY_HIP(hipGetLastError());
   }
   ev_record_part(a, 2);
@@ -2571,12 +2658,40 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
     const int64_t* hci = s.pinfo.as<int64_t>() + 32;
     if (pass == 0 && hci[CI_GATE] == 0) {  // declined: nothing was written
+      if (hci[CI_REASON] == 2 && !s.c1_kretry) {  // a key outside the field above kb: the true range
+        long long kr[2] = {INT64_MIN, INT64_MIN};
+        KHIP_TRY(s.c1scan.ensure(16));
+        KHIP_TRY_HIP(hipMemcpyAsync(s.c1scan.p, kr, 16, hipMemcpyHostToDevice, a->stream));
+        hipLaunchKernelGGL(k_c1_krange, dim3((unsigned)std::min<int64_t>(ceil_div(n, 256), 2048)), dim3(256), 0,
+                           a->stream, rows ? (const int64_t*)rows->rows : keys, rows ? (int64_t)rows->rw : 1, n,
+                           s.c1scan.as<long long>());
+        KHIP_TRY_HIP(hipMemcpyAsync(kr, s.c1scan.p, 16, hipMemcpyDeviceToHost, a->stream));
+        KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+        const int64_t kmin = (int64_t)~(uint64_t)kr[0], kmax = (int64_t)kr[1];
+        if ((uint64_t)kmax - (uint64_t)kmin < (1ULL << (val ? 31 : 32)) - 1) {  // again with kb = kmin
+          s.c1_kbase = kmin;
+          s.c1_kb_valid = true;
+          s.c1_kretry = true;
+          const khip_status r = c1_push(a, n, keys, ts, kv, rv, tot, declined, st_at, retry_wide, cols, vcol, rows);
+          s.c1_kretry = false;
+          return r;
+        }
+        *declined = true;
+        *retry_wide = !val;  // the range itself is past the compact records
+        if (*retry_wide) s.c1_wide = true;
+        return KHIP_OK;
+      }
       *declined = true;
       *retry_wide = !val && hci[CI_REASON] == 1;  // only the record format was wrong
       if (*retry_wide) s.c1_wide = true;
       return KHIP_OK;
     }
-    if (pass == 0 && wide && hci[CI_FITS]) s.c1_wide = false;  // compact records fit again next time
+    if (pass == 0 && wide && ++s.c1_wide_n % 64 == 0) s.c1_wide = false;  // now and then: compact records again?
+    if (pass == 0 && !wide) {  // the next push's key base: this one's minimum, less a margin for keys below it
+      const int64_t km = hci[CI_KMINC], slack = (int64_t)1 << (val ? 26 : 28);
+      s.c1_kbase = km >= INT64_MIN + slack ? km - slack : km;
+      s.c1_kb_valid = true;
+    }
     if (dbg) {
       unsigned long long ph[8] = {};
       if (hipMemcpy(ph, dbgbuf.p, sizeof(ph), hipMemcpyDeviceToHost) == hipSuccess) {

@@ -348,10 +348,15 @@ struct PartState {
   int64_t having_total = 0;
   bool hvalid = true;
   HostBuf pinfo;  // pinned: push info (window range, event-time span) and end-of-push stats
-  // COUNT(*) pipeline (khip_agg_c1.hip): per-tile bucket counts / offsets, bucket bases, the
+  // COUNT(*) pipeline (khip_agg_c1.hip): bucket bases, the
   // refine's per-chunk partition offsets, records of each partition in the last push (prn), and
   // whether the last push took that pipeline (k_part_chg then reads prn instead of pbase)
-  DevBuf c1hist, c1bb, c1seg, c1info, prn;
+  DevBuf c1bb, c1seg, c1info, prn;
+  DevBuf c1rc, c1rp, c1ro, c1scan, c1ci;  // step-run layout: [bucket][step] counts, their scan, step
+                                          // offsets; per refine chunk its first step and run count
+  int64_t c1_kbase = 0;             // key base for the next push's records (valid when c1_kb_valid)
+  bool c1_kb_valid = false, c1_kretry = false;
+  int64_t c1_wide_n = 0;            // pushes with wide records (compact ones are tried every 64th)
   bool last_c1 = false;
   int c1_skip = 0;  // pushes left before the pipeline is tried again after a declined push
   DevBuf c1vq;  // the value pipeline's merge parameters (device copy)
@@ -459,6 +464,15 @@ khip_status part_reset(khip_agg* a);
 // st_at: per-row stream time (ABI 5 domains other than TASK), or null (computed per handle)
 khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
                       const uint8_t* rv, const ColPtrs& cols, int64_t* tot, const int64_t* st_at);
+// Shuffled rows as the input (khip_agg_push_shuffled): khip_shuffle_pack's row layout, rw words
+// per row — [key][ts][columns except the key column][validity bits] — the argument in word
+// vword, its validity in bit vbit of the last word.  Every row has a key, a row and ts >= 0.
+struct RowsIn {
+  const uint64_t* rows;
+  int32_t rw, vword, vbit;
+};
+void shuffle_layout(const khip_shuffle* s, int* key_col, int* n_cols, const int32_t** types);
+khip_status part_push_rows(khip_agg* a, int64_t n, const RowsIn& ri, int key_col, int64_t* tot, bool* done);
 khip_status part_compact(khip_agg* a, const HavingDev& h, std::vector<uint64_t>* rows, int64_t* count);
 bool part_having_count(khip_agg* a, int64_t* n);
 khip_status part_changes(khip_agg* a, std::vector<uint64_t>* rows, std::vector<uint8_t>* tomb, int64_t* count);

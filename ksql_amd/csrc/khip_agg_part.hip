@@ -3589,7 +3589,7 @@ void part_release(khip_agg* a) {
   DevBuf* bufs[] = {&s.hcnt, &s.hnew, &s.srecA, &s.hcoarse, &s.scan_tmpB, &s.RB, &s.wr, &s.res, &s.closed, &s.closed_ctr, &s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist,
                     &s.tilemax, &s.tilemin, &s.tilekr,
                     &s.tileprefix, &s.tpart, &s.scan_tmp, &s.srec, &s.work,
-                    &s.c1hist, &s.c1bb, &s.c1seg, &s.c1info, &s.prn,
+                    &s.c1rc, &s.c1rp, &s.c1ro, &s.c1scan, &s.c1ci, &s.c1bb, &s.c1seg, &s.c1info, &s.prn, &s.c1vq,
                     &s.pbase, &s.R, &s.ctr, &s.counts};
   for (DevBuf* b : bufs) b->release();
 }
@@ -3764,6 +3764,27 @@ static void agg_probe_report(DevBuf& b, int nb) {
 }
 
 // One push slice (n < 2^31).  tot[] receives the P_* counters.
+// Shuffled rows (khip_agg_push_shuffled) through the value pipeline, read where they lie; *done =
+// false when the pipeline does not apply or declined the push (the caller unpacks the rows and
+// runs the general path, which then skips the pipeline as after any decline).
+khip_status part_push_rows(khip_agg* a, int64_t n, const RowsIn& ri, int key_col, int64_t* tot, bool* done) {
+  PartState& s = a->part;
+  *done = false;
+  while (s.log2P < SPLIT_P_LOG2 && a->occ - s.closed_n > s.P * (int64_t)s.H_eff / 2) KHIP_TRY(part_split(a));
+  s.last_c1 = false;
+  int vcol = -1;
+  if (s.c1_skip > 0 || !c1v_eligible(a, n, &vcol)) return KHIP_OK;
+  RowsIn r = ri;
+  r.vword = vcol == key_col ? 0 : 2 + vcol - (vcol > key_col ? 1 : 0);
+  r.vbit = vcol;
+  bool declined = false, retry_wide = false;
+  KHIP_TRY(c1_push(a, n, nullptr, nullptr, nullptr, nullptr, tot, &declined, nullptr, &retry_wide, nullptr, vcol, &r));
+  if (a->profile) (declined ? a->times.c1_declined : a->times.c1_pushes)++;
+  if (declined) s.c1_skip = 8;
+  *done = !declined;
+  return KHIP_OK;
+}
+
 khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
                       const uint8_t* rv, const ColPtrs& cols, int64_t* tot, const int64_t* st_at) {
   PartState& s = a->part;

@@ -177,7 +177,7 @@ bool c1_eligible(khip_agg* a, int64_t n);
 bool c1v_eligible(khip_agg* a, int64_t n, int* col);
 khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
                     const uint8_t* rv, int64_t* tot, bool* declined, const int64_t* st_at, bool* retry_wide,
-                    const ColPtrs* cols = nullptr, int vcol = -1);
+                    const ColPtrs* cols = nullptr, int vcol = -1, const RowsIn* rows = nullptr);
 __global__ void k_part_commit(const int64_t* __restrict__ gate, int P, const int64_t* __restrict__ pbase,
                               const uint32_t* __restrict__ prn, const uint32_t* __restrict__ plist, int nlist,
                               uint8_t* __restrict__ sel, int64_t* __restrict__ cnt,

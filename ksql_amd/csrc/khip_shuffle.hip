@@ -190,6 +190,15 @@ struct khip_comm {
   DevBuf cnt;
 };
 
+namespace khip {
+// The packed-row layout of a shuffle (khip_agg_push_shuffled reads received rows with it).
+void shuffle_layout(const khip_shuffle* s, int* key_col, int* n_cols, const int32_t** types) {
+  *key_col = s->desc.key_col;
+  *n_cols = s->desc.n_cols;
+  *types = s->types.data();
+}
+}  // namespace khip
+
 extern "C" {
 
 khip_status khip_shuffle_create(const khip_shuffle_desc* d, khip_shuffle** out) {

@@ -12,7 +12,9 @@ pieces of libksqldb_hip.so:
     khip_shuffle_unpack    back to a columnar device batch keyed by the new key
 
 The result feeds khip_agg_push exactly like a batch read back from the repartition topic:
-records from source rank 0 first, then rank 1, ..., each source's records in arrival order.
+records from source rank 0 first, then rank 1, ..., each source's records in arrival order — or
+goes straight into the aggregation with khip_agg_push_shuffled (Repartition.push_into: the rows
+are read where they lie, no columnar copy).
 
 The exchange is pluggable: `abi.Comm` (RCCL over xGMI, one process per GPU, the production
 path) or `GlooExchange` (any torch.distributed process group, rows staged through host memory:
@@ -63,8 +65,8 @@ class Repartition:
         self.last_counts = None
         self._send = None
 
-    def __call__(self, batch):
-        """Device batch (source partition) → (DeviceBatch of this task's rows, tensors)."""
+    def exchange(self, batch):
+        """Device batch (source partition) → (this task's received rows [n, row_words], n)."""
         import torch
         n = max(int(batch.struct.n_rows), 1)
         # a send buffer for every row the batch holds, kept across calls: one pack launch
@@ -78,7 +80,17 @@ class Repartition:
         else:
             recv, rcounts = self.comm.alltoall(send, counts, self.shuffle.row_words)
         self.last_counts = (counts, rcounts)
-        n = int(sum(rcounts))
+        return recv, int(sum(rcounts))
+
+    def push_into(self, agg, batch):
+        """The GROUP BY's aggregation reads this task's received rows where they lie
+        (khip_agg_push_shuffled); returns its batch statistics."""
+        recv, n = self.exchange(batch)
+        return agg.push_shuffled(self.shuffle, recv, n)
+
+    def __call__(self, batch):
+        """Device batch (source partition) → (DeviceBatch of this task's rows, tensors)."""
+        recv, n = self.exchange(batch)
         key, ts, cols, valid = self.shuffle.unpack(recv, n)
         out = abi.DeviceBatch(ts, keys=key, cols=cols, col_valid=valid)
         out._keep.append(recv)
