@@ -508,7 +508,7 @@ def bench_table_agg(args, lib, rank, world, local):
         return
     ms_step = elapsed * 1000.0 / args.steps
     bpr = 32 + 2 * 32 + 2 * 2 * 32  # row in (pk, region, ts, amount) + 32-B source-row RMW + undo and apply group RMWs
-    roof = roofline(bpr * n, ms_step, None, None, load_traffic(args.traffic_json, "table_agg", n), bpr,
+    roof = roofline(bpr * n, ms_step, None, None, load_traffic(args.traffic_json, "table_agg" + ("_sparse_ids" if args.sparse_ids else ""), n), bpr,
                     kernel="khip_agg_push_table (k_tagg_keys + radix sort + k_tagg_apply + finalize)")
     cpu = None
     if world == 1 and not args.no_cpu_baseline:

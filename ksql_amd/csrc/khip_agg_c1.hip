@@ -1380,10 +1380,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
       i = i < end ? i : end - 1;
       if constexpr (ROWS) {
         const uint64_t* r = ri.rows + i * (int64_t)ri.rw;
-        k[u] = (int64_t)r[0];
-        x[u] = (int64_t)r[1];
-        v[u] = (int64_t)r[ri.vword];
-        vm[u] = (uint32_t)r[ri.rw - 1];
+        if (ri.rw == 4 && ri.vword == 2) {  // [key, ts, argument, validity]: two 16-byte loads
+          const ulonglong2 a = ((const ulonglong2*)r)[0], b = ((const ulonglong2*)r)[1];
+          k[u] = (int64_t)a.x;
+          x[u] = (int64_t)a.y;
+          v[u] = (int64_t)b.x;
+          vm[u] = (uint32_t)b.y;
+        } else {
+          k[u] = (int64_t)r[0];
+          x[u] = (int64_t)r[1];
+          v[u] = (int64_t)r[ri.vword];
+          vm[u] = (uint32_t)r[ri.rw - 1];
+        }
       } else {
         x[u] = ts[i];
         k[u] = keys[i];
@@ -2572,7 +2580,18 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     vq0.having = a->having;
   }
   int64_t added_total = 0;
-  std::vector<int> sbits(s.psbits.begin(), s.psbits.end());
+  // sub-passes per partition: the pipeline's own LDS table (hmax), not the general merge's — a
+  // partition starts with enough of them for the hinted groups, and keeps those a push needed
+  {
+    const int64_t hm = val ? vq0.hmax : cq.hmax;
+    if ((int64_t)s.c1psbits.size() != P || s.c1ps_hmax != hm) {
+      int s0 = 0;
+      while (s0 < 12 && s.hint_groups / P > (hm * 7 / 10) << s0) s0++;
+      s.c1psbits.assign(P, (uint8_t)s0);
+      s.c1ps_hmax = hm;
+    }
+  }
+  std::vector<int> sbits(s.c1psbits.begin(), s.c1psbits.end());
   std::vector<uint32_t> plist, work;
   bool subs0 = false;
   for (int p = 0; p < P && !subs0; p++) subs0 = sbits[p] > 0;
@@ -2724,7 +2743,7 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     KHIP_TRY(s.work.ensure(both.size() * 4));
     KHIP_TRY_HIP(hipMemcpyAsync(s.work.p, both.data(), both.size() * 4, hipMemcpyHostToDevice, a->stream));
   }
-  for (int p = 0; p < P; p++) s.psbits[p] = (uint8_t)std::max<int>(s.psbits[p], sbits[p]);
+  for (int p = 0; p < P; p++) s.c1psbits[p] = (uint8_t)std::max<int>(s.c1psbits[p], sbits[p]);
   s.res_fresh = false;
   s.last_c1 = true;
   {

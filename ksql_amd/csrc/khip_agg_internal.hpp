@@ -357,6 +357,8 @@ struct PartState {
   int64_t c1_kbase = 0;             // key base for the next push's records (valid when c1_kb_valid)
   bool c1_kb_valid = false, c1_kretry = false;
   int64_t c1_wide_n = 0;            // pushes with wide records (compact ones are tried every 64th)
+  std::vector<uint8_t> c1psbits;    // the pipelines' sub-pass bits per partition (their own LDS tables)
+  int64_t c1ps_hmax = 0, hint_groups = 1024;
   bool last_c1 = false;
   int c1_skip = 0;  // pushes left before the pipeline is tried again after a declined push
   DevBuf c1vq;  // the value pipeline's merge parameters (device copy)

@@ -3528,6 +3528,7 @@ khip_status part_init(khip_agg* a, int64_t hint) {
   }
   // partitions: at most ~H_eff/2 groups each at the hinted size
   const int64_t groups = std::max<int64_t>(hint, 1024);
+  s.hint_groups = groups;
   // at least 64 partitions: the packed identity then holds window ranges of up to 63
   s.log2P = std::min(SPLIT_P_LOG2, std::max(6, part_ceil_log2(groups * 2 / s.H_eff)));
   // hinted groups would need sub-passes at 2^14 partitions (each re-reads the partition's

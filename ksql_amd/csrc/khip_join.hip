@@ -363,9 +363,8 @@ __global__ __launch_bounds__(256) void k_probe(const uint64_t* __restrict__ tabl
   const int lane = threadIdx.x & 63;
   int64_t key[PR];
   bool act[PR];
-  uint64_t slot[PR];
-  longlong2 h0[PR], g0[PR];  // (key, meta) of the home pair's two slots
-  uint64_t c0a[PR], c0b[PR];  // their first payload words
+  longlong2 h0[PR], g0[PR];          // (key, meta) of the home pair's two slots
+  uint64_t c0a[CMP ? 1 : PR], c0b[CMP ? 1 : PR];  // their first payload words (CMP: in the meta words)
 #pragma unroll
   for (int r = 0; r < PR; r++) {
     const int64_t i = base + r * 256 + threadIdx.x;
@@ -374,15 +373,11 @@ __global__ __launch_bounds__(256) void k_probe(const uint64_t* __restrict__ tabl
     act[r] = i < n && ts[ic] >= 0 && bit_get(kv, ic) && bit_get(rv, ic);
   }
 #pragma unroll
-  for (int r = 0; r < PR; r++) {
-    slot[r] = home_slot(key[r], mask);
-    const uint64_t* sp = table + slot[r] * (uint64_t)sw;
+  for (int r = 0; r < PR; r++) {  // the home slot is recomputed at use: fewer live registers, more waves
+    const uint64_t* sp = table + home_slot(key[r], mask) * (uint64_t)sw;
     h0[r] = *(const longlong2*)sp;
     g0[r] = *(const longlong2*)(sp + sw);
-    if constexpr (CMP) {  // the value is in the meta word: the pair is one 32-byte read
-      c0a[r] = (uint64_t)h0[r].y;
-      c0b[r] = (uint64_t)g0[r].y;
-    } else {
+    if constexpr (!CMP) {  // CMP: the value is in the meta word, the pair is one 32-byte read
       c0a[r] = sp[3];
       c0b[r] = sp[sw + 3];
     }
@@ -397,7 +392,8 @@ __global__ __launch_bounds__(256) void k_probe(const uint64_t* __restrict__ tabl
     if (act[r]) {
       uint64_t m = (uint64_t)h0[r].y;
       int64_t k0 = h0[r].x;
-      uint64_t c0 = c0a[r], c1 = c0b[r], sl = slot[r];
+      uint64_t c0 = CMP ? (uint64_t)h0[r].y : c0a[CMP ? 0 : r], c1 = CMP ? (uint64_t)g0[r].y : c0b[CMP ? 0 : r];
+      uint64_t sl = home_slot(key[r], mask);
       // c0 / c1 opaque (registers, not "loads of c0a / c0b"): otherwise the compiler sinks the
       // loads to the hit through a pointer phi (a home-pair word in a private array | a probed
       // slot), which keeps the array in scratch — each word stored right after its load, a wait
@@ -901,8 +897,8 @@ static khip_status probe_launch(khip_table* t, const khip_batch* b, int32_t join
     KHIP_TRY_HIP(hipGetLastError());
     return KHIP_OK;
   }
-  const int pr_env = (int)knob("KHIP_PROBE_PR", 8);  // measured with 16-byte slots: 8 > 4, 16 (profiles/r04/)
-  const int PR = pr_env >= 16 ? 16 : (pr_env >= 8 ? 8 : (pr_env >= 4 ? 4 : 1));
+  const int pr_env = (int)knob("KHIP_PROBE_PR", 8);  // measured with 16-byte slots: 8 > 6 > 4, 12, 16 (profiles/r04/)
+  const int PR = pr_env >= 16 ? 16 : (pr_env >= 8 ? 8 : (pr_env >= 4 ? 4 : 1));  // 6 and 12 measured slower
   auto kern = t->compact ? (PR == 16 ? k_probe<16, true> : (PR == 8 ? k_probe<8, true> : (PR == 4 ? k_probe<4, true> : k_probe<1, true>)))
                          : (PR == 16 ? k_probe<16, false> : (PR == 8 ? k_probe<8, false> : (PR == 4 ? k_probe<4, false> : k_probe<1, false>)));
   hipLaunchKernelGGL(kern, dim3(ceil_div(n, 256 * PR)), dim3(256), 0, t->stream, t->table.as<uint64_t>(),

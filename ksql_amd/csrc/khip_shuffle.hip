@@ -10,6 +10,7 @@
 //                    (wave ballots per destination + cross-wave LDS prefix keep arrival order)
 //   khip_comm_alltoall  grouped ncclSend/ncclRecv, one pair per peer over xGMI (every MI355X
 //                    pair has a direct link, so this is per-link bound, not a ring)
+//   k_shuf_pack1     one destination: the same rows in one pass (decoupled look-back, no histogram)
 //   k_shuf_unpack    packed rows → columnar batch (bitmaps built with __ballot)
 #include <rccl/rccl.h>
 
@@ -144,6 +145,102 @@ __global__ __launch_bounds__(SH_THREADS) void k_shuf_pack(ShCols c, int n_cols, 
   }
 }
 
+// One destination (a single task: the repartition keeps every row here): the pack is a stable
+// compaction, and needs no histogram pass.  Tiles are taken in ticket order; a tile counts its
+// valid rows (ballots per wave and round), publishes the count and looks back over the earlier
+// tiles' published counts / inclusive prefixes for its first output row (decoupled look-back, as
+// khip_sort.hpp's k_rs_pass), then writes its rows in arrival order.  A tile waits only on
+// tiles with earlier tickets, which are already running.  status[nT] and *ticket start at 0; the
+// last tile leaves the total in *total.
+constexpr uint64_t SH_AGG = 1ULL << 62, SH_INC = 2ULL << 62, SH_VAL = (1ULL << 62) - 1;
+
+template <int NC>  // the column count: the row is built in registers and leaves as 16-byte pairs
+__global__ __launch_bounds__(SH_THREADS) void k_shuf_pack1(ShCols c, int n_cols, int key_col,
+                                                           const uint8_t* __restrict__ rv, const int64_t* __restrict__ ts,
+                                                           int64_t n, int64_t nT, uint64_t* __restrict__ status,
+                                                           unsigned int* __restrict__ ticket, uint64_t* __restrict__ out,
+                                                           int row_words, unsigned long long* __restrict__ total) {
+  constexpr int W = SH_THREADS / 64;
+  __shared__ uint32_t wcnt[SH_ITEMS][W];
+  __shared__ int64_t lbase;
+  __shared__ uint32_t ltile;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t lt = lane ? (~0ULL >> (64 - lane)) : 0ULL;
+  if (threadIdx.x == 0) ltile = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const int64_t tile = ltile;
+  const int64_t base = tile * SH_TILE;
+  uint32_t vmask = 0;  // bit r: this thread's row of round r is kept (ts and the rows re-read below: L2)
+#pragma unroll
+  for (int r = 0; r < SH_ITEMS; r++) {
+    const int64_t i = base + (int64_t)r * SH_THREADS + threadIdx.x;
+    const bool v = i < n && ts[i] >= 0 && bit_get(rv, i) && bit_get(c.valid[key_col], i);
+    const uint64_t m = __ballot(v);
+    if (lane == 0) wcnt[r][wave] = (uint32_t)__popcll(m);
+    vmask |= (v ? 1u : 0u) << r;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // exclusive prefix in (round, wave) order = arrival order
+    uint32_t acc = 0;
+    for (int r = 0; r < SH_ITEMS; r++)
+      for (int w = 0; w < W; w++) {
+        const uint32_t e = wcnt[r][w];
+        wcnt[r][w] = acc;
+        acc += e;
+      }
+    __hip_atomic_store(status + tile, (tile == 0 ? SH_INC : SH_AGG) | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t excl = 0;
+    for (int64_t j = tile - 1; j >= 0;) {
+      const uint64_t st = __hip_atomic_load(status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!(st & ~SH_VAL)) {
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      excl += st & SH_VAL;
+      if (st & SH_INC) break;
+      j--;
+    }
+    if (tile > 0)
+      __hip_atomic_store(status + tile, SH_INC | (excl + acc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    lbase = (int64_t)excl;
+    if (tile == nT - 1) *total = excl + acc;
+  }
+  __syncthreads();
+  for (int r = 0; r < SH_ITEMS; r++) {
+    const bool v = (vmask >> r) & 1u;
+    const uint32_t rank = (uint32_t)__popcll(__ballot(v) & lt);
+    if (!v) continue;
+    const int64_t i = base + (int64_t)r * SH_THREADS + threadIdx.x;
+    constexpr int RW = 2 + NC + (NC & 1);  // words, padded to an even count (the row has 2 + NC)
+    uint64_t wd[RW];
+#pragma unroll
+    for (int k = 0; k < RW; k++) wd[k] = 0;
+    wd[0] = (uint64_t)sh_raw(c, key_col, i);
+    wd[1] = (uint64_t)ts[i];
+    uint64_t vm = 1ULL << key_col;  // the key column travels as word 0 only (its validity is implied)
+    int w = 2;
+#pragma unroll
+    for (int cc = 0; cc < NC; cc++) {
+      if (cc == key_col) continue;
+      const bool cv = bit_get(c.valid[cc], i);
+      const uint64_t x = cv ? (uint64_t)sh_raw(c, cc, i) : 0ULL;
+#pragma unroll
+      for (int k = 2; k < 2 + NC - 1; k++) wd[k] = k == w ? x : wd[k];  // no dynamic register index
+      w++;
+      vm |= (cv ? 1ULL : 0ULL) << cc;
+    }
+    wd[1 + NC] = vm;
+    uint64_t* o = out + (uint64_t)(lbase + wcnt[r][wave] + rank) * row_words;
+    if ((2 + NC) % 2 == 0) {
+#pragma unroll
+      for (int k = 0; k < RW / 2; k++) ((ulonglong2*)o)[k] = make_ulonglong2(wd[2 * k], wd[2 * k + 1]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 2 + NC; k++) o[k] = wd[k];
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_shuf_unpack(const uint64_t* __restrict__ rows, int64_t n, int n_cols,
                                                      int key_col, int row_words, ShCols types, int64_t* __restrict__ key,
                                                      int64_t* __restrict__ ts, void* const* __restrict__ col_data,
@@ -246,6 +343,25 @@ khip_status khip_shuffle_pack(khip_shuffle* s, const khip_batch* b, uint64_t* se
   }
   c.key_bytes = s->types[s->desc.key_col] == KHIP_TYPE_INT32 ? 4 : 8;
   const int64_t nT = ceil_div(n, SH_TILE);
+  if (N == 1 && send && capacity >= n) {  // one destination: a one-pass stable compaction
+    KHIP_TRY(s->R.ensure((size_t)(nT + 2) * 8));
+    uint64_t* status = s->R.as<uint64_t>();
+    unsigned int* ticket = (unsigned int*)(status + nT);
+    unsigned long long* total = (unsigned long long*)(status + nT + 1);
+    KHIP_TRY_HIP(hipMemsetAsync(status, 0, (size_t)(nT + 2) * 8, s->stream));
+    using PackFn = void (*)(ShCols, int, int, const uint8_t*, const int64_t*, int64_t, int64_t, uint64_t*, unsigned int*,
+                            uint64_t*, int, unsigned long long*);
+    static const PackFn k1[SH_MAX_COLS] = {k_shuf_pack1<1>, k_shuf_pack1<2>, k_shuf_pack1<3>, k_shuf_pack1<4>,
+                                           k_shuf_pack1<5>, k_shuf_pack1<6>, k_shuf_pack1<7>, k_shuf_pack1<8>};
+    hipLaunchKernelGGL(k1[s->desc.n_cols - 1], dim3(nT), dim3(SH_THREADS), 0, s->stream, c, s->desc.n_cols,
+                       s->desc.key_col, b->row_valid, b->ts, n, nT, status, ticket, send, 2 + s->desc.n_cols, total);
+    KHIP_TRY_HIP(hipGetLastError());
+    unsigned long long tot = 0;
+    KHIP_TRY_HIP(hipMemcpyAsync(&tot, total, 8, hipMemcpyDeviceToHost, s->stream));
+    KHIP_TRY_HIP(hipStreamSynchronize(s->stream));
+    counts[0] = (int64_t)tot;
+    return KHIP_OK;
+  }
   const int TC = (int)std::min<int64_t>(nT, 64);
   KHIP_TRY(s->hist.ensure((size_t)nT * N * 4));
   KHIP_TRY(s->csum.ensure((size_t)TC * N * 8));

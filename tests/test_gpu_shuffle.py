@@ -76,6 +76,22 @@ def test_pack_matches_oracle_partitioner(prod, orc, key_type, n_parts):
     sh.close()
 
 
+@pytest.mark.parametrize("key_type", ["INT64", "INT32"])
+@pytest.mark.parametrize("n", [1, 4095, 4097, 70_001, 1_000_003])
+def test_pack_one_destination_one_pass(prod, orc, key_type, n):
+    """One destination with a send buffer for every row: k_shuf_pack1 (decoupled look-back, no
+    histogram pass) — the same rows, in the same order, as the oracle."""
+    import torch
+    cols, types, cv, rv, ts = _random_source(n, key_type, seed=n)
+    sh = abi.ShuffleHandle(prod, 1, 0, types)
+    send = torch.empty((n, sh.row_words), dtype=torch.int64, device="cuda")
+    out, counts = sh.pack(_device_batch(cols, cv, rv, ts), send=send)
+    exp_rows, exp_counts = expected_pack(orc, 0, cols, cv, rv, ts, 1)
+    assert counts == exp_counts
+    np.testing.assert_array_equal(out[: counts[0]].cpu().numpy(), exp_rows)
+    sh.close()
+
+
 @pytest.mark.parametrize("key_col", [0, 1])
 def test_unpack_round_trip(prod, orc, key_col):
     n = 50_000
