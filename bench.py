@@ -700,8 +700,8 @@ def bench_possible_fraud(args, lib, rank, world, local):
     traffic = load_traffic(args.traffic_json, "possible_fraud" + ("_atomic" if args.engine == "atomic" else ""), n,
                            variant)
     roof = roofline(bpr * n, ms_step, push_ms, per_kernel, traffic, bpr,
-                    kernel=("khip_agg_push (COUNT(*) pipeline: k_c1_hist + offsets + k_c1_scatter + k_c1_check + "
-                            "k_c1_refine + k_c1_merge + commit) + HAVING count") if c1 else
+                    kernel=("khip_agg_push (COUNT(*) pipeline: k_c1_scatter (step runs) + run scan + k_c1_check + "
+                            "k_c1_chunks + k_c1_refine + k_c1_merge + commit) + HAVING count") if c1 else
                            "khip_agg_push (k_part_hist + scans + k_part_scatter + k_part_refine + k_part_merge + "
                            "commit) + HAVING count")
     cpu = None

@@ -2547,6 +2547,8 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
   C1VQ vq0{};
   int v_log2H = 12;
   int v_pm = 0;  // the plane mask when a specialised merge exists for it
+  const int v_nt = knob("KHIP_C1V_NT", 512) == 256 ? 256 : 512;  // merge workgroup size
+  const int v_wpc = (int)knob("KHIP_C1V_WG_PER_CU", 2);            // merge workgroups per CU
   if (val) {
     while (v_log2H > 9 && c1v_layout(a, v_log2H, 8, log2B, &vq0) > 78 * 1024) v_log2H--;
     v_log2H = (int)knob("KHIP_C1V_LOG2H", v_log2H);
@@ -2625,18 +2627,21 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
       vq.chg = a->changelog ? a->chg.as<uint8_t>() : nullptr;
       // the benchmarks' plane shapes have instantiations of their own (PM_C5, PM_C3), every other
       // one reads the planes from the parameters; AU 2 at <= 128 VGPRs (two workgroups per CU)
+      auto pick_nt = [&](auto pmc, auto ntc) {
+        constexpr int PMv = decltype(pmc)::value, NTv = decltype(ntc)::value;
+        return panes ? (idw == 0 ? k_c1v_merge<NTv, 2, uint32_t, true, 4, PMv> : k_c1v_merge<NTv, 2, uint64_t, true, 4, PMv>)
+                     : (idw == 0 ? k_c1v_merge<NTv, 2, uint32_t, false, 4, PMv> : k_c1v_merge<NTv, 2, uint64_t, false, 4, PMv>);
+      };
       auto pick = [&](auto pmc) {
-        constexpr int PMv = decltype(pmc)::value;
-        return panes ? (idw == 0 ? k_c1v_merge<512, 2, uint32_t, true, 4, PMv> : k_c1v_merge<512, 2, uint64_t, true, 4, PMv>)
-                     : (idw == 0 ? k_c1v_merge<512, 2, uint32_t, false, 4, PMv> : k_c1v_merge<512, 2, uint64_t, false, 4, PMv>);
+        return v_nt == 256 ? pick_nt(pmc, std::integral_constant<int, 256>{}) : pick_nt(pmc, std::integral_constant<int, 512>{});
       };
       auto mk = v_pm == PM_C5 ? pick(std::integral_constant<int, PM_C5>{})
                               : (v_pm == PM_C3 ? pick(std::integral_constant<int, PM_C3>{}) : pick(std::integral_constant<int, 0>{}));
       hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       KHIP_TRY(s.c1vq.ensure(sizeof(C1VQ)));
       KHIP_TRY_HIP(hipMemcpyAsync(s.c1vq.p, &vq, sizeof(C1VQ), hipMemcpyHostToDevice, a->stream));
-      const int64_t vgrid = std::min<int64_t>(nwork, (int64_t)s.n_cu * 2);
-      hipLaunchKernelGGL(mk, dim3(vgrid), dim3(512), lds, a->stream, s.c1vq.as<C1VQ>(), wk, nwork, s.c1bb.as<int64_t>(), cstart, seg,
+      const int64_t vgrid = std::min<int64_t>(nwork, (int64_t)s.n_cu * v_wpc);
+      hipLaunchKernelGGL(mk, dim3(vgrid), dim3(v_nt), lds, a->stream, s.c1vq.as<C1VQ>(), wk, nwork, s.c1bb.as<int64_t>(), cstart, seg,
                          (const ulonglong2*)s.srec.p, pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
                          s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
                          s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
