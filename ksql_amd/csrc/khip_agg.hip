@@ -410,7 +410,13 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ ta
 
 // ---------------------------------------------------------------- UTF8 dictionary
 // dict word: 0 empty | fresh: bit63 | fp22 << 40 | batch row (40 bits) | resident: bit62 | fp22 << 40
+// | o / 8 (40 bits: the entry's arena offset, so a hit reads the word and the entry only)
 // arena entry at offset o (8-aligned): [u64 hash][i64 len][bytes, padded to 8]; key id = o.
+// A lookup gives up after DICT_PROBE slots (the table is then too full: dict_map unclaims the
+// batch's fresh words, grows the table and maps the batch again).
+constexpr int DICT_PROBE = 256;
+constexpr uint64_t DICT_LOW = (1ULL << 40) - 1;
+constexpr int DICT_NCNT = 64;
 
 __global__ __launch_bounds__(256) void k_dict_lookup(uint64_t* __restrict__ dword, const int64_t* __restrict__ dkid,
                                                      uint64_t dmask, const uint8_t* __restrict__ arena,
@@ -428,13 +434,16 @@ __global__ __launch_bounds__(256) void k_dict_lookup(uint64_t* __restrict__ dwor
     }
     const int64_t o0 = koff[i], len = koff[i + 1] - o0;
     const uint8_t* kb = kbytes + o0;
-    const uint64_t h = hash_bytes_dev(kb, len);
+    const bool sk = len <= 8 * KW_MAX;  // a short key: words, not bytes
+    uint64_t kw[KW_MAX];
+    if (sk) key_words(kb, len, kw);
+    const uint64_t h = sk ? hash_key_words(kw, len) : hash_bytes_dev(kb, len);
     khash[i] = (int64_t)h;
     const uint64_t fp = (h >> 40) & 0x3FFFFFULL;
     const uint64_t fresh = (1ULL << 63) | (fp << 40) | (uint64_t)i;
     uint64_t slot = h & dmask;
     bool done = false;
-    for (int probe = 0; probe < MAX_PROBE && !done; probe++) {
+    for (int probe = 0; probe < DICT_PROBE && !done; probe++) {
       uint64_t w = ld_relaxed(&dword[slot]);
       if (w == 0) {
         const uint64_t old = atomicCAS((unsigned long long*)&dword[slot], 0ULL, (unsigned long long)fresh);
@@ -449,15 +458,24 @@ __global__ __launch_bounds__(256) void k_dict_lookup(uint64_t* __restrict__ dwor
         if (w >> 63) {  // fresh claim by another row of this batch
           const int64_t r2 = (int64_t)(w & ((1ULL << 40) - 1));
           const int64_t p2 = koff[r2], l2 = koff[r2 + 1] - p2;
-          if (l2 == len && bytes_eq(kbytes + p2, kb, len)) {
+          bool eq = l2 == len;
+          if (eq && sk) {
+            uint64_t ow[KW_MAX];
+            key_words(kbytes + p2, l2, ow);
+#pragma unroll
+            for (int k = 0; k < KW_MAX; k++) eq = eq && ow[k] == kw[k];
+          } else if (eq) {
+            eq = bytes_eq(kbytes + p2, kb, len);
+          }
+          if (eq) {
             kid[i] = -(int64_t)(slot + 1);
             done = true;
           }
         } else {  // resident
-          const int64_t o = dkid[slot];
+          const int64_t o = (int64_t)((w & DICT_LOW) << 3);
           const uint64_t eh = *(const uint64_t*)(arena + o);
           const int64_t el = *(const int64_t*)(arena + o + 8);
-          if (eh == h && el == len && bytes_eq(arena + o + 16, kb, len)) {
+          if (eh == h && el == len && (sk ? key_words_eq_aligned(kw, arena + o + 16, len) : bytes_eq(arena + o + 16, kb, len))) {
             kid[i] = o;
             done = true;
           }
@@ -481,7 +499,10 @@ __global__ __launch_bounds__(256) void k_dict_find(const uint64_t* __restrict__ 
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t o0 = koff[i], len = koff[i + 1] - o0;
     const uint8_t* kb = kbytes + o0;
-    const uint64_t h = hash_bytes_dev(kb, len);
+    const bool sk = len <= 8 * KW_MAX;
+    uint64_t kw[KW_MAX];
+    if (sk) key_words(kb, len, kw);
+    const uint64_t h = sk ? hash_key_words(kw, len) : hash_bytes_dev(kb, len);
     const uint64_t fp = (h >> 40) & 0x3FFFFFULL;
     uint64_t slot = h & dmask;
     int64_t found = -1;
@@ -489,9 +510,9 @@ __global__ __launch_bounds__(256) void k_dict_find(const uint64_t* __restrict__ 
       const uint64_t w = dword[slot];
       if (w == 0) break;
       if (((w >> 40) & 0x3FFFFFULL) == fp) {
-        const int64_t o = dkid[slot];
+        const int64_t o = (int64_t)((w & DICT_LOW) << 3);
         if (*(const uint64_t*)(arena + o) == h && *(const int64_t*)(arena + o + 8) == len &&
-            bytes_eq(arena + o + 16, kb, len)) {
+            (sk ? key_words_eq_aligned(kw, arena + o + 16, len) : bytes_eq(arena + o + 16, kb, len))) {
           found = o;
           break;
         }
@@ -504,25 +525,40 @@ __global__ __launch_bounds__(256) void k_dict_find(const uint64_t* __restrict__ 
 
 __device__ __forceinline__ int64_t entry_bytes(int64_t len) { return 16 + ((len + 7) & ~7LL); }
 
-// Per block of 256 dict slots: arena bytes needed by fresh entries.
+// Per block of 256 dict slots: arena bytes needed by fresh entries; the fresh entries are added to
+// one of DICT_NCNT counters (the host sums them).
 __global__ __launch_bounds__(256) void k_dict_count(const uint64_t* __restrict__ dword, int64_t dcap,
-                                                    const int64_t* __restrict__ koff, int64_t* __restrict__ bsum) {
-  __shared__ unsigned long long acc;
-  if (threadIdx.x == 0) acc = 0;
+                                                    const int64_t* __restrict__ koff, int64_t* __restrict__ bsum,
+                                                    unsigned long long* __restrict__ nent) {
+  __shared__ unsigned long long acc, cnt;
+  if (threadIdx.x == 0) acc = cnt = 0;
   __syncthreads();
   const int64_t slot = (int64_t)blockIdx.x * 256 + threadIdx.x;
   int64_t b = 0;
   if (slot < dcap) {
     const uint64_t w = dword[slot];
     if (w >> 63) {
-      const int64_t r = (int64_t)(w & ((1ULL << 40) - 1));
+      const int64_t r = (int64_t)(w & DICT_LOW);
       b = entry_bytes(koff[r + 1] - koff[r]);
     }
   }
+  const int c = (int)__popcll(__ballot(b != 0));
   b = wave_sum(b);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&acc, (unsigned long long)b);
+  if ((threadIdx.x & 63) == 0 && b) {
+    atomicAdd(&acc, (unsigned long long)b);
+    atomicAdd(&cnt, (unsigned long long)c);
+  }
   __syncthreads();
-  if (threadIdx.x == 0) bsum[blockIdx.x] = (int64_t)acc;
+  if (threadIdx.x == 0) {
+    bsum[blockIdx.x] = (int64_t)acc;
+    if (cnt) atomicAdd(&nent[blockIdx.x & (DICT_NCNT - 1)], cnt);  // spread: no one hot word
+  }
+}
+
+// A failed map: the batch's fresh claims → empty (the table is as before the batch).
+__global__ __launch_bounds__(256) void k_dict_unclaim(uint64_t* __restrict__ dword, int64_t dcap) {
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < dcap; s += (int64_t)gridDim.x * blockDim.x)
+    if (dword[s] >> 63) dword[s] = 0;
 }
 
 // Exclusive prefix sum of v[0..n) in place (single block); total added to *total.  Each thread
@@ -595,7 +631,7 @@ __global__ __launch_bounds__(256) void k_dict_write(uint64_t* __restrict__ dword
     *(int64_t*)(arena + o + 8) = len;
     for (int64_t k = 0; k < len; k++) arena[o + 16 + k] = kbytes[koff[r] + k];
     dkid[slot] = o;
-    dword[slot] = (1ULL << 62) | (((w >> 40) & 0x3FFFFFULL) << 40);
+    dword[slot] = (1ULL << 62) | (((w >> 40) & 0x3FFFFFULL) << 40) | ((uint64_t)o >> 3);
   }
 }
 
@@ -652,13 +688,18 @@ static khip_status dict_grow(KeyDict& d, hipStream_t s, int64_t new_cap) {
 }
 
 khip_status dict_init(KeyDict& d, hipStream_t s) {
-  KHIP_TRY(d.fail.ensure(8));
+  KHIP_TRY(d.fail.ensure(8 + 8 * DICT_NCNT));
   return dict_grow(d, s, 4096);
 }
 
 khip_status dict_map(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8_t* kbytes, int64_t key_bytes_total,
                      const uint8_t* kv, const uint8_t* rv, const int64_t* ts, int64_t n, int64_t* kid, int64_t* khash) {
-  if (2 * (d.docc + n) > d.dcap) KHIP_TRY(dict_grow(d, s, next_pow2(4 * (d.docc + n))));
+  // room for the keys this batch may add: every row on the first map, then twice the last map's
+  // new keys (at least n / 16) — a batch that brings more fails its probes and is mapped again
+  // into a larger table, so the table tracks the key count, not the batch size (a table sized
+  // for every row of a 100M-record batch is 4 GB of probe words and scans)
+  const int64_t est = d.last_added < 0 ? n : std::min<int64_t>(n, std::max<int64_t>({2 * d.last_added, n / 16, 4096}));
+  if (2 * (d.docc + est) > d.dcap) KHIP_TRY(dict_grow(d, s, next_pow2(4 * (d.docc + est))));
   const int64_t need = d.arena_used + key_bytes_total + 16 * n + 16;
   if ((size_t)need > d.arena.bytes) {
     DevBuf na;
@@ -669,14 +710,25 @@ khip_status dict_map(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8
     d.arena = na;
     na.p = nullptr;
   }
-  KHIP_TRY_HIP(hipMemsetAsync(d.fail.p, 0, 4, s));
-  hipLaunchKernelGGL(k_dict_lookup, dim3(grid_for(n, 256)), dim3(256), 0, s, d.dword.as<uint64_t>(),
-                     d.dkid.as<int64_t>(), (uint64_t)(d.dcap - 1), d.arena.as<uint8_t>(), koff, kbytes, kv, rv, ts, n,
-                     kid, khash, d.fail.as<int>());
+  unsigned long long* nent = (unsigned long long*)(d.fail.as<char>() + 8);
+  for (int attempt = 0;; attempt++) {
+    KHIP_TRY_HIP(hipMemsetAsync(d.fail.p, 0, 8 + 8 * DICT_NCNT, s));
+    hipLaunchKernelGGL(k_dict_lookup, dim3(grid_for(n, 256)), dim3(256), 0, s, d.dword.as<uint64_t>(),
+                       d.dkid.as<int64_t>(), (uint64_t)(d.dcap - 1), d.arena.as<uint8_t>(), koff, kbytes, kv, rv, ts,
+                       n, kid, khash, d.fail.as<int>());
+    KHIP_TRY_HIP(hipGetLastError());
+    int failed = 0;
+    KHIP_TRY_HIP(hipMemcpyAsync(&failed, d.fail.p, 4, hipMemcpyDeviceToHost, s));
+    KHIP_TRY_HIP(hipStreamSynchronize(s));
+    if (!failed) break;
+    if (attempt >= 6 || d.dcap >= ((int64_t)1 << 34)) return fail(KHIP_E_DEVICE, "key dictionary probe budget exhausted");
+    hipLaunchKernelGGL(k_dict_unclaim, dim3(grid_for(d.dcap, 256)), dim3(256), 0, s, d.dword.as<uint64_t>(), d.dcap);
+    KHIP_TRY(dict_grow(d, s, d.dcap * 4));
+  }
   const int64_t dnb = ceil_div(d.dcap, 256);
   KHIP_TRY(d.bsum.ensure((dnb + 1) * 8));
   hipLaunchKernelGGL(k_dict_count, dim3(dnb), dim3(256), 0, s, d.dword.as<uint64_t>(), d.dcap, koff,
-                     d.bsum.as<int64_t>());
+                     d.bsum.as<int64_t>(), nent);
   int64_t* dtotal = d.bsum.as<int64_t>() + dnb;
   KHIP_TRY_HIP(hipMemsetAsync(dtotal, 0, 8, s));
   hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, d.bsum.as<int64_t>(), dnb, dtotal);
@@ -685,14 +737,14 @@ khip_status dict_map(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8
   hipLaunchKernelGGL(k_kid_fixup, dim3(grid_for(n, 256)), dim3(256), 0, s, kid, n, d.dkid.as<int64_t>());
   KHIP_TRY_HIP(hipGetLastError());
   int64_t added = 0;
-  int failed = 0;
+  unsigned long long cnts[DICT_NCNT], keys = 0;
   KHIP_TRY_HIP(hipMemcpyAsync(&added, dtotal, 8, hipMemcpyDeviceToHost, s));
-  KHIP_TRY_HIP(hipMemcpyAsync(&failed, d.fail.p, 4, hipMemcpyDeviceToHost, s));
+  KHIP_TRY_HIP(hipMemcpyAsync(cnts, nent, sizeof(cnts), hipMemcpyDeviceToHost, s));
   KHIP_TRY_HIP(hipStreamSynchronize(s));
-  if (failed) return fail(KHIP_E_DEVICE, "key dictionary probe budget exhausted");
+  for (int k = 0; k < DICT_NCNT; k++) keys += cnts[k];
   d.arena_used += added;
-  // occupancy over-estimated (every entry takes >= 16 arena bytes): growth is decided conservatively
-  d.docc = std::min<int64_t>(d.dcap, d.docc + std::min<int64_t>(n, added / 16));
+  d.docc += (int64_t)keys;
+  d.last_added = (int64_t)keys;
   return KHIP_OK;
 }
 
@@ -705,8 +757,14 @@ khip_status dict_find(KeyDict& d, hipStream_t s, const int64_t* koff, const uint
 }
 
 khip_status dict_clear(KeyDict& d, hipStream_t s) {
-  if (d.dcap) KHIP_TRY_HIP(hipMemsetAsync(d.dword.p, 0, d.dcap * 8, s));
+  // the next batches likely bring as many keys as the dictionary held: a table far larger than
+  // that (sized by a first map's every-row estimate) is given back
+  const int64_t held = d.docc;
+  const int64_t keep = std::max<int64_t>(4096, next_pow2(4 * std::max<int64_t>(held, 1)));
   d.docc = 0;
+  if (d.dcap >= 4 * keep) KHIP_TRY(dict_grow(d, s, keep));
+  if (d.dcap) KHIP_TRY_HIP(hipMemsetAsync(d.dword.p, 0, d.dcap * 8, s));
+  if (held > 0) d.last_added = held;  // the next map re-inserts about as many
   d.arena_used = 0;
   return KHIP_OK;
 }

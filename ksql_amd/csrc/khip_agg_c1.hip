@@ -1007,7 +1007,7 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     }
     const uint64_t* src = (isel ? buf1 : buf0) + (uint64_t)p * q.cmax * q.sw;
     // 0b. closed resident rows → closed store (pass 0 only; retries skip them)
-    if (evict && first) {
+    if (evict && first && nrow > 0) {  // (no resident rows: nothing to evict, no barriers)
       int ne = 0, nh = 0;
       for (int64_t r = threadIdx.x; r < nrow; r += NT) {
         const uint64_t* row = src + r * q.sw;
@@ -1174,7 +1174,7 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       }
       n_mine++;
     }
-    lds_barrier();
+    if (nrow > 0) lds_barrier();  // the marks before the list walk reads them (uniform: nrow is the item's)
     // the wave's share of the list: new (unmatched) entries
     const int per = ((nl + NW - 1) / NW + 63) & ~63;
     const int lb0 = wave * per, lb1 = lb0 + per < nl ? lb0 + per : nl;
@@ -1256,7 +1256,7 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       }
       cur += __popcll(bl);
     }
-    lds_barrier();  // every wave's resident rows have read their entries: the list walk clears them
+    if (nrow > 0) lds_barrier();  // every wave's resident rows have read their entries: the list walk clears them
     const uint32_t wmask = wbits ? (1u << wbits) - 1u : 0u;
     for (int k = lb0; k < lb1; k += 64) {
       const int i = k + lane;
@@ -1778,9 +1778,9 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
   KLDS uint16_t* list = c1v_plane<uint16_t>(smem, q.off_list);
   KLDS uint32_t* spre = c1v_plane<uint32_t>(smem, q.off_spre);
   KLDS int32_t* sbs = (KLDS int32_t*)(spre + (C1_SEGMAX + 4));
-  KLDS int64_t* lbb = (KLDS int64_t*)(sbs + C1_SEGMAX);
-  KLDS int32_t* lcs = (KLDS int32_t*)(lbb + (1 << (q.log2P - q.fbits)) + 1);
-  KLDS uint16_t* segof = (KLDS uint16_t*)(lcs + (1 << (q.log2P - q.fbits)) + 2);
+  // the bucket tables (chunk starts, bucket bases) are read from memory per item (their 3 KB of
+  // LDS let a 2^12-entry table of 32-bit identities fit two workgroups per CU)
+  KLDS uint16_t* segof = (KLDS uint16_t*)(sbs + C1_SEGMAX);
   __shared__ int lovf, nnew;
   __shared__ int wsum[NW];
   __shared__ unsigned long long lbase;
@@ -1871,8 +1871,8 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
     }
     p = __builtin_amdgcn_readfirstlane(p);
     const int b = (int)(p >> q.fbits), f = (int)(p & (uint32_t)(F - 1));
-    const int cs = lcs[b];
-    int nseg = lcs[b + 1] - cs;
+    const int cs = cstart[b];
+    int nseg = cstart[b + 1] - cs;
     if (nseg < 0 || nseg > C1_SEGMAX) nseg = 0;
     r.p = p;
     r.sbits = sbits;
@@ -1880,7 +1880,7 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
     r.nseg = nseg;
     r.nrow = cnt[p];
     r.selw = ((const uint32_t*)sel)[p >> 2];
-    r.bb0 = lbb[b];
+    r.bb0 = bb[b];
     const int k0 = threadIdx.x * 2;
     r.s00 = r.s01 = r.s10 = r.s11 = 0;
     if (k0 < nseg) {
@@ -1961,11 +1961,7 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
     if (x.rn > 0) load(ra, 0, x.rn, x.nseg);
     if (x.rn > (int64_t)AU * NT) load(rb, (int64_t)AU * NT, x.rn, x.nseg);
   };
-  for (int k = threadIdx.x; k <= (1 << (q.log2P - q.fbits)); k += NT) {
-    lcs[k] = cstart[k];
-    lbb[k] = bb[k];
-  }
-  lds_barrier();
+  lds_barrier();  // the table and flags initialised above
   Pre pr{};
   It nx{};
   if (blockIdx.x < nwork) {
@@ -1991,7 +1987,7 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
     }
     const uint64_t* src = (isel ? buf1 : buf0) + (uint64_t)p * q.cmax * q.sw;
     // 0. closed resident rows → closed store (pass 0 only)
-    if (evict && first) {
+    if (evict && first && nrow > 0) {  // (no resident rows: nothing to evict, no barriers)
       int ne = 0, nh = 0;
       for (int64_t r = threadIdx.x; r < nrow; r += NT) {
         const uint64_t* row = src + r * q.sw;
@@ -2184,7 +2180,7 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       }
       n_mine++;
     }
-    lds_barrier();
+    if (nrow > 0) lds_barrier();  // the marks before the list walk reads them (uniform: nrow is the item's)
     const int per = ((nl + NW - 1) / NW + 63) & ~63;
     const int lb0 = wave * per, lb1 = lb0 + per < nl ? lb0 + per : nl;
     int nnw = 0;
@@ -2257,7 +2253,7 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       }
       cur += __popcll(bl);
     }
-    lds_barrier();
+    if (nrow > 0) lds_barrier();  // the resident rows have read their entries before the walk clears them
     const uint32_t wmask = wbits ? (1u << wbits) - 1u : 0u;
     for (int k = lb0; k < lb1; k += 64) {
       const int i = k + lane;
@@ -2351,6 +2347,10 @@ bool c1v_eligible(khip_agg* a, int64_t n, int* col) {
          knob("KHIP_PAD", 0) == 0 && knob("KHIP_MERGE", 1) != 0 && knob("KHIP_SCATTER2", 1) != 0;
 }
 
+// Dynamic LDS of a value merge that still fits two workgroups per CU (160 KB, less the kernel's
+// static LDS).
+constexpr size_t C1V_LDS2 = 80 * 1024 - 256;
+
 // LDS layout of k_c1v_merge (byte offsets into q); returns the bytes.
 static size_t c1v_layout(khip_agg* a, int log2H, int idw, int log2B, C1VQ* q) {
   const size_t E = ((size_t)1 << log2H) + 64, H = (size_t)1 << log2H, B = (size_t)1 << log2B;
@@ -2381,7 +2381,8 @@ static size_t c1v_layout(khip_agg* a, int log2H, int idw, int log2B, C1VQ* q) {
   q->off_list = (int32_t)off;
   off += (H * 2 + 15) & ~(size_t)15;
   q->off_spre = (int32_t)off;
-  off += (C1_SEGMAX + 4) * 4 + C1_SEGMAX * 4 + (B + 1) * 12 + 8 + C1_SEGOF * 2;
+  off += (C1_SEGMAX + 4) * 4 + C1_SEGMAX * 4 + C1_SEGOF * 2;
+  (void)B;
   return off;
 }
 
@@ -2547,10 +2548,11 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
   C1VQ vq0{};
   int v_log2H = 12;
   int v_pm = 0;  // the plane mask when a specialised merge exists for it
-  const int v_nt = knob("KHIP_C1V_NT", 512) == 256 ? 256 : 512;  // merge workgroup size
-  const int v_wpc = (int)knob("KHIP_C1V_WG_PER_CU", 2);            // merge workgroups per CU
+  const int v_wpc = (int)knob("KHIP_C1V_WG_PER_CU", 2);  // merge workgroups per CU
   if (val) {
-    while (v_log2H > 9 && c1v_layout(a, v_log2H, 8, log2B, &vq0) > 78 * 1024) v_log2H--;
+    // sized for 32-bit identities (the common case); 64-bit ones (a key range past 31 - window
+    // bits) run at one workgroup per CU when their table does not fit two
+    while (v_log2H > 9 && c1v_layout(a, v_log2H, 4, log2B, &vq0) > C1V_LDS2) v_log2H--;
     v_log2H = (int)knob("KHIP_C1V_LOG2H", v_log2H);
 
     vq0.log2P = s.log2P;
@@ -2627,21 +2629,18 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
       vq.chg = a->changelog ? a->chg.as<uint8_t>() : nullptr;
       // the benchmarks' plane shapes have instantiations of their own (PM_C5, PM_C3), every other
       // one reads the planes from the parameters; AU 2 at <= 128 VGPRs (two workgroups per CU)
-      auto pick_nt = [&](auto pmc, auto ntc) {
-        constexpr int PMv = decltype(pmc)::value, NTv = decltype(ntc)::value;
-        return panes ? (idw == 0 ? k_c1v_merge<NTv, 2, uint32_t, true, 4, PMv> : k_c1v_merge<NTv, 2, uint64_t, true, 4, PMv>)
-                     : (idw == 0 ? k_c1v_merge<NTv, 2, uint32_t, false, 4, PMv> : k_c1v_merge<NTv, 2, uint64_t, false, 4, PMv>);
-      };
       auto pick = [&](auto pmc) {
-        return v_nt == 256 ? pick_nt(pmc, std::integral_constant<int, 256>{}) : pick_nt(pmc, std::integral_constant<int, 512>{});
+        constexpr int PMv = decltype(pmc)::value;
+        return panes ? (idw == 0 ? k_c1v_merge<512, 2, uint32_t, true, 4, PMv> : k_c1v_merge<512, 2, uint64_t, true, 4, PMv>)
+                     : (idw == 0 ? k_c1v_merge<512, 2, uint32_t, false, 4, PMv> : k_c1v_merge<512, 2, uint64_t, false, 4, PMv>);
       };
       auto mk = v_pm == PM_C5 ? pick(std::integral_constant<int, PM_C5>{})
                               : (v_pm == PM_C3 ? pick(std::integral_constant<int, PM_C3>{}) : pick(std::integral_constant<int, 0>{}));
       hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       KHIP_TRY(s.c1vq.ensure(sizeof(C1VQ)));
       KHIP_TRY_HIP(hipMemcpyAsync(s.c1vq.p, &vq, sizeof(C1VQ), hipMemcpyHostToDevice, a->stream));
-      const int64_t vgrid = std::min<int64_t>(nwork, (int64_t)s.n_cu * v_wpc);
-      hipLaunchKernelGGL(mk, dim3(vgrid), dim3(v_nt), lds, a->stream, s.c1vq.as<C1VQ>(), wk, nwork, s.c1bb.as<int64_t>(), cstart, seg,
+      const int64_t vgrid = std::min<int64_t>(nwork, (int64_t)s.n_cu * (lds <= C1V_LDS2 ? v_wpc : 1));
+      hipLaunchKernelGGL(mk, dim3(vgrid), dim3(512), lds, a->stream, s.c1vq.as<C1VQ>(), wk, nwork, s.c1bb.as<int64_t>(), cstart, seg,
                          (const ulonglong2*)s.srec.p, pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
                          s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
                          s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),

@@ -173,6 +173,56 @@ __device__ __forceinline__ uint64_t hash_bytes_dev(const uint8_t* p, int64_t n) 
   return mix64(h ^ w ^ ((uint64_t)(n & 7) << 59));
 }
 
+// Short keys (n <= 8 * KW_MAX bytes) as little-endian words read with aligned 8-byte loads (only
+// the words holding key bytes; bytes past n are 0): w[k] is what an unaligned load of bytes
+// [8k, 8k + 8) would give.  One to four loads instead of a load per byte.
+constexpr int KW_MAX = 3;
+__device__ __forceinline__ void key_words(const uint8_t* p, int64_t n, uint64_t (&w)[KW_MAX]) {
+  const uint64_t a = (uint64_t)p;
+  const uint64_t* base = (const uint64_t*)(a & ~7ULL);
+  const int sh = (int)(a & 7) * 8;
+  const int na = (int)(((a & 7) + (uint64_t)n + 7) >> 3);  // aligned words holding key bytes
+  uint64_t A[KW_MAX + 1];
+#pragma unroll
+  for (int k = 0; k <= KW_MAX; k++) A[k] = k < na ? base[k] : 0ULL;
+#pragma unroll
+  for (int k = 0; k < KW_MAX; k++) {
+    uint64_t x = sh ? (A[k] >> sh) | (A[k + 1] << (64 - sh)) : A[k];
+    const int64_t left = n - 8 * k;  // key bytes in this word
+    if (left <= 0) x = 0;
+    else if (left < 8) x &= (1ULL << (8 * left)) - 1;
+    w[k] = x;
+  }
+}
+
+// hash_bytes_dev over key_words' words (the same value).
+__device__ __forceinline__ uint64_t hash_key_words(const uint64_t (&w)[KW_MAX], int64_t n) {
+  uint64_t h = 0x84222325cbf29ce4ULL ^ (uint64_t)n;
+  const int full = (int)(n >> 3);
+  uint64_t tail = 0;
+#pragma unroll
+  for (int k = 0; k < KW_MAX; k++) {
+    if (k < full) h = mix64(h ^ w[k]) * 0x9E3779B97F4A7C15ULL;
+    else if (k == full) tail = w[k];
+  }
+  return mix64(h ^ tail ^ ((uint64_t)(n & 7) << 59));
+}
+
+// key_words of a key against n bytes at an 8-aligned arena entry (padding bytes ignored).
+__device__ __forceinline__ bool key_words_eq_aligned(const uint64_t (&w)[KW_MAX], const uint8_t* e, int64_t n) {
+  const uint64_t* q = (const uint64_t*)e;
+  bool eq = true;
+#pragma unroll
+  for (int k = 0; k < KW_MAX; k++) {
+    const int64_t left = n - 8 * k;
+    if (left <= 0) break;
+    uint64_t x = q[k];
+    if (left < 8) x &= (1ULL << (8 * left)) - 1;
+    eq = eq && x == w[k];
+  }
+  return eq;
+}
+
 __device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, int64_t n) {
   for (int64_t i = 0; i < n; i++)
     if (a[i] != b[i]) return false;

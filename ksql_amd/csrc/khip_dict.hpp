@@ -18,6 +18,7 @@ namespace khip {
 struct KeyDict {
   DevBuf dword, dkid, arena, bsum, fail;
   int64_t dcap = 0, docc = 0, arena_used = 0;
+  int64_t last_added = -1;  // keys the last map inserted (-1: no map yet)
 };
 
 // Allocate the first 4096 slots.

@@ -123,6 +123,31 @@ def test_c1_utf8_keys(prod, orc):
     assert kt["c1_pushes"] == 1, kt
 
 
+def test_c1_utf8_dictionary_growth(prod, orc):
+    """The key dictionary is sized from the keys the last map added (twice that, at least n / 16),
+    not from the batch size: a push bringing far more new keys than that fails its probes and is
+    mapped again into a larger table (khip_agg.hip dict_map); a reset gives back a table sized by
+    the first map's every-row estimate.  Rounds (a reset after each): [100 keys] (the reset shrinks
+    the table), [100 keys, 150K new keys] (the second push is mapped again twice), the same again."""
+    rng = np.random.default_rng(15)
+    b1 = ["k%07d" % int(i) for i in rng.integers(0, 100, 20_000)]
+    b2 = ["n%09d" % int(i) for i in rng.permutation(150_000)]
+    _, t1 = _fraud(rng, len(b1), 1, span=5_000)
+    _, t2 = _fraud(rng, len(b2), 1, span=5_000, t0=5_000)
+    batches = [abi.HostBatch(t1, utf8_keys=b1), abi.HostBatch(t2, utf8_keys=b2)]
+    gd, od = _desc(key_type="UTF8", hint=1 << 20), _desc(key_type="UTF8", hint=1 << 20)
+    g = abi.AggHandle(prod, gd)
+    for rnd in ([batches[0]], batches, batches):  # the oracle has no reset: a fresh handle per round
+        o = abi.AggHandle(orc, od)
+        for b in rnd:
+            assert g.push(b) == o.push(b)
+        assert_snap_equal(g.snapshot(), o.snapshot(), gd)
+        assert g.count_rows(HAVING) == o.snapshot(HAVING)["n"]
+        g.reset()
+        o.close()
+    g.close()
+
+
 def test_c1_sub_passes_and_region_growth(prod, orc):
     """4096 partitions (from the hint) and ~4150 groups each: over the 3072 an LDS table takes
     (retried with 2 sub-passes) and, for some, over the 4096-row regions (grown)."""
