@@ -168,3 +168,9 @@ def test_java_layout_matches_header(c_layout, jname):
 def test_integration_states_the_abi_version():
     text = open(os.path.join(REPO, "INTEGRATION.md")).read()
     assert "khip_abi_version() == %d" % abi.ABI_VERSION in text
+
+
+def test_graft_entry_checks_the_abi_version():
+    """__graft_entry__.build() asserts the built library's ABI version; it must be this one."""
+    text = open(os.path.join(REPO, "__graft_entry__.py")).read()
+    assert "abi.ABI_VERSION == %d" % abi.ABI_VERSION in text
