@@ -47,8 +47,8 @@ constexpr int C1_TILE = 65536;   // records per hist / scatter tile (the general
 constexpr int C1_NT = 512;       // workgroup size of every kernel here
 constexpr int C1_CH = 8192;      // refine chunk (records), 16 per thread
 constexpr int C1_SEGMAX = 512;   // chunks of one bucket the merge can hold (4M records)
-constexpr int C1_SEGB = 7;       // the merge's segment lookup: one entry per 128 records of an item
-constexpr int C1_SEGOF = 512;    // ... for items of up to 64K records (larger ones binary-search)
+constexpr int C1_SEGB = 7;       // the merge's segment lookup: one entry per 32, 64 or 128 records of an
+constexpr int C1_SEGOF = 512;    // item (the finest that fits 512 entries; past 64K records: binary search)
 constexpr uint32_t C1_SENT = 0x80000000u;  // low word of a sentinel record (ts - T0 never is)
 
 // c1info (int64) slots
@@ -859,7 +859,7 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
   };
   struct It {
     uint32_t p;
-    int sbits, sub, nseg;
+    int sbits, sub, nseg, segb;  // segb: log2 of the records per segment-lookup block
     int64_t rn, nrow;
     bool isel;
   };
@@ -921,8 +921,16 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     if (lane == 63) wsum[wave] = incl;
     lds_barrier();
     int before = 0;
-    for (int k = 0; k < NW; k++) before += k < wave ? wsum[k] : 0;
+    int tot = 0;
+    for (int k = 0; k < NW; k++) {
+      before += k < wave ? wsum[k] : 0;
+      tot += wsum[k];
+    }
     const int ex = before + incl - s;
+    // the finest lookup block that covers the item in C1_SEGOF entries (segments hold C1_CH / F
+    // records on average: 32-record blocks make the lookup a read and at most a step or two)
+    const int segb = tot <= (C1_SEGOF << 5) ? 5 : (tot <= (C1_SEGOF << 6) ? 6 : C1_SEGB);
+    const int bm = (1 << segb) - 1;
     if (k0 < nseg) {
       spre[k0] = (uint32_t)ex;
       sbs[k0] = (int32_t)(base0 - ex);
@@ -931,28 +939,29 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       spre[k0 + 1] = (uint32_t)(ex + len0);
       sbs[k0 + 1] = (int32_t)(base1 - (ex + len0));
     }
-    // segment lookup: block j (records [128 j, 128 j + 128)) starts in segment segof[j]
-    for (int bj = (ex + 127) >> C1_SEGB, be = (ex + len0 + 127) >> C1_SEGB; bj < be && bj < C1_SEGOF; bj++)
+    // segment lookup: block j (records [j << segb, (j + 1) << segb)) starts in segment segof[j]
+    for (int bj = (ex + bm) >> segb, be = (ex + len0 + bm) >> segb; bj < be && bj < C1_SEGOF; bj++)
       segof[bj] = (uint16_t)k0;
-    for (int bj = (ex + len0 + 127) >> C1_SEGB, be = (ex + s + 127) >> C1_SEGB; bj < be && bj < C1_SEGOF; bj++)
+    for (int bj = (ex + len0 + bm) >> segb, be = (ex + s + bm) >> segb; bj < be && bj < C1_SEGOF; bj++)
       segof[bj] = (uint16_t)(k0 + 1);
     if (k0 < nseg && k0 + 2 >= nseg) spre[nseg] = (uint32_t)(ex + s);  // the total
     if (nseg == 0 && threadIdx.x == 0) spre[0] = 0u;
     lds_barrier();
     it.rn = spre[nseg];
+    it.segb = segb;
   };
   uint64_t ra[AU], rb[AU];
   uint32_t ta[AU], tb[AU];  // WIDE: the records' ts words
   // records li = l0 + thread + u NT of the item whose segments are in LDS (indices clamped to the
   // last record: every load is unconditional, so the waits stay counted)
-  auto load = [&](uint64_t (&x)[AU], uint32_t (&tx)[AU], int64_t l0, int64_t rn, int nseg) {
+  auto load = [&](uint64_t (&x)[AU], uint32_t (&tx)[AU], int64_t l0, int64_t rn, int nseg, int segb) {
 #pragma unroll
     for (int u = 0; u < AU; u++) {
       int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
       li = li < rn ? li : rn - 1;
       int lo = 0;  // the last segment starting at or before li
-      if (rn <= ((int64_t)C1_SEGOF << C1_SEGB)) {  // from the block's segment, a step or two on
-        lo = segof[li >> C1_SEGB];
+      if (rn <= ((int64_t)C1_SEGOF << segb)) {  // from the block's segment, a step or two on
+        lo = segof[li >> segb];
         while (lo + 1 < nseg && (int64_t)spre[lo + 1] <= li) lo++;
       } else {
         int hi = nseg;
@@ -970,8 +979,8 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
   // the item's first two chunks (register sets A and B): a chunk is always two chunks ahead of
   // the one being applied
   auto load01 = [&](const It& x) {
-    if (x.rn > 0) load(ra, ta, 0, x.rn, x.nseg);
-    if (x.rn > (int64_t)AU * NT) load(rb, tb, (int64_t)AU * NT, x.rn, x.nseg);
+    if (x.rn > 0) load(ra, ta, 0, x.rn, x.nseg, x.segb);
+    if (x.rn > (int64_t)AU * NT) load(rb, tb, (int64_t)AU * NT, x.rn, x.nseg, x.segb);
   };
   // the bucket table (chunk starts, bucket bases) in LDS for every descriptor
   for (int k = threadIdx.x; k <= (1 << (q.log2P - q.fbits)); k += NT) {
@@ -992,7 +1001,7 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
   for (int64_t w = blockIdx.x; w < nwork; w += gridDim.x) {
     const It it = nx;
     const uint32_t p = it.p;
-    const int sbits = it.sbits, sub = it.sub, nseg = it.nseg;
+    const int sbits = it.sbits, sub = it.sub, nseg = it.nseg, segb = it.segb;
     const int64_t rn = it.rn, nrow = it.nrow;
     const bool isel = it.isel;
     const int64_t wn = w + gridDim.x;
@@ -1126,12 +1135,12 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
         if (r32) apply(ra, ta, c * AU * NT, std::true_type{});
         else apply(ra, ta, c * AU * NT, std::false_type{});
         if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
-        if (c + 2 < nch) load(ra, ta, (c + 2) * AU * NT, rn, nseg);
+        if (c + 2 < nch) load(ra, ta, (c + 2) * AU * NT, rn, nseg, segb);
         if (c + 1 >= nch) break;
         if (r32) apply(rb, tb, (c + 1) * AU * NT, std::true_type{});
         else apply(rb, tb, (c + 1) * AU * NT, std::false_type{});
         if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
-        if (c + 3 < nch) load(rb, tb, (c + 3) * AU * NT, rn, nseg);
+        if (c + 3 < nch) load(rb, tb, (c + 3) * AU * NT, rn, nseg, segb);
       }
     }
     lds_barrier();
@@ -1854,7 +1863,7 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
   };
   struct It {
     uint32_t p;
-    int sbits, sub, nseg;
+    int sbits, sub, nseg, segb;  // segb: log2 of the records per segment-lookup block
     int64_t rn, nrow;
     bool isel;
   };
@@ -1916,8 +1925,16 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
     if (lane == 63) wsum[wave] = incl;
     lds_barrier();
     int before = 0;
-    for (int k = 0; k < NW; k++) before += k < wave ? wsum[k] : 0;
+    int tot = 0;
+    for (int k = 0; k < NW; k++) {
+      before += k < wave ? wsum[k] : 0;
+      tot += wsum[k];
+    }
     const int ex = before + incl - s;
+    // the finest lookup block that covers the item in C1_SEGOF entries (segments hold C1_CH / F
+    // records on average: 32-record blocks make the lookup a read and at most a step or two)
+    const int segb = tot <= (C1_SEGOF << 5) ? 5 : (tot <= (C1_SEGOF << 6) ? 6 : C1_SEGB);
+    const int bm = (1 << segb) - 1;
     if (k0 < nseg) {
       spre[k0] = (uint32_t)ex;
       sbs[k0] = (int32_t)(base0 - ex);
@@ -1926,25 +1943,26 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       spre[k0 + 1] = (uint32_t)(ex + len0);
       sbs[k0 + 1] = (int32_t)(base1 - (ex + len0));
     }
-    // segment lookup: block j (records [128 j, 128 j + 128)) starts in segment segof[j]
-    for (int bj = (ex + 127) >> C1_SEGB, be = (ex + len0 + 127) >> C1_SEGB; bj < be && bj < C1_SEGOF; bj++)
+    // segment lookup: block j (records [j << segb, (j + 1) << segb)) starts in segment segof[j]
+    for (int bj = (ex + bm) >> segb, be = (ex + len0 + bm) >> segb; bj < be && bj < C1_SEGOF; bj++)
       segof[bj] = (uint16_t)k0;
-    for (int bj = (ex + len0 + 127) >> C1_SEGB, be = (ex + s + 127) >> C1_SEGB; bj < be && bj < C1_SEGOF; bj++)
+    for (int bj = (ex + len0 + bm) >> segb, be = (ex + s + bm) >> segb; bj < be && bj < C1_SEGOF; bj++)
       segof[bj] = (uint16_t)(k0 + 1);
     if (k0 < nseg && k0 + 2 >= nseg) spre[nseg] = (uint32_t)(ex + s);
     if (nseg == 0 && threadIdx.x == 0) spre[0] = 0u;
     lds_barrier();
     it.rn = spre[nseg];
+    it.segb = segb;
   };
   ulonglong2 ra[AU], rb[AU];
-  auto load = [&](ulonglong2 (&x)[AU], int64_t l0, int64_t rn, int nseg) {
+  auto load = [&](ulonglong2 (&x)[AU], int64_t l0, int64_t rn, int nseg, int segb) {
 #pragma unroll
     for (int u = 0; u < AU; u++) {
       int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
       li = li < rn ? li : rn - 1;
       int lo = 0;  // the last segment starting at or before li
-      if (rn <= ((int64_t)C1_SEGOF << C1_SEGB)) {  // from the block's segment, a step or two on
-        lo = segof[li >> C1_SEGB];
+      if (rn <= ((int64_t)C1_SEGOF << segb)) {  // from the block's segment, a step or two on
+        lo = segof[li >> segb];
         while (lo + 1 < nseg && (int64_t)spre[lo + 1] <= li) lo++;
       } else {
         int hi = nseg;
@@ -1958,8 +1976,8 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
     }
   };
   auto load01 = [&](const It& x) {
-    if (x.rn > 0) load(ra, 0, x.rn, x.nseg);
-    if (x.rn > (int64_t)AU * NT) load(rb, (int64_t)AU * NT, x.rn, x.nseg);
+    if (x.rn > 0) load(ra, 0, x.rn, x.nseg, x.segb);
+    if (x.rn > (int64_t)AU * NT) load(rb, (int64_t)AU * NT, x.rn, x.nseg, x.segb);
   };
   lds_barrier();  // the table and flags initialised above
   Pre pr{};
@@ -1972,7 +1990,7 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
   for (int64_t w = blockIdx.x; w < nwork; w += gridDim.x) {
     const It it = nx;
     const uint32_t p = it.p;
-    const int sbits = it.sbits, sub = it.sub, nseg = it.nseg;
+    const int sbits = it.sbits, sub = it.sub, nseg = it.nseg, segb = it.segb;
     const int64_t rn = it.rn, nrow = it.nrow;
     const bool isel = it.isel;
     const int64_t wn = w + gridDim.x;
@@ -2100,12 +2118,12 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
         if (r32) apply(ra, c * AU * NT, std::true_type{});
         else apply(ra, c * AU * NT, std::false_type{});
         if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
-        if (c + 2 < nch) load(ra, (c + 2) * AU * NT, rn, nseg);
+        if (c + 2 < nch) load(ra, (c + 2) * AU * NT, rn, nseg, segb);
         if (c + 1 >= nch) break;
         if (r32) apply(rb, (c + 1) * AU * NT, std::true_type{});
         else apply(rb, (c + 1) * AU * NT, std::false_type{});
         if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
-        if (c + 3 < nch) load(rb, (c + 3) * AU * NT, rn, nseg);
+        if (c + 3 < nch) load(rb, (c + 3) * AU * NT, rn, nseg, segb);
       }
     }
     lds_barrier();

@@ -315,6 +315,8 @@ __device__ __forceinline__ bool where_ok(const uint64_t* s, uint64_t meta, const
   return false;
 }
 
+constexpr int JCTR = 64;  // emitted-row counters of a probe (khip_table_probe_device)
+
 struct JOut {
   uint8_t* emit;
   uint8_t* matched;
@@ -463,7 +465,9 @@ __global__ __launch_bounds__(256) void k_probe(const uint64_t* __restrict__ tabl
     if (out.slot_out && i < n) out.slot_out[i] = emit ? found + 1 : -1;  // 0 = emitted LEFT miss
     cnt += lane == 0 ? __popcll(be) : 0;
   }
-  if (n_emitted && lane == 0 && cnt) atomicAdd(n_emitted, (unsigned long long)cnt);
+  // one of JCTR counters per block (the host sums them): every wave adding to one word serialized
+  // at the memory side (~2M adds per 1e9-row probe)
+  if (n_emitted && lane == 0 && cnt) atomicAdd(&n_emitted[blockIdx.x & (JCTR - 1)], (unsigned long long)cnt);
 }
 
 // Probe through the dense index: one random cell read (MALL-resident for C4) per stream row,
@@ -518,7 +522,9 @@ __global__ __launch_bounds__(256) void k_probe_dense(JDense dn, const int64_t* _
     if (out.slot_out && i < n) out.slot_out[i] = emit ? (hit ? 1 : 0) : -1;
     cnt += lane == 0 ? __popcll(be) : 0;
   }
-  if (n_emitted && lane == 0 && cnt) atomicAdd(n_emitted, (unsigned long long)cnt);
+  // one of JCTR counters per block (the host sums them): every wave adding to one word serialized
+  // at the memory side (~2M adds per 1e9-row probe)
+  if (n_emitted && lane == 0 && cnt) atomicAdd(&n_emitted[blockIdx.x & (JCTR - 1)], (unsigned long long)cnt);
 }
 
 __global__ __launch_bounds__(256) void k_table_rehash(const uint64_t* __restrict__ old, int64_t ocap,
@@ -797,7 +803,7 @@ khip_status khip_table_create(const khip_table_desc* d, khip_table** out) {
   khip_status st;
   if ((st = table_alloc(t, t->table, t->cap)) != KHIP_OK ||
       (st = t->types_dev.ensure(sizeof(int32_t) * JMAX_COLS)) != KHIP_OK ||
-      (st = t->scratch.ensure(64)) != KHIP_OK || (t->utf8 && (st = dict_init(t->dict, t->stream)) != KHIP_OK)) {
+      (st = t->scratch.ensure(64 + 8 * JCTR)) != KHIP_OK || (t->utf8 && (st = dict_init(t->dict, t->stream)) != KHIP_OK)) {
     khip_table_destroy(t);
     return st;
   }
@@ -992,15 +998,17 @@ khip_status khip_table_probe_device(khip_table* t, const khip_batch* b, int32_t 
   }
   unsigned long long* ctr = nullptr;
   if (n_emitted) {
-    ctr = t->scratch.as<unsigned long long>() + 4;
-    KHIP_TRY_HIP(hipMemsetAsync(ctr, 0, 8, t->stream));
+    ctr = t->scratch.as<unsigned long long>() + 8;  // JCTR words after the 64-byte scratch block
+    KHIP_TRY_HIP(hipMemsetAsync(ctr, 0, 8 * JCTR, t->stream));
   }
   KHIP_TRY(probe_launch(t, b, join_type, w, o, ctr));
   if (n_emitted) {
-    unsigned long long v = 0;
-    KHIP_TRY_HIP(hipMemcpyAsync(&v, ctr, 8, hipMemcpyDeviceToHost, t->stream));
+    unsigned long long v[JCTR];
+    KHIP_TRY_HIP(hipMemcpyAsync(v, ctr, sizeof(v), hipMemcpyDeviceToHost, t->stream));
     KHIP_TRY_HIP(hipStreamSynchronize(t->stream));
-    *n_emitted = (int64_t)v;
+    int64_t tot = 0;
+    for (int k = 0; k < JCTR; k++) tot += (int64_t)v[k];
+    *n_emitted = tot;
   }
   return KHIP_OK;
 }
