@@ -687,7 +687,7 @@ def bench_possible_fraud(args, lib, rank, world, local):
     push_ms = sum(phase.values())
     bpr = BYTES_PER_RECORD_C2_UTF8 if args.utf8 else BYTES_PER_RECORD_C2
     c1 = kt.get("c1_pushes", 0) > 0
-    if c1:  # the COUNT(*) pipeline: keys-only histogram; scatter + refine of 8-byte (12 wide) records
+    if c1:  # the COUNT(*) pipeline: step-run scatter + refine of 8-byte (12 wide) records
         wide = args.sparse_keys
         own = {"stream_time_ms": 8, "dict_ms": 32, "partition_ms": (16 + 12 + 12 + 12) if wide else (16 + 8 + 8 + 8),
                "apply_ms": (12 if wide else 8) + 32.0 * groups / n, "finalize_ms": 0}
@@ -696,7 +696,7 @@ def bench_possible_fraud(args, lib, rank, world, local):
                "finalize_ms": 0}
     per_kernel = {k: {"ms": phase[k], "bytes_per_record": own[k],
                       "GB/s": own[k] * n / (phase[k] / 1000.0) / 1e9} for k in phase if phase[k] > 0}
-    variant = "_utf8" if args.utf8 else ("_sparse" if args.sparse_keys else "")
+    variant = "_utf8" if args.utf8 else ("_sparse_keys" if args.sparse_keys else "")  # profile_leg.sh's leg names
     traffic = load_traffic(args.traffic_json, "possible_fraud" + ("_atomic" if args.engine == "atomic" else ""), n,
                            variant)
     roof = roofline(bpr * n, ms_step, push_ms, per_kernel, traffic, bpr,
