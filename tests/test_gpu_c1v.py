@@ -176,3 +176,20 @@ def test_c1v_many_groups_subpasses(prod, orc):
     batches = _batches(rng, "all_i32", 2, 1_000_000, 900_000, 20_000)
     kt = _run(prod, orc, "all_i32", "hop3", batches, hint=1 << 16)
     assert kt["c1_pushes"] >= 1, kt
+
+
+@pytest.mark.parametrize("shape", ["sum_i64", "c3_f64"])
+def test_c1v_wide_identity(prod, orc, shape):
+    """Keys spread over 2^30 (the key field's 31 bits still hold them) with several windows per
+    push: (key - kmin) << window bits needs 64-bit identities, whose merge table is sized for the
+    32-bit ones and runs at one workgroup per CU when it does not fit two."""
+    rng = np.random.default_rng(10)
+    pool = rng.integers(0, 1 << 30, 20_000)
+    batches = []
+    for b in range(2):
+        k = pool[rng.integers(0, len(pool), 400_000)]
+        ts = b * 40_000 + (np.arange(len(k)) * 40_000) // len(k) + rng.integers(0, 500, len(k))
+        batches.append(abi.HostBatch(ts, keys=k, cols=[_values(rng, len(k), shape)],
+                                     col_valid=[rng.random(len(k)) > 0.03]))
+    kt = _run(prod, orc, shape, "tumbling", batches, hint=1_000_000)
+    assert kt["c1_pushes"] == 2 and kt["c1_declined"] == 0, kt
