@@ -191,5 +191,5 @@ def test_c1v_wide_identity(prod, orc, shape):
         ts = b * 40_000 + (np.arange(len(k)) * 40_000) // len(k) + rng.integers(0, 500, len(k))
         batches.append(abi.HostBatch(ts, keys=k, cols=[_values(rng, len(k), shape)],
                                      col_valid=[rng.random(len(k)) > 0.03]))
-    kt = _run(prod, orc, shape, "tumbling", batches, hint=1_000_000)
+    kt = _run(prod, orc, shape, "tumbling", batches, hint=3_000_000)  # (>= 2^11 partitions: eligible)
     assert kt["c1_pushes"] == 2 and kt["c1_declined"] == 0, kt
