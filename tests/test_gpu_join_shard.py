@@ -1,0 +1,143 @@
+"""Sharded stream-table join with probe routing (ksql_amd/join_shard.py) in two
+processes on one GPU, the exchange over gloo (RCCL refuses two ranks on one device; the
+production exchange is abi.Comm, the same two collective steps over RCCL).
+
+Each rank holds a source slice of the users table changelog (inserts, then updates and
+tombstones of its own keys) and of the click stream.  Table rows and clicks are routed to the rank
+Kafka's default partitioner assigns their key to (StreamTableJoinBuilder.java:77-86: the two
+sides are co-partitioned), each rank upserts and probes its shard with the product library, and
+rank 0 checks every rank against the oracle:
+- the clicks a rank received are exactly those whose key it owns, in (source rank, arrival) order;
+- its emit / matched bitmaps, right column and null bitmap equal the oracle's probe of those
+  clicks against ONE table built from every changelog row (LEFT JOIN ... WHERE level =
+  'Platinum', C4's query);
+- the shards' sizes add up to the oracle table's.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from ksql_amd import abi, synth
+
+pytestmark = pytest.mark.gpu
+
+WORLD = 2
+U = 60_000       # users
+N_CLICKS = 200_000
+
+
+def _kafka_partition(orc, keys, n_parts):
+    keys = np.ascontiguousarray(keys, dtype=np.int64)
+    out = np.zeros(len(keys), np.int32)
+    orc.dll.oracle_kafka_partition(keys.ctypes.data, len(keys), 8, n_parts, out.ctypes.data)
+    return out
+
+
+def _sources(rank):
+    """This rank's changelog slices (inserts; then updates + tombstones) and click slice."""
+    uid, level = synth.users_table(0, U)
+    uid = synth.sparse_ids(uid)
+    lo, hi = rank * U // WORLD, (rank + 1) * U // WORLD
+    k1, l1 = uid[lo:hi], level[lo:hi].astype(np.int32)
+    rng = np.random.default_rng(100 + rank)
+    pick = rng.permutation(len(k1))[: len(k1) // 10]
+    k2 = k1[pick]
+    l2 = rng.integers(0, len(synth.LEVELS), len(k2)).astype(np.int32)
+    d2 = rng.random(len(k2)) < 0.5  # half of them deleted, half updated
+    cu, cts = synth.clicks(0, N_CLICKS, U, seed_clicks=7)
+    cu = synth.sparse_ids(cu)
+    clo, chi = rank * N_CLICKS // WORLD, (rank + 1) * N_CLICKS // WORLD
+    return (k1, l1), (k2, l2, d2), (cu[clo:chi], cts[clo:chi])
+
+
+def _worker(rank, port, q):
+    import torch.distributed as dist
+    from ksql_amd.join_shard import ShardedTable
+    from ksql_amd.repartition import GlooExchange
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        torch.cuda.init()
+        prod = abi.load_product()
+        (k1, l1), (k2, l2, d2), (cu, cts) = _sources(rank)
+        dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+        st = ShardedTable(prod, ["INT32"], rank=rank, world=WORLD, comm=GlooExchange(), capacity_hint=2 * U)
+        st.upsert(dev(k1), dev(np.zeros(len(k1), np.int64)), cols=[dev(l1)])
+        st.upsert(dev(k2), dev(np.ones(len(k2), np.int64)), cols=[dev(l2)], deleted=dev(d2))
+        where = {"col": 0, "op": "EQ", "i64": synth.LEVELS.index("Platinum")}
+        out = st.probe(dev(cu), dev(cts), "LEFT", where)
+        torch.cuda.synchronize()
+        m = out["n"]
+        nb = (m + 7) // 8
+        res = {"n": m, "key": out["key"].cpu().numpy(), "ts": out["ts"].cpu().numpy(),
+               "emit": out["emit"][:nb].cpu().numpy(), "matched": out["matched"][:nb].cpu().numpy(),
+               "right": out["right"][0][:m].cpu().numpy(), "right_null": out["right_null"][0][:nb].cpu().numpy(),
+               "emitted": out["emitted"], "size": st.size()}
+        st.close()
+        gathered = [None] * WORLD
+        dist.all_gather_object(gathered, res)
+        if rank == 0:
+            q.put(gathered)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_join_two_ranks():
+    orc = abi.load_oracle()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    g = q.get(timeout=200)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    src = [_sources(r) for r in range(WORLD)]
+    table = abi.TableHandle(orc, ["INT32"], capacity_hint=2 * U)
+    for r in range(WORLD):
+        (k1, l1), _, _ = src[r]
+        table.upsert(abi.HostBatch(np.zeros(len(k1), np.int64), keys=k1, cols=[l1]))
+    for r in range(WORLD):
+        _, (k2, l2, d2), _ = src[r]
+        table.upsert(abi.HostBatch(np.ones(len(k2), np.int64), keys=k2, cols=[l2], row_valid=~d2))
+    assert sum(x["size"] for x in g) == table.size()
+    where = {"col": 0, "op": "EQ", "i64": synth.LEVELS.index("Platinum")}
+    for d in range(WORLD):
+        ek, ets = [], []
+        for r in range(WORLD):
+            cu, cts = src[r][2]
+            sel = _kafka_partition(orc, cu, WORLD) == d
+            ek.append(cu[sel]), ets.append(cts[sel])
+        ek, ets = np.concatenate(ek), np.concatenate(ets)
+        o = g[d]
+        assert o["n"] == len(ek)
+        np.testing.assert_array_equal(o["key"], ek)
+        np.testing.assert_array_equal(o["ts"], ets)
+        exp = table.probe(abi.HostBatch(ets, keys=ek), "LEFT", where)
+        every = table.probe(abi.HostBatch(ets, keys=ek), "LEFT", None)
+        n = len(ek)
+        e = np.zeros(n, bool)
+        e[exp["stream_row"]] = True
+        hit = np.zeros(n, bool)
+        hit[every["stream_row"]] = every["matched"]
+        bits = lambda b: np.packbits(b, bitorder="little")
+        assert o["emitted"] == len(exp["stream_row"])
+        np.testing.assert_array_equal(o["emit"], bits(e))
+        np.testing.assert_array_equal(o["matched"], bits(hit))
+        isnull = np.ones(n, bool)
+        isnull[every["stream_row"]] = every["nulls"][0]
+        np.testing.assert_array_equal(o["right_null"], bits(isnull))
+        val = np.zeros(n, np.int32)
+        val[every["stream_row"]] = every["cols"][0]
+        np.testing.assert_array_equal(o["right"][~isnull], val[~isnull])
+    table.close()
