@@ -2113,7 +2113,22 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       }
     };
     const int64_t nch = (rn + (int64_t)AU * NT - 1) / ((int64_t)AU * NT);
-    if (rn > 0) {
+    if (rn > 0 && PANES) {
+      // HOPPING items run many chunks (C3: ~8): a straight-line body (a chunk past the end applies
+      // nothing; its loads, clamped to the last record, read one line) whose wait for one register
+      // set counts the other set's loads as in flight; the table-full check once per two chunks
+      auto records = [&](auto R32) {
+        for (int64_t c = 0; c < nch; c += 2) {
+          apply(ra, c * AU * NT, R32);
+          load(ra, (c + 2) * AU * NT, rn, nseg, segb);
+          apply(rb, (c + 1) * AU * NT, R32);
+          load(rb, (c + 3) * AU * NT, rn, nseg, segb);
+          if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
+        }
+      };
+      if (r32) records(std::true_type{});
+      else records(std::false_type{});
+    } else if (rn > 0) {
       for (int64_t c = 0; c < nch; c += 2) {
         if (r32) apply(ra, c * AU * NT, std::true_type{});
         else apply(ra, c * AU * NT, std::false_type{});
