@@ -893,8 +893,9 @@ static khip_status probe_launch(khip_table* t, const khip_batch* b, int32_t join
   KHIP_TRY(prepare_dense(t));
   if (t->dense_ok) {
     // rows per thread: every cell read of a thread is issued before any is used (MLP); measured on
-    // C4 (1e9 probes, 100 MB of cells): 4 → 49 ms, 8 → 28 ms, 16 → 20 ms
-    const int dpr = (int)knob("KHIP_PROBE_DPR", 16);
+    // C4 (1e9 probes, 100 MB of cells): 4 → 49 ms, 8 → 28 ms, 16 → 20.1 ms, 32 → 19.8 ms, 64 →
+    // 73 ms (profiles/r04/ab/c4_dense_rows_per_thread.txt)
+    const int dpr = (int)knob("KHIP_PROBE_DPR", 32);
     auto dk = dpr >= 64 ? k_probe_dense<64>
                         : (dpr >= 32 ? k_probe_dense<32> : (dpr >= 16 ? k_probe_dense<16> : k_probe_dense<8>));
     const int pr = dpr >= 64 ? 64 : (dpr >= 32 ? 32 : (dpr >= 16 ? 16 : 8));
