@@ -37,8 +37,9 @@ Output: one JSON line (rank 0) with `roofline` and `cpu_baseline`:
   roofline.push              the same bytes ÷ the device time of the push's kernels alone (HIP
                              events on the library's stream), with a per-kernel breakdown;
   roofline.traffic           HBM bytes per step from the committed rocprofv3 PMC summary
-                             (profiles/traffic.json, FETCH_SIZE x 2 + WRITE_SIZE, gfx950
-                             correction) when it was measured on this exact configuration;
+                             (profiles/traffic.json: read requests by size,
+                             TCC_EA0_RDREQ_{32B,64B,128B} + WRITE_SIZE, tools/pmc_traffic.py)
+                             when it was measured on this exact configuration;
   cpu_baseline               the oracle (oracle/oracle.c, a C restatement of the reference
                              semantics — the JVM reference cannot run on this image) timed on a
                              bounded sample of the same workload, single-threaded and with P
@@ -165,12 +166,13 @@ def cpu_baseline_block(single, par, P, unit, sample, ks=None):
 
 def load_traffic(path, config, n, variant=""):
     """HBM bytes per step from the committed PMC summary (tools/pmc_traffic.py), if it was
-    measured on this configuration and size."""
+    measured on this configuration and size with the size-classed read counters (method_version
+    2; round-4 entries doubled FETCH_SIZE from a hand-kept kernel list and are not used)."""
     try:
         with open(path) as f:
             t = json.load(f)
         rec = t.get(config + variant)
-        if rec and rec.get("records") == n:
+        if rec and rec.get("records") == n and rec.get("method_version", 1) >= 2:
             return rec["hbm_bytes_per_step"]
     except (OSError, ValueError):
         pass
@@ -1077,15 +1079,20 @@ def bench_repartition(args, lib, rank, world, local):
     phases = {"pack": 0.0, "exchange": 0.0, "aggregate": 0.0}
     state = {"timed": False, "m": 0}
 
-    # sized for every source row: khip_shuffle_pack's counts and scatter in one call
-    send_buf = torch.empty((n, rp.shuffle.row_words), dtype=torch.int64, device=torch.device("cuda", local))
+    # one destination: sized for every source row (khip_shuffle_pack's one-pass compaction);
+    # several: khip_shuffle_pack_v's regions (one pass, khip_shuffle_pack_capacity rows)
+    send_buf = torch.empty((rp.shuffle.pack_capacity(n), rp.shuffle.row_words), dtype=torch.int64,
+                           device=torch.device("cuda", local))
 
     def step():
         t0 = time.perf_counter()
-        send, counts = rp.shuffle.pack(src, send=send_buf)
+        if world > 1:
+            send, counts, offs = rp.shuffle.pack_v(src, send=send_buf)
+        else:
+            send, counts = rp.shuffle.pack(src, send=send_buf)
         t1 = time.perf_counter()
         if world > 1:
-            recv, rc = comm.alltoall(send, counts, rp.shuffle.row_words)
+            recv, rc = comm.alltoall(send, counts, rp.shuffle.row_words, send_offsets=offs)
         else:
             recv, rc = send, counts
         m = int(sum(rc))

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KHIP_ABI_VERSION 6
+#define KHIP_ABI_VERSION 7
 
 typedef int32_t khip_status;
 #define KHIP_OK 0
@@ -490,21 +490,29 @@ khip_status khip_table_destroy(khip_table* t);
  * (S/GroupByParamsFactory.java:92-100).  Packed row (u64 words, 2 + n_cols of them):
  *   [new key][ts][value columns except key_col (raw, INT32 sign-extended)...]
  *   [validity bits: column c = bit c; the key column's bit is always set]
- * Order is stable: a destination receives each source's rows in arrival order. */
+ * Order is stable: a destination receives each source's rows in arrival order.
+ * ABI 7, KHIP_SHUFFLE_STREAM_TIME in `flags`: the rows also carry the batch's `stream_time` column
+ * (the GLOBAL stream time observed at the row, khip_stream_time_scan before routing) as one more
+ * word before the validity word:
+ *   [new key][ts][value columns except key_col...][stream_time][validity bits]
+ * so the owner's KHIP_TIME_SUPPLIED aggregation (khip_agg_push_shuffled) late-drops against the
+ * stream time one task over the whole stream would have had (TopologyTestDriver: one task per
+ * query, F/tools/TestExecutorUtil.java:123-126). */
+#define KHIP_SHUFFLE_STREAM_TIME 1
 typedef struct khip_shuffle_desc {
   int32_t n_parts;          /* destinations (tasks / GPUs)                                */
   int32_t key_col;          /* value column that becomes the new key (INT32/INT64)        */
   int32_t n_cols;           /* value columns carried (all of the batch's columns)         */
   const int32_t* col_types;
   int32_t device;
-  int32_t flags;
+  int32_t flags;            /* KHIP_SHUFFLE_*                                             */
 } khip_shuffle_desc;
 
 typedef struct khip_shuffle khip_shuffle;
 
 khip_status khip_shuffle_create(const khip_shuffle_desc* desc, khip_shuffle** out);
 
-/* Words per packed row (2 + n_cols). */
+/* Words per packed row (2 + n_cols, + 1 with KHIP_SHUFFLE_STREAM_TIME). */
 int32_t khip_shuffle_row_words(const khip_shuffle* s);
 
 /* Partition a DEVICE batch into the caller's device buffer `send` (capacity rows x row
@@ -512,6 +520,18 @@ int32_t khip_shuffle_row_words(const khip_shuffle* s);
  * (destination d's rows start at the sum of counts[0..d)). */
 khip_status khip_shuffle_pack(khip_shuffle* s, const khip_batch* in, uint64_t* send,
                               int64_t capacity, int64_t* counts);
+
+/* ABI 7.  The one-pass pack for n_parts > 1: every row is read once (no counting pass over the
+ * source).  Destination d's rows are written contiguously, in arrival order, at row offsets[d] of
+ * `send` (counts[d] of them): the library lays the destinations out in regions of a stride sized
+ * from the batch's even share n_rows / n_parts plus slack, finds each tile's place in every region
+ * by decoupled look-back over the earlier tiles' per-destination counts, and packs a batch whose
+ * largest destination overflows its region again with the exact stride (or, when that does not
+ * fit `capacity`, contiguously as khip_shuffle_pack does).  `capacity` (rows) must be at least
+ * khip_shuffle_pack_capacity(s, n_rows).  The send side of khip_comm_alltoall_v. */
+int64_t khip_shuffle_pack_capacity(const khip_shuffle* s, int64_t n_rows);
+khip_status khip_shuffle_pack_v(khip_shuffle* s, const khip_batch* in, uint64_t* send,
+                                int64_t capacity, int64_t* counts, int64_t* offsets);
 
 /* Packed rows (device) → columnar device arrays owned by the caller: key[n], ts[n],
  * col_data[c][n] (8-byte raw for every column type except INT32 = 4 bytes) and
@@ -525,6 +545,11 @@ khip_status khip_shuffle_pack(khip_shuffle* s, const khip_batch* in, uint64_t* s
 khip_status khip_shuffle_unpack(khip_shuffle* s, const uint64_t* rows, int64_t n, int64_t* key,
                                 int64_t* ts, void* const* col_data, uint8_t* const* col_valid);
 
+/* ABI 7.  KHIP_SHUFFLE_STREAM_TIME rows → their stream_time column (device, n entries): with
+ * khip_shuffle_unpack, a KHIP_TIME_SUPPLIED batch. */
+khip_status khip_shuffle_unpack_stream_time(khip_shuffle* s, const uint64_t* rows, int64_t n,
+                                            int64_t* stream_time);
+
 /* ABI 6.  Received rows straight into the aggregation that reads the repartition topic (the
  * non-key GROUP BY's aggregate, S/StreamGroupByBuilderBase.java:101-103 → StreamAggregateBuilder),
  * without materialising them as columns first: the same effect and statistics as khip_agg_push of
@@ -533,7 +558,10 @@ khip_status khip_shuffle_unpack(khip_shuffle* s, const uint64_t* rows, int64_t n
  * `rows` (device, n rows of khip_shuffle_row_words words) stays the caller's.  Pushes the value
  * pipeline takes read the rows where they lie; every other push unpacks them into the handle's
  * staging columns and runs as a device batch.  Replaces khip_shuffle_unpack + khip_agg_push at the
- * reference's repartition source (S/StreamGroupByBuilderBase.java:101-103). */
+ * reference's repartition source (S/StreamGroupByBuilderBase.java:101-103).
+ * Time domains: TASK, and SUPPLIED when the shuffle carries KHIP_SHUFFLE_STREAM_TIME (the rows'
+ * stream-time word is the batch's `stream_time` column; KHIP_E_INVALID without it).  PARTITION is
+ * KHIP_E_UNSUPPORTED: received rows carry no source partition. */
 khip_status khip_agg_push_shuffled(khip_agg* agg, const khip_shuffle* s, const uint64_t* rows, int64_t n,
                                    khip_batch_stats* stats);
 
@@ -561,6 +589,12 @@ khip_status khip_comm_exchange_counts(khip_comm* c, const int64_t* send_counts, 
 khip_status khip_comm_alltoall(khip_comm* c, const uint64_t* send, const int64_t* send_counts,
                                uint64_t* recv, int64_t recv_capacity, const int64_t* recv_counts,
                                int32_t row_words);
+/* ABI 7.  The same all-to-all with the send side laid out by khip_shuffle_pack_v: peer p's rows
+ * are send_counts[p] rows at row send_offsets[p] of `send` (regions need not be adjacent).  The
+ * received rows are laid out by source rank, as khip_comm_alltoall lays them out. */
+khip_status khip_comm_alltoall_v(khip_comm* c, const uint64_t* send, const int64_t* send_counts,
+                                 const int64_t* send_offsets, uint64_t* recv, int64_t recv_capacity,
+                                 const int64_t* recv_counts, int32_t row_words);
 khip_status khip_comm_destroy(khip_comm* c);
 
 /* ------------------------------------------ deserialization (ksqldb-serde → device columns) */

@@ -20,7 +20,7 @@ _VARIANT = os.environ.get("KSQL_AMD_LIB_VARIANT", "")
 PRODUCT_LIB = os.path.join(REPO, "ksql_amd", "libksqldb_hip_%s.so" % _VARIANT if _VARIANT else "libksqldb_hip.so")
 ORACLE_LIB = os.path.join(REPO, "oracle", "liboracle.so")
 
-ABI_VERSION = 6  # include/ksqldb_hip.h KHIP_ABI_VERSION the structs below mirror
+ABI_VERSION = 7  # include/ksqldb_hip.h KHIP_ABI_VERSION the structs below mirror
 KHIP_OK = 0
 KHIP_E_BUFFER = -5
 
@@ -39,6 +39,7 @@ FLAG_TABLE_SOURCE = 16
 RETENTION_DEFAULT = -1
 EMIT = {"CHANGES": 0, "FINAL": 1}
 TIME = {"TASK": 0, "PARTITION": 1, "SUPPLIED": 2}  # ABI 5 stream-time domains
+SHUFFLE_STREAM_TIME = 1  # ABI 7 khip_shuffle_desc.flags
 NP_TYPE = {0: np.int32, 1: np.int64, 2: np.float64}
 
 i32, i64, u8p = C.c_int32, C.c_int64, C.POINTER(C.c_uint8)
@@ -209,6 +210,8 @@ PRODUCT_ONLY = {
     "shuffle_create": ([C.POINTER(ShuffleDesc), C.POINTER(_P)]),
     "shuffle_pack": ([_P, C.POINTER(Batch), _P, i64, C.POINTER(i64)]),
     "shuffle_unpack": ([_P, _P, i64, _P, _P, C.POINTER(_P), C.POINTER(_P)]),
+    "shuffle_pack_v": ([_P, C.POINTER(Batch), _P, i64, C.POINTER(i64), C.POINTER(i64)]),
+    "shuffle_unpack_stream_time": ([_P, _P, i64, _P]),
     "agg_push_shuffled": ([_P, _P, _P, i64, C.POINTER(BatchStats)]),
     "shuffle_sync": ([_P]),
     "shuffle_destroy": ([_P]),
@@ -216,6 +219,7 @@ PRODUCT_ONLY = {
     "comm_init": ([i32, i32, C.POINTER(C.c_uint8), i32, C.POINTER(_P)]),
     "comm_exchange_counts": ([_P, C.POINTER(i64), C.POINTER(i64)]),
     "comm_alltoall": ([_P, _P, C.POINTER(i64), _P, i64, C.POINTER(i64), i32]),
+    "comm_alltoall_v": ([_P, _P, C.POINTER(i64), C.POINTER(i64), _P, i64, C.POINTER(i64), i32]),
     "comm_destroy": ([_P]),
     "serde_create": ([C.POINTER(SerdeDesc), C.POINTER(_P)]),
     "serde_decode": ([_P, C.POINTER(RawBatch), C.POINTER(Batch), C.POINTER(i64)]),
@@ -257,6 +261,8 @@ class Lib:
             self.dll.khip_build_target.restype = C.c_char_p
             self.dll.khip_shuffle_row_words.restype = i32
             self.dll.khip_shuffle_row_words.argtypes = [_P]
+            self.dll.khip_shuffle_pack_capacity.restype = i64
+            self.dll.khip_shuffle_pack_capacity.argtypes = [_P, i64]
         else:
             self.dll.oracle_kafka_partition.argtypes = [_P, i64, i32, i32, _P]
             self.dll.oracle_kafka_partition.restype = None
@@ -738,11 +744,15 @@ class ShuffleHandle:
     """Repartition of a device batch by a value column (khip_shuffle_*), the device side of
     the repartition topic StreamGroupByBuilderBase inserts for a non-key GROUP BY."""
 
-    def __init__(self, lib, n_parts, key_col, col_types, device=0):
+    def __init__(self, lib, n_parts, key_col, col_types, device=0, stream_time=False):
+        """stream_time: KHIP_SHUFFLE_STREAM_TIME (ABI 7), the rows carry the batch's stream_time
+        column (the GLOBAL stream-time domain)."""
         self.lib = lib
         self.col_types = [TYPE[t] if isinstance(t, str) else t for t in col_types]
         self._ct = (i32 * len(self.col_types))(*self.col_types)
-        self.desc = ShuffleDesc(n_parts, key_col, len(self.col_types), self._ct, device, 0)
+        self.stream_time = bool(stream_time)
+        self.desc = ShuffleDesc(n_parts, key_col, len(self.col_types), self._ct, device,
+                                SHUFFLE_STREAM_TIME if stream_time else 0)
         self.n_parts = n_parts
         self.device = device
         self.h = C.c_void_p()
@@ -762,6 +772,32 @@ class ShuffleHandle:
             st = self.lib.shuffle_pack(self.h, C.byref(batch.struct), send.data_ptr(), send.shape[0], counts)
         self.lib.check(st, "shuffle_pack")
         return send, list(counts)
+
+    def pack_capacity(self, n_rows):
+        """Rows khip_shuffle_pack_v's send buffer needs for a batch of n_rows."""
+        return int(self.lib.dll.khip_shuffle_pack_capacity(self.h, n_rows))
+
+    def pack_v(self, batch, send=None):
+        """khip_shuffle_pack_v (ABI 7, one pass): returns (send, counts, offsets) — destination d's
+        rows are send[offsets[d] : offsets[d] + counts[d]]."""
+        import torch
+        n = int(batch.struct.n_rows)
+        need = max(self.pack_capacity(n), 1)
+        if send is None or send.shape[0] < need:
+            send = torch.empty((need, self.row_words), dtype=torch.int64, device=torch.device("cuda", self.device))
+        counts = (i64 * self.n_parts)()
+        offs = (i64 * self.n_parts)()
+        self.lib.check(self.lib.shuffle_pack_v(self.h, C.byref(batch.struct), send.data_ptr(), send.shape[0],
+                                               counts, offs), "shuffle_pack_v")
+        return send, list(counts), list(offs)
+
+    def unpack_stream_time(self, rows, n):
+        """The stream_time column of KHIP_SHUFFLE_STREAM_TIME rows (device int64 tensor)."""
+        import torch
+        st = torch.empty(max(n, 1), dtype=torch.int64, device=torch.device("cuda", self.device))
+        self.lib.check(self.lib.shuffle_unpack_stream_time(self.h, None if rows is None else rows.data_ptr(), n,
+                                                           st.data_ptr()), "shuffle_unpack_stream_time")
+        return st[:n]
 
     def unpack(self, rows, n, key_as_col=False):
         """Packed rows → (key, ts, cols, col_valid bitmaps) device tensors.  key_as_col: the
@@ -812,17 +848,31 @@ class Comm:
         idb = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
         lib.check(lib.comm_init(nranks, rank, idb, device, C.byref(self.h)), "comm_init")
 
-    def alltoall(self, send, send_counts, row_words):
-        """Two collective steps: exchange counts, then the rows.  Returns (recv, recv_counts)."""
+    def alltoall(self, send, send_counts, row_words, send_offsets=None):
+        """Two collective steps: exchange counts, then the rows (send_offsets: peer p's rows start
+        at row send_offsets[p], khip_shuffle_pack_v's layout; None: adjacent, by peer).  Returns
+        (recv, recv_counts); recv holds the rows by source rank."""
         import torch
         sc = (i64 * self.nranks)(*send_counts)
         rc = (i64 * self.nranks)()
         self.lib.check(self.lib.comm_exchange_counts(self.h, sc, rc), "comm_exchange_counts")
         recv = torch.empty((max(sum(rc), 1), row_words), dtype=torch.int64, device=torch.device("cuda", self.device))
         sp = None if send is None else send.data_ptr()
-        self.lib.check(self.lib.comm_alltoall(self.h, sp, sc, recv.data_ptr(), recv.shape[0], rc, row_words),
-                       "comm_alltoall")
+        if send_offsets is None:
+            self.lib.check(self.lib.comm_alltoall(self.h, sp, sc, recv.data_ptr(), recv.shape[0], rc, row_words),
+                           "comm_alltoall")
+        else:
+            so = (i64 * self.nranks)(*send_offsets)
+            self.lib.check(self.lib.comm_alltoall_v(self.h, sp, sc, so, recv.data_ptr(), recv.shape[0], rc, row_words),
+                           "comm_alltoall_v")
         return recv, list(rc)
+
+    def allgather_i64(self, x):
+        """One int64 from every rank (the count exchange with x sent to every peer)."""
+        sc = (i64 * self.nranks)(*([int(x)] * self.nranks))
+        rc = (i64 * self.nranks)()
+        self.lib.check(self.lib.comm_exchange_counts(self.h, sc, rc), "comm_exchange_counts")
+        return list(rc)
 
     def close(self):
         if self.h:

@@ -1177,10 +1177,14 @@ khip_status khip_agg_push_shuffled(khip_agg* a, const khip_shuffle* sh, const ui
     if (types[c] != a->col_types[c]) return fail(KHIP_E_INVALID, "the shuffle's column types are not the aggregation's");
   if (a->desc.key_type == KHIP_KEY_UTF8) return fail(KHIP_E_UNSUPPORTED, "shuffled rows carry an integer GROUP BY key");
   if (a->engine == 3) return fail(KHIP_E_STATE, "table-source aggregation: use khip_agg_push_table");
-  const int rw = 2 + nc;
+  if (a->desc.time_domain == KHIP_TIME_PARTITION)
+    return fail(KHIP_E_UNSUPPORTED, "KHIP_TIME_PARTITION: received rows carry no source partition");
+  const bool sup = a->desc.time_domain == KHIP_TIME_SUPPLIED;
+  const int rw = khip_shuffle_row_words(sh);
+  if (sup && rw != 3 + nc)
+    return fail(KHIP_E_INVALID, "KHIP_TIME_SUPPLIED: the shuffle carries no stream time (KHIP_SHUFFLE_STREAM_TIME)");
   DeviceGuard g(a->device);
-  if (n > 0 && n < (1LL << 31) && a->engine == 0 && a->desc.time_domain == KHIP_TIME_TASK &&
-      a->desc.emit != KHIP_EMIT_FINAL) {
+  if (n > 0 && n < (1LL << 31) && a->engine == 0 && a->desc.emit != KHIP_EMIT_FINAL) {
     khip_batch_stats s{};
     s.rows_in = n;
     a->st_before = a->host_stream_time;
@@ -1188,7 +1192,7 @@ khip_status khip_agg_push_shuffled(khip_agg* a, const khip_shuffle* sh, const ui
     a->lost.clear();
     int64_t tot[NPART] = {0};
     bool done = false;
-    KHIP_TRY(part_push_rows(a, n, RowsIn{rows, rw, 0, 0}, kc, tot, &done));
+    KHIP_TRY(part_push_rows(a, n, RowsIn{rows, rw, 0, 0}, kc, tot, &done, sup));
     if (done) {
       a->occ += tot[P_NEW];
       if (a->profile) {
@@ -1231,6 +1235,11 @@ khip_status khip_agg_push_shuffled(khip_agg* a, const khip_shuffle* sh, const ui
     KHIP_TRY(khip_shuffle_unpack(const_cast<khip_shuffle*>(sh), rows, n, a->st_keys.as<int64_t>(), a->st_ts.as<int64_t>(),
                                  cd, cv));
   khip_batch b{};
+  if (sup) {  // the GLOBAL stream time each row was routed with
+    KHIP_TRY(a->st_col.ensure((size_t)std::max<int64_t>(n, 1) * 8));
+    if (n > 0) KHIP_TRY(khip_shuffle_unpack_stream_time(const_cast<khip_shuffle*>(sh), rows, n, a->st_col.as<int64_t>()));
+    b.stream_time = a->st_col.as<int64_t>();
+  }
   b.mem = KHIP_MEM_DEVICE;
   b.n_rows = n;
   b.n_cols = nc;
@@ -1929,7 +1938,8 @@ khip_status khip_agg_destroy(khip_agg* a) {
   if (a->stream) hipStreamSynchronize(a->stream);
   DevBuf* bufs[] = {&a->table, &a->blockmax, &a->blockprefix, &a->partials, &a->resume, &a->counters,
                     &a->stream_time, &a->st_keys, &a->st_ts, &a->st_kv, &a->st_rv, &a->st_koff,
-                    &a->st_kbytes, &a->kid, &a->khash, &a->chg, &a->lostbuf, &a->lostctr};
+                    &a->st_kbytes, &a->kid, &a->khash, &a->chg, &a->lostbuf, &a->lostctr,
+                    &a->pst, &a->pst2, &a->st_col, &a->st_agg, &a->st_seen, &a->st_part};
   for (DevBuf* b : bufs) b->release();
   for (int c = 0; c < MAX_COLS; c++) {
     a->st_cols[c].release();

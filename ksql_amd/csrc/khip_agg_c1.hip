@@ -1382,6 +1382,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   uint32_t kor = 0u;
   int64_t x[U], k[U], v[U];
   uint32_t vm[ROWS ? U : 1];  // ROWS: the rows' validity words (low half)
+  int64_t rst[ROWS && ST ? U : 1];  // ROWS && ST: the rows' stream-time words (KHIP_SHUFFLE_STREAM_TIME)
   auto load_step = [&](int64_t i0) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -1401,6 +1402,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
           v[u] = (int64_t)r[ri.vword];
           vm[u] = (uint32_t)r[ri.rw - 1];
         }
+        if constexpr (ST) rst[u] = (int64_t)r[ri.rw - 2];
       } else {
         x[u] = ts[i];
         k[u] = keys[i];
@@ -1455,7 +1457,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #endif
       }
       if constexpr (ST) {
-        const int64_t ds = st_at[ii] - T0;
+        const int64_t ds = (ROWS ? rst[ROWS ? u : 0] : st_at[ii]) - T0;
         if (valid && (ds <= (int64_t)INT32_MIN || ds > (int64_t)INT32_MAX)) lfail = 1;
         tmx = valid && (int)ds > tmx ? (int)ds : tmx;
       } else {
@@ -2505,7 +2507,7 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
   if (val) {
     const C1VCol vc{rows ? nullptr : cols->data[vcol], rows ? nullptr : cols->valid[vcol], a->ap.col_type[vcol]};
     const RowsIn ri = rows ? *rows : RowsIn{};
-    auto sk = rows ? k_c1v_scatter<UV, C1_NT, false, true>
+    auto sk = rows ? (st_at ? k_c1v_scatter<UV, C1_NT, true, true> : k_c1v_scatter<UV, C1_NT, false, true>)
                    : (st_at ? k_c1v_scatter<UV, C1_NT, true, false> : k_c1v_scatter<UV, C1_NT, false, false>);
     const size_t lds = run_stage_lds(B, UV * C1_NT, 16, false);
     if (lds > 64 * 1024) hipFuncSetAttribute((const void*)sk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -524,7 +524,8 @@ struct RowsIn {
   int32_t rw, vword, vbit;
 };
 void shuffle_layout(const khip_shuffle* s, int* key_col, int* n_cols, const int32_t** types);
-khip_status part_push_rows(khip_agg* a, int64_t n, const RowsIn& ri, int key_col, int64_t* tot, bool* done);
+khip_status part_push_rows(khip_agg* a, int64_t n, const RowsIn& ri, int key_col, int64_t* tot, bool* done,
+                           bool supplied);
 khip_status part_compact(khip_agg* a, const HavingDev& h, std::vector<uint64_t>* rows, int64_t* count);
 bool part_having_count(khip_agg* a, int64_t* n);
 khip_status part_changes(khip_agg* a, std::vector<uint64_t>* rows, std::vector<uint8_t>* tomb, int64_t* count);

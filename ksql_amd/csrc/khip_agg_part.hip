@@ -3768,7 +3768,9 @@ static void agg_probe_report(DevBuf& b, int nb) {
 // Shuffled rows (khip_agg_push_shuffled) through the value pipeline, read where they lie; *done =
 // false when the pipeline does not apply or declined the push (the caller unpacks the rows and
 // runs the general path, which then skips the pipeline as after any decline).
-khip_status part_push_rows(khip_agg* a, int64_t n, const RowsIn& ri, int key_col, int64_t* tot, bool* done) {
+// supplied: KHIP_TIME_SUPPLIED, the rows carry their stream-time word (the scatter reads it there).
+khip_status part_push_rows(khip_agg* a, int64_t n, const RowsIn& ri, int key_col, int64_t* tot, bool* done,
+                           bool supplied) {
   PartState& s = a->part;
   *done = false;
   while (s.log2P < SPLIT_P_LOG2 && a->occ - s.closed_n > s.P * (int64_t)s.H_eff / 2) KHIP_TRY(part_split(a));
@@ -3779,7 +3781,9 @@ khip_status part_push_rows(khip_agg* a, int64_t n, const RowsIn& ri, int key_col
   r.vword = vcol == key_col ? 0 : 2 + vcol - (vcol > key_col ? 1 : 0);
   r.vbit = vcol;
   bool declined = false, retry_wide = false;
-  KHIP_TRY(c1_push(a, n, nullptr, nullptr, nullptr, nullptr, tot, &declined, nullptr, &retry_wide, nullptr, vcol, &r));
+  // st_at only selects the stream-time scatter here (never read as a column: ROWS reads the word)
+  const int64_t* st_flag = supplied ? (const int64_t*)ri.rows : nullptr;
+  KHIP_TRY(c1_push(a, n, nullptr, nullptr, nullptr, nullptr, tot, &declined, st_flag, &retry_wide, nullptr, vcol, &r));
   if (a->profile) (declined ? a->times.c1_declined : a->times.c1_pushes)++;
   if (declined) s.c1_skip = 8;
   *done = !declined;

@@ -11,7 +11,12 @@
 //   khip_comm_alltoall  grouped ncclSend/ncclRecv, one pair per peer over xGMI (every MI355X
 //                    pair has a direct link, so this is per-link bound, not a ring)
 //   k_shuf_pack1     one destination: the same rows in one pass (decoupled look-back, no histogram)
+//   k_shuf_packv     several destinations in one pass (ABI 7): each wave counts its contiguous run
+//                    of the tile per destination, the tile looks back over the earlier tiles'
+//                    per-destination counts, rows go to per-destination regions of the send buffer
+//   khip_comm_alltoall_v  the all-to-all over those regions
 //   k_shuf_unpack    packed rows → columnar batch (bitmaps built with __ballot)
+// KHIP_SHUFFLE_STREAM_TIME rows carry the batch's stream_time word before the validity word.
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -34,6 +39,7 @@ struct ShCols {
   const void* data[SH_MAX_COLS];
   const uint8_t* valid[SH_MAX_COLS];
   int32_t type[SH_MAX_COLS];
+  const int64_t* st;  // KHIP_SHUFFLE_STREAM_TIME: the batch's stream_time column (else null)
 };
 
 // Kafka's default partitioner over the KAFKA-format key (big-endian 4 / 8 bytes,
@@ -133,6 +139,7 @@ __global__ __launch_bounds__(SH_THREADS) void k_shuf_pack(ShCols c, int n_cols, 
         o[w++] = cv ? (uint64_t)sh_raw(c, cc, i) : 0ULL;
         vm |= (cv ? 1ULL : 0ULL) << cc;
       }
+      if (c.st) o[w++] = (uint64_t)c.st[i];
       o[w] = vm;
     }
     __syncthreads();
@@ -154,12 +161,56 @@ __global__ __launch_bounds__(SH_THREADS) void k_shuf_pack(ShCols c, int n_cols, 
 // last tile leaves the total in *total.
 constexpr uint64_t SH_AGG = 1ULL << 62, SH_INC = 2ULL << 62, SH_VAL = (1ULL << 62) - 1;
 
-template <int NC>  // the column count: the row is built in registers and leaves as 16-byte pairs
-__global__ __launch_bounds__(SH_THREADS) void k_shuf_pack1(ShCols c, int n_cols, int key_col,
+// Batch row i as its packed row, in registers: 2 + NC + ST words, padded to an even count so that
+// a row of an even word count leaves as 16-byte pairs.
+template <int NC, int ST>
+struct ShRow {
+  static constexpr int W = 2 + NC + ST;
+  static constexpr int RW = W + (W & 1);
+  uint64_t w[RW];
+};
+
+template <int NC, int ST>
+__device__ __forceinline__ void sh_build(const ShCols& c, int key_col, const int64_t* __restrict__ ts, int64_t i,
+                                         ShRow<NC, ST>& r) {
+#pragma unroll
+  for (int k = 0; k < ShRow<NC, ST>::RW; k++) r.w[k] = 0;
+  r.w[0] = (uint64_t)sh_raw(c, key_col, i);
+  r.w[1] = (uint64_t)ts[i];
+  uint64_t vm = 1ULL << key_col;  // the key column travels as word 0 only (its validity is implied)
+  int w = 2;
+#pragma unroll
+  for (int cc = 0; cc < NC; cc++) {
+    if (cc == key_col) continue;
+    const bool cv = bit_get(c.valid[cc], i);
+    const uint64_t x = cv ? (uint64_t)sh_raw(c, cc, i) : 0ULL;
+#pragma unroll
+    for (int k = 2; k < 2 + NC - 1; k++) r.w[k] = k == w ? x : r.w[k];  // no dynamic register index
+    w++;
+    vm |= (cv ? 1ULL : 0ULL) << cc;
+  }
+  if (ST) r.w[1 + NC] = (uint64_t)c.st[i];
+  r.w[1 + NC + ST] = vm;
+}
+
+template <int NC, int ST>
+__device__ __forceinline__ void sh_store(uint64_t* o, const ShRow<NC, ST>& r) {
+  constexpr int W = ShRow<NC, ST>::W;
+  if (W % 2 == 0) {
+#pragma unroll
+    for (int k = 0; k < W / 2; k++) ((ulonglong2*)o)[k] = make_ulonglong2(r.w[2 * k], r.w[2 * k + 1]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < W; k++) o[k] = r.w[k];
+  }
+}
+
+template <int NC, int ST>  // the column count and the stream-time word: the row is built in registers
+__global__ __launch_bounds__(SH_THREADS) void k_shuf_pack1(ShCols c, int key_col,
                                                            const uint8_t* __restrict__ rv, const int64_t* __restrict__ ts,
                                                            int64_t n, int64_t nT, uint64_t* __restrict__ status,
                                                            unsigned int* __restrict__ ticket, uint64_t* __restrict__ out,
-                                                           int row_words, unsigned long long* __restrict__ total) {
+                                                           unsigned long long* __restrict__ total) {
   constexpr int W = SH_THREADS / 64;
   __shared__ uint32_t wcnt[SH_ITEMS][W];
   __shared__ int64_t lbase;
@@ -211,34 +262,103 @@ __global__ __launch_bounds__(SH_THREADS) void k_shuf_pack1(ShCols c, int n_cols,
     const uint32_t rank = (uint32_t)__popcll(__ballot(v) & lt);
     if (!v) continue;
     const int64_t i = base + (int64_t)r * SH_THREADS + threadIdx.x;
-    constexpr int RW = 2 + NC + (NC & 1);  // words, padded to an even count (the row has 2 + NC)
-    uint64_t wd[RW];
-#pragma unroll
-    for (int k = 0; k < RW; k++) wd[k] = 0;
-    wd[0] = (uint64_t)sh_raw(c, key_col, i);
-    wd[1] = (uint64_t)ts[i];
-    uint64_t vm = 1ULL << key_col;  // the key column travels as word 0 only (its validity is implied)
-    int w = 2;
-#pragma unroll
-    for (int cc = 0; cc < NC; cc++) {
-      if (cc == key_col) continue;
-      const bool cv = bit_get(c.valid[cc], i);
-      const uint64_t x = cv ? (uint64_t)sh_raw(c, cc, i) : 0ULL;
-#pragma unroll
-      for (int k = 2; k < 2 + NC - 1; k++) wd[k] = k == w ? x : wd[k];  // no dynamic register index
-      w++;
-      vm |= (cv ? 1ULL : 0ULL) << cc;
-    }
-    wd[1 + NC] = vm;
-    uint64_t* o = out + (uint64_t)(lbase + wcnt[r][wave] + rank) * row_words;
-    if ((2 + NC) % 2 == 0) {
-#pragma unroll
-      for (int k = 0; k < RW / 2; k++) ((ulonglong2*)o)[k] = make_ulonglong2(wd[2 * k], wd[2 * k + 1]);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 2 + NC; k++) o[k] = wd[k];
-    }
+    ShRow<NC, ST> row;
+    sh_build<NC, ST>(c, key_col, ts, i, row);
+    sh_store<NC, ST>(out + (uint64_t)(lbase + wcnt[r][wave] + rank) * ShRow<NC, ST>::W, row);
   }
+}
+
+// Several destinations in one pass (khip_shuffle_pack_v).  Tiles of SH_TILE rows in ticket order;
+// wave w of a tile owns the contiguous run [w * SH_TILE / W, (w + 1) * SH_TILE / W) of it, so a
+// wave's rounds are in arrival order and it ranks its rows per destination against wave-private
+// running counts in LDS (a ballot per destination present in the round, no block barrier).  One
+// barrier, then thread d (< n_parts) prefixes the waves' counts of destination d, publishes the
+// tile's count and looks back over the earlier tiles' counts / inclusive prefixes of d (decoupled
+// look-back, status[tile * n_parts + d]).  The rows (re-read: L2) are written at
+// d * stride + (the tile's place in d) + (the wave's place) + rank; a row past its region's stride
+// is not written and raises *overflow (the host packs again with the exact stride, from the totals
+// the last tile leaves in totals[d]).
+template <int NC, int ST>
+__global__ __launch_bounds__(SH_THREADS) void k_shuf_packv(ShCols c, int key_col, const uint8_t* __restrict__ rv,
+                                                           const int64_t* __restrict__ ts, int64_t n, int64_t nT,
+                                                           int n_parts, uint64_t* __restrict__ status,
+                                                           unsigned int* __restrict__ ticket, uint64_t* __restrict__ out,
+                                                           int64_t stride, unsigned long long* __restrict__ totals,
+                                                           unsigned int* __restrict__ overflow) {
+  constexpr int W = SH_THREADS / 64;
+  constexpr int PER_WAVE = SH_TILE / W;  // 1024 rows: SH_ITEMS rounds of 64
+  __shared__ uint32_t wc[W][SH_MAX_PARTS];
+  __shared__ int64_t dbase[SH_MAX_PARTS];
+  __shared__ uint32_t ltile;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t lt = lane ? (~0ULL >> (64 - lane)) : 0ULL;
+  if (threadIdx.x == 0) ltile = atomicAdd(ticket, 1u);
+  for (int d = lane; d < n_parts; d += 64) wc[wave][d] = 0;  // the wave's own counts: no barrier needed
+  __syncthreads();
+  const int64_t tile = ltile;
+  const int64_t wbase = tile * SH_TILE + (int64_t)wave * PER_WAVE;
+  uint32_t rec[SH_ITEMS];  // destination << 16 | rank within the wave's rows of that destination
+#pragma unroll
+  for (int r = 0; r < SH_ITEMS; r++) {
+    const int64_t i = wbase + (int64_t)r * 64 + lane;
+    const bool v = i < n && ts[i] >= 0 && bit_get(rv, i) && bit_get(c.valid[key_col], i);
+    const int d = v ? (int)shuffle_dest(sh_raw(c, key_col, i), c.key_bytes, n_parts) : -1;
+    uint32_t x = 0xFFFFFFFFu;
+    uint64_t pending = __ballot(v);
+    while (pending) {  // one ballot per destination present in the round
+      const int dl = __shfl(d, __ffsll((unsigned long long)pending) - 1);
+      const uint64_t m = __ballot(d == dl);
+      const uint32_t b = wc[wave][dl];
+      if (d == dl) x = ((uint32_t)dl << 16) | (b + (uint32_t)__popcll(m & lt));
+      if (lane == 0) wc[wave][dl] = b + (uint32_t)__popcll(m);
+      pending &= ~m;
+    }
+    rec[r] = x;
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < n_parts; d += SH_THREADS) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const uint32_t e = wc[w][d];
+      wc[w][d] = acc;
+      acc += e;
+    }
+    uint64_t* sd = status + (uint64_t)tile * n_parts + d;
+    __hip_atomic_store(sd, (tile == 0 ? SH_INC : SH_AGG) | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t excl = 0;
+    for (int64_t j = tile - 1; j >= 0;) {
+      const uint64_t st = __hip_atomic_load(status + (uint64_t)j * n_parts + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!(st & ~SH_VAL)) {
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      excl += st & SH_VAL;
+      if (st & SH_INC) break;
+      j--;
+    }
+    if (tile > 0) __hip_atomic_store(sd, SH_INC | (excl + acc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    dbase[d] = (int64_t)excl;
+    if (tile == nT - 1) totals[d] = excl + acc;
+  }
+  __syncthreads();
+  bool over = false;
+#pragma unroll
+  for (int r = 0; r < SH_ITEMS; r++) {
+    const uint32_t x = rec[r];
+    if (x == 0xFFFFFFFFu) continue;
+    const int d = (int)(x >> 16);
+    const int64_t pos = dbase[d] + wc[wave][d] + (x & 0xFFFFu);
+    if (pos >= stride) {
+      over = true;
+      continue;
+    }
+    const int64_t i = wbase + (int64_t)r * 64 + lane;
+    ShRow<NC, ST> row;
+    sh_build<NC, ST>(c, key_col, ts, i, row);
+    sh_store<NC, ST>(out + ((uint64_t)d * (uint64_t)stride + (uint64_t)pos) * ShRow<NC, ST>::W, row);
+  }
+  if (__ballot(over) && lane == 0) atomicOr(overflow, 1u);
 }
 
 __global__ __launch_bounds__(256) void k_shuf_unpack(const uint64_t* __restrict__ rows, int64_t n, int n_cols,
@@ -267,6 +387,12 @@ __global__ __launch_bounds__(256) void k_shuf_unpack(const uint64_t* __restrict_
       for (int k = 0; k < nbytes; k++) col_valid[c][wbase / 8 + k] = (uint8_t)(b >> (8 * k));
     }
   }
+}
+
+__global__ __launch_bounds__(256) void k_shuf_unpack_st(const uint64_t* __restrict__ rows, int64_t n, int row_words,
+                                                        int64_t* __restrict__ st) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) st[i] = (int64_t)rows[i * row_words + row_words - 2];
 }
 
 }  // namespace khip
@@ -320,48 +446,48 @@ khip_status khip_shuffle_create(const khip_shuffle_desc* d, khip_shuffle** out) 
   return KHIP_OK;
 }
 
-int32_t khip_shuffle_row_words(const khip_shuffle* s) { return s ? 2 + s->desc.n_cols : 0; }
+static int shuffle_st(const khip_shuffle* s) { return (s->desc.flags & KHIP_SHUFFLE_STREAM_TIME) ? 1 : 0; }
 
-khip_status khip_shuffle_pack(khip_shuffle* s, const khip_batch* b, uint64_t* send, int64_t capacity, int64_t* counts) {
-  clear_error();
-  if (!s || !b || !counts) return fail(KHIP_E_INVALID, "null argument");
-  if (b->mem != KHIP_MEM_DEVICE) return fail(KHIP_E_INVALID, "pack needs a device batch");
+int32_t khip_shuffle_row_words(const khip_shuffle* s) { return s ? 2 + s->desc.n_cols + shuffle_st(s) : 0; }
+
+// The rows of each destination's region in khip_shuffle_pack_v: the even share plus 1/16 and a
+// tile (a uniform hash over n_parts destinations stays within a few standard deviations, ~sqrt(n/N)).
+static int64_t packv_stride(int64_t n, int N) { return ceil_div(n, N) + ceil_div(n, 16LL * N) + SH_TILE; }
+
+int64_t khip_shuffle_pack_capacity(const khip_shuffle* s, int64_t n) {
+  if (!s || n < 0) return 0;
+  const int N = s->desc.n_parts;
+  return N == 1 ? n : std::max<int64_t>(n, (int64_t)N * packv_stride(n, N));
+}
+
+static khip_status shuffle_cols(khip_shuffle* s, const khip_batch* b, ShCols* c) {
+  if (b->n_cols < s->desc.n_cols || !b->ts || !b->col_data) return fail(KHIP_E_INVALID, "batch shape");
+  if (shuffle_st(s) && !b->stream_time)
+    return fail(KHIP_E_INVALID, "KHIP_SHUFFLE_STREAM_TIME: the batch has no stream_time column");
+  *c = ShCols{};
+  for (int k = 0; k < s->desc.n_cols; k++) {
+    c->data[k] = b->col_data[k];
+    c->valid[k] = b->col_valid ? b->col_valid[k] : nullptr;
+    c->type[k] = s->types[k];
+  }
+  c->key_bytes = s->types[s->desc.key_col] == KHIP_TYPE_INT32 ? 4 : 8;
+  c->st = shuffle_st(s) ? b->stream_time : nullptr;
+  return KHIP_OK;
+}
+
+using Pack1Fn = void (*)(ShCols, int, const uint8_t*, const int64_t*, int64_t, int64_t, uint64_t*, unsigned int*,
+                         uint64_t*, unsigned long long*);
+using PackvFn = void (*)(ShCols, int, const uint8_t*, const int64_t*, int64_t, int64_t, int, uint64_t*,
+                         unsigned int*, uint64_t*, int64_t, unsigned long long*, unsigned int*);
+#define KHIP_SH_FNS(K, ST) {K<1, ST>, K<2, ST>, K<3, ST>, K<4, ST>, K<5, ST>, K<6, ST>, K<7, ST>, K<8, ST>}
+
+// The contiguous multi-destination pack: per-tile histograms, their column prefix, the stable
+// scatter (two reads of the source's key column).  Destination d's rows at the sum of counts[0..d).
+static khip_status pack_contiguous(khip_shuffle* s, const khip_batch* b, const ShCols& c, uint64_t* send,
+                                   int64_t capacity, int64_t* counts) {
   const int64_t n = b->n_rows;
   const int N = s->desc.n_parts;
-  if (n == 0) {
-    for (int d = 0; d < N; d++) counts[d] = 0;
-    return KHIP_OK;
-  }
-  if (b->n_cols < s->desc.n_cols || !b->ts || !b->col_data) return fail(KHIP_E_INVALID, "batch shape");
-  if (n >= (1LL << 31)) return fail(KHIP_E_UNSUPPORTED, "pack batch larger than 2^31 rows");
-  DeviceGuard g(s->desc.device);
-  ShCols c{};
-  for (int k = 0; k < s->desc.n_cols; k++) {
-    c.data[k] = b->col_data[k];
-    c.valid[k] = b->col_valid ? b->col_valid[k] : nullptr;
-    c.type[k] = s->types[k];
-  }
-  c.key_bytes = s->types[s->desc.key_col] == KHIP_TYPE_INT32 ? 4 : 8;
   const int64_t nT = ceil_div(n, SH_TILE);
-  if (N == 1 && send && capacity >= n) {  // one destination: a one-pass stable compaction
-    KHIP_TRY(s->R.ensure((size_t)(nT + 2) * 8));
-    uint64_t* status = s->R.as<uint64_t>();
-    unsigned int* ticket = (unsigned int*)(status + nT);
-    unsigned long long* total = (unsigned long long*)(status + nT + 1);
-    KHIP_TRY_HIP(hipMemsetAsync(status, 0, (size_t)(nT + 2) * 8, s->stream));
-    using PackFn = void (*)(ShCols, int, int, const uint8_t*, const int64_t*, int64_t, int64_t, uint64_t*, unsigned int*,
-                            uint64_t*, int, unsigned long long*);
-    static const PackFn k1[SH_MAX_COLS] = {k_shuf_pack1<1>, k_shuf_pack1<2>, k_shuf_pack1<3>, k_shuf_pack1<4>,
-                                           k_shuf_pack1<5>, k_shuf_pack1<6>, k_shuf_pack1<7>, k_shuf_pack1<8>};
-    hipLaunchKernelGGL(k1[s->desc.n_cols - 1], dim3(nT), dim3(SH_THREADS), 0, s->stream, c, s->desc.n_cols,
-                       s->desc.key_col, b->row_valid, b->ts, n, nT, status, ticket, send, 2 + s->desc.n_cols, total);
-    KHIP_TRY_HIP(hipGetLastError());
-    unsigned long long tot = 0;
-    KHIP_TRY_HIP(hipMemcpyAsync(&tot, total, 8, hipMemcpyDeviceToHost, s->stream));
-    KHIP_TRY_HIP(hipStreamSynchronize(s->stream));
-    counts[0] = (int64_t)tot;
-    return KHIP_OK;
-  }
   const int TC = (int)std::min<int64_t>(nT, 64);
   KHIP_TRY(s->hist.ensure((size_t)nT * N * 4));
   KHIP_TRY(s->csum.ensure((size_t)TC * N * 8));
@@ -388,9 +514,100 @@ khip_status khip_shuffle_pack(khip_shuffle* s, const khip_batch* b, uint64_t* se
   for (int d = 0; d < N; d++) counts[d] = R[d];
   if (tot > capacity || !send) return fail(KHIP_E_BUFFER, "send buffer too small");
   hipLaunchKernelGGL(k_shuf_pack, dim3(nT), dim3(SH_THREADS), 0, s->stream, c, s->desc.n_cols, s->desc.key_col,
-                     b->row_valid, b->ts, n, N, s->hist.as<uint32_t>(), send, 2 + s->desc.n_cols);
+                     b->row_valid, b->ts, n, N, s->hist.as<uint32_t>(), send, khip_shuffle_row_words(s));
   KHIP_TRY_HIP(hipGetLastError());
   KHIP_TRY_HIP(hipStreamSynchronize(s->stream));
+  return KHIP_OK;
+}
+
+khip_status khip_shuffle_pack(khip_shuffle* s, const khip_batch* b, uint64_t* send, int64_t capacity, int64_t* counts) {
+  clear_error();
+  if (!s || !b || !counts) return fail(KHIP_E_INVALID, "null argument");
+  if (b->mem != KHIP_MEM_DEVICE) return fail(KHIP_E_INVALID, "pack needs a device batch");
+  const int64_t n = b->n_rows;
+  const int N = s->desc.n_parts;
+  if (n == 0) {
+    for (int d = 0; d < N; d++) counts[d] = 0;
+    return KHIP_OK;
+  }
+  if (n >= (1LL << 31)) return fail(KHIP_E_UNSUPPORTED, "pack batch larger than 2^31 rows");
+  DeviceGuard g(s->desc.device);
+  ShCols c;
+  KHIP_TRY(shuffle_cols(s, b, &c));
+  const int64_t nT = ceil_div(n, SH_TILE);
+  if (N == 1 && send && capacity >= n) {  // one destination: a one-pass stable compaction
+    KHIP_TRY(s->R.ensure((size_t)(nT + 2) * 8));
+    uint64_t* status = s->R.as<uint64_t>();
+    unsigned int* ticket = (unsigned int*)(status + nT);
+    unsigned long long* total = (unsigned long long*)(status + nT + 1);
+    KHIP_TRY_HIP(hipMemsetAsync(status, 0, (size_t)(nT + 2) * 8, s->stream));
+    static const Pack1Fn k1[2][SH_MAX_COLS] = {KHIP_SH_FNS(k_shuf_pack1, 0), KHIP_SH_FNS(k_shuf_pack1, 1)};
+    hipLaunchKernelGGL(k1[shuffle_st(s)][s->desc.n_cols - 1], dim3(nT), dim3(SH_THREADS), 0, s->stream, c,
+                       s->desc.key_col, b->row_valid, b->ts, n, nT, status, ticket, send, total);
+    KHIP_TRY_HIP(hipGetLastError());
+    unsigned long long tot = 0;
+    KHIP_TRY_HIP(hipMemcpyAsync(&tot, total, 8, hipMemcpyDeviceToHost, s->stream));
+    KHIP_TRY_HIP(hipStreamSynchronize(s->stream));
+    counts[0] = (int64_t)tot;
+    return KHIP_OK;
+  }
+  return pack_contiguous(s, b, c, send, capacity, counts);
+}
+
+khip_status khip_shuffle_pack_v(khip_shuffle* s, const khip_batch* b, uint64_t* send, int64_t capacity, int64_t* counts,
+                                int64_t* offsets) {
+  clear_error();
+  if (!s || !b || !counts || !offsets) return fail(KHIP_E_INVALID, "null argument");
+  if (b->mem != KHIP_MEM_DEVICE) return fail(KHIP_E_INVALID, "pack needs a device batch");
+  const int64_t n = b->n_rows;
+  const int N = s->desc.n_parts;
+  if (n == 0) {
+    for (int d = 0; d < N; d++) counts[d] = offsets[d] = 0;
+    return KHIP_OK;
+  }
+  if (n >= (1LL << 31)) return fail(KHIP_E_UNSUPPORTED, "pack batch larger than 2^31 rows");
+  if (!send || capacity < khip_shuffle_pack_capacity(s, n))
+    return fail(KHIP_E_BUFFER, "send buffer smaller than khip_shuffle_pack_capacity");
+  if (N == 1) {
+    offsets[0] = 0;
+    return khip_shuffle_pack(s, b, send, capacity, counts);
+  }
+  DeviceGuard g(s->desc.device);
+  ShCols c;
+  KHIP_TRY(shuffle_cols(s, b, &c));
+  const int64_t nT = ceil_div(n, SH_TILE);
+  // status[nT * N] | ticket, overflow (one word) | totals[N]
+  KHIP_TRY(s->R.ensure((size_t)(nT * N + 1 + N) * 8));
+  uint64_t* status = s->R.as<uint64_t>();
+  unsigned int* ticket = (unsigned int*)(status + nT * N);
+  unsigned int* overflow = ticket + 1;
+  unsigned long long* totals = (unsigned long long*)(status + nT * N + 1);
+  static const PackvFn kv[2][SH_MAX_COLS] = {KHIP_SH_FNS(k_shuf_packv, 0), KHIP_SH_FNS(k_shuf_packv, 1)};
+  int64_t stride = packv_stride(n, N);
+  for (int attempt = 0; attempt < 2; attempt++) {
+    KHIP_TRY_HIP(hipMemsetAsync(status, 0, (size_t)(nT * N + 1 + N) * 8, s->stream));
+    hipLaunchKernelGGL(kv[shuffle_st(s)][s->desc.n_cols - 1], dim3(nT), dim3(SH_THREADS), 0, s->stream, c,
+                       s->desc.key_col, b->row_valid, b->ts, n, nT, N, status, ticket, send, stride, totals, overflow);
+    KHIP_TRY_HIP(hipGetLastError());
+    std::vector<uint64_t> tail((size_t)N + 1);
+    KHIP_TRY_HIP(hipMemcpyAsync(tail.data(), status + nT * N, (size_t)(N + 1) * 8, hipMemcpyDeviceToHost, s->stream));
+    KHIP_TRY_HIP(hipStreamSynchronize(s->stream));
+    const bool over = (tail[0] >> 32) != 0;
+    int64_t mx = 0;
+    for (int d = 0; d < N; d++) {
+      counts[d] = (int64_t)tail[1 + d];
+      offsets[d] = (int64_t)d * stride;
+      mx = std::max(mx, counts[d]);
+    }
+    if (!over) return KHIP_OK;
+    if ((int64_t)N * mx > capacity) break;  // a skewed batch: the exact regions do not fit
+    stride = mx;                            // the exact stride always fits the largest destination
+  }
+  KHIP_TRY(pack_contiguous(s, b, c, send, capacity, counts));
+  for (int64_t d = 0, o = 0; d < N; d++) {
+    offsets[d] = o;
+    o += counts[d];
+  }
   return KHIP_OK;
 }
 
@@ -411,8 +628,22 @@ khip_status khip_shuffle_unpack(khip_shuffle* s, const uint64_t* rows, int64_t n
   }
   KHIP_TRY(s->ptrs.ensure(host.size() * 8));
   KHIP_TRY_HIP(hipMemcpyAsync(s->ptrs.p, host.data(), host.size() * 8, hipMemcpyHostToDevice, s->stream));
-  hipLaunchKernelGGL(k_shuf_unpack, dim3(ceil_div(n, 256)), dim3(256), 0, s->stream, rows, n, nc, s->desc.key_col, 2 + nc, t, key, ts,
-                     (void* const*)s->ptrs.p, (uint8_t* const*)(s->ptrs.as<uint64_t>() + SH_MAX_COLS));
+  hipLaunchKernelGGL(k_shuf_unpack, dim3(ceil_div(n, 256)), dim3(256), 0, s->stream, rows, n, nc, s->desc.key_col,
+                     khip_shuffle_row_words(s), t, key, ts, (void* const*)s->ptrs.p,
+                     (uint8_t* const*)(s->ptrs.as<uint64_t>() + SH_MAX_COLS));
+  KHIP_TRY_HIP(hipGetLastError());
+  KHIP_TRY_HIP(hipStreamSynchronize(s->stream));
+  return KHIP_OK;
+}
+
+khip_status khip_shuffle_unpack_stream_time(khip_shuffle* s, const uint64_t* rows, int64_t n, int64_t* stream_time) {
+  clear_error();
+  if (!s || (n > 0 && (!rows || !stream_time))) return fail(KHIP_E_INVALID, "null argument");
+  if (!shuffle_st(s)) return fail(KHIP_E_INVALID, "the shuffle carries no stream time (KHIP_SHUFFLE_STREAM_TIME)");
+  if (n == 0) return KHIP_OK;
+  DeviceGuard g(s->desc.device);
+  hipLaunchKernelGGL(k_shuf_unpack_st, dim3(ceil_div(n, 256)), dim3(256), 0, s->stream, rows, n,
+                     khip_shuffle_row_words(s), stream_time);
   KHIP_TRY_HIP(hipGetLastError());
   KHIP_TRY_HIP(hipStreamSynchronize(s->stream));
   return KHIP_OK;
@@ -544,6 +775,34 @@ khip_status khip_comm_alltoall(khip_comm* c, const uint64_t* send, const int64_t
       ge.note(ncclRecv(recv + ro * row_words, (size_t)recv_counts[p] * row_words, ncclUint64, p, c->comm, c->stream),
               "ncclRecv");
     so += send_counts[p];
+    ro += recv_counts[p];
+  }
+  KHIP_TRY(ge.finish(ncclGroupEnd()));
+  KHIP_TRY_HIP(hipStreamSynchronize(c->stream));
+  return KHIP_OK;
+}
+
+khip_status khip_comm_alltoall_v(khip_comm* c, const uint64_t* send, const int64_t* send_counts,
+                                 const int64_t* send_offsets, uint64_t* recv, int64_t recv_capacity,
+                                 const int64_t* recv_counts, int32_t row_words) {
+  clear_error();
+  if (!c || !send_counts || !send_offsets || !recv_counts || row_words < 1) return fail(KHIP_E_INVALID, "null argument");
+  DeviceGuard g(c->device);
+  const int N = c->nranks;
+  int64_t tot = 0;
+  for (int p = 0; p < N; p++) tot += recv_counts[p];
+  if (tot > recv_capacity) return fail(KHIP_E_BUFFER, "receive buffer smaller than the exchanged counts");
+  int64_t ro = 0;
+  KHIP_TRY_NCCL(ncclGroupStart());
+  GroupErr ge;
+  for (int p = 0; p < N; p++) {
+    if (send_counts[p])
+      ge.note(ncclSend(send + send_offsets[p] * row_words, (size_t)send_counts[p] * row_words, ncclUint64, p, c->comm,
+                       c->stream),
+              "ncclSend");
+    if (recv_counts[p])
+      ge.note(ncclRecv(recv + ro * row_words, (size_t)recv_counts[p] * row_words, ncclUint64, p, c->comm, c->stream),
+              "ncclRecv");
     ro += recv_counts[p];
   }
   KHIP_TRY(ge.finish(ncclGroupEnd()));

@@ -5,8 +5,10 @@ Mirrors what StreamGroupByBuilderBase.build does per task
 → sink "<ctx>-repartition" → source, i.e. the shuffle of SURVEY.md §8(e)) with the device
 pieces of libksqldb_hip.so:
 
-    khip_shuffle_pack      re-key by the group-by column, route with Kafka's default
-                           partitioner (murmur2 of the KAFKA-format key), stable per source
+    khip_shuffle_pack[_v]  re-key by the group-by column, route with Kafka's default
+                           partitioner (murmur2 of the KAFKA-format key), stable per source;
+                           one destination: a one-pass compaction; several: the one-pass
+                           region pack (ABI 7), each destination's rows at its own offset
     khip_comm_*            RCCL count exchange + grouped send/recv all-to-all over xGMI
                            (skipped at one task: the destination is this task)
     khip_shuffle_unpack    back to a columnar device batch keyed by the new key
@@ -16,6 +18,14 @@ records from source rank 0 first, then rank 1, ..., each source's records in arr
 goes straight into the aggregation with khip_agg_push_shuffled (Repartition.push_into: the rows
 are read where they lie, no columnar copy).
 
+GLOBAL stream time (`global_time=True`, ABI 7 KHIP_SHUFFLE_STREAM_TIME): the owner tasks late-drop
+against the stream time ONE task over the whole stream would have observed — what the reference's
+TopologyTestDriver does (one task per query, ksqldb-functional-tests/.../TestExecutorUtil.java:
+123-126).  Each rank holds a contiguous chunk of the global arrival order; before routing, it scans
+its chunk's per-row stream time (khip_stream_time_scan) seeded with max(the global stream time
+before the batch, the chunk maxima of the ranks before it) — an all-gather of one int64 per rank —
+and the rows travel with it; the owner's aggregation is KHIP_TIME_SUPPLIED.
+
 The exchange is pluggable: `abi.Comm` (RCCL over xGMI, one process per GPU, the production
 path) or `GlooExchange` (any torch.distributed process group, rows staged through host memory:
 the CPU tests, and several ranks sharing one GPU, where RCCL refuses duplicate devices).
@@ -24,8 +34,8 @@ from . import abi
 
 
 class GlooExchange:
-    """The same two collective steps as abi.Comm.alltoall (counts, then rows laid out by source
-    rank) over a torch.distributed group, through host memory."""
+    """The same collective steps as abi.Comm (counts, then rows laid out by source rank; one
+    int64 from every rank) over a torch.distributed group, through host memory."""
 
     def __init__(self, group=None):
         import torch.distributed as dist
@@ -33,7 +43,7 @@ class GlooExchange:
         self.group = group
         self.nranks = dist.get_world_size(group)
 
-    def alltoall(self, send, send_counts, row_words):
+    def alltoall(self, send, send_counts, row_words, send_offsets=None):
         import torch
         dist = self.dist
         if len(send_counts) != self.nranks:
@@ -44,8 +54,12 @@ class GlooExchange:
         rcounts = [int(x) for x in rc.tolist()]
         n_send = int(sc.sum())
         dev = send.device if send is not None else torch.device("cpu")
-        hsend = (send[:n_send].to("cpu") if send is not None and n_send
-                 else torch.empty((0, row_words), dtype=torch.int64)).contiguous()
+        if send is None or n_send == 0:
+            hsend = torch.empty((0, row_words), dtype=torch.int64)
+        elif send_offsets is None:
+            hsend = send[:n_send].to("cpu").contiguous()
+        else:  # khip_shuffle_pack_v's regions, peer by peer
+            hsend = torch.cat([send[o:o + c].to("cpu") for o, c in zip(send_offsets, send_counts)]).contiguous()
         hrecv = torch.empty((sum(rcounts), row_words), dtype=torch.int64)
         dist.all_to_all_single(hrecv.view(-1), hsend.view(-1), [c * row_words for c in rcounts],
                                [int(c) * row_words for c in send_counts], group=self.group)
@@ -53,48 +67,87 @@ class GlooExchange:
             hrecv = torch.zeros((1, row_words), dtype=torch.int64)
         return hrecv.to(dev), rcounts
 
+    def allgather_i64(self, x):
+        import torch
+        out = torch.zeros(self.nranks, dtype=torch.int64)
+        self.dist.all_gather_into_tensor(out, torch.tensor([int(x)], dtype=torch.int64), group=self.group)
+        return [int(v) for v in out.tolist()]
+
+
+class _StreamTimeBatch:
+    """The caller's device batch with a stream_time column attached (a copy of its struct)."""
+
+    def __init__(self, batch, st):
+        self.struct = abi.Batch.from_buffer_copy(batch.struct)
+        self.struct.stream_time = st.data_ptr()
+        self._keep = [batch, st]
+
 
 class Repartition:
-    def __init__(self, lib, key_col, col_types, rank=0, world=1, comm=None, device=0):
+    def __init__(self, lib, key_col, col_types, rank=0, world=1, comm=None, device=0, global_time=False):
         if world > 1 and comm is None:
             raise ValueError("world > 1 needs an exchange (abi.Comm over RCCL, or GlooExchange)")
         self.world = world
         self.rank = rank
         self.comm = comm
-        self.shuffle = abi.ShuffleHandle(lib, world, key_col, col_types, device)
+        self.global_time = bool(global_time)
+        self.shuffle = abi.ShuffleHandle(lib, world, key_col, col_types, device, stream_time=global_time)
         self.last_counts = None
+        self.gst = -1  # global_time: the stream time over every rank's rows so far
         self._send = None
 
-    def exchange(self, batch):
-        """Device batch (source partition) → (this task's received rows [n, row_words], n)."""
+    def stream_times(self, scan, batch):
+        """global_time: the GLOBAL stream time observed at each row of this rank's chunk (device
+        int64 tensor).  `scan` is any product AggHandle (khip_stream_time_scan only uses its
+        scratch)."""
         import torch
+        n = int(batch.struct.n_rows)
+        out = torch.empty(max(n, 1), dtype=torch.int64, device=torch.device("cuda", self.shuffle.device))
+        _, mx = scan.stream_time_scan(batch, -1, out)
+        maxima = self.comm.allgather_i64(mx) if self.world > 1 else [mx]
+        seed = max([self.gst] + maxima[:self.rank])
+        if seed > -1:
+            scan.stream_time_scan(batch, seed, out)
+        self.gst = max([self.gst] + maxima)
+        return out[:n]
+
+    def exchange(self, batch, scan=None):
+        """Device batch (source partition) → (this task's received rows [n, row_words], n).
+        The rows are only valid until the next exchange: at one task they ARE the send buffer,
+        which the next call reuses (copy them to keep them).  global_time needs `scan`."""
+        import torch
+        if self.global_time:
+            if scan is None:
+                raise ValueError("global_time: exchange needs a scan handle (an AggHandle)")
+            batch = _StreamTimeBatch(batch, self.stream_times(scan, batch))
         n = max(int(batch.struct.n_rows), 1)
-        # a send buffer for every row the batch holds, kept across calls: one pack launch
-        # sequence per call (no count-only pass to size the buffer)
-        if self._send is None or self._send.shape[0] < n:
-            self._send = torch.empty((n, self.shuffle.row_words), dtype=torch.int64,
-                                     device=torch.device("cuda", self.shuffle.device))
-        send, counts = self.shuffle.pack(batch, send=self._send)
         if self.world == 1:
+            # a send buffer for every row the batch holds, kept across calls: one pack launch
+            # sequence per call (no count-only pass to size the buffer)
+            if self._send is None or self._send.shape[0] < n:
+                self._send = torch.empty((n, self.shuffle.row_words), dtype=torch.int64,
+                                         device=torch.device("cuda", self.shuffle.device))
+            send, counts = self.shuffle.pack(batch, send=self._send)
             recv, rcounts = send, counts
         else:
-            recv, rcounts = self.comm.alltoall(send, counts, self.shuffle.row_words)
+            self._send, counts, offs = self.shuffle.pack_v(batch, send=self._send)
+            recv, rcounts = self.comm.alltoall(self._send, counts, self.shuffle.row_words, send_offsets=offs)
         self.last_counts = (counts, rcounts)
         return recv, int(sum(rcounts))
 
     def push_into(self, agg, batch):
         """The GROUP BY's aggregation reads this task's received rows where they lie
-        (khip_agg_push_shuffled); returns its batch statistics."""
-        recv, n = self.exchange(batch)
+        (khip_agg_push_shuffled); returns its batch statistics.  global_time: `agg` is the
+        KHIP_TIME_SUPPLIED owner task and also scans this rank's chunk."""
+        recv, n = self.exchange(batch, scan=agg if self.global_time else None)
         return agg.push_shuffled(self.shuffle, recv, n)
 
-    def __call__(self, batch):
+    def __call__(self, batch, scan=None):
         """Device batch (source partition) → (DeviceBatch of this task's rows, tensors)."""
-        recv, n = self.exchange(batch)
+        recv, n = self.exchange(batch, scan=scan)
         key, ts, cols, valid = self.shuffle.unpack(recv, n)
-        out = abi.DeviceBatch(ts, keys=key, cols=cols, col_valid=valid)
-        out._keep.append(recv)
-        return out
+        st = self.shuffle.unpack_stream_time(recv, n) if self.global_time else None
+        return abi.DeviceBatch(ts, keys=key, cols=cols, col_valid=valid, stream_time=st)
 
     def close(self):
         self.shuffle.close()

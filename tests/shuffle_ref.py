@@ -17,14 +17,16 @@ def _raw_i64(col):
     return col.astype(np.int64)
 
 
-def expected_pack(orc, key_col, cols, col_valid, row_valid, ts, n_parts):
-    """khip_shuffle_pack restated: (rows int64 [m, 2+nc], counts per destination)."""
+def expected_pack(orc, key_col, cols, col_valid, row_valid, ts, n_parts, stream_time=None):
+    """khip_shuffle_pack restated: (rows int64 [m, 2+nc], counts per destination).  stream_time
+    (KHIP_SHUFFLE_STREAM_TIME): one more word, before the validity word."""
     n = len(ts)
     width = 4 if cols[key_col].dtype == np.int32 else 8
     ok = row_valid & col_valid[key_col] & (ts >= 0)
     dest = kafka_partition(orc, cols[key_col], width, n_parts)
     nc = len(cols)
-    words = np.zeros((n, 2 + nc), np.int64)
+    st = 0 if stream_time is None else 1
+    words = np.zeros((n, 2 + nc + st), np.int64)
     words[:, 0] = cols[key_col].astype(np.int64)
     words[:, 1] = ts
     vm = np.zeros(n, np.int64)
@@ -34,6 +36,9 @@ def expected_pack(orc, key_col, cols, col_valid, row_valid, ts, n_parts):
         if c == key_col:
             continue
         words[:, w] = np.where(col_valid[c], _raw_i64(cols[c]), 0)
+        w += 1
+    if st:
+        words[:, w] = stream_time
         w += 1
     words[:, w] = vm
     rows, counts = [], []

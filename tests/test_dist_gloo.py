@@ -184,3 +184,51 @@ def test_repartition_exchange_across_ranks():
     np.testing.assert_array_equal(cn[o], ref["values"][1])
     np.testing.assert_array_equal(rt[o], ref["rowtime"])
     assert cn.sum() == WORLD * SH_N
+
+
+# ------------------------------------------------------------------ ABI 7 exchange shapes
+# khip_shuffle_pack_v leaves each destination's rows in its own region of the send buffer (gaps
+# between regions); the exchange sends region p to peer p (send_offsets), and the GLOBAL stream
+# time needs one int64 from every rank (allgather_i64).
+
+def _regions_worker(rank, port, q):
+    from ksql_amd.repartition import GlooExchange
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        ex = GlooExchange()
+        rw = 3
+        counts = [3 + rank, 5 - rank]
+        offs = [2, 20]  # regions with gaps before, between and after them
+        send = torch.full((30, rw), -1, dtype=torch.int64)
+        for p in range(WORLD):
+            for i in range(counts[p]):
+                send[offs[p] + i] = torch.tensor([rank, p, i])
+        recv, rc = ex.alltoall(send, counts, rw, send_offsets=offs)
+        got = ex.allgather_i64(1000 + 7 * rank)
+        out = {"recv": recv[:sum(rc)].numpy(), "rc": rc, "gathered": got}
+        res = [None] * WORLD
+        dist.all_gather_object(res, out)
+        if rank == 0:
+            q.put(res)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_regions_and_allgather():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_regions_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for d in range(WORLD):
+        exp = [[s, d, i] for s in range(WORLD) for i in range([3 + s, 5 - s][d])]
+        assert res[d]["rc"] == [[3 + s, 5 - s][d] for s in range(WORLD)]
+        np.testing.assert_array_equal(res[d]["recv"], np.array(exp, np.int64))
+        assert res[d]["gathered"] == [1000 + 7 * r for r in range(WORLD)]

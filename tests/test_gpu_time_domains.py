@@ -318,3 +318,122 @@ def test_supplied_domain_two_processes_gloo_one_gpu(orc):
     assert sum(r[1] for r in res) == olate > 0
     assert_snap_equal(_union([r[0] for r in res], gd), o.snapshot(), gd)
     o.close()
+
+
+# ---- GLOBAL stream time through the device repartition (ABI 7 KHIP_SHUFFLE_STREAM_TIME) ---------
+# The rows' GROUP BY column is a value column (a non-key GROUP BY): Repartition scans each rank's
+# arrival chunk, packs the rows with their stream time, exchanges them and the owner's
+# KHIP_TIME_SUPPLIED aggregation reads them where they lie (khip_agg_push_shuffled).
+
+SH_AGGS = [("COUNT_STAR", -1), ("SUM", 1), ("MAX", 1)]
+
+
+def _sh_desc(domain="SUPPLIED", grace=1000, flags=abi.FLAG_PROFILE):
+    return abi.make_agg_desc(window_kind="TUMBLING", size_ms=5000, grace_ms=grace, col_types=["INT64", "INT64"],
+                             aggs=SH_AGGS, flags=flags, capacity_hint=1 << 20, time_domain=domain)
+
+
+def _oracle_one_task(orc, stream, grace=1000):
+    o = abi.AggHandle(orc, _sh_desc("TASK", grace, 0))
+    late = sum(o.push(abi.HostBatch(t, keys=k, cols=[k, v]))["windows_late"] for k, t, v in stream)
+    s = o.snapshot()
+    o.close()
+    return s, late
+
+
+@pytest.mark.parametrize("late_heavy", [True, False])
+def test_supplied_through_repartition_one_rank(prod, orc, late_heavy):
+    """One rank: the GLOBAL stream time is the task's own; the rows' stream-time words must give
+    exactly one oracle task (late-free data: the value pipeline reads them in place)."""
+    import torch
+    from ksql_amd.repartition import Repartition
+    rng = np.random.default_rng(31 + late_heavy)
+    stream = _global_stream(rng, nb=4, per=60_000, keys=4000)
+    if not late_heavy:
+        stream = [(k, np.sort(t), v) for k, t, v in stream]
+    grace = 1000 if late_heavy else 10**9
+    h = abi.AggHandle(prod, _sh_desc(grace=grace))
+    rp = Repartition(prod, 0, ["INT64", "INT64"], global_time=True)
+    late = 0
+    for k, t, v in stream:
+        src = abi.DeviceBatch(torch.from_numpy(t).cuda(), cols=[torch.from_numpy(k).cuda(), torch.from_numpy(v).cuda()])
+        late += rp.push_into(h, src)["windows_late"]
+    exp, olate = _oracle_one_task(orc, stream, grace)
+    assert late == olate and (late > 0) == late_heavy
+    assert_snap_equal(h.snapshot(), exp, _sh_desc())
+    if not late_heavy:
+        assert h.kernel_times()["c1_pushes"] == len(stream)
+    rp.close()
+    h.close()
+
+
+def test_push_shuffled_domain_errors(prod):
+    sh = abi.ShuffleHandle(prod, 1, 0, ["INT64", "INT64"])
+    import torch
+    rows = torch.zeros((4, sh.row_words), dtype=torch.int64, device="cuda")
+    h = abi.AggHandle(prod, _sh_desc("SUPPLIED"))
+    with pytest.raises(abi.KsqlHipError, match="KHIP_SHUFFLE_STREAM_TIME"):
+        h.push_shuffled(sh, rows, 4)
+    h.close()
+    h = abi.AggHandle(prod, abi.make_agg_desc(window_kind="TUMBLING", size_ms=5000, col_types=["INT64", "INT64"],
+                                              aggs=SH_AGGS, time_domain="PARTITION", n_partitions=2))
+    with pytest.raises(abi.KsqlHipError, match="no source partition"):
+        h.push_shuffled(sh, rows, 4)
+    h.close()
+    sh.close()
+
+
+def _gloo_rank_repartition(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from ksql_amd.repartition import GlooExchange, Repartition
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        prod = abi.load_product()
+        h = abi.AggHandle(prod, _sh_desc())
+        rp = Repartition(prod, 0, ["INT64", "INT64"], rank=rank, world=world, comm=GlooExchange(), global_time=True)
+        rng = np.random.default_rng(21)  # every rank generates the same global stream, keeps its chunk
+        stream = _global_stream(rng, nb=4, per=60_000, keys=4000)
+        late = 0
+        for k, t, v in stream:
+            n = len(t)
+            lo, hi = n * rank // world, n * (rank + 1) // world
+            src = abi.DeviceBatch(torch.from_numpy(t[lo:hi]).cuda(),
+                                  cols=[torch.from_numpy(k[lo:hi]).cuda(), torch.from_numpy(v[lo:hi]).cuda()])
+            late += rp.push_into(h, src)["windows_late"]
+        s = h.snapshot()
+        res = [None] * world
+        dist.all_gather_object(res, (s, late, rp.gst))
+        h.close()
+        rp.close()
+        if rank == 0:
+            q.put(res)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_supplied_through_repartition_two_processes_gloo(orc):
+    """Two source ranks on this GPU: rows routed by Kafka's partitioner of the GROUP BY column
+    through the product pack_v / exchange / push_shuffled with their GLOBAL stream time; the owners'
+    tables together equal ONE oracle task over the whole late-heavy stream, late drops included."""
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_rank_repartition, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(21)
+    stream = _global_stream(rng, nb=4, per=60_000, keys=4000)
+    exp, olate = _oracle_one_task(orc, stream)
+    assert sum(r[1] for r in res) == olate > 0
+    assert res[0][2] == res[1][2] == max(int(t.max()) for _, t, _ in stream)
+    gd = _sh_desc()
+    assert_snap_equal(_union([r[0] for r in res], gd), exp, gd)

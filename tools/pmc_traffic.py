@@ -1,23 +1,24 @@
 #!/usr/bin/env python3
-"""HBM traffic per bench step from rocprofv3 FETCH_SIZE / WRITE_SIZE passes (separate runs).
+"""HBM traffic per bench step from rocprofv3 counter passes (separate runs of the same command).
 
 The profiled command is `bench.py --config <leg> --steps S --warmup W --no-cpu-baseline
---no-extras`: every library dispatch of the run belongs to one of the S + W identical steps
-(the generators and the copy-rate probe are torch kernels and are excluded by name), so
-bytes per step = sum over the library's dispatches / (S + W).
+--no-extras`: every library dispatch of the run belongs to one of the S + W identical steps (the
+generators and the copy-rate probe are torch kernels and are excluded by name), so bytes per step
+= sum over the library's dispatches / (S + W).
 
-Units and the gfx950 correction (MI355X_MICROARCH.md:297-299, HBM / rocprofv3): FETCH_SIZE and
-WRITE_SIZE are in KB; FETCH_SIZE reports 1/2 of the bytes of a wide coalesced streaming read
-(16 B per lane), so the reads of the STREAMING kernels below are doubled.  Every other kernel's
-reads (random gathers: hash-probe slots, dense-index cells, dictionary / source-table rows, serde
-byte loads) are reported raw, labelled "gather": the correction is not established for them, and
-FETCH_SIZE counts L2 → fabric requests, Infinity-Cache (MALL) hits included, so their figure is
-L2-miss bytes, not HBM bytes.  WRITE_SIZE is taken as reported.  Where the run contains
-k_part_hist, whose reads are exactly 16 B x records (key + ts) per step, the measured factor
-(true bytes / raw FETCH bytes, per step) is reported beside the 2.0 as a check.
+Read bytes are MEASURED per dispatch from the L2's memory-side read requests by size, collected in
+one pass: TCC_EA0_RDREQ_32B_sum x 32 + TCC_EA0_RDREQ_64B_sum x 64 + TCC_EA0_RDREQ_128B_sum x 128.
+No kernel list decides a correction.  The derived FETCH_SIZE (its own pass) is kept beside it as
+`fetch_size_raw`: on gfx950 FETCH_SIZE tallies a 128-B request at 64 B (MI355X_MICROARCH.md, HBM /
+rocprofv3: "FETCH_SIZE reports exactly 1/2 of the bytes of a wide coalesced streaming read"), so
+for a streaming kernel read_bytes ≈ 2 x fetch_size_raw, for a gather of 32/64-B lines ≈ 1 x.
+Round 4 applied the x 2 from a hand-kept list of kernel names, which went stale as kernels were
+added; the size-classed count cannot.  Request bytes count L2 -> fabric
+traffic, Infinity-Cache (MALL) hits included: for a gather whose table is MALL-resident they are
+L2-miss bytes, not HBM bytes.  WRITE_SIZE (own pass) is taken as reported.
 
-usage: pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv> <records>
-                      <steps incl. warmup> <out json> <config key>
+usage: pmc_traffic.py <rdreq csv> <fetch csv | -> <write csv> <records> <steps incl. warmup>
+                      <out json> <config key>
 """
 import csv
 import json
@@ -34,16 +35,8 @@ def kname(raw):
 # library kernels that run outside the timed step of a leg (the join's table build)
 OUTSIDE_STEP = ("k_upsert_claim", "k_upsert_finalize", "k_upsert_apply", "k_table_rehash", "k_count_live")
 
-
-# wide coalesced streaming readers (16-B-per-lane loads of contiguous runs): FETCH_SIZE x 2
-STREAMING = ("k_part_hist", "k_part_scatter", "k_part_scatter_r8", "k_part_scatter_w", "k_part_refine", "k_part_refine_r8", "k_part_merge", "k_part_merge_c1", "k_part_agg",
-             "k_part_colsum", "k_part_colbase", "k_part_colprefix", "k_part_pscan", "k_scan_blocks", "k_part_rows",
-             "k_part_chg", "k_part_stats", "k_part_wrange", "k_part_commit", "k_part_reset", "k_part_tsrange",
-             "k_shuf_hist", "k_shuf_pack", "k_shuf_unpack", "k_shuf_colsum", "k_shuf_prefix", "k_init_table")
-
-
-def fetch_factor(name):
-    return 2.0 if name in STREAMING else 1.0
+REQ_BYTES = {"TCC_EA0_RDREQ_32B_sum": 32.0, "TCC_EA0_RDREQ_64B_sum": 64.0, "TCC_EA0_RDREQ_128B_sum": 128.0,
+             "TCC_EA0_RDREQ_32B": 32.0, "TCC_EA0_RDREQ_64B": 64.0, "TCC_EA0_RDREQ_128B": 128.0}
 
 
 def library_kernel(name):
@@ -51,44 +44,52 @@ def library_kernel(name):
     return name.startswith("k_") and name not in OUTSIDE_STEP
 
 
-def load(path, counter):
-    per = defaultdict(list)
+def load(path, counters, scale):
+    """{kernel: {dispatch id: bytes}} summed over the given counters (x their scale)."""
+    per = defaultdict(lambda: defaultdict(float))
+    if path in (None, "-"):
+        return per
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter:
+        c = r["Counter_Name"]
+        if c not in counters:
             continue
         name = kname(r["Kernel_Name"])
         if library_kernel(name):
-            per[name].append(float(r["Counter_Value"]) * 1024.0)
+            per[name][r["Dispatch_Id"]] += float(r["Counter_Value"]) * scale(c)
     return per
 
 
-def main():
-    fetch = load(sys.argv[1], "FETCH_SIZE")
-    write = load(sys.argv[2], "WRITE_SIZE")
-    n = int(sys.argv[3])
-    steps = int(sys.argv[4])
-    out_path, cfg = sys.argv[5], sys.argv[6]
+def summarize(rdreq, fetch, write, n, steps):
     per_kernel = {}
     total = 0.0
-    gather = 0.0
-    for k in sorted(set(fetch) | set(write)):
-        f = fetch_factor(k)
-        rd = f * sum(fetch.get(k, [])) / steps
-        wr = sum(write.get(k, [])) / steps
-        per_kernel[k] = {"read_bytes_per_step": rd, "write_bytes_per_step": wr, "fetch_factor": f,
-                         "read_class": "stream" if f == 2.0 else "gather (raw L2->fabric bytes, MALL hits included)",
-                         "dispatches_per_step": len(fetch.get(k, write.get(k, []))) / steps}
+    for k in sorted(set(rdreq) | set(write)):
+        rd = sum(rdreq.get(k, {}).values()) / steps
+        wr = sum(write.get(k, {}).values()) / steps
+        fs = sum(fetch.get(k, {}).values()) / steps if k in fetch else None
+        d = {"read_bytes_per_step": rd, "write_bytes_per_step": wr,
+             "dispatches_per_step": len(rdreq.get(k, write.get(k, {}))) / steps}
+        if fs is not None:
+            d["fetch_size_raw_per_step"] = fs
+            d["read_over_fetch_size"] = rd / fs if fs > 0 else None
+        per_kernel[k] = d
         total += rd + wr
-        if f != 2.0:
-            gather += rd
-    rec = {"records": n, "hbm_bytes_per_step": total, "hbm_bytes_per_record": total / n,
-           "gather_read_bytes_per_step": gather, "per_kernel": per_kernel,
-           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over the same bench "
-                     "command; library kernels only; FETCH_SIZE x 2 for the streaming kernels (gfx950 "
-                     "wide-stream correction), x 1 (raw) for gathers"}
-    hist = fetch.get("k_part_hist")
-    if hist:  # true / raw, per step: 16 B x records of key + ts per step over the raw bytes per step
-        rec["k_part_hist_fetch_factor_measured"] = (16.0 * n) / (sum(hist) / steps)
+    return {"records": n, "method_version": 2, "hbm_bytes_per_step": total, "hbm_bytes_per_record": total / n,
+            "per_kernel": per_kernel,
+            "method": "rocprofv3 passes over the same bench command: TCC_EA0_RDREQ_{32B,64B,128B}_sum (read "
+                      "requests by size, bytes = count x size), WRITE_SIZE, and FETCH_SIZE as a cross-check "
+                      "(fetch_size_raw); library kernels only; per step = sum / (steps + warmup)"}
+
+
+def main():
+    rdreq = load(sys.argv[1], REQ_BYTES, lambda c: REQ_BYTES[c])
+    fetch = load(sys.argv[2], ("FETCH_SIZE",), lambda c: 1024.0)
+    write = load(sys.argv[3], ("WRITE_SIZE",), lambda c: 1024.0)
+    n = int(sys.argv[4])
+    steps = int(sys.argv[5])
+    out_path, cfg = sys.argv[6], sys.argv[7]
+    if not rdreq:
+        sys.exit("no TCC_EA0_RDREQ_*B rows for library kernels in %s" % sys.argv[1])
+    rec = summarize(rdreq, fetch, write, n, steps)
     try:
         prev = json.load(open(out_path))
     except (OSError, ValueError):
@@ -96,6 +97,10 @@ def main():
     prev[cfg] = rec
     json.dump(prev, open(out_path, "w"), indent=1)
     print(json.dumps({cfg: {k: v for k, v in rec.items() if k != "per_kernel"}}, indent=1))
+    for k, d in sorted(rec["per_kernel"].items(), key=lambda kv: -kv[1]["read_bytes_per_step"])[:12]:
+        print("%-28s read %8.1f MB  write %8.1f MB  read/FETCH_SIZE %s" % (
+            k, d["read_bytes_per_step"] / 1e6, d["write_bytes_per_step"] / 1e6,
+            "%.2f" % d["read_over_fetch_size"] if d.get("read_over_fetch_size") else "-"))
 
 
 if __name__ == "__main__":
