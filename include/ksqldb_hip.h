@@ -155,10 +155,12 @@ typedef struct khip_batch_stats {
  *   partition, C/util/KsqlConstants.java:42): each partition has its own stream time, set by the
  *   batch's `partition` column.  The GROUP BY key must determine the partition (co-partitioned
  *   input, as groupByKey requires), so the tasks' stores are disjoint and one table holds them.
- *   Closed windows are evicted by the smallest partition stream time; retention and EMIT FINAL
- *   are not offered in this domain (KHIP_E_UNSUPPORTED for a RETENTION or EMIT FINAL
- *   descriptor; snapshots, pull queries and row counts see every window, as tasks whose
- *   retention covers the whole stream would).
+ *   Retention and EMIT FINAL are per task (ABI 7): the library records every key's partition
+ *   (KHIP_E_INVALID when a key arrives on two partitions) and a row expires from snapshots, pull
+ *   queries and row counts, or closes for EMIT FINAL, by its own partition's stream time.  Closed
+ *   windows leave the live table by the smallest partition stream time, so every declared
+ *   partition should receive records: an idle one holds that eviction back (memory and step
+ *   time grow; results do not change).
  * SUPPLIED: one GLOBAL stream time over several handles (ranks): each row carries the stream
  *   time observed at it over the global arrival order (`stream_time` column), computed where the
  *   rows were read, before routing: rank r scans its contiguous arrival chunk with

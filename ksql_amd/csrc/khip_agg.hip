@@ -881,10 +881,17 @@ static khip_status grow_table(khip_agg* a, int64_t new_cap) { return agg_grow_ta
 namespace khip {
 
 int64_t visible_from(const khip_agg* a) {
-  if (!a->windowed || a->host_stream_time < 0) return INT64_MIN;
-  // PARTITION: every task's store would expire by its own stream time, which needs each row's
-  // partition; the handle keeps every window visible instead (retention is not offered there)
-  if (a->desc.time_domain == KHIP_TIME_PARTITION) return INT64_MIN;
+  if (!a->windowed) return INT64_MIN;
+  // PARTITION: every task's store expires by its own stream time (per row through the key map,
+  // partition_bounds); the handle-wide bound is the smallest of the tasks' (what every task has
+  // expired), INT64_MIN while some task has expired nothing
+  if (a->desc.time_domain == KHIP_TIME_PARTITION) {
+    if (a->pst_host.empty()) return INT64_MIN;
+    int64_t m = INT64_MAX;
+    for (int64_t t : a->pst_host) m = std::min(m, partition_vis_from(a, t));
+    return m;
+  }
+  if (a->host_stream_time < 0) return INT64_MIN;
   const int64_t adv = a->desc.advance_ms;
   const int64_t vf = a->host_stream_time / adv * adv - a->retention;  // the store's observed time - retention
   return vf > 0 ? vf : INT64_MIN;  // window starts are >= 0: nothing has expired yet
@@ -1005,9 +1012,8 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
   if (d.time_domain != KHIP_TIME_TASK) {
     if (d.window_kind == KHIP_WINDOW_SESSION) return fail(KHIP_E_UNSUPPORTED, "stream-time domains on SESSION windows");
     if (d.flags & KHIP_FLAG_TABLE_SOURCE) return fail(KHIP_E_UNSUPPORTED, "stream-time domains of a table source");
-    if (d.emit == KHIP_EMIT_FINAL) return fail(KHIP_E_UNSUPPORTED, "EMIT FINAL with a stream-time domain");
-    if (d.time_domain == KHIP_TIME_PARTITION && d.retention_ms != KHIP_RETENTION_DEFAULT)
-      return fail(KHIP_E_UNSUPPORTED, "RETENTION with per-partition stream times");
+    if (d.emit == KHIP_EMIT_FINAL && d.time_domain == KHIP_TIME_SUPPLIED)
+      return fail(KHIP_E_UNSUPPORTED, "EMIT FINAL with a supplied stream time");
     if (d.time_domain == KHIP_TIME_PARTITION && (d.n_partitions < 1 || d.n_partitions > 65536))
       return fail(KHIP_E_INVALID, "n_partitions must be in [1, 65536]");
   }
@@ -1377,9 +1383,11 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   ColPtrs cols{};
   int64_t key_bytes_total = 0;
   KHIP_TRY(resolve_batch(a, b, &keys, &ts, &kv, &rv, &koff, &kbytes, &cols, &key_bytes_total));
-  if (final_emit) KHIP_TRY(emit_final_lost(a, ts, kv, rv, n, 0, nullptr));
+  const bool pdomain = a->desc.time_domain == KHIP_TIME_PARTITION;
+  if (final_emit && !pdomain) KHIP_TRY(emit_final_lost(a, ts, kv, rv, n, 0, nullptr));
   // ---- ABI 5 stream-time domains: the stream time observed at every row
   const int64_t* st_at = nullptr;
+  const int32_t* part = nullptr;
   if (a->desc.time_domain == KHIP_TIME_SUPPLIED) {
     if (!b->stream_time) return fail(KHIP_E_INVALID, "KHIP_TIME_SUPPLIED: the batch has no stream_time column");
     if (b->mem == KHIP_MEM_HOST) {
@@ -1390,7 +1398,7 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
     }
   } else if (a->desc.time_domain == KHIP_TIME_PARTITION) {
     if (!b->partition) return fail(KHIP_E_INVALID, "KHIP_TIME_PARTITION: the batch has no partition column");
-    const int32_t* part = b->partition;
+    part = b->partition;
     if (b->mem == KHIP_MEM_HOST) {
       KHIP_TRY(stage(a, a->st_part, b->partition, n * 4));
       part = a->st_part.as<int32_t>();
@@ -1398,6 +1406,7 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
     KHIP_TRY(a->st_col.ensure((size_t)n * 8));
     KHIP_TRY(stream_time_column(a, ts, kv, rv, part, n, -1, a->st_col.as<int64_t>(), nullptr));
     st_at = a->st_col.as<int64_t>();
+    if (final_emit) KHIP_TRY(partition_lost(a, ts, kv, rv, part, st_at, n));
   }
   // ---- UTF8 keys → stable key ids
   const int64_t* hkeys = keys;
@@ -1412,6 +1421,8 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
     hkeys = a->khash.as<int64_t>();
     ev_record(a, 2);
   }
+  // per-task retention / EMIT FINAL: every accepted key's partition (the tasks share one table)
+  if (pdomain && a->windowed) KHIP_TRY(pmap_insert(a, keys, kv, rv, ts, part, n));
   int64_t tot[NPART] = {0};
   if (a->engine == 2) {
     if (n >= (1LL << 31)) return fail(KHIP_E_UNSUPPORTED, "SESSION pushes above 2^31 rows");
@@ -1503,13 +1514,16 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
     KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
   }
   // one task per partition: the handle's stream time (closing windows, retention) is the slowest's
-  if (a->desc.time_domain == KHIP_TIME_PARTITION) KHIP_TRY(stream_time_partition_min(a));
-  if (final_emit) KHIP_TRY(finish_lost(a, ts, kv, rv, n));
+  if (pdomain) KHIP_TRY(stream_time_partition_min(a));
+  if (final_emit) KHIP_TRY(pdomain ? partition_lost_finish(a) : finish_lost(a, ts, kv, rv, n));
   if (a->engine == 0 && a->windowed) {  // retention: drop expired windows from the closed store
     HavingDev vis{};
     vis.vis = 1;
     vis.vis_from = visible_from(a);
-    if (vis.vis_from != INT64_MIN) KHIP_TRY(part_purge_closed(a, vis));
+    if (vis.vis_from != INT64_MIN) {
+      KHIP_TRY(partition_bounds(a, vis));  // PARTITION: each row by its own task's bound
+      KHIP_TRY(part_purge_closed(a, vis));
+    }
   }
   s.rows_accepted = tot[P_ACCEPTED];
   s.dropped_null_key = tot[P_NULL_KEY];
@@ -1559,6 +1573,11 @@ khip_status khip_stream_time_scan(khip_agg* a, const khip_batch* b, int64_t seed
 // bound is at or above the first visible window start.  The atomic engine keeps every row.
 static bool no_expired_live(const khip_agg* a) {
   if (a->engine == 2) return true;  // the session store drops expired sessions at every push
+  if (a->desc.time_domain == KHIP_TIME_PARTITION && a->windowed) {  // no task has expired a window
+    for (int64_t t : a->pst_host)
+      if (partition_vis_from(a, t) != INT64_MIN) return false;
+    return true;
+  }
   const int64_t vf = visible_from(a);
   if (vf == INT64_MIN) return true;
   if (a->engine != 0 || a->st_before < 0) return false;
@@ -1574,6 +1593,7 @@ static khip_status compact_rows(khip_agg* a, const khip_having* h, std::vector<u
     hd.vis_from = visible_from(a);
   }
   hd.session = a->engine == 2;
+  KHIP_TRY(partition_bounds(a, hd));  // PARTITION: each row's retention / EMIT FINAL bounds are its task's
   if (h) {
     if (h->agg_index < 0 || h->agg_index >= a->desc.n_aggs) return fail(KHIP_E_INVALID, "having agg index");
     if (h->op < KHIP_OP_GT || h->op > KHIP_OP_NE) return fail(KHIP_E_INVALID, "having op");
@@ -1830,6 +1850,14 @@ static khip_status compute_changes(khip_agg* a) {
     fd.fin_c0 = a->st_before - a->grace;
     fd.fin_c1 = a->host_stream_time - a->grace;
     fd.fin_size = a->desc.size_ms;
+    if (a->desc.time_domain == KHIP_TIME_PARTITION) {
+      // per task (partition_bounds): a row closes when ITS partition's stream time passes its end;
+      // a row whose key is not in the map closes nowhere
+      fd.fin_c0 = fd.fin_c1 = 0;
+      bool moved = false;
+      for (size_t p = 0; p < a->pst_host.size(); p++) moved = moved || a->pst_host[p] > a->pst_prev_host[p];
+      if (moved) fd.fin_c1 = 1;  // (only gates the compaction below)
+    }
     DevBuf dl;
     if (!a->lost.empty()) {
       KHIP_TRY(dl.ensure(a->lost.size() * 8));
@@ -1837,8 +1865,10 @@ static khip_status compute_changes(khip_agg* a) {
       fd.lost = dl.as<int64_t>();
       fd.n_lost = (int32_t)(a->lost.size() / 2);
     }
-    if (fd.fin_c1 > fd.fin_c0)
+    if (fd.fin_c1 > fd.fin_c0) {
+      if (a->desc.time_domain == KHIP_TIME_PARTITION) fd.fin_c1 = 0;
       KHIP_TRY(compact_rows(a, a->desc.has_having ? &a->desc.having : nullptr, &a->chg_rows, &a->chg_n, &fd));
+    }
     a->chg_tomb.assign((size_t)a->chg_n, 0);
   } else if (a->changelog && a->engine == 2) {
     KHIP_TRY(sess_changes(a, &a->chg_rows, &a->chg_tomb, &a->chg_n));
@@ -1902,8 +1932,14 @@ khip_status khip_agg_reset(khip_agg* a) {
   if (a->desc.key_type == KHIP_KEY_UTF8) {
     KHIP_TRY(dict_clear(a->dict, a->stream));
   }
-  if (a->desc.time_domain == KHIP_TIME_PARTITION)
+  if (a->desc.time_domain == KHIP_TIME_PARTITION) {
     KHIP_TRY_HIP(hipMemsetAsync(a->pst.p, 0xFF, (size_t)a->desc.n_partitions * 8, a->stream));
+    a->pst_host.assign((size_t)a->desc.n_partitions, -1);
+    a->pst_prev_host.assign((size_t)a->desc.n_partitions, -1);
+    a->plost.clear();
+    a->plost_off.clear();
+    KHIP_TRY(pmap_clear(a));  // forget the keys' partitions (keeps the allocation)
+  }
   // asynchronous on the handle's stream (every later call on the handle is ordered behind it)
   KHIP_TRY_HIP(hipGetLastError());
   a->occ = 0;
@@ -1946,6 +1982,7 @@ khip_status khip_agg_destroy(khip_agg* a) {
     a->st_cval[c].release();
   }
   dict_release(a->dict);
+  pmap_release(a);
   tagg_release(a);
   part_release(a);
   sess_release(a);

@@ -81,22 +81,67 @@ struct HavingDev {
   int64_t fin_c0, fin_c1, fin_size;
   const int64_t* lost;
   int32_t session;  // SESSION rows: WINDOWEND is the row's own end (word 2), not ws + size
+  // KHIP_TIME_PARTITION: retention and EMIT FINAL per task.  A row's task is its key's partition
+  // (co-partitioned keys), found through the handle's key map (pm_key / pm_part, open addressing,
+  // INT64_MIN = empty; the key INT64_MIN itself at pm_part[pm_mask + 1]); its bounds are that
+  // partition's: p_vis[p] (vis_from), p_fin[2p], p_fin[2p + 1] (fin_c0, fin_c1) and the lost ws
+  // ranges p_lost[2 * p_lost_off[p] .. 2 * p_lost_off[p + 1]).  pm_key == null: the fields above.
+  const int64_t* pm_key;
+  const int32_t* pm_part;
+  uint64_t pm_mask;
+  const int64_t* p_vis;
+  const int64_t* p_fin;
+  const int64_t* p_lost_off;
+  const int64_t* p_lost;
 };
+
+__device__ __forceinline__ uint64_t pmap_hash(int64_t k) {
+  uint64_t z = (uint64_t)k * 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 31)) * 0xBF58476D1CE4E5B9ULL;
+  return z ^ (z >> 29);
+}
+
+// The partition of key k in the key map, or -1 when the key never reached it.
+__device__ __forceinline__ int pmap_find(const int64_t* __restrict__ keys, const int32_t* __restrict__ parts,
+                                         uint64_t mask, int64_t k) {
+  if (k == INT64_MIN) return parts[mask + 1];
+  uint64_t s = pmap_hash(k) & mask;
+  for (uint64_t probe = 0; probe <= mask; probe++) {
+    const int64_t c = keys[s];
+    if (c == k) return parts[s];
+    if (c == INT64_MIN) return -1;
+    s = (s + 1) & mask;
+  }
+  return -1;
+}
 
 // Retention and EMIT FINAL selection of a row [key, ws, ...] (no-ops unless h.vis / h.fin).
 __device__ __forceinline__ bool store_ok(const uint64_t* s, const HavingDev& h) {
   const int64_t ws = (int64_t)s[1];
-  if (h.vis && ws < h.vis_from) return false;
+  int64_t vis_from = h.vis_from, c0 = h.fin_c0, c1 = h.fin_c1;
+  const int64_t* lost = h.lost;
+  int n_lost = h.n_lost;
+  if (h.pm_key && (h.vis || h.fin)) {  // KHIP_TIME_PARTITION: the bounds of the row's own task
+    const int p = pmap_find(h.pm_key, h.pm_part, h.pm_mask, (int64_t)s[0]);
+    if (p >= 0) {
+      vis_from = h.p_vis[p];
+      c0 = h.p_fin[2 * p];
+      c1 = h.p_fin[2 * p + 1];
+      lost = h.p_lost + 2 * h.p_lost_off[p];
+      n_lost = (int)(h.p_lost_off[p + 1] - h.p_lost_off[p]);
+    }
+  }
+  if (h.vis && ws < vis_from) return false;
   if (h.fin) {
     const int64_t end = ws + h.fin_size;
-    if (end <= h.fin_c0 || end > h.fin_c1) return false;
-    int lo = 0, hi = h.n_lost;  // first range starting after ws
+    if (end <= c0 || end > c1) return false;
+    int lo = 0, hi = n_lost;  // first range starting after ws
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
-      if (h.lost[2 * mid] <= ws) lo = mid + 1;
+      if (lost[2 * mid] <= ws) lo = mid + 1;
       else hi = mid;
     }
-    if (lo > 0 && ws <= h.lost[2 * (lo - 1) + 1]) return false;
+    if (lo > 0 && ws <= lost[2 * (lo - 1) + 1]) return false;
   }
   return true;
 }
@@ -493,6 +538,14 @@ struct khip_agg {
   // ---- stream-time domains (ABI 5, khip_stream_time.hip): per-partition stream times (pst,
   // pst2 = the next batch's), the push's per-row stream time, scan scratch, staged partition ids
   DevBuf pst, pst2, st_col, st_agg, st_seen, st_part;
+  // KHIP_TIME_PARTITION, windowed: per-task retention and EMIT FINAL (khip_stream_time.hip).  The
+  // key map (key → partition, pm_key / pm_part), its capacity (power of two) and keys; host copies
+  // of the partitions' stream times after / before the last push; the last push's lost ws ranges
+  // per partition (EMIT FINAL: plost pairs, plost_off[P + 1]); pdom: the per-partition bounds of
+  // one compaction (device)
+  DevBuf pm_key, pm_part, pm_ctr, pdom;
+  int64_t pm_cap = 0, pm_occ = 0, pm_last = -1;
+  std::vector<int64_t> pst_host, pst_prev_host, plost, plost_off;
 };
 
 // Emission flags of a row written by the last push (khip_agg::chg): touched by one of its
@@ -526,6 +579,19 @@ struct RowsIn {
 void shuffle_layout(const khip_shuffle* s, int* key_col, int* n_cols, const int32_t** types);
 khip_status part_push_rows(khip_agg* a, int64_t n, const RowsIn& ri, int key_col, int64_t* tot, bool* done,
                            bool supplied);
+// KHIP_TIME_PARTITION, windowed (khip_stream_time.hip): record every accepted row's key → partition
+// (KHIP_E_INVALID when a key arrives on two partitions); EMIT FINAL's lost ws ranges per partition
+// from the push's per-row stream time (st) — collected into a->plost by partition_lost_finish;
+// the per-partition bounds of a compaction (retention: h.vis; EMIT FINAL: h.fin) attached to h.
+khip_status pmap_insert(khip_agg* a, const int64_t* keys, const uint8_t* kv, const uint8_t* rv, const int64_t* ts,
+                        const int32_t* part, int64_t n);
+khip_status partition_lost(khip_agg* a, const int64_t* ts, const uint8_t* kv, const uint8_t* rv, const int32_t* part,
+                           const int64_t* st, int64_t n);
+khip_status partition_lost_finish(khip_agg* a);
+khip_status partition_bounds(khip_agg* a, HavingDev& h);
+int64_t partition_vis_from(const khip_agg* a, int64_t pst);
+khip_status pmap_clear(khip_agg* a);
+void pmap_release(khip_agg* a);
 khip_status part_compact(khip_agg* a, const HavingDev& h, std::vector<uint64_t>* rows, int64_t* count);
 bool part_having_count(khip_agg* a, int64_t* n);
 khip_status part_changes(khip_agg* a, std::vector<uint64_t>* rows, std::vector<uint8_t>* tomb, int64_t* count);

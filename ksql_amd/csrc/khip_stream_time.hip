@@ -21,6 +21,7 @@
 //   k_st_min     the smallest partition stream time → the handle's stream time (eviction of closed
 //                windows must wait for the slowest task)
 #include <algorithm>
+#include <array>
 
 #include "khip_agg_internal.hpp"
 
@@ -218,15 +219,295 @@ khip_status stream_time_column(khip_agg* a, const int64_t* ts, const uint8_t* kv
   return KHIP_OK;
 }
 
-// The handle's stream time in the PARTITION domain: the smallest partition stream time.
+// The handle's stream time in the PARTITION domain: the smallest partition stream time.  Every
+// declared partition counts, one that has not received a record yet included (its stream time is
+// -1): closed windows leave the live table by this bound, and a partition that starts late must
+// still find its windows there.  An idle partition therefore holds eviction back (memory, not
+// results: visibility, retention and EMIT FINAL are per partition, partition_bounds).  The host
+// keeps copies of the partitions' stream times after and before the push.
 khip_status stream_time_partition_min(khip_agg* a) {
   hipLaunchKernelGGL(k_st_min, dim3(1), dim3(256), 0, a->stream, a->pst.as<int64_t>(), a->desc.n_partitions,
                      a->stream_time.as<int64_t>());
   KHIP_TRY_HIP(hipGetLastError());
   int64_t h = -1;
+  const size_t P = (size_t)a->desc.n_partitions;
+  a->pst_host.resize(P);
+  a->pst_prev_host.resize(P);
   KHIP_TRY_HIP(hipMemcpyAsync(&h, a->stream_time.p, 8, hipMemcpyDeviceToHost, a->stream));
+  KHIP_TRY_HIP(hipMemcpyAsync(a->pst_host.data(), a->pst.p, P * 8, hipMemcpyDeviceToHost, a->stream));
+  KHIP_TRY_HIP(hipMemcpyAsync(a->pst_prev_host.data(), a->pst2.p, P * 8, hipMemcpyDeviceToHost, a->stream));
   KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
   a->host_stream_time = h;
+  return KHIP_OK;
+}
+
+// ------------------------------------------------------------------ per-task retention / EMIT FINAL
+// KHIP_TIME_PARTITION runs n_partitions tasks in one table; each task's window store expires and
+// closes windows by ITS stream time (StreamAggregateBuilder.java:282-285 emitStrategy, :293
+// window.getRetention(), applied per task by Kafka Streams).  Rows carry no partition, but keys
+// are co-partitioned, so a key map (key → partition) recorded at every push gives each row its
+// task at compaction time (store_ok).
+
+constexpr int PM_PROBE = 256;
+
+// ctr[0]: keys added (wave sums), ctr[1]: probe budget exhausted, ctr[2]: a key on two partitions
+__global__ __launch_bounds__(256) void k_pmap_insert(const int64_t* __restrict__ keys, const uint8_t* __restrict__ kv,
+                                                     const uint8_t* __restrict__ rv, const int64_t* __restrict__ ts,
+                                                     const int32_t* __restrict__ part, int64_t n,
+                                                     int64_t* __restrict__ pk, int32_t* __restrict__ pp, uint64_t mask,
+                                                     unsigned long long* __restrict__ ctr) {
+  int64_t added = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!(bit_get(kv, i) && bit_get(rv, i) && ts[i] >= 0)) continue;
+    const int64_t k = keys[i];
+    const int32_t p = part[i];
+    if (k == INT64_MIN) {
+      const int old = atomicCAS(&pp[mask + 1], -1, p);
+      if (old != -1 && old != p) atomicOr(&ctr[2], 1ULL);
+      continue;
+    }
+    uint64_t sl = pmap_hash(k) & mask;
+    bool done = false;
+    for (int probe = 0; probe < PM_PROBE && !done; probe++) {
+      int64_t c = (int64_t)__hip_atomic_load((uint64_t*)&pk[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (c == INT64_MIN) {
+        const unsigned long long old = atomicCAS((unsigned long long*)&pk[sl], (unsigned long long)INT64_MIN,
+                                                 (unsigned long long)k);
+        if ((int64_t)old == INT64_MIN) {
+          __hip_atomic_store(&pp[sl], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          added++;
+          done = true;
+          break;
+        }
+        c = (int64_t)old;
+      }
+      if (c == k) {  // (the claimer's partition may not be stored yet: -1 is not a conflict)
+        const int32_t q = __hip_atomic_load(&pp[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (q != -1 && q != p) atomicOr(&ctr[2], 1ULL);
+        done = true;
+        break;
+      }
+      sl = (sl + 1) & mask;
+    }
+    if (!done) atomicOr(&ctr[1], 1ULL);
+  }
+  added = wave_sum(added);
+  if ((threadIdx.x & 63) == 0 && added) atomicAdd(&ctr[0], (unsigned long long)added);
+}
+
+__global__ __launch_bounds__(256) void k_pmap_rehash(const int64_t* __restrict__ ok, const int32_t* __restrict__ op,
+                                                     int64_t ocap, int64_t* __restrict__ nk, int32_t* __restrict__ np,
+                                                     uint64_t nmask) {
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < ocap; s += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = ok[s];
+    if (k == INT64_MIN) continue;
+    uint64_t d = pmap_hash(k) & nmask;
+    while (atomicCAS((unsigned long long*)&nk[d], (unsigned long long)INT64_MIN, (unsigned long long)k) !=
+           (unsigned long long)INT64_MIN)
+      d = (d + 1) & nmask;
+    np[d] = op[s];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_fill_i64(int64_t* __restrict__ p, int64_t n, int64_t v) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+static int pm_grid(int64_t n) { return (int)std::min<int64_t>(std::max<int64_t>(ceil_div(n, 256), 1), 8192); }
+
+static khip_status pmap_grow(khip_agg* a, int64_t cap) {
+  DevBuf nk, np;
+  KHIP_TRY(nk.ensure((size_t)cap * 8));
+  KHIP_TRY(np.ensure((size_t)(cap + 1) * 4));
+  hipLaunchKernelGGL(k_fill_i64, dim3(pm_grid(cap)), dim3(256), 0, a->stream, nk.as<int64_t>(), cap, INT64_MIN);
+  KHIP_TRY_HIP(hipMemsetAsync(np.p, 0xFF, (size_t)(cap + 1) * 4, a->stream));
+  if (a->pm_cap > 0) {
+    hipLaunchKernelGGL(k_pmap_rehash, dim3(pm_grid(a->pm_cap)), dim3(256), 0, a->stream, a->pm_key.as<int64_t>(),
+                       a->pm_part.as<int32_t>(), a->pm_cap, nk.as<int64_t>(), np.as<int32_t>(), (uint64_t)(cap - 1));
+    KHIP_TRY_HIP(hipMemcpyAsync(np.as<int32_t>() + cap, a->pm_part.as<int32_t>() + a->pm_cap, 4,
+                                hipMemcpyDeviceToDevice, a->stream));
+  }
+  KHIP_TRY_HIP(hipGetLastError());
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  a->pm_key.release();
+  a->pm_part.release();
+  a->pm_key = nk;
+  a->pm_part = np;
+  nk.p = np.p = nullptr;
+  a->pm_cap = cap;
+  return KHIP_OK;
+}
+
+khip_status pmap_insert(khip_agg* a, const int64_t* keys, const uint8_t* kv, const uint8_t* rv, const int64_t* ts,
+                        const int32_t* part, int64_t n) {
+  if (n <= 0) return KHIP_OK;
+  // room for the keys this batch may add (as the key dictionary sizes itself: every row on the
+  // first push, then twice the last push's new keys, at least n / 16); a batch that brings more
+  // exhausts a probe budget and is inserted again into a larger map (inserts are idempotent)
+  const int64_t est = a->pm_last < 0 ? n : std::min<int64_t>(n, std::max<int64_t>({2 * a->pm_last, n / 16, 4096}));
+  if (a->pm_cap == 0 || 2 * (a->pm_occ + est) > a->pm_cap)
+    KHIP_TRY(pmap_grow(a, next_pow2(std::max<int64_t>(4 * (a->pm_occ + est), 4096))));
+  KHIP_TRY(a->pm_ctr.ensure(24));
+  for (int attempt = 0;; attempt++) {
+    KHIP_TRY_HIP(hipMemsetAsync(a->pm_ctr.p, 0, 24, a->stream));
+    hipLaunchKernelGGL(k_pmap_insert, dim3(pm_grid(n)), dim3(256), 0, a->stream, keys, kv, rv, ts, part, n,
+                       a->pm_key.as<int64_t>(), a->pm_part.as<int32_t>(), (uint64_t)(a->pm_cap - 1),
+                       a->pm_ctr.as<unsigned long long>());
+    KHIP_TRY_HIP(hipGetLastError());
+    unsigned long long c[3];
+    KHIP_TRY_HIP(hipMemcpyAsync(c, a->pm_ctr.p, 24, hipMemcpyDeviceToHost, a->stream));
+    KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+    a->pm_occ += (int64_t)c[0];
+    if (c[2]) return fail(KHIP_E_INVALID, "KHIP_TIME_PARTITION: a GROUP BY key arrived on two partitions "
+                                          "(keys must be co-partitioned)");
+    if (!c[1]) {
+      a->pm_last = (int64_t)c[0];
+      return KHIP_OK;
+    }
+    if (attempt >= 6) return fail(KHIP_E_DEVICE, "partition key map probe budget exhausted");
+    KHIP_TRY(pmap_grow(a, a->pm_cap * 4));
+  }
+}
+
+khip_status pmap_clear(khip_agg* a) {
+  if (a->pm_cap == 0) return KHIP_OK;
+  hipLaunchKernelGGL(k_fill_i64, dim3(pm_grid(a->pm_cap)), dim3(256), 0, a->stream, a->pm_key.as<int64_t>(), a->pm_cap,
+                     INT64_MIN);
+  KHIP_TRY_HIP(hipMemsetAsync(a->pm_part.p, 0xFF, (size_t)(a->pm_cap + 1) * 4, a->stream));
+  KHIP_TRY_HIP(hipGetLastError());
+  a->pm_occ = 0;
+  return KHIP_OK;
+}
+
+void pmap_release(khip_agg* a) {
+  a->pm_key.release();
+  a->pm_part.release();
+  a->pm_ctr.release();
+  a->pdom.release();
+  a->pm_cap = a->pm_occ = 0;
+  a->pm_last = -1;
+}
+
+// EMIT FINAL, per task: the k_emit_lost rule with each record's own partition stream time before it
+// (the previous row of its run, or the partition's stream time before the batch).  lost: (p, lo, hi).
+__global__ __launch_bounds__(256) void k_emit_lost_part(const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
+                                                        const uint8_t* __restrict__ rv, const int32_t* __restrict__ part,
+                                                        const int64_t* __restrict__ st,
+                                                        const int64_t* __restrict__ pst_before, int64_t n, int64_t size,
+                                                        int64_t adv, int64_t grace, int64_t retention,
+                                                        int64_t* __restrict__ lost, int64_t cap,
+                                                        unsigned long long* __restrict__ ctr) {
+  const int64_t sg = size + grace;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!bit_get(kv, i) || !bit_get(rv, i)) continue;
+    const int32_t p = part[i];
+    const int64_t mp = (i > 0 && part[i - 1] == p) ? st[i - 1] : pst_before[p];
+    const int64_t t = ts[i];
+    if (t <= mp) continue;
+    const int64_t bp = mp < 0 ? -1 : mp / adv, b = t / adv;
+    if (b <= bp) continue;
+    int64_t lo = mp - sg + 1;
+    int64_t hi = t - sg;
+    const int64_t exp_hi = b * adv - retention - 1;
+    hi = hi < exp_hi ? hi : exp_hi;
+    lo = lo < 0 ? 0 : lo;
+    lo = (lo + adv - 1) / adv * adv;
+    if (lo <= hi) {
+      const unsigned long long slot = atomicAdd(ctr, 1ULL);
+      if ((int64_t)slot < cap) {
+        lost[3 * slot] = p;
+        lost[3 * slot + 1] = lo;
+        lost[3 * slot + 2] = hi;
+      }
+    }
+  }
+}
+
+// Call after stream_time_column (a->pst2 = the partitions' stream times before the batch).
+khip_status partition_lost(khip_agg* a, const int64_t* ts, const uint8_t* kv, const uint8_t* rv, const int32_t* part,
+                           const int64_t* st, int64_t n) {
+  KHIP_TRY(a->lostctr.ensure(16));
+  if (a->lost_cap == 0) a->lost_cap = 4096;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    KHIP_TRY(a->lostbuf.ensure((size_t)a->lost_cap * 24));
+    KHIP_TRY_HIP(hipMemsetAsync(a->lostctr.p, 0, 8, a->stream));
+    hipLaunchKernelGGL(k_emit_lost_part, dim3(pm_grid(n)), dim3(256), 0, a->stream, ts, kv, rv, part, st,
+                       a->pst2.as<int64_t>(), n, a->desc.size_ms, a->desc.advance_ms, a->grace, a->retention,
+                       a->lostbuf.as<int64_t>(), a->lost_cap, a->lostctr.as<unsigned long long>());
+    KHIP_TRY_HIP(hipGetLastError());
+    int64_t cnt = 0;
+    KHIP_TRY_HIP(hipMemcpyAsync(&cnt, a->lostctr.p, 8, hipMemcpyDeviceToHost, a->stream));
+    KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+    if (cnt <= a->lost_cap) break;
+    a->lost_cap = next_pow2(cnt);
+    a->lostbuf.release();
+  }
+  return KHIP_OK;
+}
+
+// The lost (p, lo, hi) triples of the last push → per partition sorted, merged ws ranges.
+khip_status partition_lost_finish(khip_agg* a) {
+  int64_t cnt = 0;
+  KHIP_TRY_HIP(hipMemcpyAsync(&cnt, a->lostctr.p, 8, hipMemcpyDeviceToHost, a->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  std::vector<int64_t> t((size_t)cnt * 3);
+  if (cnt) KHIP_TRY_HIP(hipMemcpyAsync(t.data(), a->lostbuf.p, (size_t)cnt * 24, hipMemcpyDeviceToHost, a->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  std::vector<std::array<int64_t, 3>> r((size_t)cnt);
+  for (int64_t k = 0; k < cnt; k++) r[k] = {t[3 * k], t[3 * k + 1], t[3 * k + 2]};
+  std::sort(r.begin(), r.end());
+  const int P = a->desc.n_partitions;
+  a->plost.clear();
+  a->plost_off.assign((size_t)P + 1, 0);
+  int64_t cur_p = -1;
+  for (auto& x : r) {
+    if (x[0] == cur_p && !a->plost.empty() && x[1] <= a->plost.back() + 1) {
+      a->plost.back() = std::max(a->plost.back(), x[2]);
+    } else {
+      a->plost.push_back(x[1]);
+      a->plost.push_back(x[2]);
+      a->plost_off[(size_t)x[0] + 1]++;
+      cur_p = x[0];
+    }
+  }
+  for (int p = 0; p < P; p++) a->plost_off[p + 1] += a->plost_off[p];
+  return KHIP_OK;
+}
+
+// A partition's first visible window start (the visible_from rule with its own stream time).
+int64_t partition_vis_from(const khip_agg* a, int64_t pst) {
+  if (pst < 0) return INT64_MIN;
+  const int64_t adv = a->desc.advance_ms;
+  const int64_t vf = pst / adv * adv - a->retention;
+  return vf > 0 ? vf : INT64_MIN;
+}
+
+khip_status partition_bounds(khip_agg* a, HavingDev& h) {
+  if (a->desc.time_domain != KHIP_TIME_PARTITION || !a->windowed || a->pm_cap == 0 || !(h.vis || h.fin))
+    return KHIP_OK;
+  const int P = a->desc.n_partitions;
+  std::vector<int64_t> host;
+  host.reserve((size_t)P * 4 + 2 + a->plost.size());
+  const bool have = a->pst_host.size() == (size_t)P;
+  for (int p = 0; p < P; p++) host.push_back(partition_vis_from(a, have ? a->pst_host[p] : -1));
+  for (int p = 0; p < P; p++) {
+    host.push_back((have ? a->pst_prev_host[p] : -1) - a->grace);
+    host.push_back((have ? a->pst_host[p] : -1) - a->grace);
+  }
+  const bool lost_ok = a->plost_off.size() == (size_t)P + 1;
+  for (int p = 0; p <= P; p++) host.push_back(lost_ok ? a->plost_off[p] : 0);
+  host.insert(host.end(), a->plost.begin(), a->plost.end());
+  KHIP_TRY(a->pdom.ensure(host.size() * 8));
+  KHIP_TRY_HIP(hipMemcpyAsync(a->pdom.p, host.data(), host.size() * 8, hipMemcpyHostToDevice, a->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));  // `host` goes out of scope
+  const int64_t* d = a->pdom.as<int64_t>();
+  h.pm_key = a->pm_key.as<int64_t>();
+  h.pm_part = a->pm_part.as<int32_t>();
+  h.pm_mask = (uint64_t)(a->pm_cap - 1);
+  h.p_vis = d;
+  h.p_fin = d + P;
+  h.p_lost_off = d + 3 * P;
+  h.p_lost = d + 4 * P + 1;
   return KHIP_OK;
 }
 

@@ -45,3 +45,52 @@ def test_single_gpu_does_not_relaunch(monkeypatch):
         pytest.skip("would run the benchmark")
     with pytest.raises(Exception):  # no GPU here: fails at the first device call, not at relaunch
         bench.main()
+
+
+# ---- profiles/traffic.json: the counter bytes the bench line's roofline.traffic comes from -------
+# Read bytes are measured from request counts by size (tools/pmc_traffic.py, method_version 2).
+# A kernel that streams its input once cannot read less than that input: a figure below it means
+# the counters were mis-read or mis-scaled (round 4 halved them for kernels missing from a hand-kept
+# list).  Floors, in bytes per record of the entry's `records`, per kernel whose reads are known:
+TRAFFIC_FLOORS = {
+    "possible_fraud": {"k_c1_scatter": 16},             # key + ts
+    "possible_fraud_sparse_keys": {"k_c1_scatter": 16},
+    "hopping_double": {"k_c1v_scatter": 24},            # key + ts + amount (per record of the leg)
+    "repartition_sum": {"k_shuf_pack1": 24},            # region + ts + amount
+}
+
+
+def _traffic():
+    import json
+    with open(os.path.join(os.path.dirname(bench.__file__), "profiles", "traffic.json")) as f:
+        return json.load(f)
+
+
+def test_traffic_entries_read_at_least_their_streamed_input():
+    t = _traffic()
+    checked = 0
+    for cfg, floors in TRAFFIC_FLOORS.items():
+        rec = t.get(cfg)
+        if not rec or rec.get("method_version", 1) < 2:
+            continue
+        for k, per_record in floors.items():
+            pk = rec["per_kernel"].get(k)
+            if pk is None:
+                continue
+            floor = 0.97 * per_record * rec["records"]
+            assert pk["read_bytes_per_step"] >= floor, (cfg, k, pk["read_bytes_per_step"], floor)
+            checked += 1
+    assert checked >= 1, "no method_version-2 entry to check"
+
+
+def test_bench_uses_only_measured_traffic_entries():
+    """bench.load_traffic ignores entries from before the size-classed read counters."""
+    import json
+    import tempfile
+    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
+        json.dump({"x": {"records": 10, "hbm_bytes_per_step": 5.0},
+                   "y": {"records": 10, "hbm_bytes_per_step": 7.0, "method_version": 2}}, f)
+    assert bench.load_traffic(f.name, "x", 10) is None
+    assert bench.load_traffic(f.name, "y", 10) == 7.0
+    assert bench.load_traffic(f.name, "y", 11) is None
+    os.unlink(f.name)

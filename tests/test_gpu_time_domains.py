@@ -93,8 +93,8 @@ def test_partition_domain_matches_independent_tasks(prod, orc, engine, window):
     flags = abi.FLAG_ENGINE_ATOMIC if engine == "atomic" else 0
     gd = _desc(time_domain="PARTITION", n_partitions=P, flags=flags, **kw)
     g = abi.AggHandle(prod, gd)
-    # the handle keeps every window visible (no retention in this domain): so do the tasks
-    tasks = [abi.AggHandle(orc, _desc(retention_ms=1 << 40, **kw)) for _ in range(P)]
+    # every task's store expires windows by its own stream time (default retention: size + grace)
+    tasks = [abi.AggHandle(orc, _desc(**kw)) for _ in range(P)]
     late = 0
     for k, t, v, p in batches:
         gs = g.push(abi.HostBatch(t, keys=k, cols=[v], partition=p))
@@ -148,6 +148,52 @@ def test_partition_domain_count_pipeline(prod, orc):
     g.close()
     for h in tasks:
         h.close()
+
+
+@pytest.mark.parametrize("engine", ["part", "atomic"])
+@pytest.mark.parametrize("window", ["TUMBLING", "HOPPING"])
+def test_partition_domain_retention_and_emit_final(prod, orc, engine, window):
+    """RETENTION and EMIT FINAL per task (StreamAggregateBuilder.java:282-285 emitStrategy, :293
+    window.getRetention()): per push, the windows EMIT FINAL closes, and the table a snapshot / a
+    pull query / a row count sees, equal P independent oracle tasks' — each task expiring and
+    closing windows by its own stream time."""
+    rng = np.random.default_rng(41 + (engine == "atomic") + 2 * (window == "HOPPING"))
+    P = 4
+    batches = _partition_batches(rng, P, nb=4, per=30_000, keys_per_part=2000)
+    kw = dict(window=window, adv=2500 if window == "HOPPING" else 0, retention_ms=20_000)
+    flags = abi.FLAG_ENGINE_ATOMIC if engine == "atomic" else 0
+    for emit in ("CHANGES", "FINAL"):
+        gd = _desc(time_domain="PARTITION", n_partitions=P, flags=flags, emit=emit, **kw)
+        g = abi.AggHandle(prod, gd)
+        tasks = [abi.AggHandle(orc, _desc(emit=emit, **kw)) for _ in range(P)]
+        closed = 0
+        for k, t, v, p in batches:
+            gs = g.push(abi.HostBatch(t, keys=k, cols=[v], partition=p))
+            os_ = [tasks[q].push(abi.HostBatch(t[p == q], keys=k[p == q], cols=[v[p == q]])) for q in range(P)]
+            assert gs["windows_late"] == sum(o["windows_late"] for o in os_)
+            if emit == "FINAL":
+                got = g.changes()
+                exp = _union([h.changes() for h in tasks], gd)
+                assert_snap_equal(got, exp, gd)
+                closed += got["n"]
+            assert g.count_rows() == sum(h.count_rows() for h in tasks)
+        assert_snap_equal(g.snapshot(), _union([h.snapshot() for h in tasks], gd), gd)
+        some = np.unique(batches[-1][0])[:50]
+        assert_snap_equal(g.get(keys=some), _union([h.get(keys=some) for h in tasks], gd), gd)
+        if emit == "FINAL":
+            assert closed > 0
+        g.close()
+        for h in tasks:
+            h.close()
+
+
+def test_partition_domain_key_on_two_partitions(prod):
+    g = abi.AggHandle(prod, _desc(time_domain="PARTITION", n_partitions=2))
+    k = np.array([5, 6, 7, 5], np.int64)
+    t = np.arange(4, dtype=np.int64) * 100
+    with pytest.raises(abi.KsqlHipError, match="two partitions"):
+        g.push(abi.HostBatch(t, keys=k, cols=[np.zeros(4, np.int64)], partition=np.array([0, 0, 1, 1], np.int32)))
+    g.close()
 
 
 def test_partition_domain_rejects_bad_batches(prod):
