@@ -18,7 +18,7 @@
 // Per micro-batch (all on the handle's stream):
 //   k_blockmax → k_scan_blocks : stream time before each 2048-record block
 //                                (exclusive prefix max, carried across batches)
-//   [UTF8] k_dict_lookup → k_dict_count/k_scan_excl/k_dict_write → k_kid_fixup
+//   [UTF8] k_dict_probe → k_dict_commit → k_dict_resolve (khip_dict.hpp)
 //   k_apply     : in-block prefix max → late test → window fan-out → find-or-claim the
 //                 (key, ws) slot with one 64-bit CAS whose value references the batch
 //                 row (no spin, no fence) → agent-scope atomics for the state
@@ -408,114 +408,242 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ ta
   }
 }
 
-// ---------------------------------------------------------------- UTF8 dictionary
-// dict word: 0 empty | fresh: bit63 | fp22 << 40 | batch row (40 bits) | resident: bit62 | fp22 << 40
-// | o / 8 (40 bits: the entry's arena offset, so a hit reads the word and the entry only)
-// arena entry at offset o (8-aligned): [u64 hash][i64 len][bytes, padded to 8]; key id = o.
-// A lookup gives up after DICT_PROBE slots (the table is then too full: dict_map unclaims the
+// ---------------------------------------------------------------- UTF8 dictionary (khip_dict.hpp)
+// Slot (32 B, one random access): w0 dict word: 0 empty | fresh: bit63 | fp22 << 40 | batch row
+// (40 bits) | resident: bit62 | fp22 << 40 | o / 8 (40 bits); w1 = o | min(len, 0xFFFF) << 48 (the
+// key's id = its arena offset o, and its length); w2, w3 = the key's first 16 bytes as words
+// (keys of up to 16 bytes compare there; longer ones against the arena entry).  Arena entry at o
+// (8-aligned): [u64 hash][i64 len][bytes, padded to 8].  A map is three passes, none over the
+// whole table:
+//   k_dict_probe    per row: hash, probe; a resident slot compares in place; an empty slot is
+//                   claimed (fresh word naming the row; the slot goes to one of DICT_NL claim lists,
+//                   one wave-aggregated append); a fresh slot of the same fingerprint, claimed by
+//                   another row of this batch, leaves the row PENDING on it
+//   k_dict_commit   per claim: the arena entry (its offset from one wave-aggregated bump), the slot
+//                   made resident with the key's words, the claiming row's id
+//   k_dict_resolve  per pending row: the (now resident) slot compares; a different key of the same
+//                   fingerprint goes on a retry list (probed again: the slot no longer misleads it)
+// A probe gives up after DICT_PROBE slots (the table is then too full: dict_map unclaims the
 // batch's fresh words, grows the table and maps the batch again).
 constexpr int DICT_PROBE = 256;
 constexpr uint64_t DICT_LOW = (1ULL << 40) - 1;
-constexpr int DICT_NCNT = 64;
+constexpr int DICT_NL = 64;  // claim lists (one per block residue: no hot append word)
+constexpr int64_t KID_PEND = (int64_t)1 << 62;
+constexpr uint64_t DICT_ID = (1ULL << 48) - 1;
 
-__global__ __launch_bounds__(256) void k_dict_lookup(uint64_t* __restrict__ dword, const int64_t* __restrict__ dkid,
-                                                     uint64_t dmask, const uint8_t* __restrict__ arena,
-                                                     const int64_t* __restrict__ koff,
-                                                     const uint8_t* __restrict__ kbytes,
-                                                     const uint8_t* __restrict__ kv, const uint8_t* __restrict__ rv,
-                                                     const int64_t* __restrict__ ts, int64_t n,
-                                                     int64_t* __restrict__ kid, int64_t* __restrict__ khash,
-                                                     int* __restrict__ fail) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (!(bit_get(kv, i) && bit_get(rv, i) && (ts == nullptr || ts[i] >= 0))) {
-      kid[i] = 0;
-      khash[i] = 0;
-      continue;
-    }
-    const int64_t o0 = koff[i], len = koff[i + 1] - o0;
-    const uint8_t* kb = kbytes + o0;
-    const bool sk = len <= 8 * KW_MAX;  // a short key: words, not bytes
-    uint64_t kw[KW_MAX];
-    if (sk) key_words(kb, len, kw);
-    const uint64_t h = sk ? hash_key_words(kw, len) : hash_bytes_dev(kb, len);
-    khash[i] = (int64_t)h;
-    const uint64_t fp = (h >> 40) & 0x3FFFFFULL;
-    const uint64_t fresh = (1ULL << 63) | (fp << 40) | (uint64_t)i;
-    uint64_t slot = h & dmask;
-    bool done = false;
-    for (int probe = 0; probe < DICT_PROBE && !done; probe++) {
-      uint64_t w = ld_relaxed(&dword[slot]);
-      if (w == 0) {
-        const uint64_t old = atomicCAS((unsigned long long*)&dword[slot], 0ULL, (unsigned long long)fresh);
-        if (old == 0) {
-          kid[i] = -(int64_t)(slot + 1);
-          done = true;
-          break;
+__device__ __forceinline__ int64_t entry_bytes(int64_t len) { return 16 + ((len + 7) & ~7LL); }
+
+#ifdef KHIP_TUNING
+// Tuning build: KHIP_DICT_HASHMASK keeps only these bits of every key hash (different keys then
+// share whole hashes, not just fingerprints: tests/test_gpu_dict.py).
+__constant__ uint64_t g_dict_hmask = ~0ULL;
+#endif
+
+// The key of batch row i: words (short keys), hash.
+struct DKey {
+  uint64_t kw[KW_MAX];
+  uint64_t h;
+  int64_t len;
+  const uint8_t* kb;
+  bool sk;
+};
+__device__ __forceinline__ void dkey_load(DKey& k, const int64_t* __restrict__ koff, const uint8_t* __restrict__ kbytes,
+                                          int64_t i) {
+  const int64_t o0 = koff[i];
+  k.len = koff[i + 1] - o0;
+  k.kb = kbytes + o0;
+  k.sk = k.len <= 8 * KW_MAX;
+  if (k.sk) key_words(k.kb, k.len, k.kw);
+  k.h = k.sk ? hash_key_words(k.kw, k.len) : hash_bytes_dev(k.kb, k.len);
+#ifdef KHIP_TUNING
+  k.h &= g_dict_hmask;
+#endif
+}
+
+// A resident slot (w0 fingerprint already matched) holds key k?
+__device__ __forceinline__ bool dslot_eq(const ulonglong2& a, const ulonglong2& b, const DKey& k,
+                                         const uint8_t* __restrict__ arena) {
+  const int64_t slen = (int64_t)(a.y >> 48);
+  if (k.len <= 16) return slen == k.len && b.x == k.kw[0] && b.y == (k.len > 8 ? k.kw[1] : 0ULL);
+  if (slen != (k.len < 0xFFFF ? k.len : 0xFFFF)) return false;
+  const int64_t o = (int64_t)(a.y & DICT_ID);
+  if (*(const uint64_t*)(arena + o) != k.h || *(const int64_t*)(arena + o + 8) != k.len) return false;
+  return k.sk ? key_words_eq_aligned(k.kw, arena + o + 16, k.len) : bytes_eq(arena + o + 16, k.kb, k.len);
+}
+
+// rows: null (row j = j) or a row list (the retry pass).  lists: DICT_NL regions of lcap slots.
+__global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slots, uint64_t dmask,
+                                                    const uint8_t* __restrict__ arena, const int64_t* __restrict__ koff,
+                                                    const uint8_t* __restrict__ kbytes, const uint8_t* __restrict__ kv,
+                                                    const uint8_t* __restrict__ rv, const int64_t* __restrict__ ts,
+                                                    const int64_t* __restrict__ rows, int64_t n,
+                                                    int64_t* __restrict__ kid, int64_t* __restrict__ khash,
+                                                    uint64_t* __restrict__ lists, int64_t lcap,
+                                                    unsigned long long* __restrict__ lcnt, int* __restrict__ fail,
+                                                    uint64_t fpm) {
+  const int lane = threadIdx.x & 63;
+  const int L = blockIdx.x & (DICT_NL - 1);
+  for (int64_t j0 = blockIdx.x * (int64_t)blockDim.x; j0 < n; j0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = j0 + threadIdx.x;
+    bool claimed = false;
+    uint64_t cslot = 0;
+    if (j < n) {
+      const int64_t i = rows ? rows[j] : j;
+      if (!(bit_get(kv, i) && bit_get(rv, i) && (ts == nullptr || ts[i] >= 0))) {
+        kid[i] = 0;
+        khash[i] = 0;
+      } else {
+        DKey k;
+        dkey_load(k, koff, kbytes, i);
+        khash[i] = (int64_t)k.h;
+        const uint64_t fp = (k.h >> 40) & fpm;
+        const uint64_t fresh = (1ULL << 63) | (fp << 40) | (uint64_t)i;
+        uint64_t slot = k.h & dmask;
+        bool done = false;
+        for (int probe = 0; probe < DICT_PROBE && !done; probe++) {
+          ulonglong2 a = slots[2 * slot];  // a stale empty / fresh word is settled by the CAS below
+          uint64_t w = a.x;
+          if (w == 0) {
+            const uint64_t old = atomicCAS((unsigned long long*)&slots[2 * slot].x, 0ULL, (unsigned long long)fresh);
+            if (old == 0) {
+              kid[i] = -(int64_t)(slot + 1);  // commit writes the id
+              claimed = true;
+              cslot = slot;
+              done = true;
+              break;
+            }
+            w = old;
+          }
+          if (((w >> 40) & 0x3FFFFFULL) == fp) {
+            if (w >> 63) {  // claimed by another row of this batch: resolved after the commit
+              kid[i] = -(int64_t)(slot + 1) - KID_PEND;
+              done = true;
+            } else {
+              const ulonglong2 b = slots[2 * slot + 1];
+              if (a.x != w) a = slots[2 * slot];  // (the word moved on since the first read)
+              if (dslot_eq(a, b, k, arena)) {
+                kid[i] = (int64_t)(a.y & DICT_ID);
+                done = true;
+              }
+            }
+          }
+          if (!done) slot = (slot + 1) & dmask;
         }
-        w = old;
-      }
-      if (((w >> 40) & 0x3FFFFFULL) == fp) {
-        if (w >> 63) {  // fresh claim by another row of this batch
-          const int64_t r2 = (int64_t)(w & ((1ULL << 40) - 1));
-          const int64_t p2 = koff[r2], l2 = koff[r2 + 1] - p2;
-          bool eq = l2 == len;
-          if (eq && sk) {
-            uint64_t ow[KW_MAX];
-            key_words(kbytes + p2, l2, ow);
-#pragma unroll
-            for (int k = 0; k < KW_MAX; k++) eq = eq && ow[k] == kw[k];
-          } else if (eq) {
-            eq = bytes_eq(kbytes + p2, kb, len);
-          }
-          if (eq) {
-            kid[i] = -(int64_t)(slot + 1);
-            done = true;
-          }
-        } else {  // resident
-          const int64_t o = (int64_t)((w & DICT_LOW) << 3);
-          const uint64_t eh = *(const uint64_t*)(arena + o);
-          const int64_t el = *(const int64_t*)(arena + o + 8);
-          if (eh == h && el == len && (sk ? key_words_eq_aligned(kw, arena + o + 16, len) : bytes_eq(arena + o + 16, kb, len))) {
-            kid[i] = o;
-            done = true;
-          }
+        if (!done) {
+          kid[i] = 0;
+          *fail = 1;
         }
       }
-      if (!done) slot = (slot + 1) & dmask;
     }
-    if (!done) {
-      kid[i] = 0;
-      *fail = 1;
+    // the wave's claims → list L (one append per wave)
+    const uint64_t bal = __ballot(claimed);
+    if (bal) {
+      const int leader = __ffsll((unsigned long long)bal) - 1;
+      unsigned long long base = 0;
+      if (lane == leader) base = atomicAdd(&lcnt[L], (unsigned long long)__popcll(bal));
+      base = __shfl(base, leader);
+      if (claimed) {
+        const uint64_t at = base + __popcll(bal & ((1ULL << lane) - 1));
+        if ((int64_t)at < lcap) lists[(uint64_t)L * lcap + at] = cslot;
+        else *fail = 2;  // (lcap covers every row a list's blocks can claim)
+      }
     }
   }
 }
 
-// Read-only dictionary probe (pull queries): key bytes → resident key id (arena offset), or -1
-// when the key was never seen.  Every dictionary word is resident between pushes.
-__global__ __launch_bounds__(256) void k_dict_find(const uint64_t* __restrict__ dword, const int64_t* __restrict__ dkid,
-                                                   uint64_t dmask, const uint8_t* __restrict__ arena,
+// One thread per claim (list L, entry t < lcnt[L]): arena entry, resident slot, the row's id.
+// bump[0] = the arena bytes used (one atomic per wave).
+__global__ __launch_bounds__(256) void k_dict_commit(ulonglong2* __restrict__ slots, const uint64_t* __restrict__ lists,
+                                                     int64_t lcap, const unsigned long long* __restrict__ lcnt,
+                                                     uint8_t* __restrict__ arena, unsigned long long* __restrict__ bump,
+                                                     const int64_t* __restrict__ koff, const uint8_t* __restrict__ kbytes,
+                                                     int64_t* __restrict__ kid, unsigned long long* __restrict__ nkeys) {
+  const int L = blockIdx.y;
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool on = t < (int64_t)lcnt[L];
+  uint64_t slot = 0, w = 0;
+  int64_t r = 0, eb = 0;
+  DKey k;
+  if (on) {
+    slot = lists[(uint64_t)L * lcap + t];
+    w = slots[2 * slot].x;
+    r = (int64_t)(w & DICT_LOW);
+    dkey_load(k, koff, kbytes, r);
+    eb = entry_bytes(k.len);
+  }
+  int64_t incl = eb;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  const int64_t tot = __shfl(incl, 63);
+  const int non = __popcll(__ballot(on));
+  unsigned long long base = 0;
+  if (lane == 0 && tot) {
+    base = atomicAdd(bump, (unsigned long long)tot);
+    atomicAdd(nkeys, (unsigned long long)non);
+  }
+  base = __shfl(base, 0);
+  if (!on) return;
+  const int64_t o = (int64_t)base + incl - eb;
+  *(uint64_t*)(arena + o) = k.h;
+  *(int64_t*)(arena + o + 8) = k.len;
+  if (k.sk) {
+    for (int q = 0; q < (int)((k.len + 7) >> 3); q++) ((uint64_t*)(arena + o + 16))[q] = k.kw[q];
+  } else {
+    for (int64_t b = 0; b < k.len; b++) arena[o + 16 + b] = k.kb[b];
+  }
+  const uint64_t fp = (w >> 40) & 0x3FFFFFULL;
+  const uint64_t lenw = (uint64_t)(k.len < 0xFFFF ? k.len : 0xFFFF) << 48;
+  slots[2 * slot + 1] = make_ulonglong2(k.len <= 16 ? k.kw[0] : 0ULL, k.len <= 16 && k.len > 8 ? k.kw[1] : 0ULL);
+  slots[2 * slot] = make_ulonglong2((1ULL << 62) | (fp << 40) | ((uint64_t)o >> 3), (uint64_t)o | lenw);
+  kid[r] = o;
+}
+
+// Rows left pending on a slot another row claimed: the slot is resident now.  A different key of
+// the same fingerprint goes on the retry list.
+__global__ __launch_bounds__(256) void k_dict_resolve(const ulonglong2* __restrict__ slots,
+                                                      const uint8_t* __restrict__ arena,
+                                                      const int64_t* __restrict__ koff,
+                                                      const uint8_t* __restrict__ kbytes, const int64_t* __restrict__ rows,
+                                                      int64_t n, int64_t* __restrict__ kid,
+                                                      int64_t* __restrict__ retry, unsigned long long* __restrict__ nretry) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = rows ? rows[j] : j;
+    const int64_t x = kid[i];
+    if (x >= -KID_PEND) continue;  // an id, or the claimer's (written by the commit)
+    const uint64_t slot = (uint64_t)(-(x + KID_PEND) - 1);
+    DKey k;
+    dkey_load(k, koff, kbytes, i);
+    const ulonglong2 a = slots[2 * slot], b = slots[2 * slot + 1];
+    if (dslot_eq(a, b, k, arena)) {
+      kid[i] = (int64_t)(a.y & DICT_ID);
+    } else {
+      kid[i] = 0;
+      retry[atomicAdd(nretry, 1ULL)] = i;
+    }
+  }
+}
+
+// Read-only dictionary probe (pull queries, join probes): key bytes → resident key id (arena
+// offset), or -1 when the key was never seen.  Every slot is resident between maps.
+__global__ __launch_bounds__(256) void k_dict_find(const ulonglong2* __restrict__ slots, uint64_t dmask,
+                                                   const uint8_t* __restrict__ arena,
                                                    const int64_t* __restrict__ koff, const uint8_t* __restrict__ kbytes,
-                                                   int64_t n, int64_t* __restrict__ kid) {
+                                                   int64_t n, int64_t* __restrict__ kid, uint64_t fpm) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t o0 = koff[i], len = koff[i + 1] - o0;
-    const uint8_t* kb = kbytes + o0;
-    const bool sk = len <= 8 * KW_MAX;
-    uint64_t kw[KW_MAX];
-    if (sk) key_words(kb, len, kw);
-    const uint64_t h = sk ? hash_key_words(kw, len) : hash_bytes_dev(kb, len);
-    const uint64_t fp = (h >> 40) & 0x3FFFFFULL;
-    uint64_t slot = h & dmask;
+    DKey k;
+    dkey_load(k, koff, kbytes, i);
+    const uint64_t fp = (k.h >> 40) & fpm;
+    uint64_t slot = k.h & dmask;
     int64_t found = -1;
     for (int probe = 0; probe <= (int)dmask && probe < (1 << 20); probe++) {
-      const uint64_t w = dword[slot];
-      if (w == 0) break;
-      if (((w >> 40) & 0x3FFFFFULL) == fp) {
-        const int64_t o = (int64_t)((w & DICT_LOW) << 3);
-        if (*(const uint64_t*)(arena + o) == h && *(const int64_t*)(arena + o + 8) == len &&
-            (sk ? key_words_eq_aligned(kw, arena + o + 16, len) : bytes_eq(arena + o + 16, kb, len))) {
-          found = o;
-          break;
-        }
+      const ulonglong2 a = slots[2 * slot];
+      if (a.x == 0) break;
+      if (((a.x >> 40) & 0x3FFFFFULL) == fp && dslot_eq(a, slots[2 * slot + 1], k, arena)) {
+        found = (int64_t)(a.y & DICT_ID);
+        break;
       }
       slot = (slot + 1) & dmask;
     }
@@ -523,42 +651,10 @@ __global__ __launch_bounds__(256) void k_dict_find(const uint64_t* __restrict__ 
   }
 }
 
-__device__ __forceinline__ int64_t entry_bytes(int64_t len) { return 16 + ((len + 7) & ~7LL); }
-
-// Per block of 256 dict slots: arena bytes needed by fresh entries; the fresh entries are added to
-// one of DICT_NCNT counters (the host sums them).
-__global__ __launch_bounds__(256) void k_dict_count(const uint64_t* __restrict__ dword, int64_t dcap,
-                                                    const int64_t* __restrict__ koff, int64_t* __restrict__ bsum,
-                                                    unsigned long long* __restrict__ nent) {
-  __shared__ unsigned long long acc, cnt;
-  if (threadIdx.x == 0) acc = cnt = 0;
-  __syncthreads();
-  const int64_t slot = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  int64_t b = 0;
-  if (slot < dcap) {
-    const uint64_t w = dword[slot];
-    if (w >> 63) {
-      const int64_t r = (int64_t)(w & DICT_LOW);
-      b = entry_bytes(koff[r + 1] - koff[r]);
-    }
-  }
-  const int c = (int)__popcll(__ballot(b != 0));
-  b = wave_sum(b);
-  if ((threadIdx.x & 63) == 0 && b) {
-    atomicAdd(&acc, (unsigned long long)b);
-    atomicAdd(&cnt, (unsigned long long)c);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    bsum[blockIdx.x] = (int64_t)acc;
-    if (cnt) atomicAdd(&nent[blockIdx.x & (DICT_NCNT - 1)], cnt);  // spread: no one hot word
-  }
-}
-
 // A failed map: the batch's fresh claims → empty (the table is as before the batch).
-__global__ __launch_bounds__(256) void k_dict_unclaim(uint64_t* __restrict__ dword, int64_t dcap) {
+__global__ __launch_bounds__(256) void k_dict_unclaim(ulonglong2* __restrict__ slots, int64_t dcap) {
   for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < dcap; s += (int64_t)gridDim.x * blockDim.x)
-    if (dword[s] >> 63) dword[s] = 0;
+    if (slots[2 * s].x >> 63) slots[2 * s] = make_ulonglong2(0ULL, 0ULL);
 }
 
 // Exclusive prefix sum of v[0..n) in place (single block); total added to *total.  Each thread
@@ -599,61 +695,17 @@ __global__ __launch_bounds__(1024) void k_scan_excl(int64_t* __restrict__ v, int
   if (threadIdx.x == 0) *total += carry;
 }
 
-__global__ __launch_bounds__(256) void k_dict_write(uint64_t* __restrict__ dword, int64_t* __restrict__ dkid,
-                                                    int64_t dcap, const int64_t* __restrict__ boff,
-                                                    int64_t arena_used, uint8_t* __restrict__ arena,
-                                                    const int64_t* __restrict__ koff,
-                                                    const uint8_t* __restrict__ kbytes,
-                                                    const int64_t* __restrict__ khash) {
-  __shared__ int64_t lds[256];
-  const int64_t slot = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  uint64_t w = 0;
-  int64_t b = 0, r = 0;
-  if (slot < dcap) {
-    w = dword[slot];
-    if (w >> 63) {
-      r = (int64_t)(w & ((1ULL << 40) - 1));
-      b = entry_bytes(koff[r + 1] - koff[r]);
-    }
-  }
-  lds[threadIdx.x] = b;
-  __syncthreads();
-  for (int off = 1; off < 256; off <<= 1) {
-    int64_t y = threadIdx.x >= off ? lds[threadIdx.x - off] : 0;
-    __syncthreads();
-    lds[threadIdx.x] += y;
-    __syncthreads();
-  }
-  if (b) {
-    const int64_t o = arena_used + boff[blockIdx.x] + lds[threadIdx.x] - b;
-    const int64_t len = koff[r + 1] - koff[r];
-    *(int64_t*)(arena + o) = khash[r];
-    *(int64_t*)(arena + o + 8) = len;
-    for (int64_t k = 0; k < len; k++) arena[o + 16 + k] = kbytes[koff[r] + k];
-    dkid[slot] = o;
-    dword[slot] = (1ULL << 62) | (((w >> 40) & 0x3FFFFFULL) << 40) | ((uint64_t)o >> 3);
-  }
-}
-
-__global__ __launch_bounds__(256) void k_kid_fixup(int64_t* __restrict__ kid, int64_t n,
-                                                   const int64_t* __restrict__ dkid) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t k = kid[i];
-    if (k < 0) kid[i] = dkid[-k - 1];
-  }
-}
-
-__global__ __launch_bounds__(256) void k_dict_rehash(const uint64_t* __restrict__ ow, const int64_t* __restrict__ ok,
-                                                     int64_t ocap, uint64_t* __restrict__ nw, int64_t* __restrict__ nk,
-                                                     uint64_t nmask, const uint8_t* __restrict__ arena) {
+__global__ __launch_bounds__(256) void k_dict_rehash(const ulonglong2* __restrict__ os, int64_t ocap,
+                                                     ulonglong2* __restrict__ ns, uint64_t nmask,
+                                                     const uint8_t* __restrict__ arena) {
   for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < ocap; s += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t w = ow[s];
-    if (w == 0) continue;
-    const int64_t o = ok[s];
-    const uint64_t h = *(const uint64_t*)(arena + o);
+    const ulonglong2 a = os[2 * s];
+    if (a.x == 0) continue;
+    const uint64_t h = *(const uint64_t*)(arena + (a.y & DICT_ID));
     uint64_t d = h & nmask;
-    while (atomicCAS((unsigned long long*)&nw[d], 0ULL, (unsigned long long)w) != 0ULL) d = (d + 1) & nmask;
-    nk[d] = o;
+    while (atomicCAS((unsigned long long*)&ns[2 * d].x, 0ULL, (unsigned long long)a.x) != 0ULL) d = (d + 1) & nmask;
+    ns[2 * d + 1] = os[2 * s + 1];
+    ns[2 * d].y = a.y;
   }
 }
 
@@ -666,40 +718,86 @@ static int grid_for(int64_t work, int per_block, int cap_blocks = 2048 * 8) {
 
 // ---- KeyDict (khip_dict.hpp)
 
+// The fingerprint bits a probe compares before the key (22; the tuning build's KHIP_DICT_FPMASK
+// narrows them so that different keys meet on claimed slots: the pending / retry rounds).
+static uint64_t dict_fp_mask() { return (uint64_t)knob("KHIP_DICT_FPMASK", 0x3FFFFF) & 0x3FFFFFULL; }
+
 static khip_status dict_grow(KeyDict& d, hipStream_t s, int64_t new_cap) {
-  DevBuf nw, nk;
-  KHIP_TRY(nw.ensure((size_t)new_cap * 8));
-  KHIP_TRY(nk.ensure((size_t)new_cap * 8));
-  KHIP_TRY_HIP(hipMemsetAsync(nw.p, 0, (size_t)new_cap * 8, s));
+  DevBuf ns;
+  KHIP_TRY(ns.ensure((size_t)new_cap * 32));
+  KHIP_TRY_HIP(hipMemsetAsync(ns.p, 0, (size_t)new_cap * 32, s));
   if (d.dcap > 0 && d.docc > 0) {
-    hipLaunchKernelGGL(k_dict_rehash, dim3(grid_for(d.dcap, 256)), dim3(256), 0, s, d.dword.as<uint64_t>(),
-                       d.dkid.as<int64_t>(), d.dcap, nw.as<uint64_t>(), nk.as<int64_t>(), (uint64_t)(new_cap - 1),
-                       d.arena.as<uint8_t>());
+    hipLaunchKernelGGL(k_dict_rehash, dim3(grid_for(d.dcap, 256)), dim3(256), 0, s, d.slots.as<ulonglong2>(), d.dcap,
+                       ns.as<ulonglong2>(), (uint64_t)(new_cap - 1), d.arena.as<uint8_t>());
     KHIP_TRY_HIP(hipGetLastError());
   }
   KHIP_TRY_HIP(hipStreamSynchronize(s));
-  d.dword.release();
-  d.dkid.release();
-  d.dword = nw;
-  d.dkid = nk;
-  nw.p = nk.p = nullptr;
+  d.slots.release();
+  d.slots = ns;
+  ns.p = nullptr;
   d.dcap = new_cap;
   return KHIP_OK;
 }
 
 khip_status dict_init(KeyDict& d, hipStream_t s) {
-  KHIP_TRY(d.fail.ensure(8 + 8 * DICT_NCNT));
+#ifdef KHIP_TUNING
+  const uint64_t hm = (uint64_t)knob("KHIP_DICT_HASHMASK", -1);
+  KHIP_TRY_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_dict_hmask), &hm, 8));
+#endif
+  // [0] probe failure | [8] arena bump | [16] keys added | [24] retries | [32..] DICT_NL list counts
+  KHIP_TRY(d.ctr.ensure(32 + 8 * DICT_NL));
   return dict_grow(d, s, 4096);
+}
+
+// One round over `rows` (null: every row): probe, commit the claims, resolve the pending rows.
+// Returns the rows to retry (a different key behind a pending row's fingerprint) in d.retry,
+// their count in *nretry; *failed when a probe ran out of budget (nothing committed then).
+static khip_status dict_round(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8_t* kbytes, const uint8_t* kv,
+                              const uint8_t* rv, const int64_t* ts, const int64_t* rows, int64_t n, int64_t* kid,
+                              int64_t* khash, int64_t* nretry, bool* failed) {
+  unsigned long long* c = d.ctr.as<unsigned long long>();
+  const int g = grid_for(n, 256);
+  // a list takes the claims of blocks L, L + 64, ...: at most every row those blocks visit
+  const int64_t lcap = ceil_div(g, DICT_NL) * 256 * ceil_div(n, 256LL * g);
+  KHIP_TRY(d.lists.ensure((size_t)lcap * DICT_NL * 8));
+  KHIP_TRY_HIP(hipMemsetAsync(c, 0, 8, s));
+  KHIP_TRY_HIP(hipMemsetAsync(c + 3, 0, 8 + 8 * DICT_NL, s));
+  hipLaunchKernelGGL(k_dict_probe, dim3(g), dim3(256), 0, s, d.slots.as<ulonglong2>(), (uint64_t)(d.dcap - 1),
+                     d.arena.as<uint8_t>(), koff, kbytes, kv, rv, ts, rows, n, kid, khash, d.lists.as<uint64_t>(), lcap,
+                     c + 4, (int*)c, dict_fp_mask());
+  KHIP_TRY_HIP(hipGetLastError());
+  unsigned long long h[4 + DICT_NL];
+  KHIP_TRY_HIP(hipMemcpyAsync(h, c, sizeof(h), hipMemcpyDeviceToHost, s));
+  KHIP_TRY_HIP(hipStreamSynchronize(s));
+  *failed = h[0] != 0;
+  *nretry = 0;
+  if (*failed) return KHIP_OK;
+  int64_t mx = 0;
+  for (int L = 0; L < DICT_NL; L++) mx = std::max<int64_t>(mx, (int64_t)h[4 + L]);
+  if (mx > 0) {
+    hipLaunchKernelGGL(k_dict_commit, dim3((unsigned)ceil_div(mx, 256), DICT_NL), dim3(256), 0, s,
+                       d.slots.as<ulonglong2>(), d.lists.as<uint64_t>(), lcap, c + 4, d.arena.as<uint8_t>(), c + 1, koff,
+                       kbytes, kid, c + 2);
+    KHIP_TRY_HIP(hipGetLastError());
+  }
+  KHIP_TRY(d.retry.ensure((size_t)std::max<int64_t>(n, 1) * 8));
+  hipLaunchKernelGGL(k_dict_resolve, dim3(g), dim3(256), 0, s, d.slots.as<ulonglong2>(), d.arena.as<uint8_t>(), koff,
+                     kbytes, rows, n, kid, d.retry.as<int64_t>(), c + 3);
+  KHIP_TRY_HIP(hipGetLastError());
+  unsigned long long r = 0;
+  KHIP_TRY_HIP(hipMemcpyAsync(&r, c + 3, 8, hipMemcpyDeviceToHost, s));
+  KHIP_TRY_HIP(hipStreamSynchronize(s));
+  *nretry = (int64_t)r;
+  return KHIP_OK;
 }
 
 khip_status dict_map(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8_t* kbytes, int64_t key_bytes_total,
                      const uint8_t* kv, const uint8_t* rv, const int64_t* ts, int64_t n, int64_t* kid, int64_t* khash) {
-  // room for the keys this batch may add: every row on the first map, then twice the last map's
-  // new keys (at least n / 16) — a batch that brings more fails its probes and is mapped again
-  // into a larger table, so the table tracks the key count, not the batch size (a table sized
-  // for every row of a 100M-record batch is 4 GB of probe words and scans)
+  // room for the keys this batch may add at load <= 1/2: every row on the first map, then twice
+  // the last map's new keys (at least n / 16) — a batch that brings more fails its probes and is
+  // mapped again into a larger table, so the table tracks the key count, not the batch size
   const int64_t est = d.last_added < 0 ? n : std::min<int64_t>(n, std::max<int64_t>({2 * d.last_added, n / 16, 4096}));
-  if (2 * (d.docc + est) > d.dcap) KHIP_TRY(dict_grow(d, s, next_pow2(4 * (d.docc + est))));
+  if (2 * (d.docc + est) > d.dcap) KHIP_TRY(dict_grow(d, s, next_pow2(2 * (d.docc + est))));
   const int64_t need = d.arena_used + key_bytes_total + 16 * n + 16;
   if ((size_t)need > d.arena.bytes) {
     DevBuf na;
@@ -710,48 +808,43 @@ khip_status dict_map(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8
     d.arena = na;
     na.p = nullptr;
   }
-  unsigned long long* nent = (unsigned long long*)(d.fail.as<char>() + 8);
-  for (int attempt = 0;; attempt++) {
-    KHIP_TRY_HIP(hipMemsetAsync(d.fail.p, 0, 8 + 8 * DICT_NCNT, s));
-    hipLaunchKernelGGL(k_dict_lookup, dim3(grid_for(n, 256)), dim3(256), 0, s, d.dword.as<uint64_t>(),
-                       d.dkid.as<int64_t>(), (uint64_t)(d.dcap - 1), d.arena.as<uint8_t>(), koff, kbytes, kv, rv, ts,
-                       n, kid, khash, d.fail.as<int>());
-    KHIP_TRY_HIP(hipGetLastError());
-    int failed = 0;
-    KHIP_TRY_HIP(hipMemcpyAsync(&failed, d.fail.p, 4, hipMemcpyDeviceToHost, s));
-    KHIP_TRY_HIP(hipStreamSynchronize(s));
-    if (!failed) break;
-    if (attempt >= 6 || d.dcap >= ((int64_t)1 << 34)) return fail(KHIP_E_DEVICE, "key dictionary probe budget exhausted");
-    hipLaunchKernelGGL(k_dict_unclaim, dim3(grid_for(d.dcap, 256)), dim3(256), 0, s, d.dword.as<uint64_t>(), d.dcap);
-    KHIP_TRY(dict_grow(d, s, d.dcap * 4));
+  unsigned long long* c = d.ctr.as<unsigned long long>();
+  const unsigned long long start[3] = {0ULL, (unsigned long long)d.arena_used, 0ULL};
+  KHIP_TRY_HIP(hipMemcpyAsync(c, start, 24, hipMemcpyHostToDevice, s));
+  const int64_t* rows = nullptr;
+  int64_t m = n;
+  DevBuf rl;  // a retry round's rows (the previous round's retry list)
+  for (int round = 0, grown = 0; m > 0; round++) {
+    int64_t nretry = 0;
+    bool failed = false;
+    KHIP_TRY(dict_round(d, s, koff, kbytes, kv, rv, ts, rows, m, kid, khash, &nretry, &failed));
+    if (failed) {  // undo this round's claims, grow, and map its rows again
+      if (++grown > 6 || d.dcap >= ((int64_t)1 << 34)) return fail(KHIP_E_DEVICE, "key dictionary probe budget exhausted");
+      hipLaunchKernelGGL(k_dict_unclaim, dim3(grid_for(d.dcap, 256)), dim3(256), 0, s, d.slots.as<ulonglong2>(), d.dcap);
+      KHIP_TRY_HIP(hipGetLastError());
+      KHIP_TRY(dict_grow(d, s, d.dcap * 4));
+      continue;
+    }
+    if (round > 64) return fail(KHIP_E_DEVICE, "key dictionary: rows unresolved after 64 rounds");
+    if (nretry == 0) break;
+    KHIP_TRY(rl.ensure((size_t)nretry * 8));
+    KHIP_TRY_HIP(hipMemcpyAsync(rl.p, d.retry.p, (size_t)nretry * 8, hipMemcpyDeviceToDevice, s));
+    rows = rl.as<int64_t>();
+    m = nretry;
   }
-  const int64_t dnb = ceil_div(d.dcap, 256);
-  KHIP_TRY(d.bsum.ensure((dnb + 1) * 8));
-  hipLaunchKernelGGL(k_dict_count, dim3(dnb), dim3(256), 0, s, d.dword.as<uint64_t>(), d.dcap, koff,
-                     d.bsum.as<int64_t>(), nent);
-  int64_t* dtotal = d.bsum.as<int64_t>() + dnb;
-  KHIP_TRY_HIP(hipMemsetAsync(dtotal, 0, 8, s));
-  hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, d.bsum.as<int64_t>(), dnb, dtotal);
-  hipLaunchKernelGGL(k_dict_write, dim3(dnb), dim3(256), 0, s, d.dword.as<uint64_t>(), d.dkid.as<int64_t>(), d.dcap,
-                     d.bsum.as<int64_t>(), d.arena_used, d.arena.as<uint8_t>(), koff, kbytes, khash);
-  hipLaunchKernelGGL(k_kid_fixup, dim3(grid_for(n, 256)), dim3(256), 0, s, kid, n, d.dkid.as<int64_t>());
-  KHIP_TRY_HIP(hipGetLastError());
-  int64_t added = 0;
-  unsigned long long cnts[DICT_NCNT], keys = 0;
-  KHIP_TRY_HIP(hipMemcpyAsync(&added, dtotal, 8, hipMemcpyDeviceToHost, s));
-  KHIP_TRY_HIP(hipMemcpyAsync(cnts, nent, sizeof(cnts), hipMemcpyDeviceToHost, s));
+  unsigned long long h[3];
+  KHIP_TRY_HIP(hipMemcpyAsync(h, c, 24, hipMemcpyDeviceToHost, s));
   KHIP_TRY_HIP(hipStreamSynchronize(s));
-  for (int k = 0; k < DICT_NCNT; k++) keys += cnts[k];
-  d.arena_used += added;
-  d.docc += (int64_t)keys;
-  d.last_added = (int64_t)keys;
+  d.arena_used = (int64_t)h[1];
+  d.docc += (int64_t)h[2];
+  d.last_added = (int64_t)h[2];
   return KHIP_OK;
 }
 
 khip_status dict_find(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8_t* kbytes, int64_t n, int64_t* kid) {
   if (n <= 0) return KHIP_OK;
-  hipLaunchKernelGGL(k_dict_find, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, d.dword.as<uint64_t>(),
-                     d.dkid.as<int64_t>(), (uint64_t)(d.dcap - 1), d.arena.as<uint8_t>(), koff, kbytes, n, kid);
+  hipLaunchKernelGGL(k_dict_find, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, d.slots.as<ulonglong2>(),
+                     (uint64_t)(d.dcap - 1), d.arena.as<uint8_t>(), koff, kbytes, n, kid, dict_fp_mask());
   KHIP_TRY_HIP(hipGetLastError());
   return KHIP_OK;
 }
@@ -763,14 +856,14 @@ khip_status dict_clear(KeyDict& d, hipStream_t s) {
   const int64_t keep = std::max<int64_t>(4096, next_pow2(4 * std::max<int64_t>(held, 1)));
   d.docc = 0;
   if (d.dcap >= 4 * keep) KHIP_TRY(dict_grow(d, s, keep));
-  if (d.dcap) KHIP_TRY_HIP(hipMemsetAsync(d.dword.p, 0, d.dcap * 8, s));
+  if (d.dcap) KHIP_TRY_HIP(hipMemsetAsync(d.slots.p, 0, d.dcap * 32, s));
   if (held > 0) d.last_added = held;  // the next map re-inserts about as many
   d.arena_used = 0;
   return KHIP_OK;
 }
 
 void dict_release(KeyDict& d) {
-  DevBuf* bufs[] = {&d.dword, &d.dkid, &d.arena, &d.bsum, &d.fail};
+  DevBuf* bufs[] = {&d.slots, &d.arena, &d.ctr, &d.lists, &d.retry};
   for (DevBuf* b : bufs) b->release();
   d.dcap = d.docc = d.arena_used = 0;
 }

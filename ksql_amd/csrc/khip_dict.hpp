@@ -5,18 +5,19 @@
 // (S/JoinParamsFactory.java:65-84 only requires both join sides' key types to
 // match).  The dictionary maps key bytes to a stable int64 id — the byte offset of the key's
 // entry in an append-only arena — so every downstream kernel works on 8-byte ids.
-//   dword[slot]: 0 empty | fresh claim: bit63 | fp22 << 40 | batch row (40 bits)
-//                        | resident:    bit62 | fp22 << 40
+//   slot (32 B): [dict word][id | len << 48][first 16 key bytes as two words]
+//     dict word: 0 empty | fresh claim: bit63 | fp22 << 40 | batch row (40 bits)
+//                        | resident:    bit62 | fp22 << 40 | id / 8
 //   arena entry at id o (8-aligned): [u64 hash][i64 len][bytes, padded to 8]
-// Kernels live in khip_agg.hip (k_dict_lookup / k_dict_count / k_dict_write / k_kid_fixup,
-// k_dict_find, k_dict_rehash).
+// A map: k_dict_probe (claims, in-place compares, pending rows) → k_dict_commit (per claim) →
+// k_dict_resolve (per pending row); kernels in khip_agg.hip.
 #pragma once
 #include "khip_util.hpp"
 
 namespace khip {
 
 struct KeyDict {
-  DevBuf dword, dkid, arena, bsum, fail;
+  DevBuf slots, arena, ctr, lists, retry;
   int64_t dcap = 0, docc = 0, arena_used = 0;
   int64_t last_added = -1;  // keys the last map inserted (-1: no map yet)
 };
