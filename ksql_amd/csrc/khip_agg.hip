@@ -416,18 +416,18 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ ta
 // (8-aligned): [u64 hash][i64 len][bytes, padded to 8].  A map is three passes, none over the
 // whole table:
 //   k_dict_probe    per row: hash, probe; a resident slot compares in place; an empty slot is
-//                   claimed (fresh word naming the row; the slot goes to one of DICT_NL claim lists,
-//                   one wave-aggregated append); a fresh slot of the same fingerprint, claimed by
+//                   claimed (fresh word naming the row; the slot and its arena entry's place go to
+//                   one of DICT_NL claim lists, one block-aggregated append); a fresh slot of the same fingerprint, claimed by
 //                   another row of this batch, leaves the row PENDING on it
-//   k_dict_commit   per claim: the arena entry (its offset from one wave-aggregated bump), the slot
-//                   made resident with the key's words, the claiming row's id
+//   k_dict_commit   per claim: the arena entry (its list's base + its place in the list), the slot
+//                   made resident with the key's words, the claiming row's id (no atomics)
 //   k_dict_resolve  per pending row: the (now resident) slot compares; a different key of the same
 //                   fingerprint goes on a retry list (probed again: the slot no longer misleads it)
 // A probe gives up after DICT_PROBE slots (the table is then too full: dict_map unclaims the
 // batch's fresh words, grows the table and maps the batch again).
 constexpr int DICT_PROBE = 256;
 constexpr uint64_t DICT_LOW = (1ULL << 40) - 1;
-constexpr int DICT_NL = 64;  // claim lists (one per block residue: no hot append word)
+constexpr int DICT_NL = 1024;  // claim lists (one per block residue: no hot append word)
 constexpr int64_t KID_PEND = (int64_t)1 << 62;
 constexpr uint64_t DICT_ID = (1ULL << 48) - 1;
 
@@ -471,7 +471,8 @@ __device__ __forceinline__ bool dslot_eq(const ulonglong2& a, const ulonglong2& 
   return k.sk ? key_words_eq_aligned(k.kw, arena + o + 16, k.len) : bytes_eq(arena + o + 16, k.kb, k.len);
 }
 
-// rows: null (row j = j) or a row list (the retry pass).  lists: DICT_NL regions of lcap slots.
+// rows: null (row j = j) or a row list (the retry pass).  lists: DICT_NL regions of lcap entries
+// [slot | the entry's byte offset in its list << 34]; lw[L]: entries << 40 | entry bytes of list L.
 __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slots, uint64_t dmask,
                                                     const uint8_t* __restrict__ arena, const int64_t* __restrict__ koff,
                                                     const uint8_t* __restrict__ kbytes, const uint8_t* __restrict__ kv,
@@ -479,14 +480,16 @@ __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slo
                                                     const int64_t* __restrict__ rows, int64_t n,
                                                     int64_t* __restrict__ kid, int64_t* __restrict__ khash,
                                                     uint64_t* __restrict__ lists, int64_t lcap,
-                                                    unsigned long long* __restrict__ lcnt, int* __restrict__ fail,
+                                                    unsigned long long* __restrict__ lw, int* __restrict__ fail,
                                                     uint64_t fpm) {
-  const int lane = threadIdx.x & 63;
+  __shared__ unsigned long long wsum[4];  // per wave: claims << 40 | entry bytes
+  __shared__ unsigned long long bbase;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int L = blockIdx.x & (DICT_NL - 1);
   for (int64_t j0 = blockIdx.x * (int64_t)blockDim.x; j0 < n; j0 += (int64_t)gridDim.x * blockDim.x) {
     const int64_t j = j0 + threadIdx.x;
     bool claimed = false;
-    uint64_t cslot = 0;
+    uint64_t cslot = 0, eb = 0;
     if (j < n) {
       const int64_t i = rows ? rows[j] : j;
       if (!(bit_get(kv, i) && bit_get(rv, i) && (ts == nullptr || ts[i] >= 0))) {
@@ -509,6 +512,7 @@ __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slo
               kid[i] = -(int64_t)(slot + 1);  // commit writes the id
               claimed = true;
               cslot = slot;
+              eb = (uint64_t)entry_bytes(k.len);
               done = true;
               break;
             }
@@ -535,58 +539,48 @@ __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slo
         }
       }
     }
-    // the wave's claims → list L (one append per wave)
-    const uint64_t bal = __ballot(claimed);
-    if (bal) {
-      const int leader = __ffsll((unsigned long long)bal) - 1;
-      unsigned long long base = 0;
-      if (lane == leader) base = atomicAdd(&lcnt[L], (unsigned long long)__popcll(bal));
-      base = __shfl(base, leader);
-      if (claimed) {
-        const uint64_t at = base + __popcll(bal & ((1ULL << lane) - 1));
-        if ((int64_t)at < lcap) lists[(uint64_t)L * lcap + at] = cslot;
-        else *fail = 2;  // (lcap covers every row a list's blocks can claim)
-      }
+    // the block's claims → list L: one atomic per block and tile for both the count and the bytes
+    const uint64_t x = claimed ? ((1ULL << 40) | eb) : 0ULL;
+    uint64_t incl = x;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint64_t y = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint64_t before = 0, tot = 0;
+    for (int k = 0; k < 4; k++) {
+      before += k < wave ? wsum[k] : 0;
+      tot += wsum[k];
+    }
+    if (threadIdx.x == 0) bbase = tot ? atomicAdd(&lw[L], (unsigned long long)tot) : 0ULL;
+    __syncthreads();
+    if (claimed) {
+      const uint64_t at = bbase + before + incl - x;  // this claim's entries << 40 | bytes before it
+      const uint64_t idx = at >> 40, boff = at & ((1ULL << 40) - 1);
+      if ((int64_t)idx < lcap && boff < (1ULL << 30)) lists[(uint64_t)L * lcap + idx] = cslot | (boff << 34);
+      else *fail = 2;  // (lcap covers every row a list's blocks can claim)
     }
   }
 }
 
-// One thread per claim (list L, entry t < lcnt[L]): arena entry, resident slot, the row's id.
-// bump[0] = the arena bytes used (one atomic per wave).
+// One thread per claim (list L, entry t): the arena entry at its list's base + its byte offset, the
+// slot made resident with the key's words, the claiming row's id.  lbase[L]: the list's arena base.
 __global__ __launch_bounds__(256) void k_dict_commit(ulonglong2* __restrict__ slots, const uint64_t* __restrict__ lists,
-                                                     int64_t lcap, const unsigned long long* __restrict__ lcnt,
-                                                     uint8_t* __restrict__ arena, unsigned long long* __restrict__ bump,
+                                                     int64_t lcap, const unsigned long long* __restrict__ lw,
+                                                     const int64_t* __restrict__ lbase, uint8_t* __restrict__ arena,
                                                      const int64_t* __restrict__ koff, const uint8_t* __restrict__ kbytes,
-                                                     int64_t* __restrict__ kid, unsigned long long* __restrict__ nkeys) {
+                                                     int64_t* __restrict__ kid) {
   const int L = blockIdx.y;
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  const bool on = t < (int64_t)lcnt[L];
-  uint64_t slot = 0, w = 0;
-  int64_t r = 0, eb = 0;
+  if (t >= (int64_t)(lw[L] >> 40)) return;
+  const uint64_t le = lists[(uint64_t)L * lcap + t];
+  const uint64_t slot = le & ((1ULL << 34) - 1);
+  const uint64_t w = slots[2 * slot].x;
+  const int64_t r = (int64_t)(w & DICT_LOW);
   DKey k;
-  if (on) {
-    slot = lists[(uint64_t)L * lcap + t];
-    w = slots[2 * slot].x;
-    r = (int64_t)(w & DICT_LOW);
-    dkey_load(k, koff, kbytes, r);
-    eb = entry_bytes(k.len);
-  }
-  int64_t incl = eb;
-  for (int off = 1; off < 64; off <<= 1) {
-    const int64_t y = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += y;
-  }
-  const int64_t tot = __shfl(incl, 63);
-  const int non = __popcll(__ballot(on));
-  unsigned long long base = 0;
-  if (lane == 0 && tot) {
-    base = atomicAdd(bump, (unsigned long long)tot);
-    atomicAdd(nkeys, (unsigned long long)non);
-  }
-  base = __shfl(base, 0);
-  if (!on) return;
-  const int64_t o = (int64_t)base + incl - eb;
+  dkey_load(k, koff, kbytes, r);
+  const int64_t o = lbase[L] + (int64_t)(le >> 34);
   *(uint64_t*)(arena + o) = k.h;
   *(int64_t*)(arena + o + 8) = k.len;
   if (k.sk) {
@@ -744,40 +738,53 @@ khip_status dict_init(KeyDict& d, hipStream_t s) {
   const uint64_t hm = (uint64_t)knob("KHIP_DICT_HASHMASK", -1);
   KHIP_TRY_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_dict_hmask), &hm, 8));
 #endif
-  // [0] probe failure | [8] arena bump | [16] keys added | [24] retries | [32..] DICT_NL list counts
-  KHIP_TRY(d.ctr.ensure(32 + 8 * DICT_NL));
+  KHIP_TRY(d.ctr.ensure(32 + 16 * DICT_NL));  // (dict_round's counters)
   return dict_grow(d, s, 4096);
 }
 
 // One round over `rows` (null: every row): probe, commit the claims, resolve the pending rows.
 // Returns the rows to retry (a different key behind a pending row's fingerprint) in d.retry,
 // their count in *nretry; *failed when a probe ran out of budget (nothing committed then).
+// Counters (d.ctr, u64): [0] probe failure | [1] arena bytes used | [2] keys added | [3] retries |
+// [4 ..] DICT_NL list words | then DICT_NL list arena bases.
 static khip_status dict_round(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8_t* kbytes, const uint8_t* kv,
                               const uint8_t* rv, const int64_t* ts, const int64_t* rows, int64_t n, int64_t* kid,
                               int64_t* khash, int64_t* nretry, bool* failed) {
   unsigned long long* c = d.ctr.as<unsigned long long>();
+  unsigned long long* lw = c + 4;
+  int64_t* lbase = (int64_t*)(c + 4 + DICT_NL);
   const int g = grid_for(n, 256);
-  // a list takes the claims of blocks L, L + 64, ...: at most every row those blocks visit
+  // a list takes the claims of blocks L, L + DICT_NL, ...: at most every row those blocks visit
   const int64_t lcap = ceil_div(g, DICT_NL) * 256 * ceil_div(n, 256LL * g);
   KHIP_TRY(d.lists.ensure((size_t)lcap * DICT_NL * 8));
   KHIP_TRY_HIP(hipMemsetAsync(c, 0, 8, s));
   KHIP_TRY_HIP(hipMemsetAsync(c + 3, 0, 8 + 8 * DICT_NL, s));
   hipLaunchKernelGGL(k_dict_probe, dim3(g), dim3(256), 0, s, d.slots.as<ulonglong2>(), (uint64_t)(d.dcap - 1),
                      d.arena.as<uint8_t>(), koff, kbytes, kv, rv, ts, rows, n, kid, khash, d.lists.as<uint64_t>(), lcap,
-                     c + 4, (int*)c, dict_fp_mask());
+                     lw, (int*)c, dict_fp_mask());
   KHIP_TRY_HIP(hipGetLastError());
-  unsigned long long h[4 + DICT_NL];
-  KHIP_TRY_HIP(hipMemcpyAsync(h, c, sizeof(h), hipMemcpyDeviceToHost, s));
+  std::vector<unsigned long long> h(4 + DICT_NL);
+  KHIP_TRY_HIP(hipMemcpyAsync(h.data(), c, h.size() * 8, hipMemcpyDeviceToHost, s));
   KHIP_TRY_HIP(hipStreamSynchronize(s));
   *failed = h[0] != 0;
   *nretry = 0;
   if (*failed) return KHIP_OK;
-  int64_t mx = 0;
-  for (int L = 0; L < DICT_NL; L++) mx = std::max<int64_t>(mx, (int64_t)h[4 + L]);
+  // each list's arena region: the prefix of the lists' entry bytes after the arena's used part
+  std::vector<int64_t> base(DICT_NL);
+  int64_t used = (int64_t)h[1], mx = 0, keys = 0;
+  for (int L = 0; L < DICT_NL; L++) {
+    base[L] = used;
+    used += (int64_t)(h[4 + L] & ((1ULL << 40) - 1));
+    mx = std::max<int64_t>(mx, (int64_t)(h[4 + L] >> 40));
+    keys += (int64_t)(h[4 + L] >> 40);
+  }
+  const unsigned long long tot[2] = {(unsigned long long)used, (unsigned long long)((int64_t)h[2] + keys)};
   if (mx > 0) {
+    KHIP_TRY_HIP(hipMemcpyAsync(lbase, base.data(), DICT_NL * 8, hipMemcpyHostToDevice, s));
+    KHIP_TRY_HIP(hipMemcpyAsync(c + 1, tot, 16, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_dict_commit, dim3((unsigned)ceil_div(mx, 256), DICT_NL), dim3(256), 0, s,
-                       d.slots.as<ulonglong2>(), d.lists.as<uint64_t>(), lcap, c + 4, d.arena.as<uint8_t>(), c + 1, koff,
-                       kbytes, kid, c + 2);
+                       d.slots.as<ulonglong2>(), d.lists.as<uint64_t>(), lcap, lw, lbase, d.arena.as<uint8_t>(), koff,
+                       kbytes, kid);
     KHIP_TRY_HIP(hipGetLastError());
   }
   KHIP_TRY(d.retry.ensure((size_t)std::max<int64_t>(n, 1) * 8));
@@ -786,7 +793,7 @@ static khip_status dict_round(KeyDict& d, hipStream_t s, const int64_t* koff, co
   KHIP_TRY_HIP(hipGetLastError());
   unsigned long long r = 0;
   KHIP_TRY_HIP(hipMemcpyAsync(&r, c + 3, 8, hipMemcpyDeviceToHost, s));
-  KHIP_TRY_HIP(hipStreamSynchronize(s));
+  KHIP_TRY_HIP(hipStreamSynchronize(s));  // (also: `base` / `tot` were read)
   *nretry = (int64_t)r;
   return KHIP_OK;
 }

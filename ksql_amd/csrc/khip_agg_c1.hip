@@ -723,6 +723,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #endif
 
 // ------------------------------------------------------------------ k_c1_merge
+// KHIP_C1M_DEFER: the record loops test for a full table once, after the item's records, not after
+// every chunk (the test is an LDS read that drains every outstanding LDS operation of the wave;
+// a full table cannot overflow the claim list: claims are table slots).
+#ifndef KHIP_C1M_DEFER
+#define KHIP_C1M_DEFER 0
+#endif
+#ifndef KHIP_C1M_NOLOAD
+#define KHIP_C1M_NOLOAD 0
+#endif
+// KHIP_C1M_NOLIST: no claim list — a record's claim only counts (one non-returning LDS add per
+// wave), and the count / write-out / clear phases walk the wave's slice of the table instead.
+#ifndef KHIP_C1M_NOLIST
+#define KHIP_C1M_NOLIST 0
+#endif
 struct C1Q {
   int32_t log2P, fbits, log2H, sw, hv_active, hv_op, hmax;
   int64_t size, adv, cmax, hv_i64;
@@ -955,6 +969,15 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
   // records li = l0 + thread + u NT of the item whose segments are in LDS (indices clamped to the
   // last record: every load is unconditional, so the waits stay counted)
   auto load = [&](uint64_t (&x)[AU], uint32_t (&tx)[AU], int64_t l0, int64_t rn, int nseg, int segb) {
+#if KHIP_C1M_NOLOAD  // timing experiment only (wrong results): records synthesized, no lookup, no load
+#pragma unroll
+    for (int u = 0; u < AU; u++) {
+      const uint32_t li = (uint32_t)(l0 + threadIdx.x + (int64_t)u * NT);
+      x[u] = ((uint64_t)((li * 2654435761u) % 1400u) << 32) | (uint32_t)tmin32;
+      tx[u] = 0;
+    }
+    return;
+#endif
 #pragma unroll
     for (int u = 0; u < AU; u++) {
       int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
@@ -1120,7 +1143,14 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
         bool cl[AU];
 #pragma unroll
         for (int u = 0; u < AU; u++) cl[u] = claimed[u] && id[u] != EMPTY;
-        mg_list_append_n<AU>(cl, e, list, &nnew);
+        if (KHIP_C1M_NOLIST) {
+          int tot = 0;
+#pragma unroll
+          for (int u = 0; u < AU; u++) tot += __popcll(__ballot(cl[u]));
+          if (lane == 0 && tot) __hip_atomic_fetch_add(&nnew, tot, WG_RLX);
+        } else {
+          mg_list_append_n<AU>(cl, e, list, &nnew);
+        }
       }
 #pragma unroll
       for (int u = 0; u < AU; u++) {
@@ -1134,12 +1164,12 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       for (int64_t c = 0; c < nch; c += 2) {
         if (r32) apply(ra, ta, c * AU * NT, std::true_type{});
         else apply(ra, ta, c * AU * NT, std::false_type{});
-        if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
+        if (!KHIP_C1M_DEFER && (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax)) break;
         if (c + 2 < nch) load(ra, ta, (c + 2) * AU * NT, rn, nseg, segb);
         if (c + 1 >= nch) break;
         if (r32) apply(rb, tb, (c + 1) * AU * NT, std::true_type{});
         else apply(rb, tb, (c + 1) * AU * NT, std::false_type{});
-        if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
+        if (!KHIP_C1M_DEFER && (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax)) break;
         if (c + 3 < nch) load(rb, tb, (c + 3) * AU * NT, rn, nseg, segb);
       }
     }
@@ -1151,11 +1181,13 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       load01(nx);
     }
     C1M_T(1);
-    const int nl = nnew < H ? nnew : H;
+    const int nl = KHIP_C1M_NOLIST ? H : (nnew < H ? nnew : H);  // NOLIST: the walks cover the table
+    // entry of walk position i: the list's, or (NOLIST) the table slot itself
+    auto walk_e = [&](int i) -> uint32_t { return KHIP_C1M_NOLIST ? (uint32_t)i : (uint32_t)list[i]; };
     if (lovf || nnew > q.hmax) {  // more groups than the table takes: retried with 2x sub-passes
       if (threadIdx.x == 0) fail[p] |= 1;
       for (int i = threadIdx.x; i < nl; i += NT) {
-        const uint32_t e = list[i];
+        const uint32_t e = walk_e(i);
         ids[e] = EMPTY;
         rt[e] = 0u;
         ct[e] = 0u;
@@ -1190,7 +1222,8 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     int nnw = 0;
     for (int k = lb0; k < lb1; k += 64) {
       const int i = k + lane;
-      const bool isnew = i < lb1 && !(rt[list[i]] & RT_MATCHED);
+      const uint32_t e = i < lb1 ? walk_e(i) : dummy;
+      const bool isnew = i < lb1 && (!KHIP_C1M_NOLIST || ids[e] != EMPTY) && !(rt[e] & RT_MATCHED);
       nnw += (int)__popcll(__ballot(isnew));
     }
     // 3. per-wave row counts → the partition's region range (one atomic per work item)
@@ -1269,9 +1302,10 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     const uint32_t wmask = wbits ? (1u << wbits) - 1u : 0u;
     for (int k = lb0; k < lb1; k += 64) {
       const int i = k + lane;
-      const uint32_t e = i < lb1 ? list[i] : dummy;
+      const uint32_t e = i < lb1 ? walk_e(i) : dummy;
       const uint32_t rv = rt[e];
-      const bool isnew = i < lb1 && !(rv & RT_MATCHED);
+      const bool used = i < lb1 && (!KHIP_C1M_NOLIST || ids[e] != EMPTY);
+      const bool isnew = used && !(rv & RT_MATCHED);
       const uint64_t bl = __ballot(isnew);
       if (isnew) {
         const uint64_t ri = cur + __popcll(bl & lt);
@@ -1295,7 +1329,7 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
         nh += q.hv_active && now ? 1 : 0;
         if (q.chg) q.chg[(uint64_t)p * q.cmax + ri] = (uint8_t)(CHG_TOUCHED | (now ? CHG_NEW : 0));
       }
-      if (i < lb1) {  // every listed entry leaves cleared for the next item
+      if (used) {  // every listed (used) entry leaves cleared for the next item
         ids[e] = EMPTY;
         rt[e] = 0u;
         ct[e] = 0u;
@@ -1726,11 +1760,19 @@ __device__ __forceinline__ void c1v_clear(const C1VQ& q, char* smem, int e) {
 
 // One (record or pane) contribution into delta entry e: row time, then the update planes.
 // cv: the argument's non-null count (a record: 0 / 1), sum its bits (sum), mn / mx its order keys.
+// KHIP_C1V_CONDMM: the MIN / MAX / row-time planes are read first (a plain LDS read: lanes of one
+// entry broadcast, no bank conflict) and updated by an atomic only when the record moves them — most
+// records of a busy entry do not, and same-entry atomics of one wave serialize.  A stale read only
+// costs an atomic that changes nothing: the planes move one way.
+#ifndef KHIP_C1V_CONDMM
+#define KHIP_C1V_CONDMM 0
+#endif
 template <int PM>
 __device__ __forceinline__ void c1v_add(const C1VQ& q, char* smem, uint32_t e, uint32_t tr, uint32_t cs, uint32_t cv,
                                         uint64_t sum, int64_t mn, int64_t mx) {
   const C1VP<PM> v{q};
-  __hip_atomic_fetch_max(&c1v_plane<uint32_t>(smem, q.off_rt)[e], tr, WG_RLX);
+  KLDS uint32_t* prt = &c1v_plane<uint32_t>(smem, q.off_rt)[e];
+  if (!KHIP_C1V_CONDMM || tr > *prt) __hip_atomic_fetch_max(prt, tr, WG_RLX);
   if (v.star() && cs) __hip_atomic_fetch_add(&c1v_plane<uint32_t>(smem, q.off_star)[e], cs, WG_RLX);
   if (cv) {
     if (v.cnt()) __hip_atomic_fetch_add(&c1v_plane<uint32_t>(smem, q.off_cnt)[e], cv, WG_RLX);
@@ -1743,8 +1785,14 @@ __device__ __forceinline__ void c1v_add(const C1VQ& q, char* smem, uint32_t e, u
         __hip_atomic_fetch_add(&c1v_plane<uint64_t>(smem, q.off_sum)[e], sum, WG_RLX);
       }
     }
-    if (v.mn()) __hip_atomic_fetch_min(&c1v_plane<int64_t>(smem, q.off_min)[e], mn, WG_RLX);
-    if (v.mx()) __hip_atomic_fetch_max(&c1v_plane<int64_t>(smem, q.off_max)[e], mx, WG_RLX);
+    if (v.mn()) {
+      KLDS int64_t* pm = &c1v_plane<int64_t>(smem, q.off_min)[e];
+      if (!KHIP_C1V_CONDMM || mn < *pm) __hip_atomic_fetch_min(pm, mn, WG_RLX);
+    }
+    if (v.mx()) {
+      KLDS int64_t* pm = &c1v_plane<int64_t>(smem, q.off_max)[e];
+      if (!KHIP_C1V_CONDMM || mx > *pm) __hip_atomic_fetch_max(pm, mx, WG_RLX);
+    }
   }
 }
 
@@ -2134,12 +2182,12 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       for (int64_t c = 0; c < nch; c += 2) {
         if (r32) apply(ra, c * AU * NT, std::true_type{});
         else apply(ra, c * AU * NT, std::false_type{});
-        if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
+        if (!KHIP_C1M_DEFER && (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax)) break;
         if (c + 2 < nch) load(ra, (c + 2) * AU * NT, rn, nseg, segb);
         if (c + 1 >= nch) break;
         if (r32) apply(rb, (c + 1) * AU * NT, std::true_type{});
         else apply(rb, (c + 1) * AU * NT, std::false_type{});
-        if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
+        if (!KHIP_C1M_DEFER && (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax)) break;
         if (c + 3 < nch) load(rb, (c + 3) * AU * NT, rn, nseg, segb);
       }
     }

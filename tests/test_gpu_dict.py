@@ -34,6 +34,7 @@ def _check():
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from ksql_amd import abi
     from test_gpu_parity import assert_snap_equal
+    from test_gpu_pull import _filter
     prod, orc = abi.load_product(), abi.load_oracle()
     assert prod.path.endswith("libksqldb_hip_tune.so"), prod.path
     rng = np.random.default_rng(5)
@@ -50,9 +51,12 @@ def _check():
             t0 += 20_000
             batch = abi.HostBatch(ts, utf8_keys=keys)
             assert g.push(batch) == o.push(batch)
-        assert_snap_equal(g.snapshot(), o.snapshot(), gd)
-        probe = sorted(set(keys[:300]))[:100] + [b"never-seen"]
-        assert_snap_equal(g.get(keys=probe), o.get(keys=probe), gd)
+        osnap = o.snapshot()
+        assert_snap_equal(g.snapshot(), osnap, gd)
+        # pull query (the read-only probe) against the oracle's table filtered the same way
+        probe = list(osnap["key"][::997][:100])
+        probe.append(type(probe[0])("never-seen") if isinstance(probe[0], str) else b"never-seen")
+        assert_snap_equal(g.get(keys=probe), _filter(osnap, probe, (None, None), (None, None), True), gd)
         g.close()
         o.close()
     print("OK")
