@@ -494,11 +494,11 @@ __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slo
       const int64_t i = rows ? rows[j] : j;
       if (!(bit_get(kv, i) && bit_get(rv, i) && (ts == nullptr || ts[i] >= 0))) {
         kid[i] = 0;
-        khash[i] = 0;
+        if (khash) khash[i] = 0;
       } else {
         DKey k;
         dkey_load(k, koff, kbytes, i);
-        khash[i] = (int64_t)k.h;
+        if (khash) khash[i] = (int64_t)k.h;
         const uint64_t fp = (k.h >> 40) & fpm;
         const uint64_t fresh = (1ULL << 63) | (fp << 40) | (uint64_t)i;
         uint64_t slot = k.h & dmask;
@@ -1514,11 +1514,13 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
     KHIP_TRY_HIP(hipStreamSynchronize(a->stream));  // key_bytes_total for device batches
     ev_record(a, 1);
     KHIP_TRY(a->kid.ensure(n * 8));
-    KHIP_TRY(a->khash.ensure(n * 8));
+    // the key hashes only feed the global-atomic engine's slot hashing (the others hash the ids)
+    const bool want_hash = a->engine == 1;
+    if (want_hash) KHIP_TRY(a->khash.ensure(n * 8));
     KHIP_TRY(dict_map(a->dict, a->stream, koff, kbytes, key_bytes_total, kv, rv, ts, n, a->kid.as<int64_t>(),
-                      a->khash.as<int64_t>()));
+                      want_hash ? a->khash.as<int64_t>() : nullptr));
     keys = a->kid.as<int64_t>();
-    hkeys = a->khash.as<int64_t>();
+    hkeys = want_hash ? a->khash.as<int64_t>() : keys;
     ev_record(a, 2);
   }
   // per-task retention / EMIT FINAL: every accepted key's partition (the tasks share one table)

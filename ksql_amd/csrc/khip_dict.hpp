@@ -27,7 +27,8 @@ khip_status dict_init(KeyDict& d, hipStream_t s);
 
 // Batch keys (device offsets[n+1] into device bytes) → ids, inserting unseen keys.  Rows that fail
 // kv, rv or ts >= 0 (each check skipped when its pointer is null) get id 0 and are not inserted.
-// kid[n] and khash[n] (the key's 64-bit hash) are device outputs.  key_bytes_total = koff[n].
+// kid[n] and khash[n] (the key's 64-bit hash; khash may be null) are device outputs.
+// key_bytes_total = koff[n].
 // Synchronises the stream.
 khip_status dict_map(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8_t* kbytes, int64_t key_bytes_total,
                      const uint8_t* kv, const uint8_t* rv, const int64_t* ts, int64_t n, int64_t* kid, int64_t* khash);

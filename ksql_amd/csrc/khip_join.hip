@@ -186,10 +186,71 @@ __device__ __forceinline__ bool dense_cell(const JDense& d, uint64_t raw, bool i
   return true;
 }
 
+// Hashed probe index (one INT/BIGINT value column whose keys are too spread for the dense one,
+// e.g. C4 --sparse-ids: user ids over 2^40): open addressing over 8-byte words
+// [(key - kmin) << cb | cell] (cell as the dense index's, cb bits; EMPTY = all ones; a deleted key
+// keeps its word with cell 0).  A key's home is the first word of an aligned pair, so a lookup is
+// ONE 16-byte read — the slot table's compact pair is two (32 bytes) — and the index is a quarter
+// of the slot table.  Built like the dense index, kept in step by the upserts' winning rows.
+struct JHix {
+  int32_t active;
+  int32_t cb;            // cell bits
+  int64_t kmin;
+  uint64_t krel_max;     // keys kmin .. kmin + krel_max - 1 encodable
+  uint64_t mask;         // words - 1 (a power of two >= 2)
+  int64_t vmin;
+  uint64_t vspan;        // values vmin .. vmin + vspan - 1 encodable
+  uint64_t* words;
+  int* invalid;          // set when a key / value falls outside the ranges or a probe runs long
+};
+constexpr uint64_t HIX_EMPTY = ~0ULL;
+constexpr int HIX_PROBE = 512;
+
+__device__ __forceinline__ uint64_t hix_home(int64_t k, uint64_t mask) { return key_hash(k) & mask & ~1ULL; }
+
+// Insert or overwrite key k's cell (one writer per key at a time); false when the probe ran long.
+__device__ __forceinline__ bool hix_put(const JHix& h, int64_t k, uint64_t cell) {
+  const uint64_t krel = (uint64_t)(k - h.kmin);
+  const uint64_t word = (krel << h.cb) | cell;
+  uint64_t d = hix_home(k, h.mask);
+  for (int probe = 0; probe < HIX_PROBE; probe++) {
+    uint64_t w = __hip_atomic_load(&h.words[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (w == HIX_EMPTY) {
+      w = atomicCAS((unsigned long long*)&h.words[d], (unsigned long long)HIX_EMPTY, (unsigned long long)word);
+      if (w == HIX_EMPTY) return true;
+    }
+    if ((w >> h.cb) == krel) {
+      __hip_atomic_store(&h.words[d], word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return true;
+    }
+    d = (d + 1) & h.mask;
+  }
+  return false;
+}
+
+// Key k of the upsert's winning row → its index cell (cell 0: deleted); any miss of the ranges
+// invalidates the index (rebuilt over the new ranges by the next probe).
+__device__ __forceinline__ void hix_update(const JHix& h, int64_t k, bool del, uint64_t raw, bool isnull) {
+  if (!h.active) return;
+  const uint64_t krel = (uint64_t)(k - h.kmin);
+  uint64_t cell = 0;
+  bool ok = k >= h.kmin && krel < h.krel_max;
+  if (ok && !del) {
+    if (isnull) {
+      cell = 3;
+    } else {
+      const uint64_t off = (uint64_t)((int64_t)raw - h.vmin);
+      ok = (int64_t)raw >= h.vmin && off < h.vspan;
+      cell = 1 | (off << 2);
+    }
+  }
+  if (!ok || !hix_put(h, k, cell)) *h.invalid = 1;
+}
+
 __global__ __launch_bounds__(256) void k_upsert_apply(uint64_t* __restrict__ table, int sw,
                                                       const int64_t* __restrict__ slot_of,
                                                       const uint8_t* __restrict__ rv, int64_t n, int ncols, const int32_t* __restrict__ types_dev, JCols cols,
-                                                      JDense dn, uint64_t* __restrict__ tags) {
+                                                      JDense dn, uint64_t* __restrict__ tags, JHix hx) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t slot = slot_of[i];
     if (slot < 0) continue;
@@ -203,6 +264,7 @@ __global__ __launch_bounds__(256) void k_upsert_apply(uint64_t* __restrict__ tab
     if (!bit_get(rv, i)) {
       s[1] = M_RESIDENT;  // tombstone: delete
       if (kin) dense_store(dn, kidx, 0);
+      hix_update(hx, (int64_t)s[0], true, 0, false);
       continue;
     }
     if (tags) {  // COMPACT: the INT value in the meta word
@@ -214,6 +276,7 @@ __global__ __launch_bounds__(256) void k_upsert_apply(uint64_t* __restrict__ tab
         if (dense_cell(dn, (uint64_t)(int64_t)x, !v, &cell)) dense_store(dn, kidx, cell);
         else *dn.invalid = 1;
       }
+      hix_update(hx, (int64_t)s[0], false, (uint64_t)(int64_t)x, !v);
       continue;
     }
     uint64_t nullmask = 0;
@@ -234,6 +297,7 @@ __global__ __launch_bounds__(256) void k_upsert_apply(uint64_t* __restrict__ tab
       if (dense_cell(dn, s[3], nullmask & 1, &cell)) dense_store(dn, kidx, cell);
       else *dn.invalid = 1;
     }
+    hix_update(hx, (int64_t)s[0], false, s[3], nullmask & 1);
   }
 }
 
@@ -287,6 +351,18 @@ __global__ __launch_bounds__(256) void k_dense_build(const uint64_t* __restrict_
     uint64_t cell;
     if (dense_cell(dn, slot_col(s, m, 0, cmp), slot_null(m, 0, cmp), &cell)) dense_store(dn, (int64_t)s[0] - dn.kmin, cell);
     else *dn.invalid = 1;
+  }
+}
+
+// Fill the hashed index from the live slots (words start EMPTY).
+__global__ __launch_bounds__(256) void k_hix_build(const uint64_t* __restrict__ table, int64_t cap, int sw, JHix hx,
+                                                   int cmp) {
+  for (int64_t slot = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; slot < cap;
+       slot += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t* s = table + slot * (uint64_t)sw;
+    const uint64_t m = s[1];
+    if (!(m & M_LIVE)) continue;
+    hix_update(hx, (int64_t)s[0], false, slot_col(s, m, 0, cmp), slot_null(m, 0, cmp));
   }
 }
 
@@ -527,6 +603,78 @@ __global__ __launch_bounds__(256) void k_probe_dense(JDense dn, const int64_t* _
   if (n_emitted && lane == 0 && cnt) atomicAdd(&n_emitted[blockIdx.x & (JCTR - 1)], (unsigned long long)cnt);
 }
 
+// Probe through the hashed index: one 16-byte read (the home pair) per stream row, PR rows per
+// thread issued before any is used; linear probing past the pair (rare at load <= 1/2) reads on.
+// Output identical to k_probe_dense.
+template <int PR>
+__global__ __launch_bounds__(256) void k_probe_hix(JHix hx, const int64_t* __restrict__ keys,
+                                                   const int64_t* __restrict__ ts, const uint8_t* __restrict__ kv,
+                                                   const uint8_t* __restrict__ rv, int64_t n, int inner, JWhere w,
+                                                   int32_t ctype, JOut out, unsigned long long* __restrict__ n_emitted) {
+  const int64_t base = (int64_t)blockIdx.x * 256 * PR;
+  const int lane = threadIdx.x & 63;
+  const uint64_t cmask = (1ULL << hx.cb) - 1;
+  bool act[PR];
+  int64_t key[PR];
+  ulonglong2 pw[PR];
+#pragma unroll
+  for (int r = 0; r < PR; r++) {
+    const int64_t i = base + r * 256 + threadIdx.x;
+    const int64_t ic = i < n ? i : n - 1;
+    key[r] = keys[ic];
+    act[r] = i < n && ts[ic] >= 0 && bit_get(kv, ic) && bit_get(rv, ic);
+    pw[r] = *(const ulonglong2*)(hx.words + hix_home(key[r], hx.mask));
+  }
+  int cnt = 0;
+#pragma unroll
+  for (int r = 0; r < PR; r++) {
+    const int64_t i = base + r * 256 + threadIdx.x;
+    const uint64_t krel = (uint64_t)(key[r] - hx.kmin);
+    uint64_t cell = 0;
+    if (act[r] && key[r] >= hx.kmin && krel < hx.krel_max) {
+      uint64_t wd = pw[r].x;
+      uint64_t d = hix_home(key[r], hx.mask);
+      for (int probe = 0; probe < HIX_PROBE; probe++) {
+        if (wd == HIX_EMPTY) break;
+        if ((wd >> hx.cb) == krel) {
+          cell = wd & cmask;
+          break;
+        }
+        d = (d + 1) & hx.mask;
+        wd = probe == 0 ? pw[r].y : hx.words[d];
+      }
+    }
+    const bool hit = act[r] && (cell & 1);
+    const bool isnull = !hit || (cell & 2);
+    const uint64_t raw = isnull ? 0 : (uint64_t)(hx.vmin + (int64_t)(cell >> 2));
+    bool emit = act[r] && (inner ? hit : true);
+    if (emit && w.active) emit = hit && where_ok_raw(raw, isnull ? 1ULL : 0ULL, w);
+    const uint64_t be = __ballot(emit), bh = __ballot(hit), bn = __ballot(i < n && isnull);
+    const int64_t wbase = i - lane;
+    if (lane == 0 && wbase < n) {
+      const int64_t nbytes = std::min<int64_t>(8, (n - wbase + 7) / 8);
+      if (nbytes == 8 && !(((uintptr_t)out.emit | (uintptr_t)out.matched | (uintptr_t)out.col_null[0]) & 7)) {
+        if (out.emit) *(uint64_t*)(out.emit + wbase / 8) = be;
+        if (out.matched) *(uint64_t*)(out.matched + wbase / 8) = bh;
+        if (out.col_null[0]) *(uint64_t*)(out.col_null[0] + wbase / 8) = bn;
+      } else {
+        for (int b = 0; b < nbytes; b++) {
+          if (out.emit) out.emit[wbase / 8 + b] = (uint8_t)(be >> (8 * b));
+          if (out.matched) out.matched[wbase / 8 + b] = (uint8_t)(bh >> (8 * b));
+          if (out.col_null[0]) out.col_null[0][wbase / 8 + b] = (uint8_t)(bn >> (8 * b));
+        }
+      }
+    }
+    if (i < n && out.col_data[0]) {
+      if (ctype == KHIP_TYPE_INT32) ((int32_t*)out.col_data[0])[i] = (int32_t)raw;
+      else ((uint64_t*)out.col_data[0])[i] = raw;
+    }
+    if (out.slot_out && i < n) out.slot_out[i] = emit ? (hit ? 1 : 0) : -1;
+    cnt += lane == 0 ? __popcll(be) : 0;
+  }
+  if (n_emitted && lane == 0 && cnt) atomicAdd(&n_emitted[blockIdx.x & (JCTR - 1)], (unsigned long long)cnt);
+}
+
 __global__ __launch_bounds__(256) void k_table_rehash(const uint64_t* __restrict__ old, int64_t ocap,
                                                       uint64_t* __restrict__ nt, uint64_t nmask, int sw, int cmp) {
   for (int64_t slot = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; slot < ocap;
@@ -580,17 +728,26 @@ struct khip_table {
   int64_t dense_eval_occ = -1;  // resident keys when eligibility was last evaluated (-1: never)
   JDense dn{};
   DevBuf dcells, dinvalid, drange;
+  // hashed probe index (JHix): keys too spread for the dense one
+  bool hix_ok = false;
+  JHix hx{};
+  DevBuf hwords, hinvalid;
   // STRING keys
   bool utf8 = false;
   KeyDict dict;
   DevBuf kid, khash, st_koff, st_kbytes;
 };
 
-// Build the dense probe index if the table qualifies: one INT/BIGINT value column, live keys
-// spanning at most 4x their count (or 2^20), values fitting a 1/2/4/8-byte cell.  Evaluated
-// again only after the table doubled since an unsuccessful try.
+static khip_status prepare_hix(khip_table* t, int64_t live, int64_t kmin, int64_t kmax, int64_t vmin,
+                               unsigned __int128 vrange);
+
+// Build a probe index if the table qualifies — one INT/BIGINT value column, values fitting a cell
+// of at most 24 bits: the dense index when the live keys span at most 4x their count (or 2^20),
+// else the hashed index when (key - kmin) and the cell fit 64 bits.  Evaluated again only after
+// the table doubled since an unsuccessful try.
 static khip_status prepare_dense(khip_table* t) {
-  if (t->dense_ok || t->utf8 || t->desc.n_cols != 1 || t->col_types[0] == KHIP_TYPE_DOUBLE || !knob("KHIP_PROBE_DENSE", 1))
+  if (t->dense_ok || t->hix_ok || t->utf8 || t->desc.n_cols != 1 || t->col_types[0] == KHIP_TYPE_DOUBLE ||
+      !knob("KHIP_PROBE_DENSE", 1))
     return KHIP_OK;
   if (t->dense_eval_occ >= 0 && t->occ < 2 * t->dense_eval_occ) return KHIP_OK;
   t->dense_eval_occ = std::max<int64_t>(t->occ, 1);
@@ -610,8 +767,9 @@ static khip_status prepare_dense(khip_table* t) {
   int64_t vmin = (int64_t)(r[2] ^ bias), vmax = (int64_t)(r[3] ^ bias);
   if (r[2] == ~0ULL) vmin = vmax = 0;  // every value NULL
   const unsigned __int128 krange = (unsigned __int128)((__int128)kmax - (__int128)kmin) + 1;
-  if (krange > (unsigned __int128)std::max<int64_t>(4 * live, 1 << 20) || krange > ((unsigned __int128)1 << 34)) return KHIP_OK;
   const unsigned __int128 vrange = (unsigned __int128)((__int128)vmax - (__int128)vmin) + 1;
+  if (krange > (unsigned __int128)std::max<int64_t>(4 * live, 1 << 20) || krange > ((unsigned __int128)1 << 34))
+    return prepare_hix(t, live, kmin, kmax, vmin, vrange);
   int bits = 2;
   while (bits < 64 && ((unsigned __int128)1 << (bits - 2)) < vrange) bits++;
   if (((unsigned __int128)1 << (bits - 2)) < vrange) return KHIP_OK;
@@ -640,6 +798,43 @@ static khip_status prepare_dense(khip_table* t) {
   if (bad) return KHIP_OK;
   t->dn = d;
   t->dense_ok = true;
+  return KHIP_OK;
+}
+
+static khip_status prepare_hix(khip_table* t, int64_t live, int64_t kmin, int64_t kmax, int64_t vmin,
+                               unsigned __int128 vrange) {
+  if (!knob("KHIP_PROBE_HIX", 1)) return KHIP_OK;
+  int cb = 2;
+  while (cb < 24 && ((unsigned __int128)1 << (cb - 2)) < vrange) cb++;
+  if (((unsigned __int128)1 << (cb - 2)) < vrange) return KHIP_OK;
+  // keys appended past the current maximum keep their words while they fit (key - kmin) < krel_max
+  const unsigned __int128 krange = (unsigned __int128)((__int128)kmax - (__int128)kmin) + 1;
+  const uint64_t krel_max = (1ULL << (64 - cb)) - 1;
+  if (krange >= (unsigned __int128)krel_max) return KHIP_OK;
+  const int64_t words = next_pow2(std::max<int64_t>(2 * live + live / 4, 1024));
+  KHIP_TRY(t->hwords.ensure((size_t)words * 8));
+  KHIP_TRY(t->hinvalid.ensure(8));
+  KHIP_TRY_HIP(hipMemsetAsync(t->hwords.p, 0xFF, (size_t)words * 8, t->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(t->hinvalid.p, 0, 8, t->stream));
+  JHix h{};
+  h.active = 1;
+  h.cb = cb;
+  h.kmin = kmin;
+  h.krel_max = krel_max;
+  h.mask = (uint64_t)(words - 1);
+  h.vmin = vmin;
+  h.vspan = 1ULL << (cb - 2);
+  h.words = t->hwords.as<uint64_t>();
+  h.invalid = t->hinvalid.as<int>();
+  hipLaunchKernelGGL(k_hix_build, dim3(jgrid(t->cap, 8192)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->cap,
+                     t->sw, h, t->compact ? 1 : 0);
+  KHIP_TRY_HIP(hipGetLastError());
+  int bad = 0;
+  KHIP_TRY_HIP(hipMemcpyAsync(&bad, t->hinvalid.p, 4, hipMemcpyDeviceToHost, t->stream));
+  KHIP_TRY_HIP(hipStreamSynchronize(t->stream));
+  if (bad) return KHIP_OK;
+  t->hx = h;
+  t->hix_ok = true;
   return KHIP_OK;
 }
 
@@ -846,18 +1041,22 @@ khip_status khip_table_upsert(khip_table* t, const khip_batch* b) {
                      t->claimed.as<int64_t>(), (const unsigned long long*)ctr);
   hipLaunchKernelGGL(k_upsert_apply, dim3(jgrid(n)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->sw,
                      t->slot_of.as<int64_t>(), rv, n, t->desc.n_cols, t->types_dev.as<int32_t>(), cols,
-                     t->dense_ok ? t->dn : JDense{}, t->compact ? t->tags.as<uint64_t>() : (uint64_t*)nullptr);
+                     t->dense_ok ? t->dn : JDense{}, t->compact ? t->tags.as<uint64_t>() : (uint64_t*)nullptr,
+                     t->hix_ok ? t->hx : JHix{});
   KHIP_TRY_HIP(hipGetLastError());
   unsigned long long added = 0;
-  int failed = 0, dense_bad = 0;
+  int failed = 0, dense_bad = 0, hix_bad = 0;
   KHIP_TRY_HIP(hipMemcpyAsync(&added, ctr, 8, hipMemcpyDeviceToHost, t->stream));
   KHIP_TRY_HIP(hipMemcpyAsync(&failed, failp, 4, hipMemcpyDeviceToHost, t->stream));
   if (t->dense_ok) KHIP_TRY_HIP(hipMemcpyAsync(&dense_bad, t->dinvalid.p, 4, hipMemcpyDeviceToHost, t->stream));
+  if (t->hix_ok) KHIP_TRY_HIP(hipMemcpyAsync(&hix_bad, t->hinvalid.p, 4, hipMemcpyDeviceToHost, t->stream));
   KHIP_TRY_HIP(hipStreamSynchronize(t->stream));
   if (failed) return fail(KHIP_E_DEVICE, "table probe budget exhausted");
   t->occ += (int64_t)added;
-  if (dense_bad) {  // a key or value outside the index: rebuilt over the new ranges by the next probe
-    t->dense_ok = false;
+  // a key or value outside an index, or a hashed index filling up (resident keys, deleted ones
+  // included, against its words): rebuilt over the new ranges / size by the next probe
+  if (dense_bad || hix_bad || (t->hix_ok && 5 * t->occ > 3 * (int64_t)(t->hx.mask + 1))) {
+    t->dense_ok = t->hix_ok = false;
     t->dense_eval_occ = -1;
   }
   return KHIP_OK;
@@ -900,6 +1099,15 @@ static khip_status probe_launch(khip_table* t, const khip_batch* b, int32_t join
                         : (dpr >= 32 ? k_probe_dense<32> : (dpr >= 16 ? k_probe_dense<16> : k_probe_dense<8>));
     const int pr = dpr >= 64 ? 64 : (dpr >= 32 ? 32 : (dpr >= 16 ? 16 : 8));
     hipLaunchKernelGGL(dk, dim3(ceil_div(n, 256 * pr)), dim3(256), 0, t->stream, t->dn, keys, ts, kv, rv, n,
+                       join_type == KHIP_JOIN_INNER ? 1 : 0, jw, t->col_types[0], out, n_emitted);
+    KHIP_TRY_HIP(hipGetLastError());
+    return KHIP_OK;
+  }
+  if (t->hix_ok) {
+    const int hpr = (int)knob("KHIP_PROBE_HPR", 16);
+    auto hk = hpr >= 32 ? k_probe_hix<32> : (hpr >= 16 ? k_probe_hix<16> : (hpr >= 8 ? k_probe_hix<8> : k_probe_hix<4>));
+    const int pr = hpr >= 32 ? 32 : (hpr >= 16 ? 16 : (hpr >= 8 ? 8 : 4));
+    hipLaunchKernelGGL(hk, dim3(ceil_div(n, 256 * pr)), dim3(256), 0, t->stream, t->hx, keys, ts, kv, rv, n,
                        join_type == KHIP_JOIN_INNER ? 1 : 0, jw, t->col_types[0], out, n_emitted);
     KHIP_TRY_HIP(hipGetLastError());
     return KHIP_OK;
@@ -1027,7 +1235,7 @@ khip_status khip_table_destroy(khip_table* t) {
   if (t->stream) hipStreamSynchronize(t->stream);
   DevBuf* bufs[] = {&t->table, &t->types_dev, &t->slot_of, &t->claimed, &t->scratch, &t->st_keys, &t->st_ts, &t->st_kv,
                     &t->st_rv, &t->out_emit, &t->out_matched, &t->out_slot, &t->dcells, &t->dinvalid, &t->drange,
-                    &t->kid, &t->khash, &t->st_koff, &t->st_kbytes};
+                    &t->kid, &t->khash, &t->st_koff, &t->st_kbytes, &t->tags, &t->hwords, &t->hinvalid};
   for (DevBuf* x : bufs) x->release();
   dict_release(t->dict);
   for (int c = 0; c < JMAX_COLS; c++) {
