@@ -723,53 +723,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #endif
 
 // ------------------------------------------------------------------ k_c1_merge
-// KHIP_C1M_DEFER: the record loops test for a full table once, after the item's records, not after
-// every chunk (the test is an LDS read that drains every outstanding LDS operation of the wave;
-// a full table cannot overflow the claim list: claims are table slots).
-#ifndef KHIP_C1M_DEFER
-#define KHIP_C1M_DEFER 0
-#endif
-#ifndef KHIP_C1M_NOLOAD
-#define KHIP_C1M_NOLOAD 0
-#endif
-// KHIP_C1M_BLK: a record's segment base from ONE 8-byte entry per 32-record block (the block's
-// first segment's base and where up to two more segments start in it), so the AU lookups of a
-// load are independent LDS reads issued together — the segof / spre walk was a loop per record
-// with an LDS wait in every step, the AU walks one after the other.
-#ifndef KHIP_C1M_BLK
-#define KHIP_C1M_BLK 0
-#endif
-// Block entry: bits 0-23 base - (bb0 - C1_BLK_OFF) | 24-38 d1 | 39-43 r1 | 44-58 d2 | 59-63 r2
-// (segment s starts the block; s + 1 starts r1 records in with base + d1, s + 2 r2 in with
-// + d2; r = 0: no such start); all ones in bits 0-23: the block needs the slow walk.
-constexpr int64_t C1_BLK_OFF = (int64_t)C1_SEGOF << 5;
-constexpr uint64_t C1_BLK_SLOW = 0xFFFFFFull;
-__device__ __forceinline__ uint64_t c1_blk_entry(int32_t P, int32_t br, int32_t s1, int32_t d1, bool h1, int32_t s2,
-                                                 int32_t d2, bool h2, int32_t s3, bool h3) {
-  // P: the block's first record; segment s holds it, br = its base - (bb0 - C1_BLK_OFF); s + 1 /
-  // s + 2 / s + 3 start at s1 / s2 / s3 (exist: h1 / h2 / h3), bases + d1, + d1 + d2
-  const int32_t r1 = h1 ? s1 - P : 32, r2 = h2 ? s2 - P : 32, r3 = h3 ? s3 - P : 32;
-  if (r3 < 32 || br < 0 || br >= (int32_t)C1_BLK_SLOW || (r1 < 32 && (d1 < 0 || d1 > 0x7FFF)) ||
-      (r2 < 32 && (d2 < 0 || d2 > 0x7FFF)))
-    return ~0ull;
-  const int64_t b1 = d1, b2 = d2, b0 = 0;
-  uint64_t e = (uint64_t)br;
-  if (r1 < 32) e |= ((uint64_t)(b1 - b0) << 24) | ((uint64_t)r1 << 39);
-  if (r2 < 32) e |= ((uint64_t)b2 << 44) | ((uint64_t)r2 << 59);
-  return e;
-}
-__device__ __forceinline__ int64_t c1_blk_base(uint64_t e, int64_t bb0, int r) {
-  const int r1 = (int)((e >> 39) & 31), r2 = (int)(e >> 59);
-  int64_t b = (int64_t)(e & C1_BLK_SLOW) + (bb0 - C1_BLK_OFF);
-  if (r1 && r >= r1) b += (int64_t)((e >> 24) & 0x7FFF);
-  if (r2 && r >= r2) b += (int64_t)((e >> 44) & 0x7FFF);
-  return b;
-}
-// KHIP_C1M_NOLIST: no claim list — a record's claim only counts (one non-returning LDS add per
-// wave), and the count / write-out / clear phases walk the wave's slice of the table instead.
-#ifndef KHIP_C1M_NOLIST
-#define KHIP_C1M_NOLIST 0
-#endif
 struct C1Q {
   int32_t log2P, fbits, log2H, sw, hv_active, hv_op, hmax;
   int64_t size, adv, cmax, hv_i64;
@@ -903,18 +856,13 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     int64_t nrow, bb0;
     uint32_t selw;
     uint16_t s00, s01, s10, s11;  // seg[k0][f], seg[k0][f + 1], seg[k0 + 1][f], seg[k0 + 1][f + 1]
-    uint32_t s2x;                 // KHIP_C1M_BLK: seg[k0 + 2][f] | seg[k0 + 2][f + 1] << 16
-    uint32_t s30;                 //               seg[k0 + 3][f] (the next thread's segments)
   };
   struct It {
     uint32_t p;
     int sbits, sub, nseg, segb;  // segb: log2 of the records per segment-lookup block
-    int64_t rn, nrow, bb0;
+    int64_t rn, nrow;
     bool isel;
   };
-  // KHIP_C1M_BLK: [C1_SEGOF] block entries, 8-byte aligned after segof
-  KLDS uint64_t* blk =
-      (KLDS uint64_t*)((KLDS char*)smem + ((((KLDS char*)(segof + C1_SEGOF) - (KLDS char*)smem) + 7) & ~(ptrdiff_t)7));
   auto fetch = [&](int64_t w, Pre& r) {
     uint32_t p;
     int sbits = 0, sub = 0;
@@ -950,12 +898,6 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       r.s10 = sg[0];
       r.s11 = sg[1];
     }
-    r.s2x = r.s30 = 0;
-    if (KHIP_C1M_BLK && k0 + 2 < nseg) {
-      const uint16_t* sg = seg + (int64_t)(cs + k0 + 2) * (F + 1) + f;
-      r.s2x = (uint32_t)sg[0] | ((uint32_t)sg[1] << 16);
-    }
-    if (KHIP_C1M_BLK && k0 + 3 < nseg) r.s30 = seg[(int64_t)(cs + k0 + 3) * (F + 1) + f];
   };
   auto prep = [&](const Pre& r, It& it) {
     const int nseg = r.nseg;
@@ -964,7 +906,6 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     it.sub = r.sub;
     it.nseg = nseg;
     it.nrow = r.nrow;
-    it.bb0 = r.bb0;
     it.isel = ((r.selw >> (8 * (r.p & 3))) & 0xFFu) != 0;
     const int k0 = threadIdx.x * 2;
     const int len0 = k0 < nseg ? (int)r.s01 - (int)r.s00 : 0;
@@ -1003,24 +944,6 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       segof[bj] = (uint16_t)k0;
     for (int bj = (ex + len0 + bm) >> segb, be = (ex + s + bm) >> segb; bj < be && bj < C1_SEGOF; bj++)
       segof[bj] = (uint16_t)(k0 + 1);
-    if (KHIP_C1M_BLK && segb == 5) {  // block entries for the blocks starting in this thread's segments
-      // bases relative to bb0 - C1_BLK_OFF, 32-bit: segment k's base is bb0 + k CH + its start in its
-      // chunk - its first record's place in the item
-      const int32_t s20 = (int32_t)(r.s2x & 0xFFFFu), s21 = (int32_t)(r.s2x >> 16);
-      const int32_t len2 = k0 + 2 < nseg ? s21 - s20 : 0;
-      const int32_t p1 = ex + len0, p2 = p1 + len1, p3 = p2 + len2;
-      const int32_t z = (int32_t)C1_BLK_OFF;
-      const int32_t b0 = z + k0 * C1_CH + (int32_t)r.s00 - ex, b1 = z + (k0 + 1) * C1_CH + (int32_t)r.s10 - p1;
-      const int32_t b2 = z + (k0 + 2) * C1_CH + s20 - p2, b3 = z + (k0 + 3) * C1_CH + (int32_t)r.s30 - p3;
-      for (int bj = (ex + 31) >> 5, be = (p1 + 31) >> 5; bj < be && bj < C1_SEGOF; bj++)
-        blk[bj] = c1_blk_entry(bj << 5, b0, p1, b1 - b0, k0 + 1 < nseg, p2, b2 - b1, k0 + 2 < nseg, p3, k0 + 3 < nseg);
-      // (segment k0 + 4's start is p3 + len(k0 + 3), unknown here: blocks starting in k0 + 1 that
-      // reach segment k0 + 3 take the slow walk)
-      for (int bj = (p1 + 31) >> 5, be = (p2 + 31) >> 5; bj < be && bj < C1_SEGOF; bj++)
-        blk[bj] = (k0 + 3 < nseg && p3 - (bj << 5) < 31)
-                      ? ~0ull
-                      : c1_blk_entry(bj << 5, b1, p2, b2 - b1, k0 + 2 < nseg, p3, b3 - b2, k0 + 3 < nseg, 0, false);
-    }
     if (k0 < nseg && k0 + 2 >= nseg) spre[nseg] = (uint32_t)(ex + s);  // the total
     if (nseg == 0 && threadIdx.x == 0) spre[0] = 0u;
     lds_barrier();
@@ -1031,45 +954,7 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
   uint32_t ta[AU], tb[AU];  // WIDE: the records' ts words
   // records li = l0 + thread + u NT of the item whose segments are in LDS (indices clamped to the
   // last record: every load is unconditional, so the waits stay counted)
-  auto load = [&](uint64_t (&x)[AU], uint32_t (&tx)[AU], int64_t l0, int64_t rn, int nseg, int segb, int64_t bb0) {
-#if KHIP_C1M_NOLOAD  // timing experiment only (wrong results): records synthesized, no lookup, no load
-#pragma unroll
-    for (int u = 0; u < AU; u++) {
-      const uint32_t li = (uint32_t)(l0 + threadIdx.x + (int64_t)u * NT);
-      x[u] = ((uint64_t)((li * 2654435761u) % 1400u) << 32) | (uint32_t)tmin32;
-      tx[u] = 0;
-    }
-    return;
-#endif
-    if (KHIP_C1M_BLK && segb == 5 && rn <= C1_BLK_OFF) {
-      constexpr int G = AU >= 2 ? 2 : 1;  // entries read G at a time, then one LDS wait (registers)
-#pragma unroll
-      for (int u0 = 0; u0 < AU; u0 += G) {
-        uint64_t e[G];
-        int32_t lu[G];
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-          int32_t li = (int32_t)(l0 + threadIdx.x + (int64_t)(u0 + g) * NT);
-          li = li < (int32_t)rn ? li : (int32_t)rn - 1;
-          lu[g] = li;
-          e[g] = blk[li >> 5];
-        }
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-          int64_t at;
-          if ((e[g] & C1_BLK_SLOW) != C1_BLK_SLOW) {
-            at = c1_blk_base(e[g], bb0, lu[g] & 31) + lu[g];
-          } else {  // a block of four or more segments: the walk
-            int lo = segof[lu[g] >> 5];
-            while (lo + 1 < nseg && (int32_t)spre[lo + 1] <= lu[g]) lo++;
-            at = (int64_t)sbs[lo] + lu[g];
-          }
-          x[u0 + g] = __builtin_nontemporal_load(srec + at);
-          if constexpr (WIDE) tx[u0 + g] = __builtin_nontemporal_load(srecT + at);
-        }
-      }
-      return;
-    }
+  auto load = [&](uint64_t (&x)[AU], uint32_t (&tx)[AU], int64_t l0, int64_t rn, int nseg, int segb) {
 #pragma unroll
     for (int u = 0; u < AU; u++) {
       int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
@@ -1094,8 +979,8 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
   // the item's first two chunks (register sets A and B): a chunk is always two chunks ahead of
   // the one being applied
   auto load01 = [&](const It& x) {
-    if (x.rn > 0) load(ra, ta, 0, x.rn, x.nseg, x.segb, x.bb0);
-    if (x.rn > (int64_t)AU * NT) load(rb, tb, (int64_t)AU * NT, x.rn, x.nseg, x.segb, x.bb0);
+    if (x.rn > 0) load(ra, ta, 0, x.rn, x.nseg, x.segb);
+    if (x.rn > (int64_t)AU * NT) load(rb, tb, (int64_t)AU * NT, x.rn, x.nseg, x.segb);
   };
   // the bucket table (chunk starts, bucket bases) in LDS for every descriptor
   for (int k = threadIdx.x; k <= (1 << (q.log2P - q.fbits)); k += NT) {
@@ -1235,14 +1120,7 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
         bool cl[AU];
 #pragma unroll
         for (int u = 0; u < AU; u++) cl[u] = claimed[u] && id[u] != EMPTY;
-        if (KHIP_C1M_NOLIST) {
-          int tot = 0;
-#pragma unroll
-          for (int u = 0; u < AU; u++) tot += __popcll(__ballot(cl[u]));
-          if (lane == 0 && tot) __hip_atomic_fetch_add(&nnew, tot, WG_RLX);
-        } else {
-          mg_list_append_n<AU>(cl, e, list, &nnew);
-        }
+        mg_list_append_n<AU>(cl, e, list, &nnew);
       }
 #pragma unroll
       for (int u = 0; u < AU; u++) {
@@ -1256,13 +1134,13 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       for (int64_t c = 0; c < nch; c += 2) {
         if (r32) apply(ra, ta, c * AU * NT, std::true_type{});
         else apply(ra, ta, c * AU * NT, std::false_type{});
-        if (!KHIP_C1M_DEFER && (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax)) break;
-        if (c + 2 < nch) load(ra, ta, (c + 2) * AU * NT, rn, nseg, segb, it.bb0);
+        if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
+        if (c + 2 < nch) load(ra, ta, (c + 2) * AU * NT, rn, nseg, segb);
         if (c + 1 >= nch) break;
         if (r32) apply(rb, tb, (c + 1) * AU * NT, std::true_type{});
         else apply(rb, tb, (c + 1) * AU * NT, std::false_type{});
-        if (!KHIP_C1M_DEFER && (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax)) break;
-        if (c + 3 < nch) load(rb, tb, (c + 3) * AU * NT, rn, nseg, segb, it.bb0);
+        if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
+        if (c + 3 < nch) load(rb, tb, (c + 3) * AU * NT, rn, nseg, segb);
       }
     }
     lds_barrier();
@@ -1273,13 +1151,11 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       load01(nx);
     }
     C1M_T(1);
-    const int nl = KHIP_C1M_NOLIST ? H : (nnew < H ? nnew : H);  // NOLIST: the walks cover the table
-    // entry of walk position i: the list's, or (NOLIST) the table slot itself
-    auto walk_e = [&](int i) -> uint32_t { return KHIP_C1M_NOLIST ? (uint32_t)i : (uint32_t)list[i]; };
+    const int nl = nnew < H ? nnew : H;
     if (lovf || nnew > q.hmax) {  // more groups than the table takes: retried with 2x sub-passes
       if (threadIdx.x == 0) fail[p] |= 1;
       for (int i = threadIdx.x; i < nl; i += NT) {
-        const uint32_t e = walk_e(i);
+        const uint32_t e = list[i];
         ids[e] = EMPTY;
         rt[e] = 0u;
         ct[e] = 0u;
@@ -1314,8 +1190,8 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     int nnw = 0;
     for (int k = lb0; k < lb1; k += 64) {
       const int i = k + lane;
-      const uint32_t e = i < lb1 ? walk_e(i) : dummy;
-      const bool isnew = i < lb1 && (!KHIP_C1M_NOLIST || ids[e] != EMPTY) && !(rt[e] & RT_MATCHED);
+      const uint32_t e = i < lb1 ? list[i] : dummy;
+      const bool isnew = i < lb1 && !(rt[e] & RT_MATCHED);
       nnw += (int)__popcll(__ballot(isnew));
     }
     // 3. per-wave row counts → the partition's region range (one atomic per work item)
@@ -1394,9 +1270,9 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     const uint32_t wmask = wbits ? (1u << wbits) - 1u : 0u;
     for (int k = lb0; k < lb1; k += 64) {
       const int i = k + lane;
-      const uint32_t e = i < lb1 ? walk_e(i) : dummy;
+      const uint32_t e = i < lb1 ? list[i] : dummy;
       const uint32_t rv = rt[e];
-      const bool used = i < lb1 && (!KHIP_C1M_NOLIST || ids[e] != EMPTY);
+      const bool used = i < lb1;
       const bool isnew = used && !(rv & RT_MATCHED);
       const uint64_t bl = __ballot(isnew);
       if (isnew) {
@@ -1852,19 +1728,12 @@ __device__ __forceinline__ void c1v_clear(const C1VQ& q, char* smem, int e) {
 
 // One (record or pane) contribution into delta entry e: row time, then the update planes.
 // cv: the argument's non-null count (a record: 0 / 1), sum its bits (sum), mn / mx its order keys.
-// KHIP_C1V_CONDMM: the MIN / MAX / row-time planes are read first (a plain LDS read: lanes of one
-// entry broadcast, no bank conflict) and updated by an atomic only when the record moves them — most
-// records of a busy entry do not, and same-entry atomics of one wave serialize.  A stale read only
-// costs an atomic that changes nothing: the planes move one way.
-#ifndef KHIP_C1V_CONDMM
-#define KHIP_C1V_CONDMM 0
-#endif
 template <int PM>
 __device__ __forceinline__ void c1v_add(const C1VQ& q, char* smem, uint32_t e, uint32_t tr, uint32_t cs, uint32_t cv,
                                         uint64_t sum, int64_t mn, int64_t mx) {
   const C1VP<PM> v{q};
   KLDS uint32_t* prt = &c1v_plane<uint32_t>(smem, q.off_rt)[e];
-  if (!KHIP_C1V_CONDMM || tr > *prt) __hip_atomic_fetch_max(prt, tr, WG_RLX);
+  __hip_atomic_fetch_max(prt, tr, WG_RLX);
   if (v.star() && cs) __hip_atomic_fetch_add(&c1v_plane<uint32_t>(smem, q.off_star)[e], cs, WG_RLX);
   if (cv) {
     if (v.cnt()) __hip_atomic_fetch_add(&c1v_plane<uint32_t>(smem, q.off_cnt)[e], cv, WG_RLX);
@@ -1879,11 +1748,11 @@ __device__ __forceinline__ void c1v_add(const C1VQ& q, char* smem, uint32_t e, u
     }
     if (v.mn()) {
       KLDS int64_t* pm = &c1v_plane<int64_t>(smem, q.off_min)[e];
-      if (!KHIP_C1V_CONDMM || mn < *pm) __hip_atomic_fetch_min(pm, mn, WG_RLX);
+      __hip_atomic_fetch_min(pm, mn, WG_RLX);
     }
     if (v.mx()) {
       KLDS int64_t* pm = &c1v_plane<int64_t>(smem, q.off_max)[e];
-      if (!KHIP_C1V_CONDMM || mx > *pm) __hip_atomic_fetch_max(pm, mx, WG_RLX);
+      __hip_atomic_fetch_max(pm, mx, WG_RLX);
     }
   }
 }
@@ -2274,12 +2143,12 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       for (int64_t c = 0; c < nch; c += 2) {
         if (r32) apply(ra, c * AU * NT, std::true_type{});
         else apply(ra, c * AU * NT, std::false_type{});
-        if (!KHIP_C1M_DEFER && (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax)) break;
+        if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
         if (c + 2 < nch) load(ra, (c + 2) * AU * NT, rn, nseg, segb);
         if (c + 1 >= nch) break;
         if (r32) apply(rb, (c + 1) * AU * NT, std::true_type{});
         else apply(rb, (c + 1) * AU * NT, std::false_type{});
-        if (!KHIP_C1M_DEFER && (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax)) break;
+        if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
         if (c + 3 < nch) load(rb, (c + 3) * AU * NT, rn, nseg, segb);
       }
     }
@@ -2475,7 +2344,7 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
 size_t c1_merge_lds(int log2H, int idw, int log2B) {
   const size_t H = (size_t)1 << log2H, B = (size_t)1 << log2B;
   return (H + 64) * (idw + 8) + ((H * 2 + 15) & ~(size_t)15) + (C1_SEGMAX + 4) * 4 + C1_SEGMAX * 4 + (B + 1) * 12 + 8 +
-         C1_SEGOF * 2 + (KHIP_C1M_BLK ? C1_SEGOF * 8 + 8 : 0);
+         C1_SEGOF * 2;
 }
 
 // Whether the COUNT(*) pipeline may take this push (the general path's c1 plan, TUMBLING, the
