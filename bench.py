@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--records", type=int, default=None, help="records per GPU (default: the config's)")
     ap.add_argument("--keys", type=int, default=10_000_000, help="possible_fraud: card numbers per GPU")
     ap.add_argument("--utf8", action="store_true", help="possible_fraud: VARCHAR card numbers (16 bytes)")
+    ap.add_argument("--card-format", choices=["digits", "alnum"], default="digits",
+                    help="possible_fraud --utf8: 16 decimal digits (SURVEY §8(d); inline key ids), or the same "
+                         "numbers with a letter first ('C' for the leading '4': every key through the dictionary)")
     ap.add_argument("--sparse-keys", action="store_true",
                     help="possible_fraud: card numbers spread over [0, 2^53) by a bijection of the dense ids "
                          "(the key range does not fit 32 bits)")
@@ -636,6 +639,8 @@ def bench_possible_fraud(args, lib, rank, world, local):
         card = (card * SPARSE_MULT) & ((1 << 53) - 1)
     if args.utf8:
         offs, kbytes = synth.card_utf8(card, xp="torch")
+        if args.card_format == "alnum":
+            kbytes[offs[:-1]] = ord("C")
         batch = abi.DeviceBatch(ts, key_offsets=offs, key_bytes=kbytes)
     else:
         batch = abi.DeviceBatch(ts, keys=card)
@@ -698,7 +703,8 @@ def bench_possible_fraud(args, lib, rank, world, local):
                "finalize_ms": 0}
     per_kernel = {k: {"ms": phase[k], "bytes_per_record": own[k],
                       "GB/s": own[k] * n / (phase[k] / 1000.0) / 1e9} for k in phase if phase[k] > 0}
-    variant = "_utf8" if args.utf8 else ("_sparse_keys" if args.sparse_keys else "")  # profile_leg.sh's leg names
+    variant = ("_utf8" + ("_card_format_alnum" if args.card_format == "alnum" else "") if args.utf8 else
+               ("_sparse_keys" if args.sparse_keys else ""))  # profile_leg.sh's leg names
     traffic = load_traffic(args.traffic_json, "possible_fraud" + ("_atomic" if args.engine == "atomic" else ""), n,
                            variant)
     roof = roofline(bpr * n, ms_step, push_ms, per_kernel, traffic, bpr,
@@ -717,6 +723,8 @@ def bench_possible_fraud(args, lib, rank, world, local):
          "synthetic (splitmix64, ksql_amd/synth.py), device-resident columnar batch",
          {"workload": "possible_fraud", "key": ("VARCHAR(16) card_number" if args.utf8 else "BIGINT card_number") +
                                                  (" spread over 2^53" if args.sparse_keys else ""),
+          "key_ids": (("inline (16 ASCII digits: exact 64-bit ids, no dictionary)" if args.card_format == "digits"
+                       else "device dictionary (letter-led keys)") if args.utf8 else None),
           "records_per_gpu": n, "keys_per_gpu": args.keys, "window": "TUMBLING 5s, grace default",
           "having": "COUNT(*) > 3", "groups_per_gpu": groups, "having_rows_per_gpu": int(rows),
           "parallelism": "key-hash shards x%d" % world},

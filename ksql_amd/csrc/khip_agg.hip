@@ -362,7 +362,8 @@ __global__ __launch_bounds__(256) void k_rehash(const uint64_t* __restrict__ old
     const int64_t ws = (int64_t)s[1];
     if (ws == EMPTY_WS) continue;
     const int64_t key = (int64_t)s[0];
-    const int64_t hkey = utf8 ? *(const int64_t*)(arena + key) : key;
+    // (a UTF8 group's hash key: its key hash, or an inline id itself — as k_dict_probe's khash)
+    const int64_t hkey = utf8 && !kid_inline(key) ? *(const int64_t*)(arena + key) : key;
     uint64_t d = group_hash(hkey, ws) & nmask;
     while (true) {
       uint64_t* q = nt + d * (uint64_t)sw;
@@ -435,8 +436,10 @@ __device__ __forceinline__ int64_t entry_bytes(int64_t len) { return 16 + ((len 
 
 #ifdef KHIP_TUNING
 // Tuning build: KHIP_DICT_HASHMASK keeps only these bits of every key hash (different keys then
-// share whole hashes, not just fingerprints: tests/test_gpu_dict.py).
+// share whole hashes, not just fingerprints: tests/test_gpu_dict.py); KHIP_KEY_INLINE=0 sends the
+// digit keys through the dictionary too.
 __constant__ uint64_t g_dict_hmask = ~0ULL;
+__constant__ int g_key_inline = 1;
 #endif
 
 // The key of batch row i: words (short keys), hash.
@@ -447,17 +450,45 @@ struct DKey {
   const uint8_t* kb;
   bool sk;
 };
-__device__ __forceinline__ void dkey_load(DKey& k, const int64_t* __restrict__ koff, const uint8_t* __restrict__ kbytes,
-                                          int64_t i) {
+__device__ __forceinline__ void dkey_words(DKey& k, const int64_t* __restrict__ koff, const uint8_t* __restrict__ kbytes,
+                                           int64_t i) {
   const int64_t o0 = koff[i];
   k.len = koff[i + 1] - o0;
   k.kb = kbytes + o0;
   k.sk = k.len <= 8 * KW_MAX;
   if (k.sk) key_words(k.kb, k.len, k.kw);
+}
+__device__ __forceinline__ void dkey_hash(DKey& k) {
   k.h = k.sk ? hash_key_words(k.kw, k.len) : hash_bytes_dev(k.kb, k.len);
 #ifdef KHIP_TUNING
   k.h &= g_dict_hmask;
 #endif
+}
+__device__ __forceinline__ void dkey_load(DKey& k, const int64_t* __restrict__ koff, const uint8_t* __restrict__ kbytes,
+                                          int64_t i) {
+  dkey_words(k, koff, kbytes, i);
+  dkey_hash(k);
+}
+
+// Key k's inline id (khip_dict.hpp), when it is 0..17 ASCII digits.
+__device__ __forceinline__ bool key_inline(const DKey& k, int64_t* code) {
+#ifdef KHIP_TUNING
+  if (!g_key_inline) return false;
+#endif
+  if (!k.sk || k.len > KEY_INLINE_MAX) return false;
+  static_assert(KW_MAX * 8 >= KEY_INLINE_MAX, "inline keys are read from the key words");
+  uint64_t v = 0;
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < KEY_INLINE_MAX; j++) {
+    if (j < k.len) {
+      const uint32_t d = ((uint32_t)(k.kw[j >> 3] >> (8 * (j & 7))) & 0xFFu) - 0x30u;
+      ok = ok && d <= 9u;
+      v = v * 10u + d;
+    }
+  }
+  *code = KID_INLINE | ((int64_t)k.len << 57) | (int64_t)v;
+  return ok;
 }
 
 // A resident slot (w0 fingerprint already matched) holds key k?
@@ -473,6 +504,8 @@ __device__ __forceinline__ bool dslot_eq(const ulonglong2& a, const ulonglong2& 
 
 // rows: null (row j = j) or a row list (the retry pass).  lists: DICT_NL regions of lcap entries
 // [slot | the entry's byte offset in its list << 34]; lw[L]: entries << 40 | entry bytes of list L.
+// nd[0] += the rows that probed (valid, not inline), nd[1] += the rows left pending (one atomic
+// per block each; a block without claims skips the list append).
 __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slots, uint64_t dmask,
                                                     const uint8_t* __restrict__ arena, const int64_t* __restrict__ koff,
                                                     const uint8_t* __restrict__ kbytes, const uint8_t* __restrict__ kv,
@@ -481,14 +514,14 @@ __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slo
                                                     int64_t* __restrict__ kid, int64_t* __restrict__ khash,
                                                     uint64_t* __restrict__ lists, int64_t lcap,
                                                     unsigned long long* __restrict__ lw, int* __restrict__ fail,
-                                                    uint64_t fpm) {
+                                                    uint64_t fpm, unsigned long long* __restrict__ nd) {
   __shared__ unsigned long long wsum[4];  // per wave: claims << 40 | entry bytes
   __shared__ unsigned long long bbase;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int L = blockIdx.x & (DICT_NL - 1);
   for (int64_t j0 = blockIdx.x * (int64_t)blockDim.x; j0 < n; j0 += (int64_t)gridDim.x * blockDim.x) {
     const int64_t j = j0 + threadIdx.x;
-    bool claimed = false;
+    bool claimed = false, probed = false, pending = false;
     uint64_t cslot = 0, eb = 0;
     if (j < n) {
       const int64_t i = rows ? rows[j] : j;
@@ -497,12 +530,18 @@ __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slo
         if (khash) khash[i] = 0;
       } else {
         DKey k;
-        dkey_load(k, koff, kbytes, i);
-        if (khash) khash[i] = (int64_t)k.h;
+        dkey_words(k, koff, kbytes, i);
+        int64_t code;
+        const bool inl = key_inline(k, &code);
+        k.h = 0;
+        if (!inl) dkey_hash(k);
+        probed = !inl;
+        if (khash) khash[i] = inl ? code : (int64_t)k.h;
         const uint64_t fp = (k.h >> 40) & fpm;
         const uint64_t fresh = (1ULL << 63) | (fp << 40) | (uint64_t)i;
         uint64_t slot = k.h & dmask;
-        bool done = false;
+        bool done = inl;
+        if (inl) kid[i] = code;
         for (int probe = 0; probe < DICT_PROBE && !done; probe++) {
           ulonglong2 a = slots[2 * slot];  // a stale empty / fresh word is settled by the CAS below
           uint64_t w = a.x;
@@ -521,6 +560,7 @@ __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slo
           if (((w >> 40) & 0x3FFFFFULL) == fp) {
             if (w >> 63) {  // claimed by another row of this batch: resolved after the commit
               kid[i] = -(int64_t)(slot + 1) - KID_PEND;
+              pending = true;
               done = true;
             } else {
               const ulonglong2 b = slots[2 * slot + 1];
@@ -539,6 +579,10 @@ __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slo
         }
       }
     }
+    const int nprobed = __syncthreads_count(probed), npend = __syncthreads_count(pending);
+    if (threadIdx.x == 0 && nprobed) atomicAdd(&nd[0], (unsigned long long)nprobed);
+    if (threadIdx.x == 0 && npend) atomicAdd(&nd[1], (unsigned long long)npend);
+    if (!__syncthreads_or(claimed)) continue;  // (uniform) no claims: nothing to append
     // the block's claims → list L: one atomic per block and tile for both the count and the bytes
     const uint64_t x = claimed ? ((1ULL << 40) | eb) : 0ULL;
     uint64_t incl = x;
@@ -628,7 +672,13 @@ __global__ __launch_bounds__(256) void k_dict_find(const ulonglong2* __restrict_
                                                    int64_t n, int64_t* __restrict__ kid, uint64_t fpm) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     DKey k;
-    dkey_load(k, koff, kbytes, i);
+    dkey_words(k, koff, kbytes, i);
+    int64_t code;
+    if (key_inline(k, &code)) {
+      kid[i] = code;
+      continue;
+    }
+    dkey_hash(k);
     const uint64_t fp = (k.h >> 40) & fpm;
     uint64_t slot = k.h & dmask;
     int64_t found = -1;
@@ -737,8 +787,10 @@ khip_status dict_init(KeyDict& d, hipStream_t s) {
 #ifdef KHIP_TUNING
   const uint64_t hm = (uint64_t)knob("KHIP_DICT_HASHMASK", -1);
   KHIP_TRY_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_dict_hmask), &hm, 8));
+  const int inl = (int)knob("KHIP_KEY_INLINE", 1);
+  KHIP_TRY_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_key_inline), &inl, 4));
 #endif
-  KHIP_TRY(d.ctr.ensure(32 + 16 * DICT_NL));  // (dict_round's counters)
+  KHIP_TRY(d.ctr.ensure(64 + 16 * DICT_NL));  // (dict_round's counters)
   return dict_grow(d, s, 4096);
 }
 
@@ -746,28 +798,34 @@ khip_status dict_init(KeyDict& d, hipStream_t s) {
 // Returns the rows to retry (a different key behind a pending row's fingerprint) in d.retry,
 // their count in *nretry; *failed when a probe ran out of budget (nothing committed then).
 // Counters (d.ctr, u64): [0] probe failure | [1] arena bytes used | [2] keys added | [3] retries |
-// [4 ..] DICT_NL list words | then DICT_NL list arena bases.
+// [4 ..] DICT_NL list words | then DICT_NL list arena bases | rows probed | rows pending.
 static khip_status dict_round(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8_t* kbytes, const uint8_t* kv,
                               const uint8_t* rv, const int64_t* ts, const int64_t* rows, int64_t n, int64_t* kid,
                               int64_t* khash, int64_t* nretry, bool* failed) {
   unsigned long long* c = d.ctr.as<unsigned long long>();
   unsigned long long* lw = c + 4;
   int64_t* lbase = (int64_t*)(c + 4 + DICT_NL);
+  unsigned long long* nd = c + 4 + 2 * DICT_NL;
   const int g = grid_for(n, 256);
   // a list takes the claims of blocks L, L + DICT_NL, ...: at most every row those blocks visit
   const int64_t lcap = ceil_div(g, DICT_NL) * 256 * ceil_div(n, 256LL * g);
   KHIP_TRY(d.lists.ensure((size_t)lcap * DICT_NL * 8));
   KHIP_TRY_HIP(hipMemsetAsync(c, 0, 8, s));
   KHIP_TRY_HIP(hipMemsetAsync(c + 3, 0, 8 + 8 * DICT_NL, s));
+  KHIP_TRY_HIP(hipMemsetAsync(nd, 0, 16, s));
   hipLaunchKernelGGL(k_dict_probe, dim3(g), dim3(256), 0, s, d.slots.as<ulonglong2>(), (uint64_t)(d.dcap - 1),
                      d.arena.as<uint8_t>(), koff, kbytes, kv, rv, ts, rows, n, kid, khash, d.lists.as<uint64_t>(), lcap,
-                     lw, (int*)c, dict_fp_mask());
+                     lw, (int*)c, dict_fp_mask(), nd);
   KHIP_TRY_HIP(hipGetLastError());
   std::vector<unsigned long long> h(4 + DICT_NL);
+  unsigned long long hn[2];
   KHIP_TRY_HIP(hipMemcpyAsync(h.data(), c, h.size() * 8, hipMemcpyDeviceToHost, s));
+  KHIP_TRY_HIP(hipMemcpyAsync(hn, nd, 16, hipMemcpyDeviceToHost, s));
   KHIP_TRY_HIP(hipStreamSynchronize(s));
   *failed = h[0] != 0;
   *nretry = 0;
+  d.round_probed = (int64_t)hn[0];
+  if (!rows) d.last_probed = d.round_probed;  // (the first round sees every row)
   if (*failed) return KHIP_OK;
   // each list's arena region: the prefix of the lists' entry bytes after the arena's used part
   std::vector<int64_t> base(DICT_NL);
@@ -787,6 +845,10 @@ static khip_status dict_round(KeyDict& d, hipStream_t s, const int64_t* koff, co
                        kbytes, kid);
     KHIP_TRY_HIP(hipGetLastError());
   }
+  if (hn[1] == 0) {  // no row pending on another's claim: nothing to resolve or retry
+    if (mx > 0) KHIP_TRY_HIP(hipStreamSynchronize(s));  // (`base` / `tot` were read)
+    return KHIP_OK;
+  }
   KHIP_TRY(d.retry.ensure((size_t)std::max<int64_t>(n, 1) * 8));
   hipLaunchKernelGGL(k_dict_resolve, dim3(g), dim3(256), 0, s, d.slots.as<ulonglong2>(), d.arena.as<uint8_t>(), koff,
                      kbytes, rows, n, kid, d.retry.as<int64_t>(), c + 3);
@@ -800,10 +862,13 @@ static khip_status dict_round(KeyDict& d, hipStream_t s, const int64_t* koff, co
 
 khip_status dict_map(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8_t* kbytes, int64_t key_bytes_total,
                      const uint8_t* kv, const uint8_t* rv, const int64_t* ts, int64_t n, int64_t* kid, int64_t* khash) {
-  // room for the keys this batch may add at load <= 1/2: every row on the first map, then twice
-  // the last map's new keys (at least n / 16) — a batch that brings more fails its probes and is
-  // mapped again into a larger table, so the table tracks the key count, not the batch size
-  const int64_t est = d.last_added < 0 ? n : std::min<int64_t>(n, std::max<int64_t>({2 * d.last_added, n / 16, 4096}));
+  // room for the keys this batch may add at load <= 1/2: an eighth of the rows on the first map,
+  // then twice the last map's new keys (at least 1/16 of the rows that reached the dictionary:
+  // inline keys never do) — a batch that brings more fails its probes and is mapped again into a
+  // larger table, so the table tracks the key count, not the batch size
+  const int64_t est =
+      d.last_added < 0 ? std::max<int64_t>(n / 8, 4096)
+                       : std::min<int64_t>(n, std::max<int64_t>({2 * d.last_added, std::min(n, d.last_probed) / 16, 4096}));
   if (2 * (d.docc + est) > d.dcap) KHIP_TRY(dict_grow(d, s, next_pow2(2 * (d.docc + est))));
   const int64_t need = d.arena_used + key_bytes_total + 16 * n + 16;
   if ((size_t)need > d.arena.bytes) {
@@ -829,7 +894,8 @@ khip_status dict_map(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8
       if (++grown > 6 || d.dcap >= ((int64_t)1 << 34)) return fail(KHIP_E_DEVICE, "key dictionary probe budget exhausted");
       hipLaunchKernelGGL(k_dict_unclaim, dim3(grid_for(d.dcap, 256)), dim3(256), 0, s, d.slots.as<ulonglong2>(), d.dcap);
       KHIP_TRY_HIP(hipGetLastError());
-      KHIP_TRY(dict_grow(d, s, d.dcap * 4));
+      // (room for every row that probed, as distinct keys, at load <= 1/2)
+      KHIP_TRY(dict_grow(d, s, std::max<int64_t>(d.dcap * 4, next_pow2(2 * (d.docc + d.round_probed)))));
       continue;
     }
     if (round > 64) return fail(KHIP_E_DEVICE, "key dictionary: rows unresolved after 64 rounds");
@@ -1754,6 +1820,17 @@ khip_status khip_agg_count_rows(khip_agg* a, const khip_having* h, int64_t* n) {
   return compact_rows(a, h, nullptr, n);
 }
 
+// The host copy of a UTF8 handle's arena: an id's key length (an inline id's is in the id).
+static khip_status arena_host(khip_agg* a, std::vector<uint8_t>* arena) {
+  arena->resize(a->dict.arena_used);
+  if (a->dict.arena_used)
+    KHIP_TRY_HIP(hipMemcpy(arena->data(), a->dict.arena.p, a->dict.arena_used, hipMemcpyDeviceToHost));
+  return KHIP_OK;
+}
+static int64_t kid_len(const std::vector<uint8_t>& arena, int64_t kid) {
+  return kid_inline(kid) ? (kid >> 57) & 31 : *(const int64_t*)(arena.data() + kid + 8);
+}
+
 khip_status khip_agg_snapshot_size(khip_agg* a, int64_t* n_rows, int64_t* key_bytes) {
   clear_error();
   if (!a) return fail(KHIP_E_INVALID, "null argument");
@@ -1767,10 +1844,10 @@ khip_status khip_agg_snapshot_size(khip_agg* a, int64_t* n_rows, int64_t* key_by
       std::vector<uint64_t> rows;
       int64_t n = 0;
       KHIP_TRY(compact_rows(a, nullptr, &rows, &n));
-      std::vector<uint8_t> arena(a->dict.arena_used);
-      if (a->dict.arena_used) KHIP_TRY_HIP(hipMemcpy(arena.data(), a->dict.arena.p, a->dict.arena_used, hipMemcpyDeviceToHost));
+      std::vector<uint8_t> arena;
+      KHIP_TRY(arena_host(a, &arena));
       int64_t kb = 0;
-      for (int64_t r = 0; r < n; r++) kb += *(const int64_t*)(arena.data() + rows[r * a->sw] + 8);
+      for (int64_t r = 0; r < n; r++) kb += kid_len(arena, (int64_t)rows[r * a->sw]);
       *key_bytes = kb;
     } else {
       *key_bytes = 0;
@@ -1785,13 +1862,30 @@ static khip_status emit_snapshot(khip_agg* a, const std::vector<uint64_t>& rows,
                                  const std::vector<uint8_t>* tomb_in = nullptr, uint8_t* tomb_out = nullptr) {
   const int sw = a->sw;
   const bool utf8 = a->desc.key_type == KHIP_KEY_UTF8;
-  std::vector<uint8_t> arena;
+  // UTF8: each row's key bytes — its arena entry, or its inline id's digits (decoded once per row)
+  std::vector<uint8_t> arena, inl;
+  std::vector<const uint8_t*> kp;
+  std::vector<int64_t> kl;
   if (utf8) {
-    arena.resize(a->dict.arena_used);
-    if (a->dict.arena_used) KHIP_TRY_HIP(hipMemcpy(arena.data(), a->dict.arena.p, a->dict.arena_used, hipMemcpyDeviceToHost));
+    KHIP_TRY(arena_host(a, &arena));
+    int64_t ni = 0;
+    for (int64_t r = 0; r < n; r++) ni += kid_inline((int64_t)rows[r * sw]) ? 1 : 0;
+    inl.resize((size_t)ni * KEY_INLINE_MAX);
+    kp.resize(n);
+    kl.resize(n);
+    ni = 0;
+    for (int64_t r = 0; r < n; r++) {
+      const int64_t kid = (int64_t)rows[r * sw];
+      if (kid_inline(kid)) {
+        uint8_t* o = inl.data() + ni++ * KEY_INLINE_MAX;
+        kl[r] = kid_inline_bytes(kid, o);
+        kp[r] = o;
+      } else {
+        kl[r] = *(const int64_t*)(arena.data() + kid + 8);
+        kp[r] = arena.data() + kid + 16;
+      }
+    }
   }
-  auto kptr = [&](int64_t kid) { return arena.data() + kid + 16; };
-  auto klen = [&](int64_t kid) { return *(const int64_t*)(arena.data() + kid + 8); };
   std::vector<int64_t> order(n);
   std::iota(order.begin(), order.end(), 0);
   const bool session = a->engine == 2;
@@ -1799,8 +1893,8 @@ static khip_status emit_snapshot(khip_agg* a, const std::vector<uint64_t>& rows,
     const int64_t kx = (int64_t)rows[x * sw], ky = (int64_t)rows[y * sw];
     if (kx != ky) {
       if (!utf8) return kx < ky;
-      const int64_t lx = klen(kx), ly = klen(ky);
-      const int c = memcmp(kptr(kx), kptr(ky), (size_t)std::min(lx, ly));
+      const int64_t lx = kl[x], ly = kl[y];
+      const int c = memcmp(kp[x], kp[y], (size_t)std::min(lx, ly));
       if (c) return c < 0;
       if (lx != ly) return lx < ly;
     }
@@ -1819,9 +1913,9 @@ static khip_status emit_snapshot(khip_agg* a, const std::vector<uint64_t>& rows,
     const int64_t key = (int64_t)s[0], ws = (int64_t)s[1];
     if (tomb_out) tomb_out[r] = tomb_in ? (*tomb_in)[order[r]] : 0;
     if (utf8) {
-      const int64_t len = klen(key);
+      const int64_t len = kl[order[r]];
       if (kb + len > out->key_bytes_capacity) return fail(KHIP_E_BUFFER, "snapshot key bytes capacity too small");
-      if (out->key_bytes && len) memcpy(out->key_bytes + kb, kptr(key), (size_t)len);
+      if (out->key_bytes && len) memcpy(out->key_bytes + kb, kp[order[r]], (size_t)len);
       kb += len;
       if (out->key_offsets) out->key_offsets[r + 1] = kb;
     } else if (out->key_i64) {
@@ -1902,10 +1996,11 @@ khip_status khip_agg_get(khip_agg* a, const khip_pull* q, const khip_having* h, 
   DevBuf dkeys;
   std::vector<int64_t> k;  // outlives the copy: compact_rows synchronises the stream
   if (q->n_keys > 0 && utf8) {
-    // key bytes → dictionary ids on the device (read-only probe); unseen keys match nothing
+    // key bytes → dictionary ids on the device (read-only probe; digit keys: their inline ids);
+    // unseen keys match nothing
     const int64_t nk = q->n_keys, nb = q->key_offsets[nk];
     k.assign((size_t)nk, -1);
-    if (a->dict.docc > 0) {
+    {
       DevBuf doff, dbytes, dkid;
       KHIP_TRY(doff.ensure((size_t)(nk + 1) * 8));
       KHIP_TRY(dbytes.ensure((size_t)std::max<int64_t>(nb, 1)));
@@ -1992,9 +2087,9 @@ khip_status khip_agg_changes_size(khip_agg* a, int64_t* n_rows, int64_t* key_byt
   if (key_bytes) {
     int64_t kb = 0;
     if (a->desc.key_type == KHIP_KEY_UTF8 && a->chg_n) {
-      std::vector<uint8_t> arena(a->dict.arena_used);
-      if (a->dict.arena_used) KHIP_TRY_HIP(hipMemcpy(arena.data(), a->dict.arena.p, a->dict.arena_used, hipMemcpyDeviceToHost));
-      for (int64_t r = 0; r < a->chg_n; r++) kb += *(const int64_t*)(arena.data() + a->chg_rows[r * a->sw] + 8);
+      std::vector<uint8_t> arena;
+      KHIP_TRY(arena_host(a, &arena));
+      for (int64_t r = 0; r < a->chg_n; r++) kb += kid_len(arena, (int64_t)a->chg_rows[r * a->sw]);
     }
     *key_bytes = kb;
   }

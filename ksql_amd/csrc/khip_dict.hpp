@@ -11,15 +11,40 @@
 //   arena entry at id o (8-aligned): [u64 hash][i64 len][bytes, padded to 8]
 // A map: k_dict_probe (claims, in-place compares, pending rows) → k_dict_commit (per claim) →
 // k_dict_resolve (per pending row); kernels in khip_agg.hip.
+//
+// Inline keys: a key of 0..17 ASCII decimal digits ('0'-'9': card, account and phone numbers,
+// numeric ids kept as VARCHAR) has an exact 64-bit form and never enters the dictionary — its id
+// is KID_INLINE | length << 57 | its decimal value (10^17 < 2^57; the length keeps leading zeros
+// apart: "007" != "7").  Arena offsets stay below 2^48, so the two id spaces are disjoint and id
+// equality is still byte equality.  Such a row costs its key bytes and nothing else: no slot
+// probe, no arena entry.
 #pragma once
 #include "khip_util.hpp"
 
 namespace khip {
 
+constexpr int64_t KID_INLINE = (int64_t)1 << 62;
+constexpr int KEY_INLINE_MAX = 17;
+
+__host__ __device__ inline bool kid_inline(int64_t kid) { return kid >= KID_INLINE; }
+
+// The key bytes of an inline id (out: KEY_INLINE_MAX bytes); returns the length.
+inline int kid_inline_bytes(int64_t kid, uint8_t* out) {
+  const int len = (int)((kid >> 57) & 31);
+  uint64_t v = (uint64_t)kid & ((1ULL << 57) - 1);
+  for (int j = len - 1; j >= 0; j--) {
+    out[j] = (uint8_t)('0' + v % 10);
+    v /= 10;
+  }
+  return len;
+}
+
 struct KeyDict {
   DevBuf slots, arena, ctr, lists, retry;
   int64_t dcap = 0, docc = 0, arena_used = 0;
-  int64_t last_added = -1;  // keys the last map inserted (-1: no map yet)
+  int64_t last_added = -1;   // keys the last map inserted (-1: no map yet)
+  int64_t last_probed = 0;   // rows of the last map that probed the table (not inline)
+  int64_t round_probed = 0;  // rows of the last probe round that probed it
 };
 
 // Allocate the first 4096 slots.

@@ -63,7 +63,8 @@ def _check():
 
 
 @pytest.mark.parametrize("knobs", [{"KHIP_DICT_FPMASK": "0"}, {"KHIP_DICT_FPMASK": "1"}, {"KHIP_DICT_FPMASK": "255"},
-                                   {"KHIP_DICT_HASHMASK": str(0x3FFFF)}],
+                                   {"KHIP_DICT_HASHMASK": str(0x3FFFF)},
+                                   {"KHIP_KEY_INLINE": "0", "KHIP_DICT_FPMASK": "0"}],
                          ids=lambda k: ",".join("%s=%s" % kv for kv in k.items()))
 def test_dictionary_hash_collisions(knobs):
     if not os.path.exists(TUNE_LIB):
@@ -72,3 +73,64 @@ def test_dictionary_hash_collisions(knobs):
     p = subprocess.run([sys.executable, "-c", "import sys; sys.path.insert(0, %r); import test_gpu_dict as t; t._check()"
                         % os.path.join(REPO, "tests")], cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0 and p.stdout.strip().endswith("OK"), (p.stdout[-2000:], p.stderr[-3000:])
+
+
+# Keys on both sides of the inline boundary (khip_dict.hpp): 0..17 ASCII digits are inline ids;
+# 18+ digits, signs, spaces, a decimal point, full-width digits and letters are dictionary ids.
+EDGE_KEYS = ["", "0", "00", "000", "7", "07", "007", "10", "12345678901234567", "99999999999999999",
+             "00000000000000000", "01234567890123456", "123456789012345678", "000000000000000000",
+             "1234567890123456789012", "12a", "a12", " 12", "12 ", "-12", "+12", "1.5", "\uff11\uff12", "x",
+             "4000000000000000", "4000000000000001", "40000000000000010"]
+
+
+@pytest.mark.parametrize("flags", [0, 2, 8], ids=["partitioned", "atomic", "changelog"])
+def test_inline_and_dictionary_keys_vs_oracle(flags):
+    from ksql_amd import abi
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from test_gpu_parity import assert_snap_equal
+    from test_gpu_pull import _filter
+    prod, orc = abi.load_product(), abi.load_oracle()
+    rng = np.random.default_rng(11 + flags)
+    kw = dict(window_kind="TUMBLING", size_ms=5000, key_type="UTF8", col_types=["INT64"],
+              aggs=[("COUNT_STAR", -1), ("SUM", 0), ("MAX", 0)])
+    gd, od = abi.make_agg_desc(**dict(kw, flags=flags)), abi.make_agg_desc(**kw)
+    g, o = abi.AggHandle(prod, gd), abi.AggHandle(orc, od)
+    t0 = 0
+    for b in range(4):
+        n = 30_000
+        pool = EDGE_KEYS + ["%d" % v for v in rng.integers(0, 10**12, 500)] + ["k%d" % v for v in range(300)]
+        keys = [pool[i] for i in rng.integers(0, len(pool), n)]
+        ts = t0 + (np.arange(n) * 12_000) // n
+        t0 += 9_000
+        batch = abi.HostBatch(ts, utf8_keys=keys, cols=[rng.integers(-50, 50, n)])
+        assert g.push(batch) == o.push(batch)
+        if flags == 8:
+            gc, oc = g.changes(), o.changes()
+            assert_snap_equal(gc, oc, gd)
+    osnap = o.snapshot()
+    assert_snap_equal(g.snapshot(), osnap, gd)
+    probe = EDGE_KEYS + ["12345", "never-seen", "5" * 17]
+    assert_snap_equal(g.get(keys=probe), _filter(osnap, probe, (None, None), (None, None), True), gd)
+    g.close()
+    o.close()
+
+
+def test_first_map_of_all_new_keys_grows_and_matches_oracle():
+    """A first push of all-distinct dictionary keys outgrows the first map's table (sized for an
+    eighth of the rows): the round is undone, the table grows for every probed row, and the map
+    runs again; then a push of only inline keys, then dictionary keys again."""
+    from ksql_amd import abi
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from test_gpu_parity import assert_snap_equal
+    prod, orc = abi.load_product(), abi.load_oracle()
+    kw = dict(window_kind="TUMBLING", size_ms=1000, key_type="UTF8", aggs=[("COUNT_STAR", -1)])
+    gd = abi.make_agg_desc(**kw)
+    g, o = abi.AggHandle(prod, gd), abi.AggHandle(orc, abi.make_agg_desc(**kw))
+    n = 400_000
+    for b, keys in enumerate((["key-%d" % v for v in range(n)], ["%d" % v for v in range(n)],
+                              ["key-%d" % (v * 3) for v in range(n)])):
+        batch = abi.HostBatch(np.full(n, 500 * b, np.int64), utf8_keys=keys)
+        assert g.push(batch) == o.push(batch)
+    assert_snap_equal(g.snapshot(), o.snapshot(), gd)
+    g.close()
+    o.close()

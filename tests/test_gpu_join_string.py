@@ -24,11 +24,18 @@ def orc():
 
 
 def _skey(k):
-    # a bijection onto ASCII, multi-byte UTF-8 and the empty key (lengths 0..~24)
+    # a bijection onto ASCII, multi-byte UTF-8, digit keys (inline ids, khip_dict.hpp: with and
+    # without leading zeros; 18 digits: too long to inline) and the empty key (lengths 0..~24)
     if k == 0:
         return ""
     if k % 13 == 0:
         return "usér-%d-ünïcødé" % k
+    if k % 7 == 0:
+        return "%d" % k
+    if k % 11 == 0:
+        return "%018d" % k
+    if k % 17 == 0:
+        return "0%d" % k
     return "user_%d" % k
 
 

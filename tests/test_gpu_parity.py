@@ -129,7 +129,9 @@ def _random_batch(rng, n, key_type, nkeys, span, disorder, null_frac=0.05, t0=0,
     cols = [c_i32, c_i64, c_dbl, c_abs]
     if key_type == "UTF8":
         ids = rng.integers(0, nkeys, n)
-        keys = ["k%d" % k if k % 7 else "éè-%d" % k for k in ids]
+        # dictionary keys and digit keys (inline ids, khip_dict.hpp; "00.." keeps leading zeros apart)
+        keys = ["%d" % k if k % 3 == 0 else "00%d" % k if k % 5 == 0 else "k%d" % k if k % 7 else "éè-%d" % k
+                for k in ids]
         return abi.HostBatch(ts, utf8_keys=keys, key_valid=kv, row_valid=rv, cols=cols, col_valid=vals)
     keys = rng.integers(-nkeys, nkeys, n) * 1_000_003
     return abi.HostBatch(ts, keys=keys, key_valid=kv, row_valid=rv, cols=cols, col_valid=vals)
