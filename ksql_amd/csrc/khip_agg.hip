@@ -475,20 +475,8 @@ __device__ __forceinline__ bool key_inline(const DKey& k, int64_t* code) {
 #ifdef KHIP_TUNING
   if (!g_key_inline) return false;
 #endif
-  if (!k.sk || k.len > KEY_INLINE_MAX) return false;
-  static_assert(KW_MAX * 8 >= KEY_INLINE_MAX, "inline keys are read from the key words");
-  uint64_t v = 0;
-  bool ok = true;
-#pragma unroll
-  for (int j = 0; j < KEY_INLINE_MAX; j++) {
-    if (j < k.len) {
-      const uint32_t d = ((uint32_t)(k.kw[j >> 3] >> (8 * (j & 7))) & 0xFFu) - 0x30u;
-      ok = ok && d <= 9u;
-      v = v * 10u + d;
-    }
-  }
-  *code = KID_INLINE | ((int64_t)k.len << 57) | (int64_t)v;
-  return ok;
+  static_assert(KW_MAX == 3, "inline keys are read from three key words");
+  return k.sk && inline_id_words(k.kw, k.len, code);
 }
 
 // A resident slot (w0 fingerprint already matched) holds key k?
@@ -519,6 +507,7 @@ __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slo
   __shared__ unsigned long long bbase;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int L = blockIdx.x & (DICT_NL - 1);
+  unsigned long long bprobed = 0, bpend = 0;  // (thread 0: the block's counts over its tiles)
   for (int64_t j0 = blockIdx.x * (int64_t)blockDim.x; j0 < n; j0 += (int64_t)gridDim.x * blockDim.x) {
     const int64_t j = j0 + threadIdx.x;
     bool claimed = false, probed = false, pending = false;
@@ -579,9 +568,8 @@ __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slo
         }
       }
     }
-    const int nprobed = __syncthreads_count(probed), npend = __syncthreads_count(pending);
-    if (threadIdx.x == 0 && nprobed) atomicAdd(&nd[0], (unsigned long long)nprobed);
-    if (threadIdx.x == 0 && npend) atomicAdd(&nd[1], (unsigned long long)npend);
+    bprobed += (unsigned long long)__syncthreads_count(probed);
+    bpend += (unsigned long long)__syncthreads_count(pending);
     if (!__syncthreads_or(claimed)) continue;  // (uniform) no claims: nothing to append
     // the block's claims → list L: one atomic per block and tile for both the count and the bytes
     const uint64_t x = claimed ? ((1ULL << 40) | eb) : 0ULL;
@@ -606,6 +594,56 @@ __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slo
       else *fail = 2;  // (lcap covers every row a list's blocks can claim)
     }
   }
+  if (threadIdx.x == 0 && bprobed) atomicAdd(&nd[0], bprobed);
+  if (threadIdx.x == 0 && bpend) atomicAdd(&nd[1], bpend);
+}
+
+// The inline ids of a batch, before any dictionary work: rows without a key get 0, inline keys
+// their id (khash: the id), other keys KID_DICT; nd[0] += the rows left for the dictionary, nd[1]
+// += the inline rows (one atomic per block each; ts is not read: a late row's id is never used).  Eight rows per thread in
+// flight (the offset loads, then the key words).
+constexpr int64_t KID_DICT = INT64_MIN;
+__global__ __launch_bounds__(256) void k_key_inline(const int64_t* __restrict__ koff, const uint8_t* __restrict__ kbytes,
+                                                    const uint8_t* __restrict__ kv, const uint8_t* __restrict__ rv,
+                                                    const int64_t* __restrict__ ts, int64_t n, int64_t* __restrict__ kid,
+                                                    int64_t* __restrict__ khash, unsigned long long* __restrict__ nd) {
+  constexpr int R = 8;
+  (void)ts;
+  __shared__ unsigned int bsum[2];
+  if (threadIdx.x < 2) bsum[threadIdx.x] = 0;
+  unsigned int cnt = 0, ninl = 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j0 < n; j0 += stride * R) {
+    DKey k[R];
+    bool ok[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int64_t i = j0 + r * stride;
+      ok[r] = i < n && bit_get(kv, i) && bit_get(rv, i);
+      if (ok[r]) dkey_words(k[r], koff, kbytes, i);
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int64_t i = j0 + r * stride;
+      if (i >= n) break;
+      int64_t code = 0;
+      if (ok[r]) {
+        if (key_inline(k[r], &code)) {
+          ninl++;
+        } else {
+          code = KID_DICT;
+          cnt++;
+        }
+      }
+      kid[i] = code;
+      if (khash) khash[i] = code;
+    }
+  }
+  __syncthreads();
+  if (cnt) atomicAdd(&bsum[0], cnt);
+  if (ninl) atomicAdd(&bsum[1], ninl);
+  __syncthreads();
+  if (threadIdx.x < 2 && bsum[threadIdx.x]) atomicAdd(&nd[threadIdx.x], (unsigned long long)bsum[threadIdx.x]);
 }
 
 // One thread per claim (list L, entry t): the arena entry at its list's base + its byte offset, the
@@ -862,6 +900,25 @@ static khip_status dict_round(KeyDict& d, hipStream_t s, const int64_t* koff, co
 
 khip_status dict_map(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8_t* kbytes, int64_t key_bytes_total,
                      const uint8_t* kv, const uint8_t* rv, const int64_t* ts, int64_t n, int64_t* kid, int64_t* khash) {
+  // inline ids first: a batch whose keys are all inline (or invalid) never touches the dictionary.
+  // (Skipped while the maps find no inline key at all — the probe turns inline keys into their ids
+  // too — and tried again every 16th map.)
+  if (d.last_inline != 0 || (++d.maps & 15) == 0) {
+    unsigned long long* nd = d.ctr.as<unsigned long long>() + 4 + 2 * DICT_NL + 2;
+    KHIP_TRY_HIP(hipMemsetAsync(nd, 0, 16, s));
+    hipLaunchKernelGGL(k_key_inline, dim3(grid_for(ceil_div(n, 8LL), 256, 4096)), dim3(256), 0, s, koff, kbytes, kv, rv,
+                       ts, n, kid, khash, nd);
+    KHIP_TRY_HIP(hipGetLastError());
+    unsigned long long h[2] = {0, 0};
+    KHIP_TRY_HIP(hipMemcpyAsync(h, nd, 16, hipMemcpyDeviceToHost, s));
+    KHIP_TRY_HIP(hipStreamSynchronize(s));
+    d.last_inline = (int64_t)h[1];
+    if (h[0] == 0) {
+      d.last_probed = d.round_probed = 0;
+      if (d.last_added < 0) d.last_added = 0;
+      return KHIP_OK;
+    }
+  }
   // room for the keys this batch may add at load <= 1/2: an eighth of the rows on the first map,
   // then twice the last map's new keys (at least 1/16 of the rows that reached the dictionary:
   // inline keys never do) — a batch that brings more fails its probes and is mapped again into a

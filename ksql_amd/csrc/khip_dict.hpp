@@ -19,12 +19,10 @@
 // equality is still byte equality.  Such a row costs its key bytes and nothing else: no slot
 // probe, no arena entry.
 #pragma once
+#include "khip_inline_id.hpp"
 #include "khip_util.hpp"
 
 namespace khip {
-
-constexpr int64_t KID_INLINE = (int64_t)1 << 62;
-constexpr int KEY_INLINE_MAX = 17;
 
 __host__ __device__ inline bool kid_inline(int64_t kid) { return kid >= KID_INLINE; }
 
@@ -45,6 +43,8 @@ struct KeyDict {
   int64_t last_added = -1;   // keys the last map inserted (-1: no map yet)
   int64_t last_probed = 0;   // rows of the last map that probed the table (not inline)
   int64_t round_probed = 0;  // rows of the last probe round that probed it
+  int64_t last_inline = -1;  // inline rows the last inline pass found (-1: none ran yet)
+  int64_t maps = 0;
 };
 
 // Allocate the first 4096 slots.

@@ -604,7 +604,9 @@ __global__ __launch_bounds__(256) void k_probe_dense(JDense dn, const int64_t* _
 }
 
 // Probe through the hashed index: one 16-byte read (the home pair) per stream row, PR rows per
-// thread issued before any is used; linear probing past the pair (rare at load <= 1/2) reads on.
+// thread issued before any is used.  A row whose key is neither in its home pair nor stopped by an
+// empty word there (≈ α² of them) chases the following pairs — every such row of the thread in the
+// same round, so their dependent reads overlap instead of running one row after another.
 // Output identical to k_probe_dense.
 template <int PR>
 __global__ __launch_bounds__(256) void k_probe_hix(JHix hx, const int64_t* __restrict__ keys,
@@ -615,35 +617,61 @@ __global__ __launch_bounds__(256) void k_probe_hix(JHix hx, const int64_t* __res
   const int lane = threadIdx.x & 63;
   const uint64_t cmask = (1ULL << hx.cb) - 1;
   bool act[PR];
-  int64_t key[PR];
+  uint64_t krel[PR];
   ulonglong2 pw[PR];
 #pragma unroll
   for (int r = 0; r < PR; r++) {
     const int64_t i = base + r * 256 + threadIdx.x;
     const int64_t ic = i < n ? i : n - 1;
-    key[r] = keys[ic];
+    const int64_t key = keys[ic];
     act[r] = i < n && ts[ic] >= 0 && bit_get(kv, ic) && bit_get(rv, ic);
-    pw[r] = *(const ulonglong2*)(hx.words + hix_home(key[r], hx.mask));
+    krel[r] = (uint64_t)(key - hx.kmin);
+    act[r] = act[r] && key >= hx.kmin && krel[r] < hx.krel_max;  // (else: no such key)
+    pw[r] = *(const ulonglong2*)(hx.words + hix_home(key, hx.mask));
+  }
+  // the home pairs; pend bit r: row r chases on from pair dd[r]
+  uint32_t cellv[PR];
+  uint64_t dd[PR];
+  uint32_t pend = 0;
+#pragma unroll
+  for (int r = 0; r < PR; r++) {
+    cellv[r] = 0;
+    dd[r] = hix_home((int64_t)krel[r] + hx.kmin, hx.mask);
+    if (!act[r] || pw[r].x == HIX_EMPTY) continue;
+    if ((pw[r].x >> hx.cb) == krel[r]) cellv[r] = (uint32_t)(pw[r].x & cmask);
+    else if (pw[r].y == HIX_EMPTY) continue;
+    else if ((pw[r].y >> hx.cb) == krel[r]) cellv[r] = (uint32_t)(pw[r].y & cmask);
+    else pend |= 1u << r;
+  }
+  for (int round = 1; round < HIX_PROBE / 2 && __ballot(pend != 0); round++) {
+    ulonglong2 q[PR];
+#pragma unroll
+    for (int r = 0; r < PR; r++) {
+      if (!((pend >> r) & 1u)) continue;
+      dd[r] = (dd[r] + 2) & hx.mask;
+      q[r] = *(const ulonglong2*)(hx.words + dd[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < PR; r++) {
+      if (!((pend >> r) & 1u)) continue;
+      bool stop = true;
+      if (q[r].x == HIX_EMPTY) {
+      } else if ((q[r].x >> hx.cb) == krel[r]) {
+        cellv[r] = (uint32_t)(q[r].x & cmask);
+      } else if (q[r].y == HIX_EMPTY) {
+      } else if ((q[r].y >> hx.cb) == krel[r]) {
+        cellv[r] = (uint32_t)(q[r].y & cmask);
+      } else {
+        stop = false;
+      }
+      if (stop) pend &= ~(1u << r);
+    }
   }
   int cnt = 0;
 #pragma unroll
   for (int r = 0; r < PR; r++) {
     const int64_t i = base + r * 256 + threadIdx.x;
-    const uint64_t krel = (uint64_t)(key[r] - hx.kmin);
-    uint64_t cell = 0;
-    if (act[r] && key[r] >= hx.kmin && krel < hx.krel_max) {
-      uint64_t wd = pw[r].x;
-      uint64_t d = hix_home(key[r], hx.mask);
-      for (int probe = 0; probe < HIX_PROBE; probe++) {
-        if (wd == HIX_EMPTY) break;
-        if ((wd >> hx.cb) == krel) {
-          cell = wd & cmask;
-          break;
-        }
-        d = (d + 1) & hx.mask;
-        wd = probe == 0 ? pw[r].y : hx.words[d];
-      }
-    }
+    const uint64_t cell = cellv[r];
     const bool hit = act[r] && (cell & 1);
     const bool isnull = !hit || (cell & 2);
     const uint64_t raw = isnull ? 0 : (uint64_t)(hx.vmin + (int64_t)(cell >> 2));
