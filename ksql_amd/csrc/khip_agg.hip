@@ -492,8 +492,8 @@ __device__ __forceinline__ bool dslot_eq(const ulonglong2& a, const ulonglong2& 
 
 // rows: null (row j = j) or a row list (the retry pass).  lists: DICT_NL regions of lcap entries
 // [slot | the entry's byte offset in its list << 34]; lw[L]: entries << 40 | entry bytes of list L.
-// nd[0] += the rows that probed (valid, not inline), nd[1] += the rows left pending (one atomic
-// per block each; a block without claims skips the list append).
+// nd[0] += the rows that probed (valid, not inline), nd[1] += the rows left pending (counted per
+// wave by ballots, one atomic per wave at the end: no barrier of their own).
 __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slots, uint64_t dmask,
                                                     const uint8_t* __restrict__ arena, const int64_t* __restrict__ koff,
                                                     const uint8_t* __restrict__ kbytes, const uint8_t* __restrict__ kv,
@@ -507,7 +507,7 @@ __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slo
   __shared__ unsigned long long bbase;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int L = blockIdx.x & (DICT_NL - 1);
-  unsigned long long bprobed = 0, bpend = 0;  // (thread 0: the block's counts over its tiles)
+  unsigned long long bprobed = 0, bpend = 0;  // (the wave's counts over its tiles)
   for (int64_t j0 = blockIdx.x * (int64_t)blockDim.x; j0 < n; j0 += (int64_t)gridDim.x * blockDim.x) {
     const int64_t j = j0 + threadIdx.x;
     bool claimed = false, probed = false, pending = false;
@@ -568,9 +568,8 @@ __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slo
         }
       }
     }
-    bprobed += (unsigned long long)__syncthreads_count(probed);
-    bpend += (unsigned long long)__syncthreads_count(pending);
-    if (!__syncthreads_or(claimed)) continue;  // (uniform) no claims: nothing to append
+    bprobed += (unsigned long long)__popcll(__ballot(probed));
+    bpend += (unsigned long long)__popcll(__ballot(pending));
     // the block's claims → list L: one atomic per block and tile for both the count and the bytes
     const uint64_t x = claimed ? ((1ULL << 40) | eb) : 0ULL;
     uint64_t incl = x;
@@ -594,8 +593,8 @@ __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slo
       else *fail = 2;  // (lcap covers every row a list's blocks can claim)
     }
   }
-  if (threadIdx.x == 0 && bprobed) atomicAdd(&nd[0], bprobed);
-  if (threadIdx.x == 0 && bpend) atomicAdd(&nd[1], bpend);
+  if (lane == 0 && bprobed) atomicAdd(&nd[0], bprobed);
+  if (lane == 0 && bpend) atomicAdd(&nd[1], bpend);
 }
 
 // The inline ids of a batch, before any dictionary work: rows without a key get 0, inline keys

@@ -2043,7 +2043,9 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
           continue;
         for (int k = 0; k < q.sw; k++) dst[k] = row[k];
         dst += q.sw;
-        nh += having_ok(row, q.having) ? 1 : 0;
+        // (the query's HAVING alone: the merge's copy never carries pull / retention / FINAL bounds)
+        nh += having_ok_words(q.having.a.w_val >= 0 ? row[q.having.a.w_val] : 0,
+                              q.having.a.w_cnt >= 0 ? row[q.having.a.w_cnt] : 0, q.having) ? 1 : 0;
       }
       if (q.having.active) {
         nh = (int)wave_sum(nh);

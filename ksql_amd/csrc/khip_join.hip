@@ -617,6 +617,7 @@ __global__ __launch_bounds__(256) void k_probe_hix(JHix hx, const int64_t* __res
   const int lane = threadIdx.x & 63;
   const uint64_t cmask = (1ULL << hx.cb) - 1;
   bool act[PR];
+  uint32_t inr = 0;  // bit r: row r's key is inside the index's key range (else: no such key)
   uint64_t krel[PR];
   ulonglong2 pw[PR];
 #pragma unroll
@@ -626,7 +627,7 @@ __global__ __launch_bounds__(256) void k_probe_hix(JHix hx, const int64_t* __res
     const int64_t key = keys[ic];
     act[r] = i < n && ts[ic] >= 0 && bit_get(kv, ic) && bit_get(rv, ic);
     krel[r] = (uint64_t)(key - hx.kmin);
-    act[r] = act[r] && key >= hx.kmin && krel[r] < hx.krel_max;  // (else: no such key)
+    if (key >= hx.kmin && krel[r] < hx.krel_max) inr |= 1u << r;
     pw[r] = *(const ulonglong2*)(hx.words + hix_home(key, hx.mask));
   }
   // the home pairs; pend bit r: row r chases on from pair dd[r]
@@ -637,7 +638,7 @@ __global__ __launch_bounds__(256) void k_probe_hix(JHix hx, const int64_t* __res
   for (int r = 0; r < PR; r++) {
     cellv[r] = 0;
     dd[r] = hix_home((int64_t)krel[r] + hx.kmin, hx.mask);
-    if (!act[r] || pw[r].x == HIX_EMPTY) continue;
+    if (!act[r] || !((inr >> r) & 1u) || pw[r].x == HIX_EMPTY) continue;
     if ((pw[r].x >> hx.cb) == krel[r]) cellv[r] = (uint32_t)(pw[r].x & cmask);
     else if (pw[r].y == HIX_EMPTY) continue;
     else if ((pw[r].y >> hx.cb) == krel[r]) cellv[r] = (uint32_t)(pw[r].y & cmask);
@@ -1132,7 +1133,9 @@ static khip_status probe_launch(khip_table* t, const khip_batch* b, int32_t join
     return KHIP_OK;
   }
   if (t->hix_ok) {
-    const int hpr = (int)knob("KHIP_PROBE_HPR", 16);
+    // (8: 96 VGPRs, 5 waves per SIMD — 16 rows held 184 and ran at 2: 30.9 -> 25.0 ms per 1e9
+    // probes, profiles/r05/ab/c4_sparse_hpr.txt)
+    const int hpr = (int)knob("KHIP_PROBE_HPR", 8);
     auto hk = hpr >= 32 ? k_probe_hix<32> : (hpr >= 16 ? k_probe_hix<16> : (hpr >= 8 ? k_probe_hix<8> : k_probe_hix<4>));
     const int pr = hpr >= 32 ? 32 : (hpr >= 16 ? 16 : (hpr >= 8 ? 8 : 4));
     hipLaunchKernelGGL(hk, dim3(ceil_div(n, 256 * pr)), dim3(256), 0, t->stream, t->hx, keys, ts, kv, rv, n,

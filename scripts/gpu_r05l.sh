@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 O=gpurun_out/r05l; mkdir -p $O
-timeout -k 10 600 python -u -m pytest -q -x --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "join" \
+timeout -k 10 600 python -u -m pytest -q -x --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_c1v.py -k "join or c1v or hopping or c3 or c5" \
   tests/test_gpu_join_string.py tests/test_gpu_join_shard.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 3; }
 tail -1 $O/tests.log
 BENCH_ARGS="--config clickstream_join --sparse-ids --steps 3 --warmup 1 --no-cpu-baseline --no-extras" KGREP="k_probe" \
