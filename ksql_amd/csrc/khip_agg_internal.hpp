@@ -224,7 +224,8 @@ __device__ __forceinline__ uint64_t hash_bytes_dev(const uint8_t* p, int64_t n) 
 constexpr int KW_MAX = 3;
 __device__ __forceinline__ void key_words(const uint8_t* p, int64_t n, uint64_t (&w)[KW_MAX]) {
   const uint64_t a = (uint64_t)p;
-  const uint64_t* base = (const uint64_t*)(a & ~7ULL);
+  // (pointer arithmetic, not an integer cast: the loads stay global_load, not flat_load)
+  const uint64_t* base = (const uint64_t*)(p - (a & 7));
   const int sh = (int)(a & 7) * 8;
   const int na = (int)(((a & 7) + (uint64_t)n + 7) >> 3);  // aligned words holding key bytes
   uint64_t A[KW_MAX + 1];

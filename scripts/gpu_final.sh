@@ -7,11 +7,11 @@
 # The first failure ends the script (tests: a crash or time limit; test failures are reported).
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-ITAG=${ITAG:-r03z}
+ITAG=${ITAG:-r05_final}
 D=gpurun_out/$ITAG
 mkdir -p $D
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-ALL_LEGS="hourly_metrics hopping_double clickstream_join clickstream_join:--sparse-ids repartition_sum serde_json serde_avro sink_json table_agg session"
+ALL_LEGS="possible_fraud:--sparse-keys possible_fraud:--utf8 possible_fraud:--utf8:--card-format:alnum hourly_metrics hopping_double clickstream_join clickstream_join:--sparse-ids repartition_sum serde_json serde_avro sink_json table_agg table_agg:--sparse-ids session"
 case ${PART:?} in
 tests)
   timeout -k 10 720 python -u -m pytest tests -m gpu -q --maxfail=20 --timeout 300 --timeout-method thread \
@@ -26,7 +26,7 @@ tests)
   ;;
 legs)
   for LA in ${LEGS:-$ALL_LEGS}; do
-    L=${LA%%:*}; X=""; [ "$LA" != "$L" ] && X=${LA#*:}
+    L=${LA%%:*}; X=""; [ "$LA" != "$L" ] && X=$(echo "${LA#*:}" | tr ':' ' ')
     T=$L$(echo "$X" | tr -c 'a-z0-9' '_' | sed 's/_*$//')
     timeout -k 10 400 python -u bench.py --config $L $X > $D/leg_$T.jsonl 2> $D/leg_$T.err || { echo "leg $LA failed"; tail -20 $D/leg_$T.err; exit 5; }
     cut -c1-250 $D/leg_$T.jsonl
@@ -34,7 +34,7 @@ legs)
   ;;
 prof)
   for LA in ${LEGS:?}; do
-    L=${LA%%:*}; X=""; [ "$LA" != "$L" ] && X=${LA#*:}
+    L=${LA%%:*}; X=""; [ "$LA" != "$L" ] && X=$(echo "${LA#*:}" | tr ':' ' ')
     STEPS=${STEPS:-3} bash scripts/profile_leg.sh $ITAG $L $X > /dev/null || { echo "prof $LA failed"; exit 6; }
     echo "prof $LA ok"
   done
