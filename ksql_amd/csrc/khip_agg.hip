@@ -599,35 +599,66 @@ __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slo
 
 // The inline ids of a batch, before any dictionary work: rows without a key get 0, inline keys
 // their id (khash: the id), other keys KID_DICT; nd[0] += the rows left for the dictionary, nd[1]
-// += the inline rows (one atomic per block each; ts is not read: a late row's id is never used).  Eight rows per thread in
-// flight (the offset loads, then the key words).
+// += the inline rows (one atomic per block each; ts is not read: a late row's id is never used).
+// Branch-free loads, R rows per thread: every row's offsets, then every row's first four aligned
+// key words (clamped to the words that hold its bytes, so no load leaves the key column; an empty
+// key reads the word of the column's first byte, or nothing when the column is empty), then the
+// SWAR check per row.
 constexpr int64_t KID_DICT = INT64_MIN;
+template <int R>
 __global__ __launch_bounds__(256) void k_key_inline(const int64_t* __restrict__ koff, const uint8_t* __restrict__ kbytes,
                                                     const uint8_t* __restrict__ kv, const uint8_t* __restrict__ rv,
                                                     const int64_t* __restrict__ ts, int64_t n, int64_t* __restrict__ kid,
                                                     int64_t* __restrict__ khash, unsigned long long* __restrict__ nd) {
-  constexpr int R = 8;
   (void)ts;
+  const int64_t kfirst = koff[0];
+  const bool has_bytes = koff[n] > kfirst;
+  const uint8_t* anchor = kbytes + kfirst;  // (a byte of the column when has_bytes)
   __shared__ unsigned int bsum[2];
   if (threadIdx.x < 2) bsum[threadIdx.x] = 0;
   unsigned int cnt = 0, ninl = 0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t j0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j0 < n; j0 += stride * R) {
-    DKey k[R];
-    bool ok[R];
+    int64_t o0[R], len[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {
-      const int64_t i = j0 + r * stride;
-      ok[r] = i < n && bit_get(kv, i) && bit_get(rv, i);
-      if (ok[r]) dkey_words(k[r], koff, kbytes, i);
+      const int64_t i = j0 + r * stride < n ? j0 + r * stride : n - 1;
+      o0[r] = koff[i];
+      len[r] = koff[i + 1] - o0[r];
+    }
+    uint64_t A[R][KW_MAX + 1];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const uint8_t* p = kbytes + o0[r];
+      const int64_t lb = len[r] < 8 * KW_MAX ? len[r] : 8 * KW_MAX;  // (longer keys are never inline)
+      const uint64_t a = (uint64_t)p;
+      const uint64_t* base = (const uint64_t*)(p - (a & 7));
+      const int last = lb > 0 ? (int)(((a & 7) + (uint64_t)lb - 1) >> 3) : 0;
+      const uint64_t* b0 = lb > 0 ? base : (const uint64_t*)(anchor - ((uint64_t)anchor & 7));
+#pragma unroll
+      for (int k = 0; k <= KW_MAX; k++) A[r][k] = has_bytes ? b0[k < last ? k : last] : 0ULL;
     }
 #pragma unroll
     for (int r = 0; r < R; r++) {
       const int64_t i = j0 + r * stride;
       if (i >= n) break;
       int64_t code = 0;
-      if (ok[r]) {
-        if (key_inline(k[r], &code)) {
+      if (bit_get(kv, i) && bit_get(rv, i)) {
+        // key_words from the loaded aligned words
+        const uint64_t a = (uint64_t)(kbytes + o0[r]);
+        const int sh = (int)(a & 7) * 8;
+        DKey k;
+        k.len = len[r];
+        k.sk = k.len <= 8 * KW_MAX;
+#pragma unroll
+        for (int q = 0; q < KW_MAX; q++) {
+          uint64_t x = sh ? (A[r][q] >> sh) | (A[r][q + 1] << (64 - sh)) : A[r][q];
+          const int64_t left = k.len - 8 * q;
+          if (left <= 0) x = 0;
+          else if (left < 8) x &= (1ULL << (8 * left)) - 1;
+          k.kw[q] = x;
+        }
+        if (key_inline(k, &code)) {
           ninl++;
         } else {
           code = KID_DICT;
@@ -905,8 +936,11 @@ khip_status dict_map(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8
   if (d.last_inline != 0 || (++d.maps & 15) == 0) {
     unsigned long long* nd = d.ctr.as<unsigned long long>() + 4 + 2 * DICT_NL + 2;
     KHIP_TRY_HIP(hipMemsetAsync(nd, 0, 16, s));
-    hipLaunchKernelGGL(k_key_inline, dim3(grid_for(ceil_div(n, 8LL), 256, 4096)), dim3(256), 0, s, koff, kbytes, kv, rv,
-                       ts, n, kid, khash, nd);
+    // rows per thread (1 / 2 / 4 / 8: 751 / 740 / 807 / 982 us on C2 --utf8, profiles/r05/ab/inline_rows.txt)
+    const int ir = (int)knob("KHIP_INLINE_R", 2);
+    auto ik = ir >= 8 ? k_key_inline<8> : (ir >= 4 ? k_key_inline<4> : (ir >= 2 ? k_key_inline<2> : k_key_inline<1>));
+    hipLaunchKernelGGL(ik, dim3(grid_for(ceil_div(n, (int64_t)std::max(ir, 1)), 256, 4096)), dim3(256), 0, s, koff, kbytes, kv,
+                       rv, ts, n, kid, khash, nd);
     KHIP_TRY_HIP(hipGetLastError());
     unsigned long long h[2] = {0, 0};
     KHIP_TRY_HIP(hipMemcpyAsync(h, nd, 16, hipMemcpyDeviceToHost, s));
