@@ -493,7 +493,7 @@ __device__ __forceinline__ bool dslot_eq(const ulonglong2& a, const ulonglong2& 
 // rows: null (row j = j) or a row list (the retry pass).  lists: DICT_NL regions of lcap entries
 // [slot | the entry's byte offset in its list << 34]; lw[L]: entries << 40 | entry bytes of list L.
 // nd[0] += the rows that probed (valid, not inline), nd[1] += the rows left pending (counted per
-// wave by ballots, one atomic per wave at the end: no barrier of their own).
+// wave by ballots, summed per block in LDS at the end: one global atomic per block).
 __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slots, uint64_t dmask,
                                                     const uint8_t* __restrict__ arena, const int64_t* __restrict__ koff,
                                                     const uint8_t* __restrict__ kbytes, const uint8_t* __restrict__ kv,
@@ -505,8 +505,10 @@ __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slo
                                                     uint64_t fpm, unsigned long long* __restrict__ nd) {
   __shared__ unsigned long long wsum[4];  // per wave: claims << 40 | entry bytes
   __shared__ unsigned long long bbase;
+  __shared__ unsigned long long bsum[2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int L = blockIdx.x & (DICT_NL - 1);
+  if (threadIdx.x < 2) bsum[threadIdx.x] = 0;
   unsigned long long bprobed = 0, bpend = 0;  // (the wave's counts over its tiles)
   for (int64_t j0 = blockIdx.x * (int64_t)blockDim.x; j0 < n; j0 += (int64_t)gridDim.x * blockDim.x) {
     const int64_t j = j0 + threadIdx.x;
@@ -593,8 +595,11 @@ __global__ __launch_bounds__(256) void k_dict_probe(ulonglong2* __restrict__ slo
       else *fail = 2;  // (lcap covers every row a list's blocks can claim)
     }
   }
-  if (lane == 0 && bprobed) atomicAdd(&nd[0], bprobed);
-  if (lane == 0 && bpend) atomicAdd(&nd[1], bpend);
+  __syncthreads();
+  if (lane == 0 && bprobed) atomicAdd(&bsum[0], bprobed);
+  if (lane == 0 && bpend) atomicAdd(&bsum[1], bpend);
+  __syncthreads();
+  if (threadIdx.x < 2 && bsum[threadIdx.x]) atomicAdd(&nd[threadIdx.x], bsum[threadIdx.x]);
 }
 
 // The inline ids of a batch, before any dictionary work: rows without a key get 0, inline keys
@@ -676,16 +681,57 @@ __global__ __launch_bounds__(256) void k_key_inline(const int64_t* __restrict__ 
   if (threadIdx.x < 2 && bsum[threadIdx.x]) atomicAdd(&nd[threadIdx.x], (unsigned long long)bsum[threadIdx.x]);
 }
 
-// One thread per claim (list L, entry t): the arena entry at its list's base + its byte offset, the
-// slot made resident with the key's words, the claiming row's id.  lbase[L]: the list's arena base.
+// The lists' arena bases after a probe round (one block, a thread per list): lbase[L] = the arena's
+// used bytes + the entry bytes of the lists before L; the used bytes and the key count advance.
+// Nothing when the round failed (c's first word: the probe's failure flag).
+__global__ __launch_bounds__(1024) void k_dict_bases(unsigned long long* __restrict__ c,
+                                                     const unsigned long long* __restrict__ lw,
+                                                     int64_t* __restrict__ lbase) {
+  static_assert(DICT_NL == 1024, "a thread per list");
+  __shared__ unsigned long long ws[16], wk[16];
+  if (*(const volatile int*)c != 0) return;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const unsigned long long x = lw[t];
+  const unsigned long long by = x & ((1ULL << 40) - 1), ke = x >> 40;
+  unsigned long long incl = by, kin = ke;
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long y = __shfl_up(incl, off, 64), z = __shfl_up(kin, off, 64);
+    if (lane >= off) {
+      incl += y;
+      kin += z;
+    }
+  }
+  if (lane == 63) {
+    ws[wave] = incl;
+    wk[wave] = kin;
+  }
+  __syncthreads();
+  unsigned long long before = 0, tot = 0, ktot = 0;
+  for (int k = 0; k < 16; k++) {
+    before += k < wave ? ws[k] : 0ULL;
+    tot += ws[k];
+    ktot += wk[k];
+  }
+  lbase[t] = (int64_t)(c[1] + before + incl - by);
+  __syncthreads();  // (every thread has read c[1])
+  if (t == 0) {
+    c[1] += tot;
+    c[2] += ktot;
+  }
+}
+
+// One thread per claim (list L, entries t, t + stride, ...): the arena entry at its list's base +
+// its byte offset, the slot made resident with the key's words, the claiming row's id.  lbase[L]:
+// the list's arena base.  Nothing when the round failed.
 __global__ __launch_bounds__(256) void k_dict_commit(ulonglong2* __restrict__ slots, const uint64_t* __restrict__ lists,
                                                      int64_t lcap, const unsigned long long* __restrict__ lw,
                                                      const int64_t* __restrict__ lbase, uint8_t* __restrict__ arena,
                                                      const int64_t* __restrict__ koff, const uint8_t* __restrict__ kbytes,
-                                                     int64_t* __restrict__ kid) {
+                                                     int64_t* __restrict__ kid, const unsigned long long* __restrict__ c) {
+  if (*(const volatile int*)c != 0) return;
   const int L = blockIdx.y;
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (t >= (int64_t)(lw[L] >> 40)) return;
+  const int64_t cntL = (int64_t)(lw[L] >> 40);
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < cntL; t += (int64_t)gridDim.x * blockDim.x) {
   const uint64_t le = lists[(uint64_t)L * lcap + t];
   const uint64_t slot = le & ((1ULL << 34) - 1);
   const uint64_t w = slots[2 * slot].x;
@@ -705,6 +751,7 @@ __global__ __launch_bounds__(256) void k_dict_commit(ulonglong2* __restrict__ sl
   slots[2 * slot + 1] = make_ulonglong2(k.len <= 16 ? k.kw[0] : 0ULL, k.len <= 16 && k.len > 8 ? k.kw[1] : 0ULL);
   slots[2 * slot] = make_ulonglong2((1ULL << 62) | (fp << 40) | ((uint64_t)o >> 3), (uint64_t)o | lenw);
   kid[r] = o;
+  }
 }
 
 // Rows left pending on a slot another row claimed: the slot is resident now.  A different key of
@@ -714,7 +761,10 @@ __global__ __launch_bounds__(256) void k_dict_resolve(const ulonglong2* __restri
                                                       const int64_t* __restrict__ koff,
                                                       const uint8_t* __restrict__ kbytes, const int64_t* __restrict__ rows,
                                                       int64_t n, int64_t* __restrict__ kid,
-                                                      int64_t* __restrict__ retry, unsigned long long* __restrict__ nretry) {
+                                                      int64_t* __restrict__ retry, unsigned long long* __restrict__ nretry,
+                                                      const unsigned long long* __restrict__ c,
+                                                      const unsigned long long* __restrict__ npend) {
+  if (*(const volatile int*)c != 0 || *npend == 0) return;  // (a failed round, or no row pending)
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = rows ? rows[j] : j;
     const int64_t x = kid[i];
@@ -878,53 +928,35 @@ static khip_status dict_round(KeyDict& d, hipStream_t s, const int64_t* koff, co
   // a list takes the claims of blocks L, L + DICT_NL, ...: at most every row those blocks visit
   const int64_t lcap = ceil_div(g, DICT_NL) * 256 * ceil_div(n, 256LL * g);
   KHIP_TRY(d.lists.ensure((size_t)lcap * DICT_NL * 8));
+  KHIP_TRY(d.retry.ensure((size_t)std::max<int64_t>(n, 1) * 8));
   KHIP_TRY_HIP(hipMemsetAsync(c, 0, 8, s));
   KHIP_TRY_HIP(hipMemsetAsync(c + 3, 0, 8 + 8 * DICT_NL, s));
   KHIP_TRY_HIP(hipMemsetAsync(nd, 0, 16, s));
+  // probe → list bases → commit → resolve, with no host round trip in between: each later kernel
+  // does nothing when the probe failed (the table is grown and the round mapped again)
   hipLaunchKernelGGL(k_dict_probe, dim3(g), dim3(256), 0, s, d.slots.as<ulonglong2>(), (uint64_t)(d.dcap - 1),
                      d.arena.as<uint8_t>(), koff, kbytes, kv, rv, ts, rows, n, kid, khash, d.lists.as<uint64_t>(), lcap,
                      lw, (int*)c, dict_fp_mask(), nd);
-  KHIP_TRY_HIP(hipGetLastError());
-  std::vector<unsigned long long> h(4 + DICT_NL);
-  unsigned long long hn[2];
-  KHIP_TRY_HIP(hipMemcpyAsync(h.data(), c, h.size() * 8, hipMemcpyDeviceToHost, s));
-  KHIP_TRY_HIP(hipMemcpyAsync(hn, nd, 16, hipMemcpyDeviceToHost, s));
-  KHIP_TRY_HIP(hipStreamSynchronize(s));
-  *failed = h[0] != 0;
-  *nretry = 0;
-  d.round_probed = (int64_t)hn[0];
-  if (!rows) d.last_probed = d.round_probed;  // (the first round sees every row)
-  if (*failed) return KHIP_OK;
-  // each list's arena region: the prefix of the lists' entry bytes after the arena's used part
-  std::vector<int64_t> base(DICT_NL);
-  int64_t used = (int64_t)h[1], mx = 0, keys = 0;
-  for (int L = 0; L < DICT_NL; L++) {
-    base[L] = used;
-    used += (int64_t)(h[4 + L] & ((1ULL << 40) - 1));
-    mx = std::max<int64_t>(mx, (int64_t)(h[4 + L] >> 40));
-    keys += (int64_t)(h[4 + L] >> 40);
-  }
-  const unsigned long long tot[2] = {(unsigned long long)used, (unsigned long long)((int64_t)h[2] + keys)};
-  if (mx > 0) {
-    KHIP_TRY_HIP(hipMemcpyAsync(lbase, base.data(), DICT_NL * 8, hipMemcpyHostToDevice, s));
-    KHIP_TRY_HIP(hipMemcpyAsync(c + 1, tot, 16, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_dict_commit, dim3((unsigned)ceil_div(mx, 256), DICT_NL), dim3(256), 0, s,
-                       d.slots.as<ulonglong2>(), d.lists.as<uint64_t>(), lcap, lw, lbase, d.arena.as<uint8_t>(), koff,
-                       kbytes, kid);
-    KHIP_TRY_HIP(hipGetLastError());
-  }
-  if (hn[1] == 0) {  // no row pending on another's claim: nothing to resolve or retry
-    if (mx > 0) KHIP_TRY_HIP(hipStreamSynchronize(s));  // (`base` / `tot` were read)
-    return KHIP_OK;
-  }
-  KHIP_TRY(d.retry.ensure((size_t)std::max<int64_t>(n, 1) * 8));
+  hipLaunchKernelGGL(k_dict_bases, dim3(1), dim3(DICT_NL), 0, s, c, (const unsigned long long*)lw, lbase);
+  hipLaunchKernelGGL(k_dict_commit, dim3((unsigned)std::min<int64_t>(4, ceil_div(lcap, 256LL)), DICT_NL), dim3(256), 0,
+                     s, d.slots.as<ulonglong2>(), d.lists.as<uint64_t>(), lcap, lw, lbase, d.arena.as<uint8_t>(), koff,
+                     kbytes, kid, (const unsigned long long*)c);
   hipLaunchKernelGGL(k_dict_resolve, dim3(g), dim3(256), 0, s, d.slots.as<ulonglong2>(), d.arena.as<uint8_t>(), koff,
-                     kbytes, rows, n, kid, d.retry.as<int64_t>(), c + 3);
+                     kbytes, rows, n, kid, d.retry.as<int64_t>(), c + 3, (const unsigned long long*)c,
+                     (const unsigned long long*)(nd + 1));
   KHIP_TRY_HIP(hipGetLastError());
-  unsigned long long r = 0;
-  KHIP_TRY_HIP(hipMemcpyAsync(&r, c + 3, 8, hipMemcpyDeviceToHost, s));
-  KHIP_TRY_HIP(hipStreamSynchronize(s));  // (also: `base` / `tot` were read)
-  *nretry = (int64_t)r;
+  unsigned long long h[6];
+  KHIP_TRY_HIP(hipMemcpyAsync(h, c, 32, hipMemcpyDeviceToHost, s));
+  KHIP_TRY_HIP(hipMemcpyAsync(h + 4, nd, 16, hipMemcpyDeviceToHost, s));
+  KHIP_TRY_HIP(hipStreamSynchronize(s));
+  *failed = (h[0] & 0xFFFFFFFFULL) != 0;
+  d.round_probed = (int64_t)h[4];
+  if (!rows) d.last_probed = d.round_probed;  // (the first round sees every row)
+  *nretry = *failed ? 0 : (int64_t)h[3];
+  if (!*failed) {  // (cumulative over the map's rounds)
+    d.round_used = (int64_t)h[1];
+    d.round_keys = (int64_t)h[2];
+  }
   return KHIP_OK;
 }
 
@@ -973,6 +1005,8 @@ khip_status dict_map(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8
   unsigned long long* c = d.ctr.as<unsigned long long>();
   const unsigned long long start[3] = {0ULL, (unsigned long long)d.arena_used, 0ULL};
   KHIP_TRY_HIP(hipMemcpyAsync(c, start, 24, hipMemcpyHostToDevice, s));
+  d.round_used = d.arena_used;
+  d.round_keys = 0;
   const int64_t* rows = nullptr;
   int64_t m = n;
   DevBuf rl;  // a retry round's rows (the previous round's retry list)
@@ -995,12 +1029,9 @@ khip_status dict_map(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8
     rows = rl.as<int64_t>();
     m = nretry;
   }
-  unsigned long long h[3];
-  KHIP_TRY_HIP(hipMemcpyAsync(h, c, 24, hipMemcpyDeviceToHost, s));
-  KHIP_TRY_HIP(hipStreamSynchronize(s));
-  d.arena_used = (int64_t)h[1];
-  d.docc += (int64_t)h[2];
-  d.last_added = (int64_t)h[2];
+  d.arena_used = d.round_used;
+  d.docc += d.round_keys;
+  d.last_added = d.round_keys;
   return KHIP_OK;
 }
 

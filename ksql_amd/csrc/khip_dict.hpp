@@ -44,6 +44,7 @@ struct KeyDict {
   int64_t last_probed = 0;   // rows of the last map that probed the table (not inline)
   int64_t round_probed = 0;  // rows of the last probe round that probed it
   int64_t last_inline = -1;  // inline rows the last inline pass found (-1: none ran yet)
+  int64_t round_used = 0, round_keys = 0;  // arena bytes used / keys added after the last good round
   int64_t maps = 0;
 };
 

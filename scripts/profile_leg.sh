@@ -10,7 +10,7 @@ set -u
 TAG=$1; CFG=$2; shift 2
 EXTRA="$*"
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-SUF=$(echo "$EXTRA" | tr -c 'a-z0-9' '_' | sed 's/_*$//; s/^_*//')
+SUF=$(echo "$EXTRA" | tr -c 'a-z0-9' '_' | tr -s '_' | sed 's/_*$//; s/^_*//')
 OUT=gpurun_out/prof_$TAG/$CFG${SUF:+_$SUF}
 mkdir -p $OUT
 export TMPDIR=/tmp

@@ -58,10 +58,11 @@ def _changelog(rng, n, nsrc, ngroups, utf8_src, utf8_group):
     c1 = rng.integers(-10**15, 10**15, n)
     c2 = rng.uniform(-100, 100, n)
     cv = [rng.random(n) > 0.07 for _ in range(3)]
-    ka = {"utf8_keys": ["g%d" % g for g in grp]} if utf8_group else {"keys": grp}
+    # (digit keys take inline ids, the others the dictionary: khip_dict.hpp)
+    ka = {"utf8_keys": ["%d" % g if g % 2 else "g%d" % g for g in grp]} if utf8_group else {"keys": grp}
     b = abi.HostBatch(ts, key_valid=gvalid, row_valid=rvalid, cols=[c0, c1, c2], col_valid=cv, **ka)
-    sa = {"src_utf8_keys": ["pk-%d" % k if v else None for k, v in zip(pk, pkv)]} if utf8_src else \
-        {"src_keys": pk, "src_key_valid": pkv}
+    sa = {"src_utf8_keys": [("%d" % k if k % 3 == 0 else "pk-%d" % k) if v else None for k, v in zip(pk, pkv)]} \
+        if utf8_src else {"src_keys": pk, "src_key_valid": pkv}
     return b, sa, np.abs(c2)
 
 
