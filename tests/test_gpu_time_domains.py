@@ -499,10 +499,12 @@ def test_destroy_releases_stream_time_buffers(prod):
     k = rng.integers(0, 10_000, n)
     v = rng.integers(-100, 100, n)
     p = (k % P).astype(np.int32)
+    o = np.argsort(p, kind="stable")  # (each partition's rows one contiguous run, in time order)
+    tp, kp, vp, pp = t[o], k[o], v[o], p[o]
 
     def cycle():
         g = abi.AggHandle(prod, _desc(time_domain="PARTITION", n_partitions=P))
-        g.push(abi.HostBatch(t, keys=k, cols=[v], partition=p))
+        g.push(abi.HostBatch(tp, keys=kp, cols=[vp], partition=pp))
         g.close()
         h = abi.AggHandle(prod, _desc(time_domain="SUPPLIED"))
         st, _ = h.stream_time_scan(abi.HostBatch(t, keys=k), -1)

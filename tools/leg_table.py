@@ -2,7 +2,9 @@
 """DESIGN.md's measurement table from bench JSON lines: one row per file (the last JSON line of
 each), with records/s, ms/step, the byte basis of roofline.frac, frac, counter bytes per record
 (roofline.traffic / records) and the CPU baseline at 1 / 4 / 16 threads.
-usage: leg_table.py <label>=<file.jsonl> ..."""
+usage: leg_table.py <label>=<file.jsonl>[@<traffic.json key>] ...  (@key: the counter bytes from
+profiles/traffic.json instead of the line's own roofline.traffic, for lines run before the leg's
+counters were measured)"""
 import json
 import sys
 
@@ -16,6 +18,9 @@ def main():
     print("|---|---:|---:|---:|---:|---:|---|")
     for arg in sys.argv[1:]:
         label, path = arg.rsplit("=", 1)
+        tkey = None
+        if "@" in path:
+            path, tkey = path.split("@", 1)
         d = [json.loads(l) for l in open(path) if l.startswith("{")][-1]
         r = d.get("roofline") or {}
         c = d.get("cpu_baseline") or {}
@@ -24,6 +29,10 @@ def main():
              cfg.get("records") or 0)
         tr = r.get("traffic")
         cb = "%.0f" % (tr / n) if tr and n else "—"
+        if tkey:
+            import os
+            with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "traffic.json")) as f:
+                cb = "%.0f" % json.load(f)[tkey]["hbm_bytes_per_record"]
         cpu = "—"
         if c:
             one = (c.get("single_thread") or {}).get("value")
