@@ -74,7 +74,6 @@ enum {
   CI_KBASE = 18,   // the key base of this push's records (the scatters)
   CI_KSHIFT = 19,  // kmin - kbase: the refines rebase the records to the key minimum
   CI_KFAIL = 20,   // some key fell outside the records' key field above kbase (the scatters)
-  CI_COMB = 21,    // value records of this push are combined per (key, pane) by the refine (HOPPING)
   CI_N = 24
 };
 
@@ -473,7 +472,7 @@ __device__ __forceinline__ void chunk_map(const uint32_t* __restrict__ rp, const
 // merge and commit use.  Declined: nothing persistent is touched.
 __global__ __launch_bounds__(1024) void k_c1_check(
     const int64_t* __restrict__ tilestat, int64_t nT, int64_t size, int64_t adv, FastDiv fd, int64_t grace,
-    int64_t close0, int fresh, int log2B, int log2P, int wide, int ch, int kbmax, int pbits, int comb,
+    int64_t close0, int fresh, int log2B, int log2P, int wide, int ch, int kbmax, int pbits,
     const int64_t* __restrict__ bb, int* __restrict__ cstart,
     int64_t* __restrict__ ci, int64_t* __restrict__ stream_time, int64_t* __restrict__ res,
     unsigned long long* __restrict__ ctr, unsigned long long* __restrict__ closed_ctr, unsigned long long closed_n) {
@@ -590,9 +589,6 @@ __global__ __launch_bounds__(1024) void k_c1_check(
   ci[CI_KRANGE] = (int64_t)krange;
   ci[CI_ID32] = !wide && kbits + wbits + pbits <= 31 ? 1 : 0;  // pbits: the pane flag
   ci[CI_WIDE] = wide;
-  // partials (k_c1v_refine_comb) when asked for and the push's times fit the 32-bit form the merge
-  // and the refine compute panes in (ts - window start < 2^32)
-  ci[CI_COMB] = comb && pbits && gmx >= 0 && (uint64_t)(gmx - lo * adv) < ((uint64_t)1 << 32) ? 1 : 0;
   ci[CI_TMIN] = gmx >= 0 ? gmn : 0;
   ci[CI_TMAX] = gmx;
   ci[CI_NCHUNK] = acc;
@@ -1540,7 +1536,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     int log2P, int fbits, ulonglong2* __restrict__ srec, uint16_t* __restrict__ seg, const int64_t* __restrict__ ci,
     const uint32_t* __restrict__ rpos, const uint16_t* __restrict__ roff, int64_t nSt, int64_t S,
     const uint32_t* __restrict__ cinfo) {
-  if (ci_ld(ci, CI_GATE) == 0 || ci_ld(ci, CI_COMB) != 0) return;  // (combined: k_c1v_refine_comb)
+  if (ci_ld(ci, CI_GATE) == 0) return;
   const int w = blockIdx.x;
   if (w >= (int)ci_ld(ci, CI_NCHUNK)) return;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1619,205 +1615,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (rank[u] != 0xFFFFFFFFu) stage[sbase[f[u]] + rank[u]] = r[u];
   __syncthreads();
   for (int j = threadIdx.x; j < nv; j += NT) srec[lo + j] = stage[j];
-}
-
-// HOPPING pushes (k_c1_check sets CI_COMB): the chunk's records of one (key, pane) become ONE
-// partial record before the merge.  A refine chunk spreads C1V_CH records over F partitions, ~32
-// per partition, and a partition holds few keys whose records of a chunk share a pane (C3: ~6 keys:
-// ~5 records per (key, pane)), so the merge applies several times fewer updates.  The records are
-// counting-sorted by (partition, HB bits of the key hash) — a key's records become contiguous
-// unless another key shares its bin — and each of NT / 2 threads cuts its 2U consecutive records
-// into runs of one (key, pane): a run is a partial, written at its place in the chunk's order
-// (3 pairs, 48 B): {krel << 32 | largest ts - T0, COUNT(*) << 32 | non-null count}, {sum of the
-// non-null values (f64 / i64 bits), smallest order key}, {largest order key, 0}.  The segment
-// table counts partials.  Runs are cut at thread boundaries (a run = a partial, never a mix).
-constexpr int C1V_HB = 4;  // key-hash bits below the partition in the sort (F << HB bins)
-__device__ __forceinline__ void c1v_partial_store(ulonglong2* __restrict__ dst, uint64_t krel, int32_t tmax, uint32_t cs,
-                                                  uint32_t cv, uint64_t sum, int64_t mn, int64_t mx) {
-  dst[0] = make_ulonglong2((krel << 32) | (uint32_t)tmax, ((uint64_t)cs << 32) | cv);
-  dst[1] = make_ulonglong2(sum, (uint64_t)mn);
-  dst[2] = make_ulonglong2((uint64_t)mx, 0ULL);
-}
-template <int U, int NT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_c1v_refine_comb(
-    const ulonglong2* __restrict__ srcA, const int64_t* __restrict__ bb, const int* __restrict__ cstart, int log2B,
-    int log2P, int fbits, ulonglong2* __restrict__ srecP, uint16_t* __restrict__ seg, const int64_t* __restrict__ ci,
-    const uint32_t* __restrict__ rpos, const uint16_t* __restrict__ roff, int64_t nSt, int64_t S,
-    const uint32_t* __restrict__ cinfo, FastDiv32 fd32, int64_t adv, int f64) {
-  if (ci_ld(ci, CI_GATE) == 0 || ci_ld(ci, CI_COMB) == 0) return;
-  const int w = blockIdx.x;
-  if (w >= (int)ci_ld(ci, CI_NCHUNK)) return;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ int lb, lnv;
-  __shared__ int wsum[NT / 64];
-  constexpr int CH = U * NT;
-  static_assert(CH == C1V_CH, "refine chunk");
-  constexpr int R2 = 2 * U;  // records per combining thread (NT / 2 of them)
-  const int F = 1 << fbits, B = 1 << log2B;
-  const int NB = F << C1V_HB;
-  const int CW = NB > CH / 2 ? NB : CH / 2;  // words of the bins / run-place area
-  uint32_t* cnt = (uint32_t*)smem;            // [NB] bin counts → bases; then [CH] u16 run places
-  uint32_t* posF = cnt + CW;                  // [F + 1] each partition's first position
-  ulonglong2* stage = (ulonglong2*)(smem + ((((size_t)CW + F + 1) * 4 + 15) & ~(size_t)15));
-  for (int k = threadIdx.x; k < NB; k += NT) cnt[k] = 0u;
-  if (threadIdx.x == 0) lb = -1;
-  __syncthreads();
-  for (int b = threadIdx.x; b < B; b += NT)
-    if (cstart[b] <= w && w < cstart[b + 1]) lb = b;
-  __syncthreads();
-  const int b = lb;
-  if (b < 0) return;
-  const int64_t lo = bb[b] + (int64_t)(w - cstart[b]) * CH;
-  const int64_t bend = bb[b + 1];
-  const int len = (int)(bend - lo < CH ? bend - lo : CH);
-  const int64_t kmin = ci_ld(ci, CI_KMINC);
-  const uint64_t kshift = (uint64_t)ci_ld(ci, CI_KSHIFT) << 32;  // records hold key - kb
-  const int shift = 64 - log2P;
-  const uint32_t tsh32 = (uint32_t)(ci_ld(ci, CI_T0) - ci_ld(ci, CI_WBASE) * adv);  // ts - wstart = ts32 + tsh32
-  const uint32_t* rp = rpos + (int64_t)b * nSt;
-  const uint16_t* ro = roff + (int64_t)b * nSt;
-  chunk_map(rp, ro, cinfo, w, S, lo, len, (uint32_t*)stage);
-  ulonglong2 r[U];
-  uint32_t bin[U], rank[U];
-#pragma unroll
-  for (int u = 0; u < U; u++) {
-    const int j = threadIdx.x + u * NT;
-    const uint32_t src = ((const uint32_t*)stage)[j < len ? j : len - 1];
-    r[u] = ld_nt2(srcA + src);
-    r[u].x -= kshift;
-  }
-#pragma unroll
-  for (int u = 0; u < U; u++) {
-    const int j = threadIdx.x + u * NT;
-    const bool v = j < len && (uint32_t)r[u].x != C1_SENT;
-    const uint64_t kh = key_hash(kmin + (int64_t)((r[u].x >> 32) & 0x7FFFFFFFull));
-    bin[u] = (uint32_t)((((kh >> shift) & (uint64_t)(F - 1)) << C1V_HB) | ((kh >> (shift - C1V_HB)) & ((1u << C1V_HB) - 1)));
-    rank[u] = v ? atomicAdd(&cnt[bin[u]], 1u) : 0xFFFFFFFFu;
-  }
-  __syncthreads();
-  {  // exclusive prefix over the NB bins in place (each thread a run of consecutive bins)
-    const int per = (NB + NT - 1) / NT, k0 = threadIdx.x * per;
-    uint32_t sum = 0;
-    for (int k = k0; k < k0 + per && k < NB; k++) sum += cnt[k];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t incl = sum;
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t y = __shfl_up(incl, off, 64);
-      if (lane >= off) incl += y;
-    }
-    if (lane == 63) wsum[wave] = (int)incl;
-    __syncthreads();
-    uint32_t run = incl - sum, tot = 0;
-    for (int k = 0; k < NT / 64; k++) {
-      run += k < wave ? (uint32_t)wsum[k] : 0u;
-      tot += (uint32_t)wsum[k];
-    }
-    for (int k = k0; k < k0 + per && k < NB; k++) {
-      const uint32_t c = cnt[k];
-      cnt[k] = run;
-      run += c;
-    }
-    if (threadIdx.x == 0) lnv = (int)tot;
-  }
-  __syncthreads();
-  const int nv = lnv;
-  for (int f = threadIdx.x; f <= F; f += NT) posF[f] = f < F ? cnt[f << C1V_HB] : (uint32_t)nv;
-#pragma unroll
-  for (int u = 0; u < U; u++)
-    if (rank[u] != 0xFFFFFFFFu) stage[cnt[bin[u]] + rank[u]] = r[u];
-  __syncthreads();
-  // runs: thread t < NT / 2 owns stage positions [R2 t, R2 t + R2)
-  const int j0 = (int)threadIdx.x * R2;
-  auto ident = [&](const ulonglong2& x, uint64_t* krel, uint32_t* pane) {
-    *krel = (x.x >> 32) & 0x7FFFFFFFull;
-    *pane = fast_udiv32((uint32_t)x.x + tsh32, fd32);
-  };
-  int heads = 0;
-  if (threadIdx.x < NT / 2) {
-    uint64_t pk = ~0ULL;
-    uint32_t pp = 0;
-    for (int j = j0; j < j0 + R2 && j < nv; j++) {
-      uint64_t k;
-      uint32_t pn;
-      ident(stage[j], &k, &pn);
-      heads += (j == j0 || k != pk || pn != pp) ? 1 : 0;
-      pk = k;
-      pp = pn;
-    }
-  }
-  int hbase;
-  {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int incl = heads;
-    for (int off = 1; off < 64; off <<= 1) {
-      const int y = __shfl_up(incl, off, 64);
-      if (lane >= off) incl += y;
-    }
-    __syncthreads();  // (every thread is done with the bin bases: cnt becomes the run places)
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    int before = 0, tot = 0;
-    for (int k = 0; k < NT / 64; k++) {
-      before += k < wave ? wsum[k] : 0;
-      tot += wsum[k];
-    }
-    hbase = before + incl - heads;
-    if (threadIdx.x == 0) lnv = tot;
-  }
-  uint16_t* hp = (uint16_t*)cnt;  // [CH + 1]: the partial index of each run's first position
-  if (threadIdx.x < NT / 2 && j0 < nv) {
-    int o = hbase - 1;
-    uint64_t pk = ~0ULL, ksum = 0;
-    uint32_t pp = 0, cs = 0, cv = 0;
-    int32_t tmax = INT32_MIN;
-    int64_t mn = INT64_MAX, mx = INT64_MIN;
-    double dsum = 0.0;
-    for (int j = j0; j < j0 + R2 && j < nv; j++) {
-      const ulonglong2 x = stage[j];
-      uint64_t k;
-      uint32_t pn;
-      ident(x, &k, &pn);
-      if (j == j0 || k != pk || pn != pp) {
-        if (o >= hbase)
-          c1v_partial_store(srecP + 3 * (lo + o), pk, tmax, cs, cv, f64 ? __builtin_bit_cast(uint64_t, dsum) : ksum, mn, mx);
-        o++;
-        hp[j] = (uint16_t)o;
-        pk = k;
-        pp = pn;
-        cs = cv = 0;
-        tmax = INT32_MIN;
-        mn = INT64_MAX;
-        mx = INT64_MIN;
-        dsum = 0.0;
-        ksum = 0;
-      }
-      const int32_t t32 = (int32_t)(uint32_t)x.x;
-      tmax = t32 > tmax ? t32 : tmax;
-      cs++;
-      if (x.x >> 63) {  // a non-null value
-        cv++;
-        int64_t okey;
-        if (f64) {
-          const double d = __builtin_bit_cast(double, x.y);
-          dsum += d;
-          okey = f64_order_key(d);
-        } else {
-          ksum += x.y;
-          okey = (int64_t)x.y;
-        }
-        mn = okey < mn ? okey : mn;
-        mx = okey > mx ? okey : mx;
-      }
-    }
-    c1v_partial_store(srecP + 3 * (lo + o), pk, tmax, cs, cv, f64 ? __builtin_bit_cast(uint64_t, dsum) : ksum, mn, mx);
-  }
-  __syncthreads();
-  const int np = lnv;
-  for (int f = threadIdx.x; f < F; f += NT) {
-    const uint32_t pos = posF[f];
-    seg[(int64_t)w * (F + 1) + f] = (uint16_t)(pos < (uint32_t)nv ? hp[pos] : np);
-  }
-  if (threadIdx.x == 0) seg[(int64_t)w * (F + 1) + F] = (uint16_t)np;
 }
 
 // Merge parameters of the value pipeline.  LDS: ids ID[H + 64] | 8-byte planes (sum, min, max,
@@ -1978,7 +1775,7 @@ __device__ __forceinline__ bool c1v_is_pane(ID id, int wbits) {
 
 // WPE: waves per SIMD the register budget allows (4: <= 128 VGPRs, two workgroups per CU; 2:
 // <= 256, one)
-template <int NT, int AU0, class ID, bool PANES, int WPE, int PM, bool COMB = false>
+template <int NT, int AU, class ID, bool PANES, int WPE, int PM>
 __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
     const C1VQ* __restrict__ qp, const uint32_t* __restrict__ work, int64_t nwork, const int64_t* __restrict__ bb,
     const int* __restrict__ cstart, const uint16_t* __restrict__ seg, const ulonglong2* __restrict__ srec, int first,
@@ -1989,9 +1786,6 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
     unsigned long long* __restrict__ hclosed, uint32_t* __restrict__ prn, unsigned long long* __restrict__ dbg) {
   if (ci_ld(ci, CI_GATE) == 0) return;
   if ((ci_ld(ci, CI_ID32) != 0) != (sizeof(ID) == 4)) return;  // the other identity width's
-  if ((ci_ld(ci, CI_COMB) != 0) != COMB) return;               // the other record form's
-  // COMB: the records are k_c1v_refine_comb's 48-byte partials (3 pairs), one per lane and chunk
-  constexpr int AU = COMB ? 1 : AU0;
   const C1VQ& q = *qp;  // in device memory: its fields are loaded where used (SGPR pressure)
   constexpr int NW = NT / 64;
   constexpr ID EMPTY = (ID)~(ID)0;
@@ -2171,9 +1965,8 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
     it.rn = spre[nseg];
     it.segb = segb;
   };
-  ulonglong2 ra[AU], rb[AU], ra1[AU], rb1[AU], ra2[AU], rb2[AU];  // (x1, x2: COMB partials' pairs 1, 2)
-  auto load = [&](ulonglong2 (&x)[AU], ulonglong2 (&x1)[AU], ulonglong2 (&x2)[AU], int64_t l0, int64_t rn, int nseg,
-                  int segb) {
+  ulonglong2 ra[AU], rb[AU];
+  auto load = [&](ulonglong2 (&x)[AU], int64_t l0, int64_t rn, int nseg, int segb) {
 #pragma unroll
     for (int u = 0; u < AU; u++) {
       int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
@@ -2190,19 +1983,12 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
           else hi = mid;
         }
       }
-      const int64_t at = (int64_t)sbs[lo] + li;
-      if constexpr (COMB) {
-        x[u] = ld_nt2(srec + 3 * at);
-        x1[u] = ld_nt2(srec + 3 * at + 1);
-        x2[u] = ld_nt2(srec + 3 * at + 2);
-      } else {
-        x[u] = ld_nt2(srec + at);
-      }
+      x[u] = ld_nt2(srec + ((int64_t)sbs[lo] + li));
     }
   };
   auto load01 = [&](const It& x) {
-    if (x.rn > 0) load(ra, ra1, ra2, 0, x.rn, x.nseg, x.segb);
-    if (x.rn > (int64_t)AU * NT) load(rb, rb1, rb2, (int64_t)AU * NT, x.rn, x.nseg, x.segb);
+    if (x.rn > 0) load(ra, 0, x.rn, x.nseg, x.segb);
+    if (x.rn > (int64_t)AU * NT) load(rb, (int64_t)AU * NT, x.rn, x.nseg, x.segb);
   };
   lds_barrier();  // the table and flags initialised above
   Pre pr{};
@@ -2270,8 +2056,7 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
     C1M_T(0);
     // 1. records → their pane (window) entries: the AU identities' CASes back to back, then the
     //    collisions probe on together (as k_c1_merge)
-    auto apply = [&](const ulonglong2 (&xr)[AU], const ulonglong2 (&x1)[AU], const ulonglong2 (&x2)[AU], int64_t l0,
-                     auto R32) {
+    auto apply = [&](const ulonglong2 (&xr)[AU], int64_t l0, auto R32) {
       ID id[AU];
       uint32_t e[AU];
       bool pend[AU], claimed[AU];
@@ -2330,19 +2115,14 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       for (int u = 0; u < AU; u++) {
         if (id[u] == EMPTY) continue;
         const uint64_t w0 = xr[u].x;
-        const uint32_t tr = (uint32_t)((int32_t)(uint32_t)w0 - tmin32) + 1u;
-        if constexpr (COMB) {  // a partial: its counts, sum and order-key bounds
-          c1v_add<PM>(q, smem, e[u], tr, (uint32_t)(xr[u].y >> 32), (uint32_t)xr[u].y, x1[u].x, (int64_t)x1[u].y,
-                      (int64_t)x2[u].x);
-        } else {
-          int64_t ok_ = (int64_t)xr[u].y;
-          if (C1VP<PM>{q}.f64() && (C1VP<PM>{q}.mn() || C1VP<PM>{q}.mx())) {
-            double d;
-            __builtin_memcpy(&d, &xr[u].y, 8);
-            ok_ = f64_order_key(d);
-          }
-          c1v_add<PM>(q, smem, e[u], tr, 1u, (w0 >> 63) ? 1u : 0u, xr[u].y, ok_, ok_);
+        int64_t ok_ = (int64_t)xr[u].y;
+        if (C1VP<PM>{q}.f64() && (C1VP<PM>{q}.mn() || C1VP<PM>{q}.mx())) {
+          double d;
+          __builtin_memcpy(&d, &xr[u].y, 8);
+          ok_ = f64_order_key(d);
         }
+        c1v_add<PM>(q, smem, e[u], (uint32_t)((int32_t)(uint32_t)w0 - tmin32) + 1u, 1u, (w0 >> 63) ? 1u : 0u, xr[u].y, ok_,
+                ok_);
       }
     };
     const int64_t nch = (rn + (int64_t)AU * NT - 1) / ((int64_t)AU * NT);
@@ -2352,10 +2132,10 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       // set counts the other set's loads as in flight; the table-full check once per two chunks
       auto records = [&](auto R32) {
         for (int64_t c = 0; c < nch; c += 2) {
-          apply(ra, ra1, ra2, c * AU * NT, R32);
-          load(ra, ra1, ra2, (c + 2) * AU * NT, rn, nseg, segb);
-          apply(rb, rb1, rb2, (c + 1) * AU * NT, R32);
-          load(rb, rb1, rb2, (c + 3) * AU * NT, rn, nseg, segb);
+          apply(ra, c * AU * NT, R32);
+          load(ra, (c + 2) * AU * NT, rn, nseg, segb);
+          apply(rb, (c + 1) * AU * NT, R32);
+          load(rb, (c + 3) * AU * NT, rn, nseg, segb);
           if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
         }
       };
@@ -2363,15 +2143,15 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       else records(std::false_type{});
     } else if (rn > 0) {
       for (int64_t c = 0; c < nch; c += 2) {
-        if (r32) apply(ra, ra1, ra2, c * AU * NT, std::true_type{});
-        else apply(ra, ra1, ra2, c * AU * NT, std::false_type{});
+        if (r32) apply(ra, c * AU * NT, std::true_type{});
+        else apply(ra, c * AU * NT, std::false_type{});
         if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
-        if (c + 2 < nch) load(ra, ra1, ra2, (c + 2) * AU * NT, rn, nseg, segb);
+        if (c + 2 < nch) load(ra, (c + 2) * AU * NT, rn, nseg, segb);
         if (c + 1 >= nch) break;
-        if (r32) apply(rb, rb1, rb2, (c + 1) * AU * NT, std::true_type{});
-        else apply(rb, rb1, rb2, (c + 1) * AU * NT, std::false_type{});
+        if (r32) apply(rb, (c + 1) * AU * NT, std::true_type{});
+        else apply(rb, (c + 1) * AU * NT, std::false_type{});
         if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
-        if (c + 3 < nch) load(rb, rb1, rb2, (c + 3) * AU * NT, rn, nseg, segb);
+        if (c + 3 < nch) load(rb, (c + 3) * AU * NT, rn, nseg, segb);
       }
     }
     lds_barrier();
@@ -2691,15 +2471,6 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
   }
   KHIP_TRY(s.srec.ensure((size_t)(n + 1) * 16));  // (s.rw >= 2: no-ops)
   KHIP_TRY(s.srecA.ensure((size_t)(n + 1) * std::max(s.rw, 2) * 8));
-  // HOPPING value records: the refine combines a chunk's records per (key, pane) into partials
-  // (k_c1_check keeps the raw records when the push's times do not fit the 32-bit pane form)
-  const bool comb = panes && knob("KHIP_C1V_COMB", 0) != 0;
-  bool vq_f64 = false;
-  if (val) {
-    for (int o = 0; o < a->ap.n_ops; o++) vq_f64 = vq_f64 || a->ap.ops[o].kind == OP_ADD_F64;
-    vq_f64 = vq_f64 || a->ap.col_type[vcol] == KHIP_TYPE_DOUBLE;
-  }
-  if (comb) KHIP_TRY(s.srecP.ensure((size_t)(n + 1) * 48));
   if (!s.c1info.p) {
     KHIP_TRY(s.c1info.ensure(CI_N * 8));
     int64_t init[CI_N] = {};
@@ -2775,7 +2546,7 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
   // 4. accept or decline
   hipLaunchKernelGGL(k_c1_check, dim3(1), dim3(1024), 0, a->stream, s.tilemax.as<int64_t>(), nT,
                      a->desc.size_ms, adv, fd, a->grace, close0, s.res_fresh ? 1 : 0, log2B, s.log2P, wide ? 1 : 0,
-                     val ? C1V_CH : C1_CH, val ? 31 : 32, pbits, comb ? 1 : 0, s.c1bb.as<int64_t>(), cstart, ci,
+                     val ? C1V_CH : C1_CH, val ? 31 : 32, pbits, s.c1bb.as<int64_t>(), cstart, ci,
                      a->stream_time.as<int64_t>(), s.res.as<int64_t>(),
                      s.ctr.as<unsigned long long>(), s.closed_ctr.as<unsigned long long>(),
                      (unsigned long long)s.closed_n);
@@ -2791,16 +2562,6 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     hipLaunchKernelGGL(rk, dim3((unsigned)nchunk_max), dim3(C1_NT), lds, a->stream, (const ulonglong2*)s.srecA.p,
                        s.c1bb.as<int64_t>(), cstart, log2B, s.log2P, fbits, (ulonglong2*)s.srec.p, seg, ci,
                        (const uint32_t*)rp, (const uint16_t*)ro, nSt, S, (const uint32_t*)s.c1ci.as<uint32_t>());
-    if (comb) {  // (one of the two refines exits at once: CI_COMB)
-      auto ck = k_c1v_refine_comb<C1V_CH / C1_NT, C1_NT>;
-      const size_t cw = std::max<size_t>((size_t)F << C1V_HB, C1V_CH / 2);
-      const size_t clds = (((cw + F + 1) * 4 + 15) & ~(size_t)15) + (size_t)C1V_CH * 16;
-      hipFuncSetAttribute((const void*)ck, hipFuncAttributeMaxDynamicSharedMemorySize, (int)clds);
-      hipLaunchKernelGGL(ck, dim3((unsigned)nchunk_max), dim3(C1_NT), clds, a->stream, (const ulonglong2*)s.srecA.p,
-                         s.c1bb.as<int64_t>(), cstart, log2B, s.log2P, fbits, (ulonglong2*)s.srecP.p, seg, ci,
-                         (const uint32_t*)rp, (const uint16_t*)ro, nSt, S, (const uint32_t*)s.c1ci.as<uint32_t>(),
-                         make_fastdiv32((uint32_t)adv), adv, vq_f64 ? 1 : 0);
-    }
     KHIP_TRY_HIP(hipGetLastError());
   } else {
     constexpr int U = C1_CH / C1_NT;
@@ -2915,30 +2676,23 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
       vq.chg = a->changelog ? a->chg.as<uint8_t>() : nullptr;
       // the benchmarks' plane shapes have instantiations of their own (PM_C5, PM_C3), every other
       // one reads the planes from the parameters; AU 2 at <= 128 VGPRs (two workgroups per CU)
-      // (combining pushes launch the partial-record merge too; the one CI_COMB did not choose exits)
-      for (int cmb = 0; cmb < (comb ? 2 : 1); cmb++) {
-        auto pick = [&](auto pmc) {
-          constexpr int PMv = decltype(pmc)::value;
-          if (cmb)
-            return idw == 0 ? k_c1v_merge<512, 2, uint32_t, true, 4, PMv, true> : k_c1v_merge<512, 2, uint64_t, true, 4, PMv, true>;
-          return panes ? (idw == 0 ? k_c1v_merge<512, 2, uint32_t, true, 4, PMv> : k_c1v_merge<512, 2, uint64_t, true, 4, PMv>)
-                       : (idw == 0 ? k_c1v_merge<512, 2, uint32_t, false, 4, PMv> : k_c1v_merge<512, 2, uint64_t, false, 4, PMv>);
-        };
-        auto mk = v_pm == PM_C5 ? pick(std::integral_constant<int, PM_C5>{})
-                                : (v_pm == PM_C3 ? pick(std::integral_constant<int, PM_C3>{}) : pick(std::integral_constant<int, 0>{}));
-        hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (cmb == 0) {
-          KHIP_TRY(s.c1vq.ensure(sizeof(C1VQ)));
-          KHIP_TRY_HIP(hipMemcpyAsync(s.c1vq.p, &vq, sizeof(C1VQ), hipMemcpyHostToDevice, a->stream));
-        }
-        const int64_t vgrid = std::min<int64_t>(nwork, (int64_t)s.n_cu * (lds <= C1V_LDS2 ? v_wpc : 1));
-        hipLaunchKernelGGL(mk, dim3(vgrid), dim3(512), lds, a->stream, s.c1vq.as<C1VQ>(), wk, nwork, s.c1bb.as<int64_t>(), cstart, seg,
-                           (const ulonglong2*)(cmb ? s.srecP.p : s.srec.p), pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(),
-                           s.buf[1].as<uint64_t>(), s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
-                           s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
-                           s.closed_ctr.as<unsigned long long>(), ci,
-                           s.hnew.as<unsigned long long>(), s.ctr.as<unsigned long long>() + 12, s.prn.as<uint32_t>(), dbg);
-      }
+      auto pick = [&](auto pmc) {
+        constexpr int PMv = decltype(pmc)::value;
+        return panes ? (idw == 0 ? k_c1v_merge<512, 2, uint32_t, true, 4, PMv> : k_c1v_merge<512, 2, uint64_t, true, 4, PMv>)
+                     : (idw == 0 ? k_c1v_merge<512, 2, uint32_t, false, 4, PMv> : k_c1v_merge<512, 2, uint64_t, false, 4, PMv>);
+      };
+      auto mk = v_pm == PM_C5 ? pick(std::integral_constant<int, PM_C5>{})
+                              : (v_pm == PM_C3 ? pick(std::integral_constant<int, PM_C3>{}) : pick(std::integral_constant<int, 0>{}));
+      hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      KHIP_TRY(s.c1vq.ensure(sizeof(C1VQ)));
+      KHIP_TRY_HIP(hipMemcpyAsync(s.c1vq.p, &vq, sizeof(C1VQ), hipMemcpyHostToDevice, a->stream));
+      const int64_t vgrid = std::min<int64_t>(nwork, (int64_t)s.n_cu * (lds <= C1V_LDS2 ? v_wpc : 1));
+      hipLaunchKernelGGL(mk, dim3(vgrid), dim3(512), lds, a->stream, s.c1vq.as<C1VQ>(), wk, nwork, s.c1bb.as<int64_t>(), cstart, seg,
+                         (const ulonglong2*)s.srec.p, pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
+                         s.sel.as<uint8_t>(), s.cnt.as<int64_t>(), s.newcnt.as<unsigned long long>(),
+                         s.fail.as<uint8_t>(), s.ctr.as<unsigned long long>() + 2, close0, s.closed.as<uint64_t>(),
+                         s.closed_ctr.as<unsigned long long>(), ci,
+                         s.hnew.as<unsigned long long>(), s.ctr.as<unsigned long long>() + 12, s.prn.as<uint32_t>(), dbg);
     }
     for (int idw = wide ? 1 : 0; idw < 2 && !val; idw++) {
       auto mk = wide ? k_c1_merge<512, 3, uint64_t, true>

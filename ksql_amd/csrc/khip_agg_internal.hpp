@@ -429,7 +429,6 @@ struct PartState {
   bool res_fresh = true;
   // two-level scatter: pass-A records, per-tile bucket histogram / offsets, bucket scans
   DevBuf srecA, hcoarse, scan_tmpB, RB;
-  DevBuf srecP;  // HOPPING value records combined per (key, pane): k_c1v_refine_comb's partials
   // k_part_merge (delta-only LDS): entries, LDS bytes, plane layout (khip_agg_part.hip)
   int mH = 0, m_lds = 0, rt_off = 0, m_list_off = 0, n_cu = 256;
   int flag_off = 0;       // k_part_agg: LDS byte offset of the changelog flag plane

@@ -3587,7 +3587,7 @@ khip_status part_init(khip_agg* a, int64_t hint) {
 void part_release(khip_agg* a) {
   PartState& s = a->part;
   s.pinfo.release();
-  DevBuf* bufs[] = {&s.hcnt, &s.hnew, &s.srecA, &s.srecP, &s.hcoarse, &s.scan_tmpB, &s.RB, &s.wr, &s.res, &s.closed, &s.closed_ctr, &s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist,
+  DevBuf* bufs[] = {&s.hcnt, &s.hnew, &s.srecA, &s.hcoarse, &s.scan_tmpB, &s.RB, &s.wr, &s.res, &s.closed, &s.closed_ctr, &s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist,
                     &s.tilemax, &s.tilemin, &s.tilekr,
                     &s.tileprefix, &s.tpart, &s.scan_tmp, &s.srec, &s.work,
                     &s.c1rc, &s.c1rp, &s.c1ro, &s.c1scan, &s.c1ci, &s.c1bb, &s.c1seg, &s.c1info, &s.prn, &s.c1vq,
