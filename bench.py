@@ -924,7 +924,10 @@ def bench_hopping_double(args, lib, rank, world, local):
          {"workload": "hopping_double", "records_per_gpu": n, "keys_per_gpu": keys_here,
           "window": "HOPPING 60s/10s GRACE 60s (F=6)", "micro_batch": S, "pushes": len(batches),
           "windows_applied": st["windows_applied"], "windows_late": st["windows_late"],
-          "groups_per_gpu": int(groups), "parallelism": "key-hash shards x%d" % world},
+          "groups_per_gpu": int(groups), "parallelism": "key-hash shards x%d" % world,
+          "double_tolerance": "SUM / AVG within 1e-12 x sum|x| of the oracle's (summation order differs; equal to "
+                              "the north star's relative 1e-12 for these non-negative values, looser under "
+                              "cancellation: tests/test_gpu_parity.py assert_snap_equal); MIN / MAX, counts bit-exact"},
          roof, cpu)
 
 
