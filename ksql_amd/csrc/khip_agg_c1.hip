@@ -51,10 +51,6 @@ constexpr int C1_SEGB = 7;       // the merge's segment lookup: one entry per 32
 constexpr int C1_SEGOF = 512;    // item (the finest that fits 512 entries; past 64K records: binary search)
 constexpr uint32_t C1_SENT = 0x80000000u;  // low word of a sentinel record (ts - T0 never is)
 
-#ifndef KHIP_C1M_NOBR
-#define KHIP_C1M_NOBR 0
-#endif
-
 // c1info (int64) slots
 enum {
   CI_KMIN = 0,   // atomics (the scatters), reset by k_c1_check for the next push
@@ -1128,15 +1124,9 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       }
 #pragma unroll
       for (int u = 0; u < AU; u++) {
-#if KHIP_C1M_NOBR  // no branch: a lane without a record updates its dummy entry (never read)
-        const uint32_t ee = id[u] != EMPTY ? e[u] : dummy;
-        __hip_atomic_fetch_max(&rt[ee], tr[u], WG_RLX);
-        __hip_atomic_fetch_add(&ct[ee], 1u, WG_RLX);
-#else
         if (id[u] == EMPTY) continue;
         __hip_atomic_fetch_max(&rt[e[u]], tr[u], WG_RLX);
         __hip_atomic_fetch_add(&ct[e[u]], 1u, WG_RLX);
-#endif
       }
     };
     const int64_t nch = (rn + (int64_t)AU * NT - 1) / ((int64_t)AU * NT);
