@@ -775,8 +775,9 @@ typedef struct khip_sink_out {
 } khip_sink_out;
 
 /* Serialize rows into sink records (key bytes, value bytes or null).  The encoding runs on the
- * device; host rows are staged in and host outputs copied back.  On KHIP_E_BUFFER nothing is
- * written except key_len / value_len. */
+ * device; host rows are staged in and host outputs copied back.  On KHIP_E_BUFFER key_len /
+ * value_len hold the sizes needed and no bytes are written (device offset arrays, the lengths'
+ * workspace, are overwritten). */
 khip_status khip_sink_encode(khip_sink* s, const khip_sink_rows* rows, khip_sink_out* out);
 khip_status khip_sink_sync(khip_sink* s);
 khip_status khip_sink_destroy(khip_sink* s);

@@ -1067,9 +1067,10 @@ class SinkHandle:
                               bitorder="little")[:n].astype(bool)
         return [data[offs[i]:offs[i + 1]] if valid[i] else None for i in range(n)]
 
-    def encode(self, snap, tombstone=None, key_serialized=False):
+    def encode(self, snap, tombstone=None, key_serialized=False, device_out=False, align=0):
         """snap: a snapshot dict (AggHandle.snapshot() / changes() layout: key or key_bytes/key_offsets,
-        ws, we, values, nulls); host rows.  Returns (keys, values): lists of bytes / None."""
+        ws, we, values, nulls); host rows.  Returns (keys, values): lists of bytes / None.
+        device_out: into device buffers (the one-pass encoder), `align` bytes past 16-byte alignment."""
         n = int(snap["n"])
         keep = []
 
@@ -1104,6 +1105,8 @@ class SinkHandle:
         rows.col_null = cn
         if tombstone is not None:
             rows.tombstone = arr(np.asarray(tombstone, np.uint8), np.uint8)
+        if device_out:
+            return self._encode_device(rows, n, align)
         out = SinkOut()
         out.mem = MEM_HOST
         koff = np.zeros(n + 1, np.int64)
@@ -1123,6 +1126,44 @@ class SinkHandle:
         kbs, vbs = kb.tobytes(), vb.tobytes()
         keys = [kbs[koff[i]:koff[i + 1]] for i in range(n)]
         values = [None if vnull[i] else vbs[voff[i]:voff[i + 1]] for i in range(n)]
+        return keys, values
+
+    def _encode_device(self, rows, n, align):
+        """encode() into device outputs (tests): a first call with 1-byte capacities (KHIP_E_BUFFER
+        unless everything fits), then buffers of the exact sizes starting `align` bytes into a
+        0xAB-filled allocation with 16 guard bytes either side, which must come back untouched."""
+        import torch
+        dev = torch.device("cuda")
+        koff = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        voff = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        vnull = torch.zeros(max(n, 1), dtype=torch.uint8, device=dev)
+        out = SinkOut()
+        out.mem = MEM_DEVICE
+        out.key_offsets, out.value_offsets, out.value_null = koff.data_ptr(), voff.data_ptr(), vnull.data_ptr()
+        small = torch.zeros(2, dtype=torch.uint8, device=dev)
+        out.key_capacity = out.value_capacity = 1
+        out.key_bytes = out.value_bytes = small.data_ptr()
+        st = self.lib.sink_encode(self.h, C.byref(rows), C.byref(out))
+        kl, vl = out.key_len, out.value_len
+        if st == KHIP_E_BUFFER:
+            assert kl > 1 or vl > 1, (kl, vl)
+        else:
+            self.lib.check(st, "sink_encode")
+        g = 16 + align
+        kbuf = torch.full((g + kl + 16,), 0xAB, dtype=torch.uint8, device=dev)
+        vbuf = torch.full((g + vl + 16,), 0xAB, dtype=torch.uint8, device=dev)
+        out.key_capacity, out.value_capacity = kl, vl
+        out.key_bytes, out.value_bytes = kbuf.data_ptr() + g, vbuf.data_ptr() + g
+        self.lib.check(self.lib.sink_encode(self.h, C.byref(rows), C.byref(out)), "sink_encode")
+        assert (out.key_len, out.value_len) == (kl, vl)
+        kb, vb = kbuf.cpu().numpy(), vbuf.cpu().numpy()
+        for b, ln in ((kb, kl), (vb, vl)):
+            assert (b[:g] == 0xAB).all() and (b[g + ln:] == 0xAB).all(), "write outside the output bytes"
+        ko, vo, vn = koff.cpu().numpy(), voff.cpu().numpy(), vnull.cpu().numpy()
+        assert ko[0] == 0 and vo[0] == 0 and ko[n] == kl and vo[n] == vl
+        kbs, vbs = kb[g:g + kl].tobytes(), vb[g:g + vl].tobytes()
+        keys = [kbs[ko[i]:ko[i + 1]] for i in range(n)]
+        values = [None if vn[i] else vbs[vo[i]:vo[i + 1]] for i in range(n)]
         return keys, values
 
     def close(self):

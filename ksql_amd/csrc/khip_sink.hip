@@ -5,10 +5,13 @@
 // Streams' windowed key suffix, the value in the value format or a null value for a tombstone —
 // and several GROUP BY columns become the serialized composite key the aggregate groups by.
 //
-// Two passes over the rows, one thread per row: k_sink_measure runs the very encoder the write
-// pass runs, with a counting writer, so a row's length and its bytes can never disagree; the
-// lengths become offsets by a decoupled three-step scan (block sums → one block over the sums →
-// block-local scan plus carry), then k_sink_write writes each record at its offset.  Doubles print
+// Two passes over tiles of 2048 rows, one thread per row and round: k_sink_measure runs the very
+// encoder the write pass runs, with a counting writer, so a row's length and its bytes can never
+// disagree, and sums each tile's lengths; one block scans the tile sums; k_sink_write scans its
+// tile's lengths in the block, adds the tile's carry and writes each record at its offset, and
+// the offsets.  A KAFKA INT32 / BIGINT key has a fixed width (no key lengths; a BIGINT key and its
+// window suffix leave as 8-byte words), and a JSON column's '{' / ',' + escaped name + ':' is built
+// once on the host.  Doubles print
 // through the Schubfach shortest-decimal algorithm (R. Giulietti 2020; java.lang.Double.toString
 // since JDK 19) with the 126-bit powers of ten of tools/gen_dtoa.py, so every digit is computed
 // exactly with 64-bit integer arithmetic.  Byte parity of DOUBLE text therefore assumes the
@@ -26,6 +29,7 @@ namespace khip {
 
 constexpr int SK_MAX = KHIP_SINK_MAX_COLS;
 constexpr int SK_NAME = 64;
+constexpr int SK_PRE = 72;  // a JSON column's text before its value, escaped name included
 constexpr int SK_SCAN_T = 1024;
 constexpr int SK_SCAN_I = 8;  // items per thread per scan block
 
@@ -38,6 +42,11 @@ struct SinkParams {
   int32_t ktype[SK_MAX], vtype[SK_MAX], vsrc[SK_MAX];
   int32_t kname_len[SK_MAX], vname_len[SK_MAX];
   uint8_t kname[SK_MAX][SK_NAME], vname[SK_MAX][SK_NAME];
+  // JSON object columns: '{' (first) or ',', the escaped quoted name and ':' — built once on the
+  // host by the device's own escaper (put_json_str); length -1 when longer than SK_PRE
+  int32_t kpre_len[SK_MAX], vpre_len[SK_MAX];
+  alignas(8) uint8_t kpre[SK_MAX][SK_PRE];
+  alignas(8) uint8_t vpre[SK_MAX][SK_PRE];
 };
 
 // ------------------------------------------------------------------ writers
@@ -50,6 +59,14 @@ struct MemW {
   uint8_t* p;
   __device__ __forceinline__ void put(uint8_t c) { *p++ = c; }
 };
+struct HostW {  // host: a JSON column prefix (SinkParams::kpre / vpre)
+  uint8_t* p;
+  int n, cap;
+  void put(uint8_t c) {
+    if (n < cap) p[n] = c;
+    n++;
+  }
+};
 struct BufW {  // a field's text, for the CSV quoting decision
   uint8_t b[40];
   int n = 0;
@@ -58,17 +75,36 @@ struct BufW {  // a field's text, for the CSV quoting decision
 
 // ------------------------------------------------------------------ numbers
 
+// Long.toString.  The digits collect in a 24-byte shift register (d2:d1:d0, each new digit in at
+// the bottom, so the most significant ends in byte 0): registers, where a digit array indexed by a
+// variable would live in scratch memory.
 template <class W>
-__device__ void put_i64(W& w, int64_t v) {
-  uint8_t buf[20];
-  int n = 0;
+__device__ __forceinline__ void put_i64(W& w, int64_t v) {
   uint64_t u = v < 0 ? 0ULL - (uint64_t)v : (uint64_t)v;
-  do {
-    buf[n++] = (uint8_t)('0' + u % 10);
+  uint64_t d0 = 0, d1 = 0, d2 = 0;
+  int n = 0;
+  auto push = [&](uint64_t dig) {
+    d2 = (d2 << 8) | (d1 >> 56);
+    d1 = (d1 << 8) | (d0 >> 56);
+    d0 = (d0 << 8) | ('0' + dig);
+    n++;
+  };
+  while (u >> 32) {
+    push(u % 10);
     u /= 10;
-  } while (u);
+  }
+  uint32_t x = (uint32_t)u;
+  do {
+    push(x % 10);
+    x /= 10;
+  } while (x);
   if (v < 0) w.put('-');
-  while (n) w.put(buf[--n]);
+  for (; n; n--) {
+    w.put((uint8_t)d0);
+    d0 = (d0 >> 8) | (d1 << 56);
+    d1 = (d1 >> 8) | (d2 << 56);
+    d2 >>= 8;
+  }
 }
 
 __device__ __forceinline__ int flog10pow2(int q) { return (int)(((int64_t)q * 661971961083LL) >> 41); }
@@ -229,7 +265,7 @@ __device__ void put_be(W& w, uint64_t v, int nbytes) {
 
 // Jackson's string escaping: quote, backslash, the short escapes, \u00XX for other control bytes
 template <class W>
-__device__ void put_json_str(W& w, const uint8_t* s, int64_t len) {
+__host__ __device__ void put_json_str(W& w, const uint8_t* s, int64_t len) {
   w.put('"');
   for (int64_t i = 0; i < len; i++) {
     const uint8_t c = s[i];
@@ -331,6 +367,17 @@ __device__ void put_kafka_val(W& w, int type, const Val& v) {
 }
 
 // the inner key (never null: a null GROUP BY value drops the row upstream)
+// A column prefix: 8-byte words from the parameters, put byte by byte from registers.
+template <class W>
+__device__ __forceinline__ void put_pre(W& w, const uint8_t* pre, int len) {
+  for (int j = 0; j < len; j += 8) {
+    const uint64_t x = *(const uint64_t*)(pre + j);
+#pragma unroll
+    for (int b = 0; b < 8; b++)
+      if (j + b < len) w.put((uint8_t)(x >> (8 * b)));
+  }
+}
+
 template <class W, class F>
 __device__ void put_key(W& w, const SinkParams& q, F&& kval) {
   if (q.key_format == KHIP_FMT_KAFKA) {
@@ -339,11 +386,14 @@ __device__ void put_key(W& w, const SinkParams& q, F&& kval) {
     if (q.n_key == 1) {
       put_json_val(w, q.ktype[0], kval(0));
     } else {
-      w.put('{');
       for (int i = 0; i < q.n_key; i++) {
-        if (i) w.put(',');
-        put_json_str(w, q.kname[i], q.kname_len[i]);
-        w.put(':');
+        if (q.kpre_len[i] >= 0) {
+          put_pre(w, q.kpre[i], q.kpre_len[i]);
+        } else {
+          w.put(i ? ',' : '{');
+          put_json_str(w, q.kname[i], q.kname_len[i]);
+          w.put(':');
+        }
         put_json_val(w, q.ktype[i], kval(i));
       }
       w.put('}');
@@ -361,11 +411,15 @@ __device__ void put_value(W& w, const SinkParams& q, F&& vval) {
   if (q.value_format == KHIP_FMT_KAFKA) {
     put_kafka_val(w, q.vtype[0], vval(0));
   } else if (q.value_format == KHIP_FMT_JSON) {
-    w.put('{');
+    if (q.n_val == 0) w.put('{');
     for (int i = 0; i < q.n_val; i++) {
-      if (i) w.put(',');
-      put_json_str(w, q.vname[i], q.vname_len[i]);
-      w.put(':');
+      if (q.vpre_len[i] >= 0) {
+        put_pre(w, q.vpre[i], q.vpre_len[i]);
+      } else {
+        w.put(i ? ',' : '{');
+        put_json_str(w, q.vname[i], q.vname_len[i]);
+        w.put(':');
+      }
       put_json_val(w, q.vtype[i], vval(i));
     }
     w.put('}');
@@ -438,32 +492,150 @@ __device__ __forceinline__ bool value_is_null(const SinkParams& q, const RowsDev
   return q.value_format == KHIP_FMT_KAFKA && row_value_val(q, r, i, 0).null;
 }
 
-__global__ __launch_bounds__(256) void k_sink_measure(const SinkParams* __restrict__ qp, RowsDev r, int64_t n,
-                                                      int64_t* __restrict__ klen, int64_t* __restrict__ vlen) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const SinkParams& q = *qp;
-  CountW kw, vw;
-  encode_key_row(kw, q, r, i);
-  if (!value_is_null(q, r, i)) put_value(vw, q, [&](int c) { return row_value_val(q, r, i, c); });
-  klen[i + 1] = kw.n;  // offsets arrays: lengths at [i + 1], scanned in place
-  vlen[i + 1] = vw.n;
+// Tiles of SK_TILE rows, one block of 256 threads, row u * 256 + thread in round u.  One round:
+// more keep the write pass's row state live across rounds (171 VGPRs for 8, against 96).
+constexpr int SK_TR = 1;
+// k_sink_write at 4 waves per SIMD (<= 128 VGPRs; the spills are in the DOUBLE printer): 782-802
+// us per 22M rows against 840 at 5 and 890 uncapped (138 VGPRs), profiles/r05/ab/sink_two_pass.txt
+#ifndef KHIP_SINK_MINB
+#define KHIP_SINK_MINB 4
+#endif
+#define KHIP_SINK_WRITE_LB __launch_bounds__(256, KHIP_SINK_MINB)
+constexpr int SK_TILE = 256 * SK_TR;
+
+// Sums of (a, b) over the block; every thread gets them.
+__device__ __forceinline__ void sk_block_sum2(int64_t& a, int64_t& b, int64_t (*ws)[4]) {
+  for (int off = 32; off; off >>= 1) {
+    a += __shfl_xor(a, off, 64);
+    b += __shfl_xor(b, off, 64);
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    ws[0][wave] = a;
+    ws[1][wave] = b;
+  }
+  __syncthreads();
+  a = ws[0][0] + ws[0][1] + ws[0][2] + ws[0][3];
+  b = ws[1][0] + ws[1][1] + ws[1][2] + ws[1][3];
+  __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void k_sink_write(const SinkParams* __restrict__ qp, RowsDev r, int64_t n,
-                                                    const int64_t* __restrict__ koff, uint8_t* __restrict__ kb,
-                                                    const int64_t* __restrict__ voff, uint8_t* __restrict__ vb,
-                                                    uint8_t* __restrict__ vnull) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
+// Exclusive scans of (a, b) over the block; the block totals in ta, tb.
+__device__ __forceinline__ void sk_block_scan2(int64_t& a, int64_t& b, int64_t& ta, int64_t& tb, int64_t (*ws)[4]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int64_t ia = a, ib = b;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t ya = __shfl_up(ia, off, 64), yb = __shfl_up(ib, off, 64);
+    if (lane >= off) {
+      ia += ya;
+      ib += yb;
+    }
+  }
+  if (lane == 63) {
+    ws[0][wave] = ia;
+    ws[1][wave] = ib;
+  }
+  __syncthreads();
+  int64_t pa = 0, pb = 0;
+  ta = tb = 0;
+  for (int w = 0; w < 4; w++) {
+    pa += w < wave ? ws[0][w] : 0;
+    pb += w < wave ? ws[1][w] : 0;
+    ta += ws[0][w];
+    tb += ws[1][w];
+  }
+  __syncthreads();
+  a = pa + ia - a;
+  b = pb + ib - b;
+}
+
+// Pass 1: each row's key / value length at klen / vlen[i + 1] (keys skipped when every key is kfix
+// bytes), each tile's sums at tsum[1 + tile] (keys) and tsum[nT + 2 + tile] (values).
+__global__ __launch_bounds__(256) void k_sink_measure(const SinkParams* __restrict__ qp, RowsDev r, int64_t n, int kfix,
+                                                      int64_t nT, int64_t* __restrict__ klen, int64_t* __restrict__ vlen,
+                                                      int64_t* __restrict__ tsum) {
+  __shared__ int64_t ws[2][4];
   const SinkParams& q = *qp;
-  MemW kw{kb + koff[i]};
-  encode_key_row(kw, q, r, i);
-  const bool isnull = value_is_null(q, r, i);
-  vnull[i] = isnull ? 1 : 0;
-  if (!isnull) {
-    MemW vw{vb + voff[i]};
-    put_value(vw, q, [&](int c) { return row_value_val(q, r, i, c); });
+  const int64_t base = (int64_t)blockIdx.x * SK_TILE;
+  int64_t sk = 0, sv = 0;
+#pragma unroll 1
+  for (int u = 0; u < SK_TR; u++) {
+    const int64_t i = base + u * 256 + threadIdx.x;
+    if (i >= n) break;
+    if (!kfix) {
+      CountW kw;
+      encode_key_row(kw, q, r, i);
+      klen[i + 1] = kw.n;
+      sk += kw.n;
+    }
+    CountW vw;
+    if (!value_is_null(q, r, i)) put_value(vw, q, [&](int c) { return row_value_val(q, r, i, c); });
+    vlen[i + 1] = vw.n;
+    sv += vw.n;
+  }
+  sk_block_sum2(sk, sv, ws);
+  if (threadIdx.x == 0) {
+    tsum[1 + blockIdx.x] = sk;
+    tsum[nT + 2 + blockIdx.x] = sv;
+  }
+}
+
+// A fixed-width KAFKA BIGINT key and its window suffix as big-endian 8-byte words (kb + 8-aligned).
+__device__ __forceinline__ void put_key_words(const SinkParams& q, const RowsDev& r, int64_t i, uint64_t* o) {
+  o[0] = __builtin_bswap64((uint64_t)r.key_i64[i]);
+  if (q.window_kind == KHIP_WINDOW_TUMBLING || q.window_kind == KHIP_WINDOW_HOPPING) {
+    o[1] = __builtin_bswap64((uint64_t)r.ws[i]);
+  } else if (q.window_kind == KHIP_WINDOW_SESSION) {
+    o[1] = __builtin_bswap64((uint64_t)r.we[i]);
+    o[2] = __builtin_bswap64((uint64_t)r.ws[i]);
+  }
+}
+
+// Pass 2 (after sk_scan made tsum the tiles' offsets): the tile scans its rows' lengths in the
+// block, adds its carry, writes each row's bytes at its offset and its end offset
+// over its own length slot (koff / voff[i + 1]; only this thread reads that slot, so no other
+// tile's lengths are overwritten before they are read).  kwords: the key as kfix / 8 words.
+__global__ KHIP_SINK_WRITE_LB void k_sink_write(const SinkParams* __restrict__ qp, RowsDev r, int64_t n, int kfix,
+                                                    int kwords, int64_t nT, const int64_t* __restrict__ tsum,
+                                                    int64_t* __restrict__ koff, uint8_t* __restrict__ kb,
+                                                    int64_t* __restrict__ voff, uint8_t* __restrict__ vb,
+                                                    uint8_t* __restrict__ vnull) {
+  __shared__ int64_t ws[2][4];
+  const SinkParams& q = *qp;
+  const int64_t base = (int64_t)blockIdx.x * SK_TILE;
+  int64_t ck = kfix ? base * kfix : tsum[blockIdx.x], cv = tsum[nT + 1 + blockIdx.x];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    koff[0] = 0;
+    voff[0] = 0;
+  }
+#pragma unroll 1
+  for (int u = 0; u < SK_TR; u++) {
+    const int64_t i = base + u * 256 + threadIdx.x;
+    if (base + u * 256 >= n) break;  // uniform over the block
+    const bool in = i < n;
+    const int64_t kl = !in ? 0 : kfix ? kfix : koff[i + 1];
+    const int64_t vl = in ? voff[i + 1] : 0;
+    int64_t ek = kl, ev = vl, tk, tv;
+    sk_block_scan2(ek, ev, tk, tv, ws);
+    if (in) {
+      const int64_t ko = ck + ek, vo = cv + ev;
+      if (kwords) {
+        put_key_words(q, r, i, (uint64_t*)(kb + ko));
+      } else {
+        MemW kw{kb + ko};
+        encode_key_row(kw, q, r, i);
+      }
+      const bool isnull = value_is_null(q, r, i);
+      vnull[i] = isnull ? 1 : 0;
+      if (!isnull) {
+        MemW vw{vb + vo};
+        put_value(vw, q, [&](int c) { return row_value_val(q, r, i, c); });
+      }
+      koff[i + 1] = ko + kl;
+      voff[i + 1] = vo + vl;
+    }
+    ck += tk;
+    cv += tv;
   }
 }
 
@@ -597,7 +769,7 @@ struct khip_sink {
   SinkParams q{};
   int device = 0;
   hipStream_t stream = nullptr;
-  DevBuf dq, bsum, koff, kbytes, kvalid, voff, vbytes, vnull;
+  DevBuf dq, bsum, bsum2, tsum, koff, kbytes, kvalid, voff, vbytes, vnull;
   DevBuf st_key, st_koff, st_kbytes, st_ws, st_we, st_tomb, st_col[SK_MAX], st_null[SK_MAX], st_cv[SK_MAX];
   std::vector<int64_t> h_koff;  // khip_sink_key of a host batch: the keys, in host memory
   std::vector<uint8_t> h_kbytes, h_kvalid;
@@ -617,17 +789,19 @@ khip_status sk_stage(khip_sink* s, DevBuf& b, const void* src, size_t bytes, con
 }
 
 // in place: off[1..n] lengths → off[0..n] offsets; returns the total (synchronises the stream)
-khip_status sk_scan(khip_sink* s, int64_t* off, int64_t n, int64_t* total) {
+// v[1..n] lengths → v[0..n] offsets, in place, on the stream (ws: the block sums); *total ← v[n]
+// (a host copy: complete once the stream is synchronised, here when sync).
+khip_status sk_scan(khip_sink* s, DevBuf& ws, int64_t* off, int64_t n, int64_t* total, bool sync = true) {
   const int64_t per = (int64_t)SK_SCAN_T * SK_SCAN_I;
   const int64_t nb = std::max<int64_t>(1, ceil_div(n, per));
-  KHIP_TRY(s->bsum.ensure((size_t)(nb + 1) * 8));
-  int64_t* bs = s->bsum.as<int64_t>();
+  KHIP_TRY(ws.ensure((size_t)(nb + 1) * 8));
+  int64_t* bs = ws.as<int64_t>();
   hipLaunchKernelGGL(k_sk_scan1, dim3(nb), dim3(SK_SCAN_T), 0, s->stream, off, n, bs);
   hipLaunchKernelGGL(k_sk_scan2, dim3(1), dim3(SK_SCAN_T), 0, s->stream, bs, nb);
   hipLaunchKernelGGL(k_sk_scan3, dim3(nb), dim3(SK_SCAN_T), 0, s->stream, off, n, bs);
   KHIP_TRY_HIP(hipGetLastError());
   KHIP_TRY_HIP(hipMemcpyAsync(total, bs + nb, 8, hipMemcpyDeviceToHost, s->stream));
-  KHIP_TRY_HIP(hipStreamSynchronize(s->stream));
+  if (sync) KHIP_TRY_HIP(hipStreamSynchronize(s->stream));
   return KHIP_OK;
 }
 
@@ -699,6 +873,18 @@ khip_status khip_sink_create(const khip_sink_desc* d, khip_sink** out) {
       return fail(KHIP_E_INVALID, "JSON value column names (<= 64 bytes) required");
     }
   }
+  auto prefix = [](int i, const uint8_t* nm, int len, uint8_t* dst, int32_t* dlen) {
+    HostW w{dst, 0, SK_PRE};
+    w.put(i ? ',' : '{');
+    put_json_str(w, nm, len);
+    w.put(':');
+    *dlen = w.n <= SK_PRE ? w.n : -1;
+  };
+  for (int i = 0; i < SK_MAX; i++) q.kpre_len[i] = q.vpre_len[i] = -1;
+  if (kf == KHIP_FMT_JSON && q.n_key > 1)
+    for (int i = 0; i < q.n_key; i++) prefix(i, q.kname[i], q.kname_len[i], q.kpre[i], &q.kpre_len[i]);
+  if (vf == KHIP_FMT_JSON)
+    for (int i = 0; i < q.n_val; i++) prefix(i, q.vname[i], q.vname_len[i], q.vpre[i], &q.vpre_len[i]);
   s->device = d->device;
   DeviceGuard g(s->device);
   if (hipStreamCreateWithFlags(&s->stream, hipStreamDefault) != hipSuccess) {
@@ -759,7 +945,7 @@ khip_status khip_sink_key(khip_sink* s, const khip_batch* in, const khip_key_col
     hipLaunchKernelGGL(k_key_measure, dim3(ceil_div(n, 256)), dim3(256), 0, s->stream, s->dq.as<SinkParams>(), k, n, koff,
                        s->kvalid.as<uint8_t>());
     KHIP_TRY_HIP(hipGetLastError());
-    KHIP_TRY(sk_scan(s, koff, n, &total));
+    KHIP_TRY(sk_scan(s, s->bsum, koff, n, &total));
     KHIP_TRY(s->kbytes.ensure((size_t)std::max<int64_t>(total, 8)));
     hipLaunchKernelGGL(k_key_write, dim3(ceil_div(n, 256)), dim3(256), 0, s->stream, s->dq.as<SinkParams>(), k, n, koff,
                        s->kbytes.as<uint8_t>());
@@ -872,12 +1058,23 @@ khip_status khip_sink_encode(khip_sink* s, const khip_sink_rows* rows, khip_sink
     voff = s->voff.as<int64_t>();
   }
   int64_t ktot = 0, vtot = 0;
+  const int64_t nT = ceil_div(n, SK_TILE);
+  // every key the same width: a KAFKA INT32 / BIGINT key and its window suffix
+  int kfix = 0;
+  if (!rows->key_serialized && q.key_format == KHIP_FMT_KAFKA && q.ktype[0] != KHIP_TYPE_STRING)
+    kfix = (q.ktype[0] == KHIP_TYPE_INT64 ? 8 : 4) +
+           (q.window_kind == KHIP_WINDOW_SESSION ? 16 : q.window_kind != KHIP_WINDOW_NONE ? 8 : 0);
   if (n) {
-    hipLaunchKernelGGL(k_sink_measure, dim3(ceil_div(n, 256)), dim3(256), 0, s->stream, s->dq.as<SinkParams>(), r, n, koff,
-                       voff);
+    KHIP_TRY(s->tsum.ensure((size_t)(2 * (nT + 1)) * 8));
+    int64_t* ts = s->tsum.as<int64_t>();
+    hipLaunchKernelGGL(k_sink_measure, dim3((unsigned)nT), dim3(256), 0, s->stream, s->dq.as<SinkParams>(), r, n, kfix, nT,
+                       koff, voff, ts);
     KHIP_TRY_HIP(hipGetLastError());
-    KHIP_TRY(sk_scan(s, koff, n, &ktot));
-    KHIP_TRY(sk_scan(s, voff, n, &vtot));
+    int64_t tk = 0, tv = 0;
+    if (!kfix) KHIP_TRY(sk_scan(s, s->bsum, ts, nT, &tk, false));
+    KHIP_TRY(sk_scan(s, s->bsum2, ts + nT + 1, nT, &tv, true));
+    ktot = kfix ? (int64_t)kfix * n : tk;
+    vtot = tv;
   } else {
     const int64_t z = 0;
     if (dev_out) {
@@ -901,8 +1098,9 @@ khip_status khip_sink_encode(khip_sink* s, const khip_sink_rows* rows, khip_sink
     vn = s->vnull.as<uint8_t>();
   }
   if (n) {
-    hipLaunchKernelGGL(k_sink_write, dim3(ceil_div(n, 256)), dim3(256), 0, s->stream, s->dq.as<SinkParams>(), r, n, koff,
-                       kb, voff, vb, vn);
+    const int kwords = kfix && q.ktype[0] == KHIP_TYPE_INT64 && ((uintptr_t)kb & 7) == 0 ? kfix / 8 : 0;
+    hipLaunchKernelGGL(k_sink_write, dim3((unsigned)nT), dim3(256), 0, s->stream, s->dq.as<SinkParams>(), r, n, kfix,
+                       kwords, nT, s->tsum.as<int64_t>(), koff, kb, voff, vb, vn);
     KHIP_TRY_HIP(hipGetLastError());
   }
   if (!dev_out) {
@@ -928,7 +1126,7 @@ khip_status khip_sink_destroy(khip_sink* s) {
   if (!s) return KHIP_OK;
   DeviceGuard g(s->device);
   if (s->stream) hipStreamSynchronize(s->stream);
-  DevBuf* bufs[] = {&s->dq, &s->bsum, &s->koff, &s->kbytes, &s->kvalid, &s->voff, &s->vbytes, &s->vnull, &s->st_key,
+  DevBuf* bufs[] = {&s->dq, &s->bsum, &s->bsum2, &s->tsum, &s->koff, &s->kbytes, &s->kvalid, &s->voff, &s->vbytes, &s->vnull, &s->st_key,
                     &s->st_koff, &s->st_kbytes, &s->st_ws, &s->st_we, &s->st_tomb};
   for (DevBuf* b : bufs) b->release();
   for (int c = 0; c < SK_MAX; c++) {

@@ -50,7 +50,8 @@ def _special_doubles(rng, n):
 
 
 @pytest.mark.parametrize("vfmt", ["JSON", "DELIMITED"])
-def test_doubles_and_longs(prod, vfmt):
+@pytest.mark.parametrize("dev_out", [False, True])
+def test_doubles_and_longs(prod, vfmt, dev_out):
     rng = np.random.default_rng(11)
     d = _special_doubles(rng, 4000)
     n = len(d)
@@ -59,7 +60,7 @@ def test_doubles_and_longs(prod, vfmt):
     dn = rng.random(n) < 0.05
     s = abi.SinkHandle(prod, "KAFKA", [("K", "INT64")], vfmt, [("D", "DOUBLE", 0), ("L", "INT64", 1)])
     keys, vals = s.encode(_rows(n, keys=np.arange(n, dtype=np.int64), values=[d, ints],
-                                nulls=[dn, np.zeros(n, bool)]))
+                                nulls=[dn, np.zeros(n, bool)]), device_out=dev_out, align=5)
     bad = []
     for i in range(n):
         exp = sink_ref.encode_value(vfmt, [("D", "DOUBLE"), ("L", "INT64")], [None if dn[i] else float(d[i]), int(ints[i])])
@@ -76,7 +77,8 @@ WINDOWS = ["NONE", "TUMBLING", "SESSION"]
 @pytest.mark.parametrize("window", WINDOWS)
 @pytest.mark.parametrize("kfmt,ktype", [("KAFKA", "INT64"), ("KAFKA", "INT32"), ("KAFKA", "STRING"),
                                         ("JSON", "INT64"), ("JSON", "STRING"), ("DELIMITED", "STRING")])
-def test_keys_windows_tombstones(prod, window, kfmt, ktype):
+@pytest.mark.parametrize("dev_out", [False, True])
+def test_keys_windows_tombstones(prod, window, kfmt, ktype, dev_out):
     rng = np.random.default_rng(hash((window, kfmt, ktype)) % 1000)
     n = 3000
     if ktype == "STRING":
@@ -93,7 +95,8 @@ def test_keys_windows_tombstones(prod, window, kfmt, ktype):
     for vfmt in ("JSON", "DELIMITED", "KAFKA"):
         vc = vcols[:1] if vfmt == "KAFKA" else vcols
         s = abi.SinkHandle(prod, kfmt, [("K", ktype)], vfmt, vc, window_kind=window)
-        kb, vb = s.encode(_rows(n, keys=keys, ws=ws, we=we, values=[cnt], nulls=[np.zeros(n, bool)]), tombstone=tomb)
+        kb, vb = s.encode(_rows(n, keys=keys, ws=ws, we=we, values=[cnt], nulls=[np.zeros(n, bool)]), tombstone=tomb,
+                          device_out=dev_out, align=len(vfmt) % 16)
         for i in range(n):
             kv = keys[i] if ktype == "STRING" else int(keys[i])
             exp_k = sink_ref.encode_key(kfmt, [("K", ktype)], [kv]) + sink_ref.window_suffix(window, int(ws[i]), int(we[i]))
@@ -102,6 +105,71 @@ def test_keys_windows_tombstones(prod, window, kfmt, ktype):
                                           [int(cnt[i]), int(ws[i]), int(we[i])][:len(vc)], tombstone=bool(tomb[i]))
             assert vb[i] == exp_v, (i, vb[i], exp_v)
         s.close()
+
+
+@pytest.mark.parametrize("n", [1, 255, 256, 257, 70_000])
+def test_device_outputs_long_rows(prod, n):
+    """Device outputs (offsets, bytes and nulls written in place) against host outputs and the CPU
+    restatement: keys of 0..300 bytes, JSON values of five columns (most NULL in some rows),
+    tombstones (empty values), several tiles of rows, every output alignment, guard bytes either
+    side of the outputs untouched."""
+    rng = np.random.default_rng(n)
+    lens = rng.integers(0, 300, n)
+    short = rng.random(n) < 0.5
+    lens[short] = rng.integers(0, 60, int(short.sum()))
+    keys = ["".join(chr(97 + (i + j) % 26) for j in range(int(lens[i]))) for i in range(n)]
+    names = ["C%d_" % c + "X" * int(rng.integers(1, 12)) for c in range(5)]
+    vc = [(nm, "INT64" if c % 2 else "DOUBLE", c) for c, nm in enumerate(names)]
+    cols = [rng.uniform(-1e9, 1e9, n) if c % 2 == 0 else rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64)
+            for c in range(5)]
+    few = rng.random(n) < 0.3  # short values: most columns NULL
+    nulls = [few & (c > 0) for c in range(5)]
+    tomb = (rng.random(n) < 0.1).astype(np.uint8)
+    ws = rng.integers(0, 2**40, n, dtype=np.int64)
+    s = abi.SinkHandle(prod, "KAFKA", [("K", "STRING")], "JSON", vc, window_kind="TUMBLING")
+    snap = _rows(n, keys=keys, ws=ws, we=ws + 1000, values=cols, nulls=nulls)
+    host = s.encode(snap, tombstone=tomb)
+    for align in (0, 7, 13) if n < 1000 else (3,):
+        assert s.encode(snap, tombstone=tomb, device_out=True, align=align) == host
+    for i in range(0, n, max(1, n // 300)):
+        exp_k = sink_ref.encode_key("KAFKA", [("K", "STRING")], [keys[i]]) + sink_ref.window_suffix(
+            "TUMBLING", int(ws[i]), int(ws[i]) + 1000)
+        assert host[0][i] == exp_k
+        exp_v = sink_ref.encode_value("JSON", [(c[0], c[1]) for c in vc],
+                                      [None if nulls[c][i] else (float(cols[c][i]) if c % 2 == 0 else int(cols[c][i]))
+                                       for c in range(5)], tombstone=bool(tomb[i]))
+        assert host[1][i] == exp_v, (i, host[1][i], exp_v)
+    if n >= 255:
+        assert any(len(k) > 52 for k in host[0]) and any(len(k) <= 52 for k in host[0])
+        assert any(v and len(v) > 116 for v in host[1]) and any(v and len(v) <= 116 for v in host[1])
+    s.close()
+
+
+@pytest.mark.parametrize("dev_out", [False, True])
+def test_json_column_names_escaped(prod, dev_out):
+    """JSON object columns print '{' / ',' + the escaped name + ':' from text built once on the
+    host by the device escaper; a name whose escaped text passes 72 bytes (64 control characters:
+    384) is escaped per row instead.  Both against sink_ref, for value and composite-key objects."""
+    names = ['a"b', "back\\slash", "ctl\x01x\x1f", "tab\there", "é", "\x02" * 64, "K" * 64, "Z"]
+    n = 700
+    rng = np.random.default_rng(9)
+    cols = [rng.integers(-10**6, 10**6, n, dtype=np.int64) for _ in names]
+    vc = [(nm, "INT64", c) for c, nm in enumerate(names)]
+    kc = [(nm, "INT64") for nm in names[:4]] + [(names[5], "INT32")]
+    s = abi.SinkHandle(prod, "KAFKA", [("K", "INT64")], "JSON", vc)
+    kb, vb = s.encode(_rows(n, values=cols, nulls=[np.zeros(n, bool)] * len(names)), device_out=dev_out, align=1)
+    for i in range(n):
+        exp = sink_ref.encode_value("JSON", [(c[0], c[1]) for c in vc], [int(cols[c][i]) for c in range(len(names))])
+        assert vb[i] == exp, (i, vb[i], exp)
+    s.close()
+    s = abi.SinkHandle(prod, "JSON", kc, "JSON", [])  # composite keys: khip_sink_key
+    hb = abi.HostBatch(np.arange(n, dtype=np.int64), keys=np.zeros(n, np.int64))
+    kcols = [cols[0], cols[1], cols[2], cols[3], cols[4].astype(np.int32)]
+    got = s.key_bytes(s.key(hb, kcols))
+    for i in range(n):
+        exp = sink_ref.encode_key("JSON", kc, [int(kcols[c][i]) for c in range(len(kc))])
+        assert got[i] == exp, (i, got[i], exp)
+    s.close()
 
 
 def test_value_null_kafka_and_empty(prod):
