@@ -30,6 +30,17 @@ namespace khip {
 constexpr int SK_MAX = KHIP_SINK_MAX_COLS;
 constexpr int SK_NAME = 64;
 constexpr int SK_PRE = 72;  // a JSON column's text before its value, escaped name included
+// The write pass's outputs leave as nontemporal stores: k_sink_write 717 / 719 us per 22M rows
+// against 750 / 751 (profiles/r05/ab/sink_two_pass.txt).
+#ifndef KHIP_SINK_NT
+#define KHIP_SINK_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ void sk_st(T* p, T v) {
+  if (KHIP_SINK_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 constexpr int SK_SCAN_T = 1024;
 constexpr int SK_SCAN_I = 8;  // items per thread per scan block
 
@@ -258,6 +269,21 @@ struct Val {
   bool null;
 };
 
+// f(byte) over s[0..len), the bytes loaded eight at a time: on gfx950 a load issued behind a store
+// waits for the store (one vmcnt counts both), so a byte-by-byte copy would wait a memory round
+// trip per byte.
+template <class F>
+__host__ __device__ __forceinline__ void for_bytes(const uint8_t* s, int64_t len, F&& f) {
+  for (int64_t j = 0; j < len; j += 8) {
+    uint64_t x = 0;
+#pragma unroll
+    for (int b = 0; b < 8; b++)
+      if (j + b < len) x |= (uint64_t)s[j + b] << (8 * b);
+    const int m = len - j < 8 ? (int)(len - j) : 8;
+    for (int b = 0; b < m; b++) f((uint8_t)(x >> (8 * b)));
+  }
+}
+
 template <class W>
 __device__ void put_be(W& w, uint64_t v, int nbytes) {
   for (int b = nbytes - 1; b >= 0; b--) w.put((uint8_t)(v >> (8 * b)));
@@ -267,8 +293,7 @@ __device__ void put_be(W& w, uint64_t v, int nbytes) {
 template <class W>
 __host__ __device__ void put_json_str(W& w, const uint8_t* s, int64_t len) {
   w.put('"');
-  for (int64_t i = 0; i < len; i++) {
-    const uint8_t c = s[i];
+  for_bytes(s, len, [&](uint8_t c) {
     if (c == '"' || c == '\\') {
       w.put('\\');
       w.put(c);
@@ -290,7 +315,7 @@ __host__ __device__ void put_json_str(W& w, const uint8_t* s, int64_t len) {
     } else {
       w.put(c);
     }
-  }
+  });
   w.put('"');
 }
 
@@ -337,10 +362,10 @@ __device__ void put_csv_text(W& w, const uint8_t* s, int64_t len, bool first, ui
     }
   }
   if (quote) w.put('"');
-  for (int64_t i = 0; i < len; i++) {
-    if (quote && s[i] == '"') w.put('"');
-    w.put(s[i]);
-  }
+  for_bytes(s, len, [&](uint8_t c) {
+    if (quote && c == '"') w.put('"');
+    w.put(c);
+  });
   if (quote) w.put('"');
 }
 
@@ -362,7 +387,7 @@ template <class W>
 __device__ void put_kafka_val(W& w, int type, const Val& v) {
   if (type == KHIP_TYPE_INT32) put_be(w, (uint64_t)(uint32_t)v.i, 4);
   else if (type == KHIP_TYPE_STRING)
-    for (int64_t i = 0; i < v.len; i++) w.put(v.s[i]);
+    for_bytes(v.s, v.len, [&](uint8_t c) { w.put(c); });
   else put_be(w, (uint64_t)v.i, 8);
 }
 
@@ -407,7 +432,7 @@ __device__ void put_key(W& w, const SinkParams& q, F&& kval) {
 }
 
 template <class W, class F>
-__device__ void put_value(W& w, const SinkParams& q, F&& vval) {
+__device__ __forceinline__ void put_value(W& w, const SinkParams& q, F&& vval) {
   if (q.value_format == KHIP_FMT_KAFKA) {
     put_kafka_val(w, q.vtype[0], vval(0));
   } else if (q.value_format == KHIP_FMT_JSON) {
@@ -471,18 +496,32 @@ __device__ __forceinline__ Val row_value_val(const SinkParams& q, const RowsDev&
   return v;
 }
 
+// The row's window bounds, loaded before any of its bytes are stored.
+struct RowWin {
+  int64_t ws, we;
+};
+__device__ __forceinline__ RowWin row_win(const SinkParams& q, const RowsDev& r, int64_t i) {
+  RowWin x{0, 0};
+  if (q.window_kind != KHIP_WINDOW_NONE) x.ws = r.ws[i];
+  if (q.window_kind == KHIP_WINDOW_SESSION) x.we = r.we[i];
+  return x;
+}
+
 template <class W>
-__device__ void encode_key_row(W& w, const SinkParams& q, const RowsDev& r, int64_t i) {
+__device__ __forceinline__ void encode_key_row(W& w, const SinkParams& q, const RowsDev& r, int64_t i) {
+  const RowWin win = row_win(q, r, i);
   if (r.key_serialized) {
-    for (int64_t b = r.key_off[i]; b < r.key_off[i + 1]; b++) w.put(r.key_bytes[b]);
+    const int64_t b0 = r.key_off[i], b1 = r.key_off[i + 1];
+    for_bytes(r.key_bytes + b0, b1 - b0, [&](uint8_t c) { w.put(c); });
   } else {
-    put_key(w, q, [&](int) { return row_key_val(q, r, i); });
+    const Val kv = row_key_val(q, r, i);
+    put_key(w, q, [&](int) { return kv; });
   }
   if (q.window_kind == KHIP_WINDOW_TUMBLING || q.window_kind == KHIP_WINDOW_HOPPING) {
-    put_be(w, (uint64_t)r.ws[i], 8);
+    put_be(w, (uint64_t)win.ws, 8);
   } else if (q.window_kind == KHIP_WINDOW_SESSION) {
-    put_be(w, (uint64_t)r.we[i], 8);
-    put_be(w, (uint64_t)r.ws[i], 8);
+    put_be(w, (uint64_t)win.we, 8);
+    put_be(w, (uint64_t)win.ws, 8);
   }
 }
 
@@ -492,8 +531,8 @@ __device__ __forceinline__ bool value_is_null(const SinkParams& q, const RowsDev
   return q.value_format == KHIP_FMT_KAFKA && row_value_val(q, r, i, 0).null;
 }
 
-// Tiles of SK_TILE rows, one block of 256 threads, row u * 256 + thread in round u.  One round:
-// more keep the write pass's row state live across rounds (171 VGPRs for 8, against 96).
+// Tiles of SK_TILE rows, one block of 256 threads, a row per thread (eight rows per thread, in
+// rounds, kept the write pass's row state live across rounds: 171 VGPRs).
 constexpr int SK_TR = 1;
 // k_sink_write at 4 waves per SIMD (<= 128 VGPRs; the spills are in the DOUBLE printer): 782-802
 // us per 22M rows against 840 at 5 and 890 uncapped (138 VGPRs), profiles/r05/ab/sink_two_pass.txt
@@ -580,62 +619,135 @@ __global__ __launch_bounds__(256) void k_sink_measure(const SinkParams* __restri
   }
 }
 
-// A fixed-width KAFKA BIGINT key and its window suffix as big-endian 8-byte words (kb + 8-aligned).
+// A fixed-width KAFKA BIGINT key and its window suffix as big-endian 8-byte words (kb + 8-aligned),
+// every load before the first store.
 __device__ __forceinline__ void put_key_words(const SinkParams& q, const RowsDev& r, int64_t i, uint64_t* o) {
-  o[0] = __builtin_bswap64((uint64_t)r.key_i64[i]);
+  const RowWin win = row_win(q, r, i);
+  const uint64_t k = __builtin_bswap64((uint64_t)r.key_i64[i]);
   if (q.window_kind == KHIP_WINDOW_TUMBLING || q.window_kind == KHIP_WINDOW_HOPPING) {
-    o[1] = __builtin_bswap64((uint64_t)r.ws[i]);
+    if (((uintptr_t)o & 15) == 0) {
+      if (KHIP_SINK_NT) {
+        __builtin_nontemporal_store(k, o);
+        __builtin_nontemporal_store(__builtin_bswap64((uint64_t)win.ws), o + 1);
+      } else {
+        *(ulonglong2*)o = make_ulonglong2(k, __builtin_bswap64((uint64_t)win.ws));
+      }
+    } else {
+      o[0] = k;
+      o[1] = __builtin_bswap64((uint64_t)win.ws);
+    }
   } else if (q.window_kind == KHIP_WINDOW_SESSION) {
-    o[1] = __builtin_bswap64((uint64_t)r.we[i]);
-    o[2] = __builtin_bswap64((uint64_t)r.ws[i]);
+    o[0] = k;
+    o[1] = __builtin_bswap64((uint64_t)win.we);
+    o[2] = __builtin_bswap64((uint64_t)win.ws);
+  } else {
+    o[0] = k;
   }
 }
 
+// A wave's value bytes, staged contiguously in LDS (lds[0..L)), to dst[0..L): 16-byte aligned
+// chunks, one per lane and round — whole 16-byte stores inside, bytes at the two edge chunks
+// (shared with the neighbouring waves).  lds has 16 readable bytes past L.
+__device__ __forceinline__ void sk_wave_copy(const uint8_t* lds, int L, uint8_t* __restrict__ dst) {
+  const int lane = threadIdx.x & 63;
+  const int A = (int)((uintptr_t)dst & 15);
+  const int nch = (A + L + 15) >> 4;
+  const uint32_t* l32 = (const uint32_t*)lds;
+  for (int c = lane; c < nch; c += 64) {
+    const int o = 16 * c - A;
+    uint8_t* g = dst + o;
+    if (o >= 0 && o + 16 <= L) {
+      const int ao = o >> 2, sh = o & 3;
+      const uint32_t w0 = l32[ao], w1 = l32[ao + 1], w2 = l32[ao + 2], w3 = l32[ao + 3], w4 = l32[ao + 4];
+      uint4 v;
+      v.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
+      v.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+      v.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
+      v.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
+      if (KHIP_SINK_NT) {
+        __builtin_nontemporal_store(v.x, (uint32_t*)g);
+        __builtin_nontemporal_store(v.y, (uint32_t*)g + 1);
+        __builtin_nontemporal_store(v.z, (uint32_t*)g + 2);
+        __builtin_nontemporal_store(v.w, (uint32_t*)g + 3);
+      } else {
+        *(uint4*)g = v;
+      }
+    } else {
+      for (int b = 0; b < 16; b++)
+        if (o + b >= 0 && o + b < L) g[b] = lds[o + b];
+    }
+  }
+}
+
+constexpr int SK_WBUF = 2048;  // staged value bytes per wave: 64 rows of 32
+
+
 // Pass 2 (after sk_scan made tsum the tiles' offsets): the tile scans its rows' lengths in the
-// block, adds its carry, writes each row's bytes at its offset and its end offset
-// over its own length slot (koff / voff[i + 1]; only this thread reads that slot, so no other
-// tile's lengths are overwritten before they are read).  kwords: the key as kfix / 8 words.
+// block and adds its carry.  A wave whose 64 values take at most SK_WBUF bytes (one contiguous
+// range of the output) encodes them into LDS at their places in that range and copies the range
+// out in 16-byte stores (sk_wave_copy); a longer wave writes each value at its offset byte by byte.
+// Every load of a row comes before its first global store (on gfx950 a load behind a store waits
+// for the store).  Each row's end offsets go over its own length slots (koff / voff[i + 1]: only
+// this thread reads them, so no other tile's lengths are overwritten before they are read).
+// kwords: the key as kfix / 8 words.
 __global__ KHIP_SINK_WRITE_LB void k_sink_write(const SinkParams* __restrict__ qp, RowsDev r, int64_t n, int kfix,
                                                     int kwords, int64_t nT, const int64_t* __restrict__ tsum,
                                                     int64_t* __restrict__ koff, uint8_t* __restrict__ kb,
                                                     int64_t* __restrict__ voff, uint8_t* __restrict__ vb,
                                                     uint8_t* __restrict__ vnull) {
   __shared__ int64_t ws[2][4];
+  __shared__ uint32_t vst[4][SK_WBUF / 4 + 4];
   const SinkParams& q = *qp;
-  const int64_t base = (int64_t)blockIdx.x * SK_TILE;
-  int64_t ck = kfix ? base * kfix : tsum[blockIdx.x], cv = tsum[nT + 1 + blockIdx.x];
+  const int wave = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * SK_TILE + threadIdx.x;
+  const bool in = i < n;
+  const int64_t kl = !in ? 0 : kfix ? kfix : koff[i + 1];
+  const int64_t vl = in ? voff[i + 1] : 0;
+  int64_t ko = kl, vo = vl, tk, tv;
+  sk_block_scan2(ko, vo, tk, tv, ws);
+  ko += kfix ? (int64_t)blockIdx.x * SK_TILE * kfix : tsum[blockIdx.x];
+  vo += tsum[nT + 1 + blockIdx.x];
+  const int64_t wbase = __shfl(vo, 0, 64), wlen = __shfl(vo + vl, 63, 64) - wbase;  // past-n lanes: vl 0
+  const bool staged = wlen <= SK_WBUF;
+  uint8_t* vls = (uint8_t*)vst[wave];
+  bool isnull = true;
+  Val v0{0, nullptr, 0, true}, v1 = v0, v2 = v0, v3 = v0;  // the first four value columns
+  if (in) {
+    isnull = value_is_null(q, r, i);
+    if (!isnull) {
+      if (q.n_val > 0) v0 = row_value_val(q, r, i, 0);
+      if (q.n_val > 1) v1 = row_value_val(q, r, i, 1);
+      if (q.n_val > 2) v2 = row_value_val(q, r, i, 2);
+      if (q.n_val > 3) v3 = row_value_val(q, r, i, 3);
+    }
+  }
+  auto vget = [&](int c) {
+    return c == 0 ? v0 : c == 1 ? v1 : c == 2 ? v2 : c == 3 ? v3 : row_value_val(q, r, i, c);
+  };
+  if (in && staged && !isnull) {
+    MemW vw{vls + (vo - wbase)};
+    put_value(vw, q, vget);
+  }
+  __syncthreads();
+  if (staged && wlen > 0) sk_wave_copy(vls, (int)wlen, vb + wbase);
+  if (in) {
+    if (kwords) {
+      put_key_words(q, r, i, (uint64_t*)(kb + ko));
+    } else {
+      MemW kw{kb + ko};
+      encode_key_row(kw, q, r, i);
+    }
+    sk_st(vnull + i, (uint8_t)(isnull ? 1 : 0));
+    if (!staged && !isnull) {
+      MemW vw{vb + vo};
+      put_value(vw, q, vget);
+    }
+    sk_st(koff + i + 1, ko + kl);
+    sk_st(voff + i + 1, vo + vl);
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     koff[0] = 0;
     voff[0] = 0;
-  }
-#pragma unroll 1
-  for (int u = 0; u < SK_TR; u++) {
-    const int64_t i = base + u * 256 + threadIdx.x;
-    if (base + u * 256 >= n) break;  // uniform over the block
-    const bool in = i < n;
-    const int64_t kl = !in ? 0 : kfix ? kfix : koff[i + 1];
-    const int64_t vl = in ? voff[i + 1] : 0;
-    int64_t ek = kl, ev = vl, tk, tv;
-    sk_block_scan2(ek, ev, tk, tv, ws);
-    if (in) {
-      const int64_t ko = ck + ek, vo = cv + ev;
-      if (kwords) {
-        put_key_words(q, r, i, (uint64_t*)(kb + ko));
-      } else {
-        MemW kw{kb + ko};
-        encode_key_row(kw, q, r, i);
-      }
-      const bool isnull = value_is_null(q, r, i);
-      vnull[i] = isnull ? 1 : 0;
-      if (!isnull) {
-        MemW vw{vb + vo};
-        put_value(vw, q, [&](int c) { return row_value_val(q, r, i, c); });
-      }
-      koff[i + 1] = ko + kl;
-      voff[i + 1] = vo + vl;
-    }
-    ck += tk;
-    cv += tv;
   }
 }
 
