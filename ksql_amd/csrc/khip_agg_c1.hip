@@ -794,9 +794,9 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
   KLDS uint32_t* rt = (KLDS uint32_t*)((KLDS char*)smem + (size_t)(H + 64) * sizeof(ID));
   KLDS uint32_t* ct = rt + (H + 64);
   KLDS uint16_t* list = (KLDS uint16_t*)(ct + (H + 64));
-  KLDS uint32_t* spre = (KLDS uint32_t*)((KLDS char*)list + (((size_t)H * 2 + 15) & ~(size_t)15));
-  KLDS int32_t* sbs = (KLDS int32_t*)((KLDS char*)spre + (size_t)(C1_SEGMAX + 4) * 4);
-  KLDS int64_t* lbb = (KLDS int64_t*)(sbs + C1_SEGMAX);  // [B + 1] bucket bases
+  // segment k: prefix of the lengths | (base - prefix) << 32, so a lookup reads k and k + 1 at once
+  KLDS uint64_t* sg2 = (KLDS uint64_t*)((KLDS char*)list + (((size_t)H * 2 + 15) & ~(size_t)15));
+  KLDS int64_t* lbb = (KLDS int64_t*)(sg2 + C1_SEGMAX + 4);  // [B + 1] bucket bases
   KLDS int32_t* lcs = (KLDS int32_t*)(lbb + (1 << (q.log2P - q.fbits)) + 1);  // [B + 1] chunk starts
   KLDS uint16_t* segof = (KLDS uint16_t*)(lcs + (1 << (q.log2P - q.fbits)) + 2);  // [C1_SEGOF] block → segment
   __shared__ int lovf, nnew;
@@ -931,23 +931,17 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     // records on average: 32-record blocks make the lookup a read and at most a step or two)
     const int segb = tot <= (C1_SEGOF << 5) ? 5 : (tot <= (C1_SEGOF << 6) ? 6 : C1_SEGB);
     const int bm = (1 << segb) - 1;
-    if (k0 < nseg) {
-      spre[k0] = (uint32_t)ex;
-      sbs[k0] = (int32_t)(base0 - ex);
-    }
-    if (k0 + 1 < nseg) {
-      spre[k0 + 1] = (uint32_t)(ex + len0);
-      sbs[k0 + 1] = (int32_t)(base1 - (ex + len0));
-    }
+    if (k0 < nseg) sg2[k0] = (uint32_t)ex | (uint64_t)(uint32_t)(int32_t)(base0 - ex) << 32;
+    if (k0 + 1 < nseg) sg2[k0 + 1] = (uint32_t)(ex + len0) | (uint64_t)(uint32_t)(int32_t)(base1 - (ex + len0)) << 32;
     // segment lookup: block j (records [j << segb, (j + 1) << segb)) starts in segment segof[j]
     for (int bj = (ex + bm) >> segb, be = (ex + len0 + bm) >> segb; bj < be && bj < C1_SEGOF; bj++)
       segof[bj] = (uint16_t)k0;
     for (int bj = (ex + len0 + bm) >> segb, be = (ex + s + bm) >> segb; bj < be && bj < C1_SEGOF; bj++)
       segof[bj] = (uint16_t)(k0 + 1);
-    if (k0 < nseg && k0 + 2 >= nseg) spre[nseg] = (uint32_t)(ex + s);  // the total
-    if (nseg == 0 && threadIdx.x == 0) spre[0] = 0u;
+    if (k0 < nseg && k0 + 2 >= nseg) sg2[nseg] = (uint32_t)(ex + s);  // the total
+    if (nseg == 0 && threadIdx.x == 0) sg2[0] = 0u;
     lds_barrier();
-    it.rn = spre[nseg];
+    it.rn = (uint32_t)sg2[nseg];
     it.segb = segb;
   };
   uint64_t ra[AU], rb[AU];
@@ -960,18 +954,25 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
       li = li < rn ? li : rn - 1;
       int lo = 0;  // the last segment starting at or before li
+      int64_t at;
       if (rn <= ((int64_t)C1_SEGOF << segb)) {  // from the block's segment, a step or two on
         lo = segof[li >> segb];
-        while (lo + 1 < nseg && (int64_t)spre[lo + 1] <= li) lo++;
+        uint64_t sa = sg2[lo], sb = sg2[lo + 1];  // one ds_read2_b64
+        while (lo + 1 < nseg && (int64_t)(uint32_t)sb <= li) {
+          lo++;
+          sa = sb;
+          sb = sg2[lo + 1];
+        }
+        at = (int64_t)(int32_t)(sa >> 32) + li;
       } else {
         int hi = nseg;
         while (hi - lo > 1) {
           const int mid = (lo + hi) >> 1;
-          if ((int64_t)spre[mid] <= li) lo = mid;
+          if ((int64_t)(uint32_t)sg2[mid] <= li) lo = mid;
           else hi = mid;
         }
+        at = (int64_t)(int32_t)(sg2[lo] >> 32) + li;
       }
-      const int64_t at = (int64_t)sbs[lo] + li;
       x[u] = __builtin_nontemporal_load(srec + at);
       if constexpr (WIDE) tx[u] = __builtin_nontemporal_load(srecT + at);
     }
@@ -1796,11 +1797,10 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
   KLDS ID* ids = (KLDS ID*)(KLDS char*)smem;
   KLDS uint32_t* rt = c1v_plane<uint32_t>(smem, q.off_rt);
   KLDS uint16_t* list = c1v_plane<uint16_t>(smem, q.off_list);
-  KLDS uint32_t* spre = c1v_plane<uint32_t>(smem, q.off_spre);
-  KLDS int32_t* sbs = (KLDS int32_t*)(spre + (C1_SEGMAX + 4));
+  KLDS uint64_t* sg2 = c1v_plane<uint64_t>(smem, q.off_spre);  // as k_c1_merge's
+  KLDS uint16_t* segof = (KLDS uint16_t*)(sg2 + C1_SEGMAX + 4);
   // the bucket tables (chunk starts, bucket bases) are read from memory per item (their 3 KB of
   // LDS let a 2^12-entry table of 32-bit identities fit two workgroups per CU)
-  KLDS uint16_t* segof = (KLDS uint16_t*)(sbs + C1_SEGMAX);
   __shared__ int lovf, nnew;
   __shared__ int wsum[NW];
   __shared__ unsigned long long lbase;
@@ -1947,22 +1947,20 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
     const int segb = tot <= (C1_SEGOF << 5) ? 5 : (tot <= (C1_SEGOF << 6) ? 6 : C1_SEGB);
     const int bm = (1 << segb) - 1;
     if (k0 < nseg) {
-      spre[k0] = (uint32_t)ex;
-      sbs[k0] = (int32_t)(base0 - ex);
+      sg2[k0] = (uint32_t)ex | (uint64_t)(uint32_t)(int32_t)(base0 - ex) << 32;
     }
     if (k0 + 1 < nseg) {
-      spre[k0 + 1] = (uint32_t)(ex + len0);
-      sbs[k0 + 1] = (int32_t)(base1 - (ex + len0));
+      sg2[k0 + 1] = (uint32_t)(ex + len0) | (uint64_t)(uint32_t)(int32_t)(base1 - (ex + len0)) << 32;
     }
     // segment lookup: block j (records [j << segb, (j + 1) << segb)) starts in segment segof[j]
     for (int bj = (ex + bm) >> segb, be = (ex + len0 + bm) >> segb; bj < be && bj < C1_SEGOF; bj++)
       segof[bj] = (uint16_t)k0;
     for (int bj = (ex + len0 + bm) >> segb, be = (ex + s + bm) >> segb; bj < be && bj < C1_SEGOF; bj++)
       segof[bj] = (uint16_t)(k0 + 1);
-    if (k0 < nseg && k0 + 2 >= nseg) spre[nseg] = (uint32_t)(ex + s);
-    if (nseg == 0 && threadIdx.x == 0) spre[0] = 0u;
+    if (k0 < nseg && k0 + 2 >= nseg) sg2[nseg] = (uint32_t)(ex + s);
+    if (nseg == 0 && threadIdx.x == 0) sg2[0] = 0u;
     lds_barrier();
-    it.rn = spre[nseg];
+    it.rn = (uint32_t)sg2[nseg];
     it.segb = segb;
   };
   ulonglong2 ra[AU], rb[AU];
@@ -1972,18 +1970,26 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
       li = li < rn ? li : rn - 1;
       int lo = 0;  // the last segment starting at or before li
+      int64_t at;
       if (rn <= ((int64_t)C1_SEGOF << segb)) {  // from the block's segment, a step or two on
         lo = segof[li >> segb];
-        while (lo + 1 < nseg && (int64_t)spre[lo + 1] <= li) lo++;
+        uint64_t sa = sg2[lo], sb = sg2[lo + 1];
+        while (lo + 1 < nseg && (int64_t)(uint32_t)sb <= li) {
+          lo++;
+          sa = sb;
+          sb = sg2[lo + 1];
+        }
+        at = (int64_t)(int32_t)(sa >> 32) + li;
       } else {
         int hi = nseg;
         while (hi - lo > 1) {
           const int mid = (lo + hi) >> 1;
-          if ((int64_t)spre[mid] <= li) lo = mid;
+          if ((int64_t)(uint32_t)sg2[mid] <= li) lo = mid;
           else hi = mid;
         }
+        at = (int64_t)(int32_t)(sg2[lo] >> 32) + li;
       }
-      x[u] = ld_nt2(srec + ((int64_t)sbs[lo] + li));
+      x[u] = ld_nt2(srec + at);
     }
   };
   auto load01 = [&](const It& x) {
@@ -2345,8 +2351,8 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
 
 size_t c1_merge_lds(int log2H, int idw, int log2B) {
   const size_t H = (size_t)1 << log2H, B = (size_t)1 << log2B;
-  return (H + 64) * (idw + 8) + ((H * 2 + 15) & ~(size_t)15) + (C1_SEGMAX + 4) * 4 + C1_SEGMAX * 4 + (B + 1) * 12 + 8 +
-         C1_SEGOF * 2;
+  return (H + 64) * (idw + 8) + ((H * 2 + 15) & ~(size_t)15) + (C1_SEGMAX + 4) * 8 + (B + 1) * 12 + 8 +
+         C1_SEGOF * 2;  // (segment table: 8 B per entry, both layouts fit)
 }
 
 // Whether the COUNT(*) pipeline may take this push (the general path's c1 plan, TUMBLING, the
@@ -2427,7 +2433,7 @@ static size_t c1v_layout(khip_agg* a, int log2H, int idw, int log2B, C1VQ* q) {
   q->off_list = (int32_t)off;
   off += (H * 2 + 15) & ~(size_t)15;
   q->off_spre = (int32_t)off;
-  off += (C1_SEGMAX + 4) * 4 + C1_SEGMAX * 4 + C1_SEGOF * 2;
+  off += (C1_SEGMAX + 4) * 8 + C1_SEGOF * 2;
   (void)B;
   return off;
 }
