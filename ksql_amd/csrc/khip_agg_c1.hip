@@ -92,15 +92,14 @@ __device__ __forceinline__ int64_t ci_ld(const int64_t* ci, int k) {
 // The scatters write no bucket-contiguous output (that needs every tile's bucket counts first: a
 // histogram pass over the keys): each step of S records leaves as ONE contiguous run of S records
 // in bucket order at out[gs * S], and its per-bucket count / offset go to rcnt[b][gs] / roff[b][gs]
-// (bucket-major).  The exclusive scan of rcnt gives each (bucket, step) run's place in the bucket's
+// (bucket-major; held in LDS for the tile's steps and written per bucket at its end).  The exclusive scan of rcnt gives each (bucket, step) run's place in the bucket's
 // order (rpos); the refine reads a bucket's chunk from its step runs.  The key range, the time base
 // and the bucket counts are all learned in the one read of the input.
 template <int U, int NT, class R, bool W>
 __device__ __forceinline__ uint32_t stage_step_runs(const R (&rec)[U], const uint32_t (&t32)[U], const uint32_t (&bin)[U],
                                                 const bool (&ok)[U], int nb, uint32_t* cnt, uint32_t* sbase, int* wsum,
                                                 R* sp, uint32_t* lt32, R* __restrict__ out, uint32_t* __restrict__ outT,
-                                                int64_t gs, int64_t nSt, uint32_t* __restrict__ rcnt,
-                                                uint16_t* __restrict__ roff) {
+                                                int64_t gs, uint32_t* lrc, uint16_t* lro) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   uint32_t rank[U];
 #pragma unroll
@@ -122,8 +121,8 @@ __device__ __forceinline__ uint32_t stage_step_runs(const R (&rec)[U], const uin
   }
   if (t < nb) {
     sbase[t] = before + incl - c;
-    rcnt[(int64_t)t * nSt + gs] = c;
-    roff[(int64_t)t * nSt + gs] = (uint16_t)(before + incl - c);
+    lrc[t] = c;  // the step's row of the tile's run counts / offsets (flush_run_counts)
+    lro[t] = (uint16_t)(before + incl - c);
     cnt[t] = 0u;
   }
   lds_barrier();
@@ -174,6 +173,41 @@ __device__ __forceinline__ void step_krange(const R* sp, uint32_t tot, uint32_t 
 // their ts words when W).
 __host__ __device__ constexpr size_t run_stage_lds(int nb, int S, int rec_bytes, bool w) {
   return (size_t)nb * 8 + (size_t)S * rec_bytes + (w ? (size_t)S * 4 : 0);
+}
+// ... then the tile's run counts u32[spt][nb] and offsets u16[spt][nb], written out per bucket at
+// the end of the tile
+__host__ __device__ constexpr size_t run_cnt_lds(int nb, int spt) { return (size_t)nb * spt * 6; }
+
+// The tile's SPT run counts / offsets of bucket b leave as whole 16-byte stores (rcnt[b][t * SPT ..],
+// roff[b][t * SPT ..]: 64 + 32 B for SPT = 16) instead of a 4-byte and a 2-byte store per step and
+// bucket, which the memory side turned into 32-byte partial writes (C2: ~250 MB a push).  Steps
+// past the input (the last tile's) are empty runs.  Thread b wrote row entries lrc[st][b] itself.
+template <int SPT, int NT>
+__device__ __forceinline__ void flush_run_counts(const uint32_t* lrc, const uint16_t* lro, int B, int st_last, int64_t t,
+                                                 int64_t nSt, uint32_t* __restrict__ rcnt, uint16_t* __restrict__ roff) {
+  static_assert(SPT % 8 == 0, "whole 16-byte stores");
+  for (int b = threadIdx.x; b < B; b += NT) {
+    uint32_t* rc = rcnt + (int64_t)b * nSt + t * SPT;
+    uint16_t* ro = roff + (int64_t)b * nSt + t * SPT;
+#pragma unroll
+    for (int q = 0; q < SPT / 4; q++) {
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) v[k] = 4 * q + k <= st_last ? lrc[(4 * q + k) * B + b] : 0u;
+      *(uint4*)(rc + 4 * q) = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+#pragma unroll
+    for (int q = 0; q < SPT / 8; q++) {
+      uint32_t w[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int s0 = 8 * q + 2 * k;
+        const uint32_t lo = s0 <= st_last ? lro[s0 * B + b] : 0u, hi = s0 + 1 <= st_last ? lro[(s0 + 1) * B + b] : 0u;
+        w[k] = lo | hi << 16;
+      }
+      *(uint4*)(ro + 8 * q) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
 }
 
 // The time base, the key base and the tile's key range — shared by both scatters.  T0: the stream
@@ -231,6 +265,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   uint32_t* sbase = cnt + B;
   int64_t* sp = (int64_t*)(smem + (size_t)B * 8);
   uint32_t* lt32 = (uint32_t*)(sp + S);  // WIDE: the staged ts - T0
+  uint32_t* lrc = (uint32_t*)(smem + run_stage_lds(B, S, 8, WIDE));
+  uint16_t* lro = (uint16_t*)(lrc + SPT * B);
   for (int b = threadIdx.x; b < B; b += NT) cnt[b] = 0u;
   if (threadIdx.x < 4) lc[threadIdx.x] = 0;
   if (threadIdx.x < 2) {
@@ -331,7 +367,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     // the next step's loads go into x / k (dead now) and stay in flight through this step's stage
     if (s0 + S < end) load_step(i0 + S, x, k);
     const uint32_t tot = stage_step_runs<U, NT, int64_t, WIDE>(rec, t32, bin, ok, B, cnt, sbase, wsum, sp, lt32,
-                                                               (int64_t*)srec, srecT, t * SPT + st, nSt, rcnt, roff);
+                                                               (int64_t*)srec, srecT, t * SPT + st, lrc + st * B,
+                                                               lro + st * B);
     if (!WIDE) step_krange<NT, int64_t>(sp, tot, 0xFFFFFFFFu, lkr);
     // the step's ts range: the wave's first (one LDS atomic per wave, not 64 to one address),
     // after the stage so that its registers are free; published by thread 0 one step later
@@ -347,9 +384,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
     if (threadIdx.x == 0 && st > 0) publish(s0 - S, st - 1);
   }
-  // the last tile's steps past the input: empty runs
-  for (int st = st_last + 1; st < SPT; st++)
-    for (int b = threadIdx.x; b < B; b += NT) rcnt[(int64_t)b * nSt + t * SPT + st] = 0u;
+  flush_run_counts<SPT, NT>(lrc, lro, B, st_last, t, nSt, rcnt, roff);
   if (!WIDE && kor) lkfail = 1;
   __syncthreads();
   if (threadIdx.x == 0 && s0 > base) publish(s0 - S, st_last);
@@ -1363,6 +1398,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   uint32_t* cnt = (uint32_t*)smem;
   uint32_t* sbase = cnt + B;
   ulonglong2* sp = (ulonglong2*)(smem + (size_t)B * 8);  // B >= 32: 16-byte aligned
+  uint32_t* lrc = (uint32_t*)(smem + run_stage_lds(B, S, 16, false));
+  uint16_t* lro = (uint16_t*)(lrc + SPT * B);
   for (int b = threadIdx.x; b < B; b += NT) cnt[b] = 0u;
   if (threadIdx.x < 5) lc[threadIdx.x] = 0;
   if (threadIdx.x < 2) {
@@ -1480,7 +1517,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (s0 + S < end) load_step(i0 + S);
     uint32_t t32u[U];  // (no ts words: 16-byte records carry the ts)
     const uint32_t tot = stage_step_runs<U, NT, ulonglong2, false>(rec, t32u, bin, ok, B, cnt, sbase, wsum, sp, nullptr,
-                                                                   srec, nullptr, t * SPT + st, nSt, rcnt, roff);
+                                                                   srec, nullptr, t * SPT + st, lrc + st * B,
+                                                                   lro + st * B);
     step_krange<NT, ulonglong2>(sp, tot, 0x7FFFFFFFu, lkr);
     for (int off = 32; off > 0; off >>= 1) {
       const int a = __shfl_xor(tmx, off, 64), b = __shfl_xor(tmn, off, 64);
@@ -1493,8 +1531,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
     if (threadIdx.x == 0 && st > 0) publish(s0 - S, st - 1);
   }
-  for (int st = st_last + 1; st < SPT; st++)  // the last tile's steps past the input: empty runs
-    for (int b = threadIdx.x; b < B; b += NT) rcnt[(int64_t)b * nSt + t * SPT + st] = 0u;
+  flush_run_counts<SPT, NT>(lrc, lro, B, st_last, t, nSt, rcnt, roff);
   if (kor) lkfail = 1;
   __syncthreads();
   if (threadIdx.x == 0 && s0 > base) publish(s0 - S, st_last);
@@ -2526,7 +2563,7 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     const RowsIn ri = rows ? *rows : RowsIn{};
     auto sk = rows ? (st_at ? k_c1v_scatter<UV, C1_NT, true, true> : k_c1v_scatter<UV, C1_NT, false, true>)
                    : (st_at ? k_c1v_scatter<UV, C1_NT, true, false> : k_c1v_scatter<UV, C1_NT, false, false>);
-    const size_t lds = run_stage_lds(B, UV * C1_NT, 16, false);
+    const size_t lds = run_stage_lds(B, UV * C1_NT, 16, false) + run_cnt_lds(B, C1_TILE / (UV * C1_NT));
     if (lds > 64 * 1024) hipFuncSetAttribute((const void*)sk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(sk, dim3(nT), dim3(C1_NT), lds, a->stream, keys, ts, kv, rv, vc, ri, n, nT, log2B, rc, ro, nSt,
                        (ulonglong2*)s.srecA.p, s.tilemax.as<int64_t>(), s.tpart.as<int64_t>(), ci, st_at,
@@ -2537,7 +2574,7 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     constexpr int U = 8;
     auto sk = wide ? (st_at ? k_c1_scatter<U, C1_NT, true, true> : k_c1_scatter<U, C1_NT, true, false>)
                    : (st_at ? k_c1_scatter<U, C1_NT, false, true> : k_c1_scatter<U, C1_NT, false, false>);
-    const size_t lds = run_stage_lds(B, U * C1_NT, 8, wide);
+    const size_t lds = run_stage_lds(B, U * C1_NT, 8, wide) + run_cnt_lds(B, C1_TILE / (U * C1_NT));
     if (lds > 64 * 1024) hipFuncSetAttribute((const void*)sk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(sk, dim3(nT), dim3(C1_NT), lds, a->stream, keys, ts, kv, rv, n, nT, log2B, rc, ro, nSt,
                        s.srecA.as<uint64_t>(), s.tilemax.as<int64_t>(), s.tpart.as<int64_t>(), ci, st_at, srecAT,
