@@ -46,6 +46,13 @@ namespace khip {
 constexpr int C1_TILE = 65536;   // records per hist / scatter tile (the general path's tile)
 constexpr int C1_NT = 512;       // workgroup size of every kernel here
 constexpr int C1_CH = 8192;      // refine chunk (records), 16 per thread
+// Record loads of the refines and merges: plain loads.  Nontemporal ones (rounds 3-5) re-fetched
+// the lines two neighbouring runs or segments share and cost C2 1.94 -> 1.88 ms / step, C5's
+// value refine 921 -> 839 us (profiles/r05/ab/record_loads_temporal.txt).
+template <class T>
+__device__ __forceinline__ T c1_ld(const T* p) {
+  return *p;
+}
 constexpr int C1_SEGMAX = 512;   // chunks of one bucket the merge can hold (4M records)
 constexpr int C1_SEGB = 7;       // the merge's segment lookup: one entry per 32, 64 or 128 records of an
 constexpr int C1_SEGOF = 512;    // item (the finest that fits 512 entries; past 64K records: binary search)
@@ -681,8 +688,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   for (int u = 0; u < U; u++) {
     const int j = threadIdx.x + u * NT;
     const uint32_t src = ((const uint32_t*)stage)[j < len ? j : len - 1];
-    r[u] = __builtin_nontemporal_load(srcA + src) - kshift;
-    if constexpr (WIDE) t32[u] = __builtin_nontemporal_load(srcAT + src);
+    r[u] = c1_ld(srcA + src) - kshift;
+    if constexpr (WIDE) t32[u] = c1_ld(srcAT + src);
   }
 #pragma unroll
   for (int u = 0; u < U; u++) {
@@ -1008,8 +1015,8 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
         }
         at = (int64_t)(int32_t)(sg2[lo] >> 32) + li;
       }
-      x[u] = __builtin_nontemporal_load(srec + at);
-      if constexpr (WIDE) tx[u] = __builtin_nontemporal_load(srecT + at);
+      x[u] = c1_ld(srec + at);
+      if constexpr (WIDE) tx[u] = c1_ld(srecT + at);
     }
   };
   // the item's first two chunks (register sets A and B): a chunk is always two chunks ahead of
@@ -1363,8 +1370,8 @@ constexpr int C1V_CH = 4096;  // refine chunk of 16-byte records (64 KB of LDS s
 constexpr int C1V_MAXW = 8;   // row words (key, ws, rowtime + at most 5 state words)
 
 typedef uint64_t c1v_u2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ ulonglong2 ld_nt2(const ulonglong2* p) {  // streaming 16-byte load
-  const c1v_u2 v = __builtin_nontemporal_load((const c1v_u2*)p);
+__device__ __forceinline__ ulonglong2 ld_nt2(const ulonglong2* p) {  // 16-byte load (c1_ld)
+  const c1v_u2 v = c1_ld((const c1v_u2*)p);
   return make_ulonglong2(v.x, v.y);
 }
 
