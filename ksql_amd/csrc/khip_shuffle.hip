@@ -28,9 +28,6 @@
 namespace khip {
 
 
-#ifndef KHIP_PACK1_LTS
-#define KHIP_PACK1_LTS 0
-#endif
 constexpr int SH_THREADS = 256;
 constexpr int SH_ITEMS = 16;
 constexpr int64_t SH_TILE = (int64_t)SH_THREADS * SH_ITEMS;
@@ -222,9 +219,7 @@ __global__ __launch_bounds__(SH_THREADS) void k_shuf_pack1(ShCols c, int key_col
   __shared__ uint32_t wcnt[SH_ITEMS][W];
   __shared__ int64_t lbase;
   __shared__ uint32_t ltile;
-#if KHIP_PACK1_LTS
   __shared__ int64_t lts[SH_ITEMS][SH_THREADS];  // the tile's ts, read once (the second pass missed L2)
-#endif
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t lt = lane ? (~0ULL >> (64 - lane)) : 0ULL;
   if (threadIdx.x == 0) ltile = atomicAdd(ticket, 1u);
@@ -235,13 +230,9 @@ __global__ __launch_bounds__(SH_THREADS) void k_shuf_pack1(ShCols c, int key_col
 #pragma unroll
   for (int r = 0; r < SH_ITEMS; r++) {
     const int64_t i = base + (int64_t)r * SH_THREADS + threadIdx.x;
-#if KHIP_PACK1_LTS
     const int64_t tv = i < n ? ts[i] : -1;
     lts[r][threadIdx.x] = tv;
     const bool v = i < n && tv >= 0 && bit_get(rv, i) && bit_get(c.valid[key_col], i);
-#else
-    const bool v = i < n && ts[i] >= 0 && bit_get(rv, i) && bit_get(c.valid[key_col], i);
-#endif
     const uint64_t m = __ballot(v);
     if (lane == 0) wcnt[r][wave] = (uint32_t)__popcll(m);
     vmask |= (v ? 1u : 0u) << r;
@@ -279,11 +270,7 @@ __global__ __launch_bounds__(SH_THREADS) void k_shuf_pack1(ShCols c, int key_col
     if (!v) continue;
     const int64_t i = base + (int64_t)r * SH_THREADS + threadIdx.x;
     ShRow<NC, ST> row;
-#if KHIP_PACK1_LTS
     sh_build_t<NC, ST>(c, key_col, lts[r][threadIdx.x], i, row);
-#else
-    sh_build<NC, ST>(c, key_col, ts, i, row);
-#endif
     sh_store<NC, ST>(out + (uint64_t)(lbase + wcnt[r][wave] + rank) * ShRow<NC, ST>::W, row);
   }
 }
