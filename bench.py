@@ -243,6 +243,45 @@ def push_phases(kt, launches):
     return {k: kt[k] / launches for k in ("stream_time_ms", "dict_ms", "partition_ms", "apply_ms", "finalize_ms")}
 
 
+# The library's phase events (khip_agg_kernel_times) bracket, on the COUNT(*) pipeline
+# (ksql_amd/csrc/khip_agg_c1.hip, ev_record_part 0..3):
+#   stream_time_ms  k_c1_scatter + the run scan + k_c1_bases   key 8 + ts 8 read, one record written
+#   partition_ms    k_c1_check + k_c1_chunks + k_c1_refine     one record read, one record written
+#   apply_ms        k_c1_merge (+ retries) + k_part_commit     one record read + the rows written
+#   dict_ms         UTF-8 keys: k_key_inline (offsets 8 + key bytes 16 read, id 8 written; a lower
+#                   bound on the dictionary path, whose slot reads are random)
+# and on the general partitioned engine (khip_agg_part.hip): k_part_hist + scans (key + ts read),
+# scatter + refine (key + ts read, a record written, read and written again), merge.
+# A record is 8 bytes (12 when the key range does not fit 32 bits: --sparse-keys).  These are the
+# bytes the phases move, so their sum is the pipeline's bytes per record — not SURVEY §8(d)'s
+# hash-update model (80 B/record), which the sort-based engine does not perform.
+def c2_phase_bytes(c1, wide, utf8, groups, n):
+    rows = 32.0 * groups / n  # every group's 32-byte row written once (the table is reset each step)
+    rec = 12 if wide else 8
+    if c1:
+        own = {"stream_time_ms": 16 + rec, "partition_ms": rec + rec, "apply_ms": rec + rows}
+    else:
+        own = {"stream_time_ms": 16, "partition_ms": 16 + rec + rec + rec, "apply_ms": rec + rows}
+    own["dict_ms"] = 32 if utf8 else 0
+    own["finalize_ms"] = 0
+    return own
+
+
+def value_phase_bytes(rows_in):
+    """The value-record pipeline's phases (k_c1v_scatter | k_c1v_refine | k_c1v_merge), per record:
+    the scatter reads key + ts + the argument + its validity bit (or one received 32-byte row,
+    `khip_agg_push_shuffled`) and writes a 16-byte record; the refine reads and writes it; the merge
+    reads it — plus the resident rows' read-modify-write, not counted here (a lower bound)."""
+    return {"stream_time_ms": (32 if rows_in else 24.125) + 16, "partition_ms": 32, "apply_ms": 16,
+            "dict_ms": 0, "finalize_ms": 0}
+
+
+def per_phase_block(phase, own, n):
+    """Per-phase device time and rate over the bytes the phase moves (c2_phase_bytes)."""
+    return {k: {"ms": phase[k], "bytes_per_record": own[k],
+                "GB/s": own[k] * n / (phase[k] / 1000.0) / 1e9} for k in phase if phase[k] > 0 and own.get(k)}
+
+
 def stream_copy_gbs(nbytes=1 << 31):
     """Achievable HBM rate on this box: one device-to-device copy (read + write bytes / time)."""
     import torch
@@ -694,24 +733,27 @@ def bench_possible_fraud(args, lib, rank, world, local):
     push_ms = sum(phase.values())
     bpr = BYTES_PER_RECORD_C2_UTF8 if args.utf8 else BYTES_PER_RECORD_C2
     c1 = kt.get("c1_pushes", 0) > 0
-    if c1:  # the COUNT(*) pipeline: step-run scatter + refine of 8-byte (12 wide) records
-        wide = args.sparse_keys
-        own = {"stream_time_ms": 8, "dict_ms": 32, "partition_ms": (16 + 12 + 12 + 12) if wide else (16 + 8 + 8 + 8),
-               "apply_ms": (12 if wide else 8) + 32.0 * groups / n, "finalize_ms": 0}
-    else:
-        own = {"stream_time_ms": 16, "dict_ms": 32, "partition_ms": 32, "apply_ms": 16 + 32.0 * groups / n,
-               "finalize_ms": 0}
-    per_kernel = {k: {"ms": phase[k], "bytes_per_record": own[k],
-                      "GB/s": own[k] * n / (phase[k] / 1000.0) / 1e9} for k in phase if phase[k] > 0}
+    own = c2_phase_bytes(c1, args.sparse_keys, args.utf8, groups, n)
+    per_kernel = per_phase_block(phase, own, n)
     variant = ("_utf8" + ("_card_format_alnum" if args.card_format == "alnum" else "") if args.utf8 else
                ("_sparse_keys" if args.sparse_keys else ""))  # profile_leg.sh's leg names
     traffic = load_traffic(args.traffic_json, "possible_fraud" + ("_atomic" if args.engine == "atomic" else ""), n,
                            variant)
+    # beside SURVEY's model: the I/O floor (the input read once, every group's row written once)
+    floor = (16 + 16 + 8 if args.utf8 else 16) + 32.0 * groups / n
+    pipe = sum(own.values())
     roof = roofline(bpr * n, ms_step, push_ms, per_kernel, traffic, bpr,
                     kernel=("khip_agg_push (COUNT(*) pipeline: k_c1_scatter (step runs) + run scan + k_c1_check + "
                             "k_c1_chunks + k_c1_refine + k_c1_merge + commit) + HAVING count") if c1 else
                            "khip_agg_push (k_part_hist + scans + k_part_scatter + k_part_refine + k_part_merge + "
-                           "commit) + HAVING count")
+                           "commit) + HAVING count",
+                    extra={"floor_bytes_per_record": floor,
+                           "floor_basis": "input once (key + ts%s) + each group's 32-B row written once" %
+                                          (" + key bytes + offsets" if args.utf8 else ""),
+                           "floor_frac": floor * n / (ms_step / 1000.0) / 1e9 / HBM_PEAK_GBS,
+                           "pipeline_bytes_per_record": pipe,
+                           "pipeline_basis": "sum of the per-phase bytes (push.per_kernel): what the passes move",
+                           "pipeline_frac": pipe * n / (ms_step / 1000.0) / 1e9 / HBM_PEAK_GBS})
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_agg(
@@ -911,7 +953,9 @@ def bench_hopping_double(args, lib, rank, world, local):
                            "streamed_frac": moved * n / (ms_step / 1000.0) / 1e9 / HBM_PEAK_GBS,
                            "survey_algorithmic_bytes_per_record": BYTES_PER_RECORD_C3,
                            "survey_equivalent_frac": BYTES_PER_RECORD_C3 * n / (ms_step / 1000.0) / 1e9 / HBM_PEAK_GBS,
-                           "phase_ms_per_step": phase, "stream_copy_GBps": stream_copy_gbs()})
+                           "phase_ms_per_step": phase,
+                           "per_kernel": per_phase_block(phase, value_phase_bytes(False), n),
+                           "stream_copy_GBps": stream_copy_gbs()})
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_agg(lambda m: synth.hopping_double(0, m, n), False,
@@ -1138,10 +1182,12 @@ def bench_repartition(args, lib, rank, world, local):
         return
     ms_step = elapsed * 1000.0 / args.steps
     per = {k: v * 1000.0 / args.steps for k, v in phases.items()}
-    push_ms = sum(push_phases(kt, kt["apply_launches"]).values())
+    pph = push_phases(kt, kt["apply_launches"])
+    push_ms = sum(pph.values())
     roof = roofline(BYTES_PER_RECORD_C5 * n, ms_step, None, None, load_traffic(args.traffic_json, "repartition_sum", n),
                     BYTES_PER_RECORD_C5, kernel="whole step: pack + all-to-all + khip_agg_push_shuffled (or unpack + khip_agg_push) + row count",
-                    extra={"phase_ms": per, "push_device_ms": push_ms})
+                    extra={"phase_ms": per, "push_device_ms": push_ms,
+                           "push_per_kernel": per_phase_block(pph, value_phase_bytes(not args.unpack), m)})
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_repartition(n, args.cpu_seconds)

@@ -94,3 +94,68 @@ def test_bench_uses_only_measured_traffic_entries():
     assert bench.load_traffic(f.name, "y", 10) == 7.0
     assert bench.load_traffic(f.name, "y", 11) is None
     os.unlink(f.name)
+
+
+# ---- the bench line's per-phase figures: bytes a phase really moves, never above peak -----------
+# partition_ms was credited with 40 B/record (scatter + refine) while its events
+# bracket check + chunks + refine only, so the line showed 10 TB/s against an 8 TB/s peak.
+
+def _check_per_kernel(per_kernel, n, pipeline=None):
+    tot = 0.0
+    for k, v in per_kernel.items():
+        gbs = v["bytes_per_record"] * n / (v["ms"] / 1000.0) / 1e9
+        assert abs(gbs - v["GB/s"]) <= 1e-6 * gbs, (k, gbs, v)
+        assert v["GB/s"] <= bench.HBM_PEAK_GBS, (k, v)
+        tot += v["bytes_per_record"]
+    if pipeline is not None:
+        assert abs(tot - pipeline) < 1e-9, (tot, pipeline)
+
+
+def test_c2_phase_bytes_replayed_on_the_r05_line():
+    """Replay the committed round-5 default line's phase times through today's byte map."""
+    import json
+    path = os.path.join(os.path.dirname(bench.__file__), "profiles", "r05", "final2", "bench.jsonl")
+    d = json.loads(open(path).readline())
+    n, groups = d["config"]["records_per_gpu"], d["config"]["groups_per_gpu"]
+    phase = {k: v["ms"] for k, v in d["roofline"]["push"]["per_kernel"].items()}
+    for wide in (False, True):
+        own = bench.c2_phase_bytes(True, wide, False, groups, n)
+        pk = bench.per_phase_block(phase, own, n)
+        assert set(pk) == set(phase)
+        _check_per_kernel(pk, n, sum(own.values()))
+    own = bench.c2_phase_bytes(True, False, False, groups, n)
+    assert own["stream_time_ms"] == 24 and own["partition_ms"] == 16  # scatter 16 in + 8 out; refine 8 + 8
+    assert abs(own["apply_ms"] - (8 + 32.0 * groups / n)) < 1e-12
+
+
+def test_value_phase_bytes():
+    own = bench.value_phase_bytes(False)
+    assert own["stream_time_ms"] == 40.125 and own["partition_ms"] == 32 and own["apply_ms"] == 16
+    assert bench.value_phase_bytes(True)["stream_time_ms"] == 48
+
+
+def test_committed_r06_lines_per_phase_below_peak():
+    """Every bench line committed this round under profiles/r06/: per-phase GB/s at or below peak,
+    and on the C2 line the phases' bytes sum to pipeline_bytes_per_record."""
+    import glob
+    import json
+    root = os.path.join(os.path.dirname(bench.__file__), "profiles", "r06")
+    seen = 0
+    for path in glob.glob(os.path.join(root, "**", "*.jsonl"), recursive=True):
+        for ln in open(path):
+            if not ln.startswith("{"):
+                continue
+            d = json.loads(ln)
+            roof = d.get("roofline") or {}
+            n = (d.get("config") or {}).get("records_per_gpu")
+            if not n:
+                continue
+            pk = (roof.get("push") or {}).get("per_kernel")
+            if pk:
+                _check_per_kernel(pk, n, roof.get("pipeline_bytes_per_record"))
+                seen += 1
+            if roof.get("per_kernel"):  # C3: per step of n records
+                _check_per_kernel(roof["per_kernel"], n)
+                seen += 1
+    if seen == 0:
+        pytest.skip("no round-6 bench lines committed yet")
