@@ -552,6 +552,13 @@ khip_status khip_shuffle_unpack(khip_shuffle* s, const uint64_t* rows, int64_t n
 khip_status khip_shuffle_unpack_stream_time(khip_shuffle* s, const uint64_t* rows, int64_t n,
                                             int64_t* stream_time);
 
+/* ABI 8.  KHIP_SHUFFLE_STREAM_TIME: the packs that follow write max(seed, stream_time[i]) as a
+ * row's stream-time word (the default seed, -1, leaves the column as it is).  A rank scans its
+ * arrival chunk ONCE, unseeded (khip_stream_time_scan with seed -1), learns the chunk maxima of
+ * the ranks before it, and hands their max here: a seeded prefix max is the unseeded one raised
+ * to the seed, so the column needs no second scan. */
+khip_status khip_shuffle_stream_time_seed(khip_shuffle* s, int64_t seed);
+
 /* ABI 6.  Received rows straight into the aggregation that reads the repartition topic (the
  * non-key GROUP BY's aggregate, S/StreamGroupByBuilderBase.java:101-103 → StreamAggregateBuilder),
  * without materialising them as columns first: the same effect and statistics as khip_agg_push of

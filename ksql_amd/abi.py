@@ -212,6 +212,7 @@ PRODUCT_ONLY = {
     "shuffle_unpack": ([_P, _P, i64, _P, _P, C.POINTER(_P), C.POINTER(_P)]),
     "shuffle_pack_v": ([_P, C.POINTER(Batch), _P, i64, C.POINTER(i64), C.POINTER(i64)]),
     "shuffle_unpack_stream_time": ([_P, _P, i64, _P]),
+    "shuffle_stream_time_seed": ([_P, i64]),
     "agg_push_shuffled": ([_P, _P, _P, i64, C.POINTER(BatchStats)]),
     "shuffle_sync": ([_P]),
     "shuffle_destroy": ([_P]),
@@ -790,6 +791,10 @@ class ShuffleHandle:
         self.lib.check(self.lib.shuffle_pack_v(self.h, C.byref(batch.struct), send.data_ptr(), send.shape[0],
                                                counts, offs), "shuffle_pack_v")
         return send, list(counts), list(offs)
+
+    def stream_time_seed(self, seed):
+        """khip_shuffle_stream_time_seed (ABI 8): the next packs write max(seed, stream_time[i])."""
+        self.lib.check(self.lib.shuffle_stream_time_seed(self.h, int(seed)), "shuffle_stream_time_seed")
 
     def unpack_stream_time(self, rows, n):
         """The stream_time column of KHIP_SHUFFLE_STREAM_TIME rows (device int64 tensor)."""

@@ -1711,7 +1711,16 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
     ev_record(a, 2);
   }
   // per-task retention / EMIT FINAL: every accepted key's partition (the tasks share one table)
-  if (pdomain && a->windowed) KHIP_TRY(pmap_insert(a, keys, kv, rv, ts, part, n));
+  // A batch that puts a key on a second partition is rejected before it changes the handle's
+  // stream times: the partitions' stream times go back to their values before the batch (the
+  // batch's new keys stay recorded with the partitions it named, as its dictionary entries stay).
+  if (pdomain && a->windowed) {
+    const khip_status ps = pmap_insert(a, keys, kv, rv, ts, part, n);
+    if (ps != KHIP_OK) {
+      std::swap(a->pst, a->pst2);
+      return ps;
+    }
+  }
   int64_t tot[NPART] = {0};
   if (a->engine == 2) {
     if (n >= (1LL << 31)) return fail(KHIP_E_UNSUPPORTED, "SESSION pushes above 2^31 rows");

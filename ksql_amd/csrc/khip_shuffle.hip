@@ -40,7 +40,13 @@ struct ShCols {
   const uint8_t* valid[SH_MAX_COLS];
   int32_t type[SH_MAX_COLS];
   const int64_t* st;  // KHIP_SHUFFLE_STREAM_TIME: the batch's stream_time column (else null)
+  int64_t st_seed;    // the word written is max(st_seed, st[i]) (khip_shuffle_stream_time_seed)
 };
+
+__device__ __forceinline__ uint64_t sh_st(const ShCols& c, int64_t i) {
+  const int64_t v = c.st[i];
+  return (uint64_t)(v > c.st_seed ? v : c.st_seed);
+}
 
 // Kafka's default partitioner over the KAFKA-format key (big-endian 4 / 8 bytes,
 // ksqldb-serde/.../kafka/KafkaSerdeFactory.java:42-43): toPositive(murmur2(bytes)) % n_parts,
@@ -139,7 +145,7 @@ __global__ __launch_bounds__(SH_THREADS) void k_shuf_pack(ShCols c, int n_cols, 
         o[w++] = cv ? (uint64_t)sh_raw(c, cc, i) : 0ULL;
         vm |= (cv ? 1ULL : 0ULL) << cc;
       }
-      if (c.st) o[w++] = (uint64_t)c.st[i];
+      if (c.st) o[w++] = sh_st(c, i);
       o[w] = vm;
     }
     __syncthreads();
@@ -188,7 +194,7 @@ __device__ __forceinline__ void sh_build_t(const ShCols& c, int key_col, int64_t
     w++;
     vm |= (cv ? 1ULL : 0ULL) << cc;
   }
-  if (ST) r.w[1 + NC] = (uint64_t)c.st[i];
+  if (ST) r.w[1 + NC] = sh_st(c, i);
   r.w[1 + NC + ST] = vm;
 }
 template <int NC, int ST>
@@ -411,6 +417,7 @@ struct khip_shuffle {
   std::vector<int32_t> types;
   hipStream_t stream = nullptr;
   DevBuf hist, csum, pbase, R, ptrs;
+  int64_t st_seed = -1;  // khip_shuffle_stream_time_seed
 };
 
 struct khip_comm {
@@ -479,6 +486,7 @@ static khip_status shuffle_cols(khip_shuffle* s, const khip_batch* b, ShCols* c)
   }
   c->key_bytes = s->types[s->desc.key_col] == KHIP_TYPE_INT32 ? 4 : 8;
   c->st = shuffle_st(s) ? b->stream_time : nullptr;
+  c->st_seed = s->st_seed;
   return KHIP_OK;
 }
 
@@ -653,6 +661,14 @@ khip_status khip_shuffle_unpack_stream_time(khip_shuffle* s, const uint64_t* row
                      khip_shuffle_row_words(s), stream_time);
   KHIP_TRY_HIP(hipGetLastError());
   KHIP_TRY_HIP(hipStreamSynchronize(s->stream));
+  return KHIP_OK;
+}
+
+khip_status khip_shuffle_stream_time_seed(khip_shuffle* s, int64_t seed) {
+  clear_error();
+  if (!s) return fail(KHIP_E_INVALID, "null argument");
+  if (!shuffle_st(s)) return fail(KHIP_E_INVALID, "the shuffle carries no stream time (KHIP_SHUFFLE_STREAM_TIME)");
+  s->st_seed = seed < -1 ? -1 : seed;
   return KHIP_OK;
 }
 

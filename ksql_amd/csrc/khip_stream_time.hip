@@ -281,8 +281,15 @@ __global__ __launch_bounds__(256) void k_pmap_insert(const int64_t* __restrict__
         }
         c = (int64_t)old;
       }
-      if (c == k) {  // (the claimer's partition may not be stored yet: -1 is not a conflict)
-        const int32_t q = __hip_atomic_load(&pp[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (c == k) {
+        // the claimer (another row of this batch, already past its CAS) stores its partition right
+        // after it: wait for it, so that the same new key on two partitions in one batch is seen
+        int32_t q = __hip_atomic_load(&pp[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int spin = 0; q == -1 && spin < (1 << 20); spin++) {
+          __builtin_amdgcn_s_sleep(1);
+          q = __hip_atomic_load(&pp[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (q == -1) atomicOr(&ctr[1], 1ULL);  // (never seen: counted as a failed insert, retried)
         if (q != -1 && q != p) atomicOr(&ctr[2], 1ULL);
         done = true;
         break;

@@ -83,6 +83,17 @@ class _StreamTimeBatch:
         self._keep = [batch, st]
 
 
+class _RekeyedView:
+    """The caller's batch as the GROUP BY sees it for the stream-time scan: the key validity is
+    the GROUP BY column's (all valid when the batch has no bitmap for it)."""
+
+    def __init__(self, batch, key_col):
+        self.struct = abi.Batch.from_buffer_copy(batch.struct)
+        cv = batch.struct.col_valid
+        self.struct.key_valid = cv[key_col] if cv else None
+        self._keep = batch
+
+
 class Repartition:
     def __init__(self, lib, key_col, col_types, rank=0, world=1, comm=None, device=0, global_time=False):
         if world > 1 and comm is None:
@@ -98,16 +109,26 @@ class Repartition:
 
     def stream_times(self, scan, batch):
         """global_time: the GLOBAL stream time observed at each row of this rank's chunk (device
-        int64 tensor).  `scan` is any product AggHandle (khip_stream_time_scan only uses its
-        scratch)."""
+        int64 tensor), as the pack will write it.  `scan` is any product AggHandle
+        (khip_stream_time_scan only uses its scratch).
+
+        Which rows raise it: those that reach the owner's aggregate — a non-null value
+        (StreamGroupByBuilderBase.java:102 filters null values), a non-null GROUP BY column
+        (GroupByParamsFactory.java:92-100: a null one excludes the row, so Kafka Streams' repartition
+        never forwards it) and ts >= 0 — the pack's own row test.  The source key plays no part, so
+        the scan sees the batch re-keyed by the GROUP BY column (its validity as the key bitmap).
+
+        One pass per rank: the chunk is scanned unseeded; the seed (the global stream time before
+        the batch and the chunk maxima of the ranks before this one) is applied by the pack as
+        max(seed, st[i]) (khip_shuffle_stream_time_seed): a seeded prefix max is the unseeded one
+        raised to the seed."""
         import torch
         n = int(batch.struct.n_rows)
         out = torch.empty(max(n, 1), dtype=torch.int64, device=torch.device("cuda", self.shuffle.device))
-        _, mx = scan.stream_time_scan(batch, -1, out)
+        _, mx = scan.stream_time_scan(_RekeyedView(batch, self.shuffle.desc.key_col), -1, out)
         maxima = self.comm.allgather_i64(mx) if self.world > 1 else [mx]
         seed = max([self.gst] + maxima[:self.rank])
-        if seed > -1:
-            scan.stream_time_scan(batch, seed, out)
+        self.shuffle.stream_time_seed(seed)
         self.gst = max([self.gst] + maxima)
         return out[:n]
 

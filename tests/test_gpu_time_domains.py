@@ -381,35 +381,73 @@ def _sh_desc(domain="SUPPLIED", grace=1000, flags=abi.FLAG_PROFILE):
                              aggs=SH_AGGS, flags=flags, capacity_hint=1 << 20, time_domain=domain)
 
 
+def _with_nulls(rng, stream):
+    """NULL GROUP BY values, null values (rows) and null SOURCE keys.  The first
+    two never reach the aggregate (GroupByParamsFactory.java:92-100, StreamGroupByBuilderBase.java:102)
+    and must not raise the global stream time — they get ts far ahead, so counting them would drop
+    more windows; a null source key plays no part (the row is re-keyed), so those rows raise it."""
+    out = []
+    for k, t, v in stream:
+        n = len(t)
+        gbv, rv, skv = rng.random(n) > 0.03, rng.random(n) > 0.02, rng.random(n) > 0.05
+        t = t.copy()
+        t[~gbv] += 15_000
+        t[~rv] += 15_000
+        t[~skv] += 4_000
+        out.append((k, t, v, gbv, rv, skv))
+    return out
+
+
+def _oracle_batch(x):
+    if len(x) == 3:
+        k, t, v = x
+        return abi.HostBatch(t, keys=k, cols=[k, v])
+    k, t, v, gbv, rv, _ = x  # the re-keyed stream: the GROUP BY column is the key
+    return abi.HostBatch(t, keys=k, key_valid=gbv, row_valid=rv, cols=[k, v], col_valid=[gbv, None])
+
+
+def _device_src(x, lo=0, hi=None):
+    import torch
+    hi = len(x[1]) if hi is None else hi
+    d = lambda a: torch.from_numpy(a[lo:hi]).cuda()
+    if len(x) == 3:
+        k, t, v = x
+        return abi.DeviceBatch(d(t), cols=[d(k), d(v)])
+    k, t, v, gbv, rv, skv = x
+    bm = lambda a: abi.bitmap_torch(d(a))
+    return abi.DeviceBatch(d(t), key_valid=bm(skv), row_valid=bm(rv), cols=[d(k), d(v)], col_valid=[bm(gbv), None])
+
+
 def _oracle_one_task(orc, stream, grace=1000):
     o = abi.AggHandle(orc, _sh_desc("TASK", grace, 0))
-    late = sum(o.push(abi.HostBatch(t, keys=k, cols=[k, v]))["windows_late"] for k, t, v in stream)
+    late = sum(o.push(_oracle_batch(x))["windows_late"] for x in stream)
     s = o.snapshot()
     o.close()
     return s, late
 
 
-@pytest.mark.parametrize("late_heavy", [True, False])
-def test_supplied_through_repartition_one_rank(prod, orc, late_heavy):
+@pytest.mark.parametrize("late_heavy,nulls", [(True, False), (False, False), (True, True)])
+def test_supplied_through_repartition_one_rank(prod, orc, late_heavy, nulls):
     """One rank: the GLOBAL stream time is the task's own; the rows' stream-time words must give
-    exactly one oracle task (late-free data: the value pipeline reads them in place)."""
-    import torch
+    exactly one oracle task (late-free data: the value pipeline reads them in place).  nulls: NULL
+    GROUP BY values, null rows and null source keys (_with_nulls)."""
     from ksql_amd.repartition import Repartition
     rng = np.random.default_rng(31 + late_heavy)
     stream = _global_stream(rng, nb=4, per=60_000, keys=4000)
     if not late_heavy:
         stream = [(k, np.sort(t), v) for k, t, v in stream]
+    if nulls:
+        stream = _with_nulls(rng, stream)
     grace = 1000 if late_heavy else 10**9
     h = abi.AggHandle(prod, _sh_desc(grace=grace))
     rp = Repartition(prod, 0, ["INT64", "INT64"], global_time=True)
     late = 0
-    for k, t, v in stream:
-        src = abi.DeviceBatch(torch.from_numpy(t).cuda(), cols=[torch.from_numpy(k).cuda(), torch.from_numpy(v).cuda()])
-        late += rp.push_into(h, src)["windows_late"]
+    for x in stream:
+        late += rp.push_into(h, _device_src(x))["windows_late"]
     exp, olate = _oracle_one_task(orc, stream, grace)
     assert late == olate and (late > 0) == late_heavy
     assert_snap_equal(h.snapshot(), exp, _sh_desc())
-    if not late_heavy:
+    if not late_heavy and not nulls:
         assert h.kernel_times()["c1_pushes"] == len(stream)
     rp.close()
     h.close()
@@ -431,7 +469,7 @@ def test_push_shuffled_domain_errors(prod):
     sh.close()
 
 
-def _gloo_rank_repartition(rank, world, port, q):
+def _gloo_rank_repartition(rank, world, port, q, nulls=False):
     import torch
     import torch.distributed as dist
     from ksql_amd.repartition import GlooExchange, Repartition
@@ -443,13 +481,13 @@ def _gloo_rank_repartition(rank, world, port, q):
         rp = Repartition(prod, 0, ["INT64", "INT64"], rank=rank, world=world, comm=GlooExchange(), global_time=True)
         rng = np.random.default_rng(21)  # every rank generates the same global stream, keeps its chunk
         stream = _global_stream(rng, nb=4, per=60_000, keys=4000)
+        if nulls:
+            stream = _with_nulls(rng, stream)
         late = 0
-        for k, t, v in stream:
-            n = len(t)
+        for x in stream:
+            n = len(x[1])
             lo, hi = n * rank // world, n * (rank + 1) // world
-            src = abi.DeviceBatch(torch.from_numpy(t[lo:hi]).cuda(),
-                                  cols=[torch.from_numpy(k[lo:hi]).cuda(), torch.from_numpy(v[lo:hi]).cuda()])
-            late += rp.push_into(h, src)["windows_late"]
+            late += rp.push_into(h, _device_src(x, lo, hi))["windows_late"]
         s = h.snapshot()
         res = [None] * world
         dist.all_gather_object(res, (s, late, rp.gst))
@@ -462,16 +500,18 @@ def _gloo_rank_repartition(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_supplied_through_repartition_two_processes_gloo(orc):
+@pytest.mark.parametrize("nulls", [False, True])
+def test_supplied_through_repartition_two_processes_gloo(orc, nulls):
     """Two source ranks on this GPU: rows routed by Kafka's partitioner of the GROUP BY column
-    through the product pack_v / exchange / push_shuffled with their GLOBAL stream time; the owners'
-    tables together equal ONE oracle task over the whole late-heavy stream, late drops included."""
+    through the product pack_v / exchange / push_shuffled with their GLOBAL stream time (rank 1's
+    chunk scanned once, the seed applied by the pack); the owners' tables together equal ONE oracle
+    task over the whole late-heavy stream, late drops included.  nulls: _with_nulls."""
     import torch.multiprocessing as mp
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gloo_rank_repartition, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_gloo_rank_repartition, args=(r, world, port, q, nulls)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=180)
@@ -480,9 +520,12 @@ def test_supplied_through_repartition_two_processes_gloo(orc):
         assert p.exitcode == 0
     rng = np.random.default_rng(21)
     stream = _global_stream(rng, nb=4, per=60_000, keys=4000)
+    if nulls:
+        stream = _with_nulls(rng, stream)
     exp, olate = _oracle_one_task(orc, stream)
     assert sum(r[1] for r in res) == olate > 0
-    assert res[0][2] == res[1][2] == max(int(t.max()) for _, t, _ in stream)
+    counted = [x[1][x[3] & x[4]] if nulls else x[1] for x in stream]  # rows that reach the aggregate
+    assert res[0][2] == res[1][2] == max(int(t.max()) for t in counted)
     gd = _sh_desc()
     assert_snap_equal(_union([r[0] for r in res], gd), exp, gd)
 
