@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KHIP_ABI_VERSION 7
+#define KHIP_ABI_VERSION 8
 
 typedef int32_t khip_status;
 #define KHIP_OK 0

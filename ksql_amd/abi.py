@@ -20,7 +20,7 @@ _VARIANT = os.environ.get("KSQL_AMD_LIB_VARIANT", "")
 PRODUCT_LIB = os.path.join(REPO, "ksql_amd", "libksqldb_hip_%s.so" % _VARIANT if _VARIANT else "libksqldb_hip.so")
 ORACLE_LIB = os.path.join(REPO, "oracle", "liboracle.so")
 
-ABI_VERSION = 7  # include/ksqldb_hip.h KHIP_ABI_VERSION the structs below mirror
+ABI_VERSION = 8  # include/ksqldb_hip.h KHIP_ABI_VERSION the structs below mirror
 KHIP_OK = 0
 KHIP_E_BUFFER = -5
 

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_version_and_target():
     lib = abi.load_product()
-    assert lib.dll.khip_abi_version() == abi.ABI_VERSION == 7
+    assert lib.dll.khip_abi_version() == abi.ABI_VERSION == 8
     assert lib.dll.khip_build_target() == b"gfx950"
 
 

