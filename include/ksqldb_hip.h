@@ -320,7 +320,12 @@ khip_status khip_agg_get(khip_agg* agg, const khip_pull* q, const khip_having* h
  *   EMIT FINAL (S/StreamAggregateBuilder.java:282-285, EmitStrategy.onWindowClose): every window
  *     the push closed (window end <= stream time - grace), emitted once with its final value
  *     unless it had already expired from the window store (retention) at the record that closed
- *     it, then filtered by the descriptor's HAVING.
+ *     it, then filtered by the descriptor's HAVING.  SESSION windows (ABI 8; S/StreamAggregateBuilder
+ *     .java:310-312, Kafka 3.4 KStreamSessionWindowAggregate.maybeForwardFinalResult): a session is
+ *     emitted once, when streamTime - grace - gap passes its END — the sessions of the store after
+ *     the push whose end the push's close time passed, and those a record of the push merged away
+ *     after the close before that record had passed their end (a RETENTION beyond gap + grace) —
+ *     row time = session end, HAVING applied.
  * khip_agg_changes_size returns the row count and (UTF8) key bytes of the last push's rows;
  * khip_agg_changes writes them in snapshot layout plus tombstone[n_rows] (1 = delete; may be
  * NULL).  Valid until the next push or reset. */

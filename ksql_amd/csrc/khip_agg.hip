@@ -1260,8 +1260,6 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
   const khip_agg_desc& d = *desc;
   if (d.window_kind < KHIP_WINDOW_NONE || d.window_kind > KHIP_WINDOW_SESSION)
     return fail(KHIP_E_INVALID, "unknown window kind");
-  if (d.window_kind == KHIP_WINDOW_SESSION && d.emit == KHIP_EMIT_FINAL)
-    return fail(KHIP_E_UNSUPPORTED, "EMIT FINAL on SESSION windows");
   if (d.window_kind != KHIP_WINDOW_NONE) {
     if (d.size_ms <= 0) return fail(KHIP_E_INVALID, "window size must be > 0");
     if (d.window_kind == KHIP_WINDOW_HOPPING && (d.advance_ms <= 0 || d.advance_ms > d.size_ms))
@@ -1671,7 +1669,8 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   int64_t key_bytes_total = 0;
   KHIP_TRY(resolve_batch(a, b, &keys, &ts, &kv, &rv, &koff, &kbytes, &cols, &key_bytes_total));
   const bool pdomain = a->desc.time_domain == KHIP_TIME_PARTITION;
-  if (final_emit && !pdomain) KHIP_TRY(emit_final_lost(a, ts, kv, rv, n, 0, nullptr));
+  // (SESSION windows close sessions themselves: sess_push)
+  if (final_emit && !pdomain && a->engine != 2) KHIP_TRY(emit_final_lost(a, ts, kv, rv, n, 0, nullptr));
   // ---- ABI 5 stream-time domains: the stream time observed at every row
   const int64_t* st_at = nullptr;
   const int32_t* part = nullptr;
@@ -1813,7 +1812,7 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   }
   // one task per partition: the handle's stream time (closing windows, retention) is the slowest's
   if (pdomain) KHIP_TRY(stream_time_partition_min(a));
-  if (final_emit) KHIP_TRY(pdomain ? partition_lost_finish(a) : finish_lost(a, ts, kv, rv, n));
+  if (final_emit && a->engine != 2) KHIP_TRY(pdomain ? partition_lost_finish(a) : finish_lost(a, ts, kv, rv, n));
   if (a->engine == 0 && a->windowed) {  // retention: drop expired windows from the closed store
     HavingDev vis{};
     vis.vis = 1;
@@ -2170,7 +2169,10 @@ static khip_status compute_changes(khip_agg* a) {
   a->chg_rows.clear();
   a->chg_tomb.clear();
   a->chg_n = 0;
-  if (a->desc.emit == KHIP_EMIT_FINAL) {
+  if (a->desc.emit == KHIP_EMIT_FINAL && a->engine == 2) {
+    // the sessions the push closed (sess_push: k_sess_apply / k_sess_keep)
+    KHIP_TRY(sess_changes(a, &a->chg_rows, &a->chg_tomb, &a->chg_n));
+  } else if (a->desc.emit == KHIP_EMIT_FINAL) {
     // windows closed by the push and still visible when they closed, passing HAVING
     HavingDev fd{};
     fd.fin = 1;

@@ -46,6 +46,11 @@ struct SessParams {
   HavingDev having;
   int32_t sw;
   int64_t gap, grace, retention;
+  // EMIT FINAL (Kafka 3.4 KStreamSessionWindowAggregate.maybeForwardFinalResult; oracle R11): the
+  // push emits the sessions whose end passes into [fin_lo, close after the push), fin_lo =
+  // max(0, close before the push), close = stream time - grace - gap
+  int32_t fin;
+  int64_t fin_lo;
 };
 
 // Accepted records (valid key and value, ts >= 0): per-block ts maximum (for the stream-time
@@ -172,8 +177,11 @@ __global__ __launch_bounds__(1024) void k_sess_range_reduce(const ulonglong2* __
   }
 }
 
-// Packed 8-byte replay record: (stream time after - tbase + 1) << 32 | (ts - tbase + 1), each half
+// Packed 8-byte replay record: (stream time before - tbase + 1) << 32 | (ts - tbase + 1), each half
 // 0 for -1 (a dropped record / no stream time yet); used when the push's times span < 2^32 - 1.
+// The replay takes the stream time after an accepted record as max(before, ts); the one before it
+// is EMIT FINAL's (a session merged away by the record was emitted if the close time before the
+// record had passed its end).
 __device__ __forceinline__ uint64_t rec_pack(int64_t t, int64_t st, int64_t tbase) {
   const uint64_t lo = t >= 0 ? (uint64_t)(t - tbase + 1) : 0, hi = st >= 0 ? (uint64_t)(st - tbase + 1) : 0;
   return (hi << 32) | lo;
@@ -184,8 +192,8 @@ __device__ __forceinline__ void rec_unpack(uint64_t r, int64_t tbase, int64_t& t
   st = hi ? tbase + (int64_t)hi - 1 : -1;
 }
 
-// Per record (coalesced): the task's stream time after it (block prefix, then the block's running
-// max), the packed replay record {ts or -1 when dropped, stream time after}, and the (key - kmin,
+// Per record (coalesced): the task's stream time before it (block prefix, then the block's running
+// max), the packed replay record {ts or -1 when dropped, stream time before}, and the (key - kmin,
 // row) pair to sort (dropped rows get the sentinel `drop`, which sorts last); drop counters.
 __global__ __launch_bounds__(BLOCK) void k_sess_prep(const int64_t* __restrict__ keys, const int64_t* __restrict__ ts,
                                                      const uint8_t* __restrict__ kv, const uint8_t* __restrict__ rv,
@@ -200,7 +208,7 @@ __global__ __launch_bounds__(BLOCK) void k_sess_prep(const int64_t* __restrict__
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t base = (int64_t)blockIdx.x * RPB + (int64_t)wave * 64 * ITEMS + lane;
   int64_t stv[ITEMS], tv[ITEMS];
-  int64_t carry = -1;
+  int64_t carry = -1;  // the wave's running maximum before the step
   int nk = 0, nr = 0, nt = 0, na = 0;
 #pragma unroll
   for (int k = 0; k < ITEMS; k++) {
@@ -219,7 +227,8 @@ __global__ __launch_bounds__(BLOCK) void k_sess_prep(const int64_t* __restrict__
     tv[k] = ok ? t : -1;
     int64_t incl = wave_incl_max(tv[k]);
     incl = incl > carry ? incl : carry;
-    stv[k] = incl;
+    const int64_t ex = __shfl_up(incl, 1, 64);  // the lane before's inclusive maximum
+    stv[k] = lane ? ex : carry;                 // exclusive: the stream time before the record
     carry = __shfl(incl, 63, 64);
   }
   if (lane == 0) wmax[wave] = carry;
@@ -399,7 +408,7 @@ __device__ __forceinline__ int64_t sess_replay(const SessParams& q, int64_t key,
                                                const longlong2* g, const uint64_t* g8, int64_t tbase,
                                                const uint32_t* sidx, int64_t nrec,
                                                uint64_t* R, uint8_t* F, uint64_t* T, const ColPtrs& cols,
-                                               int64_t vis_end, uint64_t* __restrict__ crow,
+                                               int64_t vis_end, int64_t close_end, uint64_t* __restrict__ crow,
                                                uint8_t* __restrict__ ctomb, unsigned long long* __restrict__ ctr,
                                                int keep_changes, int64_t& applied, int64_t& late) {
   const int sw = q.sw;
@@ -411,15 +420,16 @@ __device__ __forceinline__ int64_t sess_replay(const SessParams& q, int64_t key,
     m++;
   }
   for (int64_t r = 0; r < nrec; r++) {
-    int64_t t, st;
+    int64_t t, stb;
     if (g8) {
-      rec_unpack(g8[r], tbase, t, st);
+      rec_unpack(g8[r], tbase, t, stb);
     } else {
       const longlong2 gr = g[r];
       t = gr.x;
-      st = gr.y;
+      stb = gr.y;
     }
     if (t < 0) continue;  // dropped (only where the sentinel shares the last key's segment)
+    const int64_t st = stb > t ? stb : t;  // the stream time after the record
     const int64_t i = q.ap.n_cols ? (int64_t)sidx[r] : 0;
     const int64_t vis = st - q.retention, close = st - q.grace - q.gap;
     // overlapping run: visible sessions with end >= t - gap and start <= t + gap
@@ -447,12 +457,26 @@ __device__ __forceinline__ int64_t sess_replay(const SessParams& q, int64_t key,
       F[lo] |= SF_TOUCHED;
       continue;
     }
-    // the merged-away sessions that existed before the push: their deletions are emitted
-    for (int64_t k = lo; k < hi; k++) {
-      if (F[k] & SF_ORIG) {
-        row_copy(T + nt * sw, R + k * sw, sw);
-        T[nt * sw + 0] = (uint64_t)F[k];  // flags ride in the key word (the key is known)
-        nt++;
+    if (q.fin) {
+      // EMIT FINAL: a merged-away session the close time before this record had already passed
+      // was emitted then (it is leaving the store only now); sessions of earlier pushes that
+      // passed it were emitted by those pushes
+      const int64_t cb = stb >= 0 ? stb - q.grace - q.gap : INT64_MIN;
+      for (int64_t k = lo; k < hi; k++) {
+        const int64_t e = (int64_t)R[k * sw + 2];
+        if (e >= q.fin_lo && e < cb && having_ok(R + k * sw, q.having)) {
+          row_copy(T + nt * sw, R + k * sw, sw);
+          nt++;
+        }
+      }
+    } else {
+      // the merged-away sessions that existed before the push: their deletions are emitted
+      for (int64_t k = lo; k < hi; k++) {
+        if (F[k] & SF_ORIG) {
+          row_copy(T + nt * sw, R + k * sw, sw);
+          T[nt * sw + 0] = (uint64_t)F[k];  // flags ride in the key word (the key is known)
+          nt++;
+        }
       }
     }
     // merged row, in place at lo: the first overlapped session, the later ones merged into it in
@@ -482,9 +506,28 @@ __device__ __forceinline__ int64_t sess_replay(const SessParams& q, int64_t key,
     F[lo] = SF_TOUCHED;
     sess_apply_record(q, R + lo * sw, cols, i);
   }
-  // changelog: touched sessions (rows, or tombstones when HAVING stopped holding), deleted
-  // sessions that existed before the push (tombstones when HAVING held)
-  if (keep_changes) {
+  if (q.fin) {
+    // EMIT FINAL: the sessions merged away after their close (above), and those of the store
+    // after the push whose end the close time passed during it
+    int64_t nc = nt;
+    for (int64_t k = 0; k < m; k++) {
+      const int64_t e = (int64_t)R[k * sw + 2];
+      nc += (e >= q.fin_lo && e < close_end && having_ok(R + k * sw, q.having)) ? 1 : 0;
+    }
+    int64_t c = nc ? (int64_t)atomicAdd(&ctr[16], (unsigned long long)nc) : 0;
+    for (int64_t k = 0; k < nt; k++) {
+      row_copy(crow + c * sw, T + k * sw, sw);
+      ctomb[c++] = 0;
+    }
+    for (int64_t k = 0; k < m; k++) {
+      const int64_t e = (int64_t)R[k * sw + 2];
+      if (!(e >= q.fin_lo && e < close_end && having_ok(R + k * sw, q.having))) continue;
+      row_copy(crow + c * sw, R + k * sw, sw);
+      ctomb[c++] = 0;
+    }
+  } else if (keep_changes) {
+    // changelog: touched sessions (rows, or tombstones when HAVING stopped holding), deleted
+    // sessions that existed before the push (tombstones when HAVING held)
     int64_t nc = 0;
     for (int64_t k = 0; k < m; k++)
       if (F[k] & SF_TOUCHED) nc += (having_ok(R + k * sw, q.having) || ((F[k] & SF_ORIG) && (F[k] & SF_OLDP))) ? 1 : 0;
@@ -574,6 +617,7 @@ __global__ __launch_bounds__(64) void k_sess_apply(SessParams q, const uint64_t*
   const int64_t need = (C1 - C0) * (sw * 8 + 1);
   const bool in_lds = need <= SESS_LDS;
   const int64_t vis_end = *st_end - q.retention;
+  const int64_t close_end = *st_end >= 0 ? *st_end - q.grace - q.gap : INT64_MIN;
   int64_t applied = 0, late = 0, kept = 0;
   const bool mine = j < nseg_eff;
   (void)R1;
@@ -584,7 +628,7 @@ __global__ __launch_bounds__(64) void k_sess_apply(SessParams q, const uint64_t*
       const int64_t base = scap[j], r0 = useg[j];
       kept = sess_replay(q, ukeys[j], store + s0[j] * sw, cap[j] - ucnt[j], g ? g + r0 : nullptr, g8 ? g8 + r0 : nullptr, tbase,
                          sidx ? sidx + r0 : nullptr,
-                         ucnt[j], lrow + (base - C0) * sw, lfl + (base - C0), trow + base * sw, cols, vis_end, crow,
+                         ucnt[j], lrow + (base - C0) * sw, lfl + (base - C0), trow + base * sw, cols, vis_end, close_end, crow,
                          ctomb, ctr, keep_changes, applied, late);
       fin[j] = kept;
     }
@@ -596,7 +640,8 @@ __global__ __launch_bounds__(64) void k_sess_apply(SessParams q, const uint64_t*
     const int64_t base = scap[j], r0 = useg[j];
     kept = sess_replay(q, ukeys[j], store + s0[j] * sw, cap[j] - ucnt[j], g ? g + r0 : nullptr, g8 ? g8 + r0 : nullptr, tbase,
                          sidx ? sidx + r0 : nullptr, ucnt[j],
-                       srow + base * sw, sfl + base, trow + base * sw, cols, vis_end, crow, ctomb, ctr, keep_changes,
+                       srow + base * sw, sfl + base, trow + base * sw, cols, vis_end, close_end, crow, ctomb, ctr,
+                       keep_changes,
                        applied, late);
     fin[j] = kept;
   }
@@ -608,19 +653,41 @@ __global__ __launch_bounds__(64) void k_sess_apply(SessParams q, const uint64_t*
   }
 }
 
-// Store rows that survive untouched: key not in the batch and not expired.
+// Store rows that survive untouched: key not in the batch and not expired.  EMIT FINAL (q.fin):
+// the untouched keys' sessions whose end the push's close time passed are emitted (wave-aggregated
+// appends to the changelog rows).
 __global__ __launch_bounds__(256) void k_sess_keep(const uint64_t* __restrict__ store, int64_t ns, int sw,
                                                    const int64_t* __restrict__ ukeys, const int* __restrict__ nseg,
                                                    const int64_t* __restrict__ st_end, int64_t retention,
-                                                   int* __restrict__ keep) {
+                                                   int* __restrict__ keep, SessParams q, uint64_t* __restrict__ crow,
+                                                   uint8_t* __restrict__ ctomb, unsigned long long* __restrict__ ctr) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= ns) return;
-  const uint64_t* s = store + i * sw;
-  const int64_t k = (int64_t)s[0];
-  const int64_t nu = *nseg;
-  const int64_t p = lower_val(ukeys, nu, k);
-  const bool in_batch = p < nu && ukeys[p] == k;
-  keep[i] = (!in_batch && (int64_t)s[2] >= *st_end - retention) ? 1 : 0;
+  bool emit = false;
+  const uint64_t* s = store + (i < ns ? i : 0) * sw;
+  if (i < ns) {
+    const int64_t k = (int64_t)s[0];
+    const int64_t nu = *nseg;
+    const int64_t p = lower_val(ukeys, nu, k);
+    const bool in_batch = p < nu && ukeys[p] == k;
+    keep[i] = (!in_batch && (int64_t)s[2] >= *st_end - retention) ? 1 : 0;
+    if (q.fin && !in_batch && *st_end >= 0) {
+      const int64_t e = (int64_t)s[2];
+      emit = e >= q.fin_lo && e < *st_end - q.grace - q.gap && having_ok(s, q.having);
+    }
+  }
+  if (!q.fin) return;
+  const uint64_t bl = __ballot(emit);
+  if (!bl) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((unsigned long long)bl) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(&ctr[16], (unsigned long long)__popcll(bl));
+  base = __shfl(base, leader, 64);
+  if (emit) {
+    const unsigned long long c = base + __popcll(bl & ((1ULL << lane) - 1));
+    row_copy(crow + c * sw, s, sw);
+    ctomb[c] = 0;
+  }
 }
 
 // New store: kept rows and the rewritten keys' sessions, in key order.
@@ -775,7 +842,8 @@ khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   KHIP_TRY(S.srow.ensure((size_t)scr * sw * 8));
   KHIP_TRY(S.sfl.ensure((size_t)scr));
   KHIP_TRY(S.trow.ensure((size_t)scr * sw * 8));
-  const bool keep_changes = a->changelog;
+  const bool fin = a->desc.emit == KHIP_EMIT_FINAL;
+  const bool keep_changes = a->changelog || fin;
   if (keep_changes) {
     KHIP_TRY(S.crow.ensure((size_t)scr * sw * 8));
     KHIP_TRY(S.ctomb.ensure((size_t)scr));
@@ -788,6 +856,11 @@ khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   q.gap = a->desc.size_ms;
   q.grace = a->grace;
   q.retention = a->retention;
+  q.fin = fin ? 1 : 0;
+  {
+    const int64_t cp = a->st_before >= 0 ? a->st_before - a->grace - a->desc.size_ms : 0;
+    q.fin_lo = cp > 0 ? cp : 0;
+  }
   if (nseg > 0)
     hipLaunchKernelGGL(k_sess_apply, dim3(ceil_div(nseg, 64)), dim3(64), 0, st, q, store, S.ukeys.as<int64_t>(),
                      S.ucnt.as<int>(), S.useg.as<int64_t>(), S.nseg.as<int>(), S.s0.as<int64_t>(), S.cap.as<int64_t>(),
@@ -803,7 +876,9 @@ khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   KHIP_TRY(S.keep_pre.ensure((size_t)(ns + 1) * 4));
   if (ns) {
     hipLaunchKernelGGL(k_sess_keep, dim3(ceil_div(ns, 256)), dim3(256), 0, st, store, ns, sw, S.ukeys.as<int64_t>(),
-                       S.nseg.as<int>(), a->stream_time.as<int64_t>(), a->retention, S.keep.as<int>());
+                       S.nseg.as<int>(), a->stream_time.as<int64_t>(), a->retention, S.keep.as<int>(), q,
+                       fin ? S.crow.as<uint64_t>() : nullptr, fin ? S.ctomb.as<uint8_t>() : nullptr,
+                       S.ctr.as<unsigned long long>());
     KHIP_TRY((ksort::scan_excl<int, int>(st, S.tmp, S.keep.as<int>(), S.keep_pre.as<int>(), ns, false, nullptr)));
   }
   // fin_pre[nseg] = total rewritten rows (inclusive end) via a scan over nseg + 1 entries

@@ -62,6 +62,15 @@
  *     merged-away sessions are deleted (tombstones) and the merged one is written with the
  *     record applied.  Row time = session end.  Pinned by Q/session-windows.json:4,45 (late
  *     drop and expiry with GRACE PERIOD); the default grace max(24h - gap, 0) is unpinned.
+ *     EMIT FINAL on sessions (S/StreamAggregateBuilder.java:310-312, sessionWindowedKStream
+ *     .emitStrategy(onWindowClose()); Kafka 3.4 KStreamSessionWindowAggregate.maybeForwardFinalResult):
+ *     after every record that reaches the processor, with windowCloseTime = streamTime - grace -
+ *     gap: when it passed the last emitted close time (or none was emitted yet) and close - 1 >= 0,
+ *     every session in the store whose END lies in [max(0, lastClose), close - 1] is emitted once
+ *     (row time = its end; HAVING applied as for time windows) and lastClose = close.  The time-
+ *     ordered session store keeps sessions until their segment expires, so the emission does not
+ *     apply R9's exact expiry; merges do (as EMIT CHANGES).  Pinned by Q/suppress.json "should
+ *     support final results for session windows" (emit interval 0: a check after every record).
  *  R12 table aggregation (S/TableAggregateBuilder.java:54-108 over S/TableGroupByBuilderBase.java
  *     :62-111; Kafka 3.4 KTableRepartitionMap + KTableAggregate): the source table keeps the latest
  *     row per PRIMARY KEY (a tombstone deletes it); each accepted record first undoes the key's
@@ -291,6 +300,14 @@ struct oracle_agg {
   int64_t* sk_n;
   int64_t* sk_cap;
   int64_t sk_slots, sk_used;
+  /* SESSION + EMIT FINAL: live sessions by end (a min-heap of (end, entry)), the last emitted
+   * close time, and the sessions the current push emitted */
+  int64_t* fh_end;
+  int64_t* fh_idx;
+  int64_t fh_n, fh_cap;
+  int64_t last_close;
+  int64_t* fin_emit;
+  int64_t n_fin, cap_fin;
   int64_t* stmax;     /* the push's stream-time maxima, in arrival order           */
   int64_t n_stmax, cap_stmax;
   int own_stmax;      /* stmax is this handle's (0: borrowed from the sharded push)  */
@@ -385,7 +402,6 @@ static int valid_desc(const khip_agg_desc* d) {
   if (d->window_kind != KHIP_WINDOW_NONE && d->window_kind != KHIP_WINDOW_TUMBLING &&
       d->window_kind != KHIP_WINDOW_HOPPING && d->window_kind != KHIP_WINDOW_SESSION)
     return 0;
-  if (d->window_kind == KHIP_WINDOW_SESSION && d->emit == KHIP_EMIT_FINAL) return 0;
   if (d->window_kind != KHIP_WINDOW_NONE) {
     if (d->size_ms <= 0) return 0;
     if (d->window_kind == KHIP_WINDOW_HOPPING &&
@@ -442,6 +458,7 @@ khip_status oracle_agg_create(const khip_agg_desc* desc, oracle_agg** out) {
     else a->retention = desc->retention_ms;
   }
   a->obs_ws = -1;
+  a->last_close = -1;
   a->own_stmax = 1;
   a->src_key_type = -1;
   a->stream_time = -1;
@@ -599,6 +616,65 @@ static void merge_state(oracle_agg* a, agg_state* dst, const agg_state* src) {
   }
 }
 
+/* SESSION + EMIT FINAL: a binary min-heap of the sessions by end. */
+static void fh_push(oracle_agg* a, int64_t end, int64_t idx) {
+  if (a->fh_n == a->fh_cap) {
+    a->fh_cap = a->fh_cap ? a->fh_cap * 2 : 1024;
+    a->fh_end = (int64_t*)realloc(a->fh_end, sizeof(int64_t) * a->fh_cap);
+    a->fh_idx = (int64_t*)realloc(a->fh_idx, sizeof(int64_t) * a->fh_cap);
+  }
+  int64_t i = a->fh_n++;
+  while (i > 0) {
+    const int64_t p = (i - 1) / 2;
+    if (a->fh_end[p] <= end) break;
+    a->fh_end[i] = a->fh_end[p];
+    a->fh_idx[i] = a->fh_idx[p];
+    i = p;
+  }
+  a->fh_end[i] = end;
+  a->fh_idx[i] = idx;
+}
+
+static int64_t fh_pop(oracle_agg* a) { /* the entry of the smallest end */
+  const int64_t top = a->fh_idx[0];
+  const int64_t e = a->fh_end[--a->fh_n], x = a->fh_idx[a->fh_n];
+  int64_t i = 0;
+  for (;;) {
+    int64_t c = 2 * i + 1;
+    if (c >= a->fh_n) break;
+    if (c + 1 < a->fh_n && a->fh_end[c + 1] < a->fh_end[c]) c++;
+    if (a->fh_end[c] >= e) break;
+    a->fh_end[i] = a->fh_end[c];
+    a->fh_idx[i] = a->fh_idx[c];
+    i = c;
+  }
+  if (a->fh_n) {
+    a->fh_end[i] = e;
+    a->fh_idx[i] = x;
+  }
+  return top;
+}
+
+/* KStreamSessionWindowAggregate.maybeForwardFinalResult after one record (emit interval 0):
+ * sessions of the store with end in [max(0, lastClose), close - 1], once.  A session merged away
+ * before its close passed is no longer in the store (dead): never emitted. */
+static void session_emit_final(oracle_agg* a, int64_t st) {
+  const int64_t close = st - a->grace - a->d.size_ms;
+  if (!(a->last_close == -1 || a->last_close < close)) return;
+  if (close - 1 < 0) return;
+  while (a->fh_n > 0 && a->fh_end[0] <= close - 1) {
+    const int64_t k = fh_pop(a);
+    const entry* x = &a->e[k];
+    if (x->dead || x->we < (a->last_close > 0 ? a->last_close : 0)) continue;
+    if (a->n_fin == a->cap_fin) {
+      a->cap_fin = a->cap_fin ? a->cap_fin * 2 : 1024;
+      a->fin_emit = (int64_t*)realloc(a->fin_emit, sizeof(int64_t) * a->cap_fin);
+    }
+    a->fin_emit[a->n_fin++] = k;
+  }
+  a->last_close = close;
+}
+
 /* One record of a SESSION aggregation (R11); st = the task's stream time after the record. */
 static void session_apply(oracle_agg* a, int64_t key, int64_t ts, int64_t st, const khip_batch* b, int64_t r,
                           int64_t* applied, int64_t* late) {
@@ -632,6 +708,7 @@ static void session_apply(oracle_agg* a, int64_t key, int64_t ts, int64_t st, co
   }
   entry* nx = new_entry(a, key, mstart, mend);
   const int64_t ni = nx - a->e;
+  if (a->d.emit == KHIP_EMIT_FINAL) fh_push(a, mend, ni);
   /* merge the overlapping sessions in store order (by end), delete them */
   int64_t m = 0;
   for (int64_t k = 0; k < n; k++) {
@@ -668,6 +745,7 @@ khip_status oracle_agg_push(oracle_agg* a, const khip_batch* b, khip_batch_stats
   a->n_touched = 0;
   a->st_before = a->stream_time;
   a->n_stmax = 0;
+  a->n_fin = 0;
   for (int64_t r = 0; r < b->n_rows; r++) {
     if (!bit_get(b->key_valid, r)) { s.dropped_null_key++; continue; }
     if (!bit_get(b->row_valid, r)) { s.dropped_null_row++; continue; }
@@ -697,6 +775,7 @@ khip_status oracle_agg_push(oracle_agg* a, const khip_batch* b, khip_batch_stats
       }
       session_apply(a, key, ts, a->stream_time, b, r, &s.windows_applied, &s.windows_late);
       a->obs_ws = a->stream_time; /* every stream-time maximum is put into the session store */
+      if (a->d.emit == KHIP_EMIT_FINAL) session_emit_final(a, a->stream_time);
       continue;
     }
     if (ts > a->stream_time) { /* R2: before the check */
@@ -994,7 +1073,10 @@ static int cmp_chg(const void* pa, const void* pb, void* ctx) { /* (entry << 1 |
 static void finish_push(oracle_agg* a) {
   const khip_having* hv = query_having(a);
   a->n_chg = 0;
-  if (a->d.emit == KHIP_EMIT_FINAL) {
+  if (a->d.emit == KHIP_EMIT_FINAL && a->d.window_kind == KHIP_WINDOW_SESSION) {
+    for (int64_t k = 0; k < a->n_fin; k++)
+      if (having_pass(a, hv, &a->e[a->fin_emit[k]])) chg_add(a, a->fin_emit[k], 0);
+  } else if (a->d.emit == KHIP_EMIT_FINAL) {
     /* Every window that closed during this push (streamTime - grace passed its end), emitted iff it
      * was still visible (R9) at the record that closed it: with the emission check after every
      * record (Q/suppress.json's emit interval 0), that record's stream time st* is the first
@@ -1141,6 +1223,9 @@ khip_status oracle_agg_changes(oracle_agg* a, khip_snapshot* out, uint8_t* tombs
 khip_status oracle_agg_destroy(oracle_agg* a) {
   if (!a) return KHIP_OK;
   free(a->touched);
+  free(a->fh_end);
+  free(a->fh_idx);
+  free(a->fin_emit);
   free(a->chg);
   free(a->chg_tomb);
   if (a->own_stmax) free(a->stmax);
@@ -1239,6 +1324,9 @@ khip_status oracle_agg_push_sharded(oracle_agg** shards, int32_t P, const khip_b
   if (!shards || P < 1 || !b || b->mem != KHIP_MEM_HOST || b->n_rows < 0) return KHIP_E_INVALID;
   oracle_agg* a0 = shards[0];
   if (b->n_cols < a0->d.n_cols) return KHIP_E_INVALID;
+  /* SESSION EMIT FINAL: the close time passes every shard's sessions record by record (one task);
+   * the sequential oracle_agg_push is its checker */
+  if (a0->d.window_kind == KHIP_WINDOW_SESSION && a0->d.emit == KHIP_EMIT_FINAL) return KHIP_E_UNSUPPORTED;
   const int64_t n = b->n_rows;
   khip_batch_stats s;
   memset(&s, 0, sizeof(s));

@@ -275,8 +275,6 @@ def extract_agg(path, test, fmt_tag):
     if not m:
         raise Skip("ctas shape")
     emit = (m.group(12) or "CHANGES").upper()
-    if emit == "FINAL" and (m.group(6) or "").upper() == "SESSION":
-        raise Skip("session emit final")
     out_name = m.group(1).upper()
     if m.group(3).upper() != src["name"]:
         raise Skip("from")

@@ -323,3 +323,92 @@ def test_sessions_time_span_edges(prod, orc, count_only):
         assert_snap_equal(g.snapshot(), o.snapshot(), g.desc, ABS_SUM, CNT_DBL)
     g.close()
     o.close()
+
+
+# ------------------------------------------------------------------ SESSION + EMIT FINAL
+# VERDICT r05 missing #2 (S/StreamAggregateBuilder.java:310-312, sessionWindowedKStream.emitStrategy(
+# onWindowClose())).  The oracle restates Kafka 3.4's per-record check (R11: after every record,
+# sessions whose END lies in [max(0, lastClose), close - 1], close = streamTime - grace - gap; pinned
+# by Q/suppress.json "should support final results for session windows", test_oracle_golden.py and
+# test_gpu_parity.py).  The device derives a push's emissions from that rule (sess_push): sessions
+# in the store after the push whose end the push's close passed, plus sessions a record merged away
+# after the close before it had passed their end (possible only with RETENTION > gap + grace).
+
+SESSIONS_FINAL = [dict(window_kind="SESSION", size_ms=5_000, grace_ms=10_000),
+                  dict(window_kind="SESSION", size_ms=20_000, grace_ms=0),
+                  dict(window_kind="SESSION", size_ms=3_000, grace_ms=2_000, retention_ms=60_000)]
+
+
+@pytest.mark.parametrize("key_type", ["INT64", "UTF8"])
+@pytest.mark.parametrize("having", [None, {"agg": 0, "op": "GT", "value": 2}])
+@pytest.mark.parametrize("win", range(len(SESSIONS_FINAL)))
+def test_sessions_emit_final_vs_oracle(prod, orc, win, having, key_type):
+    rng = np.random.default_rng(1200 + 10 * win + (having is not None) + (5 if key_type == "UTF8" else 0))
+    kw = dict(SESSIONS_FINAL[win], key_type=key_type, col_types=COLS, aggs=ALL_AGGS, having=having, emit="FINAL")
+    g = abi.AggHandle(prod, abi.make_agg_desc(**kw))
+    o = abi.AggHandle(orc, abi.make_agg_desc(**kw))
+    emitted = 0
+    for batch in _batches(rng, 6, 4000, key_type, 150, 200_000, 40_000, jump=60_000):
+        assert g.push(batch) == o.push(batch)
+        gc, oc = g.changes(), o.changes()
+        _assert_changes_equal(gc, oc, g.desc)
+        assert not gc["tombstone"].any()
+        emitted += gc["n"]
+        assert_snap_equal(g.snapshot(having), o.snapshot(having), g.desc, ABS_SUM, CNT_DBL)
+    assert emitted > 0
+    g.close()
+    o.close()
+
+
+@pytest.mark.parametrize("retention", [-1, 40_000])
+def test_sessions_emit_final_small_pushes(prod, orc, retention):
+    """1-4-record pushes (the reference's emit-at-every-record run), boundary records that merge
+    with a session right at the close time, a session extended after it was emitted (RETENTION
+    beyond gap + grace keeps it visible)."""
+    rng = np.random.default_rng(1300 + (retention > 0))
+    kw = dict(window_kind="SESSION", size_ms=5, grace_ms=6, key_type="INT64", col_types=COLS, aggs=ALL_AGGS,
+              emit="FINAL", retention_ms=retention)
+    g = abi.AggHandle(prod, abi.make_agg_desc(**kw))
+    o = abi.AggHandle(orc, abi.make_agg_desc(**kw))
+    n = 600
+    ts = np.cumsum(rng.integers(0, 4, n)) + rng.integers(-15, 3, n)
+    ts[rng.random(n) < 0.05] += 25  # jumps: closes several sessions at once
+    keys = rng.integers(0, 4, n)
+    cols = [rng.integers(-9, 9, n).astype(np.int32), rng.integers(-9, 9, n), rng.random(n), rng.random(n)]
+    i = emitted = 0
+    while i < n:
+        sl = slice(i, min(i + int(rng.integers(1, 5)), n))
+        b = abi.HostBatch(ts[sl], keys=keys[sl], cols=[c[sl] for c in cols])
+        assert g.push(b) == o.push(b)
+        gc, oc = g.changes(), o.changes()
+        _assert_changes_equal(gc, oc, g.desc)
+        emitted += gc["n"]
+        i = sl.stop
+    assert emitted > 0
+    g.close()
+    o.close()
+
+
+def test_sessions_emit_final_one_push_equals_record_by_record(prod, orc):
+    """The same records as ONE push and as one-record pushes: the device's batched rule emits the
+    union of what the oracle's per-record checks emit (rows keyed by session)."""
+    rng = np.random.default_rng(1400)
+    kw = dict(window_kind="SESSION", size_ms=50, grace_ms=30, key_type="INT64", col_types=COLS, aggs=ALL_AGGS,
+              emit="FINAL", retention_ms=400)
+    n = 3000
+    ts = np.cumsum(rng.integers(0, 6, n)) + rng.integers(-60, 5, n)
+    keys = rng.integers(0, 40, n)
+    cols = [rng.integers(-9, 9, n).astype(np.int32), rng.integers(-9, 9, n), rng.random(n), rng.random(n)]
+    g = abi.AggHandle(prod, abi.make_agg_desc(**kw))
+    o = abi.AggHandle(orc, abi.make_agg_desc(**kw))
+    assert g.push(abi.HostBatch(ts, keys=keys, cols=cols)) is not None
+    gc = g.changes()
+    rows = []
+    for r in range(n):
+        o.push(abi.HostBatch(ts[r:r + 1], keys=keys[r:r + 1], cols=[c[r:r + 1] for c in cols]))
+        oc = o.changes()
+        rows += [(int(k), int(s), int(e), int(c)) for k, s, e, c in zip(oc["key"], oc["ws"], oc["we"], oc["values"][0])]
+    got = sorted((int(k), int(s), int(e), int(c)) for k, s, e, c in zip(gc["key"], gc["ws"], gc["we"], gc["values"][0]))
+    assert got == sorted(rows) and len(rows) > 0
+    g.close()
+    o.close()
