@@ -270,7 +270,7 @@ def test_c3_signed_cancellation(prod, orc, say):
     keyh, tsh, valh, validh = synth.hopping_double(0, n, n, keys=10_000)
     valh = valh * 2.0 - 1000.0  # U[-1000, 1000)
     absh = np.abs(valh)
-    desc = abi.make_agg_desc(**kw, capacity_hint=10_000 * 60, flags=abi.FLAG_PROFILE)
+    desc = abi.make_agg_desc(**kw, capacity_hint=4_000_000, flags=abi.FLAG_PROFILE)  # >= 2^11 partitions: the pipeline
     h = abi.AggHandle(prod, desc)
     o = abi.ShardedOracleAgg(orc, abi.make_agg_desc(**kw), THREADS)
     oa = abi.ShardedOracleAgg(orc, abi.make_agg_desc(**kabs), THREADS)
