@@ -273,6 +273,25 @@ khip_status khip_agg_push(khip_agg* agg, const khip_batch* batch,
 khip_status khip_stream_time_scan(khip_agg* agg, const khip_batch* batch, int64_t seed, int64_t* out,
                                   int64_t* out_max);
 
+/* ABI 8.  EMIT FINAL in the GLOBAL domain (KHIP_TIME_SUPPLIED: StreamAggregateBuilder.java:282-285
+ * applies onWindowClose however the stream was repartitioned).  A window that the stream time's
+ * jump at one record both closes and expires (retention) is never emitted (R9/R10); which windows
+ * those are is a property of the global stream time alone, known where the rows are read:
+ *   khip_agg_lost_windows: the window-start ranges [lo, hi] (n_ranges pairs into `ranges`,
+ *     KHIP_E_BUFFER past `capacity`) that the jumps of `batch` — one rank's contiguous arrival
+ *     chunk, its stream time starting at `seed` — close after they expired.  `agg` is an EMIT FINAL
+ *     TUMBLING / HOPPING handle with the query's windows (its scratch only is used).
+ *   khip_agg_supplied_close: before each push of a KHIP_TIME_SUPPLIED EMIT FINAL handle (required),
+ *     or of any SUPPLIED handle that should keep the GLOBAL stream time: the global stream time
+ *     before and after the whole global batch, and the union of every rank's lost ranges.  The
+ *     push then closes the windows whose end lies in (before - grace, after - grace], except the
+ *     lost ones — also when no row of the batch was routed to this handle (n_rows = 0) — and the
+ *     handle's stream time becomes `st_after`. */
+khip_status khip_agg_lost_windows(khip_agg* agg, const khip_batch* batch, int64_t seed, int64_t* ranges,
+                                  int64_t capacity, int64_t* n_ranges);
+khip_status khip_agg_supplied_close(khip_agg* agg, int64_t st_before, int64_t st_after, const int64_t* ranges,
+                                    int64_t n_ranges);
+
 /* Number of rows and key bytes the next snapshot will produce (no HAVING).  Snapshots, pull
  * queries and row counts read the window store: windows with start < obs - retention (obs =
  * the largest window start put, i.e. floor(streamTime / advance) * advance) have expired. */

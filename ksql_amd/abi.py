@@ -213,6 +213,8 @@ PRODUCT_ONLY = {
     "shuffle_pack_v": ([_P, C.POINTER(Batch), _P, i64, C.POINTER(i64), C.POINTER(i64)]),
     "shuffle_unpack_stream_time": ([_P, _P, i64, _P]),
     "shuffle_stream_time_seed": ([_P, i64]),
+    "agg_lost_windows": ([_P, _P, i64, _P, i64, _P]),
+    "agg_supplied_close": ([_P, i64, i64, _P, i64]),
     "agg_push_shuffled": ([_P, _P, _P, i64, C.POINTER(BatchStats)]),
     "shuffle_sync": ([_P]),
     "shuffle_destroy": ([_P]),
@@ -580,6 +582,29 @@ class AggHandle:
                        "stream_time_scan")
         return out, mx.value
 
+    def lost_windows(self, batch, seed=-1):
+        """khip_agg_lost_windows (ABI 8): [(lo, hi), ...] window-start ranges the batch's stream-time
+        jumps (from `seed`) close after they expired."""
+        cap = 64
+        while True:
+            buf = np.zeros(2 * cap, np.int64)
+            n = i64()
+            st = self.lib.agg_lost_windows(self.h, C.byref(batch.struct), int(seed), buf.ctypes.data, cap,
+                                                    C.byref(n))
+            if st == KHIP_E_BUFFER and n.value > cap:
+                cap = int(n.value)
+                continue
+            self.lib.check(st, "agg_lost_windows")
+            return [(int(buf[2 * k]), int(buf[2 * k + 1])) for k in range(n.value)]
+
+    def supplied_close(self, st_before, st_after, ranges=()):
+        """khip_agg_supplied_close (ABI 8): the GLOBAL stream time around the next push and the
+        union of the ranks' lost ranges."""
+        r = np.asarray([x for p in ranges for x in p], np.int64)
+        self.lib.check(self.lib.agg_supplied_close(self.h, int(st_before), int(st_after),
+                                                   r.ctypes.data if len(r) else None, len(r) // 2),
+                       "agg_supplied_close")
+
     def kernel_times(self, reset=False):
         kt = KernelTimes()
         self.lib.check(self.lib.agg_kernel_times(self.h, C.byref(kt), 1 if reset else 0), "agg_kernel_times")
@@ -871,6 +896,16 @@ class Comm:
             self.lib.check(self.lib.comm_alltoall_v(self.h, sp, sc, so, recv.data_ptr(), recv.shape[0], rc, row_words),
                            "comm_alltoall_v")
         return recv, list(rc)
+
+    def allgather_ranges(self, ranges):
+        """Every rank's list of (lo, hi) int64 pairs, concatenated in rank order: the all-to-all
+        with this rank's list sent to every peer from one region (send offsets all 0)."""
+        import torch
+        m = len(ranges)
+        send = torch.tensor([list(r) for r in ranges] if m else [[0, 0]], dtype=torch.int64,
+                            device=torch.device("cuda", self.device))
+        recv, rc = self.alltoall(send, [m] * self.nranks, 2, send_offsets=[0] * self.nranks)
+        return [tuple(r) for r in recv[:sum(rc)].cpu().tolist()]
 
     def allgather_i64(self, x):
         """One int64 from every rank (the count exchange with x sent to every peer)."""

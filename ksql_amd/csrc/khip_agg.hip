@@ -1187,7 +1187,7 @@ int64_t visible_from(const khip_agg* a) {
 // EMIT FINAL: the window starts this batch closes after they expired (k_emit_lost), computed from
 // the batch alone before the engine runs; collected by finish_lost() after the push's sync.
 khip_status emit_final_lost(khip_agg* a, const int64_t* ts, const uint8_t* kv, const uint8_t* rv, int64_t n,
-                            int64_t, const int64_t*) {
+                            int64_t seed_st, const int64_t*) {
   const int64_t nb = ceil_div(n, RPB);
   KHIP_TRY(a->blockmax.ensure(nb * 8));
   KHIP_TRY(a->blockprefix.ensure(nb * 8 + 8));
@@ -1199,7 +1199,7 @@ khip_status emit_final_lost(khip_agg* a, const int64_t* ts, const uint8_t* kv, c
   int64_t* seed = a->blockprefix.as<int64_t>() + nb;  // stream time before the batch
   KHIP_TRY(a->part.pinfo.ensure(512));
   int64_t* hs = a->part.pinfo.as<int64_t>() + 24;
-  hs[0] = a->st_before;
+  hs[0] = seed_st;  // the stream time before the batch
   KHIP_TRY_HIP(hipMemcpyAsync(seed, hs, 8, hipMemcpyHostToDevice, a->stream));
   KHIP_TRY_HIP(hipMemsetAsync(a->lostctr.p, 0, 8, a->stream));
   hipLaunchKernelGGL(k_blockmax, dim3(nb), dim3(BLOCK), 0, a->stream, ts, kv, rv, n, a->blockmax.as<int64_t>(),
@@ -1215,14 +1215,15 @@ khip_status emit_final_lost(khip_agg* a, const int64_t* ts, const uint8_t* kv, c
 
 // After the push's sync: the lost ranges → host (sorted, merged); re-run with room if the
 // buffer overflowed (the batch is still valid: the caller owns it until the push returns).
-static khip_status finish_lost(khip_agg* a, const int64_t* ts, const uint8_t* kv, const uint8_t* rv, int64_t n) {
+static khip_status finish_lost_seed(khip_agg* a, const int64_t* ts, const uint8_t* kv, const uint8_t* rv, int64_t n,
+                                   int64_t seed_st) {
   int64_t cnt = 0;
   KHIP_TRY_HIP(hipMemcpy(&cnt, a->lostctr.p, 8, hipMemcpyDeviceToHost));
   if (cnt > a->lost_cap) {
     a->lost_cap = next_pow2(cnt);
     a->lostbuf.release();
     KHIP_TRY(a->lostbuf.ensure((size_t)a->lost_cap * 16));
-    KHIP_TRY(emit_final_lost(a, ts, kv, rv, n, 0, nullptr));
+    KHIP_TRY(emit_final_lost(a, ts, kv, rv, n, seed_st, nullptr));
     KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
     KHIP_TRY_HIP(hipMemcpy(&cnt, a->lostctr.p, 8, hipMemcpyDeviceToHost));
   }
@@ -1239,6 +1240,25 @@ static khip_status finish_lost(khip_agg* a, const int64_t* ts, const uint8_t* kv
     }
   }
   return KHIP_OK;
+}
+
+static khip_status finish_lost(khip_agg* a, const int64_t* ts, const uint8_t* kv, const uint8_t* rv, int64_t n) {
+  return finish_lost_seed(a, ts, kv, rv, n, a->st_before);
+}
+
+// Sorted [lo, hi] pairs, overlapping or adjacent ones merged.
+static std::vector<int64_t> merge_ranges(std::vector<std::pair<int64_t, int64_t>> r) {
+  std::sort(r.begin(), r.end());
+  std::vector<int64_t> out;
+  for (auto& x : r) {
+    if (!out.empty() && x.first <= out.back() + 1) {
+      out.back() = std::max(out.back(), x.second);
+    } else {
+      out.push_back(x.first);
+      out.push_back(x.second);
+    }
+  }
+  return out;
 }
 
 }  // namespace khip
@@ -1297,8 +1317,6 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
   if (d.time_domain != KHIP_TIME_TASK) {
     if (d.window_kind == KHIP_WINDOW_SESSION) return fail(KHIP_E_UNSUPPORTED, "stream-time domains on SESSION windows");
     if (d.flags & KHIP_FLAG_TABLE_SOURCE) return fail(KHIP_E_UNSUPPORTED, "stream-time domains of a table source");
-    if (d.emit == KHIP_EMIT_FINAL && d.time_domain == KHIP_TIME_SUPPLIED)
-      return fail(KHIP_E_UNSUPPORTED, "EMIT FINAL with a supplied stream time");
     if (d.time_domain == KHIP_TIME_PARTITION && (d.n_partitions < 1 || d.n_partitions > 65536))
       return fail(KHIP_E_INVALID, "n_partitions must be in [1, 65536]");
   }
@@ -1449,6 +1467,20 @@ static khip_status resolve_batch(khip_agg* a, const khip_batch* b, const int64_t
   *kbytes_o = kbytes;
   *cols_o = cols;
   *key_bytes_total_o = key_bytes_total;
+  return KHIP_OK;
+}
+
+// KHIP_TIME_SUPPLIED with a close context: the handle's stream time becomes the GLOBAL one after the
+// batch (closing windows and retention as one task over the whole stream).
+static khip_status supplied_advance(khip_agg* a) {
+  if (a->sup_after > a->host_stream_time) {
+    a->host_stream_time = a->sup_after;
+    KHIP_TRY(a->part.pinfo.ensure(512));
+    int64_t* hs = a->part.pinfo.as<int64_t>() + 25;
+    hs[0] = a->sup_after;
+    KHIP_TRY_HIP(hipMemcpyAsync(a->stream_time.p, hs, 8, hipMemcpyHostToDevice, a->stream));
+    KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  }
   return KHIP_OK;
 }
 
@@ -1647,12 +1679,25 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   DeviceGuard g(a->device);
   khip_batch_stats s{};
   s.rows_in = n;
-  a->st_before = a->host_stream_time;
+  const bool supd = a->desc.time_domain == KHIP_TIME_SUPPLIED;
+  if (supd && a->desc.emit == KHIP_EMIT_FINAL && !a->sup_set)
+    return fail(KHIP_E_INVALID, "KHIP_TIME_SUPPLIED + EMIT FINAL: khip_agg_supplied_close before every push");
+  const bool sctx = supd && a->sup_set;
+  a->sup_set = false;
+  a->st_before = sctx ? a->sup_before : a->host_stream_time;
   a->chg_ready = false;
   a->lost.clear();
-  if (n == 0) {  // nothing changes, nothing closes
+  if (n == 0 && !sctx) {  // nothing changes, nothing closes
     a->chg_ready = true;
     a->chg_n = 0;
+    s.stream_time = a->host_stream_time;
+    if (stats) *stats = s;
+    return KHIP_OK;
+  }
+  if (n == 0) {  // SUPPLIED: nothing arrived here, but the GLOBAL stream time may close windows
+    KHIP_TRY(supplied_advance(a));
+    if (a->desc.emit == KHIP_EMIT_FINAL) a->lost = a->sup_lost;
+    else a->chg_ready = true, a->chg_n = 0;
     s.stream_time = a->host_stream_time;
     if (stats) *stats = s;
     return KHIP_OK;
@@ -1670,7 +1715,7 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   KHIP_TRY(resolve_batch(a, b, &keys, &ts, &kv, &rv, &koff, &kbytes, &cols, &key_bytes_total));
   const bool pdomain = a->desc.time_domain == KHIP_TIME_PARTITION;
   // (SESSION windows close sessions themselves: sess_push)
-  if (final_emit && !pdomain && a->engine != 2) KHIP_TRY(emit_final_lost(a, ts, kv, rv, n, 0, nullptr));
+  if (final_emit && !pdomain && !sctx && a->engine != 2) KHIP_TRY(emit_final_lost(a, ts, kv, rv, n, a->st_before, nullptr));
   // ---- ABI 5 stream-time domains: the stream time observed at every row
   const int64_t* st_at = nullptr;
   const int32_t* part = nullptr;
@@ -1812,7 +1857,9 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   }
   // one task per partition: the handle's stream time (closing windows, retention) is the slowest's
   if (pdomain) KHIP_TRY(stream_time_partition_min(a));
-  if (final_emit && a->engine != 2) KHIP_TRY(pdomain ? partition_lost_finish(a) : finish_lost(a, ts, kv, rv, n));
+  if (sctx) KHIP_TRY(supplied_advance(a));  // one task over the whole stream: the GLOBAL stream time
+  if (final_emit && sctx) a->lost = a->sup_lost;
+  else if (final_emit && a->engine != 2) KHIP_TRY(pdomain ? partition_lost_finish(a) : finish_lost(a, ts, kv, rv, n));
   if (a->engine == 0 && a->windowed) {  // retention: drop expired windows from the closed store
     HavingDev vis{};
     vis.vis = 1;
@@ -1861,6 +1908,60 @@ khip_status khip_stream_time_scan(khip_agg* a, const khip_batch* b, int64_t seed
   if (b->mem == KHIP_MEM_HOST) KHIP_TRY_HIP(hipMemcpyAsync(out, dst, (size_t)n * 8, hipMemcpyDeviceToHost, a->stream));
   KHIP_TRY_HIP(hipMemcpyAsync(out_max, last, 8, hipMemcpyDeviceToHost, a->stream));
   KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  return KHIP_OK;
+}
+
+khip_status khip_agg_lost_windows(khip_agg* a, const khip_batch* b, int64_t seed, int64_t* ranges, int64_t capacity,
+                                  int64_t* n_ranges) {
+  clear_error();
+  if (!a || !b || !n_ranges || (b->n_rows > 0 && !b->ts)) return fail(KHIP_E_INVALID, "null argument");
+  if (b->n_rows < 0) return fail(KHIP_E_INVALID, "batch shape");
+  if (!a->windowed || a->engine == 2 || a->desc.emit != KHIP_EMIT_FINAL)
+    return fail(KHIP_E_INVALID, "lost windows: an EMIT FINAL TUMBLING / HOPPING aggregation");
+  DeviceGuard g(a->device);
+  const int64_t n = b->n_rows;
+  *n_ranges = 0;
+  if (n == 0) return KHIP_OK;
+  const int64_t* ts = b->ts;
+  const uint8_t *kv = b->key_valid, *rv = b->row_valid;
+  const size_t bm = (size_t)(n + 7) / 8;
+  if (b->mem == KHIP_MEM_HOST) {
+    KHIP_TRY(stage(a, a->st_ts, b->ts, n * 8));
+    ts = a->st_ts.as<int64_t>();
+    if (kv) { KHIP_TRY(stage(a, a->st_kv, kv, bm)); kv = a->st_kv.as<uint8_t>(); }
+    if (rv) { KHIP_TRY(stage(a, a->st_rv, rv, bm)); rv = a->st_rv.as<uint8_t>(); }
+  } else if (b->mem != KHIP_MEM_DEVICE) {
+    return fail(KHIP_E_INVALID, "batch mem");
+  }
+  const int64_t sd = seed < -1 ? -1 : seed;
+  KHIP_TRY(emit_final_lost(a, ts, kv, rv, n, sd, nullptr));
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
+  const std::vector<int64_t> keep = a->lost;  // (the handle's own last push)
+  KHIP_TRY(finish_lost_seed(a, ts, kv, rv, n, sd));
+  std::vector<int64_t> got;
+  got.swap(a->lost);
+  a->lost = keep;
+  *n_ranges = (int64_t)got.size() / 2;
+  if (*n_ranges > capacity || (*n_ranges > 0 && !ranges)) return fail(KHIP_E_BUFFER, "ranges capacity");
+  std::copy(got.begin(), got.end(), ranges);
+  return KHIP_OK;
+}
+
+khip_status khip_agg_supplied_close(khip_agg* a, int64_t st_before, int64_t st_after, const int64_t* ranges,
+                                    int64_t n_ranges) {
+  clear_error();
+  if (!a || n_ranges < 0 || (n_ranges > 0 && !ranges)) return fail(KHIP_E_INVALID, "null argument");
+  if (a->desc.time_domain != KHIP_TIME_SUPPLIED) return fail(KHIP_E_INVALID, "handle not KHIP_TIME_SUPPLIED");
+  if (st_after < st_before) return fail(KHIP_E_INVALID, "stream time after the batch below the one before");
+  std::vector<std::pair<int64_t, int64_t>> r((size_t)n_ranges);
+  for (int64_t k = 0; k < n_ranges; k++) {
+    if (ranges[2 * k] > ranges[2 * k + 1]) return fail(KHIP_E_INVALID, "lost range with lo > hi");
+    r[k] = {ranges[2 * k], ranges[2 * k + 1]};
+  }
+  a->sup_lost = merge_ranges(std::move(r));
+  a->sup_before = st_before < -1 ? -1 : st_before;
+  a->sup_after = st_after < -1 ? -1 : st_after;
+  a->sup_set = true;
   return KHIP_OK;
 }
 

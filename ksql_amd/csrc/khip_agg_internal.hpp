@@ -532,6 +532,11 @@ struct khip_agg {
   DevBuf lostbuf, lostctr;   // EMIT FINAL: expired-at-close ws ranges found by the last push
   int64_t lost_cap = 0;
   std::vector<int64_t> lost; // sorted [lo, hi] pairs of the last push
+  // KHIP_TIME_SUPPLIED (khip_agg_supplied_close, ABI 8): the GLOBAL stream time around the next
+  // push and the union of the ranks' lost ranges, consumed by that push
+  bool sup_set = false;
+  int64_t sup_before = -1, sup_after = -1;
+  std::vector<int64_t> sup_lost;
   bool chg_ready = false;    // changes of the last push computed (rows / tombstones below)
   std::vector<uint64_t> chg_rows;
   std::vector<uint8_t> chg_tomb;

@@ -73,6 +73,12 @@ class GlooExchange:
         self.dist.all_gather_into_tensor(out, torch.tensor([int(x)], dtype=torch.int64), group=self.group)
         return [int(v) for v in out.tolist()]
 
+    def allgather_ranges(self, ranges):
+        """Every rank's list of (lo, hi) pairs, concatenated in rank order."""
+        out = [None] * self.nranks
+        self.dist.all_gather_object(out, list(ranges), group=self.group)
+        return [tuple(r) for rs in out for r in rs]
+
 
 class _StreamTimeBatch:
     """The caller's device batch with a stream_time column attached (a copy of its struct)."""
@@ -129,8 +135,22 @@ class Repartition:
         maxima = self.comm.allgather_i64(mx) if self.world > 1 else [mx]
         seed = max([self.gst] + maxima[:self.rank])
         self.shuffle.stream_time_seed(seed)
+        before = self.gst
         self.gst = max([self.gst] + maxima)
+        self._ctx = (seed, before, self.gst)
         return out[:n]
+
+    def final_context(self, agg, batch):
+        """global_time + EMIT FINAL (ABI 8): the owner closes windows by the GLOBAL stream time, as
+        one task over the whole stream (StreamAggregateBuilder.java:282-285).  After exchange():
+        this rank's chunk's lost windows (khip_agg_lost_windows: closed after they expired, by the
+        stream-time jumps of the chunk from its seed) are gathered from every rank, and the owner
+        gets them with the global stream time before / after the batch (khip_agg_supplied_close).
+        Collective: every rank calls it once per batch."""
+        seed, before, after = self._ctx
+        mine = agg.lost_windows(_RekeyedView(batch, self.shuffle.desc.key_col), seed)
+        every = self.comm.allgather_ranges(mine) if self.world > 1 else mine
+        agg.supplied_close(before, after, every)
 
     def exchange(self, batch, scan=None):
         """Device batch (source partition) → (this task's received rows [n, row_words], n).
@@ -161,6 +181,8 @@ class Repartition:
         (khip_agg_push_shuffled); returns its batch statistics.  global_time: `agg` is the
         KHIP_TIME_SUPPLIED owner task and also scans this rank's chunk."""
         recv, n = self.exchange(batch, scan=agg if self.global_time else None)
+        if self.global_time and agg.desc.emit == abi.EMIT["FINAL"]:
+            self.final_context(agg, batch)
         return agg.push_shuffled(self.shuffle, recv, n)
 
     def __call__(self, batch, scan=None):
