@@ -842,8 +842,8 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
   KLDS int32_t* lcs = (KLDS int32_t*)(lbb + (1 << (q.log2P - q.fbits)) + 1);  // [B + 1] chunk starts
   KLDS uint16_t* segof = (KLDS uint16_t*)(lcs + (1 << (q.log2P - q.fbits)) + 2);  // [C1_SEGOF] block → segment
   __shared__ int lovf, nnew;
-  __shared__ int wsum[NW];
-  __shared__ unsigned long long lbase;
+  __shared__ int wsum[NW], csum[NW];
+  __shared__ unsigned long long lbase, cbase;
   const int F = 1 << q.fbits;
   const int64_t wbase = ci_ld(ci, CI_WBASE), whi = ci_ld(ci, CI_WHI), T0 = ci_ld(ci, CI_T0), tmin = ci_ld(ci, CI_TMIN);
   const int wbits = (int)ci_ld(ci, CI_WBITS);
@@ -1058,47 +1058,8 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       continue;
     }
     const uint64_t* src = (isel ? buf1 : buf0) + (uint64_t)p * q.cmax * q.sw;
-    // 0b. closed resident rows → closed store (pass 0 only; retries skip them)
-    if (evict && first && nrow > 0) {  // (no resident rows: nothing to evict, no barriers)
-      int ne = 0, nh = 0;
-      for (int64_t r = threadIdx.x; r < nrow; r += NT) {
-        const uint64_t* row = src + r * q.sw;
-        ID id;
-        uint32_t h;
-        row_id(row, &id, &h);
-        ne += ((int64_t)row[1] + q.size <= close0) && (sbits == 0 || (int)c1_sub(h, sbits) == sub);
-      }
-      int incl = ne;
-      for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
-      }
-      if (lane == 63) wsum[wave] = incl;
-      lds_barrier();
-      int before = 0, total = 0;
-      for (int k = 0; k < NW; k++) {
-        if (k < wave) before += wsum[k];
-        total += wsum[k];
-      }
-      if (threadIdx.x == 0) lbase = total ? atomicAdd(closed_n, (unsigned long long)total) : 0ULL;
-      lds_barrier();
-      uint64_t* dst = closed + (lbase + (uint64_t)(before + incl - ne)) * q.sw;
-      for (int64_t r = threadIdx.x; r < nrow; r += NT) {
-        const uint64_t* row = src + r * q.sw;
-        ID id;
-        uint32_t h;
-        row_id(row, &id, &h);
-        if (!((int64_t)row[1] + q.size <= close0) || !(sbits == 0 || (int)c1_sub(h, sbits) == sub)) continue;
-        for (int k = 0; k < q.sw; k++) dst[k] = row[k];
-        dst += q.sw;
-        nh += q.hv_active && c1q_having(q, row[3]) ? 1 : 0;
-      }
-      if (q.hv_active) {
-        nh = (int)wave_sum(nh);
-        if (lane == 0 && nh) atomicAdd(hclosed, (unsigned long long)nh);
-      }
-      lds_barrier();
-    }
+    // (closed resident rows leave for the closed store in the write-out, phase 4: one pass over the
+    // resident rows there, the closed store's slots reserved with the region's)
     C1M_T(0);
     // 1. records → delta entries, two register sets (chunk c + 1 in flight while c is applied;
     //    chunk 0 was loaded with the item's segments)
@@ -1211,15 +1172,18 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       lds_barrier();
       continue;
     }
-    // 2. resident rows: mark the delta entries they absorb; count live rows
-    int n_mine = 0;
+    // 2. resident rows: mark the delta entries they absorb; count live and closed rows
+    int n_mine = 0, n_cl = 0;
     for (int64_t r = threadIdx.x; r < nrow; r += NT) {
       const uint64_t* row = src + r * q.sw;
-      if (evict && (int64_t)row[1] + q.size <= close0) continue;
       ID id;
       uint32_t h;
       const bool has = row_id(row, &id, &h);
       if (sbits && (int)c1_sub(h, sbits) != sub) continue;
+      if (evict && (int64_t)row[1] + q.size <= close0) {
+        n_cl++;
+        continue;
+      }
       if (has) {
         const int e = c1_find_id<ID>(ids, id, h >> (32 - log2H), H);
         if (e >= 0) rt[e] |= RT_MATCHED;  // one resident row per identity: a plain store
@@ -1237,14 +1201,20 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
       const bool isnew = i < lb1 && !(rt[e] & RT_MATCHED);
       nnw += (int)__popcll(__ballot(isnew));
     }
-    // 3. per-wave row counts → the partition's region range (one atomic per work item)
+    // 3. per-wave row counts → the partition's region range (one atomic per work item), and the
+    //    closed store's slots for its closed rows
     const int wave_rows = (int)wave_sum(n_mine) + nnw;
-    if (lane == 0) wsum[wave] = wave_rows;
+    const int wave_cl = (int)wave_sum(n_cl);
+    if (lane == 0) {
+      wsum[wave] = wave_rows;
+      csum[wave] = wave_cl;
+    }
     lds_barrier();
-    int wave_before = 0, total = 0;
+    int wave_before = 0, total = 0, cl_before = 0, cl_total = 0;
     for (int k = 0; k < NW; k++) {
-      if (k < wave) wave_before += wsum[k];
+      if (k < wave) wave_before += wsum[k], cl_before += csum[k];
       total += wsum[k];
+      cl_total += csum[k];
     }
     if (threadIdx.x == 0) {
       if (work) lbase = total ? atomicAdd(&newcnt[p], (unsigned long long)total) : 0ULL;
@@ -1252,6 +1222,8 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
         lbase = 0;
         newcnt[p] = (unsigned long long)total;
       }
+      // (an item that does not fit its region is retried and reserves nothing here)
+      cbase = cl_total && (int64_t)(lbase + total) <= q.cmax ? atomicAdd(closed_n, (unsigned long long)cl_total) : 0ULL;
     }
     lds_barrier();
     if ((int64_t)(lbase + total) > q.cmax) {
@@ -1274,20 +1246,30 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     // 4. write: resident rows (merged), then the wave's new entries (ballot ranks: consecutive rows)
     uint64_t* dst0 = (isel ? buf0 : buf1) + (uint64_t)p * q.cmax * q.sw;
     uint64_t cur = lbase + (uint64_t)wave_before;
+    uint64_t ccur = cbase + (uint64_t)cl_before;
     const uint64_t lt = (1ULL << lane) - 1;
-    int nh = 0;
+    int nh = 0, nhc = 0;
     for (int64_t r0 = wave * 64; r0 < nrow; r0 += NT) {
       const int64_t r = r0 + lane;
       const uint64_t* row = src + (r < nrow ? r : 0) * q.sw;
-      bool live = r < nrow && !(evict && (int64_t)row[1] + q.size <= close0);
+      bool live = r < nrow, cl = false;
       int e = -1;
       if (live) {
         ID id;
         uint32_t h;
         const bool has = row_id(row, &id, &h);
         if (sbits) live = (int)c1_sub(h, sbits) == sub;
+        cl = live && evict && (int64_t)row[1] + q.size <= close0;
+        live = live && !cl;
         if (live && has) e = c1_find_id<ID>(ids, id, h >> (32 - log2H), H);
       }
+      const uint64_t bc = __ballot(cl);
+      if (cl) {
+        uint64_t* cd = closed + (ccur + __popcll(bc & lt)) * q.sw;
+        for (int k = 0; k < q.sw; k++) cd[k] = row[k];
+        nhc += q.hv_active && c1q_having(q, row[3]) ? 1 : 0;
+      }
+      ccur += __popcll(bc);
       const uint64_t bl = __ballot(live);
       if (live) {
         const uint64_t ri = cur + __popcll(bl & lt);
@@ -1349,7 +1331,9 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     }
     if (q.hv_active) {
       nh = (int)wave_sum(nh);
+      nhc = (int)wave_sum(nhc);
       if (lane == 0 && nh) atomicAdd(&hnew[p], (unsigned long long)nh);
+      if (lane == 0 && nhc) atomicAdd(hclosed, (unsigned long long)nhc);
     }
     lds_barrier();  // the table is clear for the next item
     C1M_T(4);
@@ -1846,8 +1830,8 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
   // the bucket tables (chunk starts, bucket bases) are read from memory per item (their 3 KB of
   // LDS let a 2^12-entry table of 32-bit identities fit two workgroups per CU)
   __shared__ int lovf, nnew;
-  __shared__ int wsum[NW];
-  __shared__ unsigned long long lbase;
+  __shared__ int wsum[NW], csum[NW];
+  __shared__ unsigned long long lbase, cbase;
   const int F = 1 << q.fbits;
   const int64_t wbase = ci_ld(ci, CI_WBASE), whi = ci_ld(ci, CI_WHI), T0 = ci_ld(ci, CI_T0), tmin = ci_ld(ci, CI_TMIN);
   const int wbits = (int)ci_ld(ci, CI_WBITS);
@@ -2065,44 +2049,8 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       continue;
     }
     const uint64_t* src = (isel ? buf1 : buf0) + (uint64_t)p * q.cmax * q.sw;
-    // 0. closed resident rows → closed store (pass 0 only)
-    if (evict && first && nrow > 0) {  // (no resident rows: nothing to evict, no barriers)
-      int ne = 0, nh = 0;
-      for (int64_t r = threadIdx.x; r < nrow; r += NT) {
-        const uint64_t* row = src + r * q.sw;
-        ne += ((int64_t)row[1] + q.size <= close0) && (sbits == 0 || (int)c1_sub(subh((int64_t)row[0]), sbits) == sub);
-      }
-      int incl = ne;
-      for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
-      }
-      if (lane == 63) wsum[wave] = incl;
-      lds_barrier();
-      int before = 0, total = 0;
-      for (int k = 0; k < NW; k++) {
-        if (k < wave) before += wsum[k];
-        total += wsum[k];
-      }
-      if (threadIdx.x == 0) lbase = total ? atomicAdd(closed_n, (unsigned long long)total) : 0ULL;
-      lds_barrier();
-      uint64_t* dst = closed + (lbase + (uint64_t)(before + incl - ne)) * q.sw;
-      for (int64_t r = threadIdx.x; r < nrow; r += NT) {
-        const uint64_t* row = src + r * q.sw;
-        if (!((int64_t)row[1] + q.size <= close0) || !(sbits == 0 || (int)c1_sub(subh((int64_t)row[0]), sbits) == sub))
-          continue;
-        for (int k = 0; k < q.sw; k++) dst[k] = row[k];
-        dst += q.sw;
-        // (the query's HAVING alone: the merge's copy never carries pull / retention / FINAL bounds)
-        nh += having_ok_words(q.having.a.w_val >= 0 ? row[q.having.a.w_val] : 0,
-                              q.having.a.w_cnt >= 0 ? row[q.having.a.w_cnt] : 0, q.having) ? 1 : 0;
-      }
-      if (q.having.active) {
-        nh = (int)wave_sum(nh);
-        if (lane == 0 && nh) atomicAdd(hclosed, (unsigned long long)nh);
-      }
-      lds_barrier();
-    }
+    // (closed resident rows leave for the closed store in the write-out, phase 4: one pass over the
+    // resident rows there, the closed store's slots reserved with the region's)
     C1M_T(0);
     // 1. records → their pane (window) entries: the AU identities' CASes back to back, then the
     //    collisions probe on together (as k_c1_merge)
@@ -2261,12 +2209,15 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       lds_barrier();
       continue;
     }
-    // 2. resident rows: mark the delta entries they absorb; count live rows
-    int n_mine = 0;
+    // 2. resident rows: mark the delta entries they absorb; count live and closed rows
+    int n_mine = 0, n_cl = 0;
     for (int64_t r = threadIdx.x; r < nrow; r += NT) {
       const uint64_t* row = src + r * q.sw;
-      if (evict && (int64_t)row[1] + q.size <= close0) continue;
       if (sbits && (int)c1_sub(subh((int64_t)row[0]), sbits) != sub) continue;
+      if (evict && (int64_t)row[1] + q.size <= close0) {
+        n_cl++;
+        continue;
+      }
       ID id;
       uint32_t h;
       const bool has = row_id(row, &id, &h);
@@ -2286,14 +2237,19 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       const bool isnew = i < lb1 && !(rt[e] & RT_MATCHED) && !c1v_is_pane<ID, PANES>(ids[e], wbits);
       nnw += (int)__popcll(__ballot(isnew));
     }
-    // 3. the partition's region range
+    // 3. the partition's region range, and the closed store's slots for its closed rows
     const int wave_rows = (int)wave_sum(n_mine) + nnw;
-    if (lane == 0) wsum[wave] = wave_rows;
+    const int wave_cl = (int)wave_sum(n_cl);
+    if (lane == 0) {
+      wsum[wave] = wave_rows;
+      csum[wave] = wave_cl;
+    }
     lds_barrier();
-    int wave_before = 0, total = 0;
+    int wave_before = 0, total = 0, cl_before = 0, cl_total = 0;
     for (int k = 0; k < NW; k++) {
-      if (k < wave) wave_before += wsum[k];
+      if (k < wave) wave_before += wsum[k], cl_before += csum[k];
       total += wsum[k];
+      cl_total += csum[k];
     }
     if (threadIdx.x == 0) {
       if (work) lbase = total ? atomicAdd(&newcnt[p], (unsigned long long)total) : 0ULL;
@@ -2301,6 +2257,8 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
         lbase = 0;
         newcnt[p] = (unsigned long long)total;
       }
+      // (an item that does not fit its region is retried and reserves nothing here)
+      cbase = cl_total && (int64_t)(lbase + total) <= q.cmax ? atomicAdd(closed_n, (unsigned long long)cl_total) : 0ULL;
     }
     lds_barrier();
     if ((int64_t)(lbase + total) > q.cmax) {
@@ -2319,22 +2277,33 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       continue;
     }
     C1M_T(3);
-    // 4. write: resident rows (merged), then the wave's new window entries
+    // 4. write: resident rows (merged; closed ones to the closed store), then the wave's new window
+    //    entries
     uint64_t* dst0 = (isel ? buf0 : buf1) + (uint64_t)p * q.cmax * q.sw;
     uint64_t cur = lbase + (uint64_t)wave_before;
+    uint64_t ccur = cbase + (uint64_t)cl_before;
     const uint64_t lt = (1ULL << lane) - 1;
-    int nh = 0;
+    int nh = 0, nhc = 0;
     for (int64_t r0 = wave * 64; r0 < nrow; r0 += NT) {
       const int64_t r = r0 + lane;
       const uint64_t* row = src + (r < nrow ? r : 0) * q.sw;
-      bool live = r < nrow && !(evict && (int64_t)row[1] + q.size <= close0);
+      const bool mine = r < nrow && (!sbits || (int)c1_sub(subh((int64_t)row[0]), sbits) == sub);
+      const bool cl = mine && evict && (int64_t)row[1] + q.size <= close0;
+      const bool live = mine && !cl;
       int e = -1;
       if (live) {
-        if (sbits) live = (int)c1_sub(subh((int64_t)row[0]), sbits) == sub;
         ID id;
         uint32_t h;
-        if (live && row_id(row, &id, &h)) e = c1_find_id<ID>(ids, id, h >> (32 - log2H), H);
+        if (row_id(row, &id, &h)) e = c1_find_id<ID>(ids, id, h >> (32 - log2H), H);
       }
+      const uint64_t bc = __ballot(cl);
+      if (cl) {  // (the query's HAVING alone: the merge's copy never carries pull / retention / FINAL bounds)
+        uint64_t* cd = closed + (ccur + __popcll(bc & lt)) * q.sw;
+        for (int k = 0; k < q.sw; k++) cd[k] = row[k];
+        nhc += having_ok_words(q.having.a.w_val >= 0 ? row[q.having.a.w_val] : 0,
+                               q.having.a.w_cnt >= 0 ? row[q.having.a.w_cnt] : 0, q.having) ? 1 : 0;
+      }
+      ccur += __popcll(bc);
       const uint64_t bl = __ballot(live);
       if (live) {
         const uint64_t ri = cur + __popcll(bl & lt);
@@ -2382,7 +2351,9 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
     }
     if (q.having.active) {
       nh = (int)wave_sum(nh);
+      nhc = (int)wave_sum(nhc);
       if (lane == 0 && nh) atomicAdd(&hnew[p], (unsigned long long)nh);
+      if (lane == 0 && nhc) atomicAdd(hclosed, (unsigned long long)nhc);
     }
     lds_barrier();
     C1M_T(4);
@@ -2852,7 +2823,10 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     s.having_total = (int64_t)(hc[11] + hc[12]);
   }
   const unsigned long long* st = s.pinfo.as<unsigned long long>() + 8;
-  const int64_t cn = (int64_t)st[3 + T_NPART];
+  // the closed store's rows after every pass (closed rows leave in the pass that writes their item)
+  unsigned long long cnu = 0;
+  KHIP_TRY_HIP(hipMemcpy(&cnu, s.closed_ctr.p, 8, hipMemcpyDeviceToHost));
+  const int64_t cn = (int64_t)cnu;
   added_total += cn - s.closed_n;  // evicted rows left the live regions but are still groups
   s.closed_n = cn;
   a->host_stream_time = (int64_t)st[4 + T_NPART];
