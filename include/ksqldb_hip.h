@@ -160,13 +160,19 @@ typedef struct khip_batch_stats {
  *   queries and row counts, or closes for EMIT FINAL, by its own partition's stream time.  Closed
  *   windows leave the live table by the smallest partition stream time, so every declared
  *   partition should receive records: an idle one holds that eviction back (memory and step
- *   time grow; results do not change).
+ *   time grow; results do not change).  The key → partition map keeps every key ever accepted
+ *   until khip_agg_reset (it does not shrink with retention: memory grows with the distinct
+ *   keys).  A batch rejected because a key arrived on a second partition leaves the partitions'
+ *   stream times as they were before it; its new keys stay recorded with the partitions it named.
  * SUPPLIED: one GLOBAL stream time over several handles (ranks): each row carries the stream
  *   time observed at it over the global arrival order (`stream_time` column), computed where the
  *   rows were read, before routing: rank r scans its contiguous arrival chunk with
  *   khip_stream_time_scan seeded with max(global stream time before the batch, the maxima of the
- *   chunks of ranks < r) — an all-gather of one int64 per rank.  The union of the ranks' tables
- *   then equals one task over the whole stream. */
+ *   chunks of ranks < r) — an all-gather of one int64 per rank (or scans once unseeded and lets
+ *   the pack apply the seed: khip_shuffle_stream_time_seed, ABI 8).  The rows that raise it are
+ *   those the GROUP BY keeps (non-null value, non-null GROUP BY columns, ts >= 0).  The union of
+ *   the ranks' tables then equals one task over the whole stream; EMIT FINAL closes windows by the
+ *   GLOBAL stream time through khip_agg_supplied_close (ABI 8). */
 #define KHIP_TIME_TASK 0
 #define KHIP_TIME_PARTITION 1
 #define KHIP_TIME_SUPPLIED 2

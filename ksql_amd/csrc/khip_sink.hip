@@ -5,7 +5,7 @@
 // Streams' windowed key suffix, the value in the value format or a null value for a tombstone —
 // and several GROUP BY columns become the serialized composite key the aggregate groups by.
 //
-// Two passes over tiles of 2048 rows, one thread per row and round: k_sink_measure runs the very
+// Two passes over tiles of 256 rows, one thread per row: k_sink_measure runs the very
 // encoder the write pass runs, with a counting writer, so a row's length and its bytes can never
 // disagree, and sums each tile's lengths; one block scans the tile sums; k_sink_write scans its
 // tile's lengths in the block, adds the tile's carry and writes each record at its offset, and
@@ -531,8 +531,9 @@ __device__ __forceinline__ bool value_is_null(const SinkParams& q, const RowsDev
   return q.value_format == KHIP_FMT_KAFKA && row_value_val(q, r, i, 0).null;
 }
 
-// Tiles of SK_TILE rows, one block of 256 threads, a row per thread (eight rows per thread, in
-// rounds, kept the write pass's row state live across rounds: 171 VGPRs).
+// Tiles of SK_TILE = 256 rows, one block of 256 threads, one row per thread (eight rows per
+// thread in rounds, measured earlier, kept the write pass's row state live across rounds: 171
+// VGPRs).
 constexpr int SK_TR = 1;
 // k_sink_write at 4 waves per SIMD (<= 128 VGPRs; the spills are in the DOUBLE printer): 782-802
 // us per 22M rows against 840 at 5 and 890 uncapped (138 VGPRs), profiles/r05/ab/sink_two_pass.txt
