@@ -1065,7 +1065,11 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
     //    chunk 0 was loaded with the item's segments)
     // R32: the push's record times relative to the first window's start fit 32 bits (a 32-bit
     // window division instead of the 64-bit one)
-    auto apply = [&](const uint64_t (&xr)[AU], const uint32_t (&txr)[AU], int64_t l0, auto R32) {
+    // The record set's next chunk is loaded into the same registers right after its identities'
+    // CASes are issued (prefetch): the chunk's segment lookups and the table-full flag then return
+    // with the CASes (LDS returns in order), not behind this chunk's plane atomics, and the loads
+    // have a whole chunk to land.  Returns false when the table is (about to be) full.
+    auto apply = [&](const uint64_t (&xr)[AU], const uint32_t (&txr)[AU], int64_t l0, auto R32, auto&& prefetch) -> bool {
       ID id[AU];
       uint32_t e[AU], tr[AU];
       bool pend[AU], claimed[AU];
@@ -1089,13 +1093,19 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
         e[u] = act ? h >> (32 - log2H) : dummy;
         tr[u] = (uint32_t)(t32 - tmin32) + 1u;
       }
+      ID old[AU];
 #pragma unroll
       for (int u = 0; u < AU; u++) {
-        ID old = EMPTY;
-        __hip_atomic_compare_exchange_strong(&ids[e[u]], &old, id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+        old[u] = EMPTY;
+        __hip_atomic_compare_exchange_strong(&ids[e[u]], &old[u], id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-        claimed[u] = id[u] != EMPTY && old == EMPTY;
-        pend[u] = old != EMPTY && old != id[u];
+      }
+      const int full = *(volatile KLDS int*)&lovf;
+      prefetch();
+#pragma unroll
+      for (int u = 0; u < AU; u++) {
+        claimed[u] = id[u] != EMPTY && old[u] == EMPTY;
+        pend[u] = old[u] != EMPTY && old[u] != id[u];
       }
       for (int probes = 1;; probes++) {  // collisions: every pending record probes on together
         bool anyp = false;
@@ -1120,11 +1130,12 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
           pend[u] = o2 != EMPTY && o2 != id[u];
         }
       }
+      int nnow;
       {
         bool cl[AU];
 #pragma unroll
         for (int u = 0; u < AU; u++) cl[u] = claimed[u] && id[u] != EMPTY;
-        mg_list_append_n<AU>(cl, e, list, &nnew);
+        nnow = mg_list_append_n<AU>(cl, e, list, &nnew);
       }
 #pragma unroll
       for (int u = 0; u < AU; u++) {
@@ -1132,19 +1143,18 @@ __global__ __launch_bounds__(NT, 4) void k_c1_merge(
         __hip_atomic_fetch_max(&rt[e[u]], tr[u], WG_RLX);
         __hip_atomic_fetch_add(&ct[e[u]], 1u, WG_RLX);
       }
+      return !full && nnow <= q.hmax;
     };
     const int64_t nch = (rn + (int64_t)AU * NT - 1) / ((int64_t)AU * NT);
-    if (rn > 0) {  // chunks 0 and 1 are in flight (load01); each set is reloaded once applied
+    if (rn > 0) {  // chunks 0 and 1 are in flight (load01); each set is reloaded as it is applied
       for (int64_t c = 0; c < nch; c += 2) {
-        if (r32) apply(ra, ta, c * AU * NT, std::true_type{});
-        else apply(ra, ta, c * AU * NT, std::false_type{});
-        if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
-        if (c + 2 < nch) load(ra, ta, (c + 2) * AU * NT, rn, nseg, segb);
-        if (c + 1 >= nch) break;
-        if (r32) apply(rb, tb, (c + 1) * AU * NT, std::true_type{});
-        else apply(rb, tb, (c + 1) * AU * NT, std::false_type{});
-        if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
-        if (c + 3 < nch) load(rb, tb, (c + 3) * AU * NT, rn, nseg, segb);
+        auto pa = [&] { if (c + 2 < nch) load(ra, ta, (c + 2) * AU * NT, rn, nseg, segb); };
+        const bool ga = r32 ? apply(ra, ta, c * AU * NT, std::true_type{}, pa) : apply(ra, ta, c * AU * NT, std::false_type{}, pa);
+        if (!ga || c + 1 >= nch) break;
+        auto pb = [&] { if (c + 3 < nch) load(rb, tb, (c + 3) * AU * NT, rn, nseg, segb); };
+        const bool gb = r32 ? apply(rb, tb, (c + 1) * AU * NT, std::true_type{}, pb)
+                            : apply(rb, tb, (c + 1) * AU * NT, std::false_type{}, pb);
+        if (!gb) break;
       }
     }
     lds_barrier();
@@ -2054,14 +2064,20 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
     C1M_T(0);
     // 1. records → their pane (window) entries: the AU identities' CASes back to back, then the
     //    collisions probe on together (as k_c1_merge)
-    auto apply = [&](const ulonglong2 (&xr)[AU], int64_t l0, auto R32) {
+    //    The set's next chunk is loaded into the same registers right after the CASes are issued
+    //    (prefetch; what the planes need is kept aside first), as k_c1_merge.
+    auto apply = [&](const ulonglong2 (&xr)[AU], int64_t l0, auto R32, auto&& prefetch) -> bool {
       ID id[AU];
-      uint32_t e[AU];
-      bool pend[AU], claimed[AU];
+      uint32_t e[AU], trv[AU];
+      uint64_t arg[AU];
+      bool pend[AU], claimed[AU], nn[AU];
 #pragma unroll
       for (int u = 0; u < AU; u++) {
         const int64_t li = l0 + threadIdx.x + (int64_t)u * NT;
         const uint64_t w0 = xr[u].x;
+        trv[u] = (uint32_t)((int32_t)(uint32_t)w0 - tmin32) + 1u;
+        nn[u] = (w0 >> 63) != 0;
+        arg[u] = xr[u].y;
         const uint64_t krel = (w0 >> 32) & 0x7FFFFFFFull;
         uint64_t wi;
         if constexpr (decltype(R32)::value) wi = fast_udiv32((uint32_t)w0 + tsh32, q.fd32);
@@ -2072,13 +2088,19 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
         id[u] = act ? x : EMPTY;
         e[u] = act ? c1_hash<ID>(x) >> (32 - log2H) : dummy;
       }
+      ID old[AU];
 #pragma unroll
       for (int u = 0; u < AU; u++) {
-        ID old = EMPTY;
-        __hip_atomic_compare_exchange_strong(&ids[e[u]], &old, id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+        old[u] = EMPTY;
+        __hip_atomic_compare_exchange_strong(&ids[e[u]], &old[u], id[u], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-        claimed[u] = id[u] != EMPTY && old == EMPTY;
-        pend[u] = old != EMPTY && old != id[u];
+      }
+      const int full = *(volatile KLDS int*)&lovf;
+      prefetch();
+#pragma unroll
+      for (int u = 0; u < AU; u++) {
+        claimed[u] = id[u] != EMPTY && old[u] == EMPTY;
+        pend[u] = old[u] != EMPTY && old[u] != id[u];
       }
       for (int probes = 1;; probes++) {
         bool anyp = false;
@@ -2103,25 +2125,25 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
           pend[u] = o2 != EMPTY && o2 != id[u];
         }
       }
+      int nnow;
       {
         bool cl[AU];
 #pragma unroll
         for (int u = 0; u < AU; u++) cl[u] = claimed[u] && id[u] != EMPTY;
-        mg_list_append_n<AU>(cl, e, list, &nnew);
+        nnow = mg_list_append_n<AU>(cl, e, list, &nnew);
       }
 #pragma unroll
       for (int u = 0; u < AU; u++) {
         if (id[u] == EMPTY) continue;
-        const uint64_t w0 = xr[u].x;
-        int64_t ok_ = (int64_t)xr[u].y;
+        int64_t ok_ = (int64_t)arg[u];
         if (C1VP<PM>{q}.f64() && (C1VP<PM>{q}.mn() || C1VP<PM>{q}.mx())) {
           double d;
-          __builtin_memcpy(&d, &xr[u].y, 8);
+          __builtin_memcpy(&d, &arg[u], 8);
           ok_ = f64_order_key(d);
         }
-        c1v_add<PM>(q, smem, e[u], (uint32_t)((int32_t)(uint32_t)w0 - tmin32) + 1u, 1u, (w0 >> 63) ? 1u : 0u, xr[u].y, ok_,
-                ok_);
+        c1v_add<PM>(q, smem, e[u], trv[u], 1u, nn[u] ? 1u : 0u, arg[u], ok_, ok_);
       }
+      return !full && nnow <= q.hmax;
     };
     const int64_t nch = (rn + (int64_t)AU * NT - 1) / ((int64_t)AU * NT);
     if (rn > 0 && PANES) {
@@ -2130,26 +2152,22 @@ __global__ __launch_bounds__(NT, WPE) void k_c1v_merge(
       // set counts the other set's loads as in flight; the table-full check once per two chunks
       auto records = [&](auto R32) {
         for (int64_t c = 0; c < nch; c += 2) {
-          apply(ra, c * AU * NT, R32);
-          load(ra, (c + 2) * AU * NT, rn, nseg, segb);
-          apply(rb, (c + 1) * AU * NT, R32);
-          load(rb, (c + 3) * AU * NT, rn, nseg, segb);
-          if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
+          const bool ga = apply(ra, c * AU * NT, R32, [&] { load(ra, (c + 2) * AU * NT, rn, nseg, segb); });
+          const bool gb = apply(rb, (c + 1) * AU * NT, R32, [&] { load(rb, (c + 3) * AU * NT, rn, nseg, segb); });
+          if (!ga || !gb) break;
         }
       };
       if (r32) records(std::true_type{});
       else records(std::false_type{});
     } else if (rn > 0) {
       for (int64_t c = 0; c < nch; c += 2) {
-        if (r32) apply(ra, c * AU * NT, std::true_type{});
-        else apply(ra, c * AU * NT, std::false_type{});
-        if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
-        if (c + 2 < nch) load(ra, (c + 2) * AU * NT, rn, nseg, segb);
-        if (c + 1 >= nch) break;
-        if (r32) apply(rb, (c + 1) * AU * NT, std::true_type{});
-        else apply(rb, (c + 1) * AU * NT, std::false_type{});
-        if (*(volatile KLDS int*)&lovf || *(volatile KLDS int*)&nnew > q.hmax) break;
-        if (c + 3 < nch) load(rb, (c + 3) * AU * NT, rn, nseg, segb);
+        auto pa = [&] { if (c + 2 < nch) load(ra, (c + 2) * AU * NT, rn, nseg, segb); };
+        const bool ga = r32 ? apply(ra, c * AU * NT, std::true_type{}, pa) : apply(ra, c * AU * NT, std::false_type{}, pa);
+        if (!ga || c + 1 >= nch) break;
+        auto pb = [&] { if (c + 3 < nch) load(rb, (c + 3) * AU * NT, rn, nseg, segb); };
+        const bool gb = r32 ? apply(rb, (c + 1) * AU * NT, std::true_type{}, pb)
+                            : apply(rb, (c + 1) * AU * NT, std::false_type{}, pb);
+        if (!gb) break;
       }
     }
     lds_barrier();

@@ -64,9 +64,10 @@ __device__ __forceinline__ void mg_list_append(bool claimed, uint32_t e, KLDS ui
 }
 
 // mg_list_append for AU entries per lane at once: one LDS atomic per wave for all of them.
+// Returns the list's length after this wave's entries (0 when the wave appended none).
 template <int AU>
-__device__ __forceinline__ void mg_list_append_n(const bool (&claimed)[AU], const uint32_t (&e)[AU], KLDS uint16_t* nl,
-                                                 int* nnew) {
+__device__ __forceinline__ int mg_list_append_n(const bool (&claimed)[AU], const uint32_t (&e)[AU], KLDS uint16_t* nl,
+                                                int* nnew) {
   uint64_t b[AU];
   int tot = 0;
 #pragma unroll
@@ -74,17 +75,18 @@ __device__ __forceinline__ void mg_list_append_n(const bool (&claimed)[AU], cons
     b[u] = __ballot(claimed[u]);
     tot += __popcll(b[u]);
   }
-  if (!tot) return;
+  if (!tot) return 0;
   const int lane = threadIdx.x & 63;
   int base = 0;
   if (lane == 0) base = atomicAdd(nnew, tot);
-  base = __shfl(base, 0, 64);
+  base = __builtin_amdgcn_readfirstlane(base);  // (convergent call: lane 0 is the first active lane)
   const uint64_t lt = (1ULL << lane) - 1;
 #pragma unroll
   for (int u = 0; u < AU; u++) {
     if (claimed[u]) nl[base + __popcll(b[u] & lt)] = (uint16_t)e[u];
     base += __popcll(b[u]);
   }
+  return base;
 }
 
 constexpr uint32_t C1_GOLD = 0x9E3779B1u;
