@@ -9,6 +9,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 __device__ __forceinline__ uint64_t mix(uint64_t x) {
@@ -60,11 +61,16 @@ static double run(const uint64_t* table, uint64_t slots, int64_t n, unsigned lon
   return (double)n * reps / (ms / 1000.0);
 }
 
-int main() {
+int main(int argc, char** argv) {
   const int64_t n = 200000000;
   unsigned long long* sink;
   hipMalloc(&sink, 8);
-  const uint64_t sizes[] = {256ULL << 20, 1ULL << 30, 4ULL << 30, 8ULL << 30};
+  // table sizes (MB) from the command line, default the MALL (256 MB) to C4's slot table
+  std::vector<uint64_t> sizes = {256ULL << 20, 1ULL << 30, 4ULL << 30, 8ULL << 30};
+  if (argc > 1) {
+    sizes.clear();
+    for (int a = 1; a < argc; a++) sizes.push_back((uint64_t)atoll(argv[a]) << 20);
+  }
   printf("table_bytes,word_bytes,loads_per_thread,loads_per_s\n");
   for (uint64_t bytes : sizes) {
     uint64_t* table = nullptr;
