@@ -27,9 +27,10 @@
 //
 // Dense probe index (one INT/BIGINT value column, keys in a range at most 4x the live key
 // count, e.g. C4's users 1..1e8): cell[key - kmin] of W = 1/2/4/8 bytes, bit 0 live, bit 1
-// NULL value, bits 2.. value - vmin.  C4 is 1e8 one-byte cells (100 MB): it stays in the
-// 256 MB MALL, so the probes' random reads are cache hits instead of random 64 B HBM lines
-// into the 8.6 GB slot table.  Built from the slot table on the first probe after it became
+// NULL value, bits 2.. value - vmin — or 2-bit cells when every value is one of three and none
+// is NULL (dense_store).  C4 is 1e8 2-bit cells (25 MB): it stays in the 256 MB MALL (and more
+// of it in the XCDs' L2s than the 100 MB of byte cells), so the probes' random reads are cache
+// hits instead of random 64 B HBM lines into the 8.6 GB slot table.  Built from the slot table on the first probe after it became
 // eligible and kept in step by the upserts' winning rows (a key or value outside the index's
 // ranges drops it; the next probe rebuilds it over the new ranges).
 //
@@ -145,10 +146,14 @@ __global__ __launch_bounds__(256) void k_upsert_finalize(uint64_t* __restrict__ 
   }
 }
 
+#ifndef KHIP_JOIN_QUARTER
+#define KHIP_JOIN_QUARTER 1  // 2-bit dense cells when they fit (A/B builds set 0)
+#endif
+
 // Dense probe index parameters (active = 0: none).
 struct JDense {
   int32_t active;
-  int32_t w;         // cell bytes: 1, 2, 4, 8
+  int32_t w;         // cell bytes: 1, 2, 4, 8; 0 = 2-bit cells (see dense_load)
   int64_t kmin, nkeys;  // cells for keys kmin .. kmin + nkeys - 1
   int64_t vmin;
   uint64_t vspan;    // values vmin .. vmin + vspan - 1 encodable
@@ -156,8 +161,20 @@ struct JDense {
   int* invalid;      // set when an upsert falls outside the ranges
 };
 
+// 2-bit cells (w = 0): 0 absent, 1 + (value - vmin) for values vmin .. vmin + 2, no NULL — C4's
+// three levels over 1e8 users are 25 MB instead of 100 MB, which random gathers read at 7.1e10/s
+// instead of 5.7e10/s (more of the index hits each XCD's L2; profiles/r06/random_gather_c4_index.csv).
+// Sixteen cells share a 32-bit word, so stores are word atomics (one writer per key, never per word).
 __device__ __forceinline__ void dense_store(const JDense& d, int64_t idx, uint64_t cell) {
   switch (d.w) {
+    case 0: {
+      unsigned int* wd = (unsigned int*)d.cells + (idx >> 4);
+      const int sh = 2 * (int)(idx & 15);
+      const unsigned int c2 = (cell & 1) ? (unsigned int)(cell >> 2) + 1u : 0u;
+      atomicAnd(wd, ~(3u << sh));
+      if (c2) atomicOr(wd, c2 << sh);
+      break;
+    }
     case 1: d.cells[idx] = (uint8_t)cell; break;
     case 2: ((uint16_t*)d.cells)[idx] = (uint16_t)cell; break;
     case 4: ((uint32_t*)d.cells)[idx] = (uint32_t)cell; break;
@@ -165,8 +182,13 @@ __device__ __forceinline__ void dense_store(const JDense& d, int64_t idx, uint64
   }
 }
 
+// The cell in the common format (bit 0 live, bit 1 NULL, bits 2.. value - vmin).
 __device__ __forceinline__ uint64_t dense_load(const JDense& d, int64_t idx) {
   switch (d.w) {
+    case 0: {
+      const uint64_t c2 = (d.cells[idx >> 2] >> (2 * (int)(idx & 3))) & 3;
+      return c2 ? (1 | ((c2 - 1) << 2)) : 0;
+    }
     case 1: return d.cells[idx];
     case 2: return ((const uint16_t*)d.cells)[idx];
     case 4: return ((const uint32_t*)d.cells)[idx];
@@ -178,7 +200,7 @@ __device__ __forceinline__ uint64_t dense_load(const JDense& d, int64_t idx) {
 __device__ __forceinline__ bool dense_cell(const JDense& d, uint64_t raw, bool isnull, uint64_t* cell) {
   if (isnull) {
     *cell = 3;
-    return true;
+    return d.w != 0;  // 2-bit cells hold no NULL
   }
   const uint64_t off = (uint64_t)((int64_t)raw - d.vmin);
   if ((int64_t)raw < d.vmin || off >= d.vspan) return false;
@@ -304,7 +326,7 @@ __global__ __launch_bounds__(256) void k_upsert_apply(uint64_t* __restrict__ tab
 // Ranges of the live slots: [kmin, kmax, vmin, vmax, live] (value over non-null values).
 __global__ __launch_bounds__(256) void k_table_ranges(const uint64_t* __restrict__ table, int64_t cap, int sw,
                                                       unsigned long long* __restrict__ out, int cmp) {
-  int64_t kmn = INT64_MAX, kmx = INT64_MIN, vmn = INT64_MAX, vmx = INT64_MIN, live = 0;
+  int64_t kmn = INT64_MAX, kmx = INT64_MIN, vmn = INT64_MAX, vmx = INT64_MIN, live = 0, nulls = 0;
   for (int64_t slot = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; slot < cap;
        slot += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t* s = table + slot * (uint64_t)sw;
@@ -318,6 +340,8 @@ __global__ __launch_bounds__(256) void k_table_ranges(const uint64_t* __restrict
       const int64_t v = (int64_t)slot_col(s, m, 0, cmp);
       vmn = v < vmn ? v : vmn;
       vmx = v > vmx ? v : vmx;
+    } else {
+      nulls++;
     }
   }
   for (int off = 32; off > 0; off >>= 1) {
@@ -328,6 +352,7 @@ __global__ __launch_bounds__(256) void k_table_ranges(const uint64_t* __restrict
     vmn = c < vmn ? c : vmn;
     vmx = d > vmx ? d : vmx;
     live += __shfl_xor(live, off, 64);
+    nulls += __shfl_xor(nulls, off, 64);
   }
   if ((threadIdx.x & 63) == 0 && live) {
     // order-preserving unsigned view of the signed ranges for the 64-bit atomics
@@ -337,6 +362,7 @@ __global__ __launch_bounds__(256) void k_table_ranges(const uint64_t* __restrict
     atomicMin(&out[2], (unsigned long long)((uint64_t)vmn ^ bias));
     atomicMax(&out[3], (unsigned long long)((uint64_t)vmx ^ bias));
     atomicAdd(&out[4], (unsigned long long)live);
+    if (nulls) atomicAdd(&out[5], (unsigned long long)nulls);
   }
 }
 
@@ -781,7 +807,7 @@ static khip_status prepare_dense(khip_table* t) {
   if (t->dense_eval_occ >= 0 && t->occ < 2 * t->dense_eval_occ) return KHIP_OK;
   t->dense_eval_occ = std::max<int64_t>(t->occ, 1);
   KHIP_TRY(t->drange.ensure(64));
-  unsigned long long init[5] = {~0ULL, 0ULL, ~0ULL, 0ULL, 0ULL}, r[5];
+  unsigned long long init[6] = {~0ULL, 0ULL, ~0ULL, 0ULL, 0ULL, 0ULL}, r[6];
   unsigned long long* out = t->drange.as<unsigned long long>();
   KHIP_TRY_HIP(hipMemcpyAsync(out, init, sizeof(init), hipMemcpyHostToDevice, t->stream));
   hipLaunchKernelGGL(k_table_ranges, dim3(jgrid(t->cap, 4096)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->cap,
@@ -802,12 +828,15 @@ static khip_status prepare_dense(khip_table* t) {
   int bits = 2;
   while (bits < 64 && ((unsigned __int128)1 << (bits - 2)) < vrange) bits++;
   if (((unsigned __int128)1 << (bits - 2)) < vrange) return KHIP_OK;
-  const int w = bits <= 8 ? 1 : (bits <= 16 ? 2 : (bits <= 32 ? 4 : 8));
+  // 2-bit cells when every live value is one of three and none is NULL (C4's levels)
+  const bool quarter = vrange <= 3 && r[5] == 0 && knob("KHIP_PROBE_QUARTER", KHIP_JOIN_QUARTER);
+  const int w = quarter ? 0 : (bits <= 8 ? 1 : (bits <= 16 ? 2 : (bits <= 32 ? 4 : 8)));
   // room for keys appended past the current maximum before the index must be rebuilt
   const int64_t nkeys = (int64_t)krange + (int64_t)krange / 8 + 1024;
-  KHIP_TRY(t->dcells.ensure((size_t)nkeys * w));
+  const size_t cbytes = quarter ? (size_t)((nkeys + 15) / 16) * 4 : (size_t)nkeys * w;
+  KHIP_TRY(t->dcells.ensure(cbytes));
   KHIP_TRY(t->dinvalid.ensure(8));
-  KHIP_TRY_HIP(hipMemsetAsync(t->dcells.p, 0, (size_t)nkeys * w, t->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(t->dcells.p, 0, cbytes, t->stream));
   KHIP_TRY_HIP(hipMemsetAsync(t->dinvalid.p, 0, 8, t->stream));
   JDense d{};
   d.active = 1;
@@ -815,7 +844,7 @@ static khip_status prepare_dense(khip_table* t) {
   d.kmin = kmin;
   d.nkeys = nkeys;
   d.vmin = vmin;
-  d.vspan = w == 8 ? (1ULL << 62) : (1ULL << (8 * w - 2));
+  d.vspan = w == 0 ? 3 : (w == 8 ? (1ULL << 62) : (1ULL << (8 * w - 2)));
   d.cells = t->dcells.as<uint8_t>();
   d.invalid = t->dinvalid.as<int>();
   hipLaunchKernelGGL(k_dense_build, dim3(jgrid(t->cap, 8192)), dim3(256), 0, t->stream, t->table.as<uint64_t>(), t->cap,

@@ -367,16 +367,18 @@ def test_join_random_vs_oracle(prod, orc, join_type, where):
             assert np.array_equal(a["cols"][c][~a["nulls"][c]], b["cols"][c][~b["nulls"][c]])
 
 
-@pytest.mark.parametrize("layout", ["dense", "spread"])
+@pytest.mark.parametrize("layout", ["dense", "quarter", "spread"])
 @pytest.mark.parametrize("ctype", ["INT32", "INT64"])
 def test_join_dense_index_vs_oracle(prod, orc, ctype, layout):
-    """One value column: the probe index (khip_join.hip) — dense keys: the dense cell index;
+    """One value column: the probe index (khip_join.hip) — dense keys: the dense cell index
+    ("quarter": three values and no NULL, so 2-bit cells, until a NULL value (step 5) moves it to
+    byte cells);
     keys spread far past 4x their count: the hashed index (8-byte words, one 16-byte read per
     probe) — is built on the first probe, kept in step by upserts (deletes, NULL values), dropped
     when a key or a value leaves its ranges and rebuilt by the next probe (or the slot table probed
     when no index fits) — host and device probe outputs equal the oracle's after every step."""
     torch = pytest.importorskip("torch")
-    rng = np.random.default_rng((31 if ctype == "INT32" else 32) + (layout == "spread"))
+    rng = np.random.default_rng((31 if ctype == "INT32" else 32) + (layout == "spread") + 7 * (layout == "quarter"))
     tables = [abi.TableHandle(lib, [ctype], capacity_hint=64) for lib in (prod, orc)]
     dt = np.int32 if ctype == "INT32" else np.int64
     spread = (lambda k: k * 1000003 + 7) if layout == "spread" else (lambda k: k)
@@ -385,11 +387,14 @@ def test_join_dense_index_vs_oracle(prod, orc, ctype, layout):
         keys = spread(rng.integers(0, 5000, m))
         vals = rng.integers(0, 3, m).astype(dt)
         if step == 4:
-            keys[0] = 10**9 if layout == "dense" else -(2**62)  # a key far outside the index range: index dropped, then rebuilt
+            keys[0] = 10**9 if layout != "spread" else -(2**62)  # a key far outside the index range: index dropped, then rebuilt
         if step == 6:
             vals[0] = dt(2**30) if ctype == "INT32" else dt(2**50)  # a value outside the cell width
         rv = rng.random(m) > 0.1
         cv = rng.random(m) > 0.05
+        if layout == "quarter":
+            cv = np.ones(m, bool)
+            cv[0] = step != 5
         for t in tables:
             t.upsert(abi.HostBatch(np.zeros(m, np.int64), keys=keys, row_valid=rv, cols=[vals], col_valid=[cv]))
         k = int(rng.integers(1000, 9000))

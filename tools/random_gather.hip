@@ -22,7 +22,7 @@ __device__ __forceinline__ uint64_t mix(uint64_t x) {
 }
 
 template <int W, int R>
-__global__ __launch_bounds__(256) void k_gather(const uint64_t* __restrict__ table, uint64_t mask, int64_t n,
+__global__ __launch_bounds__(256) void k_gather(const uint64_t* __restrict__ table, uint64_t slots, int64_t n,
                                                 uint64_t seed, unsigned long long* __restrict__ sink) {
   constexpr int WW = W / 8;
   const int64_t base = (int64_t)blockIdx.x * 256 * R;
@@ -31,7 +31,7 @@ __global__ __launch_bounds__(256) void k_gather(const uint64_t* __restrict__ tab
 #pragma unroll
   for (int r = 0; r < R; r++) {
     const int64_t i = base + r * 256 + threadIdx.x;
-    const uint64_t slot = mix(seed + (uint64_t)(i < n ? i : 0)) & mask;
+    const uint64_t slot = __umul64hi(mix(seed + (uint64_t)(i < n ? i : 0)), slots);  // uniform over any size
     const uint64_t* p = table + slot * WW;
 #pragma unroll
     for (int w = 0; w < WW; w++) v[r][w] = p[w];
@@ -49,11 +49,11 @@ static double run(const uint64_t* table, uint64_t slots, int64_t n, unsigned lon
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  hipLaunchKernelGGL((k_gather<W, R>), dim3(blocks), dim3(256), 0, 0, table, slots - 1, n, 1ULL, sink);
+  hipLaunchKernelGGL((k_gather<W, R>), dim3(blocks), dim3(256), 0, 0, table, slots, n, 1ULL, sink);
   hipEventRecord(e0, 0);
   const int reps = 3;
   for (int k = 0; k < reps; k++)
-    hipLaunchKernelGGL((k_gather<W, R>), dim3(blocks), dim3(256), 0, 0, table, slots - 1, n, 7ULL + k, sink);
+    hipLaunchKernelGGL((k_gather<W, R>), dim3(blocks), dim3(256), 0, 0, table, slots, n, 7ULL + k, sink);
   hipEventRecord(e1, 0);
   hipEventSynchronize(e1);
   float ms = 0;
