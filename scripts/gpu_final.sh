@@ -7,14 +7,14 @@
 # The first failure ends the script (tests: a crash or time limit; test failures are reported).
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-ITAG=${ITAG:-r05_final}
+ITAG=${ITAG:-r06_final}
 D=gpurun_out/$ITAG
 mkdir -p $D
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 ALL_LEGS="possible_fraud:--sparse-keys possible_fraud:--utf8 possible_fraud:--utf8:--card-format:alnum hourly_metrics hopping_double clickstream_join clickstream_join:--sparse-ids repartition_sum serde_json serde_avro sink_json table_agg table_agg:--sparse-ids session"
 case ${PART:?} in
 tests)
-  timeout -k 10 720 python -u -m pytest tests -m gpu -q --maxfail=20 --timeout 300 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q --maxfail=20 --timeout 300 --timeout-method thread \
     > $D/gpu_all.log 2>&1; rc=$?
   tail -5 $D/gpu_all.log
   [ $rc -gt 1 ] && exit $rc
