@@ -172,7 +172,10 @@ typedef struct khip_batch_stats {
  *   the pack apply the seed: khip_shuffle_stream_time_seed, ABI 8).  The rows that raise it are
  *   those the GROUP BY keeps (non-null value, non-null GROUP BY columns, ts >= 0).  The union of
  *   the ranks' tables then equals one task over the whole stream; EMIT FINAL closes windows by the
- *   GLOBAL stream time through khip_agg_supplied_close (ABI 8). */
+ *   GLOBAL stream time through khip_agg_supplied_close (ABI 8).
+ *   SESSION windows take SUPPLIED with EMIT CHANGES (round 6: a non-key GROUP BY with a SESSION
+ *   window through the repartition); PARTITION, and EMIT FINAL under SUPPLIED, return
+ *   KHIP_E_UNSUPPORTED for SESSION windows (the reference CPU builder keeps them). */
 #define KHIP_TIME_TASK 0
 #define KHIP_TIME_PARTITION 1
 #define KHIP_TIME_SUPPLIED 2

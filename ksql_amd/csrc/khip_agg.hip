@@ -1315,7 +1315,11 @@ khip_status khip_agg_create(const khip_agg_desc* desc, khip_agg** out) {
   }
   if (d.time_domain < KHIP_TIME_TASK || d.time_domain > KHIP_TIME_SUPPLIED) return fail(KHIP_E_INVALID, "time domain");
   if (d.time_domain != KHIP_TIME_TASK) {
-    if (d.window_kind == KHIP_WINDOW_SESSION) return fail(KHIP_E_UNSUPPORTED, "stream-time domains on SESSION windows");
+    // SESSION windows take the SUPPLIED (GLOBAL) stream time with EMIT CHANGES: the replay reads
+    // each row's given stream time.  EMIT FINAL needs the stream time BEFORE each row, which the
+    // shuffle does not carry; PARTITION needs per-task session expiry.
+    if (d.window_kind == KHIP_WINDOW_SESSION && (d.time_domain == KHIP_TIME_PARTITION || d.emit == KHIP_EMIT_FINAL))
+      return fail(KHIP_E_UNSUPPORTED, "SESSION windows: PARTITION stream time, or EMIT FINAL under SUPPLIED");
     if (d.flags & KHIP_FLAG_TABLE_SOURCE) return fail(KHIP_E_UNSUPPORTED, "stream-time domains of a table source");
     if (d.time_domain == KHIP_TIME_PARTITION && (d.n_partitions < 1 || d.n_partitions > 65536))
       return fail(KHIP_E_INVALID, "n_partitions must be in [1, 65536]");
@@ -1768,7 +1772,10 @@ khip_status khip_agg_push(khip_agg* a, const khip_batch* b, khip_batch_stats* st
   int64_t tot[NPART] = {0};
   if (a->engine == 2) {
     if (n >= (1LL << 31)) return fail(KHIP_E_UNSUPPORTED, "SESSION pushes above 2^31 rows");
-    KHIP_TRY(sess_push(a, n, keys, ts, kv, rv, cols, tot));
+    // SUPPLIED with a close context: the GLOBAL stream time after the batch bounds the store's
+    // expiry (sess_push expires against the handle's stream time after the push)
+    if (sctx) KHIP_TRY(supplied_advance(a));
+    KHIP_TRY(sess_push(a, n, keys, ts, kv, rv, cols, tot, st_at));
   } else if (a->engine == 0) {
     // ---- partitioned engine, in slices of < 2^31 records (multiple of 8: bitmaps stay byte aligned)
     const int64_t slice = 1LL << 31;

@@ -603,7 +603,7 @@ bool part_having_count(khip_agg* a, int64_t* n);
 khip_status part_changes(khip_agg* a, std::vector<uint64_t>* rows, std::vector<uint8_t>* tomb, int64_t* count);
 khip_status part_purge_closed(khip_agg* a, const HavingDev& vis);
 khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
-                      const uint8_t* rv, const ColPtrs& cols, int64_t* tot);
+                      const uint8_t* rv, const ColPtrs& cols, int64_t* tot, const int64_t* st_at);
 khip_status sess_changes(khip_agg* a, std::vector<uint64_t>* rows, std::vector<uint8_t>* tomb, int64_t* count);
 void sess_release(khip_agg* a);
 // table source (khip_agg_table.hip): batch rows (group ids, group-key hashes, group validity kv,

@@ -71,7 +71,7 @@ __global__ __launch_bounds__(BLOCK) void k_sess_range(const int64_t* __restrict_
                                                       const uint8_t* __restrict__ kv, const uint8_t* __restrict__ rv,
                                                       int64_t n, int64_t* __restrict__ blockmax,
                                                       ulonglong2* __restrict__ blockkr, int64_t* __restrict__ blockacc,
-                                                      int64_t* __restrict__ blocktmin) {
+                                                      int64_t* __restrict__ blocktmin, const int64_t* __restrict__ st_at) {
   __shared__ int64_t lds[BLOCK / 64];
   __shared__ uint64_t lk[3][BLOCK / 64];
   __shared__ int64_t la[BLOCK / 64];
@@ -84,7 +84,8 @@ __global__ __launch_bounds__(BLOCK) void k_sess_range(const int64_t* __restrict_
     const int64_t i = base + k * BLOCK + threadIdx.x;
     int64_t t;
     if (i < n && sess_ok(kv, rv, ts, i, &t)) {
-      m = t > m ? t : m;
+      const int64_t sx = st_at ? st_at[i] : t;  // KHIP_TIME_SUPPLIED: the row's given stream time
+      m = sx > m ? sx : m;
       tmn = t < tmn ? t : tmn;
       const uint64_t u = key_ord(keys[i]);
       kmn = ~u > kmn ? ~u : kmn;
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(BLOCK) void k_sess_prep(const int64_t* __restrict__
                                                      uint64_t drop, uint64_t* __restrict__ skey,
                                                      uint32_t* __restrict__ sidx, longlong2* __restrict__ rec,
                                                      uint64_t* __restrict__ rec8, int64_t tbase,
-                                                     int64_t* __restrict__ blockcnt) {
+                                                     int64_t* __restrict__ blockcnt, const int64_t* __restrict__ st_at) {
   // wave w owns records [base + w * 64 * ITEMS, +64 * ITEMS), read 64 at a time (coalesced); the
   // running max is a wave scan per step, the earlier waves' maxima join after one block barrier
   __shared__ int64_t wmax[BLOCK / 64];
@@ -242,7 +243,10 @@ __global__ __launch_bounds__(BLOCK) void k_sess_prep(const int64_t* __restrict__
       const bool ok = tv[k] >= 0;
       skey[i] = ok ? (uint64_t)keys[i] - (uint64_t)kmin : drop;
       if (sidx) sidx[i] = (uint32_t)i;
-      const int64_t sa = stv[k] > pre ? stv[k] : pre;
+      // KHIP_TIME_SUPPLIED: the row's given stream time (the GLOBAL one after it, >= its ts), which
+      // the replay's max(before, ts) keeps as it is (EMIT CHANGES only: EMIT FINAL needs the one
+      // before the row, which the shuffle does not carry)
+      const int64_t sa = st_at ? (ok ? st_at[i] : -1) : (stv[k] > pre ? stv[k] : pre);
       if (rec8) rec8[i] = rec_pack(tv[k], sa, tbase);
       else rec[i] = make_longlong2(tv[k], sa);
     }
@@ -737,7 +741,7 @@ __global__ __launch_bounds__(256) void k_sess_scatter_seg(const uint64_t* __rest
 // ------------------------------------------------------------------ host side
 
 khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* ts, const uint8_t* kv,
-                      const uint8_t* rv, const ColPtrs& cols, int64_t* tot) {
+                      const uint8_t* rv, const ColPtrs& cols, int64_t* tot, const int64_t* st_at) {
   SessState& S = a->sess;
   hipStream_t st = a->stream;
   const int sw = a->sw;
@@ -750,7 +754,7 @@ khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   int64_t* blockacc = (int64_t*)(S.blockkr.as<char>() + nb * 16);
   int64_t* blocktmin = (int64_t*)(S.blockkr.as<char>() + nb * 24);
   hipLaunchKernelGGL(k_sess_range, dim3(nb), dim3(BLOCK), 0, st, keys, ts, kv, rv, n, a->blockmax.as<int64_t>(),
-                     S.blockkr.as<ulonglong2>(), blockacc, blocktmin);
+                     S.blockkr.as<ulonglong2>(), blockacc, blocktmin, st_at);
   hipLaunchKernelGGL(k_sess_range_reduce, dim3(1), dim3(1024), 0, st, S.blockkr.as<ulonglong2>(), blockacc, blocktmin,
                      nb, a->stream_time.as<int64_t>(), S.ctr.as<unsigned long long>());
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, st, a->blockmax.as<int64_t>(), nb,
@@ -789,7 +793,7 @@ khip_status sess_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
   hipLaunchKernelGGL(k_sess_prep, dim3(nb), dim3(BLOCK), 0, st, keys, ts, kv, rv, n, a->blockprefix.as<int64_t>(), kmin,
                      drop, S.skey.as<uint64_t>(), by_idx ? S.sidx.as<uint32_t>() : nullptr,
                      packed ? nullptr : S.st_after.as<longlong2>(), packed ? S.st_after.as<uint64_t>() : nullptr, tbase,
-                     (int64_t*)S.blockkr.p);
+                     (int64_t*)S.blockkr.p, st_at);
   hipLaunchKernelGGL(k_sess_cnt_reduce, dim3(1), dim3(1024), 0, st, (const int64_t*)S.blockkr.p, nb,
                      S.ctr.as<unsigned long long>());
   KHIP_TRY_HIP(hipGetLastError());

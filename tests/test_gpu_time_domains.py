@@ -212,9 +212,12 @@ def test_partition_domain_rejects_bad_batches(prod):
     g.close()
     with pytest.raises(abi.KsqlHipError):
         abi.AggHandle(prod, _desc(time_domain="PARTITION", n_partitions=0))
-    with pytest.raises(abi.KsqlHipError):
-        abi.AggHandle(prod, abi.make_agg_desc(window_kind="SESSION", size_ms=1000, aggs=[("COUNT_STAR", -1)],
-                                              time_domain="SUPPLIED"))
+    # SESSION windows: SUPPLIED with EMIT CHANGES only (round 6); the rest stays the CPU builder's
+    for kw in (dict(time_domain="PARTITION", n_partitions=2), dict(time_domain="SUPPLIED", emit="FINAL")):
+        with pytest.raises(abi.KsqlHipError, match="SESSION"):
+            abi.AggHandle(prod, abi.make_agg_desc(window_kind="SESSION", size_ms=1000, aggs=[("COUNT_STAR", -1)], **kw))
+    abi.AggHandle(prod, abi.make_agg_desc(window_kind="SESSION", size_ms=1000, aggs=[("COUNT_STAR", -1)],
+                                          time_domain="SUPPLIED")).close()
 
 
 def _np_stream_time(ts, valid, seed):
@@ -280,18 +283,72 @@ def _route_supplied(prod_handles, scan_handle, stream, world):
     return late
 
 
-@pytest.mark.parametrize("engine", ["part", "atomic"])
+@pytest.mark.parametrize("engine", ["part", "atomic", "session"])
 def test_supplied_domain_union_equals_one_task(prod, orc, engine):
     rng = np.random.default_rng(21)
     world = 2
     stream = _global_stream(rng, nb=4, per=60_000, keys=4000)
     flags = abi.FLAG_ENGINE_ATOMIC if engine == "atomic" else 0
-    gd = _desc(time_domain="SUPPLIED", flags=flags)
+    win = dict(window="SESSION", size=2500) if engine == "session" else {}
+    gd = _desc(time_domain="SUPPLIED", flags=flags, **win)
     hs = [abi.AggHandle(prod, gd) for _ in range(world)]
     late = _route_supplied(hs, hs[0], stream, world)
-    o = abi.AggHandle(orc, _desc())
+    o = abi.AggHandle(orc, _desc(**win))
     olate = sum(o.push(abi.HostBatch(t, keys=k, cols=[v]))["windows_late"] for k, t, v in stream)
     assert late == olate and late > 0
+    assert_snap_equal(_union([h.snapshot() for h in hs], gd), o.snapshot(), gd)
+    for h in hs + [o]:
+        h.close()
+
+
+def _union_changes(chs, desc):
+    """The owners' changelogs (disjoint keys) → one, each owner's row order kept within a key (a
+    SESSION merge emits its tombstone before the rewritten row)."""
+    pos = np.concatenate([np.arange(c["n"]) for c in chs])
+    keys = np.concatenate([c["key"] for c in chs])
+    order = np.lexsort((pos, keys))
+    cat = lambda f: np.concatenate([c[f] for c in chs])[order]
+    return {"n": int(len(keys)), "key": keys[order], "ws": cat("ws"), "we": cat("we"), "rowtime": cat("rowtime"),
+            "tombstone": cat("tombstone"),
+            "values": [np.concatenate([c["values"][a] for c in chs])[order] for a in range(desc.n_aggs)],
+            "nulls": [np.concatenate([c["nulls"][a] for c in chs])[order] for a in range(desc.n_aggs)]}
+
+
+@pytest.mark.parametrize("grace", [0, 1000])
+def test_supplied_session_changes_per_push(prod, orc, grace):
+    """Round 6: SESSION windows in the SUPPLIED domain (a non-key GROUP BY with a SESSION window
+    behind the repartition).  Two owners get their keys' rows with the GLOBAL stream time; after
+    every micro-batch the owners' EMIT CHANGES rows (merged sessions' tombstones first, then the
+    rewritten sessions) together equal one oracle task's, and so do their late counts and final
+    tables."""
+    rng = np.random.default_rng(41 + grace)
+    world = 2
+    stream = _global_stream(rng, nb=5, per=30_000, keys=3000)
+    win = dict(window="SESSION", size=2500, grace=grace)
+    gd = _desc(time_domain="SUPPLIED", flags=abi.FLAG_CHANGELOG, **win)
+    hs = [abi.AggHandle(prod, gd) for _ in range(world)]
+    o = abi.AggHandle(orc, _desc(**win))
+    gst, late, olate, emitted = -1, 0, 0, 0
+    for k, t, v in stream:
+        n = len(t)
+        bounds = [n * r // world for r in range(world + 1)]
+        maxima = [hs[0].stream_time_scan(abi.HostBatch(t[lo:hi], keys=k[lo:hi]), -1)[1]
+                  for lo, hi in zip(bounds[:-1], bounds[1:])]
+        st = np.concatenate([hs[0].stream_time_scan(abi.HostBatch(t[lo:hi], keys=k[lo:hi]), max([gst] + maxima[:r]))[0]
+                             for r, (lo, hi) in enumerate(zip(bounds[:-1], bounds[1:]))])
+        gst = max([gst] + maxima)
+        chs = []
+        for owner in range(world):
+            m = k % world == owner
+            late += hs[owner].push(abi.HostBatch(t[m], keys=k[m], cols=[v[m]], stream_time=st[m]))["windows_late"]
+            chs.append(hs[owner].changes())
+        olate += o.push(abi.HostBatch(t, keys=k, cols=[v]))["windows_late"]
+        oc = o.changes()
+        g = _union_changes(chs, gd)
+        assert_snap_equal(g, oc, gd)
+        assert np.array_equal(g["tombstone"], oc["tombstone"])
+        emitted += g["n"]
+    assert late == olate and late > 0 and emitted > 0
     assert_snap_equal(_union([h.snapshot() for h in hs], gd), o.snapshot(), gd)
     for h in hs + [o]:
         h.close()
@@ -376,8 +433,8 @@ def test_supplied_domain_two_processes_gloo_one_gpu(orc):
 SH_AGGS = [("COUNT_STAR", -1), ("SUM", 1), ("MAX", 1)]
 
 
-def _sh_desc(domain="SUPPLIED", grace=1000, flags=abi.FLAG_PROFILE):
-    return abi.make_agg_desc(window_kind="TUMBLING", size_ms=5000, grace_ms=grace, col_types=["INT64", "INT64"],
+def _sh_desc(domain="SUPPLIED", grace=1000, flags=abi.FLAG_PROFILE, window="TUMBLING", size=5000):
+    return abi.make_agg_desc(window_kind=window, size_ms=size, grace_ms=grace, col_types=["INT64", "INT64"],
                              aggs=SH_AGGS, flags=flags, capacity_hint=1 << 20, time_domain=domain)
 
 
@@ -418,8 +475,8 @@ def _device_src(x, lo=0, hi=None):
     return abi.DeviceBatch(d(t), key_valid=bm(skv), row_valid=bm(rv), cols=[d(k), d(v)], col_valid=[bm(gbv), None])
 
 
-def _oracle_one_task(orc, stream, grace=1000):
-    o = abi.AggHandle(orc, _sh_desc("TASK", grace, 0))
+def _oracle_one_task(orc, stream, grace=1000, **win):
+    o = abi.AggHandle(orc, _sh_desc("TASK", grace, 0, **win))
     late = sum(o.push(_oracle_batch(x))["windows_late"] for x in stream)
     s = o.snapshot()
     o.close()
@@ -449,6 +506,28 @@ def test_supplied_through_repartition_one_rank(prod, orc, late_heavy, nulls):
     assert_snap_equal(h.snapshot(), exp, _sh_desc())
     if not late_heavy and not nulls:
         assert h.kernel_times()["c1_pushes"] == len(stream)
+    rp.close()
+    h.close()
+
+
+@pytest.mark.parametrize("nulls", [False, True])
+def test_supplied_session_through_repartition_one_rank(prod, orc, nulls):
+    """Round 6: a SESSION window behind the device repartition (pack → push_shuffled with the rows'
+    GLOBAL stream-time words; the session engine unpacks them) equals one oracle task."""
+    from ksql_amd.repartition import Repartition
+    rng = np.random.default_rng(37 + nulls)
+    stream = _global_stream(rng, nb=4, per=40_000, keys=3000)
+    if nulls:
+        stream = _with_nulls(rng, stream)
+    win = dict(window="SESSION", size=2500)
+    h = abi.AggHandle(prod, _sh_desc(**win))
+    rp = Repartition(prod, 0, ["INT64", "INT64"], global_time=True)
+    late = 0
+    for x in stream:
+        late += rp.push_into(h, _device_src(x))["windows_late"]
+    exp, olate = _oracle_one_task(orc, stream, 1000, **win)
+    assert late == olate and late > 0
+    assert_snap_equal(h.snapshot(), exp, _sh_desc(**win))
     rp.close()
     h.close()
 
