@@ -895,7 +895,7 @@ static khip_status dict_grow(KeyDict& d, hipStream_t s, int64_t new_cap) {
   }
   KHIP_TRY_HIP(hipStreamSynchronize(s));
   d.slots.release();
-  d.slots = ns;
+  d.slots = std::move(ns);
   ns.p = nullptr;
   d.dcap = new_cap;
   return KHIP_OK;
@@ -999,7 +999,7 @@ khip_status dict_map(KeyDict& d, hipStream_t s, const int64_t* koff, const uint8
     if (d.arena_used) KHIP_TRY_HIP(hipMemcpyAsync(na.p, d.arena.p, d.arena_used, hipMemcpyDeviceToDevice, s));
     KHIP_TRY_HIP(hipStreamSynchronize(s));
     d.arena.release();
-    d.arena = na;
+    d.arena = std::move(na);
     na.p = nullptr;
   }
   unsigned long long* c = d.ctr.as<unsigned long long>();
@@ -1156,7 +1156,7 @@ khip_status khip::agg_grow_table(khip_agg* a, int64_t new_cap) {
   }
   KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
   a->table.release();
-  a->table = nt;
+  a->table = std::move(nt);
   nt.p = nullptr;
   nt.bytes = 0;
   a->cap = new_cap;

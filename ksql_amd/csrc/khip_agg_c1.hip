@@ -2539,7 +2539,7 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
       KHIP_TRY_HIP(hipMemcpyAsync(nc.p, s.closed.p, (size_t)s.closed_n * a->sw * 8, hipMemcpyDeviceToDevice, a->stream));
     KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
     s.closed.release();
-    s.closed = nc;
+    s.closed = std::move(nc);
     nc.p = nullptr;
     s.closed_cap = ncap;
   }
@@ -2724,7 +2724,10 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
                               : (v_pm == PM_C3 ? pick(std::integral_constant<int, PM_C3>{}) : pick(std::integral_constant<int, 0>{}));
       hipFuncSetAttribute((const void*)mk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       KHIP_TRY(s.c1vq.ensure(sizeof(C1VQ)));
-      KHIP_TRY_HIP(hipMemcpyAsync(s.c1vq.p, &vq, sizeof(C1VQ), hipMemcpyHostToDevice, a->stream));
+      KHIP_TRY(s.c1vq_h.ensure(2 * sizeof(C1VQ)));
+      C1VQ* hq = (C1VQ*)s.c1vq_h.p + idw;
+      *hq = vq;
+      KHIP_TRY_HIP(hipMemcpyAsync(s.c1vq.p, hq, sizeof(C1VQ), hipMemcpyHostToDevice, a->stream));
       const int64_t vgrid = std::min<int64_t>(nwork, (int64_t)s.n_cu * (lds <= C1V_LDS2 ? v_wpc : 1));
       hipLaunchKernelGGL(mk, dim3(vgrid), dim3(512), lds, a->stream, s.c1vq.as<C1VQ>(), wk, nwork, s.c1bb.as<int64_t>(), cstart, seg,
                          (const ulonglong2*)s.srec.p, pass == 0 ? 1 : 0, s.buf[0].as<uint64_t>(), s.buf[1].as<uint64_t>(),
@@ -2764,6 +2767,10 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     }
     unsigned long long* c2 = s.pinfo.as<unsigned long long>() + 8;
     KHIP_TRY_HIP(hipMemcpyAsync(c2, s.ctr.p, 13 * 8, hipMemcpyDeviceToHost, a->stream));
+    // the closed store's rows after this pass (closed rows leave in the pass that writes their
+    // item): read with the counters, no second round trip
+    KHIP_TRY_HIP(hipMemcpyAsync(s.pinfo.as<unsigned long long>() + 58, s.closed_ctr.p, 8, hipMemcpyDeviceToHost,
+                                a->stream));
     KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
     const int64_t* hci = s.pinfo.as<int64_t>() + 32;
     if (pass == 0 && hci[CI_GATE] == 0) {  // declined: nothing was written
@@ -2841,10 +2848,8 @@ khip_status c1_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t* 
     s.having_total = (int64_t)(hc[11] + hc[12]);
   }
   const unsigned long long* st = s.pinfo.as<unsigned long long>() + 8;
-  // the closed store's rows after every pass (closed rows leave in the pass that writes their item)
-  unsigned long long cnu = 0;
-  KHIP_TRY_HIP(hipMemcpy(&cnu, s.closed_ctr.p, 8, hipMemcpyDeviceToHost));
-  const int64_t cn = (int64_t)cnu;
+  // the closed store's rows after every pass (read with the last pass's counters)
+  const int64_t cn = (int64_t)s.pinfo.as<unsigned long long>()[58];
   added_total += cn - s.closed_n;  // evicted rows left the live regions but are still groups
   s.closed_n = cn;
   a->host_stream_time = (int64_t)st[4 + T_NPART];

@@ -422,6 +422,8 @@ struct PartState {
   // closed windows (ws + size <= streamTime - grace): never updated again, moved out of the
   // partition regions into an append-only store so the live table stays LDS-sized
   DevBuf closed, closed_ctr;
+  DevBuf closed2, pctr;   // the retention purge's second closed store and its counters (kept: no
+                          // allocation per push)
   int64_t closed_cap = 0, closed_n = 0;
   // identity-CAS mode: wr = [window-index base, enabled] of the current push; res = window-
   // index range of the resident rows (conservative); res_fresh = no resident rows yet
@@ -458,6 +460,8 @@ struct PartState {
   bool last_c1 = false;
   int c1_skip = 0;  // pushes left before the pipeline is tried again after a declined push
   DevBuf c1vq;  // the value pipeline's merge parameters (device copy)
+  HostBuf c1vq_h;  // their pinned staging, one slot per identity width (a pageable source would
+                   // make the copy wait for the stream: a ~20 us bubble before every merge)
   bool c1_wide = false;  // the pipeline's record format for the next push (key range past 32 bits)
 };
 

@@ -3587,7 +3587,8 @@ khip_status part_init(khip_agg* a, int64_t hint) {
 void part_release(khip_agg* a) {
   PartState& s = a->part;
   s.pinfo.release();
-  DevBuf* bufs[] = {&s.hcnt, &s.hnew, &s.srecA, &s.hcoarse, &s.scan_tmpB, &s.RB, &s.wr, &s.res, &s.closed, &s.closed_ctr, &s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist,
+  s.c1vq_h.release();
+  DevBuf* bufs[] = {&s.hcnt, &s.hnew, &s.srecA, &s.hcoarse, &s.scan_tmpB, &s.RB, &s.wr, &s.res, &s.closed, &s.closed_ctr, &s.closed2, &s.pctr, &s.buf[0], &s.buf[1], &s.sel, &s.cnt, &s.newcnt, &s.fail, &s.hist,
                     &s.tilemax, &s.tilemin, &s.tilekr,
                     &s.tileprefix, &s.tpart, &s.scan_tmp, &s.srec, &s.work,
                     &s.c1rc, &s.c1rp, &s.c1ro, &s.c1scan, &s.c1ci, &s.c1bb, &s.c1seg, &s.c1info, &s.prn, &s.c1vq,
@@ -3676,12 +3677,12 @@ khip_status part_regrow(khip_agg* a, int64_t ncmax) {
   KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
   for (int b = 0; b < 2; b++) {
     s.buf[b].release();
-    s.buf[b] = nb[b];
+    s.buf[b] = std::move(nb[b]);
     nb[b].p = nullptr;
   }
   if (a->changelog) {
     a->chg.release();
-    a->chg = nchg;
+    a->chg = std::move(nchg);
     nchg.p = nullptr;
   }
   s.cmax = ncmax;
@@ -3719,7 +3720,7 @@ static khip_status part_split(khip_agg* a) {
   DevBuf* news[] = {&nb[0], &nb[1], &ncnt, &nsel, &nnew, &nfail};
   for (int k = 0; k < 6; k++) {
     olds[k]->release();
-    *olds[k] = *news[k];
+    *olds[k] = std::move(*news[k]);
     news[k]->p = nullptr;
   }
   // a child holds about half of its parent's groups: one sub-pass bit fewer
@@ -4055,7 +4056,7 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
         KHIP_TRY_HIP(hipMemcpyAsync(nc.p, s.closed.p, (size_t)s.closed_n * a->sw * 8, hipMemcpyDeviceToDevice, a->stream));
       KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
       s.closed.release();
-      s.closed = nc;
+      s.closed = std::move(nc);
       nc.p = nullptr;
       s.closed_cap = ncap;
     }
@@ -4292,8 +4293,8 @@ khip_status part_compact(khip_agg* a, const HavingDev& h_in, std::vector<uint64_
   int64_t nl = 0;
   KHIP_TRY_HIP(hipMemcpyAsync(&nl, s.counts.as<int64_t>() + P, 8, hipMemcpyDeviceToHost, a->stream));
   // closed rows (flat store) passing h
-  DevBuf cctr;
-  KHIP_TRY(cctr.ensure(8));
+  DevBuf& cctr = s.pctr;
+  KHIP_TRY(cctr.ensure(16));
   KHIP_TRY_HIP(hipMemsetAsync(cctr.p, 0, 8, a->stream));
   if (s.closed_n) {
     hipLaunchKernelGGL(k_compact, dim3((int)std::min<int64_t>(ceil_div(s.closed_n, 256), 4096)), dim3(256), 0, a->stream,
@@ -4363,11 +4364,15 @@ khip_status part_purge_closed(khip_agg* a, const HavingDev& vis) {
   PartState& s = a->part;
   if (s.closed_n == 0 || vis.vis_from <= s.purged_to) return KHIP_OK;
   const int grid = (int)std::min<int64_t>(ceil_div(s.closed_n, 256), 4096);
-  DevBuf ctr;
+  // one pass: the kept rows go to the second store (which then becomes the store) and are counted;
+  // one host round trip for both counts (the buffers are the handle's: no allocation per push)
+  DevBuf& ctr = s.pctr;
   KHIP_TRY(ctr.ensure(16));
+  DevBuf& nc = s.closed2;
+  KHIP_TRY(nc.ensure((size_t)s.closed_cap * a->sw * 8));
   KHIP_TRY_HIP(hipMemsetAsync(ctr.p, 0, 16, a->stream));
   hipLaunchKernelGGL(k_compact, dim3(grid), dim3(256), 0, a->stream, s.closed.as<uint64_t>(), s.closed_n, a->sw, vis,
-                     (uint64_t*)nullptr, (int64_t)0, ctr.as<unsigned long long>());
+                     nc.as<uint64_t>(), s.closed_cap, ctr.as<unsigned long long>());
   HavingDev vh = vis;  // kept rows passing the query's HAVING
   vh.active = a->having.active;
   vh.op = a->having.op;
@@ -4383,23 +4388,15 @@ khip_status part_purge_closed(khip_agg* a, const HavingDev& vis) {
   KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
   s.purged_to = vis.vis_from;
   const int64_t keep = kc[0];
-  if (keep == s.closed_n) return KHIP_OK;
-  DevBuf nc;
-  KHIP_TRY(nc.ensure((size_t)s.closed_cap * a->sw * 8));
-  KHIP_TRY_HIP(hipMemsetAsync(ctr.p, 0, 8, a->stream));
-  hipLaunchKernelGGL(k_compact, dim3(grid), dim3(256), 0, a->stream, s.closed.as<uint64_t>(), s.closed_n, a->sw, vis,
-                     nc.as<uint64_t>(), keep, ctr.as<unsigned long long>());
-  KHIP_TRY_HIP(hipGetLastError());
+  if (keep == s.closed_n) return KHIP_OK;  // nothing expired: the store stays (its copy is unused)
   if (vh.active) {  // ctr[12]: closed rows passing HAVING
     unsigned long long* hc = s.pinfo.as<unsigned long long>() + 40;
     *hc = (unsigned long long)kc[1];
     KHIP_TRY_HIP(hipMemcpyAsync(s.ctr.as<unsigned long long>() + 12, hc, 8, hipMemcpyHostToDevice, a->stream));
     s.having_total += kc[1] - (int64_t)s.pinfo.as<unsigned long long>()[8 + 12];
+    KHIP_TRY_HIP(hipStreamSynchronize(a->stream));  // (hc is pinned host memory the next push reuses)
   }
-  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
-  s.closed.release();
-  s.closed = nc;
-  nc.p = nullptr;
+  std::swap(s.closed, s.closed2);
   a->occ -= s.closed_n - keep;
   s.closed_n = keep;
   return KHIP_OK;

@@ -639,7 +639,7 @@ static khip_status src_grow(khip_agg* a, int64_t new_cap, int hsw, int nwords) {
   int64_t occ = 0;
   KHIP_TRY(src_count(a, nt, new_cap, hsw, &occ));
   T.src.release();
-  T.src = nt;
+  T.src = std::move(nt);
   nt.p = nullptr;
   T.src_cap = new_cap;
   T.src_occ = occ;
@@ -659,7 +659,7 @@ static khip_status src_dense(khip_agg* a, int64_t base, int64_t cap, int dsw) {
                                 (size_t)T.src_cap * dsw * 8, hipMemcpyDeviceToDevice, a->stream));
   KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
   T.src.release();
-  T.src = nt;
+  T.src = std::move(nt);
   nt.p = nullptr;
   T.src_cap = cap;
   T.src_sw = dsw;

@@ -923,7 +923,7 @@ static khip_status table_grow(khip_table* t, int64_t new_cap) {
   KHIP_TRY_HIP(hipMemcpyAsync(&live, ctr, 8, hipMemcpyDeviceToHost, t->stream));
   KHIP_TRY_HIP(hipStreamSynchronize(t->stream));
   t->table.release();
-  t->table = nt;
+  t->table = std::move(nt);
   nt.p = nullptr;
   t->cap = new_cap;
   t->occ = (int64_t)live;

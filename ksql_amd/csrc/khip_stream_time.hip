@@ -338,8 +338,8 @@ static khip_status pmap_grow(khip_agg* a, int64_t cap) {
   KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
   a->pm_key.release();
   a->pm_part.release();
-  a->pm_key = nk;
-  a->pm_part = np;
+  a->pm_key = std::move(nk);
+  a->pm_part = std::move(np);
   nk.p = np.p = nullptr;
   a->pm_cap = cap;
   return KHIP_OK;

@@ -49,10 +49,29 @@ inline int64_t knob(const char* name, int64_t dflt) {
 #endif
 }
 
-// Grow-only device buffer.
+// Grow-only device buffer, owned: freed when it goes out of scope (a function's scratch) or with its
+// handle; moved, never copied.
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) {
+    o.p = nullptr;
+    o.bytes = 0;
+  }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    if (this != &o) {
+      release();
+      p = o.p;
+      bytes = o.bytes;
+      o.p = nullptr;
+      o.bytes = 0;
+    }
+    return *this;
+  }
+  ~DevBuf() { release(); }
   khip_status ensure(size_t want) {
     if (want <= bytes) return KHIP_OK;
     if (p) hipFree(p);
