@@ -351,6 +351,30 @@ __device__ __forceinline__ bool having_ok_words(uint64_t val, uint64_t cntw, con
   return false;
 }
 
+// The query's HAVING alone (no pull-query filter): the engines' own row checks.
+__device__ __forceinline__ bool having_only(const uint64_t* s, const HavingDev& h) {
+  if (!h.active) return true;
+  int64_t iv = 0;
+  double dv = 0.0;
+  if (!decode_result(s, h.a, &iv, &dv)) return false;
+  int c;
+  if (result_is_double(h.a)) {
+    if (dv != dv) return h.op == KHIP_OP_NE;
+    c = dv < h.f64 ? -1 : (dv > h.f64 ? 1 : 0);
+  } else {
+    c = iv < h.i64 ? -1 : (iv > h.i64 ? 1 : 0);
+  }
+  switch (h.op) {
+    case KHIP_OP_GT: return c > 0;
+    case KHIP_OP_GE: return c >= 0;
+    case KHIP_OP_LT: return c < 0;
+    case KHIP_OP_LE: return c <= 0;
+    case KHIP_OP_EQ: return c == 0;
+    case KHIP_OP_NE: return c != 0;
+  }
+  return false;
+}
+
 __device__ __forceinline__ bool having_ok(const uint64_t* s, const HavingDev& h) {
   if (!pull_ok(s, h)) return false;
   if (!h.active) return true;

@@ -410,7 +410,9 @@ __device__ __forceinline__ void row_copy(uint64_t* d, const uint64_t* s, int sw)
 // Returns the sessions left after expiry (compacted at R); chg rows appended to the changelog.
 // FIN (EMIT FINAL) is a template parameter: the EMIT CHANGES replay compiles without the close
 // checks (with them as a run-time branch the replay took 157 VGPRs and 800 B of scratch per lane
-// instead of 69 and 52: session leg 9.6 -> 11.1 ms/step).
+// instead of 69 and 52: session leg 9.6 -> 11.1 ms/step).  Rows are checked with having_only (the
+// query's HAVING; the pull-query filter of having_ok made the FINAL replay copy its parameters to
+// scratch: 81 VGPRs and no scratch now).
 template <bool FIN>
 __device__ __forceinline__ int64_t sess_replay(const SessParams& q, int64_t key, const uint64_t* orig, int64_t norig,
                                                const longlong2* g, const uint64_t* g8, int64_t tbase,
@@ -424,7 +426,7 @@ __device__ __forceinline__ int64_t sess_replay(const SessParams& q, int64_t key,
   for (int64_t k = 0; k < norig; k++) {  // the key's sessions, sorted by start (and end)
     const uint64_t* src = orig + k * sw;
     row_copy(R + m * sw, src, sw);
-    F[m] = SF_ORIG | (having_ok(src, q.having) ? SF_OLDP : 0);
+    F[m] = SF_ORIG | (having_only(src, q.having) ? SF_OLDP : 0);
     m++;
   }
   for (int64_t r = 0; r < nrec; r++) {
@@ -472,7 +474,7 @@ __device__ __forceinline__ int64_t sess_replay(const SessParams& q, int64_t key,
       const int64_t cb = stb >= 0 ? stb - q.grace - q.gap : INT64_MIN;
       for (int64_t k = lo; k < hi; k++) {
         const int64_t e = (int64_t)R[k * sw + 2];
-        if (e >= q.fin_lo && e < cb && having_ok(R + k * sw, q.having)) {
+        if (e >= q.fin_lo && e < cb && having_only(R + k * sw, q.having)) {
           row_copy(T + nt * sw, R + k * sw, sw);
           nt++;
         }
@@ -520,7 +522,7 @@ __device__ __forceinline__ int64_t sess_replay(const SessParams& q, int64_t key,
     int64_t nc = nt;
     for (int64_t k = 0; k < m; k++) {
       const int64_t e = (int64_t)R[k * sw + 2];
-      nc += (e >= q.fin_lo && e < close_end && having_ok(R + k * sw, q.having)) ? 1 : 0;
+      nc += (e >= q.fin_lo && e < close_end && having_only(R + k * sw, q.having)) ? 1 : 0;
     }
     int64_t c = nc ? (int64_t)atomicAdd(&ctr[16], (unsigned long long)nc) : 0;
     for (int64_t k = 0; k < nt; k++) {
@@ -529,7 +531,7 @@ __device__ __forceinline__ int64_t sess_replay(const SessParams& q, int64_t key,
     }
     for (int64_t k = 0; k < m; k++) {
       const int64_t e = (int64_t)R[k * sw + 2];
-      if (!(e >= q.fin_lo && e < close_end && having_ok(R + k * sw, q.having))) continue;
+      if (!(e >= q.fin_lo && e < close_end && having_only(R + k * sw, q.having))) continue;
       row_copy(crow + c * sw, R + k * sw, sw);
       ctomb[c++] = 0;
     }
@@ -538,12 +540,12 @@ __device__ __forceinline__ int64_t sess_replay(const SessParams& q, int64_t key,
     // sessions that existed before the push (tombstones when HAVING held)
     int64_t nc = 0;
     for (int64_t k = 0; k < m; k++)
-      if (F[k] & SF_TOUCHED) nc += (having_ok(R + k * sw, q.having) || ((F[k] & SF_ORIG) && (F[k] & SF_OLDP))) ? 1 : 0;
+      if (F[k] & SF_TOUCHED) nc += (having_only(R + k * sw, q.having) || ((F[k] & SF_ORIG) && (F[k] & SF_OLDP))) ? 1 : 0;
     for (int64_t k = 0; k < nt; k++) nc += (T[k * sw] & SF_OLDP) ? 1 : 0;
     int64_t c = nc ? (int64_t)atomicAdd(&ctr[16], (unsigned long long)nc) : 0;
     for (int64_t k = 0; k < m; k++) {
       if (!(F[k] & SF_TOUCHED)) continue;
-      const bool now = having_ok(R + k * sw, q.having);
+      const bool now = having_only(R + k * sw, q.having);
       if (!now && !((F[k] & SF_ORIG) && (F[k] & SF_OLDP))) continue;
       row_copy(crow + c * sw, R + k * sw, sw);
       ctomb[c++] = now ? 0 : 1;
@@ -681,7 +683,7 @@ __global__ __launch_bounds__(256) void k_sess_keep(const uint64_t* __restrict__ 
     keep[i] = (!in_batch && (int64_t)s[2] >= *st_end - retention) ? 1 : 0;
     if (q.fin && !in_batch && *st_end >= 0) {
       const int64_t e = (int64_t)s[2];
-      emit = e >= q.fin_lo && e < *st_end - q.grace - q.gap && having_ok(s, q.having);
+      emit = e >= q.fin_lo && e < *st_end - q.grace - q.gap && having_only(s, q.having);
     }
   }
   if (!q.fin) return;
