@@ -48,7 +48,6 @@ Output: one JSON line (rank 0) with `roofline` and `cpu_baseline`:
 import argparse
 import json
 import os
-import socket
 import subprocess
 import sys
 import threading
@@ -105,19 +104,13 @@ def parse():
 
 # ------------------------------------------------------------------ multi-GPU launch
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def relaunch(args):
     """--gpus N without torchrun's environment: run this script under torch.distributed.run as
-    a child (one rank per GPU) and exit with its code.  Nothing here has touched the GPU."""
+    a child (one rank per GPU) and exit with its code.  Nothing here has touched the GPU.  The
+    rendezvous binds its own port (--standalone on 127.0.0.1): a port probed here and bound later
+    by torchrun could be taken in between (EADDRINUSE on a busy box)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+           "--standalone", "--local-addr", "127.0.0.1", os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.call(cmd, env=env)

@@ -18,7 +18,7 @@ def test_multi_gpu_relaunches_under_torchrun(monkeypatch):
     (cmd, env), = calls
     assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
     assert cmd[cmd.index("--nproc-per-node") + 1] == "4"
-    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert "--standalone" in cmd and cmd[cmd.index("--local-addr") + 1] == "127.0.0.1"  # torchrun binds the port
     assert cmd[cmd.index(os.path.abspath(bench.__file__)) + 1:] == ["--gpus", "4", "--steps", "3", "--warmup", "1"]
     assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
     assert "torch" not in sys.modules or not _cuda_initialised()
