@@ -9,7 +9,6 @@ equals one task over all records (no late drops at this disorder, SURVEY.md §8(
 and that the max-over-ranks reduction the bench uses is what it claims.
 """
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -18,6 +17,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from ksql_amd import abi, synth
+from pg_store import init_gloo, store_url
 
 WORLD = 2
 N = 30_000
@@ -25,11 +25,7 @@ KEYS = 700
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    return store_url()  # the process group's FileStore (pg_store.py), not a TCP port
 
 
 def _shard_snapshot(rank, world):
@@ -43,8 +39,7 @@ def _shard_snapshot(rank, world):
 
 
 def _worker(rank, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    init_gloo(port, rank, WORLD)
     try:
         card, ts, s = _shard_snapshot(rank, WORLD)
         shard = {"key": s["key"], "ws": s["ws"], "cnt": s["values"][0], "rt": s["rowtime"],
@@ -114,8 +109,7 @@ def _shuffle_desc():
 def _shuffle_worker(rank, port, q):
     from shuffle_ref import expected_pack, expected_unpack
     from ksql_amd.repartition import GlooExchange
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    init_gloo(port, rank, WORLD)
     try:
         orc = abi.load_oracle()
         eid, ts, region, amount = synth.repartition_sum(0, SH_N, SH_N, rank=rank, world=WORLD, regions=300)
@@ -193,8 +187,7 @@ def test_repartition_exchange_across_ranks():
 
 def _regions_worker(rank, port, q):
     from ksql_amd.repartition import GlooExchange
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    init_gloo(port, rank, WORLD)
     try:
         ex = GlooExchange()
         rw = 3

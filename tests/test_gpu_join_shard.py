@@ -14,7 +14,6 @@ rank 0 checks every rank against the oracle:
 - the shards' sizes add up to the oracle table's.
 """
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -22,6 +21,7 @@ import torch
 import torch.multiprocessing as mp
 
 from ksql_amd import abi, synth
+from pg_store import init_gloo, store_url
 
 pytestmark = pytest.mark.gpu
 
@@ -58,8 +58,7 @@ def _worker(rank, port, q):
     import torch.distributed as dist
     from ksql_amd.join_shard import ShardedTable
     from ksql_amd.repartition import GlooExchange
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    init_gloo(port, rank, WORLD)
     try:
         torch.cuda.init()
         prod = abi.load_product()
@@ -89,10 +88,7 @@ def _worker(rank, port, q):
 
 def test_sharded_join_two_ranks():
     orc = abi.load_oracle()
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    port = store_url()  # (a FileStore: pg_store.py)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]

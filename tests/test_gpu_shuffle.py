@@ -15,6 +15,7 @@ import pytest
 import torch
 
 from ksql_amd import abi, synth
+from pg_store import init_gloo, store_url
 from ksql_amd.repartition import Repartition
 from shuffle_ref import expected_pack, kafka_partition
 
@@ -250,7 +251,6 @@ def test_rccl_single_rank_alltoall(prod):
 
 # ---- two source tasks in two processes (both on cuda:0), rows exchanged over gloo ----------
 import os
-import socket
 
 import torch.multiprocessing as mp
 
@@ -261,8 +261,7 @@ MP_N = 60_000
 def _mp_worker(rank, port, q):
     import torch.distributed as dist
     from ksql_amd.repartition import GlooExchange
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=MP_WORLD)
+    init_gloo(port, rank, MP_WORLD)
     try:
         torch.cuda.init()
         prod = abi.load_product()
@@ -289,10 +288,7 @@ def _mp_worker(rank, port, q):
 def test_two_process_repartition_gloo(orc):
     """Product pack → exchange between two processes → product unpack → product aggregate, per
     task equal to the oracle over the rows Kafka's partitioner routes to it (source order)."""
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    port = store_url()  # (a FileStore: pg_store.py)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_mp_worker, args=(r, port, q)) for r in range(MP_WORLD)]

@@ -20,12 +20,12 @@ disorder across window boundaries) so that the domain decides which records are 
 - khip_stream_time_scan itself against numpy, and the batch validation errors.
 """
 import os
-import socket
 
 import numpy as np
 import pytest
 
 from ksql_amd import abi
+from pg_store import init_gloo, store_url
 from test_gpu_parity import assert_snap_equal
 
 pytestmark = pytest.mark.gpu
@@ -355,18 +355,13 @@ def test_supplied_session_changes_per_push(prod, orc, grace):
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    return store_url()  # the process group's FileStore (pg_store.py), not a TCP port
 
 
 def _gloo_rank(rank, world, port, q):
     import torch
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_gloo(port, rank, world)
     try:
         prod = abi.load_product()
         h = abi.AggHandle(prod, _desc(time_domain="SUPPLIED"))
@@ -552,8 +547,7 @@ def _gloo_rank_repartition(rank, world, port, q, nulls=False):
     import torch
     import torch.distributed as dist
     from ksql_amd.repartition import GlooExchange, Repartition
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_gloo(port, rank, world)
     try:
         prod = abi.load_product()
         h = abi.AggHandle(prod, _sh_desc())
@@ -707,8 +701,7 @@ def test_supplied_emit_final_one_rank(prod, orc):
 def _gloo_rank_final(rank, world, port, q):
     import torch.distributed as dist
     from ksql_amd.repartition import GlooExchange, Repartition
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_gloo(port, rank, world)
     try:
         prod = abi.load_product()
         h = abi.AggHandle(prod, _final_desc("SUPPLIED"))
