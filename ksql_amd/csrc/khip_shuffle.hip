@@ -167,6 +167,37 @@ __global__ __launch_bounds__(SH_THREADS) void k_shuf_pack(ShCols c, int n_cols, 
 // last tile leaves the total in *total.
 constexpr uint64_t SH_AGG = 1ULL << 62, SH_INC = 2ULL << 62, SH_VAL = (1ULL << 62) - 1;
 
+// Decoupled look-back by one whole wave: the exclusive prefix of tile `tile` over the status words
+// status[j * stride] of the tiles j < tile (AGG | the tile's count, or INC | its inclusive prefix).
+// The 64 lanes read 64 predecessors at once and stop at the nearest INC: a walk by one thread paid
+// a memory round trip per predecessor, and the pack waited on that chain (C5's one-destination
+// pack ran 1.93 ms with it, 1.45 ms with no look-back at all).  A predecessor that has not
+// published yet is running (tickets are taken in dispatch order) and publishes its count before it
+// looks back itself, so the wait ends.  (Measured: pack1 1.92 -> 1.84 ms; most of the 0.48 ms the
+// look-back costs is the wait for predecessors' counts, not the walk.)
+__device__ __forceinline__ uint64_t sh_wave_lookback(const uint64_t* status, int64_t tile, uint64_t stride) {
+  const int lane = threadIdx.x & 63;
+  uint64_t excl = 0;
+  for (int64_t j0 = tile - 1; j0 >= 0; j0 -= 64) {
+    const int64_t j = j0 - lane;
+    uint64_t st = j >= 0 ? __hip_atomic_load(status + (uint64_t)j * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                         : SH_INC;  // before tile 0: an inclusive prefix of 0
+    while (__ballot(!(st & ~SH_VAL))) {
+      __builtin_amdgcn_s_sleep(1);
+      if (!(st & ~SH_VAL))
+        st = __hip_atomic_load(status + (uint64_t)j * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const uint64_t inc = __ballot((st & SH_INC) != 0);
+    const int first = inc ? __ffsll((unsigned long long)inc) - 1 : 64;
+    uint64_t v = lane <= first ? (st & SH_VAL) : 0;  // the nearest INC and the aggregates after it
+#pragma unroll
+    for (int off = 32; off; off >>= 1) v += __shfl_xor(v, off, 64);
+    excl += v;
+    if (inc) break;
+  }
+  return excl;
+}
+
 // Batch row i as its packed row, in registers: 2 + NC + ST words, padded to an even count so that
 // a row of an even word count leaves as 16-byte pairs.
 template <int NC, int ST>
@@ -244,30 +275,25 @@ __global__ __launch_bounds__(SH_THREADS) void k_shuf_pack1(ShCols c, int key_col
     vmask |= (v ? 1u : 0u) << r;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {  // exclusive prefix in (round, wave) order = arrival order
+  if (wave == 0) {
     uint32_t acc = 0;
-    for (int r = 0; r < SH_ITEMS; r++)
-      for (int w = 0; w < W; w++) {
-        const uint32_t e = wcnt[r][w];
-        wcnt[r][w] = acc;
-        acc += e;
-      }
-    __hip_atomic_store(status + tile, (tile == 0 ? SH_INC : SH_AGG) | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint64_t excl = 0;
-    for (int64_t j = tile - 1; j >= 0;) {
-      const uint64_t st = __hip_atomic_load(status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (!(st & ~SH_VAL)) {
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      excl += st & SH_VAL;
-      if (st & SH_INC) break;
-      j--;
+    if (lane == 0) {  // exclusive prefix in (round, wave) order = arrival order
+      for (int r = 0; r < SH_ITEMS; r++)
+        for (int w = 0; w < W; w++) {
+          const uint32_t e = wcnt[r][w];
+          wcnt[r][w] = acc;
+          acc += e;
+        }
+      __hip_atomic_store(status + tile, (tile == 0 ? SH_INC : SH_AGG) | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (tile > 0)
-      __hip_atomic_store(status + tile, SH_INC | (excl + acc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    lbase = (int64_t)excl;
-    if (tile == nT - 1) *total = excl + acc;
+    acc = __shfl(acc, 0, 64);
+    const uint64_t excl = sh_wave_lookback(status, tile, 1);
+    if (lane == 0) {
+      if (tile > 0)
+        __hip_atomic_store(status + tile, SH_INC | (excl + acc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lbase = (int64_t)excl;
+      if (tile == nT - 1) *total = excl + acc;
+    }
   }
   __syncthreads();
   for (int r = 0; r < SH_ITEMS; r++) {
@@ -337,6 +363,9 @@ __global__ __launch_bounds__(SH_THREADS) void k_shuf_packv(ShCols c, int key_col
       wc[w][d] = acc;
       acc += e;
     }
+    // (one thread per destination walks back: the destinations' walks run side by side in a wave;
+    // a wave-wide look-back per destination, its 64 predecessors' words strided by n_parts, ran
+    // 2.3-2.9 ms against 1.8-2.1 at 2-8 destinations)
     uint64_t* sd = status + (uint64_t)tile * n_parts + d;
     __hip_atomic_store(sd, (tile == 0 ? SH_INC : SH_AGG) | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint64_t excl = 0;
