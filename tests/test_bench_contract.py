@@ -56,7 +56,8 @@ TRAFFIC_FLOORS = {
     "possible_fraud": {"k_c1_scatter": 16},             # key + ts
     "possible_fraud_sparse_keys": {"k_c1_scatter": 16},
     "hopping_double": {"k_c1v_scatter": 24},            # key + ts + amount (per record of the leg)
-    "repartition_sum": {"k_shuf_pack1": 24},            # region + ts + amount
+    "repartition_sum": {"k_shuf_write1": 24,            # region + ts + amount
+                        "k_shuf_count1": 8},            # ts (+ the two validity bitmaps)
 }
 
 

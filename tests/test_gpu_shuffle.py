@@ -80,8 +80,8 @@ def test_pack_matches_oracle_partitioner(prod, orc, key_type, n_parts):
 @pytest.mark.parametrize("key_type", ["INT64", "INT32"])
 @pytest.mark.parametrize("n", [1, 4095, 4097, 70_001, 1_000_003])
 def test_pack_one_destination_one_pass(prod, orc, key_type, n):
-    """One destination with a send buffer for every row: k_shuf_pack1 (decoupled look-back, no
-    histogram pass) — the same rows, in the same order, as the oracle."""
+    """One destination with a send buffer for every row: k_shuf_count1 + scan + k_shuf_write1 (no
+    histogram pass, no look-back) — the same rows, in the same order, as the oracle."""
     import torch
     cols, types, cv, rv, ts = _random_source(n, key_type, seed=n)
     sh = abi.ShuffleHandle(prod, 1, 0, types)
