@@ -89,6 +89,7 @@ struct HavingDev {
   const int64_t* pm_key;
   const int32_t* pm_part;
   uint64_t pm_mask;
+  int32_t pm_pruned;  // keys whose windows had all expired left the map: a key not found is one of them
   const int64_t* p_vis;
   const int64_t* p_fin;
   const int64_t* p_lost_off;
@@ -129,6 +130,8 @@ __device__ __forceinline__ bool store_ok(const uint64_t* s, const HavingDev& h) 
       c1 = h.p_fin[2 * p + 1];
       lost = h.p_lost + 2 * h.p_lost_off[p];
       n_lost = (int)(h.p_lost_off[p + 1] - h.p_lost_off[p]);
+    } else if (h.pm_pruned) {
+      return false;  // every window of the key had expired in its task when the key left the map
     }
   }
   if (h.vis && ws < vis_from) return false;
@@ -577,8 +580,12 @@ struct khip_agg {
   // of the partitions' stream times after / before the last push; the last push's lost ws ranges
   // per partition (EMIT FINAL: plost pairs, plost_off[P + 1]); pdom: the per-partition bounds of
   // one compaction (device)
-  DevBuf pm_key, pm_part, pm_ctr, pdom;
+  // pm_ts: each key's latest record time (ts >= 0; 0 = none), by which keys whose windows have
+  // all expired leave the map (pmap_prune); pm_pruned: some have, so a row whose key is not in the
+  // map is an expired one
+  DevBuf pm_key, pm_part, pm_ts, pm_ctr, pdom;
   int64_t pm_cap = 0, pm_occ = 0, pm_last = -1;
+  bool pm_pruned = false;
   std::vector<int64_t> pst_host, pst_prev_host, plost, plost_off;
 };
 

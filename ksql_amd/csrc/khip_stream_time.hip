@@ -254,14 +254,16 @@ constexpr int PM_PROBE = 256;
 __global__ __launch_bounds__(256) void k_pmap_insert(const int64_t* __restrict__ keys, const uint8_t* __restrict__ kv,
                                                      const uint8_t* __restrict__ rv, const int64_t* __restrict__ ts,
                                                      const int32_t* __restrict__ part, int64_t n,
-                                                     int64_t* __restrict__ pk, int32_t* __restrict__ pp, uint64_t mask,
+                                                     int64_t* __restrict__ pk, int32_t* __restrict__ pp,
+                                                     unsigned long long* __restrict__ pts, uint64_t mask,
                                                      unsigned long long* __restrict__ ctr) {
   int64_t added = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     if (!(bit_get(kv, i) && bit_get(rv, i) && ts[i] >= 0)) continue;
     const int64_t k = keys[i];
     const int32_t p = part[i];
-    if (k == INT64_MIN) {
+    const unsigned long long t = (unsigned long long)ts[i];
+    if (k == INT64_MIN) {  // (its own slot, never pruned)
       const int old = atomicCAS(&pp[mask + 1], -1, p);
       if (old != -1 && old != p) atomicOr(&ctr[2], 1ULL);
       continue;
@@ -275,6 +277,7 @@ __global__ __launch_bounds__(256) void k_pmap_insert(const int64_t* __restrict__
                                                  (unsigned long long)k);
         if ((int64_t)old == INT64_MIN) {
           __hip_atomic_store(&pp[sl], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          atomicMax(&pts[sl], t);
           added++;
           done = true;
           break;
@@ -291,6 +294,7 @@ __global__ __launch_bounds__(256) void k_pmap_insert(const int64_t* __restrict__
         }
         if (q == -1) atomicOr(&ctr[1], 1ULL);  // (never seen: counted as a failed insert, retried)
         if (q != -1 && q != p) atomicOr(&ctr[2], 1ULL);
+        if (__hip_atomic_load(&pts[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < t) atomicMax(&pts[sl], t);
         done = true;
         break;
       }
@@ -302,18 +306,30 @@ __global__ __launch_bounds__(256) void k_pmap_insert(const int64_t* __restrict__
   if ((threadIdx.x & 63) == 0 && added) atomicAdd(&ctr[0], (unsigned long long)added);
 }
 
+// The map's entries into a new map; with `cut` (per partition), only the keys whose latest record
+// time reaches their partition's cut (pmap_prune).  kept: the entries moved (wave sums).
 __global__ __launch_bounds__(256) void k_pmap_rehash(const int64_t* __restrict__ ok, const int32_t* __restrict__ op,
-                                                     int64_t ocap, int64_t* __restrict__ nk, int32_t* __restrict__ np,
-                                                     uint64_t nmask) {
+                                                     const uint64_t* __restrict__ ots, int64_t ocap,
+                                                     const int64_t* __restrict__ cut, int n_parts,
+                                                     int64_t* __restrict__ nk, int32_t* __restrict__ np,
+                                                     uint64_t* __restrict__ nts, uint64_t nmask,
+                                                     unsigned long long* __restrict__ kept) {
+  int64_t moved = 0;
   for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < ocap; s += (int64_t)gridDim.x * blockDim.x) {
     const int64_t k = ok[s];
     if (k == INT64_MIN) continue;
+    const int p = op[s];
+    if (cut && p >= 0 && p < n_parts && (int64_t)ots[s] < cut[p]) continue;
     uint64_t d = pmap_hash(k) & nmask;
     while (atomicCAS((unsigned long long*)&nk[d], (unsigned long long)INT64_MIN, (unsigned long long)k) !=
            (unsigned long long)INT64_MIN)
       d = (d + 1) & nmask;
-    np[d] = op[s];
+    np[d] = p;
+    nts[d] = ots[s];
+    moved++;
   }
+  moved = wave_sum(moved);
+  if ((threadIdx.x & 63) == 0 && moved) atomicAdd(kept, (unsigned long long)moved);
 }
 
 __global__ __launch_bounds__(256) void k_fill_i64(int64_t* __restrict__ p, int64_t n, int64_t v) {
@@ -322,27 +338,68 @@ __global__ __launch_bounds__(256) void k_fill_i64(int64_t* __restrict__ p, int64
 
 static int pm_grid(int64_t n) { return (int)std::min<int64_t>(std::max<int64_t>(ceil_div(n, 256), 1), 8192); }
 
-static khip_status pmap_grow(khip_agg* a, int64_t cap) {
-  DevBuf nk, np;
+// A new map of `cap` slots holding the current one's entries — all of them, or (cut != null) those
+// of keys whose latest record time reaches their partition's cut.
+static khip_status pmap_rebuild(khip_agg* a, int64_t cap, const int64_t* cut_host) {
+  DevBuf nk, np, nt, cut;
   KHIP_TRY(nk.ensure((size_t)cap * 8));
   KHIP_TRY(np.ensure((size_t)(cap + 1) * 4));
+  KHIP_TRY(nt.ensure((size_t)cap * 8));
+  KHIP_TRY(a->pm_ctr.ensure(24));
   hipLaunchKernelGGL(k_fill_i64, dim3(pm_grid(cap)), dim3(256), 0, a->stream, nk.as<int64_t>(), cap, INT64_MIN);
   KHIP_TRY_HIP(hipMemsetAsync(np.p, 0xFF, (size_t)(cap + 1) * 4, a->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(nt.p, 0, (size_t)cap * 8, a->stream));
+  unsigned long long kept = 0;
   if (a->pm_cap > 0) {
+    const int P = a->desc.n_partitions;
+    if (cut_host) {
+      KHIP_TRY(cut.ensure((size_t)P * 8));
+      KHIP_TRY_HIP(hipMemcpyAsync(cut.p, cut_host, (size_t)P * 8, hipMemcpyHostToDevice, a->stream));
+    }
+    KHIP_TRY_HIP(hipMemsetAsync(a->pm_ctr.p, 0, 8, a->stream));
     hipLaunchKernelGGL(k_pmap_rehash, dim3(pm_grid(a->pm_cap)), dim3(256), 0, a->stream, a->pm_key.as<int64_t>(),
-                       a->pm_part.as<int32_t>(), a->pm_cap, nk.as<int64_t>(), np.as<int32_t>(), (uint64_t)(cap - 1));
+                       a->pm_part.as<int32_t>(), a->pm_ts.as<uint64_t>(), a->pm_cap,
+                       cut_host ? cut.as<int64_t>() : nullptr, P, nk.as<int64_t>(), np.as<int32_t>(), nt.as<uint64_t>(),
+                       (uint64_t)(cap - 1), a->pm_ctr.as<unsigned long long>());
     KHIP_TRY_HIP(hipMemcpyAsync(np.as<int32_t>() + cap, a->pm_part.as<int32_t>() + a->pm_cap, 4,
                                 hipMemcpyDeviceToDevice, a->stream));
+    KHIP_TRY_HIP(hipMemcpyAsync(&kept, a->pm_ctr.p, 8, hipMemcpyDeviceToHost, a->stream));
   }
   KHIP_TRY_HIP(hipGetLastError());
-  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));
-  a->pm_key.release();
-  a->pm_part.release();
+  KHIP_TRY_HIP(hipStreamSynchronize(a->stream));  // (cut_host is the caller's)
   a->pm_key = std::move(nk);
   a->pm_part = std::move(np);
-  nk.p = np.p = nullptr;
+  a->pm_ts = std::move(nt);
   a->pm_cap = cap;
+#ifdef KHIP_TUNING
+  if (cut_host && getenv("KHIP_TRACE_PMAP"))
+    fprintf(stderr, "pmap_prune: kept %llu of %lld keys\n", kept, (long long)a->pm_occ);
+#endif
+  if (cut_host && (int64_t)kept < a->pm_occ) a->pm_pruned = true;
+  a->pm_occ = (int64_t)kept;
   return KHIP_OK;
+}
+
+static khip_status pmap_grow(khip_agg* a, int64_t cap) { return pmap_rebuild(a, cap, nullptr); }
+
+// Before the map grows: the keys whose every window has expired in their task leave it (ADVICE r05:
+// the map otherwise grows with every key ever seen).  A key's windows all start at or before its
+// latest record time, so a key whose latest time is below its partition's retention cut (the
+// visible_from rule at the partition's stream time before this push) has only expired windows,
+// which with retention >= size + grace also closed before this push (EMIT FINAL emits none of them
+// again); its rows stay invisible (store_ok: a key missing from a pruned map is expired).  A key
+// that comes back is inserted afresh.  SESSION stores keep the whole map.
+static khip_status pmap_prune(khip_agg* a) {
+  const int P = a->desc.n_partitions;
+  if (a->engine == 2 || a->pst_host.size() != (size_t)P || a->retention < a->desc.size_ms + a->grace) return KHIP_OK;
+  std::vector<int64_t> cut((size_t)P);
+  bool any = false;
+  for (int p = 0; p < P; p++) {
+    cut[p] = partition_vis_from(a, a->pst_host[p]);
+    any = any || cut[p] != INT64_MIN;
+  }
+  if (!any) return KHIP_OK;
+  return pmap_rebuild(a, a->pm_cap, cut.data());
 }
 
 khip_status pmap_insert(khip_agg* a, const int64_t* keys, const uint8_t* kv, const uint8_t* rv, const int64_t* ts,
@@ -352,13 +409,15 @@ khip_status pmap_insert(khip_agg* a, const int64_t* keys, const uint8_t* kv, con
   // first push, then twice the last push's new keys, at least n / 16); a batch that brings more
   // exhausts a probe budget and is inserted again into a larger map (inserts are idempotent)
   const int64_t est = a->pm_last < 0 ? n : std::min<int64_t>(n, std::max<int64_t>({2 * a->pm_last, n / 16, 4096}));
+  if (a->pm_cap > 0 && 2 * (a->pm_occ + est) > a->pm_cap) KHIP_TRY(pmap_prune(a));
   if (a->pm_cap == 0 || 2 * (a->pm_occ + est) > a->pm_cap)
     KHIP_TRY(pmap_grow(a, next_pow2(std::max<int64_t>(4 * (a->pm_occ + est), 4096))));
   KHIP_TRY(a->pm_ctr.ensure(24));
   for (int attempt = 0;; attempt++) {
     KHIP_TRY_HIP(hipMemsetAsync(a->pm_ctr.p, 0, 24, a->stream));
     hipLaunchKernelGGL(k_pmap_insert, dim3(pm_grid(n)), dim3(256), 0, a->stream, keys, kv, rv, ts, part, n,
-                       a->pm_key.as<int64_t>(), a->pm_part.as<int32_t>(), (uint64_t)(a->pm_cap - 1),
+                       a->pm_key.as<int64_t>(), a->pm_part.as<int32_t>(), a->pm_ts.as<unsigned long long>(),
+                       (uint64_t)(a->pm_cap - 1),
                        a->pm_ctr.as<unsigned long long>());
     KHIP_TRY_HIP(hipGetLastError());
     unsigned long long c[3];
@@ -381,17 +440,21 @@ khip_status pmap_clear(khip_agg* a) {
   hipLaunchKernelGGL(k_fill_i64, dim3(pm_grid(a->pm_cap)), dim3(256), 0, a->stream, a->pm_key.as<int64_t>(), a->pm_cap,
                      INT64_MIN);
   KHIP_TRY_HIP(hipMemsetAsync(a->pm_part.p, 0xFF, (size_t)(a->pm_cap + 1) * 4, a->stream));
+  KHIP_TRY_HIP(hipMemsetAsync(a->pm_ts.p, 0, (size_t)a->pm_cap * 8, a->stream));
   KHIP_TRY_HIP(hipGetLastError());
   a->pm_occ = 0;
+  a->pm_pruned = false;
   return KHIP_OK;
 }
 
 void pmap_release(khip_agg* a) {
   a->pm_key.release();
   a->pm_part.release();
+  a->pm_ts.release();
   a->pm_ctr.release();
   a->pdom.release();
   a->pm_cap = a->pm_occ = 0;
+  a->pm_pruned = false;
   a->pm_last = -1;
 }
 
@@ -511,6 +574,7 @@ khip_status partition_bounds(khip_agg* a, HavingDev& h) {
   h.pm_key = a->pm_key.as<int64_t>();
   h.pm_part = a->pm_part.as<int32_t>();
   h.pm_mask = (uint64_t)(a->pm_cap - 1);
+  h.pm_pruned = a->pm_pruned ? 1 : 0;
   h.p_vis = d;
   h.p_fin = d + P;
   h.p_lost_off = d + 3 * P;

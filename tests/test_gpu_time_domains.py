@@ -189,6 +189,49 @@ def test_partition_domain_retention_and_emit_final(prod, orc, engine, window):
             h.close()
 
 
+@pytest.mark.parametrize("engine", ["part", "atomic"])
+@pytest.mark.parametrize("window", ["TUMBLING", "HOPPING"])
+def test_partition_domain_key_map_prunes_expired_keys(prod, orc, engine, window):
+    """The PARTITION key map (key -> partition) drops keys whose windows have all expired in their
+    task before it grows (it grew with every key ever seen).  Every batch brings fresh
+    keys and moves each partition's event time 30 s on, past the 20 s retention, so the keys of
+    two batches ago are pruned at most pushes: the tables, EMIT FINAL's per-push output, row counts
+    and pull queries on pruned keys still equal P independent oracle tasks'."""
+    rng = np.random.default_rng(71 + (engine == "atomic") + 2 * (window == "HOPPING"))
+    P, nb = 4, 8
+    kw = dict(window=window, adv=2500 if window == "HOPPING" else 0, retention_ms=20_000)
+    flags = abi.FLAG_ENGINE_ATOMIC if engine == "atomic" else 0
+    batches = []
+    for b in range(nb):
+        ks, ts, vs, ps = [], [], [], []
+        for p in rng.permutation(P):
+            n = int(rng.integers(8_000, 16_000))
+            ks.append((b * 1_000_000 + rng.integers(0, 6_000, n)) * P + p)
+            ts.append(b * 30_000 + (np.arange(n) * 30_000) // n + rng.integers(0, 2000, n) + 100_000 - p * 7_000)
+            vs.append(rng.integers(-1000, 1000, n))
+            ps.append(np.full(n, p, np.int32))
+        batches.append(tuple(np.concatenate(x) for x in (ks, ts, vs, ps)))
+    for emit in ("CHANGES", "FINAL"):
+        gd = _desc(time_domain="PARTITION", n_partitions=P, flags=flags, emit=emit, **kw)
+        g = abi.AggHandle(prod, gd)
+        tasks = [abi.AggHandle(orc, _desc(emit=emit, **kw)) for _ in range(P)]
+        for k, t, v, p in batches:
+            gs = g.push(abi.HostBatch(t, keys=k, cols=[v], partition=p))
+            os_ = [tasks[q].push(abi.HostBatch(t[p == q], keys=k[p == q], cols=[v[p == q]])) for q in range(P)]
+            assert gs["windows_late"] == sum(o["windows_late"] for o in os_)
+            if emit == "FINAL":
+                assert_snap_equal(g.changes(), _union([h.changes() for h in tasks], gd), gd)
+            assert g.count_rows() == sum(h.snapshot()["n"] for h in tasks)
+        exp = _union([h.snapshot() for h in tasks], gd)
+        assert_snap_equal(g.snapshot(), exp, gd)
+        from test_gpu_pull import _filter
+        old = np.unique(np.concatenate([batches[0][0][:40], batches[1][0][:40], batches[-1][0][:40]]))
+        assert_snap_equal(g.get(keys=old), _filter(exp, old, (None, None), (None, None), True), gd)
+        g.close()
+        for h in tasks:
+            h.close()
+
+
 def test_partition_domain_key_on_two_partitions(prod):
     g = abi.AggHandle(prod, _desc(time_domain="PARTITION", n_partitions=2))
     k = np.array([5, 6, 7, 5], np.int64)
