@@ -3816,7 +3816,15 @@ khip_status part_push(khip_agg* a, int64_t n, const int64_t* keys, const int64_t
     s.c1_skip = 8;
   }
   const int P = (int)s.P;
-  const int64_t tile = (int64_t)PT_THREADS * knob("KHIP_TILE_ITEMS", PT_ITEMS);
+  // records per thread per tile: PT_ITEMS, fewer when that leaves fewer tiles than CUs (one
+  // workgroup per tile: C1's 1M records were 16 tiles on 256 CUs — k_part_scatter_r8 87 -> 11 us and
+  // k_part_hist 39 -> 14 us at 4 items, profiles/r06/ab/c1_tile_items.txt) and the per-tile
+  // partition counts stay small (nT x P words, which the offset scans read)
+  int64_t items = PT_ITEMS;
+  while (items > 4 && ceil_div(n, (int64_t)PT_THREADS * items) < s.n_cu &&
+         ceil_div(n, (int64_t)PT_THREADS * (items >> 1)) * s.P <= (1LL << 21))
+    items >>= 1;
+  const int64_t tile = (int64_t)PT_THREADS * knob("KHIP_TILE_ITEMS", items);
   const int pad = (int)knob("KHIP_PAD", 0);
   const int64_t nT = ceil_div(n, tile);
   const int TC = (int)std::min<int64_t>(nT, TC_MAX);
