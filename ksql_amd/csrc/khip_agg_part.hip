@@ -3529,8 +3529,10 @@ khip_status part_init(khip_agg* a, int64_t hint) {
   // partitions: at most ~H_eff/2 groups each at the hinted size
   const int64_t groups = std::max<int64_t>(hint, 1024);
   s.hint_groups = groups;
-  // at least 64 partitions: the packed identity then holds window ranges of up to 63
-  s.log2P = std::min(SPLIT_P_LOG2, std::max(6, part_ceil_log2(groups * 2 / s.H_eff)));
+  // at least 256 partitions: one merge workgroup per CU for small tables (C1's 40K groups in 64
+  // partitions left three quarters of the CUs idle: k_part_merge_c1 28 -> 16 us at 256,
+  // profiles/r06/ab/c1_partitions.txt); (the packed identity needs >= 64: window ranges up to 63)
+  s.log2P = std::min(SPLIT_P_LOG2, std::max(8, part_ceil_log2(groups * 2 / s.H_eff)));
   // hinted groups would need sub-passes at 2^14 partitions (each re-reads the partition's
   // records): one more partition bit instead (measured: C5 push 12.1 → 9.8 ms)
   if (s.log2P == SPLIT_P_LOG2 && groups >> SPLIT_P_LOG2 > (int64_t)s.H_eff * 7 / 10) s.log2P = MAX_P_LOG2;
