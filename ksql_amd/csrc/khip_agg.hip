@@ -487,7 +487,7 @@ __device__ __forceinline__ bool dslot_eq(const ulonglong2& a, const ulonglong2& 
   if (slen != (k.len < 0xFFFF ? k.len : 0xFFFF)) return false;
   const int64_t o = (int64_t)(a.y & DICT_ID);
   if (*(const uint64_t*)(arena + o) != k.h || *(const int64_t*)(arena + o + 8) != k.len) return false;
-  return k.sk ? key_words_eq_aligned(k.kw, arena + o + 16, k.len) : bytes_eq(arena + o + 16, k.kb, k.len);
+  return k.sk ? key_words_eq_aligned(k.kw, arena + o + 16, k.len) : bytes_eq_aligned(arena + o + 16, k.kb, k.len);
 }
 
 // rows: null (row j = j) or a row list (the retry pass).  lists: DICT_NL regions of lcap entries

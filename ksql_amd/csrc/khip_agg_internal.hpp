@@ -208,16 +208,32 @@ __device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Bytes [8k, 8k + 8) of p (little-endian, as an unaligned load would give them) from the aligned
+// words holding them: `cur` = aligned word k, `nxt` = aligned word k + 1 (sh = 8 * (p & 7)).
+__device__ __forceinline__ uint64_t funnel_word(uint64_t cur, uint64_t nxt, int sh) {
+  return sh ? (cur >> sh) | (nxt << (64 - sh)) : cur;
+}
+
+// Long keys: 8 key bytes per step read as aligned 8-byte words (a byte per load made the chain of
+// a 40-byte URL 40 dependent loads; C1's dictionary probe), the same value as the bytewise rule:
+// h over the full little-endian words, then the tail bytes zero-extended.
 __device__ __forceinline__ uint64_t hash_bytes_dev(const uint8_t* p, int64_t n) {
   uint64_t h = 0x84222325cbf29ce4ULL ^ (uint64_t)n;
-  int64_t i = 0;
-  for (; i + 8 <= n; i += 8) {
-    uint64_t w = 0;
-    for (int b = 0; b < 8; b++) w |= (uint64_t)p[i + b] << (8 * b);
-    h = mix64(h ^ w) * 0x9E3779B97F4A7C15ULL;
+  const uint64_t a = (uint64_t)p;
+  // (pointer arithmetic, not an integer cast: the loads stay global_load, not flat_load)
+  const uint64_t* base = (const uint64_t*)(p - (a & 7));
+  const int sh = (int)(a & 7) * 8;
+  const int64_t na = n > 0 ? (int64_t)(((a & 7) + (uint64_t)n + 7) >> 3) : 0;  // aligned words holding key bytes
+  uint64_t cur = na > 0 ? base[0] : 0ULL;
+  int64_t k = 0;
+  for (; 8 * k + 8 <= n; k++) {
+    const uint64_t nxt = k + 1 < na ? base[k + 1] : 0ULL;
+    h = mix64(h ^ funnel_word(cur, nxt, sh)) * 0x9E3779B97F4A7C15ULL;
+    cur = nxt;
   }
+  const int64_t left = n - 8 * k;  // 0..7 tail bytes
   uint64_t w = 0;
-  for (int b = 0; i + b < n; b++) w |= (uint64_t)p[i + b] << (8 * b);
+  if (left > 0) w = funnel_word(cur, k + 1 < na ? base[k + 1] : 0ULL, sh) & ((1ULL << (8 * left)) - 1);
   return mix64(h ^ w ^ ((uint64_t)(n & 7) << 59));
 }
 
@@ -272,9 +288,23 @@ __device__ __forceinline__ bool key_words_eq_aligned(const uint64_t (&w)[KW_MAX]
   return eq;
 }
 
-__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, int64_t n) {
-  for (int64_t i = 0; i < n; i++)
-    if (a[i] != b[i]) return false;
+// n bytes at an 8-aligned arena entry e against the key bytes at p, 8 bytes per step (e's padding
+// past n ignored).
+__device__ __forceinline__ bool bytes_eq_aligned(const uint8_t* e, const uint8_t* p, int64_t n) {
+  const uint64_t* q = (const uint64_t*)e;
+  const uint64_t a = (uint64_t)p;
+  const uint64_t* base = (const uint64_t*)(p - (a & 7));
+  const int sh = (int)(a & 7) * 8;
+  const int64_t na = n > 0 ? (int64_t)(((a & 7) + (uint64_t)n + 7) >> 3) : 0;
+  uint64_t cur = na > 0 ? base[0] : 0ULL;
+  for (int64_t k = 0; 8 * k < n; k++) {
+    const uint64_t nxt = k + 1 < na ? base[k + 1] : 0ULL;
+    uint64_t x = funnel_word(cur, nxt, sh) ^ q[k];
+    const int64_t left = n - 8 * k;
+    if (left < 8) x &= (1ULL << (8 * left)) - 1;
+    if (x) return false;
+    cur = nxt;
+  }
   return true;
 }
 
